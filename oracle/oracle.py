@@ -1,0 +1,196 @@
+"""ctypes front-end of the CPU oracle (oracle/_ref/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, always as the checker (or the timed CPU
+baseline), never as the product. The product package never imports this.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+u32ref = C.POINTER(C.c_uint32)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "_ref", "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        sig = {
+            "or_minstd_seed": (C.c_uint32, [C.c_uint64]),
+            "or_uniform_int": (C.c_int, [u32ref, C.c_int, C.c_int]),
+            "or_gen_lsh_euclid": (C.c_uint32, [C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_float, f32p, f32p, i32p]),
+            "or_gen_lsh_cosine": (C.c_uint32, [C.c_uint64, C.c_int, C.c_int, C.c_int, f64p]),
+            "or_gen_cube_euclid": (C.c_uint32, [C.c_uint64, C.c_int, C.c_int, C.c_float, f32p, f32p]),
+            "or_gen_cube_cosine": (C.c_uint32, [C.c_uint64, C.c_int, C.c_int, f64p]),
+            "or_lsh_hash_euclid": (None, [C.c_int64, C.c_int, C.c_int, C.c_int, f32p, f32p, f32p, C.c_float,
+                                          i32p, C.c_int64, i32p, i32p, i32p]),
+            "or_lsh_hash_cosine": (None, [C.c_int64, C.c_int, C.c_int, C.c_int, f32p, f64p, i32p]),
+            "or_bucket_csr": (None, [C.c_int64, C.c_int, C.c_int64, i32p, i64p, i32p]),
+            "or_lsh_query": (C.c_int64, [C.c_int64, C.c_int, C.c_int, C.c_int64, C.c_void_p, i64p, i32p,
+                                         C.c_void_p, i32p, i32p, C.c_int64]),
+            "or_cube_h": (None, [C.c_int64, C.c_int, C.c_int, f32p, f32p, f32p, C.c_float, i32p]),
+            "or_cube_coins": (C.c_int64, [C.c_int64, C.c_int, i32p, C.c_int32, C.c_int32, i32p, u32ref, i32p]),
+            "or_cube_cosine": (None, [C.c_int64, C.c_int, C.c_int, f32p, f64p, i32p]),
+            "or_cube_probe_seq": (C.c_int64, [C.c_int32, C.c_int, C.c_int, i32p, C.c_int64]),
+            "or_lloyd_assign": (None, [C.c_int64, C.c_int, C.c_int, f32p, f64p, C.c_int, C.c_void_p, i32p, f64p]),
+            "or_kmeans_update": (C.c_int, [C.c_int64, C.c_int, C.c_int, f32p, i32p, f64p, C.c_int, C.c_double,
+                                           f64p, i64p]),
+            "or_synth": (None, [C.c_uint64, C.c_int64, C.c_int64, C.c_int, f32p]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def synth(seed, rows, d, row0=0):
+    out = np.empty((rows, d), np.float32)
+    lib().or_synth(seed, row0, rows, d, out)
+    return out
+
+
+def gen_lsh_euclid(seed, L, k, d, w):
+    V = np.empty((L, k, d), np.float32); t = np.empty((L, k), np.float32); r = np.empty((L, k), np.int32)
+    st = lib().or_gen_lsh_euclid(seed, L, k, d, w, V, t, r)
+    return V, t, r, st
+
+
+def gen_lsh_cosine(seed, L, k, d):
+    R = np.empty((L, k, d), np.float64)
+    st = lib().or_gen_lsh_cosine(seed, L, k, d, R)
+    return R, st
+
+
+def gen_cube_euclid(seed, k, d, w):
+    V = np.empty((k, d), np.float32); t = np.empty((k,), np.float32)
+    st = lib().or_gen_cube_euclid(seed, k, d, w, V, t)
+    return V, t, st
+
+
+def gen_cube_cosine(seed, k, d):
+    R = np.empty((k, d), np.float64)
+    st = lib().or_gen_cube_cosine(seed, k, d, R)
+    return R, st
+
+
+def lsh_hash_euclid(X, V, t, w, r, nb):
+    X = np.ascontiguousarray(X, np.float32)
+    N, d = X.shape; L, k = t.shape
+    tuples = np.empty((N, L, k), np.int32); phi = np.empty((N, L), np.int32); bucket = np.empty((N, L), np.int32)
+    lib().or_lsh_hash_euclid(N, d, L, k, X, np.ascontiguousarray(V, np.float32), np.ascontiguousarray(t, np.float32),
+                             float(w), np.ascontiguousarray(r, np.int32), nb, tuples, phi, bucket)
+    return tuples, phi, bucket
+
+
+def lsh_hash_cosine(X, R):
+    X = np.ascontiguousarray(X, np.float32)
+    N, d = X.shape; L, k, _ = R.shape
+    g = np.empty((N, L), np.int32)
+    lib().or_lsh_hash_cosine(N, d, L, k, X, np.ascontiguousarray(R, np.float64), g)
+    return g
+
+
+def bucket_csr(bucket, nb):
+    bucket = np.ascontiguousarray(bucket, np.int32)
+    N, L = bucket.shape
+    rp = np.empty((L, nb + 1), np.int64); idx = np.empty((L, N), np.int32)
+    lib().or_bucket_csr(N, L, nb, bucket, rp, idx)
+    return rp, idx
+
+
+def lsh_query(N, nb, row_ptr, idx, q_bucket, tuples=None, q_tuple=None):
+    L = row_ptr.shape[0]
+    k = tuples.shape[2] if tuples is not None else 0
+    qb = np.ascontiguousarray(q_bucket, np.int32)
+    cap = int(sum(row_ptr[l, qb[l] + 1] - row_ptr[l, qb[l]] for l in range(L)))
+    out = np.empty(max(cap, 1), np.int32)
+    tu = None if tuples is None else np.ascontiguousarray(tuples, np.int32)
+    qt = None if q_tuple is None else np.ascontiguousarray(q_tuple, np.int32)
+    n = lib().or_lsh_query(N, L, k, nb, _ptr(tu), row_ptr, idx, _ptr(qt), qb, out, out.size)
+    return out[:n].copy()
+
+
+def cube_h(X, V, t, w):
+    X = np.ascontiguousarray(X, np.float32)
+    N, d = X.shape; k = t.shape[0]
+    h = np.empty((N, k), np.int32)
+    lib().or_cube_h(N, d, k, X, np.ascontiguousarray(V, np.float32), np.ascontiguousarray(t, np.float32), float(w), h)
+    return h
+
+
+class CoinMemo:
+    """Dense per-f memo of the lazy Euclidean-F coins, plus the engine state."""
+
+    def __init__(self, k, state, hmin=-(1 << 16), hspan=1 << 17):
+        self.k, self.hmin, self.hspan = k, hmin, hspan
+        self.memo = np.full((k, hspan), -1, np.int32)
+        self.state = C.c_uint32(state)
+
+    def apply(self, h):
+        h = np.ascontiguousarray(h, np.int32)
+        vertex = np.empty(h.shape[0], np.int32)
+        n = lib().or_cube_coins(h.shape[0], self.k, h, self.hmin, self.hspan, self.memo, C.byref(self.state), vertex)
+        if n < 0:
+            raise ValueError("h outside memo span")
+        return vertex, n
+
+    def as_lists(self):
+        f, off = np.nonzero(self.memo >= 0)
+        return f.astype(np.int32), (off + self.hmin).astype(np.int32), self.memo[f, off].astype(np.int32)
+
+
+def cube_cosine(X, R):
+    X = np.ascontiguousarray(X, np.float32)
+    N, d = X.shape; k = R.shape[0]
+    v = np.empty(N, np.int32)
+    lib().or_cube_cosine(N, d, k, X, np.ascontiguousarray(R, np.float64), v)
+    return v
+
+
+def cube_probe_seq(vertex, probes, k):
+    cap = 1 << min(k, 24)
+    out = np.empty(cap + 1, np.int32)
+    n = lib().or_cube_probe_seq(int(vertex), int(probes), int(k), out, out.size)
+    return out[:min(n, out.size)].copy()
+
+
+def lloyd_assign(X, Cc, metric="euclidean", src_rows=None):
+    X = np.ascontiguousarray(X, np.float32)
+    Cc = np.ascontiguousarray(Cc, np.float64)
+    N, d = X.shape; K = Cc.shape[0]
+    a = np.empty(N, np.int32); dist = np.empty(N, np.float64)
+    sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
+    lib().or_lloyd_assign(N, d, K, X, Cc, 0 if metric == "euclidean" else 1, _ptr(sr), a, dist)
+    return a, dist
+
+
+def kmeans_update(X, assign, C_old, metric="euclidean", min_dist=0.0):
+    X = np.ascontiguousarray(X, np.float32)
+    N, d = X.shape; K = C_old.shape[0]
+    Cn = np.empty((K, d), np.float64); cnt = np.empty(K, np.int64)
+    cont = lib().or_kmeans_update(N, d, K, X, np.ascontiguousarray(assign, np.int32),
+                                  np.ascontiguousarray(C_old, np.float64), 0 if metric == "euclidean" else 1,
+                                  float(min_dist), Cn, cnt)
+    return Cn, cnt, bool(cont)

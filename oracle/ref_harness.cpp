@@ -1,0 +1,413 @@
+// ref_harness.cpp — runs the REFERENCE's own hot-path code to produce golden
+// fixtures and the CPU baseline. TEST INFRASTRUCTURE ONLY: nothing in the
+// product links or calls this.
+//
+// Built by oracle/Makefile from this file plus the reference's sources where
+// they lie (/root/reference/lib/*.hpp by include path, utils.cpp, tweet.cpp),
+// with g++ -O0 as the reference ships (-O1/-O2 crash on the UB at
+// cust_hashtable.hpp:65-70; clang changes M at euclidean_phi_gen.hpp:70).
+// The binary goes to oracle/_ref/ only (git-ignored).
+//
+// Determinism: the reference seeds every RNG from system_clock::now()
+// (lsh_cube.hpp:49-51,112-114; initialization.hpp:42-44,75-77). We interpose
+// std::chrono::_V2::system_clock::now() at link time and return g_seed ticks.
+//
+// Output: .npy files (little endian) into an output directory.
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <map>
+#include <random>
+#include <set>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+static long long g_seed = 12345;
+
+namespace std { namespace chrono { inline namespace _V2 {
+system_clock::time_point system_clock::now() noexcept {
+    return system_clock::time_point(system_clock::duration(g_seed));
+}
+}}}
+
+// Read generator internals (params, memo tables). Std headers are already in.
+#define private public
+#include "utils.hpp"
+#include "lsh_cube.hpp"
+#include "clustering_phases/assignment.hpp"
+#include "clustering_phases/update.hpp"
+#include "clustering_phases/initialization.hpp"
+#undef private
+
+#include "../include/lshkm_synth.h"
+
+typedef CustVector<double> Vec;
+
+// ---------------------------------------------------------------- npy writer
+template <typename T> struct NpyType;
+template <> struct NpyType<float>   { static const char* s() { return "<f4"; } };
+template <> struct NpyType<double>  { static const char* s() { return "<f8"; } };
+template <> struct NpyType<int32_t> { static const char* s() { return "<i4"; } };
+template <> struct NpyType<int64_t> { static const char* s() { return "<i8"; } };
+template <> struct NpyType<uint32_t>{ static const char* s() { return "<u4"; } };
+template <> struct NpyType<uint8_t> { static const char* s() { return "|u1"; } };
+
+template <typename T>
+static void write_npy(const std::string& path, const std::vector<T>& data, const std::vector<size_t>& shape) {
+    std::string hdr = std::string("{'descr': '") + NpyType<T>::s() + "', 'fortran_order': False, 'shape': (";
+    for (size_t i = 0; i < shape.size(); i++) hdr += std::to_string(shape[i]) + (shape.size() == 1 ? ",)" : (i + 1 < shape.size() ? ", " : ")"));
+    if (shape.empty()) hdr += ")";
+    hdr += ", }";
+    size_t total = 10 + hdr.size() + 1;
+    size_t pad = (64 - total % 64) % 64;
+    hdr += std::string(pad, ' ') + "\n";
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) { fprintf(stderr, "cannot write %s\n", path.c_str()); exit(2); }
+    unsigned char magic[8] = {0x93, 'N', 'U', 'M', 'P', 'Y', 1, 0};
+    fwrite(magic, 1, 8, f);
+    uint16_t hl = (uint16_t)hdr.size();
+    fwrite(&hl, 2, 1, f);
+    fwrite(hdr.data(), 1, hdr.size(), f);
+    if (!data.empty()) fwrite(data.data(), sizeof(T), data.size(), f);
+    fclose(f);
+}
+
+static std::vector<float> read_f32(const std::string& path, size_t count) {
+    std::vector<float> v(count);
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { fprintf(stderr, "cannot read %s\n", path.c_str()); exit(2); }
+    if (fread(v.data(), sizeof(float), count, f) != count) { fprintf(stderr, "short read %s\n", path.c_str()); exit(2); }
+    fclose(f);
+    return v;
+}
+
+static std::vector<double> read_f64(const std::string& path, size_t count) {
+    std::vector<double> v(count);
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { fprintf(stderr, "cannot read %s\n", path.c_str()); exit(2); }
+    if (fread(v.data(), sizeof(double), count, f) != count) { fprintf(stderr, "short read %s\n", path.c_str()); exit(2); }
+    fclose(f);
+    return v;
+}
+
+static std::vector<Vec> make_vectors(const std::vector<float>& x, int N, int d, const std::string& prefix) {
+    std::vector<Vec> vecs;
+    vecs.reserve(N);
+    for (int i = 0; i < N; i++) {
+        std::vector<double> dims(d);
+        for (int j = 0; j < d; j++) dims[j] = (double)x[(size_t)i * d + j];
+        vecs.emplace_back(prefix + std::to_string(i), dims);
+    }
+    return vecs;
+}
+
+static std::vector<int> split_ints(const std::string& s) {
+    std::vector<int> out;
+    std::stringstream ss(s);
+    std::string tok;
+    while (std::getline(ss, tok, ',')) if (!tok.empty()) out.push_back(std::stoi(tok));
+    return out;
+}
+
+static void csr_write(const std::string& dir, const std::string& name,
+                      const std::vector<std::vector<int32_t>>& lists) {
+    std::vector<int64_t> ptr(1, 0);
+    std::vector<int32_t> idx;
+    for (auto& l : lists) { idx.insert(idx.end(), l.begin(), l.end()); ptr.push_back((int64_t)idx.size()); }
+    write_npy(dir + "/" + name + "_ptr.npy", ptr, {ptr.size()});
+    write_npy(dir + "/" + name + "_idx.npy", idx, {idx.size()});
+}
+
+static std::vector<int32_t> to_indices(const std::vector<Vec*>& ptrs, Vec* base) {
+    std::vector<int32_t> out;
+    out.reserve(ptrs.size());
+    for (auto p : ptrs) out.push_back((int32_t)(p - base));
+    return out;
+}
+
+// ------------------------------------------------------------------ LSH mode
+// lsh IN N d metric k L div w seed OUT [QIN Q NQROWS]
+static int mode_lsh(int argc, char** argv) {
+    if (argc < 11) { fprintf(stderr, "usage: lsh IN N d metric k L div w seed OUT [QIN Q NQROWS]\n"); return 2; }
+    std::string in = argv[1]; int N = atoi(argv[2]); int d = atoi(argv[3]);
+    std::string metric = argv[4]; int k = atoi(argv[5]); int L = atoi(argv[6]);
+    int div = atoi(argv[7]); double w = atof(argv[8]); g_seed = atoll(argv[9]);
+    std::string out = argv[10];
+    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<Vec> vecs = make_vectors(x, N, d, "");
+
+    std::vector<CustHashtable<double>*> tables = create_LSH_hashtables<double>(vecs, metric, k, L, div, w);
+    int nb = (metric == "euclidean") ? N / div : (int)pow(2, k);
+
+    std::vector<int32_t> tuples, phi((size_t)N * L), bucket((size_t)N * L);
+    std::vector<float> V, T, W; std::vector<int32_t> R; std::vector<double> RC;
+    for (int l = 0; l < L; l++) {
+        HashGenerator<double>* g = tables[l]->hashGenerator;
+        if (metric == "euclidean") {
+            auto* pg = dynamic_cast<EuclideanPhiGen<double>*>(g);
+            for (int i = 0; i < k; i++) {
+                auto* h = pg->hFunctions[i];
+                for (int j = 0; j < d; j++) V.push_back((*h->v->getDimensions())[j]);
+                T.push_back(h->t); W.push_back(h->w); R.push_back(pg->rs[i]);
+            }
+        } else {
+            auto* cg = dynamic_cast<CosineGGen<double>*>(g);
+            for (int i = 0; i < k; i++)
+                for (int j = 0; j < d; j++) RC.push_back((*cg->hFunctions[i]->r->getDimensions())[j]);
+        }
+    }
+    if (metric == "euclidean") {
+        tuples.resize((size_t)N * L * k);
+        for (int n = 0; n < N; n++)
+            for (int l = 0; l < L; l++) {
+                auto* pg = dynamic_cast<EuclideanPhiGen<double>*>(tables[l]->hashGenerator);
+                std::vector<int>& t = pg->id_to_det_hashes[vecs[n].getId()];
+                for (int i = 0; i < k; i++) tuples[((size_t)n * L + l) * k + i] = t[i];
+            }
+    }
+    for (int n = 0; n < N; n++)
+        for (int l = 0; l < L; l++) {
+            phi[(size_t)n * L + l] = tables[l]->hashGenerator->generate(&vecs[n]);
+            bucket[(size_t)n * L + l] = tables[l]->getHash(&vecs[n]);
+        }
+    std::vector<std::vector<int32_t>> members;
+    for (int l = 0; l < L; l++)
+        for (int b = 0; b < nb; b++) members.push_back(to_indices(tables[l]->getBucketFromIndex(b), vecs.data()));
+
+    if (metric == "euclidean") {
+        write_npy(out + "/V.npy", V, {(size_t)L, (size_t)k, (size_t)d});
+        write_npy(out + "/t.npy", T, {(size_t)L, (size_t)k});
+        write_npy(out + "/w.npy", W, {(size_t)L, (size_t)k});
+        write_npy(out + "/r.npy", R, {(size_t)L, (size_t)k});
+        write_npy(out + "/tuples.npy", tuples, {(size_t)N, (size_t)L, (size_t)k});
+    } else {
+        write_npy(out + "/R.npy", RC, {(size_t)L, (size_t)k, (size_t)d});
+    }
+    write_npy(out + "/phi.npy", phi, {(size_t)N, (size_t)L});
+    write_npy(out + "/bucket.npy", bucket, {(size_t)N, (size_t)L});
+    csr_write(out, "members", members);
+
+    // Queries: NQROWS dataset rows (in row order), then Q external vectors.
+    if (argc >= 14) {
+        std::string qin = argv[11]; int Q = atoi(argv[12]); int nqrows = atoi(argv[13]);
+        std::vector<float> qx = read_f32(qin, (size_t)Q * d);
+        std::vector<Vec> qvecs = make_vectors(qx, Q, d, "q");
+        std::vector<std::vector<int32_t>> filt, unf;
+        for (int r = 0; r < nqrows + Q; r++) {
+            Vec* q = r < nqrows ? &vecs[r] : &qvecs[r - nqrows];
+            filt.push_back(to_indices(get_LSH_filtered_combined_buckets(tables, q), vecs.data()));
+            unf.push_back(to_indices(get_LSH_combined_buckets(tables, q), vecs.data()));
+        }
+        csr_write(out, "qfilt", filt);
+        csr_write(out, "qunf", unf);
+    }
+    for (auto t : tables) delete t;
+    return 0;
+}
+
+// ----------------------------------------------------------------- cube mode
+// cube IN N d metric k w seed PROBES_CSV OUT [QIN Q NQROWS]
+static int mode_cube(int argc, char** argv) {
+    if (argc < 9) { fprintf(stderr, "usage: cube IN N d metric k w seed PROBES OUT [QIN Q NQROWS]\n"); return 2; }
+    std::string in = argv[1]; int N = atoi(argv[2]); int d = atoi(argv[3]);
+    std::string metric = argv[4]; int k = atoi(argv[5]); double w = atof(argv[6]);
+    g_seed = atoll(argv[7]); std::vector<int> probes = split_ints(argv[8]);
+    std::string out = argv[9];
+    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<Vec> vecs = make_vectors(x, N, d, "");
+
+    CustHashtable<double>* cube = create_hypercube<double>(vecs, metric, k, w);
+    auto* hg = dynamic_cast<HypercubeGen<double>*>(cube->hashGenerator);
+    int nb = 1 << k;
+
+    std::vector<float> V, T, W; std::vector<double> RC;
+    std::vector<int32_t> memo_f, memo_h, memo_bit;
+    for (int i = 0; i < k; i++) {
+        if (metric == "euclidean") {
+            auto* fg = dynamic_cast<EuclideanFGen<double>*>(hg->fFunctions[i]);
+            for (int j = 0; j < d; j++) V.push_back((*fg->hGenerator->v->getDimensions())[j]);
+            T.push_back(fg->hGenerator->t); W.push_back(fg->hGenerator->w);
+            std::map<int, int> sorted(fg->num_to_bin_hashes.begin(), fg->num_to_bin_hashes.end());
+            for (auto& kv : sorted) { memo_f.push_back(i); memo_h.push_back(kv.first); memo_bit.push_back(kv.second); }
+        } else {
+            auto* ch = dynamic_cast<CosineHGen<double>*>(hg->fFunctions[i]);
+            for (int j = 0; j < d; j++) RC.push_back((*ch->r->getDimensions())[j]);
+        }
+    }
+    std::vector<int32_t> vertex(N), hvals;
+    for (int n = 0; n < N; n++) vertex[n] = cube->getHash(&vecs[n]);   // all h already seen: no draws
+    if (metric == "euclidean") {
+        for (int n = 0; n < N; n++)
+            for (int i = 0; i < k; i++)
+                hvals.push_back(dynamic_cast<EuclideanFGen<double>*>(hg->fFunctions[i])->hGenerator->generate(&vecs[n]));
+    }
+    std::vector<std::vector<int32_t>> members;
+    for (int b = 0; b < nb; b++) members.push_back(to_indices(cube->getBucketFromIndex(b), vecs.data()));
+
+    if (metric == "euclidean") {
+        write_npy(out + "/V.npy", V, {(size_t)k, (size_t)d});
+        write_npy(out + "/t.npy", T, {(size_t)k});
+        write_npy(out + "/w.npy", W, {(size_t)k});
+        write_npy(out + "/memo_f.npy", memo_f, {memo_f.size()});
+        write_npy(out + "/memo_h.npy", memo_h, {memo_h.size()});
+        write_npy(out + "/memo_bit.npy", memo_bit, {memo_bit.size()});
+        write_npy(out + "/h.npy", hvals, {(size_t)N, (size_t)k});
+    } else {
+        write_npy(out + "/R.npy", RC, {(size_t)k, (size_t)d});
+    }
+    write_npy(out + "/vertex.npy", vertex, {(size_t)N});
+    csr_write(out, "members", members);
+    write_npy(out + "/probes.npy", std::vector<int32_t>(probes.begin(), probes.end()), {probes.size()});
+
+    // Queries. The F-coin engine is a local of create_hypercube (lsh_cube.hpp:113)
+    // held by pointer in every EuclideanFGen (euclidean_f_gen.hpp:58): a query
+    // whose h was never seen draws from a dead stack frame (UB). Such queries are
+    // skipped here and marked in qmask; only fully-seen queries are pinned.
+    if (argc >= 13) {
+        std::string qin = argv[10]; int Q = atoi(argv[11]); int nqrows = atoi(argv[12]);
+        std::vector<float> qx = read_f32(qin, (size_t)Q * d);
+        std::vector<Vec> qvecs = make_vectors(qx, Q, d, "q");
+        std::vector<uint8_t> qmask;
+        std::vector<Vec*> qs;
+        for (int r = 0; r < nqrows + Q; r++) {
+            Vec* q = r < nqrows ? &vecs[r] : &qvecs[r - nqrows];
+            bool seen = true;
+            if (metric == "euclidean")
+                for (int i = 0; i < k; i++) {
+                    auto* fg = dynamic_cast<EuclideanFGen<double>*>(hg->fFunctions[i]);
+                    if (fg->num_to_bin_hashes.count(fg->hGenerator->generate(q)) == 0) seen = false;
+                }
+            qmask.push_back(seen ? 1 : 0);
+            if (seen) qs.push_back(q);
+        }
+        write_npy(out + "/qmask.npy", qmask, {qmask.size()});
+        for (int p : probes) {
+            std::vector<std::vector<int32_t>> res;
+            for (Vec* q : qs) res.push_back(to_indices(get_hypercube_combined_buckets(*cube, q, p, k), vecs.data()));
+            csr_write(out, "q_probes" + std::to_string(p), res);
+        }
+    }
+    delete cube;
+    return 0;
+}
+
+// ---------------------------------------------------------------- lloyd mode
+// lloyd IN N d K metric iters min_dist OUT [CENTERS_F64 | -]  [rows_csv]
+// Initial centroids: dataset rows i*(N/K) (or rows_csv), or an fp64 file of
+// K*d external centers (ids "c<i>", not dataset rows).
+static int mode_lloyd(int argc, char** argv) {
+    if (argc < 9) { fprintf(stderr, "usage: lloyd IN N d K metric iters min_dist OUT [CENTERS|-] [rows]\n"); return 2; }
+    std::string in = argv[1]; int N = atoi(argv[2]); int d = atoi(argv[3]); int K = atoi(argv[4]);
+    std::string metric = argv[5]; int iters = atoi(argv[6]); double min_dist = atof(argv[7]);
+    std::string out = argv[8];
+    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<Vec> vecs = make_vectors(x, N, d, "");
+    std::vector<Vec*> centroids(K);
+    std::vector<Vec> ext;
+    std::vector<int32_t> src_rows(K, -1);
+    if (argc >= 10 && std::string(argv[9]) != "-") {
+        std::vector<double> c = read_f64(argv[9], (size_t)K * d);
+        ext.reserve(K);
+        for (int i = 0; i < K; i++) ext.emplace_back("c" + std::to_string(i), std::vector<double>(c.begin() + (size_t)i * d, c.begin() + (size_t)(i + 1) * d));
+        for (int i = 0; i < K; i++) centroids[i] = &ext[i];
+    } else {
+        std::vector<int> rows;
+        if (argc >= 11) rows = split_ints(argv[10]);
+        for (int i = 0; i < K; i++) {
+            int r = rows.empty() ? i * (N / K) : rows[i];
+            centroids[i] = &vecs[r]; src_rows[i] = r;
+        }
+    }
+    write_npy(out + "/src_rows.npy", src_rows, {(size_t)K});
+    std::vector<double> c0;
+    for (int c = 0; c < K; c++) for (int j = 0; j < d; j++) c0.push_back((*centroids[c]->getDimensions())[j]);
+    write_npy(out + "/centers0.npy", c0, {(size_t)K, (size_t)d});
+
+    bool cont = true; int it = 0;
+    std::vector<int32_t> flags;
+    while (cont && it < iters) {
+        lloyds_assignment(vecs, centroids, metric);
+        std::vector<int32_t> assign(N); std::vector<double> dist(N);
+        for (int n = 0; n < N; n++) { assign[n] = vecs[n].getCluster(); dist[n] = vecs[n].getDistFromCentroid(); }
+        write_npy(out + "/assign" + std::to_string(it) + ".npy", assign, {(size_t)N});
+        write_npy(out + "/dist" + std::to_string(it) + ".npy", dist, {(size_t)N});
+        cont = k_means(vecs, centroids, metric, min_dist);
+        flags.push_back(cont ? 1 : 0);
+        std::vector<double> cs;
+        for (int c = 0; c < K; c++) for (int j = 0; j < d; j++) cs.push_back((*centroids[c]->getDimensions())[j]);
+        write_npy(out + "/centers" + std::to_string(it + 1) + ".npy", cs, {(size_t)K, (size_t)d});
+        it++;
+    }
+    write_npy(out + "/cont.npy", flags, {flags.size()});
+    for (auto c : centroids) if (c->getId() == "k_means_center") delete c;
+    return 0;
+}
+
+// ------------------------------------------------------------ kmeanspp mode
+// kmeanspp IN N d K metric seed OUT  — k-means++ seeding (initialization.hpp:71-156)
+static int mode_kmeanspp(int argc, char** argv) {
+    if (argc < 8) { fprintf(stderr, "usage: kmeanspp IN N d K metric seed OUT\n"); return 2; }
+    std::string in = argv[1]; int N = atoi(argv[2]); int d = atoi(argv[3]); int K = atoi(argv[4]);
+    std::string metric = argv[5]; g_seed = atoll(argv[6]); std::string out = argv[7];
+    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<Vec> vecs = make_vectors(x, N, d, "");
+    std::vector<Vec*> c = k_means_pp(vecs, K, metric);
+    std::vector<Vec*> r = rand_selection(vecs, K);
+    std::vector<int32_t> rows, rrows;
+    for (auto p : c) rows.push_back((int32_t)(p - vecs.data()));
+    for (auto p : r) rrows.push_back((int32_t)(p - vecs.data()));
+    write_npy(out + "/kpp_rows.npy", rows, {rows.size()});
+    write_npy(out + "/rand_rows.npy", rrows, {rrows.size()});
+    return 0;
+}
+
+// --------------------------------------------------------------- bench mode
+// bench NH NA K seed — the reference's own CPU path on synthetic data, one
+// thread, as shipped (-O0). Prints one JSON line.
+static int mode_bench(int argc, char** argv) {
+    if (argc < 5) { fprintf(stderr, "usage: bench NH NA K seed\n"); return 2; }
+    int NH = atoi(argv[1]); int NA = atoi(argv[2]); int K = atoi(argv[3]); uint64_t seed = strtoull(argv[4], 0, 10);
+    const int d = 128;
+    int NX = NH > NA ? NH : NA;
+    std::vector<float> x((size_t)NX * d);
+    for (size_t i = 0; i < (size_t)NX; i++)
+        for (int j = 0; j < d; j++) x[i * d + j] = lshkm_synth_value(seed, i, d, j);
+    std::vector<Vec> vh = make_vectors(std::vector<float>(x.begin(), x.begin() + (size_t)NH * d), NH, d, "");
+    std::vector<Vec> va = make_vectors(std::vector<float>(x.begin(), x.begin() + (size_t)NA * d), NA, d, "");
+    g_seed = 12345;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<CustHashtable<double>*> tables = create_LSH_hashtables<double>(vh, "euclidean", 4, 5, 100, 0.4);
+    auto t1 = std::chrono::steady_clock::now();
+    std::vector<Vec*> cents(K);
+    for (int i = 0; i < K; i++) cents[i] = &va[i * (NA / K)];
+    auto t2 = std::chrono::steady_clock::now();
+    lloyds_assignment(va, cents, std::string("euclidean"));
+    auto t3 = std::chrono::steady_clock::now();
+    double th = std::chrono::duration<double>(t1 - t0).count();
+    double ta = std::chrono::duration<double>(t3 - t2).count();
+    printf("{\"hash_pts\": %d, \"hash_s\": %.6f, \"assign_pts\": %d, \"assign_s\": %.6f, \"K\": %d}\n", NH, th, NA, ta, K);
+    for (auto t : tables) delete t;
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) { fprintf(stderr, "usage: ref_harness {lsh|cube|lloyd|kmeanspp|bench} ...\n"); return 2; }
+    std::string m = argv[1];
+    if (m == "lsh") return mode_lsh(argc - 1, argv + 1);
+    if (m == "cube") return mode_cube(argc - 1, argv + 1);
+    if (m == "lloyd") return mode_lloyd(argc - 1, argv + 1);
+    if (m == "kmeanspp") return mode_kmeanspp(argc - 1, argv + 1);
+    if (m == "bench") return mode_bench(argc - 1, argv + 1);
+    fprintf(stderr, "unknown mode %s\n", m.c_str());
+    return 2;
+}

@@ -1,0 +1,135 @@
+"""Regenerate the golden fixtures from the REFERENCE's own code.
+
+Runs oracle/_ref/ref_harness (the reference's lsh_cube.hpp / assignment.hpp /
+update.hpp / initialization.hpp compiled from /root/reference with g++ -O0,
+clock interposed — see oracle/Makefile) on synthetic inputs and stores the
+outputs as tests/golden/<case>.npz plus tests/golden/cases.json.
+
+Inputs are NOT stored: they are the synthetic generator of
+include/lshkm_synth.h at the (seed, rows, d) recorded in cases.json, except
+external fp64 centroids, which are stored.
+
+Only runs in the build container (the reference is absent on the GPU box).
+Usage: python tests/golden/make_golden.py
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle  # noqa: E402
+
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+
+LSH_CASES = [
+    # name, N, d, metric, k, L, div, w, seed, data_seed, nqrows, Q
+    ("lsh_e", 1000, 128, "euclidean", 4, 5, 10, 0.4, 777, 1, 20, 10),
+    ("lsh_e_w4", 1000, 128, "euclidean", 4, 5, 50, 4.0, 778, 2, 25, 10),
+    ("lsh_e_odd", 600, 17, "euclidean", 3, 3, 7, 1.0, 31337, 3, 15, 8),
+    ("lsh_c", 1000, 128, "cosine", 4, 5, 0, 0.0, 4242, 4, 10, 5),
+    ("lsh_c_odd", 500, 17, "cosine", 5, 2, 0, 0.0, 99, 5, 10, 5),
+]
+CUBE_CASES = [
+    # name, N, d, metric, k, w, seed, data_seed, probes, nqrows, Q
+    ("cube_e", 1500, 128, "euclidean", 8, 4.0, 1001, 6, "0,1,2,5,8,20,300", 20, 30),
+    ("cube_e14", 3000, 128, "euclidean", 14, 2.0, 1002, 7, "1,14,15", 20, 10),
+    ("cube_e_odd", 700, 17, "euclidean", 6, 1.5, 1003, 8, "0,1,3,6,64", 15, 20),
+    ("cube_c", 1500, 128, "cosine", 10, 0.0, 1004, 9, "0,1,3,10,50", 20, 10),
+]
+LLOYD_CASES = [
+    # name, N, d, K, metric, iters, min_dist, data_seed, init ("rows" | "ext" | csv of rows)
+    ("lloyd_e16", 1000, 128, 16, "euclidean", 3, 0.05, 10, "rows"),
+    ("lloyd_e256", 2048, 128, 256, "euclidean", 2, 0.05, 11, "rows"),
+    ("lloyd_c16", 1000, 128, 16, "cosine", 3, 0.05, 12, "rows"),
+    ("lloyd_ext", 1000, 128, 12, "euclidean", 2, 0.05, 13, "ext"),
+    ("lloyd_dup", 800, 32, 8, "euclidean", 3, 0.0, 14, "0,7,7,100,200,200,300,400"),
+    ("lloyd_conv", 400, 16, 4, "euclidean", 6, 1e9, 15, "rows"),
+]
+KPP_CASES = [
+    # name, N, d, K, metric, seed, data_seed   (config 1 plumbing: 1k x d=16, K=8)
+    ("kpp_c1", 1000, 16, 8, "cosine", 2024, 16),
+]
+
+
+def run(args):
+    subprocess.run([HARNESS] + [str(a) for a in args], check=True)
+
+
+def load_dir(d):
+    return {f[:-4]: np.load(os.path.join(d, f)) for f in sorted(os.listdir(d)) if f.endswith(".npy")}
+
+
+def ext_centers(seed, K, d):
+    # Deterministic non-fp32 fp64 centers: synth rows scaled by (1 + small irrational offsets).
+    base = oracle.synth(seed, K, d).astype(np.float64)
+    j = np.arange(d, dtype=np.float64)[None, :]
+    c = np.arange(K, dtype=np.float64)[:, None]
+    return base * (1.0 + 1e-3 * np.sin(1.0 + j * 0.7 + c * 1.3)) + 1e-4 * np.cos(j + c)
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    meta = {}
+    tmp = tempfile.mkdtemp()
+    try:
+        for (name, N, d, metric, k, L, div, w, seed, dseed, nqrows, Q) in LSH_CASES:
+            out = os.path.join(tmp, name); os.makedirs(out)
+            x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
+            q = oracle.synth(dseed + 1000, Q, d); q.tofile(os.path.join(tmp, "q.f32"))
+            run(["lsh", os.path.join(tmp, "x.f32"), N, d, metric, k, L, div if div else 1, w, seed, out,
+                 os.path.join(tmp, "q.f32"), Q, nqrows])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
+            meta[name] = dict(kind="lsh", N=N, d=d, metric=metric, k=k, L=L, div=div, w=w, seed=seed,
+                              data_seed=dseed, query_seed=dseed + 1000, nqrows=nqrows, Q=Q,
+                              nb=(N // div) if metric == "euclidean" else 2 ** k)
+        for (name, N, d, metric, k, w, seed, dseed, probes, nqrows, Q) in CUBE_CASES:
+            out = os.path.join(tmp, name); os.makedirs(out)
+            x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
+            q = oracle.synth(dseed + 1000, Q, d); q.tofile(os.path.join(tmp, "q.f32"))
+            run(["cube", os.path.join(tmp, "x.f32"), N, d, metric, k, w, seed, probes, out,
+                 os.path.join(tmp, "q.f32"), Q, nqrows])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
+            meta[name] = dict(kind="cube", N=N, d=d, metric=metric, k=k, w=w, seed=seed, data_seed=dseed,
+                              query_seed=dseed + 1000, probes=[int(p) for p in probes.split(",")],
+                              nqrows=nqrows, Q=Q)
+        for (name, N, d, K, metric, iters, min_dist, dseed, init) in LLOYD_CASES:
+            out = os.path.join(tmp, name); os.makedirs(out)
+            x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
+            args = ["lloyd", os.path.join(tmp, "x.f32"), N, d, K, metric, iters, repr(min_dist), out]
+            extra = {}
+            if init == "ext":
+                c = ext_centers(dseed + 500, K, d)
+                c.tofile(os.path.join(tmp, "c.f64"))
+                args += [os.path.join(tmp, "c.f64")]
+                extra["ext_centers"] = c
+            elif init != "rows":
+                args += ["-", init]
+            run(args)
+            res = load_dir(out); res.update(extra)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+            meta[name] = dict(kind="lloyd", N=N, d=d, K=K, metric=metric, iters=iters, min_dist=min_dist,
+                              data_seed=dseed, init=init)
+        for (name, N, d, K, metric, seed, dseed) in KPP_CASES:
+            out = os.path.join(tmp, name); os.makedirs(out)
+            x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
+            run(["kmeanspp", os.path.join(tmp, "x.f32"), N, d, K, metric, seed, out])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
+            meta[name] = dict(kind="kmeanspp", N=N, d=d, K=K, metric=metric, seed=seed, data_seed=dseed)
+    finally:
+        shutil.rmtree(tmp)
+    with open(os.path.join(HERE, "cases.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    total = sum(os.path.getsize(os.path.join(HERE, n + ".npz")) for n in meta)
+    print(f"wrote {len(meta)} cases, {total / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+"""Pin the CPU oracle (oracle/lshkm_oracle.c) against the reference's own
+outputs (tests/golden, made by oracle/_ref/ref_harness from /root/reference).
+
+Everything here is bit-exact: integer outputs by array_equal, fp64 outputs by
+bitwise equality. CPU only.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import cases, golden, golden_meta
+
+META = golden_meta()
+
+
+@pytest.mark.parametrize("name", cases("lsh"))
+def test_lsh_params(name):
+    m, g = META[name], golden(name)
+    if m["metric"] == "euclidean":
+        V, t, r, _ = oracle.gen_lsh_euclid(m["seed"], m["L"], m["k"], m["d"], np.float32(m["w"]))
+        assert np.array_equal(V, g["V"]) and np.array_equal(t, g["t"]) and np.array_equal(r, g["r"])
+        assert np.all(g["w"] == np.float32(m["w"]))
+    else:
+        R, _ = oracle.gen_lsh_cosine(m["seed"], m["L"], m["k"], m["d"])
+        assert np.array_equal(R.view(np.uint64), g["R"].view(np.uint64))
+
+
+@pytest.mark.parametrize("name", cases("lsh"))
+def test_lsh_hash_and_buckets(name):
+    m, g = META[name], golden(name)
+    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    if m["metric"] == "euclidean":
+        tu, phi, b = oracle.lsh_hash_euclid(X, g["V"], g["t"], g["w"][0, 0], g["r"], m["nb"])
+        assert np.array_equal(tu, g["tuples"])
+        assert np.array_equal(phi, g["phi"])
+    else:
+        b = oracle.lsh_hash_cosine(X, g["R"])
+        assert np.array_equal(b, g["phi"])
+    assert np.array_equal(b, g["bucket"])
+    rp, idx = oracle.bucket_csr(b, m["nb"])
+    # golden CSR is the concatenation over tables of nb buckets each
+    L, nb = m["L"], m["nb"]
+    gp, gi = g["members_ptr"], g["members_idx"]
+    for l in range(L):
+        assert np.array_equal(rp[l], gp[l * nb:(l + 1) * nb + 1] - gp[l * nb])
+        assert np.array_equal(idx[l], gi[gp[l * nb]:gp[(l + 1) * nb]])
+
+
+@pytest.mark.parametrize("name", cases("lsh"))
+def test_lsh_queries(name):
+    m, g = META[name], golden(name)
+    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    Qx = oracle.synth(m["query_seed"], m["Q"], m["d"])
+    allq = np.concatenate([X[:m["nqrows"]], Qx])
+    nb, L = m["nb"], m["L"]
+    if m["metric"] == "euclidean":
+        tu, _, b = oracle.lsh_hash_euclid(X, g["V"], g["t"], g["w"][0, 0], g["r"], nb)
+        qtu, _, qb = oracle.lsh_hash_euclid(allq, g["V"], g["t"], g["w"][0, 0], g["r"], nb)
+    else:
+        b = oracle.lsh_hash_cosine(X, g["R"]); qb = oracle.lsh_hash_cosine(allq, g["R"])
+        tu = qtu = None
+    rp, idx = oracle.bucket_csr(b, nb)
+    for kind in ("qfilt", "qunf"):
+        ptr, gidx = g[kind + "_ptr"], g[kind + "_idx"]
+        for q in range(allq.shape[0]):
+            filt = kind == "qfilt" and tu is not None
+            got = oracle.lsh_query(m["N"], nb, rp, idx, qb[q], tu if filt else None, qtu[q] if filt else None)
+            assert np.array_equal(got, gidx[ptr[q]:ptr[q + 1]]), (kind, q)
+
+
+@pytest.mark.parametrize("name", cases("cube"))
+def test_cube(name):
+    m, g = META[name], golden(name)
+    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    k = m["k"]
+    if m["metric"] == "euclidean":
+        V, t, st = oracle.gen_cube_euclid(m["seed"], k, m["d"], np.float32(m["w"]))
+        assert np.array_equal(V, g["V"]) and np.array_equal(t, g["t"])
+        h = oracle.cube_h(X, V, t, g["w"][0])
+        assert np.array_equal(h, g["h"])
+        memo = oracle.CoinMemo(k, st)
+        vertex, draws = memo.apply(h)
+        f, hh, bit = memo.as_lists()
+        o = np.lexsort((hh, f))
+        assert np.array_equal(f[o], g["memo_f"]) and np.array_equal(hh[o], g["memo_h"])
+        assert np.array_equal(bit[o], g["memo_bit"])
+        assert draws == len(g["memo_h"])
+    else:
+        R, _ = oracle.gen_cube_cosine(m["seed"], k, m["d"])
+        assert np.array_equal(R.view(np.uint64), g["R"].view(np.uint64))
+        vertex = oracle.cube_cosine(X, R)
+    assert np.array_equal(vertex, g["vertex"])
+    rp, idx = oracle.bucket_csr(vertex[:, None], 1 << k)
+    assert np.array_equal(rp[0], g["members_ptr"]) and np.array_equal(idx[0], g["members_idx"])
+    # probe queries (only the fully-seen ones are pinned: qmask)
+    Qx = oracle.synth(m["query_seed"], m["Q"], m["d"])
+    allq = np.concatenate([X[:m["nqrows"]], Qx])[g["qmask"].astype(bool)]
+    if m["metric"] == "euclidean":
+        qv, _ = memo.apply(oracle.cube_h(allq, V, t, g["w"][0]))
+        assert memo.as_lists()[0].size == len(g["memo_h"])  # no new draws for seen queries
+    else:
+        qv = oracle.cube_cosine(allq, R)
+    for p in m["probes"]:
+        ptr, gi = g[f"q_probes{p}_ptr"], g[f"q_probes{p}_idx"]
+        for q in range(allq.shape[0]):
+            seq = oracle.cube_probe_seq(qv[q], p, k)
+            got = np.concatenate([idx[0][rp[0][v]:rp[0][v + 1]] for v in seq])
+            assert np.array_equal(got, gi[ptr[q]:ptr[q + 1]]), (p, q)
+
+
+@pytest.mark.parametrize("name", cases("lloyd"))
+def test_lloyd_and_update(name):
+    m, g = META[name], golden(name)
+    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    C = g["centers0"]
+    src = g["src_rows"]
+    if m["init"] == "ext":
+        assert np.array_equal(C, g["ext_centers"])
+    for it in range(len(g["cont"])):
+        a, dist = oracle.lloyd_assign(X, C, m["metric"], src if it == 0 else None)
+        assert np.array_equal(a, g[f"assign{it}"]), it
+        assert np.array_equal(dist.view(np.uint64), g[f"dist{it}"].view(np.uint64)), it
+        Cn, cnt, cont = oracle.kmeans_update(X, a, C, m["metric"], m["min_dist"])
+        assert cont == bool(g["cont"][it])
+        C = Cn if cont else C
+        assert np.array_equal(C.view(np.uint64), g[f"centers{it + 1}"].view(np.uint64)), it
+
+
+def test_probe_sequence_rules():
+    # lsh_cube.hpp:148-150 quirk: probes == 1 skips Hamming distance 1.
+    assert list(oracle.cube_probe_seq(0, 1, 4)) == [0, 0b11]
+    assert list(oracle.cube_probe_seq(0, 0, 4)) == [0]
+    assert list(oracle.cube_probe_seq(0, 2, 4)) == [0, 1, 2]
+    # exhausted cube stops (lsh_cube.hpp:171-172): k=2 -> 3 neighbours max
+    assert list(oracle.cube_probe_seq(0, 50, 2)) == [0, 1, 2, 3]
+    # distance-2 order: (0,1),(0,2),(0,3),(1,2),...
+    assert list(oracle.cube_probe_seq(0, 6, 4))[5:] == [0b0011, 0b0101]
+
+
+def test_minstd_and_uniform_int():
+    import ctypes
+    s = ctypes.c_uint32(oracle.lib().or_minstd_seed(1))
+    # minstd_rand0 from seed 1: 16807, 282475249, ...
+    vals = [oracle.lib().or_uniform_int(ctypes.byref(s), 0, 2147483645) for _ in range(2)]
+    assert vals == [16806, 282475248]
+    assert oracle.lib().or_minstd_seed(0) == 1 and oracle.lib().or_minstd_seed(2147483647) == 1
