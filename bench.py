@@ -1,0 +1,211 @@
+"""Headline benchmark: point hash+assign ops/sec at d=128, N=10M per GPU, K=256.
+
+One step = one pass of the hot path over the rank's resident shard:
+  LSH hashing (L=5 tables x k=4 EuclideanH functions, w=0.4, nb = N_total/100:
+  k-tuples + bucket IDs)  +  Lloyd assignment over K=256 centroids (cluster ID +
+  exact-order fp64 distance).
+Points are synthetic (include/lshkm_synth.h), generated in HBM before timing.
+Multi-GPU: contiguous row shards, one process per GPU, no data-path collective
+(hash and assign are independent per point) -> weak scaling.
+
+python bench.py --gpus N --steps K --warmup W   (torch.distributed.run for N>1)
+"""
+import argparse
+import ctypes as C
+import importlib.util
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+D, L_TABLES, K_FUNCS, W, BUCKET_DIV, SEED_DATA, SEED_PARAMS = 128, 5, 4, 0.4, 100, 0x5EED, 12345
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+FP32_MFMA_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: FP32 matrix peak
+
+
+def load_pkg():
+    spec = importlib.util.spec_from_file_location("lshkm_amd", os.path.join(ROOT, "crypto-recommendation_amd", "lshkm.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(sample_hash, sample_assign, K):
+    """The reference's own CPU path (oracle/_ref/ref_harness: g++ -O0 as shipped,
+    1 thread) on a bounded sample; falls back to the C restatement (port)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if os.path.exists(harness):
+        out = subprocess.run([harness, "bench", str(sample_hash), str(sample_assign), str(K), str(SEED_DATA)],
+                             check=True, capture_output=True, text=True).stdout
+        res = json.loads(out.strip().splitlines()[-1])
+        kind, cores = "reference", 1
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        os.environ.setdefault("OMP_NUM_THREADS", "1")
+        X = oracle.synth(SEED_DATA, max(sample_hash, sample_assign), D)
+        V, t, r, _ = oracle.gen_lsh_euclid(SEED_PARAMS, L_TABLES, K_FUNCS, D, np.float32(W))
+        t0 = time.perf_counter()
+        oracle.lsh_hash_euclid(X[:sample_hash], V, t, np.float32(W), r, max(sample_hash // BUCKET_DIV, 1))
+        t1 = time.perf_counter()
+        rows = np.arange(K) * (sample_assign // K)
+        oracle.lloyd_assign(X[:sample_assign], X[rows].astype(np.float64), "euclidean", rows.astype(np.int32))
+        t2 = time.perf_counter()
+        res = dict(hash_pts=sample_hash, hash_s=t1 - t0, assign_pts=sample_assign, assign_s=t2 - t1)
+        kind, cores = "port", int(os.environ.get("OMP_NUM_THREADS", "1"))
+    per_pt = res["hash_s"] / res["hash_pts"] + res["assign_s"] / res["assign_pts"]
+    return {
+        "value": 1.0 / per_pt, "unit": "point hash+assign ops/s", "cores": cores, "kind": kind,
+        "sample": f"{res['hash_pts']} pts hashed (L=5,k=4) + {res['assign_pts']} pts assigned (K={K}), d=128, "
+                  f"1 thread, {platform.processor() or platform.machine()}; hash {res['hash_s']:.2f}s, "
+                  f"assign {res['assign_s']:.2f}s",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU")
+    ap.add_argument("--k", type=int, default=256, help="centroids")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-hash-sample", type=int, default=100_000)
+    ap.add_argument("--cpu-assign-sample", type=int, default=12_000)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 PMC passes (see profiles/)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    lk = load_pkg()
+    ctx = lk.Context(local)
+    lib = lk.lib()
+    N, K = args.n, args.k
+    N_total = N * world
+    nb = N_total // BUCKET_DIV
+
+    # Resident shard + parameters (untimed).
+    X = ctx.synth(SEED_DATA, N, D, row0=rank * N)
+    V, t, r, _ = lk.params_lsh_euclidean(SEED_PARAMS, L_TABLES, K_FUNCS, D, W)
+    lsh = lk.LSH(ctx, "euclidean", D, K_FUNCS, L_TABLES, nb, W, V=V, t=t, r=r)
+    rows = np.arange(K, dtype=np.int64) * (N_total // K)          # reference init: rows i*floor(N/K)
+    Cc = torch.empty((K, D), dtype=torch.float64, device=dev)
+    for i, row in enumerate(rows):                                 # centroids may live on other shards
+        Cc[i] = ctx.synth(SEED_DATA, 1, D, row0=int(row))[0].double()
+    src = np.array([row - rank * N if rank * N <= row < (rank + 1) * N else -1 for row in rows], np.int32)
+    tuples = torch.empty((N, L_TABLES, K_FUNCS), dtype=torch.int32, device=dev)
+    bucket = torch.empty((N, L_TABLES), dtype=torch.int32, device=dev)
+    assign = torch.empty((N,), dtype=torch.int32, device=dev)
+    dist_ = torch.empty((N,), dtype=torch.float64, device=dev)
+    p = lambda t_: C.c_void_p(t_.data_ptr())
+    src_p = src.ctypes.data_as(C.c_void_p)
+
+    def hash_step():
+        lk._ck(lib.lshkm_lsh_hash(lsh.h, p(X), N, p(tuples), None, p(bucket)))
+
+    def assign_step():
+        lk._ck(lib.lshkm_lloyd_assign(ctx.h, p(X), N, D, p(Cc), K, lk.EUCLIDEAN, src_p, p(assign), p(dist_)))
+
+    def step():
+        hash_step()
+        assign_step()
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ctx.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(e.item())
+    ambig = ctx.stat(lk.STAT_ASSIGN_AMBIG)
+    hexact = ctx.stat(lk.STAT_HASH_EXACT)
+
+    # Per-kernel timing with HIP events on the stream the kernels run on
+    # (the context runs on torch's current stream, so torch events bracket them).
+    reps = max(3, args.steps)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    for _ in range(reps):
+        assign_step()
+    ev[1].record()
+    for _ in range(reps):
+        hash_step()
+    ev[2].record()
+    torch.cuda.synchronize(dev)
+    t_assign = ev[0].elapsed_time(ev[1]) / reps / 1e3
+    t_hash = ev[1].elapsed_time(ev[2]) / reps / 1e3
+
+    assign_flops = 2.0 * D * K * N                     # 65,536 flop/pt at K=256
+    hash_bytes = N * (4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES)    # 612 B/pt
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("N") == N and tj.get("K") == K:
+            traffic = tj.get("assign_hbm_bytes_per_launch")
+
+    if rank == 0:
+        value = N_total * args.steps / elapsed
+        line = {
+            "metric": "point hash+assign ops/sec at d=128, N=10M, K=256; 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "point hash+assign ops/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32 storage; fp32-MFMA scores, fp64/x87-exact results",
+            "data": "synthetic (include/lshkm_synth.h), resident in HBM",
+            "config": {"workload": f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128",
+                       "N_per_gpu": N, "N_total": N_total, "d": D, "K": K, "L": L_TABLES, "k": K_FUNCS,
+                       "w": W, "nb": nb, "parallelism": f"dp{world} (row shards)"},
+            "roofline": {
+                "bound": "mfma", "kernel": "assign_mfma_kernel<128> (+prep/exact/override launches)",
+                "achieved": assign_flops / t_assign / 1e12, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": assign_flops / t_assign / 1e12 / FP32_MFMA_PEAK_TFS,
+                "traffic": traffic,
+                "assign_ms": t_assign * 1e3,
+                "hash_kernel": {"bound": "hbm", "achieved_GBs": hash_bytes / t_hash / 1e9, "peak_GBs": HBM_PEAK_GBS,
+                                "frac": hash_bytes / t_hash / 1e9 / HBM_PEAK_GBS, "hash_ms": t_hash * 1e3},
+            },
+            "exactness": {"assign_ambiguous_rows": ambig, "hash_exact_fallbacks": hexact},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample, K)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

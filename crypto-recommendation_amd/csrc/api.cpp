@@ -1,0 +1,315 @@
+// api.cpp — the C ABI (include/lshkm.h): contexts, handles, parameter
+// generation in the reference's RNG draw order, and stream-ordered launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/lshkm.h"
+#include "common.h"
+#include "kernels.h"
+#include "index.h"
+
+namespace lshkm {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+}  // namespace lshkm
+
+using namespace lshkm;
+
+// ---------------------------------------------------------------- device buffers
+namespace lshkm {
+
+Buf::~Buf() { if (p) hipFree(p); }
+int Buf::reserve(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) { hipFree(p); p = nullptr; cap = 0; }
+    if (hipMalloc(&p, bytes) != hipSuccess) { set_error("hipMalloc failed (" + std::to_string(bytes) + " B)"); p = nullptr; return LSHKM_ERR_NOMEM; }
+    cap = bytes;
+    return 0;
+}
+
+}  // namespace lshkm
+
+extern "C" {
+
+const char* lshkm_last_error(void) { return g_err.c_str(); }
+const char* lshkm_version(void) { return "lshkm-gfx950 0.1"; }
+
+int lshkm_ctx_create(int device, lshkm_ctx* out) {
+    LSHKM_CHECK(out, LSHKM_ERR_ARG, "out is NULL");
+    int n = 0;
+    LSHKM_HIP(hipGetDeviceCount(&n));
+    LSHKM_CHECK(device >= 0 && device < n, LSHKM_ERR_ARG, "device out of range");
+    LSHKM_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    LSHKM_HIP(hipGetDeviceProperties(&prop, device));
+    LSHKM_CHECK(std::string(prop.gcnArchName).find("gfx950") != std::string::npos, LSHKM_ERR_UNSUPPORTED,
+                std::string("liblshkm is built for gfx950 only; device is ") + prop.gcnArchName);
+    lshkm_ctx c = new lshkm_ctx_s();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; set_error("stream create failed"); return LSHKM_ERR_HIP; }
+    c->stream = c->own_stream;
+    if (c->stats.reserve(sizeof(unsigned long long) * STAT_COUNT)) { delete c; return LSHKM_ERR_NOMEM; }
+    hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * STAT_COUNT, c->stream);
+    *out = c;
+    return 0;
+}
+
+int lshkm_ctx_set_stream(lshkm_ctx ctx, void* s) {
+    LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
+    ctx->stream = (hipStream_t)s;   // verbatim: NULL is the default (null) stream
+    return 0;
+}
+
+int lshkm_ctx_sync(lshkm_ctx ctx) {
+    LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int lshkm_ctx_destroy(lshkm_ctx ctx) {
+    if (!ctx) return 0;
+    hipStreamSynchronize(ctx->stream);
+    if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return 0;
+}
+
+int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* v) {
+    LSHKM_CHECK(ctx && v && which >= 0 && which < STAT_COUNT, LSHKM_ERR_ARG, "bad stat query");
+    unsigned long long x = 0;
+    LSHKM_HIP(hipMemcpyAsync(&x, (unsigned long long*)ctx->stats.p + which, sizeof(x), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    *v = (int64_t)x;
+    return 0;
+}
+
+int lshkm_reset_stats(lshkm_ctx ctx) {
+    LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
+    LSHKM_HIP(hipMemsetAsync(ctx->stats.p, 0, sizeof(unsigned long long) * STAT_COUNT, ctx->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------ parameter generation
+// The reference's generators draw from one std::default_random_engine seeded
+// with the clock (lsh_cube.hpp:49-51); each EuclideanHGen owns a fresh
+// normal_distribution<float> (euclidean_h_gen.hpp:58) so an odd d drops the
+// cached second variate; CosineHGen likewise with double (cosine_h_gen.hpp:54).
+static uint32_t engine_state(std::default_random_engine& g) {
+    std::ostringstream os;
+    os << g;
+    return (uint32_t)std::stoul(os.str());
+}
+
+static void draw_euclid_h(std::default_random_engine& g, int d, float w, float* v, float* t) {
+    std::normal_distribution<float> nd(0, 1);
+    for (int j = 0; j < d; j++) v[j] = nd(g);
+    std::uniform_real_distribution<float> ud(0, w);
+    *t = ud(g);
+}
+
+static void draw_cosine_h(std::default_random_engine& g, int d, double* r) {
+    std::normal_distribution<double> nd(0, 1);
+    for (int j = 0; j < d; j++) r[j] = nd(g);
+}
+
+int lshkm_params_lsh_euclidean(uint64_t seed, int L, int k, int d, float w, float* V, float* t, int32_t* r,
+                               uint32_t* state) {
+    LSHKM_CHECK(L > 0 && k > 0 && d > 0 && V && t && r, LSHKM_ERR_ARG, "bad arguments");
+    std::default_random_engine g;
+    g.seed((unsigned long)seed);
+    for (int l = 0; l < L; l++) {
+        std::uniform_int_distribution<int> uid(0, 100);   // euclidean_phi_gen.hpp:63
+        for (int i = 0; i < k; i++) {
+            const size_t li = (size_t)l * k + i;
+            draw_euclid_h(g, d, w, V + li * d, t + li);
+            r[li] = uid(g);
+        }
+    }
+    if (state) *state = engine_state(g);
+    return 0;
+}
+
+int lshkm_params_lsh_cosine(uint64_t seed, int L, int k, int d, double* R, uint32_t* state) {
+    LSHKM_CHECK(L > 0 && k > 0 && d > 0 && R, LSHKM_ERR_ARG, "bad arguments");
+    std::default_random_engine g;
+    g.seed((unsigned long)seed);
+    for (int l = 0; l < L; l++)
+        for (int i = 0; i < k; i++) draw_cosine_h(g, d, R + ((size_t)l * k + i) * d);
+    if (state) *state = engine_state(g);
+    return 0;
+}
+
+int lshkm_params_cube_euclidean(uint64_t seed, int k, int d, float w, float* V, float* t, uint32_t* state) {
+    LSHKM_CHECK(k > 0 && d > 0 && V && t, LSHKM_ERR_ARG, "bad arguments");
+    std::default_random_engine g;
+    g.seed((unsigned long)seed);
+    for (int i = 0; i < k; i++) draw_euclid_h(g, d, w, V + (size_t)i * d, t + i);
+    if (state) *state = engine_state(g);
+    return 0;
+}
+
+int lshkm_params_cube_cosine(uint64_t seed, int k, int d, double* R, uint32_t* state) {
+    LSHKM_CHECK(k > 0 && d > 0 && R, LSHKM_ERR_ARG, "bad arguments");
+    std::default_random_engine g;
+    g.seed((unsigned long)seed);
+    for (int i = 0; i < k; i++) draw_cosine_h(g, d, R + (size_t)i * d);
+    if (state) *state = engine_state(g);
+    return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ projection tables
+namespace lshkm {
+
+int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float w_, const float* V, const float* t,
+                      const int32_t* r, const double* R) {
+    metric = metric_; d = d_; L = L_; k = k_; w = w_;
+    LK = L * k;
+    const int fpw = (LK + 3) / 4;
+    LKpad = 4 * fpw;
+    std::vector<double> PT((size_t)d * LKpad, 0.0), pn(LK, 0.0);
+    std::vector<float> tt(LK, 0.f);
+    std::vector<int32_t> rr(LK, 0);
+    for (int f = 0; f < LK; f++) {
+        long double n2 = 0.0L;
+        for (int j = 0; j < d; j++) {
+            const double v = metric == LSHKM_METRIC_EUCLIDEAN ? (double)V[(size_t)f * d + j] : R[(size_t)f * d + j];
+            PT[(size_t)j * LKpad + f] = v;
+            n2 += (long double)v * (long double)v;
+        }
+        pn[f] = (double)sqrtl(n2) * (1.0 + 0x1p-40);
+        if (metric == LSHKM_METRIC_EUCLIDEAN) { tt[f] = t ? t[f] : 0.f; rr[f] = r ? r[f] : 0; }
+    }
+    int rc;
+    if ((rc = PT_d.reserve(PT.size() * 8)) || (rc = t_d.reserve(LK * 4)) || (rc = pn_d.reserve(LK * 8)) ||
+        (rc = r_d.reserve(LK * 4)))
+        return rc;
+    LSHKM_HIP(hipMemcpyAsync(PT_d.p, PT.data(), PT.size() * 8, hipMemcpyHostToDevice, s));
+    LSHKM_HIP(hipMemcpyAsync(t_d.p, tt.data(), LK * 4, hipMemcpyHostToDevice, s));
+    LSHKM_HIP(hipMemcpyAsync(pn_d.p, pn.data(), LK * 8, hipMemcpyHostToDevice, s));
+    LSHKM_HIP(hipMemcpyAsync(r_d.p, rr.data(), LK * 4, hipMemcpyHostToDevice, s));
+    LSHKM_HIP(hipStreamSynchronize(s));   // host vectors go out of scope
+    // host copies kept for introspection
+    hV.assign(V ? V : (const float*)nullptr, V ? V + (size_t)LK * d : nullptr);
+    return 0;
+}
+
+HashParams ProjTable::params(int64_t nb) const {
+    HashParams p;
+    p.PT = (const double*)PT_d.p;
+    p.t = (const float*)t_d.p;
+    p.pnorm = (const double*)pn_d.p;
+    p.r = (const int32_t*)r_d.p;
+    p.w = w;
+    p.d = d; p.L = L; p.k = k; p.LK = LK; p.LKpad = LKpad;
+    p.nb = nb;
+    return p;
+}
+
+}  // namespace lshkm
+
+extern "C" {
+
+// ----------------------------------------------------------------------- LSH
+int lshkm_lsh_create(lshkm_ctx ctx, int metric, int d, int k, int L, int64_t nb, float w, const float* V,
+                     const float* t, const int32_t* r, const double* R, lshkm_lsh* out) {
+    LSHKM_CHECK(ctx && out, LSHKM_ERR_ARG, "ctx/out is NULL");
+    LSHKM_CHECK(d > 0 && d <= 1024 && k > 0 && L > 0 && L * k <= 256, LSHKM_ERR_ARG, "unsupported d/k/L");
+    LSHKM_CHECK(k <= 30, LSHKM_ERR_ARG, "k > 30");
+    if (metric == LSHKM_METRIC_EUCLIDEAN) {
+        LSHKM_CHECK(V && t && r, LSHKM_ERR_ARG, "euclidean LSH needs V, t, r");
+        LSHKM_CHECK(nb > 0 && nb < (1ll << 31), LSHKM_ERR_ARG, "nb must be in [1, 2^31)");   // mod by 0 crashes the reference
+        LSHKM_CHECK(w > 0.f, LSHKM_ERR_ARG, "w must be > 0");
+    } else if (metric == LSHKM_METRIC_COSINE) {
+        LSHKM_CHECK(R, LSHKM_ERR_ARG, "cosine LSH needs R");
+        nb = (int64_t)1 << k;
+    } else {
+        set_error("unknown metric");
+        return LSHKM_ERR_ARG;
+    }
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    lshkm_lsh h = new lshkm_lsh_s();
+    h->ctx = ctx; h->metric = metric; h->nb = nb;
+    int rc = h->proj.upload(ctx->stream, metric, d, L, k, w, V, t, r, R);
+    if (rc) { delete h; return rc; }
+    *out = h;
+    return 0;
+}
+
+int lshkm_lsh_destroy(lshkm_lsh lsh) {
+    if (!lsh) return 0;
+    (void)hipDeviceSynchronize();   // never touches lsh->ctx: it may already be destroyed
+    delete lsh;
+    return 0;
+}
+
+int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, int32_t* phi, int32_t* bucket) {
+    LSHKM_CHECK(lsh && (X || N == 0) && N >= 0, LSHKM_ERR_ARG, "bad arguments");
+    lshkm_ctx ctx = lsh->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    const int mode = lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE;
+    const int rc = launch_proj_hash(ctx->stream, mode, X, N, lsh->proj.params(lsh->nb),
+                                    mode == HM_LSH_EUCLID ? tuples : nullptr, phi, bucket,
+                                    (unsigned long long*)ctx->stats.p);
+    if (rc) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return 0;
+}
+
+// ------------------------------------------------------------------- Lloyd
+int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
+                       const int32_t* src_rows_host, int32_t* assign, double* dist) {
+    LSHKM_CHECK(ctx && X && C && assign && dist && N >= 0 && d > 0 && K > 0, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int DP = assign_dp(d);
+    int rc;
+    if (metric == LSHKM_METRIC_EUCLIDEAN && DP > 0) {
+        const int Kpad = (K + 63) / 64 * 64;
+        if ((rc = ctx->ws_c32.reserve((size_t)Kpad * DP * 4)) || (rc = ctx->ws_cconst.reserve((size_t)3 * Kpad * 4)) ||
+            (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 4)) ||
+            (rc = ctx->ws_counter.reserve(64)))
+            return rc;
+        unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
+        LSHKM_HIP(hipMemsetAsync(cnt, 0, 8, s));
+        if ((rc = launch_centroid_prep(s, C, K, Kpad, d, DP, metric, (float*)ctx->ws_c32.p, (float*)ctx->ws_cconst.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = launch_assign_mfma(s, X, N, d, DP, C, K, Kpad, (const float*)ctx->ws_c32.p, (const float*)ctx->ws_cconst.p,
+                                     assign, dist, (int32_t*)ctx->ws_ambig.p, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = launch_assign_exact(s, X, N, d, C, K, metric, (const int32_t*)ctx->ws_ambig.p, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        // ambiguous-count statistic
+        if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    } else {
+        // Exact reference-order pass over every centroid (cosine metric, or d > 256).
+        if ((rc = launch_assign_exact(s, X, N, d, C, K, metric, nullptr, nullptr, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    }
+    if (src_rows_host) {
+        if ((rc = ctx->ws_src.reserve((size_t)K * 4))) return rc;
+        // Stage through a pinned buffer so the caller's array may be freed at
+        // once and no stream sync is needed; the previous copy from the pinned
+        // buffer must have landed before we overwrite it.
+        if ((rc = ctx->pin_stage((size_t)K * 4))) return rc;
+        std::memcpy(ctx->pinned, src_rows_host, (size_t)K * 4);
+        LSHKM_HIP(hipMemcpyAsync(ctx->ws_src.p, ctx->pinned, (size_t)K * 4, hipMemcpyHostToDevice, s));
+        LSHKM_HIP(hipEventRecord(ctx->pinned_ev, s));
+        if ((rc = launch_assign_override(s, (const int32_t*)ctx->ws_src.p, K, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    }
+    return 0;
+}
+
+int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X) {
+    LSHKM_CHECK(ctx && X && rows >= 0 && d > 0, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc = launch_synth(ctx->stream, seed, row0, rows, d, X);
+    if (rc) { LSHKM_LAUNCH_CHECK(); }
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,328 @@
+// assign.hip — Lloyd's nearest-centroid assignment on gfx950.
+//
+// Replaces lloyds_assignment (lib/clustering_phases/assignment.hpp:54-80) with
+// CustVector::euclideanDistance (lib/data_structures/cust_vector.hpp:124-136)
+// and cosineDistance (:139-155).
+//
+// Fast path (euclidean): a block owns 128 points (4 waves x 32). Each wave keeps
+// its 32 points in registers as the B operand of v_mfma_f32_32x32x2_f32 (lane
+// half h holds dims [h*DP/2, (h+1)*DP/2) of point lane&31), centroids stream
+// through LDS in chunks of 64 as the A operand, and the accumulator tile
+// D[centroid][point] comes out with the point on the lane, so the per-point
+// reduction over centroids is register-local. The score is
+// s_c = ||c||^2 - 2 x.c; the MFMA result is an f32 FMA chain, so
+//   |s~_c - s_c| <= e_c = 2^-24 ((2DP+12) |x||c| + 5 ||c||^2) + 2^-40 (|x|^2+||c||^2)
+// covers the chain, the fp32 rounding of c, and the epilogue roundings; the
+// 2^-40 term also covers the reference's sequential-fp64 rounding and keeps
+// sqrt'ed ties apart. A point is certified when exactly one centroid has
+// s~_c - e_c <= min_c (s~_c + e_c); its distance is then recomputed in exact
+// reference order (fp64, no FMA contraction: sum_j (x_j - c_j)^2, j = 0..d-1,
+// then sqrt). Uncertified points (ties, duplicate centroids, near-ties) go
+// to assign_exact_kernel, which evaluates every centroid in reference order
+// and keeps the first minimum (strict '<', assignment.hpp:66).
+#include "common.h"
+#include "kernels.h"
+#include "softx87.h"
+
+namespace lshkm {
+
+constexpr int AS_THREADS = 256;
+constexpr int AS_PB = 128;   // points per block
+constexpr int AS_CC = 64;    // centroids per LDS chunk
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+int assign_dp(int d) {
+    const int dps[] = {16, 32, 64, 128, 256};
+    for (int dp : dps)
+        if (d <= dp) return dp;
+    return 0;
+}
+
+__global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, int DP,
+                                     float* __restrict__ C32, float* __restrict__ cconst) {
+    // One wave per 64-centroid chunk. cconst = cn2[Kpad] ++ {ecmax, ebmax}[Kpad/64]:
+    // the bound coefficients are taken as the max over the chunk, so the MFMA
+    // epilogue needs one per-lane bound per chunk instead of per centroid.
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    float* cn2 = cconst;
+    float* chunk = cconst + Kpad + 2 * blockIdx.x;
+    double ec = 0.0, eb = 0.0;
+    if (c >= K) {
+        for (int j = 0; j < DP; j++) C32[(size_t)c * DP + j] = 0.f;
+        cn2[c] = __builtin_inff();
+    } else {
+        double s = 0.0;
+        for (int j = 0; j < d; j++) {
+            const double v = C[(size_t)c * d + j];
+            s = fma(v, v, s);
+            C32[(size_t)c * DP + j] = (float)v;
+        }
+        for (int j = d; j < DP; j++) C32[(size_t)c * DP + j] = 0.f;
+        const double up = 1.0 + 0x1p-18;
+        const double nc = sqrt(s) * (1.0 + 0x1p-30);
+        cn2[c] = (float)s;
+        ec = 0x1p-24 * (2.0 * DP + 12.0) * nc * up;
+        eb = (0x1p-24 * 5.0 * s + 0x1p-40 * s) * up + 1e-30;
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        ec = fmax(ec, __shfl_xor(ec, off));
+        eb = fmax(eb, __shfl_xor(eb, off));
+    }
+    if (threadIdx.x == 0) {
+        chunk[0] = (float)(ec * (1.0 + 0x1p-20));
+        chunk[1] = (float)(eb * (1.0 + 0x1p-20));
+    }
+}
+
+int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d, int DP, int metric,
+                         float* C32, float* cconst) {
+    (void)metric;
+    hipLaunchKernelGGL(centroid_prep_kernel, dim3((Kpad + 63) / 64), dim3(64), 0, s, C, K, Kpad, d, DP, C32, cconst);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <int DP>
+__global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
+    const float* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int Kpad,
+    const float* __restrict__ C32, const float* __restrict__ cconst, int32_t* __restrict__ assign,
+    double* __restrict__ dist, int32_t* __restrict__ ambig, unsigned long long* __restrict__ ambig_count) {
+    constexpr int H = DP / 2;     // dims per lane half
+    constexpr int DS = DP + 4;    // padded LDS row stride (floats): conflict-free ds_read_b128
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    const int64_t pbase = (int64_t)blockIdx.x * AS_PB + wave * 32;
+
+    // ---- phase 0: this wave's 32 rows -> LDS -> registers (B operand)
+    float* xs = lds + wave * 32 * DS;
+    if (d == DP) {
+        for (int e4 = lane; e4 < 32 * DP / 4; e4 += 64) {
+            const int r = e4 / (DP / 4), j = (e4 % (DP / 4)) * 4;
+            const int64_t row = pbase + r;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < N) v = *reinterpret_cast<const float4*>(X + row * DP + j);
+            *reinterpret_cast<float4*>(xs + r * DS + j) = v;
+        }
+    } else {
+        for (int e = lane; e < 32 * DP; e += 64) {
+            const int r = e / DP, j = e % DP;
+            const int64_t row = pbase + r;
+            xs[r * DS + j] = (row < N && j < d) ? X[row * d + j] : 0.f;
+        }
+    }
+    __syncthreads();
+    float b[H];
+#pragma unroll
+    for (int s = 0; s < H; s += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(xs + col * DS + h * H + s);
+        b[s] = v.x; b[s + 1] = v.y; b[s + 2] = v.z; b[s + 3] = v.w;
+    }
+    double xn2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < H; s++) xn2 = fma((double)b[s], (double)b[s], xn2);
+    xn2 += __shfl_xor(xn2, 32);
+    const float nx = (float)(sqrt(xn2) * (1.0 + 0x1p-30));
+    const float ex = (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30);
+    __syncthreads();   // LDS now reused for centroid chunks
+
+    float L1 = __builtin_inff(), L2 = __builtin_inff(), U = __builtin_inff();
+    int i1 = 0;
+    float* cs = lds;                 // [64][DS]
+    float* cc = lds + AS_CC * DS;    // [64] cn2 of the chunk
+    const float* chunkc = cconst + Kpad;
+    for (int c0 = 0; c0 < Kpad; c0 += AS_CC) {
+        for (int e4 = threadIdx.x; e4 < AS_CC * DP / 4; e4 += AS_THREADS) {
+            const int r = e4 / (DP / 4), j = (e4 % (DP / 4)) * 4;
+            *reinterpret_cast<float4*>(cs + r * DS + j) =
+                *reinterpret_cast<const float4*>(C32 + (size_t)(c0 + r) * DP + j);
+        }
+        if (threadIdx.x < AS_CC) cc[threadIdx.x] = cconst[c0 + threadIdx.x];
+        const float E = fmaf(nx, chunkc[2 * (c0 / AS_CC)], chunkc[2 * (c0 / AS_CC) + 1] + ex);
+        __syncthreads();
+#pragma unroll 1
+        for (int t = 0; t < AS_CC / 32; t++) {
+            floatx16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[r] = 0.f;
+            const float* arow = cs + (t * 32 + col) * DS + h * H;
+#pragma unroll
+            for (int s = 0; s < H; s += 4) {
+                const float4 a = *reinterpret_cast<const float4*>(arow + s);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[s + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[s + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[s + 3], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int cb = t * 32 + 8 * g + 4 * h;   // D rows of registers 4g..4g+3
+                const float4 cn = *reinterpret_cast<const float4*>(cc + cb);
+                const float cnv[4] = {cn.x, cn.y, cn.z, cn.w};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float sc = fmaf(-2.f, acc[4 * g + q], cnv[q]);
+                    const float lo = sc - E, hi = sc + E;
+                    if (lo < L1) { L2 = L1; L1 = lo; i1 = c0 + cb + q; }
+                    else if (lo < L2) L2 = lo;
+                    U = fminf(U, hi);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- merge the two lane halves that share a point
+    const float oL1 = __shfl_xor(L1, 32), oL2 = __shfl_xor(L2, 32), oU = __shfl_xor(U, 32);
+    const int oi1 = __shfl_xor(i1, 32);
+    float nL2; int ni1;
+    if (oL1 < L1 || (oL1 == L1 && oi1 < i1)) { ni1 = oi1; nL2 = fminf(L1, oL2); }
+    else { ni1 = i1; nL2 = fminf(oL1, L2); }
+    U = fminf(U, oU);
+    const bool cert = nL2 > U;
+    const int64_t row = pbase + col;
+    const bool valid = row < N;
+
+    // ---- exact-order distance of the certified winner: lanes h=0 sum dims
+    // [0,H), hand the partial to lane h=1, which sums [H,2H) (j ascending).
+    double accd = 0.0;
+    if (h == 0 && cert && valid) {
+        const double* crow = C + (size_t)ni1 * d;
+#pragma unroll
+        for (int s = 0; s < H; s++)
+            if (s < d) {
+                const double df = __dsub_rn((double)b[s], crow[s]);
+                accd = __dadd_rn(accd, __dmul_rn(df, df));
+            }
+    }
+    const double part = __shfl_xor(accd, 32);
+    if (h == 1 && valid) {
+        if (cert) {
+            double a2 = part;
+            const double* crow = C + (size_t)ni1 * d;
+#pragma unroll
+            for (int s = 0; s < H; s++)
+                if (H + s < d) {
+                    const double df = __dsub_rn((double)b[s], crow[H + s]);
+                    a2 = __dadd_rn(a2, __dmul_rn(df, df));
+                }
+            assign[row] = ni1;
+            dist[row] = sqrt(a2);
+        } else {
+            const unsigned long long slot = atomicAdd(ambig_count, 1ull);
+            ambig[slot] = (int32_t)row;
+        }
+    }
+}
+
+int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, const double* C, int K,
+                       int Kpad, const float* C32, const float* cconst, int32_t* assign, double* dist,
+                       int32_t* ambig, unsigned long long* ambig_count) {
+    (void)K;
+    if (N <= 0) return 0;
+    const dim3 grid((unsigned)((N + AS_PB - 1) / AS_PB)), block(AS_THREADS);
+    const size_t lds = (size_t)4 * 32 * (DP + 4) * 4;   // >= chunk (64*(DP+4) + 192) floats
+    switch (DP) {
+#define AS_CASE(V) case V: hipLaunchKernelGGL(assign_mfma_kernel<V>, grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break;
+        AS_CASE(16) AS_CASE(32) AS_CASE(64) AS_CASE(128) AS_CASE(256)
+#undef AS_CASE
+        default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------- exact pass
+// One wave per listed row; lane c evaluates centroids c, c+64, ... in the
+// reference's exact order; the first minimum wins.
+__device__ inline double exact_euclid(const float* __restrict__ x, const double* __restrict__ c, int d) {
+    double acc = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double df = __dsub_rn((double)x[j], c[j]);
+        acc = __dadd_rn(acc, __dmul_rn(df, df));
+    }
+    return sqrt(acc);
+}
+
+__device__ inline double exact_cosine(const float* __restrict__ x, const double* __restrict__ c, int d) {
+    sx80 ip = sx_zero();
+    double a = 0.0, b = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j];
+        ip = sx_add_double(ip, __dmul_rn(xj, c[j]));
+        a = __dadd_rn(a, __dmul_rn(xj, xj));
+        b = __dadd_rn(b, __dmul_rn(c[j], c[j]));
+    }
+    const double denom = __dmul_rn(sqrt(a), sqrt(b));
+    const double q = sx_to_double(sx_div(ip, sx_from_double(denom)));
+    return __dsub_rn(1.0, q);
+}
+
+__global__ __launch_bounds__(256) void assign_exact_kernel(
+    const float* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int K, int metric,
+    const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,
+    int32_t* __restrict__ assign, double* __restrict__ dist) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wglobal = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    int64_t total = rows ? (int64_t)*row_count : N;
+    if (total > max_rows) total = max_rows;
+    for (int64_t it = wglobal; it < total; it += nw) {
+        const int64_t row = rows ? rows[it] : it;
+        const float* x = X + row * d;
+        double best = 0.0; int bi = -1;
+        for (int c = lane; c < K; c += 64) {
+            const double dd = metric == 0 ? exact_euclid(x, C + (size_t)c * d, d) : exact_cosine(x, C + (size_t)c * d, d);
+            if (bi < 0 || dd < best) { best = dd; bi = c; }
+        }
+        // wave argmin: smallest value, then smallest index (= first strict minimum in c order)
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ob = __shfl_xor(best, off);
+            const int oi = __shfl_xor(bi, off);
+            const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
+            if (take) { best = ob; bi = oi; }
+        }
+        if (lane == 0) {
+            assign[row] = bi < 0 ? 0 : bi;
+            dist[row] = bi < 0 ? -1.0 : best;
+        }
+    }
+}
+
+int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K, int metric,
+                        const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
+                        int32_t* assign, double* dist) {
+    if (max_rows <= 0) return 0;
+    const int64_t blocks = std::min<int64_t>((max_rows + 3) / 4, 2048);
+    hipLaunchKernelGGL(assign_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, N, d, C, K, metric,
+                       rows, row_count, max_rows, assign, dist);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Centroid override (assignment.hpp:77-78): in c order, so the last centroid
+// that points at a row wins.
+__global__ void assign_override_kernel(const int32_t* __restrict__ src, int K, int64_t N,
+                                       int32_t* __restrict__ assign, double* __restrict__ dist) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int c = 0; c < K; c++) {
+        const int32_t r = src[c];
+        if (r >= 0 && r < N) { assign[r] = c; dist[r] = 0.0; }
+    }
+}
+
+int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
+                           double* dist) {
+    hipLaunchKernelGGL(assign_override_kernel, dim3(1), dim3(64), 0, s, src_rows, K, N, assign, dist);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+__global__ void add_counter_kernel(unsigned long long* dst, const unsigned long long* src) {
+    if (threadIdx.x == 0) *dst += *src;
+}
+
+int launch_add_counter(hipStream_t s, unsigned long long* dst, const unsigned long long* src) {
+    hipLaunchKernelGGL(add_counter_kernel, dim3(1), dim3(1), 0, s, dst, src);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace lshkm

@@ -1,0 +1,89 @@
+// index.h — handle types behind the opaque C ABI pointers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+namespace lshkm {
+
+// Growable device buffer (never shrinks; freed with its owner).
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+    Buf() = default;
+    Buf(const Buf&) = delete;
+    Buf& operator=(const Buf&) = delete;
+    ~Buf();
+    int reserve(size_t bytes);
+    template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Device copy of a projection family: transposed fp64 projections + per-row
+// constants, as the hash kernel reads them.
+struct ProjTable {
+    int metric = 0, d = 0, L = 0, k = 0, LK = 0, LKpad = 0;
+    float w = 0.f;
+    Buf PT_d, t_d, pn_d, r_d;
+    std::vector<float> hV;
+    int upload(hipStream_t s, int metric, int d, int L, int k, float w, const float* V, const float* t,
+               const int32_t* r, const double* R);
+    HashParams params(int64_t nb) const;
+};
+
+}  // namespace lshkm
+
+struct lshkm_ctx_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    lshkm::Buf stats;            // STAT_COUNT x u64
+    // assignment workspace
+    lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src;
+    // scatter / query / update workspace
+    lshkm::Buf ws_a, ws_b, ws_c, ws_d, ws_e;
+    // pinned host staging for small host->device inputs
+    void* pinned = nullptr;
+    size_t pinned_cap = 0;
+    hipEvent_t pinned_ev = nullptr;
+    int pin_stage(size_t bytes) {
+        if (pinned_ev) (void)hipEventSynchronize(pinned_ev);
+        else if (hipEventCreateWithFlags(&pinned_ev, hipEventDisableTiming) != hipSuccess) return -2;
+        if (bytes <= pinned_cap) return 0;
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr; pinned_cap = 0;
+        if (hipHostMalloc(&pinned, bytes, hipHostMallocDefault) != hipSuccess) return -3;
+        pinned_cap = bytes;
+        return 0;
+    }
+    ~lshkm_ctx_s() {
+        if (pinned_ev) (void)hipEventSynchronize(pinned_ev), (void)hipEventDestroy(pinned_ev);
+        if (pinned) (void)hipHostFree(pinned);
+    }
+};
+
+struct lshkm_lsh_s {
+    lshkm_ctx_s* ctx = nullptr;
+    int metric = 0;
+    int64_t nb = 0;
+    lshkm::ProjTable proj;
+    // built index (lshkm_lsh_build)
+    int64_t N = 0;
+    lshkm::Buf tuples, bucket, row_ptr, idx;
+};
+
+struct lshkm_cube_s {
+    lshkm_ctx_s* ctx = nullptr;
+    int metric = 0;
+    int k = 0;
+    lshkm::ProjTable proj;
+    // lazy EuclideanF coin memo: memo[f][h - hmin] in {-1 (unseen), 0, 1}
+    int32_t hmin = 0, hspan = 0;
+    lshkm::Buf memo, first_row;
+    uint32_t rng_state = 1;
+    lshkm::Buf rng_d;             // device copy of the engine state
+    int64_t N = 0;
+    lshkm::Buf vertex, row_ptr, idx;
+};

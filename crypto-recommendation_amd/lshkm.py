@@ -1,0 +1,383 @@
+"""Python binding of liblshkm (the MI355X LSH / hypercube / k-means hot path).
+
+Thin ctypes layer over the C ABI in include/lshkm.h, used by the tests and
+bench.py. Device buffers are torch tensors on a ROCm device (PyTorch is the
+allocator and stream provider here, nothing more). The product is the HIP code
+in csrc/: if liblshkm.so is missing this module raises — there is no CPU
+fallback.
+
+Reference-named entry points mirror lib/lsh_cube.hpp and
+lib/clustering_phases/{assignment,update}.hpp (see the docstrings).
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblshkm.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "lshkm.h")
+
+EUCLIDEAN, COSINE = 0, 1
+STAT_HASH_EXACT, STAT_ASSIGN_AMBIG = 0, 1
+_METRIC = {"euclidean": EUCLIDEAN, "cosine": COSINE, EUCLIDEAN: EUCLIDEAN, COSINE: COSINE}
+
+_lib = None
+
+
+class LshkmError(RuntimeError):
+    pass
+
+
+def declared_symbols():
+    """Function names declared in include/lshkm.h."""
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(lshkm_\w+)\(", txt, re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LshkmError(f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        vp, i64, i32, u64, f32, f64 = C.c_void_p, C.c_int64, C.c_int, C.c_uint64, C.c_float, C.c_double
+        sigs = {
+            "lshkm_last_error": (C.c_char_p, []),
+            "lshkm_version": (C.c_char_p, []),
+            "lshkm_ctx_create": (i32, [i32, C.POINTER(vp)]),
+            "lshkm_ctx_set_stream": (i32, [vp, vp]),
+            "lshkm_ctx_sync": (i32, [vp]),
+            "lshkm_ctx_destroy": (i32, [vp]),
+            "lshkm_get_stat": (i32, [vp, i32, C.POINTER(i64)]),
+            "lshkm_reset_stats": (i32, [vp]),
+            "lshkm_params_lsh_euclidean": (i32, [u64, i32, i32, i32, f32, vp, vp, vp, C.POINTER(C.c_uint32)]),
+            "lshkm_params_lsh_cosine": (i32, [u64, i32, i32, i32, vp, C.POINTER(C.c_uint32)]),
+            "lshkm_params_cube_euclidean": (i32, [u64, i32, i32, f32, vp, vp, C.POINTER(C.c_uint32)]),
+            "lshkm_params_cube_cosine": (i32, [u64, i32, i32, vp, C.POINTER(C.c_uint32)]),
+            "lshkm_lsh_create": (i32, [vp, i32, i32, i32, i32, i64, f32, vp, vp, vp, vp, C.POINTER(vp)]),
+            "lshkm_lsh_destroy": (i32, [vp]),
+            "lshkm_lsh_hash": (i32, [vp, vp, i64, vp, vp, vp]),
+            "lshkm_lsh_build": (i32, [vp, vp, i64]),
+            "lshkm_lsh_get_buckets": (i32, [vp, i32, vp, vp]),
+            "lshkm_lsh_device_views": (i32, [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]),
+            "lshkm_lsh_query": (i32, [vp, vp, i64, vp, i32, vp, vp, i64, C.POINTER(i64)]),
+            "lshkm_cube_create": (i32, [vp, i32, i32, i32, f32, vp, vp, vp, C.c_uint32, C.POINTER(vp)]),
+            "lshkm_cube_destroy": (i32, [vp]),
+            "lshkm_cube_build": (i32, [vp, vp, i64]),
+            "lshkm_cube_vertices": (i32, [vp, vp, i64, vp]),
+            "lshkm_cube_get_buckets": (i32, [vp, vp, vp]),
+            "lshkm_cube_query": (i32, [vp, vp, i64, i32, vp, vp, i64, C.POINTER(i64)]),
+            "lshkm_cube_get_memo": (i32, [vp, vp, vp, vp, i64, C.POINTER(i64), C.POINTER(C.c_uint32)]),
+            "lshkm_lloyd_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp]),
+            "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
+            "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
+            "lshkm_kmeans_finalize": (i32, [vp, vp, vp, i32, i32, vp, i32, f64, vp, C.POINTER(i32)]),
+            "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
+        }
+        for name, (res, args) in sigs.items():
+            if not hasattr(L, name):
+                continue   # reported by tests/test_lib_cpu.py::test_exports
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ck(rc):
+    if rc != 0:
+        raise LshkmError(f"lshkm error {rc}: {lib().lshkm_last_error().decode()}")
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _t_ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+# ------------------------------------------------------------------ parameters
+def params_lsh_euclidean(seed, L, k, d, w):
+    V = np.empty((L, k, d), np.float32); t = np.empty((L, k), np.float32); r = np.empty((L, k), np.int32)
+    st = C.c_uint32()
+    _ck(lib().lshkm_params_lsh_euclidean(seed, L, k, d, float(np.float32(w)), _np_ptr(V), _np_ptr(t), _np_ptr(r), C.byref(st)))
+    return V, t, r, st.value
+
+
+def params_lsh_cosine(seed, L, k, d):
+    R = np.empty((L, k, d), np.float64); st = C.c_uint32()
+    _ck(lib().lshkm_params_lsh_cosine(seed, L, k, d, _np_ptr(R), C.byref(st)))
+    return R, st.value
+
+
+def params_cube_euclidean(seed, k, d, w):
+    V = np.empty((k, d), np.float32); t = np.empty((k,), np.float32); st = C.c_uint32()
+    _ck(lib().lshkm_params_cube_euclidean(seed, k, d, float(np.float32(w)), _np_ptr(V), _np_ptr(t), C.byref(st)))
+    return V, t, st.value
+
+
+def params_cube_cosine(seed, k, d):
+    R = np.empty((k, d), np.float64); st = C.c_uint32()
+    _ck(lib().lshkm_params_cube_cosine(seed, k, d, _np_ptr(R), C.byref(st)))
+    return R, st.value
+
+
+# --------------------------------------------------------------------- context
+class Context:
+    def __init__(self, device=0, use_torch_stream=True):
+        import torch
+        self.torch = torch
+        self.device = device
+        self.dev = torch.device("cuda", device)
+        h = C.c_void_p()
+        _ck(lib().lshkm_ctx_create(device, C.byref(h)))
+        self.h = h
+        if use_torch_stream:
+            _ck(lib().lshkm_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)))
+
+    def sync(self):
+        _ck(lib().lshkm_ctx_sync(self.h))
+
+    def stat(self, which):
+        v = C.c_int64()
+        _ck(lib().lshkm_get_stat(self.h, which, C.byref(v)))
+        return v.value
+
+    def reset_stats(self):
+        _ck(lib().lshkm_reset_stats(self.h))
+
+    def close(self):
+        if self.h:
+            lib().lshkm_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def empty(self, shape, dtype):
+        return self.torch.empty(shape, dtype=dtype, device=self.dev)
+
+    def synth(self, seed, rows, d, row0=0):
+        X = self.empty((rows, d), self.torch.float32)
+        _ck(lib().lshkm_synth(self.h, seed, row0, rows, d, _t_ptr(X)))
+        return X
+
+
+# ------------------------------------------------------------------------ LSH
+class LSH:
+    """A set of L hashtables (create_LSH_hashtables, lsh_cube.hpp:44-74)."""
+
+    def __init__(self, ctx, metric, d, k, L, nb=0, w=0.0, V=None, t=None, r=None, R=None):
+        self.ctx, self.metric, self.d, self.k, self.L = ctx, _METRIC[metric], d, k, L
+        self.nb = nb if self.metric == EUCLIDEAN else (1 << k)
+        self.w = float(np.float32(w))
+        keep = [np.ascontiguousarray(a, dt) if a is not None else None
+                for a, dt in ((V, np.float32), (t, np.float32), (r, np.int32), (R, np.float64))]
+        h = C.c_void_p()
+        _ck(lib().lshkm_lsh_create(ctx.h, self.metric, d, k, L, self.nb, self.w, *[_np_ptr(a) for a in keep], C.byref(h)))
+        self.h = h
+        self.N = 0
+
+    def close(self):
+        if self.h:
+            lib().lshkm_lsh_destroy(self.h)
+            self.h = None
+        self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def hash(self, X, tuples=True, phi=True, bucket=True):
+        torch = self.ctx.torch
+        N = X.shape[0]
+        tu = self.ctx.empty((N, self.L, self.k), torch.int32) if (tuples and self.metric == EUCLIDEAN) else None
+        ph = self.ctx.empty((N, self.L), torch.int32) if phi else None
+        bu = self.ctx.empty((N, self.L), torch.int32) if bucket else None
+        _ck(lib().lshkm_lsh_hash(self.h, _t_ptr(X), N, _t_ptr(tu), _t_ptr(ph), _t_ptr(bu)))
+        return tu, ph, bu
+
+    def build(self, X):
+        _ck(lib().lshkm_lsh_build(self.h, _t_ptr(X), X.shape[0]))
+        self.N = X.shape[0]
+
+    def buckets(self, table):
+        rp = np.empty(self.nb + 1, np.int64); idx = np.empty(max(self.N, 1), np.int32)
+        _ck(lib().lshkm_lsh_get_buckets(self.h, table, _np_ptr(rp), _np_ptr(idx)))
+        return rp, idx[:self.N]
+
+    def query(self, Q, filtered=True, alias_rows=None):
+        """Batched get_LSH_[filtered_]combined_buckets: returns (ptr[nq+1], idx) numpy."""
+        torch = self.ctx.torch
+        nq = Q.shape[0]
+        ptr = self.ctx.empty((nq + 1,), torch.int64)
+        total = C.c_int64()
+        _ck(lib().lshkm_lsh_query(self.h, _t_ptr(Q), nq, _t_ptr(alias_rows), int(filtered), _t_ptr(ptr), None, 0,
+                                  C.byref(total)))
+        out = self.ctx.empty((max(total.value, 1),), torch.int32)
+        _ck(lib().lshkm_lsh_query(self.h, _t_ptr(Q), nq, _t_ptr(alias_rows), int(filtered), _t_ptr(ptr), _t_ptr(out),
+                                  total.value, C.byref(total)))
+        self.ctx.sync()
+        return ptr.cpu().numpy(), out[:total.value].cpu().numpy()
+
+
+class Cube:
+    """The randomized hypercube (create_hypercube, lsh_cube.hpp:108-136)."""
+
+    def __init__(self, ctx, metric, d, k, w=0.0, V=None, t=None, R=None, rng_state=1):
+        self.ctx, self.metric, self.d, self.k = ctx, _METRIC[metric], d, k
+        keep = [np.ascontiguousarray(a, dt) if a is not None else None
+                for a, dt in ((V, np.float32), (t, np.float32), (R, np.float64))]
+        h = C.c_void_p()
+        _ck(lib().lshkm_cube_create(ctx.h, self.metric, d, k, float(np.float32(w)), *[_np_ptr(a) for a in keep],
+                                    rng_state, C.byref(h)))
+        self.h = h
+        self.N = 0
+
+    def close(self):
+        if self.h:
+            lib().lshkm_cube_destroy(self.h)
+            self.h = None
+        self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def build(self, X):
+        _ck(lib().lshkm_cube_build(self.h, _t_ptr(X), X.shape[0]))
+        self.N = X.shape[0]
+
+    def vertices(self, Q):
+        v = self.ctx.empty((Q.shape[0],), self.ctx.torch.int32)
+        _ck(lib().lshkm_cube_vertices(self.h, _t_ptr(Q), Q.shape[0], _t_ptr(v)))
+        return v
+
+    def buckets(self):
+        rp = np.empty((1 << self.k) + 1, np.int64); idx = np.empty(max(self.N, 1), np.int32)
+        _ck(lib().lshkm_cube_get_buckets(self.h, _np_ptr(rp), _np_ptr(idx)))
+        return rp, idx[:self.N]
+
+    def memo(self):
+        cnt = C.c_int64(); st = C.c_uint32()
+        _ck(lib().lshkm_cube_get_memo(self.h, None, None, None, 0, C.byref(cnt), C.byref(st)))
+        n = cnt.value
+        f = np.empty(max(n, 1), np.int32); hh = np.empty(max(n, 1), np.int32); b = np.empty(max(n, 1), np.int32)
+        _ck(lib().lshkm_cube_get_memo(self.h, _np_ptr(f), _np_ptr(hh), _np_ptr(b), n, C.byref(cnt), C.byref(st)))
+        return f[:n], hh[:n], b[:n], st.value
+
+    def query(self, Q, probes):
+        torch = self.ctx.torch
+        nq = Q.shape[0]
+        ptr = self.ctx.empty((nq + 1,), torch.int64)
+        total = C.c_int64()
+        _ck(lib().lshkm_cube_query(self.h, _t_ptr(Q), nq, probes, _t_ptr(ptr), None, 0, C.byref(total)))
+        out = self.ctx.empty((max(total.value, 1),), torch.int32)
+        _ck(lib().lshkm_cube_query(self.h, _t_ptr(Q), nq, probes, _t_ptr(ptr), _t_ptr(out), total.value,
+                                   C.byref(total)))
+        self.ctx.sync()
+        return ptr.cpu().numpy(), out[:total.value].cpu().numpy()
+
+
+# -------------------------------------------------------------------- k-means
+def lloyd_assign(ctx, X, Cc, metric="euclidean", src_rows=None, assign=None, dist=None):
+    """lloyds_assignment (assignment.hpp:54-80). Returns (assign int32, dist fp64) tensors."""
+    torch = ctx.torch
+    N, d = X.shape
+    K = Cc.shape[0]
+    assign = ctx.empty((N,), torch.int32) if assign is None else assign
+    dist = ctx.empty((N,), torch.float64) if dist is None else dist
+    sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
+    _ck(lib().lshkm_lloyd_assign(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _np_ptr(sr),
+                                 _t_ptr(assign), _t_ptr(dist)))
+    return assign, dist
+
+
+def kmeans_update(ctx, X, assign, C_old, metric="euclidean", min_dist=0.0):
+    """k_means (update.hpp:37-86). Returns (C_new, counts, cont)."""
+    torch = ctx.torch
+    N, d = X.shape
+    K = C_old.shape[0]
+    Cn = ctx.empty((K, d), torch.float64)
+    cnt = ctx.empty((K,), torch.int64)
+    cont = C.c_int()
+    _ck(lib().lshkm_kmeans_update(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), _t_ptr(C_old), K, _METRIC[metric],
+                                  float(min_dist), _t_ptr(Cn), _t_ptr(cnt), C.byref(cont)))
+    return Cn, cnt, bool(cont.value)
+
+
+def kmeans_partial(ctx, X, assign, K, sums=None, counts=None):
+    torch = ctx.torch
+    N, d = X.shape
+    sums = ctx.empty((K, d), torch.float64) if sums is None else sums
+    counts = ctx.empty((K,), torch.int64) if counts is None else counts
+    _ck(lib().lshkm_kmeans_partial(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K, _t_ptr(sums), _t_ptr(counts)))
+    return sums, counts
+
+
+def kmeans_finalize(ctx, sums, counts, C_old, metric="euclidean", min_dist=0.0):
+    torch = ctx.torch
+    K, d = sums.shape
+    Cn = ctx.empty((K, d), torch.float64)
+    cont = C.c_int()
+    _ck(lib().lshkm_kmeans_finalize(ctx.h, _t_ptr(sums), _t_ptr(counts), K, d, _t_ptr(C_old), _METRIC[metric],
+                                    float(min_dist), _t_ptr(Cn), C.byref(cont)))
+    return Cn, bool(cont.value)
+
+
+# ------------------------------------------------- reference-named mirrors
+def create_LSH_hashtables(ctx, X, metric_type, k, L, lsh_bucket_div, euclidean_h_w, seed):
+    """create_LSH_hashtables (lsh_cube.hpp:44-74) with an explicit seed in place of the clock."""
+    d = X.shape[1]
+    if metric_type == "euclidean":
+        V, t, r, _ = params_lsh_euclidean(seed, L, k, d, euclidean_h_w)
+        lsh = LSH(ctx, EUCLIDEAN, d, k, L, X.shape[0] // lsh_bucket_div, euclidean_h_w, V=V, t=t, r=r)
+    else:
+        R, _ = params_lsh_cosine(seed, L, k, d)
+        lsh = LSH(ctx, COSINE, d, k, L, R=R)
+    lsh.build(X)
+    return lsh
+
+
+def get_LSH_filtered_combined_buckets(lsh, Q, alias_rows=None):
+    return lsh.query(Q, True, alias_rows)
+
+
+def get_LSH_combined_buckets(lsh, Q, alias_rows=None):
+    return lsh.query(Q, False, alias_rows)
+
+
+def create_hypercube(ctx, X, metric_type, k, euclidean_h_w, seed):
+    """create_hypercube (lsh_cube.hpp:108-136) with an explicit seed."""
+    d = X.shape[1]
+    if metric_type == "euclidean":
+        V, t, st = params_cube_euclidean(seed, k, d, euclidean_h_w)
+        cube = Cube(ctx, EUCLIDEAN, d, k, euclidean_h_w, V=V, t=t, rng_state=st)
+    else:
+        R, st = params_cube_cosine(seed, k, d)
+        cube = Cube(ctx, COSINE, d, k, R=R, rng_state=st)
+    cube.build(X)
+    return cube
+
+
+def get_hypercube_combined_buckets(cube, Q, probes):
+    return cube.query(Q, probes)
+
+
+def lloyds_assignment(ctx, X, centroids, metric_type, src_rows=None):
+    return lloyd_assign(ctx, X, centroids, metric_type, src_rows)
+
+
+def k_means(ctx, X, assign, centers, metric_type, min_dist):
+    return kmeans_update(ctx, X, assign, centers, metric_type, min_dist)

@@ -1,0 +1,177 @@
+/*
+ * lshkm.h — C ABI of the MI355X (gfx950) LSH / hypercube / k-means hot path.
+ *
+ * Drop-in boundary for the reference's header-template interface
+ * (paths relative to the reference root):
+ *   create_LSH_hashtables            lib/lsh_cube.hpp:44-74
+ *   get_LSH_combined_buckets         lib/lsh_cube.hpp:77-90
+ *   get_LSH_filtered_combined_buckets lib/lsh_cube.hpp:93-106
+ *   create_hypercube                 lib/lsh_cube.hpp:108-136
+ *   get_hypercube_combined_buckets   lib/lsh_cube.hpp:139-177
+ *   lloyds_assignment                lib/clustering_phases/assignment.hpp:54-80
+ *   k_means                          lib/clustering_phases/update.hpp:37-86
+ *   HashGenerator plugin ABI         lib/generators/hash_generator.hpp:19-31
+ *   CustHashtable::getBucketFromIndex / getHash lib/data_structures/cust_hashtable.hpp:116-125
+ *
+ * Conventions
+ *   - Every function returns 0 on success or a negative LSHKM_ERR_* code;
+ *     lshkm_last_error() then describes it (thread-local).
+ *   - "_dev" pointers are device (HBM) pointers, "_host" pointers host memory.
+ *     Sizes are explicit. Device outputs are written asynchronously on the
+ *     context's stream; call lshkm_ctx_sync() before reading them on the host.
+ *   - Points are fp32 rows, N x d row-major (the reference's doubles hold
+ *     fp32-representable values). Centroids are fp64 rows, K x d.
+ *   - Bit-exact with the reference: tuples, phi, bucket IDs, bucket member
+ *     order, query results, hypercube vertices, probe order, cluster IDs.
+ *     Distances: exact-order fp64 (see DESIGN.md for the pow(x,2) note).
+ *   - One handle per thread; calls on a handle are serialised on its stream.
+ */
+#ifndef LSHKM_H
+#define LSHKM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSHKM_OK 0
+#define LSHKM_ERR_ARG (-1)
+#define LSHKM_ERR_HIP (-2)
+#define LSHKM_ERR_NOMEM (-3)
+#define LSHKM_ERR_UNSUPPORTED (-4)
+#define LSHKM_ERR_STATE (-5)
+
+#define LSHKM_METRIC_EUCLIDEAN 0
+#define LSHKM_METRIC_COSINE 1
+
+typedef struct lshkm_ctx_s* lshkm_ctx;
+typedef struct lshkm_lsh_s* lshkm_lsh;
+typedef struct lshkm_cube_s* lshkm_cube;
+
+/* ------------------------------------------------------------------ context */
+const char* lshkm_last_error(void);
+const char* lshkm_version(void);
+int lshkm_ctx_create(int device, lshkm_ctx* out);
+/* Run on a caller-owned hipStream_t (e.g. torch's current stream), used
+ * verbatim: NULL is the default (null) stream. A new context uses its own stream. */
+int lshkm_ctx_set_stream(lshkm_ctx ctx, void* hip_stream);
+int lshkm_ctx_sync(lshkm_ctx ctx);
+int lshkm_ctx_destroy(lshkm_ctx ctx);
+/* Counters: 0 = hash values resolved by the exact soft-x87 path,
+ * 1 = points whose argmin needed the exact all-centroid pass. */
+int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);
+int lshkm_reset_stats(lshkm_ctx ctx);
+
+/* ------------------------------------------- parameter generation (host)
+ * std::default_random_engine seeded with `seed`, draws in the reference's
+ * order; *rng_state_host receives the engine state after the last draw.
+ * Replaces the generator constructors:
+ *   EuclideanPhiGen  lib/generators/euclidean_phi_gen.hpp:59-71 (via euclidean_h_gen.hpp:56-69)
+ *   CosineGGen       lib/generators/cosine_g_gen.hpp:48-52     (via cosine_h_gen.hpp:53-60)
+ *   create_hypercube lib/lsh_cube.hpp:112-126                  (EuclideanFGen / CosineHGen) */
+int lshkm_params_lsh_euclidean(uint64_t seed, int L, int k, int d, float w,
+                               float* V_host /*[L][k][d]*/, float* t_host /*[L][k]*/,
+                               int32_t* r_host /*[L][k]*/, uint32_t* rng_state_host);
+int lshkm_params_lsh_cosine(uint64_t seed, int L, int k, int d, double* R_host /*[L][k][d]*/,
+                            uint32_t* rng_state_host);
+int lshkm_params_cube_euclidean(uint64_t seed, int k, int d, float w, float* V_host /*[k][d]*/,
+                                float* t_host /*[k]*/, uint32_t* rng_state_host);
+int lshkm_params_cube_cosine(uint64_t seed, int k, int d, double* R_host /*[k][d]*/,
+                             uint32_t* rng_state_host);
+
+/* ---------------------------------------------------------------- LSH index
+ * create_LSH_hashtables (lsh_cube.hpp:44-74): metric EUCLIDEAN uses
+ * EuclideanPhiGen with nb = N / lsh_bucket_div buckets; COSINE uses CosineGGen
+ * with 2^k buckets (nb ignored). Parameters are copied to the device.
+ * V/t/r for EUCLIDEAN, R for COSINE (the other may be NULL). */
+int lshkm_lsh_create(lshkm_ctx ctx, int metric, int d, int k, int L, int64_t nb, float w,
+                     const float* V_host, const float* t_host, const int32_t* r_host,
+                     const double* R_host, lshkm_lsh* out);
+int lshkm_lsh_destroy(lshkm_lsh lsh);
+/* Hash a batch without inserting: EuclideanPhiGen::generate
+ * (euclidean_phi_gen.hpp:77-92) + mod(phi, nb) (cust_hashtable.hpp:68).
+ * tuples_dev [N][L][k] (EUCLIDEAN only), phi_dev [N][L], bucket_dev [N][L];
+ * any output may be NULL. For COSINE phi == bucket == g. */
+int lshkm_lsh_hash(lshkm_lsh lsh, const float* X_dev, int64_t N, int32_t* tuples_dev,
+                   int32_t* phi_dev, int32_t* bucket_dev);
+/* Insert all N rows (create_LSH_hashtables' insert loop, lsh_cube.hpp:69-70):
+ * hashes, then a stable bucket scatter (member order = row order,
+ * vector_bucket.hpp:41-44). The dataset rows and their tuples stay
+ * device-resident in the handle (X_dev must stay valid for queries that use
+ * alias rows only through their tuples; it is not read again). */
+int lshkm_lsh_build(lshkm_lsh lsh, const float* X_dev, int64_t N);
+/* Bucket contents of one table (getBucketFromIndex, cust_hashtable.hpp:116-119):
+ * row_ptr_host [nb+1], idx_host [N]. */
+int lshkm_lsh_get_buckets(lshkm_lsh lsh, int table, int64_t* row_ptr_host, int32_t* idx_host);
+/* Device views of the built index (valid until destroy/rebuild). */
+int lshkm_lsh_device_views(lshkm_lsh lsh, const int64_t** row_ptr_dev /*[L][nb+1]*/,
+                           const int32_t** idx_dev /*[L][N]*/, const int32_t** tuples_dev /*[N][L][k]*/,
+                           const int32_t** bucket_dev /*[N][L]*/);
+/* Batched queries (get_LSH_filtered_combined_buckets, lsh_cube.hpp:93-106,
+ * or get_LSH_combined_buckets :77-90 when filtered == 0). Output per query:
+ * the deduplicated union of its L buckets, ascending row index (std::set
+ * order). alias_rows_dev[q] >= 0 says "query q has the ID of dataset row r":
+ * the reference's first-write-wins ID map (euclidean_phi_gen.hpp:94) then
+ * filters with row r's tuple. May be NULL.
+ * Two-phase: out_ptr_dev [nq+1] always written (prefix offsets); rows are
+ * written to out_idx_dev only if total <= out_cap. *total_host = total rows. */
+int lshkm_lsh_query(lshkm_lsh lsh, const float* Q_dev, int64_t nq, const int32_t* alias_rows_dev,
+                    int filtered, int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap,
+                    int64_t* total_host);
+
+/* ---------------------------------------------------------------- hypercube
+ * create_hypercube (lsh_cube.hpp:108-136): k EuclideanFGen (V,t,w + the lazy
+ * coin engine state rng_state) or k CosineHGen (R); 2^k buckets. */
+int lshkm_cube_create(lshkm_ctx ctx, int metric, int d, int k, float w, const float* V_host,
+                      const float* t_host, const double* R_host, uint32_t rng_state, lshkm_cube* out);
+int lshkm_cube_destroy(lshkm_cube cube);
+/* Insert N rows: vertices (HypercubeGen::generate, hypercube_gen.hpp:63-73)
+ * with EuclideanF coins drawn on first sight of each h in (row, f) order
+ * (euclidean_f_gen.hpp:65-79), then the stable scatter into 2^k buckets. */
+int lshkm_cube_build(lshkm_cube cube, const float* X_dev, int64_t N);
+/* Vertices of a query batch (getHash, cust_hashtable.hpp:122-125). Unseen h
+ * values draw new coins in (query, f) order from the continued engine. */
+int lshkm_cube_vertices(lshkm_cube cube, const float* Q_dev, int64_t nq, int32_t* vertex_dev);
+int lshkm_cube_get_buckets(lshkm_cube cube, int64_t* row_ptr_host /*[2^k+1]*/, int32_t* idx_host /*[N]*/);
+/* get_hypercube_combined_buckets (lsh_cube.hpp:139-177): main bucket then
+ * `probes` neighbours in get_num_hamming_dist_from order (utils.cpp:22-50),
+ * probes == 1 skipping distance 1 as the reference does. Two-phase like
+ * lshkm_lsh_query. */
+int lshkm_cube_query(lshkm_cube cube, const float* Q_dev, int64_t nq, int probes,
+                     int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap, int64_t* total_host);
+/* Coin memo export: f_host/h_host/bit_host [cap]; *count_host = entries. */
+int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f_host, int32_t* h_host, int32_t* bit_host,
+                        int64_t cap, int64_t* count_host, uint32_t* rng_state_host);
+
+/* ------------------------------------------------------------------ k-means
+ * lloyds_assignment (assignment.hpp:54-80): for each row the centroid with the
+ * smallest distance (strict '<', first index wins), its fp64 distance, then
+ * the centroid override: assign[src_rows[c]] = c, dist = 0 for c = 0..K-1
+ * (src_rows_host may be NULL; entries < 0 are ignored). */
+int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const double* C_dev,
+                       int K, int metric, const int32_t* src_rows_host, int32_t* assign_dev,
+                       double* dist_dev);
+/* k_means (update.hpp:37-86): exact-order per-cluster fp64 sums in row order,
+ * divided by the count unless empty; *cont_host = 1 iff some center moved
+ * more than min_dist. C_new_dev [K][d], counts_dev [K] (may be NULL). */
+int lshkm_kmeans_update(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
+                        const double* C_old_dev, int K, int metric, double min_dist,
+                        double* C_new_dev, int64_t* counts_dev, int* cont_host);
+/* Sharded update (fast mode): per-shard exact-order sums, no division.
+ * sums_dev [K][d], counts_dev [K]. Combine across ranks with an all-reduce,
+ * then lshkm_kmeans_finalize. */
+int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
+                         int K, double* sums_dev, int64_t* counts_dev);
+int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* counts_dev, int K, int d,
+                          const double* C_old_dev, int metric, double min_dist, double* C_new_dev,
+                          int* cont_host);
+
+/* ------------------------------------------------------------ synthetic data */
+/* include/lshkm_synth.h generator, rows [row0, row0+rows) into X_dev. */
+int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSHKM_H */

@@ -1,0 +1,85 @@
+// Host check of crypto-recommendation_amd/csrc/softx87.h against the real x87
+// long double: random + adversarial sums, divisions, floors and roundings.
+// Built and run by tests/test_softx87.py (CPU). Exit code 0 = all equal.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+#include "../crypto-recommendation_amd/csrc/softx87.h"
+
+static bool same(sx80 a, long double b) {
+    // compare via exact decomposition of b
+    if (b == 0) return a.m == 0;
+    int s = std::signbit(b) ? 1 : 0;
+    long double ab = std::fabs(b);
+    int ex;
+    long double fr = std::frexp(ab, &ex);            // ab = fr * 2^ex, fr in [0.5,1)
+    uint64_t m = (uint64_t)std::ldexp(fr, 64);       // exact: 64-bit significand
+    return a.s == s && a.m == m && a.e == ex - 64;
+}
+
+static long double to_ld(sx80 a) {
+    if (a.m == 0) return a.s ? -0.0L : 0.0L;
+    long double v = std::ldexp((long double)a.m, a.e);
+    return a.s ? -v : v;
+}
+
+int main(int argc, char** argv) {
+    long iters = argc > 1 ? atol(argv[1]) : 200000;
+    std::mt19937_64 rng(12345);
+    std::uniform_real_distribution<double> u(-1.0, 1.0);
+    std::uniform_int_distribution<int> ex(-40, 40);
+    long bad = 0, checks = 0;
+    for (long it = 0; it < iters; it++) {
+        // 1) sequential long-double sum of double products (the hash path)
+        int d = 1 + (int)(rng() % 130);
+        long double acc = 0.0L; sx80 sacc = sx_zero();
+        int mode = (int)(rng() % 4);
+        for (int j = 0; j < d; j++) {
+            double p;
+            if (mode == 0) p = (double)(float)u(rng) * (double)(float)u(rng);
+            else if (mode == 1) p = std::ldexp(u(rng), ex(rng));
+            else if (mode == 2) p = (j % 2 ? -1.0 : 1.0) * std::ldexp(1.0 + u(rng) * 1e-12, (int)(rng() % 3));   // cancellation
+            else p = std::ldexp(u(rng), -(int)(rng() % 70));
+            acc = acc + (long double)p;
+            sacc = sx_add_double(sacc, p);
+            checks++;
+            if (!same(sacc, acc)) { if (bad < 5) fprintf(stderr, "add mismatch it=%ld j=%d\n", it, j); bad++; sacc = sx_zero(); acc = 0; break; }
+        }
+        // 2) (acc + t) / w, floorl, int
+        float t = (float)std::fabs(u(rng)) * 4.0f, w = (float)(0.05 + std::fabs(u(rng)) * 4.0);
+        long double q = (acc + (long double)t) / (long double)w;
+        sx80 sq = sx_div(sx_add_double(sacc, (double)t), sx_from_float(w));
+        checks++;
+        if (!same(sq, q)) { if (bad < 5) fprintf(stderr, "div mismatch it=%ld\n", it); bad++; }
+        checks++;
+        if (fabsl(q) < 9.0e18L && (int64_t)floorl(q) != sx_floor_i64(sq)) { if (bad < 5) fprintf(stderr, "floor mismatch it=%ld\n", it); bad++; }
+        // 3) long double -> double
+        checks++;
+        double dq = (double)q, sd = sx_to_double(sq);
+        if (std::memcmp(&dq, &sd, 8) != 0) { if (bad < 5) fprintf(stderr, "to_double mismatch it=%ld\n", it); bad++; }
+        // 4) sign test
+        checks++;
+        if ((acc >= 0) != (bool)sx_ge_zero(sacc)) { bad++; }
+        // 5) division by a double (cosine distance: ld / double)
+        double den = std::ldexp(0.5 + std::fabs(u(rng)), ex(rng));
+        long double q2 = acc / (long double)den;
+        checks++;
+        if (!same(sx_div(sacc, sx_from_double(den)), q2)) { if (bad < 5) fprintf(stderr, "div2 mismatch it=%ld\n", it); bad++; }
+    }
+    // adversarial: values near integer boundaries for floor
+    for (int i = -2000; i <= 2000; i++) {
+        for (int k = -3; k <= 3; k++) {
+            long double v = (long double)i + (long double)k * std::ldexp(1.0L, -60);
+            double hi = (double)v; long double rest = v - (long double)hi;
+            sx80 s = sx_add_double(sx_from_double(hi), (double)rest);
+            long double ld = (long double)hi + (long double)(double)rest;
+            checks++;
+            if (!same(s, ld) || sx_floor_i64(s) != (int64_t)floorl(ld)) bad++;
+        }
+    }
+    printf("checks=%ld bad=%ld\n", checks, bad);
+    return bad ? 1 : 0;
+}

@@ -1,0 +1,153 @@
+"""GPU parity: projection hashes (LSH euclidean / cosine) and Lloyd assignment
+against the reference's golden outputs and the CPU oracle. Bit-exact on all
+integer outputs and on the fp64 distances."""
+import numpy as np
+import pytest
+
+import oracle
+from amd import lshkm
+from conftest import cases, golden, golden_meta
+
+META = golden_meta()
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return lshkm.Context(0)
+
+
+def to_dev(ctx, a):
+    return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+
+
+@pytest.mark.parametrize("name", cases("lsh"))
+def test_lsh_hash_golden(ctx, name):
+    m, g = META[name], golden(name)
+    X = to_dev(ctx, oracle.synth(m["data_seed"], m["N"], m["d"]))
+    if m["metric"] == "euclidean":
+        lsh = lshkm.LSH(ctx, "euclidean", m["d"], m["k"], m["L"], m["nb"], m["w"], V=g["V"], t=g["t"], r=g["r"])
+        tu, ph, bu = lsh.hash(X)
+        assert np.array_equal(tu.cpu().numpy(), g["tuples"])
+    else:
+        lsh = lshkm.LSH(ctx, "cosine", m["d"], m["k"], m["L"], R=g["R"])
+        _, ph, bu = lsh.hash(X)
+    assert np.array_equal(ph.cpu().numpy(), g["phi"])
+    assert np.array_equal(bu.cpu().numpy(), g["bucket"])
+
+
+def test_lsh_hash_large_vs_oracle(ctx):
+    # 200k points at the bench shape (d=128, L=5, k=4, w=0.4, nb=N/100); oracle = x87 restatement.
+    N, d, L, k = 200_000, 128, 5, 4
+    V, t, r, _ = lshkm.params_lsh_euclidean(12345, L, k, d, 0.4)
+    X = ctx.synth(0x5EED, N, d)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
+    tu, ph, bu = lsh.hash(X)
+    xt, xp, xb = oracle.lsh_hash_euclid(X.cpu().numpy(), V, t, np.float32(0.4), r, N // 100)
+    assert np.array_equal(tu.cpu().numpy(), xt)
+    assert np.array_equal(ph.cpu().numpy(), xp)
+    assert np.array_equal(bu.cpu().numpy(), xb)
+
+
+def _near_boundary_points(V, t, w, n, rng):
+    """Rows whose (v0.x + t)/w sits within ~1e-15 of an integer: forces the exact path."""
+    d = V.shape[-1]
+    v = V.reshape(-1, d)[0].astype(np.float64)
+    rows = []
+    for i in range(n):
+        x = np.zeros(d, np.float32)
+        target = float(rng.integers(-20, 20))
+        x[0] = np.float32((target * w - t.reshape(-1)[0]) / v[0])
+        res = (v[0] * np.float64(x[0]) + np.float64(t.reshape(-1)[0])) / w - target
+        x[1] = np.float32(-res * w / v[1])
+        res2 = (v[0] * np.float64(x[0]) + v[1] * np.float64(x[1]) + np.float64(t.reshape(-1)[0])) / w - target
+        x[2] = np.float32(-res2 * w / v[2])
+        rows.append(x)
+    return np.stack(rows)
+
+
+def test_hash_exact_path_forced(ctx):
+    d, L, k = 128, 1, 4
+    V, t, r, _ = lshkm.params_lsh_euclidean(99, L, k, d, 0.4)
+    X = _near_boundary_points(V, t, np.float32(0.4), 256, np.random.default_rng(0))
+    X = np.concatenate([X, np.zeros((8, d), np.float32)])
+    ctx.reset_stats()
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, 7, 0.4, V=V, t=t, r=r)
+    tu, ph, bu = lsh.hash(to_dev(ctx, X))
+    xt, xp, xb = oracle.lsh_hash_euclid(X, V, t, np.float32(0.4), r, 7)
+    assert np.array_equal(tu.cpu().numpy(), xt)
+    assert np.array_equal(ph.cpu().numpy(), xp)
+    assert ctx.stat(lshkm.STAT_HASH_EXACT) > 0
+    # cosine: the zero vector has an exactly-zero inner product (sign test at the boundary)
+    R, _ = lshkm.params_lsh_cosine(7, 2, 5, d)
+    cl = lshkm.LSH(ctx, "cosine", d, 5, 2, R=R)
+    Z = np.zeros((64, d), np.float32); Z[1:, :] = oracle.synth(5, 63, d)
+    ctx.reset_stats()
+    _, _, cb = cl.hash(to_dev(ctx, Z))
+    assert np.array_equal(cb.cpu().numpy(), oracle.lsh_hash_cosine(Z, R))
+    assert ctx.stat(lshkm.STAT_HASH_EXACT) >= 2
+
+
+@pytest.mark.parametrize("name", cases("lloyd"))
+def test_lloyd_golden(ctx, name):
+    m, g = META[name], golden(name)
+    X = to_dev(ctx, oracle.synth(m["data_seed"], m["N"], m["d"]))
+    for it in range(len(g["cont"])):
+        Cc = to_dev(ctx, g[f"centers{it}"])
+        src = g["src_rows"] if it == 0 else None
+        a, dist = lshkm.lloyd_assign(ctx, X, Cc, m["metric"], src)
+        assert np.array_equal(a.cpu().numpy(), g[f"assign{it}"]), it
+        gd, rd = dist.cpu().numpy(), g[f"dist{it}"]
+        fp32_centers = np.array_equal(g[f"centers{it}"], g[f"centers{it}"].astype(np.float32).astype(np.float64))
+        if fp32_centers or m["metric"] == "cosine" and it == 0:
+            # (x_j - c_j) is exact, so glibc pow(x,2) == x*x: bit-exact
+            assert np.array_equal(gd.view(np.uint64), rd.view(np.uint64)), it
+        else:
+            # General fp64 centroids: glibc pow(x,2) may differ from x*x by 1 ulp per
+            # term (DESIGN.md "Distances"); north-star tolerance is 1e-5 relative.
+            rel = np.abs(gd - rd) / np.maximum(np.abs(rd), 1e-300)
+            assert rel.max() <= 1e-14, (it, rel.max())
+            assert np.mean(gd != rd) < 0.05, it
+
+
+def test_lloyd_large_vs_oracle(ctx):
+    N, d, K = 100_000, 128, 256
+    X = ctx.synth(0x5EED, N, d)
+    rows = np.arange(K) * (N // K)
+    Cc = X[ctx.torch.from_numpy(rows.astype(np.int64)).to(ctx.dev)].double()
+    a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows.astype(np.int32))
+    sub = np.random.default_rng(1).choice(N, 3000, replace=False)
+    Xs = X.cpu().numpy()
+    oa, od = oracle.lloyd_assign(Xs[sub], Cc.cpu().numpy(), "euclidean", None)
+    ga, gd = a.cpu().numpy()[sub], dist.cpu().numpy()[sub]
+    over = np.isin(sub, rows)               # centroid rows are overridden to (c, 0)
+    assert np.array_equal(ga[~over], oa[~over])
+    assert np.array_equal(gd[~over].view(np.uint64), od[~over].view(np.uint64))
+    assert np.all(gd[over] == 0.0)
+
+
+def test_lloyd_general_fp64_centroids(ctx):
+    # centroids that are not fp32 values (after an update): distances keep exact-order fp64
+    N, d, K = 20_000, 128, 64
+    X = ctx.synth(3, N, d)
+    Cc = X[:K].double() * (1 + 1e-3) + 1e-5
+    a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
+    oa, od = oracle.lloyd_assign(X.cpu().numpy(), Cc.cpu().numpy(), "euclidean", None)
+    assert np.array_equal(a.cpu().numpy(), oa)
+    rel = np.abs(dist.cpu().numpy() - od) / np.maximum(od, 1e-300)
+    assert rel.max() <= 1e-15          # tolerance note: pow(x,2) vs x*x, DESIGN.md
+
+
+def test_lloyd_ties_and_duplicates(ctx):
+    N, d, K = 5000, 32, 16
+    X = ctx.synth(11, N, d)
+    rows = np.array([0, 1, 1, 2, 3, 3, 3, 4, 5, 6, 7, 8, 9, 9, 10, 11], np.int32)
+    Cc = X[ctx.torch.from_numpy(rows.astype(np.int64)).to(ctx.dev)].double()
+    ctx.reset_stats()
+    a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows)
+    oa, od = oracle.lloyd_assign(X.cpu().numpy(), Cc.cpu().numpy(), "euclidean", rows)
+    assert np.array_equal(a.cpu().numpy(), oa)
+    assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
+    assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0
