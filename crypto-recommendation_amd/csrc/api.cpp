@@ -173,9 +173,9 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
                       const int32_t* r, const double* R) {
     metric = metric_; d = d_; L = L_; k = k_; w = w_;
     LK = L * k;
-    const int fpw = (LK + 3) / 4;
-    LKpad = 4 * fpw;
-    std::vector<double> PT((size_t)d * LKpad, 0.0), pn(LK, 0.0);
+    LKpad = hash_lkpad(LK);
+    const int drows = (d + 3) / 4 * 4;    // zero pad rows: the kernel reads x in float4 steps
+    std::vector<double> PT((size_t)drows * LKpad, 0.0), pn(LK, 0.0);
     std::vector<float> tt(LK, 0.f);
     std::vector<int32_t> rr(LK, 0);
     for (int f = 0; f < LK; f++) {
@@ -210,6 +210,7 @@ HashParams ProjTable::params(int64_t nb) const {
     p.r = (const int32_t*)r_d.p;
     p.w = w;
     p.d = d; p.L = L; p.k = k; p.LK = LK; p.LKpad = LKpad;
+    p.dstride = (d + 3) / 4 * 4 + 4;
     p.nb = nb;
     return p;
 }

@@ -293,7 +293,9 @@ int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const d
                         const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                         int32_t* assign, double* dist) {
     if (max_rows <= 0) return 0;
-    const int64_t blocks = std::min<int64_t>((max_rows + 3) / 4, 2048);
+    // rows == NULL: every row (fallback path); else a device-counted list that is
+    // usually ~0.3% of the rows: one block per CU, waves loop over the list.
+    const int64_t blocks = std::min<int64_t>((max_rows + 3) / 4, rows ? 256 : 2048);
     hipLaunchKernelGGL(assign_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, N, d, C, K, metric,
                        rows, row_count, max_rows, assign, dist);
     return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -303,16 +305,19 @@ int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const d
 // that points at a row wins.
 __global__ void assign_override_kernel(const int32_t* __restrict__ src, int K, int64_t N,
                                        int32_t* __restrict__ assign, double* __restrict__ dist) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    for (int c = 0; c < K; c++) {
-        const int32_t r = src[c];
-        if (r >= 0 && r < N) { assign[r] = c; dist[r] = 0.0; }
-    }
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= K) return;
+    const int32_t r = src[c];
+    if (r < 0 || r >= N) return;
+    for (int c2 = c + 1; c2 < K; c2++)      // a later centroid on the same row wins
+        if (src[c2] == r) return;
+    assign[r] = c;
+    dist[r] = 0.0;
 }
 
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist) {
-    hipLaunchKernelGGL(assign_override_kernel, dim3(1), dim3(64), 0, s, src_rows, K, N, assign, dist);
+    hipLaunchKernelGGL(assign_override_kernel, dim3((K + 255) / 256), dim3(256), 0, s, src_rows, K, N, assign, dist);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

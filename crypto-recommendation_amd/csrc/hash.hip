@@ -30,57 +30,81 @@ namespace lshkm {
 
 constexpr int HASH_PB = 64;      // points per block
 constexpr int HASH_THREADS = 256;
-constexpr int HASH_FB = 8;       // projections accumulated per pass
 
-template <int MODE>
+// Per wave: FB projections (a contiguous, zero-padded column block of PT)
+// accumulated together; PT is __restrict__ const so its wave-uniform reads
+// become scalar (SMEM) loads that feed v_fma_f64 directly.
+template <int MODE, int FB>
 __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
-    const float* __restrict__ X, int64_t N, HashParams p, int32_t* __restrict__ out_h,
+    const float* __restrict__ X, int64_t N, const double* __restrict__ PT, const float* __restrict__ tvec,
+    const double* __restrict__ pnorm, const int32_t* __restrict__ rvec, HashParams p, int32_t* __restrict__ out_h,
     int32_t* __restrict__ out_phi, int32_t* __restrict__ out_bucket, unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int d = p.d, LK = p.LK, ds = d + 1;
-    float* xs = reinterpret_cast<float*>(smem);               // [64][d+1]
-    int32_t* hs = reinterpret_cast<int32_t*>(xs + HASH_PB * ds);  // [64][LK]
+    const int d = p.d, LK = p.LK, LKpad = p.LKpad, ds = p.dstride;   // ds = d rounded up to 4, + 4
+    float* xs = reinterpret_cast<float*>(smem);                       // [64][ds]
+    int32_t* hs = reinterpret_cast<int32_t*>(xs + HASH_PB * ds);      // [64][LK]
 
     const int64_t p0 = (int64_t)blockIdx.x * HASH_PB;
     const int npts = (int)min((int64_t)HASH_PB, N - p0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
 
-    // Stage rows: wave-strided rows, lane-strided columns (coalesced 256 B per instruction).
+    // Stage the block's rows (contiguous in HBM) into padded LDS rows.
     const float* src = X + p0 * d;
-    for (int pp = wave; pp < npts; pp += 4)
-        for (int j = lane; j < d; j += 64) xs[pp * ds + j] = src[(int64_t)pp * d + j];
+    if ((d & 3) == 0) {
+        const int d4 = d >> 2, tot4 = npts * d4;
+        for (int e4 = threadIdx.x; e4 < tot4; e4 += HASH_THREADS) {
+            const int r = e4 / d4, c = (e4 - r * d4) << 2;
+            *reinterpret_cast<float4*>(xs + r * ds + c) = *reinterpret_cast<const float4*>(src + (int64_t)e4 * 4);
+        }
+    } else {
+        for (int e = threadIdx.x; e < npts * d; e += HASH_THREADS) {
+            const int r = e / d, c = e - r * d;
+            xs[r * ds + c] = src[e];
+        }
+    }
+    for (int e = threadIdx.x; e < HASH_PB * (ds - d); e += HASH_THREADS) {   // zero the pad columns
+        const int r = e / (ds - d), c = d + (e - r * (ds - d));
+        xs[r * ds + c] = 0.f;
+    }
     __syncthreads();
 
-    const int fpw = (LK + 3) / 4;
-    const int f_begin = wave * fpw;
-    const int f_end = min(f_begin + fpw, LK);
     const bool valid = lane < npts;
     const float* xr = xs + (valid ? lane : 0) * ds;
+    const int chunks = LKpad / (4 * FB);
+    const int d4 = (d + 3) >> 2;
 
-    for (int fb = f_begin; fb < f_end; fb += HASH_FB) {
-        double acc[HASH_FB];
+    for (int ch = 0; ch < chunks; ch++) {
+        const int fb = (wave * chunks + ch) * FB;
+        if (fb >= LK) break;
+        double acc[FB];
 #pragma unroll
-        for (int u = 0; u < HASH_FB; u++) acc[u] = 0.0;
+        for (int u = 0; u < FB; u++) acc[u] = 0.0;
         double xn2 = 0.0;
-        const int cnt = min(HASH_FB, f_end - fb);
-        for (int j = 0; j < d; j++) {
-            const double xj = (double)xr[j];
-            xn2 = fma(xj, xj, xn2);
-            const double* prow = p.PT + (size_t)j * p.LKpad + fb;
+        // Constant address space: uniform reads here must become SMEM loads.
+        const __attribute__((address_space(4))) double* prow =
+            (const __attribute__((address_space(4))) double*)(PT + fb);
+        for (int j4 = 0; j4 < d4; j4++) {
+            const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * j4);
+            const float xa[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-            for (int u = 0; u < HASH_FB; u++)
-                if (u < cnt) acc[u] = fma(prow[u], xj, acc[u]);
+            for (int q = 0; q < 4; q++) {
+                const double xj = (double)xa[q];
+                xn2 = fma(xj, xj, xn2);
+#pragma unroll
+                for (int u = 0; u < FB; u++) acc[u] = fma(prow[u], xj, acc[u]);   // pad rows/cols are 0
+                prow += LKpad;
+            }
         }
         const double xn = sqrt(xn2) * (1.0 + 0x1p-40);
 #pragma unroll
-        for (int u = 0; u < HASH_FB; u++) {
-            if (u >= cnt) continue;
+        for (int u = 0; u < FB; u++) {
             const int f = fb + u;
-            const double P = p.pnorm[f] * xn;
+            if (f >= LK) break;
+            const double P = pnorm[f] * xn;
             int32_t hv;
             if (MODE == HM_LSH_EUCLID || MODE == HM_CUBE_EUCLID_H) {
-                const double tt = (double)p.t[f], ww = (double)p.w;
+                const double tt = (double)tvec[f], ww = (double)p.w;
                 const double y = (acc[u] + tt) / ww;
                 const double B = ((double)(d + 2) * 0x1p-52 * (P + fabs(tt))) / ww + fabs(y) * 0x1p-51;
                 const double lo = floor(y - B), hi = floor(y + B);
@@ -90,7 +114,7 @@ __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
                     // Exact: sequential x87 semantics (cust_vector.hpp:117-118, euclidean_h_gen.hpp:75).
                     sx80 s = sx_zero();
                     for (int j = 0; j < d; j++)
-                        s = sx_add_double(s, __dmul_rn(p.PT[(size_t)j * p.LKpad + f], (double)xr[j]));
+                        s = sx_add_double(s, __dmul_rn(PT[(size_t)j * LKpad + f], (double)xr[j]));
                     s = sx_add_double(s, tt);
                     hv = (int32_t)sx_floor_i64(sx_div(s, sx_from_float(p.w)));
                     if (valid) atomicAdd(stats + STAT_HASH_EXACT, 1ull);
@@ -102,7 +126,7 @@ __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
                 else {
                     sx80 s = sx_zero();
                     for (int j = 0; j < d; j++)
-                        s = sx_add_double(s, __dmul_rn(p.PT[(size_t)j * p.LKpad + f], (double)xr[j]));
+                        s = sx_add_double(s, __dmul_rn(PT[(size_t)j * LKpad + f], (double)xr[j]));
                     hv = sx_ge_zero(s) ? 1 : 0;
                     if (valid) atomicAdd(stats + STAT_HASH_EXACT, 1ull);
                 }
@@ -122,7 +146,7 @@ __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
             uint32_t hn = 0;
             for (int i = 0; i < k; i++) {
                 const int hi = hs[pp * LK + l * k + i];
-                const int64_t temp = (int64_t)(int32_t)((uint32_t)hi * (uint32_t)p.r[l * k + i]);  // int*int
+                const int64_t temp = (int64_t)(int32_t)((uint32_t)hi * (uint32_t)rvec[l * k + i]);  // int*int
                 hn += (uint32_t)(int32_t)((temp % M + M) % M);       // mod(long, int)
             }
             const uint32_t phi = (hn % 2147483647u + 2147483647u) % 2147483647u;  // mod(unsigned, int)
@@ -148,24 +172,38 @@ __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
     }
 }
 
+int hash_fb(int LK) {
+    const int fpw = (LK + 3) / 4;
+    return fpw <= 2 ? 2 : fpw <= 4 ? 4 : fpw <= 6 ? 6 : 8;
+}
+
+int hash_lkpad(int LK) {
+    const int fb = hash_fb(LK), fpw = (LK + 3) / 4;
+    return 4 * ((fpw + fb - 1) / fb) * fb;
+}
+
+template <int MODE>
+static void launch_mode(hipStream_t s, dim3 grid, dim3 block, size_t lds, const float* X, int64_t N,
+                        const HashParams& p, int32_t* out_h, int32_t* out_phi, int32_t* out_bucket,
+                        unsigned long long* stats) {
+    switch (hash_fb(p.LK)) {
+#define HF_CASE(FB) case FB: hipLaunchKernelGGL((proj_hash_kernel<MODE, FB>), grid, block, lds, s, X, N, p.PT, p.t, \
+                                              p.pnorm, p.r, p, out_h, out_phi, out_bucket, stats); break;
+        HF_CASE(2) HF_CASE(4) HF_CASE(6) HF_CASE(8)
+#undef HF_CASE
+    }
+}
+
 int launch_proj_hash(hipStream_t s, int mode, const float* X, int64_t N, const HashParams& p,
                      int32_t* out_h, int32_t* out_phi, int32_t* out_bucket, unsigned long long* stats) {
     if (N <= 0) return 0;
-    const size_t lds = (size_t)HASH_PB * (p.d + 1) * 4 + (size_t)HASH_PB * p.LK * 4;
+    const size_t lds = (size_t)HASH_PB * p.dstride * 4 + (size_t)HASH_PB * p.LK * 4;
     const dim3 grid((unsigned)((N + HASH_PB - 1) / HASH_PB)), block(HASH_THREADS);
     switch (mode) {
-        case HM_LSH_EUCLID:
-            hipLaunchKernelGGL(proj_hash_kernel<HM_LSH_EUCLID>, grid, block, lds, s, X, N, p, out_h, out_phi, out_bucket, stats);
-            break;
-        case HM_LSH_COSINE:
-            hipLaunchKernelGGL(proj_hash_kernel<HM_LSH_COSINE>, grid, block, lds, s, X, N, p, out_h, out_phi, out_bucket, stats);
-            break;
-        case HM_CUBE_EUCLID_H:
-            hipLaunchKernelGGL(proj_hash_kernel<HM_CUBE_EUCLID_H>, grid, block, lds, s, X, N, p, out_h, out_phi, out_bucket, stats);
-            break;
-        default:
-            hipLaunchKernelGGL(proj_hash_kernel<HM_CUBE_COSINE>, grid, block, lds, s, X, N, p, out_h, out_phi, out_bucket, stats);
-            break;
+        case HM_LSH_EUCLID: launch_mode<HM_LSH_EUCLID>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
+        case HM_LSH_COSINE: launch_mode<HM_LSH_COSINE>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
+        case HM_CUBE_EUCLID_H: launch_mode<HM_CUBE_EUCLID_H>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
+        default: launch_mode<HM_CUBE_COSINE>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

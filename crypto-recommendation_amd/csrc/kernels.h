@@ -20,8 +20,11 @@ struct HashParams {
     const int32_t* r;     // [LK]   (LSH euclidean)
     float w;
     int d, L, k, LK, LKpad;
+    int dstride;          // LDS row stride (floats): d rounded up to 4, plus 4
     int64_t nb;
 };
+int hash_fb(int LK);      // projections per accumulator block
+int hash_lkpad(int LK);   // padded PT row length
 
 int launch_proj_hash(hipStream_t s, int mode, const float* X, int64_t N, const HashParams& p,
                      int32_t* out_h, int32_t* out_phi, int32_t* out_bucket,
