@@ -306,7 +306,7 @@ int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
 }
 
 int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X) {
-    LSHKM_CHECK(ctx && X && rows >= 0 && d > 0, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(ctx && (X || rows == 0) && rows >= 0 && d > 0, LSHKM_ERR_ARG, "bad arguments");
     LSHKM_HIP(hipSetDevice(ctx->device));
     int rc = launch_synth(ctx->stream, seed, row0, rows, d, X);
     if (rc) { LSHKM_LAUNCH_CHECK(); }

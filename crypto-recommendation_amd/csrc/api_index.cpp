@@ -1,0 +1,391 @@
+// api_index.cpp — C ABI for index build / query (LSH, hypercube) and the
+// k-means update. Stream-ordered; host syncs only where a device-computed size
+// decides an allocation (query totals, coin counts, the continue flag).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/lshkm.h"
+#include "common.h"
+#include "index.h"
+#include "kernels.h"
+
+using namespace lshkm;
+
+namespace {
+
+// ctx->ws slot map
+enum { WS_QTUP = 0, WS_QBKT, WS_SIZES, WS_COFF, WS_KLIST, WS_KCNT, WS_QSZ, WS_SORT, WS_SKEYS, WS_ROWS, WS_CROW,
+       WS_SUMS, WS_CNTS, WS_FLAG, WS_H, WS_MASKS };
+
+template <typename T> T* slot(lshkm_ctx ctx, int i) { return ctx->ws[i].as<T>(); }
+
+int reserve(lshkm_ctx ctx, int i, size_t bytes) { return ctx->ws[i].reserve(std::max<size_t>(bytes, 64)); }
+
+int d2h(lshkm_ctx ctx, void* dst, const void* src, size_t bytes) {
+    LSHKM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+// Stable scatter of keys[i * kstride] in [0, nb) -> idx (row order kept) + row_ptr.
+int build_csr(lshkm_ctx ctx, const int32_t* keys, int64_t kstride, int64_t N, int64_t nb, int32_t* idx,
+              int64_t* row_ptr) {
+    int rc;
+    if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(N, nb))) || (rc = reserve(ctx, WS_SKEYS, (size_t)N * 4)))
+        return rc;
+    if (N > 0 && (rc = stable_sort_by_key(ctx->stream, keys, kstride, nullptr, N, nb, slot<int32_t>(ctx, WS_SKEYS), idx,
+                                          ctx->ws[WS_SORT].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if ((rc = launch_csr_bounds(ctx->stream, slot<int32_t>(ctx, WS_SKEYS), N, nb, row_ptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return 0;
+}
+
+// Probe masks of get_hypercube_combined_buckets: 0 first (main bucket), then
+// Hamming distance 1 (bit 0..k-1), 2 (lexicographic i<j), ... ; probes == 1
+// starts at distance 2 (lsh_cube.hpp:148-150); stops when the cube is exhausted.
+std::vector<int32_t> probe_masks(int probes, int k) {
+    std::vector<int32_t> m(1, 0);
+    int remaining = probes;
+    int dist = probes > 1 ? 1 : 2;
+    std::vector<int> comb(64);
+    while (remaining > 0 && dist <= k) {
+        for (int i = 0; i < dist; i++) comb[i] = i;
+        for (;;) {
+            int mask = 0;
+            for (int i = 0; i < dist; i++) mask |= 1 << comb[i];
+            m.push_back(mask);
+            if (--remaining == 0) break;
+            int p = dist - 1;
+            while (p >= 0 && comb[p] == k - dist + p) p--;
+            if (p < 0) break;
+            comb[p]++;
+            for (int q = p + 1; q < dist; q++) comb[q] = comb[q - 1] + 1;
+        }
+        dist++;
+    }
+    return m;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ----------------------------------------------------------------------- LSH
+int lshkm_lsh_build(lshkm_lsh lsh, const float* X, int64_t N) {
+    LSHKM_CHECK(lsh && (X || N == 0) && N >= 0 && N < (1ll << 31), LSHKM_ERR_ARG, "bad arguments");
+    lshkm_ctx ctx = lsh->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    const int L = lsh->proj.L, k = lsh->proj.k;
+    const int64_t nb = lsh->nb;
+    int rc;
+    if ((rc = lsh->bucket.reserve((size_t)std::max<int64_t>(N, 1) * L * 4)) ||
+        (rc = lsh->row_ptr.reserve((size_t)L * (nb + 1) * 8)) || (rc = lsh->idx.reserve((size_t)std::max<int64_t>(N, 1) * L * 4)))
+        return rc;
+    if (lsh->metric == LSHKM_METRIC_EUCLIDEAN && (rc = lsh->tuples.reserve((size_t)std::max<int64_t>(N, 1) * L * k * 4))) return rc;
+    const int mode = lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE;
+    if ((rc = launch_proj_hash(ctx->stream, mode, X, N, lsh->proj.params(nb),
+                               mode == HM_LSH_EUCLID ? lsh->tuples.as<int32_t>() : nullptr, nullptr,
+                               lsh->bucket.as<int32_t>(), (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    for (int l = 0; l < L; l++)
+        if ((rc = build_csr(ctx, lsh->bucket.as<int32_t>() + l, L, N, nb, lsh->idx.as<int32_t>() + (size_t)l * N,
+                            lsh->row_ptr.as<int64_t>() + (size_t)l * (nb + 1)))) return rc;
+    lsh->N = N;
+    lsh->built = 1;
+    return 0;
+}
+
+int lshkm_lsh_get_buckets(lshkm_lsh lsh, int table, int64_t* row_ptr, int32_t* idx) {
+    LSHKM_CHECK(lsh && lsh->built && table >= 0 && table < lsh->proj.L, LSHKM_ERR_ARG, "not built / bad table");
+    lshkm_ctx ctx = lsh->ctx;
+    const int64_t nb = lsh->nb, N = lsh->N;
+    int rc;
+    if (row_ptr && (rc = d2h(ctx, row_ptr, lsh->row_ptr.as<int64_t>() + (size_t)table * (nb + 1), (size_t)(nb + 1) * 8))) return rc;
+    if (idx && N > 0 && (rc = d2h(ctx, idx, lsh->idx.as<int32_t>() + (size_t)table * N, (size_t)N * 4))) return rc;
+    return 0;
+}
+
+int lshkm_lsh_device_views(lshkm_lsh lsh, const int64_t** row_ptr, const int32_t** idx, const int32_t** tuples,
+                           const int32_t** bucket) {
+    LSHKM_CHECK(lsh && lsh->built, LSHKM_ERR_STATE, "index not built");
+    if (row_ptr) *row_ptr = lsh->row_ptr.as<int64_t>();
+    if (idx) *idx = lsh->idx.as<int32_t>();
+    if (tuples) *tuples = lsh->metric == LSHKM_METRIC_EUCLIDEAN ? lsh->tuples.as<int32_t>() : nullptr;
+    if (bucket) *bucket = lsh->bucket.as<int32_t>();
+    return 0;
+}
+
+int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* alias, int filtered, int64_t* out_ptr,
+                    int32_t* out_idx, int64_t out_cap, int64_t* total_host) {
+    LSHKM_CHECK(lsh && lsh->built, LSHKM_ERR_STATE, "index not built (lshkm_lsh_build)");
+    LSHKM_CHECK((Q || nq == 0) && nq >= 0 && out_ptr && total_host, LSHKM_ERR_ARG, "bad arguments");
+    lshkm_ctx ctx = lsh->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int L = lsh->proj.L, k = lsh->proj.k;
+    const int64_t nb = lsh->nb, pairs = nq * L;
+    const bool eu = lsh->metric == LSHKM_METRIC_EUCLIDEAN;
+    int rc;
+    if (nq == 0) {
+        LSHKM_HIP(hipMemsetAsync(out_ptr, 0, 8, s));
+        *total_host = 0;
+        return 0;
+    }
+    if ((rc = reserve(ctx, WS_QTUP, (size_t)pairs * k * 4)) || (rc = reserve(ctx, WS_QBKT, (size_t)pairs * 4)) ||
+        (rc = reserve(ctx, WS_SIZES, (size_t)pairs * 8)) || (rc = reserve(ctx, WS_COFF, (size_t)(pairs + 1) * 8)) ||
+        (rc = reserve(ctx, WS_KCNT, (size_t)pairs * 8)) || (rc = reserve(ctx, WS_QSZ, (size_t)nq * 8)))
+        return rc;
+    if (nq > 0 && (rc = launch_proj_hash(s, eu ? HM_LSH_EUCLID : HM_LSH_COSINE, Q, nq, lsh->proj.params(nb),
+                                         eu ? slot<int32_t>(ctx, WS_QTUP) : nullptr, nullptr, slot<int32_t>(ctx, WS_QBKT),
+                                         (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    auto run = [&](int phase, int32_t* out) {
+        return launch_lsh_query(s, slot<int32_t>(ctx, WS_QBKT), slot<int32_t>(ctx, WS_QTUP), alias, nq, L, k, nb,
+                                eu && filtered ? 1 : 0, lsh->N, eu ? lsh->tuples.as<int32_t>() : nullptr,
+                                lsh->bucket.as<int32_t>(), lsh->row_ptr.as<int64_t>(), lsh->idx.as<int32_t>(),
+                                slot<int64_t>(ctx, WS_SIZES), slot<int64_t>(ctx, WS_COFF), slot<int32_t>(ctx, WS_KLIST),
+                                slot<int64_t>(ctx, WS_KCNT), slot<int64_t>(ctx, WS_QSZ), out_ptr, out, phase);
+    };
+    if ((rc = run(0, nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    int64_t cand = 0;
+    if ((rc = d2h(ctx, &cand, slot<int64_t>(ctx, WS_COFF) + pairs, 8))) return rc;
+    if ((rc = reserve(ctx, WS_KLIST, (size_t)cand * 4))) return rc;
+    if ((rc = run(1, nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    int64_t total = 0;
+    if ((rc = d2h(ctx, &total, out_ptr + nq, 8))) return rc;
+    *total_host = total;
+    if (out_idx && total <= out_cap && total > 0)
+        if ((rc = run(2, out_idx))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return 0;
+}
+
+// ----------------------------------------------------------------- hypercube
+int lshkm_cube_create(lshkm_ctx ctx, int metric, int d, int k, float w, const float* V, const float* t, const double* R,
+                      uint32_t rng_state, lshkm_cube* out) {
+    LSHKM_CHECK(ctx && out && d > 0 && d <= 1024 && k > 0 && k <= 30, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN ? (V && t && w > 0.f) : (metric == LSHKM_METRIC_COSINE && R),
+                LSHKM_ERR_ARG, "euclidean cube needs V, t, w > 0; cosine cube needs R");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    lshkm_cube c = new lshkm_cube_s();
+    c->ctx = ctx; c->metric = metric; c->k = k;
+    std::vector<int32_t> r0(k, 0);
+    int rc = c->proj.upload(ctx->stream, metric, d, 1, k, w, V, t, r0.data(), R);
+    if (!rc) rc = c->rng_d.reserve(64);
+    if (!rc) rc = c->mm.reserve(64);
+    if (!rc) rc = c->cnt.reserve(64);
+    if (rc) { delete c; return rc; }
+    if (hipMemcpy(c->rng_d.p, &rng_state, 4, hipMemcpyHostToDevice) != hipSuccess) { delete c; set_error("copy failed"); return LSHKM_ERR_HIP; }
+    *out = c;
+    return 0;
+}
+
+int lshkm_cube_destroy(lshkm_cube cube) {
+    if (!cube) return 0;
+    (void)hipDeviceSynchronize();
+    delete cube;
+    return 0;
+}
+
+// Vertices of N rows, drawing the F coins of unseen h values in (row, f) order.
+static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_t* vertex) {
+    lshkm_ctx ctx = cube->ctx;
+    hipStream_t s = ctx->stream;
+    const int k = cube->k;
+    int rc;
+    if (N == 0) return 0;
+    if (cube->metric == LSHKM_METRIC_COSINE) {
+        if ((rc = launch_proj_hash(s, HM_CUBE_COSINE, X, N, cube->proj.params(1ll << k), vertex, nullptr, nullptr,
+                                   (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        return 0;
+    }
+    LSHKM_CHECK(N * k < (1ll << 31), LSHKM_ERR_UNSUPPORTED, "rows * k must be < 2^31");
+    if ((rc = reserve(ctx, WS_H, (size_t)N * k * 4))) return rc;
+    int32_t* h = slot<int32_t>(ctx, WS_H);
+    if ((rc = launch_proj_hash(s, HM_CUBE_EUCLID_H, X, N, cube->proj.params(1ll << k), h, nullptr, nullptr,
+                               (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    // window of the dense memo: grow (re-home) when the batch's h range leaves it
+    const int32_t init_mm[2] = {0x7FFFFFFF, (int32_t)0x80000000};
+    LSHKM_HIP(hipMemcpyAsync(cube->mm.p, init_mm, 8, hipMemcpyHostToDevice, s));
+    if ((rc = launch_h_minmax(s, h, N * k, cube->mm.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    int32_t mm[2];
+    if ((rc = d2h(ctx, mm, cube->mm.p, 8))) return rc;
+    if (cube->hspan == 0 || mm[0] < cube->hmin || mm[1] >= cube->hmin + cube->hspan) {
+        const int64_t lo = cube->hspan ? std::min<int64_t>(cube->hmin, mm[0]) : mm[0];
+        const int64_t hi = cube->hspan ? std::max<int64_t>((int64_t)cube->hmin + cube->hspan - 1, mm[1]) : mm[1];
+        const int64_t margin = std::max<int64_t>(64, (hi - lo) / 2);
+        const int64_t nlo = lo - margin, nspan = hi - lo + 1 + 2 * margin;
+        LSHKM_CHECK(nspan < (1 << 26), LSHKM_ERR_UNSUPPORTED, "h range too wide for the dense coin memo");
+        if ((rc = cube->memo2.reserve((size_t)k * nspan * 4))) return rc;
+        if ((rc = launch_memo_rehome(s, cube->hspan ? cube->memo.as<int32_t>() : nullptr, cube->hmin, cube->hspan,
+                                     cube->memo2.as<int32_t>(), (int32_t)nlo, (int32_t)nspan, k))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        std::swap(cube->memo.p, cube->memo2.p);
+        std::swap(cube->memo.cap, cube->memo2.cap);
+        cube->hmin = (int32_t)nlo;
+        cube->hspan = (int32_t)nspan;
+        if ((rc = cube->first_row.reserve((size_t)k * nspan * 4))) return rc;
+        LSHKM_HIP(hipMemsetAsync(cube->first_row.p, 0x7F, (size_t)k * nspan * 4, s));   // 0x7F7F7F7F > any row
+    }
+    const int64_t total = (int64_t)k * cube->hspan;
+    // first occurrence of each unseen (f, h), then the sorted draw
+    LSHKM_HIP(hipMemsetAsync(cube->first_row.p, 0x7F, (size_t)total * 4, s));
+    if ((rc = launch_coin_first(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), cube->first_row.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    LSHKM_HIP(hipMemsetAsync(cube->cnt.p, 0, 4, s));
+    const int64_t maxe = std::min<int64_t>(total, N * k);
+    if ((rc = reserve(ctx, WS_SIZES, (size_t)maxe * 4)) || (rc = reserve(ctx, WS_COFF, (size_t)maxe * 4)) ||
+        (rc = reserve(ctx, WS_KLIST, (size_t)maxe * 4)) || (rc = reserve(ctx, WS_KCNT, (size_t)maxe * 4)))
+        return rc;
+    if ((rc = launch_coin_collect(s, cube->first_row.as<int32_t>(), total, k, cube->hspan, slot<int32_t>(ctx, WS_SIZES),
+                                        slot<int32_t>(ctx, WS_COFF), cube->cnt.as<unsigned int>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    unsigned int ncoins = 0;
+    if ((rc = d2h(ctx, &ncoins, cube->cnt.p, 4))) return rc;
+    if (ncoins > 0) {
+        if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(ncoins, N * k)))) return rc;
+        if ((rc = stable_sort_by_key(s, slot<int32_t>(ctx, WS_SIZES), 1, slot<int32_t>(ctx, WS_COFF), ncoins, N * k,
+                                     slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT), ctx->ws[WS_SORT].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = launch_coin_draw(s, slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>(), cube->hmin, cube->hspan,
+                                   cube->memo.as<int32_t>(), cube->rng_d.as<uint32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    }
+    if ((rc = launch_coin_vertex(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), vertex))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return 0;
+}
+
+int lshkm_cube_build(lshkm_cube cube, const float* X, int64_t N) {
+    LSHKM_CHECK(cube && (X || N == 0) && N >= 0 && N < (1ll << 31), LSHKM_ERR_ARG, "bad arguments");
+    lshkm_ctx ctx = cube->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    const int64_t nb = 1ll << cube->k;
+    int rc;
+    if ((rc = cube->vertex.reserve((size_t)std::max<int64_t>(N, 1) * 4)) || (rc = cube->idx.reserve((size_t)std::max<int64_t>(N, 1) * 4)) ||
+        (rc = cube->row_ptr.reserve((size_t)(nb + 1) * 8)))
+        return rc;
+    if ((rc = cube_vertices_impl(cube, X, N, cube->vertex.as<int32_t>()))) return rc;
+    if ((rc = build_csr(ctx, cube->vertex.as<int32_t>(), 1, N, nb, cube->idx.as<int32_t>(), cube->row_ptr.as<int64_t>()))) return rc;
+    cube->N = N;
+    cube->built = 1;
+    return 0;
+}
+
+int lshkm_cube_vertices(lshkm_cube cube, const float* Q, int64_t nq, int32_t* vertex) {
+    LSHKM_CHECK(cube && (Q || nq == 0) && nq >= 0 && (vertex || nq == 0), LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(cube->ctx->device));
+    return cube_vertices_impl(cube, Q, nq, vertex);
+}
+
+int lshkm_cube_get_buckets(lshkm_cube cube, int64_t* row_ptr, int32_t* idx) {
+    LSHKM_CHECK(cube && cube->built, LSHKM_ERR_STATE, "cube not built");
+    int rc;
+    if (row_ptr && (rc = d2h(cube->ctx, row_ptr, cube->row_ptr.p, (size_t)((1ll << cube->k) + 1) * 8))) return rc;
+    if (idx && cube->N > 0 && (rc = d2h(cube->ctx, idx, cube->idx.p, (size_t)cube->N * 4))) return rc;
+    return 0;
+}
+
+int lshkm_cube_query(lshkm_cube cube, const float* Q, int64_t nq, int probes, int64_t* out_ptr, int32_t* out_idx,
+                     int64_t out_cap, int64_t* total_host) {
+    LSHKM_CHECK(cube && cube->built, LSHKM_ERR_STATE, "cube not built (lshkm_cube_build)");
+    LSHKM_CHECK((Q || nq == 0) && nq >= 0 && out_ptr && total_host, LSHKM_ERR_ARG, "bad arguments");
+    lshkm_ctx ctx = cube->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const std::vector<int32_t> masks = probe_masks(probes, cube->k);
+    const int S = (int)masks.size();
+    int rc;
+    if (nq == 0) {
+        LSHKM_HIP(hipMemsetAsync(out_ptr, 0, 8, s));
+        *total_host = 0;
+        return 0;
+    }
+    if ((rc = reserve(ctx, WS_QBKT, (size_t)nq * 4)) || (rc = reserve(ctx, WS_MASKS, (size_t)S * 4)) ||
+        (rc = reserve(ctx, WS_QSZ, (size_t)nq * S * 8)) || (rc = reserve(ctx, WS_CROW, (size_t)(nq * S + 1) * 8)))
+        return rc;
+    if ((rc = cube_vertices_impl(cube, Q, nq, slot<int32_t>(ctx, WS_QBKT)))) return rc;
+    LSHKM_HIP(hipMemcpyAsync(ctx->ws[WS_MASKS].p, masks.data(), (size_t)S * 4, hipMemcpyHostToDevice, s));
+    if ((rc = launch_cube_query(s, slot<int32_t>(ctx, WS_QBKT), nq, slot<int32_t>(ctx, WS_MASKS), S, cube->row_ptr.as<int64_t>(),
+                                cube->idx.as<int32_t>(), slot<int64_t>(ctx, WS_QSZ), slot<int64_t>(ctx, WS_CROW), out_ptr,
+                                nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    int64_t total = 0;
+    if ((rc = d2h(ctx, &total, out_ptr + nq, 8))) return rc;
+    *total_host = total;
+    if (out_idx && total <= out_cap && total > 0)
+        if ((rc = launch_cube_query(s, slot<int32_t>(ctx, WS_QBKT), nq, slot<int32_t>(ctx, WS_MASKS), S,
+                                    cube->row_ptr.as<int64_t>(), cube->idx.as<int32_t>(), slot<int64_t>(ctx, WS_QSZ),
+                                    slot<int64_t>(ctx, WS_CROW), out_ptr, out_idx))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return 0;
+}
+
+int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f, int32_t* h, int32_t* bit, int64_t cap, int64_t* count,
+                        uint32_t* rng_state) {
+    LSHKM_CHECK(cube && count, LSHKM_ERR_ARG, "bad arguments");
+    lshkm_ctx ctx = cube->ctx;
+    int rc;
+    uint32_t st = 0;
+    if ((rc = d2h(ctx, &st, cube->rng_d.p, 4))) return rc;
+    if (rng_state) *rng_state = st;
+    std::vector<int32_t> memo((size_t)cube->k * cube->hspan);
+    if (!memo.empty() && (rc = d2h(ctx, memo.data(), cube->memo.p, memo.size() * 4))) return rc;
+    int64_t n = 0;
+    for (int fi = 0; fi < cube->k; fi++)
+        for (int32_t o = 0; o < cube->hspan; o++) {
+            const int32_t b = memo[(size_t)fi * cube->hspan + o];
+            if (b < 0) continue;
+            if (n < cap) {
+                if (f) f[n] = fi;
+                if (h) h[n] = cube->hmin + o;
+                if (bit) bit[n] = b;
+            }
+            n++;
+        }
+    *count = n;
+    return 0;
+}
+
+// ------------------------------------------------------------------- k-means
+static int km_sums(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K, double* sums,
+                   int64_t* counts) {
+    int rc;
+    if ((rc = reserve(ctx, WS_ROWS, (size_t)std::max<int64_t>(N, 1) * 4)) || (rc = reserve(ctx, WS_CROW, (size_t)(K + 1) * 8)))
+        return rc;
+    if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
+    if ((rc = launch_km_chain(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, sums, counts))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return 0;
+}
+
+static int km_finalize(lshkm_ctx ctx, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
+                       int metric, double min_dist, double* C_new, int* cont) {
+    int rc;
+    if ((rc = reserve(ctx, WS_FLAG, 64))) return rc;
+    LSHKM_HIP(hipMemsetAsync(ctx->ws[WS_FLAG].p, 0, 4, ctx->stream));
+    if ((rc = launch_km_finalize(ctx->stream, sums, counts, K, d, C_old, metric, min_dist, C_new, slot<int>(ctx, WS_FLAG)))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    int moved = 0;
+    if ((rc = d2h(ctx, &moved, ctx->ws[WS_FLAG].p, 4))) return rc;
+    if (cont) *cont = moved ? 1 : 0;
+    return 0;
+}
+
+int lshkm_kmeans_update(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, const double* C_old,
+                        int K, int metric, double min_dist, double* C_new, int64_t* counts, int* cont) {
+    LSHKM_CHECK(ctx && (X || N == 0) && assign && C_old && C_new && N >= 0 && N < (1ll << 31) && d > 0 && K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = reserve(ctx, WS_SUMS, (size_t)K * d * 8)) || (rc = reserve(ctx, WS_CNTS, (size_t)K * 8))) return rc;
+    int64_t* cnt = counts ? counts : slot<int64_t>(ctx, WS_CNTS);
+    if ((rc = km_sums(ctx, X, N, d, assign, K, slot<double>(ctx, WS_SUMS), cnt))) return rc;
+    return km_finalize(ctx, slot<double>(ctx, WS_SUMS), cnt, K, d, C_old, metric, min_dist, C_new, cont);
+}
+
+int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K, double* sums,
+                         int64_t* counts) {
+    LSHKM_CHECK(ctx && (X || N == 0) && assign && sums && counts && N >= 0 && N < (1ll << 31) && d > 0 && K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    return km_sums(ctx, X, N, d, assign, K, sums, counts);
+}
+
+int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
+                          int metric, double min_dist, double* C_new, int* cont) {
+    LSHKM_CHECK(ctx && sums && counts && C_old && C_new && K > 0 && d > 0, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    return km_finalize(ctx, sums, counts, K, d, C_old, metric, min_dist, C_new, cont);
+}
+
+}  // extern "C"

@@ -79,7 +79,7 @@ int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d,
                          float* C32, float* cconst) {
     (void)metric;
     hipLaunchKernelGGL(centroid_prep_kernel, dim3((Kpad + 63) / 64), dim3(64), 0, s, C, K, Kpad, d, DP, C32, cconst);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return kstatus("assign.hip");
 }
 
 template <int DP>
@@ -229,7 +229,7 @@ int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, 
 #undef AS_CASE
         default: return -4;
     }
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return kstatus("assign.hip");
 }
 
 // ---------------------------------------------------------------- exact pass
@@ -298,7 +298,7 @@ int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const d
     const int64_t blocks = std::min<int64_t>((max_rows + 3) / 4, rows ? 256 : 2048);
     hipLaunchKernelGGL(assign_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, N, d, C, K, metric,
                        rows, row_count, max_rows, assign, dist);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return kstatus("assign.hip");
 }
 
 // Centroid override (assignment.hpp:77-78): in c order, so the last centroid
@@ -318,7 +318,7 @@ __global__ void assign_override_kernel(const int32_t* __restrict__ src, int K, i
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist) {
     hipLaunchKernelGGL(assign_override_kernel, dim3((K + 255) / 256), dim3(256), 0, s, src_rows, K, N, assign, dist);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return kstatus("assign.hip");
 }
 
 __global__ void add_counter_kernel(unsigned long long* dst, const unsigned long long* src) {
@@ -327,7 +327,7 @@ __global__ void add_counter_kernel(unsigned long long* dst, const unsigned long 
 
 int launch_add_counter(hipStream_t s, unsigned long long* dst, const unsigned long long* src) {
     hipLaunchKernelGGL(add_counter_kernel, dim3(1), dim3(1), 0, s, dst, src);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return kstatus("assign.hip");
 }
 
 }  // namespace lshkm

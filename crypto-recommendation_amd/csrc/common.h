@@ -25,6 +25,23 @@ void set_error(const std::string& msg);
 
 #define LSHKM_LAUNCH_CHECK() LSHKM_HIP(hipGetLastError())
 
+// Status of the launches just issued by a launcher: 0, or -2 with the HIP
+// error recorded for lshkm_last_error().
+inline int kstatus(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return -2;
+}
+
+// Grid size for a grid-stride kernel: at least one block, at most cap.
+inline unsigned gsz(int64_t work, int64_t per_block, int64_t cap) {
+    int64_t b = (work + per_block - 1) / per_block;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (unsigned)b;
+}
+
 // Device counters kept per context (see lshkm_get_stat).
 enum Stat {
     STAT_HASH_EXACT = 0,     // hash values resolved by the soft-x87 exact path

@@ -205,7 +205,7 @@ int launch_proj_hash(hipStream_t s, int mode, const float* X, int64_t N, const H
         case HM_CUBE_EUCLID_H: launch_mode<HM_CUBE_EUCLID_H>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
         default: launch_mode<HM_CUBE_COSINE>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
     }
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return kstatus("hash.hip");
 }
 
 // ------------------------------------------------------------ synthetic data
@@ -221,7 +221,7 @@ int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d
     if (total <= 0) return 0;
     const int64_t blocks = min((total + 255) / 256, (int64_t)256 * 64);
     hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, seed, row0, total, d, X);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return kstatus("hash.hip");
 }
 
 }  // namespace lshkm

@@ -42,8 +42,8 @@ struct lshkm_ctx_s {
     lshkm::Buf stats;            // STAT_COUNT x u64
     // assignment workspace
     lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src;
-    // scatter / query / update workspace
-    lshkm::Buf ws_a, ws_b, ws_c, ws_d, ws_e;
+    // scatter / query / update workspace (see api_index.cpp for the slot map)
+    lshkm::Buf ws[16];
     // pinned host staging for small host->device inputs
     void* pinned = nullptr;
     size_t pinned_cap = 0;
@@ -70,6 +70,7 @@ struct lshkm_lsh_s {
     int64_t nb = 0;
     lshkm::ProjTable proj;
     // built index (lshkm_lsh_build)
+    int built = 0;
     int64_t N = 0;
     lshkm::Buf tuples, bucket, row_ptr, idx;
 };
@@ -81,9 +82,10 @@ struct lshkm_cube_s {
     lshkm::ProjTable proj;
     // lazy EuclideanF coin memo: memo[f][h - hmin] in {-1 (unseen), 0, 1}
     int32_t hmin = 0, hspan = 0;
-    lshkm::Buf memo, first_row;
-    uint32_t rng_state = 1;
-    lshkm::Buf rng_d;             // device copy of the engine state
+    lshkm::Buf memo, memo2, first_row;
+    lshkm::Buf rng_d;             // device copy of the engine state (uint32)
+    lshkm::Buf mm, cnt;           // h min/max, collected-entry count
+    int built = 0;
     int64_t N = 0;
     lshkm::Buf vertex, row_ptr, idx;
 };

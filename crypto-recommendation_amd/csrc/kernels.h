@@ -51,6 +51,41 @@ int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_
 
 int launch_add_counter(hipStream_t s, unsigned long long* dst, const unsigned long long* src);
 
+// Stable bucket scatter (scatter.hip).
+size_t sort_scratch_bytes(int64_t N, int64_t range);
+int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
+                       int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch);
+int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr);
+
+// Queries (query.hip).
+int launch_scan_i64(hipStream_t s, const int64_t* a, int64_t M, int64_t* out);
+int launch_lsh_query(hipStream_t s, const int32_t* qbucket, const int32_t* qtuple, const int32_t* alias, int64_t nq,
+                     int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* tuples, const int32_t* bucket,
+                     const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* cand_off,
+                     int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase);
+int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int32_t* masks, int S,
+                      const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* slot_off,
+                      int64_t* out_ptr, int32_t* out);
+
+// Hypercube coins (cube.hip).
+int launch_h_minmax(hipStream_t s, const int32_t* h, int64_t n, int32_t* mm_dev);
+int launch_coin_first(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
+                      const int32_t* memo, int32_t* first_row);
+int launch_coin_collect(hipStream_t s, int32_t* first_row, int64_t total, int k, int32_t hspan, int32_t* keys,
+                        int32_t* vals, unsigned int* count);
+int launch_coin_draw(hipStream_t s, const int32_t* sorted_vals, const unsigned int* count, int32_t hmin, int32_t hspan,
+                     int32_t* memo, uint32_t* state);
+int launch_coin_vertex(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
+                       const int32_t* memo, int32_t* vertex);
+int launch_memo_rehome(hipStream_t s, const int32_t* old_memo, int32_t old_min, int32_t old_span, int32_t* new_memo,
+                       int32_t new_min, int32_t new_span, int k);
+
+// k-means update (update.hip).
+int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K,
+                    double* sums, int64_t* counts);
+int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
+                       int metric, double min_dist, double* C_new, int* moved);
+
 // Synthetic data.
 int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X);
 

@@ -1,0 +1,206 @@
+// query.hip — batched bucket queries on gfx950.
+//
+// LSH: get_LSH_filtered_combined_buckets / get_LSH_combined_buckets
+// (lib/lsh_cube.hpp:77-106) over CustHashtable::getFilteredBucketFor /
+// getBucketFor (lib/data_structures/cust_hashtable.hpp:73-113). Per query the
+// result is the union of its L buckets (filtered: members whose stored k-tuple
+// equals the query's), deduplicated and sorted by row (std::set<CustVector*>
+// over one contiguous std::vector orders by row index).
+//   1. candidates per (query, table) = its bucket size; exclusive scan;
+//   2. one wave per (query, table) streams its bucket (already row-sorted),
+//      keeps a member iff it passes table l and fails every table l' < l
+//      (O(1): bucket[m][l'] == qbucket[l'] plus the tuple test) — so the kept
+//      lists are disjoint — and compacts them with ballot/popc, order kept;
+//   3. per-query totals -> output offsets (two-phase API);
+//   4. merge: an element at position p of kept list l lands at
+//      p + sum_{l' != l} lower_bound(kept list l', e).
+// Hypercube: get_hypercube_combined_buckets (lib/lsh_cube.hpp:139-177): main
+// bucket, then the probe buckets in get_num_hamming_dist_from order
+// (lib/utils.cpp:22-50), concatenated without dedup; the probe masks are the
+// same for every query and are built on the host.
+#include "common.h"
+#include "kernels.h"
+
+namespace lshkm {
+
+// Exclusive scan of M int64 -> out[0..M] (out[M] = total). One block.
+__global__ __launch_bounds__(1024) void scan_i64_kernel(const int64_t* __restrict__ a, int64_t M, int64_t* __restrict__ out) {
+    __shared__ int64_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t seg = (M + 1023) / 1024;
+    const int64_t lo = t * seg, hi = min(M, lo + seg);
+    int64_t s = 0;
+    for (int64_t i = lo; i < hi; i++) s += a[i];
+    part[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int64_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int64_t run = t ? part[t - 1] : 0;
+    for (int64_t i = lo; i < hi; i++) { const int64_t v = a[i]; out[i] = run; run += v; }
+    if (t == 1023) out[M] = part[1023];
+}
+
+int launch_scan_i64(hipStream_t s, const int64_t* a, int64_t M, int64_t* out) {
+    hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, a, M, out);
+    return kstatus("query.hip");
+}
+
+__global__ void lq_sizes(const int32_t* __restrict__ qbucket, int64_t nq, int L, int64_t nb,
+                         const int64_t* __restrict__ row_ptr, int64_t* __restrict__ sizes) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq * L; e += (int64_t)gridDim.x * blockDim.x) {
+        const int l = (int)(e % L);
+        const int64_t b = qbucket[e];
+        const int64_t* rp = row_ptr + (size_t)l * (nb + 1);
+        sizes[e] = rp[b + 1] - rp[b];
+    }
+}
+
+__device__ inline bool tuple_eq(const int32_t* __restrict__ a, const int32_t* __restrict__ b, int k) {
+    for (int i = 0; i < k; i++)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// One wave per (query, table).
+__global__ __launch_bounds__(256) void lq_mark(
+    const int32_t* __restrict__ qbucket, const int32_t* __restrict__ qtuple, const int32_t* __restrict__ alias,
+    int64_t nq, int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* __restrict__ tuples,
+    const int32_t* __restrict__ bucket, const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ idx,
+    const int64_t* __restrict__ cand_off, int32_t* __restrict__ klist, int64_t* __restrict__ kcount) {
+    const int lane = threadIdx.x & 63;
+    const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (pair >= nq * L) return;
+    const int64_t q = pair / L;
+    const int l = (int)(pair - q * L);
+    const int32_t* qt = nullptr;
+    if (filtered && tuples) {
+        const int64_t a = alias ? alias[q] : -1;   // first-write-wins ID map (euclidean_phi_gen.hpp:94)
+        qt = a >= 0 ? tuples + (size_t)a * L * k : qtuple + (size_t)q * L * k;
+    }
+    const int32_t* qb = qbucket + (size_t)q * L;
+    const int64_t* rp = row_ptr + (size_t)l * (nb + 1);
+    const int64_t beg = rp[qb[l]], end = rp[qb[l] + 1];
+    const int32_t* members = idx + (size_t)l * N;
+    int64_t out = cand_off[pair];
+    for (int64_t p0 = beg; p0 < end; p0 += 64) {
+        const int64_t p = p0 + lane;
+        bool keep = false;
+        int32_t m = 0;
+        if (p < end) {
+            m = members[p];
+            const int32_t* mt = tuples ? tuples + (size_t)m * L * k : nullptr;
+            keep = !qt || tuple_eq(mt + l * k, qt + l * k, k);
+            for (int l2 = 0; keep && l2 < l; l2++) {
+                const bool in2 = bucket[(size_t)m * L + l2] == qb[l2] && (!qt || tuple_eq(mt + l2 * k, qt + l2 * k, k));
+                if (in2) keep = false;
+            }
+        }
+        const unsigned long long bal = __ballot(keep);
+        if (keep) klist[out + __popcll(bal & ((1ull << lane) - 1ull))] = m;
+        out += __popcll(bal);
+    }
+    if (lane == 0) kcount[pair] = out - cand_off[pair];
+}
+
+__global__ void lq_qsizes(const int64_t* __restrict__ kcount, int64_t nq, int L, int64_t* __restrict__ qsz) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+        int64_t s = 0;
+        for (int l = 0; l < L; l++) s += kcount[q * L + l];
+        qsz[q] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void lq_merge(const int64_t* __restrict__ cand_off, const int64_t* __restrict__ kcount,
+                                                const int32_t* __restrict__ klist, int64_t nq, int L,
+                                                const int64_t* __restrict__ out_ptr, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (pair >= nq * L) return;
+    const int64_t q = pair / L;
+    const int l = (int)(pair - q * L);
+    const int64_t n = kcount[pair];
+    const int32_t* mine = klist + cand_off[pair];
+    for (int64_t p = lane; p < n; p += 64) {
+        const int32_t e = mine[p];
+        int64_t rank = p;
+        for (int l2 = 0; l2 < L; l2++) {
+            if (l2 == l) continue;
+            const int32_t* other = klist + cand_off[q * L + l2];
+            int64_t lo = 0, hi = kcount[q * L + l2];
+            while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (other[mid] < e) lo = mid + 1; else hi = mid; }
+            rank += lo;
+        }
+        out[out_ptr[q] + rank] = e;
+    }
+}
+
+int launch_lsh_query(hipStream_t s, const int32_t* qbucket, const int32_t* qtuple, const int32_t* alias, int64_t nq,
+                     int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* tuples, const int32_t* bucket,
+                     const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* cand_off,
+                     int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase) {
+    const int64_t pairs = nq * L;
+    if (phase == 0) {          // candidate counts -> cand_off[pairs + 1]
+        hipLaunchKernelGGL(lq_sizes, dim3((unsigned)std::min<int64_t>((pairs + 255) / 256, 4096)), dim3(256), 0, s, qbucket,
+                           nq, L, nb, row_ptr, sizes);
+        hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, sizes, pairs, cand_off);
+    } else if (phase == 1) {   // filter + dedup + compact -> out_ptr[nq + 1]
+        hipLaunchKernelGGL(lq_mark, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, qbucket, qtuple, alias, nq, L, k,
+                           nb, filtered, N, tuples, bucket, row_ptr, idx, cand_off, klist, kcount);
+        hipLaunchKernelGGL(lq_qsizes, dim3((unsigned)std::min<int64_t>((nq + 255) / 256, 4096)), dim3(256), 0, s, kcount,
+                           nq, L, qsz);
+        hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, qsz, nq, out_ptr);
+    } else {                   // merge into the caller's output
+        hipLaunchKernelGGL(lq_merge, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, cand_off, kcount, klist, nq, L,
+                           out_ptr, out);
+    }
+    return kstatus("query.hip");
+}
+
+// ------------------------------------------------------------------ hypercube
+__global__ void cq_sizes(const int32_t* __restrict__ qvert, int64_t nq, const int32_t* __restrict__ masks, int S,
+                         const int64_t* __restrict__ row_ptr, int64_t* __restrict__ sizes) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq * S; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = e / S;
+        const int64_t v = qvert[q] ^ masks[e - q * S];
+        sizes[e] = row_ptr[v + 1] - row_ptr[v];
+    }
+}
+
+__global__ void cq_qptr(const int64_t* __restrict__ slot_off, int64_t nq, int S, int64_t* __restrict__ out_ptr) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= nq; q += (int64_t)gridDim.x * blockDim.x)
+        out_ptr[q] = slot_off[q * S];
+}
+
+__global__ __launch_bounds__(256) void cq_copy(const int32_t* __restrict__ qvert, int64_t nq,
+                                               const int32_t* __restrict__ masks, int S,
+                                               const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ idx,
+                                               const int64_t* __restrict__ slot_off, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (e >= nq * S) return;
+    const int64_t q = e / S;
+    const int64_t v = qvert[q] ^ masks[e - q * S];
+    const int64_t beg = row_ptr[v], n = row_ptr[v + 1] - beg, dst = slot_off[e];
+    for (int64_t p = lane; p < n; p += 64) out[dst + p] = idx[beg + p];
+}
+
+int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int32_t* masks, int S,
+                      const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* slot_off,
+                      int64_t* out_ptr, int32_t* out) {
+    const int64_t slots = nq * S;
+    hipLaunchKernelGGL(cq_sizes, dim3((unsigned)std::min<int64_t>((slots + 255) / 256, 4096)), dim3(256), 0, s, qvert, nq,
+                       masks, S, row_ptr, sizes);
+    hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, sizes, slots, slot_off);
+    hipLaunchKernelGGL(cq_qptr, dim3((unsigned)std::min<int64_t>((nq + 256) / 256, 4096)), dim3(256), 0, s, slot_off, nq, S,
+                       out_ptr);
+    if (out)
+        hipLaunchKernelGGL(cq_copy, dim3((unsigned)((slots + 3) / 4)), dim3(256), 0, s, qvert, nq, masks, S, row_ptr, idx,
+                           slot_off, out);
+    return kstatus("query.hip");
+}
+
+}  // namespace lshkm

@@ -1,0 +1,180 @@
+// scatter.hip — stable bucket scatter (CSR build) on gfx950.
+//
+// Replaces the per-insert std::vector::emplace_back of
+//   CustHashtable::insertVector  lib/data_structures/cust_hashtable.hpp:65-70
+//   VectorBucket::insertVector   lib/data_structures/vector_bucket.hpp:41-44
+// whose observable contract is: bucket b holds the rows with bucket ID b in
+// insertion (= row) order. Built here as a stable LSD radix sort of
+// (bucket ID, row) pairs, then a boundary pass that writes the CSR row
+// pointers (empty buckets included). Also used for the k-means member lists
+// (cluster-sorted rows, update.hpp:52-56 order) and the F-coin draw order.
+//
+// Per pass (<= 8 digit bits): upsweep (block digit histograms in LDS) ->
+// one-block exclusive scan of the [digit][block] matrix -> downsweep, where a
+// block walks its 4096-key tile in rounds of 256 consecutive keys: each wave
+// finds the lanes sharing its digit with DB ballots (AND of matching bit
+// masks), ranks itself with popc(peers & lanemask_lt), publishes its per-digit
+// counts in LDS, and the block adds the counts of earlier waves and earlier
+// rounds: a stable rank without sorting inside the tile.
+// HBM per pass: 4 B key read (upsweep) + 8 B read + 8 B written (downsweep).
+#include "common.h"
+#include "kernels.h"
+
+namespace lshkm {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_TILE = 4096;
+
+__global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const int32_t* __restrict__ keys, int64_t kstride, int64_t N,
+                                                        int shift, int nbins, int nblocks, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    for (int b = threadIdx.x; b < nbins; b += RS_THREADS) h[b] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+    for (int e = threadIdx.x; e < RS_TILE; e += RS_THREADS) {
+        const int64_t i = base + e;
+        if (i < N) atomicAdd(&h[(keys[i * kstride] >> shift) & (nbins - 1)], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nbins; b += RS_THREADS) hist[(size_t)b * nblocks + blockIdx.x] = h[b];
+}
+
+// Exclusive scan of M uint32 in place, one block of 1024 threads.
+__global__ __launch_bounds__(1024) void rs_scan(uint32_t* __restrict__ a, int64_t M) {
+    __shared__ uint32_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t seg = (M + 1023) / 1024;
+    const int64_t lo = t * seg, hi = min(M, lo + seg);
+    uint32_t s = 0;
+    for (int64_t i = lo; i < hi; i++) s += a[i];
+    part[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {          // Hillis-Steele over the 1024 partials
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = t ? part[t - 1] : 0u;
+    for (int64_t i = lo; i < hi; i++) { const uint32_t v = a[i]; a[i] = run; run += v; }
+}
+
+__global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
+    const int32_t* __restrict__ keys, int64_t kstride, const int32_t* __restrict__ vals, int64_t N, int shift,
+    int dbits, int nblocks, const uint32_t* __restrict__ scanned, int32_t* __restrict__ keys_out,
+    int32_t* __restrict__ vals_out) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[4][256];
+    const int nbins = 1 << dbits;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int b = t; b < nbins; b += RS_THREADS) {
+        run[b] = scanned[(size_t)b * nblocks + blockIdx.x];
+        wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int r = 0; r < RS_TILE / RS_THREADS; r++) {
+        const int64_t i0 = base + (int64_t)r * RS_THREADS;
+        if (i0 >= N) break;                               // uniform
+        const int64_t i = i0 + t;
+        const bool valid = i < N;
+        const int32_t key = valid ? keys[i * kstride] : 0;
+        const int digit = (key >> shift) & (nbins - 1);
+        unsigned long long peers = __ballot(valid);
+        for (int b = 0; b < dbits; b++) {
+            const bool bit = (digit >> b) & 1;
+            const unsigned long long m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const int rank = __popcll(peers & lt);
+        if (valid && rank == 0) wcnt[w][digit] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = run[digit] + rank;
+            for (int w2 = 0; w2 < w; w2++) pos += wcnt[w2][digit];
+            keys_out[pos] = key;
+            vals_out[pos] = vals ? vals[i] : (int32_t)i;
+        }
+        __syncthreads();
+        for (int b = t; b < nbins; b += RS_THREADS) {
+            run[b] += wcnt[0][b] + wcnt[1][b] + wcnt[2][b] + wcnt[3][b];
+            wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void rs_copy(const int32_t* __restrict__ keys, int64_t kstride, const int32_t* __restrict__ vals, int64_t N,
+                        int32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        keys_out[i] = keys[i * kstride];
+        vals_out[i] = vals ? vals[i] : (int32_t)i;
+    }
+}
+
+// row_ptr[b] = first position of key >= b in the sorted keys; row_ptr[nb] = N.
+__global__ void csr_bounds(const int32_t* __restrict__ skeys, int64_t N, int64_t nb, int64_t* __restrict__ row_ptr) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= N; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t prev = i == 0 ? -1 : (int64_t)skeys[i - 1];
+        const int64_t cur = i == N ? nb : (int64_t)skeys[i];
+        for (int64_t b = prev + 1; b <= cur && b <= nb; b++) row_ptr[b] = i;
+    }
+}
+
+static int key_bits(int64_t range) {
+    int bits = 0;
+    while (bits < 31 && ((int64_t)1 << bits) < range) bits++;
+    return bits;
+}
+
+size_t sort_scratch_bytes(int64_t N, int64_t range) {
+    const int bits = key_bits(range);
+    const int P = (bits + 7) / 8;
+    const int DB = P ? (bits + P - 1) / P : 0;
+    const int64_t nblocks = (N + RS_TILE - 1) / RS_TILE;
+    return (size_t)(2 * N + 64) * 4 + (size_t)((int64_t)1 << DB) * nblocks * 4 + 256;
+}
+
+int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
+                       int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch) {
+    if (N <= 0) return 0;
+    const int bits = key_bits(range);
+    const int64_t nblocks = (N + RS_TILE - 1) / RS_TILE;
+    if (bits == 0) {
+        hipLaunchKernelGGL(rs_copy, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 4096)), dim3(256), 0, s, keys, kstride,
+                           vals, N, keys_out, vals_out);
+        return kstatus("scatter.hip");
+    }
+    const int P = (bits + 7) / 8;
+    const int DB = (bits + P - 1) / P;
+    const int nbins = 1 << DB;
+    int32_t* k2 = reinterpret_cast<int32_t*>(scratch);
+    int32_t* v2 = k2 + N;
+    uint32_t* hist = reinterpret_cast<uint32_t*>(v2 + N + 64);
+    const int32_t* kin = keys;
+    const int32_t* vin = vals;
+    int64_t kst = kstride;
+    for (int p = 0; p < P; p++) {
+        const bool to_out = ((P - 1 - p) % 2) == 0;
+        int32_t* ko = to_out ? keys_out : k2;
+        int32_t* vo = to_out ? vals_out : v2;
+        const int shift = p * DB;
+        hipLaunchKernelGGL(rs_upsweep, dim3((unsigned)nblocks), dim3(RS_THREADS), 0, s, kin, kst, N, shift, nbins,
+                           (int)nblocks, hist);
+        hipLaunchKernelGGL(rs_scan, dim3(1), dim3(1024), 0, s, hist, (int64_t)nbins * nblocks);
+        hipLaunchKernelGGL(rs_downsweep, dim3((unsigned)nblocks), dim3(RS_THREADS), 0, s, kin, kst, vin, N, shift, DB,
+                           (int)nblocks, hist, ko, vo);
+        kin = ko; vin = vo; kst = 1;
+    }
+    return kstatus("scatter.hip");
+}
+
+int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr) {
+    const int64_t threads = N + 1;
+    hipLaunchKernelGGL(csr_bounds, dim3((unsigned)std::min<int64_t>((threads + 255) / 256, 8192)), dim3(256), 0, s,
+                       sorted_keys, N, nb, row_ptr);
+    return kstatus("scatter.hip");
+}
+
+}  // namespace lshkm

@@ -1,0 +1,189 @@
+"""GPU parity: bucket scatter (CSR), LSH queries, hypercube (vertices, F coins,
+probe queries) and the k-means update, against the reference's golden outputs
+and the CPU oracle. Everything here is bit-exact."""
+import numpy as np
+import pytest
+
+import oracle
+from amd import lshkm
+from conftest import cases, golden, golden_meta
+
+META = golden_meta()
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return lshkm.Context(0)
+
+
+def to_dev(ctx, a):
+    return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+
+
+def split_csr(ptr, idx):
+    return [idx[ptr[i]:ptr[i + 1]] for i in range(len(ptr) - 1)]
+
+
+def make_lsh(ctx, m, g):
+    if m["metric"] == "euclidean":
+        return lshkm.LSH(ctx, "euclidean", m["d"], m["k"], m["L"], m["nb"], m["w"], V=g["V"], t=g["t"], r=g["r"])
+    return lshkm.LSH(ctx, "cosine", m["d"], m["k"], m["L"], R=g["R"])
+
+
+@pytest.mark.parametrize("name", cases("lsh"))
+def test_lsh_build_buckets_golden(ctx, name):
+    m, g = META[name], golden(name)
+    X = to_dev(ctx, oracle.synth(m["data_seed"], m["N"], m["d"]))
+    lsh = make_lsh(ctx, m, g)
+    lsh.build(X)
+    nb, gp, gi = m["nb"], g["members_ptr"], g["members_idx"]
+    for l in range(m["L"]):
+        rp, idx = lsh.buckets(l)
+        assert np.array_equal(rp, gp[l * nb:(l + 1) * nb + 1] - gp[l * nb]), l
+        assert np.array_equal(idx, gi[gp[l * nb]:gp[(l + 1) * nb]]), l
+
+
+@pytest.mark.parametrize("name", cases("lsh"))
+def test_lsh_queries_golden(ctx, name):
+    m, g = META[name], golden(name)
+    X = to_dev(ctx, oracle.synth(m["data_seed"], m["N"], m["d"]))
+    Q = np.concatenate([oracle.synth(m["data_seed"], m["N"], m["d"])[:m["nqrows"]],
+                        oracle.synth(m["query_seed"], m["Q"], m["d"])])
+    lsh = make_lsh(ctx, m, g)
+    lsh.build(X)
+    # dataset rows carry their own IDs: alias them (first-write-wins map)
+    alias = np.full(Q.shape[0], -1, np.int32); alias[:m["nqrows"]] = np.arange(m["nqrows"])
+    for kind, filt in (("qfilt", True), ("qunf", False)):
+        ptr, idx = lsh.query(to_dev(ctx, Q), filtered=filt, alias_rows=to_dev(ctx, alias))
+        assert np.array_equal(ptr, g[kind + "_ptr"]), kind
+        assert np.array_equal(idx, g[kind + "_idx"]), kind
+
+
+def test_lsh_build_and_query_large_vs_oracle(ctx):
+    # C2 shape: 1M x 128, L=5, k=4, w=0.4, nb = N/100 = 10,000
+    N, d, L, k = 1_000_000, 128, 5, 4
+    V, t, r, _ = lshkm.params_lsh_euclidean(12345, L, k, d, 0.4)
+    X = ctx.synth(0x5EED, N, d)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
+    lsh.build(X)
+    Xh = X.cpu().numpy()
+    tu, _, b = oracle.lsh_hash_euclid(Xh, V, t, np.float32(0.4), r, N // 100)
+    orp, oidx = oracle.bucket_csr(b, N // 100)
+    for l in range(L):
+        rp, idx = lsh.buckets(l)
+        assert np.array_equal(rp, orp[l]) and np.array_equal(idx, oidx[l]), l
+    qrows = np.random.default_rng(7).choice(N, 500, replace=False).astype(np.int32)
+    ptr, out = lsh.query(X[to_dev(ctx, qrows.astype(np.int64))], True, to_dev(ctx, qrows))
+    for q, row in enumerate(qrows):
+        exp = oracle.lsh_query(N, N // 100, orp, oidx, b[row], tu, tu[row])
+        assert np.array_equal(out[ptr[q]:ptr[q + 1]], exp), q
+        assert row in exp
+
+
+def test_lsh_query_empty_and_unbuilt(ctx):
+    m, g = META["lsh_e"], golden("lsh_e")
+    lsh = make_lsh(ctx, m, g)
+    with pytest.raises(lshkm.LshkmError):
+        lsh.query(ctx.synth(1, 4, m["d"]))
+    lsh.build(to_dev(ctx, oracle.synth(m["data_seed"], m["N"], m["d"])))
+    ptr, idx = lsh.query(ctx.synth(1, 0, m["d"]))
+    assert ptr.tolist() == [0] and idx.size == 0
+
+
+@pytest.mark.parametrize("name", cases("cube"))
+def test_cube_golden(ctx, name):
+    m, g = META[name], golden(name)
+    Xh = oracle.synth(m["data_seed"], m["N"], m["d"])
+    X = to_dev(ctx, Xh)
+    k = m["k"]
+    if m["metric"] == "euclidean":
+        V, t, st = lshkm.params_cube_euclidean(m["seed"], k, m["d"], m["w"])
+        assert np.array_equal(V, g["V"]) and np.array_equal(t, g["t"])
+        cube = lshkm.Cube(ctx, "euclidean", m["d"], k, m["w"], V=V, t=t, rng_state=st)
+    else:
+        R, st = lshkm.params_cube_cosine(m["seed"], k, m["d"])
+        cube = lshkm.Cube(ctx, "cosine", m["d"], k, R=R, rng_state=st)
+    cube.build(X)
+    rp, idx = cube.buckets()
+    assert np.array_equal(rp, g["members_ptr"]) and np.array_equal(idx, g["members_idx"])
+    assert np.array_equal(cube.vertices(X).cpu().numpy(), g["vertex"])
+    if m["metric"] == "euclidean":
+        f, h, b, _ = cube.memo()
+        o = np.lexsort((h, f))
+        assert np.array_equal(f[o], g["memo_f"]) and np.array_equal(h[o], g["memo_h"])
+        assert np.array_equal(b[o], g["memo_bit"])
+    Q = np.concatenate([Xh[:m["nqrows"]], oracle.synth(m["query_seed"], m["Q"], m["d"])])[g["qmask"].astype(bool)]
+    for p in m["probes"]:
+        ptr, out = cube.query(to_dev(ctx, Q), p)
+        assert np.array_equal(ptr, g[f"q_probes{p}_ptr"]), p
+        assert np.array_equal(out, g[f"q_probes{p}_idx"]), p
+
+
+def test_cube_large_and_continued_coins_vs_oracle(ctx):
+    # C4 shape at 1M: d'=14 euclidean; then external queries continue the coin stream
+    N, d, k, w = 1_000_000, 128, 14, 2.0
+    V, t, st = lshkm.params_cube_euclidean(4242, k, d, w)
+    X = ctx.synth(0x5EED, N, d)
+    cube = lshkm.Cube(ctx, "euclidean", d, k, w, V=V, t=t, rng_state=st)
+    cube.build(X)
+    Xh = X.cpu().numpy()
+    memo = oracle.CoinMemo(k, st)
+    ov, draws = memo.apply(oracle.cube_h(Xh, V, t, np.float32(w)))
+    rp, idx = cube.buckets()
+    orp, oidx = oracle.bucket_csr(ov[:, None], 1 << k)
+    assert np.array_equal(rp, orp[0]) and np.array_equal(idx, oidx[0])
+    # far-away queries hit unseen h values: new coins, drawn in (query, f) order
+    Qh = (oracle.synth(99, 2000, d) * 6.0).astype(np.float32)
+    qv = cube.vertices(to_dev(ctx, Qh)).cpu().numpy()
+    oq, nd = memo.apply(oracle.cube_h(Qh, V, t, np.float32(w)))
+    assert nd > 0
+    assert np.array_equal(qv, oq)
+    f, h, b, st_gpu = cube.memo()
+    of, oh, ob = memo.as_lists()
+    o1, o2 = np.lexsort((h, f)), np.lexsort((oh, of))
+    assert np.array_equal(f[o1], of[o2]) and np.array_equal(h[o1], oh[o2]) and np.array_equal(b[o1], ob[o2])
+    assert st_gpu == memo.state.value
+    ptr, out = cube.query(to_dev(ctx, Xh[:300]), 14)
+    for q in range(300):
+        seq = oracle.cube_probe_seq(ov[q], 14, k)
+        exp = np.concatenate([oidx[0][orp[0][v]:orp[0][v + 1]] for v in seq])
+        assert np.array_equal(out[ptr[q]:ptr[q + 1]], exp), q
+
+
+@pytest.mark.parametrize("name", cases("lloyd"))
+def test_kmeans_update_golden(ctx, name):
+    m, g = META[name], golden(name)
+    X = to_dev(ctx, oracle.synth(m["data_seed"], m["N"], m["d"]))
+    for it in range(len(g["cont"])):
+        a = to_dev(ctx, g[f"assign{it}"])
+        Cold = to_dev(ctx, g[f"centers{it}"])
+        Cn, cnt, cont = lshkm.kmeans_update(ctx, X, a, Cold, m["metric"], m["min_dist"])
+        assert cont == bool(g["cont"][it]), it
+        exp = g[f"centers{it + 1}"] if cont else oracle.kmeans_update(
+            oracle.synth(m["data_seed"], m["N"], m["d"]), g[f"assign{it}"], g[f"centers{it}"], m["metric"], m["min_dist"])[0]
+        assert np.array_equal(Cn.cpu().numpy().view(np.uint64), exp.view(np.uint64)), it
+        assert np.array_equal(cnt.cpu().numpy(), np.bincount(g[f"assign{it}"], minlength=m["K"])), it
+
+
+def test_kmeans_update_large_vs_oracle(ctx):
+    N, d, K = 1_000_000, 128, 256
+    X = ctx.synth(0x5EED, N, d)
+    a = ctx.torch.randint(0, K, (N,), dtype=ctx.torch.int32, device=ctx.dev)
+    a[:5] = 3                      # uneven, and one empty cluster
+    a[a == 17] = 18
+    Cold = ctx.torch.zeros((K, d), dtype=ctx.torch.float64, device=ctx.dev)
+    Cn, cnt, cont = lshkm.kmeans_update(ctx, X, a, Cold, "euclidean", 0.05)
+    on, ocnt, ocont = oracle.kmeans_update(X.cpu().numpy(), a.cpu().numpy(), Cold.cpu().numpy(), "euclidean", 0.05)
+    assert cont == ocont
+    assert np.array_equal(cnt.cpu().numpy(), ocnt) and ocnt[17] == 0
+    assert np.array_equal(Cn.cpu().numpy().view(np.uint64), on.view(np.uint64))
+    # sharded fast mode: per-shard exact-order sums + a sum of partials
+    s1, c1 = lshkm.kmeans_partial(ctx, X[:N // 2], a[:N // 2], K)
+    s2, c2 = lshkm.kmeans_partial(ctx, X[N // 2:], a[N // 2:], K)
+    C2, cont2 = lshkm.kmeans_finalize(ctx, s1 + s2, c1 + c2, Cold, "euclidean", 0.05)
+    assert np.array_equal((c1 + c2).cpu().numpy(), ocnt)
+    rel = (C2 - Cn).abs().max().item() / Cn.abs().max().item()
+    assert rel < 1e-13 and cont2 == cont
