@@ -29,11 +29,18 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 FP32_MFMA_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: FP32 matrix peak
 
 
-def load_pkg():
-    spec = importlib.util.spec_from_file_location("lshkm_amd", os.path.join(ROOT, "crypto-recommendation_amd", "lshkm.py"))
+def load_module(name, fname):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "crypto-recommendation_amd", fname))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
+
+
+def load_pkg():
+    return load_module("lshkm_amd", "lshkm.py")
+
+
+sharding = load_module("lshkm_sharding", "sharding.py")
 
 
 def cpu_baseline(sample_hash, sample_assign, K):
@@ -103,11 +110,11 @@ def main():
     X = ctx.synth(SEED_DATA, N, D, row0=rank * N)
     V, t, r, _ = lk.params_lsh_euclidean(SEED_PARAMS, L_TABLES, K_FUNCS, D, W)
     lsh = lk.LSH(ctx, "euclidean", D, K_FUNCS, L_TABLES, nb, W, V=V, t=t, r=r)
-    rows = np.arange(K, dtype=np.int64) * (N_total // K)          # reference init: rows i*floor(N/K)
+    rows = sharding.centroid_rows(N_total, K)                      # reference init: rows i*floor(N/K)
     Cc = torch.empty((K, D), dtype=torch.float64, device=dev)
     for i, row in enumerate(rows):                                 # centroids may live on other shards
         Cc[i] = ctx.synth(SEED_DATA, 1, D, row0=int(row))[0].double()
-    src = np.array([row - rank * N if rank * N <= row < (rank + 1) * N else -1 for row in rows], np.int32)
+    src = sharding.local_src_rows(rows, rank * N, N)               # centroid override, shard-local
     tuples = torch.empty((N, L_TABLES, K_FUNCS), dtype=torch.int32, device=dev)
     bucket = torch.empty((N, L_TABLES), dtype=torch.int32, device=dev)
     assign = torch.empty((N,), dtype=torch.int32, device=dev)

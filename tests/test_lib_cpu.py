@@ -1,0 +1,80 @@
+"""CPU-side checks of the product's host code (no GPU needed):
+the C-ABI library loads and exports every symbol include/lshkm.h declares,
+the host parameter generation reproduces the reference's RNG draws bit for
+bit, and the soft-x87 emulation used by the kernels' exact paths agrees with
+real x87 long double."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from amd import PKG, ROOT, lshkm
+from conftest import cases, golden, golden_meta
+
+META = golden_meta()
+
+
+def test_library_exports_declared_symbols():
+    L = lshkm.lib()
+    declared = lshkm.declared_symbols()
+    assert len(declared) >= 30
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    assert lshkm.lib().lshkm_version().decode().startswith("lshkm-gfx950")
+
+
+def test_library_is_gfx950_code_object():
+    with open(os.path.join(PKG, "liblshkm.so"), "rb") as f:
+        blob = f.read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+
+
+@pytest.mark.parametrize("name", cases("lsh"))
+def test_params_lsh_match_reference(name):
+    m, g = META[name], golden(name)
+    if m["metric"] == "euclidean":
+        V, t, r, st = lshkm.params_lsh_euclidean(m["seed"], m["L"], m["k"], m["d"], m["w"])
+        assert np.array_equal(V, g["V"]) and np.array_equal(t, g["t"]) and np.array_equal(r, g["r"])
+        assert st == oracle.gen_lsh_euclid(m["seed"], m["L"], m["k"], m["d"], np.float32(m["w"]))[3]
+    else:
+        R, st = lshkm.params_lsh_cosine(m["seed"], m["L"], m["k"], m["d"])
+        assert np.array_equal(R.view(np.uint64), g["R"].view(np.uint64))
+        assert st == oracle.gen_lsh_cosine(m["seed"], m["L"], m["k"], m["d"])[1]
+
+
+@pytest.mark.parametrize("name", cases("cube"))
+def test_params_cube_match_reference(name):
+    m, g = META[name], golden(name)
+    if m["metric"] == "euclidean":
+        V, t, st = lshkm.params_cube_euclidean(m["seed"], m["k"], m["d"], m["w"])
+        assert np.array_equal(V, g["V"]) and np.array_equal(t, g["t"])
+        assert st == oracle.gen_cube_euclid(m["seed"], m["k"], m["d"], np.float32(m["w"]))[2]
+    else:
+        R, st = lshkm.params_cube_cosine(m["seed"], m["k"], m["d"])
+        assert np.array_equal(R.view(np.uint64), g["R"].view(np.uint64))
+
+
+def test_params_bad_arguments_fail_loudly():
+    with pytest.raises(lshkm.LshkmError):
+        lshkm.params_lsh_euclidean(1, 0, 4, 128, 0.4)
+
+
+def test_softx87_matches_long_double(tmp_path):
+    exe = tmp_path / "softx87_check"
+    subprocess.run(["g++", "-O1", "-std=c++14", "-o", str(exe), os.path.join(ROOT, "tests", "softx87_check.cpp")],
+                   check=True)
+    out = subprocess.run([str(exe), "100000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad=0" in out.stdout
+
+
+def test_no_gpu_means_loud_failure():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(Exception):
+        lshkm.Context(0)
