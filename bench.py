@@ -26,7 +26,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 D, L_TABLES, K_FUNCS, W, BUCKET_DIV, SEED_DATA, SEED_PARAMS = 128, 5, 4, 0.4, 100, 0x5EED, 12345
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-FP32_MFMA_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: FP32 matrix peak
+F16_MFMA_PEAK_TFS = 2500.0     # MI355X_MICROARCH.md: FP16/BF16 MFMA dense peak
 
 
 def load_module(name, fname):
@@ -122,15 +122,9 @@ def main():
     p = lambda t_: C.c_void_p(t_.data_ptr())
     src_p = src.ctypes.data_as(C.c_void_p)
 
-    def hash_step():
-        lk._ck(lib.lshkm_lsh_hash(lsh.h, p(X), N, p(tuples), None, p(bucket)))
-
-    def assign_step():
-        lk._ck(lib.lshkm_lloyd_assign(ctx.h, p(X), N, D, p(Cc), K, lk.EUCLIDEAN, src_p, p(assign), p(dist_)))
-
     def step():
-        hash_step()
-        assign_step()
+        # one pass: tuples + bucket IDs + cluster IDs + fp64 distances (lshkm_hash_assign)
+        lk._ck(lib.lshkm_hash_assign(lsh.h, p(X), N, p(Cc), K, src_p, p(tuples), None, p(bucket), p(assign), p(dist_)))
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -154,29 +148,33 @@ def main():
     ambig = ctx.stat(lk.STAT_ASSIGN_AMBIG)
     hexact = ctx.stat(lk.STAT_HASH_EXACT)
 
-    # Per-kernel timing with HIP events on the stream the kernels run on
-    # (the context runs on torch's current stream, so torch events bracket them).
+    # Dominant kernel (fused_kernel<true>): HIP events recorded by the library
+    # around that launch, on the stream it runs on; averaged over reps steps.
     reps = max(3, args.steps)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    ev[0].record()
+    lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 1))
+    ms = C.c_float()
+    t_kernel = 0.0
     for _ in range(reps):
-        assign_step()
-    ev[1].record()
-    for _ in range(reps):
-        hash_step()
-    ev[2].record()
-    torch.cuda.synchronize(dev)
-    t_assign = ev[0].elapsed_time(ev[1]) / reps / 1e3
-    t_hash = ev[1].elapsed_time(ev[2]) / reps / 1e3
+        step()
+        lk._ck(lib.lshkm_last_kernel_ms(ctx.h, C.byref(ms)))
+        t_kernel += ms.value / 1e3
+    lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 0))
+    t_kernel /= reps
 
-    assign_flops = 2.0 * D * K * N                     # 65,536 flop/pt at K=256
-    hash_bytes = N * (4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES)    # 612 B/pt
+    # Algorithmic bytes and flops per point: 512 B read, 80 B tuples +
+    # 20 B bucket IDs + 4 B cluster ID + 8 B distance written = 624 B; 2*d*(L*k + K) flop.
+    bytes_per_pt = 4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES + 4 + 8
+    flop_per_pt = 2 * D * (L_TABLES * K_FUNCS + K)
+    kpad = (K + 63) // 64 * 64
+    mfma_flop_per_pt = 3 * 2 * D * (kpad + 32)          # 3 split-f16 products, padded tiles
+    hbm_gbs = bytes_per_pt * N / t_kernel / 1e9
+    mfma_tfs = mfma_flop_per_pt * N / t_kernel / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
         if tj.get("N") == N and tj.get("K") == K:
-            traffic = tj.get("assign_hbm_bytes_per_launch")
+            traffic = tj.get("hbm_bytes_per_launch")
 
     if rank == 0:
         value = N_total * args.steps / elapsed
@@ -191,19 +189,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32 storage; fp32-MFMA scores, fp64/x87-exact results",
+            "dtype": "fp32 points; split-f16 MFMA scores (f32 accumulate), fp64/x87-exact results",
             "data": "synthetic (include/lshkm_synth.h), resident in HBM",
             "config": {"workload": f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128",
                        "N_per_gpu": N, "N_total": N_total, "d": D, "K": K, "L": L_TABLES, "k": K_FUNCS,
                        "w": W, "nb": nb, "parallelism": f"dp{world} (row shards)"},
             "roofline": {
-                "bound": "mfma", "kernel": "assign_mfma_kernel<128> (+prep/exact/override launches)",
-                "achieved": assign_flops / t_assign / 1e12, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": assign_flops / t_assign / 1e12 / FP32_MFMA_PEAK_TFS,
+                "bound": "hbm", "kernel": "fused_kernel<true> (hash + assign, one read of X)",
+                "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "assign_ms": t_assign * 1e3,
-                "hash_kernel": {"bound": "hbm", "achieved_GBs": hash_bytes / t_hash / 1e9, "peak_GBs": HBM_PEAK_GBS,
-                                "frac": hash_bytes / t_hash / 1e9 / HBM_PEAK_GBS, "hash_ms": t_hash * 1e3},
+                "bytes_per_point": bytes_per_pt, "kernel_ms": t_kernel * 1e3,
+                "mfma": {"achieved_TFs": mfma_tfs, "peak_TFs": F16_MFMA_PEAK_TFS, "frac": mfma_tfs / F16_MFMA_PEAK_TFS,
+                         "flop_per_point_executed": mfma_flop_per_pt, "flop_per_point_algorithmic": flop_per_pt},
             },
             "exactness": {"assign_ambiguous_rows": ambig, "hash_exact_fallbacks": hexact},
         }

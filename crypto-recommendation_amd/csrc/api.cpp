@@ -90,6 +90,21 @@ int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* v) {
     return 0;
 }
 
+int lshkm_ctx_enable_timing(lshkm_ctx ctx, int on) {
+    LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
+    for (hipEvent_t& e : ctx->tev)
+        if (!e) LSHKM_HIP(hipEventCreate(&e));
+    ctx->timing = on != 0;
+    return 0;
+}
+
+int lshkm_last_kernel_ms(lshkm_ctx ctx, float* ms) {
+    LSHKM_CHECK(ctx && ms && ctx->tev[1], LSHKM_ERR_STATE, "timing not enabled");
+    LSHKM_HIP(hipEventSynchronize(ctx->tev[1]));
+    LSHKM_HIP(hipEventElapsedTime(ms, ctx->tev[0], ctx->tev[1]));
+    return 0;
+}
+
 int lshkm_reset_stats(lshkm_ctx ctx) {
     LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
     LSHKM_HIP(hipMemsetAsync(ctx->stats.p, 0, sizeof(unsigned long long) * STAT_COUNT, ctx->stream));
@@ -196,6 +211,31 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
     LSHKM_HIP(hipMemcpyAsync(t_d.p, tt.data(), LK * 4, hipMemcpyHostToDevice, s));
     LSHKM_HIP(hipMemcpyAsync(pn_d.p, pn.data(), LK * 8, hipMemcpyHostToDevice, s));
     LSHKM_HIP(hipMemcpyAsync(r_d.p, rr.data(), LK * 4, hipMemcpyHostToDevice, s));
+    // split-f16 image for the fused hash+assign kernel
+    fused_ok = metric == LSHKM_METRIC_EUCLIDEAN && d == 128 && LK <= 32;
+    std::vector<_Float16> vh, vl;
+    std::vector<double> v1;
+    if (fused_ok) {
+        vh.assign(64 * 128, (_Float16)0.f);
+        vl.assign(64 * 128, (_Float16)0.f);
+        v1.assign(LK, 0.0);
+        for (int f = 0; f < LK; f++) {
+            long double s1 = 0.0L;
+            for (int j = 0; j < 128; j++) {
+                const float v = V[(size_t)f * d + j];
+                const _Float16 hv = (_Float16)v;
+                vh[f * 128 + j] = hv;
+                vl[f * 128 + j] = (_Float16)(v - (float)hv);
+                s1 += fabsl((long double)v);
+            }
+            v1[f] = (double)s1 * (1.0 + 0x1p-40);
+        }
+        if ((rc = vh_d.reserve(vh.size() * 2)) || (rc = vl_d.reserve(vl.size() * 2)) || (rc = v1_d.reserve(LK * 8)))
+            return rc;
+        LSHKM_HIP(hipMemcpyAsync(vh_d.p, vh.data(), vh.size() * 2, hipMemcpyHostToDevice, s));
+        LSHKM_HIP(hipMemcpyAsync(vl_d.p, vl.data(), vl.size() * 2, hipMemcpyHostToDevice, s));
+        LSHKM_HIP(hipMemcpyAsync(v1_d.p, v1.data(), LK * 8, hipMemcpyHostToDevice, s));
+    }
     LSHKM_HIP(hipStreamSynchronize(s));   // host vectors go out of scope
     // host copies kept for introspection
     hV.assign(V ? V : (const float*)nullptr, V ? V + (size_t)LK * d : nullptr);
@@ -265,15 +305,59 @@ int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, in
 }
 
 // ------------------------------------------------------------------- Lloyd
-int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
-                       const int32_t* src_rows_host, int32_t* assign, double* dist) {
-    LSHKM_CHECK(ctx && X && C && assign && dist && N >= 0 && d > 0 && K > 0, LSHKM_ERR_ARG, "bad arguments");
-    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
-    LSHKM_HIP(hipSetDevice(ctx->device));
+}  // extern "C"
+
+// Kernel path for euclidean assignment: the split-f16 fused kernel (d = 128),
+// else the f32-MFMA kernel (d <= 256), else the exact pass. LSHKM_ASSIGN_PATH
+// = "f32" / "exact" forces a path (tests compare them).
+static int assign_path(int metric, int d) {
+    const char* e = getenv("LSHKM_ASSIGN_PATH");
+    if (metric != LSHKM_METRIC_EUCLIDEAN || (e && !strcmp(e, "exact"))) return 2;
+    if (d == 128 && !(e && !strcmp(e, "f32"))) return 0;
+    return assign_dp(d) > 0 ? 1 : 2;
+}
+
+static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
+                       const int32_t* src_rows_host, int32_t* assign, double* dist, lshkm_lsh lsh, int32_t* tuples,
+                       int32_t* phi, int32_t* bucket) {
     hipStream_t s = ctx->stream;
     const int DP = assign_dp(d);
+    const int path = assign_path(metric, d);
+    const bool fuse_hash = lsh && path == 0 && lsh->proj.fused_ok;
     int rc;
-    if (metric == LSHKM_METRIC_EUCLIDEAN && DP > 0) {
+    if (lsh && !fuse_hash && (rc = launch_proj_hash(s, lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE,
+                                                    X, N, lsh->proj.params(lsh->nb),
+                                                    lsh->metric == LSHKM_METRIC_EUCLIDEAN ? tuples : nullptr, phi, bucket,
+                                                    (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if (path == 0) {
+        const int Kpad = (K + 63) / 64 * 64;
+        if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) || (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4)) ||
+            (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 4)) || (rc = ctx->ws_counter.reserve(64)))
+            return rc;
+        unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
+        LSHKM_HIP(hipMemsetAsync(cnt, 0, 8, s));
+        _Float16* Ch = (_Float16*)ctx->ws_c32.p;
+        _Float16* Cl = Ch + (size_t)Kpad * 128;
+        float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
+        float* cnh = cbound + 8;
+        if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        FusedLaunch f;
+        f.X = X; f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C; f.Kpad = Kpad;
+        f.assign = assign; f.dist = dist; f.ambig = (int32_t*)ctx->ws_ambig.p; f.ambig_count = cnt;
+        f.stats = (unsigned long long*)ctx->stats.p;
+        if (fuse_hash) {
+            const ProjTable& pj = lsh->proj;
+            f.Vh = pj.vh_d.as<_Float16>(); f.Vl = pj.vl_d.as<_Float16>(); f.PT = pj.PT_d.as<double>();
+            f.tv = pj.t_d.as<float>(); f.pnorm = pj.pn_d.as<double>(); f.v1 = pj.v1_d.as<double>();
+            f.rv = pj.r_d.as<int32_t>(); f.w = pj.w; f.L = pj.L; f.k = pj.k; f.LK = pj.LK; f.LKpad = pj.LKpad;
+            f.nb = lsh->nb; f.tuples = tuples; f.phi = phi; f.bucket = bucket;
+        }
+        if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
+        if ((rc = launch_fused(s, fuse_hash, f))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
+        if ((rc = launch_assign_exact(s, X, N, d, C, K, metric, (const int32_t*)ctx->ws_ambig.p, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * DP * 4)) || (rc = ctx->ws_cconst.reserve((size_t)3 * Kpad * 4)) ||
             (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 4)) ||
@@ -303,6 +387,27 @@ int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         if ((rc = launch_assign_override(s, (const int32_t*)ctx->ws_src.p, K, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
     }
     return 0;
+}
+
+extern "C" {
+
+int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
+                       const int32_t* src_rows_host, int32_t* assign, double* dist) {
+    LSHKM_CHECK(ctx && (X || N == 0) && C && (assign || N == 0) && (dist || N == 0) && N >= 0 && d > 0 && K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    return assign_impl(ctx, X, N, d, C, K, metric, src_rows_host, assign, dist, nullptr, nullptr, nullptr, nullptr);
+}
+
+int lshkm_hash_assign(lshkm_lsh lsh, const float* X, int64_t N, const double* C, int K, const int32_t* src_rows_host,
+                      int32_t* tuples, int32_t* phi, int32_t* bucket, int32_t* assign, double* dist) {
+    LSHKM_CHECK(lsh && (X || N == 0) && C && (assign || N == 0) && (dist || N == 0) && N >= 0 && K > 0, LSHKM_ERR_ARG,
+                "bad arguments");
+    lshkm_ctx ctx = lsh->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    return assign_impl(ctx, X, N, lsh->proj.d, C, K, LSHKM_METRIC_EUCLIDEAN, src_rows_host, assign, dist, lsh, tuples,
+                       phi, bucket);
 }
 
 int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X) {

@@ -1,0 +1,379 @@
+// fused.hip — one pass over the points: LSH hashing + Lloyd assignment on gfx950.
+//
+// Replaces, in one read of each point (SURVEY §8a rows a1-a3, a7's bucket ID,
+// a12): EuclideanPhiGen::generate (lib/generators/euclidean_phi_gen.hpp:77-92)
+// for L tables of k EuclideanH functions (euclidean_h_gen.hpp:73-76), and
+// lloyds_assignment (lib/clustering_phases/assignment.hpp:54-80).
+//
+// Split-precision f16 MFMA. Every operand is split x = xh + xl (xh = f16(x),
+// xl = f16(x - xh)); a dot product is sum(xh ch) [acc_hi] + sum(xh cl + xl ch)
+// [acc_lo] on v_mfma_f32_32x32x16_f16: products of f16 values are exact in
+// f32, and the separate hi accumulator keeps the rounding of the large terms
+// at d ulps of f32. Rigorous bound on |dot~ - x.c|:
+//   A1 |x||c| + A2 (|x|_1 + |c|_1),  A1 = 1.25 * 2^-16, A2 = 2^-24,
+// which assumes nothing better than round-toward-zero accumulation. The f16
+// range is guarded: a point with |x_j| > 2^15 (or non-finite) or a centroid set
+// with |c_j| > 2^15 is never certified, so such inputs take the exact path.
+//
+// Block = 4 waves x 32 points. Wave w keeps its 32 points in registers as the
+// B operand (lane half h holds dims 16s+8h..16s+8h+7 of point lane&31, hi and
+// lo: 64 VGPRs); centroid hi/lo rows stream through LDS (64 per chunk, rows
+// padded to 272 B: conflict-free ds_read_b128) as the A operand, so the tile
+// D[centroid][point] has the point on the lane and the argmin is
+// register-local. The hash projections are one extra 32-row tile.
+// Per score: t = x.c - |c|^2/2 (argmax of t = argmin of the distance); the
+// lane tracks the largest t (m1, index i1) and the runner-up m2. A point is
+// certified iff m2 < m1 - 2E: then i1 is the reference's argmin, and its
+// distance is recomputed in reference order (fp64 chain over j, sqrt).
+// Otherwise the row goes to the exact all-centroid pass (assign.hip).
+// Hash values: y = (dot~ + t)/w in fp64 with the split bound; a floor it
+// cannot certify is redone from the exact row with the fp64 bound of
+// hash.hip, and then, if needed, with the soft-x87 emulation.
+#include "common.h"
+#include "kernels.h"
+#include "softx87.h"
+
+namespace lshkm {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int FU_THREADS = 256;
+constexpr int FU_PB = 128;               // points per block
+constexpr int FU_CC = 64;                // centroids per LDS chunk
+constexpr int FU_D = 128;                // dimension handled by this kernel
+constexpr int FU_RS = FU_D + 8;          // f16 LDS row stride (elements) = 272 B
+constexpr int FU_CH_BYTES = FU_CC * FU_RS * 2;          // one of hi / lo
+constexpr int FU_CHUNK_BYTES = 2 * FU_CH_BYTES + FU_CC * 4;
+constexpr int FU_XSTAGE_BYTES = 4 * 32 * FU_D * 4;      // 64 KiB (aliases the chunk region)
+constexpr int FU_HS_OFF = FU_XSTAGE_BYTES;              // hash values [128][32] int32
+constexpr int FU_LDS_BYTES = FU_HS_OFF + FU_PB * 32 * 4; // 80 KiB -> 2 blocks / CU
+static_assert(FU_CHUNK_BYTES <= FU_XSTAGE_BYTES, "chunk region must fit in the staging alias");
+
+constexpr double FU_A1 = 1.25 * 0x1p-16;
+constexpr double FU_A2 = 0x1p-24;
+constexpr float FU_RANGE = 32768.f;
+
+struct FusedArgs {
+    const float* X;
+    int64_t N;
+    // centroids (prepared by fused_centroid_prep)
+    const _Float16* Ch;
+    const _Float16* Cl;
+    const float* cnh;        // [Kpad] -||c||^2 / 2 (f32), -inf for padding rows
+    const float* cbound;     // [0] = ec (times |x|), [1] = eb (constant), [2] = range flag (bits)
+    const double* C64;       // [K][128] exact centroids
+    int Kpad;
+    // hash family (HASH only)
+    const _Float16* Vh;      // [32][128] f16 hi of the projections (rows >= LK zero)
+    const _Float16* Vl;
+    const double* PT;        // [128][LKpad] fp64 projections (exact paths)
+    const float* tv;         // [LK]
+    const double* pnorm;     // [LK] ||v||_2 (rounded up)
+    const double* v1;        // [LK] ||v||_1 (rounded up)
+    const int32_t* rv;       // [LK]
+    float w;
+    int L, k, LK, LKpad;
+    int64_t nb;
+    // outputs
+    int32_t* tuples;         // [N][L][k] (may be null)
+    int32_t* phi;            // [N][L] (may be null)
+    int32_t* bucket;         // [N][L] (may be null)
+    int32_t* assign;         // [N]
+    double* dist;            // [N]
+    int32_t* ambig;          // [N] uncertified rows
+    unsigned long long* ambig_count;
+    unsigned long long* stats;
+};
+
+__device__ inline void split8(const float* x, half8& hi, half8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const _Float16 hv = (_Float16)x[j];
+        hi[j] = hv;
+        lo[j] = (_Float16)(x[j] - (float)hv);
+    }
+}
+
+// Exact (reference-order) hash of one projection from the fp32 row in HBM.
+__device__ int32_t hash_exact_row(const float* __restrict__ xrow, const double* __restrict__ PT, int LKpad, int f,
+                                  float t, float w, double pn, unsigned long long* stats) {
+    double acc = 0.0, xn2 = 0.0;
+    for (int j = 0; j < FU_D; j++) {
+        const double xj = (double)xrow[j];
+        xn2 = fma(xj, xj, xn2);
+        acc = fma(PT[(size_t)j * LKpad + f], xj, acc);
+    }
+    const double P = pn * sqrt(xn2) * (1.0 + 0x1p-40);
+    const double tt = (double)t, ww = (double)w;
+    const double y = (acc + tt) / ww;
+    const double B = ((double)(FU_D + 2) * 0x1p-52 * (P + fabs(tt))) / ww + fabs(y) * 0x1p-51;
+    const double lo = floor(y - B), hi = floor(y + B);
+    if (lo == hi) return (int32_t)lo;
+    sx80 s = sx_zero();
+    for (int j = 0; j < FU_D; j++) s = sx_add_double(s, __dmul_rn(PT[(size_t)j * LKpad + f], (double)xrow[j]));
+    s = sx_add_double(s, tt);
+    atomicAdd(stats + STAT_HASH_EXACT, 1ull);
+    return (int32_t)sx_floor_i64(sx_div(s, sx_from_float(w)));
+}
+
+// Load rows [r0, r0 + 64) of a [rows][128] f16 matrix into the padded LDS image.
+__device__ inline void load_rows_f16(const _Float16* __restrict__ src, int r0, _Float16* dst) {
+    // 64 rows x 16 granules of 16 B, 256 threads -> 4 granules each
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int e = threadIdx.x + u * FU_THREADS;
+        const int row = e >> 4, g = e & 15;
+        const float4 v = *reinterpret_cast<const float4*>(src + (size_t)(r0 + row) * FU_D + g * 8);
+        *reinterpret_cast<float4*>(dst + row * FU_RS + g * 8) = v;
+    }
+}
+
+// One 32-row tile: acc_hi = sum(Ah Bh), acc_lo = sum(Ah Bl + Al Bh).
+__device__ inline void tile_mfma(const _Float16* ah_row, const _Float16* al_row, const half8 (&bh)[8],
+                                 const half8 (&bl)[8], floatx16& acc_hi, floatx16& acc_lo) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) { acc_hi[r] = 0.f; acc_lo[r] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const half8 ah = *reinterpret_cast<const half8*>(ah_row + 16 * s);
+        const half8 al = *reinterpret_cast<const half8*>(al_row + 16 * s);
+        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc_hi, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc_lo, 0, 0, 0);
+    }
+}
+
+template <bool HASH>
+__global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    const int lp = wave * 32 + col;                         // point within the block
+    const int64_t pbase = (int64_t)blockIdx.x * FU_PB + wave * 32;
+    const int64_t row = pbase + col;
+    const bool valid = row < a.N;
+
+    // ---- phase 0: stage this wave's 32 rows (XOR-swizzled 16-B granules), split to f16
+    float* xs = reinterpret_cast<float*>(smem) + wave * 32 * FU_D;
+    for (int e = lane; e < 32 * (FU_D / 4); e += 64) {
+        const int r = e >> 5, g = e & 31;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (pbase + r < a.N) v = *reinterpret_cast<const float4*>(a.X + (pbase + r) * FU_D + g * 4);
+        *reinterpret_cast<float4*>(xs + r * FU_D + 4 * (g ^ (r & 15))) = v;
+    }
+    __syncthreads();
+    half8 bh[8], bl[8];
+    float xn2f = 0.f, x1f = 0.f, xmax = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        float xv[8];
+        const int g0 = 4 * s + 2 * h;                       // granules of dims 16s+8h .. +7
+        const float4 p0 = *reinterpret_cast<const float4*>(xs + col * FU_D + 4 * (g0 ^ (col & 15)));
+        const float4 p1 = *reinterpret_cast<const float4*>(xs + col * FU_D + 4 * ((g0 + 1) ^ (col & 15)));
+        xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
+        xv[4] = p1.x; xv[5] = p1.y; xv[6] = p1.z; xv[7] = p1.w;
+        split8(xv, bh[s], bl[s]);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            xn2f = fmaf(xv[j], xv[j], xn2f);
+            x1f += fabsf(xv[j]);
+            xmax = fmaxf(xmax, fabsf(xv[j]));
+        }
+    }
+    xn2f += __shfl_xor(xn2f, 32);
+    x1f += __shfl_xor(x1f, 32);
+    xmax = fmaxf(xmax, __shfl_xor(xmax, 32));
+    // f32 sums of squares/abs: inflate by (1 + 2^-16) (> d * 2^-24) to stay upper bounds
+    const double xn2 = (double)xn2f * (1.0 + 0x1p-16);
+    const double nx = sqrt(xn2);
+    const double x1 = (double)x1f * (1.0 + 0x1p-16);
+    const bool x_ok = xmax <= FU_RANGE;                    // false for inf / nan too
+    __syncthreads();                                       // staging area becomes the chunk region
+
+    _Float16* lch = reinterpret_cast<_Float16*>(smem);
+    _Float16* lcl = reinterpret_cast<_Float16*>(smem + FU_CH_BYTES);
+    float* lcn = reinterpret_cast<float*>(smem + 2 * FU_CH_BYTES);
+    int32_t* hs = reinterpret_cast<int32_t*>(smem + FU_HS_OFF);
+    const _Float16* my_h = lch + col * FU_RS + 8 * h;      // A rows of this lane (tile 0)
+    const _Float16* my_l = lcl + col * FU_RS + 8 * h;
+
+    // ---- hash tile (projections as 32 extra rows)
+    if (HASH) {
+        load_rows_f16(a.Vh, 0, lch);
+        load_rows_f16(a.Vl, 0, lcl);   // rows 32..63 of the image are unused here
+        __syncthreads();
+        floatx16 acc_hi, acc_lo;
+        tile_mfma(my_h, my_l, bh, bl, acc_hi, acc_lo);
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int f = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (f >= a.LK || !valid) continue;
+            const float dotf = acc_hi[r] + acc_lo[r];
+            const double tt = (double)a.tv[f], ww = (double)a.w;
+            const double y = ((double)dotf + tt) / ww;
+            const double Ed = FU_A1 * a.pnorm[f] * nx + FU_A2 * (a.v1[f] + x1) + 0x1p-23 * fabs((double)dotf);
+            const double B = (Ed + 0x1p-50 * (a.pnorm[f] * nx + fabs(tt))) / ww + fabs(y) * 0x1p-50;
+            const double lo = floor(y - B), hi = floor(y + B);
+            int32_t hv;
+            if (lo == hi && x_ok) hv = (int32_t)lo;
+            else hv = hash_exact_row(a.X + row * FU_D, a.PT, a.LKpad, f, a.tv[f], a.w, a.pnorm[f], a.stats);
+            hs[lp * 32 + f] = hv;
+        }
+        __syncthreads();
+    }
+
+    // ---- centroid chunks
+    const float ecf = a.cbound[0], ebf = a.cbound[1];
+    const bool c_ok = __float_as_uint(a.cbound[2]) == 0u;
+    const float E = (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2) * (1.f + 0x1p-20f) + 1e-30f;
+    float m1 = -__builtin_inff(), m2 = -__builtin_inff();
+    int i1 = 0;
+    for (int c0 = 0; c0 < a.Kpad; c0 += FU_CC) {
+        load_rows_f16(a.Ch, c0, lch);
+        load_rows_f16(a.Cl, c0, lcl);
+        if (threadIdx.x < FU_CC) lcn[threadIdx.x] = a.cnh[c0 + threadIdx.x];
+        __syncthreads();
+#pragma unroll 1
+        for (int t = 0; t < FU_CC / 32; t++) {
+            floatx16 acc_hi, acc_lo;
+            tile_mfma(my_h + t * 32 * FU_RS, my_l + t * 32 * FU_RS, bh, bl, acc_hi, acc_lo);
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int cb = t * 32 + 8 * g + 4 * h;     // D rows of registers 4g..4g+3
+                const float4 cn = *reinterpret_cast<const float4*>(lcn + cb);
+                const float cnv[4] = {cn.x, cn.y, cn.z, cn.w};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float tv = (acc_hi[4 * g + q] + acc_lo[4 * g + q]) + cnv[q];
+                    m2 = fmaxf(m2, fminf(m1, tv));
+                    const bool c1 = tv > m1;
+                    m1 = c1 ? tv : m1;
+                    i1 = c1 ? c0 + cb + q : i1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- merge the two lane halves of each point, certify
+    const float om1 = __shfl_xor(m1, 32), om2 = __shfl_xor(m2, 32);
+    const int oi1 = __shfl_xor(i1, 32);
+    const float M2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
+    const int I1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
+    const float M1 = fmaxf(m1, om1);
+    const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * (double)E);
+
+    // ---- exact-order distance of the winner: lane h=0 dims [0,64), lane h=1 [64,128)
+    double accd = 0.0;
+    const float* xrow = a.X + row * FU_D;
+    if (h == 0 && cert && valid) {
+        const double* crow = a.C64 + (size_t)I1 * FU_D;
+        for (int j = 0; j < FU_D / 2; j++) {
+            const double df = __dsub_rn((double)xrow[j], crow[j]);
+            accd = __dadd_rn(accd, __dmul_rn(df, df));
+        }
+    }
+    const double part = __shfl_xor(accd, 32);
+    if (h == 1 && valid) {
+        if (cert) {
+            double s2 = part;
+            const double* crow = a.C64 + (size_t)I1 * FU_D;
+            for (int j = FU_D / 2; j < FU_D; j++) {
+                const double df = __dsub_rn((double)xrow[j], crow[j]);
+                s2 = __dadd_rn(s2, __dmul_rn(df, df));
+            }
+            a.assign[row] = I1;
+            a.dist[row] = sqrt(s2);
+        } else {
+            const unsigned long long slot = atomicAdd(a.ambig_count, 1ull);
+            a.ambig[slot] = (int32_t)row;
+        }
+    }
+
+    // ---- LSH outputs: tuples, phi, bucket ids (euclidean_phi_gen.hpp:77-92, cust_hashtable.hpp:68)
+    if (HASH) {
+        const int64_t p0 = (int64_t)blockIdx.x * FU_PB;
+        const int npts = (int)min((int64_t)FU_PB, a.N - p0);
+        const int LK = a.LK, L = a.L, k = a.k;
+        if (a.tuples)
+            for (int e = threadIdx.x; e < npts * LK; e += FU_THREADS) {
+                const int pp = e / LK, f = e - pp * LK;
+                a.tuples[p0 * LK + e] = hs[pp * 32 + f];
+            }
+        const int64_t M = 2147483647;   // int(pow(2,32)-5) under g++ (euclidean_phi_gen.hpp:70)
+        for (int q = threadIdx.x; q < npts * L; q += FU_THREADS) {
+            const int pp = q / L, l = q - pp * L;
+            uint32_t hn = 0;
+            for (int i = 0; i < k; i++) {
+                const int hi = hs[pp * 32 + l * k + i];
+                const int64_t temp = (int64_t)(int32_t)((uint32_t)hi * (uint32_t)a.rv[l * k + i]);
+                hn += (uint32_t)(int32_t)((temp % M + M) % M);
+            }
+            const uint32_t ph = (hn % 2147483647u + 2147483647u) % 2147483647u;
+            if (a.phi) a.phi[p0 * L + q] = (int32_t)ph;
+            if (a.bucket) a.bucket[p0 * L + q] = (int32_t)((uint64_t)ph % (uint64_t)a.nb);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ preparation
+// Centroids -> f16 hi/lo rows, -||c||^2/2, and the per-call bound maxima.
+__global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpad, _Float16* __restrict__ Ch,
+                                    _Float16* __restrict__ Cl, float* __restrict__ cnh, unsigned int* __restrict__ cb) {
+    const int c = blockIdx.x;            // one wave per centroid row (d = 128: 2 dims per lane)
+    const int lane = threadIdx.x;
+    double s2 = 0.0, s1 = 0.0;
+    bool bad = false;
+    for (int j = lane; j < FU_D; j += 64) {
+        const double v = c < K ? C[(size_t)c * FU_D + j] : 0.0;
+        const float f = (float)v;
+        const _Float16 hv = (_Float16)f;
+        Ch[(size_t)c * FU_D + j] = hv;
+        Cl[(size_t)c * FU_D + j] = (_Float16)(f - (float)hv);
+        s2 = fma(v, v, s2);
+        s1 += fabs(v);
+        bad |= !(fabs(v) <= (double)FU_RANGE);
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        s2 += __shfl_xor(s2, off);
+        s1 += __shfl_xor(s1, off);
+    }
+    const unsigned long long anybad = __ballot(bad);
+    if (lane != 0) return;
+    if (c >= K) { cnh[c] = -__builtin_inff(); return; }
+    cnh[c] = (float)(-0.5 * s2);
+    const double up = 1.0 + 0x1p-18;
+    const double nc = sqrt(s2) * (1.0 + 0x1p-30);
+    // |t~ - t| <= (A1 + 2^-22)|x||c| + A2(|x|_1 + |c|_1) + 2^-23 |c|^2 + 2^-41 (|x|^2 + |c|^2)
+    const float ec = (float)((FU_A1 + 0x1p-22) * nc * up);
+    const float eb = (float)((FU_A2 * s1 * (1.0 + 0x1p-20) + 0x1p-23 * s2 + 0x1p-41 * s2) * up);
+    atomicMax(cb + 0, __float_as_uint(ec));     // positive floats order like their bits
+    atomicMax(cb + 1, __float_as_uint(eb));
+    if (anybad) atomicOr(cb + 2, 1u);
+}
+
+int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
+                      float* cbound) {
+    (void)hipMemsetAsync(cbound, 0, 16, s);
+    hipLaunchKernelGGL(fused_centroid_prep, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, Ch, Cl, cnh,
+                       reinterpret_cast<unsigned int*>(cbound));
+    return kstatus("fused_centroid_prep");
+}
+
+int launch_fused(hipStream_t s, bool hash, const FusedLaunch& f) {
+    if (f.N <= 0) return 0;
+    FusedArgs a;
+    a.X = f.X; a.N = f.N;
+    a.Ch = f.Ch; a.Cl = f.Cl; a.cnh = f.cnh; a.cbound = f.cbound; a.C64 = f.C64; a.Kpad = f.Kpad;
+    a.Vh = f.Vh; a.Vl = f.Vl; a.PT = f.PT; a.tv = f.tv; a.pnorm = f.pnorm; a.v1 = f.v1; a.rv = f.rv;
+    a.w = f.w; a.L = f.L; a.k = f.k; a.LK = f.LK; a.LKpad = f.LKpad; a.nb = f.nb;
+    a.tuples = f.tuples; a.phi = f.phi; a.bucket = f.bucket; a.assign = f.assign; a.dist = f.dist;
+    a.ambig = f.ambig; a.ambig_count = f.ambig_count; a.stats = f.stats;
+    const dim3 grid((unsigned)((f.N + FU_PB - 1) / FU_PB)), block(FU_THREADS);
+    if (hash) hipLaunchKernelGGL(fused_kernel<true>, grid, block, FU_LDS_BYTES, s, a);
+    else hipLaunchKernelGGL(fused_kernel<false>, grid, block, FU_LDS_BYTES, s, a);
+    return kstatus("fused_kernel");
+}
+
+}  // namespace lshkm

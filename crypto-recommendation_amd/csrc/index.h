@@ -27,6 +27,10 @@ struct ProjTable {
     int metric = 0, d = 0, L = 0, k = 0, LK = 0, LKpad = 0;
     float w = 0.f;
     Buf PT_d, t_d, pn_d, r_d;
+    // split-f16 image for the fused kernel (euclidean, d == 128, L*k <= 32):
+    // Vh/Vl [64][128] f16 (rows >= LK zero), v1 = ||v||_1 rounded up
+    bool fused_ok = false;
+    Buf vh_d, vl_d, v1_d;
     std::vector<float> hV;
     int upload(hipStream_t s, int metric, int d, int L, int k, float w, const float* V, const float* t,
                const int32_t* r, const double* R);
@@ -44,6 +48,9 @@ struct lshkm_ctx_s {
     lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src;
     // scatter / query / update workspace (see api_index.cpp for the slot map)
     lshkm::Buf ws[16];
+    // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
+    bool timing = false;
+    hipEvent_t tev[2] = {nullptr, nullptr};
     // pinned host staging for small host->device inputs
     void* pinned = nullptr;
     size_t pinned_cap = 0;
@@ -59,6 +66,8 @@ struct lshkm_ctx_s {
         return 0;
     }
     ~lshkm_ctx_s() {
+        for (hipEvent_t& e : tev)
+            if (e) (void)hipEventDestroy(e);
         if (pinned_ev) (void)hipEventSynchronize(pinned_ev), (void)hipEventDestroy(pinned_ev);
         if (pinned) (void)hipHostFree(pinned);
     }

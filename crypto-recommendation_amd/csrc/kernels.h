@@ -86,6 +86,39 @@ int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, c
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
 
+// Fused hash + assign on split-f16 MFMA (fused.hip), d = 128.
+struct FusedLaunch {
+    const float* X = nullptr;
+    int64_t N = 0;
+    const _Float16* Ch = nullptr;
+    const _Float16* Cl = nullptr;
+    const float* cnh = nullptr;
+    const float* cbound = nullptr;
+    const double* C64 = nullptr;
+    int Kpad = 0;
+    const _Float16* Vh = nullptr;
+    const _Float16* Vl = nullptr;
+    const double* PT = nullptr;
+    const float* tv = nullptr;
+    const double* pnorm = nullptr;
+    const double* v1 = nullptr;
+    const int32_t* rv = nullptr;
+    float w = 0.f;
+    int L = 0, k = 0, LK = 0, LKpad = 0;
+    int64_t nb = 1;
+    int32_t* tuples = nullptr;
+    int32_t* phi = nullptr;
+    int32_t* bucket = nullptr;
+    int32_t* assign = nullptr;
+    double* dist = nullptr;
+    int32_t* ambig = nullptr;
+    unsigned long long* ambig_count = nullptr;
+    unsigned long long* stats = nullptr;
+};
+int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
+                      float* cbound);
+int launch_fused(hipStream_t s, bool hash, const FusedLaunch& f);
+
 // Synthetic data.
 int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X);
 

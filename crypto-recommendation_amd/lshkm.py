@@ -53,6 +53,8 @@ def lib():
             "lshkm_ctx_destroy": (i32, [vp]),
             "lshkm_get_stat": (i32, [vp, i32, C.POINTER(i64)]),
             "lshkm_reset_stats": (i32, [vp]),
+            "lshkm_ctx_enable_timing": (i32, [vp, i32]),
+            "lshkm_last_kernel_ms": (i32, [vp, C.POINTER(C.c_float)]),
             "lshkm_params_lsh_euclidean": (i32, [u64, i32, i32, i32, f32, vp, vp, vp, C.POINTER(C.c_uint32)]),
             "lshkm_params_lsh_cosine": (i32, [u64, i32, i32, i32, vp, C.POINTER(C.c_uint32)]),
             "lshkm_params_cube_euclidean": (i32, [u64, i32, i32, f32, vp, vp, C.POINTER(C.c_uint32)]),
@@ -72,6 +74,7 @@ def lib():
             "lshkm_cube_query": (i32, [vp, vp, i64, i32, vp, vp, i64, C.POINTER(i64)]),
             "lshkm_cube_get_memo": (i32, [vp, vp, vp, vp, i64, C.POINTER(i64), C.POINTER(C.c_uint32)]),
             "lshkm_lloyd_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp]),
+            "lshkm_hash_assign": (i32, [vp, vp, i64, vp, i32, vp, vp, vp, vp, vp, vp]),
             "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
             "lshkm_kmeans_finalize": (i32, [vp, vp, vp, i32, i32, vp, i32, f64, vp, C.POINTER(i32)]),
@@ -302,6 +305,21 @@ def lloyd_assign(ctx, X, Cc, metric="euclidean", src_rows=None, assign=None, dis
     _ck(lib().lshkm_lloyd_assign(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _np_ptr(sr),
                                  _t_ptr(assign), _t_ptr(dist)))
     return assign, dist
+
+
+def hash_assign(lsh, X, Cc, src_rows=None, tuples=True, phi=False, bucket=True):
+    """LSH hashing + Lloyd assignment in one pass. Returns (tuples, phi, bucket, assign, dist)."""
+    ctx, torch = lsh.ctx, lsh.ctx.torch
+    N = X.shape[0]
+    tu = ctx.empty((N, lsh.L, lsh.k), torch.int32) if tuples else None
+    ph = ctx.empty((N, lsh.L), torch.int32) if phi else None
+    bu = ctx.empty((N, lsh.L), torch.int32) if bucket else None
+    a = ctx.empty((N,), torch.int32)
+    dist = ctx.empty((N,), torch.float64)
+    sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
+    _ck(lib().lshkm_hash_assign(lsh.h, _t_ptr(X), N, _t_ptr(Cc), Cc.shape[0], _np_ptr(sr), _t_ptr(tu), _t_ptr(ph),
+                                _t_ptr(bu), _t_ptr(a), _t_ptr(dist)))
+    return tu, ph, bu, a, dist
 
 
 def kmeans_update(ctx, X, assign, C_old, metric="euclidean", min_dist=0.0):

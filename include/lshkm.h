@@ -62,6 +62,10 @@ int lshkm_ctx_destroy(lshkm_ctx ctx);
  * 1 = points whose argmin needed the exact all-centroid pass. */
 int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);
 int lshkm_reset_stats(lshkm_ctx ctx);
+/* HIP-event timing of the dominant kernel launch (the fused hash+assign kernel)
+ * on the context's stream; lshkm_last_kernel_ms waits for and returns the last one. */
+int lshkm_ctx_enable_timing(lshkm_ctx ctx, int on);
+int lshkm_last_kernel_ms(lshkm_ctx ctx, float* ms_host);
 
 /* ------------------------------------------- parameter generation (host)
  * std::default_random_engine seeded with `seed`, draws in the reference's
@@ -152,6 +156,15 @@ int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f_host, int32_t* h_host, int32
 int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const double* C_dev,
                        int K, int metric, const int32_t* src_rows_host, int32_t* assign_dev,
                        double* dist_dev);
+/* The hot path in one pass over the points: LSH hashing of the rows
+ * (EuclideanPhiGen::generate for every table, euclidean_phi_gen.hpp:77-92, and
+ * the bucket index of cust_hashtable.hpp:68) and lloyds_assignment
+ * (assignment.hpp:54-80) against C_dev. Outputs as lshkm_lsh_hash and
+ * lshkm_lloyd_assign (tuples/phi/bucket may be NULL). Same results as the two
+ * calls; one read of X when the index is euclidean with d = 128, L*k <= 32. */
+int lshkm_hash_assign(lshkm_lsh lsh, const float* X_dev, int64_t N, const double* C_dev, int K,
+                      const int32_t* src_rows_host, int32_t* tuples_dev, int32_t* phi_dev, int32_t* bucket_dev,
+                      int32_t* assign_dev, double* dist_dev);
 /* k_means (update.hpp:37-86): exact-order per-cluster fp64 sums in row order,
  * divided by the count unless empty; *cont_host = 1 iff some center moved
  * more than min_dist. C_new_dev [K][d], counts_dev [K] (may be NULL). */

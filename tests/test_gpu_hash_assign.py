@@ -151,3 +151,64 @@ def test_lloyd_ties_and_duplicates(ctx):
     assert np.array_equal(a.cpu().numpy(), oa)
     assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
     assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0
+
+
+def test_hash_assign_fused_vs_oracle(ctx):
+    # the headline path: one pass over the rows (split-f16 MFMA), at 200k rows
+    N, d, L, k, K = 200_000, 128, 5, 4, 256
+    V, t, r, _ = lshkm.params_lsh_euclidean(12345, L, k, d, 0.4)
+    X = ctx.synth(0x5EED, N, d)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
+    rows = (np.arange(K) * (N // K)).astype(np.int32)
+    Cc = X[to_dev(ctx, rows.astype(np.int64))].double()
+    ctx.reset_stats()
+    tu, ph, bu, a, dist = lshkm.hash_assign(lsh, X, Cc, rows, tuples=True, phi=True, bucket=True)
+    Xh = X.cpu().numpy()
+    xt, xp, xb = oracle.lsh_hash_euclid(Xh, V, t, np.float32(0.4), r, N // 100)
+    assert np.array_equal(tu.cpu().numpy(), xt)
+    assert np.array_equal(ph.cpu().numpy(), xp)
+    assert np.array_equal(bu.cpu().numpy(), xb)
+    sub = np.random.default_rng(5).choice(N, 2500, replace=False)
+    oa, od = oracle.lloyd_assign(Xh[sub], Cc.cpu().numpy(), "euclidean", None)
+    over = np.isin(sub, rows)
+    ga, gd = a.cpu().numpy()[sub], dist.cpu().numpy()[sub]
+    assert np.array_equal(ga[~over], oa[~over])
+    assert np.array_equal(gd[~over].view(np.uint64), od[~over].view(np.uint64))
+    amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG)
+    assert amb < 0.05 * N, amb          # the bound is certifying the vast majority
+
+
+@pytest.mark.parametrize("path", ["f32", "exact"])
+def test_assign_paths_agree(ctx, path, monkeypatch):
+    N, d, K = 30_000, 128, 64
+    X = ctx.synth(21, N, d)
+    Cc = X[:K].double() * 1.0001
+    a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
+    monkeypatch.setenv("LSHKM_ASSIGN_PATH", path)
+    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
+    assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
+    assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
+
+
+def test_fused_range_guard(ctx):
+    # values beyond the f16 range must never be certified by the split path
+    N, d, K, L, k = 3000, 128, 16, 5, 4
+    Xh = oracle.synth(8, N, d)
+    Xh[::7, 3] = 1.0e5
+    Xh[5, :] = 7.0e4
+    X = to_dev(ctx, Xh)
+    V, t, r, _ = lshkm.params_lsh_euclidean(3, L, k, d, 4.0)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, 30, 4.0, V=V, t=t, r=r)
+    Cc = to_dev(ctx, Xh[:K].astype(np.float64))
+    tu, _, bu, a, dist = lshkm.hash_assign(lsh, X, Cc, None)
+    xt, _, xb = oracle.lsh_hash_euclid(Xh, V, t, np.float32(4.0), r, 30)
+    oa, od = oracle.lloyd_assign(Xh, Xh[:K].astype(np.float64), "euclidean", None)
+    assert np.array_equal(tu.cpu().numpy(), xt) and np.array_equal(bu.cpu().numpy(), xb)
+    assert np.array_equal(a.cpu().numpy(), oa)
+    assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
+    # and centroids beyond the range
+    Cbig = Cc.clone(); Cbig[2, 0] = 5.0e4
+    a2, d2 = lshkm.lloyd_assign(ctx, X, Cbig, "euclidean")
+    oa2, od2 = oracle.lloyd_assign(Xh, Cbig.cpu().numpy(), "euclidean", None)
+    assert np.array_equal(a2.cpu().numpy(), oa2)
+    assert np.array_equal(d2.cpu().numpy().view(np.uint64), od2.view(np.uint64))
