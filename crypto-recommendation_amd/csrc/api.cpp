@@ -317,6 +317,17 @@ static int assign_path(int metric, int d) {
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
+// Exact reference-order pass over the rows listed in ws_ambig (count on device).
+static int exact_listed(lshkm_ctx ctx, const float* X, int d, const double* C, int K, int metric,
+                        const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist) {
+    const int32_t* rows = (const int32_t*)ctx->ws_ambig.p;
+    if (metric != LSHKM_METRIC_EUCLIDEAN)
+        return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist);
+    int rc;
+    if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 63) / 64 * 64) * 8))) return rc;
+    return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist);
+}
+
 static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
                        const int32_t* src_rows_host, int32_t* assign, double* dist, lshkm_lsh lsh, int32_t* tuples,
                        int32_t* phi, int32_t* bucket) {
@@ -332,10 +343,11 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
     if (path == 0) {
         const int Kpad = (K + 63) / 64 * 64;
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) || (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4)) ||
-            (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 4)) || (rc = ctx->ws_counter.reserve(64)))
+            (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
+            (fuse_hash && (rc = ctx->ws_hfix.reserve((size_t)std::max<int64_t>(N, 1) * 8))))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
-        LSHKM_HIP(hipMemsetAsync(cnt, 0, 8, s));
+        LSHKM_HIP(hipMemsetAsync(cnt, 0, 16, s));         // [0] ambiguous rows, [1] hash fix-up rows
         _Float16* Ch = (_Float16*)ctx->ws_c32.p;
         _Float16* Cl = Ch + (size_t)Kpad * 128;
         float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
@@ -351,11 +363,12 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
             f.tv = pj.t_d.as<float>(); f.pnorm = pj.pn_d.as<double>(); f.v1 = pj.v1_d.as<double>();
             f.rv = pj.r_d.as<int32_t>(); f.w = pj.w; f.L = pj.L; f.k = pj.k; f.LK = pj.LK; f.LKpad = pj.LKpad;
             f.nb = lsh->nb; f.tuples = tuples; f.phi = phi; f.bucket = bucket;
+            f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
         }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
         if ((rc = launch_fused(s, fuse_hash, f))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
-        if ((rc = launch_assign_exact(s, X, N, d, C, K, metric, (const int32_t*)ctx->ws_ambig.p, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;
@@ -368,7 +381,7 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         if ((rc = launch_centroid_prep(s, C, K, Kpad, d, DP, metric, (float*)ctx->ws_c32.p, (float*)ctx->ws_cconst.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_assign_mfma(s, X, N, d, DP, C, K, Kpad, (const float*)ctx->ws_c32.p, (const float*)ctx->ws_cconst.p,
                                      assign, dist, (int32_t*)ctx->ws_ambig.p, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if ((rc = launch_assign_exact(s, X, N, d, C, K, metric, (const int32_t*)ctx->ws_ambig.p, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
         // ambiguous-count statistic
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
     } else {

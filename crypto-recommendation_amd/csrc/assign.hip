@@ -301,6 +301,110 @@ int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const d
     return kstatus("assign.hip");
 }
 
+// Listed (uncertified) rows, euclidean: the same reference-order distances as
+// assign_exact_kernel, but a wave takes XB_R rows at once against a transposed
+// fp64 copy CT[j][c], so each centroid value is loaded once (coalesced, lane =
+// centroid) for XB_R rows. Lane holds centroids c0 + lane + 64i, i < 4.
+constexpr int XB_R = 8;
+constexpr int XB_WAVES = 4;
+constexpr int XB_DMAX = 256;
+
+__global__ void transpose_centroids_kernel(const double* __restrict__ C, int K, int Kpad, int d,
+                                           double* __restrict__ CT) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)d * Kpad) return;
+    const int j = (int)(e / Kpad), c = (int)(e % Kpad);
+    CT[e] = c < K ? C[(size_t)c * d + j] : 0.0;
+}
+
+__global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
+    const float* __restrict__ X, int d, const double* __restrict__ CT, int K, int Kpad,
+    const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,
+    int32_t* __restrict__ assign, double* __restrict__ dist) {
+    __shared__ float xs[XB_WAVES][XB_R][XB_DMAX];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t total = (int64_t)*row_count;
+    if (total > max_rows) total = max_rows;
+    const int64_t ngroups = (total + XB_R - 1) / XB_R;
+    for (int64_t g = (int64_t)blockIdx.x * XB_WAVES + wave; g < ngroups; g += (int64_t)gridDim.x * XB_WAVES) {
+        const int nr = (int)min((int64_t)XB_R, total - g * XB_R);
+        int64_t myrow[XB_R];
+#pragma unroll
+        for (int r = 0; r < XB_R; r++) myrow[r] = rows[g * XB_R + min(r, nr - 1)];   // pad with the last row
+#pragma unroll
+        for (int r = 0; r < XB_R; r++)
+            for (int j = lane; j < d; j += 64) xs[wave][r][j] = X[myrow[r] * d + j];
+        wave_sync();
+        double best[XB_R];
+        int bi[XB_R];
+#pragma unroll
+        for (int r = 0; r < XB_R; r++) { best[r] = 0.0; bi[r] = -1; }
+        for (int c0 = 0; c0 < K; c0 += 256) {
+            double acc[XB_R][4];
+#pragma unroll
+            for (int r = 0; r < XB_R; r++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) acc[r][i] = 0.0;
+            const double* ct = CT + c0 + lane;
+            for (int j = 0; j < d; j++) {
+                double cv[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) cv[i] = c0 + lane + 64 * i < Kpad ? ct[(size_t)j * Kpad + 64 * i] : 0.0;
+#pragma unroll
+                for (int r = 0; r < XB_R; r++) {
+                    const double xj = (double)xs[wave][r][j];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const double df = __dsub_rn(xj, cv[i]);
+                        acc[r][i] = __dadd_rn(acc[r][i], __dmul_rn(df, df));
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {           // increasing c: strict '<' keeps the first minimum
+                const int c = c0 + lane + 64 * i;
+                if (c >= K) continue;
+#pragma unroll
+                for (int r = 0; r < XB_R; r++) {
+                    const double dd = sqrt(acc[r][i]);
+                    if (bi[r] < 0 || dd < best[r]) { best[r] = dd; bi[r] = c; }
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < XB_R; r++) {
+            double b = best[r];
+            int i1 = bi[r];
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double ob = __shfl_xor(b, off);
+                const int oi = __shfl_xor(i1, off);
+                const bool take = oi >= 0 && (i1 < 0 || ob < b || (ob == b && oi < i1));
+                if (take) { b = ob; i1 = oi; }
+            }
+            if (lane == 0 && r < nr) {
+                assign[myrow[r]] = i1;
+                dist[myrow[r]] = b;
+            }
+        }
+        wave_sync();
+    }
+}
+
+int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
+                             const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
+                             int32_t* assign, double* dist) {
+    if (max_rows <= 0) return 0;
+    if (d > XB_DMAX) return launch_assign_exact(s, X, 0, d, C, K, 0, rows, row_count, max_rows, assign, dist);
+    const int Kpad = (K + 63) / 64 * 64;
+    const int64_t ne = (int64_t)d * Kpad;
+    hipLaunchKernelGGL(transpose_centroids_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, C, K, Kpad, d, CT);
+    const int64_t groups = (max_rows + XB_R - 1) / XB_R;
+    const int64_t blocks = std::min<int64_t>((groups + XB_WAVES - 1) / XB_WAVES, 2048);
+    hipLaunchKernelGGL(assign_exact_batch_kernel, dim3((unsigned)blocks), dim3(64 * XB_WAVES), 0, s, X, d, CT, K, Kpad,
+                       rows, row_count, max_rows, assign, dist);
+    return kstatus("assign_exact_batch_kernel");
+}
+
 // Centroid override (assignment.hpp:77-78): in c order, so the last centroid
 // that points at a row wins.
 __global__ void assign_override_kernel(const int32_t* __restrict__ src, int K, int64_t N,

@@ -34,6 +34,14 @@ inline int kstatus(const char* what) {
     return -2;
 }
 
+// Wave-scope LDS handoff: makes one lane's LDS writes visible to the other
+// lanes of its wave (a fence the compiler cannot move loads across).
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Grid size for a grid-stride kernel: at least one block, at most cap.
 inline unsigned gsz(int64_t work, int64_t per_block, int64_t cap) {
     int64_t b = (work + per_block - 1) / per_block;

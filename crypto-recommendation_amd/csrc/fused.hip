@@ -29,6 +29,10 @@
 // Hash values: y = (dot~ + t)/w in fp64 with the split bound; a floor it
 // cannot certify is redone from the exact row with the fp64 bound of
 // hash.hip, and then, if needed, with the soft-x87 emulation.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 #include "kernels.h"
 #include "softx87.h"
@@ -83,6 +87,8 @@ struct FusedArgs {
     double* dist;            // [N]
     int32_t* ambig;          // [N] uncertified rows
     unsigned long long* ambig_count;
+    unsigned long long* hfix;        // persistent form: rows with an uncertified floor
+    unsigned long long* hfix_count;
     unsigned long long* stats;
 };
 
@@ -93,6 +99,28 @@ __device__ inline void split8(const float* x, half8& hi, half8& lo) {
         hi[j] = hv;
         lo[j] = (_Float16)(x[j] - (float)hv);
     }
+}
+
+// EuclideanPhi arithmetic (euclidean_phi_gen.hpp:70-92) in 32-bit form, M =
+// int(pow(2,32)-5) = 2^31-1 under g++. temp = (long)(h * r) is an int32 (the
+// int product wraps), so ((temp % M) + M) % M needs only compares; the uint32
+// sum hn wraps, and (hn % M + M) % M = hn % M for hn < 2^32.
+constexpr uint32_t PHI_M = 2147483647u;
+__device__ inline uint32_t phi_term(int32_t h, int32_t r) {
+    int64_t v = (int32_t)((uint32_t)h * (uint32_t)r);    // in [-2^31, 2^31)
+    if (v >= (int64_t)PHI_M) v -= PHI_M;
+    if (v < 0) v += PHI_M;
+    if (v < 0) v += PHI_M;                                 // only v = -2^31
+    return (uint32_t)v;
+}
+__device__ inline uint32_t phi_final(uint32_t hn) {
+    if (hn >= PHI_M) hn -= PHI_M;
+    if (hn >= PHI_M) hn -= PHI_M;
+    return hn;
+}
+// phi % nb (cust_hashtable.hpp:68); phi < 2^31
+__device__ inline int32_t bucket_of(uint32_t ph, int64_t nb) {
+    return nb <= 0xFFFFFFFFll ? (int32_t)(ph % (uint32_t)nb) : (int32_t)ph;
 }
 
 // Exact (reference-order) hash of one projection from the fp32 row in HBM.
@@ -317,6 +345,311 @@ __global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
     }
 }
 
+// ------------------------------------------------------------- persistent form
+// For Kpad <= 256 the whole split centroid set (2 x 256 x 272 B) fits in LDS
+// next to the 32 hash rows, so one block per CU loads it ONCE and its 8 waves
+// then loop independently over 32-point tiles: no barrier in the main loop,
+// points go straight from HBM into registers (lane half h: dims 16s+8h..+7 of
+// point lane&31 -- the B-operand layout), and the exact fp32 row stays in
+// registers for the reference-order distance of the winner. Hashing here is
+// specialised to k = 4 (the reference default, euclidean_phi_gen.hpp): table l's
+// four values are then D-registers 4(l>>1)..+3 of lane half l&1, so phi and the
+// bucket ID are computed in-register.
+constexpr int FP_WAVES = 8;
+constexpr int FP_THREADS = 64 * FP_WAVES;
+constexpr int FP_KMAX = 256;
+constexpr int FP_HC_BYTES = 32 * (4 + 8 + 8 + 4);     // hash constants t, |v|_2, |v|_1, r
+
+__host__ __device__ constexpr int fp_lds_bytes(int Kpad, bool hash) {
+    return 2 * Kpad * FU_RS * 2 + Kpad * 4 + (hash ? 2 * 32 * FU_RS * 2 + FP_HC_BYTES : 0);
+}
+static_assert(fp_lds_bytes(FP_KMAX, true) <= 160 * 1024, "persistent LDS image exceeds 160 KiB");
+
+template <bool HASH>
+__global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int Kpad = a.Kpad;
+    _Float16* lch = reinterpret_cast<_Float16*>(smem);
+    _Float16* lcl = lch + Kpad * FU_RS;
+    float* lcn = reinterpret_cast<float*>(lcl + Kpad * FU_RS);
+    _Float16* lvh = reinterpret_cast<_Float16*>(lcn + Kpad);
+    _Float16* lvl = lvh + 32 * FU_RS;
+    double* lpn0 = reinterpret_cast<double*>(lvl + 32 * FU_RS);
+    double* lv10 = lpn0 + 32;
+    float* lt0 = reinterpret_cast<float*>(lv10 + 32);
+    int32_t* lr0 = reinterpret_cast<int32_t*>(lt0 + 32);
+
+    // ---- prologue: the block's resident image (once per block)
+    for (int e = threadIdx.x; e < Kpad * 16; e += FP_THREADS) {
+        const int r = e >> 4, g = e & 15;
+        *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Ch + (size_t)r * FU_D + g * 8);
+        *reinterpret_cast<float4*>(lcl + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Cl + (size_t)r * FU_D + g * 8);
+    }
+    for (int e = threadIdx.x; e < Kpad; e += FP_THREADS) lcn[e] = a.cnh[e];
+    if (HASH) {
+        {
+            const int r = threadIdx.x >> 4, g = threadIdx.x & 15;      // 512 threads = 32 rows x 16 granules
+            *reinterpret_cast<float4*>(lvh + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vh + r * FU_D + g * 8);
+            *reinterpret_cast<float4*>(lvl + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vl + r * FU_D + g * 8);
+        }
+        if (threadIdx.x < 32) {
+            const int f = threadIdx.x;
+            const bool on = f < a.LK;
+            lpn0[f] = on ? a.pnorm[f] : 0.0;
+            lv10[f] = on ? a.v1[f] : 0.0;
+            lt0[f] = on ? a.tv[f] : 0.f;
+            lr0[f] = on ? a.rv[f] : 0;
+        }
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    const float ecf = a.cbound[0], ebf = a.cbound[1];
+    const bool c_ok = __float_as_uint(a.cbound[2]) == 0u;
+    const _Float16* my_h = lch + col * FU_RS + 8 * h;
+    const _Float16* my_l = lcl + col * FU_RS + 8 * h;
+    const int ntile32 = Kpad >> 5;
+    const int64_t ntiles = (a.N + 31) >> 5;
+
+    for (int64_t tile = (int64_t)blockIdx.x * FP_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FP_WAVES) {
+        const int64_t row = tile * 32 + col;
+        const bool valid = row < a.N;
+
+        // ---- point -> registers (exact fp32) and the split B operand
+        float xf[64];
+        {
+            const float* xr = a.X + row * FU_D + 8 * h;
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                float4 p0 = make_float4(0.f, 0.f, 0.f, 0.f), p1 = p0;
+                if (valid) {
+                    p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
+                    p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
+                }
+                xf[8 * s + 0] = p0.x; xf[8 * s + 1] = p0.y; xf[8 * s + 2] = p0.z; xf[8 * s + 3] = p0.w;
+                xf[8 * s + 4] = p1.x; xf[8 * s + 5] = p1.y; xf[8 * s + 6] = p1.z; xf[8 * s + 7] = p1.w;
+            }
+        }
+        half8 bh[8], bl[8];
+        float xn2f = 0.f, x1f = 0.f, xmax = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            split8(xf + 8 * s, bh[s], bl[s]);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                xn2f = fmaf(xf[8 * s + j], xf[8 * s + j], xn2f);
+                x1f += fabsf(xf[8 * s + j]);
+                xmax = fmaxf(xmax, fabsf(xf[8 * s + j]));
+            }
+        }
+        xn2f += __shfl_xor(xn2f, 32);
+        x1f += __shfl_xor(x1f, 32);
+        xmax = fmaxf(xmax, __shfl_xor(xmax, 32));
+        const double xn2 = (double)xn2f * (1.0 + 0x1p-16);
+        const double nx = sqrt(xn2);
+        const double x1 = (double)x1f * (1.0 + 0x1p-16);
+        const bool x_ok = xmax <= FU_RANGE;
+
+        // ---- hash tile + LSH outputs (k = 4: table l = 2g + h lives in registers 4g..4g+3)
+        if (HASH) {
+            uint32_t fmask = 0;
+            floatx16 acc_hi, acc_lo;
+            tile_mfma(lvh + col * FU_RS + 8 * h, lvl + col * FU_RS + 8 * h, bh, bl, acc_hi, acc_lo);
+            // y and B are only estimates around the certified window, so 1/w as a
+            // product is enough: its error (< 3 ulp of y) is inside |y| 2^-50, and
+            // B is inflated by 2^-48 to stay an upper bound.
+            const double iw = 1.0 / (double)a.w;
+            // Opaque zero: keeps the per-function constants as LDS reads inside
+            // the loop instead of ~100 hoisted VGPRs (which spill).
+            int hc = 0;
+            asm volatile("" : "+v"(hc));
+            const float* lt = lt0 + hc;
+            const double* lpn = lpn0 + hc;
+            const double* lv1 = lv10 + hc;
+            const int32_t* lr = lr0 + hc;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int l = 2 * g + h;
+                if (l >= a.L || !valid) continue;
+                int32_t hv[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int f = 4 * l + q;
+                    const float dotf = acc_hi[4 * g + q] + acc_lo[4 * g + q];
+                    const double tt = (double)lt[f], pn = lpn[f];
+                    const double y = ((double)dotf + tt) * iw;
+                    const double Ed = FU_A1 * pn * nx + FU_A2 * (lv1[f] + x1) + 0x1p-23 * fabs((double)dotf);
+                    const double B = (Ed + 0x1p-50 * (pn * nx + fabs(tt))) * iw * (1.0 + 0x1p-48) + fabs(y) * 0x1p-50;
+                    const double lo = floor(y - B), hi = floor(y + B);
+                    hv[q] = (int32_t)lo;
+                    if (!(lo == hi && x_ok)) fmask |= 1u << f;   // provisional; redone by hash_fixup_kernel
+                }
+                const int64_t o = row * a.L + l;
+                if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
+                uint32_t hn = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) hn += phi_term(hv[q], lr[4 * l + q]);
+                const uint32_t ph = phi_final(hn);
+                if (a.phi) a.phi[o] = (int32_t)ph;
+                if (a.bucket) a.bucket[o] = bucket_of(ph, a.nb);
+            }
+            fmask |= __shfl_xor(fmask, 32);
+            const unsigned long long fb = __ballot(fmask != 0u && h == 1);
+            if (fb) {
+                // rows whose floor the split bound cannot certify: (row << 32 | fn mask)
+                const int leader = __builtin_ctzll(fb);
+                unsigned long long base = 0;
+                if (lane == leader) base = atomicAdd(a.hfix_count, (unsigned long long)__popcll(fb));
+                base = __shfl(base, leader);
+                if (fmask != 0u && h == 1)
+                    a.hfix[base + __popcll(fb & ((1ull << lane) - 1ull))] = ((unsigned long long)row << 32) | fmask;
+            }
+        }
+
+        // ---- all centroid tiles from the resident image
+        const float E = (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2) * (1.f + 0x1p-20f) + 1e-30f;
+        float m1 = -__builtin_inff(), m2 = -__builtin_inff();
+        int i1 = 0;
+#pragma unroll 1
+        for (int t = 0; t < ntile32; t++) {
+            floatx16 acc_hi, acc_lo;
+            tile_mfma(my_h + t * 32 * FU_RS, my_l + t * 32 * FU_RS, bh, bl, acc_hi, acc_lo);
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int cb = t * 32 + 8 * g + 4 * h;
+                const float4 cn = *reinterpret_cast<const float4*>(lcn + cb);
+                const float cnv[4] = {cn.x, cn.y, cn.z, cn.w};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float tv = (acc_hi[4 * g + q] + acc_lo[4 * g + q]) + cnv[q];
+                    m2 = fmaxf(m2, fminf(m1, tv));
+                    const bool c1 = tv > m1;
+                    m1 = c1 ? tv : m1;
+                    i1 = c1 ? cb + q : i1;
+                }
+            }
+        }
+        const float om1 = __shfl_xor(m1, 32), om2 = __shfl_xor(m2, 32);
+        const int oi1 = __shfl_xor(i1, 32);
+        const float M2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
+        const int I1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
+        const float M1 = fmaxf(m1, om1);
+        const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * (double)E);
+
+        // ---- winner distance in reference order: the squares are independent,
+        // only the sum is a chain; dims 8seg..8seg+7 belong to lane half seg & 1.
+        const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;    // I1 < K always (padding scores are -inf)
+        double acc = 0.0;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            double sq[8];
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                const double2 cc = *reinterpret_cast<const double2*>(crow + 16 * s + j);
+                const double d0 = __dsub_rn((double)xf[8 * s + j], cc.x);
+                const double d1 = __dsub_rn((double)xf[8 * s + j + 1], cc.y);
+                sq[j] = __dmul_rn(d0, d0);
+                sq[j + 1] = __dmul_rn(d1, d1);
+            }
+            if (h == 0) {                      // dims 16s .. 16s+7
+#pragma unroll
+                for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
+            }
+            const double from0 = __shfl_xor(acc, 32);          // whole wave exchanges
+            if (h == 1) {                      // dims 16s+8 .. 16s+15
+                acc = from0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
+            }
+            const double from1 = __shfl_xor(acc, 32);
+            if (h == 0) acc = from1;
+        }
+        const bool amb = valid && !cert;
+        const unsigned long long amask = __ballot(amb && h == 1);
+        if (h == 1 && valid) {
+            if (cert) {
+                a.assign[row] = I1;
+                a.dist[row] = sqrt(acc);
+            } else {
+                unsigned long long base = 0;
+                const int leader = __builtin_ctzll(amask);
+                if (lane == leader) base = atomicAdd(a.ambig_count, (unsigned long long)__popcll(amask));
+                base = __shfl(base, leader);
+                const int rank = __popcll(amask & ((1ull << lane) - 1ull));
+                a.ambig[base + rank] = (int32_t)row;
+            }
+        }
+    }
+}
+
+// Rows listed by the persistent form with an uncertified floor: one wave per
+// row, lane f recomputes projection f from the exact row (fp64 bound, then
+// soft-x87), and the first lane of each table rewrites tuple, phi and bucket.
+// The projections (128 x LKpad fp64, <= 32 KiB) and each wave's row sit in LDS.
+constexpr int HF_WAVES = 4;
+__global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) {
+    __shared__ double pts[FU_D * 32];
+    __shared__ float xs[HF_WAVES][FU_D];
+    const unsigned long long n = *a.hfix_count;
+    const int wave = threadIdx.x >> 6, f = threadIdx.x & 63;
+    if ((unsigned long long)blockIdx.x * HF_WAVES >= n) return;      // block-uniform
+    const int LKpad = a.LKpad;
+    for (int e = threadIdx.x; e < FU_D * LKpad; e += 64 * HF_WAVES) pts[e] = a.PT[e];
+    __syncthreads();
+    const bool on = f < a.LK;
+    const double tt = on ? (double)a.tv[f] : 0.0, ww = (double)a.w, pn = on ? a.pnorm[f] : 0.0;
+    const int l = on ? f / a.k : 0;
+    for (unsigned long long e = (unsigned long long)blockIdx.x * HF_WAVES + wave; e < n;
+         e += (unsigned long long)gridDim.x * HF_WAVES) {
+        const int64_t row = (int64_t)(a.hfix[e] >> 32);
+        const float* xr = a.X + row * FU_D;
+        xs[wave][f] = xr[f];
+        xs[wave][f + 64] = xr[f + 64];
+        wave_sync();
+        int32_t hv = 0;
+        if (on) {
+            // fp64 FMA chain with the rigorous bound of hash.hip; soft-x87 when it fails
+            double acc = 0.0, xn2 = 0.0;
+#pragma unroll 16
+            for (int j = 0; j < FU_D; j++) {
+                const double xj = (double)xs[wave][j];
+                xn2 = fma(xj, xj, xn2);
+                acc = fma(pts[j * LKpad + f], xj, acc);
+            }
+            const double P = pn * sqrt(xn2) * (1.0 + 0x1p-40);
+            const double y = (acc + tt) / ww;
+            const double B = ((double)(FU_D + 2) * 0x1p-52 * (P + fabs(tt))) / ww + fabs(y) * 0x1p-51;
+            const double lo = floor(y - B), hi = floor(y + B);
+            if (lo == hi) {
+                hv = (int32_t)lo;
+            } else {
+                sx80 s = sx_zero();
+                for (int j = 0; j < FU_D; j++) s = sx_add_double(s, __dmul_rn(pts[j * LKpad + f], (double)xs[wave][j]));
+                s = sx_add_double(s, tt);
+                atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
+                hv = (int32_t)sx_floor_i64(sx_div(s, sx_from_float(a.w)));
+            }
+        }
+        // gather the table's k values (all lanes take part in the shuffles)
+        uint32_t hn = 0;
+        for (int i = 0; i < a.k; i++) {
+            const int src = min(l * a.k + i, 63);
+            const int32_t hi = __shfl(hv, src);
+            hn += phi_term(hi, a.rv[min(src, a.LK - 1)]);
+        }
+        if (on) {
+            if (a.tuples) a.tuples[row * a.LK + f] = hv;
+            if (f == l * a.k) {
+                const uint32_t ph = phi_final(hn);
+                if (a.phi) a.phi[row * a.L + l] = (int32_t)ph;
+                if (a.bucket) a.bucket[row * a.L + l] = bucket_of(ph, a.nb);
+            }
+        }
+        wave_sync();
+    }
+}
+
 // ------------------------------------------------------------------ preparation
 // Centroids -> f16 hi/lo rows, -||c||^2/2, and the per-call bound maxima.
 __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpad, _Float16* __restrict__ Ch,
@@ -370,6 +703,31 @@ int launch_fused(hipStream_t s, bool hash, const FusedLaunch& f) {
     a.w = f.w; a.L = f.L; a.k = f.k; a.LK = f.LK; a.LKpad = f.LKpad; a.nb = f.nb;
     a.tuples = f.tuples; a.phi = f.phi; a.bucket = f.bucket; a.assign = f.assign; a.dist = f.dist;
     a.ambig = f.ambig; a.ambig_count = f.ambig_count; a.stats = f.stats;
+    a.hfix = f.hfix; a.hfix_count = f.hfix_count;
+    const char* force = getenv("LSHKM_FUSED_FORM");     // "chunked" forces the streaming form (tests)
+    const bool chunked = force && !strcmp(force, "chunked");
+    if (!chunked && f.Kpad <= FP_KMAX && (!hash || f.k == 4)) {
+        static int cus[64] = {0};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return kstatus("hipGetDevice");
+        if (dev < 64 && !cus[dev] &&
+            hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return kstatus("hipDeviceGetAttribute");
+        const int ncu = dev < 64 && cus[dev] > 0 ? cus[dev] : 256;
+        const int64_t ntiles = (f.N + 31) / 32;
+        const int64_t want = (ntiles + FP_WAVES - 1) / FP_WAVES;
+        const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(ncu, want))), block(FP_THREADS);
+        const size_t lds = (size_t)fp_lds_bytes(f.Kpad, hash);
+        if (!hash) {
+            hipLaunchKernelGGL(fused_persistent_kernel<false>, grid, block, lds, s, a);
+            return kstatus("fused_persistent_kernel");
+        }
+        if (!a.hfix || !a.hfix_count) return -1;
+        hipLaunchKernelGGL(fused_persistent_kernel<true>, grid, block, lds, s, a);
+        if (f.LKpad > 32) return -1;                      // pts[] holds 128 x 32 projections
+        hipLaunchKernelGGL(hash_fixup_kernel, dim3(1024), dim3(64 * HF_WAVES), 0, s, a);
+        return kstatus("fused_persistent_kernel");
+    }
     const dim3 grid((unsigned)((f.N + FU_PB - 1) / FU_PB)), block(FU_THREADS);
     if (hash) hipLaunchKernelGGL(fused_kernel<true>, grid, block, FU_LDS_BYTES, s, a);
     else hipLaunchKernelGGL(fused_kernel<false>, grid, block, FU_LDS_BYTES, s, a);

@@ -46,6 +46,10 @@ int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, 
 int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K,
                         int metric, const int32_t* rows, const unsigned long long* row_count,
                         int64_t max_rows, int32_t* assign, double* dist);
+// Euclidean, listed rows, batched (CT: d * ceil64(K) doubles of workspace).
+int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
+                             const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
+                             int32_t* assign, double* dist);
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist);
 
@@ -113,6 +117,8 @@ struct FusedLaunch {
     double* dist = nullptr;
     int32_t* ambig = nullptr;
     unsigned long long* ambig_count = nullptr;
+    unsigned long long* hfix = nullptr;          // [N] (row << 32 | fn mask) of uncertified hashes
+    unsigned long long* hfix_count = nullptr;
     unsigned long long* stats = nullptr;
 };
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,

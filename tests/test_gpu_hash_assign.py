@@ -153,9 +153,13 @@ def test_lloyd_ties_and_duplicates(ctx):
     assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0
 
 
-def test_hash_assign_fused_vs_oracle(ctx):
+@pytest.mark.parametrize("form", ["persistent", "chunked"])
+def test_hash_assign_fused_vs_oracle(ctx, form, monkeypatch):
     # the headline path: one pass over the rows (split-f16 MFMA), at 200k rows
-    N, d, L, k, K = 200_000, 128, 5, 4, 256
+    # (ragged: not a multiple of the 32-row tile); both kernel forms
+    if form == "chunked":
+        monkeypatch.setenv("LSHKM_FUSED_FORM", "chunked")
+    N, d, L, k, K = 200_003, 128, 5, 4, 256
     V, t, r, _ = lshkm.params_lsh_euclidean(12345, L, k, d, 0.4)
     X = ctx.synth(0x5EED, N, d)
     lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
@@ -190,8 +194,35 @@ def test_assign_paths_agree(ctx, path, monkeypatch):
     assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
 
 
-def test_fused_range_guard(ctx):
+@pytest.mark.parametrize("N,K,L,k", [(1, 1, 1, 4), (65, 64, 8, 4), (4099, 300, 8, 4), (777, 256, 3, 3),
+                                     (2048, 200, 2, 4), (1500, 256, 7, 2)])
+def test_hash_assign_shapes(ctx, N, K, L, k):
+    # persistent form (K <= 256, k = 4) and the chunked form (K > 256 or k != 4)
+    d = 128
+    Xh = oracle.synth(31 + N, N, d)
+    X = to_dev(ctx, Xh)
+    V, t, r, _ = lshkm.params_lsh_euclidean(7 + L, L, k, d, 0.5)
+    nb = max(N // 10, 1)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, nb, 0.5, V=V, t=t, r=r)
+    rng = np.random.default_rng(N)
+    Ch = rng.choice(Xh, K, replace=True).astype(np.float64) * 1.001
+    tu, ph, bu, a, dist = lshkm.hash_assign(lsh, X, to_dev(ctx, Ch), None, tuples=True, phi=True, bucket=True)
+    xt, xp, xb = oracle.lsh_hash_euclid(Xh, V, t, np.float32(0.5), r, nb)
+    assert np.array_equal(tu.cpu().numpy(), xt)
+    assert np.array_equal(ph.cpu().numpy(), xp)
+    assert np.array_equal(bu.cpu().numpy(), xb)
+    oa, od = oracle.lloyd_assign(Xh, Ch, "euclidean", None)
+    assert np.array_equal(a.cpu().numpy(), oa)
+    # centroids are not fp32-valued: glibc pow vs x*x may differ in the last bit
+    np.testing.assert_allclose(dist.cpu().numpy(), od, rtol=1e-14, atol=0)
+
+
+@pytest.mark.parametrize("form", ["persistent", "chunked"])
+def test_fused_range_guard(ctx, form, monkeypatch):
     # values beyond the f16 range must never be certified by the split path
+    # (in the persistent form every function of such a row goes through the fix-up pass)
+    if form == "chunked":
+        monkeypatch.setenv("LSHKM_FUSED_FORM", "chunked")
     N, d, K, L, k = 3000, 128, 16, 5, 4
     Xh = oracle.synth(8, N, d)
     Xh[::7, 3] = 1.0e5

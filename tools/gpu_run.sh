@@ -1,0 +1,37 @@
+#!/bin/bash
+# GPU-box routine (run through gpurun from the repo root):
+#   tools/gpu_run.sh TAG [tests|bench|prof|pmc]...
+# Each GPU step has its own time limit; the script stops at the first failure.
+set -u
+TAG=${1:?tag}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$R"
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest.log" 2>&1
+      rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { echo "tests rc=$rc"; exit $rc; } ;;
+    bench)
+      timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+      rc=$?; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; } ;;
+    benchq)
+      timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"
+      rc=$?; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; } ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+         -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline \
+         > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err")
+      rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      find "$OUT/prof" -name '*kernel_stats.csv' -exec head -8 {} \; ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --pmc $c --output-format csv \
+           -d "$OUT/pmc_$c" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
+           > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err")
+        rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
