@@ -318,14 +318,17 @@ static int assign_path(int metric, int d) {
 }
 
 // Exact reference-order pass over the rows listed in ws_ambig (count on device).
+// Segmented lists (seg_counts != NULL) come from the persistent fused form.
 static int exact_listed(lshkm_ctx ctx, const float* X, int d, const double* C, int K, int metric,
-                        const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist) {
+                        const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist,
+                        const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0) {
     const int32_t* rows = (const int32_t*)ctx->ws_ambig.p;
-    if (metric != LSHKM_METRIC_EUCLIDEAN)
+    if (!seg_counts && (metric != LSHKM_METRIC_EUCLIDEAN || d > 256))
         return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist);
     int rc;
     if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 63) / 64 * 64) * 8))) return rc;
-    return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist);
+    return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
+                                    seg_counts, seg_rows, nseg);
 }
 
 static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
@@ -343,8 +346,10 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
     if (path == 0) {
         const int Kpad = (K + 63) / 64 * 64;
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) || (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4)) ||
-            (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
-            (fuse_hash && (rc = ctx->ws_hfix.reserve((size_t)std::max<int64_t>(N, 1) * 8))))
+            (rc = ctx->ws_ambig.reserve((size_t)(N + FUSED_LIST_SLACK) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
+            (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)) ||
+            (fuse_hash && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8))) ||
+            (fuse_hash && !tuples && (rc = ctx->ws_tuples.reserve((size_t)std::max<int64_t>(N, 1) * lsh->proj.LK * 4))))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
         LSHKM_HIP(hipMemsetAsync(cnt, 0, 16, s));         // [0] ambiguous rows, [1] hash fix-up rows
@@ -357,18 +362,22 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         f.X = X; f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C; f.Kpad = Kpad;
         f.assign = assign; f.dist = dist; f.ambig = (int32_t*)ctx->ws_ambig.p; f.ambig_count = cnt;
         f.stats = (unsigned long long*)ctx->stats.p;
+        f.list_cap = N + FUSED_LIST_SLACK;
+        f.seg_counts = (int32_t*)ctx->ws_seg.p;
+        f.seg_cap = FUSED_MAX_SEGS;
         if (fuse_hash) {
             const ProjTable& pj = lsh->proj;
             f.Vh = pj.vh_d.as<_Float16>(); f.Vl = pj.vl_d.as<_Float16>(); f.PT = pj.PT_d.as<double>();
             f.tv = pj.t_d.as<float>(); f.pnorm = pj.pn_d.as<double>(); f.v1 = pj.v1_d.as<double>();
             f.rv = pj.r_d.as<int32_t>(); f.w = pj.w; f.L = pj.L; f.k = pj.k; f.LK = pj.LK; f.LKpad = pj.LKpad;
-            f.nb = lsh->nb; f.tuples = tuples; f.phi = phi; f.bucket = bucket;
+            f.nb = lsh->nb; f.tuples = tuples ? tuples : (int32_t*)ctx->ws_tuples.p; f.phi = phi; f.bucket = bucket;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
         }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
         if ((rc = launch_fused(s, fuse_hash, f))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
-        if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.seg_counts : nullptr,
+                               f.seg_rows, f.nseg))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;

@@ -320,13 +320,24 @@ __global__ void transpose_centroids_kernel(const double* __restrict__ C, int K, 
 __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
     const float* __restrict__ X, int d, const double* __restrict__ CT, int K, int Kpad,
     const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,
-    int32_t* __restrict__ assign, double* __restrict__ dist) {
+    int32_t* __restrict__ assign, double* __restrict__ dist, const int32_t* __restrict__ seg_counts,
+    int64_t seg_rows) {
     __shared__ float xs[XB_WAVES][XB_R][XB_DMAX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int64_t total = (int64_t)*row_count;
-    if (total > max_rows) total = max_rows;
+    int64_t total, g0, gstride;
+    if (seg_counts) {            // block b: the segment persistent block b wrote
+        rows += (int64_t)blockIdx.x * seg_rows;
+        total = seg_counts[2 * blockIdx.x];
+        g0 = wave;
+        gstride = XB_WAVES;
+    } else {
+        total = (int64_t)*row_count;
+        if (total > max_rows) total = max_rows;
+        g0 = (int64_t)blockIdx.x * XB_WAVES + wave;
+        gstride = (int64_t)gridDim.x * XB_WAVES;
+    }
     const int64_t ngroups = (total + XB_R - 1) / XB_R;
-    for (int64_t g = (int64_t)blockIdx.x * XB_WAVES + wave; g < ngroups; g += (int64_t)gridDim.x * XB_WAVES) {
+    for (int64_t g = g0; g < ngroups; g += gstride) {
         const int nr = (int)min((int64_t)XB_R, total - g * XB_R);
         int64_t myrow[XB_R];
 #pragma unroll
@@ -392,16 +403,19 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
 
 int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
-                             int32_t* assign, double* dist) {
+                             int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
     if (max_rows <= 0) return 0;
-    if (d > XB_DMAX) return launch_assign_exact(s, X, 0, d, C, K, 0, rows, row_count, max_rows, assign, dist);
+    if (d > XB_DMAX || (seg_counts && nseg <= 0)) {
+        set_error("launch_assign_exact_list: unsupported shape");
+        return -1;
+    }
     const int Kpad = (K + 63) / 64 * 64;
     const int64_t ne = (int64_t)d * Kpad;
     hipLaunchKernelGGL(transpose_centroids_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, C, K, Kpad, d, CT);
     const int64_t groups = (max_rows + XB_R - 1) / XB_R;
-    const int64_t blocks = std::min<int64_t>((groups + XB_WAVES - 1) / XB_WAVES, 2048);
+    const int64_t blocks = seg_counts ? nseg : std::min<int64_t>((groups + XB_WAVES - 1) / XB_WAVES, 2048);
     hipLaunchKernelGGL(assign_exact_batch_kernel, dim3((unsigned)blocks), dim3(64 * XB_WAVES), 0, s, X, d, CT, K, Kpad,
-                       rows, row_count, max_rows, assign, dist);
+                       rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
     return kstatus("assign_exact_batch_kernel");
 }
 

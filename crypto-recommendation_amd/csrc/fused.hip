@@ -90,6 +90,10 @@ struct FusedArgs {
     unsigned long long* hfix;        // persistent form: rows with an uncertified floor
     unsigned long long* hfix_count;
     unsigned long long* stats;
+    // persistent form: block b owns ambig/hfix entries [b * seg_rows, (b+1) * seg_rows)
+    // and reports their counts in seg_counts[2b] (ambiguous), seg_counts[2b+1] (fix-up)
+    int64_t seg_rows;
+    int32_t* seg_counts;
 };
 
 __device__ inline void split8(const float* x, half8& hi, half8& lo) {
@@ -347,21 +351,21 @@ __global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
 
 // ------------------------------------------------------------- persistent form
 // For Kpad <= 256 the whole split centroid set (2 x 256 x 272 B) fits in LDS
-// next to the 32 hash rows, so one block per CU loads it ONCE and its 8 waves
-// then loop independently over 32-point tiles: no barrier in the main loop,
-// points go straight from HBM into registers (lane half h: dims 16s+8h..+7 of
-// point lane&31 -- the B-operand layout), and the exact fp32 row stays in
-// registers for the reference-order distance of the winner. Hashing here is
+// next to the 32 hash rows, so one block per CU loads it ONCE and its 12 waves
+// (3 per SIMD, <= 168 VGPRs) then loop independently over 32-point tiles: no
+// barrier in the main loop, points go straight from HBM into registers (lane
+// half h: dims 16s+8h..+7 of point lane&31 -- the B-operand layout), and the
+// winner's reference-order distance re-reads the row from L2. Hashing here is
 // specialised to k = 4 (the reference default, euclidean_phi_gen.hpp): table l's
 // four values are then D-registers 4(l>>1)..+3 of lane half l&1, so phi and the
 // bucket ID are computed in-register.
-constexpr int FP_WAVES = 8;
+constexpr int FP_WAVES = 12;             // 3 per SIMD: <= 168 VGPRs
 constexpr int FP_THREADS = 64 * FP_WAVES;
 constexpr int FP_KMAX = 256;
-constexpr int FP_HC_BYTES = 32 * (4 + 8 + 8 + 4);     // hash constants t, |v|_2, |v|_1, r
+constexpr int FP_HC_BYTES = 32 * (4 + 4 + 4 + 4);     // hash constants |v|_2, |v|_1, t, r
 
 __host__ __device__ constexpr int fp_lds_bytes(int Kpad, bool hash) {
-    return 2 * Kpad * FU_RS * 2 + Kpad * 4 + (hash ? 2 * 32 * FU_RS * 2 + FP_HC_BYTES : 0);
+    return 16 + 2 * Kpad * FU_RS * 2 + Kpad * 4 + (hash ? 2 * 32 * FU_RS * 2 + FP_HC_BYTES : 0);
 }
 static_assert(fp_lds_bytes(FP_KMAX, true) <= 160 * 1024, "persistent LDS image exceeds 160 KiB");
 
@@ -369,14 +373,15 @@ template <bool HASH>
 __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
-    _Float16* lch = reinterpret_cast<_Float16*>(smem);
+    int* lcount = reinterpret_cast<int*>(smem);          // [0] ambiguous rows, [1] hash fix-up rows
+    _Float16* lch = reinterpret_cast<_Float16*>(smem + 16);
     _Float16* lcl = lch + Kpad * FU_RS;
     float* lcn = reinterpret_cast<float*>(lcl + Kpad * FU_RS);
     _Float16* lvh = reinterpret_cast<_Float16*>(lcn + Kpad);
     _Float16* lvl = lvh + 32 * FU_RS;
-    double* lpn0 = reinterpret_cast<double*>(lvl + 32 * FU_RS);
-    double* lv10 = lpn0 + 32;
-    float* lt0 = reinterpret_cast<float*>(lv10 + 32);
+    float* lpn0 = reinterpret_cast<float*>(lvl + 32 * FU_RS);
+    float* lv10 = lpn0 + 32;
+    float* lt0 = lv10 + 32;
     int32_t* lr0 = reinterpret_cast<int32_t*>(lt0 + 32);
 
     // ---- prologue: the block's resident image (once per block)
@@ -386,17 +391,22 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         *reinterpret_cast<float4*>(lcl + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Cl + (size_t)r * FU_D + g * 8);
     }
     for (int e = threadIdx.x; e < Kpad; e += FP_THREADS) lcn[e] = a.cnh[e];
+    if (threadIdx.x < 2) lcount[threadIdx.x] = 0;
+    // This block's list segments (no device-wide atomic in the loop: a contended
+    // global counter serialises at ~12 ns per add, MI355X_MICROARCH.md "fanin").
+    int32_t* ambig_seg = a.ambig + (int64_t)blockIdx.x * a.seg_rows;
+    unsigned long long* hfix_seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
     if (HASH) {
-        {
-            const int r = threadIdx.x >> 4, g = threadIdx.x & 15;      // 512 threads = 32 rows x 16 granules
+        for (int e = threadIdx.x; e < 32 * 16; e += FP_THREADS) {   // 32 rows x 16 granules
+            const int r = e >> 4, g = e & 15;
             *reinterpret_cast<float4*>(lvh + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vh + r * FU_D + g * 8);
             *reinterpret_cast<float4*>(lvl + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vl + r * FU_D + g * 8);
         }
         if (threadIdx.x < 32) {
             const int f = threadIdx.x;
             const bool on = f < a.LK;
-            lpn0[f] = on ? a.pnorm[f] : 0.0;
-            lv10[f] = on ? a.v1[f] : 0.0;
+            lpn0[f] = on ? (float)a.pnorm[f] * (1.f + 0x1p-20f) : 0.f;   // rounded up
+            lv10[f] = on ? (float)a.v1[f] * (1.f + 0x1p-20f) : 0.f;
             lt0[f] = on ? a.tv[f] : 0.f;
             lr0[f] = on ? a.rv[f] : 0;
         }
@@ -416,7 +426,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         const int64_t row = tile * 32 + col;
         const bool valid = row < a.N;
 
-        // ---- point -> registers (exact fp32) and the split B operand
+        // ---- point -> registers and the split B operand
         float xf[64];
         {
             const float* xr = a.X + row * FU_D + 8 * h;
@@ -456,18 +466,26 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             uint32_t fmask = 0;
             floatx16 acc_hi, acc_lo;
             tile_mfma(lvh + col * FU_RS + 8 * h, lvl + col * FU_RS + 8 * h, bh, bl, acc_hi, acc_lo);
-            // y and B are only estimates around the certified window, so 1/w as a
-            // product is enough: its error (< 3 ulp of y) is inside |y| 2^-50, and
-            // B is inflated by 2^-48 to stay an upper bound.
-            const double iw = 1.0 / (double)a.w;
+            // Certification in f32 (the floor only needs y to ~2^-20): with
+            // u = f32(dot~ + t), y = f32(u * f32(1/w)),
+            //   |y - (x.v + t)/w| <= (Ed + 2^-23 |u| + 2^-40 |t|) / w + 2^-21 |y|,
+            // Ed = A1 |v||x| + A2 (|v|_1 + |x|_1) + 2^-23 |dot~| (the split bound and
+            // the final hi + lo add; the reference's x87 / double-product roundings
+            // are below 2^-50 (|v||x| + |t|), inside the inflation). All terms are
+            // inflated by 2^-20 for their own f32 roundings, and so is the floor
+            // window: floor(y - B) == floor(y + B) certifies the reference's floorl.
+            const float iw = 1.0f / a.w;
+            const float ca = (float)(FU_A1 * nx) * (1.f + 0x1p-20f);
+            const float cb = (float)(FU_A2 * x1) * (1.f + 0x1p-20f);
             // Opaque zero: keeps the per-function constants as LDS reads inside
-            // the loop instead of ~100 hoisted VGPRs (which spill).
+            // the loop instead of hoisted VGPRs.
             int hc = 0;
             asm volatile("" : "+v"(hc));
             const float* lt = lt0 + hc;
-            const double* lpn = lpn0 + hc;
-            const double* lv1 = lv10 + hc;
+            const float* lpn = lpn0 + hc;
+            const float* lv1 = lv10 + hc;
             const int32_t* lr = lr0 + hc;
+            if (!x_ok) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int l = 2 * g + h;
@@ -477,13 +495,15 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 for (int q = 0; q < 4; q++) {
                     const int f = 4 * l + q;
                     const float dotf = acc_hi[4 * g + q] + acc_lo[4 * g + q];
-                    const double tt = (double)lt[f], pn = lpn[f];
-                    const double y = ((double)dotf + tt) * iw;
-                    const double Ed = FU_A1 * pn * nx + FU_A2 * (lv1[f] + x1) + 0x1p-23 * fabs((double)dotf);
-                    const double B = (Ed + 0x1p-50 * (pn * nx + fabs(tt))) * iw * (1.0 + 0x1p-48) + fabs(y) * 0x1p-50;
-                    const double lo = floor(y - B), hi = floor(y + B);
+                    const float tt = lt[f];
+                    const float u = dotf + tt;
+                    const float y = u * iw;
+                    float Ed = fmaf(ca, lpn[f], fmaf((float)FU_A2, lv1[f], cb));
+                    Ed = fmaf(0x1p-23f, fabsf(dotf) + fabsf(u), fmaf(0x1p-40f, fabsf(tt), Ed));
+                    const float B = fmaf(Ed * (1.f + 0x1p-20f), iw * (1.f + 0x1p-20f), fabsf(y) * 0x1p-20f);
+                    const float lo = floorf(y - B), hi = floorf(y + B);
                     hv[q] = (int32_t)lo;
-                    if (!(lo == hi && x_ok)) fmask |= 1u << f;   // provisional; redone by hash_fixup_kernel
+                    if (lo != hi) fmask |= 1u << f;   // provisional; redone by hash_fixup_kernel
                 }
                 const int64_t o = row * a.L + l;
                 if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
@@ -499,11 +519,11 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             if (fb) {
                 // rows whose floor the split bound cannot certify: (row << 32 | fn mask)
                 const int leader = __builtin_ctzll(fb);
-                unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(a.hfix_count, (unsigned long long)__popcll(fb));
+                int base = 0;
+                if (lane == leader) base = atomicAdd(lcount + 1, __popcll(fb));
                 base = __shfl(base, leader);
                 if (fmask != 0u && h == 1)
-                    a.hfix[base + __popcll(fb & ((1ull << lane) - 1ull))] = ((unsigned long long)row << 32) | fmask;
+                    hfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = ((unsigned long long)row << 32) | fmask;
             }
         }
 
@@ -539,16 +559,22 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 
         // ---- winner distance in reference order: the squares are independent,
         // only the sum is a chain; dims 8seg..8seg+7 belong to lane half seg & 1.
+        // The exact row is re-read here (L2-resident: this wave loaded it moments
+        // ago) rather than held in 64 VGPRs through the MFMA loop.
         const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;    // I1 < K always (padding scores are -inf)
+        const float* xr = a.X + (valid ? row : 0) * FU_D + 8 * h;
         double acc = 0.0;
 #pragma unroll
         for (int s = 0; s < 8; s++) {
             double sq[8];
+            const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
+            const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
+            const float xv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
                 const double2 cc = *reinterpret_cast<const double2*>(crow + 16 * s + j);
-                const double d0 = __dsub_rn((double)xf[8 * s + j], cc.x);
-                const double d1 = __dsub_rn((double)xf[8 * s + j + 1], cc.y);
+                const double d0 = __dsub_rn((double)xv[j], cc.x);
+                const double d1 = __dsub_rn((double)xv[j + 1], cc.y);
                 sq[j] = __dmul_rn(d0, d0);
                 sq[j + 1] = __dmul_rn(d1, d1);
             }
@@ -572,75 +598,104 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 a.assign[row] = I1;
                 a.dist[row] = sqrt(acc);
             } else {
-                unsigned long long base = 0;
+                int base = 0;
                 const int leader = __builtin_ctzll(amask);
-                if (lane == leader) base = atomicAdd(a.ambig_count, (unsigned long long)__popcll(amask));
+                if (lane == leader) base = atomicAdd(lcount, __popcll(amask));
                 base = __shfl(base, leader);
                 const int rank = __popcll(amask & ((1ull << lane) - 1ull));
-                a.ambig[base + rank] = (int32_t)row;
+                ambig_seg[base + rank] = (int32_t)row;
             }
         }
     }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const int c = lcount[threadIdx.x];
+        a.seg_counts[2 * blockIdx.x + threadIdx.x] = c;
+        if (c) atomicAdd(threadIdx.x == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
+    }
 }
 
-// Rows listed by the persistent form with an uncertified floor: one wave per
-// row, lane f recomputes projection f from the exact row (fp64 bound, then
-// soft-x87), and the first lane of each table rewrites tuple, phi and bucket.
-// The projections (128 x LKpad fp64, <= 32 KiB) and each wave's row sit in LDS.
+// Rows listed by the persistent form with an uncertified floor (~15% of rows
+// at w = 0.4, mostly one function each). Lane = listed row: a wave stages its
+// 64 rows into LDS with coalesced 512-B loads, then each lane recomputes every
+// function of each table its mask touches (the other k-1 values are needed for
+// phi and tuples may be NULL) with the fp64 bound of hash.hip, falling back to
+// the soft-x87 emulation, and rewrites tuple, phi and bucket.
 constexpr int HF_WAVES = 4;
+constexpr int HF_XS = FU_D + 1;                      // row stride (floats): lanes hit distinct banks
+constexpr size_t HF_LDS = (size_t)FU_D * 32 * 4 + (size_t)HF_WAVES * 64 * HF_XS * 4;
+
+__device__ int32_t fixup_hash(const float* xs, const float* pts, int LKpad, int f, double tt, double ww, double pn,
+                              float w, unsigned long long* stats) {
+    double acc = 0.0, xn2 = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < FU_D; j++) {
+        const double xj = (double)xs[j];
+        xn2 = fma(xj, xj, xn2);
+        acc = fma((double)pts[j * LKpad + f], xj, acc);
+    }
+    const double P = pn * sqrt(xn2) * (1.0 + 0x1p-40);
+    const double y = (acc + tt) / ww;
+    const double B = ((double)(FU_D + 2) * 0x1p-52 * (P + fabs(tt))) / ww + fabs(y) * 0x1p-51;
+    const double lo = floor(y - B), hi = floor(y + B);
+    if (lo == hi) return (int32_t)lo;
+    sx80 s = sx_zero();
+    for (int j = 0; j < FU_D; j++) s = sx_add_double(s, __dmul_rn((double)pts[j * LKpad + f], (double)xs[j]));
+    s = sx_add_double(s, tt);
+    atomicAdd(stats + STAT_HASH_EXACT, 1ull);
+    return (int32_t)sx_floor_i64(sx_div(s, sx_from_float(w)));
+}
+
 __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) {
-    __shared__ double pts[FU_D * 32];
-    __shared__ float xs[HF_WAVES][FU_D];
-    const unsigned long long n = *a.hfix_count;
-    const int wave = threadIdx.x >> 6, f = threadIdx.x & 63;
-    if ((unsigned long long)blockIdx.x * HF_WAVES >= n) return;      // block-uniform
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* pts = reinterpret_cast<float*>(smem);     // [128][LKpad] projections (float values: exact)
+    // block b takes the list segment persistent block b wrote
+    const int n = a.seg_counts[2 * blockIdx.x + 1];
+    const unsigned long long* seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float* xs = reinterpret_cast<float*>(smem + FU_D * 32 * 4) + wave * 64 * HF_XS;
+    if (n == 0) return;                                                 // block-uniform
     const int LKpad = a.LKpad;
-    for (int e = threadIdx.x; e < FU_D * LKpad; e += 64 * HF_WAVES) pts[e] = a.PT[e];
+    for (int e = threadIdx.x; e < FU_D * LKpad; e += 64 * HF_WAVES) pts[e] = (float)a.PT[e];
     __syncthreads();
-    const bool on = f < a.LK;
-    const double tt = on ? (double)a.tv[f] : 0.0, ww = (double)a.w, pn = on ? a.pnorm[f] : 0.0;
-    const int l = on ? f / a.k : 0;
-    for (unsigned long long e = (unsigned long long)blockIdx.x * HF_WAVES + wave; e < n;
-         e += (unsigned long long)gridDim.x * HF_WAVES) {
-        const int64_t row = (int64_t)(a.hfix[e] >> 32);
-        const float* xr = a.X + row * FU_D;
-        xs[wave][f] = xr[f];
-        xs[wave][f + 64] = xr[f + 64];
+    const double ww = (double)a.w;
+    for (int base = wave * 64; base < n; base += HF_WAVES * 64) {
+        const int cnt = min(64, n - base);
+        const unsigned long long ent = lane < cnt ? seg[base + lane] : 0ull;
+        // stage: two rows per instruction (32 lanes x 16 B each), all loads in flight
+        const int half = lane >> 5, q = lane & 31;
+        float4 v[32];
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            const int r = 2 * i + half;
+            const int64_t rr = (int64_t)(__shfl((long long)ent, min(r, cnt - 1)) >> 32);
+            v[i] = *reinterpret_cast<const float4*>(a.X + rr * FU_D + 4 * q);
+        }
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            float* d = xs + (2 * i + half) * HF_XS + 4 * q;
+            d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
+        }
         wave_sync();
-        int32_t hv = 0;
-        if (on) {
-            // fp64 FMA chain with the rigorous bound of hash.hip; soft-x87 when it fails
-            double acc = 0.0, xn2 = 0.0;
-#pragma unroll 16
-            for (int j = 0; j < FU_D; j++) {
-                const double xj = (double)xs[wave][j];
-                xn2 = fma(xj, xj, xn2);
-                acc = fma(pts[j * LKpad + f], xj, acc);
+        if (lane < cnt) {
+            const int64_t row = (int64_t)(ent >> 32);
+            const uint32_t mask = (uint32_t)ent;
+            const float* x = xs + lane * HF_XS;
+            const uint32_t kmask = a.k >= 32 ? 0xFFFFFFFFu : ((1u << a.k) - 1u);
+            // Recompute the flagged functions only (the set-bit loop runs the
+            // wave's max popcount, not the union); the table's other values are
+            // the certified ones already in tuples (always present on this path).
+            for (uint32_t m = mask; m; m &= m - 1) {
+                const int f = __builtin_ctz(m);
+                a.tuples[row * a.LK + f] = fixup_hash(x, pts, LKpad, f, (double)a.tv[f], ww, a.pnorm[f], a.w, a.stats);
             }
-            const double P = pn * sqrt(xn2) * (1.0 + 0x1p-40);
-            const double y = (acc + tt) / ww;
-            const double B = ((double)(FU_D + 2) * 0x1p-52 * (P + fabs(tt))) / ww + fabs(y) * 0x1p-51;
-            const double lo = floor(y - B), hi = floor(y + B);
-            if (lo == hi) {
-                hv = (int32_t)lo;
-            } else {
-                sx80 s = sx_zero();
-                for (int j = 0; j < FU_D; j++) s = sx_add_double(s, __dmul_rn(pts[j * LKpad + f], (double)xs[wave][j]));
-                s = sx_add_double(s, tt);
-                atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
-                hv = (int32_t)sx_floor_i64(sx_div(s, sx_from_float(a.w)));
-            }
-        }
-        // gather the table's k values (all lanes take part in the shuffles)
-        uint32_t hn = 0;
-        for (int i = 0; i < a.k; i++) {
-            const int src = min(l * a.k + i, 63);
-            const int32_t hi = __shfl(hv, src);
-            hn += phi_term(hi, a.rv[min(src, a.LK - 1)]);
-        }
-        if (on) {
-            if (a.tuples) a.tuples[row * a.LK + f] = hv;
-            if (f == l * a.k) {
+            for (int l = 0; l < a.L; l++) {
+                if (!(mask & (kmask << (l * a.k)))) continue;
+                uint32_t hn = 0;
+                for (int i = 0; i < a.k; i++) {
+                    const int f = l * a.k + i;
+                    hn += phi_term(a.tuples[row * a.LK + f], a.rv[f]);
+                }
                 const uint32_t ph = phi_final(hn);
                 if (a.phi) a.phi[row * a.L + l] = (int32_t)ph;
                 if (a.bucket) a.bucket[row * a.L + l] = bucket_of(ph, a.nb);
@@ -694,7 +749,8 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
     return kstatus("fused_centroid_prep");
 }
 
-int launch_fused(hipStream_t s, bool hash, const FusedLaunch& f) {
+int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
+    f.nseg = 0;
     if (f.N <= 0) return 0;
     FusedArgs a;
     a.X = f.X; a.N = f.N;
@@ -716,16 +772,28 @@ int launch_fused(hipStream_t s, bool hash, const FusedLaunch& f) {
         const int ncu = dev < 64 && cus[dev] > 0 ? cus[dev] : 256;
         const int64_t ntiles = (f.N + 31) / 32;
         const int64_t want = (ntiles + FP_WAVES - 1) / FP_WAVES;
-        const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(ncu, want))), block(FP_THREADS);
+        const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(ncu, want));
+        const dim3 grid((unsigned)nblk), block(FP_THREADS);
         const size_t lds = (size_t)fp_lds_bytes(f.Kpad, hash);
+        // list segments: block b's tiles hold at most FP_WAVES * 32 * ceil(tiles / (grid * FP_WAVES)) rows
+        a.seg_rows = (int64_t)FP_WAVES * 32 * ((ntiles + (int64_t)nblk * FP_WAVES - 1) / ((int64_t)nblk * FP_WAVES));
+        a.seg_counts = f.seg_counts;
+        if (!f.seg_counts || f.seg_cap < nblk || (int64_t)nblk * a.seg_rows > f.list_cap) {
+            set_error("launch_fused: list workspace too small");
+            return -1;
+        }
+        f.nseg = nblk;
+        f.seg_rows = a.seg_rows;
         if (!hash) {
             hipLaunchKernelGGL(fused_persistent_kernel<false>, grid, block, lds, s, a);
             return kstatus("fused_persistent_kernel");
         }
-        if (!a.hfix || !a.hfix_count) return -1;
+        if (!a.hfix || !a.hfix_count || !a.tuples || f.LKpad > 32) {   // pts[] holds 128 x 32 projections
+            set_error("launch_fused: hashing needs the fix-up list, a tuple buffer and L*k <= 32");
+            return -1;
+        }
         hipLaunchKernelGGL(fused_persistent_kernel<true>, grid, block, lds, s, a);
-        if (f.LKpad > 32) return -1;                      // pts[] holds 128 x 32 projections
-        hipLaunchKernelGGL(hash_fixup_kernel, dim3(1024), dim3(64 * HF_WAVES), 0, s, a);
+        hipLaunchKernelGGL(hash_fixup_kernel, grid, dim3(64 * HF_WAVES), HF_LDS, s, a);
         return kstatus("fused_persistent_kernel");
     }
     const dim3 grid((unsigned)((f.N + FU_PB - 1) / FU_PB)), block(FU_THREADS);

@@ -45,7 +45,7 @@ struct lshkm_ctx_s {
     hipStream_t own_stream = nullptr;
     lshkm::Buf stats;            // STAT_COUNT x u64
     // assignment workspace
-    lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src, ws_hfix, ws_ct;
+    lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src, ws_hfix, ws_ct, ws_seg, ws_tuples;
     // scatter / query / update workspace (see api_index.cpp for the slot map)
     lshkm::Buf ws[16];
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)

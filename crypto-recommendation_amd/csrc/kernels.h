@@ -47,9 +47,11 @@ int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const d
                         int metric, const int32_t* rows, const unsigned long long* row_count,
                         int64_t max_rows, int32_t* assign, double* dist);
 // Euclidean, listed rows, batched (CT: d * ceil64(K) doubles of workspace).
+// Segmented form (seg_counts != NULL): segment b = rows[b * seg_rows ...], count seg_counts[2b].
 int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
-                             int32_t* assign, double* dist);
+                             int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
+                             int64_t seg_rows = 0, int nseg = 0);
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist);
 
@@ -117,13 +119,23 @@ struct FusedLaunch {
     double* dist = nullptr;
     int32_t* ambig = nullptr;
     unsigned long long* ambig_count = nullptr;
-    unsigned long long* hfix = nullptr;          // [N] (row << 32 | fn mask) of uncertified hashes
+    unsigned long long* hfix = nullptr;          // (row << 32 | fn mask) of uncertified hashes
     unsigned long long* hfix_count = nullptr;
     unsigned long long* stats = nullptr;
+    // persistent form: ambig / hfix are split in per-block segments
+    int64_t list_cap = 0;                        // entries available in ambig and in hfix
+    int32_t* seg_counts = nullptr;               // [2 * seg_cap]
+    int seg_cap = 0;
+    // out: nseg > 0 when the lists are segmented (segment b = [b * seg_rows, ...))
+    int nseg = 0;
+    int64_t seg_rows = 0;
 };
+// List capacity the persistent form may need beyond N entries (grid <= 1024 blocks).
+constexpr int64_t FUSED_LIST_SLACK = 32 + 1024 * 12 * 32;
+constexpr int FUSED_MAX_SEGS = 1024;
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
                       float* cbound);
-int launch_fused(hipStream_t s, bool hash, const FusedLaunch& f);
+int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
 
 // Synthetic data.
 int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X);

@@ -32,6 +32,16 @@ for step in "$@"; do
            > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err")
         rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    sq)
+      i=0
+      for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" \
+                 "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_SALU"; do
+        i=$((i+1))
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --pmc $set --output-format csv \
+           -d "$OUT/sq$i" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
+           > "$OUT/sq$i.json" 2> "$OUT/sq$i.err")
+        rc=$?; echo "sq pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
