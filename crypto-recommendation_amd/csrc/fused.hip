@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
 
 #include "common.h"
 #include "kernels.h"
@@ -55,8 +56,31 @@ constexpr int FU_LDS_BYTES = FU_HS_OFF + FU_PB * 32 * 4; // 80 KiB -> 2 blocks /
 static_assert(FU_CHUNK_BYTES <= FU_XSTAGE_BYTES, "chunk region must fit in the staging alias");
 
 constexpr double FU_A1 = 1.25 * 0x1p-16;
+// Hash tile of the persistent form: hi products summed per 32-dim chunk in f32
+// (<= 31 roundings, 2^-18 sum|terms|), chunks in fp64; the split residuals and
+// lo terms add < 0.25 * 2^-18 as in A1's derivation.
+constexpr double FU_A1H = 1.25 * 0x1p-18;
 constexpr double FU_A2 = 0x1p-24;
 constexpr float FU_RANGE = 32768.f;
+
+// phi % nb by multiply-high (Granlund-Montgomery round-up, 31-bit numerators):
+// nb in [2, 2^31), l = ceil(log2 nb), m = floor(2^(31+l) / nb) + 1 < 2^32,
+// q = (m * phi) >> (31 + l). nb == 1 -> 0; nb >= 2^31 -> phi (phi < 2^31).
+struct BucketDiv {
+    uint32_t m, nb;
+    int sh, mode;           // mode 0: magic, 1: nb == 1, 2: nb > phi always
+};
+__host__ inline BucketDiv make_bucket_div(int64_t nb) {
+    BucketDiv b{0u, 0u, 0, 0};
+    if (nb <= 1) { b.mode = 1; return b; }
+    if (nb >= (1ll << 31)) { b.mode = 2; return b; }
+    int l = 0;
+    while ((1ll << l) < nb) l++;
+    b.m = (uint32_t)((((unsigned __int128)1 << (31 + l)) / (unsigned __int128)nb) + 1);
+    b.nb = (uint32_t)nb;
+    b.sh = l - 1;
+    return b;
+}
 
 struct FusedArgs {
     const float* X;
@@ -94,7 +118,21 @@ struct FusedArgs {
     // and reports their counts in seg_counts[2b] (ambiguous), seg_counts[2b+1] (fix-up)
     int64_t seg_rows;
     int32_t* seg_counts;
+    BucketDiv bdiv;          // phi % nb by multiply-high
+    unsigned long long* prof;        // LSHKM_PHASE_TIMING builds only: per-phase wave cycles
 };
+
+// Profiling builds (make prof -> liblshkm_prof.so) accumulate s_memtime per
+// phase of the persistent loop; the product library compiles these away.
+#ifdef LSHKM_PHASE_TIMING
+#define PT_DECL unsigned long long pt_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long pt_t = __builtin_amdgcn_s_memtime();
+#define PT_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pt_acc[i] += t_ - pt_t; pt_t = t_; }
+#define PT_FLUSH if (lane == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd(a.prof + i_, pt_acc[i_]);
+#else
+#define PT_DECL
+#define PT_MARK(i)
+#define PT_FLUSH
+#endif
 
 __device__ inline void split8(const float* x, half8& hi, half8& lo) {
 #pragma unroll
@@ -103,6 +141,32 @@ __device__ inline void split8(const float* x, half8& hi, half8& lo) {
         hi[j] = hv;
         lo[j] = (_Float16)(x[j] - (float)hv);
     }
+}
+
+typedef float float2v __attribute__((ext_vector_type(2)));
+constexpr double FU_SQRT_D = 11.313708498984761 * (1.0 + 0x1p-40);   // sqrt(128), rounded up
+
+// split8 with the residual subtraction on packed f32 (v_pk_add_f32).
+__device__ inline void split8p(const float* x, half8& hi, half8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const _Float16 h0 = (_Float16)x[j], h1 = (_Float16)x[j + 1];
+        hi[j] = h0;
+        hi[j + 1] = h1;
+        const float2v xv = {x[j], x[j + 1]}, hv = {(float)h0, (float)h1};
+        const float2v r = xv - hv;
+        lo[j] = (_Float16)r.x;
+        lo[j + 1] = (_Float16)r.y;
+    }
+}
+
+// Within each group of 4 lanes, lane q receives lane q-1's value (lane 0 its
+// own): DPP quad_perm [0,0,1,2], a VALU move.
+__device__ inline double quad_shift_up(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, 0x90, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), 0x90, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
 }
 
 // EuclideanPhi arithmetic (euclidean_phi_gen.hpp:70-92) in 32-bit form, M =
@@ -125,6 +189,18 @@ __device__ inline uint32_t phi_final(uint32_t hn) {
 // phi % nb (cust_hashtable.hpp:68); phi < 2^31
 __device__ inline int32_t bucket_of(uint32_t ph, int64_t nb) {
     return nb <= 0xFFFFFFFFll ? (int32_t)(ph % (uint32_t)nb) : (int32_t)ph;
+}
+// Certified hashes have |h| < 2^22 and r <= 100, so h * r does not wrap and
+// ((temp % M) + M) % M is one select.
+__device__ inline uint32_t phi_term_small(int32_t h, int32_t r) {
+    const int32_t p = h * r;
+    return p < 0 ? (uint32_t)p + PHI_M : (uint32_t)p;
+}
+__device__ inline int32_t bucket_fast(uint32_t ph, const BucketDiv& b) {
+    if (b.mode == 1) return 0;
+    if (b.mode == 2) return (int32_t)ph;
+    const uint32_t q = __umulhi(ph, b.m) >> b.sh;
+    return (int32_t)(ph - q * b.nb);
 }
 
 // Exact (reference-order) hash of one projection from the fp32 row in HBM.
@@ -415,13 +491,14 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = lane & 31, h = lane >> 5;
-    const float ecf = a.cbound[0], ebf = a.cbound[1];
+    const float ecf = a.cbound[0], ebf = a.cbound[1], cmaxf = a.cbound[3];
     const bool c_ok = __float_as_uint(a.cbound[2]) == 0u;
     const _Float16* my_h = lch + col * FU_RS + 8 * h;
     const _Float16* my_l = lcl + col * FU_RS + 8 * h;
     const int ntile32 = Kpad >> 5;
     const int64_t ntiles = (a.N + 31) >> 5;
 
+    PT_DECL
     for (int64_t tile = (int64_t)blockIdx.x * FP_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FP_WAVES) {
         const int64_t row = tile * 32 + col;
         const bool valid = row < a.N;
@@ -429,43 +506,74 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         // ---- point -> registers and the split B operand
         float xf[64];
         {
-            const float* xr = a.X + row * FU_D + 8 * h;
+            // rows past N read row N-1 (results for them are never written)
+            const float* xr = a.X + (valid ? row : a.N - 1) * FU_D + 8 * h;
 #pragma unroll
             for (int s = 0; s < 8; s++) {
-                float4 p0 = make_float4(0.f, 0.f, 0.f, 0.f), p1 = p0;
-                if (valid) {
-                    p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
-                    p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
-                }
+                const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
+                const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
                 xf[8 * s + 0] = p0.x; xf[8 * s + 1] = p0.y; xf[8 * s + 2] = p0.z; xf[8 * s + 3] = p0.w;
                 xf[8 * s + 4] = p1.x; xf[8 * s + 5] = p1.y; xf[8 * s + 6] = p1.z; xf[8 * s + 7] = p1.w;
             }
         }
         half8 bh[8], bl[8];
-        float xn2f = 0.f, x1f = 0.f, xmax = 0.f;
+        float2v n2a = {0.f, 0.f}, n2b = {0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 8; s++) {
-            split8(xf + 8 * s, bh[s], bl[s]);
+            split8p(xf + 8 * s, bh[s], bl[s]);
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                xn2f = fmaf(xf[8 * s + j], xf[8 * s + j], xn2f);
-                x1f += fabsf(xf[8 * s + j]);
-                xmax = fmaxf(xmax, fabsf(xf[8 * s + j]));
+            for (int j = 0; j < 8; j += 4) {
+                const float2v u = {xf[8 * s + j], xf[8 * s + j + 1]}, v = {xf[8 * s + j + 2], xf[8 * s + j + 3]};
+                n2a = __builtin_elementwise_fma(u, u, n2a);
+                n2b = __builtin_elementwise_fma(v, v, n2b);
             }
         }
+        float xn2f = (n2a.x + n2a.y) + (n2b.x + n2b.y);
         xn2f += __shfl_xor(xn2f, 32);
-        x1f += __shfl_xor(x1f, 32);
-        xmax = fmaxf(xmax, __shfl_xor(xmax, 32));
+        // f32 sum of squares: inflate by 2^-16 (> d 2^-24) to stay an upper bound;
+        // |x|_1 <= sqrt(d) |x|_2 replaces the L1 norm in the A2 terms, and
+        // |x|_2 <= 2^15 implies the f16 range guard |x_j| <= 2^15 (false for nan/inf).
         const double xn2 = (double)xn2f * (1.0 + 0x1p-16);
         const double nx = sqrt(xn2);
-        const double x1 = (double)x1f * (1.0 + 0x1p-16);
-        const bool x_ok = xmax <= FU_RANGE;
+        const double x1 = FU_SQRT_D * nx;
+        const bool x_ok = xn2f <= FU_RANGE * FU_RANGE;
 
+        PT_MARK(0)
         // ---- hash tile + LSH outputs (k = 4: table l = 2g + h lives in registers 4g..4g+3)
         if (HASH) {
             uint32_t fmask = 0;
-            floatx16 acc_hi, acc_lo;
-            tile_mfma(lvh + col * FU_RS + 8 * h, lvl + col * FU_RS + 8 * h, bh, bl, acc_hi, acc_lo);
+            // hi products: a fresh MFMA per 16-dim step (<= 15 roundings each),
+            // steps added in f32 (+7), then + lo (+1): <= 23 roundings of sum|terms|
+            // instead of 128 for one chain (FU_A1H), which cuts the floors left to
+            // the fix-up pass ~4x.
+            float acc_hi[16];
+            {
+                const _Float16* vh_row = lvh + col * FU_RS + 8 * h;
+                const _Float16* vl_row = lvl + col * FU_RS + 8 * h;
+                floatx16 acc_lo, tot;
+#pragma unroll
+                for (int s = 0; s < 8; s++) {
+                    const half8 ah = *reinterpret_cast<const half8*>(vh_row + 16 * s);
+                    const half8 al = *reinterpret_cast<const half8*>(vl_row + 16 * s);
+                    const floatx16 z = {};
+                    const floatx16 acc_s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], z, 0, 0, 0);
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], s ? acc_lo : z, 0, 0, 0);
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc_lo, 0, 0, 0);
+                    if (s == 0) {
+                        tot = acc_s;
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 16; r += 2) {
+                            const float2v t2 = {tot[r], tot[r + 1]}, a2 = {acc_s[r], acc_s[r + 1]};
+                            const float2v u2 = t2 + a2;
+                            tot[r] = u2.x;
+                            tot[r + 1] = u2.y;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc_hi[r] = tot[r] + acc_lo[r];
+            }
             // Certification in f32 (the floor only needs y to ~2^-20): with
             // u = f32(dot~ + t), y = f32(u * f32(1/w)),
             //   |y - (x.v + t)/w| <= (Ed + 2^-23 |u| + 2^-40 |t|) / w + 2^-21 |y|,
@@ -475,7 +583,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             // inflated by 2^-20 for their own f32 roundings, and so is the floor
             // window: floor(y - B) == floor(y + B) certifies the reference's floorl.
             const float iw = 1.0f / a.w;
-            const float ca = (float)(FU_A1 * nx) * (1.f + 0x1p-20f);
+            const float ca = (float)(FU_A1H * nx) * (1.f + 0x1p-20f);
             const float cb = (float)(FU_A2 * x1) * (1.f + 0x1p-20f);
             // Opaque zero: keeps the per-function constants as LDS reads inside
             // the loop instead of hoisted VGPRs.
@@ -494,7 +602,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int f = 4 * l + q;
-                    const float dotf = acc_hi[4 * g + q] + acc_lo[4 * g + q];
+                    const float dotf = acc_hi[4 * g + q];          // f32(fp64 hi sum + lo)
                     const float tt = lt[f];
                     const float u = dotf + tt;
                     const float y = u * iw;
@@ -507,12 +615,12 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 }
                 const int64_t o = row * a.L + l;
                 if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
-                uint32_t hn = 0;
+                uint32_t hn = 0;   // flagged values are provisional: the fix-up redoes their table
 #pragma unroll
-                for (int q = 0; q < 4; q++) hn += phi_term(hv[q], lr[4 * l + q]);
+                for (int q = 0; q < 4; q++) hn += phi_term_small(hv[q], lr[4 * l + q]);
                 const uint32_t ph = phi_final(hn);
                 if (a.phi) a.phi[o] = (int32_t)ph;
-                if (a.bucket) a.bucket[o] = bucket_of(ph, a.nb);
+                if (a.bucket) a.bucket[o] = bucket_fast(ph, a.bdiv);
             }
             fmask |= __shfl_xor(fmask, 32);
             const unsigned long long fb = __ballot(fmask != 0u && h == 1);
@@ -527,29 +635,43 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             }
         }
 
+        PT_MARK(1)
         // ---- all centroid tiles from the resident image
-        const float E = (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2) * (1.f + 0x1p-20f) + 1e-30f;
+        // Each score carries its in-tile index (4g+q) in its low 4 mantissa bits:
+        // a perturbation below 16 ulp <= 2^-19 |t|, |t| <= |x| cmax + cmax^2/2,
+        // charged to E (with 2x margin). The running max then identifies the
+        // winner without a compare/select per score; its tile is noted per tile.
+        const float E = (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2 +
+                                0x1p-18 * (nx * (double)cmaxf + 0.5 * (double)cmaxf * (double)cmaxf)) *
+                            (1.f + 0x1p-20f) + 1e-30f;
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
-        int i1 = 0;
+        int t1 = 0;
 #pragma unroll 1
         for (int t = 0; t < ntile32; t++) {
             floatx16 acc_hi, acc_lo;
             tile_mfma(my_h + t * 32 * FU_RS, my_l + t * 32 * FU_RS, bh, bl, acc_hi, acc_lo);
+            const float m1_prev = m1;
 #pragma unroll
             for (int g = 0; g < 4; g++) {
-                const int cb = t * 32 + 8 * g + 4 * h;
-                const float4 cn = *reinterpret_cast<const float4*>(lcn + cb);
-                const float cnv[4] = {cn.x, cn.y, cn.z, cn.w};
+                const float4 cn = *reinterpret_cast<const float4*>(lcn + t * 32 + 8 * g + 4 * h);
+                const float2v h01 = {acc_hi[4 * g], acc_hi[4 * g + 1]}, l01 = {acc_lo[4 * g], acc_lo[4 * g + 1]};
+                const float2v h23 = {acc_hi[4 * g + 2], acc_hi[4 * g + 3]}, l23 = {acc_lo[4 * g + 2], acc_lo[4 * g + 3]};
+                const float2v c01 = {cn.x, cn.y}, c23 = {cn.z, cn.w};
+                const float2v s01 = (h01 + l01) + c01, s23 = (h23 + l23) + c23;
+                const float sv[4] = {s01.x, s01.y, s23.x, s23.y};
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const float tv = (acc_hi[4 * g + q] + acc_lo[4 * g + q]) + cnv[q];
-                    m2 = fmaxf(m2, fminf(m1, tv));
-                    const bool c1 = tv > m1;
-                    m1 = c1 ? tv : m1;
-                    i1 = c1 ? cb + q : i1;
+                    const float tvp = __uint_as_float((__float_as_uint(sv[q]) & ~0xFu) | (uint32_t)(4 * g + q));
+                    m2 = __builtin_amdgcn_fmed3f(m2, m1, tvp);     // = max(m2, min(m1, tvp)) as m2 <= m1
+                    // plain v_max_f32: fmaxf would first re-quiet tvp (IEEE mode), and
+                    // tvp is never a NaN for a point that can be certified
+                    asm("v_max_f32 %0, %1, %2" : "=v"(m1) : "v"(m1), "v"(tvp));
                 }
             }
+            t1 = m1 != m1_prev ? t : t1;
         }
+        const uint32_t l1 = __float_as_uint(m1) & 0xFu;
+        const int i1 = t1 * 32 + 8 * (int)(l1 >> 2) + 4 * h + (int)(l1 & 3u);
         const float om1 = __shfl_xor(m1, 32), om2 = __shfl_xor(m2, 32);
         const int oi1 = __shfl_xor(i1, 32);
         const float M2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
@@ -561,43 +683,59 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         // only the sum is a chain; dims 8seg..8seg+7 belong to lane half seg & 1.
         // The exact row is re-read here (L2-resident: this wave loaded it moments
         // ago) rather than held in 64 VGPRs through the MFMA loop.
-        const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;    // I1 < K always (padding scores are -inf)
-        const float* xr = a.X + (valid ? row : 0) * FU_D + 8 * h;
-        double acc = 0.0;
+        // The chain is re-laid for the L1: lane (p, q) = 4 * p + q owns the
+        // contiguous quarter dims [32q, 32q+32) of point 16r + p (round r = 0, 1),
+        // so each 16-B lane load is a quarter of one 64-B sector of a row (4 lanes
+        // fill it) instead of a half-used sector per lane. The row and the winner's
+        // fp64 row are re-read from L2; the squares are formed with every lane
+        // active, then the quarters add in order, handing the sum on with a quad
+        // DPP move.
+        PT_MARK(2)
+        const int q4 = lane & 3, p4 = lane >> 2;
+#pragma unroll 1
+        for (int r = 0; r < 2; r++) {
+            const int pt = 16 * r + p4;                              // point within the tile
+            const int Ip = __shfl(I1, pt);                           // lane pt (half 0) holds it
+            const int cp = __shfl((int)cert, pt);
+            const int64_t prow = tile * 32 + pt;
+            const bool pv = prow < a.N;
+            const float* xq = a.X + (pv ? prow : a.N - 1) * FU_D + 32 * q4;
+            const double* cq = a.C64 + (size_t)Ip * FU_D + 32 * q4;  // Ip < K always (padding scores are far below)
+            double sq[32];
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
-            double sq[8];
-            const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
-            const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
-            const float xv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                const double2 cc = *reinterpret_cast<const double2*>(crow + 16 * s + j);
-                const double d0 = __dsub_rn((double)xv[j], cc.x);
-                const double d1 = __dsub_rn((double)xv[j + 1], cc.y);
-                sq[j] = __dmul_rn(d0, d0);
-                sq[j + 1] = __dmul_rn(d1, d1);
+            for (int u = 0; u < 8; u++) {
+                const float4 xv = *reinterpret_cast<const float4*>(xq + 4 * u);
+                const double2 c0 = *reinterpret_cast<const double2*>(cq + 4 * u);
+                const double2 c1 = *reinterpret_cast<const double2*>(cq + 4 * u + 2);
+                const double d0 = __dsub_rn((double)xv.x, c0.x), d1 = __dsub_rn((double)xv.y, c0.y);
+                const double d2 = __dsub_rn((double)xv.z, c1.x), d3 = __dsub_rn((double)xv.w, c1.y);
+                sq[4 * u] = __dmul_rn(d0, d0);
+                sq[4 * u + 1] = __dmul_rn(d1, d1);
+                sq[4 * u + 2] = __dmul_rn(d2, d2);
+                sq[4 * u + 3] = __dmul_rn(d3, d3);
             }
-            if (h == 0) {                      // dims 16s .. 16s+7
+            double acc = 0.0;
 #pragma unroll
-                for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
-            }
-            const double from0 = __shfl_xor(acc, 32);          // whole wave exchanges
-            if (h == 1) {                      // dims 16s+8 .. 16s+15
-                acc = from0;
+            for (int qq = 0; qq < 4; qq++) {
+                if (q4 == qq) {
 #pragma unroll
-                for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
+                    for (int j = 0; j < 32; j++) acc = __dadd_rn(acc, sq[j]);
+                }
+                if (qq < 3) {
+                    const double moved = quad_shift_up(acc);         // lane q takes lane q-1's sum
+                    if (q4 == qq + 1) acc = moved;
+                }
             }
-            const double from1 = __shfl_xor(acc, 32);
-            if (h == 0) acc = from1;
+            if (q4 == 3 && pv && cp) {
+                a.assign[prow] = Ip;
+                a.dist[prow] = sqrt(acc);
+            }
         }
+        PT_MARK(3)
         const bool amb = valid && !cert;
         const unsigned long long amask = __ballot(amb && h == 1);
         if (h == 1 && valid) {
-            if (cert) {
-                a.assign[row] = I1;
-                a.dist[row] = sqrt(acc);
-            } else {
+            if (!cert) {
                 int base = 0;
                 const int leader = __builtin_ctzll(amask);
                 if (lane == leader) base = atomicAdd(lcount, __popcll(amask));
@@ -606,7 +744,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 ambig_seg[base + rank] = (int32_t)row;
             }
         }
+        PT_MARK(4)
     }
+    PT_FLUSH
     __syncthreads();
     if (threadIdx.x < 2) {
         const int c = lcount[threadIdx.x];
@@ -729,7 +869,9 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     }
     const unsigned long long anybad = __ballot(bad);
     if (lane != 0) return;
-    if (c >= K) { cnh[c] = -__builtin_inff(); return; }
+    // padding rows: a finite score far below any real one (|x.c| < 2^38 under the
+    // range guard), so the packed-index trick never meets an inf/nan
+    if (c >= K) { cnh[c] = -0x1p100f; return; }
     cnh[c] = (float)(-0.5 * s2);
     const double up = 1.0 + 0x1p-18;
     const double nc = sqrt(s2) * (1.0 + 0x1p-30);
@@ -738,6 +880,7 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     const float eb = (float)((FU_A2 * s1 * (1.0 + 0x1p-20) + 0x1p-23 * s2 + 0x1p-41 * s2) * up);
     atomicMax(cb + 0, __float_as_uint(ec));     // positive floats order like their bits
     atomicMax(cb + 1, __float_as_uint(eb));
+    atomicMax(cb + 3, __float_as_uint((float)(nc * up)));   // max |c|, rounded up
     if (anybad) atomicOr(cb + 2, 1u);
 }
 
@@ -760,6 +903,23 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.tuples = f.tuples; a.phi = f.phi; a.bucket = f.bucket; a.assign = f.assign; a.dist = f.dist;
     a.ambig = f.ambig; a.ambig_count = f.ambig_count; a.stats = f.stats;
     a.hfix = f.hfix; a.hfix_count = f.hfix_count;
+    a.bdiv = make_bucket_div(f.nb);
+    a.prof = nullptr;
+#ifdef LSHKM_PHASE_TIMING
+    static unsigned long long* prof_d = nullptr;
+    if (!prof_d) (void)hipMalloc(&prof_d, 64);
+    (void)hipMemsetAsync(prof_d, 0, 64, s);
+    a.prof = prof_d;
+    struct PhaseReport {      // printed after the launch sequence below
+        hipStream_t s; unsigned long long* d;
+        ~PhaseReport() {
+            unsigned long long v[6];
+            (void)hipMemcpyAsync(v, d, 48, hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            fprintf(stderr, "PHASES load+split %llu hash %llu centroids %llu chain %llu lists %llu\n", v[0], v[1], v[2], v[3], v[4]);
+        }
+    } report{s, prof_d};
+#endif
     const char* force = getenv("LSHKM_FUSED_FORM");     // "chunked" forces the streaming form (tests)
     const bool chunked = force && !strcmp(force, "chunked");
     if (!chunked && f.Kpad <= FP_KMAX && (!hash || f.k == 4)) {

@@ -16,7 +16,7 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblshkm.so")
+LIB_PATH = os.environ.get("LSHKM_LIB") or os.path.join(_HERE, "liblshkm.so")   # override: profiling builds
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "lshkm.h")
 
 EUCLIDEAN, COSINE = 0, 1
