@@ -427,15 +427,21 @@ __global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
 
 // ------------------------------------------------------------- persistent form
 // For Kpad <= 256 the whole split centroid set (2 x 256 x 272 B) fits in LDS
-// next to the 32 hash rows, so one block per CU loads it ONCE and its 12 waves
-// (3 per SIMD, <= 168 VGPRs) then loop independently over 32-point tiles: no
-// barrier in the main loop, points go straight from HBM into registers (lane
-// half h: dims 16s+8h..+7 of point lane&31 -- the B-operand layout), and the
-// winner's reference-order distance re-reads the row from L2. Hashing here is
+// next to the 32 hash rows, so one block per CU loads it ONCE and its 8 waves
+// (2 per SIMD) then loop independently over 32-point tiles: no barrier in the
+// main loop, points go straight from HBM into registers (lane half h: dims
+// 16s+8h..+7 of point lane&31 -- the B-operand layout) and stay there, exact,
+// for the winner's reference-order distance. Hashing here is
 // specialised to k = 4 (the reference default, euclidean_phi_gen.hpp): table l's
 // four values are then D-registers 4(l>>1)..+3 of lane half l&1, so phi and the
 // bucket ID are computed in-register.
-constexpr int FP_WAVES = 12;             // 3 per SIMD: <= 168 VGPRs
+// FP_KEEP_X (default): the exact row stays in registers for the distance chain,
+// 8 waves/CU. 0: 12 waves/CU re-reading the row in a quad layout -- measured
+// 18% slower, the re-read mostly misses L2 (12 x 16 KiB in flight per CU).
+#ifndef FP_KEEP_X
+#define FP_KEEP_X 1
+#endif
+constexpr int FP_WAVES = FP_KEEP_X ? 8 : 12;   // 2 / 3 per SIMD: <= 256 / 168 VGPRs
 constexpr int FP_THREADS = 64 * FP_WAVES;
 constexpr int FP_KMAX = 256;
 constexpr int FP_HC_BYTES = 32 * (4 + 4 + 4 + 4);     // hash constants |v|_2, |v|_1, t, r
@@ -691,6 +697,42 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         // active, then the quarters add in order, handing the sum on with a quad
         // DPP move.
         PT_MARK(2)
+#if FP_KEEP_X
+        {
+            // exact row still in registers (B-operand layout): lane half h owns
+            // dims 16s+8h..+7; only the winner's fp64 row is loaded
+            const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
+            double acc = 0.0;
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                double sq[8];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const double2 cc = *reinterpret_cast<const double2*>(crow + 16 * s + 2 * j);
+                    const double d0 = __dsub_rn((double)xf[8 * s + 2 * j], cc.x);
+                    const double d1 = __dsub_rn((double)xf[8 * s + 2 * j + 1], cc.y);
+                    sq[2 * j] = __dmul_rn(d0, d0);
+                    sq[2 * j + 1] = __dmul_rn(d1, d1);
+                }
+                if (h == 0) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
+                }
+                const double from0 = __shfl_xor(acc, 32);
+                if (h == 1) {
+                    acc = from0;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
+                }
+                const double from1 = __shfl_xor(acc, 32);
+                if (h == 0) acc = from1;
+            }
+            if (h == 1 && valid && cert) {
+                a.assign[row] = I1;
+                a.dist[row] = sqrt(acc);
+            }
+        }
+#else
         const int q4 = lane & 3, p4 = lane >> 2;
 #pragma unroll 1
         for (int r = 0; r < 2; r++) {
@@ -731,6 +773,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 a.dist[prow] = sqrt(acc);
             }
         }
+#endif
         PT_MARK(3)
         const bool amb = valid && !cert;
         const unsigned long long amask = __ballot(amb && h == 1);

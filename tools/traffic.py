@@ -1,0 +1,74 @@
+"""Per-launch HBM traffic of the fused pass from rocprofv3 PMC passes.
+
+usage: python tools/traffic.py gpurun_out/<tag> [out.json]
+
+Reads <tag>/pmc_FETCH_SIZE/**/counter_collection.csv and pmc_WRITE_SIZE/...,
+sums the fused pass's kernels per dispatch (fused_persistent_kernel +
+hash_fixup_kernel, or fused_kernel in the chunked form) and applies the gfx950
+corrections of MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half the
+bytes of a wide streaming read -> x2; WRITE_SIZE is exact for 16-B stores.
+Both counters are in KiB."""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+FUSED = ("fused_persistent_kernel", "hash_fixup_kernel", "fused_kernel")
+
+
+def per_launch(path, counter):
+    files = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {path}")
+    by_dispatch = {}
+    names = {}
+    for fn in files:
+        for r in csv.DictReader(open(fn)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"]
+            if not any(f in k for f in FUSED):
+                continue
+            d = int(r["Dispatch_Id"])
+            by_dispatch[d] = by_dispatch.get(d, 0.0) + float(r["Counter_Value"])
+            names[d] = k
+    # group consecutive persistent + fix-up dispatches into one fused pass
+    passes, cur = [], None
+    for d in sorted(by_dispatch):
+        if "hash_fixup_kernel" in names[d] and cur is not None:
+            cur += by_dispatch[d]
+            passes[-1] = cur
+        else:
+            cur = by_dispatch[d]
+            passes.append(cur)
+    return passes
+
+
+def main():
+    tag = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    fetch = per_launch(os.path.join(tag, "pmc_FETCH_SIZE"), "FETCH_SIZE")
+    write = per_launch(os.path.join(tag, "pmc_WRITE_SIZE"), "WRITE_SIZE")
+    f_kib = statistics.median(fetch)
+    w_kib = statistics.median(write)
+    res = {
+        "N": 10_000_000, "K": 256,
+        "passes_measured": [len(fetch), len(write)],
+        "fetch_size_kib_raw": f_kib,
+        "write_size_kib": w_kib,
+        "hbm_read_bytes_per_launch": 2 * f_kib * 1024,
+        "hbm_write_bytes_per_launch": w_kib * 1024,
+        "hbm_bytes_per_launch": 2 * f_kib * 1024 + w_kib * 1024,
+        "note": "FETCH_SIZE x2 (gfx950 streaming-read correction), WRITE_SIZE as counted; "
+                "fused pass = fused_persistent_kernel + hash_fixup_kernel",
+    }
+    print(json.dumps(res, indent=1))
+    if out:
+        with open(out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
