@@ -326,7 +326,7 @@ static int exact_listed(lshkm_ctx ctx, const float* X, int d, const double* C, i
     if (!seg_counts && (metric != LSHKM_METRIC_EUCLIDEAN || d > 256))
         return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist);
     int rc;
-    if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 63) / 64 * 64) * 8))) return rc;
+    if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 255) / 256 * 256) * 8))) return rc;
     return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
                                     seg_counts, seg_rows, nseg);
 }

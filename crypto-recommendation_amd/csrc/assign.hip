@@ -307,6 +307,7 @@ int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const d
 // centroid) for XB_R rows. Lane holds centroids c0 + lane + 64i, i < 4.
 constexpr int XB_R = 8;
 constexpr int XB_WAVES = 4;
+constexpr int XB_SPLIT = 4;      // blocks per list segment: 16 waves per CU hide the CT-load latency
 constexpr int XB_DMAX = 256;
 
 __global__ void transpose_centroids_kernel(const double* __restrict__ C, int K, int Kpad, int d,
@@ -325,11 +326,12 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
     __shared__ float xs[XB_WAVES][XB_R][XB_DMAX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int64_t total, g0, gstride;
-    if (seg_counts) {            // block b: the segment persistent block b wrote
-        rows += (int64_t)blockIdx.x * seg_rows;
-        total = seg_counts[2 * blockIdx.x];
-        g0 = wave;
-        gstride = XB_WAVES;
+    if (seg_counts) {            // XB_SPLIT blocks per segment (the one persistent block b wrote)
+        const int seg = blockIdx.x / XB_SPLIT, part = blockIdx.x % XB_SPLIT;
+        rows += (int64_t)seg * seg_rows;
+        total = seg_counts[2 * seg];
+        g0 = (int64_t)part * XB_WAVES + wave;
+        gstride = (int64_t)XB_SPLIT * XB_WAVES;
     } else {
         total = (int64_t)*row_count;
         if (total > max_rows) total = max_rows;
@@ -356,11 +358,12 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
             for (int r = 0; r < XB_R; r++)
 #pragma unroll
                 for (int i = 0; i < 4; i++) acc[r][i] = 0.0;
-            const double* ct = CT + c0 + lane;
+            const double* ct = CT + c0 + lane;   // CT rows are padded to a multiple of 256 columns
+#pragma unroll 4
             for (int j = 0; j < d; j++) {
                 double cv[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++) cv[i] = c0 + lane + 64 * i < Kpad ? ct[(size_t)j * Kpad + 64 * i] : 0.0;
+                for (int i = 0; i < 4; i++) cv[i] = ct[(size_t)j * Kpad + 64 * i];
 #pragma unroll
                 for (int r = 0; r < XB_R; r++) {
                     const double xj = (double)xs[wave][r][j];
@@ -409,11 +412,11 @@ int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double*
         set_error("launch_assign_exact_list: unsupported shape");
         return -1;
     }
-    const int Kpad = (K + 63) / 64 * 64;
+    const int Kpad = (K + 255) / 256 * 256;     // CT row stride: whole 256-centroid passes, no bounds checks
     const int64_t ne = (int64_t)d * Kpad;
     hipLaunchKernelGGL(transpose_centroids_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, C, K, Kpad, d, CT);
     const int64_t groups = (max_rows + XB_R - 1) / XB_R;
-    const int64_t blocks = seg_counts ? nseg : std::min<int64_t>((groups + XB_WAVES - 1) / XB_WAVES, 2048);
+    const int64_t blocks = seg_counts ? (int64_t)nseg * XB_SPLIT : std::min<int64_t>((groups + XB_WAVES - 1) / XB_WAVES, 2048);
     hipLaunchKernelGGL(assign_exact_batch_kernel, dim3((unsigned)blocks), dim3(64 * XB_WAVES), 0, s, X, d, CT, K, Kpad,
                        rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
     return kstatus("assign_exact_batch_kernel");

@@ -798,24 +798,32 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     }
 }
 
-// Rows listed by the persistent form with an uncertified floor (~15% of rows
-// at w = 0.4, mostly one function each). Lane = listed row: a wave stages its
-// 64 rows into LDS with coalesced 512-B loads, then each lane recomputes every
-// function of each table its mask touches (the other k-1 values are needed for
-// phi and tuples may be NULL) with the fp64 bound of hash.hip, falling back to
-// the soft-x87 emulation, and rewrites tuple, phi and bucket.
+// Rows listed by the persistent form with an uncertified floor: fix-up pass.
 constexpr int HF_WAVES = 4;
-constexpr int HF_XS = FU_D + 1;                      // row stride (floats): lanes hit distinct banks
-constexpr size_t HF_LDS = (size_t)FU_D * 32 * 4 + (size_t)HF_WAVES * 64 * HF_XS * 4;
+constexpr int HF_SPLIT = 4;                           // blocks per list segment
+constexpr size_t HF_LDS = (size_t)FU_D * 32 * 4;      // the projections, f32 (exact)
 
-__device__ int32_t fixup_hash(const float* xs, const float* pts, int LKpad, int f, double tt, double ww, double pn,
-                              float w, unsigned long long* stats) {
+// fp64 projection of one row, streamed in 32-dim chunks (re-reads for a second
+// function hit L1), with the rigorous bound of hash.hip; soft-x87 fallback.
+__device__ int32_t fixup_hash(const float* xrow, const float* pts, int LKpad, int f,
+                              double tt, double ww, double pn, float w, unsigned long long* stats) {
     double acc = 0.0, xn2 = 0.0;
-#pragma unroll 8
-    for (int j = 0; j < FU_D; j++) {
-        const double xj = (double)xs[j];
-        xn2 = fma(xj, xj, xn2);
-        acc = fma((double)pts[j * LKpad + f], xj, acc);
+#pragma unroll 1
+    for (int c = 0; c < FU_D; c += 32) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const float4*>(xrow + c + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const float xs[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int j = c + 4 * u + e;
+                const double xj = (double)xs[e];
+                xn2 = fma(xj, xj, xn2);
+                acc = fma((double)pts[j * LKpad + f], xj, acc);
+            }
+        }
     }
     const double P = pn * sqrt(xn2) * (1.0 + 0x1p-40);
     const double y = (acc + tt) / ww;
@@ -823,68 +831,48 @@ __device__ int32_t fixup_hash(const float* xs, const float* pts, int LKpad, int 
     const double lo = floor(y - B), hi = floor(y + B);
     if (lo == hi) return (int32_t)lo;
     sx80 s = sx_zero();
-    for (int j = 0; j < FU_D; j++) s = sx_add_double(s, __dmul_rn((double)pts[j * LKpad + f], (double)xs[j]));
+    for (int j = 0; j < FU_D; j++) s = sx_add_double(s, __dmul_rn((double)pts[j * LKpad + f], (double)xrow[j]));
     s = sx_add_double(s, tt);
     atomicAdd(stats + STAT_HASH_EXACT, 1ull);
     return (int32_t)sx_floor_i64(sx_div(s, sx_from_float(w)));
 }
 
+// Lane = listed row (~4% of rows at w = 0.4, mostly one function each): the row
+// is loaded into registers, the flagged functions are recomputed (the set-bit
+// loop runs the wave's max popcount, not the union), and phi / bucket of each
+// touched table are rebuilt from tuples (the other values there are certified).
 __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* pts = reinterpret_cast<float*>(smem);     // [128][LKpad] projections (float values: exact)
-    // block b takes the list segment persistent block b wrote
-    const int n = a.seg_counts[2 * blockIdx.x + 1];
-    const unsigned long long* seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float* xs = reinterpret_cast<float*>(smem + FU_D * 32 * 4) + wave * 64 * HF_XS;
+    float* pts = reinterpret_cast<float*>(smem);     // [128][LKpad]
+    const int seg = blockIdx.x / HF_SPLIT, part = blockIdx.x % HF_SPLIT;
+    const int n = a.seg_counts[2 * seg + 1];
     if (n == 0) return;                                                 // block-uniform
+    const unsigned long long* list = a.hfix + (int64_t)seg * a.seg_rows;
     const int LKpad = a.LKpad;
     for (int e = threadIdx.x; e < FU_D * LKpad; e += 64 * HF_WAVES) pts[e] = (float)a.PT[e];
     __syncthreads();
     const double ww = (double)a.w;
-    for (int base = wave * 64; base < n; base += HF_WAVES * 64) {
-        const int cnt = min(64, n - base);
-        const unsigned long long ent = lane < cnt ? seg[base + lane] : 0ull;
-        // stage: two rows per instruction (32 lanes x 16 B each), all loads in flight
-        const int half = lane >> 5, q = lane & 31;
-        float4 v[32];
-#pragma unroll
-        for (int i = 0; i < 32; i++) {
-            const int r = 2 * i + half;
-            const int64_t rr = (int64_t)(__shfl((long long)ent, min(r, cnt - 1)) >> 32);
-            v[i] = *reinterpret_cast<const float4*>(a.X + rr * FU_D + 4 * q);
+    const uint32_t kmask = a.k >= 32 ? 0xFFFFFFFFu : ((1u << a.k) - 1u);
+    for (int e = part * 64 * HF_WAVES + threadIdx.x; e < n; e += HF_SPLIT * 64 * HF_WAVES) {
+        const unsigned long long ent = list[e];
+        const int64_t row = (int64_t)(ent >> 32);
+        const uint32_t mask = (uint32_t)ent;
+        const float* xrow = a.X + row * FU_D;
+        for (uint32_t m = mask; m; m &= m - 1) {
+            const int f = __builtin_ctz(m);
+            a.tuples[row * a.LK + f] = fixup_hash(xrow, pts, LKpad, f, (double)a.tv[f], ww, a.pnorm[f], a.w, a.stats);
         }
-#pragma unroll
-        for (int i = 0; i < 32; i++) {
-            float* d = xs + (2 * i + half) * HF_XS + 4 * q;
-            d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
-        }
-        wave_sync();
-        if (lane < cnt) {
-            const int64_t row = (int64_t)(ent >> 32);
-            const uint32_t mask = (uint32_t)ent;
-            const float* x = xs + lane * HF_XS;
-            const uint32_t kmask = a.k >= 32 ? 0xFFFFFFFFu : ((1u << a.k) - 1u);
-            // Recompute the flagged functions only (the set-bit loop runs the
-            // wave's max popcount, not the union); the table's other values are
-            // the certified ones already in tuples (always present on this path).
-            for (uint32_t m = mask; m; m &= m - 1) {
-                const int f = __builtin_ctz(m);
-                a.tuples[row * a.LK + f] = fixup_hash(x, pts, LKpad, f, (double)a.tv[f], ww, a.pnorm[f], a.w, a.stats);
+        for (int l = 0; l < a.L; l++) {
+            if (!(mask & (kmask << (l * a.k)))) continue;
+            uint32_t hn = 0;
+            for (int i = 0; i < a.k; i++) {
+                const int f = l * a.k + i;
+                hn += phi_term(a.tuples[row * a.LK + f], a.rv[f]);
             }
-            for (int l = 0; l < a.L; l++) {
-                if (!(mask & (kmask << (l * a.k)))) continue;
-                uint32_t hn = 0;
-                for (int i = 0; i < a.k; i++) {
-                    const int f = l * a.k + i;
-                    hn += phi_term(a.tuples[row * a.LK + f], a.rv[f]);
-                }
-                const uint32_t ph = phi_final(hn);
-                if (a.phi) a.phi[row * a.L + l] = (int32_t)ph;
-                if (a.bucket) a.bucket[row * a.L + l] = bucket_of(ph, a.nb);
-            }
+            const uint32_t ph = phi_final(hn);
+            if (a.phi) a.phi[row * a.L + l] = (int32_t)ph;
+            if (a.bucket) a.bucket[row * a.L + l] = bucket_of(ph, a.nb);
         }
-        wave_sync();
     }
 }
 
@@ -996,7 +984,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             return -1;
         }
         hipLaunchKernelGGL(fused_persistent_kernel<true>, grid, block, lds, s, a);
-        hipLaunchKernelGGL(hash_fixup_kernel, grid, dim3(64 * HF_WAVES), HF_LDS, s, a);
+        hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
         return kstatus("fused_persistent_kernel");
     }
     const dim3 grid((unsigned)((f.N + FU_PB - 1) / FU_PB)), block(FU_THREADS);
