@@ -148,8 +148,9 @@ def main():
     ambig = ctx.stat(lk.STAT_ASSIGN_AMBIG)
     hexact = ctx.stat(lk.STAT_HASH_EXACT)
 
-    # Dominant kernel (fused_kernel<true>): HIP events recorded by the library
-    # around that launch, on the stream it runs on; averaged over reps steps.
+    # Dominant kernel = the fused pass (fused_persistent_kernel<true> and its
+    # hash_fixup_kernel): HIP events recorded by the library around those
+    # launches, on the stream they run on; averaged over reps steps.
     reps = max(3, args.steps)
     lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 1))
     ms = C.c_float()
@@ -195,7 +196,8 @@ def main():
                        "N_per_gpu": N, "N_total": N_total, "d": D, "K": K, "L": L_TABLES, "k": K_FUNCS,
                        "w": W, "nb": nb, "parallelism": f"dp{world} (row shards)"},
             "roofline": {
-                "bound": "hbm", "kernel": "fused_kernel<true> (hash + assign, one read of X)",
+                "bound": "hbm",
+                "kernel": "fused pass = fused_persistent_kernel<true> + hash_fixup_kernel (hash + assign, one read of X)",
                 "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "bytes_per_point": bytes_per_pt, "kernel_ms": t_kernel * 1e3,
