@@ -170,6 +170,24 @@ int lshkm_params_cube_euclidean(uint64_t seed, int k, int d, float w, float* V, 
     return 0;
 }
 
+// EuclideanF coins on the host (sharded builds): per entry in order,
+// c = uniform_int_distribution<int>(1, 2) over the shared minstd_rand0
+// (euclidean_f_gen.hpp:68-76), bit = mod(h, c) (utils.hpp:97-98). libstdc++'s
+// own engine and distribution, resumed from the engine state value.
+int lshkm_coins_draw(uint32_t* rng_state, const int32_t* h, int64_t n, int32_t* bit) {
+    LSHKM_CHECK(rng_state && n >= 0 && (n == 0 || (h && bit)), LSHKM_ERR_ARG, "bad arguments");
+    std::default_random_engine g;
+    g.seed((unsigned long)*rng_state);
+    LSHKM_CHECK(engine_state(g) == *rng_state, LSHKM_ERR_ARG, "rng_state is not a minstd_rand0 state");
+    for (int64_t i = 0; i < n; i++) {
+        std::uniform_int_distribution<int> coin(1, 2);
+        const int c = coin(g);
+        bit[i] = (h[i] % c + c) % c;
+    }
+    *rng_state = engine_state(g);
+    return 0;
+}
+
 int lshkm_params_cube_cosine(uint64_t seed, int k, int d, double* R, uint32_t* state) {
     LSHKM_CHECK(k > 0 && d > 0 && R, LSHKM_ERR_ARG, "bad arguments");
     std::default_random_engine g;

@@ -186,29 +186,13 @@ int lshkm_cube_destroy(lshkm_cube cube) {
     return 0;
 }
 
-// Vertices of N rows, drawing the F coins of unseen h values in (row, f) order.
-static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_t* vertex) {
+// Dense coin-memo window: grow (re-home) it so that [lo, hi] is covered.
+static int cube_ensure_window(lshkm_cube cube, int32_t lo_h, int32_t hi_h) {
     lshkm_ctx ctx = cube->ctx;
     hipStream_t s = ctx->stream;
     const int k = cube->k;
     int rc;
-    if (N == 0) return 0;
-    if (cube->metric == LSHKM_METRIC_COSINE) {
-        if ((rc = launch_proj_hash(s, HM_CUBE_COSINE, X, N, cube->proj.params(1ll << k), vertex, nullptr, nullptr,
-                                   (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        return 0;
-    }
-    LSHKM_CHECK(N * k < (1ll << 31), LSHKM_ERR_UNSUPPORTED, "rows * k must be < 2^31");
-    if ((rc = reserve(ctx, WS_H, (size_t)N * k * 4))) return rc;
-    int32_t* h = slot<int32_t>(ctx, WS_H);
-    if ((rc = launch_proj_hash(s, HM_CUBE_EUCLID_H, X, N, cube->proj.params(1ll << k), h, nullptr, nullptr,
-                               (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
-    // window of the dense memo: grow (re-home) when the batch's h range leaves it
-    const int32_t init_mm[2] = {0x7FFFFFFF, (int32_t)0x80000000};
-    LSHKM_HIP(hipMemcpyAsync(cube->mm.p, init_mm, 8, hipMemcpyHostToDevice, s));
-    if ((rc = launch_h_minmax(s, h, N * k, cube->mm.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
-    int32_t mm[2];
-    if ((rc = d2h(ctx, mm, cube->mm.p, 8))) return rc;
+    const int32_t mm[2] = {lo_h, hi_h};
     if (cube->hspan == 0 || mm[0] < cube->hmin || mm[1] >= cube->hmin + cube->hspan) {
         const int64_t lo = cube->hspan ? std::min<int64_t>(cube->hmin, mm[0]) : mm[0];
         const int64_t hi = cube->hspan ? std::max<int64_t>((int64_t)cube->hmin + cube->hspan - 1, mm[1]) : mm[1];
@@ -225,8 +209,38 @@ static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_
         if ((rc = cube->first_row.reserve((size_t)k * nspan * 4))) return rc;
         LSHKM_HIP(hipMemsetAsync(cube->first_row.p, 0x7F, (size_t)k * nspan * 4, s));   // 0x7F7F7F7F > any row
     }
+    return 0;
+}
+
+// h of a batch (EuclideanH, k per row) into WS_H, and the memo window over it.
+static int cube_h_batch(lshkm_cube cube, const float* X, int64_t N, int32_t** h_out) {
+    lshkm_ctx ctx = cube->ctx;
+    hipStream_t s = ctx->stream;
+    const int k = cube->k;
+    int rc;
+    LSHKM_CHECK(N * k < (1ll << 31), LSHKM_ERR_UNSUPPORTED, "rows * k must be < 2^31");
+    if ((rc = reserve(ctx, WS_H, (size_t)N * k * 4))) return rc;
+    int32_t* h = slot<int32_t>(ctx, WS_H);
+    if ((rc = launch_proj_hash(s, HM_CUBE_EUCLID_H, X, N, cube->proj.params(1ll << k), h, nullptr, nullptr,
+                               (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    const int32_t init_mm[2] = {0x7FFFFFFF, (int32_t)0x80000000};
+    LSHKM_HIP(hipMemcpyAsync(cube->mm.p, init_mm, 8, hipMemcpyHostToDevice, s));
+    if ((rc = launch_h_minmax(s, h, N * k, cube->mm.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    int32_t mm[2];
+    if ((rc = d2h(ctx, mm, cube->mm.p, 8))) return rc;
+    if ((rc = cube_ensure_window(cube, mm[0], mm[1]))) return rc;
+    *h_out = h;
+    return 0;
+}
+
+// First occurrence of every (f, h) of the batch that has no coin yet, as
+// (key = row * k + f, memo offset) pairs in WS_SIZES / WS_COFF; count in *n.
+static int cube_unseen_impl(lshkm_cube cube, const int32_t* h, int64_t N, unsigned int* n) {
+    lshkm_ctx ctx = cube->ctx;
+    hipStream_t s = ctx->stream;
+    const int k = cube->k;
+    int rc;
     const int64_t total = (int64_t)k * cube->hspan;
-    // first occurrence of each unseen (f, h), then the sorted draw
     LSHKM_HIP(hipMemsetAsync(cube->first_row.p, 0x7F, (size_t)total * 4, s));
     if ((rc = launch_coin_first(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), cube->first_row.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     LSHKM_HIP(hipMemsetAsync(cube->cnt.p, 0, 4, s));
@@ -235,9 +249,26 @@ static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_
         (rc = reserve(ctx, WS_KLIST, (size_t)maxe * 4)) || (rc = reserve(ctx, WS_KCNT, (size_t)maxe * 4)))
         return rc;
     if ((rc = launch_coin_collect(s, cube->first_row.as<int32_t>(), total, k, cube->hspan, slot<int32_t>(ctx, WS_SIZES),
-                                        slot<int32_t>(ctx, WS_COFF), cube->cnt.as<unsigned int>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                                  slot<int32_t>(ctx, WS_COFF), cube->cnt.as<unsigned int>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return d2h(ctx, n, cube->cnt.p, 4);
+}
+
+static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_t* vertex) {
+    lshkm_ctx ctx = cube->ctx;
+    hipStream_t s = ctx->stream;
+    const int k = cube->k;
+    int rc;
+    if (N == 0) return 0;
+    if (cube->metric == LSHKM_METRIC_COSINE) {
+        if ((rc = launch_proj_hash(s, HM_CUBE_COSINE, X, N, cube->proj.params(1ll << k), vertex, nullptr, nullptr,
+                                   (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        return 0;
+    }
+    int32_t* h = nullptr;
+    if ((rc = cube_h_batch(cube, X, N, &h))) return rc;
+    // first occurrence of each unseen (f, h), then the draw in (row, f) order
     unsigned int ncoins = 0;
-    if ((rc = d2h(ctx, &ncoins, cube->cnt.p, 4))) return rc;
+    if ((rc = cube_unseen_impl(cube, h, N, &ncoins))) return rc;
     if (ncoins > 0) {
         if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(ncoins, N * k)))) return rc;
         if ((rc = stable_sort_by_key(s, slot<int32_t>(ctx, WS_SIZES), 1, slot<int32_t>(ctx, WS_COFF), ncoins, N * k,
@@ -246,6 +277,68 @@ static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_
                                    cube->memo.as<int32_t>(), cube->rng_d.as<uint32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     }
     if ((rc = launch_coin_vertex(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), vertex))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    return 0;
+}
+
+// ---- sharded EuclideanF coins: export, host draw, import
+int lshkm_cube_unseen(lshkm_cube cube, const float* X, int64_t N, int32_t* f_host, int32_t* h_host,
+                      int64_t* row_host, int64_t cap, int64_t* count_host) {
+    LSHKM_CHECK(cube && (X || N == 0) && N >= 0 && N < (1ll << 31) && count_host && (cap == 0 || (f_host && h_host && row_host)),
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(cube->metric == LSHKM_METRIC_EUCLIDEAN, LSHKM_ERR_ARG, "coins exist only for the euclidean cube");
+    lshkm_ctx ctx = cube->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    *count_host = 0;
+    if (N == 0) return 0;
+    int rc;
+    int32_t* h = nullptr;
+    if ((rc = cube_h_batch(cube, X, N, &h))) return rc;
+    unsigned int n = 0;
+    if ((rc = cube_unseen_impl(cube, h, N, &n))) return rc;
+    *count_host = n;
+    if (n == 0 || (int64_t)n > cap) return 0;
+    std::vector<int32_t> keys(n), offs(n);
+    if ((rc = d2h(ctx, keys.data(), ctx->ws[WS_SIZES].p, (size_t)n * 4)) || (rc = d2h(ctx, offs.data(), ctx->ws[WS_COFF].p, (size_t)n * 4)))
+        return rc;
+    for (unsigned int i = 0; i < n; i++) {
+        f_host[i] = keys[i] % cube->k;
+        row_host[i] = keys[i] / cube->k;
+        h_host[i] = cube->hmin + offs[i] % cube->hspan;
+    }
+    return 0;
+}
+
+int lshkm_cube_import_coins(lshkm_cube cube, const int32_t* f_host, const int32_t* h_host, const int32_t* bit_host,
+                            int64_t n, uint32_t rng_state) {
+    LSHKM_CHECK(cube && n >= 0 && (n == 0 || (f_host && h_host && bit_host)), LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(cube->metric == LSHKM_METRIC_EUCLIDEAN, LSHKM_ERR_ARG, "coins exist only for the euclidean cube");
+    lshkm_ctx ctx = cube->ctx;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc;
+    if (n > 0) {
+        int32_t lo = h_host[0], hi = h_host[0];
+        for (int64_t i = 0; i < n; i++) {
+            LSHKM_CHECK(f_host[i] >= 0 && f_host[i] < cube->k && (bit_host[i] == 0 || bit_host[i] == 1), LSHKM_ERR_ARG,
+                        "bad coin entry");
+            lo = std::min(lo, h_host[i]);
+            hi = std::max(hi, h_host[i]);
+        }
+        if ((rc = cube_ensure_window(cube, lo, hi))) return rc;
+        // memo is device-resident: patch it through a host image of the entries
+        std::vector<int32_t> off(n), bit(n);
+        for (int64_t i = 0; i < n; i++) {
+            off[i] = f_host[i] * cube->hspan + (h_host[i] - cube->hmin);
+            bit[i] = bit_host[i];
+        }
+        if ((rc = reserve(ctx, WS_KLIST, (size_t)n * 4)) || (rc = reserve(ctx, WS_KCNT, (size_t)n * 4))) return rc;
+        LSHKM_HIP(hipMemcpyAsync(ctx->ws[WS_KLIST].p, off.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+        LSHKM_HIP(hipMemcpyAsync(ctx->ws[WS_KCNT].p, bit.data(), (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+        if ((rc = launch_memo_scatter(ctx->stream, slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT), n,
+                                      cube->memo.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        LSHKM_HIP(hipStreamSynchronize(ctx->stream));      // the host images go out of scope
+    }
+    LSHKM_HIP(hipMemcpyAsync(cube->rng_d.p, &rng_state, 4, hipMemcpyHostToDevice, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     return 0;
 }
 
@@ -340,12 +433,13 @@ int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f, int32_t* h, int32_t* bit, i
 
 // ------------------------------------------------------------------- k-means
 static int km_sums(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K, double* sums,
-                   int64_t* counts) {
+                   int64_t* counts, const double* carry = nullptr, const int64_t* carry_counts = nullptr) {
     int rc;
     if ((rc = reserve(ctx, WS_ROWS, (size_t)std::max<int64_t>(N, 1) * 4)) || (rc = reserve(ctx, WS_CROW, (size_t)(K + 1) * 8)))
         return rc;
     if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
-    if ((rc = launch_km_chain(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, sums, counts))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if ((rc = launch_km_chain(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, sums, counts,
+                              carry, carry_counts))) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;
 }
 
@@ -379,6 +473,16 @@ int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X, int64_t N, int d, const 
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_HIP(hipSetDevice(ctx->device));
     return km_sums(ctx, X, N, d, assign, K, sums, counts);
+}
+
+int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K,
+                               const double* carry_sums, const int64_t* carry_counts, double* sums, int64_t* counts) {
+    LSHKM_CHECK(ctx && (X || N == 0) && (assign || N == 0) && sums && counts && N >= 0 && N < (1ll << 31) && d > 0 &&
+                    K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(sums != carry_sums, LSHKM_ERR_ARG, "sums must not alias carry_sums");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    return km_sums(ctx, X, N, d, assign, K, sums, counts, carry_sums, carry_counts);
 }
 
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums, const int64_t* counts, int K, int d, const double* C_old,

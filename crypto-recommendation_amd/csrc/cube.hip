@@ -127,6 +127,20 @@ int launch_coin_vertex(hipStream_t s, const int32_t* h, int64_t N, int k, int32_
     return kstatus("cube.hip");
 }
 
+// Imported coins (sharded builds): memo[off[i]] = bit[i].
+__global__ void memo_scatter_kernel(const int32_t* __restrict__ off, const int32_t* __restrict__ bit, int64_t n,
+                                    int32_t* __restrict__ memo) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        memo[off[i]] = bit[i];
+}
+
+int launch_memo_scatter(hipStream_t s, const int32_t* off, const int32_t* bit, int64_t n, int32_t* memo) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(memo_scatter_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s,
+                       off, bit, n, memo);
+    return kstatus("cube.hip");
+}
+
 // Re-center a memo window: copy memo[f][h - old_min] into a wider window.
 __global__ void memo_rehome_kernel(const int32_t* __restrict__ old_memo, int32_t old_min, int32_t old_span,
                                    int32_t* __restrict__ new_memo, int32_t new_min, int32_t new_span, int k) {

@@ -56,9 +56,10 @@ constexpr int FU_LDS_BYTES = FU_HS_OFF + FU_PB * 32 * 4; // 80 KiB -> 2 blocks /
 static_assert(FU_CHUNK_BYTES <= FU_XSTAGE_BYTES, "chunk region must fit in the staging alias");
 
 constexpr double FU_A1 = 1.25 * 0x1p-16;
-// Hash tile of the persistent form: hi products summed per 32-dim chunk in f32
-// (<= 31 roundings, 2^-18 sum|terms|), chunks in fp64; the split residuals and
-// lo terms add < 0.25 * 2^-18 as in A1's derivation.
+// Hash tile of the persistent form: hi products of each 16-dim step in a fresh
+// accumulator (<= 15 roundings), steps added in f32 (+7), + lo (+1): 23 * 2^-23
+// = 0.72 * 2^-18 of sum|terms|; the split residuals and lo terms add < 0.25 *
+// 2^-18 as in A1's derivation.
 constexpr double FU_A1H = 1.25 * 0x1p-18;
 constexpr double FU_A2 = 0x1p-24;
 constexpr float FU_RANGE = 32768.f;
@@ -247,8 +248,12 @@ __device__ inline void tile_mfma(const _Float16* ah_row, const _Float16* al_row,
         const half8 ah = *reinterpret_cast<const half8*>(ah_row + 16 * s);
         const half8 al = *reinterpret_cast<const half8*>(al_row + 16 * s);
         acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc_hi, 0, 0, 0);
+#ifndef ABL_NOLO   // timing experiments only: results are wrong without the lo products
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc_lo, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc_lo, 0, 0, 0);
+#else
+        (void)al;
+#endif
     }
 }
 
@@ -442,6 +447,49 @@ __global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
 #define FP_KEEP_X 1
 #endif
 constexpr int FP_WAVES = FP_KEEP_X ? 8 : 12;   // 2 / 3 per SIMD: <= 256 / 168 VGPRs
+#ifndef TILE_UNROLL
+#define TILE_UNROLL 1
+#endif
+#ifndef PIPE_TILES
+#define PIPE_TILES 0
+#endif
+
+// Scores of one 32-centroid tile: t = (hi + lo) + (-|c|^2/2) on packed f32
+// (D rows of registers 4g..4g+3 are centroids 8g+4h..+3 of the tile).
+__device__ inline void tile_scores(const floatx16& acc_hi, const floatx16& acc_lo, const float* cn_tile_h,
+                                   float (&sv)[16]) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const float4 cn = *reinterpret_cast<const float4*>(cn_tile_h + 8 * g);
+        const float2v h01 = {acc_hi[4 * g], acc_hi[4 * g + 1]}, l01 = {acc_lo[4 * g], acc_lo[4 * g + 1]};
+        const float2v h23 = {acc_hi[4 * g + 2], acc_hi[4 * g + 3]}, l23 = {acc_lo[4 * g + 2], acc_lo[4 * g + 3]};
+        const float2v c01 = {cn.x, cn.y}, c23 = {cn.z, cn.w};
+        const float2v s01 = (h01 + l01) + c01, s23 = (h23 + l23) + c23;
+        sv[4 * g] = s01.x; sv[4 * g + 1] = s01.y; sv[4 * g + 2] = s23.x; sv[4 * g + 3] = s23.y;
+    }
+}
+
+// Running best / runner-up over one tile's scores. Each score carries its
+// in-tile index (4g+q) in its low 4 mantissa bits (see E), so the best needs
+// no compare/select per score.
+__device__ inline void tile_epilogue(const float (&sv)[16], float& m1, float& m2) {
+    // two independent (best, runner-up) chains over the even / odd scores, merged
+    // at the end; max(a, b) as med3(a, b, FLT_MAX): fmaxf would first re-quiet
+    // its operand (IEEE mode), and scores are finite for any certifiable point
+    float a1 = m1, a2 = m2, b1 = -__builtin_inff(), b2 = -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+        const float ta = __uint_as_float((__float_as_uint(sv[r]) & ~0xFu) | (uint32_t)r);
+        const float tb = __uint_as_float((__float_as_uint(sv[r + 1]) & ~0xFu) | (uint32_t)(r + 1));
+        a2 = __builtin_amdgcn_fmed3f(a2, a1, ta);      // = max(a2, min(a1, ta)) as a2 <= a1
+        a1 = __builtin_amdgcn_fmed3f(a1, ta, 0x1.fffffep127f);
+        b2 = __builtin_amdgcn_fmed3f(b2, b1, tb);
+        b1 = __builtin_amdgcn_fmed3f(b1, tb, 0x1.fffffep127f);
+    }
+    // merged runner-up = max(a2, b2, min(a1, b1)); best = max(a1, b1)
+    m2 = __builtin_amdgcn_fmed3f(__builtin_amdgcn_fmed3f(a2, b2, 0x1.fffffep127f), __builtin_amdgcn_fmed3f(a1, b1, -0x1.fffffep127f), 0x1.fffffep127f);
+    m1 = __builtin_amdgcn_fmed3f(a1, b1, 0x1.fffffep127f);
+}
 constexpr int FP_THREADS = 64 * FP_WAVES;
 constexpr int FP_KMAX = 256;
 constexpr int FP_HC_BYTES = 32 * (4 + 4 + 4 + 4);     // hash constants |v|_2, |v|_1, t, r
@@ -504,6 +552,13 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     const int ntile32 = Kpad >> 5;
     const int64_t ntiles = (a.N + 31) >> 5;
 
+#if WAVE_OFFSET
+    // Waves w and w+4 share a SIMD; starting the second half of the block late
+    // keeps the two out of phase (one in its MFMA-heavy loop while the other
+    // runs VALU-heavy epilogues) instead of lockstep.
+    if (wave >= FP_WAVES / 2)
+        for (int i = 0; i < WAVE_OFFSET; i++) __builtin_amdgcn_s_sleep(127);
+#endif
     PT_DECL
     for (int64_t tile = (int64_t)blockIdx.x * FP_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FP_WAVES) {
         const int64_t row = tile * 32 + col;
@@ -652,30 +707,47 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                             (1.f + 0x1p-20f) + 1e-30f;
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
         int t1 = 0;
+#if PIPE_TILES
+        // Software pipeline: tile t's scores are formed (16 VGPRs), then tile
+        // t+1's 24 MFMAs issue with tile t's epilogue placed in their gaps
+        // (2 VALU per MFMA, well inside the 24 free cycles of each 32-cycle MFMA).
+        floatx16 acc_hi, acc_lo;
+        tile_mfma(my_h, my_l, bh, bl, acc_hi, acc_lo);
 #pragma unroll 1
+        for (int t = 0; t < ntile32; t++) {
+            float sv[16];
+            tile_scores(acc_hi, acc_lo, lcn + t * 32 + 4 * h, sv);
+            const float m1_prev = m1;
+            if (t + 1 < ntile32) {
+                tile_mfma(my_h + (t + 1) * 32 * FU_RS, my_l + (t + 1) * 32 * FU_RS, bh, bl, acc_hi, acc_lo);
+                tile_epilogue(sv, m1, m2);
+#pragma unroll
+                for (int s = 0; s < 8; s++) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read: A operands
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU: epilogue
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                }
+            } else {
+                tile_epilogue(sv, m1, m2);
+            }
+            t1 = m1 != m1_prev ? t : t1;
+        }
+#else
+#pragma unroll TILE_UNROLL
         for (int t = 0; t < ntile32; t++) {
             floatx16 acc_hi, acc_lo;
             tile_mfma(my_h + t * 32 * FU_RS, my_l + t * 32 * FU_RS, bh, bl, acc_hi, acc_lo);
             const float m1_prev = m1;
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const float4 cn = *reinterpret_cast<const float4*>(lcn + t * 32 + 8 * g + 4 * h);
-                const float2v h01 = {acc_hi[4 * g], acc_hi[4 * g + 1]}, l01 = {acc_lo[4 * g], acc_lo[4 * g + 1]};
-                const float2v h23 = {acc_hi[4 * g + 2], acc_hi[4 * g + 3]}, l23 = {acc_lo[4 * g + 2], acc_lo[4 * g + 3]};
-                const float2v c01 = {cn.x, cn.y}, c23 = {cn.z, cn.w};
-                const float2v s01 = (h01 + l01) + c01, s23 = (h23 + l23) + c23;
-                const float sv[4] = {s01.x, s01.y, s23.x, s23.y};
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const float tvp = __uint_as_float((__float_as_uint(sv[q]) & ~0xFu) | (uint32_t)(4 * g + q));
-                    m2 = __builtin_amdgcn_fmed3f(m2, m1, tvp);     // = max(m2, min(m1, tvp)) as m2 <= m1
-                    // plain v_max_f32: fmaxf would first re-quiet tvp (IEEE mode), and
-                    // tvp is never a NaN for a point that can be certified
-                    asm("v_max_f32 %0, %1, %2" : "=v"(m1) : "v"(m1), "v"(tvp));
-                }
-            }
+            float sv[16];
+            tile_scores(acc_hi, acc_lo, lcn + t * 32 + 4 * h, sv);
+            tile_epilogue(sv, m1, m2);
             t1 = m1 != m1_prev ? t : t1;
         }
+#endif
         const uint32_t l1 = __float_as_uint(m1) & 0xFu;
         const int i1 = t1 * 32 + 8 * (int)(l1 >> 2) + 4 * h + (int)(l1 & 3u);
         const float om1 = __shfl_xor(m1, 32), om2 = __shfl_xor(m2, 32);

@@ -85,10 +85,14 @@ int launch_coin_vertex(hipStream_t s, const int32_t* h, int64_t N, int k, int32_
                        const int32_t* memo, int32_t* vertex);
 int launch_memo_rehome(hipStream_t s, const int32_t* old_memo, int32_t old_min, int32_t old_span, int32_t* new_memo,
                        int32_t new_min, int32_t new_span, int k);
+int launch_memo_scatter(hipStream_t s, const int32_t* off, const int32_t* bit, int64_t n, int32_t* memo);
 
 // k-means update (update.hip).
+// carry / carry_counts (may be NULL): the running sums and counts the chain
+// continues from (exact-order sharded mode).
 int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K,
-                    double* sums, int64_t* counts);
+                    double* sums, int64_t* counts, const double* carry = nullptr,
+                    const int64_t* carry_counts = nullptr);
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
 

@@ -21,14 +21,16 @@ constexpr int KM_U = 16;
 
 __global__ __launch_bounds__(64) void km_chain_kernel(const float* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                      const int64_t* __restrict__ crow, int K,
+                                                     const double* __restrict__ carry, const int64_t* __restrict__ carry_counts,
                                                      double* __restrict__ sums, int64_t* __restrict__ counts) {
     const int c = blockIdx.x;
     const int j = blockIdx.y * 64 + threadIdx.x;
     const int64_t beg = crow[c], end = crow[c + 1];
-    if (blockIdx.y == 0 && threadIdx.x == 0 && counts) counts[c] = end - beg;
+    if (blockIdx.y == 0 && threadIdx.x == 0 && counts) counts[c] = end - beg + (carry_counts ? carry_counts[c] : 0);
     if (j >= d) return;
     const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
-    double s = 0.0;
+    // exact mode across shards: the chain continues from the previous shard's running sum
+    double s = carry ? carry[(size_t)c * d + j] : 0.0;
     int64_t p = beg;
     for (; p + KM_U <= end; p += KM_U) {
         float v[KM_U];
@@ -42,9 +44,9 @@ __global__ __launch_bounds__(64) void km_chain_kernel(const float* __restrict__ 
 }
 
 int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K,
-                    double* sums, int64_t* counts) {
+                    double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts) {
     hipLaunchKernelGGL(km_chain_kernel, dim3((unsigned)K, (unsigned)((d + 63) / 64)), dim3(64), 0, s, X, d, rows, crow, K,
-                       sums, counts);
+                       carry, carry_counts, sums, counts);
     return kstatus("update.hip");
 }
 

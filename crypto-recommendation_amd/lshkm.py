@@ -73,10 +73,14 @@ def lib():
             "lshkm_cube_get_buckets": (i32, [vp, vp, vp]),
             "lshkm_cube_query": (i32, [vp, vp, i64, i32, vp, vp, i64, C.POINTER(i64)]),
             "lshkm_cube_get_memo": (i32, [vp, vp, vp, vp, i64, C.POINTER(i64), C.POINTER(C.c_uint32)]),
+            "lshkm_cube_unseen": (i32, [vp, vp, i64, vp, vp, vp, i64, C.POINTER(i64)]),
+            "lshkm_cube_import_coins": (i32, [vp, vp, vp, vp, i64, C.c_uint32]),
+            "lshkm_coins_draw": (i32, [C.POINTER(C.c_uint32), vp, i64, vp]),
             "lshkm_lloyd_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp]),
             "lshkm_hash_assign": (i32, [vp, vp, i64, vp, i32, vp, vp, vp, vp, vp, vp]),
             "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
+            "lshkm_kmeans_partial_carry": (i32, [vp, vp, i64, i32, vp, i32, vp, vp, vp, vp]),
             "lshkm_kmeans_finalize": (i32, [vp, vp, vp, i32, i32, vp, i32, f64, vp, C.POINTER(i32)]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
         }
@@ -280,6 +284,20 @@ class Cube:
         _ck(lib().lshkm_cube_get_memo(self.h, _np_ptr(f), _np_ptr(hh), _np_ptr(b), n, C.byref(cnt), C.byref(st)))
         return f[:n], hh[:n], b[:n], st.value
 
+    def unseen(self, X):
+        """(f, h, first local row) of the (f, h) pairs in X without a coin yet (lshkm_cube_unseen)."""
+        cnt = C.c_int64()
+        _ck(lib().lshkm_cube_unseen(self.h, _t_ptr(X), X.shape[0], None, None, None, 0, C.byref(cnt)))
+        n = cnt.value
+        f = np.empty(max(n, 1), np.int32); hh = np.empty(max(n, 1), np.int32); r = np.empty(max(n, 1), np.int64)
+        _ck(lib().lshkm_cube_unseen(self.h, _t_ptr(X), X.shape[0], _np_ptr(f), _np_ptr(hh), _np_ptr(r), n,
+                                    C.byref(cnt)))
+        return f[:n], hh[:n], r[:n]
+
+    def import_coins(self, f, h, bits, rng_state):
+        f, h, bits = (np.ascontiguousarray(a, np.int32) for a in (f, h, bits))
+        _ck(lib().lshkm_cube_import_coins(self.h, _np_ptr(f), _np_ptr(h), _np_ptr(bits), len(f), rng_state))
+
     def query(self, Q, probes):
         torch = self.ctx.torch
         nq = Q.shape[0]
@@ -291,6 +309,15 @@ class Cube:
                                    C.byref(total)))
         self.ctx.sync()
         return ptr.cpu().numpy(), out[:total.value].cpu().numpy()
+
+
+def coins_draw(rng_state, h):
+    """Host EuclideanF coins in order (lshkm_coins_draw): returns (bits, new state)."""
+    h = np.ascontiguousarray(h, np.int32)
+    bits = np.empty(max(len(h), 1), np.int32)
+    st = C.c_uint32(rng_state)
+    _ck(lib().lshkm_coins_draw(C.byref(st), _np_ptr(h), len(h), _np_ptr(bits)))
+    return bits[:len(h)], st.value
 
 
 # -------------------------------------------------------------------- k-means
@@ -341,6 +368,20 @@ def kmeans_partial(ctx, X, assign, K, sums=None, counts=None):
     sums = ctx.empty((K, d), torch.float64) if sums is None else sums
     counts = ctx.empty((K,), torch.int64) if counts is None else counts
     _ck(lib().lshkm_kmeans_partial(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K, _t_ptr(sums), _t_ptr(counts)))
+    return sums, counts
+
+
+def kmeans_partial_carry(ctx, X, assign, K, carry_sums=None, carry_counts=None):
+    """Exact-mode shard update: the chains continue from the previous shard's
+    (sums, counts) -- None for the first shard (lshkm_kmeans_partial_carry)."""
+    torch = ctx.torch
+    N, d = X.shape
+    sums = ctx.empty((K, d), torch.float64)
+    counts = ctx.empty((K,), torch.int64)
+    _ck(lib().lshkm_kmeans_partial_carry(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K,
+                                         _t_ptr(carry_sums) if carry_sums is not None else None,
+                                         _t_ptr(carry_counts) if carry_counts is not None else None,
+                                         _t_ptr(sums), _t_ptr(counts)))
     return sums, counts
 
 

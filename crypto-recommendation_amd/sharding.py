@@ -60,6 +60,77 @@ def merge_cube_results(parts, slots):
     return np.asarray(ptr, np.int64), idx
 
 
+def merge_unseen(parts, k):
+    """Global first-occurrence order of the EuclideanF coins.
+
+    parts: per shard, in shard order, (f, h, global_first_row) arrays. Each
+    (f, h) is kept at its smallest global key row * k + f -- the order in which
+    the reference's single pass over the rows (HypercubeGen::generate, f = 0..k-1
+    per row) first meets it -- and the entries come back sorted by that key."""
+    if not parts:
+        return (np.zeros(0, np.int32),) * 2
+    f = np.concatenate([np.asarray(p[0], np.int64) for p in parts])
+    h = np.concatenate([np.asarray(p[1], np.int64) for p in parts])
+    key = np.concatenate([np.asarray(p[2], np.int64) for p in parts]) * k + f
+    order = np.lexsort((key, h, f))                 # by (f, h), then key
+    f, h, key = f[order], h[order], key[order]
+    first = np.ones(len(f), bool)
+    first[1:] = (f[1:] != f[:-1]) | (h[1:] != h[:-1])
+    f, h, key = f[first], h[first], key[first]
+    by_key = np.argsort(key, kind="stable")
+    return f[by_key].astype(np.int32), h[by_key].astype(np.int32)
+
+
+def cube_build_sharded(lk, cube, X_local, row0):
+    """Build this rank's part of a euclidean hypercube with the coins the
+    reference would draw over all ranks' rows in order: export the unseen
+    (f, h), all-gather, merge in global first-occurrence order, draw on the
+    host (identically on every rank), import, build. One KB-sized exchange."""
+    import torch.distributed as dist
+    f, h, r = cube.unseen(X_local)
+    mine = (f, h, np.asarray(r, np.int64) + row0)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, mine)
+    else:
+        parts = [mine]
+    fs, hs = merge_unseen(parts, cube.k)
+    state = cube.memo()[3]
+    bits, state = lk.coins_draw(state, hs)
+    cube.import_coins(fs, hs, bits, state)
+    cube.build(X_local)
+
+
+def chain_partials(local_fn, sums_like, counts_like):
+    """Exact-order sharded k-means sums (SURVEY §8e "exact mode").
+
+    Rank r receives the running (sums, counts) of rows [0, row0_r) from rank
+    r-1, continues every per-(c, j) chain over its own rows in row order
+    (``local_fn(carry_sums, carry_counts) -> (sums, counts)``, e.g.
+    ``lshkm.kmeans_partial_carry``; the carry is None on rank 0), and hands the
+    result to rank r+1: the reference's single sequential sum (update.hpp:45-58)
+    bit for bit. The last rank broadcasts the totals. ``sums_like`` /
+    ``counts_like`` are receive buffers of the right shape, dtype and device.
+    Point-to-point hops of K*d*8 bytes (1 MiB at K=1024, d=128) over RCCL/xGMI."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return local_fn(None, None)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    carry_s = carry_c = None
+    if rank > 0:
+        carry_s, carry_c = sums_like, counts_like
+        dist.recv(carry_s, src=rank - 1)
+        dist.recv(carry_c, src=rank - 1)
+    sums, counts = local_fn(carry_s, carry_c)
+    if rank + 1 < world:
+        dist.send(sums, dst=rank + 1)
+        dist.send(counts, dst=rank + 1)
+        sums, counts = sums_like, counts_like
+    dist.broadcast(sums, src=world - 1)
+    dist.broadcast(counts, src=world - 1)
+    return sums, counts
+
+
 def allreduce_partials(sums, counts):
     """Sum the per-shard (sums, counts) over all ranks in place (RCCL on GPUs, gloo on CPU)."""
     import torch.distributed as dist

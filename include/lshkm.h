@@ -144,6 +144,22 @@ int lshkm_cube_get_buckets(lshkm_cube cube, int64_t* row_ptr_host /*[2^k+1]*/, i
  * lshkm_lsh_query. */
 int lshkm_cube_query(lshkm_cube cube, const float* Q_dev, int64_t nq, int probes,
                      int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap, int64_t* total_host);
+/* Sharded build of the euclidean cube (the coins of
+ * euclidean_f_gen.hpp:65-79 must be drawn in GLOBAL first-occurrence order):
+ * 1. each shard: lshkm_cube_unseen -> the (f, h) pairs of its rows that have
+ *    no coin yet, with their first local row (row_host; add the shard's row0);
+ *    if *count_host > cap nothing is copied and the call may be repeated;
+ * 2. all-gather, keep each (f, h) at its smallest global (row * k + f), sort by
+ *    it, and draw with lshkm_coins_draw (identical on every rank);
+ * 3. each shard: lshkm_cube_import_coins (memo + the engine state after the
+ *    draws), then lshkm_cube_build (no coin left to draw). */
+int lshkm_cube_unseen(lshkm_cube cube, const float* X_dev, int64_t N, int32_t* f_host, int32_t* h_host,
+                      int64_t* row_host, int64_t cap, int64_t* count_host);
+int lshkm_cube_import_coins(lshkm_cube cube, const int32_t* f_host, const int32_t* h_host, const int32_t* bit_host,
+                            int64_t n, uint32_t rng_state);
+/* Host draw of n coins in order from *rng_state (minstd_rand0 state, updated):
+ * bit[i] = mod(h[i], uniform_int_distribution<int>(1, 2)). No device needed. */
+int lshkm_coins_draw(uint32_t* rng_state, const int32_t* h_host, int64_t n, int32_t* bit_host);
 /* Coin memo export: f_host/h_host/bit_host [cap]; *count_host = entries. */
 int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f_host, int32_t* h_host, int32_t* bit_host,
                         int64_t cap, int64_t* count_host, uint32_t* rng_state_host);
@@ -176,6 +192,13 @@ int lshkm_kmeans_update(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, con
  * then lshkm_kmeans_finalize. */
 int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
                          int K, double* sums_dev, int64_t* counts_dev);
+/* Sharded update (exact mode): the per-(c, j) chains continue from
+ * carry_sums_dev / carry_counts_dev (the previous shard's result, or NULL for
+ * the first shard), so passing the carry shard to shard in row order gives the
+ * reference's single sequential sum (update.hpp:45-58) bit for bit. */
+int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
+                               int K, const double* carry_sums_dev, const int64_t* carry_counts_dev,
+                               double* sums_dev, int64_t* counts_dev);
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* counts_dev, int K, int d,
                           const double* C_old_dev, int metric, double min_dist, double* C_new_dev,
                           int* cont_host);

@@ -153,6 +153,46 @@ def test_cube_large_and_continued_coins_vs_oracle(ctx):
         assert np.array_equal(out[ptr[q]:ptr[q + 1]], exp), q
 
 
+def test_cube_sharded_build_matches_single(ctx):
+    # shards export unseen (f, h), merge in global first-occurrence
+    # order, draw on the host, import, build -> per-shard vertices, memo and
+    # engine state equal to one cube over all rows (3 shards, one empty).
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "sharding", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                 "crypto-recommendation_amd", "sharding.py"))
+    sharding = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sharding)
+    N, d, k, w = 200_000, 128, 14, 2.0
+    V, t, st = lshkm.params_cube_euclidean(31337, k, d, w)
+    X = ctx.synth(0x5EED, N, d)
+    whole = lshkm.Cube(ctx, "euclidean", d, k, w, V=V, t=t, rng_state=st)
+    whole.build(X)
+    vw = whole.vertices(X).cpu().numpy()
+    cuts = [0, 70_000, 70_000, N]
+    cubes = [lshkm.Cube(ctx, "euclidean", d, k, w, V=V, t=t, rng_state=st) for _ in cuts[1:]]
+    parts = []
+    for cb, lo, hi in zip(cubes, cuts, cuts[1:]):
+        f, h, r = cb.unseen(X[lo:hi])
+        parts.append((f, h, r + lo))
+    fs, hs = sharding.merge_unseen(parts, k)
+    bits, st2 = lshkm.coins_draw(st, hs)
+    wf, wh, wb, wst = whole.memo()
+    assert st2 == wst and len(fs) == len(wf)
+    for cb, lo, hi in zip(cubes, cuts, cuts[1:]):
+        cb.import_coins(fs, hs, bits, st2)
+        cb.build(X[lo:hi])
+        if hi > lo:
+            assert np.array_equal(cb.vertices(X[lo:hi]).cpu().numpy(), vw[lo:hi])
+        rp, idx = cb.buckets()
+        assert rp[-1] == hi - lo
+        f, h, b, s = cb.memo()
+        assert s == wst
+        o1, o2 = np.lexsort((h, f)), np.lexsort((wh, wf))
+        assert np.array_equal(f[o1], wf[o2]) and np.array_equal(h[o1], wh[o2]) and np.array_equal(b[o1], wb[o2])
+
+
 @pytest.mark.parametrize("name", cases("lloyd"))
 def test_kmeans_update_golden(ctx, name):
     m, g = META[name], golden(name)
@@ -187,3 +227,11 @@ def test_kmeans_update_large_vs_oracle(ctx):
     assert np.array_equal((c1 + c2).cpu().numpy(), ocnt)
     rel = (C2 - Cn).abs().max().item() / Cn.abs().max().item()
     assert rel < 1e-13 and cont2 == cont
+    # sharded exact mode: 3 uneven shards (one empty) chained through carries
+    cuts = [0, N // 3, N // 3, N]
+    cs = cc = None
+    for lo, hi in zip(cuts, cuts[1:]):
+        cs, cc = lshkm.kmeans_partial_carry(ctx, X[lo:hi], a[lo:hi], K, cs, cc)
+    C3, cont3 = lshkm.kmeans_finalize(ctx, cs, cc, Cold, "euclidean", 0.05)
+    assert np.array_equal(cc.cpu().numpy(), ocnt) and cont3 == cont
+    assert np.array_equal(C3.cpu().numpy().view(np.uint64), on.view(np.uint64))      # bit-exact

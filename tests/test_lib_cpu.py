@@ -25,6 +25,14 @@ def test_library_exports_declared_symbols():
     assert lshkm.lib().lshkm_version().decode().startswith("lshkm-gfx950")
 
 
+def test_binding_declares_every_abi_signature():
+    # ctypes without argtypes passes ints as 32-bit: every ABI entry point needs
+    # an explicit signature in lshkm.lib()'s table
+    L = lshkm.lib()
+    untyped = [s for s in lshkm.declared_symbols() if getattr(L, s).argtypes is None]
+    assert not untyped, untyped
+
+
 def test_library_is_gfx950_code_object():
     with open(os.path.join(PKG, "liblshkm.so"), "rb") as f:
         blob = f.read()

@@ -115,6 +115,50 @@ def test_two_rank_sharding_reproduces_single_shard(N):
     mp.spawn(_worker, args=(2, _free_port(), N, 32, 16), nprocs=2, join=True)
 
 
+def _carry_worker(rank, world, port, N, d, K, out_path):
+    """Exact mode: each rank continues the per-(c, j) chains from the previous
+    rank's running sums (numpy restatement of lshkm_kmeans_partial_carry: a
+    sequential cumsum per cluster starting from the carry)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    oracle, sh = _imports()
+    Xall = oracle.synth(0x5EED ^ 3, N, d).astype(np.float64)
+    a_all = (np.arange(N) * 7919 + 13) % K
+    row0, n = sh.shard_range(N, world, rank)
+    X, a = Xall[row0:row0 + n], a_all[row0:row0 + n]
+
+    def local_fn(cs, cc):
+        sums = np.zeros((K, d)) if cs is None else cs.numpy().copy()
+        cnt = np.zeros(K, np.int64) if cc is None else cc.numpy().copy()
+        for c in range(K):
+            rows = X[a == c]
+            if len(rows):
+                # np.cumsum adds strictly in order (no pairwise reassociation)
+                sums[c] = np.cumsum(np.vstack([sums[c], rows]), axis=0)[-1]
+            cnt[c] += len(rows)
+        return torch.from_numpy(sums), torch.from_numpy(cnt)
+
+    sums, cnt = sh.chain_partials(local_fn, torch.zeros((K, d), dtype=torch.float64),
+                                  torch.zeros(K, dtype=torch.int64))
+    if rank == world - 1:
+        np.savez(out_path, sums=sums.numpy(), cnt=cnt.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exact_chain_partials_match_sequential(world, tmp_path):
+    N, d, K = 3001, 16, 9
+    out = str(tmp_path / "chain.npz")
+    mp.spawn(_carry_worker, args=(world, _free_port(), N, d, K, out), nprocs=world, join=True)
+    oracle, _ = _imports()
+    Xall = oracle.synth(0x5EED ^ 3, N, d).astype(np.float64)
+    a_all = (np.arange(N) * 7919 + 13) % K
+    es, ec = _seq_partials(Xall, a_all, K)
+    got = np.load(out)
+    assert np.array_equal(got["cnt"], ec)
+    assert np.array_equal(got["sums"].view(np.uint64), es.view(np.uint64))     # bit-exact vs one sequential pass
+
+
 def test_shard_ranges_cover_rows():
     _, sh = _imports()
     for n_total, world in [(10, 3), (80_000_000, 8), (7, 8)]:
