@@ -73,6 +73,43 @@ int lshkm_ctx_sync(lshkm_ctx ctx) {
     return 0;
 }
 
+int lshkm_dev_alloc(lshkm_ctx ctx, int64_t bytes, void** out) {
+    LSHKM_CHECK(ctx && out && bytes >= 0, LSHKM_ERR_ARG, "bad arguments");
+    *out = nullptr;
+    if (bytes == 0) return 0;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    if (hipMalloc(out, (size_t)bytes) != hipSuccess) {
+        *out = nullptr;
+        set_error("hipMalloc failed (" + std::to_string(bytes) + " B)");
+        return LSHKM_ERR_NOMEM;
+    }
+    return 0;
+}
+
+int lshkm_dev_free(lshkm_ctx ctx, void* p) {
+    LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
+    if (!p) return 0;
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // no launch on the stream may still read it
+    LSHKM_HIP(hipFree(p));
+    return 0;
+}
+
+int lshkm_memcpy_h2d(lshkm_ctx ctx, void* dst_dev, const void* src_host, int64_t bytes) {
+    LSHKM_CHECK(ctx && bytes >= 0 && (bytes == 0 || (dst_dev && src_host)), LSHKM_ERR_ARG, "bad arguments");
+    if (bytes == 0) return 0;
+    LSHKM_HIP(hipMemcpyAsync(dst_dev, src_host, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host buffer may be reused on return
+    return 0;
+}
+
+int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t bytes) {
+    LSHKM_CHECK(ctx && bytes >= 0 && (bytes == 0 || (dst_host && src_dev)), LSHKM_ERR_ARG, "bad arguments");
+    if (bytes == 0) return 0;
+    LSHKM_HIP(hipMemcpyAsync(dst_host, src_dev, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
 int lshkm_ctx_destroy(lshkm_ctx ctx) {
     if (!ctx) return 0;
     hipStreamSynchronize(ctx->stream);

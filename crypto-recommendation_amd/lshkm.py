@@ -51,6 +51,10 @@ def lib():
             "lshkm_ctx_set_stream": (i32, [vp, vp]),
             "lshkm_ctx_sync": (i32, [vp]),
             "lshkm_ctx_destroy": (i32, [vp]),
+            "lshkm_dev_alloc": (i32, [vp, i64, C.POINTER(vp)]),
+            "lshkm_dev_free": (i32, [vp, vp]),
+            "lshkm_memcpy_h2d": (i32, [vp, vp, vp, i64]),
+            "lshkm_memcpy_d2h": (i32, [vp, vp, vp, i64]),
             "lshkm_get_stat": (i32, [vp, i32, C.POINTER(i64)]),
             "lshkm_reset_stats": (i32, [vp]),
             "lshkm_ctx_enable_timing": (i32, [vp, i32]),

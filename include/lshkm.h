@@ -58,6 +58,13 @@ int lshkm_ctx_create(int device, lshkm_ctx* out);
 int lshkm_ctx_set_stream(lshkm_ctx ctx, void* hip_stream);
 int lshkm_ctx_sync(lshkm_ctx ctx);
 int lshkm_ctx_destroy(lshkm_ctx ctx);
+/* Device memory for callers without HIP headers (the C++ shim
+ * include/lshkm_compat.hpp, cgo/JNI bindings). Copies are ordered on the
+ * context's stream and complete before return; free waits for the stream. */
+int lshkm_dev_alloc(lshkm_ctx ctx, int64_t bytes, void** out_dev);
+int lshkm_dev_free(lshkm_ctx ctx, void* p_dev);
+int lshkm_memcpy_h2d(lshkm_ctx ctx, void* dst_dev, const void* src_host, int64_t bytes);
+int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t bytes);
 /* Counters: 0 = hash values resolved by the exact soft-x87 path,
  * 1 = points whose argmin needed the exact all-centroid pass. */
 int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);

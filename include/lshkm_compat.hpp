@@ -1,0 +1,456 @@
+/*
+ * lshkm_compat.hpp — C++ drop-in for the reference's header-template interface
+ * of the hot path, on top of the C ABI in lshkm.h.
+ *
+ * Include it AFTER the reference's own headers (it uses their CustVector,
+ * CustHashtable and HashGenerator types and adds none of its own):
+ *
+ *     #include "lsh_cube.hpp"                      // lib/lsh_cube.hpp
+ *     #include "clustering_phases/assignment.hpp"
+ *     #include "clustering_phases/update.hpp"
+ *     #include "lshkm_compat.hpp"                  // this file; link -llshkm
+ *
+ * and call lshkm_compat::X where the reference calls X:
+ *
+ *   create_LSH_hashtables   lib/lsh_cube.hpp:44-74
+ *   create_hypercube        lib/lsh_cube.hpp:108-136
+ *   lloyds_assignment       lib/clustering_phases/assignment.hpp:54-80
+ *   k_means                 lib/clustering_phases/update.hpp:37-86
+ *
+ * Same signatures, same return values and the same ownership as the
+ * reference: the hashtables are real CustHashtable objects (the caller deletes
+ * them; each deletes its generator), so get_LSH_combined_buckets,
+ * get_LSH_filtered_combined_buckets and get_hypercube_combined_buckets
+ * (lsh_cube.hpp:77-177) and every CustHashtable method work on them
+ * unchanged. Their generators are GPU-backed HashGenerator plugins
+ * (hash_generator.hpp:19-31): the dataset rows are hashed in one device pass
+ * at creation, a query vector in one device call shared by the L tables.
+ * k_means allocates and deletes centers exactly as update.hpp:66-84 does.
+ *
+ * The seed: the reference seeds from system_clock (lsh_cube.hpp:48-51,
+ * 112-114); the overloads without a seed do the same, the ones with a trailing
+ * `seed` argument make a run reproducible.
+ *
+ * Data: the device holds points as fp32. Vector components must be exactly
+ * representable in fp32 (the reference's inputs are) — anything
+ * else throws std::domain_error rather than silently rounding. Centroids are
+ * fp64 and may hold any value. Dataset rows are hashed when the table is
+ * built, as the reference's insertVector does; re-hashing a dataset row later
+ * returns that hash (the reference never mutates its input vectors).
+ *
+ * Errors from the library throw lshkm_compat::Error (std::runtime_error). The
+ * device is ordinal LSHKM_DEVICE (environment, default 0); one context per
+ * thread.
+ */
+#ifndef LSHKM_COMPAT_HPP
+#define LSHKM_COMPAT_HPP
+
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "lshkm.h"
+
+namespace lshkm_compat {
+
+struct Error : std::runtime_error {
+    explicit Error(const std::string& m) : std::runtime_error("liblshkm: " + m) {}
+};
+
+inline void check(int rc) {
+    if (rc != LSHKM_OK) throw Error(lshkm_last_error());
+}
+
+// ------------------------------------------------------------ context / memory
+class Context {
+public:
+    Context() {
+        const char* env = std::getenv("LSHKM_DEVICE");
+        check(lshkm_ctx_create(env ? std::atoi(env) : 0, &h_));
+    }
+    ~Context() { lshkm_ctx_destroy(h_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    lshkm_ctx get() const { return h_; }
+
+private:
+    lshkm_ctx h_ = nullptr;
+};
+
+inline lshkm_ctx context() {
+    static thread_local Context c;
+    return c.get();
+}
+
+// Device allocation owned by the calling thread's context.
+class DevMem {
+public:
+    DevMem() = default;
+    explicit DevMem(size_t bytes) { check(lshkm_dev_alloc(context(), (int64_t)bytes, &p_)); }
+    ~DevMem() { if (p_) lshkm_dev_free(context(), p_); }
+    DevMem(DevMem&& o) noexcept : p_(o.p_) { o.p_ = nullptr; }
+    DevMem& operator=(DevMem&& o) noexcept { std::swap(p_, o.p_); return *this; }
+    DevMem(const DevMem&) = delete;
+    DevMem& operator=(const DevMem&) = delete;
+    template <typename U> U* as() const { return static_cast<U*>(p_); }
+
+private:
+    void* p_ = nullptr;
+};
+
+template <typename U>
+DevMem upload(const U* host, size_t n) {
+    DevMem m(n * sizeof(U));
+    check(lshkm_memcpy_h2d(context(), m.as<void>(), host, (int64_t)(n * sizeof(U))));
+    return m;
+}
+
+template <typename U>
+void download(U* host, const DevMem& m, size_t n) {
+    check(lshkm_memcpy_d2h(context(), host, m.as<void>(), (int64_t)(n * sizeof(U))));
+}
+
+inline int metric_of(const std::string& metric) {
+    if (metric == "euclidean") return LSHKM_METRIC_EUCLIDEAN;
+    if (metric == "cosine") return LSHKM_METRIC_COSINE;
+    throw std::invalid_argument("lshkm_compat: unknown metric '" + metric + "'");
+}
+
+inline unsigned long clock_seed() {   // lsh_cube.hpp:48
+    return std::chrono::system_clock::now().time_since_epoch().count();
+}
+
+// One vector's components as fp32, refusing any that would round.
+template <typename T>
+void pack_row(CustVector<T>& v, size_t d, float* out) {
+    const std::vector<T>& x = *v.getDimensions();
+    if (x.size() != d)
+        throw std::invalid_argument("lshkm_compat: vector '" + v.getId() + "' has " + std::to_string(x.size()) +
+                                    " dimensions, expected " + std::to_string(d));
+    for (size_t j = 0; j < d; j++) {
+        const float f = static_cast<float>(x[j]);
+        if (static_cast<T>(f) != x[j])
+            throw std::domain_error("lshkm_compat: component " + std::to_string(j) + " of vector '" + v.getId() +
+                                    "' is not representable in fp32");
+        out[j] = f;
+    }
+}
+
+template <typename T>
+std::vector<float> pack_rows(std::vector<CustVector<T>>& vs, size_t d) {
+    std::vector<float> X(vs.size() * d);
+    for (size_t i = 0; i < vs.size(); i++) pack_row(vs[i], d, X.data() + i * d);
+    return X;
+}
+
+// Index of `v` in the dataset [base, base + n), or -1.
+template <typename T>
+int64_t row_of(const CustVector<T>* v, const CustVector<T>* base, int64_t n) {
+    if (!base || v < base || v >= base + n) return -1;
+    return v - base;
+}
+
+// ---------------------------------------------------------------- LSH tables
+// State shared by the L generators of one create_LSH_hashtables call.
+template <typename T>
+struct LshState {
+    lshkm_lsh h = nullptr;
+    int metric = 0, k = 0, L = 0;
+    size_t d = 0;
+    const CustVector<T>* base = nullptr;
+    int64_t N = 0;
+    std::vector<int32_t> value;    // [N][L] phi (euclidean) or g (cosine)
+    std::vector<int32_t> tuples;   // [N][L][k] h tuples (euclidean)
+    // last query, hashed once for all L tables
+    const CustVector<T>* q_ptr = nullptr;
+    std::vector<T> q_dims;
+    std::vector<int32_t> q_value, q_tuples;
+
+    ~LshState() { lshkm_lsh_destroy(h); }
+
+    void hash_query(CustVector<T>* v) {
+        if (v == q_ptr && *v->getDimensions() == q_dims) return;
+        std::vector<float> x(d);
+        pack_row(*v, d, x.data());
+        DevMem X = upload(x.data(), d);
+        DevMem val(sizeof(int32_t) * L), tup(sizeof(int32_t) * L * k);
+        const bool eu = metric == LSHKM_METRIC_EUCLIDEAN;
+        check(lshkm_lsh_hash(h, X.as<float>(), 1, eu ? tup.as<int32_t>() : nullptr, val.as<int32_t>(), nullptr));
+        q_value.resize(L);
+        download(q_value.data(), val, L);
+        q_tuples.assign(eu ? (size_t)L * k : 0, 0);
+        if (eu) download(q_tuples.data(), tup, (size_t)L * k);
+        q_ptr = v;
+        q_dims = *v->getDimensions();
+    }
+};
+
+// EuclideanPhiGen (euclidean_phi_gen.hpp:77-92) / CosineGGen
+// (cosine_g_gen.hpp:56-66) of table `l`, answered by the device.
+template <typename T>
+class GpuLshGenerator : public HashGenerator<T> {
+public:
+    GpuLshGenerator(std::shared_ptr<LshState<T>> st, int table) : st_(std::move(st)), l_(table) {}
+
+    int generate(CustVector<T>* v) override {
+        const LshState<T>& s = *st_;
+        const int64_t r = row_of<T>(v, s.base, s.N);
+        const int32_t* tup;
+        int value;
+        if (r >= 0) {
+            value = s.value[(size_t)r * s.L + l_];
+            tup = s.tuples.empty() ? nullptr : &s.tuples[((size_t)r * s.L + l_) * s.k];
+        } else {
+            st_->hash_query(v);
+            value = s.q_value[l_];
+            tup = s.q_tuples.empty() ? nullptr : &s.q_tuples[(size_t)l_ * s.k];
+        }
+        // first write wins per ID, as id_to_det_hashes.emplace (euclidean_phi_gen.hpp:94)
+        if (tup) detailed_.emplace(v->getId(), std::vector<int>(tup, tup + s.k));
+        return value;
+    }
+    bool hasDetailedHash() override { return st_->metric == LSHKM_METRIC_EUCLIDEAN; }
+    std::unordered_map<std::string, std::vector<int>>* getDetailedHashes() override { return &detailed_; }
+    unsigned long getSize() override {
+        unsigned long size = sizeof(*this);
+        for (const auto& e : detailed_) size += e.first.capacity() + e.second.capacity() * sizeof(int) + 64;
+        return size;
+    }
+
+private:
+    std::shared_ptr<LshState<T>> st_;
+    int l_;
+    std::unordered_map<std::string, std::vector<int>> detailed_;
+};
+
+template <typename T>
+std::vector<CustHashtable<T>*> create_LSH_hashtables(std::vector<CustVector<T>>& input_vectors,
+                                                     const std::string metric_type, int k, int L,
+                                                     int lsh_bucket_div, double euclidean_h_w, unsigned long seed) {
+    if (input_vectors.empty() || k < 1 || L < 1) throw std::invalid_argument("lshkm_compat: empty input or k, L < 1");
+    auto st = std::make_shared<LshState<T>>();
+    st->metric = metric_of(metric_type);
+    st->k = k;
+    st->L = L;
+    st->d = input_vectors[0].getDimensions()->size();
+    st->base = input_vectors.data();
+    st->N = (int64_t)input_vectors.size();
+    const int d = (int)st->d;
+    const bool eu = st->metric == LSHKM_METRIC_EUCLIDEAN;
+    const float w = (float)euclidean_h_w;   // EuclideanHGen stores float (euclidean_h_gen.hpp:36)
+    const int64_t nb = eu ? (int64_t)(input_vectors.size() / lsh_bucket_div) : (int64_t)1 << k;
+    if (nb < 1) throw std::invalid_argument("lshkm_compat: N / lsh_bucket_div is 0 buckets");
+
+    uint32_t state = 0;
+    if (eu) {
+        std::vector<float> V((size_t)L * k * d), t((size_t)L * k);
+        std::vector<int32_t> r((size_t)L * k);
+        check(lshkm_params_lsh_euclidean(seed, L, k, d, w, V.data(), t.data(), r.data(), &state));
+        check(lshkm_lsh_create(context(), st->metric, d, k, L, nb, w, V.data(), t.data(), r.data(), nullptr, &st->h));
+    } else {
+        std::vector<double> R((size_t)L * k * d);
+        check(lshkm_params_lsh_cosine(seed, L, k, d, R.data(), &state));
+        check(lshkm_lsh_create(context(), st->metric, d, k, L, nb, w, nullptr, nullptr, nullptr, R.data(), &st->h));
+    }
+
+    // every row, every table in one device pass
+    const size_t N = (size_t)st->N;
+    std::vector<float> X = pack_rows(input_vectors, st->d);
+    DevMem Xd = upload(X.data(), X.size());
+    DevMem val(sizeof(int32_t) * N * L), tup(eu ? sizeof(int32_t) * N * L * k : 0);
+    check(lshkm_lsh_hash(st->h, Xd.as<float>(), st->N, eu ? tup.as<int32_t>() : nullptr, val.as<int32_t>(), nullptr));
+    st->value.resize(N * L);
+    download(st->value.data(), val, N * L);
+    if (eu) {
+        st->tuples.resize(N * L * k);
+        download(st->tuples.data(), tup, N * L * k);
+    }
+
+    // tables in the reference's order, rows inserted in row order (lsh_cube.hpp:53-71)
+    std::vector<CustHashtable<T>*> tables;
+    tables.reserve(L);
+    for (int l = 0; l < L; l++) {
+        tables.emplace_back(new CustHashtable<T>(new GpuLshGenerator<T>(st, l), (int)nb));
+        for (size_t i = 0; i < N; i++) tables[l]->insertVector(&input_vectors[i]);
+    }
+    return tables;
+}
+
+template <typename T>
+std::vector<CustHashtable<T>*> create_LSH_hashtables(std::vector<CustVector<T>>& input_vectors,
+                                                     const std::string metric_type, int k, int L,
+                                                     int lsh_bucket_div, double euclidean_h_w) {
+    return create_LSH_hashtables(input_vectors, metric_type, k, L, lsh_bucket_div, euclidean_h_w, clock_seed());
+}
+
+// ----------------------------------------------------------------- hypercube
+template <typename T>
+struct CubeState {
+    lshkm_cube h = nullptr;
+    size_t d = 0;
+    const CustVector<T>* base = nullptr;
+    int64_t N = 0;
+    std::vector<int32_t> vertex;   // [N]
+    ~CubeState() { lshkm_cube_destroy(h); }
+};
+
+// HypercubeGen (hypercube_gen.hpp:63-73) over k EuclideanFGen / CosineHGen,
+// answered by the device; a query's unseen h values draw their coins from the
+// continued engine (euclidean_f_gen.hpp:65-79).
+template <typename T>
+class GpuCubeGenerator : public HashGenerator<T> {
+public:
+    explicit GpuCubeGenerator(std::shared_ptr<CubeState<T>> st) : st_(std::move(st)) {}
+
+    int generate(CustVector<T>* v) override {
+        const CubeState<T>& s = *st_;
+        const int64_t r = row_of<T>(v, s.base, s.N);
+        if (r >= 0) return s.vertex[(size_t)r];
+        std::vector<float> x(s.d);
+        pack_row(*v, s.d, x.data());
+        DevMem X = upload(x.data(), s.d), vert(sizeof(int32_t));
+        check(lshkm_cube_vertices(s.h, X.as<float>(), 1, vert.as<int32_t>()));
+        int32_t out = 0;
+        download(&out, vert, 1);
+        return out;
+    }
+    bool hasDetailedHash() override { return false; }
+    std::unordered_map<std::string, std::vector<int>>* getDetailedHashes() override { return nullptr; }
+    unsigned long getSize() override { return sizeof(*this) + st_->vertex.capacity() * sizeof(int32_t); }
+
+private:
+    std::shared_ptr<CubeState<T>> st_;
+};
+
+template <typename T>
+CustHashtable<T>* create_hypercube(std::vector<CustVector<T>>& input_vectors, const std::string metric_type, int k,
+                                   double euclidean_h_w, unsigned long seed) {
+    if (input_vectors.empty() || k < 1 || k > 30) throw std::invalid_argument("lshkm_compat: empty input or k out of range");
+    auto st = std::make_shared<CubeState<T>>();
+    const int metric = metric_of(metric_type);
+    st->d = input_vectors[0].getDimensions()->size();
+    st->base = input_vectors.data();
+    st->N = (int64_t)input_vectors.size();
+    const int d = (int)st->d;
+    const float w = (float)euclidean_h_w;
+    uint32_t state = 0;
+    if (metric == LSHKM_METRIC_EUCLIDEAN) {
+        std::vector<float> V((size_t)k * d), t(k);
+        check(lshkm_params_cube_euclidean(seed, k, d, w, V.data(), t.data(), &state));
+        check(lshkm_cube_create(context(), metric, d, k, w, V.data(), t.data(), nullptr, state, &st->h));
+    } else {
+        std::vector<double> R((size_t)k * d);
+        check(lshkm_params_cube_cosine(seed, k, d, R.data(), &state));
+        check(lshkm_cube_create(context(), metric, d, k, w, nullptr, nullptr, R.data(), state, &st->h));
+    }
+    // the build draws the coins in (row, f) order, as the insert loop (lsh_cube.hpp:132-133)
+    const size_t N = (size_t)st->N;
+    std::vector<float> X = pack_rows(input_vectors, st->d);
+    DevMem Xd = upload(X.data(), X.size());
+    check(lshkm_cube_build(st->h, Xd.as<float>(), st->N));
+    DevMem vert(sizeof(int32_t) * N);
+    check(lshkm_cube_vertices(st->h, Xd.as<float>(), st->N, vert.as<int32_t>()));   // all h seen: no draws
+    st->vertex.resize(N);
+    download(st->vertex.data(), vert, N);
+
+    CustHashtable<T>* cube = new CustHashtable<T>(new GpuCubeGenerator<T>(st), 1 << k);
+    for (size_t i = 0; i < N; i++) cube->insertVector(&input_vectors[i]);
+    return cube;
+}
+
+template <typename T>
+CustHashtable<T>* create_hypercube(std::vector<CustVector<T>>& input_vectors, const std::string metric_type, int k,
+                                   double euclidean_h_w) {
+    return create_hypercube(input_vectors, metric_type, k, euclidean_h_w, clock_seed());
+}
+
+// ------------------------------------------------------------------- k-means
+template <typename T>
+std::vector<double> pack_centers(std::vector<CustVector<T>*>& centers, size_t d) {
+    std::vector<double> C(centers.size() * d);
+    for (size_t c = 0; c < centers.size(); c++) {
+        const std::vector<T>& x = *centers[c]->getDimensions();
+        if (x.size() != d) throw std::invalid_argument("lshkm_compat: center dimension mismatch");
+        for (size_t j = 0; j < d; j++) C[c * d + j] = static_cast<double>(x[j]);
+    }
+    return C;
+}
+
+// lloyds_assignment (assignment.hpp:54-80): nearest centroid (strict '<',
+// first index wins) and its distance for every vector, then each centroid
+// assigned to its own cluster at distance 0.
+template <typename T>
+void lloyds_assignment(std::vector<CustVector<T>>& input_vectors, std::vector<CustVector<T>*>& centroids,
+                       std::string metric_type) {
+    const int metric = metric_of(metric_type);
+    if (input_vectors.empty() || centroids.empty()) {
+        for (size_t c = 0; c < centroids.size(); c++) centroids[c]->setCluster((int)c, 0);
+        return;
+    }
+    const size_t N = input_vectors.size(), K = centroids.size(), d = input_vectors[0].getDimensions()->size();
+    std::vector<float> X = pack_rows(input_vectors, d);
+    std::vector<double> C = pack_centers(centroids, d);
+    std::vector<int32_t> src(K);
+    for (size_t c = 0; c < K; c++) src[c] = (int32_t)row_of<T>(centroids[c], input_vectors.data(), (int64_t)N);
+    DevMem Xd = upload(X.data(), X.size()), Cd = upload(C.data(), C.size());
+    DevMem ad(sizeof(int32_t) * N), dd(sizeof(double) * N);
+    check(lshkm_lloyd_assign(context(), Xd.as<float>(), (int64_t)N, (int)d, Cd.as<double>(), (int)K, metric,
+                             src.data(), ad.as<int32_t>(), dd.as<double>()));
+    std::vector<int32_t> a(N);
+    std::vector<double> dist(N);
+    download(a.data(), ad, N);
+    download(dist.data(), dd, N);
+    for (size_t i = 0; i < N; i++) input_vectors[i].setCluster(a[i], dist[i]);
+    // centroids outside the dataset too, in centroid order (assignment.hpp:77-78)
+    for (size_t c = 0; c < K; c++) centroids[c]->setCluster((int)c, 0);
+}
+
+// k_means (update.hpp:37-86): per-cluster means of the members in row order;
+// if some center moved more than min_dist, every center is replaced by a new
+// "k_means_center" vector (old ones with that ID deleted) and true returned,
+// else the centers are left alone and false returned.
+template <typename T>
+bool k_means(std::vector<CustVector<T>>& input_vectors, std::vector<CustVector<T>*>& centers, std::string metric_type,
+             double min_dist) {
+    // the reference accumulates in the vector type (cust_vector.hpp:179-184);
+    // the device sums are fp64, i.e. the reference's CustVector<double> (main.cpp:86)
+    static_assert(std::is_same<T, double>::value, "lshkm_compat::k_means matches CustVector<double> only");
+    const int metric = metric_of(metric_type);
+    if (centers.empty()) return false;
+    const size_t N = input_vectors.size(), K = centers.size(), d = centers[0]->getDimensions()->size();
+    std::vector<float> X = pack_rows(input_vectors, d);
+    std::vector<int32_t> a(N);
+    for (size_t i = 0; i < N; i++) {
+        a[i] = input_vectors[i].getCluster();
+        if (a[i] < 0 || (size_t)a[i] >= K)
+            throw std::out_of_range("lshkm_compat: vector '" + input_vectors[i].getId() + "' has no cluster in [0, K)");
+    }
+    std::vector<double> C = pack_centers(centers, d);
+    DevMem Xd = upload(X.data(), X.size()), ad = upload(a.data(), N), Cd = upload(C.data(), C.size());
+    DevMem Cn(sizeof(double) * K * d);
+    int cont = 0;
+    check(lshkm_kmeans_update(context(), Xd.as<float>(), (int64_t)N, (int)d, ad.as<int32_t>(), Cd.as<double>(),
+                              (int)K, metric, min_dist, Cn.as<double>(), nullptr, &cont));
+    if (!cont) return false;
+    std::vector<double> Cnew(K * d);
+    download(Cnew.data(), Cn, K * d);
+    for (size_t c = 0; c < K; c++) {
+        std::vector<T> dims(d);
+        for (size_t j = 0; j < d; j++) dims[j] = static_cast<T>(Cnew[c * d + j]);
+        if (centers[c]->getId() == "k_means_center") delete centers[c];
+        centers[c] = new CustVector<T>("k_means_center", dims);
+    }
+    return true;
+}
+
+}  // namespace lshkm_compat
+
+#endif  // LSHKM_COMPAT_HPP

@@ -1,0 +1,193 @@
+// compat_check.cpp — runs the REFERENCE's own functions and the C++ drop-in
+// (include/lshkm_compat.hpp, GPU-backed) side by side on the same data and
+// seed, through the reference's own interface, and compares everything the
+// caller can observe. TEST INFRASTRUCTURE ONLY (tests/test_gpu_compat.py).
+//
+// Built by oracle/Makefile into oracle/_ref/ (git-ignored) from this file, the
+// reference's headers/sources where they lie and liblshkm.so; g++ -O0 as the
+// reference ships. The reference's clock seed is interposed as in
+// ref_harness.cpp so both sides draw from the same engine seed.
+//
+// usage: compat_check SEED N d K   -> prints "compat ok" and exits 0, or the
+// first mismatches and exits 1.
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+static long long g_seed = 1;
+
+namespace std { namespace chrono { inline namespace _V2 {
+system_clock::time_point system_clock::now() noexcept {
+    return system_clock::time_point(system_clock::duration(g_seed));
+}
+}}}
+
+#include "utils.hpp"
+#include "lsh_cube.hpp"
+#include "clustering_phases/assignment.hpp"
+#include "clustering_phases/update.hpp"
+
+#include "../include/lshkm_compat.hpp"
+#include "../include/lshkm_synth.h"
+
+typedef CustVector<double> Vec;
+
+static int g_bad = 0;
+static std::map<std::string, long> g_stat;   // coverage: how much each check exercised
+static void fail(const std::string& what) {
+    if (g_bad++ < 20) std::printf("MISMATCH %s\n", what.c_str());
+}
+
+static std::vector<Vec> make_data(uint64_t seed, int N, int d) {
+    std::vector<Vec> v;
+    v.reserve(N);
+    for (int i = 0; i < N; i++) {
+        std::vector<double> x(d);
+        for (int j = 0; j < d; j++) x[j] = (double)lshkm_synth_value(seed, i, d, j);
+        v.emplace_back("item" + std::to_string(i), x);
+    }
+    return v;
+}
+
+// queries: dataset rows (alias IDs), perturbed copies under new IDs
+static std::vector<Vec> make_queries(std::vector<Vec>& data, int nq) {
+    std::vector<Vec> q;
+    const int N = (int)data.size();
+    for (int i = 0; i < nq; i++) {
+        std::vector<double> x = *data[(i * 7919) % N].getDimensions();
+        if (i % 2) {
+            for (size_t j = 0; j < x.size(); j += 3) x[j] = (double)(float)(x[j] * 0.96875);
+            q.emplace_back("query" + std::to_string(i), x);
+        } else {
+            q.emplace_back(data[(i * 7919) % N].getId(), x);
+        }
+    }
+    return q;
+}
+
+static void cmp_ptrs(const std::vector<Vec*>& a, const std::vector<Vec*>& b, const std::string& what) {
+    if (a != b) fail(what + " (sizes " + std::to_string(a.size()) + " vs " + std::to_string(b.size()) + ")");
+}
+
+static void check_lsh(std::vector<Vec>& data, const std::string& metric, int k, int L, int div, double w) {
+    g_seed += 101;
+    std::vector<CustHashtable<double>*> ref = create_LSH_hashtables(data, metric, k, L, div, w);
+    std::vector<CustHashtable<double>*> gpu = lshkm_compat::create_LSH_hashtables(data, metric, k, L, div, w);  // same clock seed
+    const std::string tag = "lsh/" + metric + " ";
+    const int nb = metric == "euclidean" ? (int)(data.size() / div) : 1 << k;
+    for (int l = 0; l < L; l++)
+        for (int b = 0; b < nb; b++)
+            cmp_ptrs(ref[l]->getBucketFromIndex(b), gpu[l]->getBucketFromIndex(b),
+                     tag + "table " + std::to_string(l) + " bucket " + std::to_string(b));
+    std::vector<Vec> qs = make_queries(data, 24);
+    for (size_t i = 0; i < qs.size(); i++) {
+        for (int l = 0; l < L; l++)
+            if (ref[l]->getHash(&qs[i]) != gpu[l]->getHash(&qs[i])) fail(tag + "getHash query " + std::to_string(i));
+        cmp_ptrs(get_LSH_combined_buckets(ref, &qs[i]), get_LSH_combined_buckets(gpu, &qs[i]),
+                 tag + "combined query " + std::to_string(i));
+        std::vector<Vec*> fr = get_LSH_filtered_combined_buckets(ref, &qs[i]);
+        cmp_ptrs(fr, get_LSH_filtered_combined_buckets(gpu, &qs[i]), tag + "filtered query " + std::to_string(i));
+        g_stat["lsh_" + metric + "_filtered_rows"] += (long)fr.size();
+    }
+    for (auto t : ref) delete t;
+    for (auto t : gpu) delete t;
+}
+
+static void check_cube(std::vector<Vec>& data, const std::string& metric, int k, double w) {
+    g_seed += 202;
+    CustHashtable<double>* ref = create_hypercube(data, metric, k, w);
+    CustHashtable<double>* gpu = lshkm_compat::create_hypercube(data, metric, k, w);
+    const std::string tag = "cube/" + metric + " ";
+    for (int b = 0; b < (1 << k); b++)
+        cmp_ptrs(ref->getBucketFromIndex(b), gpu->getBucketFromIndex(b), tag + "bucket " + std::to_string(b));
+    // dataset rows only for the euclidean cube: a new h would draw a coin from
+    // the engine create_hypercube left on its stack (lsh_cube.hpp:112-118)
+    for (int i = 0; i < 16; i++) {
+        Vec* q = &data[(i * 613) % data.size()];
+        for (int probes : {1, 2, 5, 12}) {
+            std::vector<Vec*> pr = get_hypercube_combined_buckets(*ref, q, probes, k);
+            cmp_ptrs(pr, get_hypercube_combined_buckets(*gpu, q, probes, k),
+                     tag + "probes " + std::to_string(probes) + " query " + std::to_string(i));
+            g_stat["cube_" + metric + "_probe_rows"] += (long)pr.size();
+        }
+    }
+    if (metric == "cosine") {
+        std::vector<Vec> qs = make_queries(data, 16);
+        for (size_t i = 0; i < qs.size(); i++)
+            if (ref->getHash(&qs[i]) != gpu->getHash(&qs[i])) fail(tag + "getHash query " + std::to_string(i));
+    }
+    delete ref;
+    delete gpu;
+}
+
+static void check_kmeans(std::vector<Vec>& data, const std::string& metric, int K) {
+    std::vector<Vec> a = data, b = data;
+    std::vector<Vec*> ca, cb;
+    const int N = (int)data.size();
+    for (int c = 0; c < K; c++) {
+        ca.push_back(&a[(size_t)c * (N / K)]);
+        cb.push_back(&b[(size_t)c * (N / K)]);
+    }
+    const std::string tag = "kmeans/" + metric + " ";
+    for (int it = 0; it < 4; it++) {
+        lloyds_assignment(a, ca, metric);
+        lshkm_compat::lloyds_assignment(b, cb, metric);
+        int nd = 0;
+        for (int i = 0; i < N; i++) {
+            if (a[i].getCluster() != b[i].getCluster()) fail(tag + "cluster of row " + std::to_string(i));
+            const double da = a[i].getDistFromCentroid(), db = b[i].getDistFromCentroid();
+            if (std::fabs(da - db) > 1e-12 * std::fabs(da)) nd++;
+        }
+        if (nd) fail(tag + std::to_string(nd) + " distances beyond 1e-12 rel, iteration " + std::to_string(it));
+        const bool ra = k_means(a, ca, metric, 1e-9), rb = lshkm_compat::k_means(b, cb, metric, 1e-9);
+        if (ra != rb) fail(tag + "k_means return, iteration " + std::to_string(it));
+        for (int c = 0; c < K; c++) {
+            if (ca[c]->getId() != cb[c]->getId()) fail(tag + "center id " + std::to_string(c));
+            if (*ca[c]->getDimensions() != *cb[c]->getDimensions())
+                fail(tag + "center " + std::to_string(c) + " iteration " + std::to_string(it));
+        }
+        g_stat["kmeans_" + metric + "_iterations"]++;
+        if (!ra) break;
+    }
+    for (int c = 0; c < K; c++) {
+        if (ca[c]->getId() == "k_means_center") delete ca[c];
+        if (cb[c]->getId() == "k_means_center") delete cb[c];
+    }
+}
+
+int main(int argc, char** argv) {
+    if (argc < 5) {
+        std::fprintf(stderr, "usage: compat_check SEED N d K\n");
+        return 2;
+    }
+    g_seed = std::atoll(argv[1]);
+    const int N = std::atoi(argv[2]), d = std::atoi(argv[3]), K = std::atoi(argv[4]);
+    std::vector<Vec> data = make_data((uint64_t)g_seed, N, d);
+    try {
+        check_lsh(data, "euclidean", 4, 5, 50, 4.0);
+        check_lsh(data, "cosine", 6, 3, 8, 4.0);
+        check_cube(data, "euclidean", 8, 2.0);
+        check_cube(data, "cosine", 5, 4.0);
+        check_kmeans(data, "euclidean", K);
+        check_kmeans(data, "cosine", K);
+    } catch (const std::exception& e) {
+        std::printf("EXCEPTION %s\n", e.what());
+        return 1;
+    }
+    if (g_bad) {
+        std::printf("compat FAILED: %d mismatches\n", g_bad);
+        return 1;
+    }
+    std::printf("compat ok N=%d d=%d K=%d", N, d, K);
+    for (const auto& e : g_stat) std::printf(" %s=%ld", e.first.c_str(), e.second);
+    std::printf("\n");
+    return 0;
+}

@@ -1,0 +1,60 @@
+"""The C++ drop-in (include/lshkm_compat.hpp).
+
+CPU: the shim compiles against the reference's own headers (their
+CustVector / CustHashtable / HashGenerator types) with g++ and plain C++14.
+GPU: oracle/_ref/compat_check runs the reference's functions and the shim's
+side by side through the reference's interface (hashtable buckets, queries,
+filtered queries, hypercube probes, lloyds_assignment, k_means centers and
+ownership) and must report no mismatch."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_LIB = "/root/reference/lib"
+CHECK = os.path.join(ROOT, "oracle", "_ref", "compat_check")
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_LIB, "lsh_cube.hpp")), reason="reference headers absent")
+def test_shim_compiles_against_reference_headers(tmp_path):
+    src = tmp_path / "use_shim.cpp"
+    src.write_text(
+        '#include "utils.hpp"\n'
+        '#include "lsh_cube.hpp"\n'
+        '#include "clustering_phases/assignment.hpp"\n'
+        '#include "clustering_phases/update.hpp"\n'
+        '#include "lshkm_compat.hpp"\n'
+        "template std::vector<CustHashtable<double>*> lshkm_compat::create_LSH_hashtables<double>(\n"
+        "    std::vector<CustVector<double>>&, const std::string, int, int, int, double);\n"
+        "template CustHashtable<double>* lshkm_compat::create_hypercube<double>(\n"
+        "    std::vector<CustVector<double>>&, const std::string, int, double);\n"
+        "template void lshkm_compat::lloyds_assignment<double>(std::vector<CustVector<double>>&,\n"
+        "    std::vector<CustVector<double>*>&, std::string);\n"
+        "template bool lshkm_compat::k_means<double>(std::vector<CustVector<double>>&,\n"
+        "    std::vector<CustVector<double>*>&, std::string, double);\n"
+        "template class lshkm_compat::GpuLshGenerator<float>;\n"
+        "template class lshkm_compat::GpuCubeGenerator<int>;\n")
+    r = subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Wno-unused-function", "-I", REF_LIB,
+                        "-I", os.path.join(ROOT, "include"), str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    # and warning-free in the shim itself
+    own = [ln for ln in r.stderr.splitlines() if re.search(r"lshkm_compat\.hpp:\d+:\d+: (warning|error)", ln)]
+    assert not own, own
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [("7", "2000", "128", "16"), ("11", "900", "17", "5")])
+def test_shim_matches_reference_functions(args):
+    if not os.path.exists(CHECK):
+        pytest.skip("oracle/_ref/compat_check not built (needs the reference sources at build time)")
+    r = subprocess.run([CHECK, *args], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "compat ok" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+    # the comparison exercised something: non-empty filtered unions and probe
+    # lists, and k_means replaced its centers at least once
+    stats = dict(kv.split("=") for kv in r.stdout.split("compat ok")[1].split() if "=" in kv)
+    for key in ("lsh_euclidean_filtered_rows", "lsh_cosine_filtered_rows", "cube_euclidean_probe_rows",
+                "cube_cosine_probe_rows"):
+        assert int(stats[key]) > 0, (key, stats)
+    assert int(stats["kmeans_euclidean_iterations"]) >= 2 and int(stats["kmeans_cosine_iterations"]) >= 2, stats
