@@ -225,6 +225,60 @@ int lshkm_coins_draw(uint32_t* rng_state, const int32_t* h, int64_t n, int32_t* 
     return 0;
 }
 
+int lshkm_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows) {
+    LSHKM_CHECK(rows && N >= 1 && N <= INT32_MAX && K >= 1 && K <= N, LSHKM_ERR_ARG,
+                "bad arguments (need 1 <= K <= N < 2^31)");
+    std::default_random_engine g;
+    g.seed((unsigned long)seed);
+    std::uniform_int_distribution<int> uni(0, (int)(N - 1));
+    rows[0] = uni(g);
+    for (int i = 1; i < K; i++) {
+        int r = uni(g), c = 0;
+        while (c < i) {          // redraw on a repeat and check all again (initialization.hpp:53-61)
+            if (rows[c] == r) { r = uni(g); c = 0; }
+            else c++;
+        }
+        rows[i] = r;
+    }
+    return 0;
+}
+
+int lshkm_kmeans_pp(lshkm_ctx ctx, const float* X, int64_t N, int d, int K, int metric, uint64_t seed,
+                    int32_t* rows) {
+    LSHKM_CHECK(ctx && X && rows && N >= 1 && N <= INT32_MAX && d >= 1 && d <= 4096 && K >= 1, LSHKM_ERR_ARG,
+                "bad arguments (need N < 2^31, 1 <= d <= 4096, K >= 1)");
+    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    // every engine draw of k_means_pp up front (initialization.hpp:75-79,127-128):
+    // they do not depend on the data. uniform_real<double>(0, total) is
+    // canon * (total - 0) + 0 with canon = uniform_real<double>(0, 1).
+    std::default_random_engine g;
+    g.seed((unsigned long)seed);
+    std::uniform_int_distribution<int> uni(0, (int)(N - 1));
+    std::vector<int32_t> chosen(K, 0);
+    std::vector<double> canon(K, 0.0);
+    chosen[0] = uni(g);
+    for (int i = 1; i < K; i++) {
+        std::uniform_real_distribution<double> unit(0.0, 1.0);
+        canon[i] = unit(g);
+    }
+    Buf ws, dch, dcanon;
+    int rc;
+    if ((rc = ws.reserve(kmeans_pp_ws_bytes(N))) || (rc = dch.reserve(sizeof(int32_t) * K)) ||
+        (rc = dcanon.reserve(sizeof(double) * K)))
+        return rc;
+    LSHKM_HIP(hipMemcpyAsync(dch.p, chosen.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice, ctx->stream));
+    LSHKM_HIP(hipMemcpyAsync(dcanon.p, canon.data(), sizeof(double) * K, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = launch_kmeans_pp(ctx->stream, X, N, d, K, metric, dcanon.as<double>(), dch.as<int32_t>(), ws.p,
+                               (unsigned long long*)ctx->stats.p))) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return rc;
+    }
+    LSHKM_HIP(hipMemcpyAsync(rows, dch.p, sizeof(int32_t) * K, hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
 int lshkm_params_cube_cosine(uint64_t seed, int k, int d, double* R, uint32_t* state) {
     LSHKM_CHECK(k > 0 && d > 0 && R, LSHKM_ERR_ARG, "bad arguments");
     std::default_random_engine g;

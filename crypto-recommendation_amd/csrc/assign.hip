@@ -22,7 +22,7 @@
 // and keeps the first minimum (strict '<', assignment.hpp:66).
 #include "common.h"
 #include "kernels.h"
-#include "softx87.h"
+#include "exact.h"
 
 namespace lshkm {
 
@@ -234,30 +234,7 @@ int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, 
 
 // ---------------------------------------------------------------- exact pass
 // One wave per listed row; lane c evaluates centroids c, c+64, ... in the
-// reference's exact order; the first minimum wins.
-__device__ inline double exact_euclid(const float* __restrict__ x, const double* __restrict__ c, int d) {
-    double acc = 0.0;
-    for (int j = 0; j < d; j++) {
-        const double df = __dsub_rn((double)x[j], c[j]);
-        acc = __dadd_rn(acc, __dmul_rn(df, df));
-    }
-    return sqrt(acc);
-}
-
-__device__ inline double exact_cosine(const float* __restrict__ x, const double* __restrict__ c, int d) {
-    sx80 ip = sx_zero();
-    double a = 0.0, b = 0.0;
-    for (int j = 0; j < d; j++) {
-        const double xj = (double)x[j];
-        ip = sx_add_double(ip, __dmul_rn(xj, c[j]));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(c[j], c[j]));
-    }
-    const double denom = __dmul_rn(sqrt(a), sqrt(b));
-    const double q = sx_to_double(sx_div(ip, sx_from_double(denom)));
-    return __dsub_rn(1.0, q);
-}
-
+// reference's exact order (exact.h); the first minimum wins.
 __global__ __launch_bounds__(256) void assign_exact_kernel(
     const float* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int K, int metric,
     const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,

@@ -54,6 +54,8 @@ inline unsigned gsz(int64_t work, int64_t per_block, int64_t cap) {
 enum Stat {
     STAT_HASH_EXACT = 0,     // hash values resolved by the soft-x87 exact path
     STAT_ASSIGN_AMBIG = 1,   // points whose argmin the MFMA bound could not certify
+    STAT_KPP_CHUNKS = 2,     // k-means++ prefix-walk chunks (KPP_CHUNK rows each) ...
+    STAT_KPP_SEQ = 3,        // ... of which summed element by element (binade crossings, ties)
     STAT_COUNT = 8
 };
 

@@ -1,0 +1,34 @@
+// exact.h — the reference's point-to-centroid distances in its exact
+// operation order, for the device paths that need the value itself.
+//   euclideanDistance  lib/data_structures/cust_vector.hpp:124-136
+//     sqrt(sum_j pow(x_j - c_j, 2)), fp64, j ascending
+//   cosineDistance     lib/data_structures/cust_vector.hpp:139-155
+//     1 - (long double) inner product / (sqrt(sum x^2) * sqrt(sum c^2))
+// `this` is the point x (fp32 values), `in` the centroid c (fp64). pow(v, 2)
+// is v*v here (identical whenever v is a difference of fp32
+// values, i.e. for every dataset-row centroid). No FMA contraction.
+#pragma once
+#include "softx87.h"
+
+__device__ inline double exact_euclid(const float* __restrict__ x, const double* __restrict__ c, int d) {
+    double acc = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double df = __dsub_rn((double)x[j], c[j]);
+        acc = __dadd_rn(acc, __dmul_rn(df, df));
+    }
+    return sqrt(acc);
+}
+
+__device__ inline double exact_cosine(const float* __restrict__ x, const double* __restrict__ c, int d) {
+    sx80 ip = sx_zero();
+    double a = 0.0, b = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j];
+        ip = sx_add_double(ip, __dmul_rn(xj, c[j]));
+        a = __dadd_rn(a, __dmul_rn(xj, xj));
+        b = __dadd_rn(b, __dmul_rn(c[j], c[j]));
+    }
+    const double denom = __dmul_rn(sqrt(a), sqrt(b));
+    const double q = sx_to_double(sx_div(ip, sx_from_double(denom)));
+    return __dsub_rn(1.0, q);
+}

@@ -96,6 +96,13 @@ int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, c
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
 
+// k-means++ seeding (kmeanspp.hip): iterations 1..K-1 on the stream.
+// chosen[0] and canon[1..K-1] (the engine's canonical draws) already on the
+// device; ws holds kmeans_pp_ws_bytes(N) bytes.
+size_t kmeans_pp_ws_bytes(int64_t N);
+int launch_kmeans_pp(hipStream_t s, const float* X, int64_t N, int d, int K, int metric, const double* canon,
+                     int32_t* chosen, void* ws, unsigned long long* stats);
+
 // Fused hash + assign on split-f16 MFMA (fused.hip), d = 128.
 struct FusedLaunch {
     const float* X = nullptr;

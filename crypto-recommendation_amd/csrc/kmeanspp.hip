@@ -1,0 +1,374 @@
+// kmeanspp.hip — k-means++ seeding (k_means_pp, lib/clustering_phases/
+// initialization.hpp:71-156) on gfx950, bit-exact with the reference.
+//
+// Per new centroid i = 1..K-1 the reference
+//   (1) takes every row's min distance to centroids 0..i-1 (strict '<' after
+//       the -1 sentinel, :88-110; its ID-keyed cache only memoises),
+//   (2) the max of those minima (strict '>' from 0, :112-113),
+//   (3) overwrites them with (min/max)^2 and prefix-sums them in row order,
+//       in fp64 (:118-125),
+//   (4) draws uniform_real<double>(0, total) and binary-searches (:127-149).
+// (1) is incremental here: one exact distance per row per centroid
+// (kpp_dist_kernel), the running minimum kept in HBM. (4) needs only the
+// engine's canonical draws, which do not depend on the data, so the host draws
+// them all up front and the whole seeding runs on the stream with no host
+// round trip.
+//
+// (3) is a strictly sequential fp64 chain s_m = RN(s_{m-1} + q_m) over N rows.
+// It is reproduced exactly, in parallel, from one observation: while s stays
+// in one binade [2^e, 2^(e+1)) every s is a multiple of u = 2^(e-52), so
+// RN(s + q) = s + u * RN_u(q) unless q is a tie (q/u = k + 1/2) — the chain is
+// an integer prefix sum there. Rows are cut into chunks of KPP_CHUNK:
+//   kpp_chunk_sum_kernel    approximate chunk sums (any order)
+//   kpp_chunk_scan_kernel   approximate chunk starts (exclusive scan)
+//   kpp_chunk_units_kernel  guess each chunk's binade from its approximate
+//                           start; R = sum of RN_u(q) in units of u, or
+//                           "dirty" (tie, non-finite, crossing, tiny start)
+//   kpp_chain_kernel        one wave walks the chunks with the EXACT running
+//                           s: a chunk whose guess is right (s in binade e and
+//                           s/u + R < 2^53) advances s by R*u exactly, 64
+//                           chunks per wave-wide integer scan; any other chunk
+//                           (the first, ~log2(N) binade crossings, ties) is
+//                           summed element by element with hardware fp64 adds
+//   kpp_expand_kernel       writes s_m = s_start + u * prefix for the
+//                           integer-resolved chunks
+//   kpp_choose_kernel       the draw and the reference's binary search
+#include <climits>
+
+#include "common.h"
+#include "kernels.h"
+#include "exact.h"
+
+namespace lshkm {
+
+constexpr int KPP_THREADS = 256;
+constexpr int KPP_CHUNK = 512;                 // rows per chunk = 2 per thread
+constexpr int KPP_DIRTY = INT_MIN;
+constexpr int64_t KPP_TWO53 = 1ll << 53;
+
+// q_m = (min_m / max)^2, as :121-124 (two roundings).
+__device__ inline double kpp_q(double m, double mx) {
+    const double t = __ddiv_rn(m, mx);
+    return __dmul_rn(t, t);
+}
+
+__device__ inline double kpp_max(const unsigned long long* mx_bits) {
+    return __longlong_as_double((long long)*mx_bits);
+}
+
+// Binade exponent of a positive normal double (s in [2^e, 2^(e+1))).
+__device__ inline int kpp_binade(double s) {
+    return (int)((__double_as_longlong(s) >> 52) & 0x7ff) - 1023;
+}
+
+// ------------------------------------------------------------- (1) + (2)
+// Distances of every row to the newest centroid (row chosen[it-1]), the
+// running minimum, and the max of the minima (positive doubles order as their
+// bit patterns; the reference's max starts at 0 with '>', so only m > 0 count).
+template <int METRIC>
+__global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const float* __restrict__ X, int64_t N, int d,
+                                                               const int32_t* __restrict__ chosen, int it,
+                                                               double* __restrict__ mind,
+                                                               unsigned long long* __restrict__ mx_bits) {
+    extern __shared__ double crow[];
+    const int64_t src = chosen[it - 1];
+    for (int j = threadIdx.x; j < d; j += KPP_THREADS) crow[j] = (double)X[src * d + j];
+    __syncthreads();
+    double best = 0.0;
+    for (int64_t n = (int64_t)blockIdx.x * KPP_THREADS + threadIdx.x; n < N; n += (int64_t)gridDim.x * KPP_THREADS) {
+        const float* x = X + n * d;
+        const double dd = METRIC == 0 ? exact_euclid(x, crow, d) : exact_cosine(x, crow, d);
+        double m = dd;
+        if (it > 1) {
+            const double prev = mind[n];
+            if (!(dd < prev)) m = prev;
+        }
+        mind[n] = m;
+        if (m > best) best = m;
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double o = __shfl_xor(best, off);
+        if (o > best) best = o;
+    }
+    if ((threadIdx.x & 63) == 0 && best > 0.0) atomicMax(mx_bits, (unsigned long long)__double_as_longlong(best));
+}
+
+// --------------------------------------------------------------------- (3)
+__device__ inline double block_sum_f64(double v, double* red) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int i = 0; i < KPP_THREADS / 64; i++) t += red[i];
+    return t;
+}
+
+__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_sum_kernel(const double* __restrict__ mind, int64_t N,
+                                                                    const unsigned long long* __restrict__ mx_bits,
+                                                                    double* __restrict__ chunk_sum) {
+    __shared__ double red[KPP_THREADS / 64];
+    const double mx = kpp_max(mx_bits);
+    const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
+    double v = 0.0;
+    for (int e = threadIdx.x; e < KPP_CHUNK; e += KPP_THREADS)
+        if (c0 + e < N) v += kpp_q(mind[c0 + e], mx);
+    const double t = block_sum_f64(v, red);
+    if (threadIdx.x == 0) chunk_sum[blockIdx.x] = t;
+}
+
+// Exclusive scan of the approximate chunk sums (one block; order irrelevant).
+__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_scan_kernel(const double* __restrict__ chunk_sum, int64_t nch,
+                                                                     double* __restrict__ chunk_start) {
+    __shared__ double part[KPP_THREADS];
+    const int64_t per = (nch + KPP_THREADS - 1) / KPP_THREADS;
+    const int64_t lo = threadIdx.x * per, hi = lo + per < nch ? lo + per : nch;
+    double v = 0.0;
+    for (int64_t c = lo; c < hi; c++) v += chunk_sum[c];
+    part[threadIdx.x] = v;
+    __syncthreads();
+    double run = 0.0;
+    for (int i = 0; i < (int)threadIdx.x; i++) run += part[i];
+    for (int64_t c = lo; c < hi; c++) {
+        chunk_start[c] = run;
+        run += chunk_sum[c];
+    }
+}
+
+// RN_u(q) in units of u = 2^(e-52), or -1 if q cannot be resolved in binade e
+// (non-finite, q >= 2^(e+1), or an exact tie).
+__device__ inline int64_t kpp_units(double q, int e) {
+    if (!(q >= 0.0) || !(q < __longlong_as_double((long long)(e + 1 + 1023) << 52))) return -1;
+    const double t = ldexp(q, 52 - e);          // exact: t < 2^53
+    const double r = floor(t);
+    const double f = t - r;                     // exact
+    if (f == 0.5) return -1;
+    return (int64_t)r + (f > 0.5 ? 1 : 0);
+}
+
+struct KppChunk {
+    int64_t R;     // sum of the chunk's RN_u(q) in units of 2^(e-52)
+    int32_t e;     // guessed binade, or KPP_DIRTY
+    int32_t pad;
+};
+
+__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const double* __restrict__ mind, int64_t N,
+                                                                      const unsigned long long* __restrict__ mx_bits,
+                                                                      const double* __restrict__ chunk_start,
+                                                                      KppChunk* __restrict__ meta) {
+    __shared__ long long red[KPP_THREADS / 64];
+    const double mx = kpp_max(mx_bits);
+    const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
+    const double a = chunk_start[blockIdx.x];
+    // a guess only; tiny or non-finite starts are left to the exact walk
+    const bool usable = a >= 0x1p-900 && a < 0x1p62;
+    const int e = usable ? kpp_binade(a) : 0;
+    long long acc = usable ? 0 : -1;
+    for (int i = threadIdx.x; i < KPP_CHUNK && acc >= 0; i += KPP_THREADS) {
+        if (c0 + i >= N) break;
+        const int64_t r = kpp_units(kpp_q(mind[c0 + i], mx), e);
+        acc = r < 0 ? -1 : acc + r;
+    }
+    // any lane's -1 makes the chunk dirty
+    long long v = acc;
+    for (int off = 32; off >= 1; off >>= 1) {
+        const long long o = __shfl_xor(v, off);
+        v = (v < 0 || o < 0) ? -1 : v + o;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int w = 0; w < KPP_THREADS / 64; w++) t = (t < 0 || red[w] < 0) ? -1 : t + red[w];
+        KppChunk m;
+        m.R = t < 0 ? 0 : t;
+        m.e = t < 0 ? KPP_DIRTY : e;
+        m.pad = 0;
+        meta[blockIdx.x] = m;
+    }
+}
+
+// The exact walk (one wave). s is uniform across the wave.
+__global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict__ mind, int64_t N,
+                                                       const unsigned long long* __restrict__ mx_bits,
+                                                       const KppChunk* __restrict__ meta, int64_t nch,
+                                                       double* __restrict__ chunk_s, int32_t* __restrict__ chunk_mode,
+                                                       double* __restrict__ cum, unsigned long long* __restrict__ stats) {
+    __shared__ double qs[KPP_CHUNK];
+    const int lane = threadIdx.x;
+    const double mx = kpp_max(mx_bits);
+    double s = 0.0;
+    int64_t base = 0;
+    unsigned long long nseq = 0;
+    while (base < nch) {
+        const int64_t j = base + lane;
+        const bool valid = j < nch;
+        KppChunk m;
+        m.R = 0; m.e = KPP_DIRTY;
+        if (valid) m = meta[j];
+        const bool s_ok = s >= 0x1p-900 && s < 0x1p62;
+        const int es = s_ok ? kpp_binade(s) : 0;
+        const int64_t s_units = s_ok ? (int64_t)ldexp(s, 52 - es) : 0;
+        // inclusive prefix of R over the lanes
+        int64_t pre = m.R;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t o = __shfl_up(pre, off);
+            if (lane >= off) pre += o;
+        }
+        const bool good = valid && s_ok && m.e == es && s_units + pre < KPP_TWO53;
+        const unsigned long long bad = __ballot(!good);
+        const int f = bad ? __ffsll((long long)bad) - 1 : 64;
+        if (lane < f) {
+            chunk_s[j] = ldexp((double)(s_units + pre - m.R), es - 52);
+            chunk_mode[j] = 0;
+        }
+        if (f > 0) {
+            const int64_t adv = __shfl(pre, f - 1);
+            s = ldexp((double)(s_units + adv), es - 52);
+        }
+        if (f == 64) {
+            base += 64;
+            continue;
+        }
+        const int64_t c = base + f;
+        if (c >= nch) break;
+        // chunk c element by element with hardware fp64 adds, as :122-125
+        const int64_t r0 = c * KPP_CHUNK;
+        const int n = (int)(N - r0 < KPP_CHUNK ? N - r0 : KPP_CHUNK);
+        for (int i = lane; i < n; i += 64) qs[i] = kpp_q(mind[r0 + i], mx);
+        wave_sync();
+        if (lane == 0) {
+            chunk_s[c] = s;
+            chunk_mode[c] = 1;
+            int i = 0;
+            for (; i + 8 <= n; i += 8) {
+                double v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[k] = qs[i + k];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    // the reference's first element is q_0 itself: 0 + q_0 = q_0
+                    s = __dadd_rn(v[k], s);
+                    cum[r0 + i + k] = s;
+                }
+            }
+            for (; i < n; i++) {
+                s = __dadd_rn(qs[i], s);
+                cum[r0 + i] = s;
+            }
+        }
+        s = __shfl(s, 0);
+        wave_sync();
+        base = c + 1;
+        nseq++;
+    }
+    if (lane == 0 && stats) {
+        atomicAdd(stats + STAT_KPP_CHUNKS, (unsigned long long)nch);
+        atomicAdd(stats + STAT_KPP_SEQ, nseq);
+    }
+}
+
+// s_m = s_start + u * (inclusive prefix of RN_u(q)) for the integer-resolved chunks.
+__global__ __launch_bounds__(KPP_THREADS) void kpp_expand_kernel(const double* __restrict__ mind, int64_t N,
+                                                                 const unsigned long long* __restrict__ mx_bits,
+                                                                 const KppChunk* __restrict__ meta,
+                                                                 const double* __restrict__ chunk_s,
+                                                                 const int32_t* __restrict__ chunk_mode,
+                                                                 double* __restrict__ cum) {
+    constexpr int PER = KPP_CHUNK / KPP_THREADS;
+    __shared__ long long wsum[KPP_THREADS / 64];
+    if (chunk_mode[blockIdx.x] != 0) return;
+    const double mx = kpp_max(mx_bits);
+    const int e = meta[blockIdx.x].e;
+    const int64_t s_units = (int64_t)ldexp(chunk_s[blockIdx.x], 52 - e);
+    const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
+    // thread t owns rows c0 + t*PER .. +PER-1 (contiguous, so the scan is in row order)
+    int64_t r[PER];
+    int64_t own = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int64_t row = c0 + threadIdx.x * PER + k;
+        r[k] = row < N ? kpp_units(kpp_q(mind[row], mx), e) : 0;
+        own += r[k];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t pre = own;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t o = __shfl_up(pre, off);
+        if (lane >= off) pre += o;
+    }
+    if (lane == 63) wsum[w] = pre;
+    __syncthreads();
+    int64_t run = s_units + pre - own;
+    for (int i = 0; i < w; i++) run += wsum[i];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int64_t row = c0 + threadIdx.x * PER + k;
+        run += r[k];
+        if (row < N) cum[row] = ldexp((double)run, e - 52);
+    }
+}
+
+// --------------------------------------------------------------------- (4)
+__global__ void kpp_choose_kernel(const double* __restrict__ cum, int64_t N, const double* __restrict__ canon, int it,
+                                  int32_t* __restrict__ chosen) {
+    // uniform_real_distribution<double>(0, total): canon * (b - a) + a
+    const double total = cum[N - 1];
+    const double rd = __dadd_rn(__dmul_rn(canon[it], __dsub_rn(total, 0.0)), 0.0);
+    int64_t left = 0, right = N - 1, pick = 0;
+    if (rd > cum[left]) {
+        while (right - left > 1) {
+            const int64_t m = left + (right - left) / 2;
+            if (rd <= cum[m]) right = m;
+            else left = m;
+        }
+        pick = right;
+    }
+    chosen[it] = (int32_t)pick;
+}
+
+// Runs iterations 1..K-1; chosen[0] and canon[1..K-1] are already on the device.
+// ws: mind[N] f64, cum[N] f64, then per chunk sum/start f64, meta, s_start f64,
+// mode i32, and the max word.
+int launch_kmeans_pp(hipStream_t s, const float* X, int64_t N, int d, int K, int metric, const double* canon,
+                     int32_t* chosen, void* ws, unsigned long long* stats) {
+    const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
+    char* p = (char*)ws;
+    double* mind = (double*)p;                 p += sizeof(double) * N;
+    double* cum = (double*)p;                  p += sizeof(double) * N;
+    double* csum = (double*)p;                 p += sizeof(double) * nch;
+    double* cstart = (double*)p;               p += sizeof(double) * nch;
+    KppChunk* meta = (KppChunk*)p;             p += sizeof(KppChunk) * nch;
+    double* cs = (double*)p;                   p += sizeof(double) * nch;
+    int32_t* mode = (int32_t*)p;               p += sizeof(int32_t) * ((nch + 1) & ~1ll);
+    unsigned long long* mx = (unsigned long long*)p;
+    const unsigned dgrid = gsz(N, KPP_THREADS, 4096);
+    const size_t lds = sizeof(double) * (size_t)d;
+    for (int it = 1; it < K; it++) {
+        if (hipMemsetAsync(mx, 0, sizeof(*mx), s) != hipSuccess) return kstatus("kmeanspp.hip");
+        if (metric == 0)
+            hipLaunchKernelGGL(kpp_dist_kernel<0>, dim3(dgrid), dim3(KPP_THREADS), lds, s, X, N, d, chosen, it, mind, mx);
+        else
+            hipLaunchKernelGGL(kpp_dist_kernel<1>, dim3(dgrid), dim3(KPP_THREADS), lds, s, X, N, d, chosen, it, mind, mx);
+        hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum);
+        hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_THREADS), 0, s, csum, nch, cstart);
+        hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, cstart,
+                           meta);
+        hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, mind, N, mx, meta, nch, cs, mode, cum, stats);
+        hipLaunchKernelGGL(kpp_expand_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, meta, cs, mode,
+                           cum);
+        hipLaunchKernelGGL(kpp_choose_kernel, dim3(1), dim3(1), 0, s, cum, N, canon, it, chosen);
+        const int rc = kstatus("kmeanspp.hip");
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+size_t kmeans_pp_ws_bytes(int64_t N) {
+    const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
+    return sizeof(double) * 2 * (size_t)N + (sizeof(double) * 3 + sizeof(KppChunk)) * (size_t)nch +
+           sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64;
+}
+
+}  // namespace lshkm

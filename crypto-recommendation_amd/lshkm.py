@@ -86,6 +86,8 @@ def lib():
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
             "lshkm_kmeans_partial_carry": (i32, [vp, vp, i64, i32, vp, i32, vp, vp, vp, vp]),
             "lshkm_kmeans_finalize": (i32, [vp, vp, vp, i32, i32, vp, i32, f64, vp, C.POINTER(i32)]),
+            "lshkm_kmeans_pp": (i32, [vp, vp, i64, i32, i32, i32, u64, vp]),
+            "lshkm_rand_selection": (i32, [u64, i64, i32, vp]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
         }
         for name, (res, args) in sigs.items():
@@ -399,6 +401,21 @@ def kmeans_finalize(ctx, sums, counts, C_old, metric="euclidean", min_dist=0.0):
     return Cn, bool(cont.value)
 
 
+def kmeans_pp_rows(ctx, X, K, metric="euclidean", seed=1):
+    """k_means_pp (initialization.hpp:71-156): the K chosen dataset rows (int32 numpy)."""
+    N, d = X.shape
+    rows = np.empty(K, np.int32)
+    _ck(lib().lshkm_kmeans_pp(ctx.h, _t_ptr(X), N, d, K, _METRIC[metric], int(seed), _np_ptr(rows)))
+    return rows
+
+
+def rand_selection_rows(N, K, seed=1):
+    """rand_selection (initialization.hpp:39-69): K distinct rows (host only)."""
+    rows = np.empty(K, np.int32)
+    _ck(lib().lshkm_rand_selection(int(seed), int(N), int(K), _np_ptr(rows)))
+    return rows
+
+
 # ------------------------------------------------- reference-named mirrors
 def create_LSH_hashtables(ctx, X, metric_type, k, L, lsh_bucket_div, euclidean_h_w, seed):
     """create_LSH_hashtables (lsh_cube.hpp:44-74) with an explicit seed in place of the clock."""
@@ -444,3 +461,12 @@ def lloyds_assignment(ctx, X, centroids, metric_type, src_rows=None):
 
 def k_means(ctx, X, assign, centers, metric_type, min_dist):
     return kmeans_update(ctx, X, assign, centers, metric_type, min_dist)
+
+
+def k_means_pp(ctx, X, cluster_num, metric_type, seed):
+    """k_means_pp with an explicit seed: the chosen rows (centroids[i] = X[rows[i]])."""
+    return kmeans_pp_rows(ctx, X, cluster_num, metric_type, seed)
+
+
+def rand_selection(N, cluster_num, seed):
+    return rand_selection_rows(N, cluster_num, seed)

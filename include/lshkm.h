@@ -66,7 +66,8 @@ int lshkm_dev_free(lshkm_ctx ctx, void* p_dev);
 int lshkm_memcpy_h2d(lshkm_ctx ctx, void* dst_dev, const void* src_host, int64_t bytes);
 int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t bytes);
 /* Counters: 0 = hash values resolved by the exact soft-x87 path,
- * 1 = points whose argmin needed the exact all-centroid pass. */
+ * 1 = points whose argmin needed the exact all-centroid pass,
+ * 2 = k-means++ prefix-sum chunks walked, 3 = of which summed element by element. */
 int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);
 int lshkm_reset_stats(lshkm_ctx ctx);
 /* HIP-event timing of the dominant kernel launch (the fused hash+assign kernel)
@@ -209,6 +210,19 @@ int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X_dev, int64_t N, int
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* counts_dev, int K, int d,
                           const double* C_old_dev, int metric, double min_dist, double* C_new_dev,
                           int* cont_host);
+
+/* ----------------------------------------------------------- initialization
+ * k_means_pp (initialization.hpp:71-156): the K dataset rows chosen as initial
+ * centroids (centroids[i] = &input_vectors[rows_host[i]]), with
+ * std::default_random_engine seeded with `seed` (the reference reads the
+ * clock). D^2 seeding with the reference's exact distances, (min/max)^2
+ * prefix sums in row order and its binary search. Assumes unique vector IDs
+ * (the reference's distance cache is keyed by them). N < 2^31, d <= 4096. */
+int lshkm_kmeans_pp(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, int K, int metric, uint64_t seed,
+                    int32_t* rows_host);
+/* rand_selection (initialization.hpp:39-69): K distinct rows drawn uniformly,
+ * redrawing on a repeat. Host only. 1 <= K <= N. */
+int lshkm_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows_host);
 
 /* ------------------------------------------------------------ synthetic data */
 /* include/lshkm_synth.h generator, rows [row0, row0+rows) into X_dev. */

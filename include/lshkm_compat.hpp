@@ -16,6 +16,8 @@
  *   create_hypercube        lib/lsh_cube.hpp:108-136
  *   lloyds_assignment       lib/clustering_phases/assignment.hpp:54-80
  *   k_means                 lib/clustering_phases/update.hpp:37-86
+ *   k_means_pp              lib/clustering_phases/initialization.hpp:71-156
+ *   rand_selection          lib/clustering_phases/initialization.hpp:39-69
  *
  * Same signatures, same return values and the same ownership as the
  * reference: the hashtables are real CustHashtable objects (the caller deletes
@@ -449,6 +451,46 @@ bool k_means(std::vector<CustVector<T>>& input_vectors, std::vector<CustVector<T
         centers[c] = new CustVector<T>("k_means_center", dims);
     }
     return true;
+}
+
+// ------------------------------------------------------------ initialization
+// k_means_pp (initialization.hpp:71-156): pointers to the chosen input vectors.
+// Vector IDs must be unique (the reference's distance cache is keyed by them).
+template <typename T>
+std::vector<CustVector<T>*> k_means_pp(std::vector<CustVector<T>>& input_vectors, int cluster_num,
+                                       std::string metric_type, unsigned long seed) {
+    const int metric = metric_of(metric_type);
+    if (input_vectors.empty() || cluster_num < 1) throw std::invalid_argument("lshkm_compat: empty input or K < 1");
+    const size_t N = input_vectors.size(), d = input_vectors[0].getDimensions()->size();
+    std::vector<float> X = pack_rows(input_vectors, d);
+    DevMem Xd = upload(X.data(), X.size());
+    std::vector<int32_t> rows(cluster_num);
+    check(lshkm_kmeans_pp(context(), Xd.as<float>(), (int64_t)N, (int)d, cluster_num, metric, seed, rows.data()));
+    std::vector<CustVector<T>*> centroids(cluster_num);
+    for (int i = 0; i < cluster_num; i++) centroids[i] = &input_vectors[rows[i]];
+    return centroids;
+}
+
+template <typename T>
+std::vector<CustVector<T>*> k_means_pp(std::vector<CustVector<T>>& input_vectors, int cluster_num,
+                                       std::string metric_type) {
+    return k_means_pp(input_vectors, cluster_num, metric_type, clock_seed());
+}
+
+// rand_selection (initialization.hpp:39-69).
+template <typename T>
+std::vector<CustVector<T>*> rand_selection(std::vector<CustVector<T>>& input_vectors, int cluster_num,
+                                           unsigned long seed) {
+    std::vector<int32_t> rows(cluster_num > 0 ? cluster_num : 0);
+    check(lshkm_rand_selection(seed, (int64_t)input_vectors.size(), cluster_num, rows.data()));
+    std::vector<CustVector<T>*> centroids(cluster_num);
+    for (int i = 0; i < cluster_num; i++) centroids[i] = &input_vectors[rows[i]];
+    return centroids;
+}
+
+template <typename T>
+std::vector<CustVector<T>*> rand_selection(std::vector<CustVector<T>>& input_vectors, int cluster_num) {
+    return rand_selection(input_vectors, cluster_num, clock_seed());
 }
 
 }  // namespace lshkm_compat

@@ -1,7 +1,7 @@
 // compat_check.cpp — runs the REFERENCE's own functions and the C++ drop-in
 // (include/lshkm_compat.hpp, GPU-backed) side by side on the same data and
 // seed, through the reference's own interface, and compares everything the
-// caller can observe. TEST INFRASTRUCTURE ONLY (tests/test_gpu_compat.py).
+// caller can observe. TEST INFRASTRUCTURE ONLY (tests/test_compat.py).
 //
 // Built by oracle/Makefile into oracle/_ref/ (git-ignored) from this file, the
 // reference's headers/sources where they lie and liblshkm.so; g++ -O0 as the
@@ -34,6 +34,7 @@ system_clock::time_point system_clock::now() noexcept {
 #include "lsh_cube.hpp"
 #include "clustering_phases/assignment.hpp"
 #include "clustering_phases/update.hpp"
+#include "clustering_phases/initialization.hpp"
 
 #include "../include/lshkm_compat.hpp"
 #include "../include/lshkm_synth.h"
@@ -128,6 +129,14 @@ static void check_cube(std::vector<Vec>& data, const std::string& metric, int k,
     delete gpu;
 }
 
+static void check_init(std::vector<Vec>& data, const std::string& metric, int K) {
+    g_seed += 303;
+    const std::string tag = "init/" + metric + " ";
+    if (k_means_pp(data, K, metric) != lshkm_compat::k_means_pp(data, K, metric)) fail(tag + "k_means_pp");
+    if (rand_selection(data, K) != lshkm_compat::rand_selection(data, K)) fail(tag + "rand_selection");
+    g_stat["init_" + metric + "_calls"]++;
+}
+
 static void check_kmeans(std::vector<Vec>& data, const std::string& metric, int K) {
     std::vector<Vec> a = data, b = data;
     std::vector<Vec*> ca, cb;
@@ -178,6 +187,8 @@ int main(int argc, char** argv) {
         check_cube(data, "cosine", 5, 4.0);
         check_kmeans(data, "euclidean", K);
         check_kmeans(data, "cosine", K);
+        check_init(data, "euclidean", K);
+        check_init(data, "cosine", K);
     } catch (const std::exception& e) {
         std::printf("EXCEPTION %s\n", e.what());
         return 1;

@@ -418,6 +418,72 @@ int or_kmeans_update(int64_t N, int d, int K, const float* X, const int32_t* ass
     return 0;
 }
 
+/* ------------------------------------------------------------ initialization */
+
+/* rand_selection (initialization.hpp:39-69): uniform rows, redrawn (and all
+ * earlier picks re-checked) on a repeat. IDs are unique, so ID equality is
+ * row equality. */
+void or_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows) {
+    uint32_t s = or_minstd_seed(seed);
+    rows[0] = or_uniform_int(&s, 0, (int)(N - 1));
+    for (int i = 1; i < K; i++) {
+        int r = or_uniform_int(&s, 0, (int)(N - 1)), c = 0;
+        while (c < i) {
+            if (rows[c] == r) { r = or_uniform_int(&s, 0, (int)(N - 1)); c = 0; }
+            else c++;
+        }
+        rows[i] = r;
+    }
+}
+
+/* k_means_pp (initialization.hpp:71-156), row by row as the reference: min
+ * over centroids 0..i-1 with the -1 sentinel and strict '<' (the ID-keyed
+ * cache only memoises), max with strict '>' from 0, (min/max)^2 prefix-summed
+ * in row order, uniform_real<double>(0, total) = canon * (total - 0) + 0, and
+ * the custom binary search (:134-149). */
+void or_kmeans_pp(int64_t N, int d, int K, const float* X, int metric, uint64_t seed, int32_t* rows) {
+    uint32_t s = or_minstd_seed(seed);
+    double* md = (double*)malloc(sizeof(double) * (size_t)N);
+    double* cs = (double*)malloc(sizeof(double) * (size_t)K * d);
+    rows[0] = or_uniform_int(&s, 0, (int)(N - 1));
+    for (int i = 1; i < K; i++) {
+        for (int j = 0; j < d; j++) cs[(size_t)(i - 1) * d + j] = (double)X[(size_t)rows[i - 1] * d + j];
+        double mx = 0;
+#pragma omp parallel for schedule(static)
+        for (int64_t n = 0; n < N; n++) {
+            double mn = -1;
+            for (int c = 0; c < i; c++) {
+                const double dd = metric == 0 ? or_euclid_dist_f32_f64(X + n * d, cs + (size_t)c * d, d)
+                                              : cosine_dist_f32_f64(X + n * d, cs + (size_t)c * d, d);
+                if (mn == -1 || dd < mn) mn = dd;
+            }
+            md[n] = mn;
+        }
+        for (int64_t n = 0; n < N; n++)
+            if (md[n] > mx) mx = md[n];
+        md[0] = md[0] / mx;
+        md[0] = md[0] * md[0];
+        for (int64_t n = 1; n < N; n++) {
+            md[n] = md[n] / mx;
+            md[n] = md[n] * md[n];
+            md[n] = md[n] + md[n - 1];
+        }
+        const double rd = canon_d(&s) * (md[N - 1] - 0.0) + 0.0;
+        int64_t left = 0, right = N - 1, pick = 0;
+        if (rd > md[left]) {
+            while (right - left > 1) {
+                const int64_t m = left + (right - left) / 2;
+                if (rd <= md[m]) right = m;
+                else left = m;
+            }
+            pick = right;
+        }
+        rows[i] = (int32_t)pick;
+    }
+    free(md);
+    free(cs);
+}
+
 void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out) {
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < rows; i++)

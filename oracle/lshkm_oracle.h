@@ -81,6 +81,10 @@ double or_euclid_dist_f32_f64(const float* x, const double* c, int d);
 int or_kmeans_update(int64_t N, int d, int K, const float* X, const int32_t* assign,
                      const double* C_old, int metric, double min_dist, double* C_new, int64_t* counts);
 
+/* ---- initialization (initialization.hpp:39-156): the chosen dataset rows */
+void or_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows);
+void or_kmeans_pp(int64_t N, int d, int K, const float* X, int metric, uint64_t seed, int32_t* rows);
+
 /* ---- synthetic points (include/lshkm_synth.h) */
 void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out);
 

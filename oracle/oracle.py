@@ -51,6 +51,8 @@ def lib():
             "or_lloyd_assign": (None, [C.c_int64, C.c_int, C.c_int, f32p, f64p, C.c_int, C.c_void_p, i32p, f64p]),
             "or_kmeans_update": (C.c_int, [C.c_int64, C.c_int, C.c_int, f32p, i32p, f64p, C.c_int, C.c_double,
                                            f64p, i64p]),
+            "or_rand_selection": (None, [C.c_uint64, C.c_int64, C.c_int, i32p]),
+            "or_kmeans_pp": (None, [C.c_int64, C.c_int, C.c_int, f32p, C.c_int, C.c_uint64, i32p]),
             "or_synth": (None, [C.c_uint64, C.c_int64, C.c_int64, C.c_int, f32p]),
         }
         for name, (res, args) in sig.items():
@@ -194,3 +196,19 @@ def kmeans_update(X, assign, C_old, metric="euclidean", min_dist=0.0):
                                   np.ascontiguousarray(C_old, np.float64), 0 if metric == "euclidean" else 1,
                                   float(min_dist), Cn, cnt)
     return Cn, cnt, bool(cont)
+
+
+def kmeans_pp(X, K, metric="euclidean", seed=1):
+    """k_means_pp (initialization.hpp:71-156): the chosen rows."""
+    X = np.ascontiguousarray(X, np.float32)
+    N, d = X.shape
+    rows = np.empty(K, np.int32)
+    lib().or_kmeans_pp(N, d, K, X, 0 if metric == "euclidean" else 1, int(seed), rows)
+    return rows
+
+
+def rand_selection(N, K, seed=1):
+    """rand_selection (initialization.hpp:39-69): the chosen rows."""
+    rows = np.empty(K, np.int32)
+    lib().or_rand_selection(int(seed), int(N), int(K), rows)
+    return rows

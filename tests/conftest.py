@@ -25,6 +25,13 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 
 
+def kpp_input(name):
+    """Input rows of a k-means++ golden case (tests/golden/make_golden.py:kpp_data)."""
+    import oracle
+    m = golden_meta()[name]
+    return oracle.synth(m["data_seed"], m["N"], m["d"])[np.arange(m["N"]) // m.get("dup", 1)]
+
+
 def cases(kind):
     return sorted(n for n, m in golden_meta().items() if m["kind"] == kind)
 

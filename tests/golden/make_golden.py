@@ -10,7 +10,8 @@ include/lshkm_synth.h at the (seed, rows, d) recorded in cases.json, except
 external fp64 centroids, which are stored.
 
 Only runs in the build container (the reference is absent on the GPU box).
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp]
+(--only regenerates those kinds and keeps the other cases' entries.)
 """
 import json
 import os
@@ -53,8 +54,14 @@ LLOYD_CASES = [
     ("lloyd_conv", 400, 16, 4, "euclidean", 6, 1e9, 15, "rows"),
 ]
 KPP_CASES = [
-    # name, N, d, K, metric, seed, data_seed   (config 1 plumbing: 1k x d=16, K=8)
-    ("kpp_c1", 1000, 16, 8, "cosine", 2024, 16),
+    # name, N, d, K, metric, seed, data_seed, dup   (config 1 plumbing: 1k x d=16, K=8)
+    # dup g: row i is synth row i // g (repeated points: zero distances, repeat picks)
+    ("kpp_c1", 1000, 16, 8, "cosine", 2024, 16, 1),
+    ("kpp_e1", 1000, 16, 8, "euclidean", 2025, 17, 1),
+    ("kpp_e128", 3000, 128, 32, "euclidean", 2026, 18, 1),
+    ("kpp_e_big", 40000, 8, 12, "euclidean", 2027, 19, 1),
+    ("kpp_dup", 2000, 16, 24, "euclidean", 2028, 20, 4),
+    ("kpp_c128", 2000, 128, 16, "cosine", 2029, 21, 1),
 ]
 
 
@@ -74,13 +81,22 @@ def ext_centers(seed, K, d):
     return base * (1.0 + 1e-3 * np.sin(1.0 + j * 0.7 + c * 1.3)) + 1e-4 * np.cos(j + c)
 
 
-def main():
+def kpp_data(dseed, N, d, dup):
+    """Inputs of a k-means++ case (tests rebuild them the same way)."""
+    return oracle.synth(dseed, N, d)[np.arange(N) // dup]
+
+
+def main(only=None):
     if not os.path.exists(HARNESS):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     meta = {}
+    if only:
+        with open(os.path.join(HERE, "cases.json")) as f:
+            meta = {k: v for k, v in json.load(f).items() if v["kind"] not in only}
+    want = (lambda kind: only is None or kind in only)
     tmp = tempfile.mkdtemp()
     try:
-        for (name, N, d, metric, k, L, div, w, seed, dseed, nqrows, Q) in LSH_CASES:
+        for (name, N, d, metric, k, L, div, w, seed, dseed, nqrows, Q) in (LSH_CASES if want("lsh") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
             x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
             q = oracle.synth(dseed + 1000, Q, d); q.tofile(os.path.join(tmp, "q.f32"))
@@ -90,7 +106,7 @@ def main():
             meta[name] = dict(kind="lsh", N=N, d=d, metric=metric, k=k, L=L, div=div, w=w, seed=seed,
                               data_seed=dseed, query_seed=dseed + 1000, nqrows=nqrows, Q=Q,
                               nb=(N // div) if metric == "euclidean" else 2 ** k)
-        for (name, N, d, metric, k, w, seed, dseed, probes, nqrows, Q) in CUBE_CASES:
+        for (name, N, d, metric, k, w, seed, dseed, probes, nqrows, Q) in (CUBE_CASES if want("cube") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
             x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
             q = oracle.synth(dseed + 1000, Q, d); q.tofile(os.path.join(tmp, "q.f32"))
@@ -100,7 +116,7 @@ def main():
             meta[name] = dict(kind="cube", N=N, d=d, metric=metric, k=k, w=w, seed=seed, data_seed=dseed,
                               query_seed=dseed + 1000, probes=[int(p) for p in probes.split(",")],
                               nqrows=nqrows, Q=Q)
-        for (name, N, d, K, metric, iters, min_dist, dseed, init) in LLOYD_CASES:
+        for (name, N, d, K, metric, iters, min_dist, dseed, init) in (LLOYD_CASES if want("lloyd") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
             x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
             args = ["lloyd", os.path.join(tmp, "x.f32"), N, d, K, metric, iters, repr(min_dist), out]
@@ -117,12 +133,12 @@ def main():
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
             meta[name] = dict(kind="lloyd", N=N, d=d, K=K, metric=metric, iters=iters, min_dist=min_dist,
                               data_seed=dseed, init=init)
-        for (name, N, d, K, metric, seed, dseed) in KPP_CASES:
+        for (name, N, d, K, metric, seed, dseed, dup) in (KPP_CASES if want("kmeanspp") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
-            x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
+            x = kpp_data(dseed, N, d, dup); x.tofile(os.path.join(tmp, "x.f32"))
             run(["kmeanspp", os.path.join(tmp, "x.f32"), N, d, K, metric, seed, out])
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
-            meta[name] = dict(kind="kmeanspp", N=N, d=d, K=K, metric=metric, seed=seed, data_seed=dseed)
+            meta[name] = dict(kind="kmeanspp", N=N, d=d, K=K, metric=metric, seed=seed, data_seed=dseed, dup=dup)
     finally:
         shutil.rmtree(tmp)
     with open(os.path.join(HERE, "cases.json"), "w") as f:
@@ -132,4 +148,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    only = None
+    if len(sys.argv) > 2 and sys.argv[1] == "--only":
+        only = set(sys.argv[2].split(","))
+    main(only)

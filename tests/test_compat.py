@@ -25,6 +25,7 @@ def test_shim_compiles_against_reference_headers(tmp_path):
         '#include "lsh_cube.hpp"\n'
         '#include "clustering_phases/assignment.hpp"\n'
         '#include "clustering_phases/update.hpp"\n'
+        '#include "clustering_phases/initialization.hpp"\n'
         '#include "lshkm_compat.hpp"\n'
         "template std::vector<CustHashtable<double>*> lshkm_compat::create_LSH_hashtables<double>(\n"
         "    std::vector<CustVector<double>>&, const std::string, int, int, int, double);\n"
@@ -34,6 +35,10 @@ def test_shim_compiles_against_reference_headers(tmp_path):
         "    std::vector<CustVector<double>*>&, std::string);\n"
         "template bool lshkm_compat::k_means<double>(std::vector<CustVector<double>>&,\n"
         "    std::vector<CustVector<double>*>&, std::string, double);\n"
+        "template std::vector<CustVector<double>*> lshkm_compat::k_means_pp<double>(\n"
+        "    std::vector<CustVector<double>>&, int, std::string);\n"
+        "template std::vector<CustVector<double>*> lshkm_compat::rand_selection<double>(\n"
+        "    std::vector<CustVector<double>>&, int);\n"
         "template class lshkm_compat::GpuLshGenerator<float>;\n"
         "template class lshkm_compat::GpuCubeGenerator<int>;\n")
     r = subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Wno-unused-function", "-I", REF_LIB,

@@ -66,6 +66,18 @@ def test_params_cube_match_reference(name):
         assert np.array_equal(R.view(np.uint64), g["R"].view(np.uint64))
 
 
+@pytest.mark.parametrize("name", cases("kmeanspp"))
+def test_rand_selection_matches_reference(name):
+    # host-only entry point (lshkm_rand_selection): no GPU needed
+    m = META[name]
+    assert np.array_equal(lshkm.rand_selection_rows(m["N"], m["K"], m["seed"]), golden(name)["rand_rows"])
+
+
+def test_rand_selection_rejects_k_above_n():
+    with pytest.raises(lshkm.LshkmError):
+        lshkm.rand_selection_rows(3, 4, 1)      # the reference would loop forever
+
+
 def test_params_bad_arguments_fail_loudly():
     with pytest.raises(lshkm.LshkmError):
         lshkm.params_lsh_euclidean(1, 0, 4, 128, 0.4)

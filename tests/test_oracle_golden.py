@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import cases, golden, golden_meta
+from conftest import cases, golden, golden_meta, kpp_input
 
 META = golden_meta()
 
@@ -124,6 +124,14 @@ def test_lloyd_and_update(name):
         assert cont == bool(g["cont"][it])
         C = Cn if cont else C
         assert np.array_equal(C.view(np.uint64), g[f"centers{it + 1}"].view(np.uint64)), it
+
+
+@pytest.mark.parametrize("name", cases("kmeanspp"))
+def test_kmeans_pp_and_rand_selection(name):
+    m, g = META[name], golden(name)
+    X = kpp_input(name)
+    assert np.array_equal(oracle.kmeans_pp(X, m["K"], m["metric"], m["seed"]), g["kpp_rows"])
+    assert np.array_equal(oracle.rand_selection(m["N"], m["K"], m["seed"]), g["rand_rows"])
 
 
 def test_probe_sequence_rules():
