@@ -65,19 +65,95 @@ __device__ inline int kpp_binade(double s) {
 // Distances of every row to the newest centroid (row chosen[it-1]), the
 // running minimum, and the max of the minima (positive doubles order as their
 // bit patterns; the reference's max starts at 0 with '>', so only m > 0 count).
-template <int METRIC>
+// A block owns 256 rows (one per thread) and streams them through LDS in
+// slices of KPP_DJ dims, loaded coalesced (consecutive lanes, consecutive
+// floats of a row); each thread then accumulates its row in dim order, exactly
+// as exact.h. The centroid row is read with uniform (scalar) loads.
+// VEC (d % 32 == 0): each slice is 8 float4 per thread, all in flight at
+// once, and the next slice's loads are issued before the current one is
+// consumed (register double buffer).
+constexpr int KPP_DJ = 32;
+constexpr int KPP_V4 = KPP_THREADS * KPP_DJ / 4 / KPP_THREADS;   // float4 per thread per slice (8)
+
+template <int METRIC, bool VEC>
 __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const float* __restrict__ X, int64_t N, int d,
                                                                const int32_t* __restrict__ chosen, int it,
                                                                double* __restrict__ mind,
                                                                unsigned long long* __restrict__ mx_bits) {
-    extern __shared__ double crow[];
-    const int64_t src = chosen[it - 1];
-    for (int j = threadIdx.x; j < d; j += KPP_THREADS) crow[j] = (double)X[src * d + j];
-    __syncthreads();
+    __shared__ float tile[KPP_THREADS][KPP_DJ + 1];
+    const float* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
+    double cb = 0.0;                                    // cosine: sum c^2 (uniform)
+    if (METRIC == 1)
+        for (int j = 0; j < d; j++) {
+            const double cj = (double)c[j];
+            cb = __dadd_rn(cb, __dmul_rn(cj, cj));
+        }
     double best = 0.0;
-    for (int64_t n = (int64_t)blockIdx.x * KPP_THREADS + threadIdx.x; n < N; n += (int64_t)gridDim.x * KPP_THREADS) {
-        const float* x = X + n * d;
-        const double dd = METRIC == 0 ? exact_euclid(x, crow, d) : exact_cosine(x, crow, d);
+    for (int64_t row0 = (int64_t)blockIdx.x * KPP_THREADS; row0 < N; row0 += (int64_t)gridDim.x * KPP_THREADS) {
+        const int64_t n = row0 + threadIdx.x;
+        const int rows = (int)(N - row0 < KPP_THREADS ? N - row0 : KPP_THREADS);
+        double acc = 0.0, a = 0.0;
+        sx80 ip = sx_zero();
+        float4 pf[KPP_V4];
+        if (VEC) {
+#pragma unroll
+            for (int k = 0; k < KPP_V4; k++) {
+                const int idx = k * KPP_THREADS + threadIdx.x, r = idx >> 3, part = idx & 7;
+                if (r < rows) pf[k] = *reinterpret_cast<const float4*>(X + (row0 + r) * d + part * 4);
+            }
+        }
+        for (int j0 = 0; j0 < d; j0 += KPP_DJ) {
+            const int dj = d - j0 < KPP_DJ ? d - j0 : KPP_DJ;
+            __syncthreads();
+            if (VEC) {
+#pragma unroll
+                for (int k = 0; k < KPP_V4; k++) {
+                    const int idx = k * KPP_THREADS + threadIdx.x, r = idx >> 3, part = idx & 7;
+                    if (r < rows) {
+                        tile[r][part * 4 + 0] = pf[k].x;
+                        tile[r][part * 4 + 1] = pf[k].y;
+                        tile[r][part * 4 + 2] = pf[k].z;
+                        tile[r][part * 4 + 3] = pf[k].w;
+                    }
+                }
+            } else {
+#pragma unroll 4
+                for (int e = threadIdx.x; e < KPP_THREADS * KPP_DJ; e += KPP_THREADS) {
+                    const int r = e / KPP_DJ, jj = e % KPP_DJ;
+                    if (r < rows && jj < dj) tile[r][jj] = X[(row0 + r) * d + j0 + jj];
+                }
+            }
+            __syncthreads();
+            if (VEC && j0 + KPP_DJ < d) {
+#pragma unroll
+                for (int k = 0; k < KPP_V4; k++) {
+                    const int idx = k * KPP_THREADS + threadIdx.x, r = idx >> 3, part = idx & 7;
+                    if (r < rows)
+                        pf[k] = *reinterpret_cast<const float4*>(X + (row0 + r) * d + j0 + KPP_DJ + part * 4);
+                }
+            }
+            if (n < N) {
+                for (int jj = 0; jj < dj; jj++) {
+                    const double xj = (double)tile[threadIdx.x][jj];
+                    const double cj = (double)c[j0 + jj];
+                    if (METRIC == 0) {
+                        const double df = __dsub_rn(xj, cj);
+                        acc = __dadd_rn(acc, __dmul_rn(df, df));
+                    } else {
+                        ip = sx_add_double(ip, __dmul_rn(xj, cj));
+                        a = __dadd_rn(a, __dmul_rn(xj, xj));
+                    }
+                }
+            }
+        }
+        if (n >= N) continue;
+        double dd;
+        if (METRIC == 0) {
+            dd = sqrt(acc);
+        } else {
+            const double denom = __dmul_rn(sqrt(a), sqrt(cb));
+            dd = __dsub_rn(1.0, sx_to_double(sx_div(ip, sx_from_double(denom))));
+        }
         double m = dd;
         if (it > 1) {
             const double prev = mind[n];
@@ -119,10 +195,12 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_sum_kernel(const double
 }
 
 // Exclusive scan of the approximate chunk sums (one block; order irrelevant).
-__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_scan_kernel(const double* __restrict__ chunk_sum, int64_t nch,
-                                                                     double* __restrict__ chunk_start) {
-    __shared__ double part[KPP_THREADS];
-    const int64_t per = (nch + KPP_THREADS - 1) / KPP_THREADS;
+constexpr int KPP_SCAN_THREADS = 1024;
+
+__global__ __launch_bounds__(KPP_SCAN_THREADS) void kpp_chunk_scan_kernel(const double* __restrict__ chunk_sum,
+                                                                          int64_t nch, double* __restrict__ chunk_start) {
+    __shared__ double part[KPP_SCAN_THREADS];
+    const int64_t per = (nch + KPP_SCAN_THREADS - 1) / KPP_SCAN_THREADS;
     const int64_t lo = threadIdx.x * per, hi = lo + per < nch ? lo + per : nch;
     double v = 0.0;
     for (int64_t c = lo; c < hi; c++) v += chunk_sum[c];
@@ -182,58 +260,104 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const doub
         long long t = 0;
         for (int w = 0; w < KPP_THREADS / 64; w++) t = (t < 0 || red[w] < 0) ? -1 : t + red[w];
         KppChunk m;
-        m.R = t < 0 ? 0 : t;
-        m.e = t < 0 ? KPP_DIRTY : e;
+        const bool dirty = t < 0 || t >= KPP_TWO53;     // R >= 2^53 cannot stay in the binade
+        m.R = dirty ? 0 : t;
+        m.e = dirty ? KPP_DIRTY : e;
         m.pad = 0;
         meta[blockIdx.x] = m;
     }
 }
 
-// The exact walk (one wave). s is uniform across the wave.
+// The exact walk (one wave). s is uniform across the wave. A step covers
+// 64 lanes x CPL consecutive chunks (lane-local prefix, then a wave scan of
+// the lane totals); R < 2^53 per chunk keeps every prefix below 2^62.
 __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict__ mind, int64_t N,
                                                        const unsigned long long* __restrict__ mx_bits,
                                                        const KppChunk* __restrict__ meta, int64_t nch,
                                                        double* __restrict__ chunk_s, int32_t* __restrict__ chunk_mode,
                                                        double* __restrict__ cum, unsigned long long* __restrict__ stats) {
+    constexpr int CPL = 8;                         // chunks per lane per step
+    constexpr int STEP = 64 * CPL;
+    constexpr int WIN = 2 * STEP;                  // chunk metadata staged in LDS (16 KB)
     __shared__ double qs[KPP_CHUNK];
+    __shared__ KppChunk wm[WIN];
     const int lane = threadIdx.x;
     const double mx = kpp_max(mx_bits);
     double s = 0.0;
-    int64_t base = 0;
+    int64_t base = 0, win0 = -2 * WIN;
     unsigned long long nseq = 0;
     while (base < nch) {
-        const int64_t j = base + lane;
-        const bool valid = j < nch;
-        KppChunk m;
-        m.R = 0; m.e = KPP_DIRTY;
-        if (valid) m = meta[j];
+        if (base < win0 || base + STEP > win0 + WIN) {   // (re)fill the window at base
+            win0 = base;
+            for (int i = lane; i < WIN; i += 64)
+                if (win0 + i < nch) wm[i] = meta[win0 + i];
+            wave_sync();
+        }
         const bool s_ok = s >= 0x1p-900 && s < 0x1p62;
         const int es = s_ok ? kpp_binade(s) : 0;
         const int64_t s_units = s_ok ? (int64_t)ldexp(s, 52 - es) : 0;
-        // inclusive prefix of R over the lanes
-        int64_t pre = m.R;
+        const int64_t j0 = base + (int64_t)lane * CPL;
+        int64_t R[CPL];
+        int lbad = CPL;                            // first chunk of the lane with a wrong guess
+        int64_t tot = 0;
+#pragma unroll
+        for (int t = 0; t < CPL; t++) {
+            const int64_t j = j0 + t;
+            KppChunk m;
+            m.R = 0; m.e = KPP_DIRTY;
+            if (j < nch) m = wm[j - win0];
+            R[t] = m.R;
+            tot += m.R;
+            if (lbad == CPL && !(j < nch && s_ok && m.e == es)) lbad = t;
+        }
+        // exclusive prefix of the lane totals
+        int64_t pre = tot;
         for (int off = 1; off < 64; off <<= 1) {
             const int64_t o = __shfl_up(pre, off);
             if (lane >= off) pre += o;
         }
-        const bool good = valid && s_ok && m.e == es && s_units + pre < KPP_TWO53;
-        const unsigned long long bad = __ballot(!good);
-        const int f = bad ? __ffsll((long long)bad) - 1 : 64;
-        if (lane < f) {
-            chunk_s[j] = ldexp((double)(s_units + pre - m.R), es - 52);
-            chunk_mode[j] = 0;
+        pre -= tot;
+        // the lane's first chunk that is wrong or would leave the binade
+        int first = lbad;
+        int64_t run = s_units + pre;
+#pragma unroll
+        for (int t = 0; t < CPL; t++) {
+            if (t < first && run + R[t] >= KPP_TWO53) first = t;
+            if (t < first) run += R[t];
         }
-        if (f > 0) {
-            const int64_t adv = __shfl(pre, f - 1);
-            s = ldexp((double)(s_units + adv), es - 52);
+        const unsigned long long bad = __ballot(first < CPL);
+        const int fl = bad ? __ffsll((long long)bad) - 1 : 64;       // first lane with a stop
+        // lanes before fl: all CPL chunks resolved; lane fl: its chunks before
+        // `first` (lanes before fl have first == CPL)
+        if (lane <= fl) {
+            int64_t r = s_units + pre;
+#pragma unroll
+            for (int t = 0; t < CPL; t++) {
+                if (t < first) {
+                    chunk_s[j0 + t] = ldexp((double)r, es - 52);
+                    chunk_mode[j0 + t] = 0;
+                    r += R[t];
+                }
+            }
         }
-        if (f == 64) {
-            base += 64;
+        const int fstop = fl < 64 ? __shfl(first, fl) : CPL;
+        const int64_t c = base + (int64_t)(fl < 64 ? fl : 64) * CPL + (fl < 64 ? fstop : 0);
+        // s after the resolved chunks: `run` of lane fl (or of lane 63 if none stopped)
+        const int64_t adv = __shfl(run, fl < 64 ? fl : 63);
+        if (c > base) s = ldexp((double)adv, es - 52);
+        if (fl == 64) {
+            base += STEP;
             continue;
         }
-        const int64_t c = base + f;
         if (c >= nch) break;
-        // chunk c element by element with hardware fp64 adds, as :122-125
+        if (c >= win0 + WIN) {                     // not a stop, just the window's end
+            base = c;
+            continue;
+        }
+        // Stop chunk c, walked element-wise in passes: each pass resolves the
+        // elements that stay in s's binade as integers (EPL per lane), then
+        // adds the stopping element (binade crossing, tie, non-finite) with a
+        // hardware fp64 add as :122-125. Usually 2 passes.
         const int64_t r0 = c * KPP_CHUNK;
         const int n = (int)(N - r0 < KPP_CHUNK ? N - r0 : KPP_CHUNK);
         for (int i = lane; i < n; i += 64) qs[i] = kpp_q(mind[r0 + i], mx);
@@ -241,24 +365,67 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
         if (lane == 0) {
             chunk_s[c] = s;
             chunk_mode[c] = 1;
-            int i = 0;
-            for (; i + 8 <= n; i += 8) {
-                double v[8];
+        }
+        constexpr int EPL = KPP_CHUNK / 64;
+        int p = 0;
+        while (p < n) {
+            // modes: integer units in s's binade; s == 0 (only q == 0 keeps it);
+            // s NaN (stays NaN); s == +inf (stays inf unless q is NaN)
+            const bool nan_s = s != s, inf_s = s == __longlong_as_double(0x7ff0000000000000ll);
+            const bool ok = s >= 0x1p-900 && s < 0x1p62;
+            const int e = ok ? kpp_binade(s) : 0;
+            const int64_t su = ok ? (int64_t)ldexp(s, 52 - e) : 0;
+            int64_t r[EPL];
+            int lfirst = EPL;
+            int64_t tot = 0;
 #pragma unroll
-                for (int k = 0; k < 8; k++) v[k] = qs[i + k];
+            for (int t = 0; t < EPL; t++) {
+                const int idx = p + lane * EPL + t;
+                int64_t rr = -1;
+                if (idx < n) {
+                    const double q = qs[idx];
+                    if (nan_s) rr = 0;
+                    else if (inf_s) rr = q == q ? 0 : -1;
+                    else if (s == 0.0) rr = q == 0.0 ? 0 : -1;
+                    else if (ok) rr = kpp_units(q, e);
+                }
+                r[t] = rr < 0 ? 0 : rr;
+                if (lfirst == EPL && rr < 0) lfirst = t;
+                tot += r[t];
+            }
+            int64_t pre = tot;
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t o = __shfl_up(pre, off);
+                if (lane >= off) pre += o;
+            }
+            pre -= tot;
+            int first = lfirst;
+            int64_t run = su + pre;
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    // the reference's first element is q_0 itself: 0 + q_0 = q_0
-                    s = __dadd_rn(v[k], s);
-                    cum[r0 + i + k] = s;
+            for (int t = 0; t < EPL; t++) {
+                if (t < first && run + r[t] >= KPP_TWO53) first = t;
+                if (t < first) run += r[t];
+            }
+            const unsigned long long bad = __ballot(first < EPL);
+            const int fl = bad ? __ffsll((long long)bad) - 1 : 64;
+            if (lane <= fl) {
+                int64_t v = su + pre;
+#pragma unroll
+                for (int t = 0; t < EPL; t++) {
+                    if (t < first) {
+                        v += r[t];
+                        cum[r0 + p + lane * EPL + t] = ok ? ldexp((double)v, e - 52) : s;
+                    }
                 }
             }
-            for (; i < n; i++) {
-                s = __dadd_rn(qs[i], s);
-                cum[r0 + i] = s;
-            }
+            const int fstop = fl < 64 ? __shfl(first, fl) : EPL;
+            const int m = p + (fl < 64 ? fl : 64) * EPL + (fl < 64 ? fstop : 0);
+            if (m > p && ok) s = ldexp((double)__shfl(run, fl < 64 ? fl : 63), e - 52);
+            if (m >= n) break;
+            s = __dadd_rn(qs[m], s);           // the reference's add (0 + q_0 = q_0 for row 0)
+            if (lane == 0) cum[r0 + m] = s;
+            p = m + 1;
         }
-        s = __shfl(s, 0);
         wave_sync();
         base = c + 1;
         nseq++;
@@ -344,15 +511,23 @@ int launch_kmeans_pp(hipStream_t s, const float* X, int64_t N, int d, int K, int
     int32_t* mode = (int32_t*)p;               p += sizeof(int32_t) * ((nch + 1) & ~1ll);
     unsigned long long* mx = (unsigned long long*)p;
     const unsigned dgrid = gsz(N, KPP_THREADS, 4096);
-    const size_t lds = sizeof(double) * (size_t)d;
     for (int it = 1; it < K; it++) {
         if (hipMemsetAsync(mx, 0, sizeof(*mx), s) != hipSuccess) return kstatus("kmeanspp.hip");
-        if (metric == 0)
-            hipLaunchKernelGGL(kpp_dist_kernel<0>, dim3(dgrid), dim3(KPP_THREADS), lds, s, X, N, d, chosen, it, mind, mx);
+        const bool vec = d % KPP_DJ == 0;
+        if (metric == 0 && vec)
+            hipLaunchKernelGGL((kpp_dist_kernel<0, true>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
+                               mind, mx);
+        else if (metric == 0)
+            hipLaunchKernelGGL((kpp_dist_kernel<0, false>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
+                               mind, mx);
+        else if (vec)
+            hipLaunchKernelGGL((kpp_dist_kernel<1, true>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
+                               mind, mx);
         else
-            hipLaunchKernelGGL(kpp_dist_kernel<1>, dim3(dgrid), dim3(KPP_THREADS), lds, s, X, N, d, chosen, it, mind, mx);
+            hipLaunchKernelGGL((kpp_dist_kernel<1, false>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
+                               mind, mx);
         hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum);
-        hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_THREADS), 0, s, csum, nch, cstart);
+        hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, csum, nch, cstart);
         hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, cstart,
                            meta);
         hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, mind, N, mx, meta, nch, cs, mode, cum, stats);
