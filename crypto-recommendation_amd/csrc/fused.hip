@@ -170,6 +170,17 @@ __device__ inline double quad_shift_up(double v) {
     return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
 }
 
+// __shfl_xor(v, 32) as two v_permlane32_swap (gfx950 VALU lane-half swap)
+// instead of two LDS bpermutes: sw[0] holds the lower half's value in the
+// upper lanes, sw[1] the upper half's value in the lower lanes.
+__device__ inline double swap_halves(double v, int h) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    const uint32_t l = h ? lo[0] : lo[1], u = h ? hi[0] : hi[1];
+    return __longlong_as_double((long long)(((uint64_t)u << 32) | l));
+}
+
 // EuclideanPhi arithmetic (euclidean_phi_gen.hpp:70-92) in 32-bit form, M =
 // int(pow(2,32)-5) = 2^31-1 under g++. temp = (long)(h * r) is an int32 (the
 // int product wraps), so ((temp % M) + M) % M needs only compares; the uint32
@@ -450,6 +461,15 @@ constexpr int FP_WAVES = FP_KEEP_X ? 8 : 12;   // 2 / 3 per SIMD: <= 256 / 168 V
 #ifndef TILE_UNROLL
 #define TILE_UNROLL 1
 #endif
+#ifndef MFMA_PRIO
+#define MFMA_PRIO 1     // s_setprio inside the centroid loop (measured +1-3%)
+#endif
+#ifndef HASH_ROWB
+#define HASH_ROWB 0     // 1: one floor-certification window per row (measured: no gain, more fix-ups)
+#endif
+#ifndef YOUNG_PRIO
+#define YOUNG_PRIO 0    // s_setprio for waves FP_WAVES/2.. for the whole loop (experiment knob)
+#endif
 #ifndef PIPE_TILES
 #define PIPE_TILES 0
 #endif
@@ -547,6 +567,15 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     const int col = lane & 31, h = lane >> 5;
     const float ecf = a.cbound[0], ebf = a.cbound[1], cmaxf = a.cbound[3];
     const bool c_ok = __float_as_uint(a.cbound[2]) == 0u;
+    // maxima of the hash constants over the launch's functions (HASH_ROWB window)
+    float pnmx = 0.f, v1mx = 0.f, tmx = 0.f;
+    if (HASH && HASH_ROWB) {
+        for (int f = 0; f < 32; f++) {
+            pnmx = fmaxf(pnmx, lpn0[f]);
+            v1mx = fmaxf(v1mx, lv10[f]);
+            tmx = fmaxf(tmx, fabsf(lt0[f]));
+        }
+    }
     const _Float16* my_h = lch + col * FU_RS + 8 * h;
     const _Float16* my_l = lcl + col * FU_RS + 8 * h;
     const int ntile32 = Kpad >> 5;
@@ -558,6 +587,11 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     // runs VALU-heavy epilogues) instead of lockstep.
     if (wave >= FP_WAVES / 2)
         for (int i = 0; i < WAVE_OFFSET; i++) __builtin_amdgcn_s_sleep(127);
+#endif
+#if YOUNG_PRIO
+    // static priority for the second-dispatched half (MI355X_MICROARCH.md,
+    // "Two waves per SIMD", item 4)
+    if (wave >= FP_WAVES / 2) __builtin_amdgcn_s_setprio(YOUNG_PRIO);
 #endif
     PT_DECL
     for (int64_t tile = (int64_t)blockIdx.x * FP_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FP_WAVES) {
@@ -655,6 +689,18 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             const float* lv1 = lv10 + hc;
             const int32_t* lr = lr0 + hc;
             if (!x_ok) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
+#if HASH_ROWB
+            // One window per row: the per-function bound with each function's
+            // |v|_2, |v|_1, |t| replaced by their maxima over the launch's
+            // functions, and |dot~|, |u|, |y| by the bounds those imply. The floor
+            // is certified iff no integer lies within BR of y: with fr = y -
+            // floor(y) (exact for |y| < 2^24; larger y are integers and never
+            // pass), fr >= BR and fr <= 1 - (BR + 2^-23) (the latter rounded).
+            const float dmax = pnmx * (float)nx * (1.f + 0x1p-20f);
+            const float EdR = fmaf(ca, pnmx, fmaf((float)FU_A2, v1mx, cb)) + fmaf(0x1p-23f, 2.f * dmax + tmx, 0x1p-40f * tmx);
+            const float BR = (EdR * (1.f + 0x1p-20f)) * (iw * (1.f + 0x1p-20f)) + (dmax + tmx) * iw * 0x1p-19f;
+            const float omBR = 1.f - (BR + 0x1p-23f);
+#endif
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int l = 2 * g + h;
@@ -667,12 +713,19 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                     const float tt = lt[f];
                     const float u = dotf + tt;
                     const float y = u * iw;
+#if HASH_ROWB
+                    const float fl = floorf(y);
+                    hv[q] = (int32_t)fl;
+                    const float fr = y - fl;
+                    if (!(fr >= BR && fr <= omBR)) fmask |= 1u << f;   // provisional; redone by hash_fixup_kernel
+#else
                     float Ed = fmaf(ca, lpn[f], fmaf((float)FU_A2, lv1[f], cb));
                     Ed = fmaf(0x1p-23f, fabsf(dotf) + fabsf(u), fmaf(0x1p-40f, fabsf(tt), Ed));
                     const float B = fmaf(Ed * (1.f + 0x1p-20f), iw * (1.f + 0x1p-20f), fabsf(y) * 0x1p-20f);
                     const float lo = floorf(y - B), hi = floorf(y + B);
                     hv[q] = (int32_t)lo;
                     if (lo != hi) fmask |= 1u << f;   // provisional; redone by hash_fixup_kernel
+#endif
                 }
                 const int64_t o = row * a.L + l;
                 if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
@@ -737,6 +790,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             t1 = m1 != m1_prev ? t : t1;
         }
 #else
+#if MFMA_PRIO
+        __builtin_amdgcn_s_setprio(MFMA_PRIO);
+#endif
 #pragma unroll TILE_UNROLL
         for (int t = 0; t < ntile32; t++) {
             floatx16 acc_hi, acc_lo;
@@ -747,6 +803,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             tile_epilogue(sv, m1, m2);
             t1 = m1 != m1_prev ? t : t1;
         }
+#if MFMA_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
         const uint32_t l1 = __float_as_uint(m1) & 0xFu;
         const int i1 = t1 * 32 + 8 * (int)(l1 >> 2) + 4 * h + (int)(l1 & 3u);
@@ -790,13 +849,13 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
-                const double from0 = __shfl_xor(acc, 32);
+                const double from0 = swap_halves(acc, h);
                 if (h == 1) {
                     acc = from0;
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
-                const double from1 = __shfl_xor(acc, 32);
+                const double from1 = swap_halves(acc, h);
                 if (h == 0) acc = from1;
             }
             if (h == 1 && valid && cert) {
