@@ -250,7 +250,10 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
         double best = 0.0; int bi = -1;
         for (int c = lane; c < K; c += 64) {
             const double dd = metric == 0 ? exact_euclid(x, C + (size_t)c * d, d) : exact_cosine(x, C + (size_t)c * d, d);
-            if (bi < 0 || dd < best) { best = dd; bi = c; }
+            // assignment.hpp:66: the -1 sentinel takes centroid 0's distance even
+            // if NaN (a zero vector under cosine), which then blocks every later
+            // '<'; any other NaN is never taken
+            if (bi < 0 ? (dd == dd || c == 0) : dd < best) { best = dd; bi = c; }
         }
         // wave argmin: smallest value, then smallest index (= first strict minimum in c order)
         for (int off = 32; off >= 1; off >>= 1) {

@@ -19,6 +19,20 @@ __device__ inline double exact_euclid(const float* __restrict__ x, const double*
     return sqrt(acc);
 }
 
+// double(ip / (long double)denom) for denom = sqrt(.) * sqrt(.) >= +0, with
+// x87's results for a zero denominator (a zero vector): 0/0 is the default
+// NaN "real indefinite" (sign set: 0xFFF8... as a double), x/0 = +-inf.
+__device__ inline double x87_quot(sx80 ip, double denom) {
+    if (denom == 0.0) {
+        if (ip.m == 0) return __longlong_as_double((long long)0xFFF8000000000000ull);
+        return ip.s ? -__builtin_inf() : __builtin_inf();
+    }
+    return sx_to_double(sx_div(ip, sx_from_double(denom)));
+}
+
+// 1 - q as SSE subsd computes it: a NaN q comes back unchanged.
+__device__ inline double one_minus(double q) { return q != q ? q : __dsub_rn(1.0, q); }
+
 __device__ inline double exact_cosine(const float* __restrict__ x, const double* __restrict__ c, int d) {
     sx80 ip = sx_zero();
     double a = 0.0, b = 0.0;
@@ -29,6 +43,5 @@ __device__ inline double exact_cosine(const float* __restrict__ x, const double*
         b = __dadd_rn(b, __dmul_rn(c[j], c[j]));
     }
     const double denom = __dmul_rn(sqrt(a), sqrt(b));
-    const double q = sx_to_double(sx_div(ip, sx_from_double(denom)));
-    return __dsub_rn(1.0, q);
+    return one_minus(x87_quot(ip, denom));
 }

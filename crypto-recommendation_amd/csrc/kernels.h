@@ -103,6 +103,16 @@ size_t kmeans_pp_ws_bytes(int64_t N);
 int launch_kmeans_pp(hipStream_t s, const float* X, int64_t N, int d, int K, int metric, const double* canon,
                      int32_t* chosen, void* ws, unsigned long long* stats);
 
+// Recommend step (recom.hip): fp64 rows, per-user candidate CSR.
+int launch_rc_norms(hipStream_t s, const double* X, int64_t N, int d, double* xa);
+int launch_rc_p_closest(hipStream_t s, const double* X, const double* xa, int d, const double* U, int64_t nq,
+                        const int64_t* cand_ptr, const int32_t* cand_idx, int P, double* sim, double* key,
+                        int32_t* pos, int32_t* out_idx, double* out_sim, int32_t* out_cnt, int32_t* replay,
+                        unsigned int* replay_count);
+int launch_rc_top_n(hipStream_t s, const double* X, const double* x_mean, int d, const double* u_mean, int64_t nq,
+                    const int64_t* unk_ptr, const int32_t* unk_idx, const int32_t* nb_idx, const double* nb_sim,
+                    const int32_t* nb_cnt, int P, int n_top, double* pred, int32_t* pidx, int32_t* out);
+
 // Fused hash + assign on split-f16 MFMA (fused.hip), d = 128.
 struct FusedLaunch {
     const float* X = nullptr;

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const float* __re
             dd = sqrt(acc);
         } else {
             const double denom = __dmul_rn(sqrt(a), sqrt(cb));
-            dd = __dsub_rn(1.0, sx_to_double(sx_div(ip, sx_from_double(denom))));
+            dd = one_minus(x87_quot(ip, denom));
         }
         double m = dd;
         if (it > 1) {

@@ -1,0 +1,230 @@
+// recom.hip — the recommend step on gfx950:
+//   get_P_closest          lib/crypto_rec.hpp:213-231
+//   parallel_quickSort     lib/crypto_rec.hpp:234-277 (Lomuto, pivot = last, '>=')
+//   get_predicted_user_sim lib/crypto_rec.hpp:280-302
+//   get_top_N_recom        lib/crypto_rec.hpp:305-325
+// for a batch of users, each with its candidate neighbour rows (the output of
+// an LSH / hypercube query). Vectors are fp64 rows.
+//
+// Ordering. With distinct, non-NaN keys the reference's quicksort yields the
+// keys in descending order, so the first P positions are the P largest. Equal
+// keys are permuted by Lomuto's swap sequence and NaNs fail every '>='; the
+// order then depends on the whole array. One wave per user therefore extracts
+// the top P+1 similarities in parallel and, only if a NaN is present or two of
+// the first P+1 are equal (a tie touching the first P positions), hands the user
+// to lomuto_sort, which replays the reference's quicksort exactly (one lane per
+// user; disjoint subarrays, so the order they are sorted in does not matter).
+#include "common.h"
+#include "kernels.h"
+#include "exact.h"
+
+namespace lshkm {
+
+constexpr int RC_WAVES = 4;
+
+// CustVector::cosineSimilarity (cust_vector.hpp:158-174), this = neighbour x,
+// in = user u: long-double inner product of double products, fp64 norms
+// (xa, ub: sum of squares in dim order), long-double division, then double.
+__device__ inline double rc_cos_sim(const double* __restrict__ x, const double* __restrict__ u, int d, double xa,
+                                    double ub) {
+    sx80 ip = sx_zero();
+    for (int j = 0; j < d; j++) ip = sx_add_double(ip, __dmul_rn(x[j], u[j]));
+    return x87_quot(ip, __dmul_rn(sqrt(xa), sqrt(ub)));
+}
+
+__device__ inline double rc_sumsq(const double* __restrict__ x, int d) {
+    double a = 0.0;
+    for (int j = 0; j < d; j++) a = __dadd_rn(a, __dmul_rn(x[j], x[j]));
+    return a;
+}
+
+__global__ __launch_bounds__(256) void rc_norm_kernel(const double* __restrict__ X, int64_t N, int d,
+                                                      double* __restrict__ xa) {
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256)
+        xa[r] = rc_sumsq(X + r * d, d);
+}
+
+// The reference's quicksort on key/val[0..n), exactly (crypto_rec.hpp:234-277).
+// Explicit stack, smaller part first: depth <= log2(n) + 1.
+__device__ void lomuto_sort(double* key, int32_t* val, int n) {
+    int lo_s[64], hi_s[64];
+    int sp = 0;
+    if (n > 1) { lo_s[0] = 0; hi_s[0] = n - 1; sp = 1; }
+    while (sp > 0) {
+        sp--;
+        int low = lo_s[sp], high = hi_s[sp];
+        while (low < high) {
+            const double pivot = key[high];
+            int i = low - 1;
+            for (int j = low; j <= high - 1; j++) {
+                const double kj = key[j];
+                if (kj >= pivot) {
+                    i++;
+                    const double tk = key[i]; key[i] = kj; key[j] = tk;
+                    const int32_t tv = val[i]; val[i] = val[j]; val[j] = tv;
+                }
+            }
+            const double tk = key[i + 1]; key[i + 1] = key[high]; key[high] = tk;
+            const int32_t tv = val[i + 1]; val[i + 1] = val[high]; val[high] = tv;
+            const int pi = i + 1;
+            // parts [low, pi-1] and [pi+1, high]: push the larger, continue with the smaller
+            if (pi - low < high - pi) {
+                if (pi + 1 < high) { lo_s[sp] = pi + 1; hi_s[sp] = high; sp++; }
+                high = pi - 1;
+            } else {
+                if (low < pi - 1) { lo_s[sp] = low; hi_s[sp] = pi - 1; sp++; }
+                low = pi + 1;
+            }
+        }
+    }
+}
+
+// One wave per user: similarities (sim, in candidate order), then the top P+1
+// by repeated wave-wide max over a work copy (key). Users with a NaN or a tie
+// in the first P+1 go to the exact replay list.
+__global__ __launch_bounds__(64 * RC_WAVES) void rc_p_closest_kernel(
+    const double* __restrict__ X, const double* __restrict__ xa, int d, const double* __restrict__ U, int64_t nq,
+    const int64_t* __restrict__ cand_ptr, const int32_t* __restrict__ cand_idx, int P, double* __restrict__ sim,
+    double* __restrict__ key, int32_t* __restrict__ out_idx, double* __restrict__ out_sim,
+    int32_t* __restrict__ out_cnt, int32_t* __restrict__ replay, unsigned int* __restrict__ replay_count) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * RC_WAVES + (threadIdx.x >> 6);
+    for (int64_t q = w0; q < nq; q += (int64_t)gridDim.x * RC_WAVES) {
+        const int64_t o = cand_ptr[q];
+        const int n = (int)(cand_ptr[q + 1] - o);
+        const double* u = U + q * d;
+        const double ub = rc_sumsq(u, d);
+        bool nan = false;
+        for (int i = lane; i < n; i += 64) {
+            const int32_t r = cand_idx[o + i];
+            const double s = rc_cos_sim(X + (int64_t)r * d, u, d, xa[r], ub);
+            sim[o + i] = s;
+            key[o + i] = s;
+            nan |= s != s;
+        }
+        const int c = n < P ? n : P;
+        if (lane == 0) out_cnt[q] = c;
+        for (int i = c + lane; i < P; i += 64) {
+            out_idx[q * P + i] = -1;
+            out_sim[q * P + i] = 0.0;
+        }
+        bool replay_me = __ballot(nan) != 0;
+        const int ext = n < P + 1 ? n : P + 1;
+        double prev = 0.0;
+        for (int k = 0; k < ext && !replay_me; k++) {
+            double best = -__builtin_inf();
+            int bpos = 0x7fffffff;
+            for (int i = lane; i < n; i += 64) {
+                const double v = key[o + i];
+                if (v > best) { best = v; bpos = i; }
+            }
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double ob = __shfl_xor(best, off);
+                const int op = __shfl_xor(bpos, off);
+                if (ob > best || (ob == best && op < bpos)) { best = ob; bpos = op; }
+            }
+            if (k > 0 && best == prev) {          // a tie touching the first P positions
+                replay_me = true;
+                break;
+            }
+            prev = best;
+            if (k < c && lane == 0) {
+                out_idx[q * P + k] = cand_idx[o + bpos];
+                out_sim[q * P + k] = best;
+            }
+            if (lane == (bpos & 63)) key[o + bpos] = -__builtin_inf();
+            wave_sync();
+        }
+        if (replay_me && lane == 0) replay[atomicAdd(replay_count, 1u)] = (int32_t)q;
+    }
+}
+
+// Exact replay of the reference's quicksort for the listed users (one lane each).
+__global__ __launch_bounds__(64) void rc_replay_kernel(const int64_t* __restrict__ cand_ptr,
+                                                       const int32_t* __restrict__ cand_idx, int P,
+                                                       const double* __restrict__ sim, double* __restrict__ key,
+                                                       int32_t* __restrict__ pos, const int32_t* __restrict__ replay,
+                                                       const unsigned int* __restrict__ replay_count,
+                                                       int32_t* __restrict__ out_idx, double* __restrict__ out_sim) {
+    const unsigned int total = *replay_count;
+    for (unsigned int t = blockIdx.x * 64 + threadIdx.x; t < total; t += gridDim.x * 64) {
+        const int64_t q = replay[t];
+        const int64_t o = cand_ptr[q];
+        const int n = (int)(cand_ptr[q + 1] - o);
+        for (int i = 0; i < n; i++) {
+            key[o + i] = sim[o + i];
+            pos[o + i] = cand_idx[o + i];
+        }
+        lomuto_sort(key + o, pos + o, n);
+        const int c = n < P ? n : P;
+        for (int i = 0; i < c; i++) {
+            out_idx[q * P + i] = pos[o + i];
+            out_sim[q * P + i] = key[o + i];
+        }
+    }
+}
+
+// get_top_N_recom with get_predicted_user_sim: one wave per user, lane per
+// unknown index (sums over the neighbours in their sorted order), then the
+// exact quicksort of the predictions by lane 0 and the first n_top, 0-padded.
+__global__ __launch_bounds__(64 * RC_WAVES) void rc_top_n_kernel(
+    const double* __restrict__ X, const double* __restrict__ x_mean, int d, const double* __restrict__ u_mean,
+    int64_t nq, const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx,
+    const int32_t* __restrict__ nb_idx, const double* __restrict__ nb_sim, const int32_t* __restrict__ nb_cnt, int P,
+    int n_top, double* __restrict__ pred, int32_t* __restrict__ pidx, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * RC_WAVES + (threadIdx.x >> 6);
+    for (int64_t q = w0; q < nq; q += (int64_t)gridDim.x * RC_WAVES) {
+        const int64_t o = unk_ptr[q];
+        const int m = (int)(unk_ptr[q + 1] - o);
+        const int cnt = nb_cnt[q];
+        const double um = u_mean[q];
+        for (int e = lane; e < m; e += 64) {
+            const int index = unk_idx[o + e];
+            double main_sum = 0.0, abs_sum = 0.0;
+            for (int i = 0; i < cnt; i++) {
+                const double cs = nb_sim[q * P + i];
+                abs_sum = __dadd_rn(abs_sum, fabs(cs));
+                const int32_t r = nb_idx[q * P + i];
+                main_sum = __dadd_rn(main_sum, __dmul_rn(cs, __dsub_rn(X[(int64_t)r * d + index], x_mean[r])));
+            }
+            pred[o + e] = __dadd_rn(__ddiv_rn(main_sum, abs_sum), um);
+            pidx[o + e] = index;
+        }
+        __threadfence_block();
+        wave_sync();
+        if (lane == 0) {
+            lomuto_sort(pred + o, pidx + o, m);
+            for (int i = 0; i < n_top; i++) out[q * n_top + i] = i < m ? pidx[o + i] : 0;
+        }
+    }
+}
+
+int launch_rc_norms(hipStream_t s, const double* X, int64_t N, int d, double* xa) {
+    hipLaunchKernelGGL(rc_norm_kernel, dim3(gsz(N, 256, 4096)), dim3(256), 0, s, X, N, d, xa);
+    return kstatus("recom.hip");
+}
+
+int launch_rc_p_closest(hipStream_t s, const double* X, const double* xa, int d, const double* U, int64_t nq,
+                        const int64_t* cand_ptr, const int32_t* cand_idx, int P, double* sim, double* key,
+                        int32_t* pos, int32_t* out_idx, double* out_sim, int32_t* out_cnt, int32_t* replay,
+                        unsigned int* replay_count) {
+    if (nq <= 0) return 0;
+    if (hipMemsetAsync(replay_count, 0, sizeof(unsigned int), s) != hipSuccess) return kstatus("recom.hip");
+    hipLaunchKernelGGL(rc_p_closest_kernel, dim3(gsz(nq, RC_WAVES, 8192)), dim3(64 * RC_WAVES), 0, s, X, xa, d, U, nq,
+                       cand_ptr, cand_idx, P, sim, key, out_idx, out_sim, out_cnt, replay, replay_count);
+    hipLaunchKernelGGL(rc_replay_kernel, dim3(gsz(nq, 64, 1024)), dim3(64), 0, s, cand_ptr, cand_idx, P, sim, key, pos,
+                       replay, replay_count, out_idx, out_sim);
+    return kstatus("recom.hip");
+}
+
+int launch_rc_top_n(hipStream_t s, const double* X, const double* x_mean, int d, const double* u_mean, int64_t nq,
+                    const int64_t* unk_ptr, const int32_t* unk_idx, const int32_t* nb_idx, const double* nb_sim,
+                    const int32_t* nb_cnt, int P, int n_top, double* pred, int32_t* pidx, int32_t* out) {
+    if (nq <= 0) return 0;
+    hipLaunchKernelGGL(rc_top_n_kernel, dim3(gsz(nq, RC_WAVES, 8192)), dim3(64 * RC_WAVES), 0, s, X, x_mean, d, u_mean,
+                       nq, unk_ptr, unk_idx, nb_idx, nb_sim, nb_cnt, P, n_top, pred, pidx, out);
+    return kstatus("recom.hip");
+}
+
+}  // namespace lshkm

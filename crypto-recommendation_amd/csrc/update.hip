@@ -13,7 +13,7 @@
 // indices are wave-uniform scalar loads). Bytes: 4d per row read once.
 #include "common.h"
 #include "kernels.h"
-#include "softx87.h"
+#include "exact.h"
 
 namespace lshkm {
 
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64) void km_finalize_kernel(const double* __restric
             y = __dadd_rn(y, __dmul_rn(b[j], b[j]));
         }
         const double denom = __dmul_rn(sqrt(x), sqrt(y));
-        dist = __dsub_rn(1.0, sx_to_double(sx_div(ip, sx_from_double(denom))));
+        dist = one_minus(x87_quot(ip, denom));
     }
     if (dist > min_dist) atomicOr(moved, 1);
 }

@@ -88,6 +88,8 @@ def lib():
             "lshkm_kmeans_finalize": (i32, [vp, vp, vp, i32, i32, vp, i32, f64, vp, C.POINTER(i32)]),
             "lshkm_kmeans_pp": (i32, [vp, vp, i64, i32, i32, i32, u64, vp]),
             "lshkm_rand_selection": (i32, [u64, i64, i32, vp]),
+            "lshkm_p_closest": (i32, [vp, vp, i64, i32, vp, i64, vp, vp, i32, vp, vp, vp]),
+            "lshkm_top_n_recom": (i32, [vp, vp, vp, i64, i32, vp, i64, vp, vp, vp, vp, vp, i32, i32, vp]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
         }
         for name, (res, args) in sigs.items():
@@ -414,6 +416,35 @@ def rand_selection_rows(N, K, seed=1):
     rows = np.empty(K, np.int32)
     _ck(lib().lshkm_rand_selection(int(seed), int(N), int(K), _np_ptr(rows)))
     return rows
+
+
+# ------------------------------------------------------------ recommendation
+def p_closest(ctx, X, U, cand_ptr, cand_idx, P):
+    """get_P_closest (crypto_rec.hpp:213-231) for all users of U at once.
+    X [N][d], U [nq][d] fp64 device tensors; cand_ptr [nq+1] int64 / cand_idx
+    int32 device tensors. Returns (idx [nq][P] -1-padded, sim [nq][P], cnt [nq])."""
+    torch = ctx.torch
+    N, d = X.shape
+    nq = U.shape[0]
+    idx = ctx.empty((nq, P), torch.int32)
+    sim = ctx.empty((nq, P), torch.float64)
+    cnt = ctx.empty((nq,), torch.int32)
+    _ck(lib().lshkm_p_closest(ctx.h, _t_ptr(X), N, d, _t_ptr(U), nq, _t_ptr(cand_ptr),
+                              _t_ptr(cand_idx) if cand_idx.numel() else None, P, _t_ptr(idx), _t_ptr(sim),
+                              _t_ptr(cnt)))
+    return idx, sim, cnt
+
+
+def top_n_recom(ctx, X, x_mean, u_mean, unk_ptr, unk_idx, nb_idx, nb_sim, nb_cnt, n_top):
+    """get_top_N_recom (crypto_rec.hpp:305-325) over p_closest's lists: [nq][n_top] int32."""
+    torch = ctx.torch
+    N, d = X.shape
+    nq, P = nb_idx.shape
+    out = ctx.empty((nq, n_top), torch.int32)
+    _ck(lib().lshkm_top_n_recom(ctx.h, _t_ptr(X), _t_ptr(x_mean), N, d, _t_ptr(u_mean), nq, _t_ptr(unk_ptr),
+                                _t_ptr(unk_idx) if unk_idx.numel() else None, _t_ptr(nb_idx), _t_ptr(nb_sim),
+                                _t_ptr(nb_cnt), P, n_top, _t_ptr(out)))
+    return out
 
 
 # ------------------------------------------------- reference-named mirrors

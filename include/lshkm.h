@@ -224,6 +224,31 @@ int lshkm_kmeans_pp(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, int K, 
  * redrawing on a repeat. Host only. 1 <= K <= N. */
 int lshkm_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows_host);
 
+/* ----------------------------------------------------------- recommendation
+ * get_P_closest (crypto_rec.hpp:213-231) for nq users at once. User q's
+ * neighbours are the dataset rows cand_idx_dev[cand_ptr_dev[q] ..
+ * cand_ptr_dev[q+1]) in the order the reference's neighbour vector holds them
+ * (ascending row: a query's output). Similarity = cosineSimilarity(neighbour,
+ * user) (cust_vector.hpp:158-174); order = the reference's quicksort
+ * (parallel_quickSort, :234-277, ties and NaNs included); first P kept.
+ * Rows are fp64 (X_dev [N][d] neighbour pool, U_dev [nq][d] users).
+ * out_idx_dev / out_sim_dev [nq][P] (-1 / 0 past the count), out_cnt_dev [nq]
+ * = min(P, neighbours). Bit-exact when the squares of the components are exact
+ * in fp64 (the reference's pow(x, 2)); otherwise within an ulp. */
+int lshkm_p_closest(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const double* U_dev, int64_t nq,
+                    const int64_t* cand_ptr_dev, const int32_t* cand_idx_dev, int P, int32_t* out_idx_dev,
+                    double* out_sim_dev, int32_t* out_cnt_dev);
+/* get_top_N_recom (crypto_rec.hpp:305-325) over lshkm_p_closest's lists:
+ * predicted scores of each user's unknown indexes (get_predicted_user_sim,
+ * :280-302; unk_* = CSR of the ascending unknown indexes, std::set order),
+ * sorted by the same quicksort, first n_top (0-padded like vector::resize).
+ * x_mean_dev [N] / u_mean_dev [nq]: getKnownMean of the rows / users.
+ * out_dev [nq][n_top]. */
+int lshkm_top_n_recom(lshkm_ctx ctx, const double* X_dev, const double* x_mean_dev, int64_t N, int d,
+                      const double* u_mean_dev, int64_t nq, const int64_t* unk_ptr_dev, const int32_t* unk_idx_dev,
+                      const int32_t* nb_idx_dev, const double* nb_sim_dev, const int32_t* nb_cnt_dev, int P,
+                      int n_top, int32_t* out_dev);
+
 /* ------------------------------------------------------------ synthetic data */
 /* include/lshkm_synth.h generator, rows [row0, row0+rows) into X_dev. */
 int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X_dev);

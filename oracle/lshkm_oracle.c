@@ -484,6 +484,91 @@ void or_kmeans_pp(int64_t N, int d, int K, const float* X, int metric, uint64_t 
     free(cs);
 }
 
+/* ------------------------------------------------------------ recommendation */
+
+/* CustVector::cosineSimilarity (cust_vector.hpp:158-174), this = a, in = b. */
+static double cos_sim_f64(const double* a, const double* b, int d) {
+    long double ip = 0.0L;
+    for (int j = 0; j < d; j++) ip = ip + (long double)(a[j] * b[j]);
+    double x = 0, y = 0;
+    for (int j = 0; j < d; j++) { x = x + pow(a[j], 2); y = y + pow(b[j], 2); }
+    double denom = sqrt(x) * sqrt(y);
+    return (double)(ip / (long double)denom);
+}
+
+/* parallel_quickSort / parralel_partition (crypto_rec.hpp:234-277): Lomuto,
+ * pivot = last, elements >= pivot to the front, recursion left then right. */
+static void lomuto_desc(double* key, int32_t* val, int low, int high) {
+    if (low < high) {
+        const double pivot = key[high];
+        int i = low - 1;
+        for (int j = low; j <= high - 1; j++) {
+            if (key[j] >= pivot) {
+                i++;
+                double tk = key[i]; key[i] = key[j]; key[j] = tk;
+                int32_t tv = val[i]; val[i] = val[j]; val[j] = tv;
+            }
+        }
+        double tk = key[i + 1]; key[i + 1] = key[high]; key[high] = tk;
+        int32_t tv = val[i + 1]; val[i + 1] = val[high]; val[high] = tv;
+        lomuto_desc(key, val, low, i);
+        lomuto_desc(key, val, i + 2, high);
+    }
+}
+
+/* get_P_closest (crypto_rec.hpp:213-231) per user q over its candidates
+ * cand_idx[cand_ptr[q] .. cand_ptr[q+1]): similarities, the quicksort, first P.
+ * out_idx / out_sim [nq][P]; out_cnt[q] = min(P, n). */
+void or_p_closest(int d, const double* X, int64_t nq, const double* U, const int64_t* cand_ptr,
+                  const int32_t* cand_idx, int P, int32_t* out_idx, double* out_sim, int32_t* out_cnt) {
+    for (int64_t q = 0; q < nq; q++) {
+        const int64_t o = cand_ptr[q];
+        const int n = (int)(cand_ptr[q + 1] - o);
+        double* s = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+        int32_t* r = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+        for (int i = 0; i < n; i++) {
+            r[i] = cand_idx[o + i];
+            s[i] = cos_sim_f64(X + (size_t)r[i] * d, U + (size_t)q * d, d);
+        }
+        lomuto_desc(s, r, 0, n - 1);
+        const int c = n < P ? n : P;
+        for (int i = 0; i < c; i++) { out_idx[q * P + i] = r[i]; out_sim[q * P + i] = s[i]; }
+        out_cnt[q] = c;
+        free(s); free(r);
+    }
+}
+
+/* get_top_N_recom (crypto_rec.hpp:305-325) with get_predicted_user_sim
+ * (:280-302) over the P-closest lists; unknown indexes per user as CSR
+ * (ascending, std::set order); out [nq][N], padded with 0 (vector::resize). */
+void or_top_n_recom(int d, const double* X, const double* x_mean, int64_t nq, const double* U,
+                    const double* u_mean, const int64_t* unk_ptr, const int32_t* unk_idx, const int32_t* nb_idx,
+                    const double* nb_sim, const int32_t* nb_cnt, int P, int N, int32_t* out) {
+    for (int64_t q = 0; q < nq; q++) {
+        const int64_t o = unk_ptr[q];
+        const int m = (int)(unk_ptr[q + 1] - o);
+        double* pred = (double*)malloc(sizeof(double) * (size_t)(m > 0 ? m : 1));
+        int32_t* ix = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m > 0 ? m : 1));
+        for (int u = 0; u < m; u++) {
+            const int index = unk_idx[o + u];
+            double main_sum = 0, abs_sum = 0;
+            for (int i = 0; i < nb_cnt[q]; i++) {
+                const double cs = nb_sim[q * P + i];
+                abs_sum = abs_sum + fabs(cs);
+                const int32_t r = nb_idx[q * P + i];
+                main_sum = main_sum + (cs * (X[(size_t)r * d + index] - x_mean[r]));
+            }
+            double p = main_sum / abs_sum;
+            p = p + u_mean[q];
+            pred[u] = p;
+            ix[u] = index;
+        }
+        lomuto_desc(pred, ix, 0, m - 1);
+        for (int i = 0; i < N; i++) out[q * N + i] = i < m ? ix[i] : 0;
+        free(pred); free(ix);
+    }
+}
+
 void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out) {
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < rows; i++)

@@ -53,6 +53,9 @@ def lib():
                                            f64p, i64p]),
             "or_rand_selection": (None, [C.c_uint64, C.c_int64, C.c_int, i32p]),
             "or_kmeans_pp": (None, [C.c_int64, C.c_int, C.c_int, f32p, C.c_int, C.c_uint64, i32p]),
+            "or_p_closest": (None, [C.c_int, f64p, C.c_int64, f64p, i64p, i32p, C.c_int, i32p, f64p, i32p]),
+            "or_top_n_recom": (None, [C.c_int, f64p, f64p, C.c_int64, f64p, f64p, i64p, i32p, i32p, f64p, i32p,
+                                      C.c_int, C.c_int, i32p]),
             "or_synth": (None, [C.c_uint64, C.c_int64, C.c_int64, C.c_int, f32p]),
         }
         for name, (res, args) in sig.items():
@@ -212,3 +215,28 @@ def rand_selection(N, K, seed=1):
     rows = np.empty(K, np.int32)
     lib().or_rand_selection(int(seed), int(N), int(K), rows)
     return rows
+
+
+def p_closest(X, U, cand_ptr, cand_idx, P):
+    """get_P_closest (crypto_rec.hpp:213-231) per user: (idx [Q][P] -1-padded, sim [Q][P], cnt [Q])."""
+    X = np.ascontiguousarray(X, np.float64); U = np.ascontiguousarray(U, np.float64)
+    Q, d = U.shape
+    idx = np.full((Q, P), -1, np.int32); sim = np.zeros((Q, P), np.float64); cnt = np.zeros(Q, np.int32)
+    ci = np.ascontiguousarray(cand_idx, np.int32)
+    lib().or_p_closest(d, X, Q, U, np.ascontiguousarray(cand_ptr, np.int64), ci if len(ci) else np.zeros(1, np.int32),
+                       P, idx, sim, cnt)
+    return idx, sim, cnt
+
+
+def top_n_recom(X, x_mean, U, u_mean, unk_ptr, unk_idx, nb_idx, nb_sim, nb_cnt, N):
+    """get_top_N_recom (crypto_rec.hpp:305-325) over get_P_closest lists: [Q][N], 0-padded."""
+    X = np.ascontiguousarray(X, np.float64); U = np.ascontiguousarray(U, np.float64)
+    Q, d = U.shape
+    P = nb_idx.shape[1]
+    out = np.zeros((Q, N), np.int32)
+    ui = np.ascontiguousarray(unk_idx, np.int32)
+    lib().or_top_n_recom(d, X, np.ascontiguousarray(x_mean, np.float64), Q, U, np.ascontiguousarray(u_mean, np.float64),
+                         np.ascontiguousarray(unk_ptr, np.int64), ui if len(ui) else np.zeros(1, np.int32),
+                         np.ascontiguousarray(nb_idx, np.int32), np.ascontiguousarray(nb_sim, np.float64),
+                         np.ascontiguousarray(nb_cnt, np.int32), P, N, out)
+    return out

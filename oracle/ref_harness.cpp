@@ -47,6 +47,7 @@ system_clock::time_point system_clock::now() noexcept {
 #include "clustering_phases/assignment.hpp"
 #include "clustering_phases/update.hpp"
 #include "clustering_phases/initialization.hpp"
+#include "crypto_rec.hpp"
 #undef private
 
 #include "../include/lshkm_synth.h"
@@ -96,6 +97,17 @@ static std::vector<double> read_f64(const std::string& path, size_t count) {
     FILE* f = fopen(path.c_str(), "rb");
     if (!f) { fprintf(stderr, "cannot read %s\n", path.c_str()); exit(2); }
     if (fread(v.data(), sizeof(double), count, f) != count) { fprintf(stderr, "short read %s\n", path.c_str()); exit(2); }
+    fclose(f);
+    return v;
+}
+
+template <typename T>
+static std::vector<T> read_raw(const std::string& path, size_t count) {
+    std::vector<T> v(count);
+    if (count == 0) return v;
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { fprintf(stderr, "cannot read %s\n", path.c_str()); exit(2); }
+    if (fread(v.data(), sizeof(T), count, f) != count) { fprintf(stderr, "short read %s\n", path.c_str()); exit(2); }
     fclose(f);
     return v;
 }
@@ -371,6 +383,56 @@ static int mode_kmeanspp(int argc, char** argv) {
     return 0;
 }
 
+// ------------------------------------------------------------ recom mode
+// recom DIR N d Q P NTOP — the recommend step (crypto_rec.hpp:213-345) as main.cpp
+// uses it (:160-168): per user, get_P_closest over its candidate neighbours, then
+// get_top_N_recom with those similarities. DIR holds x.f64 [N][d], xmean.f64
+// [N], u.f64 [Q][d], umean.f64 [Q], unk_ptr.i64 / unk_idx.i32 (each user's
+// unknown indexes), cand_ptr.i64 / cand_idx.i32 (neighbour rows, in order).
+// Outputs into DIR: pc_idx [Q][P] (-1 pad), pc_sim [Q][P] (0 pad), pc_cnt [Q],
+// top [Q][NTOP] (-1 for users without neighbours, which main.cpp skips).
+static int mode_recom(int argc, char** argv) {
+    if (argc < 7) { fprintf(stderr, "usage: recom DIR N d Q P NTOP\n"); return 2; }
+    std::string dir = argv[1];
+    int N = atoi(argv[2]), d = atoi(argv[3]), Q = atoi(argv[4]), P = atoi(argv[5]), NT = atoi(argv[6]);
+    std::vector<double> x = read_raw<double>(dir + "/x.f64", (size_t)N * d);
+    std::vector<double> xm = read_raw<double>(dir + "/xmean.f64", N);
+    std::vector<double> u = read_raw<double>(dir + "/u.f64", (size_t)Q * d);
+    std::vector<double> um = read_raw<double>(dir + "/umean.f64", Q);
+    std::vector<int64_t> up = read_raw<int64_t>(dir + "/unk_ptr.i64", Q + 1);
+    std::vector<int32_t> ui = read_raw<int32_t>(dir + "/unk_idx.i32", (size_t)up[Q]);
+    std::vector<int64_t> cp = read_raw<int64_t>(dir + "/cand_ptr.i64", Q + 1);
+    std::vector<int32_t> ci = read_raw<int32_t>(dir + "/cand_idx.i32", (size_t)cp[Q]);
+    std::vector<Vec> pool;
+    pool.reserve(N);
+    for (int i = 0; i < N; i++)
+        pool.emplace_back("p" + std::to_string(i), std::vector<double>(x.begin() + (size_t)i * d, x.begin() + (size_t)(i + 1) * d),
+                          std::set<int>(), xm[i]);
+    std::vector<int32_t> pc_idx((size_t)Q * P, -1), pc_cnt(Q, 0), top((size_t)Q * NT, -1);
+    std::vector<double> pc_sim((size_t)Q * P, 0.0);
+    for (int q = 0; q < Q; q++) {
+        std::set<int> unk(ui.begin() + up[q], ui.begin() + up[q + 1]);
+        Vec user("u" + std::to_string(q), std::vector<double>(u.begin() + (size_t)q * d, u.begin() + (size_t)(q + 1) * d),
+                 unk, um[q]);
+        std::vector<Vec*> nb;
+        for (int64_t e = cp[q]; e < cp[q + 1]; e++) nb.push_back(&pool[ci[e]]);
+        if (nb.empty()) continue;
+        std::vector<double> sims = get_P_closest(nb, user, P);
+        for (size_t i = 0; i < nb.size(); i++) {
+            pc_idx[(size_t)q * P + i] = (int32_t)(nb[i] - pool.data());
+            pc_sim[(size_t)q * P + i] = sims[i];
+        }
+        pc_cnt[q] = (int32_t)nb.size();
+        std::vector<int> t = get_top_N_recom(nb, user, NT, sims);
+        for (int i = 0; i < NT; i++) top[(size_t)q * NT + i] = t[i];
+    }
+    write_npy(dir + "/pc_idx.npy", pc_idx, {(size_t)Q, (size_t)P});
+    write_npy(dir + "/pc_sim.npy", pc_sim, {(size_t)Q, (size_t)P});
+    write_npy(dir + "/pc_cnt.npy", pc_cnt, {(size_t)Q});
+    write_npy(dir + "/top.npy", top, {(size_t)Q, (size_t)NT});
+    return 0;
+}
+
 // --------------------------------------------------------------- bench mode
 // bench NH NA K seed — the reference's own CPU path on synthetic data, one
 // thread, as shipped (-O0). Prints one JSON line.
@@ -408,6 +470,7 @@ int main(int argc, char** argv) {
     if (m == "lloyd") return mode_lloyd(argc - 1, argv + 1);
     if (m == "kmeanspp") return mode_kmeanspp(argc - 1, argv + 1);
     if (m == "bench") return mode_bench(argc - 1, argv + 1);
+    if (m == "recom") return mode_recom(argc - 1, argv + 1);
     fprintf(stderr, "unknown mode %s\n", m.c_str());
     return 2;
 }

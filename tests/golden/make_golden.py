@@ -10,7 +10,7 @@ include/lshkm_synth.h at the (seed, rows, d) recorded in cases.json, except
 external fp64 centroids, which are stored.
 
 Only runs in the build container (the reference is absent on the GPU box).
-Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp]
+Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,recom]
 (--only regenerates those kinds and keeps the other cases' entries.)
 """
 import json
@@ -63,6 +63,45 @@ KPP_CASES = [
     ("kpp_dup", 2000, 16, 24, "euclidean", 2028, 20, 4),
     ("kpp_c128", 2000, 128, 16, "cosine", 2029, 21, 1),
 ]
+RECOM_CASES = [
+    # name, N, d, Q, P, NTOP, seed, values ("dyadic": k/8, squares exact; "f64": general doubles)
+    ("recom_dy", 300, 20, 80, 10, 5, 4001, "dyadic"),
+    ("recom_f64", 400, 24, 60, 15, 2, 4002, "f64"),
+    ("recom_big", 3000, 16, 12, 40, 5, 4003, "dyadic"),
+]
+
+
+def recom_inputs(N, d, Q, seed, values):
+    """Pool rows (with duplicates and a zero row: equal / NaN similarities),
+    users (some are pool rows, as in main.cpp's part A), means, unknown index
+    sets and ascending candidate lists of every size class (0, 1, P, N)."""
+    rng = np.random.default_rng(seed)
+    if values == "dyadic":
+        X = rng.integers(-40, 41, size=(N, d)).astype(np.float64) / 8.0
+        xm = rng.integers(-32, 33, size=N).astype(np.float64) / 16.0
+    else:
+        X = rng.standard_normal((N, d)) * 1.7
+        xm = rng.standard_normal(N)
+    for i in range(0, N, 7):                      # duplicates of earlier rows
+        X[i] = X[(i * 13) % max(i, 1)]
+    X[N // 2] = 0.0                               # zero row: NaN similarities
+    X[N // 3] = 2.0 * X[N // 5]                   # parallel rows: equal similarities
+    U = X[rng.integers(0, N, size=Q)].copy()
+    for q in range(0, Q, 3):
+        U[q] = (rng.integers(-40, 41, size=d) / 8.0) if values == "dyadic" else rng.standard_normal(d)
+    um = (rng.integers(-32, 33, size=Q) / 16.0) if values == "dyadic" else rng.standard_normal(Q)
+    unk, cand = [], []
+    sizes = [0, 1, 2, 5, 10, 11, 40, N]
+    for q in range(Q):
+        m = int(rng.integers(0, d + 1)) if q % 5 else int(rng.integers(0, 3))
+        unk.append(np.sort(rng.choice(d, size=m, replace=False)).astype(np.int32))
+        n = sizes[q % len(sizes)] if q < 2 * len(sizes) else int(rng.integers(0, N + 1))
+        cand.append(np.sort(rng.choice(N, size=n, replace=False)).astype(np.int32))
+    csr = lambda ls: (np.cumsum([0] + [len(l) for l in ls]).astype(np.int64),
+                      np.concatenate(ls).astype(np.int32) if ls else np.zeros(0, np.int32))
+    up, ui = csr(unk)
+    cp, ci = csr(cand)
+    return dict(x=X, xmean=xm, u=U, umean=um.astype(np.float64), unk_ptr=up, unk_idx=ui, cand_ptr=cp, cand_idx=ci)
 
 
 def run(args):
@@ -139,6 +178,17 @@ def main(only=None):
             run(["kmeanspp", os.path.join(tmp, "x.f32"), N, d, K, metric, seed, out])
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
             meta[name] = dict(kind="kmeanspp", N=N, d=d, K=K, metric=metric, seed=seed, data_seed=dseed, dup=dup)
+        for (name, N, d, Q, P, NT, seed, values) in (RECOM_CASES if want("recom") else []):
+            out = os.path.join(tmp, name); os.makedirs(out)
+            inp = recom_inputs(N, d, Q, seed, values)
+            ext = dict(x="f64", xmean="f64", u="f64", umean="f64", unk_ptr="i64", unk_idx="i32",
+                       cand_ptr="i64", cand_idx="i32")
+            for k, e in ext.items():
+                inp[k].tofile(os.path.join(out, f"{k}.{e}"))
+            run(["recom", out, N, d, Q, P, NT])
+            res = load_dir(out); res.update(inp)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+            meta[name] = dict(kind="recom", N=N, d=d, Q=Q, P=P, NTOP=NT, seed=seed, values=values)
     finally:
         shutil.rmtree(tmp)
     with open(os.path.join(HERE, "cases.json"), "w") as f:

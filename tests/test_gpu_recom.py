@@ -1,0 +1,78 @@
+"""GPU parity: the recommend step — get_P_closest and
+get_top_N_recom (crypto_rec.hpp:213-325) — against the reference's golden
+outputs (tests/golden/recom_*.npz, made by oracle/_ref/ref_harness) and, at
+larger sizes, the CPU oracle. Ties and NaN similarities (duplicate / parallel /
+zero rows) exercise the exact quicksort replay."""
+import numpy as np
+import pytest
+
+import oracle
+from amd import lshkm
+from conftest import cases, golden, golden_meta
+
+META = golden_meta()
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return lshkm.Context(0)
+
+
+def dev(ctx, a):
+    return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+
+
+def run_gpu(ctx, X, xm, U, um, up, ui, cp, ci, P, NT):
+    idx, sim, cnt = lshkm.p_closest(ctx, dev(ctx, X), dev(ctx, U), dev(ctx, cp), dev(ctx, ci), P)
+    top = lshkm.top_n_recom(ctx, dev(ctx, X), dev(ctx, xm), dev(ctx, um), dev(ctx, up), dev(ctx, ui), idx, sim, cnt, NT)
+    return idx.cpu().numpy(), sim.cpu().numpy(), cnt.cpu().numpy(), top.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", cases("recom"))
+def test_recommend_golden(ctx, name):
+    m, g = META[name], golden(name)
+    idx, sim, cnt, top = run_gpu(ctx, g["x"], g["xmean"], g["u"], g["umean"], g["unk_ptr"], g["unk_idx"],
+                                 g["cand_ptr"], g["cand_idx"], m["P"], m["NTOP"])
+    assert np.array_equal(cnt, g["pc_cnt"])
+    has = cnt > 0                     # main.cpp:161 skips users without neighbours
+    if m["values"] == "dyadic":       # squares exact: pow(x, 2) == x * x, bit-exact everywhere
+        assert np.array_equal(idx, g["pc_idx"])
+        assert np.array_equal(sim.view(np.uint64), g["pc_sim"].view(np.uint64))
+        assert np.array_equal(top[has], g["top"][has])
+    else:                             # general doubles: glibc pow(x, 2) may differ from x * x by an ulp
+        assert np.allclose(sim, g["pc_sim"], rtol=1e-13, atol=1e-15, equal_nan=True)
+        agree = (idx == g["pc_idx"]).all(axis=1) & (top == g["top"]).all(axis=1)
+        assert agree[has].mean() >= 0.95, agree[has].mean()
+
+
+@pytest.mark.parametrize("N,d,nq,P,NT,levels,seed", [
+    (20_000, 32, 1500, 20, 5, 41, 1),       # dyadic values, mostly distinct similarities
+    (5_000, 8, 800, 15, 4, 3, 2),           # values in {-1, 0, 1}: ties everywhere (exact replay)
+    (3_000, 64, 300, 64, 8, 81, 3),         # P = 64, long lists
+])
+def test_recommend_matches_oracle(ctx, N, d, nq, P, NT, levels, seed):
+    rng = np.random.default_rng(seed)
+    half = levels // 2
+    X = rng.integers(-half, half + 1, size=(N, d)).astype(np.float64) / (8.0 if levels > 3 else 1.0)
+    X[7] = 0.0
+    U = rng.integers(-half, half + 1, size=(nq, d)).astype(np.float64) / (8.0 if levels > 3 else 1.0)
+    xm = rng.integers(-16, 17, size=N) / 16.0
+    um = rng.integers(-16, 17, size=nq) / 16.0
+    sizes = rng.integers(0, 3 * P, size=nq)
+    sizes[::7] = rng.integers(0, N // 2, size=len(sizes[::7]))
+    cand = [np.sort(rng.choice(N, size=int(s), replace=False)).astype(np.int32) for s in sizes]
+    cp = np.cumsum([0] + [len(c) for c in cand]).astype(np.int64)
+    ci = np.concatenate(cand).astype(np.int32)
+    unk = [np.sort(rng.choice(d, size=int(rng.integers(0, d + 1)), replace=False)).astype(np.int32) for _ in range(nq)]
+    up = np.cumsum([0] + [len(u) for u in unk]).astype(np.int64)
+    ui = np.concatenate(unk).astype(np.int32)
+    w_idx, w_sim, w_cnt = oracle.p_closest(X, U, cp, ci, P)
+    w_top = oracle.top_n_recom(X, xm, U, um, up, ui, w_idx, w_sim, w_cnt, NT)
+    idx, sim, cnt, top = run_gpu(ctx, X, xm, U, um, up, ui, cp, ci, P, NT)
+    assert np.array_equal(cnt, w_cnt)
+    assert np.array_equal(idx, w_idx)
+    assert np.array_equal(sim.view(np.uint64), w_sim.view(np.uint64))
+    assert np.array_equal(top, w_top)

@@ -134,6 +134,19 @@ def test_kmeans_pp_and_rand_selection(name):
     assert np.array_equal(oracle.rand_selection(m["N"], m["K"], m["seed"]), g["rand_rows"])
 
 
+@pytest.mark.parametrize("name", cases("recom"))
+def test_recommend_step(name):
+    m, g = META[name], golden(name)
+    idx, sim, cnt = oracle.p_closest(g["x"], g["u"], g["cand_ptr"], g["cand_idx"], m["P"])
+    assert np.array_equal(cnt, g["pc_cnt"])
+    assert np.array_equal(idx, g["pc_idx"])
+    assert np.array_equal(sim.view(np.uint64), g["pc_sim"].view(np.uint64))
+    top = oracle.top_n_recom(g["x"], g["xmean"], g["u"], g["umean"], g["unk_ptr"], g["unk_idx"], idx, sim, cnt,
+                             m["NTOP"])
+    has = cnt > 0                     # main.cpp:161 skips users without neighbours
+    assert np.array_equal(top[has], g["top"][has])
+
+
 def test_probe_sequence_rules():
     # lsh_cube.hpp:148-150 quirk: probes == 1 skips Hamming distance 1.
     assert list(oracle.cube_probe_seq(0, 1, 4)) == [0, 0b11]
