@@ -493,6 +493,82 @@ std::vector<CustVector<T>*> rand_selection(std::vector<CustVector<T>>& input_vec
     return rand_selection(input_vectors, cluster_num, clock_seed());
 }
 
+// ------------------------------------------------------------ recommendation
+// get_P_closest (crypto_rec.hpp:213-231): sorts `neighbors` by similarity to
+// `user` as the reference's quicksort does, keeps the first P, returns their
+// similarities. fp64 throughout (no fp32 restriction here).
+template <typename T>
+std::vector<double> get_P_closest(std::vector<CustVector<T>*>& neighbors, CustVector<T>& user, int P) {
+    static_assert(std::is_same<T, double>::value, "lshkm_compat::get_P_closest matches CustVector<double> only");
+    const size_t n = neighbors.size(), d = user.getDimensions()->size();
+    if (n == 0 || P < 1) return std::vector<double>();
+    std::vector<double> X(n * d);
+    for (size_t i = 0; i < n; i++) {
+        const std::vector<T>& x = *neighbors[i]->getDimensions();
+        if (x.size() != d) throw std::invalid_argument("lshkm_compat: neighbour dimension mismatch");
+        for (size_t j = 0; j < d; j++) X[i * d + j] = x[j];
+    }
+    std::vector<int64_t> ptr = {0, (int64_t)n};
+    std::vector<int32_t> cand(n);
+    for (size_t i = 0; i < n; i++) cand[i] = (int32_t)i;
+    DevMem Xd = upload(X.data(), X.size()), Ud = upload(user.getDimensions()->data(), d);
+    DevMem pd = upload(ptr.data(), 2), cd = upload(cand.data(), n);
+    DevMem oi(sizeof(int32_t) * P), os(sizeof(double) * P), oc(sizeof(int32_t));
+    check(lshkm_p_closest(context(), Xd.as<double>(), (int64_t)n, (int)d, Ud.as<double>(), 1, pd.as<int64_t>(),
+                          cd.as<int32_t>(), P, oi.as<int32_t>(), os.as<double>(), oc.as<int32_t>()));
+    int32_t c = 0;
+    download(&c, oc, 1);
+    std::vector<int32_t> idx(P);
+    std::vector<double> sim(P);
+    download(idx.data(), oi, P);
+    download(sim.data(), os, P);
+    // the reference sorts the whole vector, then resizes it to P if longer:
+    // either way the caller sees the first min(n, P) in sorted order
+    std::vector<CustVector<T>*> sorted(c);
+    for (int i = 0; i < c; i++) sorted[i] = neighbors[idx[i]];
+    neighbors = sorted;
+    sim.resize(c);
+    return sim;
+}
+
+// get_top_N_recom (crypto_rec.hpp:305-325) with the similarities of get_P_closest.
+template <typename T>
+std::vector<int> get_top_N_recom(std::vector<CustVector<T>*>& neighbors, CustVector<T>& user, int N,
+                                 std::vector<double> similarities) {
+    static_assert(std::is_same<T, double>::value, "lshkm_compat::get_top_N_recom matches CustVector<double> only");
+    const size_t n = neighbors.size(), d = user.getDimensions()->size();
+    const std::vector<int> unk = user.getUnknownIndexes();
+    std::vector<int> out(N > 0 ? N : 0, 0);
+    if (N <= 0) return out;
+    if (similarities.size() < n) throw std::invalid_argument("lshkm_compat: fewer similarities than neighbours");
+    const size_t rows = n > 0 ? n : 1;
+    std::vector<double> X(rows * d, 0.0), xm(rows, 0.0);
+    for (size_t i = 0; i < n; i++) {
+        const std::vector<T>& x = *neighbors[i]->getDimensions();
+        for (size_t j = 0; j < d && j < x.size(); j++) X[i * d + j] = x[j];
+        xm[i] = neighbors[i]->getKnownMean();
+    }
+    const int P = n > 0 ? (int)n : 1;
+    std::vector<int32_t> nb(P, 0), cnt = {(int32_t)n};
+    std::vector<double> sm(P, 0.0);
+    for (size_t i = 0; i < n; i++) { nb[i] = (int32_t)i; sm[i] = similarities[i]; }
+    std::vector<int64_t> up = {0, (int64_t)unk.size()};
+    std::vector<int32_t> ui(unk.begin(), unk.end());
+    if (ui.empty()) ui.push_back(0);
+    const double um = user.getKnownMean();
+    DevMem Xd = upload(X.data(), X.size()), xmd = upload(xm.data(), rows), umd = upload(&um, 1);
+    DevMem upd = upload(up.data(), 2), uid = upload(ui.data(), ui.size());
+    DevMem nbd = upload(nb.data(), nb.size()), smd = upload(sm.data(), sm.size()), cnd = upload(cnt.data(), 1);
+    DevMem od(sizeof(int32_t) * N);
+    check(lshkm_top_n_recom(context(), Xd.as<double>(), xmd.as<double>(), (int64_t)rows, (int)d, umd.as<double>(), 1,
+                            upd.as<int64_t>(), uid.as<int32_t>(), nbd.as<int32_t>(), smd.as<double>(),
+                            cnd.as<int32_t>(), P, N, od.as<int32_t>()));
+    std::vector<int32_t> o(N);
+    download(o.data(), od, N);
+    for (int i = 0; i < N; i++) out[i] = o[i];
+    return out;
+}
+
 }  // namespace lshkm_compat
 
 #endif  // LSHKM_COMPAT_HPP

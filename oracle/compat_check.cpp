@@ -35,6 +35,7 @@ system_clock::time_point system_clock::now() noexcept {
 #include "clustering_phases/assignment.hpp"
 #include "clustering_phases/update.hpp"
 #include "clustering_phases/initialization.hpp"
+#include "crypto_rec.hpp"
 
 #include "../include/lshkm_compat.hpp"
 #include "../include/lshkm_synth.h"
@@ -129,6 +130,50 @@ static void check_cube(std::vector<Vec>& data, const std::string& metric, int k,
     delete gpu;
 }
 
+// get_P_closest + get_top_N_recom as main.cpp:160-168 chains them. Pool rows
+// carry dyadic known means; users get unknown-index sets. Neighbour lists
+// include duplicates of one row (ties) and a zero row (NaN similarities).
+static void check_recom(std::vector<Vec>& data, int P) {
+    const int N = (int)data.size(), d = (int)data[0].getDimensions()->size();
+    std::vector<Vec> pool;
+    pool.reserve(N + 8);
+    for (int i = 0; i < N; i++) {
+        std::set<int> none;
+        pool.emplace_back("pool" + std::to_string(i), *data[i].getDimensions(), none, ((i * 37) % 33 - 16) / 16.0);
+    }
+    for (int k = 0; k < 6; k++) {          // duplicates of row 5 and a zero row
+        std::set<int> none;
+        std::vector<double> v = k < 5 ? *data[5].getDimensions() : std::vector<double>(d, 0.0);
+        pool.emplace_back("dup" + std::to_string(k), v, none, 0.25 * k);
+    }
+    const std::string tag = "recom ";
+    for (int q = 0; q < 40; q++) {
+        std::set<int> unk;
+        for (int j = 0; j < d; j++)
+            if ((j * 7 + q * 3) % 5 == 0) unk.insert(j);
+        Vec ua("user" + std::to_string(q), *data[(q * 131) % N].getDimensions(), unk, ((q * 11) % 17 - 8) / 8.0);
+        Vec ub = ua;
+        std::vector<Vec*> na, nb;
+        const int n = (q * 53) % (3 * P + 5);
+        for (int i = 0; i < n; i++) {
+            Vec* p = &pool[(i * 97 + q) % pool.size()];
+            na.push_back(p);
+        }
+        if (q % 4 == 0)
+            for (int k = 0; k < 6; k++) na.push_back(&pool[N + k]);
+        nb = na;
+        if (na.empty()) continue;
+        std::vector<double> sa = get_P_closest(na, ua, P);
+        std::vector<double> sb = lshkm_compat::get_P_closest(nb, ub, P);
+        cmp_ptrs(na, nb, tag + "P-closest order, user " + std::to_string(q));
+        if (sa.size() != sb.size() || (!sa.empty() && std::memcmp(sa.data(), sb.data(), sa.size() * sizeof(double))))
+            fail(tag + "similarities, user " + std::to_string(q));
+        if (get_top_N_recom(na, ua, 5, sa) != lshkm_compat::get_top_N_recom(nb, ub, 5, sb))
+            fail(tag + "top-N, user " + std::to_string(q));
+        g_stat["recom_users"]++;
+    }
+}
+
 static void check_init(std::vector<Vec>& data, const std::string& metric, int K) {
     g_seed += 303;
     const std::string tag = "init/" + metric + " ";
@@ -189,6 +234,7 @@ int main(int argc, char** argv) {
         check_kmeans(data, "cosine", K);
         check_init(data, "euclidean", K);
         check_init(data, "cosine", K);
+        check_recom(data, 10);
     } catch (const std::exception& e) {
         std::printf("EXCEPTION %s\n", e.what());
         return 1;

@@ -39,6 +39,10 @@ def test_shim_compiles_against_reference_headers(tmp_path):
         "    std::vector<CustVector<double>>&, int, std::string);\n"
         "template std::vector<CustVector<double>*> lshkm_compat::rand_selection<double>(\n"
         "    std::vector<CustVector<double>>&, int);\n"
+        "template std::vector<double> lshkm_compat::get_P_closest<double>(std::vector<CustVector<double>*>&,\n"
+        "    CustVector<double>&, int);\n"
+        "template std::vector<int> lshkm_compat::get_top_N_recom<double>(std::vector<CustVector<double>*>&,\n"
+        "    CustVector<double>&, int, std::vector<double>);\n"
         "template class lshkm_compat::GpuLshGenerator<float>;\n"
         "template class lshkm_compat::GpuCubeGenerator<int>;\n")
     r = subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Wno-unused-function", "-I", REF_LIB,
@@ -63,3 +67,4 @@ def test_shim_matches_reference_functions(args):
                 "cube_cosine_probe_rows"):
         assert int(stats[key]) > 0, (key, stats)
     assert int(stats["kmeans_euclidean_iterations"]) >= 2 and int(stats["kmeans_cosine_iterations"]) >= 2, stats
+    assert int(stats["recom_users"]) >= 30, stats
