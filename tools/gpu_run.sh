@@ -11,7 +11,7 @@ cd "$R"
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest.log" 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
       rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { echo "tests rc=$rc"; exit $rc; } ;;
     bench)
       timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
