@@ -541,6 +541,97 @@ int lshkm_hash_assign(lshkm_lsh lsh, const float* X, int64_t N, const double* C,
                        phi, bucket);
 }
 
+int lshkm_range_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
+                       const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key_host,
+                       const int32_t* src_rows_host, int32_t* assign, double* dist, int* passes_host) {
+    LSHKM_CHECK(ctx && (X || N == 0) && C && comb_ptr && (assign || N == 0) && (dist || N == 0) && N >= 0 &&
+                    N < (1ll << 31) && d > 0 && K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    lshkm::Buf* w = ctx->ws_range;
+    int rc;
+    int64_t M = 0;
+    LSHKM_HIP(hipMemcpyAsync(&M, comb_ptr + K, 8, hipMemcpyDeviceToHost, s));
+    LSHKM_HIP(hipStreamSynchronize(s));
+    LSHKM_CHECK(M >= 0 && (M == 0 || comb_idx), LSHKM_ERR_ARG, "bad combined-bucket CSR");
+    const size_t scratch = sort_scratch_bytes(std::max<int64_t>(M, 1), std::max<int64_t>(N, 1));
+    if ((rc = w[0].reserve(64)) || (rc = w[1].reserve((size_t)std::max<int64_t>(M, 1) * 4 * 4)) ||
+        (rc = w[2].reserve(scratch)) || (rc = w[3].reserve((size_t)(N + 1) * 8)) ||
+        (rc = w[4].reserve((size_t)std::max<int64_t>(M, 1) * 9)) || (rc = w[5].reserve((size_t)K * 4)))
+        return rc;
+    double* r0 = (double*)w[0].p;                          // [0] r0, [1] pass count, [2] unassigned count
+    unsigned long long* cnt = (unsigned long long*)w[0].p + 1;
+    int32_t* rows = (int32_t*)w[1].p;
+    int32_t* cents = rows + std::max<int64_t>(M, 1);
+    int32_t* rows_s = cents + std::max<int64_t>(M, 1);
+    int32_t* cents_s = rows_s + std::max<int64_t>(M, 1);
+    int64_t* vptr = (int64_t*)w[3].p;
+    double* cache = (double*)w[4].p;
+    int8_t* cached = (int8_t*)(cache + std::max<int64_t>(M, 1));
+    const int32_t* key = nullptr;
+    if (key_host) {
+        LSHKM_HIP(hipMemcpyAsync(w[5].p, key_host, (size_t)K * 4, hipMemcpyHostToDevice, s));
+        key = (const int32_t*)w[5].p;
+    }
+    if ((rc = launch_range_radius(s, C, K, d, metric, r0))) return rc;
+    if ((rc = launch_range_init(s, N, assign, dist))) return rc;
+    int passes = 0;
+    if (M > 0 && N > 0) {
+        if ((rc = launch_range_pairs(s, comb_ptr, comb_idx, K, rows, cents))) return rc;
+        if ((rc = stable_sort_by_key(s, rows, 1, cents, M, N, rows_s, cents_s, w[2].p))) return rc;
+        if ((rc = launch_csr_bounds(s, rows_s, M, N, vptr))) return rc;
+        LSHKM_HIP(hipMemsetAsync(cached, 0, (size_t)M, s));
+        // the do-while of assignment.hpp:160-216, one launch per pass
+        for (;;) {
+            unsigned long long assigned = 0;
+            LSHKM_HIP(hipMemsetAsync(cnt, 0, 8, s));
+            if ((rc = launch_range_pass(s, X, d, C, K, metric, key, vptr, cents_s, cache, cached, N, r0, passes,
+                                        assign, dist, cnt)))
+                return rc;
+            passes++;
+            LSHKM_HIP(hipMemcpyAsync(&assigned, cnt, 8, hipMemcpyDeviceToHost, s));
+            LSHKM_HIP(hipStreamSynchronize(s));
+            if (!assigned) break;
+        }
+    } else {
+        passes = 1;     // one pass over empty buckets assigns nothing
+    }
+    // lloyds_for_remaining (assignment.hpp:83-104): the Lloyd path on the rows left unassigned
+    if (N > 0) {
+        if ((rc = w[6].reserve((size_t)N * 4))) return rc;
+        int32_t* list = (int32_t*)w[6].p;
+        unsigned long long* ucnt = cnt + 1;
+        unsigned long long U = 0;
+        LSHKM_HIP(hipMemsetAsync(ucnt, 0, 8, s));
+        if ((rc = launch_range_unassigned(s, assign, N, list, ucnt))) return rc;
+        LSHKM_HIP(hipMemcpyAsync(&U, ucnt, 8, hipMemcpyDeviceToHost, s));
+        LSHKM_HIP(hipStreamSynchronize(s));
+        if (U > 0) {
+            if ((rc = w[7].reserve((size_t)U * d * 4)) || (rc = w[8].reserve((size_t)U * 12))) return rc;
+            float* Xr = (float*)w[7].p;
+            double* dr = (double*)w[8].p;
+            int32_t* ar = (int32_t*)(dr + U);
+            if ((rc = launch_range_gather(s, X, d, list, (int64_t)U, Xr))) return rc;
+            if ((rc = assign_impl(ctx, Xr, (int64_t)U, d, C, K, metric, nullptr, ar, dr, nullptr, nullptr, nullptr,
+                                  nullptr)))
+                return rc;
+            if ((rc = launch_range_scatter(s, list, (int64_t)U, ar, dr, assign, dist))) return rc;
+        }
+    }
+    // the centroid override (assignment.hpp:125-127, :143-145)
+    if (src_rows_host) {
+        if ((rc = ctx->ws_src.reserve((size_t)K * 4))) return rc;
+        LSHKM_HIP(hipMemcpyAsync(ctx->ws_src.p, src_rows_host, (size_t)K * 4, hipMemcpyHostToDevice, s));
+        if ((rc = launch_assign_override(s, (const int32_t*)ctx->ws_src.p, K, N, assign, dist))) return rc;
+        LSHKM_HIP(hipStreamSynchronize(s));     // the host arrays may be freed on return
+    }
+    if (key_host) LSHKM_HIP(hipStreamSynchronize(s));
+    if (passes_host) *passes_host = passes;
+    return 0;
+}
+
 int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X) {
     LSHKM_CHECK(ctx && (X || rows == 0) && rows >= 0 && d > 0, LSHKM_ERR_ARG, "bad arguments");
     LSHKM_HIP(hipSetDevice(ctx->device));

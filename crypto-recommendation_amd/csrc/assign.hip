@@ -416,9 +416,34 @@ __global__ void assign_override_kernel(const int32_t* __restrict__ src, int K, i
     dist[r] = 0.0;
 }
 
+// Same, one block with the K source rows in LDS (K <= OV_LDS_MAX): the
+// later-centroid scan reads LDS instead of K^2/2 global loads.
+constexpr int OV_LDS_MAX = 8192;
+__global__ __launch_bounds__(1024) void assign_override_lds_kernel(const int32_t* __restrict__ src, int K, int64_t N,
+                                                                  int32_t* __restrict__ assign,
+                                                                  double* __restrict__ dist) {
+    __shared__ int32_t ls[OV_LDS_MAX];
+    for (int c = threadIdx.x; c < K; c += blockDim.x) ls[c] = src[c];
+    __syncthreads();
+    for (int c = threadIdx.x; c < K; c += blockDim.x) {
+        const int32_t r = ls[c];
+        if (r < 0 || r >= N) continue;
+        bool last = true;
+        for (int c2 = c + 1; c2 < K && last; c2++) last = ls[c2] != r;
+        if (last) {
+            assign[r] = c;
+            dist[r] = 0.0;
+        }
+    }
+}
+
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist) {
-    hipLaunchKernelGGL(assign_override_kernel, dim3((K + 255) / 256), dim3(256), 0, s, src_rows, K, N, assign, dist);
+    if (K <= OV_LDS_MAX)
+        hipLaunchKernelGGL(assign_override_lds_kernel, dim3(1), dim3(1024), 0, s, src_rows, K, N, assign, dist);
+    else
+        hipLaunchKernelGGL(assign_override_kernel, dim3((K + 255) / 256), dim3(256), 0, s, src_rows, K, N, assign,
+                           dist);
     return kstatus("assign.hip");
 }
 

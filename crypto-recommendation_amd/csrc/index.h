@@ -48,6 +48,8 @@ struct lshkm_ctx_s {
     lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src, ws_hfix, ws_ct, ws_seg, ws_tuples;
     // scatter / query / update workspace (see api_index.cpp for the slot map)
     lshkm::Buf ws[16];
+    // range assignment workspace (lshkm_range_assign)
+    lshkm::Buf ws_range[12];
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
     bool timing = false;
     hipEvent_t tev[2] = {nullptr, nullptr};

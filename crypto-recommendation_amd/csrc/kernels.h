@@ -158,6 +158,20 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
                       float* cbound);
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
 
+// Range assignment (range.hip).
+int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0);
+int launch_range_pairs(hipStream_t s, const int64_t* comb_ptr, const int32_t* comb_idx, int K, int32_t* rows,
+                       int32_t* cents);
+int launch_range_init(hipStream_t s, int64_t N, int32_t* assign, double* dist);
+int launch_range_pass(hipStream_t s, const float* X, int d, const double* C, int K, int metric, const int32_t* key,
+                      const int64_t* vptr, const int32_t* cents, double* cache, int8_t* cached, int64_t N,
+                      const double* r0, int64_t pass, int32_t* assign, double* dist, unsigned long long* count);
+int launch_range_unassigned(hipStream_t s, const int32_t* assign, int64_t N, int32_t* list,
+                            unsigned long long* count);
+int launch_range_gather(hipStream_t s, const float* X, int d, const int32_t* list, int64_t M, float* Xr);
+int launch_range_scatter(hipStream_t s, const int32_t* list, int64_t M, const int32_t* ar, const double* dr,
+                         int32_t* assign, double* dist);
+
 // Synthetic data.
 int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X);
 

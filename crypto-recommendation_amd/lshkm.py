@@ -81,6 +81,7 @@ def lib():
             "lshkm_cube_import_coins": (i32, [vp, vp, vp, vp, i64, C.c_uint32]),
             "lshkm_coins_draw": (i32, [C.POINTER(C.c_uint32), vp, i64, vp]),
             "lshkm_lloyd_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp]),
+            "lshkm_range_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp, C.POINTER(i32)]),
             "lshkm_hash_assign": (i32, [vp, vp, i64, vp, i32, vp, vp, vp, vp, vp, vp]),
             "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
@@ -340,6 +341,26 @@ def lloyd_assign(ctx, X, Cc, metric="euclidean", src_rows=None, assign=None, dis
     _ck(lib().lshkm_lloyd_assign(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _np_ptr(sr),
                                  _t_ptr(assign), _t_ptr(dist)))
     return assign, dist
+
+
+def range_assign(ctx, X, Cc, comb_ptr, comb_idx, metric="euclidean", key=None, src_rows=None):
+    """lsh_range_assignment / cube_range_assignment (assignment.hpp:108-145) over
+    the centroids' combined buckets (device or host CSR). Returns (assign, dist, passes)."""
+    torch = ctx.torch
+    N, d = X.shape
+    K = Cc.shape[0]
+    cp = torch.as_tensor(np.ascontiguousarray(comb_ptr, np.int64)).to(ctx.dev) if isinstance(comb_ptr, np.ndarray) else comb_ptr
+    ci = torch.as_tensor(np.ascontiguousarray(comb_idx, np.int32)).to(ctx.dev) if isinstance(comb_idx, np.ndarray) else comb_idx
+    if ci.numel() == 0:
+        ci = ctx.empty((1,), torch.int32)
+    assign = ctx.empty((N,), torch.int32)
+    dist = ctx.empty((N,), torch.float64)
+    kk = None if key is None else np.ascontiguousarray(key, np.int32)
+    sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
+    passes = C.c_int32(0)
+    _ck(lib().lshkm_range_assign(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _t_ptr(cp), _t_ptr(ci),
+                                 _np_ptr(kk), _np_ptr(sr), _t_ptr(assign), _t_ptr(dist), C.byref(passes)))
+    return assign, dist, passes.value
 
 
 def hash_assign(lsh, X, Cc, src_rows=None, tuples=True, phi=False, bucket=True):

@@ -10,6 +10,7 @@
  *   get_hypercube_combined_buckets   lib/lsh_cube.hpp:139-177
  *   lloyds_assignment                lib/clustering_phases/assignment.hpp:54-80
  *   k_means                          lib/clustering_phases/update.hpp:37-86
+ *   lsh_/cube_range_assignment       lib/clustering_phases/assignment.hpp:108-217
  *   HashGenerator plugin ABI         lib/generators/hash_generator.hpp:19-31
  *   CustHashtable::getBucketFromIndex / getHash lib/data_structures/cust_hashtable.hpp:116-125
  *
@@ -210,6 +211,23 @@ int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X_dev, int64_t N, int
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* counts_dev, int K, int d,
                           const double* C_old_dev, int metric, double min_dist, double* C_new_dev,
                           int* cont_host);
+
+/* --------------------------------------------------------- range assignment
+ * lsh_range_assignment / cube_range_assignment (assignment.hpp:108-145):
+ * remove_clustering, range_assignment (:148-217) over the combined buckets of
+ * the centroids, lloyds_for_remaining (:83-104) for the rows left unassigned,
+ * then the centroid override (src_rows_host as in lshkm_lloyd_assign).
+ * comb_ptr_dev [K+1] / comb_idx_dev: centroid i's combined bucket, in the
+ * reference's order — what lshkm_lsh_query (filtered = 0) or lshkm_cube_query
+ * returns for the centroid rows. Radius: find_min_vector_distance of the
+ * centroids / 2 (utils.hpp:161-178), doubled after every centroid.
+ * key_host [K] (may be NULL = all distinct): the reference caches distances by
+ * "<centroid id>to<row id>" (:176-186), so centroids with the same ID share
+ * entries (every "k_means_center" after k_means): give them equal keys.
+ * *passes_host (may be NULL) = passes of the do-while loop. N < 2^31. */
+int lshkm_range_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const double* C_dev, int K, int metric,
+                       const int64_t* comb_ptr_dev, const int32_t* comb_idx_dev, const int32_t* key_host,
+                       const int32_t* src_rows_host, int32_t* assign_dev, double* dist_dev, int* passes_host);
 
 /* ----------------------------------------------------------- initialization
  * k_means_pp (initialization.hpp:71-156): the K dataset rows chosen as initial

@@ -574,3 +574,96 @@ void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out) {
     for (int64_t i = 0; i < rows; i++)
         for (int j = 0; j < d; j++) out[i * d + j] = lshkm_synth_value(seed, (uint64_t)(row0 + i), (uint64_t)d, (uint64_t)j);
 }
+
+/* ---------------------------------------------------------- range assignment */
+
+/* find_min_vector_distance (utils.hpp:161-178) over the centroid rows: pairs
+ * (i, j > i) in order, the -1 sentinel and strict '<'. */
+static double min_pair_dist(int K, int d, const double* C, int metric) {
+    double mn = -1;
+    for (int i = 0; i < K; i++)
+        for (int j = i + 1; j < K; j++) {
+            const double dd = metric == 0 ? euclid_f64(C + (size_t)i * d, C + (size_t)j * d, d)
+                                          : cosine_f64(C + (size_t)i * d, C + (size_t)j * d, d);
+            if (mn == -1 || dd < mn) mn = dd;
+        }
+    return mn;
+}
+
+/* The reference's distanceMap (assignment.hpp:157,176-186), keyed by
+ * (centroid key, row): open addressing over 64-bit keys. */
+typedef struct { uint64_t* k; double* v; size_t cap; } dmap_t;
+static size_t dmap_slot(const dmap_t* m, uint64_t key) {
+    size_t h = (size_t)(lshkm_splitmix64(key) & (m->cap - 1));
+    while (m->k[h] != ~0ull && m->k[h] != key) h = (h + 1) & (m->cap - 1);
+    return h;
+}
+
+/* range_assignment (assignment.hpp:148-217) over the given combined buckets
+ * (comb_ptr/comb_idx: centroid i's bucket rows in the reference's order),
+ * preceded by remove_clustering and followed by lloyds_for_remaining
+ * (:83-104) and the centroid override (:125-127, :143-145), as
+ * lsh_range_assignment / cube_range_assignment (:108-145) run them.
+ * key[K] (or NULL = all distinct): centroids with equal keys share distance
+ * cache entries, as centroids with equal IDs do in the reference (e.g. every
+ * "k_means_center" after k_means, update.hpp:46). Returns the passes of the
+ * do-while loop. */
+int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, int metric,
+                    const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key,
+                    const int32_t* src_rows, int32_t* assign, double* dist) {
+    for (int64_t n = 0; n < N; n++) { assign[n] = -1; dist[n] = 0; }
+    double radius = min_pair_dist(K, d, C, metric) / 2;
+    double min_radius = 0;
+    const int64_t total = comb_ptr[K];
+    dmap_t m;
+    m.cap = 16;
+    while (m.cap < (size_t)(2 * total + 16)) m.cap <<= 1;
+    m.k = (uint64_t*)malloc(m.cap * sizeof(uint64_t));
+    m.v = (double*)malloc(m.cap * sizeof(double));
+    for (size_t i = 0; i < m.cap; i++) m.k[i] = ~0ull;
+    int passes = 0;
+    int64_t assigned;
+    do {
+        assigned = 0;
+        passes++;
+        for (int i = 0; i < K; i++) {
+            const uint64_t kc = (uint64_t)(uint32_t)(key ? key[i] : i) << 32;
+            for (int64_t e = comb_ptr[i]; e < comb_ptr[i + 1]; e++) {
+                const int32_t v = comb_idx[e];
+                if (assign[v] == -1 || (assign[v] != -1 && dist[v] >= min_radius)) {
+                    const size_t h = dmap_slot(&m, kc | (uint32_t)v);
+                    double dd;
+                    if (m.k[h] != ~0ull) dd = m.v[h];
+                    else {
+                        dd = metric == 0 ? or_euclid_dist_f32_f64(X + (size_t)v * d, C + (size_t)i * d, d)
+                                         : cosine_dist_f32_f64(X + (size_t)v * d, C + (size_t)i * d, d);
+                        m.k[h] = kc | (uint32_t)v;
+                        m.v[h] = dd;
+                    }
+                    if (dd >= min_radius && dd < radius) {
+                        if (assign[v] == -1) { assign[v] = i; dist[v] = dd; assigned++; }
+                        else if (dist[v] > dd) { assign[v] = i; dist[v] = dd; assigned++; }
+                    }
+                }
+            }
+            min_radius = radius;
+            radius = radius * 2;
+        }
+    } while (assigned > 0);
+    free(m.k); free(m.v);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t n = 0; n < N; n++) {
+        if (assign[n] != -1) continue;
+        double mn = -1; int arg = 0;
+        for (int c = 0; c < K; c++) {
+            double dd = metric == 0 ? or_euclid_dist_f32_f64(X + n * d, C + (size_t)c * d, d)
+                                    : cosine_dist_f32_f64(X + n * d, C + (size_t)c * d, d);
+            if (mn == -1 || dd < mn) { mn = dd; arg = c; }
+        }
+        assign[n] = arg; dist[n] = mn;
+    }
+    if (src_rows)
+        for (int c = 0; c < K; c++)
+            if (src_rows[c] >= 0) { assign[src_rows[c]] = c; dist[src_rows[c]] = 0; }
+    return passes;
+}

@@ -81,6 +81,13 @@ double or_euclid_dist_f32_f64(const float* x, const double* c, int d);
 int or_kmeans_update(int64_t N, int d, int K, const float* X, const int32_t* assign,
                      const double* C_old, int metric, double min_dist, double* C_new, int64_t* counts);
 
+/* ---- range assignment (assignment.hpp:108-217): combined buckets per
+ * centroid as a CSR, key[K] = distance-cache key per centroid (NULL = all
+ * distinct). Returns the number of passes. */
+int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, int metric,
+                    const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key,
+                    const int32_t* src_rows, int32_t* assign, double* dist);
+
 /* ---- initialization (initialization.hpp:39-156): the chosen dataset rows */
 void or_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows);
 void or_kmeans_pp(int64_t N, int d, int K, const float* X, int metric, uint64_t seed, int32_t* rows);

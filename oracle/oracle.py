@@ -51,6 +51,8 @@ def lib():
             "or_lloyd_assign": (None, [C.c_int64, C.c_int, C.c_int, f32p, f64p, C.c_int, C.c_void_p, i32p, f64p]),
             "or_kmeans_update": (C.c_int, [C.c_int64, C.c_int, C.c_int, f32p, i32p, f64p, C.c_int, C.c_double,
                                            f64p, i64p]),
+            "or_range_assign": (C.c_int, [C.c_int64, C.c_int, C.c_int, f32p, f64p, C.c_int, i64p, i32p,
+                                          C.c_void_p, C.c_void_p, i32p, f64p]),
             "or_rand_selection": (None, [C.c_uint64, C.c_int64, C.c_int, i32p]),
             "or_kmeans_pp": (None, [C.c_int64, C.c_int, C.c_int, f32p, C.c_int, C.c_uint64, i32p]),
             "or_p_closest": (None, [C.c_int, f64p, C.c_int64, f64p, i64p, i32p, C.c_int, i32p, f64p, i32p]),
@@ -189,6 +191,21 @@ def lloyd_assign(X, Cc, metric="euclidean", src_rows=None):
     sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
     lib().or_lloyd_assign(N, d, K, X, Cc, 0 if metric == "euclidean" else 1, _ptr(sr), a, dist)
     return a, dist
+
+
+def range_assign(X, Cc, comb_ptr, comb_idx, metric="euclidean", key=None, src_rows=None):
+    """range_assignment + lloyds_for_remaining + override (assignment.hpp:108-217).
+    Returns (assign, dist, passes)."""
+    X = np.ascontiguousarray(X, np.float32)
+    Cc = np.ascontiguousarray(Cc, np.float64)
+    N, d = X.shape; K = Cc.shape[0]
+    a = np.empty(N, np.int32); dist = np.empty(N, np.float64)
+    kk = None if key is None else np.ascontiguousarray(key, np.int32)
+    sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
+    passes = lib().or_range_assign(N, d, K, X, Cc, 0 if metric == "euclidean" else 1,
+                                   np.ascontiguousarray(comb_ptr, np.int64), np.ascontiguousarray(comb_idx, np.int32),
+                                   _ptr(kk), _ptr(sr), a, dist)
+    return a, dist, passes
 
 
 def kmeans_update(X, assign, C_old, metric="euclidean", min_dist=0.0):

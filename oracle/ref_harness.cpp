@@ -462,6 +462,67 @@ static int mode_bench(int argc, char** argv) {
     return 0;
 }
 
+// ------------------------------------------------------------- range mode
+// range IN N d K metric family k L div w probes iters min_dist seed OUT
+// lsh_range_assignment / cube_range_assignment (assignment.hpp:108-145) with
+// centroids = rows i*(N/K), then k_means (update.hpp:37-86), `iters` times.
+// Per iteration: the combined buckets of each centroid (comb<it>_ptr/idx,
+// lsh_cube.hpp:77-90 / :139-177, computed before the call as the call does),
+// assign<it>/dist<it>, centers<it> (the centroids used). The cube family is
+// only pinned at iteration 0 (later centers may hash to unseen h, whose coins
+// come from a dead engine, lsh_cube.hpp:113).
+static int mode_range(int argc, char** argv) {
+    if (argc < 16) { fprintf(stderr, "usage: range IN N d K metric family k L div w probes iters min_dist seed OUT\n"); return 2; }
+    std::string in = argv[1]; int N = atoi(argv[2]); int d = atoi(argv[3]); int K = atoi(argv[4]);
+    std::string metric = argv[5], family = argv[6];
+    int k = atoi(argv[7]), L = atoi(argv[8]), div = atoi(argv[9]); double w = atof(argv[10]);
+    int probes = atoi(argv[11]), iters = atoi(argv[12]); double min_dist = atof(argv[13]);
+    g_seed = atoll(argv[14]); std::string out = argv[15];
+    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<Vec> vecs = make_vectors(x, N, d, "");
+    std::vector<CustHashtable<double>*> tables;
+    CustHashtable<double>* cube = nullptr;
+    if (family == "lsh") tables = create_LSH_hashtables<double>(vecs, metric, k, L, div, w);
+    else cube = create_hypercube<double>(vecs, metric, k, w);
+    std::vector<Vec*> centroids(K);
+    std::vector<int32_t> src_rows(K);
+    for (int i = 0; i < K; i++) { centroids[i] = &vecs[i * (N / K)]; src_rows[i] = i * (N / K); }
+    write_npy(out + "/src_rows.npy", src_rows, {(size_t)K});
+    bool cont = true; int it = 0;
+    while (cont && it < iters) {
+        std::vector<double> cs;
+        for (int c = 0; c < K; c++) for (int j = 0; j < d; j++) cs.push_back((*centroids[c]->getDimensions())[j]);
+        write_npy(out + "/centers" + std::to_string(it) + ".npy", cs, {(size_t)K, (size_t)d});
+        std::vector<int32_t> key(K);
+        for (int c = 0; c < K; c++) {
+            key[c] = c;
+            for (int c2 = 0; c2 < c; c2++) if (centroids[c2]->getId() == centroids[c]->getId()) { key[c] = key[c2]; break; }
+        }
+        write_npy(out + "/key" + std::to_string(it) + ".npy", key, {(size_t)K});
+        std::vector<std::vector<int32_t>> comb;
+        for (int c = 0; c < K; c++)
+            comb.push_back(to_indices(family == "lsh" ? get_LSH_combined_buckets<double>(tables, centroids[c])
+                                                      : get_hypercube_combined_buckets<double>(*cube, centroids[c], probes, k),
+                                      vecs.data()));
+        csr_write(out, "comb" + std::to_string(it), comb);
+        if (family == "lsh") lsh_range_assignment(vecs, tables, centroids, metric);
+        else cube_range_assignment(vecs, *cube, centroids, metric, probes, k);
+        std::vector<int32_t> assign(N); std::vector<double> dist(N);
+        for (int n = 0; n < N; n++) { assign[n] = vecs[n].getCluster(); dist[n] = vecs[n].getDistFromCentroid(); }
+        write_npy(out + "/assign" + std::to_string(it) + ".npy", assign, {(size_t)N});
+        write_npy(out + "/dist" + std::to_string(it) + ".npy", dist, {(size_t)N});
+        cont = k_means(vecs, centroids, metric, min_dist);
+        it++;
+        if (family != "lsh") break;
+    }
+    std::vector<int32_t> nit(1, it);
+    write_npy(out + "/iters.npy", nit, {1});
+    for (auto c : centroids) if (c->getId() == "k_means_center") delete c;
+    for (auto t : tables) delete t;
+    delete cube;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness {lsh|cube|lloyd|kmeanspp|bench} ...\n"); return 2; }
     std::string m = argv[1];
@@ -471,6 +532,7 @@ int main(int argc, char** argv) {
     if (m == "kmeanspp") return mode_kmeanspp(argc - 1, argv + 1);
     if (m == "bench") return mode_bench(argc - 1, argv + 1);
     if (m == "recom") return mode_recom(argc - 1, argv + 1);
+    if (m == "range") return mode_range(argc - 1, argv + 1);
     fprintf(stderr, "unknown mode %s\n", m.c_str());
     return 2;
 }

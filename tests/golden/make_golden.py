@@ -10,7 +10,7 @@ include/lshkm_synth.h at the (seed, rows, d) recorded in cases.json, except
 external fp64 centroids, which are stored.
 
 Only runs in the build container (the reference is absent on the GPU box).
-Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,recom]
+Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,range,recom]
 (--only regenerates those kinds and keeps the other cases' entries.)
 """
 import json
@@ -62,6 +62,16 @@ KPP_CASES = [
     ("kpp_e_big", 40000, 8, 12, "euclidean", 2027, 19, 1),
     ("kpp_dup", 2000, 16, 24, "euclidean", 2028, 20, 4),
     ("kpp_c128", 2000, 128, 16, "cosine", 2029, 21, 1),
+]
+RANGE_CASES = [
+    # name, N, d, K, metric, family, k, L, div, w, probes, iters, min_dist, seed, data_seed, dup
+    # (dup g: row i is synth row i // g; g > N/K makes centroids 0 and 1 equal: radius 0)
+    ("range_lsh_e", 1500, 128, 16, "euclidean", "lsh", 4, 5, 10, 4.0, 0, 3, 0.01, 5001, 30, 1),
+    ("range_lsh_c", 1200, 64, 12, "cosine", "lsh", 5, 3, 1, 0.0, 0, 2, 0.01, 5002, 31, 1),
+    ("range_lsh_k3", 900, 16, 3, "euclidean", "lsh", 3, 4, 9, 2.0, 0, 3, 0.0, 5003, 32, 1),
+    ("range_lsh_dup", 800, 24, 8, "euclidean", "lsh", 3, 3, 8, 2.0, 0, 2, 0.0, 5004, 33, 150),
+    ("range_cube_e", 1500, 32, 12, "euclidean", "cube", 6, 1, 1, 2.0, 3, 1, 0.0, 5005, 34, 1),
+    ("range_cube_c", 1500, 128, 20, "cosine", "cube", 8, 1, 1, 0.0, 8, 1, 0.0, 5006, 35, 1),
 ]
 RECOM_CASES = [
     # name, N, d, Q, P, NTOP, seed, values ("dyadic": k/8, squares exact; "f64": general doubles)
@@ -178,6 +188,15 @@ def main(only=None):
             run(["kmeanspp", os.path.join(tmp, "x.f32"), N, d, K, metric, seed, out])
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
             meta[name] = dict(kind="kmeanspp", N=N, d=d, K=K, metric=metric, seed=seed, data_seed=dseed, dup=dup)
+        for (name, N, d, K, metric, fam, k, L, div, w, probes, iters, md, seed, dseed, dup) in \
+                (RANGE_CASES if want("range") else []):
+            out = os.path.join(tmp, name); os.makedirs(out)
+            x = kpp_data(dseed, N, d, dup); x.tofile(os.path.join(tmp, "x.f32"))
+            run(["range", os.path.join(tmp, "x.f32"), N, d, K, metric, fam, k, L, div, w, probes, iters,
+                 repr(md), seed, out])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
+            meta[name] = dict(kind="range", N=N, d=d, K=K, metric=metric, family=fam, k=k, L=L, div=div, w=w,
+                              probes=probes, iters=iters, min_dist=md, seed=seed, data_seed=dseed, dup=dup)
         for (name, N, d, Q, P, NT, seed, values) in (RECOM_CASES if want("recom") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
             inp = recom_inputs(N, d, Q, seed, values)

@@ -1,0 +1,144 @@
+"""GPU parity: range assignment (lsh_range_assignment / cube_range_assignment,
+assignment.hpp:108-217) — cluster IDs and distances bit-exact against the
+reference's golden outputs (incl. the shared-ID distance cache of
+"k_means_center" centroids) and, at larger sizes, against the CPU oracle on
+the combined buckets our own GPU queries produce."""
+import numpy as np
+import pytest
+
+import oracle
+from amd import lshkm
+from conftest import cases, golden, golden_meta, kpp_input
+
+META = golden_meta()
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return lshkm.Context(0)
+
+
+def to_dev(ctx, a):
+    return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+
+
+def same_bits(a, b):
+    return np.array_equal(np.asarray(a, np.float64).view(np.uint64), np.asarray(b, np.float64).view(np.uint64))
+
+
+@pytest.mark.parametrize("name", cases("range"))
+def test_range_golden(ctx, name):
+    m, g = META[name], golden(name)
+    X = to_dev(ctx, kpp_input(name).astype(np.float32))
+    for it in range(int(g["iters"][0])):
+        C = to_dev(ctx, g[f"centers{it}"])
+        a, dist, passes = lshkm.range_assign(ctx, X, C, g[f"comb{it}_ptr"], g[f"comb{it}_idx"], m["metric"],
+                                             key=g[f"key{it}"], src_rows=g["src_rows"] if it == 0 else None)
+        assert np.array_equal(a.cpu().numpy(), g[f"assign{it}"]), it
+        if it == 0:
+            # dataset-row centroids: (x_j - c_j) is exact, glibc pow(x,2) == x*x
+            assert same_bits(dist.cpu().numpy(), g[f"dist{it}"]), it
+        else:
+            # "k_means_center" fp64 means: pow(x,2) may differ from x*x by an ulp
+            # per term; the north star's tolerance is 1e-5 relative
+            want = g[f"dist{it}"]
+            rel = np.abs(dist.cpu().numpy() - want) / np.maximum(np.abs(want), 1e-300)
+            assert rel.max() <= 1e-14, (it, rel.max())
+        assert passes >= 1
+
+
+def build_index(ctx, m, X):
+    """The reference's tables for a range case, from its seed (draw order of
+    lsh_cube.hpp:44-74 / :108-136)."""
+    d, k = m["d"], m["k"]
+    if m["family"] == "lsh":
+        if m["metric"] == "euclidean":
+            V, t, r, _ = lshkm.params_lsh_euclidean(m["seed"], m["L"], k, d, m["w"])
+            idx = lshkm.LSH(ctx, "euclidean", d, k, m["L"], m["N"] // m["div"], m["w"], V=V, t=t, r=r)
+        else:
+            R, _ = lshkm.params_lsh_cosine(m["seed"], m["L"], k, d)
+            idx = lshkm.LSH(ctx, "cosine", d, k, m["L"], R=R)
+    else:
+        if m["metric"] == "euclidean":
+            V, t, st = lshkm.params_cube_euclidean(m["seed"], k, d, m["w"])
+            idx = lshkm.Cube(ctx, "euclidean", d, k, m["w"], V=V, t=t, rng_state=st)
+        else:
+            R, _ = lshkm.params_cube_cosine(m["seed"], k, d)
+            idx = lshkm.Cube(ctx, "cosine", d, k, R=R)
+    idx.build(X)
+    return idx
+
+
+@pytest.mark.parametrize("name", cases("range"))
+def test_range_end_to_end_first_iteration(ctx, name):
+    # iteration 0 from scratch: our index, our queries of the centroid rows
+    # (get_LSH_combined_buckets / get_hypercube_combined_buckets), our range pass
+    m, g = META[name], golden(name)
+    Xh = kpp_input(name).astype(np.float32)
+    X = to_dev(ctx, Xh)
+    idx = build_index(ctx, m, X)
+    src = g["src_rows"]
+    Q = X[to_dev(ctx, src.astype(np.int64))]
+    if m["family"] == "lsh":
+        ptr, ci = idx.query(Q, filtered=False)
+    else:
+        ptr, ci = idx.query(Q, m["probes"])
+    assert np.array_equal(ptr, g["comb0_ptr"]) and np.array_equal(ci, g["comb0_idx"])
+    a, dist, _ = lshkm.range_assign(ctx, X, to_dev(ctx, g["centers0"]), ptr, ci, m["metric"], key=g["key0"],
+                                    src_rows=src)
+    assert np.array_equal(a.cpu().numpy(), g["assign0"])
+    assert same_bits(dist.cpu().numpy(), g["dist0"])
+
+
+@pytest.mark.parametrize("metric,shared_key", [("euclidean", False), ("euclidean", True), ("cosine", False)])
+def test_range_large_vs_oracle(ctx, metric, shared_key):
+    # 200K x 128, K = 64 centroid rows, LSH L=5 k=4 (euclidean: w=4, nb=N/100;
+    # cosine: 16 buckets, so most rows sit in many combined buckets)
+    N, d, K, L, k = 200_000, 128, 64, 5, 4
+    X = ctx.synth(0x5EED + 7, N, d)
+    if metric == "euclidean":
+        V, t, r, _ = lshkm.params_lsh_euclidean(77, L, k, d, 4.0)
+        lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 4.0, V=V, t=t, r=r)
+    else:
+        R, _ = lshkm.params_lsh_cosine(78, L, 3, d)
+        lsh = lshkm.LSH(ctx, "cosine", d, 3, L, R=R)
+    lsh.build(X)
+    src = (np.arange(K) * (N // K)).astype(np.int32)
+    ptr, ci = lsh.query(X[to_dev(ctx, src.astype(np.int64))], filtered=False)
+    Cc = X[to_dev(ctx, src.astype(np.int64))].double()
+    key = np.zeros(K, np.int32) if shared_key else None
+    a, dist, passes = lshkm.range_assign(ctx, X, Cc, ptr, ci, metric, key=key, src_rows=src)
+    oa, od, op = oracle.range_assign(X.cpu().numpy(), Cc.cpu().numpy(), ptr, ci, metric, key=key, src_rows=src)
+    assert passes == op
+    assert np.array_equal(a.cpu().numpy(), oa)
+    assert same_bits(dist.cpu().numpy(), od)
+
+
+def test_range_edge_cases(ctx):
+    rng = np.random.default_rng(5)
+    N, d = 3000, 8
+    Xh = (rng.integers(-8, 9, size=(N, d)) / 4).astype(np.float32)
+    X = to_dev(ctx, Xh)
+    # (1) empty combined buckets: every row goes through lloyds_for_remaining
+    # (2) one centroid: no pairs, radius -0.5, nothing in range
+    # (3) duplicate centroids: radius 0, nothing in range
+    # (4) a row in every bucket, plus ragged buckets
+    for K, rows, comb in (
+        (4, [0, 10, 20, 30], [[], [], [], []]),
+        (1, [5], [list(range(0, N, 3))]),
+        (3, [7, 7, 100], [[1, 2, 3], [3, 4], list(range(50, 900))]),
+        (5, [1, 2, 3, 4, 5], [[0, 9, 11], list(range(N)), [], [0], list(range(0, N, 2))]),
+    ):
+        src = np.array(rows, np.int32)
+        ptr = np.cumsum([0] + [len(c) for c in comb]).astype(np.int64)
+        ci = np.array([v for c in comb for v in c], np.int32)
+        Cc = Xh[src].astype(np.float64)
+        for metric in ("euclidean", "cosine"):
+            a, dist, passes = lshkm.range_assign(ctx, X, to_dev(ctx, Cc), ptr, ci, metric, src_rows=src)
+            oa, od, op = oracle.range_assign(Xh, Cc, ptr, ci, metric, src_rows=src)
+            assert passes == op, (K, metric)
+            assert np.array_equal(a.cpu().numpy(), oa), (K, metric)
+            assert same_bits(dist.cpu().numpy(), od), (K, metric)

@@ -165,3 +165,17 @@ def test_minstd_and_uniform_int():
     vals = [oracle.lib().or_uniform_int(ctypes.byref(s), 0, 2147483645) for _ in range(2)]
     assert vals == [16806, 282475248]
     assert oracle.lib().or_minstd_seed(0) == 1 and oracle.lib().or_minstd_seed(2147483647) == 1
+
+
+@pytest.mark.parametrize("name", cases("range"))
+def test_range_assignment(name):
+    # lsh_/cube_range_assignment (assignment.hpp:108-145) on the reference's own
+    # combined buckets; iterations >= 1 run on "k_means_center" centroids whose
+    # shared ID collapses the distance cache (key = all zeros).
+    m, g = META[name], golden(name)
+    X = kpp_input(name)
+    for it in range(int(g["iters"][0])):
+        a, dist, _ = oracle.range_assign(X, g[f"centers{it}"], g[f"comb{it}_ptr"], g[f"comb{it}_idx"], m["metric"],
+                                         key=g[f"key{it}"], src_rows=g["src_rows"] if it == 0 else None)
+        assert np.array_equal(a, g[f"assign{it}"]), it
+        assert np.array_equal(dist.view(np.uint64), g[f"dist{it}"].view(np.uint64)), it
