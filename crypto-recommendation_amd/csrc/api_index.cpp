@@ -492,4 +492,33 @@ int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums, const int64_t* coun
     return km_finalize(ctx, sums, counts, K, d, C_old, metric, min_dist, C_new, cont);
 }
 
+int lshkm_silhouette(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, const double* C, int K,
+                     int metric, double* out_host, double* s_dev) {
+    LSHKM_CHECK(ctx && (X || N == 0) && (assign || N == 0) && C && out_host && N >= 0 && N < (1ll << 31) && d > 0 &&
+                    K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    int rc;
+    lshkm::Buf& wn = ctx->ws_range[9];     // near [K] int32, then raw [K] + out [K+1] doubles
+    lshkm::Buf& ws = ctx->ws_range[10];    // s [N] when the caller gives none
+    if ((rc = reserve(ctx, WS_ROWS, (size_t)std::max<int64_t>(N, 1) * 4)) || (rc = reserve(ctx, WS_CROW, (size_t)(K + 1) * 8)) ||
+        (rc = wn.reserve((size_t)K * 4 + 8 + (size_t)(2 * K + 1) * 8)) ||
+        (!s_dev && (rc = ws.reserve((size_t)std::max<int64_t>(N, 1) * 8))))
+        return rc;
+    int32_t* near = (int32_t*)wn.p;
+    double* raw = (double*)((char*)wn.p + ((size_t)K * 4 + 8) / 8 * 8);
+    double* out = raw + K;
+    double* sv = s_dev ? s_dev : (double*)ws.p;
+    // separate_clusters_from_input (utils.hpp:150-158): members in row order
+    if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
+    if ((rc = launch_sil_near(s, C, K, d, metric, near))) return rc;
+    if ((rc = launch_sil_points(s, X, d, metric, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), assign, near,
+                                N, sv)))
+        return rc;
+    if ((rc = launch_sil_sum(s, sv, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, N, raw, out))) return rc;
+    return d2h(ctx, out_host, out, (size_t)(K + 1) * 8);
+}
+
 }  // extern "C"

@@ -45,3 +45,33 @@ __device__ inline double exact_cosine(const float* __restrict__ x, const double*
     const double denom = __dmul_rn(sqrt(a), sqrt(b));
     return one_minus(x87_quot(ip, denom));
 }
+
+// Either metric, `this` = x of any real type (fp32 dataset rows, fp64
+// centroids), `in` = c; metric 0 = euclidean, 1 = cosine.
+template <typename T, typename U>
+__device__ inline double exact_dist(const T* __restrict__ x, const U* __restrict__ c, int d, int metric) {
+    if (metric == 0) {
+        double acc = 0.0;
+        for (int j = 0; j < d; j++) {
+            const double df = __dsub_rn((double)x[j], (double)c[j]);
+            acc = __dadd_rn(acc, __dmul_rn(df, df));
+        }
+        return sqrt(acc);
+    }
+    sx80 ip = sx_zero();
+    double a = 0.0, b = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j], cj = (double)c[j];
+        ip = sx_add_double(ip, __dmul_rn(xj, cj));
+        a = __dadd_rn(a, __dmul_rn(xj, xj));
+        b = __dadd_rn(b, __dmul_rn(cj, cj));
+    }
+    return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
+}
+
+// x86 SSE produces one NaN from non-NaN operands: the default NaN, sign set
+// (0xFFF8...), which every later operation propagates. Device NaNs are mapped
+// to it wherever a reference double that may be NaN is written.
+__device__ inline double x86_nan(double v) {
+    return v != v ? __longlong_as_double((long long)0xFFF8000000000000ull) : v;
+}

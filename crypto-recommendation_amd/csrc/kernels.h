@@ -172,6 +172,13 @@ int launch_range_gather(hipStream_t s, const float* X, int d, const int32_t* lis
 int launch_range_scatter(hipStream_t s, const int32_t* list, int64_t M, const int32_t* ar, const double* dr,
                          int32_t* assign, double* dist);
 
+// Silhouette (silhouette.hip).
+int launch_sil_near(hipStream_t s, const double* C, int K, int d, int metric, int32_t* near);
+int launch_sil_points(hipStream_t s, const float* X, int d, int metric, const int32_t* rows, const int64_t* crow,
+                      const int32_t* assign, const int32_t* near, int64_t N, double* s_out);
+int launch_sil_sum(hipStream_t s, const double* sv, const int32_t* rows, const int64_t* crow, int K, int64_t N,
+                   double* raw, double* out);
+
 // Synthetic data.
 int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X);
 

@@ -27,27 +27,6 @@
 
 namespace lshkm {
 
-template <typename T>
-__device__ inline double rg_dist(const T* __restrict__ x, const double* __restrict__ c, int d, int metric) {
-    if (metric == 0) {
-        double acc = 0.0;
-        for (int j = 0; j < d; j++) {
-            const double df = __dsub_rn((double)x[j], c[j]);
-            acc = __dadd_rn(acc, __dmul_rn(df, df));
-        }
-        return sqrt(acc);
-    }
-    sx80 ip = sx_zero();
-    double a = 0.0, b = 0.0;
-    for (int j = 0; j < d; j++) {
-        const double xj = (double)x[j];
-        ip = sx_add_double(ip, __dmul_rn(xj, c[j]));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(c[j], c[j]));
-    }
-    return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
-}
-
 // find_min_vector_distance over the centroid rows, /2: the sequential scan
 // with the -1 sentinel keeps the first pair's value if it is NaN and is
 // otherwise the minimum of the non-NaN values (the sign of a zero never
@@ -62,7 +41,7 @@ __global__ __launch_bounds__(RG_MIN_THREADS) void rg_min_pair_kernel(const doubl
     for (int64_t p = threadIdx.x; p < (int64_t)K * K; p += RG_MIN_THREADS) {
         const int i = (int)(p / K), j = (int)(p % K);
         if (j <= i) continue;                                    // pairs (i, j > i), utils.hpp:164-165
-        const double dd = rg_dist(C + (size_t)i * d, C + (size_t)j * d, d, metric);
+        const double dd = exact_dist(C + (size_t)i * d, C + (size_t)j * d, d, metric);
         if (p == 1 && dd != dd) { *r0 = dd / 2; any = true; }   // first pair (0, 1) NaN: the scan stays NaN
         if (dd < mn) mn = dd;
     }
@@ -119,7 +98,7 @@ __global__ void rg_pass_kernel(const float* __restrict__ X, int d, const double*
                 if (cached[e]) {
                     dd = cache[e];
                 } else {
-                    dd = rg_dist(X + (size_t)n * d, C + (size_t)i * d, d, metric);
+                    dd = exact_dist(X + (size_t)n * d, C + (size_t)i * d, d, metric);
                     const int g = key ? key[i] : i;
                     for (int64_t f = e0; f < e1; f++)
                         if (f == e || (key ? key[cents[f]] == g : cents[f] == i)) {

@@ -82,6 +82,7 @@ def lib():
             "lshkm_coins_draw": (i32, [C.POINTER(C.c_uint32), vp, i64, vp]),
             "lshkm_lloyd_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp]),
             "lshkm_range_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp, C.POINTER(i32)]),
+            "lshkm_silhouette": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]),
             "lshkm_hash_assign": (i32, [vp, vp, i64, vp, i32, vp, vp, vp, vp, vp, vp]),
             "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
@@ -361,6 +362,17 @@ def range_assign(ctx, X, Cc, comb_ptr, comb_idx, metric="euclidean", key=None, s
     _ck(lib().lshkm_range_assign(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _t_ptr(cp), _t_ptr(ci),
                                  _np_ptr(kk), _np_ptr(sr), _t_ptr(assign), _t_ptr(dist), C.byref(passes)))
     return assign, dist, passes.value
+
+
+def silhouette(ctx, X, assign, Cc, metric="euclidean"):
+    """silhouette_cluster (silhouette.hpp:31-80). Returns (sils [K+1] numpy, s [N] tensor)."""
+    N, d = X.shape
+    K = Cc.shape[0]
+    out = np.empty(K + 1, np.float64)
+    s = ctx.empty((max(N, 1),), ctx.torch.float64)
+    _ck(lib().lshkm_silhouette(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), _t_ptr(Cc), K, _METRIC[metric], _np_ptr(out),
+                               _t_ptr(s)))
+    return out, s[:N]
 
 
 def hash_assign(lsh, X, Cc, src_rows=None, tuples=True, phi=False, bucket=True):

@@ -11,6 +11,7 @@
  *   lloyds_assignment                lib/clustering_phases/assignment.hpp:54-80
  *   k_means                          lib/clustering_phases/update.hpp:37-86
  *   lsh_/cube_range_assignment       lib/clustering_phases/assignment.hpp:108-217
+ *   silhouette_cluster               lib/clustering_phases/silhouette.hpp:31-144
  *   HashGenerator plugin ABI         lib/generators/hash_generator.hpp:19-31
  *   CustHashtable::getBucketFromIndex / getHash lib/data_structures/cust_hashtable.hpp:116-125
  *
@@ -228,6 +229,16 @@ int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* 
 int lshkm_range_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const double* C_dev, int K, int metric,
                        const int64_t* comb_ptr_dev, const int32_t* comb_idx_dev, const int32_t* key_host,
                        const int32_t* src_rows_host, int32_t* assign_dev, double* dist_dev, int* passes_host);
+
+/* --------------------------------------------------------------- silhouette
+ * silhouette_cluster (silhouette.hpp:31-80) over the clusters of `assign`
+ * (separate_clusters_from_input, utils.hpp:150-158: members in row order)
+ * with the K centroids C_dev (nearest other centroid = neighbour cluster).
+ * out_host [K+1]: per-cluster mean s(i), then the overall mean; s_dev [N]
+ * (may be NULL): silhouette_of_i of every row (:83-144). Exact distances in
+ * the reference's order; NaNs as x86 produces them (empty cluster: 0/0). */
+int lshkm_silhouette(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
+                     const double* C_dev, int K, int metric, double* out_host, double* s_dev);
 
 /* ----------------------------------------------------------- initialization
  * k_means_pp (initialization.hpp:71-156): the K dataset rows chosen as initial

@@ -667,3 +667,66 @@ int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, in
             if (src_rows[c] >= 0) { assign[src_rows[c]] = c; dist[src_rows[c]] = 0; }
     return passes;
 }
+
+/* ---------------------------------------------------------------- silhouette */
+
+/* silhouette_cluster (silhouette.hpp:31-80) over separate_clusters_from_input
+ * (utils.hpp:150-158), silhouette_of_i (:83-144). The reference's distance
+ * cache is left out: it returns d(x_j, x_i) for d(x_i, x_j), which is the same
+ * double in both metrics (unique IDs). out[K+1]; s[N] (may be NULL) per row. */
+void or_silhouette(int64_t N, int d, int K, const float* X, const int32_t* assign, const double* C, int metric,
+                   double* out, double* s) {
+    int32_t* near = (int32_t*)malloc(sizeof(int32_t) * (size_t)K);
+    for (int c = 0; c < K; c++) {
+        double mn = -1; int arg = 0;
+        for (int i = 0; i < K; i++) {
+            if (i == c) continue;
+            const double dd = metric == 0 ? euclid_f64(C + (size_t)c * d, C + (size_t)i * d, d)
+                                          : cosine_f64(C + (size_t)c * d, C + (size_t)i * d, d);
+            if (mn == -1 || dd < mn) { mn = dd; arg = i; }
+        }
+        near[c] = arg;
+    }
+    int64_t* cnt = (int64_t*)calloc((size_t)K + 1, sizeof(int64_t));
+    for (int64_t n = 0; n < N; n++) cnt[assign[n] + 1]++;
+    for (int c = 0; c < K; c++) cnt[c + 1] += cnt[c];
+    int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * (size_t)K);
+    int32_t* rows = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+    for (int c = 0; c < K; c++) fill[c] = cnt[c];
+    for (int64_t n = 0; n < N; n++) rows[fill[assign[n]]++] = (int32_t)n;
+    double* sv = (double*)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1));
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t p = 0; p < N; p++) {
+        const int32_t r = rows[p];
+        const int c = assign[r];
+        double* xr = (double*)malloc(sizeof(double) * (size_t)d);
+        double a = 0, b = 0;
+        for (int64_t j = cnt[c]; j < cnt[c + 1]; j++) {
+            for (int t = 0; t < d; t++) xr[t] = X[(size_t)rows[j] * d + t];
+            a = a + (metric == 0 ? or_euclid_dist_f32_f64(X + (size_t)r * d, xr, d)
+                                 : cosine_dist_f32_f64(X + (size_t)r * d, xr, d));
+        }
+        if (cnt[c + 1] - cnt[c] != 1) a = a / (double)(size_t)(cnt[c + 1] - cnt[c] - 1);
+        const int nc = near[c];
+        for (int64_t j = cnt[nc]; j < cnt[nc + 1]; j++) {
+            for (int t = 0; t < d; t++) xr[t] = X[(size_t)rows[j] * d + t];
+            b = b + (metric == 0 ? or_euclid_dist_f32_f64(X + (size_t)r * d, xr, d)
+                                 : cosine_dist_f32_f64(X + (size_t)r * d, xr, d));
+        }
+        b = b / (double)(size_t)(cnt[nc + 1] - cnt[nc]);
+        double mx = a;
+        if (b > a) mx = b;
+        sv[p] = (b - a) / mx;
+        if (s) s[r] = sv[p];
+        free(xr);
+    }
+    out[K] = 0;
+    for (int c = 0; c < K; c++) {
+        out[c] = 0;
+        for (int64_t p = cnt[c]; p < cnt[c + 1]; p++) out[c] = out[c] + sv[p];
+        out[K] = out[K] + out[c];
+        out[c] = out[c] / (double)(size_t)(cnt[c + 1] - cnt[c]);
+    }
+    out[K] = out[K] / (double)(int)N;
+    free(near); free(cnt); free(fill); free(rows); free(sv);
+}

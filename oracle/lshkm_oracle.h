@@ -88,6 +88,10 @@ int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, in
                     const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key,
                     const int32_t* src_rows, int32_t* assign, double* dist);
 
+/* ---- silhouette_cluster (silhouette.hpp:31-144): out[K+1], s[N] (or NULL) */
+void or_silhouette(int64_t N, int d, int K, const float* X, const int32_t* assign, const double* C, int metric,
+                   double* out, double* s);
+
 /* ---- initialization (initialization.hpp:39-156): the chosen dataset rows */
 void or_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows);
 void or_kmeans_pp(int64_t N, int d, int K, const float* X, int metric, uint64_t seed, int32_t* rows);

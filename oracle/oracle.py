@@ -53,6 +53,7 @@ def lib():
                                            f64p, i64p]),
             "or_range_assign": (C.c_int, [C.c_int64, C.c_int, C.c_int, f32p, f64p, C.c_int, i64p, i32p,
                                           C.c_void_p, C.c_void_p, i32p, f64p]),
+            "or_silhouette": (None, [C.c_int64, C.c_int, C.c_int, f32p, i32p, f64p, C.c_int, f64p, C.c_void_p]),
             "or_rand_selection": (None, [C.c_uint64, C.c_int64, C.c_int, i32p]),
             "or_kmeans_pp": (None, [C.c_int64, C.c_int, C.c_int, f32p, C.c_int, C.c_uint64, i32p]),
             "or_p_closest": (None, [C.c_int, f64p, C.c_int64, f64p, i64p, i32p, C.c_int, i32p, f64p, i32p]),
@@ -206,6 +207,17 @@ def range_assign(X, Cc, comb_ptr, comb_idx, metric="euclidean", key=None, src_ro
                                    np.ascontiguousarray(comb_ptr, np.int64), np.ascontiguousarray(comb_idx, np.int32),
                                    _ptr(kk), _ptr(sr), a, dist)
     return a, dist, passes
+
+
+def silhouette(X, assign, Cc, metric="euclidean"):
+    """silhouette_cluster (silhouette.hpp:31-144): (sils [K+1], s [N])."""
+    X = np.ascontiguousarray(X, np.float32)
+    Cc = np.ascontiguousarray(Cc, np.float64)
+    N, d = X.shape; K = Cc.shape[0]
+    out = np.empty(K + 1, np.float64); s = np.empty(max(N, 1), np.float64)
+    lib().or_silhouette(N, d, K, X, np.ascontiguousarray(assign, np.int32), Cc, 0 if metric == "euclidean" else 1,
+                        out, _ptr(s))
+    return out, s[:N]
 
 
 def kmeans_update(X, assign, C_old, metric="euclidean", min_dist=0.0):

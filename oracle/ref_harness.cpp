@@ -48,6 +48,7 @@ system_clock::time_point system_clock::now() noexcept {
 #include "clustering_phases/update.hpp"
 #include "clustering_phases/initialization.hpp"
 #include "crypto_rec.hpp"
+#include "clustering_phases/silhouette.hpp"
 #undef private
 
 #include "../include/lshkm_synth.h"
@@ -353,6 +354,9 @@ static int mode_lloyd(int argc, char** argv) {
         for (int n = 0; n < N; n++) { assign[n] = vecs[n].getCluster(); dist[n] = vecs[n].getDistFromCentroid(); }
         write_npy(out + "/assign" + std::to_string(it) + ".npy", assign, {(size_t)N});
         write_npy(out + "/dist" + std::to_string(it) + ".npy", dist, {(size_t)N});
+        // silhouette_cluster (silhouette.hpp:31-80) of this assignment
+        std::vector<double> sil = silhouette_cluster(separate_clusters_from_input(vecs, K), centroids, metric);
+        write_npy(out + "/sil" + std::to_string(it) + ".npy", sil, {sil.size()});
         cont = k_means(vecs, centroids, metric, min_dist);
         flags.push_back(cont ? 1 : 0);
         std::vector<double> cs;
@@ -511,6 +515,9 @@ static int mode_range(int argc, char** argv) {
         for (int n = 0; n < N; n++) { assign[n] = vecs[n].getCluster(); dist[n] = vecs[n].getDistFromCentroid(); }
         write_npy(out + "/assign" + std::to_string(it) + ".npy", assign, {(size_t)N});
         write_npy(out + "/dist" + std::to_string(it) + ".npy", dist, {(size_t)N});
+        // silhouette_cluster (silhouette.hpp:31-80) of this assignment
+        std::vector<double> sil = silhouette_cluster(separate_clusters_from_input(vecs, K), centroids, metric);
+        write_npy(out + "/sil" + std::to_string(it) + ".npy", sil, {sil.size()});
         cont = k_means(vecs, centroids, metric, min_dist);
         it++;
         if (family != "lsh") break;

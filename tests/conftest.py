@@ -32,6 +32,17 @@ def kpp_input(name):
     return oracle.synth(m["data_seed"], m["N"], m["d"])[np.arange(m["N"]) // m.get("dup", 1)]
 
 
+def lloyd_input(name):
+    """Input rows of a Lloyd golden case (tests/golden/make_golden.py:lloyd_data)."""
+    import oracle
+    m = golden_meta()[name]
+    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    z = m.get("zero_every", 0)
+    if z:
+        X[5::z] = 0.0
+    return X
+
+
 def cases(kind):
     return sorted(n for n, m in golden_meta().items() if m["kind"] == kind)
 

@@ -52,7 +52,22 @@ LLOYD_CASES = [
     ("lloyd_ext", 1000, 128, 12, "euclidean", 2, 0.05, 13, "ext"),
     ("lloyd_dup", 800, 32, 8, "euclidean", 3, 0.0, 14, "0,7,7,100,200,200,300,400"),
     ("lloyd_conv", 400, 16, 4, "euclidean", 6, 1e9, 15, "rows"),
+    # zero rows (every 37th from row 5): NaN cosine distances and silhouettes
+    ("lloyd_c_zero", 600, 24, 6, "cosine", 2, 0.05, 16, "rows"),
+    ("lloyd_e_zero", 500, 8, 5, "euclidean", 2, 0.05, 17, "rows"),
+    # an external center far from the data: an empty cluster (0/0 silhouette)
+    ("lloyd_ext_empty", 700, 16, 6, "euclidean", 2, 0.05, 18, "ext_far"),
 ]
+LLOYD_ZERO_EVERY = {"lloyd_c_zero": 37, "lloyd_e_zero": 37}
+
+
+def lloyd_data(name, dseed, N, d):
+    """Inputs of a Lloyd case (tests rebuild them with conftest.lloyd_input)."""
+    x = oracle.synth(dseed, N, d)
+    z = LLOYD_ZERO_EVERY.get(name, 0)
+    if z:
+        x[5::z] = 0.0
+    return x
 KPP_CASES = [
     # name, N, d, K, metric, seed, data_seed, dup   (config 1 plumbing: 1k x d=16, K=8)
     # dup g: row i is synth row i // g (repeated points: zero distances, repeat picks)
@@ -167,11 +182,13 @@ def main(only=None):
                               nqrows=nqrows, Q=Q)
         for (name, N, d, K, metric, iters, min_dist, dseed, init) in (LLOYD_CASES if want("lloyd") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
-            x = oracle.synth(dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
+            x = lloyd_data(name, dseed, N, d); x.tofile(os.path.join(tmp, "x.f32"))
             args = ["lloyd", os.path.join(tmp, "x.f32"), N, d, K, metric, iters, repr(min_dist), out]
             extra = {}
-            if init == "ext":
+            if init in ("ext", "ext_far"):
                 c = ext_centers(dseed + 500, K, d)
+                if init == "ext_far":
+                    c[K // 2] += 1e3
                 c.tofile(os.path.join(tmp, "c.f64"))
                 args += [os.path.join(tmp, "c.f64")]
                 extra["ext_centers"] = c
@@ -181,7 +198,7 @@ def main(only=None):
             res = load_dir(out); res.update(extra)
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
             meta[name] = dict(kind="lloyd", N=N, d=d, K=K, metric=metric, iters=iters, min_dist=min_dist,
-                              data_seed=dseed, init=init)
+                              data_seed=dseed, init=init, zero_every=LLOYD_ZERO_EVERY.get(name, 0))
         for (name, N, d, K, metric, seed, dseed, dup) in (KPP_CASES if want("kmeanspp") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
             x = kpp_data(dseed, N, d, dup); x.tofile(os.path.join(tmp, "x.f32"))

@@ -6,7 +6,7 @@ import pytest
 
 import oracle
 from amd import lshkm
-from conftest import cases, golden, golden_meta
+from conftest import cases, golden, golden_meta, lloyd_input
 
 META = golden_meta()
 pytestmark = pytest.mark.gpu
@@ -196,14 +196,14 @@ def test_cube_sharded_build_matches_single(ctx):
 @pytest.mark.parametrize("name", cases("lloyd"))
 def test_kmeans_update_golden(ctx, name):
     m, g = META[name], golden(name)
-    X = to_dev(ctx, oracle.synth(m["data_seed"], m["N"], m["d"]))
+    X = to_dev(ctx, lloyd_input(name))
     for it in range(len(g["cont"])):
         a = to_dev(ctx, g[f"assign{it}"])
         Cold = to_dev(ctx, g[f"centers{it}"])
         Cn, cnt, cont = lshkm.kmeans_update(ctx, X, a, Cold, m["metric"], m["min_dist"])
         assert cont == bool(g["cont"][it]), it
         exp = g[f"centers{it + 1}"] if cont else oracle.kmeans_update(
-            oracle.synth(m["data_seed"], m["N"], m["d"]), g[f"assign{it}"], g[f"centers{it}"], m["metric"], m["min_dist"])[0]
+            lloyd_input(name), g[f"assign{it}"], g[f"centers{it}"], m["metric"], m["min_dist"])[0]
         assert np.array_equal(Cn.cpu().numpy().view(np.uint64), exp.view(np.uint64)), it
         assert np.array_equal(cnt.cpu().numpy(), np.bincount(g[f"assign{it}"], minlength=m["K"])), it
 

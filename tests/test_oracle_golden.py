@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import cases, golden, golden_meta, kpp_input
+from conftest import cases, golden, golden_meta, kpp_input, lloyd_input
 
 META = golden_meta()
 
@@ -111,10 +111,10 @@ def test_cube(name):
 @pytest.mark.parametrize("name", cases("lloyd"))
 def test_lloyd_and_update(name):
     m, g = META[name], golden(name)
-    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    X = lloyd_input(name)
     C = g["centers0"]
     src = g["src_rows"]
-    if m["init"] == "ext":
+    if m["init"] in ("ext", "ext_far"):
         assert np.array_equal(C, g["ext_centers"])
     for it in range(len(g["cont"])):
         a, dist = oracle.lloyd_assign(X, C, m["metric"], src if it == 0 else None)
@@ -179,3 +179,13 @@ def test_range_assignment(name):
                                          key=g[f"key{it}"], src_rows=g["src_rows"] if it == 0 else None)
         assert np.array_equal(a, g[f"assign{it}"]), it
         assert np.array_equal(dist.view(np.uint64), g[f"dist{it}"].view(np.uint64)), it
+
+
+@pytest.mark.parametrize("name", cases("lloyd"))
+def test_silhouette(name):
+    # silhouette_cluster (silhouette.hpp:31-144) of every golden assignment, NaN bits included
+    m, g = META[name], golden(name)
+    X = lloyd_input(name)
+    for it in range(len(g["cont"])):
+        out, _ = oracle.silhouette(X, g[f"assign{it}"], g[f"centers{it}"], m["metric"])
+        assert np.array_equal(out.view(np.uint64), g[f"sil{it}"].view(np.uint64)), it
