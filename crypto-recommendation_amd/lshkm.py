@@ -83,6 +83,15 @@ def lib():
             "lshkm_lloyd_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp]),
             "lshkm_range_assign": (i32, [vp, vp, i64, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp, C.POINTER(i32)]),
             "lshkm_silhouette": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]),
+            "lshkm_vectors_read": (i32, [C.c_char_p, C.c_char, i32, i32, C.POINTER(vp)]),
+            "lshkm_vectors_info": (i32, [vp, C.POINTER(i64), C.POINTER(i32), C.POINTER(i64), C.POINTER(i32),
+                                         C.POINTER(i32), C.POINTER(i32)]),
+            "lshkm_vectors_values": (i32, [vp, vp, vp]),
+            "lshkm_vectors_ids": (i32, [vp, vp, vp]),
+            "lshkm_vectors_meta": (i32, [vp, i32, C.c_char_p, i64, C.POINTER(i64)]),
+            "lshkm_vectors_free": (i32, [vp]),
+            "lshkm_config_value": (i32, [C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(i32)]),
+            "lshkm_config_load": (i32, [C.c_char_p, vp]),
             "lshkm_hash_assign": (i32, [vp, vp, i64, vp, i32, vp, vp, vp, vp, vp, vp]),
             "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
@@ -373,6 +382,58 @@ def silhouette(ctx, X, assign, Cc, metric="euclidean"):
     _ck(lib().lshkm_silhouette(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), _t_ptr(Cc), K, _METRIC[metric], _np_ptr(out),
                                _t_ptr(s)))
     return out, s[:N]
+
+
+# ------------------------------------------------------------- input formats
+class Config(C.Structure):
+    """lshkm_config: get_config's values (main.cpp:512-554)."""
+    _fields_ = [("proj_2_input", C.c_char * 1024), ("proj_2_csv_delimiter", C.c_char), ("proj_2_cluster_num", C.c_int32),
+                ("cluster_num", C.c_int32), ("has_cluster_num", C.c_int32), ("k", C.c_int32), ("L", C.c_int32),
+                ("lsh_bucket_div", C.c_int32), ("euclidean_h_w", C.c_double), ("csv_delimiter", C.c_char),
+                ("max_algo_iterations", C.c_int32), ("min_dist_kmeans", C.c_double),
+                ("lexicon_file", C.c_char * 1024), ("query_file", C.c_char * 1024)]
+
+
+def load_config(path):
+    c = Config()
+    _ck(lib().lshkm_config_load(path.encode(), C.byref(c)))
+    return c
+
+
+def config_value(path, key):
+    buf = C.create_string_buffer(4096)
+    found = C.c_int32(0)
+    _ck(lib().lshkm_config_value(path.encode(), key.encode(), buf, len(buf), C.byref(found)))
+    return buf.value.decode() if found.value else None
+
+
+def read_vectors(path, delimiter=",", strt_line=1, threads=0):
+    """VectorReader<double>::read (vector_reader.hpp:54-85): (ids list, X fp64 [n][d],
+    fp32_exact flag, metadata lines)."""
+    h = C.c_void_p()
+    _ck(lib().lshkm_vectors_read(path.encode(), delimiter.encode()[:1], strt_line, threads, C.byref(h)))
+    try:
+        n, d, ib, rg, ex, nm = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int32(), C.c_int32(), C.c_int32()
+        _ck(lib().lshkm_vectors_info(h, C.byref(n), C.byref(d), C.byref(ib), C.byref(rg), C.byref(ex), C.byref(nm)))
+        if rg.value:
+            raise LshkmError("ragged rows: no N x d layout")
+        X = np.empty((n.value, d.value), np.float64)
+        _ck(lib().lshkm_vectors_values(h, _np_ptr(X), None))
+        raw = C.create_string_buffer(max(ib.value, 1))
+        off = np.empty(n.value + 1, np.int64)
+        _ck(lib().lshkm_vectors_ids(h, raw, _np_ptr(off)))
+        b = raw.raw
+        ids = [b[off[i]:off[i + 1]].decode() for i in range(n.value)]
+        meta = []
+        for i in range(nm.value):
+            ln = C.c_int64()
+            _ck(lib().lshkm_vectors_meta(h, i, None, 0, C.byref(ln)))
+            buf = C.create_string_buffer(ln.value + 1)
+            _ck(lib().lshkm_vectors_meta(h, i, buf, len(buf), None))
+            meta.append(buf.value.decode())
+        return ids, X, bool(ex.value), meta
+    finally:
+        lib().lshkm_vectors_free(h)
 
 
 def hash_assign(lsh, X, Cc, src_rows=None, tuples=True, phi=False, bucket=True):

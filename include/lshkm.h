@@ -12,6 +12,8 @@
  *   k_means                          lib/clustering_phases/update.hpp:37-86
  *   lsh_/cube_range_assignment       lib/clustering_phases/assignment.hpp:108-217
  *   silhouette_cluster               lib/clustering_phases/silhouette.hpp:31-144
+ *   VectorReader<double>::read       lib/in_out/vector_reader.hpp:54-85
+ *   file_to_args + ArgParser, get_config  lib/utils.cpp:53-69, lib/in_out/arg_parser.cpp, main.cpp:512-554
  *   HashGenerator plugin ABI         lib/generators/hash_generator.hpp:19-31
  *   CustHashtable::getBucketFromIndex / getHash lib/data_structures/cust_hashtable.hpp:116-125
  *
@@ -50,6 +52,7 @@ extern "C" {
 typedef struct lshkm_ctx_s* lshkm_ctx;
 typedef struct lshkm_lsh_s* lshkm_lsh;
 typedef struct lshkm_cube_s* lshkm_cube;
+typedef struct lshkm_vectors_s* lshkm_vectors;
 
 /* ------------------------------------------------------------------ context */
 const char* lshkm_last_error(void);
@@ -277,6 +280,48 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X_dev, const double* x_mean_d
                       const double* u_mean_dev, int64_t nq, const int64_t* unk_ptr_dev, const int32_t* unk_idx_dev,
                       const int32_t* nb_idx_dev, const double* nb_sim_dev, const int32_t* nb_cnt_dev, int P,
                       int n_top, int32_t* out_dev);
+
+/* ------------------------------------------------------------ input formats
+ * Host only (no device needed). VectorReader<double>::read
+ * (vector_reader.hpp:54-85): lines 1..strt_line-1 kept as metadata, then one
+ * vector per line: '\r' removed, ID = text before the first delimiter, values
+ * = std::stod of each delimiter-separated token (getline semantics). A token
+ * std::stod would throw on fails the call. threads <= 0: all hardware threads. */
+int lshkm_vectors_read(const char* path, char delimiter, int strt_line, int threads, lshkm_vectors* out);
+/* n rows, d = values of row 0, id_bytes = total ID length, ragged = rows of
+ * different lengths, fp32_exact = every value is an fp32 value (the hot
+ * path's storage contract), n_meta = metadata lines. Any pointer may be NULL. */
+int lshkm_vectors_info(lshkm_vectors v, int64_t* n, int* d, int64_t* id_bytes, int* ragged, int* fp32_exact,
+                       int* n_meta);
+/* Row-major values: X64_host [n][d] and/or X32_host [n][d] (either may be NULL). */
+int lshkm_vectors_values(lshkm_vectors v, double* X64_host, float* X32_host);
+/* IDs: bytes_host [id_bytes] concatenated, offsets_host [n+1]. */
+int lshkm_vectors_ids(lshkm_vectors v, char* bytes_host, int64_t* offsets_host);
+/* getMetaLine(index) (vector_reader.hpp:91-96): "" past the saved lines. */
+int lshkm_vectors_meta(lshkm_vectors v, int index, char* buf, int64_t cap, int64_t* len);
+int lshkm_vectors_free(lshkm_vectors v);
+
+/* cluster.conf: file_to_args(path, ' ') + ArgParser::getFlagValue — the token
+ * after the first occurrence of key (*found = 0: absent, or last token). */
+int lshkm_config_value(const char* path, const char* key, char* buf, int64_t cap, int* found);
+/* get_config (main.cpp:512-554): the reference's defaults (main.cpp:50-63),
+ * then every key present; csv_delimiter is an ASCII code, proj_2_csv_delimiter
+ * the first character. Fails where the reference's stoi / stod would throw. */
+typedef struct lshkm_config {
+    char proj_2_input[1024];
+    char proj_2_csv_delimiter;
+    int proj_2_cluster_num;
+    int cluster_num;
+    int has_cluster_num;      /* 0: the reference would ask on stdin */
+    int k, L, lsh_bucket_div;
+    double euclidean_h_w;
+    char csv_delimiter;
+    int max_algo_iterations;
+    double min_dist_kmeans;
+    char lexicon_file[1024];
+    char query_file[1024];
+} lshkm_config;
+int lshkm_config_load(const char* path, lshkm_config* out);
 
 /* ------------------------------------------------------------ synthetic data */
 /* include/lshkm_synth.h generator, rows [row0, row0+rows) into X_dev. */

@@ -49,6 +49,8 @@ system_clock::time_point system_clock::now() noexcept {
 #include "clustering_phases/initialization.hpp"
 #include "crypto_rec.hpp"
 #include "clustering_phases/silhouette.hpp"
+#include "in_out/vector_reader.hpp"
+#include "in_out/arg_parser.h"
 #undef private
 
 #include "../include/lshkm_synth.h"
@@ -530,6 +532,94 @@ static int mode_range(int argc, char** argv) {
     return 0;
 }
 
+// --------------------------------------------------------------- csv mode
+// csv PATH DELIM_ASCII STRT_LINE OUT — VectorReader<double>::read
+// (vector_reader.hpp:54-85) with main.cpp:82's stod: ids (bytes + offsets),
+// values (the rows must be of equal length here), metadata lines.
+static int mode_csv(int argc, char** argv) {
+    if (argc < 5) { fprintf(stderr, "usage: csv PATH DELIM_ASCII STRT_LINE OUT\n"); return 2; }
+    VectorReader<double> rd(argv[1]);
+    const char delim = (char)atoi(argv[2]);
+    rd.read(delim, atoi(argv[3]), [](const std::string& x) { return std::stod(x); });
+    std::string out = argv[4];
+    std::vector<Vec> vs = rd.getReadVectors();
+    std::vector<uint8_t> idb; std::vector<int64_t> off(1, 0); std::vector<double> x;
+    size_t d = vs.empty() ? 0 : vs[0].getDimensions()->size();
+    for (auto& v : vs) {
+        std::string id = v.getId();
+        idb.insert(idb.end(), id.begin(), id.end());
+        off.push_back((int64_t)idb.size());
+        if (v.getDimensions()->size() != d) { fprintf(stderr, "ragged\n"); return 3; }
+        x.insert(x.end(), v.getDimensions()->begin(), v.getDimensions()->end());
+    }
+    write_npy(out + "/id_bytes.npy", idb, {idb.size()});
+    write_npy(out + "/id_off.npy", off, {off.size()});
+    write_npy(out + "/x.npy", x, {vs.size(), d});
+    std::vector<uint8_t> mb; std::vector<int64_t> moff(1, 0);
+    for (int i = 0; i < atoi(argv[3]) - 1; i++) {
+        std::string m = rd.getMetaLine(i);
+        mb.insert(mb.end(), m.begin(), m.end());
+        moff.push_back((int64_t)mb.size());
+    }
+    write_npy(out + "/meta_bytes.npy", mb, {mb.size()});
+    write_npy(out + "/meta_off.npy", moff, {moff.size()});
+    return 0;
+}
+
+// -------------------------------------------------------------- conf mode
+// conf PATH KEY... — ArgParser(file_to_args(PATH, ' ')) (utils.cpp:53-69,
+// arg_parser.cpp:21-33): one line per key, "1 <value>" or "0" when the flag is
+// absent or the last token (getFlagValue would build std::string(NULL)).
+static int mode_conf(int argc, char** argv) {
+    if (argc < 2) { fprintf(stderr, "usage: conf PATH KEY...\n"); return 2; }
+    std::vector<std::string> args = file_to_args(argv[1], ' ');
+    ArgParser ap(args);
+    for (int i = 2; i < argc; i++) {
+        std::string key = argv[i];
+        auto it = std::find(args.begin(), args.end(), key);
+        if (!ap.flagExists(key) || it + 1 == args.end()) printf("0\n");
+        else printf("1 %s\n", ap.getFlagValue(key).c_str());
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------- c1 mode
+// c1 CSV DELIM_ASCII K iters min_dist seed OUT — main.cpp:81-111 (config C1):
+// VectorReader<double> + stod, k_means_pp (cosine), then lloyds_assignment +
+// k_means until converged or `iters`; writes kpp_rows, assign/centers per
+// iteration, iters.
+static int mode_c1(int argc, char** argv) {
+    if (argc < 8) { fprintf(stderr, "usage: c1 CSV DELIM K iters min_dist seed OUT\n"); return 2; }
+    VectorReader<double> rd(argv[1]);
+    rd.read((char)atoi(argv[2]), 1, [](const std::string& x) { return std::stod(x); });
+    std::vector<Vec> vecs = rd.getReadVectors();
+    int K = atoi(argv[3]), iters = atoi(argv[4]); double min_dist = atof(argv[5]);
+    g_seed = atoll(argv[6]); std::string out = argv[7];
+    const std::string metric = "cosine";
+    std::vector<Vec*> centroids = k_means_pp(vecs, K, metric);
+    std::vector<int32_t> rows;
+    for (auto p : centroids) rows.push_back((int32_t)(p - vecs.data()));
+    write_npy(out + "/kpp_rows.npy", rows, {rows.size()});
+    int it = 0; bool cont = true;
+    while (cont && it < iters) {
+        lloyds_assignment(vecs, centroids, metric);
+        std::vector<int32_t> assign; std::vector<double> dist;
+        for (auto& v : vecs) { assign.push_back(v.getCluster()); dist.push_back(v.getDistFromCentroid()); }
+        write_npy(out + "/assign" + std::to_string(it) + ".npy", assign, {assign.size()});
+        write_npy(out + "/dist" + std::to_string(it) + ".npy", dist, {dist.size()});
+        cont = k_means(vecs, centroids, metric, min_dist);
+        std::vector<double> cs;
+        for (int c = 0; c < K; c++) for (double x : *centroids[c]->getDimensions()) cs.push_back(x);
+        write_npy(out + "/centers" + std::to_string(it + 1) + ".npy", cs, {(size_t)K, cs.size() / K});
+        it++;
+    }
+    std::vector<int32_t> nit(1, it), fl(1, cont ? 1 : 0);
+    write_npy(out + "/iters.npy", nit, {1});
+    write_npy(out + "/cont.npy", fl, {1});
+    for (auto c : centroids) if (c->getId() == "k_means_center") delete c;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness {lsh|cube|lloyd|kmeanspp|bench} ...\n"); return 2; }
     std::string m = argv[1];
@@ -540,6 +630,9 @@ int main(int argc, char** argv) {
     if (m == "bench") return mode_bench(argc - 1, argv + 1);
     if (m == "recom") return mode_recom(argc - 1, argv + 1);
     if (m == "range") return mode_range(argc - 1, argv + 1);
+    if (m == "csv") return mode_csv(argc - 1, argv + 1);
+    if (m == "conf") return mode_conf(argc - 1, argv + 1);
+    if (m == "c1") return mode_c1(argc - 1, argv + 1);
     fprintf(stderr, "unknown mode %s\n", m.c_str());
     return 2;
 }

@@ -10,7 +10,7 @@ include/lshkm_synth.h at the (seed, rows, d) recorded in cases.json, except
 external fp64 centroids, which are stored.
 
 Only runs in the build container (the reference is absent on the GPU box).
-Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,range,recom]
+Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,range,csv,conf,c1,recom]
 (--only regenerates those kinds and keeps the other cases' entries.)
 """
 import json
@@ -88,6 +88,66 @@ RANGE_CASES = [
     ("range_cube_e", 1500, 32, 12, "euclidean", "cube", 6, 1, 1, 2.0, 3, 1, 0.0, 5005, 34, 1),
     ("range_cube_c", 1500, 128, 20, "cosine", "cube", 8, 1, 1, 0.0, 8, 1, 0.0, 5006, 35, 1),
 ]
+# Input-format cases: files written here under tests/golden/io/ (our own data in
+# the reference's formats), parsed by the reference's VectorReader / ArgParser.
+CSV_CASES = [
+    # name, delimiter (ASCII), strt_line, N, d, seed
+    ("csv_comma", 44, 1, 400, 16, 6001),
+    ("csv_tab_meta", 9, 3, 300, 7, 6002),
+    ("csv_space", 32, 2, 200, 33, 6003),
+]
+# Config C1 (BASELINE.json configs[0]): main.cpp:81-111 on a 1k x 16 CSV, K=8
+C1_CASES = [
+    # name, N, d, K, iters, min_dist, seed, data_seed
+    ("c1_proj2", 1000, 16, 8, 30, 0.05, 7001, 7002),
+    ("c1_proj2_b", 1500, 16, 8, 5, 0.0, 7003, 7004),
+]
+CONF_KEYS = ["proj_2_input", "proj_2_csv_delimiter", "proj_2_number_of_clusters", "number_of_clusters",
+             "number_of_hash_functions", "number_of_hash_tables", "csv_delimiter", "lsh_bucket_div", "euclidean_h_w",
+             "cube_range_c", "cube_probes", "max_algo_iterations", "min_dist_kmeans", "metric_type", "lexicon_file",
+             "query_file", "missing_key", "//", "k"]
+CONF_CASES = {
+    "conf_a": "// options, one per line\nproj_2_input ./p2.csv\nproj_2_csv_delimiter ,\nproj_2_number_of_clusters 8\n\n"
+              "number_of_clusters 12 // k\nnumber_of_hash_functions 3 //default:4\nnumber_of_hash_tables  6\n"
+              "csv_delimiter 9 // ASCII CODE\r\nlsh_bucket_div 50\neuclidean_h_w 0.25\nmax_algo_iterations 7\n"
+              "min_dist_kmeans 1e-3\nmetric_type euclidean\nlexicon_file lex.csv\nquery_file q.csv",
+    "conf_c": "proj_2_input ../in.csv\nproj_2_csv_delimiter ;\nproj_2_number_of_clusters 20\n\nnumber_of_clusters 30 // k\n"
+              "number_of_hash_functions 4 //default:4\nnumber_of_hash_tables 5 //default:L=5\n\ncsv_delimiter 44 // ASCII CODE\n\n"
+              "lsh_bucket_div 100\neuclidean_h_w 0.4\n\nmax_algo_iterations 1\nmin_dist_kmeans 0.05\n\nmetric_type cosine\n",
+    "conf_b": "number_of_clusters 4\nnumber_of_clusters 9\neuclidean_h_w -2.5e+1xyz\nquery_file\n",
+}
+
+
+def csv_text(name, delim, strt, N, d, seed):
+    """Numbers in many spellings std::stod accepts: %.17g, short, exponent,
+    hex float, signs, leading blanks, inf/nan; \r\n on some lines, a trailing
+    delimiter on others."""
+    rng = np.random.default_rng(seed)
+    D = chr(delim)
+    lines = [f"meta line {i} {D} x" for i in range(strt - 1)]
+    for i in range(N):
+        vals = []
+        for j in range(d):
+            v = rng.standard_normal() * 10.0 ** int(rng.integers(-6, 7))
+            k = int(rng.integers(0, 12))
+            if k == 0: t = "%.17g" % v
+            elif k == 1: t = "%g" % v
+            elif k == 2: t = "%.3e" % v
+            elif k == 3: t = float(np.float32(v)).hex()
+            elif k == 4: t = "+%d" % int(v) if v >= 0 else "%d" % int(v)
+            elif k == 5: t = ("  " if D != " " else "") + repr(float(np.float32(v)))
+            elif k == 6: t = "-0"
+            elif k == 7 and (i + j) % 97 == 0: t = "inf" if v > 0 else "-INF"
+            elif k == 8 and (i + j) % 89 == 0: t = "nan"
+            else: t = repr(float(v))
+            vals.append(t)
+        line = f"u{i:05d}" + D + D.join(vals)
+        if i % 7 == 3: line += D
+        if i % 5 == 1: line += "\r"
+        lines.append(line)
+    return "\n".join(lines) + ("\n" if seed % 2 else "")
+
+
 RECOM_CASES = [
     # name, N, d, Q, P, NTOP, seed, values ("dyadic": k/8, squares exact; "f64": general doubles)
     ("recom_dy", 300, 20, 80, 10, 5, 4001, "dyadic"),
@@ -214,6 +274,39 @@ def main(only=None):
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
             meta[name] = dict(kind="range", N=N, d=d, K=K, metric=metric, family=fam, k=k, L=L, div=div, w=w,
                               probes=probes, iters=iters, min_dist=md, seed=seed, data_seed=dseed, dup=dup)
+        iodir = os.path.join(HERE, "io")
+        if want("csv") or want("conf"):
+            os.makedirs(iodir, exist_ok=True)
+        for (name, delim, strt, N, d, seed) in (CSV_CASES if want("csv") else []):
+            path = os.path.join(iodir, name + ".csv")
+            with open(path, "w", newline="") as f:
+                f.write(csv_text(name, delim, strt, N, d, seed))
+            out = os.path.join(tmp, name); os.makedirs(out)
+            run(["csv", path, delim, strt, out])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
+            meta[name] = dict(kind="csv", delim=delim, strt_line=strt, N=N, d=d, file="io/" + name + ".csv")
+        if want("c1"):
+            os.makedirs(iodir, exist_ok=True)
+        for (name, N, d, K, iters, md, seed, dseed) in (C1_CASES if want("c1") else []):
+            x = oracle.synth(dseed, N, d)
+            path = os.path.join(iodir, name + ".csv")
+            with open(path, "w") as f:
+                for i in range(N):
+                    f.write(f"{i}," + ",".join(repr(float(v)) for v in x[i]) + "\n")
+            out = os.path.join(tmp, name); os.makedirs(out)
+            run(["c1", path, 44, K, iters, repr(md), seed, out])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
+            meta[name] = dict(kind="c1", N=N, d=d, K=K, iters=iters, min_dist=md, seed=seed, data_seed=dseed,
+                              file="io/" + name + ".csv")
+        for name, text in (CONF_CASES.items() if want("conf") else []):
+            path = os.path.join(iodir, name + ".conf")
+            with open(path, "w", newline="") as f:
+                f.write(text)
+            res = subprocess.run([HARNESS, "conf", path] + CONF_KEYS, check=True, capture_output=True, text=True)
+            vals = {}
+            for key, ln in zip(CONF_KEYS, res.stdout.split("\n")):
+                vals[key] = ln[2:] if ln.startswith("1 ") else None
+            meta[name] = dict(kind="conf", file="io/" + name + ".conf", values=vals)
         for (name, N, d, Q, P, NT, seed, values) in (RECOM_CASES if want("recom") else []):
             out = os.path.join(tmp, name); os.makedirs(out)
             inp = recom_inputs(N, d, Q, seed, values)
@@ -229,7 +322,7 @@ def main(only=None):
         shutil.rmtree(tmp)
     with open(os.path.join(HERE, "cases.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
-    total = sum(os.path.getsize(os.path.join(HERE, n + ".npz")) for n in meta)
+    total = sum(os.path.getsize(os.path.join(HERE, n + ".npz")) for n in meta if os.path.exists(os.path.join(HERE, n + ".npz")))
     print(f"wrote {len(meta)} cases, {total / 1e6:.2f} MB")
 
 
