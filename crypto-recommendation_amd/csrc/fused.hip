@@ -147,17 +147,31 @@ __device__ inline void split8(const float* x, half8& hi, half8& lo) {
 typedef float float2v __attribute__((ext_vector_type(2)));
 constexpr double FU_SQRT_D = 11.313708498984761 * (1.0 + 0x1p-40);   // sqrt(128), rounded up
 
-// split8 with the residual subtraction on packed f32 (v_pk_add_f32).
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+// x - f32(h) in one v_fma_mix_f32 (x * 1 - h, the f16 operand widened exactly,
+// one rounding: the same value as x - (float)h), h the low / high half of hp.
+__device__ inline float resid_lo(float x, half2v hp) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(x), "v"(hp));
+    return r;
+}
+__device__ inline float resid_hi(float x, half2v hp) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(x), "v"(hp));
+    return r;
+}
+
+// split8 in 2 VALU per element: v_cvt_pk_f16_f32 (hi pair), two residuals by
+// v_fma_mix_f32, v_cvt_pk_f16_f32 (lo pair).
 __device__ inline void split8p(const float* x, half8& hi, half8& lo) {
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-        const _Float16 h0 = (_Float16)x[j], h1 = (_Float16)x[j + 1];
-        hi[j] = h0;
-        hi[j + 1] = h1;
-        const float2v xv = {x[j], x[j + 1]}, hv = {(float)h0, (float)h1};
-        const float2v r = xv - hv;
-        lo[j] = (_Float16)r.x;
-        lo[j + 1] = (_Float16)r.y;
+        const half2v hp = {(_Float16)x[j], (_Float16)x[j + 1]};
+        hi[j] = hp.x;
+        hi[j + 1] = hp.y;
+        const half2v lp = {(_Float16)resid_lo(x[j], hp), (_Float16)resid_hi(x[j + 1], hp)};
+        lo[j] = lp.x;
+        lo[j + 1] = lp.y;
     }
 }
 
@@ -464,14 +478,18 @@ constexpr int FP_WAVES = FP_KEEP_X ? 8 : 12;   // 2 / 3 per SIMD: <= 256 / 168 V
 #ifndef MFMA_PRIO
 #define MFMA_PRIO 1     // s_setprio inside the centroid loop (measured +1-3%)
 #endif
-#ifndef HASH_ROWB
-#define HASH_ROWB 0     // 1: one floor-certification window per row (measured: no gain, more fix-ups)
-#endif
 #ifndef YOUNG_PRIO
 #define YOUNG_PRIO 0    // s_setprio for waves FP_WAVES/2.. for the whole loop (experiment knob)
 #endif
 #ifndef PIPE_TILES
 #define PIPE_TILES 0
+#endif
+// Winner-row loads of the distance chain issued CHAIN_PF 16-dim steps ahead.
+// Measured (fused pass, N = 10M): 1 -> 3.03 ms, 2 -> 3.11, 4 -> 3.16, 8 -> 3.32:
+// the chain's L2 round trips are not what limits the pass (the SIMDs' VALU +
+// MFMA issue is), and the prefetch registers cost more than they hide.
+#ifndef CHAIN_PF
+#define CHAIN_PF 1
 #endif
 
 // Scores of one 32-centroid tile: t = (hi + lo) + (-|c|^2/2) on packed f32
@@ -555,8 +573,11 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         if (threadIdx.x < 32) {
             const int f = threadIdx.x;
             const bool on = f < a.LK;
-            lpn0[f] = on ? (float)a.pnorm[f] * (1.f + 0x1p-20f) : 0.f;   // rounded up
-            lv10[f] = on ? (float)a.v1[f] * (1.f + 0x1p-20f) : 0.f;
+            // floor-window coefficients P_f, Q_f (certification below), rounded up
+            const double iwu = (double)(1.0f / a.w) * (1.0 + 0x1p-20);      // >= 1/w
+            lpn0[f] = on ? (float)((FU_A1H * a.pnorm[f] * (1.0 + 0x1p-20) + FU_A2 * FU_SQRT_D) * iwu * (1.0 + 0x1p-18)) : 0.f;
+            lv10[f] = on ? (float)((FU_A2 * a.v1[f] * (1.0 + 0x1p-20) + (0x1p-40 + 0x1p-23) * fabs((double)a.tv[f])) *
+                                   iwu * (1.0 + 0x1p-18)) : 0.f;
             lt0[f] = on ? a.tv[f] : 0.f;
             lr0[f] = on ? a.rv[f] : 0;
         }
@@ -567,15 +588,6 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     const int col = lane & 31, h = lane >> 5;
     const float ecf = a.cbound[0], ebf = a.cbound[1], cmaxf = a.cbound[3];
     const bool c_ok = __float_as_uint(a.cbound[2]) == 0u;
-    // maxima of the hash constants over the launch's functions (HASH_ROWB window)
-    float pnmx = 0.f, v1mx = 0.f, tmx = 0.f;
-    if (HASH && HASH_ROWB) {
-        for (int f = 0; f < 32; f++) {
-            pnmx = fmaxf(pnmx, lpn0[f]);
-            v1mx = fmaxf(v1mx, lv10[f]);
-            tmx = fmaxf(tmx, fabsf(lt0[f]));
-        }
-    }
     const _Float16* my_h = lch + col * FU_RS + 8 * h;
     const _Float16* my_l = lcl + col * FU_RS + 8 * h;
     const int ntile32 = Kpad >> 5;
@@ -674,33 +686,24 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             //   |y - (x.v + t)/w| <= (Ed + 2^-23 |u| + 2^-40 |t|) / w + 2^-21 |y|,
             // Ed = A1 |v||x| + A2 (|v|_1 + |x|_1) + 2^-23 |dot~| (the split bound and
             // the final hi + lo add; the reference's x87 / double-product roundings
-            // are below 2^-50 (|v||x| + |t|), inside the inflation). All terms are
-            // inflated by 2^-20 for their own f32 roundings, and so is the floor
-            // window: floor(y - B) == floor(y + B) certifies the reference's floorl.
+            // are below 2^-50 (|v||x| + |t|)). With |x|_1 <= sqrt(d) |x|, |dot~| <=
+            // |u| + |t| and |u| / w <= |y| (1 + 2^-19), that is at most
+            //   B = |y| G + |x| P_f + Q_f,   G = (2^-22 + 2^-20)(1 + 2^-18),
+            //   P_f = (A1 |v| + A2 sqrt(d)) / w,  Q_f = (A2 |v|_1 + (2^-23 + 2^-40)|t|) / w
+            // (prologue; the 1 + 2^-18 factors cover the f32 roundings of B, y - B,
+            // y + B): floor(y - B) == floor(y + B) certifies the reference's floorl.
             const float iw = 1.0f / a.w;
-            const float ca = (float)(FU_A1H * nx) * (1.f + 0x1p-20f);
-            const float cb = (float)(FU_A2 * x1) * (1.f + 0x1p-20f);
+            const float nxf = (float)nx * (1.f + 0x1p-20f);
+            constexpr float G = (0x1p-22f + 0x1p-20f) * (1.f + 0x1p-18f);
             // Opaque zero: keeps the per-function constants as LDS reads inside
             // the loop instead of hoisted VGPRs.
             int hc = 0;
             asm volatile("" : "+v"(hc));
             const float* lt = lt0 + hc;
-            const float* lpn = lpn0 + hc;
-            const float* lv1 = lv10 + hc;
+            const float* lP = lpn0 + hc;
+            const float* lQ = lv10 + hc;
             const int32_t* lr = lr0 + hc;
             if (!x_ok) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
-#if HASH_ROWB
-            // One window per row: the per-function bound with each function's
-            // |v|_2, |v|_1, |t| replaced by their maxima over the launch's
-            // functions, and |dot~|, |u|, |y| by the bounds those imply. The floor
-            // is certified iff no integer lies within BR of y: with fr = y -
-            // floor(y) (exact for |y| < 2^24; larger y are integers and never
-            // pass), fr >= BR and fr <= 1 - (BR + 2^-23) (the latter rounded).
-            const float dmax = pnmx * (float)nx * (1.f + 0x1p-20f);
-            const float EdR = fmaf(ca, pnmx, fmaf((float)FU_A2, v1mx, cb)) + fmaf(0x1p-23f, 2.f * dmax + tmx, 0x1p-40f * tmx);
-            const float BR = (EdR * (1.f + 0x1p-20f)) * (iw * (1.f + 0x1p-20f)) + (dmax + tmx) * iw * 0x1p-19f;
-            const float omBR = 1.f - (BR + 0x1p-23f);
-#endif
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int l = 2 * g + h;
@@ -709,23 +712,12 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int f = 4 * l + q;
-                    const float dotf = acc_hi[4 * g + q];          // f32(fp64 hi sum + lo)
-                    const float tt = lt[f];
-                    const float u = dotf + tt;
+                    const float u = acc_hi[4 * g + q] + lt[f];       // f32(hi + lo sums) + t
                     const float y = u * iw;
-#if HASH_ROWB
-                    const float fl = floorf(y);
-                    hv[q] = (int32_t)fl;
-                    const float fr = y - fl;
-                    if (!(fr >= BR && fr <= omBR)) fmask |= 1u << f;   // provisional; redone by hash_fixup_kernel
-#else
-                    float Ed = fmaf(ca, lpn[f], fmaf((float)FU_A2, lv1[f], cb));
-                    Ed = fmaf(0x1p-23f, fabsf(dotf) + fabsf(u), fmaf(0x1p-40f, fabsf(tt), Ed));
-                    const float B = fmaf(Ed * (1.f + 0x1p-20f), iw * (1.f + 0x1p-20f), fabsf(y) * 0x1p-20f);
+                    const float B = fmaf(fabsf(y), G, fmaf(nxf, lP[f], lQ[f]));
                     const float lo = floorf(y - B), hi = floorf(y + B);
                     hv[q] = (int32_t)lo;
                     if (lo != hi) fmask |= 1u << f;   // provisional; redone by hash_fixup_kernel
-#endif
                 }
                 const int64_t o = row * a.L + l;
                 if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
@@ -834,12 +826,25 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             // dims 16s+8h..+7; only the winner's fp64 row is loaded
             const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
             double acc = 0.0;
+            double2 cbuf[CHAIN_PF][4];
+#pragma unroll
+            for (int s = 0; s < CHAIN_PF; s++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) cbuf[s][j] = *reinterpret_cast<const double2*>(crow + 16 * s + 2 * j);
 #pragma unroll
             for (int s = 0; s < 8; s++) {
                 double sq[8];
+                double2 cur[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) cur[j] = cbuf[s % CHAIN_PF][j];
+                if (s + CHAIN_PF < 8) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        cbuf[s % CHAIN_PF][j] = *reinterpret_cast<const double2*>(crow + 16 * (s + CHAIN_PF) + 2 * j);
+                }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const double2 cc = *reinterpret_cast<const double2*>(crow + 16 * s + 2 * j);
+                    const double2 cc = cur[j];
                     const double d0 = __dsub_rn((double)xf[8 * s + 2 * j], cc.x);
                     const double d1 = __dsub_rn((double)xf[8 * s + 2 * j + 1], cc.y);
                     sq[2 * j] = __dmul_rn(d0, d0);
