@@ -509,24 +509,45 @@ __device__ inline void tile_scores(const floatx16& acc_hi, const floatx16& acc_l
 
 // Running best / runner-up over one tile's scores. Each score carries its
 // in-tile index (4g+q) in its low 4 mantissa bits (see E), so the best needs
-// no compare/select per score.
+// no compare/select per score. Per pair (ta, tb) of new scores:
+//   m2 = max(m2, med3(m1, ta, tb)),  m1 = max3(m1, ta, tb)
+// (the runner-up of {m1 >= m2, ta, tb} is the larger of m2 and the median of
+// the other three): 3 VALU per 2 scores. v_max3 / v_med3 as instructions:
+// fmaxf would first re-quiet its operands (IEEE mode); scores are finite for
+// any certifiable point.
+__device__ inline float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+#ifndef EPI_MAX3
+#define EPI_MAX3 1
+#endif
 __device__ inline void tile_epilogue(const float (&sv)[16], float& m1, float& m2) {
-    // two independent (best, runner-up) chains over the even / odd scores, merged
-    // at the end; max(a, b) as med3(a, b, FLT_MAX): fmaxf would first re-quiet
-    // its operand (IEEE mode), and scores are finite for any certifiable point
+#if EPI_MAX3
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+        const float ta = __uint_as_float((__float_as_uint(sv[r]) & ~0xFu) | (uint32_t)r);
+        const float tb = __uint_as_float((__float_as_uint(sv[r + 1]) & ~0xFu) | (uint32_t)(r + 1));
+        m2 = __builtin_amdgcn_fmed3f(m2, __builtin_amdgcn_fmed3f(m1, ta, tb), 0x1.fffffep127f);
+        m1 = vmax3(m1, ta, tb);
+    }
+#else
+    // two independent (best, runner-up) chains over the even / odd scores,
+    // merged at the end; max(a, b) as med3(a, b, FLT_MAX)
     float a1 = m1, a2 = m2, b1 = -__builtin_inff(), b2 = -__builtin_inff();
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
         const float ta = __uint_as_float((__float_as_uint(sv[r]) & ~0xFu) | (uint32_t)r);
         const float tb = __uint_as_float((__float_as_uint(sv[r + 1]) & ~0xFu) | (uint32_t)(r + 1));
-        a2 = __builtin_amdgcn_fmed3f(a2, a1, ta);      // = max(a2, min(a1, ta)) as a2 <= a1
+        a2 = __builtin_amdgcn_fmed3f(a2, a1, ta);
         a1 = __builtin_amdgcn_fmed3f(a1, ta, 0x1.fffffep127f);
         b2 = __builtin_amdgcn_fmed3f(b2, b1, tb);
         b1 = __builtin_amdgcn_fmed3f(b1, tb, 0x1.fffffep127f);
     }
-    // merged runner-up = max(a2, b2, min(a1, b1)); best = max(a1, b1)
     m2 = __builtin_amdgcn_fmed3f(__builtin_amdgcn_fmed3f(a2, b2, 0x1.fffffep127f), __builtin_amdgcn_fmed3f(a1, b1, -0x1.fffffep127f), 0x1.fffffep127f);
     m1 = __builtin_amdgcn_fmed3f(a1, b1, 0x1.fffffep127f);
+#endif
 }
 constexpr int FP_THREADS = 64 * FP_WAVES;
 constexpr int FP_KMAX = 256;
