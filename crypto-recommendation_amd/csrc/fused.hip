@@ -507,6 +507,40 @@ __device__ inline void tile_scores(const floatx16& acc_hi, const floatx16& acc_l
     }
 }
 
+// One accumulator per tile (ONE_ACC): the lo products first (their partial sums
+// stay below 2^-10 |x||c|, so their <= 256 roundings add < 2^-25 |x||c|), then
+// the 8 hi MFMAs continue the same chain (<= 128 roundings of sum |terms|, as
+// acc_hi had): A1 still bounds the error, and the hi + lo add disappears.
+__device__ inline void tile_mfma1(const _Float16* ah_row, const _Float16* al_row, const half8 (&bh)[8],
+                                  const half8 (&bl)[8], floatx16& acc) {
+    const floatx16 z = {};
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const half8 ah = *reinterpret_cast<const half8*>(ah_row + 16 * s);
+        const half8 al = *reinterpret_cast<const half8*>(al_row + 16 * s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], s ? acc : z, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const half8 ah = *reinterpret_cast<const half8*>(ah_row + 16 * s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+    }
+}
+__device__ inline void tile_scores1(const floatx16& acc, const float* cn_tile_h, float (&sv)[16]) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const float4 cn = *reinterpret_cast<const float4*>(cn_tile_h + 8 * g);
+        const float2v a01 = {acc[4 * g], acc[4 * g + 1]}, a23 = {acc[4 * g + 2], acc[4 * g + 3]};
+        const float2v c01 = {cn.x, cn.y}, c23 = {cn.z, cn.w};
+        const float2v s01 = a01 + c01, s23 = a23 + c23;
+        sv[4 * g] = s01.x; sv[4 * g + 1] = s01.y; sv[4 * g + 2] = s23.x; sv[4 * g + 3] = s23.y;
+    }
+}
+#ifndef ONE_ACC
+#define ONE_ACC 0       // measured: 2.95 ms vs 2.91 with two accumulators (A/B on one box)
+#endif
+
 // Running best / runner-up over one tile's scores. Each score carries its
 // in-tile index (4g+q) in its low 4 mantissa bits (see E), so the best needs
 // no compare/select per score. Per pair (ta, tb) of new scores:
@@ -808,11 +842,17 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 #endif
 #pragma unroll TILE_UNROLL
         for (int t = 0; t < ntile32; t++) {
-            floatx16 acc_hi, acc_lo;
-            tile_mfma(my_h + t * 32 * FU_RS, my_l + t * 32 * FU_RS, bh, bl, acc_hi, acc_lo);
             const float m1_prev = m1;
             float sv[16];
+#if ONE_ACC
+            floatx16 acc;
+            tile_mfma1(my_h + t * 32 * FU_RS, my_l + t * 32 * FU_RS, bh, bl, acc);
+            tile_scores1(acc, lcn + t * 32 + 4 * h, sv);
+#else
+            floatx16 acc_hi, acc_lo;
+            tile_mfma(my_h + t * 32 * FU_RS, my_l + t * 32 * FU_RS, bh, bl, acc_hi, acc_lo);
             tile_scores(acc_hi, acc_lo, lcn + t * 32 + 4 * h, sv);
+#endif
             tile_epilogue(sv, m1, m2);
             t1 = m1 != m1_prev ? t : t1;
         }
