@@ -384,6 +384,267 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
     }
 }
 
+// ------------------------------------------------------- pruned exact pass
+// Listed rows, euclidean, K <= 256 (the persistent fused form's lists): a wave
+// takes XB_R rows; phase 1 scores every centroid in f32 (an FMA chain over a
+// transposed f32 copy CT32[j][c], loaded once per XB_R rows) with the bound e_c
+// of the f32 path above; the candidates are the centroids with
+// s~_c - e_c <= min (s~ + e) -- every other centroid's reference distance is
+// provably larger than some candidate's -- and phase 2 evaluates only those in
+// the reference's exact order (one lane each), keeping the first minimum.
+// A row whose f32 scores are not all finite, or with more than 64 candidates,
+// evaluates every centroid exactly instead.
+constexpr int XP_R = 8;
+constexpr int XP_WAVES = 4;
+constexpr int XP_SPLIT = 4;
+
+// exact_euclid with the centroid row loaded 16 values at a time (one L2 round
+// trip per 16 terms instead of one per term); x in LDS.
+__device__ inline double exact_euclid_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
+    double acc = 0.0;
+    for (int j0 = 0; j0 < d; j0 += 16) {
+        double cv[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++) cv[t] = j0 + t < d ? c[j0 + t] : 0.0;
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+            if (j0 + t < d) {
+                const double df = __dsub_rn((double)x[j0 + t], cv[t]);
+                acc = __dadd_rn(acc, __dmul_rn(df, df));
+            }
+    }
+    return sqrt(acc);
+}
+
+__global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, float* __restrict__ CT32,
+                                  float* __restrict__ cconst) {
+    // one wave per 64-centroid chunk: CT32 [d][Kpad], cconst = cn2[Kpad] ++ {ec, eb}[Kpad/64]
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    float* cn2 = cconst;
+    float* chunk = cconst + Kpad + 2 * blockIdx.x;
+    double ec = 0.0, eb = 0.0;
+    if (c >= K) {
+        for (int j = 0; j < d; j++) CT32[(size_t)j * Kpad + c] = 0.f;
+        cn2[c] = __builtin_inff();
+    } else {
+        double sq = 0.0;
+        for (int j = 0; j < d; j++) {
+            const double v = C[(size_t)c * d + j];
+            sq = fma(v, v, sq);
+            CT32[(size_t)j * Kpad + c] = (float)v;
+        }
+        const double up = 1.0 + 0x1p-18;
+        const double nc = sqrt(sq) * (1.0 + 0x1p-30);
+        cn2[c] = (float)sq;
+        ec = 0x1p-24 * (2.0 * d + 12.0) * nc * up;
+        eb = (0x1p-24 * 5.0 * sq + 0x1p-40 * sq) * up + 1e-30;
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        ec = fmax(ec, __shfl_xor(ec, off));
+        eb = fmax(eb, __shfl_xor(eb, off));
+    }
+    if (threadIdx.x == 0) {
+        chunk[0] = (float)(ec * (1.0 + 0x1p-20));
+        chunk[1] = (float)(eb * (1.0 + 0x1p-20));
+    }
+}
+
+__global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
+    const float* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
+    const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
+    const unsigned long long* __restrict__ row_count, int64_t max_rows, int32_t* __restrict__ assign,
+    double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows) {
+    __shared__ float xs[XP_WAVES][XP_R][XB_DMAX];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t total, g0, gstride;
+    if (seg_counts) {
+        const int seg = blockIdx.x / XP_SPLIT, part = blockIdx.x % XP_SPLIT;
+        rows += (int64_t)seg * seg_rows;
+        total = seg_counts[2 * seg];
+        g0 = (int64_t)part * XP_WAVES + wave;
+        gstride = (int64_t)XP_SPLIT * XP_WAVES;
+    } else {
+        total = (int64_t)*row_count;
+        if (total > max_rows) total = max_rows;
+        g0 = (int64_t)blockIdx.x * XP_WAVES + wave;
+        gstride = (int64_t)gridDim.x * XP_WAVES;
+    }
+    const float* chunkc = cconst + Kpad;
+    const int64_t ngroups = (total + XP_R - 1) / XP_R;
+    for (int64_t g = g0; g < ngroups; g += gstride) {
+        const int nr = (int)min((int64_t)XP_R, total - g * XP_R);
+        int32_t myrow[XP_R];
+#pragma unroll
+        for (int r = 0; r < XP_R; r++) myrow[r] = rows[g * XP_R + min(r, nr - 1)];   // pad with the last row
+        float xn2p[XP_R];
+#pragma unroll
+        for (int r = 0; r < XP_R; r++) {
+            float q = 0.f;
+            for (int j = lane; j < d; j += 64) {
+                const float v = X[(int64_t)myrow[r] * d + j];
+                xs[wave][r][j] = v;
+                q = fmaf(v, v, q);
+            }
+            xn2p[r] = q;
+        }
+        wave_sync();
+        // phase 1: f32 scores of centroids c = lane + 64 i
+        float acc[XP_R][4];
+#pragma unroll
+        for (int r = 0; r < XP_R; r++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) acc[r][i] = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < d; j++) {
+            float cv[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) cv[i] = 64 * i < Kpad ? CT32[(size_t)j * Kpad + 64 * i + lane] : 0.f;
+#pragma unroll
+            for (int r = 0; r < XP_R; r++) {
+                const float xj = xs[wave][r][j];
+#pragma unroll
+                for (int i = 0; i < 4; i++) acc[r][i] = fmaf(xj, cv[i], acc[r][i]);
+            }
+        }
+        // per row: bound, U = min (s~ + e), candidate masks (wave-uniform)
+        unsigned long long cm[XP_R][4];
+        int ncand[XP_R];
+        bool pr[XP_R];
+#pragma unroll
+        for (int r = 0; r < XP_R; r++) {
+            // |x|^2 in fp64 over the lanes' f32 partials, rounded up (as the f32 path)
+            double xn2 = (double)xn2p[r];
+            for (int off = 32; off >= 1; off >>= 1) xn2 += __shfl_xor(xn2, off);
+            xn2 *= 1.0 + 0x1p-20;
+            const float nx = (float)(sqrt(xn2) * (1.0 + 0x1p-30));
+            const float ex = (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30);
+            float lo[4];
+            float U = __builtin_inff();
+            bool finite = nx <= 3.0e38f;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int c = lane + 64 * i;
+                lo[i] = __builtin_inff();
+                if (c < K) {
+                    const float E = fmaf(nx, chunkc[2 * i], chunkc[2 * i + 1] + ex);
+                    const float sc = fmaf(-2.f, acc[r][i], cconst[c]);
+                    lo[i] = sc - E;
+                    const float hi = sc + E;
+                    finite = finite && (hi - lo[i]) <= 3.0e38f;   // false for inf / nan
+                    U = fminf(U, hi);
+                }
+            }
+            for (int off = 32; off >= 1; off >>= 1) U = fminf(U, __shfl_xor(U, off));
+            ncand[r] = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                cm[r][i] = __ballot(lo[i] <= U);
+                ncand[r] += __popcll(cm[r][i]);
+            }
+            pr[r] = r < nr && __all(finite) && ncand[r] >= 1;
+        }
+        // rows with <= 8 candidates: lane 8r + k evaluates row r's k-th candidate
+        {
+            const int r = lane >> 3, k = lane & 7;
+            int c = -1;
+            int seen = 0;
+#pragma unroll
+            for (int rr = 0; rr < XP_R; rr++) {
+                if (rr != r || !pr[rr] || ncand[rr] > 8) continue;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int n = __popcll(cm[rr][i]);
+                    if (c < 0 && k >= seen && k < seen + n) {
+                        unsigned long long m = cm[rr][i];
+                        for (int t = k - seen; t > 0; t--) m &= m - 1;
+                        c = 64 * i + __builtin_ctzll(m);
+                    }
+                    seen += n;
+                }
+            }
+            double best = 0.0;
+            int bi = -1;
+            if (c >= 0) {
+                best = exact_euclid_b16(xs[wave][r], C + (size_t)c * d, d);
+                bi = c;
+            }
+            for (int off = 4; off >= 1; off >>= 1) {        // within the row's 8 lanes
+                const double ob = __shfl_xor(best, off);
+                const int oi = __shfl_xor(bi, off);
+                const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
+                if (take) { best = ob; bi = oi; }
+            }
+            if (k == 0 && bi >= 0) {
+                assign[myrow[r]] = bi;
+                dist[myrow[r]] = best;
+            }
+        }
+        // the other rows, one at a time with the whole wave
+        for (int r = 0; r < nr; r++) {
+            if (pr[r] && ncand[r] <= 8) continue;
+            const bool prune = pr[r] && ncand[r] <= 64;
+            const float* xr = xs[wave][r];
+            double best = 0.0;
+            int bi = -1;
+            if (prune) {
+                // lane k takes the k-th candidate (increasing c)
+                int c = -1, seen = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int n = __popcll(cm[r][i]);
+                    if (c < 0 && lane >= seen && lane < seen + n) {
+                        unsigned long long m = cm[r][i];
+                        for (int t = lane - seen; t > 0; t--) m &= m - 1;
+                        c = 64 * i + __builtin_ctzll(m);
+                    }
+                    seen += n;
+                }
+                if (c >= 0) {
+                    best = exact_euclid_b16(xr, C + (size_t)c * d, d);
+                    bi = c;
+                }
+            } else {
+                for (int c = lane; c < K; c += 64) {
+                    const double dd = exact_euclid_b16(xr, C + (size_t)c * d, d);
+                    // assignment.hpp:66: the -1 sentinel takes centroid 0's distance
+                    // even if NaN, which then blocks every later '<'
+                    if (bi < 0 ? (dd == dd || c == 0) : dd < best) { best = dd; bi = c; }
+                }
+            }
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double ob = __shfl_xor(best, off);
+                const int oi = __shfl_xor(bi, off);
+                const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
+                if (take) { best = ob; bi = oi; }
+            }
+            if (lane == 0) {
+                assign[myrow[r]] = bi < 0 ? 0 : bi;
+                dist[myrow[r]] = bi < 0 ? -1.0 : best;
+            }
+        }
+        wave_sync();
+    }
+}
+
+int launch_assign_pruned_list(hipStream_t s, const float* X, int d, const double* C, int K, float* ws,
+                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
+                              int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
+    if (max_rows <= 0) return 0;
+    if (d > XB_DMAX || K > 256 || (seg_counts && nseg <= 0)) {
+        set_error("launch_assign_pruned_list: unsupported shape");
+        return -1;
+    }
+    const int Kpad = (K + 63) / 64 * 64;
+    float* CT32 = ws;
+    float* cconst = ws + (size_t)d * Kpad;
+    hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)(Kpad / 64)), dim3(64), 0, s, C, K, Kpad, d, CT32, cconst);
+    const int64_t groups = (max_rows + XP_R - 1) / XP_R;
+    const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
+    hipLaunchKernelGGL(assign_pruned_kernel, dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, X, d, C, CT32, cconst,
+                       K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+    return kstatus("assign_pruned_kernel");
+}
+
 int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                              int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {

@@ -52,6 +52,12 @@ int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double*
                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                              int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
                              int64_t seg_rows = 0, int nseg = 0);
+// Euclidean, listed rows, K <= 256: f32 candidate pruning, then exact order on
+// the candidates only (ws: d * ceil64(K) + ceil64(K) + ceil64(K)/32 floats).
+int launch_assign_pruned_list(hipStream_t s, const float* X, int d, const double* C, int K, float* ws,
+                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
+                              int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
+                              int64_t seg_rows = 0, int nseg = 0);
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist);
 

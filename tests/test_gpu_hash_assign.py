@@ -246,3 +246,35 @@ def test_fused_range_guard(ctx, form, monkeypatch):
     oa2, od2 = oracle.lloyd_assign(Xh, Cbig.cpu().numpy(), "euclidean", None)
     assert np.array_equal(a2.cpu().numpy(), oa2)
     assert np.array_equal(d2.cpu().numpy().view(np.uint64), od2.view(np.uint64))
+
+
+@pytest.mark.parametrize("case", ["ties", "near", "nonfinite"])
+def test_pruned_exact_pass(ctx, case, monkeypatch):
+    # the listed-row pass (f32 candidate pruning + exact order on the candidates)
+    # against the every-centroid pass and the oracle: duplicate centroids (exact
+    # ties, first index must win), near-duplicates (many candidates), and rows
+    # beyond the f16 range / non-finite centroids (every centroid evaluated)
+    N, d, K = 40_000, 128, 256
+    Xh = oracle.synth(77, N, d)
+    rng = np.random.default_rng(3)
+    Ch = Xh[rng.choice(N, K, replace=False)].astype(np.float64)
+    if case == "ties":
+        Ch[1::2] = Ch[0::2]                       # every centroid duplicated
+    elif case == "near":
+        Ch[100:164] = Ch[99] * (1.0 + 1e-7 * np.arange(1, 65)[:, None])
+    else:
+        Xh[::11, 5] = 4.0e4                       # f16 range guard: rows listed
+        Ch[7, 3] = np.inf
+    X = to_dev(ctx, Xh)
+    C = to_dev(ctx, Ch)
+    ctx.reset_stats()
+    a, dist = lshkm.lloyd_assign(ctx, X, C, "euclidean")
+    assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0
+    monkeypatch.setenv("LSHKM_EXACT_PASS", "full")
+    a1, d1 = lshkm.lloyd_assign(ctx, X, C, "euclidean")
+    assert np.array_equal(a.cpu().numpy(), a1.cpu().numpy())
+    assert np.array_equal(dist.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
+    sub = np.random.default_rng(4).choice(N, 3000, replace=False)
+    oa, od = oracle.lloyd_assign(Xh[sub], Ch, "euclidean", None)
+    assert np.array_equal(a.cpu().numpy()[sub], oa)
+    np.testing.assert_allclose(dist.cpu().numpy()[sub], od, rtol=1e-14, atol=0)
