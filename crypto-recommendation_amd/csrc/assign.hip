@@ -418,35 +418,26 @@ __device__ inline double exact_euclid_b16(const float* __restrict__ x, const dou
 
 __global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, float* __restrict__ CT32,
                                   float* __restrict__ cconst) {
-    // one wave per 64-centroid chunk: CT32 [d][Kpad], cconst = cn2[Kpad] ++ {ec, eb}[Kpad/64]
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    float* cn2 = cconst;
-    float* chunk = cconst + Kpad + 2 * blockIdx.x;
-    double ec = 0.0, eb = 0.0;
-    if (c >= K) {
-        for (int j = 0; j < d; j++) CT32[(size_t)j * Kpad + c] = 0.f;
-        cn2[c] = __builtin_inff();
-    } else {
-        double sq = 0.0;
-        for (int j = 0; j < d; j++) {
-            const double v = C[(size_t)c * d + j];
-            sq = fma(v, v, sq);
-            CT32[(size_t)j * Kpad + c] = (float)v;
-        }
-        const double up = 1.0 + 0x1p-18;
-        const double nc = sqrt(sq) * (1.0 + 0x1p-30);
-        cn2[c] = (float)sq;
-        ec = 0x1p-24 * (2.0 * d + 12.0) * nc * up;
-        eb = (0x1p-24 * 5.0 * sq + 0x1p-40 * sq) * up + 1e-30;
+    // one wave per centroid: CT32 [d][Kpad], cconst = cn2[Kpad] ++ {ec, eb}[Kpad/64]
+    // (chunk maxima by atomicMax on the bits of positive floats; zeroed first)
+    const int c = blockIdx.x, lane = threadIdx.x;
+    double sq = 0.0;
+    for (int j = lane; j < d; j += 64) {
+        const double v = c < K ? C[(size_t)c * d + j] : 0.0;
+        sq = fma(v, v, sq);
+        CT32[(size_t)j * Kpad + c] = (float)v;
     }
-    for (int off = 32; off >= 1; off >>= 1) {
-        ec = fmax(ec, __shfl_xor(ec, off));
-        eb = fmax(eb, __shfl_xor(eb, off));
-    }
-    if (threadIdx.x == 0) {
-        chunk[0] = (float)(ec * (1.0 + 0x1p-20));
-        chunk[1] = (float)(eb * (1.0 + 0x1p-20));
-    }
+    for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+    if (lane != 0) return;
+    if (c >= K) { cconst[c] = __builtin_inff(); return; }
+    const double up = 1.0 + 0x1p-18;
+    const double nc = sqrt(sq) * (1.0 + 0x1p-30);
+    cconst[c] = (float)sq;
+    const double ec = 0x1p-24 * (2.0 * d + 12.0) * nc * up;
+    const double eb = (0x1p-24 * 5.0 * sq + 0x1p-40 * sq) * up + 1e-30;
+    unsigned int* chunk = reinterpret_cast<unsigned int*>(cconst + Kpad + 2 * (c / 64));
+    atomicMax(chunk, __float_as_uint((float)(ec * (1.0 + 0x1p-20))));
+    atomicMax(chunk + 1, __float_as_uint((float)(eb * (1.0 + 0x1p-20))));
 }
 
 __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
@@ -637,7 +628,8 @@ int launch_assign_pruned_list(hipStream_t s, const float* X, int d, const double
     const int Kpad = (K + 63) / 64 * 64;
     float* CT32 = ws;
     float* cconst = ws + (size_t)d * Kpad;
-    hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)(Kpad / 64)), dim3(64), 0, s, C, K, Kpad, d, CT32, cconst);
+    (void)hipMemsetAsync(cconst + Kpad, 0, (size_t)(Kpad / 64) * 2 * 4, s);
+    hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, d, CT32, cconst);
     const int64_t groups = (max_rows + XP_R - 1) / XP_R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
     hipLaunchKernelGGL(assign_pruned_kernel, dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, X, d, C, CT32, cconst,
