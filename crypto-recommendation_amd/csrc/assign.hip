@@ -394,9 +394,16 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
 // the reference's exact order (one lane each), keeping the first minimum.
 // A row whose f32 scores are not all finite, or with more than 64 candidates,
 // evaluates every centroid exactly instead.
-constexpr int XP_R = 8;
+#ifndef XP_ROWS
+#define XP_ROWS 8
+#endif
+#ifndef XP_SPLITS
+#define XP_SPLITS 4
+#endif
+constexpr int XP_R = XP_ROWS;
 constexpr int XP_WAVES = 4;
-constexpr int XP_SPLIT = 4;
+constexpr int XP_SPLIT = XP_SPLITS;
+constexpr int XP_L = 64 / XP_R;      // lanes per row in the candidate phase
 
 // exact_euclid with the centroid row loaded 16 values at a time (one L2 round
 // trip per 16 terms instead of one per term); x in LDS.
@@ -534,14 +541,14 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
             }
             pr[r] = r < nr && __all(finite) && ncand[r] >= 1;
         }
-        // rows with <= 8 candidates: lane 8r + k evaluates row r's k-th candidate
+        // rows with <= XP_L candidates: lane XP_L r + k evaluates row r's k-th candidate
         {
-            const int r = lane >> 3, k = lane & 7;
+            const int r = lane / XP_L, k = lane % XP_L;
             int c = -1;
             int seen = 0;
 #pragma unroll
             for (int rr = 0; rr < XP_R; rr++) {
-                if (rr != r || !pr[rr] || ncand[rr] > 8) continue;
+                if (rr != r || !pr[rr] || ncand[rr] > XP_L) continue;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const int n = __popcll(cm[rr][i]);
@@ -559,7 +566,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
                 best = exact_euclid_b16(xs[wave][r], C + (size_t)c * d, d);
                 bi = c;
             }
-            for (int off = 4; off >= 1; off >>= 1) {        // within the row's 8 lanes
+            for (int off = XP_L / 2; off >= 1; off >>= 1) {   // within the row's lanes
                 const double ob = __shfl_xor(best, off);
                 const int oi = __shfl_xor(bi, off);
                 const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
@@ -572,7 +579,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         }
         // the other rows, one at a time with the whole wave
         for (int r = 0; r < nr; r++) {
-            if (pr[r] && ncand[r] <= 8) continue;
+            if (pr[r] && ncand[r] <= XP_L) continue;
             const bool prune = pr[r] && ncand[r] <= 64;
             const float* xr = xs[wave][r];
             double best = 0.0;
