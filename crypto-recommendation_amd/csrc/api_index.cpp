@@ -438,6 +438,15 @@ static int km_sums(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_
     if ((rc = reserve(ctx, WS_ROWS, (size_t)std::max<int64_t>(N, 1) * 4)) || (rc = reserve(ctx, WS_CROW, (size_t)(K + 1) * 8)))
         return rc;
     if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
+    // Parallel exact sums (fixed point where the chain provably never rounds);
+    // LSHKM_KM_PATH=chain runs every (c, j) chain sequentially.
+    const char* kp = getenv("LSHKM_KM_PATH");
+    if (!(kp && !strcmp(kp, "chain"))) {
+        if ((rc = ctx->ws_range[11].reserve(km_fx_ws_bytes(K, d)))) return rc;
+        if ((rc = launch_km_sums_fx(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, N,
+                                    sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        return 0;
+    }
     if ((rc = launch_km_chain(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, sums, counts,
                               carry, carry_counts))) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;

@@ -676,21 +676,32 @@ __global__ void assign_override_kernel(const int32_t* __restrict__ src, int K, i
     dist[r] = 0.0;
 }
 
-// Same, one block with the K source rows in LDS (K <= OV_LDS_MAX): the
-// later-centroid scan reads LDS instead of K^2/2 global loads.
+// Same, one block with the K source rows in LDS (K <= OV_LDS_MAX): thread c
+// scans the later entries 4 at a time (ds_read_b128, 4 independent reads in
+// flight) instead of K^2/2 dependent global loads.
 constexpr int OV_LDS_MAX = 8192;
 __global__ __launch_bounds__(1024) void assign_override_lds_kernel(const int32_t* __restrict__ src, int K, int64_t N,
                                                                   int32_t* __restrict__ assign,
                                                                   double* __restrict__ dist) {
-    __shared__ int32_t ls[OV_LDS_MAX];
-    for (int c = threadIdx.x; c < K; c += blockDim.x) ls[c] = src[c];
+    __shared__ __attribute__((aligned(16))) int32_t ls[OV_LDS_MAX + 16];
+    const int Kp = (K + 15) & ~15;
+    for (int c = threadIdx.x; c < Kp + 16; c += blockDim.x) ls[c] = c < K ? src[c] : -1;
     __syncthreads();
     for (int c = threadIdx.x; c < K; c += blockDim.x) {
         const int32_t r = ls[c];
         if (r < 0 || r >= N) continue;
-        bool last = true;
-        for (int c2 = c + 1; c2 < K && last; c2++) last = ls[c2] != r;
-        if (last) {
+        bool later = false;
+        for (int b = (c + 1) & ~15; b < Kp && !later; b += 16) {
+            const int4 v0 = *reinterpret_cast<const int4*>(ls + b);
+            const int4 v1 = *reinterpret_cast<const int4*>(ls + b + 4);
+            const int4 v2 = *reinterpret_cast<const int4*>(ls + b + 8);
+            const int4 v3 = *reinterpret_cast<const int4*>(ls + b + 12);
+            const int w[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                               v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+#pragma unroll
+            for (int t = 0; t < 16; t++) later |= b + t > c && w[t] == r;
+        }
+        if (!later) {                     // a later centroid on the same row wins
             assign[r] = c;
             dist[r] = 0.0;
         }

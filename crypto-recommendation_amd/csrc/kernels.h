@@ -99,6 +99,11 @@ int launch_memo_scatter(hipStream_t s, const int32_t* off, const int32_t* bit, i
 int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K,
                     double* sums, int64_t* counts, const double* carry = nullptr,
                     const int64_t* carry_counts = nullptr);
+// Same sums, parallel: exact int128 fixed-point sums wherever the sequential
+// chain provably never rounds, the sequential chain elsewhere (ws: km_fx_ws_bytes).
+size_t km_fx_ws_bytes(int K, int d);
+int launch_km_sums_fx(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                      double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws);
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
 

@@ -50,6 +50,195 @@ int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, c
     return kstatus("update.hip");
 }
 
+// ------------------------------------------------------------------ parallel form
+// The reference's chain s = ((0 + x_1) + x_2) + ... rounds only when a partial
+// sum is not a double. Every partial is an integer multiple of 2^q (q = the
+// lowest set bit over the chain's values) bounded by A = sum |x_i| <
+// count * 2^t (t = the highest bit position + 1), so when
+// ceil(log2 count) + t - q <= 53 no step rounds and the chain's result is the
+// exact sum -- which integer (fixed-point) arithmetic computes in any order.
+// Values are accumulated as int128 multiples of 2^-KMF (KMF = 80): every fp32
+// value with lowest bit >= 2^-80 and magnitude < 2^23 fits; a chain with
+// anything else (huge, tiny, inf, nan), or whose range test fails, is flagged
+// and recomputed by the sequential kernel above (km_chain_kernel).
+// Work: waves stream 512 consecutive member positions of the cluster-sorted
+// list (lane = dimension), flushing their int128 partial to the (c, j)
+// accumulator with two 64-bit atomics (the carry of the low word is exact mod
+// 2^128) whenever the cluster changes.
+constexpr int KMF = 80;
+constexpr int KMF_CH = 512;
+constexpr int KMF_BAD = 1 << 20;     // qmin marker of a chain that needs the sequential kernel
+
+struct KmFx {                        // per (c, j), zeroed / initialised by km_fx_init_kernel
+    unsigned long long lo;
+    long long hi;
+    int qmin;                        // lowest set-bit exponent, KMF_BAD if flagged
+    int tmax;                        // highest bit position + 1
+};
+
+__global__ void km_fx_init_kernel(KmFx* __restrict__ acc, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { acc[i].lo = 0; acc[i].hi = 0; acc[i].qmin = 1 << 30; acc[i].tmax = -(1 << 30); }
+}
+
+__device__ inline void km_fx_flush(KmFx* a, __int128 v, int qmin, int tmax, bool bad) {
+    const unsigned long long vlo = (unsigned long long)v;
+    const long long vhi = (long long)(v >> 64);
+    const unsigned long long old = atomicAdd(&a->lo, vlo);
+    const long long carry = (old + vlo < old) ? 1 : 0;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a->hi), (unsigned long long)(vhi + carry));
+    atomicMin(&a->qmin, bad ? -KMF_BAD : qmin);
+    atomicMax(&a->tmax, tmax);
+}
+
+__global__ __launch_bounds__(64) void km_fx_kernel(const float* __restrict__ X, int d, const int32_t* __restrict__ rows,
+                                                  const int64_t* __restrict__ crow, int K, int64_t M,
+                                                  KmFx* __restrict__ acc) {
+    const int64_t p0 = (int64_t)blockIdx.x * KMF_CH;
+    if (p0 >= M) return;
+    const int64_t p1 = min(M, p0 + KMF_CH);
+    const int j = blockIdx.y * 64 + threadIdx.x;
+    const bool on = j < d;
+    const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
+    // cluster of position p0: the last c with crow[c] <= p0 (wave-uniform binary search)
+    int lo = 0, hi = K;              // crow[lo] <= p0 < crow[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (crow[mid] <= p0) lo = mid; else hi = mid;
+    }
+    int c = lo;
+    int64_t cend = crow[c + 1];
+    __int128 s = 0;
+    int qmin = 1 << 30, tmax = -(1 << 30);
+    bool bad = false;
+    for (int64_t p = p0; p < p1; p += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = (on && p + u < p1) ? X[(int64_t)r4[p + u] * d + j] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            if (p + u >= p1) break;
+            while (p + u >= cend) {              // cluster boundary: flush, move on (skipping empty clusters)
+                if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
+                s = 0; qmin = 1 << 30; tmax = -(1 << 30); bad = false;
+                c++;
+                cend = crow[c + 1];
+            }
+            const uint32_t b = __float_as_uint(v[u]);
+            const int E = (int)((b >> 23) & 255u);
+            const uint32_t f = b & 0x7FFFFFu;
+            if (E == 0 && f == 0) continue;      // +-0 adds nothing (and -0 + 0 = +0 either way)
+            if (E == 255) { bad = true; continue; }
+            const uint32_t m = E ? (f | 0x800000u) : f;
+            const int e = (E ? E : 1) - 150;     // value = m * 2^e
+            const int q = e + __builtin_ctz(m), t = e + 32 - __builtin_clz(m);
+            qmin = min(qmin, q);
+            tmax = max(tmax, t);
+            if (q < -KMF || t > 23) { bad = true; continue; }
+            const __int128 w = (__int128)m << (e + KMF);
+            s += (b >> 31) ? -w : w;
+        }
+    }
+    if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
+}
+
+// Per (c, j): the exact sum if the chain provably never rounds, else a flag for
+// the sequential kernel. carry (sharded exact mode): the chain starts from it.
+__global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_t* __restrict__ crow, int K, int d,
+                                      const double* __restrict__ carry, const int64_t* __restrict__ carry_counts,
+                                      double* __restrict__ sums, int* __restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)K * d) return;
+    const int c = (int)(i / d);
+    const KmFx a = acc[i];
+    int64_t cnt = crow[c + 1] - crow[c];
+    __int128 s = ((__int128)a.hi << 64) | (__int128)a.lo;
+    int qmin = a.qmin, tmax = a.tmax;
+    bool ok = qmin > -KMF_BAD / 2;
+    if (carry && ok) {
+        const double s0 = carry[i];
+        cnt += 1;
+        if (s0 != 0.0) {
+            const uint64_t b = (uint64_t)__double_as_longlong(s0);
+            const int E = (int)((b >> 52) & 2047u);
+            const uint64_t f = b & 0xFFFFFFFFFFFFFull;
+            const uint64_t m = E ? (f | (1ull << 52)) : f;
+            const int e = (E ? E : 1) - 1075;
+            const int q = e + __builtin_ctzll(m), t = e + 64 - __builtin_clzll(m);
+            if (E == 2047 || q < -KMF || t > 23) ok = false;
+            else {
+                qmin = min(qmin, q);
+                tmax = max(tmax, t);
+                const __int128 w = (__int128)(m >> (q - e)) << (q + KMF);
+                s += (b >> 63) ? -w : w;
+            }
+        }
+    }
+    int lc = 0;
+    while (((int64_t)1 << lc) < cnt) lc++;          // ceil(log2 count)
+    if (ok && qmin <= tmax && lc + tmax - qmin > 53) ok = false;
+    if (ok) {
+        // |s| < 2^(53 + qmin + KMF): the conversion is exact, and so is the scaling
+        sums[i] = ldexp((double)s, -KMF);
+    } else {
+        atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));   // chain block (c, j/64) goes sequential
+    }
+}
+
+// The sequential chains of the flagged (c, 64-dim block)s only.
+__global__ __launch_bounds__(64) void km_chain_flagged_kernel(const float* __restrict__ X, int d,
+                                                             const int32_t* __restrict__ rows,
+                                                             const int64_t* __restrict__ crow, int K,
+                                                             const double* __restrict__ carry,
+                                                             const int* __restrict__ flag, double* __restrict__ sums) {
+    const int c = blockIdx.x;
+    if (!((flag[c] >> min(31, (int)blockIdx.y)) & 1)) return;
+    const int j = blockIdx.y * 64 + threadIdx.x;
+    if (j >= d) return;
+    const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
+    double s = carry ? carry[(size_t)c * d + j] : 0.0;
+    const int64_t beg = crow[c], end = crow[c + 1];
+    int64_t p = beg;
+    for (; p + KM_U <= end; p += KM_U) {
+        float v[KM_U];
+#pragma unroll
+        for (int u = 0; u < KM_U; u++) v[u] = X[(int64_t)r4[p + u] * d + j];
+#pragma unroll
+        for (int u = 0; u < KM_U; u++) s = __dadd_rn(s, (double)v[u]);
+    }
+    for (; p < end; p++) s = __dadd_rn(s, (double)X[(int64_t)r4[p] * d + j]);
+    sums[(size_t)c * d + j] = s;
+}
+
+__global__ void km_counts_kernel(const int64_t* __restrict__ crow, int K, const int64_t* __restrict__ carry_counts,
+                                 int64_t* __restrict__ counts) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < K) counts[c] = crow[c + 1] - crow[c] + (carry_counts ? carry_counts[c] : 0);
+}
+
+size_t km_fx_ws_bytes(int K, int d) { return (size_t)K * d * sizeof(KmFx) + (size_t)K * 4 + 64; }
+
+int launch_km_sums_fx(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                      double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws) {
+    KmFx* acc = reinterpret_cast<KmFx*>(ws);
+    int* flag = reinterpret_cast<int*>(acc + (size_t)K * d);
+    const int64_t n = (int64_t)K * d;
+    (void)hipMemsetAsync(flag, 0, (size_t)K * 4, s);
+    hipLaunchKernelGGL(km_fx_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, n);
+    const int jb = (d + 63) / 64;
+    if (M > 0)
+        hipLaunchKernelGGL(km_fx_kernel, dim3((unsigned)((M + KMF_CH - 1) / KMF_CH), (unsigned)jb), dim3(64), 0, s, X, d,
+                           rows, crow, K, M, acc);
+    hipLaunchKernelGGL(km_fx_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, crow, K, d, carry,
+                       carry_counts, sums, flag);
+    hipLaunchKernelGGL(km_chain_flagged_kernel, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K,
+                       carry, flag, sums);
+    if (counts)
+        hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
+                           counts);
+    return kstatus("update.hip (fixed point)");
+}
+
 // One wave per cluster: divide (unless empty), then the reference's movement
 // test with euclideanDistance(new, old) or cosineDistance(new, old).
 __global__ __launch_bounds__(64) void km_finalize_kernel(const double* __restrict__ sums, const int64_t* __restrict__ counts,

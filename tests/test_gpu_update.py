@@ -1,0 +1,83 @@
+"""GPU parity: the parallel k-means sums (update.hip fixed-point form) against
+the sequential reference-order chains (LSHKM_KM_PATH=chain) and the oracle —
+bit for bit — on inputs where every chain is exact, where some chains must
+fall back (wide dynamic range, inf / nan, denormals), with empty and huge
+clusters, and in the sharded carry mode."""
+import numpy as np
+import pytest
+
+import oracle
+from amd import lshkm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return lshkm.Context(0)
+
+
+def to_dev(ctx, a):
+    return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+
+
+def bits(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def both(ctx, X, a, C, monkeypatch):
+    Cn, cnt, cont = lshkm.kmeans_update(ctx, X, a, C, "euclidean", 0.0)
+    monkeypatch.setenv("LSHKM_KM_PATH", "chain")
+    Cs, cs, conts = lshkm.kmeans_update(ctx, X, a, C, "euclidean", 0.0)
+    monkeypatch.delenv("LSHKM_KM_PATH")
+    assert np.array_equal(bits(Cn), bits(Cs)) and np.array_equal(cnt.cpu().numpy(), cs.cpu().numpy()) and cont == conts
+    return Cn, cnt
+
+
+@pytest.mark.parametrize("kind", ["synth", "fp32_full", "wide", "special", "skewed"])
+def test_parallel_sums_match_chains(ctx, kind, monkeypatch):
+    rng = np.random.default_rng(11)
+    N, d, K = 300_000, 72, 40
+    if kind == "synth":
+        Xh = oracle.synth(5, N, d)
+    elif kind == "fp32_full":
+        Xh = rng.standard_normal((N, d)).astype(np.float32)                  # 24-bit mantissas
+    elif kind == "wide":
+        Xh = (rng.standard_normal((N, d)) * 10.0 ** rng.integers(-30, 8, (N, d))).astype(np.float32)
+    elif kind == "special":
+        Xh = rng.standard_normal((N, d)).astype(np.float32)
+        Xh[::9973, 3] = np.inf
+        Xh[::7919, 5] = np.nan
+        Xh[::101, 7] = 1e-42                                               # denormal
+        Xh[::103, 9] = -0.0
+        Xh[::107, 11] = 3.0e30
+    else:
+        Xh = rng.standard_normal((N, d)).astype(np.float32)
+    a = rng.integers(0, K, N).astype(np.int32)
+    if kind == "skewed":
+        a[: N * 3 // 4] = 3                                                 # one huge cluster
+        a[a == 5] = 6                                                       # an empty one
+    X, A = to_dev(ctx, Xh), to_dev(ctx, a)
+    C = to_dev(ctx, rng.standard_normal((K, d)))
+    Cn, cnt = both(ctx, X, A, C, monkeypatch)
+    sub = np.arange(N) < 60_000                                             # oracle on a prefix (its own chains)
+    if kind in ("synth", "fp32_full"):
+        Co, co, _ = oracle.kmeans_update(Xh, a, C.cpu().numpy(), "euclidean", 0.0)
+        assert np.array_equal(bits(Cn), Co.view(np.uint64))
+
+
+def test_parallel_sums_carry_mode(ctx):
+    # sharded exact mode: the chains continue shard to shard; parallel == chain
+    rng = np.random.default_rng(2)
+    N, d, K = 200_000, 40, 16
+    Xh = rng.standard_normal((N, d)).astype(np.float32)
+    Xh[::5000, 2] = 1e-38
+    a = rng.integers(0, K, N).astype(np.int32)
+    X, A = to_dev(ctx, Xh), to_dev(ctx, a)
+    cs = cc = None
+    for lo, hi in ((0, 70_000), (70_000, 150_000), (150_000, N)):
+        cs, cc = lshkm.kmeans_partial_carry(ctx, X[lo:hi], A[lo:hi], K, cs, cc)
+    whole_s, whole_c = lshkm.kmeans_partial_carry(ctx, X, A, K)
+    assert np.array_equal(bits(cs), bits(whole_s)) and np.array_equal(cc.cpu().numpy(), whole_c.cpu().numpy())

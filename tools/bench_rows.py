@@ -1,0 +1,210 @@
+"""Timings of the SURVEY §8 rows beside the headline (one MI355X): each row's
+device call at a production-like size (HIP-synchronised wall time, median of
+reps, inputs resident in HBM), next to the CPU restatement (oracle/, one
+thread, OMP_NUM_THREADS=1, kind "port") on a bounded sample of the same
+workload, scaled to the row's unit. Prints one JSON line per row.
+
+    python tools/bench_rows.py [--rows kpp,range,sil,update,lsh,cube,recom,csv] [--no-cpu]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+os.environ.setdefault("OMP_NUM_THREADS", "1")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import oracle  # noqa: E402
+from amd import lshkm  # noqa: E402
+
+
+def gpu_time(ctx, fn, reps=5):
+    fn()
+    ctx.sync()
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        ctx.sync()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def cpu_time(fn):
+    t0 = time.perf_counter()
+    fn()
+    return time.perf_counter() - t0
+
+
+def emit(row, unit, units, t_gpu, cpu=None, note=""):
+    line = {"row": row, "unit": unit, "units": units, "gpu_s": t_gpu, "gpu_rate": units / t_gpu}
+    if cpu:
+        cu, ct, sample = cpu
+        line["cpu_baseline"] = {"rate": cu / ct, "kind": "port", "cores": 1, "sample": sample}
+        line["gpu_over_cpu"] = line["gpu_rate"] / line["cpu_baseline"]["rate"]
+    if note:
+        line["note"] = note
+    print(json.dumps(line), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", default="kpp,range,sil,update,lsh,cube,recom,csv")
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+    rows = set(a.rows.split(","))
+    ctx = lshkm.Context(0)
+    cpu = not a.no_cpu
+
+    if "update" in rows:     # k_means (update.hpp:37-86), exact-order sums, C3 shape
+        N, d, K = 10_000_000, 128, 256
+        X = ctx.synth(0x5EED, N, d)
+        src = (np.arange(K) * (N // K)).astype(np.int64)
+        C = X[torch.from_numpy(src).to(ctx.dev)].double()
+        asg, _ = lshkm.lloyd_assign(ctx, X, C, "euclidean", src.astype(np.int32))
+        t = gpu_time(ctx, lambda: lshkm.kmeans_update(ctx, X, asg, C, "euclidean", 0.05))
+        c = None
+        if cpu:
+            n = 1_000_000
+            Xh, ah = X[:n].cpu().numpy(), asg[:n].cpu().numpy()
+            c = (n, cpu_time(lambda: oracle.kmeans_update(Xh, ah, C.cpu().numpy(), "euclidean", 0.05)),
+                 f"{n} rows, K={K}, d={d}")
+        emit("k_means update", "rows/s", N, t, c, "N=10M, d=128, K=256")
+        del X
+
+    if "kpp" in rows:        # k_means_pp (initialization.hpp:71-156)
+        N, d, K = 1_000_000, 128, 64
+        X = ctx.synth(0x5EED + 1, N, d)
+        t = gpu_time(ctx, lambda: lshkm.kmeans_pp_rows(ctx, X, K, "euclidean", 7), reps=3)
+        c = None
+        if cpu:
+            n = 100_000
+            Xh = X[:n].cpu().numpy()
+            c = (n * K, cpu_time(lambda: oracle.kmeans_pp(Xh, K, "euclidean", 7)), f"{n} rows, K={K}")
+        emit("k_means_pp", "row-centroid steps/s", N * K, t, c, "N=1M, d=128, K=64, euclidean")
+        del X
+
+    if "range" in rows:      # lsh_range_assignment (assignment.hpp:108-217)
+        N, d, K, L, k = 1_000_000, 128, 256, 5, 4
+        X = ctx.synth(0x5EED + 2, N, d)
+        V, tt, r, _ = lshkm.params_lsh_euclidean(77, L, k, d, 4.0)
+        lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 4.0, V=V, t=tt, r=r)
+        lsh.build(X)
+        src = (np.arange(K) * (N // K)).astype(np.int32)
+        Q = X[torch.from_numpy(src.astype(np.int64)).to(ctx.dev)]
+        C = Q.double()
+
+        def run():
+            ptr, ci = lsh.query(Q, filtered=False)
+            return lshkm.range_assign(ctx, X, C, ptr, ci, "euclidean", src_rows=src)
+        t = gpu_time(ctx, run, reps=3)
+        c = None
+        if cpu:
+            n = 100_000
+            Xs = X[:n].contiguous()
+            lsh2 = lshkm.LSH(ctx, "euclidean", d, k, L, n // 100, 4.0, V=V, t=tt, r=r)
+            lsh2.build(Xs)
+            s2 = (np.arange(K) * (n // K)).astype(np.int32)
+            Q2 = Xs[torch.from_numpy(s2.astype(np.int64)).to(ctx.dev)]
+            p2, c2 = lsh2.query(Q2, filtered=False)
+            Xh, C2 = Xs.cpu().numpy(), Q2.double().cpu().numpy()
+            c = (n, cpu_time(lambda: oracle.range_assign(Xh, C2, p2, c2, "euclidean", src_rows=s2)), f"{n} rows, K={K}")
+        emit("lsh_range_assignment", "rows/s", N, t, c, "N=1M, d=128, K=256, L=5, k=4, w=4 (query + range + Lloyd rest)")
+        del X
+
+    if "sil" in rows:        # silhouette_cluster (silhouette.hpp:31-144)
+        N, d, K = 100_000, 128, 16
+        X = ctx.synth(0x5EED + 3, N, d)
+        src = (np.arange(K) * (N // K)).astype(np.int64)
+        C = X[torch.from_numpy(src).to(ctx.dev)].double()
+        asg, _ = lshkm.lloyd_assign(ctx, X, C, "euclidean", src.astype(np.int32))
+        pairs = float(np.sum(np.bincount(asg.cpu().numpy(), minlength=K).astype(np.float64) ** 2) * 2)
+        t = gpu_time(ctx, lambda: lshkm.silhouette(ctx, X, asg, C, "euclidean"), reps=3)
+        c = None
+        if cpu:
+            n = 10_000
+            Xh = X[:n].cpu().numpy()
+            ah, _ = oracle.lloyd_assign(Xh, C.cpu().numpy(), "euclidean", None)
+            p2 = float(np.sum(np.bincount(ah, minlength=K).astype(np.float64) ** 2) * 2)
+            c = (p2, cpu_time(lambda: oracle.silhouette(Xh, ah, C.cpu().numpy(), "euclidean")), f"{n} rows, K={K}")
+        emit("silhouette_cluster", "distance pairs/s", pairs, t, c, "N=100k, d=128, K=16")
+        del X
+
+    if "lsh" in rows:        # create_LSH_hashtables + get_LSH_filtered_combined_buckets (C2)
+        N, d, L, k = 1_000_000, 128, 5, 4
+        X = ctx.synth(0x5EED, N, d)
+        V, tt, r, _ = lshkm.params_lsh_euclidean(12345, L, k, d, 0.4)
+        lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=tt, r=r)
+        tb = gpu_time(ctx, lambda: lsh.build(X))
+        c = None
+        if cpu:
+            n = 200_000
+            Xh = X[:n].cpu().numpy()
+            c = (n, cpu_time(lambda: oracle.bucket_csr(oracle.lsh_hash_euclid(Xh, V, tt, np.float32(0.4), r, N // 100)[2],
+                                                       N // 100)), f"{n} rows")
+        emit("create_LSH_hashtables", "rows/s", N, tb, c, "C2: N=1M, d=128, L=5, k=4, w=0.4, nb=10k")
+        nq = 65_536
+        qrows = torch.arange(nq, device=ctx.dev) * (N // nq)
+        Q = X[qrows]
+        alias = qrows.to(torch.int32)
+        tq = gpu_time(ctx, lambda: lsh.query(Q, True, alias))
+        emit("get_LSH_filtered_combined_buckets", "queries/s", nq, tq, None, "65,536 dataset-row queries, C2 index")
+        del X
+
+    if "cube" in rows:       # create_hypercube + get_hypercube_combined_buckets (C4)
+        N, d, k = 10_000_000, 128, 14
+        X = ctx.synth(0x5EED, N, d)
+        V, tt, st = lshkm.params_cube_euclidean(4242, k, d, 2.0)
+        cube = lshkm.Cube(ctx, "euclidean", d, k, 2.0, V=V, t=tt, rng_state=st)
+        tb = gpu_time(ctx, lambda: cube.build(X), reps=3)
+        emit("create_hypercube", "rows/s", N, tb, None, "C4: N=10M, d=128, d'=14, w=2 (euclidean F coins)")
+        nq = 65_536
+        Q = X[torch.arange(nq, device=ctx.dev) * (N // nq)]
+        tq = gpu_time(ctx, lambda: cube.query(Q, 14), reps=3)
+        emit("get_hypercube_combined_buckets", "queries/s", nq, tq, None, "65,536 queries, probes=14 (Hamming<=1)")
+        del X
+
+    if "recom" in rows:      # get_P_closest + get_top_N_recom (crypto_rec.hpp:213-325)
+        N, d, Q, P, NT = 200_000, 100, 20_000, 20, 5
+        rng = np.random.default_rng(5)
+        Xh = rng.integers(-40, 41, size=(N, d)).astype(np.float64) / 8.0
+        X = torch.from_numpy(Xh).to(ctx.dev)
+        Uh = Xh[rng.integers(0, N, Q)]
+        U = torch.from_numpy(Uh).to(ctx.dev)
+        cand = [np.sort(rng.choice(N, 200, replace=False)).astype(np.int32) for _ in range(Q)]
+        cp = torch.from_numpy(np.cumsum([0] + [len(c) for c in cand]).astype(np.int64)).to(ctx.dev)
+        ci = torch.from_numpy(np.concatenate(cand)).to(ctx.dev)
+        t = gpu_time(ctx, lambda: lshkm.p_closest(ctx, X, U, cp, ci, P))
+        c = None
+        if cpu:
+            q2 = 2000
+            cph, cih = cp[:q2 + 1].cpu().numpy(), ci[:int(cp[q2])].cpu().numpy()
+            c = (q2, cpu_time(lambda: oracle.p_closest(Xh, Uh[:q2], cph, cih, P)), f"{q2} users x 200 candidates")
+        emit("get_P_closest", "users/s", Q, t, c, f"N={N}, d={d}, {Q} users x 200 candidates, P={P}")
+
+    if "csv" in rows:        # VectorReader (vector_reader.hpp:54-85)
+        n, d = 200_000, 64
+        Xh = np.random.default_rng(9).standard_normal((n, d)).astype(np.float32)
+        with tempfile.NamedTemporaryFile("w", suffix=".csv", delete=False) as f:
+            for i in range(n):
+                f.write(f"{i}," + ",".join(repr(float(v)) for v in Xh[i]) + "\n")
+            path = f.name
+        mb = os.path.getsize(path) / 1e6
+        t0 = time.perf_counter(); lshkm.read_vectors(path, ",", 1, 0); t = time.perf_counter() - t0
+        t1 = time.perf_counter(); lshkm.read_vectors(path, ",", 1, 1); t1 = time.perf_counter() - t1
+        os.unlink(path)
+        emit("VectorReader::read", "MB/s", mb, t, (mb, t1, f"{mb:.0f} MB, 1 thread of the same parser"),
+             f"{n} x {d} CSV, all host threads (host-side row)")
+
+
+if __name__ == "__main__":
+    main()
