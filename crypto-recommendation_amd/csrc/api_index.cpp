@@ -140,11 +140,13 @@ int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* al
                                          eu ? slot<int32_t>(ctx, WS_QTUP) : nullptr, nullptr, slot<int32_t>(ctx, WS_QBKT),
                                          (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
     auto run = [&](int phase, int32_t* out) {
+        if (ctx->ws_scan.reserve(scan_ws_bytes(nq * L + nq))) return LSHKM_ERR_NOMEM;
         return launch_lsh_query(s, slot<int32_t>(ctx, WS_QBKT), slot<int32_t>(ctx, WS_QTUP), alias, nq, L, k, nb,
                                 eu && filtered ? 1 : 0, lsh->N, eu ? lsh->tuples.as<int32_t>() : nullptr,
                                 lsh->bucket.as<int32_t>(), lsh->row_ptr.as<int64_t>(), lsh->idx.as<int32_t>(),
                                 slot<int64_t>(ctx, WS_SIZES), slot<int64_t>(ctx, WS_COFF), slot<int32_t>(ctx, WS_KLIST),
-                                slot<int64_t>(ctx, WS_KCNT), slot<int64_t>(ctx, WS_QSZ), out_ptr, out, phase);
+                                slot<int64_t>(ctx, WS_KCNT), slot<int64_t>(ctx, WS_QSZ), out_ptr, out, phase,
+                                ctx->ws_scan.as<int64_t>());
     };
     if ((rc = run(0, nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
     int64_t cand = 0;
@@ -388,20 +390,21 @@ int lshkm_cube_query(lshkm_cube cube, const float* Q, int64_t nq, int probes, in
         return 0;
     }
     if ((rc = reserve(ctx, WS_QBKT, (size_t)nq * 4)) || (rc = reserve(ctx, WS_MASKS, (size_t)S * 4)) ||
-        (rc = reserve(ctx, WS_QSZ, (size_t)nq * S * 8)) || (rc = reserve(ctx, WS_CROW, (size_t)(nq * S + 1) * 8)))
+        (rc = reserve(ctx, WS_QSZ, (size_t)nq * S * 8)) || (rc = reserve(ctx, WS_CROW, (size_t)(nq * S + 1) * 8)) ||
+        (rc = ctx->ws_scan.reserve(scan_ws_bytes(nq * S))))
         return rc;
     if ((rc = cube_vertices_impl(cube, Q, nq, slot<int32_t>(ctx, WS_QBKT)))) return rc;
     LSHKM_HIP(hipMemcpyAsync(ctx->ws[WS_MASKS].p, masks.data(), (size_t)S * 4, hipMemcpyHostToDevice, s));
     if ((rc = launch_cube_query(s, slot<int32_t>(ctx, WS_QBKT), nq, slot<int32_t>(ctx, WS_MASKS), S, cube->row_ptr.as<int64_t>(),
                                 cube->idx.as<int32_t>(), slot<int64_t>(ctx, WS_QSZ), slot<int64_t>(ctx, WS_CROW), out_ptr,
-                                nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                                nullptr, ctx->ws_scan.as<int64_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     int64_t total = 0;
     if ((rc = d2h(ctx, &total, out_ptr + nq, 8))) return rc;
     *total_host = total;
     if (out_idx && total <= out_cap && total > 0)
         if ((rc = launch_cube_query(s, slot<int32_t>(ctx, WS_QBKT), nq, slot<int32_t>(ctx, WS_MASKS), S,
                                     cube->row_ptr.as<int64_t>(), cube->idx.as<int32_t>(), slot<int64_t>(ctx, WS_QSZ),
-                                    slot<int64_t>(ctx, WS_CROW), out_ptr, out_idx))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                                    slot<int64_t>(ctx, WS_CROW), out_ptr, out_idx, ctx->ws_scan.as<int64_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;
 }
 

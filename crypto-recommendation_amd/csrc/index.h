@@ -50,6 +50,7 @@ struct lshkm_ctx_s {
     lshkm::Buf ws[16];
     // range assignment workspace (lshkm_range_assign)
     lshkm::Buf ws_range[12];
+    lshkm::Buf ws_scan;          // multi-block scans of large query size arrays
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
     bool timing = false;
     hipEvent_t tev[2] = {nullptr, nullptr};

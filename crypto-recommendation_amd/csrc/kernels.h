@@ -70,14 +70,16 @@ int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, cons
 int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr);
 
 // Queries (query.hip).
-int launch_scan_i64(hipStream_t s, const int64_t* a, int64_t M, int64_t* out);
+size_t scan_ws_bytes(int64_t M);
+int launch_scan_i64(hipStream_t s, const int64_t* a, int64_t M, int64_t* out, int64_t* scratch = nullptr);
 int launch_lsh_query(hipStream_t s, const int32_t* qbucket, const int32_t* qtuple, const int32_t* alias, int64_t nq,
                      int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* tuples, const int32_t* bucket,
                      const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* cand_off,
-                     int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase);
+                     int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase,
+                     int64_t* scan_ws = nullptr);
 int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int32_t* masks, int S,
                       const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* slot_off,
-                      int64_t* out_ptr, int32_t* out);
+                      int64_t* out_ptr, int32_t* out, int64_t* scan_ws = nullptr);
 
 // Hypercube coins (cube.hip).
 int launch_h_minmax(hipStream_t s, const int32_t* h, int64_t n, int32_t* mm_dev);

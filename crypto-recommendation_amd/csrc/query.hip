@@ -44,8 +44,60 @@ __global__ __launch_bounds__(1024) void scan_i64_kernel(const int64_t* __restric
     if (t == 1023) out[M] = part[1023];
 }
 
-int launch_scan_i64(hipStream_t s, const int64_t* a, int64_t M, int64_t* out) {
-    hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, a, M, out);
+// Large M: reduce-then-scan over SC_CH-element chunks (one block each, 8
+// consecutive elements per thread), the chunk totals scanned by one block.
+constexpr int SC_CH = 8192;
+__global__ __launch_bounds__(1024) void scan_chunk_sum_kernel(const int64_t* __restrict__ a, int64_t M,
+                                                             int64_t* __restrict__ part) {
+    __shared__ int64_t red[1024];
+    const int64_t base = (int64_t)blockIdx.x * SC_CH + threadIdx.x * 8;
+    int64_t s = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) s += base + u < M ? a[base + u] : 0;
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(1024) void scan_chunk_kernel(const int64_t* __restrict__ a, int64_t M,
+                                                         const int64_t* __restrict__ part_off, int64_t* __restrict__ out) {
+    __shared__ int64_t sh[1024];
+    const int t = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * SC_CH + t * 8;
+    int64_t v[8], s = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) { v[u] = base + u < M ? a[base + u] : 0; s += v[u]; }
+    sh[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {          // Hillis-Steele inclusive scan of the thread sums
+        const int64_t w = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += w;
+        __syncthreads();
+    }
+    int64_t run = part_off[blockIdx.x] + (t ? sh[t - 1] : 0);
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+        if (base + u < M) { out[base + u] = run; run += v[u]; }
+    if (blockIdx.x == gridDim.x - 1 && t == 1023) out[M] = part_off[gridDim.x];
+}
+
+size_t scan_ws_bytes(int64_t M) { return (size_t)(2 * ((M + SC_CH - 1) / SC_CH + 1)) * 8; }
+
+// scratch: scan_ws_bytes(M) bytes, or NULL (then one block scans everything)
+int launch_scan_i64(hipStream_t s, const int64_t* a, int64_t M, int64_t* out, int64_t* scratch) {
+    if (M <= 4 * SC_CH || !scratch) {
+        hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, a, M, out);
+        return kstatus("query.hip");
+    }
+    const int64_t nb = (M + SC_CH - 1) / SC_CH;
+    hipLaunchKernelGGL(scan_chunk_sum_kernel, dim3((unsigned)nb), dim3(1024), 0, s, a, M, scratch);
+    hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, scratch, nb, scratch + nb + 1);
+    hipLaunchKernelGGL(scan_chunk_kernel, dim3((unsigned)nb), dim3(1024), 0, s, a, M, scratch + nb + 1, out);
     return kstatus("query.hip");
 }
 
@@ -141,18 +193,19 @@ __global__ __launch_bounds__(256) void lq_merge(const int64_t* __restrict__ cand
 int launch_lsh_query(hipStream_t s, const int32_t* qbucket, const int32_t* qtuple, const int32_t* alias, int64_t nq,
                      int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* tuples, const int32_t* bucket,
                      const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* cand_off,
-                     int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase) {
+                     int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase,
+                     int64_t* scan_ws) {
     const int64_t pairs = nq * L;
     if (phase == 0) {          // candidate counts -> cand_off[pairs + 1]
         hipLaunchKernelGGL(lq_sizes, dim3((unsigned)std::min<int64_t>((pairs + 255) / 256, 4096)), dim3(256), 0, s, qbucket,
                            nq, L, nb, row_ptr, sizes);
-        hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, sizes, pairs, cand_off);
+        if (launch_scan_i64(s, sizes, pairs, cand_off, scan_ws)) return -2;
     } else if (phase == 1) {   // filter + dedup + compact -> out_ptr[nq + 1]
         hipLaunchKernelGGL(lq_mark, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, qbucket, qtuple, alias, nq, L, k,
                            nb, filtered, N, tuples, bucket, row_ptr, idx, cand_off, klist, kcount);
         hipLaunchKernelGGL(lq_qsizes, dim3((unsigned)std::min<int64_t>((nq + 255) / 256, 4096)), dim3(256), 0, s, kcount,
                            nq, L, qsz);
-        hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, qsz, nq, out_ptr);
+        if (launch_scan_i64(s, qsz, nq, out_ptr, scan_ws)) return -2;
     } else {                   // merge into the caller's output
         hipLaunchKernelGGL(lq_merge, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, cand_off, kcount, klist, nq, L,
                            out_ptr, out);
@@ -190,11 +243,11 @@ __global__ __launch_bounds__(256) void cq_copy(const int32_t* __restrict__ qvert
 
 int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int32_t* masks, int S,
                       const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* slot_off,
-                      int64_t* out_ptr, int32_t* out) {
+                      int64_t* out_ptr, int32_t* out, int64_t* scan_ws) {
     const int64_t slots = nq * S;
     hipLaunchKernelGGL(cq_sizes, dim3((unsigned)std::min<int64_t>((slots + 255) / 256, 4096)), dim3(256), 0, s, qvert, nq,
                        masks, S, row_ptr, sizes);
-    hipLaunchKernelGGL(scan_i64_kernel, dim3(1), dim3(1024), 0, s, sizes, slots, slot_off);
+    if (launch_scan_i64(s, sizes, slots, slot_off, scan_ws)) return -2;
     hipLaunchKernelGGL(cq_qptr, dim3((unsigned)std::min<int64_t>((nq + 256) / 256, 4096)), dim3(256), 0, s, slot_off, nq, S,
                        out_ptr);
     if (out)

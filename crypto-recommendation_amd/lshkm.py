@@ -241,7 +241,7 @@ class LSH:
         _ck(lib().lshkm_lsh_get_buckets(self.h, table, _np_ptr(rp), _np_ptr(idx)))
         return rp, idx[:self.N]
 
-    def query(self, Q, filtered=True, alias_rows=None):
+    def query(self, Q, filtered=True, alias_rows=None, device=False):
         """Batched get_LSH_[filtered_]combined_buckets: returns (ptr[nq+1], idx) numpy."""
         torch = self.ctx.torch
         nq = Q.shape[0]
@@ -253,6 +253,8 @@ class LSH:
         _ck(lib().lshkm_lsh_query(self.h, _t_ptr(Q), nq, _t_ptr(alias_rows), int(filtered), _t_ptr(ptr), _t_ptr(out),
                                   total.value, C.byref(total)))
         self.ctx.sync()
+        if device:                                   # device tensors, no host copy
+            return ptr, out[:total.value]
         return ptr.cpu().numpy(), out[:total.value].cpu().numpy()
 
 
@@ -317,7 +319,7 @@ class Cube:
         f, h, bits = (np.ascontiguousarray(a, np.int32) for a in (f, h, bits))
         _ck(lib().lshkm_cube_import_coins(self.h, _np_ptr(f), _np_ptr(h), _np_ptr(bits), len(f), rng_state))
 
-    def query(self, Q, probes):
+    def query(self, Q, probes, device=False):
         torch = self.ctx.torch
         nq = Q.shape[0]
         ptr = self.ctx.empty((nq + 1,), torch.int64)
@@ -327,6 +329,8 @@ class Cube:
         _ck(lib().lshkm_cube_query(self.h, _t_ptr(Q), nq, probes, _t_ptr(ptr), _t_ptr(out), total.value,
                                    C.byref(total)))
         self.ctx.sync()
+        if device:                                   # device tensors, no host copy
+            return ptr, out[:total.value]
         return ptr.cpu().numpy(), out[:total.value].cpu().numpy()
 
 

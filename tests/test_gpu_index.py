@@ -235,3 +235,42 @@ def test_kmeans_update_large_vs_oracle(ctx):
     C3, cont3 = lshkm.kmeans_finalize(ctx, cs, cc, Cold, "euclidean", 0.05)
     assert np.array_equal(cc.cpu().numpy(), ocnt) and cont3 == cont
     assert np.array_equal(C3.cpu().numpy().view(np.uint64), on.view(np.uint64))      # bit-exact
+
+
+def test_queries_large_batches_multiblock_scan(ctx):
+    # query batches whose per-slot size arrays exceed one scan block (nq * S and
+    # nq * L > 32768): the multi-block scan must give the same CSR as the sizes
+    N, d, k = 200_000, 32, 10
+    X = ctx.synth(41, N, d)
+    Xh = X.cpu().numpy()
+    V, t, st = lshkm.params_cube_euclidean(5, k, d, 2.0)
+    cube = lshkm.Cube(ctx, "euclidean", d, k, 2.0, V=V, t=t, rng_state=st)
+    cube.build(X)
+    nq, probes = 40_000, 10
+    rows = np.random.default_rng(1).choice(N, nq, replace=False)
+    Q = X[to_dev(ctx, rows.astype(np.int64))]
+    ptr, idx = cube.query(Q, probes)
+    rp, bidx = cube.buckets()
+    qv = cube.vertices(Q).cpu().numpy()
+    sizes = np.diff(rp)
+    want = np.zeros(nq + 1, np.int64)
+    seqs = [oracle.cube_probe_seq(int(v), probes, k) for v in qv]
+    want[1:] = np.cumsum([sizes[s].sum() for s in seqs])
+    assert np.array_equal(ptr, want)
+    for q in np.random.default_rng(2).choice(nq, 200, replace=False):
+        got = idx[ptr[q]:ptr[q + 1]]
+        exp = np.concatenate([bidx[rp[v]:rp[v + 1]] for v in seqs[q]])
+        assert np.array_equal(got, exp), q
+    # LSH: 30k queries x L = 5 tables
+    L, kk = 5, 4
+    V2, t2, r2, _ = lshkm.params_lsh_euclidean(9, L, kk, d, 1.0)
+    lsh = lshkm.LSH(ctx, "euclidean", d, kk, L, N // 100, 1.0, V=V2, t=t2, r=r2)
+    lsh.build(X)
+    qr = rows[:30_000]
+    ptr2, out2 = lsh.query(Q[:30_000], False)
+    _, _, qb = oracle.lsh_hash_euclid(Xh[qr], V2, t2, np.float32(1.0), r2, N // 100)
+    _, _, b = oracle.lsh_hash_euclid(Xh, V2, t2, np.float32(1.0), r2, N // 100)
+    orp, oidx = oracle.bucket_csr(b, N // 100)
+    for q in np.random.default_rng(3).choice(30_000, 100, replace=False):
+        exp = oracle.lsh_query(N, N // 100, orp, oidx, qb[q])
+        assert np.array_equal(out2[ptr2[q]:ptr2[q + 1]], exp), q

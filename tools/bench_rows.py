@@ -104,7 +104,7 @@ def main():
         C = Q.double()
 
         def run():
-            ptr, ci = lsh.query(Q, filtered=False)
+            ptr, ci = lsh.query(Q, filtered=False, device=True)
             return lshkm.range_assign(ctx, X, C, ptr, ci, "euclidean", src_rows=src)
         t = gpu_time(ctx, run, reps=3)
         c = None
@@ -156,7 +156,7 @@ def main():
         qrows = torch.arange(nq, device=ctx.dev) * (N // nq)
         Q = X[qrows]
         alias = qrows.to(torch.int32)
-        tq = gpu_time(ctx, lambda: lsh.query(Q, True, alias))
+        tq = gpu_time(ctx, lambda: lsh.query(Q, True, alias, device=True))
         emit("get_LSH_filtered_combined_buckets", "queries/s", nq, tq, None, "65,536 dataset-row queries, C2 index")
         del X
 
@@ -169,7 +169,7 @@ def main():
         emit("create_hypercube", "rows/s", N, tb, None, "C4: N=10M, d=128, d'=14, w=2 (euclidean F coins)")
         nq = 65_536
         Q = X[torch.arange(nq, device=ctx.dev) * (N // nq)]
-        tq = gpu_time(ctx, lambda: cube.query(Q, 14), reps=3)
+        tq = gpu_time(ctx, lambda: cube.query(Q, 14, device=True), reps=3)
         emit("get_hypercube_combined_buckets", "queries/s", nq, tq, None, "65,536 queries, probes=14 (Hamming<=1)")
         del X
 
