@@ -232,13 +232,24 @@ __global__ __launch_bounds__(256) void cq_copy(const int32_t* __restrict__ qvert
                                                const int32_t* __restrict__ masks, int S,
                                                const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ idx,
                                                const int64_t* __restrict__ slot_off, int32_t* __restrict__ out) {
+    // persistent waves over the (query, probe) slots: a launch of one wave per
+    // slot spent more time in block dispatch than in the copy
     const int lane = threadIdx.x & 63;
-    const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (e >= nq * S) return;
-    const int64_t q = e / S;
-    const int64_t v = qvert[q] ^ masks[e - q * S];
-    const int64_t beg = row_ptr[v], n = row_ptr[v + 1] - beg, dst = slot_off[e];
-    for (int64_t p = lane; p < n; p += 64) out[dst + p] = idx[beg + p];
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < nq * S; e += nw) {
+        const int64_t q = e / S;
+        const int64_t v = qvert[q] ^ masks[e - q * S];
+        const int64_t beg = row_ptr[v], n = row_ptr[v + 1] - beg, dst = slot_off[e];
+        // 8 loads in flight per lane before the stores (a bucket is ~N / 2^k rows)
+        for (int64_t p = lane; p < n; p += 512) {
+            int32_t w[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) w[u] = p + 64 * u < n ? idx[beg + p + 64 * u] : 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (p + 64 * u < n) out[dst + p + 64 * u] = w[u];
+        }
+    }
 }
 
 int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int32_t* masks, int S,
@@ -251,7 +262,7 @@ int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int
     hipLaunchKernelGGL(cq_qptr, dim3((unsigned)std::min<int64_t>((nq + 256) / 256, 4096)), dim3(256), 0, s, slot_off, nq, S,
                        out_ptr);
     if (out)
-        hipLaunchKernelGGL(cq_copy, dim3((unsigned)((slots + 3) / 4)), dim3(256), 0, s, qvert, nq, masks, S, row_ptr, idx,
+        hipLaunchKernelGGL(cq_copy, dim3((unsigned)std::min<int64_t>((slots + 3) / 4, 4096)), dim3(256), 0, s, qvert, nq, masks, S, row_ptr, idx,
                            slot_off, out);
     return kstatus("query.hip");
 }
