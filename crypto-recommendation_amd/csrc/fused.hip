@@ -471,7 +471,12 @@ __global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
 #ifndef FP_KEEP_X
 #define FP_KEEP_X 1
 #endif
-constexpr int FP_WAVES = FP_KEEP_X ? 8 : 12;   // 2 / 3 per SIMD: <= 256 / 168 VGPRs
+// FP_WAVES_SET = 4 (one wave per SIMD, 512 registers, TILE_UNROLL 8): measured
+// 3.50 ms vs 2.93 -- the second wave's overlap is worth more than the registers.
+#ifndef FP_WAVES_SET
+#define FP_WAVES_SET 0
+#endif
+constexpr int FP_WAVES = FP_WAVES_SET ? FP_WAVES_SET : FP_KEEP_X ? 8 : 12;   // 2 / 3 per SIMD: <= 256 / 168 VGPRs
 #ifndef TILE_UNROLL
 #define TILE_UNROLL 1
 #endif
@@ -482,7 +487,7 @@ constexpr int FP_WAVES = FP_KEEP_X ? 8 : 12;   // 2 / 3 per SIMD: <= 256 / 168 V
 #define YOUNG_PRIO 0    // s_setprio for waves FP_WAVES/2.. for the whole loop (experiment knob)
 #endif
 #ifndef PIPE_TILES
-#define PIPE_TILES 0
+#define PIPE_TILES 0    // 1: measured 3.13 ms vs 2.91 (WAVE_OFFSET 8: 2.96, TILE_UNROLL 2: 2.91)
 #endif
 // Winner-row loads of the distance chain issued CHAIN_PF 16-dim steps ahead.
 // Measured (fused pass, N = 10M): 1 -> 3.03 ms, 2 -> 3.11, 4 -> 3.16, 8 -> 3.32:
