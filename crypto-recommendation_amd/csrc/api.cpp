@@ -416,13 +416,14 @@ int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, in
 // ------------------------------------------------------------------- Lloyd
 }  // extern "C"
 
-// Kernel path for euclidean assignment: the split-f16 fused kernel (d = 128),
-// else the f32-MFMA kernel (d <= 256), else the exact pass. LSHKM_ASSIGN_PATH
-// = "f32" / "exact" forces a path (tests compare them).
+// Kernel path for assignment: euclidean takes the split-f16 fused kernel
+// (d = 128), else the f32-MFMA kernel (d <= 256), else the exact pass; cosine
+// takes the f32-MFMA kernel (certified -x.c/|c| scores) for d <= 256.
+// LSHKM_ASSIGN_PATH = "f32" / "exact" forces a path (tests compare them).
 static int assign_path(int metric, int d) {
     const char* e = getenv("LSHKM_ASSIGN_PATH");
-    if (metric != LSHKM_METRIC_EUCLIDEAN || (e && !strcmp(e, "exact"))) return 2;
-    if (d == 128 && !(e && !strcmp(e, "f32"))) return 0;
+    if (e && !strcmp(e, "exact")) return 2;
+    if (metric == LSHKM_METRIC_EUCLIDEAN && d == 128 && !(e && !strcmp(e, "f32"))) return 0;
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
@@ -503,7 +504,7 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
         LSHKM_HIP(hipMemsetAsync(cnt, 0, 8, s));
         if ((rc = launch_centroid_prep(s, C, K, Kpad, d, DP, metric, (float*)ctx->ws_c32.p, (float*)ctx->ws_cconst.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if ((rc = launch_assign_mfma(s, X, N, d, DP, C, K, Kpad, (const float*)ctx->ws_c32.p, (const float*)ctx->ws_cconst.p,
+        if ((rc = launch_assign_mfma(s, X, N, d, DP, C, K, Kpad, metric, (const float*)ctx->ws_c32.p, (const float*)ctx->ws_cconst.p,
                                      assign, dist, (int32_t*)ctx->ws_ambig.p, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
         // ambiguous-count statistic

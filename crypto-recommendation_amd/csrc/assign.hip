@@ -39,18 +39,23 @@ int assign_dp(int d) {
     return 0;
 }
 
-__global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, int DP,
+__global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, int DP, int metric,
                                      float* __restrict__ C32, float* __restrict__ cconst) {
     // One wave per 64-centroid chunk. cconst = cn2[Kpad] ++ {ecmax, ebmax}[Kpad/64]:
     // the bound coefficients are taken as the max over the chunk, so the MFMA
     // epilogue needs one per-lane bound per chunk instead of per centroid.
+    // Cosine (metric 1): cn2[c] = f32(1 / |c|) and the score is -(x.c)/|c|
+    // (argmin = the reference's argmin of 1 - cos): |s~ - s| <= (DP + 4) 2^-24 |x|
+    // (the f32 chain, c's f32 rounding, 1/|c| and the product's rounding), plus
+    // 2^-40 |x| over the reference's last-bit roundings of 1 - ip / denom; a zero
+    // centroid (and padding) gets NaN: never taken, never lowers the bound min.
     const int c = blockIdx.x * 64 + threadIdx.x;
     float* cn2 = cconst;
     float* chunk = cconst + Kpad + 2 * blockIdx.x;
     double ec = 0.0, eb = 0.0;
     if (c >= K) {
         for (int j = 0; j < DP; j++) C32[(size_t)c * DP + j] = 0.f;
-        cn2[c] = __builtin_inff();
+        cn2[c] = metric ? __builtin_nanf("") : __builtin_inff();
     } else {
         double s = 0.0;
         for (int j = 0; j < d; j++) {
@@ -61,9 +66,23 @@ __global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kp
         for (int j = d; j < DP; j++) C32[(size_t)c * DP + j] = 0.f;
         const double up = 1.0 + 0x1p-18;
         const double nc = sqrt(s) * (1.0 + 0x1p-30);
-        cn2[c] = (float)s;
-        ec = 0x1p-24 * (2.0 * DP + 12.0) * nc * up;
-        eb = (0x1p-24 * 5.0 * s + 0x1p-40 * s) * up + 1e-30;
+        if (metric == 0) {
+            cn2[c] = (float)s;
+            ec = 0x1p-24 * (2.0 * DP + 12.0) * nc * up;
+            eb = (0x1p-24 * 5.0 * s + 0x1p-40 * s) * up + 1e-30;
+        } else {
+            // 1e-20 <= |c|^2 < 1e30 keeps the f32 chain clear of overflow and of
+            // flushed denormals beyond eb ((DP + 4) 2^-124 / |c| for products and
+            // c's entries, 2^-116 for x's); outside it,
+            // and for a zero centroid 0 (whose NaN the reference's sentinel takes
+            // for every row, assignment.hpp:66), eb = inf leaves no certificate
+            const bool ok = s >= 1e-20 && s < 1e30;
+            const double rc = ok ? 1.0 / sqrt(s) : 0.0;
+            cn2[c] = ok ? (float)rc : __builtin_nanf("");
+            ec = (0x1p-24 * (DP + 20.0) + 0x1p-40) * up;
+            eb = ok ? ((DP + 4.0) * 0x1p-124 * rc + 0x1p-116) * up
+                    : (s == 0.0 && c > 0 ? 0.0 : __builtin_inf());
+        }
     }
     for (int off = 32; off >= 1; off >>= 1) {
         ec = fmax(ec, __shfl_xor(ec, off));
@@ -77,12 +96,12 @@ __global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kp
 
 int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d, int DP, int metric,
                          float* C32, float* cconst) {
-    (void)metric;
-    hipLaunchKernelGGL(centroid_prep_kernel, dim3((Kpad + 63) / 64), dim3(64), 0, s, C, K, Kpad, d, DP, C32, cconst);
+    hipLaunchKernelGGL(centroid_prep_kernel, dim3((Kpad + 63) / 64), dim3(64), 0, s, C, K, Kpad, d, DP, metric, C32,
+                       cconst);
     return kstatus("assign.hip");
 }
 
-template <int DP>
+template <int DP, int MET>
 __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
     const float* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int Kpad,
     const float* __restrict__ C32, const float* __restrict__ cconst, int32_t* __restrict__ assign,
@@ -124,7 +143,10 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
     for (int s = 0; s < H; s++) xn2 = fma((double)b[s], (double)b[s], xn2);
     xn2 += __shfl_xor(xn2, 32);
     const float nx = (float)(sqrt(xn2) * (1.0 + 0x1p-30));
-    const float ex = (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30);
+    // cosine: |x| >= 1e18 may overflow the f32 products (|c| < 1e15 is checked
+    // in the prep): no certificate, the row goes to the exact pass
+    const float ex = MET == 0 ? (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30)
+                              : (xn2 < 1e36 ? 0.f : __builtin_inff());
     __syncthreads();   // LDS now reused for centroid chunks
 
     float L1 = __builtin_inff(), L2 = __builtin_inff(), U = __builtin_inff();
@@ -162,7 +184,7 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
                 const float cnv[4] = {cn.x, cn.y, cn.z, cn.w};
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const float sc = fmaf(-2.f, acc[4 * g + q], cnv[q]);
+                    const float sc = MET == 0 ? fmaf(-2.f, acc[4 * g + q], cnv[q]) : -acc[4 * g + q] * cnv[q];
                     const float lo = sc - E, hi = sc + E;
                     if (lo < L1) { L2 = L1; L1 = lo; i1 = c0 + cb + q; }
                     else if (lo < L2) L2 = lo;
@@ -186,6 +208,47 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
 
     // ---- exact-order distance of the certified winner: lanes h=0 sum dims
     // [0,H), hand the partial to lane h=1, which sums [H,2H) (j ascending).
+    if (MET == 1) {
+        // cosine (metric.hpp cosine distance, exact.h exact_cosine): the x87
+        // inner product and both squared-norm chains travel between the halves
+        sx80 ip = sx_zero();
+        double na = 0.0, nb = 0.0;
+        if (h == 0 && cert && valid) {
+            const double* crow = C + (size_t)ni1 * d;
+#pragma unroll
+            for (int s = 0; s < H; s++)
+                if (s < d) {
+                    const double xj = (double)b[s], cj = crow[s];
+                    ip = sx_add_double(ip, __dmul_rn(xj, cj));
+                    na = __dadd_rn(na, __dmul_rn(xj, xj));
+                    nb = __dadd_rn(nb, __dmul_rn(cj, cj));
+                }
+        }
+        const unsigned long long om = (unsigned long long)__shfl_xor((long long)ip.m, 32);
+        const int oe = __shfl_xor(ip.e, 32), os = __shfl_xor(ip.s, 32);
+        const double ona = __shfl_xor(na, 32), onb = __shfl_xor(nb, 32);
+        if (h == 1 && valid) {
+            if (cert) {
+                sx80 p; p.m = om; p.e = oe; p.s = os;
+                double a2 = ona, b2 = onb;
+                const double* crow = C + (size_t)ni1 * d;
+#pragma unroll
+                for (int s = 0; s < H; s++)
+                    if (H + s < d) {
+                        const double xj = (double)b[s], cj = crow[H + s];
+                        p = sx_add_double(p, __dmul_rn(xj, cj));
+                        a2 = __dadd_rn(a2, __dmul_rn(xj, xj));
+                        b2 = __dadd_rn(b2, __dmul_rn(cj, cj));
+                    }
+                assign[row] = ni1;
+                dist[row] = one_minus(x87_quot(p, __dmul_rn(sqrt(a2), sqrt(b2))));
+            } else {
+                const unsigned long long slot = atomicAdd(ambig_count, 1ull);
+                ambig[slot] = (int32_t)row;
+            }
+        }
+        return;
+    }
     double accd = 0.0;
     if (h == 0 && cert && valid) {
         const double* crow = C + (size_t)ni1 * d;
@@ -217,14 +280,16 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
 }
 
 int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, const double* C, int K,
-                       int Kpad, const float* C32, const float* cconst, int32_t* assign, double* dist,
+                       int Kpad, int metric, const float* C32, const float* cconst, int32_t* assign, double* dist,
                        int32_t* ambig, unsigned long long* ambig_count) {
     (void)K;
     if (N <= 0) return 0;
     const dim3 grid((unsigned)((N + AS_PB - 1) / AS_PB)), block(AS_THREADS);
     const size_t lds = (size_t)4 * 32 * (DP + 4) * 4;   // >= chunk (64*(DP+4) + 192) floats
-    switch (DP) {
-#define AS_CASE(V) case V: hipLaunchKernelGGL(assign_mfma_kernel<V>, grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break;
+    switch (DP * 2 + (metric ? 1 : 0)) {
+#define AS_CASE(V) \
+        case 2 * V: hipLaunchKernelGGL((assign_mfma_kernel<V, 0>), grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break; \
+        case 2 * V + 1: hipLaunchKernelGGL((assign_mfma_kernel<V, 1>), grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break;
         AS_CASE(16) AS_CASE(32) AS_CASE(64) AS_CASE(128) AS_CASE(256)
 #undef AS_CASE
         default: return -4;

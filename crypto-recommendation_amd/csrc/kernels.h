@@ -41,7 +41,7 @@ int assign_dp(int d);    // padded dimension used by the MFMA kernel (0 = unsupp
 int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d, int DP, int metric,
                          float* C32, float* cconst);
 int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, const double* C, int K,
-                       int Kpad, const float* C32, const float* cconst, int32_t* assign, double* dist,
+                       int Kpad, int metric, const float* C32, const float* cconst, int32_t* assign, double* dist,
                        int32_t* ambig, unsigned long long* ambig_count);
 int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K,
                         int metric, const int32_t* rows, const unsigned long long* row_count,

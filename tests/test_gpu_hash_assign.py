@@ -197,6 +197,47 @@ def test_assign_paths_agree(ctx, path, monkeypatch):
     assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
 
 
+@pytest.mark.parametrize("d,K,case", [(128, 256, "rows"), (100, 64, "rows"), (16, 1, "rows"), (256, 300, "scaled"),
+                                      (64, 40, "dups"), (32, 20, "zero_c0"), (32, 20, "zero_c5"),
+                                      (48, 30, "special")])
+def test_cosine_mfma_vs_exact(ctx, d, K, case, monkeypatch):
+    # cosine Lloyd: the certified f32-MFMA path (-x.c/|c| scores) must agree bit
+    # for bit with the exact all-centroid pass and with the oracle (assignment.hpp:52-75)
+    N = 20_011
+    X = ctx.synth(0xC05 + d, N, d)
+    rng = np.random.default_rng(d + K)
+    rows = rng.choice(N, K, replace=False).astype(np.int64)
+    Cc = X[to_dev(ctx, rows)].double()
+    if case == "scaled":
+        Cc = Cc * to_dev(ctx, rng.uniform(1e-3, 1e3, (K, 1)))    # |c| spread (cosine ignores it)
+    elif case == "dups":
+        Cc[1::3] = Cc[0::3][: Cc[1::3].shape[0]] * 2.0          # parallel centroids: exact ties
+        X[5::7] = X[5::7] * 0.0                                   # zero rows (NaN everywhere)
+    elif case == "zero_c0":
+        Cc[0] = 0.0                     # the sentinel takes centroid 0's NaN for every row
+    elif case == "zero_c5":
+        Cc[5] = 0.0                     # never taken
+    elif case == "special":
+        X[3, 2] = float("inf"); X[10, 0] = float("nan"); X[20] = 1e-41   # inf / nan / denormal rows
+        X[30] = X[30] * 1e19                                              # |x| past the f32 range guard
+        Cc[7, 1] = 1e-300; Cc[8] = Cc[8] * 1e-12                          # fp32-underflowing entry, tiny norm
+    ctx.reset_stats()
+    a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
+    amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG)
+    monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
+    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
+    assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
+    assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
+    sub = np.random.default_rng(7).choice(N, 1500, replace=False)
+    oa, od = oracle.lloyd_assign(X.cpu().numpy()[sub], Cc.cpu().numpy(), "cosine", None)
+    assert np.array_equal(a0.cpu().numpy()[sub], oa)
+    assert np.array_equal(d0.cpu().numpy()[sub].view(np.uint64), od.view(np.uint64))
+    if case in ("rows", "scaled"):
+        assert amb < 0.05 * N, amb      # the bound certifies the vast majority
+    if case == "zero_c0":
+        assert amb == N
+
+
 @pytest.mark.parametrize("N,K,L,k", [(1, 1, 1, 4), (65, 64, 8, 4), (4099, 300, 8, 4), (777, 256, 3, 3),
                                      (2048, 200, 2, 4), (1500, 256, 7, 2)])
 def test_hash_assign_shapes(ctx, N, K, L, k):
