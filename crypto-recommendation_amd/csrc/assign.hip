@@ -210,19 +210,22 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
     // [0,H), hand the partial to lane h=1, which sums [H,2H) (j ascending).
     if (MET == 1) {
         // cosine (metric.hpp cosine distance, exact.h exact_cosine): the x87
-        // inner product and both squared-norm chains travel between the halves
+        // inner product and both squared-norm chains travel between the halves.
+        // The row is re-read from memory (L2): a loop over b[] would not unroll
+        // around the soft-x87 adds and would move b[] to scratch.
         sx80 ip = sx_zero();
         double na = 0.0, nb = 0.0;
+        const float* xrow = X + row * d;
         if (h == 0 && cert && valid) {
             const double* crow = C + (size_t)ni1 * d;
-#pragma unroll
-            for (int s = 0; s < H; s++)
-                if (s < d) {
-                    const double xj = (double)b[s], cj = crow[s];
-                    ip = sx_add_double(ip, __dmul_rn(xj, cj));
-                    na = __dadd_rn(na, __dmul_rn(xj, xj));
-                    nb = __dadd_rn(nb, __dmul_rn(cj, cj));
-                }
+            const int e = min(H, d);
+#pragma unroll 1
+            for (int s = 0; s < e; s++) {
+                const double xj = (double)xrow[s], cj = crow[s];
+                ip = sx_add_double(ip, __dmul_rn(xj, cj));
+                na = __dadd_rn(na, __dmul_rn(xj, xj));
+                nb = __dadd_rn(nb, __dmul_rn(cj, cj));
+            }
         }
         const unsigned long long om = (unsigned long long)__shfl_xor((long long)ip.m, 32);
         const int oe = __shfl_xor(ip.e, 32), os = __shfl_xor(ip.s, 32);
@@ -232,14 +235,13 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
                 sx80 p; p.m = om; p.e = oe; p.s = os;
                 double a2 = ona, b2 = onb;
                 const double* crow = C + (size_t)ni1 * d;
-#pragma unroll
-                for (int s = 0; s < H; s++)
-                    if (H + s < d) {
-                        const double xj = (double)b[s], cj = crow[H + s];
-                        p = sx_add_double(p, __dmul_rn(xj, cj));
-                        a2 = __dadd_rn(a2, __dmul_rn(xj, xj));
-                        b2 = __dadd_rn(b2, __dmul_rn(cj, cj));
-                    }
+#pragma unroll 1
+                for (int j = H; j < d; j++) {
+                    const double xj = (double)xrow[j], cj = crow[j];
+                    p = sx_add_double(p, __dmul_rn(xj, cj));
+                    a2 = __dadd_rn(a2, __dmul_rn(xj, xj));
+                    b2 = __dadd_rn(b2, __dmul_rn(cj, cj));
+                }
                 assign[row] = ni1;
                 dist[row] = one_minus(x87_quot(p, __dmul_rn(sqrt(a2), sqrt(b2))));
             } else {
