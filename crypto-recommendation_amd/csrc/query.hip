@@ -228,26 +228,67 @@ __global__ void cq_qptr(const int64_t* __restrict__ slot_off, int64_t nq, int S,
         out_ptr[q] = slot_off[q * S];
 }
 
-__global__ __launch_bounds__(256) void cq_copy(const int32_t* __restrict__ qvert, int64_t nq,
-                                               const int32_t* __restrict__ masks, int S,
-                                               const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ idx,
-                                               const int64_t* __restrict__ slot_off, int32_t* __restrict__ out) {
-    // persistent waves over the (query, probe) slots: a launch of one wave per
-    // slot spent more time in block dispatch than in the copy
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    for (int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < nq * S; e += nw) {
+// Per-slot source offset idx position of the slot's bucket, written over the
+// sizes array once the scan has consumed it.
+__global__ void cq_beg(const int32_t* __restrict__ qvert, int64_t nq, const int32_t* __restrict__ masks, int S,
+                       const int64_t* __restrict__ row_ptr, int64_t* __restrict__ beg) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq * S; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t q = e / S;
-        const int64_t v = qvert[q] ^ masks[e - q * S];
-        const int64_t beg = row_ptr[v], n = row_ptr[v + 1] - beg, dst = slot_off[e];
-        // 8 loads in flight per lane before the stores (a bucket is ~N / 2^k rows)
-        for (int64_t p = lane; p < n; p += 512) {
-            int32_t w[8];
+        beg[e] = row_ptr[qvert[q] ^ masks[e - q * S]];
+    }
+}
+
+// Last s in [0, hi] with a[s] <= x (a non-decreasing, a[0] <= x): a 64-ary
+// search, one probe per lane per round (log64 of the slot count rounds of
+// L2-resident loads), wave-uniform result.
+__device__ inline int64_t last_le64(const int64_t* __restrict__ a, int64_t hi, int64_t x, int lane) {
+    int64_t lo = 0;
+    while (hi - lo >= 64) {
+        const int64_t step = (hi - lo + 62) / 63;            // lo + 63 step >= hi
+        const int64_t pj = min(lo + (int64_t)lane * step, hi);
+        const unsigned long long b = __ballot(a[pj] <= x);   // a prefix of the lanes
+        const int m = __popcll(b);                           // >= 1 (lane 0 probes lo)
+        const int64_t nlo = min(lo + (int64_t)(m - 1) * step, hi);
+        hi = m < 64 ? min(lo + (int64_t)m * step, hi) - 1 : hi;
+        lo = nlo;
+    }
+    const unsigned long long b = __ballot(lo + lane <= hi && a[min(lo + lane, hi)] <= x);
+    return lo + __popcll(b) - 1;
+}
+
+// Load-balanced copy: waves own contiguous CQ_CH-element chunks of the OUTPUT
+// (not slots), so a skewed bucket-size distribution (a few huge vertices)
+// spreads over every CU. A chunk finds its first slot by the 64-ary search and
+// walks the slots it spans; within a slot the lanes copy 512 elements per
+// round with 8 loads in flight, stores contiguous.
+constexpr int64_t CQ_CH = 4096;
+__global__ __launch_bounds__(256) void cq_copy(const int64_t* __restrict__ slot_off, int64_t slots,
+                                               const int64_t* __restrict__ beg, const int32_t* __restrict__ idx,
+                                               int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t total = slot_off[slots];
+    const int64_t nch = (total + CQ_CH - 1) / CQ_CH;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nch; c += nw) {
+        int64_t p = c * CQ_CH;
+        const int64_t oe = min(p + CQ_CH, total);
+        int64_t s = last_le64(slot_off, slots, p, lane);     // slot_off[s] <= p < slot_off[s + 1]
+        int64_t so = slot_off[s];
+        while (p < oe) {
+            const int64_t send = slot_off[s + 1];
+            const int64_t stop = min(send, oe);
+            const int32_t* src = idx + (beg[s] - so);        // output i <- idx[beg[s] + i - slot_off[s]]
+            for (int64_t i = p + lane; i < stop; i += 512) {
+                int32_t w[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) w[u] = p + 64 * u < n ? idx[beg + p + 64 * u] : 0;
+                for (int u = 0; u < 8; u++) w[u] = i + 64 * u < stop ? src[i + 64 * u] : 0;
 #pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (p + 64 * u < n) out[dst + p + 64 * u] = w[u];
+                for (int u = 0; u < 8; u++)
+                    if (i + 64 * u < stop) out[i + 64 * u] = w[u];
+            }
+            p = stop;
+            so = send;
+            s++;
         }
     }
 }
@@ -261,9 +302,12 @@ int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int
     if (launch_scan_i64(s, sizes, slots, slot_off, scan_ws)) return -2;
     hipLaunchKernelGGL(cq_qptr, dim3((unsigned)std::min<int64_t>((nq + 256) / 256, 4096)), dim3(256), 0, s, slot_off, nq, S,
                        out_ptr);
-    if (out)
-        hipLaunchKernelGGL(cq_copy, dim3((unsigned)std::min<int64_t>((slots + 3) / 4, 4096)), dim3(256), 0, s, qvert, nq, masks, S, row_ptr, idx,
-                           slot_off, out);
+    if (out) {
+        // sizes[] is dead after the scan: it now holds each slot's bucket start
+        hipLaunchKernelGGL(cq_beg, dim3((unsigned)std::min<int64_t>((slots + 255) / 256, 4096)), dim3(256), 0, s, qvert, nq,
+                           masks, S, row_ptr, sizes);
+        hipLaunchKernelGGL(cq_copy, dim3(2048), dim3(256), 0, s, slot_off, slots, sizes, idx, out);
+    }
     return kstatus("query.hip");
 }
 

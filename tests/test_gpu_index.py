@@ -274,3 +274,29 @@ def test_queries_large_batches_multiblock_scan(ctx):
     for q in np.random.default_rng(3).choice(30_000, 100, replace=False):
         exp = oracle.lsh_query(N, N // 100, orp, oidx, qb[q])
         assert np.array_equal(out2[ptr2[q]:ptr2[q + 1]], exp), q
+
+
+@pytest.mark.parametrize("k,w", [(14, 2.0), (10, 40.0)])
+def test_cube_query_load_balanced_copy_full(ctx, k, w):
+    # every output element checked (vectorised): k = 14 leaves most slots tiny
+    # (a chunk spans many slots, some empty); w = 40 puts
+    # most rows in a few huge vertices (slots far larger than a chunk)
+    N, d = 200_000, 32
+    X = ctx.synth(43, N, d)
+    V, t, st = lshkm.params_cube_euclidean(7, k, d, w)
+    cube = lshkm.Cube(ctx, "euclidean", d, k, w, V=V, t=t, rng_state=st)
+    cube.build(X)
+    nq, probes = 20_000, k
+    rows = np.random.default_rng(4).choice(N, nq, replace=False)
+    Q = X[to_dev(ctx, rows.astype(np.int64))]
+    ptr, out = cube.query(Q, probes)
+    rp, bidx = cube.buckets()
+    qv = cube.vertices(Q).cpu().numpy()
+    seqs = np.array([oracle.cube_probe_seq(int(v), probes, k) for v in qv], np.int64)   # [nq, S]
+    sz = (rp[seqs + 1] - rp[seqs]).ravel()
+    slot_off = np.zeros(sz.size + 1, np.int64)
+    slot_off[1:] = np.cumsum(sz)
+    assert np.array_equal(ptr, slot_off[::seqs.shape[1]])
+    assert sz.max() > 4096 or np.median(sz) < 64            # the regime each case is for
+    src = np.repeat(rp[seqs.ravel()] - slot_off[:-1], sz) + np.arange(slot_off[-1], dtype=np.int64)
+    assert np.array_equal(out, bidx[src])
