@@ -498,15 +498,18 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * DP * 4)) || (rc = ctx->ws_cconst.reserve((size_t)3 * Kpad * 4)) ||
-            (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 4)) ||
+            (rc = ctx->ws_ambig.reserve((size_t)std::max<int64_t>(N, 1) * 2 * 4)) ||   // ambiguous rows | cosine fix-ups
             (rc = ctx->ws_counter.reserve(64)))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
-        LSHKM_HIP(hipMemsetAsync(cnt, 0, 8, s));
+        LSHKM_HIP(hipMemsetAsync(cnt, 0, 16, s));
         if ((rc = launch_centroid_prep(s, C, K, Kpad, d, DP, metric, (float*)ctx->ws_c32.p, (float*)ctx->ws_cconst.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_assign_mfma(s, X, N, d, DP, C, K, Kpad, metric, (const float*)ctx->ws_c32.p, (const float*)ctx->ws_cconst.p,
                                      assign, dist, (int32_t*)ctx->ws_ambig.p, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if (metric != LSHKM_METRIC_EUCLIDEAN &&
+            (rc = launch_cos_fix(s, X, N, d, C, (const int32_t*)ctx->ws_ambig.p + N, cnt + 1, assign, dist) ||
+             launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1))) { LSHKM_LAUNCH_CHECK(); return rc; }
         // ambiguous-count statistic
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
     } else {

@@ -209,45 +209,30 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
     // ---- exact-order distance of the certified winner: lanes h=0 sum dims
     // [0,H), hand the partial to lane h=1, which sums [H,2H) (j ascending).
     if (MET == 1) {
-        // cosine (metric.hpp cosine distance, exact.h exact_cosine): the x87
-        // inner product and both squared-norm chains travel between the halves.
-        // The row is re-read from memory (L2): a loop over b[] would not unroll
-        // around the soft-x87 adds and would move b[] to scratch.
-        sx80 ip = sx_zero();
-        double na = 0.0, nb = 0.0;
-        const float* xrow = X + row * d;
-        if (h == 0 && cert && valid) {
-            const double* crow = C + (size_t)ni1 * d;
-            const int e = min(H, d);
-#pragma unroll 1
-            for (int s = 0; s < e; s++) {
-                const double xj = (double)xrow[s], cj = crow[s];
-                ip = sx_add_double(ip, __dmul_rn(xj, cj));
-                na = __dadd_rn(na, __dmul_rn(xj, xj));
-                nb = __dadd_rn(nb, __dmul_rn(cj, cj));
-            }
-        }
-        const unsigned long long om = (unsigned long long)__shfl_xor((long long)ip.m, 32);
-        const int oe = __shfl_xor(ip.e, 32), os = __shfl_xor(ip.s, 32);
-        const double ona = __shfl_xor(na, 32), onb = __shfl_xor(nb, 32);
+        // cosine (metric.hpp cosine distance): exact.h's certified fast form,
+        // soft-x87 for the rows it cannot certify
+        // soft-x87 for the rows it cannot certify, listed (after the ambiguous
+        // rows' half of the list) for cos_fix_kernel: inline, one failing lane
+        // would make its whole wave pay the soft chain
+        bool fix = false;
         if (h == 1 && valid) {
             if (cert) {
-                sx80 p; p.m = om; p.e = oe; p.s = os;
-                double a2 = ona, b2 = onb;
-                const double* crow = C + (size_t)ni1 * d;
-#pragma unroll 1
-                for (int j = H; j < d; j++) {
-                    const double xj = (double)xrow[j], cj = crow[j];
-                    p = sx_add_double(p, __dmul_rn(xj, cj));
-                    a2 = __dadd_rn(a2, __dmul_rn(xj, xj));
-                    b2 = __dadd_rn(b2, __dmul_rn(cj, cj));
-                }
                 assign[row] = ni1;
-                dist[row] = one_minus(x87_quot(p, __dmul_rn(sqrt(a2), sqrt(b2))));
+                double v;
+                if (cosine_fast(X + row * d, C + (size_t)ni1 * d, d, v)) dist[row] = v;
+                else fix = true;
             } else {
                 const unsigned long long slot = atomicAdd(ambig_count, 1ull);
                 ambig[slot] = (int32_t)row;
             }
+        }
+        const unsigned long long fb = __ballot(fix);
+        if (fb) {
+            const int leader = __builtin_ctzll(fb);
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(ambig_count + 1, (unsigned long long)__popcll(fb));
+            base = __shfl(base, leader);
+            if (fix) ambig[N + base + __popcll(fb & ((1ull << lane) - 1ull))] = (int32_t)row;
         }
         return;
     }
@@ -299,7 +284,29 @@ int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, 
     return kstatus("assign.hip");
 }
 
+// Certified cosine winners whose distance IpAcc could not certify: one lane
+// per listed row, the soft-x87 chain (exact.h exact_cosine_x87).
+__global__ __launch_bounds__(256) void cos_fix_kernel(const float* __restrict__ X, int d, const double* __restrict__ C,
+                                                      const int32_t* __restrict__ rows,
+                                                      const unsigned long long* __restrict__ count,
+                                                      const int32_t* __restrict__ assign, double* __restrict__ dist) {
+    const int64_t n = (int64_t)*count;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int64_t row = rows[i];
+        dist[row] = exact_cosine_x87(X + row * d, C + (size_t)assign[row] * d, d);
+    }
+}
+
+int launch_cos_fix(hipStream_t s, const float* X, int64_t N, int d, const double* C, const int32_t* rows,
+                   const unsigned long long* count, const int32_t* assign, double* dist) {
+    if (N <= 0) return 0;
+    hipLaunchKernelGGL(cos_fix_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 2048)), dim3(256), 0, s, X, d, C,
+                       rows, count, assign, dist);
+    return kstatus("assign.hip");
+}
+
 // ---------------------------------------------------------------- exact pass
+constexpr int XC_MAXV = 4;   // cosine candidate form: K <= 256 (values kept per lane)
 // One wave per listed row; lane c evaluates centroids c, c+64, ... in the
 // reference's exact order (exact.h); the first minimum wins.
 __global__ __launch_bounds__(256) void assign_exact_kernel(
@@ -315,6 +322,48 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
         const int64_t row = rows ? rows[it] : it;
         const float* x = X + row * d;
         double best = 0.0; int bi = -1;
+        if (metric == 1 && K <= 64 * XC_MAXV) {
+            // cosine: certified values (exact.h cosine_interval) for every
+            // centroid, the soft-x87 chain only for those whose interval can
+            // still reach the minimum; a row with an unknown value (zero
+            // vectors, NaN/inf, extreme ranges) takes the full soft pass below
+            double v[XC_MAXV], rad[XC_MAXV];
+            int st[XC_MAXV];
+            double U = __builtin_inf();
+            bool unknown = false;
+#pragma unroll
+            for (int k = 0; k < XC_MAXV; k++) {
+                const int c = lane + 64 * k;
+                st[k] = 0; v[k] = 0.0; rad[k] = 0.0;
+                if (c < K) {
+                    st[k] = cosine_interval(x, C + (size_t)c * d, d, v[k], rad[k]);
+                    unknown |= st[k] == 2;
+                    if (st[k] != 2) U = fmin(U, v[k] + rad[k]);
+                }
+            }
+            if (!__ballot(unknown)) {
+                for (int off = 32; off >= 1; off >>= 1) U = fmin(U, __shfl_xor(U, off));
+#pragma unroll
+                for (int k = 0; k < XC_MAXV; k++) {
+                    const int c = lane + 64 * k;
+                    if (c < K && v[k] - rad[k] <= U) {     // non-candidates are strictly above the minimum
+                        const double dd = st[k] == 0 ? v[k] : exact_cosine_x87(x, C + (size_t)c * d, d);
+                        if (bi < 0 || dd < best) { best = dd; bi = c; }
+                    }
+                }
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const double ob = __shfl_xor(best, off);
+                    const int oi = __shfl_xor(bi, off);
+                    const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
+                    if (take) { best = ob; bi = oi; }
+                }
+                if (lane == 0) {
+                    assign[row] = bi;
+                    dist[row] = best;
+                }
+                continue;
+            }
+        }
         for (int c = lane; c < K; c += 64) {
             const double dd = metric == 0 ? exact_euclid(x, C + (size_t)c * d, d) : exact_cosine(x, C + (size_t)c * d, d);
             // assignment.hpp:66: the -1 sentinel takes centroid 0's distance even

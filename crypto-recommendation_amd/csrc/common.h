@@ -56,6 +56,7 @@ enum Stat {
     STAT_ASSIGN_AMBIG = 1,   // points whose argmin the MFMA bound could not certify
     STAT_KPP_CHUNKS = 2,     // k-means++ prefix-walk chunks (KPP_CHUNK rows each) ...
     STAT_KPP_SEQ = 3,        // ... of which summed element by element (binade crossings, ties)
+    STAT_COS_FIX = 4,        // cosine Lloyd winners whose distance took the soft-x87 chain
     STAT_COUNT = 8
 };
 

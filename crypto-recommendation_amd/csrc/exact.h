@@ -33,17 +33,116 @@ __device__ inline double x87_quot(sx80 ip, double denom) {
 // 1 - q as SSE subsd computes it: a NaN q comes back unchanged.
 __device__ inline double one_minus(double q) { return q != q ? q : __dsub_rn(1.0, q); }
 
-__device__ inline double exact_cosine(const float* __restrict__ x, const double* __restrict__ c, int d) {
+// The soft-x87 form: every inner-product add emulated (~150 integer ops each).
+template <typename T, typename U>
+__device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __restrict__ c, int d) {
     sx80 ip = sx_zero();
     double a = 0.0, b = 0.0;
     for (int j = 0; j < d; j++) {
-        const double xj = (double)x[j];
-        ip = sx_add_double(ip, __dmul_rn(xj, c[j]));
+        const double xj = (double)x[j], cj = (double)c[j];
+        ip = sx_add_double(ip, __dmul_rn(xj, cj));
         a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(c[j], c[j]));
+        b = __dadd_rn(b, __dmul_rn(cj, cj));
     }
-    const double denom = __dmul_rn(sqrt(a), sqrt(b));
-    return one_minus(x87_quot(ip, denom));
+    return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
+}
+
+// Certified fast form of the x87 inner product's quotient (~12 fp64 ops per
+// element instead of a soft-x87 add). The products p_j are the reference's
+// doubles; their sum is carried exactly enough as a double-double (TwoSum),
+// and the x87 chain's own roundings are bounded: each add rounds to 64 bits,
+// |err_k| <= 2^-64 |s_k|, so |ip87 - sum p| <= 2^-64 (1 + 2^-30) sum_k |S_k|
+// (ts below; the partial sums' low parts and second-order terms sit far inside
+// the 2^-30). With y = sum p / denom as yh + yl and R bounding ip87 / denom's
+// distance from it plus FDIV's own 64-bit rounding, double(FDIV result) == yh
+// whenever [yh + yl - R, yh + yl + R] lies strictly between yh's two
+// neighbouring rounding midpoints. quot() returns false (the caller takes the
+// soft-x87 form) when that fails (a few % of random rows) or any quantity is
+// outside the ranges the bound assumes (zero vectors, NaN/inf, 2^+-800).
+struct IpAcc {
+    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0;
+    __device__ inline void add(double p) {
+        const double s = __dadd_rn(sh, p);
+        const double bb = __dsub_rn(s, sh);
+        const double e = __dadd_rn(__dsub_rn(sh, __dsub_rn(s, bb)), __dsub_rn(p, bb));   // TwoSum: sh + p = s + e
+        sh = s;
+        sl = __dadd_rn(sl, e);
+        ts = __dadd_rn(ts, fabs(s));
+        mx = fmax(mx, fabs(s));
+    }
+    // double(ip87 / (long double)denom): 0 = certified (q exact), 1 = not
+    // certified but |q - double(ip87 / denom)| <= qrad, 2 = declined (a quantity
+    // outside the ranges the bound assumes; q meaningless)
+    __device__ inline int quot_status(double denom, double& q, double& qrad) const {
+        if (!(denom >= 0x1p-800 && denom < 0x1p800 && mx >= 0x1p-800 && mx < 0x1p800 && ts < 0x1p800)) return 2;
+        const double yh = sh / denom;
+        const double r = fma(-yh, denom, sh);              // exact remainder
+        const double yl = __dadd_rn(r, sl) / denom;
+        const double ay = fabs(yh);
+        if (!(ay >= 0x1p-800 && ay < 0x1p800)) return 2;
+        const double R = (__dadd_rn(ts * (0x1p-64 * (1.0 + 0x1p-30)), mx * 0x1p-88) / denom + fabs(yl) * 0x1p-51 +
+                          ay * 0x1p-63) * (1.0 + 0x1p-20);
+        const long long bits = __double_as_longlong(ay);
+        const double up = __dsub_rn(__longlong_as_double(bits + 1), ay);   // ulp above |yh|
+        const double dn = __dsub_rn(ay, __longlong_as_double(bits - 1));   // ulp below (half at a power of 2)
+        const double dl = yh < 0.0 ? -yl : yl;
+        q = yh;
+        qrad = 0.0;
+        if (!(__dadd_rn(dl, R) < 0.5 * up && __dsub_rn(dl, R) > -0.5 * dn)) {
+            qrad = (R + fabs(yl) + 4.0 * up) * (1.0 + 0x1p-20);   // + the final double rounding
+            return 1;
+        }
+        return 0;
+    }
+    __device__ inline bool quot(double denom, double& q) const {
+        double qr;
+        return quot_status(denom, q, qr) == 0;
+    }
+};
+
+// Cosine distance with its certificate status (IpAcc::quot_status): 0 = v is
+// the reference's value, 1 = the reference's value lies within v +- rad,
+// 2 = unknown.
+template <typename T, typename U>
+__device__ inline int cosine_interval(const T* __restrict__ x, const U* __restrict__ c, int d, double& v, double& rad) {
+    IpAcc ip;
+    double a = 0.0, b = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j], cj = (double)c[j];
+        ip.add(__dmul_rn(xj, cj));
+        a = __dadd_rn(a, __dmul_rn(xj, xj));
+        b = __dadd_rn(b, __dmul_rn(cj, cj));
+    }
+    double q = 0.0, qr = 0.0;
+    const int st = ip.quot_status(__dmul_rn(sqrt(a), sqrt(b)), q, qr);
+    v = __dsub_rn(1.0, q);
+    rad = st == 1 ? qr + 0x1p-50 : 0.0;      // + both roundings of 1 - q (|1 - q| < 4)
+    return st;
+}
+
+template <typename T, typename U>
+__device__ inline bool cosine_fast(const T* __restrict__ x, const U* __restrict__ c, int d, double& out) {
+    IpAcc ip;
+    double a = 0.0, b = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j], cj = (double)c[j];
+        ip.add(__dmul_rn(xj, cj));
+        a = __dadd_rn(a, __dmul_rn(xj, xj));
+        b = __dadd_rn(b, __dmul_rn(cj, cj));
+    }
+    double q;
+    if (!ip.quot(__dmul_rn(sqrt(a), sqrt(b)), q)) return false;
+    out = __dsub_rn(1.0, q);
+    return true;
+}
+
+// Paths where lanes evaluate different pairs take the soft form directly: a
+// wave pays the soft chain if any one lane's certificate fails (~14% of random
+// pairs, mostly near-orthogonal ones), so fast + fallback inline is slower.
+// The Lloyd winner path (assign.hip) lists its failures for a lane-per-row pass.
+template <typename T, typename U>
+__device__ inline double exact_cosine(const T* __restrict__ x, const U* __restrict__ c, int d) {
+    return exact_cosine_x87(x, c, d);
 }
 
 // Either metric, `this` = x of any real type (fp32 dataset rows, fp64
@@ -58,15 +157,7 @@ __device__ inline double exact_dist(const T* __restrict__ x, const U* __restrict
         }
         return sqrt(acc);
     }
-    sx80 ip = sx_zero();
-    double a = 0.0, b = 0.0;
-    for (int j = 0; j < d; j++) {
-        const double xj = (double)x[j], cj = (double)c[j];
-        ip = sx_add_double(ip, __dmul_rn(xj, cj));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(cj, cj));
-    }
-    return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
+    return exact_cosine(x, c, d);
 }
 
 // x86 SSE produces one NaN from non-NaN operands: the default NaN, sign set

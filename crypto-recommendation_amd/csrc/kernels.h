@@ -43,6 +43,10 @@ int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d,
 int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, const double* C, int K,
                        int Kpad, int metric, const float* C32, const float* cconst, int32_t* assign, double* dist,
                        int32_t* ambig, unsigned long long* ambig_count);
+// Lloyd cosine winners whose distance the certified form declined (list at
+// rows[0..*count), written by assign_mfma_kernel<., 1>): soft-x87 distances.
+int launch_cos_fix(hipStream_t s, const float* X, int64_t N, int d, const double* C, const int32_t* rows,
+                   const unsigned long long* count, const int32_t* assign, double* dist);
 int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K,
                         int metric, const int32_t* rows, const unsigned long long* row_count,
                         int64_t max_rows, int32_t* assign, double* dist);

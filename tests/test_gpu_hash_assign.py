@@ -319,3 +319,36 @@ def test_pruned_exact_pass(ctx, case, monkeypatch):
     oa, od = oracle.lloyd_assign(Xh[sub], Ch, "euclidean", None)
     assert np.array_equal(a.cpu().numpy()[sub], oa)
     np.testing.assert_allclose(dist.cpu().numpy()[sub], od, rtol=1e-14, atol=0)
+
+
+@pytest.mark.parametrize("case", ["near_parallel", "near_orthogonal", "cancelling"])
+def test_cosine_certified_quotient_adversarial(ctx, case, monkeypatch):
+    # exact.h IpAcc: the double-double inner product with the bounded x87
+    # rounding must give the soft-x87 bits or decline; every row is checked
+    # against the oracle (real long double) on both assignment paths
+    N, d, K = 3001, 64, 12
+    rng = np.random.default_rng(11)
+    Xh = ctx.synth(0xADD, N, d).cpu().numpy().astype(np.float64)
+    if case == "near_parallel":          # q = 1 - O(2^-20): 1 - q keeps few bits
+        base = Xh[rng.choice(N, K, replace=False)]
+        Ch = base * (1.0 + rng.uniform(-2.0**-20, 2.0**-20, base.shape))
+        Xh[:K * 50] = np.repeat(base, 50, axis=0).astype(np.float32)
+    elif case == "near_orthogonal":      # x.c ~ 0: |S| << sum|S_k|
+        Ch = rng.standard_normal((K, d))
+        for i in range(K):
+            v = Xh[i * 7]
+            Ch[i] -= v * (Ch[i] @ v) / (v @ v)
+    else:                                # large terms that cancel
+        Ch = rng.standard_normal((K, d))
+        Ch[:, 0] = 1e8
+        Ch[:, 1] = -1e8
+        Xh[:, 1] = Xh[:, 0]
+    X = to_dev(ctx, Xh.astype(np.float32))
+    Cc = to_dev(ctx, np.ascontiguousarray(Ch))
+    a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
+    monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
+    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
+    oa, od = oracle.lloyd_assign(X.cpu().numpy(), Ch, "cosine", None)
+    for a, dd in ((a0, d0), (a1, d1)):
+        assert np.array_equal(a.cpu().numpy(), oa)
+        assert np.array_equal(dd.cpu().numpy().view(np.uint64), od.view(np.uint64))
