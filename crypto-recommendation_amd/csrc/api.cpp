@@ -416,14 +416,18 @@ int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, in
 // ------------------------------------------------------------------- Lloyd
 }  // extern "C"
 
-// Kernel path for assignment: euclidean takes the split-f16 fused kernel
-// (d = 128), else the f32-MFMA kernel (d <= 256), else the exact pass; cosine
-// takes the f32-MFMA kernel (certified -x.c/|c| scores) for d <= 256.
+// Kernel path for assignment: d = 128 takes the split-f16 fused kernel
+// (euclidean any K; cosine K <= 256: normalised centroids, its persistent
+// form), else the f32-MFMA kernel (d <= 256), else the exact pass.
 // LSHKM_ASSIGN_PATH = "f32" / "exact" forces a path (tests compare them).
-static int assign_path(int metric, int d) {
+static int assign_path(int metric, int d, int K) {
     const char* e = getenv("LSHKM_ASSIGN_PATH");
     if (e && !strcmp(e, "exact")) return 2;
-    if (metric == LSHKM_METRIC_EUCLIDEAN && d == 128 && !(e && !strcmp(e, "f32"))) return 0;
+    const bool f32 = e && !strcmp(e, "f32");
+    if (d == 128 && !f32 && (metric == LSHKM_METRIC_EUCLIDEAN || K <= 256)) {
+        const char* ff = getenv("LSHKM_FUSED_FORM");
+        if (metric == LSHKM_METRIC_EUCLIDEAN || !(ff && !strcmp(ff, "chunked"))) return 0;
+    }
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
@@ -433,8 +437,9 @@ static int exact_listed(lshkm_ctx ctx, const float* X, int d, const double* C, i
                         const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist,
                         const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0) {
     const int32_t* rows = (const int32_t*)ctx->ws_ambig.p;
-    if (!seg_counts && (metric != LSHKM_METRIC_EUCLIDEAN || d > 256))
-        return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist);
+    if (metric != LSHKM_METRIC_EUCLIDEAN || (!seg_counts && d > 256))
+        return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist, seg_counts,
+                                   seg_rows, nseg);
     int rc;
     if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 255) / 256 * 256) * 8))) return rc;
     // K <= 256: score every centroid in f32 first and run the exact order only on
@@ -452,8 +457,8 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
                        int32_t* phi, int32_t* bucket) {
     hipStream_t s = ctx->stream;
     const int DP = assign_dp(d);
-    const int path = assign_path(metric, d);
-    const bool fuse_hash = lsh && path == 0 && lsh->proj.fused_ok;
+    const int path = assign_path(metric, d, K);
+    const bool fuse_hash = lsh && path == 0 && metric == LSHKM_METRIC_EUCLIDEAN && lsh->proj.fused_ok;
     int rc;
     if (lsh && !fuse_hash && (rc = launch_proj_hash(s, lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE,
                                                     X, N, lsh->proj.params(lsh->nb),
@@ -461,10 +466,12 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
                                                     (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
     if (path == 0) {
         const int Kpad = (K + 63) / 64 * 64;
-        if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) || (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4)) ||
+        const bool cosine = metric != LSHKM_METRIC_EUCLIDEAN;
+        if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) ||
+            (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4 + (size_t)Kpad * 8)) ||
             (rc = ctx->ws_ambig.reserve((size_t)(N + FUSED_LIST_SLACK) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
             (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)) ||
-            (fuse_hash && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8))) ||
+            ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8))) ||
             (fuse_hash && !tuples && (rc = ctx->ws_tuples.reserve((size_t)std::max<int64_t>(N, 1) * lsh->proj.LK * 4))))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
@@ -473,7 +480,8 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         _Float16* Cl = Ch + (size_t)Kpad * 128;
         float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
         float* cnh = cbound + 8;
-        if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        double* nbv = (double*)(cnh + Kpad);               // cosine: [Kpad] sequential |c|^2 (Kpad % 64 == 0: aligned)
+        if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv))) { LSHKM_LAUNCH_CHECK(); return rc; }
         FusedLaunch f;
         f.X = X; f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C; f.Kpad = Kpad;
         f.assign = assign; f.dist = dist; f.ambig = (int32_t*)ctx->ws_ambig.p; f.ambig_count = cnt;
@@ -481,6 +489,10 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         f.list_cap = N + FUSED_LIST_SLACK;
         f.seg_counts = (int32_t*)ctx->ws_seg.p;
         f.seg_cap = FUSED_MAX_SEGS;
+        if (cosine) {
+            f.metric = 1; f.nbv = nbv;
+            f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
+        }
         if (fuse_hash) {
             const ProjTable& pj = lsh->proj;
             f.Vh = pj.vh_d.as<_Float16>(); f.Vl = pj.vl_d.as<_Float16>(); f.PT = pj.PT_d.as<double>();
@@ -495,6 +507,8 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.seg_counts : nullptr,
                                f.seg_rows, f.nseg))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if (cosine && ((rc = launch_cos_fix_seg(s, X, C, f.hfix, f.seg_counts, f.seg_rows, f.nseg, assign, dist)) ||
+                       (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1)))) { LSHKM_LAUNCH_CHECK(); return rc; }
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * DP * 4)) || (rc = ctx->ws_cconst.reserve((size_t)3 * Kpad * 4)) ||

@@ -307,16 +307,25 @@ int launch_cos_fix(hipStream_t s, const float* X, int64_t N, int d, const double
 
 // ---------------------------------------------------------------- exact pass
 constexpr int XC_MAXV = 4;   // cosine candidate form: K <= 256 (values kept per lane)
+constexpr int XE_SPLIT = 2;  // blocks per list segment (segmented form)
 // One wave per listed row; lane c evaluates centroids c, c+64, ... in the
 // reference's exact order (exact.h); the first minimum wins.
 __global__ __launch_bounds__(256) void assign_exact_kernel(
     const float* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int K, int metric,
     const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,
-    int32_t* __restrict__ assign, double* __restrict__ dist) {
+    int32_t* __restrict__ assign, double* __restrict__ dist, const int32_t* __restrict__ seg_counts,
+    int64_t seg_rows) {
     const int lane = threadIdx.x & 63;
-    const int64_t wglobal = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t nw = (int64_t)gridDim.x * 4;
+    int64_t wglobal = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int64_t nw = (int64_t)gridDim.x * 4;
     int64_t total = rows ? (int64_t)*row_count : N;
+    if (seg_counts) {            // XE_SPLIT blocks per segment of the persistent fused form's list
+        const int seg = blockIdx.x / XE_SPLIT;
+        rows += (int64_t)seg * seg_rows;
+        total = seg_counts[2 * seg];
+        wglobal = (int64_t)(blockIdx.x % XE_SPLIT) * 4 + (threadIdx.x >> 6);
+        nw = XE_SPLIT * 4;
+    }
     if (total > max_rows) total = max_rows;
     for (int64_t it = wglobal; it < total; it += nw) {
         const int64_t row = rows ? rows[it] : it;
@@ -387,13 +396,14 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
 
 int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K, int metric,
                         const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
-                        int32_t* assign, double* dist) {
+                        int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
     if (max_rows <= 0) return 0;
     // rows == NULL: every row (fallback path); else a device-counted list that is
     // usually ~0.3% of the rows: one block per CU, waves loop over the list.
-    const int64_t blocks = std::min<int64_t>((max_rows + 3) / 4, rows ? 256 : 2048);
+    const int64_t blocks = seg_counts ? (int64_t)nseg * XE_SPLIT : std::min<int64_t>((max_rows + 3) / 4, rows ? 256 : 2048);
+    if (blocks <= 0) return 0;
     hipLaunchKernelGGL(assign_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, N, d, C, K, metric,
-                       rows, row_count, max_rows, assign, dist);
+                       rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
     return kstatus("assign.hip");
 }
 

@@ -136,6 +136,23 @@ __device__ inline bool cosine_fast(const T* __restrict__ x, const U* __restrict_
     return true;
 }
 
+// The same with the centroid's sequential sum of squares given (nbv, computed
+// once per centroid in the reference's order).
+template <typename T, typename U>
+__device__ inline bool cosine_fast_nb(const T* __restrict__ x, const U* __restrict__ c, int d, double nbv, double& out) {
+    IpAcc ip;
+    double a = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j];
+        ip.add(__dmul_rn(xj, (double)c[j]));
+        a = __dadd_rn(a, __dmul_rn(xj, xj));
+    }
+    double q;
+    if (!ip.quot(__dmul_rn(sqrt(a), sqrt(nbv)), q)) return false;
+    out = __dsub_rn(1.0, q);
+    return true;
+}
+
 // Paths where lanes evaluate different pairs take the soft form directly: a
 // wave pays the soft chain if any one lane's certificate fails (~14% of random
 // pairs, mostly near-orthogonal ones), so fast + fallback inline is slower.

@@ -37,6 +37,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "softx87.h"
+#include "exact.h"
 
 namespace lshkm {
 
@@ -120,6 +121,7 @@ struct FusedArgs {
     int64_t seg_rows;
     int32_t* seg_counts;
     BucketDiv bdiv;          // phi % nb by multiply-high
+    const double* nbv;       // cosine: [K] sequential sum of c_j^2 (cust_vector.hpp:139-155)
     unsigned long long* prof;        // LSHKM_PHASE_TIMING builds only: per-phase wave cycles
 };
 
@@ -597,7 +599,9 @@ __host__ __device__ constexpr int fp_lds_bytes(int Kpad, bool hash) {
 }
 static_assert(fp_lds_bytes(FP_KMAX, true) <= 160 * 1024, "persistent LDS image exceeds 160 KiB");
 
-template <bool HASH>
+// MET = 1: cosine Lloyd (HASH = false): centroids are normalised in the prep
+// (score x.c/|c|, cnh = 0), the winner distance is exact.h's certified form.
+template <bool HASH, int MET = 0>
 __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
@@ -807,9 +811,14 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         // a perturbation below 16 ulp <= 2^-19 |t|, |t| <= |x| cmax + cmax^2/2,
         // charged to E (with 2x margin). The running max then identifies the
         // winner without a compare/select per score; its tile is noted per tile.
-        const float E = (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2 +
-                                0x1p-18 * (nx * (double)cmaxf + 0.5 * (double)cmaxf * (double)cmaxf)) *
-                            (1.f + 0x1p-20f) + 1e-30f;
+        // cosine: |t| <= |x| |c^| (no -|c|^2/2 term); + 2^-43 |x| covers the
+        // normalisation's roundings and the reference's own: its q = x.c / (|x||c|)
+        // carries <= 2^-46 relative (the fp64 norm chains), and 1 - q rounds at 2^-52
+        const float E = MET == 0
+            ? (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2 +
+                      0x1p-18 * (nx * (double)cmaxf + 0.5 * (double)cmaxf * (double)cmaxf)) * (1.f + 0x1p-20f) + 1e-30f
+            : (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2 +
+                      0x1p-18 * nx * (double)cmaxf + 0x1p-43 * nx) * (1.f + 0x1p-20f) + 1e-30f;
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
         int t1 = 0;
 #if PIPE_TILES
@@ -886,6 +895,25 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         // active, then the quarters add in order, handing the sum on with a quad
         // DPP move.
         PT_MARK(2)
+        if constexpr (MET == 1) {
+            // cosine winner: one lane per point re-reads its row (L2) and the
+            // winner's fp64 row; declined certificates -> the fix-up list
+            bool fix = false;
+            if (h == 1 && valid && cert) {
+                a.assign[row] = I1;
+                double v;
+                if (cosine_fast_nb(a.X + row * FU_D, a.C64 + (size_t)I1 * FU_D, FU_D, a.nbv[I1], v)) a.dist[row] = v;
+                else fix = true;
+            }
+            const unsigned long long fb = __ballot(fix);
+            if (fb) {
+                const int leader = __builtin_ctzll(fb);
+                int base = 0;
+                if (lane == leader) base = atomicAdd(lcount + 1, __popcll(fb));
+                base = __shfl(base, leader);
+                if (fix) hfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
+            }
+        } else {
 #if FP_KEEP_X
         {
             // exact row still in registers (B-operand layout): lane half h owns
@@ -976,6 +1004,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             }
         }
 #endif
+        }
         PT_MARK(3)
         const bool amb = valid && !cert;
         const unsigned long long amask = __ballot(amb && h == 1);
@@ -1081,13 +1110,35 @@ __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) 
 // ------------------------------------------------------------------ preparation
 // Centroids -> f16 hi/lo rows, -||c||^2/2, and the per-call bound maxima.
 __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpad, _Float16* __restrict__ Ch,
-                                    _Float16* __restrict__ Cl, float* __restrict__ cnh, unsigned int* __restrict__ cb) {
+                                    _Float16* __restrict__ Cl, float* __restrict__ cnh, unsigned int* __restrict__ cb,
+                                    int metric, double* __restrict__ nbv) {
     const int c = blockIdx.x;            // one wave per centroid row (d = 128: 2 dims per lane)
     const int lane = threadIdx.x;
     double s2 = 0.0, s1 = 0.0;
     bool bad = false;
+    double scale = 1.0;                  // cosine: the row is normalised (score x.c/|c|)
+    if (metric == 1) {
+        double q = 0.0;
+        for (int j = lane; j < FU_D; j += 64) {
+            const double v = c < K ? C[(size_t)c * FU_D + j] : 0.0;
+            q = fma(v, v, q);
+        }
+        for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+        // zero / extreme-norm centroids (the reference's NaN for a zero vector,
+        // assignment.hpp:66) leave the call uncertified: every row goes exact
+        if (c < K && !(q >= 1e-200 && q <= 1e200)) bad = true;
+        scale = (q >= 1e-200 && q <= 1e200) ? 1.0 / sqrt(q) : 0.0;
+        if (lane == 0 && c < K) {
+            double b = 0.0;
+            for (int j = 0; j < FU_D; j++) {
+                const double cj = C[(size_t)c * FU_D + j];
+                b = __dadd_rn(b, __dmul_rn(cj, cj));
+            }
+            nbv[c] = b;
+        }
+    }
     for (int j = lane; j < FU_D; j += 64) {
-        const double v = c < K ? C[(size_t)c * FU_D + j] : 0.0;
+        const double v = c < K ? C[(size_t)c * FU_D + j] * scale : 0.0;
         const float f = (float)v;
         const _Float16 hv = (_Float16)f;
         Ch[(size_t)c * FU_D + j] = hv;
@@ -1105,12 +1156,13 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     // padding rows: a finite score far below any real one (|x.c| < 2^38 under the
     // range guard), so the packed-index trick never meets an inf/nan
     if (c >= K) { cnh[c] = -0x1p100f; return; }
-    cnh[c] = (float)(-0.5 * s2);
+    cnh[c] = metric == 1 ? 0.f : (float)(-0.5 * s2);
     const double up = 1.0 + 0x1p-18;
     const double nc = sqrt(s2) * (1.0 + 0x1p-30);
     // |t~ - t| <= (A1 + 2^-22)|x||c| + A2(|x|_1 + |c|_1) + 2^-23 |c|^2 + 2^-41 (|x|^2 + |c|^2)
+    // (cosine: no |c|^2 term in t, c = the normalised row)
     const float ec = (float)((FU_A1 + 0x1p-22) * nc * up);
-    const float eb = (float)((FU_A2 * s1 * (1.0 + 0x1p-20) + 0x1p-23 * s2 + 0x1p-41 * s2) * up);
+    const float eb = (float)((FU_A2 * s1 * (1.0 + 0x1p-20) + (metric == 1 ? 0.0 : 0x1p-23 * s2) + 0x1p-41 * s2) * up);
     atomicMax(cb + 0, __float_as_uint(ec));     // positive floats order like their bits
     atomicMax(cb + 1, __float_as_uint(eb));
     atomicMax(cb + 3, __float_as_uint((float)(nc * up)));   // max |c|, rounded up
@@ -1118,10 +1170,14 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
 }
 
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
-                      float* cbound) {
+                      float* cbound, int metric, double* nbv) {
+    if (metric == 1 && !nbv) {
+        set_error("launch_fused_prep: cosine needs the norm array");
+        return -1;
+    }
     (void)hipMemsetAsync(cbound, 0, 16, s);
     hipLaunchKernelGGL(fused_centroid_prep, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, Ch, Cl, cnh,
-                       reinterpret_cast<unsigned int*>(cbound));
+                       reinterpret_cast<unsigned int*>(cbound), metric, nbv);
     return kstatus("fused_centroid_prep");
 }
 
@@ -1137,6 +1193,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.ambig = f.ambig; a.ambig_count = f.ambig_count; a.stats = f.stats;
     a.hfix = f.hfix; a.hfix_count = f.hfix_count;
     a.bdiv = make_bucket_div(f.nb);
+    a.nbv = f.nbv;
     a.prof = nullptr;
 #ifdef LSHKM_PHASE_TIMING
     static unsigned long long* prof_d = nullptr;
@@ -1155,6 +1212,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 #endif
     const char* force = getenv("LSHKM_FUSED_FORM");     // "chunked" forces the streaming form (tests)
     const bool chunked = force && !strcmp(force, "chunked");
+    if (f.metric == 1 && (hash || chunked || f.Kpad > FP_KMAX || !f.nbv || !f.hfix || !f.hfix_count)) {
+        set_error("launch_fused: cosine runs the persistent form only (K <= 256, no hashing, fix-up list)");
+        return -1;
+    }
     if (!chunked && f.Kpad <= FP_KMAX && (!hash || f.k == 4)) {
         static int cus[64] = {0};
         int dev = 0;
@@ -1178,7 +1239,12 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         f.nseg = nblk;
         f.seg_rows = a.seg_rows;
         if (!hash) {
-            hipLaunchKernelGGL(fused_persistent_kernel<false>, grid, block, lds, s, a);
+            if (f.metric == 1) {
+                a.hfix = f.hfix; a.hfix_count = f.hfix_count;
+                hipLaunchKernelGGL((fused_persistent_kernel<false, 1>), grid, block, lds, s, a);
+            } else {
+                hipLaunchKernelGGL(fused_persistent_kernel<false>, grid, block, lds, s, a);
+            }
             return kstatus("fused_persistent_kernel");
         }
         if (!a.hfix || !a.hfix_count || !a.tuples || f.LKpad > 32) {   // pts[] holds 128 x 32 projections
@@ -1193,6 +1259,30 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     if (hash) hipLaunchKernelGGL(fused_kernel<true>, grid, block, FU_LDS_BYTES, s, a);
     else hipLaunchKernelGGL(fused_kernel<false>, grid, block, FU_LDS_BYTES, s, a);
     return kstatus("fused_kernel");
+}
+
+// Cosine winners listed by fused_persistent_kernel<false, 1>: lane per row,
+// the soft-x87 chain. Blocks own list segments (CF_SPLIT per segment).
+constexpr int CF_SPLIT = 2;
+__global__ __launch_bounds__(256) void cos_fix_seg_kernel(const float* __restrict__ X, const double* __restrict__ C,
+                                                          const unsigned long long* __restrict__ list,
+                                                          const int32_t* __restrict__ seg_counts, int64_t seg_rows,
+                                                          const int32_t* __restrict__ assign, double* __restrict__ dist) {
+    const int seg = blockIdx.x / CF_SPLIT, part = blockIdx.x % CF_SPLIT;
+    const int n = seg_counts[2 * seg + 1];
+    const unsigned long long* l = list + (int64_t)seg * seg_rows;
+    for (int i = part * 256 + threadIdx.x; i < n; i += CF_SPLIT * 256) {
+        const int64_t row = (int64_t)l[i];
+        dist[row] = exact_cosine_x87(X + row * FU_D, C + (size_t)assign[row] * FU_D, FU_D);
+    }
+}
+
+int launch_cos_fix_seg(hipStream_t s, const float* X, const double* C, const unsigned long long* list,
+                       const int32_t* seg_counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist) {
+    if (nseg <= 0) return 0;
+    hipLaunchKernelGGL(cos_fix_seg_kernel, dim3((unsigned)nseg * CF_SPLIT), dim3(256), 0, s, X, C, list, seg_counts,
+                       seg_rows, assign, dist);
+    return kstatus("cos_fix_seg_kernel");
 }
 
 }  // namespace lshkm

@@ -49,7 +49,8 @@ int launch_cos_fix(hipStream_t s, const float* X, int64_t N, int d, const double
                    const unsigned long long* count, const int32_t* assign, double* dist);
 int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K,
                         int metric, const int32_t* rows, const unsigned long long* row_count,
-                        int64_t max_rows, int32_t* assign, double* dist);
+                        int64_t max_rows, int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
+                        int64_t seg_rows = 0, int nseg = 0);
 // Euclidean, listed rows, batched (CT: d * ceil64(K) doubles of workspace).
 // Segmented form (seg_counts != NULL): segment b = rows[b * seg_rows ...], count seg_counts[2b].
 int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
@@ -167,13 +168,22 @@ struct FusedLaunch {
     // out: nseg > 0 when the lists are segmented (segment b = [b * seg_rows, ...))
     int nseg = 0;
     int64_t seg_rows = 0;
+    // cosine Lloyd (metric 1, no hashing): nbv[c] = the reference's sequential
+    // sum of c_j^2; hfix/hfix_count then list the rows whose winner distance the
+    // certified form declined (cos_fix_seg pass)
+    int metric = 0;
+    const double* nbv = nullptr;
 };
 // List capacity the persistent form may need beyond N entries (grid <= 1024 blocks).
 constexpr int64_t FUSED_LIST_SLACK = 32 + 1024 * 12 * 32;
 constexpr int FUSED_MAX_SEGS = 1024;
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
-                      float* cbound);
+                      float* cbound, int metric = 0, double* nbv = nullptr);
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
+// Cosine winners listed by the persistent form (segment b: hfix[b * seg_rows ..],
+// count seg_counts[2b + 1]): soft-x87 distances.
+int launch_cos_fix_seg(hipStream_t s, const float* X, const double* C, const unsigned long long* list,
+                       const int32_t* seg_counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist);
 
 // Range assignment (range.hip).
 int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0);

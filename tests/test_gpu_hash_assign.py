@@ -321,12 +321,14 @@ def test_pruned_exact_pass(ctx, case, monkeypatch):
     np.testing.assert_allclose(dist.cpu().numpy()[sub], od, rtol=1e-14, atol=0)
 
 
+@pytest.mark.parametrize("d", [64, 128])
 @pytest.mark.parametrize("case", ["near_parallel", "near_orthogonal", "cancelling"])
-def test_cosine_certified_quotient_adversarial(ctx, case, monkeypatch):
+def test_cosine_certified_quotient_adversarial(ctx, case, d, monkeypatch):
     # exact.h IpAcc: the double-double inner product with the bounded x87
     # rounding must give the soft-x87 bits or decline; every row is checked
-    # against the oracle (real long double) on both assignment paths
-    N, d, K = 3001, 64, 12
+    # against the oracle (real long double) on both assignment paths (d = 128:
+    # the split-f16 persistent kernel with normalised centroids)
+    N, K = 3001, 12
     rng = np.random.default_rng(11)
     Xh = ctx.synth(0xADD, N, d).cpu().numpy().astype(np.float64)
     if case == "near_parallel":          # q = 1 - O(2^-20): 1 - q keeps few bits

@@ -99,7 +99,7 @@ def main():
             Xh = X[:n].cpu().numpy()
             c = (n, cpu_time(lambda: oracle.lloyd_assign(Xh, C.cpu().numpy(), "cosine", None)), f"{n} rows, K={K}")
         emit("lloyds_assignment (cosine)", "rows/s", N, t, c,
-             f"N=10M, d=128, K=256; f32-MFMA certified path, {amb:.0f} rows/call to the exact pass, "
+             f"N=10M, d=128, K=256; split-f16 persistent kernel (normalised centroids), {amb:.0f} rows/call to the exact pass, "
              f"{cfix:.0f} winner distances/call to the soft-x87 chain; "
              f"exact all-K pass alone {te * 1e3:.1f} ms")
         del X
