@@ -417,14 +417,15 @@ int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, in
 }  // extern "C"
 
 // Kernel path for assignment: d = 128 takes the split-f16 fused kernel
-// (euclidean any K; cosine K <= 256: normalised centroids, its persistent
-// form), else the f32-MFMA kernel (d <= 256), else the exact pass.
+// (persistent form, one launch per 256-centroid slice; cosine: normalised
+// centroids), else the f32-MFMA kernel (d <= 256), else the exact pass.
 // LSHKM_ASSIGN_PATH = "f32" / "exact" forces a path (tests compare them).
 static int assign_path(int metric, int d, int K) {
     const char* e = getenv("LSHKM_ASSIGN_PATH");
     if (e && !strcmp(e, "exact")) return 2;
     const bool f32 = e && !strcmp(e, "f32");
-    if (d == 128 && !f32 && (metric == LSHKM_METRIC_EUCLIDEAN || K <= 256)) {
+    (void)K;
+    if (d == 128 && !f32) {
         const char* ff = getenv("LSHKM_FUSED_FORM");
         if (metric == LSHKM_METRIC_EUCLIDEAN || !(ff && !strcmp(ff, "chunked"))) return 0;
     }
@@ -472,6 +473,7 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
             (rc = ctx->ws_ambig.reserve((size_t)(N + FUSED_LIST_SLACK) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
             (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)) ||
             ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8))) ||
+            (Kpad > 256 && (rc = ctx->ws_part.reserve((size_t)((N + 31) / 32) * 64 * 16))) ||
             (fuse_hash && !tuples && (rc = ctx->ws_tuples.reserve((size_t)std::max<int64_t>(N, 1) * lsh->proj.LK * 4))))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
@@ -489,6 +491,7 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         f.list_cap = N + FUSED_LIST_SLACK;
         f.seg_counts = (int32_t*)ctx->ws_seg.p;
         f.seg_cap = FUSED_MAX_SEGS;
+        if (Kpad > 256) { f.part = ctx->ws_part.p; f.part_bytes = (int64_t)((N + 31) / 32) * 64 * 16; }
         if (cosine) {
             f.metric = 1; f.nbv = nbv;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;

@@ -122,6 +122,11 @@ struct FusedArgs {
     int32_t* seg_counts;
     BucketDiv bdiv;          // phi % nb by multiply-high
     const double* nbv;       // cosine: [K] sequential sum of c_j^2 (cust_vector.hpp:139-155)
+    // multi-pass persistent form (K > 256): this launch scores centroid tiles
+    // t0.. of the slice in Ch/Cl/cnh (Kpad rows); the running state per lane
+    // crosses passes in part[tile * 64 + lane]
+    float4* part;
+    int t0, pass_first, pass_last;
     unsigned long long* prof;        // LSHKM_PHASE_TIMING builds only: per-phase wave cycles
 };
 
@@ -601,7 +606,9 @@ static_assert(fp_lds_bytes(FP_KMAX, true) <= 160 * 1024, "persistent LDS image e
 
 // MET = 1: cosine Lloyd (HASH = false): centroids are normalised in the prep
 // (score x.c/|c|, cnh = 0), the winner distance is exact.h's certified form.
-template <bool HASH, int MET = 0>
+// MP: multi-pass (K > 256) form; the single-pass instantiation compiles without
+// the pass-state code.
+template <bool HASH, int MET = 0, bool MP = false>
 __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
@@ -821,6 +828,11 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                       0x1p-18 * nx * (double)cmaxf + 0x1p-43 * nx) * (1.f + 0x1p-20f) + 1e-30f;
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
         int t1 = 0;
+        if (MP && !a.pass_first) {
+            const float4 st = a.part[tile * 64 + lane];
+            m1 = st.x; m2 = st.y; t1 = __float_as_int(st.z);
+        }
+        const int tg0 = MP ? a.t0 : 0;        // global index of this slice's first tile
 #if PIPE_TILES
         // Software pipeline: tile t's scores are formed (16 VGPRs), then tile
         // t+1's 24 MFMAs issue with tile t's epilogue placed in their gaps
@@ -848,7 +860,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             } else {
                 tile_epilogue(sv, m1, m2);
             }
-            t1 = m1 != m1_prev ? t : t1;
+            t1 = m1 != m1_prev ? t + tg0 : t1;
         }
 #else
 #if MFMA_PRIO
@@ -868,12 +880,16 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             tile_scores(acc_hi, acc_lo, lcn + t * 32 + 4 * h, sv);
 #endif
             tile_epilogue(sv, m1, m2);
-            t1 = m1 != m1_prev ? t : t1;
+            t1 = m1 != m1_prev ? t + tg0 : t1;
         }
 #if MFMA_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
 #endif
+        if (MP && !a.pass_last) {             // more slices to come: carry the state
+            a.part[tile * 64 + lane] = make_float4(m1, m2, __int_as_float(t1), 0.f);
+            continue;
+        }
         const uint32_t l1 = __float_as_uint(m1) & 0xFu;
         const int i1 = t1 * 32 + 8 * (int)(l1 >> 2) + 4 * h + (int)(l1 & 3u);
         const float om1 = __shfl_xor(m1, 32), om2 = __shfl_xor(m2, 32);
@@ -1022,7 +1038,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     }
     PT_FLUSH
     __syncthreads();
-    if (threadIdx.x < 2) {
+    // slot 0: ambiguous rows (the last pass decides them); slot 1: the hash
+    // fix-up list (the hashing pass) or the cosine fix-up list (the last pass)
+    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? a.pass_last != 0 : (HASH || (MET == 1 && a.pass_last))))) {
         const int c = lcount[threadIdx.x];
         a.seg_counts[2 * blockIdx.x + threadIdx.x] = c;
         if (c) atomicAdd(threadIdx.x == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
@@ -1194,6 +1212,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.hfix = f.hfix; a.hfix_count = f.hfix_count;
     a.bdiv = make_bucket_div(f.nb);
     a.nbv = f.nbv;
+    a.part = nullptr; a.t0 = 0; a.pass_first = 1; a.pass_last = 1;
     a.prof = nullptr;
 #ifdef LSHKM_PHASE_TIMING
     static unsigned long long* prof_d = nullptr;
@@ -1212,11 +1231,13 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 #endif
     const char* force = getenv("LSHKM_FUSED_FORM");     // "chunked" forces the streaming form (tests)
     const bool chunked = force && !strcmp(force, "chunked");
-    if (f.metric == 1 && (hash || chunked || f.Kpad > FP_KMAX || !f.nbv || !f.hfix || !f.hfix_count)) {
-        set_error("launch_fused: cosine runs the persistent form only (K <= 256, no hashing, fix-up list)");
+    const int npass = (f.Kpad + FP_KMAX - 1) / FP_KMAX;
+    const bool multi_ok = npass == 1 || (f.part && f.part_bytes >= ((f.N + 31) / 32) * 64 * 16);
+    if (f.metric == 1 && (hash || chunked || !multi_ok || !f.nbv || !f.hfix || !f.hfix_count)) {
+        set_error("launch_fused: cosine runs the persistent form only (no hashing, fix-up list, pass state)");
         return -1;
     }
-    if (!chunked && f.Kpad <= FP_KMAX && (!hash || f.k == 4)) {
+    if (!chunked && multi_ok && (!hash || f.k == 4)) {
         static int cus[64] = {0};
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return kstatus("hipGetDevice");
@@ -1228,7 +1249,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         const int64_t want = (ntiles + FP_WAVES - 1) / FP_WAVES;
         const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(ncu, want));
         const dim3 grid((unsigned)nblk), block(FP_THREADS);
-        const size_t lds = (size_t)fp_lds_bytes(f.Kpad, hash);
+        const int kslice = std::min(f.Kpad, FP_KMAX);
+        const size_t lds = (size_t)fp_lds_bytes(kslice, hash);
+        const size_t lds_nohash = (size_t)fp_lds_bytes(kslice, false);
         // list segments: block b's tiles hold at most FP_WAVES * 32 * ceil(tiles / (grid * FP_WAVES)) rows
         a.seg_rows = (int64_t)FP_WAVES * 32 * ((ntiles + (int64_t)nblk * FP_WAVES - 1) / ((int64_t)nblk * FP_WAVES));
         a.seg_counts = f.seg_counts;
@@ -1238,21 +1261,29 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         }
         f.nseg = nblk;
         f.seg_rows = a.seg_rows;
-        if (!hash) {
-            if (f.metric == 1) {
-                a.hfix = f.hfix; a.hfix_count = f.hfix_count;
-                hipLaunchKernelGGL((fused_persistent_kernel<false, 1>), grid, block, lds, s, a);
-            } else {
-                hipLaunchKernelGGL(fused_persistent_kernel<false>, grid, block, lds, s, a);
-            }
-            return kstatus("fused_persistent_kernel");
-        }
-        if (!a.hfix || !a.hfix_count || !a.tuples || f.LKpad > 32) {   // pts[] holds 128 x 32 projections
+        if (hash && (!a.hfix || !a.hfix_count || !a.tuples || f.LKpad > 32)) {   // pts[] holds 128 x 32 projections
             set_error("launch_fused: hashing needs the fix-up list, a tuple buffer and L*k <= 32");
             return -1;
         }
-        hipLaunchKernelGGL(fused_persistent_kernel<true>, grid, block, lds, s, a);
-        hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
+        if (f.metric == 1) { a.hfix = f.hfix; a.hfix_count = f.hfix_count; }
+        a.part = reinterpret_cast<float4*>(f.part);
+        // one launch per 256-centroid slice (the hashing rides on the first)
+        for (int p = 0; p < npass; p++) {
+            const int c0 = p * FP_KMAX;
+            a.Ch = f.Ch + (size_t)c0 * FU_D; a.Cl = f.Cl + (size_t)c0 * FU_D; a.cnh = f.cnh + c0;
+            a.Kpad = std::min(FP_KMAX, f.Kpad - c0);
+            a.t0 = c0 / 32; a.pass_first = p == 0; a.pass_last = p == npass - 1;
+            if (npass == 1) {
+                if (hash) hipLaunchKernelGGL((fused_persistent_kernel<true>), grid, block, lds, s, a);
+                else if (f.metric == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 1>), grid, block, lds_nohash, s, a);
+                else hipLaunchKernelGGL((fused_persistent_kernel<false>), grid, block, lds_nohash, s, a);
+            } else {
+                if (hash && p == 0) hipLaunchKernelGGL((fused_persistent_kernel<true, 0, true>), grid, block, lds, s, a);
+                else if (f.metric == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 1, true>), grid, block, lds_nohash, s, a);
+                else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true>), grid, block, lds_nohash, s, a);
+            }
+        }
+        if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
         return kstatus("fused_persistent_kernel");
     }
     const dim3 grid((unsigned)((f.N + FU_PB - 1) / FU_PB)), block(FU_THREADS);

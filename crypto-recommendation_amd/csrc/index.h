@@ -45,7 +45,7 @@ struct lshkm_ctx_s {
     hipStream_t own_stream = nullptr;
     lshkm::Buf stats;            // STAT_COUNT x u64
     // assignment workspace
-    lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src, ws_hfix, ws_ct, ws_seg, ws_tuples;
+    lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src, ws_hfix, ws_ct, ws_seg, ws_tuples, ws_part;
     // scatter / query / update workspace (see api_index.cpp for the slot map)
     lshkm::Buf ws[16];
     // range assignment workspace (lshkm_range_assign)

@@ -173,7 +173,12 @@ struct FusedLaunch {
     // certified form declined (cos_fix_seg pass)
     int metric = 0;
     const double* nbv = nullptr;
+    // K > 256 on the persistent form: passes over 256-centroid slices carry each
+    // lane's (best, runner-up, tile) in part[] (32 B per point)
+    void* part = nullptr;
+    int64_t part_bytes = 0;
 };
+constexpr int64_t FUSED_PART_BYTES_PER_ROW = 32;
 // List capacity the persistent form may need beyond N entries (grid <= 1024 blocks).
 constexpr int64_t FUSED_LIST_SLACK = 32 + 1024 * 12 * 32;
 constexpr int FUSED_MAX_SEGS = 1024;

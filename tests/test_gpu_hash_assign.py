@@ -354,3 +354,28 @@ def test_cosine_certified_quotient_adversarial(ctx, case, d, monkeypatch):
     for a, dd in ((a0, d0), (a1, d1)):
         assert np.array_equal(a.cpu().numpy(), oa)
         assert np.array_equal(dd.cpu().numpy().view(np.uint64), od.view(np.uint64))
+
+
+@pytest.mark.parametrize("metric", ["euclidean", "cosine"])
+def test_multipass_persistent_k1024(ctx, metric, monkeypatch):
+    # K > 256 on the persistent form: one launch per 256-centroid slice with the
+    # per-lane (best, runner-up, tile) carried across launches; duplicates in
+    # different slices (exact ties: the first index must win) and a ragged last
+    # slice (K = 1000 -> 4 launches, the last of 232 rows)
+    N, d, K = 20_011, 128, 1000
+    X = ctx.synth(0x1024, N, d)
+    rng = np.random.default_rng(9)
+    rows = rng.choice(N, K, replace=False).astype(np.int64)
+    Cc = X[to_dev(ctx, rows)].double()
+    Cc[600:610] = Cc[100:110]                         # ties across slices
+    Cc[900] = Cc[3] * (2.0 if metric == "cosine" else 1.0)
+    ctx.reset_stats()
+    a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, metric)
+    monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
+    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, metric)
+    assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
+    assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
+    sub = np.random.default_rng(2).choice(N, 600, replace=False)
+    oa, od = oracle.lloyd_assign(X.cpu().numpy()[sub], Cc.cpu().numpy(), metric, None)
+    assert np.array_equal(a0.cpu().numpy()[sub], oa)
+    assert np.array_equal(d0.cpu().numpy()[sub].view(np.uint64), od.view(np.uint64))
