@@ -37,12 +37,160 @@ __global__ void sil_near_kernel(const double* __restrict__ C, int K, int d, int 
     near[c] = arg;
 }
 
-// One thread per member (cluster-sorted order): s(i) (silhouette.hpp:83-144).
-// Lanes of a wave mostly share their cluster, so the x_j loads broadcast.
-__global__ void sil_point_kernel(const float* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows,
-                                 const int64_t* __restrict__ crow, const int32_t* __restrict__ assign,
-                                 const int32_t* __restrict__ near, int64_t N, double* __restrict__ s_out) {
-    // s_out is indexed by row
+// One wave per member i (cluster-sorted order): s(i) (silhouette.hpp:83-144).
+// x_i sits in LDS (broadcast reads); lane L evaluates d(x_i, x_j) for member
+// j = jb + L of a 64-member batch, then every lane adds the batch's 64
+// distances in member order (readlane: the sum stays the reference's sequential
+// chain). A thread-per-member form ran one latency-bound chain per lane with too
+// few waves to hide it (N / 64 waves).
+constexpr int SP_WAVES = 4;
+constexpr int SIL_DMAX = 512;
+
+// x_i (LDS, fp32) vs x_j (global, fp32): the exact.h order, 4-wide loads
+__device__ inline double sil_euclid(const float* __restrict__ xi, const float* __restrict__ xj, int d) {
+    double acc = 0.0;
+    int k = 0;
+    if ((d & 3) == 0) {
+#pragma unroll 4
+        for (; k < d; k += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(xi + k);
+            const float4 b = *reinterpret_cast<const float4*>(xj + k);
+            const double d0 = __dsub_rn((double)a.x, (double)b.x), d1 = __dsub_rn((double)a.y, (double)b.y);
+            const double d2 = __dsub_rn((double)a.z, (double)b.z), d3 = __dsub_rn((double)a.w, (double)b.w);
+            acc = __dadd_rn(acc, __dmul_rn(d0, d0));
+            acc = __dadd_rn(acc, __dmul_rn(d1, d1));
+            acc = __dadd_rn(acc, __dmul_rn(d2, d2));
+            acc = __dadd_rn(acc, __dmul_rn(d3, d3));
+        }
+    }
+    for (; k < d; k++) {
+        const double df = __dsub_rn((double)xi[k], (double)xj[k]);
+        acc = __dadd_rn(acc, __dmul_rn(df, df));
+    }
+    return sqrt(acc);
+}
+
+// sum_{j in [j0, j1)} d(x_i, x_rows[j]) in j order (wave-uniform result)
+__device__ inline double sil_segment(const float* __restrict__ xi, const float* __restrict__ X, int d, int metric,
+                                     const int32_t* __restrict__ rows, int64_t j0, int64_t j1, int lane) {
+    double acc = 0.0;
+    for (int64_t jb = j0; jb < j1; jb += 64) {
+        const int64_t j = jb + lane;
+        double dj = 0.0;
+        if (j < j1) {
+            const float* xj = X + (size_t)rows[j] * d;
+            dj = metric == 0 ? sil_euclid(xi, xj, d) : exact_dist(xi, xj, d, metric);
+        }
+        const int n = (int)min<int64_t>(64, j1 - jb);
+        for (int t = 0; t < n; t++) acc = __dadd_rn(acc, __shfl(dj, t));
+    }
+    return acc;
+}
+
+// Two members (same cluster) against the same x_j: each x_j load serves both.
+__device__ inline void sil_euclid2(const float* __restrict__ xa, const float* __restrict__ xb,
+                                   const float* __restrict__ xj, int d, double& da, double& db) {
+    double aa = 0.0, ab = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < d; k += 4) {
+        const float4 b = *reinterpret_cast<const float4*>(xj + k);
+        const float4 u = *reinterpret_cast<const float4*>(xa + k);
+        const float4 v = *reinterpret_cast<const float4*>(xb + k);
+        const double b0 = (double)b.x, b1 = (double)b.y, b2 = (double)b.z, b3 = (double)b.w;
+        const double u0 = __dsub_rn((double)u.x, b0), u1 = __dsub_rn((double)u.y, b1);
+        const double u2 = __dsub_rn((double)u.z, b2), u3 = __dsub_rn((double)u.w, b3);
+        const double v0 = __dsub_rn((double)v.x, b0), v1 = __dsub_rn((double)v.y, b1);
+        const double v2 = __dsub_rn((double)v.z, b2), v3 = __dsub_rn((double)v.w, b3);
+        aa = __dadd_rn(aa, __dmul_rn(u0, u0)); ab = __dadd_rn(ab, __dmul_rn(v0, v0));
+        aa = __dadd_rn(aa, __dmul_rn(u1, u1)); ab = __dadd_rn(ab, __dmul_rn(v1, v1));
+        aa = __dadd_rn(aa, __dmul_rn(u2, u2)); ab = __dadd_rn(ab, __dmul_rn(v2, v2));
+        aa = __dadd_rn(aa, __dmul_rn(u3, u3)); ab = __dadd_rn(ab, __dmul_rn(v3, v3));
+    }
+    da = sqrt(aa);
+    db = sqrt(ab);
+}
+
+__device__ inline void sil_segment2(const float* __restrict__ xa, const float* __restrict__ xb,
+                                    const float* __restrict__ X, int d, const int32_t* __restrict__ rows, int64_t j0,
+                                    int64_t j1, int lane, double& sa, double& sb) {
+    double acc_a = 0.0, acc_b = 0.0;
+    for (int64_t jb = j0; jb < j1; jb += 64) {
+        const int64_t j = jb + lane;
+        double da = 0.0, db = 0.0;
+        if (j < j1) sil_euclid2(xa, xb, X + (size_t)rows[j] * d, d, da, db);
+        const int n = (int)min<int64_t>(64, j1 - jb);
+        for (int t = 0; t < n; t++) {
+            acc_a = __dadd_rn(acc_a, __shfl(da, t));
+            acc_b = __dadd_rn(acc_b, __shfl(db, t));
+        }
+    }
+    sa = acc_a;
+    sb = acc_b;
+}
+
+__device__ inline double sil_value(double a, double b, int64_t c0, int64_t c1, int64_t n0, int64_t n1) {
+    if (c1 - c0 != 1) a = __ddiv_rn(a, (double)(c1 - c0 - 1));
+    b = x86_nan(__ddiv_rn(b, (double)(n1 - n0)));
+    a = x86_nan(a);
+    double mx = a;
+    if (b > a) mx = b;
+    // NaN operands: x86 returns the first NaN operand; both are the default NaN here
+    return x86_nan(__ddiv_rn(__dsub_rn(b, a), mx));
+}
+
+__global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
+    const float* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows, const int64_t* __restrict__ crow,
+    const int32_t* __restrict__ assign, const int32_t* __restrict__ near, int64_t N, double* __restrict__ s_out) {
+    __shared__ __attribute__((aligned(16))) float xs[SP_WAVES][2][SIL_DMAX];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float* xa = xs[wave][0];
+    float* xb = xs[wave][1];
+    // a wave takes members p, p + 1 (cluster-sorted): one pass over the x_j when
+    // they share a cluster (euclidean, d % 4 == 0); s_out is indexed by row
+    const int64_t npair = (N + 1) / 2;
+    for (int64_t q = (int64_t)blockIdx.x * SP_WAVES + wave; q < npair; q += (int64_t)gridDim.x * SP_WAVES) {
+        const int64_t p = 2 * q;
+        const bool has2 = p + 1 < N;
+        const int32_t ra = rows[p], rb = has2 ? rows[p + 1] : ra;
+        const int ca = assign[ra], cb = assign[rb];
+        __builtin_amdgcn_wave_barrier();                      // previous members' reads of xs are done
+        for (int k = lane; k < d; k += 64) {
+            xa[k] = X[(size_t)ra * d + k];
+            xb[k] = X[(size_t)rb * d + k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (has2 && ca == cb && metric == 0 && (d & 3) == 0) {
+            const int64_t c0 = crow[ca], c1 = crow[ca + 1];
+            const int nc = near[ca];
+            const int64_t n0 = crow[nc], n1 = crow[nc + 1];
+            double a0, a1, b0, b1;
+            sil_segment2(xa, xb, X, d, rows, c0, c1, lane, a0, a1);
+            sil_segment2(xa, xb, X, d, rows, n0, n1, lane, b0, b1);
+            if (lane == 0) {
+                s_out[ra] = sil_value(a0, b0, c0, c1, n0, n1);
+                s_out[rb] = sil_value(a1, b1, c0, c1, n0, n1);
+            }
+            continue;
+        }
+        for (int m = 0; m < (has2 ? 2 : 1); m++) {
+            const float* xi = m ? xb : xa;
+            const int c = m ? cb : ca;
+            const int64_t c0 = crow[c], c1 = crow[c + 1];
+            const double a = sil_segment(xi, X, d, metric, rows, c0, c1, lane);
+            const int nc = near[c];
+            const int64_t n0 = crow[nc], n1 = crow[nc + 1];
+            const double b = sil_segment(xi, X, d, metric, rows, n0, n1, lane);
+            if (lane == 0) s_out[m ? rb : ra] = sil_value(a, b, c0, c1, n0, n1);
+        }
+    }
+}
+
+// d > SIL_DMAX: one thread per member, the same sums.
+__global__ void sil_point_thread_kernel(const float* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows,
+                                        const int64_t* __restrict__ crow, const int32_t* __restrict__ assign,
+                                        const int32_t* __restrict__ near, int64_t N, double* __restrict__ s_out) {
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x) {
         const int32_t r = rows[p];
         const int c = assign[r];
@@ -59,7 +207,6 @@ __global__ void sil_point_kernel(const float* __restrict__ X, int d, int metric,
         a = x86_nan(a);
         double mx = a;
         if (b > a) mx = b;
-        // NaN operands: x86 returns the first NaN operand; both are the default NaN here
         s_out[r] = x86_nan(__ddiv_rn(__dsub_rn(b, a), mx));
     }
 }
@@ -93,8 +240,13 @@ int launch_sil_near(hipStream_t s, const double* C, int K, int d, int metric, in
 int launch_sil_points(hipStream_t s, const float* X, int d, int metric, const int32_t* rows, const int64_t* crow,
                       const int32_t* assign, const int32_t* near, int64_t N, double* s_out) {
     if (N == 0) return 0;
-    hipLaunchKernelGGL(sil_point_kernel, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X, d, metric, rows, crow, assign,
-                       near, N, s_out);
+    if (d > SIL_DMAX) {
+        hipLaunchKernelGGL(sil_point_thread_kernel, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X, d, metric, rows, crow,
+                           assign, near, N, s_out);
+        return kstatus("sil_point_thread_kernel");
+    }
+    hipLaunchKernelGGL(sil_point_kernel, dim3(gsz((N + 1) / 2, SP_WAVES, 16384)), dim3(64 * SP_WAVES), 0, s, X, d, metric, rows,
+                       crow, assign, near, N, s_out);
     return kstatus("sil_point_kernel");
 }
 
