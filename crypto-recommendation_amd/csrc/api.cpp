@@ -602,7 +602,7 @@ int lshkm_range_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         LSHKM_HIP(hipMemcpyAsync(w[5].p, key_host, (size_t)K * 4, hipMemcpyHostToDevice, s));
         key = (const int32_t*)w[5].p;
     }
-    if ((rc = launch_range_radius(s, C, K, d, metric, r0))) return rc;
+    if ((rc = launch_range_radius(s, C, K, d, metric, r0, (unsigned long long*)w[0].p + 4))) return rc;
     if ((rc = launch_range_init(s, N, assign, dist))) return rc;
     int passes = 0;
     if (M > 0 && N > 0) {

@@ -191,7 +191,8 @@ int launch_cos_fix_seg(hipStream_t s, const float* X, const double* C, const uns
                        const int32_t* seg_counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist);
 
 // Range assignment (range.hip).
-int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0);
+int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0,
+                        unsigned long long* tmp);
 int launch_range_pairs(hipStream_t s, const int64_t* comb_ptr, const int32_t* comb_idx, int K, int32_t* rows,
                        int32_t* cents);
 int launch_range_init(hipStream_t s, int64_t N, int32_t* assign, double* dist);

@@ -30,28 +30,49 @@ namespace lshkm {
 // find_min_vector_distance over the centroid rows, /2: the sequential scan
 // with the -1 sentinel keeps the first pair's value if it is NaN and is
 // otherwise the minimum of the non-NaN values (the sign of a zero never
-// reaches a comparison downstream). One block.
-constexpr int RG_MIN_THREADS = 1024;
+// reaches a comparison downstream).
+// Many blocks, one pair per thread iteration (a single block ran K^2 / 1024
+// sequential exact chains per thread: 2.4 ms at K = 256); the minimum is an
+// atomicMin over order-preserving keys of the doubles (NaNs never enter it),
+// tmp[0] = key, tmp[1] = "pair (0, 1) is NaN", tmp[2] = that NaN's bits.
+constexpr int RG_MIN_THREADS = 256;
+__device__ inline unsigned long long rg_key(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ inline double rg_unkey(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
+}
+__global__ void rg_min_init_kernel(unsigned long long* __restrict__ tmp) {
+    tmp[0] = ~0ull;
+    tmp[1] = 0ull;
+}
 __global__ __launch_bounds__(RG_MIN_THREADS) void rg_min_pair_kernel(const double* __restrict__ C, int K, int d,
-                                                                     int metric, double* __restrict__ r0) {
-    __shared__ double red[RG_MIN_THREADS];
-    const int64_t pairs = (int64_t)K * (K - 1) / 2;
-    double mn = __builtin_inf();
-    bool any = false;
-    for (int64_t p = threadIdx.x; p < (int64_t)K * K; p += RG_MIN_THREADS) {
+                                                                     int metric, unsigned long long* __restrict__ tmp) {
+    __shared__ unsigned long long red[RG_MIN_THREADS];
+    unsigned long long mk = ~0ull;
+    const int64_t kk = (int64_t)K * K;
+    for (int64_t p = (int64_t)blockIdx.x * RG_MIN_THREADS + threadIdx.x; p < kk; p += (int64_t)gridDim.x * RG_MIN_THREADS) {
         const int i = (int)(p / K), j = (int)(p % K);
         if (j <= i) continue;                                    // pairs (i, j > i), utils.hpp:164-165
         const double dd = exact_dist(C + (size_t)i * d, C + (size_t)j * d, d, metric);
-        if (p == 1 && dd != dd) { *r0 = dd / 2; any = true; }   // first pair (0, 1) NaN: the scan stays NaN
-        if (dd < mn) mn = dd;
+        if (p == 1 && dd != dd) { tmp[2] = (unsigned long long)__double_as_longlong(dd); tmp[1] = 1ull; }
+        if (dd == dd) mk = min(mk, rg_key(dd));
     }
-    red[threadIdx.x] = mn;
-    const int first_nan = __syncthreads_or(any);
+    red[threadIdx.x] = mk;
+    __syncthreads();
     for (int off = RG_MIN_THREADS / 2; off > 0; off >>= 1) {
-        if (threadIdx.x < off) red[threadIdx.x] = fmin(red[threadIdx.x], red[threadIdx.x + off]);
+        if (threadIdx.x < off) red[threadIdx.x] = min(red[threadIdx.x], red[threadIdx.x + off]);
         __syncthreads();
     }
-    if (threadIdx.x == 0 && !first_nan) *r0 = (pairs == 0 ? -1.0 : red[0]) / 2;
+    if (threadIdx.x == 0 && red[0] != ~0ull) atomicMin(tmp, red[0]);
+}
+// r0 = (first pair NaN) ? NaN / 2 : (no pairs ? -1 : min) / 2 (the reference's
+// scan: a NaN first value stays, later NaNs never win a '<')
+__global__ void rg_min_final_kernel(const unsigned long long* __restrict__ tmp, int K, double* __restrict__ r0) {
+    const int64_t pairs = (int64_t)K * (K - 1) / 2;
+    if (tmp[1]) *r0 = __longlong_as_double((long long)tmp[2]) / 2;
+    else *r0 = (pairs == 0 ? -1.0 : (tmp[0] == ~0ull ? __builtin_inf() : rg_unkey(tmp[0]))) / 2;
 }
 
 // (row, centroid) incidences of the combined buckets, centroid-major.
@@ -152,8 +173,13 @@ __global__ void rg_scatter_kernel(const int32_t* __restrict__ list, int64_t M, c
     }
 }
 
-int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0) {
-    hipLaunchKernelGGL(rg_min_pair_kernel, dim3(1), dim3(RG_MIN_THREADS), 0, s, C, K, d, metric, r0);
+int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0,
+                        unsigned long long* tmp) {
+    const int64_t kk = (int64_t)K * K;
+    hipLaunchKernelGGL(rg_min_init_kernel, dim3(1), dim3(1), 0, s, tmp);
+    hipLaunchKernelGGL(rg_min_pair_kernel, dim3(gsz(kk, RG_MIN_THREADS, 2048)), dim3(RG_MIN_THREADS), 0, s, C, K, d,
+                       metric, tmp);
+    hipLaunchKernelGGL(rg_min_final_kernel, dim3(1), dim3(1), 0, s, tmp, K, r0);
     return kstatus("rg_min_pair_kernel");
 }
 
