@@ -21,6 +21,7 @@
 namespace lshkm {
 
 constexpr int RC_WAVES = 4;
+constexpr int RC_MAXV = 8;       // candidates per lane held in registers (n <= 512 per user)
 
 // CustVector::cosineSimilarity (cust_vector.hpp:158-174), this = neighbour x,
 // in = user u: long-double inner product of double products, fp64 norms
@@ -95,12 +96,83 @@ __global__ __launch_bounds__(64 * RC_WAVES) void rc_p_closest_kernel(
         const double* u = U + q * d;
         const double ub = rc_sumsq(u, d);
         bool nan = false;
-        for (int i = lane; i < n; i += 64) {
-            const int32_t r = cand_idx[o + i];
-            const double s = rc_cos_sim(X + (int64_t)r * d, u, d, xa[r], ub);
-            sim[o + i] = s;
-            key[o + i] = s;
-            nan |= s != s;
+        unsigned inexact = 0;            // this lane's candidates still held as intervals
+        if (n <= 64 * RC_MAXV) {
+            // Certified similarities first (exact.h IpAcc: q exact, or the exact
+            // value within q +- qr); the soft-x87 chain only for candidates whose
+            // interval reaches T, the (P+1)-th largest lower bound -- nothing
+            // below T can enter the top P+1 -- and for declined ones (zero
+            // vectors, NaN/inf). A replayed user (NaN or tie) gets every value exact.
+            double qv[RC_MAXV], qr[RC_MAXV];
+#pragma unroll
+            for (int k = 0; k < RC_MAXV; k++) {
+                qv[k] = -__builtin_inf(); qr[k] = 0.0;
+                const int i = lane + 64 * k;
+                if (i < n) {
+                    const int32_t r = cand_idx[o + i];
+                    const double* x = X + (int64_t)r * d;
+                    IpAcc ip;
+                    for (int j = 0; j < d; j++) ip.add(__dmul_rn(x[j], u[j]));
+                    const int st = ip.quot_status(__dmul_rn(sqrt(xa[r]), sqrt(ub)), qv[k], qr[k]);
+                    if (st == 2) { qv[k] = rc_cos_sim(x, u, d, xa[r], ub); qr[k] = 0.0; }
+                    else if (st == 0) qr[k] = 0.0;
+                    nan |= qv[k] != qv[k];
+                }
+            }
+            const bool any_nan = __ballot(nan) != 0;
+            double T = -__builtin_inf();
+            if (!any_nan) {
+                // T: the (P+1)-th largest lower bound (repeated wave max, first position)
+                double lo[RC_MAXV];
+#pragma unroll
+                for (int k = 0; k < RC_MAXV; k++) lo[k] = lane + 64 * k < n ? qv[k] - qr[k] : -__builtin_inf();
+                const int ext0 = n < P + 1 ? n : P + 1;
+                for (int e = 0; e < ext0; e++) {
+                    double best = -__builtin_inf();
+                    int bk = -1;
+#pragma unroll
+                    for (int k = 0; k < RC_MAXV; k++)
+                        if (lo[k] > best || bk < 0) { best = lo[k]; bk = k; }
+                    int bl = lane;
+                    for (int off = 32; off >= 1; off >>= 1) {
+                        const double ob = __shfl_xor(best, off);
+                        const int ol = __shfl_xor(bl, off);
+                        if (ob > best || (ob == best && ol < bl)) { best = ob; bl = ol; }
+                    }
+                    T = best;
+                    if (lane == bl) {
+#pragma unroll
+                        for (int k = 0; k < RC_MAXV; k++)
+                            if (k == bk) lo[k] = -__builtin_inf();
+                    }
+                }
+                if (n <= P + 1) T = -__builtin_inf();     // every candidate is in the top P+1
+            }
+#pragma unroll
+            for (int k = 0; k < RC_MAXV; k++) {
+                const int i = lane + 64 * k;
+                if (i < n && qr[k] != 0.0 && (any_nan || qv[k] + qr[k] >= T)) {
+                    const int32_t r = cand_idx[o + i];
+                    qv[k] = rc_cos_sim(X + (int64_t)r * d, u, d, xa[r], ub);
+                    qr[k] = 0.0;
+                }
+                if (i < n) {
+                    sim[o + i] = qv[k];
+                    key[o + i] = qv[k];
+                }
+            }
+            // a tie found below makes this user a replay: its values must all be exact
+#pragma unroll
+            for (int k = 0; k < RC_MAXV; k++)
+                if (qr[k] != 0.0) inexact |= 1u << k;
+        } else {
+            for (int i = lane; i < n; i += 64) {
+                const int32_t r = cand_idx[o + i];
+                const double s = rc_cos_sim(X + (int64_t)r * d, u, d, xa[r], ub);
+                sim[o + i] = s;
+                key[o + i] = s;
+                nan |= s != s;
+            }
         }
         const int c = n < P ? n : P;
         if (lane == 0) out_cnt[q] = c;
@@ -134,6 +206,14 @@ __global__ __launch_bounds__(64 * RC_WAVES) void rc_p_closest_kernel(
             }
             if (lane == (bpos & 63)) key[o + bpos] = -__builtin_inf();
             wave_sync();
+        }
+        if (replay_me && __ballot(inexact != 0u)) {
+            for (int k = 0; k < RC_MAXV; k++)
+                if ((inexact >> k) & 1u) {
+                    const int i = lane + 64 * k;
+                    const int32_t r = cand_idx[o + i];
+                    sim[o + i] = rc_cos_sim(X + (int64_t)r * d, u, d, xa[r], ub);
+                }
         }
         if (replay_me && lane == 0) replay[atomicAdd(replay_count, 1u)] = (int32_t)q;
     }

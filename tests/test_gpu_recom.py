@@ -76,3 +76,34 @@ def test_recommend_matches_oracle(ctx, N, d, nq, P, NT, levels, seed):
     assert np.array_equal(idx, w_idx)
     assert np.array_equal(sim.view(np.uint64), w_sim.view(np.uint64))
     assert np.array_equal(top, w_top)
+
+
+@pytest.mark.parametrize("dup", [False, True])
+def test_p_closest_certified_intervals(ctx, dup):
+    # continuous data: most similarities are held as certified intervals and
+    # only those reaching the (P+1)-th lower bound get the soft-x87 chain;
+    # dup: a near-top candidate repeated (an exact tie -> replay, which needs
+    # every value exact, including the interval-held ones)
+    rng = np.random.default_rng(17)
+    N, d, nq, P = 6000, 100, 600, 20
+    # 26-bit values: squares are exact (glibc pow(x, 2) == x * x),
+    # products carry 52 bits, so the fp64 partial sums round and the x87 ones do not
+    X = rng.integers(-2**25, 2**25, size=(N, d)).astype(np.float64) / 2**25
+    U = rng.integers(-2**25, 2**25, size=(nq, d)).astype(np.float64) / 2**25
+    cand = []
+    for q in range(nq):
+        c = rng.choice(N, size=int(rng.integers(P + 2, 500)), replace=False)
+        if dup and q % 3 == 0:
+            X_best = int(c[np.argmax(X[c] @ U[q] / np.linalg.norm(X[c], axis=1))])
+            X[N - 1 - (q % 50)] = X[X_best]                     # same row under another index
+            c = np.unique(np.append(c, N - 1 - (q % 50)))
+        cand.append(np.sort(c).astype(np.int32))
+    cp = np.cumsum([0] + [len(c) for c in cand]).astype(np.int64)
+    ci = np.concatenate(cand).astype(np.int32)
+    xm = np.zeros(N); um = np.zeros(nq)
+    up = np.zeros(nq + 1, np.int64); ui = np.zeros(1, np.int32)
+    w_idx, w_sim, w_cnt = oracle.p_closest(X, U, cp, ci, P)
+    idx, sim, cnt, _ = run_gpu(ctx, X, xm, U, um, up, ui[:0], cp, ci, P, 1)
+    assert np.array_equal(cnt, w_cnt)
+    assert np.array_equal(idx, w_idx)
+    assert np.array_equal(sim.view(np.uint64), w_sim.view(np.uint64))
