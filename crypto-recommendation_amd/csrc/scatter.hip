@@ -206,7 +206,7 @@ int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, cons
         hipLaunchKernelGGL(rs_upsweep, dim3((unsigned)nblocks), dim3(RS_THREADS), 0, s, kin, kst, N, shift, nbins,
                            (int)nblocks, hist);
         const int64_t M = (int64_t)nbins * nblocks;
-        if (M <= 4 * RS_SC) {
+        if (M <= RS_SC) {
             hipLaunchKernelGGL(rs_scan, dim3(1), dim3(1024), 0, s, hist, M);
         } else {
             uint32_t* part = hist + M;
