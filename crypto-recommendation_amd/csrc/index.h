@@ -51,6 +51,7 @@ struct lshkm_ctx_s {
     // range assignment workspace (lshkm_range_assign)
     lshkm::Buf ws_range[12];
     lshkm::Buf ws_scan;          // multi-block scans of large query size arrays
+    uint64_t ws_epoch = 0;       // bumped by every user of the ws[] slots (api_index.cpp reserve)
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
     bool timing = false;
     hipEvent_t tev[2] = {nullptr, nullptr};
@@ -85,6 +86,14 @@ struct lshkm_lsh_s {
     int built = 0;
     int64_t N = 0;
     lshkm::Buf tuples, bucket, row_ptr, idx;
+    // two-phase query: the sizing call's device state, reused by the filling
+    // call when nothing else touched the context's slots in between
+    bool q_valid = false;
+    uint64_t q_epoch = 0;
+    const void* q_Q = nullptr;
+    const void* q_alias = nullptr;
+    int64_t q_nq = 0, q_total = 0;
+    int q_filtered = 0;
 };
 
 struct lshkm_cube_s {

@@ -133,7 +133,11 @@ int lshkm_lsh_device_views(lshkm_lsh lsh, const int64_t** row_ptr_dev /*[L][nb+1
  * the reference's first-write-wins ID map (euclidean_phi_gen.hpp:94) then
  * filters with row r's tuple. May be NULL.
  * Two-phase: out_ptr_dev [nq+1] always written (prefix offsets); rows are
- * written to out_idx_dev only if total <= out_cap. *total_host = total rows. */
+ * written to out_idx_dev only if total <= out_cap. *total_host = total rows.
+ * A filling call (out_idx_dev != NULL) right after a sizing call (NULL) with
+ * the same Q_dev, nq, alias_rows_dev and filtered -- and no other call on the
+ * context's workspace in between -- reuses the sizing call's device state
+ * (Q and alias contents must not change between the two calls). */
 int lshkm_lsh_query(lshkm_lsh lsh, const float* Q_dev, int64_t nq, const int32_t* alias_rows_dev,
                     int filtered, int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap,
                     int64_t* total_host);

@@ -300,3 +300,39 @@ def test_cube_query_load_balanced_copy_full(ctx, k, w):
     assert sz.max() > 4096 or np.median(sz) < 64            # the regime each case is for
     src = np.repeat(rp[seqs.ravel()] - slot_off[:-1], sz) + np.arange(slot_off[-1], dtype=np.int64)
     assert np.array_equal(out, bidx[src])
+
+
+def test_lsh_two_phase_reuse_guards(ctx):
+    # the filling call reuses the sizing call's state only for the same query
+    # batch with nothing in between; interleaved sizing calls must not leak
+    import ctypes as C
+    N, d, L, k = 50_000, 32, 5, 4
+    X = ctx.synth(77, N, d)
+    V, t, r, _ = lshkm.params_lsh_euclidean(3, L, k, d, 1.0)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 1.0, V=V, t=t, r=r)
+    lsh.build(X)
+    Q1, Q2 = X[:3000].clone(), X[20_000:24_000].clone()
+    want1 = lsh.query(Q1, True)
+    lib, p = lshkm.lib(), lshkm._t_ptr
+    for q in (Q1, Q2):
+        ptr = ctx.empty((q.shape[0] + 1,), ctx.torch.int64)
+        tot = C.c_int64()
+        lshkm._ck(lib.lshkm_lsh_query(lsh.h, p(q), q.shape[0], None, 1, p(ptr), None, 0, C.byref(tot)))
+    # state now belongs to Q2: a fill for Q1 must recompute everything
+    ptr1 = ctx.empty((Q1.shape[0] + 1,), ctx.torch.int64)
+    out1 = ctx.empty((max(len(want1[1]), 1),), ctx.torch.int32)
+    tot = C.c_int64()
+    lshkm._ck(lib.lshkm_lsh_query(lsh.h, p(Q1), Q1.shape[0], None, 1, p(ptr1), p(out1), out1.shape[0], C.byref(tot)))
+    ctx.sync()
+    assert tot.value == len(want1[1])
+    assert np.array_equal(ptr1.cpu().numpy(), want1[0]) and np.array_equal(out1.cpu().numpy()[:tot.value], want1[1])
+    # a sizing call, then another context user (k-means update scatter), then the fill
+    ptr2 = ctx.empty((Q1.shape[0] + 1,), ctx.torch.int64)
+    lshkm._ck(lib.lshkm_lsh_query(lsh.h, p(Q1), Q1.shape[0], None, 1, p(ptr2), None, 0, C.byref(tot)))
+    lsh2 = lshkm.LSH(ctx, "euclidean", d, k, L, N // 50, 1.0, V=V, t=t, r=r)
+    lsh2.build(X)                                       # reuses the context's scatter slots
+    lsh2.query(Q2, True)
+    out2 = ctx.empty((max(len(want1[1]), 1),), ctx.torch.int32)
+    lshkm._ck(lib.lshkm_lsh_query(lsh.h, p(Q1), Q1.shape[0], None, 1, p(ptr2), p(out2), out2.shape[0], C.byref(tot)))
+    ctx.sync()
+    assert np.array_equal(ptr2.cpu().numpy(), want1[0]) and np.array_equal(out2.cpu().numpy()[:tot.value], want1[1])
