@@ -25,10 +25,10 @@ using namespace lshkm;
 // ---------------------------------------------------------------- device buffers
 namespace lshkm {
 
-Buf::~Buf() { if (p) hipFree(p); }
+Buf::~Buf() { if (p) (void)hipFree(p); }
 int Buf::reserve(size_t bytes) {
     if (bytes <= cap) return 0;
-    if (p) { hipFree(p); p = nullptr; cap = 0; }
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
     if (hipMalloc(&p, bytes) != hipSuccess) { set_error("hipMalloc failed (" + std::to_string(bytes) + " B)"); p = nullptr; return LSHKM_ERR_NOMEM; }
     cap = bytes;
     return 0;
@@ -56,7 +56,7 @@ int lshkm_ctx_create(int device, lshkm_ctx* out) {
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; set_error("stream create failed"); return LSHKM_ERR_HIP; }
     c->stream = c->own_stream;
     if (c->stats.reserve(sizeof(unsigned long long) * STAT_COUNT)) { delete c; return LSHKM_ERR_NOMEM; }
-    hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * STAT_COUNT, c->stream);
+    (void)hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * STAT_COUNT, c->stream);
     *out = c;
     return 0;
 }
@@ -112,8 +112,8 @@ int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t
 
 int lshkm_ctx_destroy(lshkm_ctx ctx) {
     if (!ctx) return 0;
-    hipStreamSynchronize(ctx->stream);
-    if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return 0;
 }
@@ -243,9 +243,10 @@ int lshkm_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows) {
     return 0;
 }
 
-int lshkm_kmeans_pp(lshkm_ctx ctx, const float* X, int64_t N, int d, int K, int metric, uint64_t seed,
-                    int32_t* rows) {
-    LSHKM_CHECK(ctx && X && rows && N >= 1 && N <= INT32_MAX && d >= 1 && d <= 4096 && K >= 1, LSHKM_ERR_ARG,
+}  // extern "C"
+
+static int kmeans_pp_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, int K, int metric, uint64_t seed, int32_t* rows) {
+    LSHKM_CHECK(ctx && X.p && rows && N >= 1 && N <= INT32_MAX && d >= 1 && d <= 4096 && K >= 1, LSHKM_ERR_ARG,
                 "bad arguments (need N < 2^31, 1 <= d <= 4096, K >= 1)");
     LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
     LSHKM_HIP(hipSetDevice(ctx->device));
@@ -277,6 +278,18 @@ int lshkm_kmeans_pp(lshkm_ctx ctx, const float* X, int64_t N, int d, int K, int 
     LSHKM_HIP(hipMemcpyAsync(rows, dch.p, sizeof(int32_t) * K, hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     return 0;
+}
+
+extern "C" {
+
+int lshkm_kmeans_pp(lshkm_ctx ctx, const float* X, int64_t N, int d, int K, int metric, uint64_t seed,
+                    int32_t* rows) {
+    return kmeans_pp_impl(ctx, X, N, d, K, metric, seed, rows);
+}
+
+int lshkm_kmeans_pp_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, int K, int metric, uint64_t seed,
+                        int32_t* rows) {
+    return kmeans_pp_impl(ctx, X, N, d, K, metric, seed, rows);
 }
 
 int lshkm_params_cube_cosine(uint64_t seed, int k, int d, double* R, uint32_t* state) {
@@ -359,7 +372,6 @@ HashParams ProjTable::params(int64_t nb) const {
     p.r = (const int32_t*)r_d.p;
     p.w = w;
     p.d = d; p.L = L; p.k = k; p.LK = LK; p.LKpad = LKpad;
-    p.dstride = (d + 3) / 4 * 4 + 4;
     p.nb = nb;
     return p;
 }
@@ -401,8 +413,10 @@ int lshkm_lsh_destroy(lshkm_lsh lsh) {
     return 0;
 }
 
-int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, int32_t* phi, int32_t* bucket) {
-    LSHKM_CHECK(lsh && (X || N == 0) && N >= 0, LSHKM_ERR_ARG, "bad arguments");
+}  // extern "C"
+
+static int lsh_hash_impl(lshkm_lsh lsh, Pts X, int64_t N, int32_t* tuples, int32_t* phi, int32_t* bucket) {
+    LSHKM_CHECK(lsh && (X.p || N == 0) && N >= 0, LSHKM_ERR_ARG, "bad arguments");
     lshkm_ctx ctx = lsh->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
     const int mode = lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE;
@@ -413,6 +427,16 @@ int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, in
     return 0;
 }
 
+extern "C" {
+
+int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, int32_t* phi, int32_t* bucket) {
+    return lsh_hash_impl(lsh, X, N, tuples, phi, bucket);
+}
+
+int lshkm_lsh_hash_f64(lshkm_lsh lsh, const double* X, int64_t N, int32_t* tuples, int32_t* phi, int32_t* bucket) {
+    return lsh_hash_impl(lsh, X, N, tuples, phi, bucket);
+}
+
 // ------------------------------------------------------------------- Lloyd
 }  // extern "C"
 
@@ -420,12 +444,14 @@ int lshkm_lsh_hash(lshkm_lsh lsh, const float* X, int64_t N, int32_t* tuples, in
 // (persistent form, one launch per 256-centroid slice; cosine: normalised
 // centroids), else the f32-MFMA kernel (d <= 256), else the exact pass.
 // LSHKM_ASSIGN_PATH = "f32" / "exact" forces a path (tests compare them).
-static int assign_path(int metric, int d, int K) {
+// fp64 rows take the f32-MFMA kernel (rows rounded to f32 on load, the bound
+// widened accordingly) or the exact pass.
+static int assign_path(int metric, int d, int K, bool f64) {
     const char* e = getenv("LSHKM_ASSIGN_PATH");
     if (e && !strcmp(e, "exact")) return 2;
     const bool f32 = e && !strcmp(e, "f32");
     (void)K;
-    if (d == 128 && !f32) {
+    if (d == 128 && !f32 && !f64) {
         const char* ff = getenv("LSHKM_FUSED_FORM");
         if (metric == LSHKM_METRIC_EUCLIDEAN || !(ff && !strcmp(ff, "chunked"))) return 0;
     }
@@ -434,7 +460,7 @@ static int assign_path(int metric, int d, int K) {
 
 // Exact reference-order pass over the rows listed in ws_ambig (count on device).
 // Segmented lists (seg_counts != NULL) come from the persistent fused form.
-static int exact_listed(lshkm_ctx ctx, const float* X, int d, const double* C, int K, int metric,
+static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int metric,
                         const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist,
                         const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0) {
     const int32_t* rows = (const int32_t*)ctx->ws_ambig.p;
@@ -453,12 +479,12 @@ static int exact_listed(lshkm_ctx ctx, const float* X, int d, const double* C, i
                                     seg_counts, seg_rows, nseg);
 }
 
-static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
+static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, int K, int metric,
                        const int32_t* src_rows_host, int32_t* assign, double* dist, lshkm_lsh lsh, int32_t* tuples,
                        int32_t* phi, int32_t* bucket) {
     hipStream_t s = ctx->stream;
     const int DP = assign_dp(d);
-    const int path = assign_path(metric, d, K);
+    const int path = assign_path(metric, d, K, X.f64);
     const bool fuse_hash = lsh && path == 0 && metric == LSHKM_METRIC_EUCLIDEAN && lsh->proj.fused_ok;
     int rc;
     if (lsh && !fuse_hash && (rc = launch_proj_hash(s, lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE,
@@ -485,7 +511,7 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         double* nbv = (double*)(cnh + Kpad);               // cosine: [Kpad] sequential |c|^2 (Kpad % 64 == 0: aligned)
         if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv))) { LSHKM_LAUNCH_CHECK(); return rc; }
         FusedLaunch f;
-        f.X = X; f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C; f.Kpad = Kpad;
+        f.X = X.f(); f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C; f.Kpad = Kpad;
         f.assign = assign; f.dist = dist; f.ambig = (int32_t*)ctx->ws_ambig.p; f.ambig_count = cnt;
         f.stats = (unsigned long long*)ctx->stats.p;
         f.list_cap = N + FUSED_LIST_SLACK;
@@ -510,7 +536,7 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.seg_counts : nullptr,
                                f.seg_rows, f.nseg))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if (cosine && ((rc = launch_cos_fix_seg(s, X, C, f.hfix, f.seg_counts, f.seg_rows, f.nseg, assign, dist)) ||
+        if (cosine && ((rc = launch_cos_fix_seg(s, X.f(), C, f.hfix, f.seg_counts, f.seg_rows, f.nseg, assign, dist)) ||
                        (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1)))) { LSHKM_LAUNCH_CHECK(); return rc; }
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;
@@ -520,7 +546,7 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
         LSHKM_HIP(hipMemsetAsync(cnt, 0, 16, s));
-        if ((rc = launch_centroid_prep(s, C, K, Kpad, d, DP, metric, (float*)ctx->ws_c32.p, (float*)ctx->ws_cconst.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = launch_centroid_prep(s, C, K, Kpad, d, DP, metric, X.f64, (float*)ctx->ws_c32.p, (float*)ctx->ws_cconst.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_assign_mfma(s, X, N, d, DP, C, K, Kpad, metric, (const float*)ctx->ws_c32.p, (const float*)ctx->ws_cconst.p,
                                      assign, dist, (int32_t*)ctx->ws_ambig.p, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
@@ -547,20 +573,18 @@ static int assign_impl(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
     return 0;
 }
 
-extern "C" {
-
-int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
-                       const int32_t* src_rows_host, int32_t* assign, double* dist) {
-    LSHKM_CHECK(ctx && (X || N == 0) && C && (assign || N == 0) && (dist || N == 0) && N >= 0 && d > 0 && K > 0,
+static int lloyd_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, int K, int metric,
+                      const int32_t* src_rows_host, int32_t* assign, double* dist) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && C && (assign || N == 0) && (dist || N == 0) && N >= 0 && d > 0 && K > 0,
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
     LSHKM_HIP(hipSetDevice(ctx->device));
     return assign_impl(ctx, X, N, d, C, K, metric, src_rows_host, assign, dist, nullptr, nullptr, nullptr, nullptr);
 }
 
-int lshkm_hash_assign(lshkm_lsh lsh, const float* X, int64_t N, const double* C, int K, const int32_t* src_rows_host,
-                      int32_t* tuples, int32_t* phi, int32_t* bucket, int32_t* assign, double* dist) {
-    LSHKM_CHECK(lsh && (X || N == 0) && C && (assign || N == 0) && (dist || N == 0) && N >= 0 && K > 0, LSHKM_ERR_ARG,
+static int hash_assign_impl(lshkm_lsh lsh, Pts X, int64_t N, const double* C, int K, const int32_t* src_rows_host,
+                            int32_t* tuples, int32_t* phi, int32_t* bucket, int32_t* assign, double* dist) {
+    LSHKM_CHECK(lsh && (X.p || N == 0) && C && (assign || N == 0) && (dist || N == 0) && N >= 0 && K > 0, LSHKM_ERR_ARG,
                 "bad arguments");
     lshkm_ctx ctx = lsh->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
@@ -568,10 +592,10 @@ int lshkm_hash_assign(lshkm_lsh lsh, const float* X, int64_t N, const double* C,
                        phi, bucket);
 }
 
-int lshkm_range_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
-                       const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key_host,
-                       const int32_t* src_rows_host, int32_t* assign, double* dist, int* passes_host) {
-    LSHKM_CHECK(ctx && (X || N == 0) && C && comb_ptr && (assign || N == 0) && (dist || N == 0) && N >= 0 &&
+static int range_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, int K, int metric,
+                      const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key_host,
+                      const int32_t* src_rows_host, int32_t* assign, double* dist, int* passes_host) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && C && comb_ptr && (assign || N == 0) && (dist || N == 0) && N >= 0 &&
                     N < (1ll << 31) && d > 0 && K > 0,
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
@@ -636,11 +660,11 @@ int lshkm_range_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
         LSHKM_HIP(hipMemcpyAsync(&U, ucnt, 8, hipMemcpyDeviceToHost, s));
         LSHKM_HIP(hipStreamSynchronize(s));
         if (U > 0) {
-            if ((rc = w[7].reserve((size_t)U * d * 4)) || (rc = w[8].reserve((size_t)U * 12))) return rc;
-            float* Xr = (float*)w[7].p;
+            if ((rc = w[7].reserve((size_t)U * d * X.esize())) || (rc = w[8].reserve((size_t)U * 12))) return rc;
             double* dr = (double*)w[8].p;
             int32_t* ar = (int32_t*)(dr + U);
-            if ((rc = launch_range_gather(s, X, d, list, (int64_t)U, Xr))) return rc;
+            if ((rc = launch_range_gather(s, X, d, list, (int64_t)U, w[7].p))) return rc;
+            const Pts Xr = X.f64 ? Pts(w[7].as<double>()) : Pts(w[7].as<float>());
             if ((rc = assign_impl(ctx, Xr, (int64_t)U, d, C, K, metric, nullptr, ar, dr, nullptr, nullptr, nullptr,
                                   nullptr)))
                 return rc;
@@ -657,6 +681,43 @@ int lshkm_range_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const do
     if (key_host) LSHKM_HIP(hipStreamSynchronize(s));
     if (passes_host) *passes_host = passes;
     return 0;
+}
+
+extern "C" {
+
+int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
+                       const int32_t* src_rows_host, int32_t* assign, double* dist) {
+    return lloyd_impl(ctx, X, N, d, C, K, metric, src_rows_host, assign, dist);
+}
+
+int lshkm_lloyd_assign_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const double* C, int K, int metric,
+                           const int32_t* src_rows_host, int32_t* assign, double* dist) {
+    return lloyd_impl(ctx, X, N, d, C, K, metric, src_rows_host, assign, dist);
+}
+
+int lshkm_hash_assign(lshkm_lsh lsh, const float* X, int64_t N, const double* C, int K, const int32_t* src_rows_host,
+                      int32_t* tuples, int32_t* phi, int32_t* bucket, int32_t* assign, double* dist) {
+    return hash_assign_impl(lsh, X, N, C, K, src_rows_host, tuples, phi, bucket, assign, dist);
+}
+
+int lshkm_hash_assign_f64(lshkm_lsh lsh, const double* X, int64_t N, const double* C, int K,
+                          const int32_t* src_rows_host, int32_t* tuples, int32_t* phi, int32_t* bucket,
+                          int32_t* assign, double* dist) {
+    return hash_assign_impl(lsh, X, N, C, K, src_rows_host, tuples, phi, bucket, assign, dist);
+}
+
+int lshkm_range_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,
+                       const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key_host,
+                       const int32_t* src_rows_host, int32_t* assign, double* dist, int* passes_host) {
+    return range_impl(ctx, X, N, d, C, K, metric, comb_ptr, comb_idx, key_host, src_rows_host, assign, dist,
+                      passes_host);
+}
+
+int lshkm_range_assign_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const double* C, int K, int metric,
+                           const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key_host,
+                           const int32_t* src_rows_host, int32_t* assign, double* dist, int* passes_host) {
+    return range_impl(ctx, X, N, d, C, K, metric, comb_ptr, comb_idx, key_host, src_rows_host, assign, dist,
+                      passes_host);
 }
 
 int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X) {

@@ -27,6 +27,12 @@ int reserve(lshkm_ctx ctx, int i, size_t bytes) {
     return ctx->ws[i].reserve(std::max<size_t>(bytes, 64));
 }
 
+// the scan workspace is context state too: its users bump the epoch as well
+int reserve_scan(lshkm_ctx ctx, size_t bytes) {
+    ctx->ws_epoch++;
+    return ctx->ws_scan.reserve(bytes);
+}
+
 int d2h(lshkm_ctx ctx, void* dst, const void* src, size_t bytes) {
     LSHKM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
@@ -73,11 +79,9 @@ std::vector<int32_t> probe_masks(int probes, int k) {
 
 }  // namespace
 
-extern "C" {
-
 // ----------------------------------------------------------------------- LSH
-int lshkm_lsh_build(lshkm_lsh lsh, const float* X, int64_t N) {
-    LSHKM_CHECK(lsh && (X || N == 0) && N >= 0 && N < (1ll << 31), LSHKM_ERR_ARG, "bad arguments");
+static int lsh_build_impl(lshkm_lsh lsh, Pts X, int64_t N) {
+    LSHKM_CHECK(lsh && (X.p || N == 0) && N >= 0 && N < (1ll << 31), LSHKM_ERR_ARG, "bad arguments");
     lshkm_ctx ctx = lsh->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
     const int L = lsh->proj.L, k = lsh->proj.k;
@@ -99,6 +103,11 @@ int lshkm_lsh_build(lshkm_lsh lsh, const float* X, int64_t N) {
     return 0;
 }
 
+extern "C" {
+
+int lshkm_lsh_build(lshkm_lsh lsh, const float* X, int64_t N) { return lsh_build_impl(lsh, X, N); }
+int lshkm_lsh_build_f64(lshkm_lsh lsh, const double* X, int64_t N) { return lsh_build_impl(lsh, X, N); }
+
 int lshkm_lsh_get_buckets(lshkm_lsh lsh, int table, int64_t* row_ptr, int32_t* idx) {
     LSHKM_CHECK(lsh && lsh->built && table >= 0 && table < lsh->proj.L, LSHKM_ERR_ARG, "not built / bad table");
     lshkm_ctx ctx = lsh->ctx;
@@ -119,10 +128,12 @@ int lshkm_lsh_device_views(lshkm_lsh lsh, const int64_t** row_ptr, const int32_t
     return 0;
 }
 
-int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* alias, int filtered, int64_t* out_ptr,
-                    int32_t* out_idx, int64_t out_cap, int64_t* total_host) {
+}  // extern "C"
+
+static int lsh_query_impl(lshkm_lsh lsh, Pts Q, int64_t nq, const int32_t* alias, int filtered, int64_t* out_ptr,
+                          int32_t* out_idx, int64_t out_cap, int64_t* total_host) {
     LSHKM_CHECK(lsh && lsh->built, LSHKM_ERR_STATE, "index not built (lshkm_lsh_build)");
-    LSHKM_CHECK((Q || nq == 0) && nq >= 0 && out_ptr && total_host, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK((Q.p || nq == 0) && nq >= 0 && out_ptr && total_host, LSHKM_ERR_ARG, "bad arguments");
     lshkm_ctx ctx = lsh->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -130,11 +141,12 @@ int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* al
     const int64_t nb = lsh->nb, pairs = nq * L;
     const bool eu = lsh->metric == LSHKM_METRIC_EUCLIDEAN;
     int rc;
-    // the filling call of the two-phase protocol (same Q, nq, alias, filtered,
-    // out_ptr filled by the sizing call just before, nothing else on the
-    // context's slots in between): only the merge runs again
-    const bool reuse = out_idx && lsh->q_valid && lsh->q_epoch == ctx->ws_epoch && lsh->q_Q == Q && lsh->q_nq == nq &&
-                       lsh->q_alias == alias && lsh->q_filtered == filtered;
+    // the filling call of the two-phase protocol (same Q, nq, alias, filtered
+    // and out_ptr buffer -- whose prefix offsets the sizing call just wrote --,
+    // nothing else on the context's slots in between): only the merge runs again
+    const bool reuse = out_idx && lsh->q_valid && lsh->q_epoch == ctx->ws_epoch && lsh->q_Q == Q.p &&
+                       lsh->q_f64 == Q.f64 && lsh->q_nq == nq && lsh->q_alias == alias &&
+                       lsh->q_filtered == filtered && lsh->q_out_ptr == out_ptr;
     lsh->q_valid = false;
     if (nq == 0) {
         LSHKM_HIP(hipMemsetAsync(out_ptr, 0, 8, s));
@@ -149,7 +161,7 @@ int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* al
                                    lsh->bucket.as<int32_t>(), lsh->row_ptr.as<int64_t>(), lsh->idx.as<int32_t>(),
                                    slot<int64_t>(ctx, WS_SIZES), slot<int64_t>(ctx, WS_COFF), slot<int32_t>(ctx, WS_KLIST),
                                    slot<int64_t>(ctx, WS_KCNT), slot<int64_t>(ctx, WS_QSZ), out_ptr, out_idx, 2,
-                                   ctx->ws_scan.as<int64_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                                   nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
         return 0;
     }
     if ((rc = reserve(ctx, WS_QTUP, (size_t)pairs * k * 4)) || (rc = reserve(ctx, WS_QBKT, (size_t)pairs * 4)) ||
@@ -160,7 +172,7 @@ int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* al
                                          eu ? slot<int32_t>(ctx, WS_QTUP) : nullptr, nullptr, slot<int32_t>(ctx, WS_QBKT),
                                          (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
     auto run = [&](int phase, int32_t* out) {
-        if (ctx->ws_scan.reserve(scan_ws_bytes(nq * L + nq))) return LSHKM_ERR_NOMEM;
+        if (reserve_scan(ctx, scan_ws_bytes(nq * L + nq))) return LSHKM_ERR_NOMEM;
         return launch_lsh_query(s, slot<int32_t>(ctx, WS_QBKT), slot<int32_t>(ctx, WS_QTUP), alias, nq, L, k, nb,
                                 eu && filtered ? 1 : 0, lsh->N, eu ? lsh->tuples.as<int32_t>() : nullptr,
                                 lsh->bucket.as<int32_t>(), lsh->row_ptr.as<int64_t>(), lsh->idx.as<int32_t>(),
@@ -179,10 +191,22 @@ int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* al
     if (out_idx && total <= out_cap && total > 0)
         if ((rc = run(2, out_idx))) { LSHKM_LAUNCH_CHECK(); return rc; }
     if (!out_idx) {
-        lsh->q_valid = true; lsh->q_epoch = ctx->ws_epoch; lsh->q_Q = Q; lsh->q_nq = nq; lsh->q_alias = alias;
-        lsh->q_filtered = filtered; lsh->q_total = total;
+        lsh->q_valid = true; lsh->q_epoch = ctx->ws_epoch; lsh->q_Q = Q.p; lsh->q_f64 = Q.f64; lsh->q_nq = nq;
+        lsh->q_alias = alias; lsh->q_filtered = filtered; lsh->q_total = total; lsh->q_out_ptr = out_ptr;
     }
     return 0;
+}
+
+extern "C" {
+
+int lshkm_lsh_query(lshkm_lsh lsh, const float* Q, int64_t nq, const int32_t* alias, int filtered, int64_t* out_ptr,
+                    int32_t* out_idx, int64_t out_cap, int64_t* total_host) {
+    return lsh_query_impl(lsh, Q, nq, alias, filtered, out_ptr, out_idx, out_cap, total_host);
+}
+
+int lshkm_lsh_query_f64(lshkm_lsh lsh, const double* Q, int64_t nq, const int32_t* alias, int filtered,
+                        int64_t* out_ptr, int32_t* out_idx, int64_t out_cap, int64_t* total_host) {
+    return lsh_query_impl(lsh, Q, nq, alias, filtered, out_ptr, out_idx, out_cap, total_host);
 }
 
 // ----------------------------------------------------------------- hypercube
@@ -239,7 +263,7 @@ static int cube_ensure_window(lshkm_cube cube, int32_t lo_h, int32_t hi_h) {
 }
 
 // h of a batch (EuclideanH, k per row) into WS_H, and the memo window over it.
-static int cube_h_batch(lshkm_cube cube, const float* X, int64_t N, int32_t** h_out) {
+static int cube_h_batch(lshkm_cube cube, Pts X, int64_t N, int32_t** h_out) {
     lshkm_ctx ctx = cube->ctx;
     hipStream_t s = ctx->stream;
     const int k = cube->k;
@@ -279,7 +303,7 @@ static int cube_unseen_impl(lshkm_cube cube, const int32_t* h, int64_t N, unsign
     return d2h(ctx, n, cube->cnt.p, 4);
 }
 
-static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_t* vertex) {
+static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex) {
     lshkm_ctx ctx = cube->ctx;
     hipStream_t s = ctx->stream;
     const int k = cube->k;
@@ -307,9 +331,9 @@ static int cube_vertices_impl(lshkm_cube cube, const float* X, int64_t N, int32_
 }
 
 // ---- sharded EuclideanF coins: export, host draw, import
-int lshkm_cube_unseen(lshkm_cube cube, const float* X, int64_t N, int32_t* f_host, int32_t* h_host,
-                      int64_t* row_host, int64_t cap, int64_t* count_host) {
-    LSHKM_CHECK(cube && (X || N == 0) && N >= 0 && N < (1ll << 31) && count_host && (cap == 0 || (f_host && h_host && row_host)),
+static int cube_unseen_api(lshkm_cube cube, Pts X, int64_t N, int32_t* f_host, int32_t* h_host, int64_t* row_host,
+                           int64_t cap, int64_t* count_host) {
+    LSHKM_CHECK(cube && (X.p || N == 0) && N >= 0 && N < (1ll << 31) && count_host && (cap == 0 || (f_host && h_host && row_host)),
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_CHECK(cube->metric == LSHKM_METRIC_EUCLIDEAN, LSHKM_ERR_ARG, "coins exist only for the euclidean cube");
     lshkm_ctx ctx = cube->ctx;
@@ -332,6 +356,16 @@ int lshkm_cube_unseen(lshkm_cube cube, const float* X, int64_t N, int32_t* f_hos
         h_host[i] = cube->hmin + offs[i] % cube->hspan;
     }
     return 0;
+}
+
+int lshkm_cube_unseen(lshkm_cube cube, const float* X, int64_t N, int32_t* f_host, int32_t* h_host,
+                      int64_t* row_host, int64_t cap, int64_t* count_host) {
+    return cube_unseen_api(cube, X, N, f_host, h_host, row_host, cap, count_host);
+}
+
+int lshkm_cube_unseen_f64(lshkm_cube cube, const double* X, int64_t N, int32_t* f_host, int32_t* h_host,
+                          int64_t* row_host, int64_t cap, int64_t* count_host) {
+    return cube_unseen_api(cube, X, N, f_host, h_host, row_host, cap, count_host);
 }
 
 int lshkm_cube_import_coins(lshkm_cube cube, const int32_t* f_host, const int32_t* h_host, const int32_t* bit_host,
@@ -368,8 +402,8 @@ int lshkm_cube_import_coins(lshkm_cube cube, const int32_t* f_host, const int32_
     return 0;
 }
 
-int lshkm_cube_build(lshkm_cube cube, const float* X, int64_t N) {
-    LSHKM_CHECK(cube && (X || N == 0) && N >= 0 && N < (1ll << 31), LSHKM_ERR_ARG, "bad arguments");
+static int cube_build_impl(lshkm_cube cube, Pts X, int64_t N) {
+    LSHKM_CHECK(cube && (X.p || N == 0) && N >= 0 && N < (1ll << 31), LSHKM_ERR_ARG, "bad arguments");
     lshkm_ctx ctx = cube->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
     const int64_t nb = 1ll << cube->k;
@@ -384,10 +418,21 @@ int lshkm_cube_build(lshkm_cube cube, const float* X, int64_t N) {
     return 0;
 }
 
-int lshkm_cube_vertices(lshkm_cube cube, const float* Q, int64_t nq, int32_t* vertex) {
-    LSHKM_CHECK(cube && (Q || nq == 0) && nq >= 0 && (vertex || nq == 0), LSHKM_ERR_ARG, "bad arguments");
+int lshkm_cube_build(lshkm_cube cube, const float* X, int64_t N) { return cube_build_impl(cube, X, N); }
+int lshkm_cube_build_f64(lshkm_cube cube, const double* X, int64_t N) { return cube_build_impl(cube, X, N); }
+
+static int cube_vertices_api(lshkm_cube cube, Pts Q, int64_t nq, int32_t* vertex) {
+    LSHKM_CHECK(cube && (Q.p || nq == 0) && nq >= 0 && (vertex || nq == 0), LSHKM_ERR_ARG, "bad arguments");
     LSHKM_HIP(hipSetDevice(cube->ctx->device));
     return cube_vertices_impl(cube, Q, nq, vertex);
+}
+
+int lshkm_cube_vertices(lshkm_cube cube, const float* Q, int64_t nq, int32_t* vertex) {
+    return cube_vertices_api(cube, Q, nq, vertex);
+}
+
+int lshkm_cube_vertices_f64(lshkm_cube cube, const double* Q, int64_t nq, int32_t* vertex) {
+    return cube_vertices_api(cube, Q, nq, vertex);
 }
 
 int lshkm_cube_get_buckets(lshkm_cube cube, int64_t* row_ptr, int32_t* idx) {
@@ -398,10 +443,10 @@ int lshkm_cube_get_buckets(lshkm_cube cube, int64_t* row_ptr, int32_t* idx) {
     return 0;
 }
 
-int lshkm_cube_query(lshkm_cube cube, const float* Q, int64_t nq, int probes, int64_t* out_ptr, int32_t* out_idx,
-                     int64_t out_cap, int64_t* total_host) {
+static int cube_query_impl(lshkm_cube cube, Pts Q, int64_t nq, int probes, int64_t* out_ptr, int32_t* out_idx,
+                           int64_t out_cap, int64_t* total_host) {
     LSHKM_CHECK(cube && cube->built, LSHKM_ERR_STATE, "cube not built (lshkm_cube_build)");
-    LSHKM_CHECK((Q || nq == 0) && nq >= 0 && out_ptr && total_host, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK((Q.p || nq == 0) && nq >= 0 && out_ptr && total_host, LSHKM_ERR_ARG, "bad arguments");
     lshkm_ctx ctx = cube->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -415,7 +460,7 @@ int lshkm_cube_query(lshkm_cube cube, const float* Q, int64_t nq, int probes, in
     }
     if ((rc = reserve(ctx, WS_QBKT, (size_t)nq * 4)) || (rc = reserve(ctx, WS_MASKS, (size_t)S * 4)) ||
         (rc = reserve(ctx, WS_QSZ, (size_t)nq * S * 8)) || (rc = reserve(ctx, WS_CROW, (size_t)(nq * S + 1) * 8)) ||
-        (rc = ctx->ws_scan.reserve(scan_ws_bytes(nq * S))))
+        (rc = reserve_scan(ctx, scan_ws_bytes(nq * S))))
         return rc;
     if ((rc = cube_vertices_impl(cube, Q, nq, slot<int32_t>(ctx, WS_QBKT)))) return rc;
     LSHKM_HIP(hipMemcpyAsync(ctx->ws[WS_MASKS].p, masks.data(), (size_t)S * 4, hipMemcpyHostToDevice, s));
@@ -430,6 +475,16 @@ int lshkm_cube_query(lshkm_cube cube, const float* Q, int64_t nq, int probes, in
                                     cube->row_ptr.as<int64_t>(), cube->idx.as<int32_t>(), slot<int64_t>(ctx, WS_QSZ),
                                     slot<int64_t>(ctx, WS_CROW), out_ptr, out_idx, ctx->ws_scan.as<int64_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;
+}
+
+int lshkm_cube_query(lshkm_cube cube, const float* Q, int64_t nq, int probes, int64_t* out_ptr, int32_t* out_idx,
+                     int64_t out_cap, int64_t* total_host) {
+    return cube_query_impl(cube, Q, nq, probes, out_ptr, out_idx, out_cap, total_host);
+}
+
+int lshkm_cube_query_f64(lshkm_cube cube, const double* Q, int64_t nq, int probes, int64_t* out_ptr,
+                         int32_t* out_idx, int64_t out_cap, int64_t* total_host) {
+    return cube_query_impl(cube, Q, nq, probes, out_ptr, out_idx, out_cap, total_host);
 }
 
 int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f, int32_t* h, int32_t* bit, int64_t cap, int64_t* count,
@@ -459,7 +514,7 @@ int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f, int32_t* h, int32_t* bit, i
 }
 
 // ------------------------------------------------------------------- k-means
-static int km_sums(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K, double* sums,
+static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign, int K, double* sums,
                    int64_t* counts, const double* carry = nullptr, const int64_t* carry_counts = nullptr) {
     int rc;
     if ((rc = reserve(ctx, WS_ROWS, (size_t)std::max<int64_t>(N, 1) * 4)) || (rc = reserve(ctx, WS_CROW, (size_t)(K + 1) * 8)))
@@ -491,9 +546,9 @@ static int km_finalize(lshkm_ctx ctx, const double* sums, const int64_t* counts,
     return 0;
 }
 
-int lshkm_kmeans_update(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, const double* C_old,
-                        int K, int metric, double min_dist, double* C_new, int64_t* counts, int* cont) {
-    LSHKM_CHECK(ctx && (X || N == 0) && assign && C_old && C_new && N >= 0 && N < (1ll << 31) && d > 0 && K > 0,
+static int kmeans_update_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign, const double* C_old,
+                              int K, int metric, double min_dist, double* C_new, int64_t* counts, int* cont) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && assign && C_old && C_new && N >= 0 && N < (1ll << 31) && d > 0 && K > 0,
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_HIP(hipSetDevice(ctx->device));
     int rc;
@@ -503,22 +558,55 @@ int lshkm_kmeans_update(lshkm_ctx ctx, const float* X, int64_t N, int d, const i
     return km_finalize(ctx, slot<double>(ctx, WS_SUMS), cnt, K, d, C_old, metric, min_dist, C_new, cont);
 }
 
-int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K, double* sums,
-                         int64_t* counts) {
-    LSHKM_CHECK(ctx && (X || N == 0) && assign && sums && counts && N >= 0 && N < (1ll << 31) && d > 0 && K > 0,
+static int kmeans_partial_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign, int K, double* sums,
+                               int64_t* counts) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && assign && sums && counts && N >= 0 && N < (1ll << 31) && d > 0 && K > 0,
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_HIP(hipSetDevice(ctx->device));
     return km_sums(ctx, X, N, d, assign, K, sums, counts);
 }
 
-int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K,
-                               const double* carry_sums, const int64_t* carry_counts, double* sums, int64_t* counts) {
-    LSHKM_CHECK(ctx && (X || N == 0) && (assign || N == 0) && sums && counts && N >= 0 && N < (1ll << 31) && d > 0 &&
+static int kmeans_partial_carry_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign, int K,
+                                     const double* carry_sums, const int64_t* carry_counts, double* sums,
+                                     int64_t* counts) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && (assign || N == 0) && sums && counts && N >= 0 && N < (1ll << 31) && d > 0 &&
                     K > 0,
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_CHECK(sums != carry_sums, LSHKM_ERR_ARG, "sums must not alias carry_sums");
     LSHKM_HIP(hipSetDevice(ctx->device));
     return km_sums(ctx, X, N, d, assign, K, sums, counts, carry_sums, carry_counts);
+}
+
+int lshkm_kmeans_update(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, const double* C_old,
+                        int K, int metric, double min_dist, double* C_new, int64_t* counts, int* cont) {
+    return kmeans_update_impl(ctx, X, N, d, assign, C_old, K, metric, min_dist, C_new, counts, cont);
+}
+
+int lshkm_kmeans_update_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int32_t* assign,
+                            const double* C_old, int K, int metric, double min_dist, double* C_new, int64_t* counts,
+                            int* cont) {
+    return kmeans_update_impl(ctx, X, N, d, assign, C_old, K, metric, min_dist, C_new, counts, cont);
+}
+
+int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K, double* sums,
+                         int64_t* counts) {
+    return kmeans_partial_impl(ctx, X, N, d, assign, K, sums, counts);
+}
+
+int lshkm_kmeans_partial_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int32_t* assign, int K,
+                             double* sums, int64_t* counts) {
+    return kmeans_partial_impl(ctx, X, N, d, assign, K, sums, counts);
+}
+
+int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K,
+                               const double* carry_sums, const int64_t* carry_counts, double* sums, int64_t* counts) {
+    return kmeans_partial_carry_impl(ctx, X, N, d, assign, K, carry_sums, carry_counts, sums, counts);
+}
+
+int lshkm_kmeans_partial_carry_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int32_t* assign, int K,
+                                   const double* carry_sums, const int64_t* carry_counts, double* sums,
+                                   int64_t* counts) {
+    return kmeans_partial_carry_impl(ctx, X, N, d, assign, K, carry_sums, carry_counts, sums, counts);
 }
 
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
@@ -528,9 +616,23 @@ int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums, const int64_t* coun
     return km_finalize(ctx, sums, counts, K, d, C_old, metric, min_dist, C_new, cont);
 }
 
-int lshkm_silhouette(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, const double* C, int K,
-                     int metric, double* out_host, double* s_dev) {
-    LSHKM_CHECK(ctx && (X || N == 0) && (assign || N == 0) && C && out_host && N >= 0 && N < (1ll << 31) && d > 0 &&
+// separate_clusters_from_input (utils.hpp:150-158) as a CSR over the K clusters:
+// members of cluster c = rows_dev[crow_dev[c] .. crow_dev[c+1]) in row order.
+static int clusters_impl(lshkm_ctx ctx, const int32_t* assign, int64_t N, int K, int64_t* crow, int32_t* rows) {
+    return build_csr(ctx, assign, 1, N, K, rows, crow);
+}
+
+int lshkm_clusters(lshkm_ctx ctx, const int32_t* assign_dev, int64_t N, int K, int64_t* crow_dev, int32_t* rows_dev) {
+    LSHKM_CHECK(ctx && (assign_dev || N == 0) && crow_dev && (rows_dev || N == 0) && N >= 0 && N < (1ll << 31) &&
+                    K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    return clusters_impl(ctx, assign_dev, N, K, crow_dev, rows_dev);
+}
+
+static int silhouette_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign, const double* C, int K,
+                           int metric, double* out_host, double* s_dev) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && (assign || N == 0) && C && out_host && N >= 0 && N < (1ll << 31) && d > 0 &&
                     K > 0,
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
@@ -555,6 +657,16 @@ int lshkm_silhouette(lshkm_ctx ctx, const float* X, int64_t N, int d, const int3
         return rc;
     if ((rc = launch_sil_sum(s, sv, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, N, raw, out))) return rc;
     return d2h(ctx, out_host, out, (size_t)(K + 1) * 8);
+}
+
+int lshkm_silhouette(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, const double* C, int K,
+                     int metric, double* out_host, double* s_dev) {
+    return silhouette_impl(ctx, X, N, d, assign, C, K, metric, out_host, s_dev);
+}
+
+int lshkm_silhouette_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int32_t* assign, const double* C,
+                         int K, int metric, double* out_host, double* s_dev) {
+    return silhouette_impl(ctx, X, N, d, assign, C, K, metric, out_host, s_dev);
 }
 
 }  // extern "C"

@@ -40,7 +40,7 @@ int assign_dp(int d) {
 }
 
 __global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, int DP, int metric,
-                                     float* __restrict__ C32, float* __restrict__ cconst) {
+                                     int xf64, float* __restrict__ C32, float* __restrict__ cconst) {
     // One wave per 64-centroid chunk. cconst = cn2[Kpad] ++ {ecmax, ebmax}[Kpad/64]:
     // the bound coefficients are taken as the max over the chunk, so the MFMA
     // epilogue needs one per-lane bound per chunk instead of per centroid.
@@ -49,7 +49,11 @@ __global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kp
     // (the f32 chain, c's f32 rounding, 1/|c| and the product's rounding), plus
     // 2^-40 |x| over the reference's last-bit roundings of 1 - ip / denom; a zero
     // centroid (and padding) gets NaN: never taken, never lowers the bound min.
+    // fp64 rows (xf64) reach the MFMA rounded to f32: |x_j - f32(x_j)| <= 2^-24 |x_j|
+    // + 2^-150, i.e. 2 2^-24 |x||c| more on the euclidean score (2^-24 |x| on the
+    // cosine one) plus 2^-150 |c|_1 <= 2^-146 |c| (flushed tiny entries).
     const int c = blockIdx.x * 64 + threadIdx.x;
+    const double xw = xf64 ? 2.0 : 0.0;
     float* cn2 = cconst;
     float* chunk = cconst + Kpad + 2 * blockIdx.x;
     double ec = 0.0, eb = 0.0;
@@ -67,9 +71,12 @@ __global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kp
         const double up = 1.0 + 0x1p-18;
         const double nc = sqrt(s) * (1.0 + 0x1p-30);
         if (metric == 0) {
-            cn2[c] = (float)s;
-            ec = 0x1p-24 * (2.0 * DP + 12.0) * nc * up;
-            eb = (0x1p-24 * 5.0 * s + 0x1p-40 * s) * up + 1e-30;
+            // |c| >= 2^50 (or non-finite) may overflow the f32 chain: no
+            // certificate in this call (flag after the chunk bounds)
+            cn2[c] = s < 0x1p100 ? (float)s : __builtin_inff();
+            if (!(s < 0x1p100)) atomicOr(reinterpret_cast<unsigned int*>(cconst + Kpad + Kpad / 32), 1u);
+            ec = 0x1p-24 * (2.0 * DP + 12.0 + xw) * nc * up;
+            eb = (0x1p-24 * 5.0 * s + 0x1p-40 * s + (xf64 ? 0x1p-140 * nc : 0.0)) * up + 1e-30;
         } else {
             // 1e-20 <= |c|^2 < 1e30 keeps the f32 chain clear of overflow and of
             // flushed denormals beyond eb ((DP + 4) 2^-124 / |c| for products and
@@ -79,7 +86,7 @@ __global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kp
             const bool ok = s >= 1e-20 && s < 1e30;
             const double rc = ok ? 1.0 / sqrt(s) : 0.0;
             cn2[c] = ok ? (float)rc : __builtin_nanf("");
-            ec = (0x1p-24 * (DP + 20.0) + 0x1p-40) * up;
+            ec = (0x1p-24 * (DP + 20.0 + xw) + 0x1p-40) * up;
             eb = ok ? ((DP + 4.0) * 0x1p-124 * rc + 0x1p-116) * up
                     : (s == 0.0 && c > 0 ? 0.0 : __builtin_inf());
         }
@@ -94,16 +101,17 @@ __global__ void centroid_prep_kernel(const double* __restrict__ C, int K, int Kp
     }
 }
 
-int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d, int DP, int metric,
+int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d, int DP, int metric, bool xf64,
                          float* C32, float* cconst) {
-    hipLaunchKernelGGL(centroid_prep_kernel, dim3((Kpad + 63) / 64), dim3(64), 0, s, C, K, Kpad, d, DP, metric, C32,
-                       cconst);
+    (void)hipMemsetAsync(cconst + Kpad + Kpad / 32, 0, 4, s);
+    hipLaunchKernelGGL(centroid_prep_kernel, dim3((Kpad + 63) / 64), dim3(64), 0, s, C, K, Kpad, d, DP, metric,
+                       xf64 ? 1 : 0, C32, cconst);
     return kstatus("assign.hip");
 }
 
-template <int DP, int MET>
+template <int DP, int MET, typename TX>
 __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
-    const float* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int Kpad,
+    const TX* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int Kpad,
     const float* __restrict__ C32, const float* __restrict__ cconst, int32_t* __restrict__ assign,
     double* __restrict__ dist, int32_t* __restrict__ ambig, unsigned long long* __restrict__ ambig_count) {
     constexpr int H = DP / 2;     // dims per lane half
@@ -121,14 +129,20 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
             const int r = e4 / (DP / 4), j = (e4 % (DP / 4)) * 4;
             const int64_t row = pbase + r;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (row < N) v = *reinterpret_cast<const float4*>(X + row * DP + j);
+            if constexpr (sizeof(TX) == 4) {
+                if (row < N) v = *reinterpret_cast<const float4*>(X + row * DP + j);
+            } else if (row < N) {
+                const double2 a = *reinterpret_cast<const double2*>(X + row * DP + j);
+                const double2 b = *reinterpret_cast<const double2*>(X + row * DP + j + 2);
+                v = make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+            }
             *reinterpret_cast<float4*>(xs + r * DS + j) = v;
         }
     } else {
         for (int e = lane; e < 32 * DP; e += 64) {
             const int r = e / DP, j = e % DP;
             const int64_t row = pbase + r;
-            xs[r * DS + j] = (row < N && j < d) ? X[row * d + j] : 0.f;
+            xs[r * DS + j] = (row < N && j < d) ? (float)X[row * d + j] : 0.f;
         }
     }
     __syncthreads();
@@ -142,10 +156,13 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
 #pragma unroll
     for (int s = 0; s < H; s++) xn2 = fma((double)b[s], (double)b[s], xn2);
     xn2 += __shfl_xor(xn2, 32);
+    if (sizeof(TX) == 8) xn2 = xn2 * (1.0 + 0x1p-21) + 0x1p-280;   // |x|^2 from the f32-rounded row: still an upper bound
     const float nx = (float)(sqrt(xn2) * (1.0 + 0x1p-30));
     // cosine: |x| >= 1e18 may overflow the f32 products (|c| < 1e15 is checked
     // in the prep): no certificate, the row goes to the exact pass
-    const float ex = MET == 0 ? (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30)
+    // |x| >= 2^50 (euclidean) / 1e18 (cosine) may overflow the f32 products: no
+    // certificate, the row goes to the exact pass (false for inf / nan too)
+    const float ex = MET == 0 ? (xn2 < 0x1p100 ? (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30) : __builtin_inff())
                               : (xn2 < 1e36 ? 0.f : __builtin_inff());
     __syncthreads();   // LDS now reused for centroid chunks
 
@@ -202,7 +219,8 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
     if (oL1 < L1 || (oL1 == L1 && oi1 < i1)) { ni1 = oi1; nL2 = fminf(L1, oL2); }
     else { ni1 = i1; nL2 = fminf(oL1, L2); }
     U = fminf(U, oU);
-    const bool cert = nL2 > U;
+    const bool cbad = __float_as_uint(cconst[Kpad + Kpad / 32]) != 0u;   // centroid out of the f32 range
+    const bool cert = !cbad && nL2 > U;
     const int64_t row = pbase + col;
     const bool valid = row < N;
 
@@ -237,12 +255,14 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
         return;
     }
     double accd = 0.0;
+    const TX* xrow = X + (valid ? row : 0) * d;
     if (h == 0 && cert && valid) {
         const double* crow = C + (size_t)ni1 * d;
 #pragma unroll
         for (int s = 0; s < H; s++)
             if (s < d) {
-                const double df = __dsub_rn((double)b[s], crow[s]);
+                const double xv = sizeof(TX) == 4 ? (double)b[s] : (double)xrow[s];
+                const double df = __dsub_rn(xv, crow[s]);
                 accd = __dadd_rn(accd, __dmul_rn(df, df));
             }
     }
@@ -254,7 +274,8 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
 #pragma unroll
             for (int s = 0; s < H; s++)
                 if (H + s < d) {
-                    const double df = __dsub_rn((double)b[s], crow[H + s]);
+                    const double xv = sizeof(TX) == 4 ? (double)b[s] : (double)xrow[H + s];
+                    const double df = __dsub_rn(xv, crow[H + s]);
                     a2 = __dadd_rn(a2, __dmul_rn(df, df));
                 }
             assign[row] = ni1;
@@ -266,17 +287,16 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
     }
 }
 
-int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, const double* C, int K,
-                       int Kpad, int metric, const float* C32, const float* cconst, int32_t* assign, double* dist,
-                       int32_t* ambig, unsigned long long* ambig_count) {
-    (void)K;
-    if (N <= 0) return 0;
+template <typename TX>
+static int assign_mfma_tx(hipStream_t s, const TX* X, int64_t N, int d, int DP, const double* C, int Kpad, int metric,
+                          const float* C32, const float* cconst, int32_t* assign, double* dist, int32_t* ambig,
+                          unsigned long long* ambig_count) {
     const dim3 grid((unsigned)((N + AS_PB - 1) / AS_PB)), block(AS_THREADS);
     const size_t lds = (size_t)4 * 32 * (DP + 4) * 4;   // >= chunk (64*(DP+4) + 192) floats
     switch (DP * 2 + (metric ? 1 : 0)) {
 #define AS_CASE(V) \
-        case 2 * V: hipLaunchKernelGGL((assign_mfma_kernel<V, 0>), grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break; \
-        case 2 * V + 1: hipLaunchKernelGGL((assign_mfma_kernel<V, 1>), grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break;
+        case 2 * V: hipLaunchKernelGGL((assign_mfma_kernel<V, 0, TX>), grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break; \
+        case 2 * V + 1: hipLaunchKernelGGL((assign_mfma_kernel<V, 1, TX>), grid, block, lds, s, X, N, d, C, Kpad, C32, cconst, assign, dist, ambig, ambig_count); break;
         AS_CASE(16) AS_CASE(32) AS_CASE(64) AS_CASE(128) AS_CASE(256)
 #undef AS_CASE
         default: return -4;
@@ -284,9 +304,19 @@ int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, 
     return kstatus("assign.hip");
 }
 
+int launch_assign_mfma(hipStream_t s, Pts X, int64_t N, int d, int DP, const double* C, int K, int Kpad, int metric,
+                       const float* C32, const float* cconst, int32_t* assign, double* dist, int32_t* ambig,
+                       unsigned long long* ambig_count) {
+    (void)K;
+    if (N <= 0) return 0;
+    return X.f64 ? assign_mfma_tx(s, X.d(), N, d, DP, C, Kpad, metric, C32, cconst, assign, dist, ambig, ambig_count)
+                 : assign_mfma_tx(s, X.f(), N, d, DP, C, Kpad, metric, C32, cconst, assign, dist, ambig, ambig_count);
+}
+
 // Certified cosine winners whose distance IpAcc could not certify: one lane
 // per listed row, the soft-x87 chain (exact.h exact_cosine_x87).
-__global__ __launch_bounds__(256) void cos_fix_kernel(const float* __restrict__ X, int d, const double* __restrict__ C,
+template <typename TX>
+__global__ __launch_bounds__(256) void cos_fix_kernel(const TX* __restrict__ X, int d, const double* __restrict__ C,
                                                       const int32_t* __restrict__ rows,
                                                       const unsigned long long* __restrict__ count,
                                                       const int32_t* __restrict__ assign, double* __restrict__ dist) {
@@ -297,11 +327,12 @@ __global__ __launch_bounds__(256) void cos_fix_kernel(const float* __restrict__ 
     }
 }
 
-int launch_cos_fix(hipStream_t s, const float* X, int64_t N, int d, const double* C, const int32_t* rows,
+int launch_cos_fix(hipStream_t s, Pts X, int64_t N, int d, const double* C, const int32_t* rows,
                    const unsigned long long* count, const int32_t* assign, double* dist) {
     if (N <= 0) return 0;
-    hipLaunchKernelGGL(cos_fix_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 2048)), dim3(256), 0, s, X, d, C,
-                       rows, count, assign, dist);
+    const dim3 grid((unsigned)std::min<int64_t>((N + 255) / 256, 2048));
+    if (X.f64) hipLaunchKernelGGL(cos_fix_kernel<double>, grid, dim3(256), 0, s, X.d(), d, C, rows, count, assign, dist);
+    else hipLaunchKernelGGL(cos_fix_kernel<float>, grid, dim3(256), 0, s, X.f(), d, C, rows, count, assign, dist);
     return kstatus("assign.hip");
 }
 
@@ -310,8 +341,9 @@ constexpr int XC_MAXV = 4;   // cosine candidate form: K <= 256 (values kept per
 constexpr int XE_SPLIT = 2;  // blocks per list segment (segmented form)
 // One wave per listed row; lane c evaluates centroids c, c+64, ... in the
 // reference's exact order (exact.h); the first minimum wins.
+template <typename TX>
 __global__ __launch_bounds__(256) void assign_exact_kernel(
-    const float* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int K, int metric,
+    const TX* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int K, int metric,
     const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,
     int32_t* __restrict__ assign, double* __restrict__ dist, const int32_t* __restrict__ seg_counts,
     int64_t seg_rows) {
@@ -329,7 +361,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
     if (total > max_rows) total = max_rows;
     for (int64_t it = wglobal; it < total; it += nw) {
         const int64_t row = rows ? rows[it] : it;
-        const float* x = X + row * d;
+        const TX* x = X + row * d;
         double best = 0.0; int bi = -1;
         if (metric == 1 && K <= 64 * XC_MAXV) {
             // cosine: certified values (exact.h cosine_interval) for every
@@ -394,7 +426,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
     }
 }
 
-int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K, int metric,
+int launch_assign_exact(hipStream_t s, Pts X, int64_t N, int d, const double* C, int K, int metric,
                         const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                         int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
     if (max_rows <= 0) return 0;
@@ -402,8 +434,12 @@ int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const d
     // usually ~0.3% of the rows: one block per CU, waves loop over the list.
     const int64_t blocks = seg_counts ? (int64_t)nseg * XE_SPLIT : std::min<int64_t>((max_rows + 3) / 4, rows ? 256 : 2048);
     if (blocks <= 0) return 0;
-    hipLaunchKernelGGL(assign_exact_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, N, d, C, K, metric,
-                       rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+    if (X.f64)
+        hipLaunchKernelGGL(assign_exact_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s, X.d(), N, d, C, K,
+                           metric, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+    else
+        hipLaunchKernelGGL(assign_exact_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, X.f(), N, d, C, K,
+                           metric, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
     return kstatus("assign.hip");
 }
 
@@ -424,12 +460,13 @@ __global__ void transpose_centroids_kernel(const double* __restrict__ C, int K, 
     CT[e] = c < K ? C[(size_t)c * d + j] : 0.0;
 }
 
+template <typename TX>
 __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
-    const float* __restrict__ X, int d, const double* __restrict__ CT, int K, int Kpad,
+    const TX* __restrict__ X, int d, const double* __restrict__ CT, int K, int Kpad,
     const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,
     int32_t* __restrict__ assign, double* __restrict__ dist, const int32_t* __restrict__ seg_counts,
     int64_t seg_rows) {
-    __shared__ float xs[XB_WAVES][XB_R][XB_DMAX];
+    __shared__ TX xs[XB_WAVES][XB_R][XB_DMAX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int64_t total, g0, gstride;
     if (seg_counts) {            // XB_SPLIT blocks per segment (the one persistent block b wrote)
@@ -533,7 +570,8 @@ constexpr int XP_L = 64 / XP_R;      // lanes per row in the candidate phase
 
 // exact_euclid with the centroid row loaded 16 values at a time (one L2 round
 // trip per 16 terms instead of one per term); x in LDS.
-__device__ inline double exact_euclid_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
+template <typename TX>
+__device__ inline double exact_euclid_b16(const TX* __restrict__ x, const double* __restrict__ c, int d) {
     double acc = 0.0;
     for (int j0 = 0; j0 < d; j0 += 16) {
         double cv[16];
@@ -549,8 +587,8 @@ __device__ inline double exact_euclid_b16(const float* __restrict__ x, const dou
     return sqrt(acc);
 }
 
-__global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, float* __restrict__ CT32,
-                                  float* __restrict__ cconst) {
+__global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, int xf64,
+                                  float* __restrict__ CT32, float* __restrict__ cconst) {
     // one wave per centroid: CT32 [d][Kpad], cconst = cn2[Kpad] ++ {ec, eb}[Kpad/64]
     // (chunk maxima by atomicMax on the bits of positive floats; zeroed first)
     const int c = blockIdx.x, lane = threadIdx.x;
@@ -566,19 +604,21 @@ __global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad,
     const double up = 1.0 + 0x1p-18;
     const double nc = sqrt(sq) * (1.0 + 0x1p-30);
     cconst[c] = (float)sq;
-    const double ec = 0x1p-24 * (2.0 * d + 12.0) * nc * up;
-    const double eb = (0x1p-24 * 5.0 * sq + 0x1p-40 * sq) * up + 1e-30;
+    // fp64 rows are scored from their f32 roundings (as centroid_prep_kernel)
+    const double ec = 0x1p-24 * (2.0 * d + 12.0 + (xf64 ? 2.0 : 0.0)) * nc * up;
+    const double eb = (0x1p-24 * 5.0 * sq + 0x1p-40 * sq + (xf64 ? 0x1p-140 * nc : 0.0)) * up + 1e-30;
     unsigned int* chunk = reinterpret_cast<unsigned int*>(cconst + Kpad + 2 * (c / 64));
     atomicMax(chunk, __float_as_uint((float)(ec * (1.0 + 0x1p-20))));
     atomicMax(chunk + 1, __float_as_uint((float)(eb * (1.0 + 0x1p-20))));
 }
 
+template <typename TX>
 __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
-    const float* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
+    const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
     const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
     const unsigned long long* __restrict__ row_count, int64_t max_rows, int32_t* __restrict__ assign,
     double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows) {
-    __shared__ float xs[XP_WAVES][XP_R][XB_DMAX];
+    __shared__ TX xs[XP_WAVES][XP_R][XB_DMAX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int64_t total, g0, gstride;
     if (seg_counts) {
@@ -605,9 +645,9 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         for (int r = 0; r < XP_R; r++) {
             float q = 0.f;
             for (int j = lane; j < d; j += 64) {
-                const float v = X[(int64_t)myrow[r] * d + j];
+                const TX v = X[(int64_t)myrow[r] * d + j];
                 xs[wave][r][j] = v;
-                q = fmaf(v, v, q);
+                q = fmaf((float)v, (float)v, q);
             }
             xn2p[r] = q;
         }
@@ -625,7 +665,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
             for (int i = 0; i < 4; i++) cv[i] = 64 * i < Kpad ? CT32[(size_t)j * Kpad + 64 * i + lane] : 0.f;
 #pragma unroll
             for (int r = 0; r < XP_R; r++) {
-                const float xj = xs[wave][r][j];
+                const float xj = (float)xs[wave][r][j];
 #pragma unroll
                 for (int i = 0; i < 4; i++) acc[r][i] = fmaf(xj, cv[i], acc[r][i]);
             }
@@ -639,7 +679,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
             // |x|^2 in fp64 over the lanes' f32 partials, rounded up (as the f32 path)
             double xn2 = (double)xn2p[r];
             for (int off = 32; off >= 1; off >>= 1) xn2 += __shfl_xor(xn2, off);
-            xn2 *= 1.0 + 0x1p-20;
+            xn2 = xn2 * (sizeof(TX) == 4 ? 1.0 + 0x1p-20 : 1.0 + 0x1p-19) + (sizeof(TX) == 4 ? 0.0 : 0x1p-280);
             const float nx = (float)(sqrt(xn2) * (1.0 + 0x1p-30));
             const float ex = (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30);
             float lo[4];
@@ -707,7 +747,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         for (int r = 0; r < nr; r++) {
             if (pr[r] && ncand[r] <= XP_L) continue;
             const bool prune = pr[r] && ncand[r] <= 64;
-            const float* xr = xs[wave][r];
+            const TX* xr = xs[wave][r];
             double best = 0.0;
             int bi = -1;
             if (prune) {
@@ -750,7 +790,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
     }
 }
 
-int launch_assign_pruned_list(hipStream_t s, const float* X, int d, const double* C, int K, float* ws,
+int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
     if (max_rows <= 0) return 0;
@@ -762,15 +802,20 @@ int launch_assign_pruned_list(hipStream_t s, const float* X, int d, const double
     float* CT32 = ws;
     float* cconst = ws + (size_t)d * Kpad;
     (void)hipMemsetAsync(cconst + Kpad, 0, (size_t)(Kpad / 64) * 2 * 4, s);
-    hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, d, CT32, cconst);
+    hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, d, X.f64 ? 1 : 0, CT32,
+                       cconst);
     const int64_t groups = (max_rows + XP_R - 1) / XP_R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
-    hipLaunchKernelGGL(assign_pruned_kernel, dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, X, d, C, CT32, cconst,
-                       K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+    if (X.f64)
+        hipLaunchKernelGGL(assign_pruned_kernel<double>, dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, X.d(), d, C,
+                           CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+    else
+        hipLaunchKernelGGL(assign_pruned_kernel<float>, dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, X.f(), d, C,
+                           CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
     return kstatus("assign_pruned_kernel");
 }
 
-int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
+int launch_assign_exact_list(hipStream_t s, Pts X, int d, const double* C, int K, double* CT,
                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                              int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
     if (max_rows <= 0) return 0;
@@ -783,8 +828,12 @@ int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double*
     hipLaunchKernelGGL(transpose_centroids_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, C, K, Kpad, d, CT);
     const int64_t groups = (max_rows + XB_R - 1) / XB_R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XB_SPLIT : std::min<int64_t>((groups + XB_WAVES - 1) / XB_WAVES, 2048);
-    hipLaunchKernelGGL(assign_exact_batch_kernel, dim3((unsigned)blocks), dim3(64 * XB_WAVES), 0, s, X, d, CT, K, Kpad,
-                       rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+    if (X.f64)
+        hipLaunchKernelGGL(assign_exact_batch_kernel<double>, dim3((unsigned)blocks), dim3(64 * XB_WAVES), 0, s, X.d(),
+                           d, CT, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+    else
+        hipLaunchKernelGGL(assign_exact_batch_kernel<float>, dim3((unsigned)blocks), dim3(64 * XB_WAVES), 0, s, X.f(),
+                           d, CT, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
     return kstatus("assign_exact_batch_kernel");
 }
 

@@ -4,13 +4,15 @@
 //     sqrt(sum_j pow(x_j - c_j, 2)), fp64, j ascending
 //   cosineDistance     lib/data_structures/cust_vector.hpp:139-155
 //     1 - (long double) inner product / (sqrt(sum x^2) * sqrt(sum c^2))
-// `this` is the point x (fp32 values), `in` the centroid c (fp64). pow(v, 2)
-// is v*v here (identical whenever v is a difference of fp32
-// values, i.e. for every dataset-row centroid). No FMA contraction.
+// `this` is the point x (fp32 or fp64 values), `in` the centroid c (fp64).
+// pow(v, 2) is v*v here (identical whenever v is a difference of
+// fp32 values, i.e. for every dataset-row centroid of fp32 data; within an ulp
+// otherwise). No FMA contraction.
 #pragma once
 #include "softx87.h"
 
-__device__ inline double exact_euclid(const float* __restrict__ x, const double* __restrict__ c, int d) {
+template <typename T>
+__device__ inline double exact_euclid(const T* __restrict__ x, const double* __restrict__ c, int d) {
     double acc = 0.0;
     for (int j = 0; j < d; j++) {
         const double df = __dsub_rn((double)x[j], c[j]);
@@ -175,6 +177,16 @@ __device__ inline double exact_dist(const T* __restrict__ x, const U* __restrict
         return sqrt(acc);
     }
     return exact_cosine(x, c, d);
+}
+
+// Four consecutive row values (16-B aligned) widened to double.
+__device__ inline void ld4d(const float* p, double (&o)[4]) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+__device__ inline void ld4d(const double* p, double (&o)[4]) {
+    const double2 a = *reinterpret_cast<const double2*>(p), b = *reinterpret_cast<const double2*>(p + 2);
+    o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
 }
 
 // x86 SSE produces one NaN from non-NaN operands: the default NaN, sign set

@@ -28,34 +28,59 @@
 
 namespace lshkm {
 
-constexpr int HASH_PB = 64;      // points per block
+constexpr int HASH_PB = 64;      // points per block (at most; fewer for long rows)
 constexpr int HASH_THREADS = 256;
+constexpr size_t HASH_LDS_MAX = 96 * 1024;
+
+// Row staging: 16-B loads when the row length allows (float4 / double2).
+__device__ inline void hash_ld4(const float* p, double (&o)[4]) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+__device__ inline void hash_ld4(const double* p, double (&o)[4]) {
+    const double2 a = *reinterpret_cast<const double2*>(p), b = *reinterpret_cast<const double2*>(p + 2);
+    o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+}
+template <typename TX> __host__ __device__ constexpr int hash_vec() { return 16 / sizeof(TX); }
+
+// LDS row stride (elements): d rounded up to 4, plus 4 floats / 2 doubles
+// (16 B), so the lanes' 16-B reads of their rows spread over the banks.
+template <typename TX> __host__ __device__ inline int hash_dstride(int d) {
+    return (d + 3) / 4 * 4 + (int)(16 / sizeof(TX));
+}
 
 // Per wave: FB projections (a contiguous, zero-padded column block of PT)
 // accumulated together; PT is __restrict__ const so its wave-uniform reads
 // become scalar (SMEM) loads that feed v_fma_f64 directly.
-template <int MODE, int FB>
+// TX = float: products v_j x_j are exact in fp64. TX = double: the reference
+// rounds each product to double (SSE) before the x87 add; the FMA chain keeps
+// them exact, so the two differ by the products' roundings (<= 2^-53 |v_j x_j|
+// each) plus both chains' roundings: (d + 2) 2^-53 sum|v_j x_j| <= the
+// (d + 2) 2^-52 |v||x| already charged, plus d 2^-1075 for subnormal products.
+template <int MODE, int FB, typename TX>
 __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
-    const float* __restrict__ X, int64_t N, const double* __restrict__ PT, const float* __restrict__ tvec,
-    const double* __restrict__ pnorm, const int32_t* __restrict__ rvec, HashParams p, int32_t* __restrict__ out_h,
-    int32_t* __restrict__ out_phi, int32_t* __restrict__ out_bucket, unsigned long long* __restrict__ stats) {
+    const TX* __restrict__ X, int64_t N, const double* __restrict__ PT, const float* __restrict__ tvec,
+    const double* __restrict__ pnorm, const int32_t* __restrict__ rvec, HashParams p, int pb,
+    int32_t* __restrict__ out_h, int32_t* __restrict__ out_phi, int32_t* __restrict__ out_bucket,
+    unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int d = p.d, LK = p.LK, LKpad = p.LKpad, ds = p.dstride;   // ds = d rounded up to 4, + 4
-    float* xs = reinterpret_cast<float*>(smem);                       // [64][ds]
-    int32_t* hs = reinterpret_cast<int32_t*>(xs + HASH_PB * ds);      // [64][LK]
+    const int d = p.d, LK = p.LK, LKpad = p.LKpad, ds = hash_dstride<TX>(d);
+    TX* xs = reinterpret_cast<TX*>(smem);                             // [pb][ds]
+    int32_t* hs = reinterpret_cast<int32_t*>(xs + pb * ds);           // [pb][LK]
 
-    const int64_t p0 = (int64_t)blockIdx.x * HASH_PB;
-    const int npts = (int)min((int64_t)HASH_PB, N - p0);
+    const int64_t p0 = (int64_t)blockIdx.x * pb;
+    const int npts = (int)min((int64_t)pb, N - p0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
 
     // Stage the block's rows (contiguous in HBM) into padded LDS rows.
-    const float* src = X + p0 * d;
-    if ((d & 3) == 0) {
-        const int d4 = d >> 2, tot4 = npts * d4;
-        for (int e4 = threadIdx.x; e4 < tot4; e4 += HASH_THREADS) {
-            const int r = e4 / d4, c = (e4 - r * d4) << 2;
-            *reinterpret_cast<float4*>(xs + r * ds + c) = *reinterpret_cast<const float4*>(src + (int64_t)e4 * 4);
+    const TX* src = X + p0 * d;
+    constexpr int V = hash_vec<TX>();
+    if (d % V == 0) {
+        const int dv = d / V, totv = npts * dv;
+        for (int e = threadIdx.x; e < totv; e += HASH_THREADS) {
+            const int r = e / dv, c = (e - r * dv) * V;
+            *reinterpret_cast<float4*>(xs + r * ds + c) = *reinterpret_cast<const float4*>(src + (int64_t)e * V);
         }
     } else {
         for (int e = threadIdx.x; e < npts * d; e += HASH_THREADS) {
@@ -63,14 +88,14 @@ __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
             xs[r * ds + c] = src[e];
         }
     }
-    for (int e = threadIdx.x; e < HASH_PB * (ds - d); e += HASH_THREADS) {   // zero the pad columns
+    for (int e = threadIdx.x; e < pb * (ds - d); e += HASH_THREADS) {   // zero the pad columns
         const int r = e / (ds - d), c = d + (e - r * (ds - d));
-        xs[r * ds + c] = 0.f;
+        xs[r * ds + c] = (TX)0;
     }
     __syncthreads();
 
     const bool valid = lane < npts;
-    const float* xr = xs + (valid ? lane : 0) * ds;
+    const TX* xr = xs + (lane < pb ? lane : 0) * ds;
     const int chunks = LKpad / (4 * FB);
     const int d4 = (d + 3) >> 2;
 
@@ -85,11 +110,11 @@ __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
         const __attribute__((address_space(4))) double* prow =
             (const __attribute__((address_space(4))) double*)(PT + fb);
         for (int j4 = 0; j4 < d4; j4++) {
-            const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * j4);
-            const float xa[4] = {xv.x, xv.y, xv.z, xv.w};
+            double xa[4];
+            hash_ld4(xr + 4 * j4, xa);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const double xj = (double)xa[q];
+                const double xj = xa[q];
                 xn2 = fma(xj, xj, xn2);
 #pragma unroll
                 for (int u = 0; u < FB; u++) acc[u] = fma(prow[u], xj, acc[u]);   // pad rows/cols are 0
@@ -106,28 +131,29 @@ __global__ __launch_bounds__(HASH_THREADS) void proj_hash_kernel(
             if (MODE == HM_LSH_EUCLID || MODE == HM_CUBE_EUCLID_H) {
                 const double tt = (double)tvec[f], ww = (double)p.w;
                 const double y = (acc[u] + tt) / ww;
-                const double B = ((double)(d + 2) * 0x1p-52 * (P + fabs(tt))) / ww + fabs(y) * 0x1p-51;
+                const double B = ((double)(d + 2) * 0x1p-52 * (P + fabs(tt)) + 0x1p-1000) / ww + fabs(y) * 0x1p-51;
                 const double lo = floor(y - B), hi = floor(y + B);
-                if (lo == hi) {
+                // certified, and inside the int range (the reference's FISTP stores
+                // INT_MIN outside it); inf / nan never pass
+                if (lo == hi && fabs(lo) < 0x1p31) {
                     hv = (int32_t)lo;
                 } else {
                     // Exact: sequential x87 semantics (cust_vector.hpp:117-118, euclidean_h_gen.hpp:75).
-                    sx80 s = sx_zero();
-                    for (int j = 0; j < d; j++)
-                        s = sx_add_double(s, __dmul_rn(PT[(size_t)j * LKpad + f], (double)xr[j]));
-                    s = sx_add_double(s, tt);
-                    hv = (int32_t)sx_floor_i64(sx_div(s, sx_from_float(p.w)));
+                    SxSum s;
+                    s.init();
+                    for (int j = 0; j < d; j++) s.add(__dmul_rn(PT[(size_t)j * LKpad + f], (double)xr[j]));
+                    hv = sx_hash_floor(s, tt, p.w);
                     if (valid) atomicAdd(stats + STAT_HASH_EXACT, 1ull);
                 }
             } else {
-                const double B = (double)(d + 3) * 0x1p-52 * P;
-                if (acc[u] > B) hv = 1;
-                else if (acc[u] < -B) hv = 0;
+                const double B = (double)(d + 3) * 0x1p-52 * P + 0x1p-1000;
+                if (acc[u] > B && acc[u] < 0x1p1000) hv = 1;       // finite: no product overflowed
+                else if (acc[u] < -B && acc[u] > -0x1p1000) hv = 0;
                 else {
-                    sx80 s = sx_zero();
-                    for (int j = 0; j < d; j++)
-                        s = sx_add_double(s, __dmul_rn(PT[(size_t)j * LKpad + f], (double)xr[j]));
-                    hv = sx_ge_zero(s) ? 1 : 0;
+                    SxSum s;
+                    s.init();
+                    for (int j = 0; j < d; j++) s.add(__dmul_rn(PT[(size_t)j * LKpad + f], (double)xr[j]));
+                    hv = sx_hash_sign(s);
                     if (valid) atomicAdd(stats + STAT_HASH_EXACT, 1ull);
                 }
             }
@@ -182,29 +208,38 @@ int hash_lkpad(int LK) {
     return 4 * ((fpw + fb - 1) / fb) * fb;
 }
 
-template <int MODE>
-static void launch_mode(hipStream_t s, dim3 grid, dim3 block, size_t lds, const float* X, int64_t N,
-                        const HashParams& p, int32_t* out_h, int32_t* out_phi, int32_t* out_bucket,
-                        unsigned long long* stats) {
+template <int MODE, typename TX>
+static void launch_mode(hipStream_t s, const TX* X, int64_t N, const HashParams& p, int32_t* out_h, int32_t* out_phi,
+                        int32_t* out_bucket, unsigned long long* stats) {
+    // points per block: 64 unless the staged rows would crowd the CU's LDS
+    int pb = HASH_PB;
+    auto lds_of = [&](int b) { return (size_t)b * hash_dstride<TX>(p.d) * sizeof(TX) + (size_t)b * p.LK * 4; };
+    while (pb > 8 && lds_of(pb) > HASH_LDS_MAX) pb >>= 1;
+    const dim3 grid((unsigned)((N + pb - 1) / pb)), block(HASH_THREADS);
     switch (hash_fb(p.LK)) {
-#define HF_CASE(FB) case FB: hipLaunchKernelGGL((proj_hash_kernel<MODE, FB>), grid, block, lds, s, X, N, p.PT, p.t, \
-                                              p.pnorm, p.r, p, out_h, out_phi, out_bucket, stats); break;
+#define HF_CASE(FB) case FB: hipLaunchKernelGGL((proj_hash_kernel<MODE, FB, TX>), grid, block, lds_of(pb), s, X, N, p.PT, \
+                                              p.t, p.pnorm, p.r, p, pb, out_h, out_phi, out_bucket, stats); break;
         HF_CASE(2) HF_CASE(4) HF_CASE(6) HF_CASE(8)
 #undef HF_CASE
     }
 }
 
-int launch_proj_hash(hipStream_t s, int mode, const float* X, int64_t N, const HashParams& p,
+template <typename TX>
+static void launch_tx(hipStream_t s, int mode, const TX* X, int64_t N, const HashParams& p, int32_t* out_h,
+                      int32_t* out_phi, int32_t* out_bucket, unsigned long long* stats) {
+    switch (mode) {
+        case HM_LSH_EUCLID: launch_mode<HM_LSH_EUCLID>(s, X, N, p, out_h, out_phi, out_bucket, stats); break;
+        case HM_LSH_COSINE: launch_mode<HM_LSH_COSINE>(s, X, N, p, out_h, out_phi, out_bucket, stats); break;
+        case HM_CUBE_EUCLID_H: launch_mode<HM_CUBE_EUCLID_H>(s, X, N, p, out_h, out_phi, out_bucket, stats); break;
+        default: launch_mode<HM_CUBE_COSINE>(s, X, N, p, out_h, out_phi, out_bucket, stats); break;
+    }
+}
+
+int launch_proj_hash(hipStream_t s, int mode, Pts X, int64_t N, const HashParams& p,
                      int32_t* out_h, int32_t* out_phi, int32_t* out_bucket, unsigned long long* stats) {
     if (N <= 0) return 0;
-    const size_t lds = (size_t)HASH_PB * p.dstride * 4 + (size_t)HASH_PB * p.LK * 4;
-    const dim3 grid((unsigned)((N + HASH_PB - 1) / HASH_PB)), block(HASH_THREADS);
-    switch (mode) {
-        case HM_LSH_EUCLID: launch_mode<HM_LSH_EUCLID>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
-        case HM_LSH_COSINE: launch_mode<HM_LSH_COSINE>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
-        case HM_CUBE_EUCLID_H: launch_mode<HM_CUBE_EUCLID_H>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
-        default: launch_mode<HM_CUBE_COSINE>(s, grid, block, lds, X, N, p, out_h, out_phi, out_bucket, stats); break;
-    }
+    if (X.f64) launch_tx(s, mode, X.d(), N, p, out_h, out_phi, out_bucket, stats);
+    else launch_tx(s, mode, X.f(), N, p, out_h, out_phi, out_bucket, stats);
     return kstatus("hash.hip");
 }
 

@@ -91,7 +91,9 @@ struct lshkm_lsh_s {
     bool q_valid = false;
     uint64_t q_epoch = 0;
     const void* q_Q = nullptr;
+    bool q_f64 = false;
     const void* q_alias = nullptr;
+    const int64_t* q_out_ptr = nullptr;
     int64_t q_nq = 0, q_total = 0;
     int q_filtered = 0;
 };

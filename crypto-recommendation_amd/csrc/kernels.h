@@ -5,6 +5,28 @@
 
 namespace lshkm {
 
+// Dataset rows in HBM: fp32 (the storage the hot path is tuned for: the
+// synthetic / proj-2 values are fp32-representable) or fp64 (general doubles,
+// e.g. the recommender's user vectors, crypto_rec.hpp:78-140).
+// Kernels that read rows are templated on the element type; launchers take a
+// Pts and dispatch.
+struct Pts {
+    const void* p = nullptr;
+    bool f64 = false;
+    Pts() = default;
+    Pts(const float* x) : p(x), f64(false) {}
+    Pts(const double* x) : p(x), f64(true) {}
+    const float* f() const { return static_cast<const float*>(p); }
+    const double* d() const { return static_cast<const double*>(p); }
+    size_t esize() const { return f64 ? 8 : 4; }
+    // row r of a [.][d] matrix
+    Pts row(int64_t r, int d) const {
+        Pts q = *this;
+        q.p = static_cast<const char*>(p) + (size_t)r * d * esize();
+        return q;
+    }
+};
+
 // Projection families, one launcher (hash.hip).
 enum HashMode {
     HM_LSH_EUCLID = 0,    // EuclideanPhiGen: tuples + phi + bucket
@@ -20,13 +42,12 @@ struct HashParams {
     const int32_t* r;     // [LK]   (LSH euclidean)
     float w;
     int d, L, k, LK, LKpad;
-    int dstride;          // LDS row stride (floats): d rounded up to 4, plus 4
     int64_t nb;
 };
 int hash_fb(int LK);      // projections per accumulator block
 int hash_lkpad(int LK);   // padded PT row length
 
-int launch_proj_hash(hipStream_t s, int mode, const float* X, int64_t N, const HashParams& p,
+int launch_proj_hash(hipStream_t s, int mode, Pts X, int64_t N, const HashParams& p,
                      int32_t* out_h, int32_t* out_phi, int32_t* out_bucket,
                      unsigned long long* stats);
 
@@ -38,28 +59,28 @@ struct AssignWorkspace {
     unsigned long long* counters;  // [0] = ambiguous count (device)
 };
 int assign_dp(int d);    // padded dimension used by the MFMA kernel (0 = unsupported)
-int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d, int DP, int metric,
+int launch_centroid_prep(hipStream_t s, const double* C, int K, int Kpad, int d, int DP, int metric, bool xf64,
                          float* C32, float* cconst);
-int launch_assign_mfma(hipStream_t s, const float* X, int64_t N, int d, int DP, const double* C, int K,
+int launch_assign_mfma(hipStream_t s, Pts X, int64_t N, int d, int DP, const double* C, int K,
                        int Kpad, int metric, const float* C32, const float* cconst, int32_t* assign, double* dist,
                        int32_t* ambig, unsigned long long* ambig_count);
 // Lloyd cosine winners whose distance the certified form declined (list at
 // rows[0..*count), written by assign_mfma_kernel<., 1>): soft-x87 distances.
-int launch_cos_fix(hipStream_t s, const float* X, int64_t N, int d, const double* C, const int32_t* rows,
+int launch_cos_fix(hipStream_t s, Pts X, int64_t N, int d, const double* C, const int32_t* rows,
                    const unsigned long long* count, const int32_t* assign, double* dist);
-int launch_assign_exact(hipStream_t s, const float* X, int64_t N, int d, const double* C, int K,
+int launch_assign_exact(hipStream_t s, Pts X, int64_t N, int d, const double* C, int K,
                         int metric, const int32_t* rows, const unsigned long long* row_count,
                         int64_t max_rows, int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
                         int64_t seg_rows = 0, int nseg = 0);
 // Euclidean, listed rows, batched (CT: d * ceil64(K) doubles of workspace).
 // Segmented form (seg_counts != NULL): segment b = rows[b * seg_rows ...], count seg_counts[2b].
-int launch_assign_exact_list(hipStream_t s, const float* X, int d, const double* C, int K, double* CT,
+int launch_assign_exact_list(hipStream_t s, Pts X, int d, const double* C, int K, double* CT,
                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                              int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
                              int64_t seg_rows = 0, int nseg = 0);
 // Euclidean, listed rows, K <= 256: f32 candidate pruning, then exact order on
 // the candidates only (ws: d * ceil64(K) + ceil64(K) + ceil64(K)/32 floats).
-int launch_assign_pruned_list(hipStream_t s, const float* X, int d, const double* C, int K, float* ws,
+int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
                               int64_t seg_rows = 0, int nseg = 0);
@@ -103,13 +124,13 @@ int launch_memo_scatter(hipStream_t s, const int32_t* off, const int32_t* bit, i
 // k-means update (update.hip).
 // carry / carry_counts (may be NULL): the running sums and counts the chain
 // continues from (exact-order sharded mode).
-int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K,
+int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K,
                     double* sums, int64_t* counts, const double* carry = nullptr,
                     const int64_t* carry_counts = nullptr);
 // Same sums, parallel: exact int128 fixed-point sums wherever the sequential
 // chain provably never rounds, the sequential chain elsewhere (ws: km_fx_ws_bytes).
 size_t km_fx_ws_bytes(int K, int d);
-int launch_km_sums_fx(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
                       double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws);
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
@@ -118,7 +139,7 @@ int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts,
 // chosen[0] and canon[1..K-1] (the engine's canonical draws) already on the
 // device; ws holds kmeans_pp_ws_bytes(N) bytes.
 size_t kmeans_pp_ws_bytes(int64_t N);
-int launch_kmeans_pp(hipStream_t s, const float* X, int64_t N, int d, int K, int metric, const double* canon,
+int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, const double* canon,
                      int32_t* chosen, void* ws, unsigned long long* stats);
 
 // Recommend step (recom.hip): fp64 rows, per-user candidate CSR.
@@ -196,18 +217,19 @@ int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric
 int launch_range_pairs(hipStream_t s, const int64_t* comb_ptr, const int32_t* comb_idx, int K, int32_t* rows,
                        int32_t* cents);
 int launch_range_init(hipStream_t s, int64_t N, int32_t* assign, double* dist);
-int launch_range_pass(hipStream_t s, const float* X, int d, const double* C, int K, int metric, const int32_t* key,
+int launch_range_pass(hipStream_t s, Pts X, int d, const double* C, int K, int metric, const int32_t* key,
                       const int64_t* vptr, const int32_t* cents, double* cache, int8_t* cached, int64_t N,
                       const double* r0, int64_t pass, int32_t* assign, double* dist, unsigned long long* count);
 int launch_range_unassigned(hipStream_t s, const int32_t* assign, int64_t N, int32_t* list,
                             unsigned long long* count);
-int launch_range_gather(hipStream_t s, const float* X, int d, const int32_t* list, int64_t M, float* Xr);
+// Xr: rows of the same element type as X
+int launch_range_gather(hipStream_t s, Pts X, int d, const int32_t* list, int64_t M, void* Xr);
 int launch_range_scatter(hipStream_t s, const int32_t* list, int64_t M, const int32_t* ar, const double* dr,
                          int32_t* assign, double* dist);
 
 // Silhouette (silhouette.hip).
 int launch_sil_near(hipStream_t s, const double* C, int K, int d, int metric, int32_t* near);
-int launch_sil_points(hipStream_t s, const float* X, int d, int metric, const int32_t* rows, const int64_t* crow,
+int launch_sil_points(hipStream_t s, Pts X, int d, int metric, const int32_t* rows, const int64_t* crow,
                       const int32_t* assign, const int32_t* near, int64_t N, double* s_out);
 int launch_sil_sum(hipStream_t s, const double* sv, const int32_t* rows, const int64_t* crow, int K, int64_t N,
                    double* raw, double* out);

@@ -75,13 +75,16 @@ __device__ inline int kpp_binade(double s) {
 constexpr int KPP_DJ = 32;
 constexpr int KPP_V4 = KPP_THREADS * KPP_DJ / 4 / KPP_THREADS;   // float4 per thread per slice (8)
 
-template <int METRIC, bool VEC>
-__global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const float* __restrict__ X, int64_t N, int d,
+// TX: fp32 or fp64 rows (VEC only for fp32).
+template <int METRIC, bool VEC, typename TX>
+__global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restrict__ X, int64_t N, int d,
                                                                const int32_t* __restrict__ chosen, int it,
                                                                double* __restrict__ mind,
                                                                unsigned long long* __restrict__ mx_bits) {
-    __shared__ float tile[KPP_THREADS][KPP_DJ + 1];
-    const float* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
+    static_assert(!VEC || sizeof(TX) == 4, "the float4 form reads fp32 rows");
+    constexpr int DJ = sizeof(TX) == 4 ? KPP_DJ : KPP_DJ / 2;     // tile <= 34 KiB either way
+    __shared__ TX tile[KPP_THREADS][DJ + 1];
+    const TX* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
     double cb = 0.0;                                    // cosine: sum c^2 (uniform)
     if (METRIC == 1)
         for (int j = 0; j < d; j++) {
@@ -102,8 +105,8 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const float* __re
                 if (r < rows) pf[k] = *reinterpret_cast<const float4*>(X + (row0 + r) * d + part * 4);
             }
         }
-        for (int j0 = 0; j0 < d; j0 += KPP_DJ) {
-            const int dj = d - j0 < KPP_DJ ? d - j0 : KPP_DJ;
+        for (int j0 = 0; j0 < d; j0 += DJ) {
+            const int dj = d - j0 < DJ ? d - j0 : DJ;
             __syncthreads();
             if (VEC) {
 #pragma unroll
@@ -118,18 +121,18 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const float* __re
                 }
             } else {
 #pragma unroll 4
-                for (int e = threadIdx.x; e < KPP_THREADS * KPP_DJ; e += KPP_THREADS) {
-                    const int r = e / KPP_DJ, jj = e % KPP_DJ;
+                for (int e = threadIdx.x; e < KPP_THREADS * DJ; e += KPP_THREADS) {
+                    const int r = e / DJ, jj = e % DJ;
                     if (r < rows && jj < dj) tile[r][jj] = X[(row0 + r) * d + j0 + jj];
                 }
             }
             __syncthreads();
-            if (VEC && j0 + KPP_DJ < d) {
+            if (VEC && j0 + DJ < d) {
 #pragma unroll
                 for (int k = 0; k < KPP_V4; k++) {
                     const int idx = k * KPP_THREADS + threadIdx.x, r = idx >> 3, part = idx & 7;
                     if (r < rows)
-                        pf[k] = *reinterpret_cast<const float4*>(X + (row0 + r) * d + j0 + KPP_DJ + part * 4);
+                        pf[k] = *reinterpret_cast<const float4*>(X + (row0 + r) * d + j0 + DJ + part * 4);
                 }
             }
             if (n < N) {
@@ -498,7 +501,7 @@ __global__ void kpp_choose_kernel(const double* __restrict__ cum, int64_t N, con
 // Runs iterations 1..K-1; chosen[0] and canon[1..K-1] are already on the device.
 // ws: mind[N] f64, cum[N] f64, then per chunk sum/start f64, meta, s_start f64,
 // mode i32, and the max word.
-int launch_kmeans_pp(hipStream_t s, const float* X, int64_t N, int d, int K, int metric, const double* canon,
+int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, const double* canon,
                      int32_t* chosen, void* ws, unsigned long long* stats) {
     const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
     char* p = (char*)ws;
@@ -513,19 +516,19 @@ int launch_kmeans_pp(hipStream_t s, const float* X, int64_t N, int d, int K, int
     const unsigned dgrid = gsz(N, KPP_THREADS, 4096);
     for (int it = 1; it < K; it++) {
         if (hipMemsetAsync(mx, 0, sizeof(*mx), s) != hipSuccess) return kstatus("kmeanspp.hip");
-        const bool vec = d % KPP_DJ == 0;
-        if (metric == 0 && vec)
-            hipLaunchKernelGGL((kpp_dist_kernel<0, true>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
-                               mind, mx);
+        const bool vec = d % KPP_DJ == 0 && !X.f64;
+        const dim3 g(dgrid), b(KPP_THREADS);
+        if (X.f64) {
+            if (metric == 0) hipLaunchKernelGGL((kpp_dist_kernel<0, false, double>), g, b, 0, s, X.d(), N, d, chosen, it, mind, mx);
+            else hipLaunchKernelGGL((kpp_dist_kernel<1, false, double>), g, b, 0, s, X.d(), N, d, chosen, it, mind, mx);
+        } else if (metric == 0 && vec)
+            hipLaunchKernelGGL((kpp_dist_kernel<0, true, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
         else if (metric == 0)
-            hipLaunchKernelGGL((kpp_dist_kernel<0, false>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
-                               mind, mx);
+            hipLaunchKernelGGL((kpp_dist_kernel<0, false, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
         else if (vec)
-            hipLaunchKernelGGL((kpp_dist_kernel<1, true>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
-                               mind, mx);
+            hipLaunchKernelGGL((kpp_dist_kernel<1, true, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
         else
-            hipLaunchKernelGGL((kpp_dist_kernel<1, false>), dim3(dgrid), dim3(KPP_THREADS), 0, s, X, N, d, chosen, it,
-                               mind, mx);
+            hipLaunchKernelGGL((kpp_dist_kernel<1, false, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
         hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum);
         hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, csum, nch, cstart);
         hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, cstart,

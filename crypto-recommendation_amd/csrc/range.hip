@@ -95,7 +95,8 @@ __global__ void rg_init_kernel(int64_t N, int32_t* __restrict__ assign, double* 
 // One pass of the do-while loop (assignment.hpp:160-216) for every row.
 // Incidence e of row n: centroid cents[e]; cache[e] / cached[e] hold the
 // distanceMap entry of (key[cents[e]], n) once it exists.
-__global__ void rg_pass_kernel(const float* __restrict__ X, int d, const double* __restrict__ C, int K, int metric,
+template <typename TX>
+__global__ void rg_pass_kernel(const TX* __restrict__ X, int d, const double* __restrict__ C, int K, int metric,
                                const int32_t* __restrict__ key, const int64_t* __restrict__ vptr,
                                const int32_t* __restrict__ cents, double* __restrict__ cache,
                                int8_t* __restrict__ cached, int64_t N, const double* __restrict__ r0p, int64_t pass,
@@ -155,8 +156,9 @@ __global__ void rg_unassigned_kernel(const int32_t* __restrict__ assign, int64_t
     }
 }
 
-__global__ void rg_gather_kernel(const float* __restrict__ X, int d, const int32_t* __restrict__ list, int64_t M,
-                                 float* __restrict__ Xr) {
+template <typename TX>
+__global__ void rg_gather_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ list, int64_t M,
+                                 TX* __restrict__ Xr) {
     const int64_t tot = M * d;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = e / d;
@@ -196,12 +198,16 @@ int launch_range_init(hipStream_t s, int64_t N, int32_t* assign, double* dist) {
     return kstatus("rg_init_kernel");
 }
 
-int launch_range_pass(hipStream_t s, const float* X, int d, const double* C, int K, int metric, const int32_t* key,
+int launch_range_pass(hipStream_t s, Pts X, int d, const double* C, int K, int metric, const int32_t* key,
                       const int64_t* vptr, const int32_t* cents, double* cache, int8_t* cached, int64_t N,
                       const double* r0, int64_t pass, int32_t* assign, double* dist, unsigned long long* count) {
     if (N == 0) return 0;
-    hipLaunchKernelGGL(rg_pass_kernel, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X, d, C, K, metric, key, vptr,
-                       cents, cache, cached, N, r0, pass, assign, dist, count);
+    if (X.f64)
+        hipLaunchKernelGGL(rg_pass_kernel<double>, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X.d(), d, C, K, metric,
+                           key, vptr, cents, cache, cached, N, r0, pass, assign, dist, count);
+    else
+        hipLaunchKernelGGL(rg_pass_kernel<float>, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X.f(), d, C, K, metric,
+                           key, vptr, cents, cache, cached, N, r0, pass, assign, dist, count);
     return kstatus("rg_pass_kernel");
 }
 
@@ -212,9 +218,14 @@ int launch_range_unassigned(hipStream_t s, const int32_t* assign, int64_t N, int
     return kstatus("rg_unassigned_kernel");
 }
 
-int launch_range_gather(hipStream_t s, const float* X, int d, const int32_t* list, int64_t M, float* Xr) {
+int launch_range_gather(hipStream_t s, Pts X, int d, const int32_t* list, int64_t M, void* Xr) {
     if (M == 0) return 0;
-    hipLaunchKernelGGL(rg_gather_kernel, dim3(gsz(M * d, 256, 16384)), dim3(256), 0, s, X, d, list, M, Xr);
+    if (X.f64)
+        hipLaunchKernelGGL(rg_gather_kernel<double>, dim3(gsz(M * d, 256, 16384)), dim3(256), 0, s, X.d(), d, list, M,
+                           static_cast<double*>(Xr));
+    else
+        hipLaunchKernelGGL(rg_gather_kernel<float>, dim3(gsz(M * d, 256, 16384)), dim3(256), 0, s, X.f(), d, list, M,
+                           static_cast<float*>(Xr));
     return kstatus("rg_gather_kernel");
 }
 

@@ -46,21 +46,22 @@ __global__ void sil_near_kernel(const double* __restrict__ C, int K, int d, int 
 constexpr int SP_WAVES = 4;
 constexpr int SIL_DMAX = 512;
 
-// x_i (LDS, fp32) vs x_j (global, fp32): the exact.h order, 4-wide loads
-__device__ inline double sil_euclid(const float* __restrict__ xi, const float* __restrict__ xj, int d) {
+// x_i (LDS) vs x_j (global), rows of fp32 or fp64: the exact.h order, 4-wide loads
+template <typename TX>
+__device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restrict__ xj, int d) {
     double acc = 0.0;
     int k = 0;
     if ((d & 3) == 0) {
 #pragma unroll 4
         for (; k < d; k += 4) {
-            const float4 a = *reinterpret_cast<const float4*>(xi + k);
-            const float4 b = *reinterpret_cast<const float4*>(xj + k);
-            const double d0 = __dsub_rn((double)a.x, (double)b.x), d1 = __dsub_rn((double)a.y, (double)b.y);
-            const double d2 = __dsub_rn((double)a.z, (double)b.z), d3 = __dsub_rn((double)a.w, (double)b.w);
-            acc = __dadd_rn(acc, __dmul_rn(d0, d0));
-            acc = __dadd_rn(acc, __dmul_rn(d1, d1));
-            acc = __dadd_rn(acc, __dmul_rn(d2, d2));
-            acc = __dadd_rn(acc, __dmul_rn(d3, d3));
+            double a[4], b[4];
+            ld4d(xi + k, a);
+            ld4d(xj + k, b);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const double df = __dsub_rn(a[u], b[u]);
+                acc = __dadd_rn(acc, __dmul_rn(df, df));
+            }
         }
     }
     for (; k < d; k++) {
@@ -71,14 +72,15 @@ __device__ inline double sil_euclid(const float* __restrict__ xi, const float* _
 }
 
 // sum_{j in [j0, j1)} d(x_i, x_rows[j]) in j order (wave-uniform result)
-__device__ inline double sil_segment(const float* __restrict__ xi, const float* __restrict__ X, int d, int metric,
+template <typename TX>
+__device__ inline double sil_segment(const TX* __restrict__ xi, const TX* __restrict__ X, int d, int metric,
                                      const int32_t* __restrict__ rows, int64_t j0, int64_t j1, int lane) {
     double acc = 0.0;
     for (int64_t jb = j0; jb < j1; jb += 64) {
         const int64_t j = jb + lane;
         double dj = 0.0;
         if (j < j1) {
-            const float* xj = X + (size_t)rows[j] * d;
+            const TX* xj = X + (size_t)rows[j] * d;
             dj = metric == 0 ? sil_euclid(xi, xj, d) : exact_dist(xi, xj, d, metric);
         }
         const int n = (int)min<int64_t>(64, j1 - jb);
@@ -88,30 +90,30 @@ __device__ inline double sil_segment(const float* __restrict__ xi, const float* 
 }
 
 // Two members (same cluster) against the same x_j: each x_j load serves both.
-__device__ inline void sil_euclid2(const float* __restrict__ xa, const float* __restrict__ xb,
-                                   const float* __restrict__ xj, int d, double& da, double& db) {
+template <typename TX>
+__device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restrict__ xb,
+                                   const TX* __restrict__ xj, int d, double& da, double& db) {
     double aa = 0.0, ab = 0.0;
 #pragma unroll 4
     for (int k = 0; k < d; k += 4) {
-        const float4 b = *reinterpret_cast<const float4*>(xj + k);
-        const float4 u = *reinterpret_cast<const float4*>(xa + k);
-        const float4 v = *reinterpret_cast<const float4*>(xb + k);
-        const double b0 = (double)b.x, b1 = (double)b.y, b2 = (double)b.z, b3 = (double)b.w;
-        const double u0 = __dsub_rn((double)u.x, b0), u1 = __dsub_rn((double)u.y, b1);
-        const double u2 = __dsub_rn((double)u.z, b2), u3 = __dsub_rn((double)u.w, b3);
-        const double v0 = __dsub_rn((double)v.x, b0), v1 = __dsub_rn((double)v.y, b1);
-        const double v2 = __dsub_rn((double)v.z, b2), v3 = __dsub_rn((double)v.w, b3);
-        aa = __dadd_rn(aa, __dmul_rn(u0, u0)); ab = __dadd_rn(ab, __dmul_rn(v0, v0));
-        aa = __dadd_rn(aa, __dmul_rn(u1, u1)); ab = __dadd_rn(ab, __dmul_rn(v1, v1));
-        aa = __dadd_rn(aa, __dmul_rn(u2, u2)); ab = __dadd_rn(ab, __dmul_rn(v2, v2));
-        aa = __dadd_rn(aa, __dmul_rn(u3, u3)); ab = __dadd_rn(ab, __dmul_rn(v3, v3));
+        double b[4], u[4], v[4];
+        ld4d(xj + k, b);
+        ld4d(xa + k, u);
+        ld4d(xb + k, v);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const double du = __dsub_rn(u[e], b[e]), dv = __dsub_rn(v[e], b[e]);
+            aa = __dadd_rn(aa, __dmul_rn(du, du));
+            ab = __dadd_rn(ab, __dmul_rn(dv, dv));
+        }
     }
     da = sqrt(aa);
     db = sqrt(ab);
 }
 
-__device__ inline void sil_segment2(const float* __restrict__ xa, const float* __restrict__ xb,
-                                    const float* __restrict__ X, int d, const int32_t* __restrict__ rows, int64_t j0,
+template <typename TX>
+__device__ inline void sil_segment2(const TX* __restrict__ xa, const TX* __restrict__ xb,
+                                    const TX* __restrict__ X, int d, const int32_t* __restrict__ rows, int64_t j0,
                                     int64_t j1, int lane, double& sa, double& sb) {
     double acc_a = 0.0, acc_b = 0.0;
     for (int64_t jb = j0; jb < j1; jb += 64) {
@@ -138,13 +140,14 @@ __device__ inline double sil_value(double a, double b, int64_t c0, int64_t c1, i
     return x86_nan(__ddiv_rn(__dsub_rn(b, a), mx));
 }
 
+template <typename TX>
 __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
-    const float* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows, const int64_t* __restrict__ crow,
+    const TX* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows, const int64_t* __restrict__ crow,
     const int32_t* __restrict__ assign, const int32_t* __restrict__ near, int64_t N, double* __restrict__ s_out) {
-    __shared__ __attribute__((aligned(16))) float xs[SP_WAVES][2][SIL_DMAX];
+    __shared__ __attribute__((aligned(16))) TX xs[SP_WAVES][2][SIL_DMAX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float* xa = xs[wave][0];
-    float* xb = xs[wave][1];
+    TX* xa = xs[wave][0];
+    TX* xb = xs[wave][1];
     // a wave takes members p, p + 1 (cluster-sorted): one pass over the x_j when
     // they share a cluster (euclidean, d % 4 == 0); s_out is indexed by row
     const int64_t npair = (N + 1) / 2;
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
             continue;
         }
         for (int m = 0; m < (has2 ? 2 : 1); m++) {
-            const float* xi = m ? xb : xa;
+            const TX* xi = m ? xb : xa;
             const int c = m ? cb : ca;
             const int64_t c0 = crow[c], c1 = crow[c + 1];
             const double a = sil_segment(xi, X, d, metric, rows, c0, c1, lane);
@@ -188,13 +191,14 @@ __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
 }
 
 // d > SIL_DMAX: one thread per member, the same sums.
-__global__ void sil_point_thread_kernel(const float* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows,
+template <typename TX>
+__global__ void sil_point_thread_kernel(const TX* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows,
                                         const int64_t* __restrict__ crow, const int32_t* __restrict__ assign,
                                         const int32_t* __restrict__ near, int64_t N, double* __restrict__ s_out) {
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x) {
         const int32_t r = rows[p];
         const int c = assign[r];
-        const float* xi = X + (size_t)r * d;
+        const TX* xi = X + (size_t)r * d;
         const int64_t c0 = crow[c], c1 = crow[c + 1];
         double a = 0.0;
         for (int64_t j = c0; j < c1; j++) a = __dadd_rn(a, exact_dist(xi, X + (size_t)rows[j] * d, d, metric));
@@ -237,17 +241,24 @@ int launch_sil_near(hipStream_t s, const double* C, int K, int d, int metric, in
     return kstatus("sil_near_kernel");
 }
 
-int launch_sil_points(hipStream_t s, const float* X, int d, int metric, const int32_t* rows, const int64_t* crow,
-                      const int32_t* assign, const int32_t* near, int64_t N, double* s_out) {
-    if (N == 0) return 0;
+template <typename TX>
+static int sil_points_tx(hipStream_t s, const TX* X, int d, int metric, const int32_t* rows, const int64_t* crow,
+                         const int32_t* assign, const int32_t* near, int64_t N, double* s_out) {
     if (d > SIL_DMAX) {
-        hipLaunchKernelGGL(sil_point_thread_kernel, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X, d, metric, rows, crow,
-                           assign, near, N, s_out);
+        hipLaunchKernelGGL(sil_point_thread_kernel<TX>, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X, d, metric, rows,
+                           crow, assign, near, N, s_out);
         return kstatus("sil_point_thread_kernel");
     }
-    hipLaunchKernelGGL(sil_point_kernel, dim3(gsz((N + 1) / 2, SP_WAVES, 16384)), dim3(64 * SP_WAVES), 0, s, X, d, metric, rows,
-                       crow, assign, near, N, s_out);
+    hipLaunchKernelGGL(sil_point_kernel<TX>, dim3(gsz((N + 1) / 2, SP_WAVES, 16384)), dim3(64 * SP_WAVES), 0, s, X, d,
+                       metric, rows, crow, assign, near, N, s_out);
     return kstatus("sil_point_kernel");
+}
+
+int launch_sil_points(hipStream_t s, Pts X, int d, int metric, const int32_t* rows, const int64_t* crow,
+                      const int32_t* assign, const int32_t* near, int64_t N, double* s_out) {
+    if (N == 0) return 0;
+    return X.f64 ? sil_points_tx(s, X.d(), d, metric, rows, crow, assign, near, N, s_out)
+                 : sil_points_tx(s, X.f(), d, metric, rows, crow, assign, near, N, s_out);
 }
 
 int launch_sil_sum(hipStream_t s, const double* sv, const int32_t* rows, const int64_t* crow, int K, int64_t N,

@@ -17,8 +17,10 @@
 
 #if defined(__HIPCC__)
 #define SX_HD __host__ __device__ inline
+#define SX_MD __host__ __device__ inline
 #else
 #define SX_HD static inline
+#define SX_MD inline
 #endif
 
 struct sx80 {
@@ -185,6 +187,46 @@ SX_HD int64_t sx_floor_i64(sx80 v) {
 }
 
 SX_HD int sx_ge_zero(sx80 v) { return v.m == 0 || v.s == 0; }
+
+// int(floorl(v)) as g++ -O0 compiles it (FISTP with truncation after floorl):
+// a value outside the int range stores the x87 "integer indefinite" INT_MIN.
+SX_HD int32_t sx_floor_int32(sx80 v) {
+    if (v.m != 0 && v.e >= 0) return (int32_t)0x80000000;    // |v| >= 2^63
+    const int64_t f = sx_floor_i64(v);
+    return (f < -2147483648ll || f > 2147483647ll) ? (int32_t)0x80000000 : (int32_t)f;
+}
+
+// The reference's inner product (cust_vector.hpp:105-121): a long double
+// chain over double products, which may be inf or NaN for fp64 inputs (SSE
+// products overflow; the x87 sum of finite doubles never does). Finite products
+// go through the soft FADD; special ones are tracked as IEEE addition would
+// combine them (any NaN, or +inf with -inf, gives NaN).
+struct SxSum {
+    sx80 s;
+    int pinf, ninf, nan;
+    SX_MD void init() { s = sx_zero(); pinf = ninf = nan = 0; }
+    SX_MD void add(double p) {
+        union { double d; uint64_t u; } c; c.d = p;
+        if (((c.u >> 52) & 0x7FF) != 0x7FF) { s = sx_add_double(s, p); return; }
+        if (c.u & 0xFFFFFFFFFFFFFull) nan = 1;
+        else if (c.u >> 63) ninf = 1;
+        else pinf = 1;
+    }
+    // 0 finite (s holds it), 1 +inf, -1 -inf, 2 NaN
+    SX_MD int special() const { return (nan || (pinf && ninf)) ? 2 : pinf ? 1 : ninf ? -1 : 0; }
+};
+
+// EuclideanHGen::generate (euclidean_h_gen.hpp:79-82): int(floorl((ip + t) / w)).
+SX_HD int32_t sx_hash_floor(const SxSum& ip, double t, float w) {
+    if (ip.special()) return (int32_t)0x80000000;             // floorl(inf / nan) -> indefinite
+    return sx_floor_int32(sx_div(sx_add_double(ip.s, t), sx_from_float(w)));
+}
+
+// CosineHGen::generate (cosine_h_gen.hpp:71-76): ip >= 0 (false for NaN).
+SX_HD int sx_hash_sign(const SxSum& ip) {
+    const int sp = ip.special();
+    return sp == 0 ? sx_ge_zero(ip.s) : sp == 1 ? 1 : 0;
+}
 
 // Round to double, nearest-even (x87 FST m64 / the long double -> double cast).
 SX_HD double sx_to_double(sx80 v) {

@@ -19,7 +19,8 @@ namespace lshkm {
 
 constexpr int KM_U = 16;
 
-__global__ __launch_bounds__(64) void km_chain_kernel(const float* __restrict__ X, int d, const int32_t* __restrict__ rows,
+template <typename TX>
+__global__ __launch_bounds__(64) void km_chain_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                      const int64_t* __restrict__ crow, int K,
                                                      const double* __restrict__ carry, const int64_t* __restrict__ carry_counts,
                                                      double* __restrict__ sums, int64_t* __restrict__ counts) {
@@ -33,7 +34,7 @@ __global__ __launch_bounds__(64) void km_chain_kernel(const float* __restrict__ 
     double s = carry ? carry[(size_t)c * d + j] : 0.0;
     int64_t p = beg;
     for (; p + KM_U <= end; p += KM_U) {
-        float v[KM_U];
+        TX v[KM_U];
 #pragma unroll
         for (int u = 0; u < KM_U; u++) v[u] = X[(int64_t)r4[p + u] * d + j];
 #pragma unroll
@@ -43,10 +44,15 @@ __global__ __launch_bounds__(64) void km_chain_kernel(const float* __restrict__ 
     sums[(size_t)c * d + j] = s;
 }
 
-int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K,
+int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K,
                     double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts) {
-    hipLaunchKernelGGL(km_chain_kernel, dim3((unsigned)K, (unsigned)((d + 63) / 64)), dim3(64), 0, s, X, d, rows, crow, K,
-                       carry, carry_counts, sums, counts);
+    const dim3 grid((unsigned)K, (unsigned)((d + 63) / 64));
+    if (X.f64)
+        hipLaunchKernelGGL(km_chain_kernel<double>, grid, dim3(64), 0, s, X.d(), d, rows, crow, K, carry, carry_counts,
+                           sums, counts);
+    else
+        hipLaunchKernelGGL(km_chain_kernel<float>, grid, dim3(64), 0, s, X.f(), d, rows, crow, K, carry, carry_counts,
+                           sums, counts);
     return kstatus("update.hip");
 }
 
@@ -57,10 +63,12 @@ int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, c
 // count * 2^t (t = the highest bit position + 1), so when
 // ceil(log2 count) + t - q <= 53 no step rounds and the chain's result is the
 // exact sum -- which integer (fixed-point) arithmetic computes in any order.
-// Values are accumulated as int128 multiples of 2^-KMF (KMF = 80): every fp32
-// value with lowest bit >= 2^-80 and magnitude < 2^23 fits; a chain with
-// anything else (huge, tiny, inf, nan), or whose range test fails, is flagged
-// and recomputed by the sequential kernel above (km_chain_kernel).
+// Values are accumulated as int128 multiples of 2^-KMF (KMF = 80): every value
+// with lowest bit >= 2^-80 and magnitude < 2^46 fits (fp32 rows, and fp64 rows
+// whose values have short mantissas); a chain with anything else (huge, tiny,
+// inf, nan), whose range test fails, or whose exact sum could leave the int128
+// range (ceil(log2 count) + top bit + KMF >= 127) is flagged and recomputed by
+// the sequential kernel above (km_chain_kernel).
 // Work: waves stream 512 consecutive member positions of the cluster-sorted
 // list (lane = dimension), flushing their int128 partial to the (c, j)
 // accumulator with two 64-bit atomics (the carry of the low word is exact mod
@@ -68,6 +76,7 @@ int launch_km_chain(hipStream_t s, const float* X, int d, const int32_t* rows, c
 constexpr int KMF = 80;
 constexpr int KMF_CH = 512;
 constexpr int KMF_BAD = 1 << 20;     // qmin marker of a chain that needs the sequential kernel
+constexpr int KMF_TMAX = 46;         // one value < 2^46: m 2^(e + KMF) < 2^126
 
 struct KmFx {                        // per (c, j), zeroed / initialised by km_fx_init_kernel
     unsigned long long lo;
@@ -91,7 +100,33 @@ __device__ inline void km_fx_flush(KmFx* a, __int128 v, int qmin, int tmax, bool
     atomicMax(&a->tmax, tmax);
 }
 
-__global__ __launch_bounds__(64) void km_fx_kernel(const float* __restrict__ X, int d, const int32_t* __restrict__ rows,
+// value = (-1)^sign * m * 2^e of an fp32 / fp64 row element; false for +-0 / inf / nan
+// (inf / nan set bad)
+__device__ inline bool km_fx_split(float v, uint64_t& m, int& e, bool& neg, bool& bad) {
+    const uint32_t b = __float_as_uint(v);
+    const int E = (int)((b >> 23) & 255u);
+    const uint32_t f = b & 0x7FFFFFu;
+    if (E == 255) { bad = true; return false; }
+    if (E == 0 && f == 0) return false;   // +-0 adds nothing (and -0 + 0 = +0 either way)
+    m = E ? (f | 0x800000u) : f;
+    e = (E ? E : 1) - 150;
+    neg = (b >> 31) != 0;
+    return true;
+}
+__device__ inline bool km_fx_split(double v, uint64_t& m, int& e, bool& neg, bool& bad) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const int E = (int)((b >> 52) & 2047u);
+    const uint64_t f = b & 0xFFFFFFFFFFFFFull;
+    if (E == 2047) { bad = true; return false; }
+    if (E == 0 && f == 0) return false;
+    m = E ? (f | (1ull << 52)) : f;
+    e = (E ? E : 1) - 1075;
+    neg = (b >> 63) != 0;
+    return true;
+}
+
+template <typename TX>
+__global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                   const int64_t* __restrict__ crow, int K, int64_t M,
                                                   KmFx* __restrict__ acc) {
     const int64_t p0 = (int64_t)blockIdx.x * KMF_CH;
@@ -112,9 +147,9 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const float* __restrict__ X, 
     int qmin = 1 << 30, tmax = -(1 << 30);
     bool bad = false;
     for (int64_t p = p0; p < p1; p += 16) {
-        float v[16];
+        TX v[16];
 #pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = (on && p + u < p1) ? X[(int64_t)r4[p + u] * d + j] : 0.f;
+        for (int u = 0; u < 16; u++) v[u] = (on && p + u < p1) ? X[(int64_t)r4[p + u] * d + j] : (TX)0;
 #pragma unroll
         for (int u = 0; u < 16; u++) {
             if (p + u >= p1) break;
@@ -124,19 +159,17 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const float* __restrict__ X, 
                 c++;
                 cend = crow[c + 1];
             }
-            const uint32_t b = __float_as_uint(v[u]);
-            const int E = (int)((b >> 23) & 255u);
-            const uint32_t f = b & 0x7FFFFFu;
-            if (E == 0 && f == 0) continue;      // +-0 adds nothing (and -0 + 0 = +0 either way)
-            if (E == 255) { bad = true; continue; }
-            const uint32_t m = E ? (f | 0x800000u) : f;
-            const int e = (E ? E : 1) - 150;     // value = m * 2^e
-            const int q = e + __builtin_ctz(m), t = e + 32 - __builtin_clz(m);
+            uint64_t m;
+            int e;
+            bool neg;
+            if (!km_fx_split(v[u], m, e, neg, bad)) continue;     // value = m * 2^e
+            const int q = e + __builtin_ctzll(m), t = e + 64 - __builtin_clzll(m);
             qmin = min(qmin, q);
             tmax = max(tmax, t);
-            if (q < -KMF || t > 23) { bad = true; continue; }
-            const __int128 w = (__int128)m << (e + KMF);
-            s += (b >> 31) ? -w : w;
+            if (q < -KMF || t > KMF_TMAX) { bad = true; continue; }
+            // shift out the trailing zeros first: e + KMF may be negative (q >= -KMF is not)
+            const __int128 w = (__int128)(m >> (q - e)) << (q + KMF);
+            s += neg ? -w : w;
         }
     }
     if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
@@ -165,7 +198,7 @@ __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_
             const uint64_t m = E ? (f | (1ull << 52)) : f;
             const int e = (E ? E : 1) - 1075;
             const int q = e + __builtin_ctzll(m), t = e + 64 - __builtin_clzll(m);
-            if (E == 2047 || q < -KMF || t > 23) ok = false;
+            if (E == 2047 || q < -KMF || t > KMF_TMAX) ok = false;
             else {
                 qmin = min(qmin, q);
                 tmax = max(tmax, t);
@@ -177,6 +210,8 @@ __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_
     int lc = 0;
     while (((int64_t)1 << lc) < cnt) lc++;          // ceil(log2 count)
     if (ok && qmin <= tmax && lc + tmax - qmin > 53) ok = false;
+    // |exact sum| < count 2^tmax must stay inside the int128 accumulator
+    if (ok && qmin <= tmax && lc + tmax + KMF >= 127) ok = false;
     if (ok) {
         // |s| < 2^(53 + qmin + KMF): the conversion is exact, and so is the scaling
         sums[i] = ldexp((double)s, -KMF);
@@ -186,7 +221,8 @@ __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_
 }
 
 // The sequential chains of the flagged (c, 64-dim block)s only.
-__global__ __launch_bounds__(64) void km_chain_flagged_kernel(const float* __restrict__ X, int d,
+template <typename TX>
+__global__ __launch_bounds__(64) void km_chain_flagged_kernel(const TX* __restrict__ X, int d,
                                                              const int32_t* __restrict__ rows,
                                                              const int64_t* __restrict__ crow, int K,
                                                              const double* __restrict__ carry,
@@ -200,7 +236,7 @@ __global__ __launch_bounds__(64) void km_chain_flagged_kernel(const float* __res
     const int64_t beg = crow[c], end = crow[c + 1];
     int64_t p = beg;
     for (; p + KM_U <= end; p += KM_U) {
-        float v[KM_U];
+        TX v[KM_U];
 #pragma unroll
         for (int u = 0; u < KM_U; u++) v[u] = X[(int64_t)r4[p + u] * d + j];
 #pragma unroll
@@ -218,7 +254,7 @@ __global__ void km_counts_kernel(const int64_t* __restrict__ crow, int K, const 
 
 size_t km_fx_ws_bytes(int K, int d) { return (size_t)K * d * sizeof(KmFx) + (size_t)K * 4 + 64; }
 
-int launch_km_sums_fx(hipStream_t s, const float* X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
                       double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws) {
     KmFx* acc = reinterpret_cast<KmFx*>(ws);
     int* flag = reinterpret_cast<int*>(acc + (size_t)K * d);
@@ -226,13 +262,19 @@ int launch_km_sums_fx(hipStream_t s, const float* X, int d, const int32_t* rows,
     (void)hipMemsetAsync(flag, 0, (size_t)K * 4, s);
     hipLaunchKernelGGL(km_fx_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, n);
     const int jb = (d + 63) / 64;
-    if (M > 0)
-        hipLaunchKernelGGL(km_fx_kernel, dim3((unsigned)((M + KMF_CH - 1) / KMF_CH), (unsigned)jb), dim3(64), 0, s, X, d,
-                           rows, crow, K, M, acc);
+    const dim3 fgrid((unsigned)((M + KMF_CH - 1) / KMF_CH), (unsigned)jb);
+    if (M > 0) {
+        if (X.f64) hipLaunchKernelGGL(km_fx_kernel<double>, fgrid, dim3(64), 0, s, X.d(), d, rows, crow, K, M, acc);
+        else hipLaunchKernelGGL(km_fx_kernel<float>, fgrid, dim3(64), 0, s, X.f(), d, rows, crow, K, M, acc);
+    }
     hipLaunchKernelGGL(km_fx_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, crow, K, d, carry,
                        carry_counts, sums, flag);
-    hipLaunchKernelGGL(km_chain_flagged_kernel, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K,
-                       carry, flag, sums);
+    if (X.f64)
+        hipLaunchKernelGGL(km_chain_flagged_kernel<double>, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X.d(), d,
+                           rows, crow, K, carry, flag, sums);
+    else
+        hipLaunchKernelGGL(km_chain_flagged_kernel<float>, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X.f(), d,
+                           rows, crow, K, carry, flag, sums);
     if (counts)
         hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
                            counts);

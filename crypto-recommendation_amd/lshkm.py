@@ -102,13 +102,15 @@ def lib():
             "lshkm_p_closest": (i32, [vp, vp, i64, i32, vp, i64, vp, vp, i32, vp, vp, vp]),
             "lshkm_top_n_recom": (i32, [vp, vp, vp, i64, i32, vp, i64, vp, vp, vp, vp, vp, i32, i32, vp]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
+            "lshkm_clusters": (i32, [vp, vp, i64, i32, vp, vp]),
         }
         for name, (res, args) in sigs.items():
-            if not hasattr(L, name):
-                continue   # reported by tests/test_lib_cpu.py::test_exports
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
+            for nm in (name, name + "_f64"):     # fp64-row twins share the signature
+                if not hasattr(L, nm):
+                    continue   # reported by tests/test_lib_cpu.py::test_exports
+                fn = getattr(L, nm)
+                fn.restype = res
+                fn.argtypes = args
         _lib = L
     return _lib
 
@@ -124,6 +126,18 @@ def _np_ptr(a):
 
 def _t_ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
+
+
+# Entry points that read dataset rows exist for fp32 rows (name) and fp64 rows
+# (name_f64, SURVEY §8a: general doubles such as the recommender's user
+# vectors); the rows' dtype picks one.
+def _fn(name, X):
+    dt = str(X.dtype)
+    if dt.endswith("float32"):
+        return getattr(lib(), name)
+    if dt.endswith("float64"):
+        return getattr(lib(), name + "_f64")
+    raise LshkmError(f"{name}: rows must be float32 or float64, got {dt}")
 
 
 # ------------------------------------------------------------------ parameters
@@ -229,11 +243,11 @@ class LSH:
         tu = self.ctx.empty((N, self.L, self.k), torch.int32) if (tuples and self.metric == EUCLIDEAN) else None
         ph = self.ctx.empty((N, self.L), torch.int32) if phi else None
         bu = self.ctx.empty((N, self.L), torch.int32) if bucket else None
-        _ck(lib().lshkm_lsh_hash(self.h, _t_ptr(X), N, _t_ptr(tu), _t_ptr(ph), _t_ptr(bu)))
+        _ck(_fn("lshkm_lsh_hash", X)(self.h, _t_ptr(X), N, _t_ptr(tu), _t_ptr(ph), _t_ptr(bu)))
         return tu, ph, bu
 
     def build(self, X):
-        _ck(lib().lshkm_lsh_build(self.h, _t_ptr(X), X.shape[0]))
+        _ck(_fn("lshkm_lsh_build", X)(self.h, _t_ptr(X), X.shape[0]))
         self.N = X.shape[0]
 
     def buckets(self, table):
@@ -247,10 +261,10 @@ class LSH:
         nq = Q.shape[0]
         ptr = self.ctx.empty((nq + 1,), torch.int64)
         total = C.c_int64()
-        _ck(lib().lshkm_lsh_query(self.h, _t_ptr(Q), nq, _t_ptr(alias_rows), int(filtered), _t_ptr(ptr), None, 0,
+        _ck(_fn("lshkm_lsh_query", Q)(self.h, _t_ptr(Q), nq, _t_ptr(alias_rows), int(filtered), _t_ptr(ptr), None, 0,
                                   C.byref(total)))
         out = self.ctx.empty((max(total.value, 1),), torch.int32)
-        _ck(lib().lshkm_lsh_query(self.h, _t_ptr(Q), nq, _t_ptr(alias_rows), int(filtered), _t_ptr(ptr), _t_ptr(out),
+        _ck(_fn("lshkm_lsh_query", Q)(self.h, _t_ptr(Q), nq, _t_ptr(alias_rows), int(filtered), _t_ptr(ptr), _t_ptr(out),
                                   total.value, C.byref(total)))
         self.ctx.sync()
         if device:                                   # device tensors, no host copy
@@ -284,12 +298,12 @@ class Cube:
             pass
 
     def build(self, X):
-        _ck(lib().lshkm_cube_build(self.h, _t_ptr(X), X.shape[0]))
+        _ck(_fn("lshkm_cube_build", X)(self.h, _t_ptr(X), X.shape[0]))
         self.N = X.shape[0]
 
     def vertices(self, Q):
         v = self.ctx.empty((Q.shape[0],), self.ctx.torch.int32)
-        _ck(lib().lshkm_cube_vertices(self.h, _t_ptr(Q), Q.shape[0], _t_ptr(v)))
+        _ck(_fn("lshkm_cube_vertices", Q)(self.h, _t_ptr(Q), Q.shape[0], _t_ptr(v)))
         return v
 
     def buckets(self):
@@ -308,10 +322,10 @@ class Cube:
     def unseen(self, X):
         """(f, h, first local row) of the (f, h) pairs in X without a coin yet (lshkm_cube_unseen)."""
         cnt = C.c_int64()
-        _ck(lib().lshkm_cube_unseen(self.h, _t_ptr(X), X.shape[0], None, None, None, 0, C.byref(cnt)))
+        _ck(_fn("lshkm_cube_unseen", X)(self.h, _t_ptr(X), X.shape[0], None, None, None, 0, C.byref(cnt)))
         n = cnt.value
         f = np.empty(max(n, 1), np.int32); hh = np.empty(max(n, 1), np.int32); r = np.empty(max(n, 1), np.int64)
-        _ck(lib().lshkm_cube_unseen(self.h, _t_ptr(X), X.shape[0], _np_ptr(f), _np_ptr(hh), _np_ptr(r), n,
+        _ck(_fn("lshkm_cube_unseen", X)(self.h, _t_ptr(X), X.shape[0], _np_ptr(f), _np_ptr(hh), _np_ptr(r), n,
                                     C.byref(cnt)))
         return f[:n], hh[:n], r[:n]
 
@@ -324,9 +338,9 @@ class Cube:
         nq = Q.shape[0]
         ptr = self.ctx.empty((nq + 1,), torch.int64)
         total = C.c_int64()
-        _ck(lib().lshkm_cube_query(self.h, _t_ptr(Q), nq, probes, _t_ptr(ptr), None, 0, C.byref(total)))
+        _ck(_fn("lshkm_cube_query", Q)(self.h, _t_ptr(Q), nq, probes, _t_ptr(ptr), None, 0, C.byref(total)))
         out = self.ctx.empty((max(total.value, 1),), torch.int32)
-        _ck(lib().lshkm_cube_query(self.h, _t_ptr(Q), nq, probes, _t_ptr(ptr), _t_ptr(out), total.value,
+        _ck(_fn("lshkm_cube_query", Q)(self.h, _t_ptr(Q), nq, probes, _t_ptr(ptr), _t_ptr(out), total.value,
                                    C.byref(total)))
         self.ctx.sync()
         if device:                                   # device tensors, no host copy
@@ -352,7 +366,7 @@ def lloyd_assign(ctx, X, Cc, metric="euclidean", src_rows=None, assign=None, dis
     assign = ctx.empty((N,), torch.int32) if assign is None else assign
     dist = ctx.empty((N,), torch.float64) if dist is None else dist
     sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
-    _ck(lib().lshkm_lloyd_assign(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _np_ptr(sr),
+    _ck(_fn("lshkm_lloyd_assign", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _np_ptr(sr),
                                  _t_ptr(assign), _t_ptr(dist)))
     return assign, dist
 
@@ -372,7 +386,7 @@ def range_assign(ctx, X, Cc, comb_ptr, comb_idx, metric="euclidean", key=None, s
     kk = None if key is None else np.ascontiguousarray(key, np.int32)
     sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
     passes = C.c_int32(0)
-    _ck(lib().lshkm_range_assign(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _t_ptr(cp), _t_ptr(ci),
+    _ck(_fn("lshkm_range_assign", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(Cc), K, _METRIC[metric], _t_ptr(cp), _t_ptr(ci),
                                  _np_ptr(kk), _np_ptr(sr), _t_ptr(assign), _t_ptr(dist), C.byref(passes)))
     return assign, dist, passes.value
 
@@ -383,7 +397,7 @@ def silhouette(ctx, X, assign, Cc, metric="euclidean"):
     K = Cc.shape[0]
     out = np.empty(K + 1, np.float64)
     s = ctx.empty((max(N, 1),), ctx.torch.float64)
-    _ck(lib().lshkm_silhouette(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), _t_ptr(Cc), K, _METRIC[metric], _np_ptr(out),
+    _ck(_fn("lshkm_silhouette", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), _t_ptr(Cc), K, _METRIC[metric], _np_ptr(out),
                                _t_ptr(s)))
     return out, s[:N]
 
@@ -450,7 +464,7 @@ def hash_assign(lsh, X, Cc, src_rows=None, tuples=True, phi=False, bucket=True):
     a = ctx.empty((N,), torch.int32)
     dist = ctx.empty((N,), torch.float64)
     sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
-    _ck(lib().lshkm_hash_assign(lsh.h, _t_ptr(X), N, _t_ptr(Cc), Cc.shape[0], _np_ptr(sr), _t_ptr(tu), _t_ptr(ph),
+    _ck(_fn("lshkm_hash_assign", X)(lsh.h, _t_ptr(X), N, _t_ptr(Cc), Cc.shape[0], _np_ptr(sr), _t_ptr(tu), _t_ptr(ph),
                                 _t_ptr(bu), _t_ptr(a), _t_ptr(dist)))
     return tu, ph, bu, a, dist
 
@@ -463,7 +477,7 @@ def kmeans_update(ctx, X, assign, C_old, metric="euclidean", min_dist=0.0):
     Cn = ctx.empty((K, d), torch.float64)
     cnt = ctx.empty((K,), torch.int64)
     cont = C.c_int()
-    _ck(lib().lshkm_kmeans_update(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), _t_ptr(C_old), K, _METRIC[metric],
+    _ck(_fn("lshkm_kmeans_update", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), _t_ptr(C_old), K, _METRIC[metric],
                                   float(min_dist), _t_ptr(Cn), _t_ptr(cnt), C.byref(cont)))
     return Cn, cnt, bool(cont.value)
 
@@ -473,7 +487,7 @@ def kmeans_partial(ctx, X, assign, K, sums=None, counts=None):
     N, d = X.shape
     sums = ctx.empty((K, d), torch.float64) if sums is None else sums
     counts = ctx.empty((K,), torch.int64) if counts is None else counts
-    _ck(lib().lshkm_kmeans_partial(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K, _t_ptr(sums), _t_ptr(counts)))
+    _ck(_fn("lshkm_kmeans_partial", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K, _t_ptr(sums), _t_ptr(counts)))
     return sums, counts
 
 
@@ -484,7 +498,7 @@ def kmeans_partial_carry(ctx, X, assign, K, carry_sums=None, carry_counts=None):
     N, d = X.shape
     sums = ctx.empty((K, d), torch.float64)
     counts = ctx.empty((K,), torch.int64)
-    _ck(lib().lshkm_kmeans_partial_carry(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K,
+    _ck(_fn("lshkm_kmeans_partial_carry", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K,
                                          _t_ptr(carry_sums) if carry_sums is not None else None,
                                          _t_ptr(carry_counts) if carry_counts is not None else None,
                                          _t_ptr(sums), _t_ptr(counts)))
@@ -505,8 +519,20 @@ def kmeans_pp_rows(ctx, X, K, metric="euclidean", seed=1):
     """k_means_pp (initialization.hpp:71-156): the K chosen dataset rows (int32 numpy)."""
     N, d = X.shape
     rows = np.empty(K, np.int32)
-    _ck(lib().lshkm_kmeans_pp(ctx.h, _t_ptr(X), N, d, K, _METRIC[metric], int(seed), _np_ptr(rows)))
+    _ck(_fn("lshkm_kmeans_pp", X)(ctx.h, _t_ptr(X), N, d, K, _METRIC[metric], int(seed), _np_ptr(rows)))
     return rows
+
+
+def clusters(ctx, assign, K):
+    """separate_clusters_from_input (utils.hpp:150-158): the member lists of the K
+    clusters as a CSR (crow [K+1] int64, rows [N] int32 device tensors; members
+    in row order)."""
+    torch = ctx.torch
+    N = assign.shape[0]
+    crow = ctx.empty((K + 1,), torch.int64)
+    rows = ctx.empty((max(N, 1),), torch.int32)
+    _ck(lib().lshkm_clusters(ctx.h, _t_ptr(assign), N, K, _t_ptr(crow), _t_ptr(rows)))
+    return crow, rows[:N]
 
 
 def rand_selection_rows(N, K, seed=1):

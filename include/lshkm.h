@@ -23,8 +23,12 @@
  *   - "_dev" pointers are device (HBM) pointers, "_host" pointers host memory.
  *     Sizes are explicit. Device outputs are written asynchronously on the
  *     context's stream; call lshkm_ctx_sync() before reading them on the host.
- *   - Points are fp32 rows, N x d row-major (the reference's doubles hold
- *     fp32-representable values). Centroids are fp64 rows, K x d.
+ *   - Points are N x d row-major rows of fp32 (the synthetic / proj-2 values
+ *     are fp32-representable: the tuned storage) or of fp64: every entry
+ *     point that reads dataset rows has a `_f64` twin taking `const double*`
+ *     rows with the same results contract (the reference's CustVector<double>
+ *     holds general doubles, e.g. the recommender's user vectors,
+ *     crypto_rec.hpp:78-140). Centroids are fp64 rows, K x d.
  *   - Bit-exact with the reference: tuples, phi, bucket IDs, bucket member
  *     order, query results, hypercube vertices, probe order, cluster IDs.
  *     Distances: exact-order fp64 (see DESIGN.md for the pow(x,2) note).
@@ -113,12 +117,15 @@ int lshkm_lsh_destroy(lshkm_lsh lsh);
  * any output may be NULL. For COSINE phi == bucket == g. */
 int lshkm_lsh_hash(lshkm_lsh lsh, const float* X_dev, int64_t N, int32_t* tuples_dev,
                    int32_t* phi_dev, int32_t* bucket_dev);
+int lshkm_lsh_hash_f64(lshkm_lsh lsh, const double* X_dev, int64_t N, int32_t* tuples_dev,
+                       int32_t* phi_dev, int32_t* bucket_dev);
 /* Insert all N rows (create_LSH_hashtables' insert loop, lsh_cube.hpp:69-70):
  * hashes, then a stable bucket scatter (member order = row order,
  * vector_bucket.hpp:41-44). The dataset rows and their tuples stay
  * device-resident in the handle (X_dev must stay valid for queries that use
  * alias rows only through their tuples; it is not read again). */
 int lshkm_lsh_build(lshkm_lsh lsh, const float* X_dev, int64_t N);
+int lshkm_lsh_build_f64(lshkm_lsh lsh, const double* X_dev, int64_t N);
 /* Bucket contents of one table (getBucketFromIndex, cust_hashtable.hpp:116-119):
  * row_ptr_host [nb+1], idx_host [N]. */
 int lshkm_lsh_get_buckets(lshkm_lsh lsh, int table, int64_t* row_ptr_host, int32_t* idx_host);
@@ -135,12 +142,16 @@ int lshkm_lsh_device_views(lshkm_lsh lsh, const int64_t** row_ptr_dev /*[L][nb+1
  * Two-phase: out_ptr_dev [nq+1] always written (prefix offsets); rows are
  * written to out_idx_dev only if total <= out_cap. *total_host = total rows.
  * A filling call (out_idx_dev != NULL) right after a sizing call (NULL) with
- * the same Q_dev, nq, alias_rows_dev and filtered -- and no other call on the
- * context's workspace in between -- reuses the sizing call's device state
- * (Q and alias contents must not change between the two calls). */
+ * the same Q_dev, nq, alias_rows_dev, filtered and out_ptr_dev buffer -- and no
+ * other call on the context's workspace in between -- reuses the sizing call's
+ * device state: the contents of Q, alias and out_ptr must not change between
+ * the two calls. Any other filling call recomputes everything. */
 int lshkm_lsh_query(lshkm_lsh lsh, const float* Q_dev, int64_t nq, const int32_t* alias_rows_dev,
                     int filtered, int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap,
                     int64_t* total_host);
+int lshkm_lsh_query_f64(lshkm_lsh lsh, const double* Q_dev, int64_t nq, const int32_t* alias_rows_dev,
+                        int filtered, int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap,
+                        int64_t* total_host);
 
 /* ---------------------------------------------------------------- hypercube
  * create_hypercube (lsh_cube.hpp:108-136): k EuclideanFGen (V,t,w + the lazy
@@ -152,9 +163,11 @@ int lshkm_cube_destroy(lshkm_cube cube);
  * with EuclideanF coins drawn on first sight of each h in (row, f) order
  * (euclidean_f_gen.hpp:65-79), then the stable scatter into 2^k buckets. */
 int lshkm_cube_build(lshkm_cube cube, const float* X_dev, int64_t N);
+int lshkm_cube_build_f64(lshkm_cube cube, const double* X_dev, int64_t N);
 /* Vertices of a query batch (getHash, cust_hashtable.hpp:122-125). Unseen h
  * values draw new coins in (query, f) order from the continued engine. */
 int lshkm_cube_vertices(lshkm_cube cube, const float* Q_dev, int64_t nq, int32_t* vertex_dev);
+int lshkm_cube_vertices_f64(lshkm_cube cube, const double* Q_dev, int64_t nq, int32_t* vertex_dev);
 int lshkm_cube_get_buckets(lshkm_cube cube, int64_t* row_ptr_host /*[2^k+1]*/, int32_t* idx_host /*[N]*/);
 /* get_hypercube_combined_buckets (lsh_cube.hpp:139-177): main bucket then
  * `probes` neighbours in get_num_hamming_dist_from order (utils.cpp:22-50),
@@ -162,6 +175,8 @@ int lshkm_cube_get_buckets(lshkm_cube cube, int64_t* row_ptr_host /*[2^k+1]*/, i
  * lshkm_lsh_query. */
 int lshkm_cube_query(lshkm_cube cube, const float* Q_dev, int64_t nq, int probes,
                      int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap, int64_t* total_host);
+int lshkm_cube_query_f64(lshkm_cube cube, const double* Q_dev, int64_t nq, int probes,
+                         int64_t* out_ptr_dev, int32_t* out_idx_dev, int64_t out_cap, int64_t* total_host);
 /* Sharded build of the euclidean cube (the coins of
  * euclidean_f_gen.hpp:65-79 must be drawn in GLOBAL first-occurrence order):
  * 1. each shard: lshkm_cube_unseen -> the (f, h) pairs of its rows that have
@@ -173,6 +188,8 @@ int lshkm_cube_query(lshkm_cube cube, const float* Q_dev, int64_t nq, int probes
  *    draws), then lshkm_cube_build (no coin left to draw). */
 int lshkm_cube_unseen(lshkm_cube cube, const float* X_dev, int64_t N, int32_t* f_host, int32_t* h_host,
                       int64_t* row_host, int64_t cap, int64_t* count_host);
+int lshkm_cube_unseen_f64(lshkm_cube cube, const double* X_dev, int64_t N, int32_t* f_host, int32_t* h_host,
+                          int64_t* row_host, int64_t cap, int64_t* count_host);
 int lshkm_cube_import_coins(lshkm_cube cube, const int32_t* f_host, const int32_t* h_host, const int32_t* bit_host,
                             int64_t n, uint32_t rng_state);
 /* Host draw of n coins in order from *rng_state (minstd_rand0 state, updated):
@@ -190,6 +207,9 @@ int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f_host, int32_t* h_host, int32
 int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const double* C_dev,
                        int K, int metric, const int32_t* src_rows_host, int32_t* assign_dev,
                        double* dist_dev);
+int lshkm_lloyd_assign_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const double* C_dev,
+                           int K, int metric, const int32_t* src_rows_host, int32_t* assign_dev,
+                           double* dist_dev);
 /* The hot path in one pass over the points: LSH hashing of the rows
  * (EuclideanPhiGen::generate for every table, euclidean_phi_gen.hpp:77-92, and
  * the bucket index of cust_hashtable.hpp:68) and lloyds_assignment
@@ -199,17 +219,25 @@ int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, cons
 int lshkm_hash_assign(lshkm_lsh lsh, const float* X_dev, int64_t N, const double* C_dev, int K,
                       const int32_t* src_rows_host, int32_t* tuples_dev, int32_t* phi_dev, int32_t* bucket_dev,
                       int32_t* assign_dev, double* dist_dev);
+int lshkm_hash_assign_f64(lshkm_lsh lsh, const double* X_dev, int64_t N, const double* C_dev, int K,
+                          const int32_t* src_rows_host, int32_t* tuples_dev, int32_t* phi_dev, int32_t* bucket_dev,
+                          int32_t* assign_dev, double* dist_dev);
 /* k_means (update.hpp:37-86): exact-order per-cluster fp64 sums in row order,
  * divided by the count unless empty; *cont_host = 1 iff some center moved
  * more than min_dist. C_new_dev [K][d], counts_dev [K] (may be NULL). */
 int lshkm_kmeans_update(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
                         const double* C_old_dev, int K, int metric, double min_dist,
                         double* C_new_dev, int64_t* counts_dev, int* cont_host);
+int lshkm_kmeans_update_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int32_t* assign_dev,
+                            const double* C_old_dev, int K, int metric, double min_dist,
+                            double* C_new_dev, int64_t* counts_dev, int* cont_host);
 /* Sharded update (fast mode): per-shard exact-order sums, no division.
  * sums_dev [K][d], counts_dev [K]. Combine across ranks with an all-reduce,
  * then lshkm_kmeans_finalize. */
 int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
                          int K, double* sums_dev, int64_t* counts_dev);
+int lshkm_kmeans_partial_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int32_t* assign_dev,
+                             int K, double* sums_dev, int64_t* counts_dev);
 /* Sharded update (exact mode): the per-(c, j) chains continue from
  * carry_sums_dev / carry_counts_dev (the previous shard's result, or NULL for
  * the first shard), so passing the carry shard to shard in row order gives the
@@ -217,9 +245,19 @@ int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, co
 int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
                                int K, const double* carry_sums_dev, const int64_t* carry_counts_dev,
                                double* sums_dev, int64_t* counts_dev);
+int lshkm_kmeans_partial_carry_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d,
+                                   const int32_t* assign_dev, int K, const double* carry_sums_dev,
+                                   const int64_t* carry_counts_dev, double* sums_dev, int64_t* counts_dev);
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* counts_dev, int K, int d,
                           const double* C_old_dev, int metric, double min_dist, double* C_new_dev,
                           int* cont_host);
+/* separate_clusters_from_input (utils.hpp:150-158): the clusters' member lists
+ * as a CSR, cluster c = rows_dev[crow_dev[c] .. crow_dev[c+1]) in row order
+ * (the insertion order of the reference's per-cluster vectors). assign_dev
+ * values must lie in [0, K) (what lshkm_lloyd_assign writes). crow_dev [K+1],
+ * rows_dev [N]. */
+int lshkm_clusters(lshkm_ctx ctx, const int32_t* assign_dev, int64_t N, int K, int64_t* crow_dev,
+                   int32_t* rows_dev);
 
 /* --------------------------------------------------------- range assignment
  * lsh_range_assignment / cube_range_assignment (assignment.hpp:108-145):
@@ -237,6 +275,10 @@ int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* 
 int lshkm_range_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const double* C_dev, int K, int metric,
                        const int64_t* comb_ptr_dev, const int32_t* comb_idx_dev, const int32_t* key_host,
                        const int32_t* src_rows_host, int32_t* assign_dev, double* dist_dev, int* passes_host);
+int lshkm_range_assign_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const double* C_dev, int K,
+                           int metric, const int64_t* comb_ptr_dev, const int32_t* comb_idx_dev,
+                           const int32_t* key_host, const int32_t* src_rows_host, int32_t* assign_dev,
+                           double* dist_dev, int* passes_host);
 
 /* --------------------------------------------------------------- silhouette
  * silhouette_cluster (silhouette.hpp:31-80) over the clusters of `assign`
@@ -247,6 +289,8 @@ int lshkm_range_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, cons
  * the reference's order; NaNs as x86 produces them (empty cluster: 0/0). */
 int lshkm_silhouette(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int32_t* assign_dev,
                      const double* C_dev, int K, int metric, double* out_host, double* s_dev);
+int lshkm_silhouette_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int32_t* assign_dev,
+                         const double* C_dev, int K, int metric, double* out_host, double* s_dev);
 
 /* ----------------------------------------------------------- initialization
  * k_means_pp (initialization.hpp:71-156): the K dataset rows chosen as initial
@@ -257,6 +301,8 @@ int lshkm_silhouette(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const 
  * (the reference's distance cache is keyed by them). N < 2^31, d <= 4096. */
 int lshkm_kmeans_pp(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, int K, int metric, uint64_t seed,
                     int32_t* rows_host);
+int lshkm_kmeans_pp_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, int K, int metric, uint64_t seed,
+                        int32_t* rows_host);
 /* rand_selection (initialization.hpp:39-69): K distinct rows drawn uniformly,
  * redrawing on a repeat. Host only. 1 <= K <= N. */
 int lshkm_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows_host);

@@ -33,12 +33,13 @@
  * 112-114); the overloads without a seed do the same, the ones with a trailing
  * `seed` argument make a run reproducible.
  *
- * Data: the device holds points as fp32. Vector components must be exactly
- * representable in fp32 (the reference's inputs are) — anything
- * else throws std::domain_error rather than silently rounding. Centroids are
- * fp64 and may hold any value. Dataset rows are hashed when the table is
- * built, as the reference's insertVector does; re-hashing a dataset row later
- * returns that hash (the reference never mutates its input vectors).
+ * Data: vectors go to the device as fp32 rows when every component is an fp32
+ * value (the tuned storage: the synthetic and proj-2 inputs are) and as fp64
+ * rows otherwise (the `_f64` entry points: general doubles such as the
+ * recommender's user vectors, crypto_rec.hpp:78-140); the results are the
+ * same either way. Centroids are fp64. Dataset rows are hashed when the table
+ * is built, as the reference's insertVector does; re-hashing a dataset row
+ * later returns that hash (the reference never mutates its input vectors).
  *
  * Errors from the library throw lshkm_compat::Error (std::runtime_error). The
  * device is ordinal LSHKM_DEVICE (environment, default 0); one context per
@@ -130,27 +131,58 @@ inline unsigned long clock_seed() {   // lsh_cube.hpp:48
     return std::chrono::system_clock::now().time_since_epoch().count();
 }
 
-// One vector's components as fp32, refusing any that would round.
+// Rows on the device: fp32 when every component is an fp32 value, else fp64.
+struct DevRows {
+    DevMem m;
+    bool f64 = false;
+    const float* f() const { return m.as<float>(); }
+    const double* d() const { return m.as<double>(); }
+};
+
 template <typename T>
-void pack_row(CustVector<T>& v, size_t d, float* out) {
+const std::vector<T>& dims_of(CustVector<T>& v, size_t d) {
     const std::vector<T>& x = *v.getDimensions();
     if (x.size() != d)
         throw std::invalid_argument("lshkm_compat: vector '" + v.getId() + "' has " + std::to_string(x.size()) +
                                     " dimensions, expected " + std::to_string(d));
-    for (size_t j = 0; j < d; j++) {
-        const float f = static_cast<float>(x[j]);
-        if (static_cast<T>(f) != x[j])
-            throw std::domain_error("lshkm_compat: component " + std::to_string(j) + " of vector '" + v.getId() +
-                                    "' is not representable in fp32");
-        out[j] = f;
-    }
+    return x;
 }
 
 template <typename T>
-std::vector<float> pack_rows(std::vector<CustVector<T>>& vs, size_t d) {
-    std::vector<float> X(vs.size() * d);
-    for (size_t i = 0; i < vs.size(); i++) pack_row(vs[i], d, X.data() + i * d);
-    return X;
+DevRows upload_rows(CustVector<T>* const* vs, size_t n, size_t d) {
+    bool fp32 = true;
+    for (size_t i = 0; i < n && fp32; i++) {
+        const std::vector<T>& x = dims_of(*vs[i], d);
+        for (size_t j = 0; j < d; j++)
+            if (static_cast<T>(static_cast<float>(x[j])) != x[j]) { fp32 = false; break; }
+    }
+    DevRows r;
+    r.f64 = !fp32;
+    if (fp32) {
+        std::vector<float> X(n * d);
+        for (size_t i = 0; i < n; i++)
+            for (size_t j = 0; j < d; j++) X[i * d + j] = static_cast<float>((*vs[i]->getDimensions())[j]);
+        r.m = upload(X.data(), X.size());
+    } else {
+        std::vector<double> X(n * d);
+        for (size_t i = 0; i < n; i++)
+            for (size_t j = 0; j < d; j++) X[i * d + j] = static_cast<double>((*vs[i]->getDimensions())[j]);
+        r.m = upload(X.data(), X.size());
+    }
+    return r;
+}
+
+template <typename T>
+DevRows upload_rows(std::vector<CustVector<T>>& vs, size_t d) {
+    std::vector<CustVector<T>*> p(vs.size());
+    for (size_t i = 0; i < vs.size(); i++) p[i] = &vs[i];
+    return upload_rows(p.data(), p.size(), d);
+}
+
+template <typename T>
+DevRows upload_row(CustVector<T>& v, size_t d) {
+    CustVector<T>* p = &v;
+    return upload_rows(&p, 1, d);
 }
 
 // Index of `v` in the dataset [base, base + n), or -1.
@@ -180,12 +212,12 @@ struct LshState {
 
     void hash_query(CustVector<T>* v) {
         if (v == q_ptr && *v->getDimensions() == q_dims) return;
-        std::vector<float> x(d);
-        pack_row(*v, d, x.data());
-        DevMem X = upload(x.data(), d);
+        const DevRows X = upload_row(*v, d);
         DevMem val(sizeof(int32_t) * L), tup(sizeof(int32_t) * L * k);
         const bool eu = metric == LSHKM_METRIC_EUCLIDEAN;
-        check(lshkm_lsh_hash(h, X.as<float>(), 1, eu ? tup.as<int32_t>() : nullptr, val.as<int32_t>(), nullptr));
+        int32_t* tp = eu ? tup.as<int32_t>() : nullptr;
+        check(X.f64 ? lshkm_lsh_hash_f64(h, X.d(), 1, tp, val.as<int32_t>(), nullptr)
+                    : lshkm_lsh_hash(h, X.f(), 1, tp, val.as<int32_t>(), nullptr));
         q_value.resize(L);
         download(q_value.data(), val, L);
         q_tuples.assign(eu ? (size_t)L * k : 0, 0);
@@ -265,10 +297,11 @@ std::vector<CustHashtable<T>*> create_LSH_hashtables(std::vector<CustVector<T>>&
 
     // every row, every table in one device pass
     const size_t N = (size_t)st->N;
-    std::vector<float> X = pack_rows(input_vectors, st->d);
-    DevMem Xd = upload(X.data(), X.size());
+    const DevRows Xd = upload_rows(input_vectors, st->d);
     DevMem val(sizeof(int32_t) * N * L), tup(eu ? sizeof(int32_t) * N * L * k : 0);
-    check(lshkm_lsh_hash(st->h, Xd.as<float>(), st->N, eu ? tup.as<int32_t>() : nullptr, val.as<int32_t>(), nullptr));
+    int32_t* tp = eu ? tup.as<int32_t>() : nullptr;
+    check(Xd.f64 ? lshkm_lsh_hash_f64(st->h, Xd.d(), st->N, tp, val.as<int32_t>(), nullptr)
+                 : lshkm_lsh_hash(st->h, Xd.f(), st->N, tp, val.as<int32_t>(), nullptr));
     st->value.resize(N * L);
     download(st->value.data(), val, N * L);
     if (eu) {
@@ -316,10 +349,10 @@ public:
         const CubeState<T>& s = *st_;
         const int64_t r = row_of<T>(v, s.base, s.N);
         if (r >= 0) return s.vertex[(size_t)r];
-        std::vector<float> x(s.d);
-        pack_row(*v, s.d, x.data());
-        DevMem X = upload(x.data(), s.d), vert(sizeof(int32_t));
-        check(lshkm_cube_vertices(s.h, X.as<float>(), 1, vert.as<int32_t>()));
+        const DevRows X = upload_row(*v, s.d);
+        DevMem vert(sizeof(int32_t));
+        check(X.f64 ? lshkm_cube_vertices_f64(s.h, X.d(), 1, vert.as<int32_t>())
+                    : lshkm_cube_vertices(s.h, X.f(), 1, vert.as<int32_t>()));
         int32_t out = 0;
         download(&out, vert, 1);
         return out;
@@ -355,11 +388,12 @@ CustHashtable<T>* create_hypercube(std::vector<CustVector<T>>& input_vectors, co
     }
     // the build draws the coins in (row, f) order, as the insert loop (lsh_cube.hpp:132-133)
     const size_t N = (size_t)st->N;
-    std::vector<float> X = pack_rows(input_vectors, st->d);
-    DevMem Xd = upload(X.data(), X.size());
-    check(lshkm_cube_build(st->h, Xd.as<float>(), st->N));
+    const DevRows Xd = upload_rows(input_vectors, st->d);
+    check(Xd.f64 ? lshkm_cube_build_f64(st->h, Xd.d(), st->N) : lshkm_cube_build(st->h, Xd.f(), st->N));
     DevMem vert(sizeof(int32_t) * N);
-    check(lshkm_cube_vertices(st->h, Xd.as<float>(), st->N, vert.as<int32_t>()));   // all h seen: no draws
+    // all h seen: no draws
+    check(Xd.f64 ? lshkm_cube_vertices_f64(st->h, Xd.d(), st->N, vert.as<int32_t>())
+                 : lshkm_cube_vertices(st->h, Xd.f(), st->N, vert.as<int32_t>()));
     st->vertex.resize(N);
     download(st->vertex.data(), vert, N);
 
@@ -398,14 +432,16 @@ void lloyds_assignment(std::vector<CustVector<T>>& input_vectors, std::vector<Cu
         return;
     }
     const size_t N = input_vectors.size(), K = centroids.size(), d = input_vectors[0].getDimensions()->size();
-    std::vector<float> X = pack_rows(input_vectors, d);
+    const DevRows Xd = upload_rows(input_vectors, d);
     std::vector<double> C = pack_centers(centroids, d);
     std::vector<int32_t> src(K);
     for (size_t c = 0; c < K; c++) src[c] = (int32_t)row_of<T>(centroids[c], input_vectors.data(), (int64_t)N);
-    DevMem Xd = upload(X.data(), X.size()), Cd = upload(C.data(), C.size());
+    DevMem Cd = upload(C.data(), C.size());
     DevMem ad(sizeof(int32_t) * N), dd(sizeof(double) * N);
-    check(lshkm_lloyd_assign(context(), Xd.as<float>(), (int64_t)N, (int)d, Cd.as<double>(), (int)K, metric,
-                             src.data(), ad.as<int32_t>(), dd.as<double>()));
+    check(Xd.f64 ? lshkm_lloyd_assign_f64(context(), Xd.d(), (int64_t)N, (int)d, Cd.as<double>(), (int)K, metric,
+                                          src.data(), ad.as<int32_t>(), dd.as<double>())
+                 : lshkm_lloyd_assign(context(), Xd.f(), (int64_t)N, (int)d, Cd.as<double>(), (int)K, metric,
+                                      src.data(), ad.as<int32_t>(), dd.as<double>()));
     std::vector<int32_t> a(N);
     std::vector<double> dist(N);
     download(a.data(), ad, N);
@@ -428,7 +464,7 @@ bool k_means(std::vector<CustVector<T>>& input_vectors, std::vector<CustVector<T
     const int metric = metric_of(metric_type);
     if (centers.empty()) return false;
     const size_t N = input_vectors.size(), K = centers.size(), d = centers[0]->getDimensions()->size();
-    std::vector<float> X = pack_rows(input_vectors, d);
+    const DevRows Xd = upload_rows(input_vectors, d);
     std::vector<int32_t> a(N);
     for (size_t i = 0; i < N; i++) {
         a[i] = input_vectors[i].getCluster();
@@ -436,11 +472,13 @@ bool k_means(std::vector<CustVector<T>>& input_vectors, std::vector<CustVector<T
             throw std::out_of_range("lshkm_compat: vector '" + input_vectors[i].getId() + "' has no cluster in [0, K)");
     }
     std::vector<double> C = pack_centers(centers, d);
-    DevMem Xd = upload(X.data(), X.size()), ad = upload(a.data(), N), Cd = upload(C.data(), C.size());
+    DevMem ad = upload(a.data(), N), Cd = upload(C.data(), C.size());
     DevMem Cn(sizeof(double) * K * d);
     int cont = 0;
-    check(lshkm_kmeans_update(context(), Xd.as<float>(), (int64_t)N, (int)d, ad.as<int32_t>(), Cd.as<double>(),
-                              (int)K, metric, min_dist, Cn.as<double>(), nullptr, &cont));
+    check(Xd.f64 ? lshkm_kmeans_update_f64(context(), Xd.d(), (int64_t)N, (int)d, ad.as<int32_t>(), Cd.as<double>(),
+                                           (int)K, metric, min_dist, Cn.as<double>(), nullptr, &cont)
+                 : lshkm_kmeans_update(context(), Xd.f(), (int64_t)N, (int)d, ad.as<int32_t>(), Cd.as<double>(),
+                                       (int)K, metric, min_dist, Cn.as<double>(), nullptr, &cont));
     if (!cont) return false;
     std::vector<double> Cnew(K * d);
     download(Cnew.data(), Cn, K * d);
@@ -462,10 +500,10 @@ std::vector<CustVector<T>*> k_means_pp(std::vector<CustVector<T>>& input_vectors
     const int metric = metric_of(metric_type);
     if (input_vectors.empty() || cluster_num < 1) throw std::invalid_argument("lshkm_compat: empty input or K < 1");
     const size_t N = input_vectors.size(), d = input_vectors[0].getDimensions()->size();
-    std::vector<float> X = pack_rows(input_vectors, d);
-    DevMem Xd = upload(X.data(), X.size());
+    const DevRows Xd = upload_rows(input_vectors, d);
     std::vector<int32_t> rows(cluster_num);
-    check(lshkm_kmeans_pp(context(), Xd.as<float>(), (int64_t)N, (int)d, cluster_num, metric, seed, rows.data()));
+    check(Xd.f64 ? lshkm_kmeans_pp_f64(context(), Xd.d(), (int64_t)N, (int)d, cluster_num, metric, seed, rows.data())
+                 : lshkm_kmeans_pp(context(), Xd.f(), (int64_t)N, (int)d, cluster_num, metric, seed, rows.data()));
     std::vector<CustVector<T>*> centroids(cluster_num);
     for (int i = 0; i < cluster_num; i++) centroids[i] = &input_vectors[rows[i]];
     return centroids;

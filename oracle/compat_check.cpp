@@ -8,8 +8,9 @@
 // reference ships. The reference's clock seed is interposed as in
 // ref_harness.cpp so both sides draw from the same engine seed.
 //
-// usage: compat_check SEED N d K   -> prints "compat ok" and exits 0, or the
-// first mismatches and exits 1.
+// usage: compat_check SEED N d K [f64]  -> prints "compat ok" and exits 0, or
+// the first mismatches and exits 1. "f64": the components are general doubles
+// (not fp32 values; the shim then takes the `_f64` entry points).
 
 #include <chrono>
 #include <cstdio>
@@ -48,12 +49,15 @@ static void fail(const std::string& what) {
     if (g_bad++ < 20) std::printf("MISMATCH %s\n", what.c_str());
 }
 
-static std::vector<Vec> make_data(uint64_t seed, int N, int d) {
+static std::vector<Vec> make_data(uint64_t seed, int N, int d, bool f64) {
     std::vector<Vec> v;
     v.reserve(N);
     for (int i = 0; i < N; i++) {
         std::vector<double> x(d);
-        for (int j = 0; j < d; j++) x[j] = (double)lshkm_synth_value(seed, i, d, j);
+        for (int j = 0; j < d; j++) {
+            x[j] = (double)lshkm_synth_value(seed, i, d, j);
+            if (f64) x[j] = x[j] * (1.0 + 1e-3 * std::sin(1.0 + 0.7 * j + 1.3 * i)) + 1e-4 * std::cos(j + 0.5 * i);
+        }
         v.emplace_back("item" + std::to_string(i), x);
     }
     return v;
@@ -174,6 +178,42 @@ static void check_recom(std::vector<Vec>& data, int P) {
     }
 }
 
+// main.cpp:149-176 (Part A) as written: cosine LSH over the user vectors, then
+// per user get_LSH_filtered_combined_buckets, get_P_closest, get_top_N_recom.
+static void check_chain(std::vector<Vec>& data, int k, int L, int P) {
+    g_seed += 404;
+    std::vector<Vec> users;
+    users.reserve(data.size());
+    for (size_t i = 0; i < data.size(); i++) {
+        std::set<int> unk;
+        const int d = (int)data[i].getDimensions()->size();
+        for (int j = 0; j < d; j++)
+            if ((j * 5 + (int)i) % 7 == 0) unk.insert(j);
+        users.emplace_back("u" + std::to_string(i), *data[i].getDimensions(), unk, ((int)(i % 9) - 4) / 8.0);
+    }
+    std::vector<CustHashtable<double>*> ref = create_LSH_hashtables<double>(users, "cosine", k, L, 100, 0.4);
+    std::vector<CustHashtable<double>*> gpu = lshkm_compat::create_LSH_hashtables<double>(users, "cosine", k, L, 100, 0.4);
+    const std::string tag = "chain ";
+    for (size_t q = 0; q < users.size(); q += 3) {
+        Vec& user = users[q];
+        std::vector<Vec*> na = get_LSH_filtered_combined_buckets(ref, &user);
+        std::vector<Vec*> nb = get_LSH_filtered_combined_buckets(gpu, &user);
+        cmp_ptrs(na, nb, tag + "neighbours, user " + std::to_string(q));
+        if (na.empty() || na != nb) continue;
+        std::vector<double> sa = get_P_closest(na, user, P);
+        std::vector<double> sb = lshkm_compat::get_P_closest(nb, user, P);
+        cmp_ptrs(na, nb, tag + "P-closest order, user " + std::to_string(q));
+        for (size_t i = 0; i < sa.size() && i < sb.size(); i++)
+            if (std::fabs(sa[i] - sb[i]) > 1e-14 * std::fabs(sa[i])) fail(tag + "similarity, user " + std::to_string(q));
+        if (sa.size() != sb.size()) fail(tag + "similarity count, user " + std::to_string(q));
+        if (get_top_N_recom(na, user, 5, sa) != lshkm_compat::get_top_N_recom(nb, user, 5, sb))
+            fail(tag + "top-N, user " + std::to_string(q));
+        g_stat["chain_users"]++;
+    }
+    for (auto t : ref) delete t;
+    for (auto t : gpu) delete t;
+}
+
 static void check_init(std::vector<Vec>& data, const std::string& metric, int K) {
     g_seed += 303;
     const std::string tag = "init/" + metric + " ";
@@ -219,12 +259,13 @@ static void check_kmeans(std::vector<Vec>& data, const std::string& metric, int 
 
 int main(int argc, char** argv) {
     if (argc < 5) {
-        std::fprintf(stderr, "usage: compat_check SEED N d K\n");
+        std::fprintf(stderr, "usage: compat_check SEED N d K [f64]\n");
         return 2;
     }
     g_seed = std::atoll(argv[1]);
     const int N = std::atoi(argv[2]), d = std::atoi(argv[3]), K = std::atoi(argv[4]);
-    std::vector<Vec> data = make_data((uint64_t)g_seed, N, d);
+    const bool f64 = argc > 5 && std::string(argv[5]) == "f64";
+    std::vector<Vec> data = make_data((uint64_t)g_seed, N, d, f64);
     try {
         check_lsh(data, "euclidean", 4, 5, 50, 4.0);
         check_lsh(data, "cosine", 6, 3, 8, 4.0);
@@ -235,6 +276,7 @@ int main(int argc, char** argv) {
         check_init(data, "euclidean", K);
         check_init(data, "cosine", K);
         check_recom(data, 10);
+        check_chain(data, 4, 5, 20);
     } catch (const std::exception& e) {
         std::printf("EXCEPTION %s\n", e.what());
         return 1;

@@ -159,7 +159,7 @@ uint32_t or_gen_cube_cosine(uint64_t seed, int k, int d, double* R) {
 
 /* EuclideanHGen::generate (euclidean_h_gen.hpp:73-76) over
  * CustVector<float>::inner_product<double> (cust_vector.hpp:105-121). */
-int32_t or_euclid_h(const float* v, const float* x, int d, float t, float w) {
+int32_t or_euclid_h(const float* v, const double* x, int d, float t, float w) {
     long double acc = 0.0L;
     for (int j = 0; j < d; j++) {
         double p = (double)v[j] * (double)x[j];
@@ -169,7 +169,7 @@ int32_t or_euclid_h(const float* v, const float* x, int d, float t, float w) {
 }
 
 /* CosineHGen::generate (cosine_h_gen.hpp:67-74). */
-int32_t or_cosine_h(const double* r, const float* x, int d) {
+int32_t or_cosine_h(const double* r, const double* x, int d) {
     long double acc = 0.0L;
     for (int j = 0; j < d; j++) {
         double p = r[j] * (double)x[j];
@@ -184,13 +184,13 @@ static int32_t mod_long_int(long x, int n) { return (int32_t)((x % n + n) % n); 
 /* EuclideanPhiGen::generate (euclidean_phi_gen.hpp:77-92) + insertVector's
  * mod(phi, buckets.size()) (cust_hashtable.hpp:68). M = int(pow(2,32)-5)
  * folds to 2147483647 under g++. */
-void or_lsh_hash_euclid(int64_t N, int d, int L, int k, const float* X, const float* V,
+void or_lsh_hash_euclid(int64_t N, int d, int L, int k, const double* X, const float* V,
                         const float* t, float w, const int32_t* r, int64_t nb,
                         int32_t* tuples, int32_t* phi, int32_t* bucket) {
     const int M = 2147483647;
 #pragma omp parallel for schedule(static)
     for (int64_t n = 0; n < N; n++) {
-        const float* x = X + n * d;
+        const double* x = X + n * d;
         for (int l = 0; l < L; l++) {
             uint32_t hash_num = 0;
             for (int i = 0; i < k; i++) {
@@ -209,7 +209,7 @@ void or_lsh_hash_euclid(int64_t N, int d, int L, int k, const float* X, const fl
 
 /* CosineGGen::generate (cosine_g_gen.hpp:58-66): bits MSB-first; buckets 2^k
  * so mod(g, 2^k) = g (lsh_cube.hpp:65). */
-void or_lsh_hash_cosine(int64_t N, int d, int L, int k, const float* X, const double* R, int32_t* g) {
+void or_lsh_hash_cosine(int64_t N, int d, int L, int k, const double* X, const double* R, int32_t* g) {
 #pragma omp parallel for schedule(static)
     for (int64_t n = 0; n < N; n++) {
         for (int l = 0; l < L; l++) {
@@ -272,7 +272,7 @@ int64_t or_lsh_query(int64_t N, int L, int k, int64_t nb, const int32_t* tuples,
 }
 
 /* ----------------------------------------------------------------- hypercube */
-void or_cube_h(int64_t N, int d, int k, const float* X, const float* V, const float* t, float w, int32_t* h) {
+void or_cube_h(int64_t N, int d, int k, const double* X, const float* V, const float* t, float w, int32_t* h) {
 #pragma omp parallel for schedule(static)
     for (int64_t n = 0; n < N; n++)
         for (int i = 0; i < k; i++) h[n * k + i] = or_euclid_h(V + (size_t)i * d, X + n * d, d, t[i], w);
@@ -303,7 +303,7 @@ int64_t or_cube_coins(int64_t N, int k, const int32_t* h, int32_t hmin, int32_t 
     return draws;
 }
 
-void or_cube_cosine(int64_t N, int d, int k, const float* X, const double* R, int32_t* vertex) {
+void or_cube_cosine(int64_t N, int d, int k, const double* X, const double* R, int32_t* vertex) {
 #pragma omp parallel for schedule(static)
     for (int64_t n = 0; n < N; n++) {
         int v = 0;
@@ -345,14 +345,14 @@ int64_t or_cube_probe_seq(int32_t vertex, int probes, int k, int32_t* out, int64
 /* -------------------------------------------------------------------- Lloyd */
 
 /* CustVector::euclideanDistance (cust_vector.hpp:124-136), this = x, in = c. */
-double or_euclid_dist_f32_f64(const float* x, const double* c, int d) {
+double or_euclid_dist(const double* x, const double* c, int d) {
     double acc = 0;
     for (int j = 0; j < d; j++) acc = acc + pow((double)x[j] - c[j], 2);
     return sqrt(acc);
 }
 
 /* CustVector::cosineDistance (cust_vector.hpp:139-155), this = x, in = c. */
-static double cosine_dist_f32_f64(const float* x, const double* c, int d) {
+static double cosine_dist(const double* x, const double* c, int d) {
     long double ip = 0.0L;
     for (int j = 0; j < d; j++) ip = ip + (long double)((double)x[j] * c[j]);
     double a = 0, b = 0;
@@ -363,14 +363,14 @@ static double cosine_dist_f32_f64(const float* x, const double* c, int d) {
 
 /* lloyds_assignment (assignment.hpp:54-80): strict '<' with the -1 sentinel,
  * then the centroid override (:77-78). */
-void or_lloyd_assign(int64_t N, int d, int K, const float* X, const double* C, int metric,
+void or_lloyd_assign(int64_t N, int d, int K, const double* X, const double* C, int metric,
                      const int32_t* src_rows, int32_t* assign, double* dist) {
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t n = 0; n < N; n++) {
         double mn = -1; int arg = 0;
         for (int c = 0; c < K; c++) {
-            double dd = metric == 0 ? or_euclid_dist_f32_f64(X + n * d, C + (size_t)c * d, d)
-                                    : cosine_dist_f32_f64(X + n * d, C + (size_t)c * d, d);
+            double dd = metric == 0 ? or_euclid_dist(X + n * d, C + (size_t)c * d, d)
+                                    : cosine_dist(X + n * d, C + (size_t)c * d, d);
             if (mn == -1 || dd < mn) { mn = dd; arg = c; }
         }
         assign[n] = arg; dist[n] = mn;
@@ -397,7 +397,7 @@ static double cosine_f64(const double* a, const double* b, int d) {
 
 /* k_means (update.hpp:37-86): per-cluster sequential fp64 sum in input order,
  * divide unless empty, continue iff some center moved > min_dist. */
-int or_kmeans_update(int64_t N, int d, int K, const float* X, const int32_t* assign,
+int or_kmeans_update(int64_t N, int d, int K, const double* X, const int32_t* assign,
                      const double* C_old, int metric, double min_dist, double* C_new, int64_t* counts) {
     memset(C_new, 0, sizeof(double) * (size_t)K * d);
     memset(counts, 0, sizeof(int64_t) * K);
@@ -441,7 +441,7 @@ void or_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows) {
  * cache only memoises), max with strict '>' from 0, (min/max)^2 prefix-summed
  * in row order, uniform_real<double>(0, total) = canon * (total - 0) + 0, and
  * the custom binary search (:134-149). */
-void or_kmeans_pp(int64_t N, int d, int K, const float* X, int metric, uint64_t seed, int32_t* rows) {
+void or_kmeans_pp(int64_t N, int d, int K, const double* X, int metric, uint64_t seed, int32_t* rows) {
     uint32_t s = or_minstd_seed(seed);
     double* md = (double*)malloc(sizeof(double) * (size_t)N);
     double* cs = (double*)malloc(sizeof(double) * (size_t)K * d);
@@ -453,8 +453,8 @@ void or_kmeans_pp(int64_t N, int d, int K, const float* X, int metric, uint64_t 
         for (int64_t n = 0; n < N; n++) {
             double mn = -1;
             for (int c = 0; c < i; c++) {
-                const double dd = metric == 0 ? or_euclid_dist_f32_f64(X + n * d, cs + (size_t)c * d, d)
-                                              : cosine_dist_f32_f64(X + n * d, cs + (size_t)c * d, d);
+                const double dd = metric == 0 ? or_euclid_dist(X + n * d, cs + (size_t)c * d, d)
+                                              : cosine_dist(X + n * d, cs + (size_t)c * d, d);
                 if (mn == -1 || dd < mn) mn = dd;
             }
             md[n] = mn;
@@ -608,7 +608,7 @@ static size_t dmap_slot(const dmap_t* m, uint64_t key) {
  * cache entries, as centroids with equal IDs do in the reference (e.g. every
  * "k_means_center" after k_means, update.hpp:46). Returns the passes of the
  * do-while loop. */
-int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, int metric,
+int or_range_assign(int64_t N, int d, int K, const double* X, const double* C, int metric,
                     const int64_t* comb_ptr, const int32_t* comb_idx, const int32_t* key,
                     const int32_t* src_rows, int32_t* assign, double* dist) {
     for (int64_t n = 0; n < N; n++) { assign[n] = -1; dist[n] = 0; }
@@ -635,8 +635,8 @@ int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, in
                     double dd;
                     if (m.k[h] != ~0ull) dd = m.v[h];
                     else {
-                        dd = metric == 0 ? or_euclid_dist_f32_f64(X + (size_t)v * d, C + (size_t)i * d, d)
-                                         : cosine_dist_f32_f64(X + (size_t)v * d, C + (size_t)i * d, d);
+                        dd = metric == 0 ? or_euclid_dist(X + (size_t)v * d, C + (size_t)i * d, d)
+                                         : cosine_dist(X + (size_t)v * d, C + (size_t)i * d, d);
                         m.k[h] = kc | (uint32_t)v;
                         m.v[h] = dd;
                     }
@@ -656,8 +656,8 @@ int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, in
         if (assign[n] != -1) continue;
         double mn = -1; int arg = 0;
         for (int c = 0; c < K; c++) {
-            double dd = metric == 0 ? or_euclid_dist_f32_f64(X + n * d, C + (size_t)c * d, d)
-                                    : cosine_dist_f32_f64(X + n * d, C + (size_t)c * d, d);
+            double dd = metric == 0 ? or_euclid_dist(X + n * d, C + (size_t)c * d, d)
+                                    : cosine_dist(X + n * d, C + (size_t)c * d, d);
             if (mn == -1 || dd < mn) { mn = dd; arg = c; }
         }
         assign[n] = arg; dist[n] = mn;
@@ -674,7 +674,7 @@ int or_range_assign(int64_t N, int d, int K, const float* X, const double* C, in
  * (utils.hpp:150-158), silhouette_of_i (:83-144). The reference's distance
  * cache is left out: it returns d(x_j, x_i) for d(x_i, x_j), which is the same
  * double in both metrics (unique IDs). out[K+1]; s[N] (may be NULL) per row. */
-void or_silhouette(int64_t N, int d, int K, const float* X, const int32_t* assign, const double* C, int metric,
+void or_silhouette(int64_t N, int d, int K, const double* X, const int32_t* assign, const double* C, int metric,
                    double* out, double* s) {
     int32_t* near = (int32_t*)malloc(sizeof(int32_t) * (size_t)K);
     for (int c = 0; c < K; c++) {
@@ -703,15 +703,15 @@ void or_silhouette(int64_t N, int d, int K, const float* X, const int32_t* assig
         double a = 0, b = 0;
         for (int64_t j = cnt[c]; j < cnt[c + 1]; j++) {
             for (int t = 0; t < d; t++) xr[t] = X[(size_t)rows[j] * d + t];
-            a = a + (metric == 0 ? or_euclid_dist_f32_f64(X + (size_t)r * d, xr, d)
-                                 : cosine_dist_f32_f64(X + (size_t)r * d, xr, d));
+            a = a + (metric == 0 ? or_euclid_dist(X + (size_t)r * d, xr, d)
+                                 : cosine_dist(X + (size_t)r * d, xr, d));
         }
         if (cnt[c + 1] - cnt[c] != 1) a = a / (double)(size_t)(cnt[c + 1] - cnt[c] - 1);
         const int nc = near[c];
         for (int64_t j = cnt[nc]; j < cnt[nc + 1]; j++) {
             for (int t = 0; t < d; t++) xr[t] = X[(size_t)rows[j] * d + t];
-            b = b + (metric == 0 ? or_euclid_dist_f32_f64(X + (size_t)r * d, xr, d)
-                                 : cosine_dist_f32_f64(X + (size_t)r * d, xr, d));
+            b = b + (metric == 0 ? or_euclid_dist(X + (size_t)r * d, xr, d)
+                                 : cosine_dist(X + (size_t)r * d, xr, d));
         }
         b = b / (double)(size_t)(cnt[nc + 1] - cnt[nc]);
         double mx = a;

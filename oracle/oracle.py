@@ -38,24 +38,24 @@ def lib():
             "or_gen_lsh_cosine": (C.c_uint32, [C.c_uint64, C.c_int, C.c_int, C.c_int, f64p]),
             "or_gen_cube_euclid": (C.c_uint32, [C.c_uint64, C.c_int, C.c_int, C.c_float, f32p, f32p]),
             "or_gen_cube_cosine": (C.c_uint32, [C.c_uint64, C.c_int, C.c_int, f64p]),
-            "or_lsh_hash_euclid": (None, [C.c_int64, C.c_int, C.c_int, C.c_int, f32p, f32p, f32p, C.c_float,
+            "or_lsh_hash_euclid": (None, [C.c_int64, C.c_int, C.c_int, C.c_int, f64p, f32p, f32p, C.c_float,
                                           i32p, C.c_int64, i32p, i32p, i32p]),
-            "or_lsh_hash_cosine": (None, [C.c_int64, C.c_int, C.c_int, C.c_int, f32p, f64p, i32p]),
+            "or_lsh_hash_cosine": (None, [C.c_int64, C.c_int, C.c_int, C.c_int, f64p, f64p, i32p]),
             "or_bucket_csr": (None, [C.c_int64, C.c_int, C.c_int64, i32p, i64p, i32p]),
             "or_lsh_query": (C.c_int64, [C.c_int64, C.c_int, C.c_int, C.c_int64, C.c_void_p, i64p, i32p,
                                          C.c_void_p, i32p, i32p, C.c_int64]),
-            "or_cube_h": (None, [C.c_int64, C.c_int, C.c_int, f32p, f32p, f32p, C.c_float, i32p]),
+            "or_cube_h": (None, [C.c_int64, C.c_int, C.c_int, f64p, f32p, f32p, C.c_float, i32p]),
             "or_cube_coins": (C.c_int64, [C.c_int64, C.c_int, i32p, C.c_int32, C.c_int32, i32p, u32ref, i32p]),
-            "or_cube_cosine": (None, [C.c_int64, C.c_int, C.c_int, f32p, f64p, i32p]),
+            "or_cube_cosine": (None, [C.c_int64, C.c_int, C.c_int, f64p, f64p, i32p]),
             "or_cube_probe_seq": (C.c_int64, [C.c_int32, C.c_int, C.c_int, i32p, C.c_int64]),
-            "or_lloyd_assign": (None, [C.c_int64, C.c_int, C.c_int, f32p, f64p, C.c_int, C.c_void_p, i32p, f64p]),
-            "or_kmeans_update": (C.c_int, [C.c_int64, C.c_int, C.c_int, f32p, i32p, f64p, C.c_int, C.c_double,
+            "or_lloyd_assign": (None, [C.c_int64, C.c_int, C.c_int, f64p, f64p, C.c_int, C.c_void_p, i32p, f64p]),
+            "or_kmeans_update": (C.c_int, [C.c_int64, C.c_int, C.c_int, f64p, i32p, f64p, C.c_int, C.c_double,
                                            f64p, i64p]),
-            "or_range_assign": (C.c_int, [C.c_int64, C.c_int, C.c_int, f32p, f64p, C.c_int, i64p, i32p,
+            "or_range_assign": (C.c_int, [C.c_int64, C.c_int, C.c_int, f64p, f64p, C.c_int, i64p, i32p,
                                           C.c_void_p, C.c_void_p, i32p, f64p]),
-            "or_silhouette": (None, [C.c_int64, C.c_int, C.c_int, f32p, i32p, f64p, C.c_int, f64p, C.c_void_p]),
+            "or_silhouette": (None, [C.c_int64, C.c_int, C.c_int, f64p, i32p, f64p, C.c_int, f64p, C.c_void_p]),
             "or_rand_selection": (None, [C.c_uint64, C.c_int64, C.c_int, i32p]),
-            "or_kmeans_pp": (None, [C.c_int64, C.c_int, C.c_int, f32p, C.c_int, C.c_uint64, i32p]),
+            "or_kmeans_pp": (None, [C.c_int64, C.c_int, C.c_int, f64p, C.c_int, C.c_uint64, i32p]),
             "or_p_closest": (None, [C.c_int, f64p, C.c_int64, f64p, i64p, i32p, C.c_int, i32p, f64p, i32p]),
             "or_top_n_recom": (None, [C.c_int, f64p, f64p, C.c_int64, f64p, f64p, i64p, i32p, i32p, f64p, i32p,
                                       C.c_int, C.c_int, i32p]),
@@ -67,6 +67,11 @@ def lib():
             fn.argtypes = args
         _LIB = L
     return _LIB
+
+
+def rows64(X):
+    """Dataset rows as the reference holds them (fp64; fp32 data widens exactly)."""
+    return np.ascontiguousarray(X, np.float64)
 
 
 def _ptr(a):
@@ -104,7 +109,7 @@ def gen_cube_cosine(seed, k, d):
 
 
 def lsh_hash_euclid(X, V, t, w, r, nb):
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     N, d = X.shape; L, k = t.shape
     tuples = np.empty((N, L, k), np.int32); phi = np.empty((N, L), np.int32); bucket = np.empty((N, L), np.int32)
     lib().or_lsh_hash_euclid(N, d, L, k, X, np.ascontiguousarray(V, np.float32), np.ascontiguousarray(t, np.float32),
@@ -113,7 +118,7 @@ def lsh_hash_euclid(X, V, t, w, r, nb):
 
 
 def lsh_hash_cosine(X, R):
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     N, d = X.shape; L, k, _ = R.shape
     g = np.empty((N, L), np.int32)
     lib().or_lsh_hash_cosine(N, d, L, k, X, np.ascontiguousarray(R, np.float64), g)
@@ -141,7 +146,7 @@ def lsh_query(N, nb, row_ptr, idx, q_bucket, tuples=None, q_tuple=None):
 
 
 def cube_h(X, V, t, w):
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     N, d = X.shape; k = t.shape[0]
     h = np.empty((N, k), np.int32)
     lib().or_cube_h(N, d, k, X, np.ascontiguousarray(V, np.float32), np.ascontiguousarray(t, np.float32), float(w), h)
@@ -170,7 +175,7 @@ class CoinMemo:
 
 
 def cube_cosine(X, R):
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     N, d = X.shape; k = R.shape[0]
     v = np.empty(N, np.int32)
     lib().or_cube_cosine(N, d, k, X, np.ascontiguousarray(R, np.float64), v)
@@ -185,7 +190,7 @@ def cube_probe_seq(vertex, probes, k):
 
 
 def lloyd_assign(X, Cc, metric="euclidean", src_rows=None):
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     Cc = np.ascontiguousarray(Cc, np.float64)
     N, d = X.shape; K = Cc.shape[0]
     a = np.empty(N, np.int32); dist = np.empty(N, np.float64)
@@ -197,7 +202,7 @@ def lloyd_assign(X, Cc, metric="euclidean", src_rows=None):
 def range_assign(X, Cc, comb_ptr, comb_idx, metric="euclidean", key=None, src_rows=None):
     """range_assignment + lloyds_for_remaining + override (assignment.hpp:108-217).
     Returns (assign, dist, passes)."""
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     Cc = np.ascontiguousarray(Cc, np.float64)
     N, d = X.shape; K = Cc.shape[0]
     a = np.empty(N, np.int32); dist = np.empty(N, np.float64)
@@ -211,7 +216,7 @@ def range_assign(X, Cc, comb_ptr, comb_idx, metric="euclidean", key=None, src_ro
 
 def silhouette(X, assign, Cc, metric="euclidean"):
     """silhouette_cluster (silhouette.hpp:31-144): (sils [K+1], s [N])."""
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     Cc = np.ascontiguousarray(Cc, np.float64)
     N, d = X.shape; K = Cc.shape[0]
     out = np.empty(K + 1, np.float64); s = np.empty(max(N, 1), np.float64)
@@ -221,7 +226,7 @@ def silhouette(X, assign, Cc, metric="euclidean"):
 
 
 def kmeans_update(X, assign, C_old, metric="euclidean", min_dist=0.0):
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     N, d = X.shape; K = C_old.shape[0]
     Cn = np.empty((K, d), np.float64); cnt = np.empty(K, np.int64)
     cont = lib().or_kmeans_update(N, d, K, X, np.ascontiguousarray(assign, np.int32),
@@ -232,7 +237,7 @@ def kmeans_update(X, assign, C_old, metric="euclidean", min_dist=0.0):
 
 def kmeans_pp(X, K, metric="euclidean", seed=1):
     """k_means_pp (initialization.hpp:71-156): the chosen rows."""
-    X = np.ascontiguousarray(X, np.float32)
+    X = rows64(X)
     N, d = X.shape
     rows = np.empty(K, np.int32)
     lib().or_kmeans_pp(N, d, K, X, 0 if metric == "euclidean" else 1, int(seed), rows)

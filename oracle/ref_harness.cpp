@@ -115,7 +115,16 @@ static std::vector<T> read_raw(const std::string& path, size_t count) {
     return v;
 }
 
-static std::vector<Vec> make_vectors(const std::vector<float>& x, int N, int d, const std::string& prefix) {
+// Input rows: a ".f64" file holds doubles (general values, the `_f64` paths),
+// anything else fp32 values, widened exactly into the reference's doubles.
+static std::vector<double> read_rows(const std::string& path, size_t count) {
+    if (path.size() > 4 && path.compare(path.size() - 4, 4, ".f64") == 0) return read_f64(path, count);
+    std::vector<float> x = read_f32(path, count);
+    return std::vector<double>(x.begin(), x.end());
+}
+
+template <typename T>
+static std::vector<Vec> make_vectors(const std::vector<T>& x, int N, int d, const std::string& prefix) {
     std::vector<Vec> vecs;
     vecs.reserve(N);
     for (int i = 0; i < N; i++) {
@@ -158,7 +167,7 @@ static int mode_lsh(int argc, char** argv) {
     std::string metric = argv[4]; int k = atoi(argv[5]); int L = atoi(argv[6]);
     int div = atoi(argv[7]); double w = atof(argv[8]); g_seed = atoll(argv[9]);
     std::string out = argv[10];
-    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<double> x = read_rows(in, (size_t)N * d);
     std::vector<Vec> vecs = make_vectors(x, N, d, "");
 
     std::vector<CustHashtable<double>*> tables = create_LSH_hashtables<double>(vecs, metric, k, L, div, w);
@@ -215,7 +224,7 @@ static int mode_lsh(int argc, char** argv) {
     // Queries: NQROWS dataset rows (in row order), then Q external vectors.
     if (argc >= 14) {
         std::string qin = argv[11]; int Q = atoi(argv[12]); int nqrows = atoi(argv[13]);
-        std::vector<float> qx = read_f32(qin, (size_t)Q * d);
+        std::vector<double> qx = read_rows(qin, (size_t)Q * d);
         std::vector<Vec> qvecs = make_vectors(qx, Q, d, "q");
         std::vector<std::vector<int32_t>> filt, unf;
         for (int r = 0; r < nqrows + Q; r++) {
@@ -238,7 +247,7 @@ static int mode_cube(int argc, char** argv) {
     std::string metric = argv[4]; int k = atoi(argv[5]); double w = atof(argv[6]);
     g_seed = atoll(argv[7]); std::vector<int> probes = split_ints(argv[8]);
     std::string out = argv[9];
-    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<double> x = read_rows(in, (size_t)N * d);
     std::vector<Vec> vecs = make_vectors(x, N, d, "");
 
     CustHashtable<double>* cube = create_hypercube<double>(vecs, metric, k, w);
@@ -290,7 +299,7 @@ static int mode_cube(int argc, char** argv) {
     // skipped here and marked in qmask; only fully-seen queries are pinned.
     if (argc >= 13) {
         std::string qin = argv[10]; int Q = atoi(argv[11]); int nqrows = atoi(argv[12]);
-        std::vector<float> qx = read_f32(qin, (size_t)Q * d);
+        std::vector<double> qx = read_rows(qin, (size_t)Q * d);
         std::vector<Vec> qvecs = make_vectors(qx, Q, d, "q");
         std::vector<uint8_t> qmask;
         std::vector<Vec*> qs;
@@ -325,7 +334,7 @@ static int mode_lloyd(int argc, char** argv) {
     std::string in = argv[1]; int N = atoi(argv[2]); int d = atoi(argv[3]); int K = atoi(argv[4]);
     std::string metric = argv[5]; int iters = atoi(argv[6]); double min_dist = atof(argv[7]);
     std::string out = argv[8];
-    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<double> x = read_rows(in, (size_t)N * d);
     std::vector<Vec> vecs = make_vectors(x, N, d, "");
     std::vector<Vec*> centroids(K);
     std::vector<Vec> ext;
@@ -377,7 +386,7 @@ static int mode_kmeanspp(int argc, char** argv) {
     if (argc < 8) { fprintf(stderr, "usage: kmeanspp IN N d K metric seed OUT\n"); return 2; }
     std::string in = argv[1]; int N = atoi(argv[2]); int d = atoi(argv[3]); int K = atoi(argv[4]);
     std::string metric = argv[5]; g_seed = atoll(argv[6]); std::string out = argv[7];
-    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<double> x = read_rows(in, (size_t)N * d);
     std::vector<Vec> vecs = make_vectors(x, N, d, "");
     std::vector<Vec*> c = k_means_pp(vecs, K, metric);
     std::vector<Vec*> r = rand_selection(vecs, K);
@@ -484,7 +493,7 @@ static int mode_range(int argc, char** argv) {
     int k = atoi(argv[7]), L = atoi(argv[8]), div = atoi(argv[9]); double w = atof(argv[10]);
     int probes = atoi(argv[11]), iters = atoi(argv[12]); double min_dist = atof(argv[13]);
     g_seed = atoll(argv[14]); std::string out = argv[15];
-    std::vector<float> x = read_f32(in, (size_t)N * d);
+    std::vector<double> x = read_rows(in, (size_t)N * d);
     std::vector<Vec> vecs = make_vectors(x, N, d, "");
     std::vector<CustHashtable<double>*> tables;
     CustHashtable<double>* cube = nullptr;
@@ -620,6 +629,82 @@ static int mode_c1(int argc, char** argv) {
     return 0;
 }
 
+// ------------------------------------------------------------- chain mode
+// chain DIR N Q d k L div w seed P NTOP SELF — the cosine-LSH recommender of
+// main.cpp:149-176 (Part A, SELF = 1: the users are the indexed vectors
+// themselves) / :186-222 (Part B, SELF = 0: tables over another pool):
+// create_LSH_hashtables<double>(pool, "cosine", k, L, div, w), then per user
+// get_LSH_filtered_combined_buckets, get_P_closest (P) and get_top_N_recom
+// (NTOP), skipping users without neighbours. DIR holds pool.f64 [N][d],
+// pmean.f64 [N], punk_ptr.i64 / punk_idx.i32 (the pool's unknown indexes)
+// and, for SELF = 0, users.f64 [Q][d], umean.f64, uunk_ptr.i64 / uunk_idx.i32.
+// Outputs: R [L][k][d], g [N][L] (bucket of every pool vector), nb_ptr/nb_idx
+// (each user's combined bucket, row order), pc_idx/pc_sim [Q][P] (-1 / 0 pad),
+// pc_cnt [Q], top [Q][NTOP] (-1 rows for skipped users).
+static std::vector<Vec> read_user_vectors(const std::string& dir, const std::string& pre, int N, int d,
+                                          const std::string& id) {
+    std::vector<double> x = read_raw<double>(dir + "/" + pre + ".f64", (size_t)N * d);
+    std::vector<double> m = read_raw<double>(dir + "/" + (pre == "pool" ? std::string("pmean") : std::string("umean")) + ".f64", N);
+    const std::string u = pre == "pool" ? "punk" : "uunk";
+    std::vector<int64_t> up = read_raw<int64_t>(dir + "/" + u + "_ptr.i64", N + 1);
+    std::vector<int32_t> ui = read_raw<int32_t>(dir + "/" + u + "_idx.i32", (size_t)up[N]);
+    std::vector<Vec> v;
+    v.reserve(N);
+    for (int i = 0; i < N; i++)
+        v.emplace_back(id + std::to_string(i), std::vector<double>(x.begin() + (size_t)i * d, x.begin() + (size_t)(i + 1) * d),
+                       std::set<int>(ui.begin() + up[i], ui.begin() + up[i + 1]), m[i]);
+    return v;
+}
+
+static int mode_chain(int argc, char** argv) {
+    if (argc < 13) { fprintf(stderr, "usage: chain DIR N Q d k L div w seed P NTOP SELF\n"); return 2; }
+    std::string dir = argv[1];
+    int N = atoi(argv[2]), Q = atoi(argv[3]), d = atoi(argv[4]), k = atoi(argv[5]), L = atoi(argv[6]);
+    int div = atoi(argv[7]); double w = atof(argv[8]); g_seed = atoll(argv[9]);
+    int P = atoi(argv[10]), NT = atoi(argv[11]); bool self = atoi(argv[12]) != 0;
+    std::vector<Vec> pool = read_user_vectors(dir, "pool", N, d, "u");
+    std::vector<Vec> others;
+    if (!self) others = read_user_vectors(dir, "users", Q, d, "q");
+    std::vector<Vec>& users = self ? pool : others;
+    if (self) Q = N;
+    std::vector<CustHashtable<double>*> tables = create_LSH_hashtables<double>(pool, "cosine", k, L, div, w);
+    std::vector<double> RC;
+    for (int l = 0; l < L; l++) {
+        auto* cg = dynamic_cast<CosineGGen<double>*>(tables[l]->hashGenerator);
+        for (int i = 0; i < k; i++)
+            for (int j = 0; j < d; j++) RC.push_back((*cg->hFunctions[i]->r->getDimensions())[j]);
+    }
+    std::vector<int32_t> g((size_t)N * L);
+    for (int n = 0; n < N; n++)
+        for (int l = 0; l < L; l++) g[(size_t)n * L + l] = tables[l]->getHash(&pool[n]);
+    std::vector<std::vector<int32_t>> nbl;
+    std::vector<int32_t> pc_idx((size_t)Q * P, -1), pc_cnt(Q, 0), top((size_t)Q * NT, -1);
+    std::vector<double> pc_sim((size_t)Q * P, 0.0);
+    for (int q = 0; q < Q; q++) {
+        Vec& user = users[q];
+        std::vector<Vec*> neighbors = get_LSH_filtered_combined_buckets(tables, &user);
+        nbl.push_back(to_indices(neighbors, pool.data()));
+        if (neighbors.empty()) continue;
+        std::vector<double> sims = get_P_closest(neighbors, user, P);
+        for (size_t i = 0; i < neighbors.size(); i++) {
+            pc_idx[(size_t)q * P + i] = (int32_t)(neighbors[i] - pool.data());
+            pc_sim[(size_t)q * P + i] = sims[i];
+        }
+        pc_cnt[q] = (int32_t)neighbors.size();
+        std::vector<int> t = get_top_N_recom(neighbors, user, NT, sims);
+        for (int i = 0; i < NT; i++) top[(size_t)q * NT + i] = t[i];
+    }
+    write_npy(dir + "/R.npy", RC, {(size_t)L, (size_t)k, (size_t)d});
+    write_npy(dir + "/g.npy", g, {(size_t)N, (size_t)L});
+    csr_write(dir, "nb", nbl);
+    write_npy(dir + "/pc_idx.npy", pc_idx, {(size_t)Q, (size_t)P});
+    write_npy(dir + "/pc_sim.npy", pc_sim, {(size_t)Q, (size_t)P});
+    write_npy(dir + "/pc_cnt.npy", pc_cnt, {(size_t)Q});
+    write_npy(dir + "/top.npy", top, {(size_t)Q, (size_t)NT});
+    for (auto t : tables) delete t;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness {lsh|cube|lloyd|kmeanspp|bench} ...\n"); return 2; }
     std::string m = argv[1];
@@ -633,6 +718,7 @@ int main(int argc, char** argv) {
     if (m == "csv") return mode_csv(argc - 1, argv + 1);
     if (m == "conf") return mode_conf(argc - 1, argv + 1);
     if (m == "c1") return mode_c1(argc - 1, argv + 1);
+    if (m == "chain") return mode_chain(argc - 1, argv + 1);
     fprintf(stderr, "unknown mode %s\n", m.c_str());
     return 2;
 }

@@ -43,6 +43,32 @@ def lloyd_input(name):
     return X
 
 
+def case_rows(name):
+    """Dataset rows of a golden case: stored fp64 rows (f64_* kinds) or the
+    synthetic generator the case was made with (fp32)."""
+    m = golden_meta()[name]
+    g = golden(name)
+    if "x64" in g.files:
+        return g["x64"]
+    kind = m["kind"]
+    if kind in ("kmeanspp", "range"):
+        return kpp_input(name)
+    if kind == "lloyd":
+        return lloyd_input(name)
+    import oracle
+    return oracle.synth(m["data_seed"], m["N"], m["d"])
+
+
+def case_queries(name):
+    """External query rows of an LSH / cube golden case."""
+    m = golden_meta()[name]
+    g = golden(name)
+    if "q64" in g.files:
+        return g["q64"]
+    import oracle
+    return oracle.synth(m["query_seed"], m["Q"], m["d"])
+
+
 def cases(kind):
     return sorted(n for n, m in golden_meta().items() if m["kind"] == kind)
 

@@ -10,7 +10,11 @@ include/lshkm_synth.h at the (seed, rows, d) recorded in cases.json, except
 external fp64 centroids, which are stored.
 
 Only runs in the build container (the reference is absent on the GPU box).
-Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,range,csv,conf,c1,recom]
+fp64 cases (kind f64_*, chain, c1 with "f64": true) run on general doubles shaped
+like the recommender's user vectors (user_vectors below); their inputs ARE
+stored (x64 / q64 / pool ... arrays), as fixtures.
+
+Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,range,csv,conf,c1,recom,f64,chain]
 (--only regenerates those kinds and keeps the other cases' entries.)
 """
 import json
@@ -189,6 +193,75 @@ def recom_inputs(N, d, Q, seed, values):
     return dict(x=X, xmean=xm, u=U, umean=um.astype(np.float64), unk_ptr=up, unk_idx=ui, cand_ptr=cp, cand_idx=ci)
 
 
+def user_vectors(seed, N, d):
+    """General doubles shaped like tweets_to_user_vectors (crypto_rec.hpp:78-140):
+    per user a few tweets, each mentioning 1-3 coins with a sentiment score
+    s = x / sqrt(x^2 + 15) (tweet.cpp) over a lexicon sum x of +-k/4 words;
+    positive scores accumulate on the mentioned coins; every unmentioned coin
+    gets the mean of the known ones (summed in index order, as the reference).
+    Users with an all-zero vector are redrawn (the reference drops them).
+    Returns (X [N][d] fp64, unknown index lists, known means)."""
+    rng = np.random.RandomState(seed)
+    X = np.zeros((N, d))
+    unk, means = [], np.zeros(N)
+    for i in range(N):
+        while True:
+            x = np.zeros(d)
+            known = np.zeros(d, bool)
+            for _ in range(1 + rng.poisson(4)):
+                coins = rng.choice(d, size=1 + rng.randint(3), replace=False)
+                lex = float(sum(rng.randint(-8, 9) for _ in range(1 + rng.randint(4)))) / 4.0
+                sc = lex / np.sqrt(lex * lex + 15.0)
+                for c in coins:
+                    if sc > 0:
+                        x[c] = x[c] + sc
+                    known[c] = True
+            if (x != 0).any():
+                break
+        tot, cnt = 0.0, 0
+        for j in range(d):
+            if known[j]:
+                tot = tot + x[j]
+                cnt += 1
+        mean = tot / cnt
+        x[~known] = mean
+        X[i] = x
+        unk.append(np.nonzero(~known)[0].astype(np.int32))
+        means[i] = mean
+    return X, unk, means
+
+
+def csr_of(lists):
+    return (np.cumsum([0] + [len(l) for l in lists]).astype(np.int64),
+            np.concatenate(lists).astype(np.int32) if lists else np.zeros(0, np.int32))
+
+
+F64_CASES = [
+    # name, kind, N, d, params..., data seed  (rows: user_vectors(seed, N, d); queries: seed + 1)
+    ("lsh_e64", "lsh", 700, 100, dict(metric="euclidean", k=4, L=5, div=10, w=0.4, seed=811, nqrows=20, Q=15), 8001),
+    ("lsh_c64", "lsh", 700, 100, dict(metric="cosine", k=4, L=5, div=1, w=0.0, seed=812, nqrows=20, Q=15), 8002),
+    ("lsh_e64_odd", "lsh", 400, 23, dict(metric="euclidean", k=3, L=3, div=7, w=0.25, seed=813, nqrows=10, Q=10), 8003),
+    ("cube_e64", "cube", 900, 100, dict(metric="euclidean", k=8, w=0.5, seed=821, probes="0,1,2,8,30", nqrows=20, Q=15), 8004),
+    ("cube_c64", "cube", 900, 100, dict(metric="cosine", k=10, w=0.0, seed=822, probes="0,1,3,10", nqrows=20, Q=15), 8005),
+    ("lloyd_e64", "lloyd", 1000, 100, dict(K=16, metric="euclidean", iters=3, min_dist=0.0), 8006),
+    ("lloyd_c64", "lloyd", 1000, 100, dict(K=12, metric="cosine", iters=3, min_dist=0.0), 8007),
+    ("lloyd_e64_k80", "lloyd", 1200, 40, dict(K=80, metric="euclidean", iters=2, min_dist=0.0), 8008),
+    ("kpp_e64", "kmeanspp", 1500, 100, dict(K=16, metric="euclidean", seed=831), 8009),
+    ("kpp_c64", "kmeanspp", 1500, 100, dict(K=16, metric="cosine", seed=832), 8010),
+    ("range_lsh_e64", "range", 900, 100, dict(K=12, metric="euclidean", family="lsh", k=4, L=5, div=10, w=1.0,
+                                             probes=0, iters=2, min_dist=0.0, seed=841), 8011),
+    ("range_cube_c64", "range", 900, 100, dict(K=12, metric="cosine", family="cube", k=8, L=1, div=1, w=0.0,
+                                              probes=6, iters=1, min_dist=0.0, seed=842), 8012),
+]
+# main.cpp's cosine LSH recommender, Part A (users indexed and queried) and Part B
+# (tables over another pool, queried with the users): name, N, Q, d, k, L, w, seed, P, NTOP, self, data seed
+CHAIN_CASES = [
+    ("chain_a", 600, 600, 100, 4, 5, 0.4, 851, 20, 5, 1, 8101),
+    ("chain_b", 500, 300, 100, 4, 5, 0.4, 852, 20, 2, 0, 8102),
+    ("chain_a_k6", 400, 400, 60, 6, 3, 0.4, 853, 10, 5, 1, 8103),
+]
+
+
 def run(args):
     subprocess.run([HARNESS] + [str(a) for a in args], check=True)
 
@@ -285,7 +358,7 @@ def main(only=None):
             run(["csv", path, delim, strt, out])
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
             meta[name] = dict(kind="csv", delim=delim, strt_line=strt, N=N, d=d, file="io/" + name + ".csv")
-        if want("c1"):
+        if want("c1") or want("csv") or want("conf"):
             os.makedirs(iodir, exist_ok=True)
         for (name, N, d, K, iters, md, seed, dseed) in (C1_CASES if want("c1") else []):
             x = oracle.synth(dseed, N, d)
@@ -298,6 +371,65 @@ def main(only=None):
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
             meta[name] = dict(kind="c1", N=N, d=d, K=K, iters=iters, min_dist=md, seed=seed, data_seed=dseed,
                               file="io/" + name + ".csv")
+        # config C1 on an unquantized CSV: general doubles written with %.17g
+        for (name, N, d, K, iters, md, seed, dseed) in ([("c1_proj2_f64", 1000, 16, 8, 30, 0.05, 7005, 7006)]
+                                                       if want("c1") else []):
+            rng = np.random.RandomState(dseed)
+            x = rng.standard_normal((N, d)) * np.exp(rng.uniform(-2, 2, size=(N, 1)))
+            path = os.path.join(iodir, name + ".csv")
+            with open(path, "w") as f:
+                for i in range(N):
+                    f.write(f"{i}," + ",".join("%.17g" % float(v) for v in x[i]) + "\n")
+            out = os.path.join(tmp, name); os.makedirs(out)
+            run(["c1", path, 44, K, iters, repr(md), seed, out])
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **load_dir(out))
+            meta[name] = dict(kind="c1", N=N, d=d, K=K, iters=iters, min_dist=md, seed=seed, data_seed=dseed,
+                              file="io/" + name + ".csv", f64=True)
+        for (name, kind, N, d, pr, dseed) in (F64_CASES if want("f64") else []):
+            out = os.path.join(tmp, name); os.makedirs(out)
+            x, _, _ = user_vectors(dseed, N, d)
+            xf = os.path.join(tmp, "x.f64"); x.tofile(xf)
+            stored = dict(x64=x)
+            if kind == "lsh":
+                q, _, _ = user_vectors(dseed + 1, pr["Q"], d); qf = os.path.join(tmp, "q.f64"); q.tofile(qf)
+                stored["q64"] = q
+                run(["lsh", xf, N, d, pr["metric"], pr["k"], pr["L"], pr["div"], pr["w"], pr["seed"], out, qf,
+                     pr["Q"], pr["nqrows"]])
+                pr = dict(pr, nb=(N // pr["div"]) if pr["metric"] == "euclidean" else 2 ** pr["k"])
+            elif kind == "cube":
+                q, _, _ = user_vectors(dseed + 1, pr["Q"], d); qf = os.path.join(tmp, "q.f64"); q.tofile(qf)
+                stored["q64"] = q
+                run(["cube", xf, N, d, pr["metric"], pr["k"], pr["w"], pr["seed"], pr["probes"], out, qf, pr["Q"],
+                     pr["nqrows"]])
+                pr = dict(pr, probes=[int(v) for v in pr["probes"].split(",")])
+            elif kind == "lloyd":
+                run(["lloyd", xf, N, d, pr["K"], pr["metric"], pr["iters"], repr(pr["min_dist"]), out])
+            elif kind == "kmeanspp":
+                run(["kmeanspp", xf, N, d, pr["K"], pr["metric"], pr["seed"], out])
+            elif kind == "range":
+                run(["range", xf, N, d, pr["K"], pr["metric"], pr["family"], pr["k"], pr["L"], pr["div"], pr["w"],
+                     pr["probes"], pr["iters"], repr(pr["min_dist"]), pr["seed"], out])
+            res = load_dir(out); res.update(stored)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+            meta[name] = dict(kind="f64_" + kind, N=N, d=d, data_seed=dseed, **pr)
+        for (name, N, Q, d, k, L, w, seed, P, NT, self_, dseed) in (CHAIN_CASES if want("chain") else []):
+            out = os.path.join(tmp, name); os.makedirs(out)
+            pool, punk, pmean = user_vectors(dseed, N, d)
+            inp = dict(pool=pool, pmean=pmean)
+            inp["punk_ptr"], inp["punk_idx"] = csr_of(punk)
+            if not self_:
+                users, uunk, umean = user_vectors(dseed + 1, Q, d)
+                inp.update(users=users, umean=umean)
+                inp["uunk_ptr"], inp["uunk_idx"] = csr_of(uunk)
+            ext = dict(pool="f64", pmean="f64", punk_ptr="i64", punk_idx="i32", users="f64", umean="f64",
+                       uunk_ptr="i64", uunk_idx="i32")
+            for kk, v in inp.items():
+                v.tofile(os.path.join(out, f"{kk}.{ext[kk]}"))
+            run(["chain", out, N, Q, d, k, L, 1, w, seed, P, NT, self_])
+            res = load_dir(out); res.update(inp)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+            meta[name] = dict(kind="chain", N=N, Q=N if self_ else Q, d=d, k=k, L=L, w=w, seed=seed, P=P, NTOP=NT,
+                              self=bool(self_), data_seed=dseed)
         for name, text in (CONF_CASES.items() if want("conf") else []):
             path = os.path.join(iodir, name + ".conf")
             with open(path, "w", newline="") as f:

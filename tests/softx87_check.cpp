@@ -80,6 +80,33 @@ int main(int argc, char** argv) {
             if (!same(s, ld) || sx_floor_i64(s) != (int64_t)floorl(ld)) bad++;
         }
     }
+    // the full hash values on fp64 rows (EuclideanHGen / CosineHGen over
+    // general doubles): special products (inf / nan), huge and tiny values, and
+    // int(floorl(.)) outside the int range -> INT_MIN (x87 FISTP "indefinite")
+    const double specials[] = {INFINITY, -INFINITY, NAN, 1e308, -1e308, 1e300, 5e-324, -2.5e-310, 0.0, -0.0};
+    for (long it = 0; it < iters / 4 + 64; it++) {
+        int d = 1 + (int)(rng() % 40);
+        long double acc = 0.0L;
+        SxSum s;
+        s.init();
+        for (int j = 0; j < d; j++) {
+            double p;
+            const int m = (int)(rng() % 16);
+            if (m == 0) p = specials[rng() % 10];
+            else if (m < 3) p = std::ldexp(u(rng), (int)(rng() % 2000) - 1000);
+            else p = u(rng) * 1e9;
+            acc = acc + (long double)p;
+            s.add(p);
+        }
+        float t = (float)std::fabs(u(rng)), w = (float)(1e-3 + std::fabs(u(rng)));
+        volatile long double fl = floorl((acc + (long double)t) / (long double)w);
+        int32_t want;
+        if (!(fl >= -2147483648.0L && fl <= 2147483647.0L)) want = (int32_t)0x80000000;   // FISTP indefinite
+        else want = (int32_t)(int64_t)fl;
+        checks += 2;
+        if (sx_hash_floor(s, (double)t, w) != want) { if (bad < 5) fprintf(stderr, "hash floor mismatch it=%ld\n", it); bad++; }
+        if (sx_hash_sign(s) != (acc >= 0 ? 1 : 0)) { if (bad < 5) fprintf(stderr, "hash sign mismatch it=%ld\n", it); bad++; }
+    }
     printf("checks=%ld bad=%ld\n", checks, bad);
     return bad ? 1 : 0;
 }

@@ -54,7 +54,8 @@ def test_shim_compiles_against_reference_headers(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("args", [("7", "2000", "128", "16"), ("11", "900", "17", "5")])
+@pytest.mark.parametrize("args", [("7", "2000", "128", "16"), ("11", "900", "17", "5"),
+                                  ("13", "1500", "100", "12", "f64")])
 def test_shim_matches_reference_functions(args):
     if not os.path.exists(CHECK):
         pytest.skip("oracle/_ref/compat_check not built (needs the reference sources at build time)")
@@ -68,3 +69,4 @@ def test_shim_matches_reference_functions(args):
         assert int(stats[key]) > 0, (key, stats)
     assert int(stats["kmeans_euclidean_iterations"]) >= 2 and int(stats["kmeans_cosine_iterations"]) >= 2, stats
     assert int(stats["recom_users"]) >= 30, stats
+    assert int(stats["chain_users"]) >= 100, stats

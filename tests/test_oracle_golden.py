@@ -8,12 +8,19 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import cases, golden, golden_meta, kpp_input, lloyd_input
+from conftest import case_queries, case_rows, cases, golden, golden_meta, kpp_input, lloyd_input
 
 META = golden_meta()
+# the same checks over general fp64 rows (fixtures made from user-vector-shaped
+# doubles, tests/golden/make_golden.py:user_vectors; inputs stored in the npz)
+LSH = cases("lsh") + cases("f64_lsh")
+CUBE = cases("cube") + cases("f64_cube")
+LLOYD = cases("lloyd") + cases("f64_lloyd")
+KPP = cases("kmeanspp") + cases("f64_kmeanspp")
+RANGE = cases("range") + cases("f64_range")
 
 
-@pytest.mark.parametrize("name", cases("lsh"))
+@pytest.mark.parametrize("name", LSH)
 def test_lsh_params(name):
     m, g = META[name], golden(name)
     if m["metric"] == "euclidean":
@@ -25,10 +32,10 @@ def test_lsh_params(name):
         assert np.array_equal(R.view(np.uint64), g["R"].view(np.uint64))
 
 
-@pytest.mark.parametrize("name", cases("lsh"))
+@pytest.mark.parametrize("name", LSH)
 def test_lsh_hash_and_buckets(name):
     m, g = META[name], golden(name)
-    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    X = case_rows(name)
     if m["metric"] == "euclidean":
         tu, phi, b = oracle.lsh_hash_euclid(X, g["V"], g["t"], g["w"][0, 0], g["r"], m["nb"])
         assert np.array_equal(tu, g["tuples"])
@@ -46,11 +53,11 @@ def test_lsh_hash_and_buckets(name):
         assert np.array_equal(idx[l], gi[gp[l * nb]:gp[(l + 1) * nb]])
 
 
-@pytest.mark.parametrize("name", cases("lsh"))
+@pytest.mark.parametrize("name", LSH)
 def test_lsh_queries(name):
     m, g = META[name], golden(name)
-    X = oracle.synth(m["data_seed"], m["N"], m["d"])
-    Qx = oracle.synth(m["query_seed"], m["Q"], m["d"])
+    X = case_rows(name)
+    Qx = case_queries(name)
     allq = np.concatenate([X[:m["nqrows"]], Qx])
     nb, L = m["nb"], m["L"]
     if m["metric"] == "euclidean":
@@ -68,10 +75,10 @@ def test_lsh_queries(name):
             assert np.array_equal(got, gidx[ptr[q]:ptr[q + 1]]), (kind, q)
 
 
-@pytest.mark.parametrize("name", cases("cube"))
+@pytest.mark.parametrize("name", CUBE)
 def test_cube(name):
     m, g = META[name], golden(name)
-    X = oracle.synth(m["data_seed"], m["N"], m["d"])
+    X = case_rows(name)
     k = m["k"]
     if m["metric"] == "euclidean":
         V, t, st = oracle.gen_cube_euclid(m["seed"], k, m["d"], np.float32(m["w"]))
@@ -93,7 +100,7 @@ def test_cube(name):
     rp, idx = oracle.bucket_csr(vertex[:, None], 1 << k)
     assert np.array_equal(rp[0], g["members_ptr"]) and np.array_equal(idx[0], g["members_idx"])
     # probe queries (only the fully-seen ones are pinned: qmask)
-    Qx = oracle.synth(m["query_seed"], m["Q"], m["d"])
+    Qx = case_queries(name)
     allq = np.concatenate([X[:m["nqrows"]], Qx])[g["qmask"].astype(bool)]
     if m["metric"] == "euclidean":
         qv, _ = memo.apply(oracle.cube_h(allq, V, t, g["w"][0]))
@@ -108,13 +115,13 @@ def test_cube(name):
             assert np.array_equal(got, gi[ptr[q]:ptr[q + 1]]), (p, q)
 
 
-@pytest.mark.parametrize("name", cases("lloyd"))
+@pytest.mark.parametrize("name", LLOYD)
 def test_lloyd_and_update(name):
     m, g = META[name], golden(name)
-    X = lloyd_input(name)
+    X = case_rows(name)
     C = g["centers0"]
     src = g["src_rows"]
-    if m["init"] in ("ext", "ext_far"):
+    if m.get("init") in ("ext", "ext_far"):
         assert np.array_equal(C, g["ext_centers"])
     for it in range(len(g["cont"])):
         a, dist = oracle.lloyd_assign(X, C, m["metric"], src if it == 0 else None)
@@ -126,10 +133,10 @@ def test_lloyd_and_update(name):
         assert np.array_equal(C.view(np.uint64), g[f"centers{it + 1}"].view(np.uint64)), it
 
 
-@pytest.mark.parametrize("name", cases("kmeanspp"))
+@pytest.mark.parametrize("name", KPP)
 def test_kmeans_pp_and_rand_selection(name):
     m, g = META[name], golden(name)
-    X = kpp_input(name)
+    X = case_rows(name)
     assert np.array_equal(oracle.kmeans_pp(X, m["K"], m["metric"], m["seed"]), g["kpp_rows"])
     assert np.array_equal(oracle.rand_selection(m["N"], m["K"], m["seed"]), g["rand_rows"])
 
@@ -167,13 +174,13 @@ def test_minstd_and_uniform_int():
     assert oracle.lib().or_minstd_seed(0) == 1 and oracle.lib().or_minstd_seed(2147483647) == 1
 
 
-@pytest.mark.parametrize("name", cases("range"))
+@pytest.mark.parametrize("name", RANGE)
 def test_range_assignment(name):
     # lsh_/cube_range_assignment (assignment.hpp:108-145) on the reference's own
     # combined buckets; iterations >= 1 run on "k_means_center" centroids whose
     # shared ID collapses the distance cache (key = all zeros).
     m, g = META[name], golden(name)
-    X = kpp_input(name)
+    X = case_rows(name)
     for it in range(int(g["iters"][0])):
         a, dist, _ = oracle.range_assign(X, g[f"centers{it}"], g[f"comb{it}_ptr"], g[f"comb{it}_idx"], m["metric"],
                                          key=g[f"key{it}"], src_rows=g["src_rows"] if it == 0 else None)
@@ -181,11 +188,39 @@ def test_range_assignment(name):
         assert np.array_equal(dist.view(np.uint64), g[f"dist{it}"].view(np.uint64)), it
 
 
-@pytest.mark.parametrize("name", cases("lloyd"))
+@pytest.mark.parametrize("name", LLOYD)
 def test_silhouette(name):
     # silhouette_cluster (silhouette.hpp:31-144) of every golden assignment, NaN bits included
     m, g = META[name], golden(name)
-    X = lloyd_input(name)
+    X = case_rows(name)
     for it in range(len(g["cont"])):
         out, _ = oracle.silhouette(X, g[f"assign{it}"], g[f"centers{it}"], m["metric"])
         assert np.array_equal(out.view(np.uint64), g[f"sil{it}"].view(np.uint64)), it
+
+
+@pytest.mark.parametrize("name", cases("chain"))
+def test_recommender_chain(name):
+    # main.cpp:149-222: cosine LSH over user vectors (general doubles), filtered
+    # combined buckets per user, get_P_closest, get_top_N_recom
+    m, g = META[name], golden(name)
+    pool = g["pool"]
+    users = pool if m["self"] else g["users"]
+    R, _ = oracle.gen_lsh_cosine(m["seed"], m["L"], m["k"], m["d"])
+    assert np.array_equal(R.view(np.uint64), g["R"].view(np.uint64))
+    b = oracle.lsh_hash_cosine(pool, R)
+    assert np.array_equal(b, g["g"])
+    nb = 1 << m["k"]
+    rp, idx = oracle.bucket_csr(b, nb)
+    qb = oracle.lsh_hash_cosine(users, R)
+    lists = [oracle.lsh_query(m["N"], nb, rp, idx, qb[q]) for q in range(m["Q"])]
+    ptr = np.cumsum([0] + [len(l) for l in lists]).astype(np.int64)
+    cand = np.concatenate(lists).astype(np.int32)
+    assert np.array_equal(ptr, g["nb_ptr"]) and np.array_equal(cand, g["nb_idx"])
+    idx_, sim, cnt = oracle.p_closest(pool, users, ptr, cand, m["P"])
+    assert np.array_equal(cnt, g["pc_cnt"]) and np.array_equal(idx_, g["pc_idx"])
+    assert np.array_equal(sim.view(np.uint64), g["pc_sim"].view(np.uint64))
+    up, ui = (g["punk_ptr"], g["punk_idx"]) if m["self"] else (g["uunk_ptr"], g["uunk_idx"])
+    um = g["pmean"] if m["self"] else g["umean"]
+    top = oracle.top_n_recom(pool, g["pmean"], users, um, up, ui, idx_, sim, cnt, m["NTOP"])
+    has = cnt > 0
+    assert np.array_equal(top[has], g["top"][has])
