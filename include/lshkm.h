@@ -203,7 +203,7 @@ int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f_host, int32_t* h_host, int32
  * lloyds_assignment (assignment.hpp:54-80): for each row the centroid with the
  * smallest distance (strict '<', first index wins), its fp64 distance, then
  * the centroid override: assign[src_rows[c]] = c, dist = 0 for c = 0..K-1
- * (src_rows_host may be NULL; entries < 0 are ignored). */
+ * (src_rows_host may be NULL; entries outside [0, N) are ignored). */
 int lshkm_lloyd_assign(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const double* C_dev,
                        int K, int metric, const int32_t* src_rows_host, int32_t* assign_dev,
                        double* dist_dev);

@@ -377,7 +377,7 @@ void or_lloyd_assign(int64_t N, int d, int K, const double* X, const double* C, 
     }
     if (src_rows)
         for (int c = 0; c < K; c++)
-            if (src_rows[c] >= 0) { assign[src_rows[c]] = c; dist[src_rows[c]] = 0; }
+            if (src_rows[c] >= 0 && src_rows[c] < N) { assign[src_rows[c]] = c; dist[src_rows[c]] = 0; }   /* as lshkm_lloyd_assign: rows outside [0, N) ignored */
 }
 
 static double euclid_f64(const double* a, const double* b, int d) {
@@ -664,7 +664,7 @@ int or_range_assign(int64_t N, int d, int K, const double* X, const double* C, i
     }
     if (src_rows)
         for (int c = 0; c < K; c++)
-            if (src_rows[c] >= 0) { assign[src_rows[c]] = c; dist[src_rows[c]] = 0; }
+            if (src_rows[c] >= 0 && src_rows[c] < N) { assign[src_rows[c]] = c; dist[src_rows[c]] = 0; }   /* as lshkm_lloyd_assign: rows outside [0, N) ignored */
     return passes;
 }
 

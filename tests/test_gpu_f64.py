@@ -229,8 +229,9 @@ def test_f64_large_vs_oracle(ctx, metric):
     rows = (np.arange(K) * (N // K)).astype(np.int32)
     Ch = Xh[rows]
     sub = slice(0, 40_000)                            # the oracle's Lloyd is O(N K d) on the host
-    a, dist = lshkm.lloyd_assign(ctx, X[sub], to_dev(ctx, Ch), metric, rows)
-    oa, od = oracle.lloyd_assign(Xh[sub], Ch, metric, rows)
+    src = np.where(rows < 40_000, rows, -1).astype(np.int32)   # centroid rows inside the slice
+    a, dist = lshkm.lloyd_assign(ctx, X[sub], to_dev(ctx, Ch), metric, src)
+    oa, od = oracle.lloyd_assign(Xh[sub], Ch, metric, src)
     assert np.array_equal(a.cpu().numpy(), oa)
     assert_close_f64(dist.cpu().numpy(), od)
     Cn, cnt, _ = lshkm.kmeans_update(ctx, X[sub], a, to_dev(ctx, Ch), metric, 0.0)
