@@ -1,14 +1,18 @@
 """Headline benchmark: point hash+assign ops/sec at d=128, N=10M per GPU, K=256.
 
-One step = one pass of the hot path over the rank's resident shard:
-  LSH hashing (L=5 tables x k=4 EuclideanH functions, w=0.4, nb = N_total/100:
-  k-tuples + bucket IDs)  +  Lloyd assignment over K=256 centroids (cluster ID +
-  exact-order fp64 distance).
+--workload c3 (default; BASELINE.json configs[2] + the C2 hashing): one step =
+  one pass of the hot path over the rank's resident shard: LSH hashing (L=5
+  tables x k=4 EuclideanH functions, w=0.4, nb = N_total/100: k-tuples + bucket
+  IDs) + Lloyd assignment over K=256 centroids (cluster ID + exact-order fp64
+  distance). Multi-GPU: contiguous row shards, one process per GPU, no
+  data-path collective (hash and assign are per point) -> weak scaling.
+--workload c5 (configs[4]: 80M x 128, K=1024 over 8 GPUs = 10M per GPU): one
+  step = one full iteration, sharding.ShardedLloyd: lshkm_hash_assign (K=1024)
+  + lshkm_kmeans_partial + all-reduce of the K x d sums and K counts over RCCL
+  + lshkm_kmeans_finalize (centers replaced as k_means does).
 Points are synthetic (include/lshkm_synth.h), generated in HBM before timing.
-Multi-GPU: contiguous row shards, one process per GPU, no data-path collective
-(hash and assign are independent per point) -> weak scaling.
 
-python bench.py --gpus N --steps K --warmup W   (torch.distributed.run for N>1)
+python bench.py --gpus N --steps K --warmup W [--workload c5]   (torch.distributed.run for N>1)
 """
 import argparse
 import ctypes as C
@@ -41,6 +45,23 @@ def load_pkg():
 
 
 sharding = load_module("lshkm_sharding", "sharding.py")
+
+
+def port_all_cores(sample_hash, sample_assign, K):
+    """The C restatement (oracle/_ref/liboracle.so, -O2, OpenMP over rows) on all
+    of this rank's host cores (OMP_NUM_THREADS, 16 on the GPU box), in a child
+    process so the thread count is set before the library loads."""
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    env = dict(os.environ, OMP_NUM_THREADS=str(cores))
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "bench_port.py"), str(sample_hash),
+                          str(sample_assign), str(K), str(SEED_DATA)], check=True, capture_output=True, text=True,
+                         env=env).stdout
+    res = json.loads(out.strip().splitlines()[-1])
+    per_pt = res["hash_s"] / res["hash_pts"] + res["assign_s"] / res["assign_pts"]
+    return {"value": 1.0 / per_pt, "unit": "point hash+assign ops/s", "cores": cores, "kind": "port",
+            "sample": f"{res['hash_pts']} pts hashed (L=5,k=4) + {res['assign_pts']} pts assigned (K={K}), d=128, "
+                      f"{cores} OpenMP threads, C restatement at -O2; hash {res['hash_s']:.2f}s, "
+                      f"assign {res['assign_s']:.2f}s"}
 
 
 def cpu_baseline(sample_hash, sample_assign, K):
@@ -81,7 +102,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU")
-    ap.add_argument("--k", type=int, default=256, help="centroids")
+    ap.add_argument("--workload", choices=["c3", "c5"], default="c3")
+    ap.add_argument("--k", type=int, default=None, help="centroids (default 256 for c3, 1024 for c5)")
+    ap.add_argument("--cpu-port-hash-sample", type=int, default=400_000)
+    ap.add_argument("--cpu-port-assign-sample", type=int, default=300_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-hash-sample", type=int, default=100_000)
     ap.add_argument("--cpu-assign-sample", type=int, default=12_000)
@@ -102,7 +126,8 @@ def main():
     lk = load_pkg()
     ctx = lk.Context(local)
     lib = lk.lib()
-    N, K = args.n, args.k
+    N = args.n
+    K = args.k or (1024 if args.workload == "c5" else 256)
     N_total = N * world
     nb = N_total // BUCKET_DIV
 
@@ -122,9 +147,18 @@ def main():
     p = lambda t_: C.c_void_p(t_.data_ptr())
     src_p = src.ctypes.data_as(C.c_void_p)
 
-    def step():
-        # one pass: tuples + bucket IDs + cluster IDs + fp64 distances (lshkm_hash_assign)
-        lk._ck(lib.lshkm_hash_assign(lsh.h, p(X), N, p(Cc), K, src_p, p(tuples), None, p(bucket), p(assign), p(dist_)))
+    if args.workload == "c5":
+        # one full iteration: hash + assign, per-shard sums, RCCL all-reduce, finalize
+        del tuples, bucket, assign, dist_
+        it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="fast")
+
+        def step():
+            it.step()
+    else:
+        def step():
+            # one pass: tuples + bucket IDs + cluster IDs + fp64 distances (lshkm_hash_assign)
+            lk._ck(lib.lshkm_hash_assign(lsh.h, p(X), N, p(Cc), K, src_p, p(tuples), None, p(bucket), p(assign),
+                                         p(dist_)))
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -149,8 +183,9 @@ def main():
     hexact = ctx.stat(lk.STAT_HASH_EXACT)
 
     # Dominant kernel = the fused pass (fused_persistent_kernel<true> and its
-    # hash_fixup_kernel): HIP events recorded by the library around those
-    # launches, on the stream they run on; averaged over reps steps.
+    # hash_fixup_kernel; at K > 256 one launch per 256-centroid slice): HIP
+    # events recorded by the library around those launches, on the stream they
+    # run on; averaged over reps steps.
     reps = max(3, args.steps)
     lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 1))
     ms = C.c_float()
@@ -174,7 +209,7 @@ def main():
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("N") == N and tj.get("K") == K:
+        if tj.get("N") == N and tj.get("K") == K and tj.get("workload", "c3") == args.workload:
             traffic = tj.get("hbm_bytes_per_launch")
 
     if rank == 0:
@@ -192,7 +227,10 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32 points; split-f16 MFMA scores (f32 accumulate), fp64/x87-exact results",
             "data": "synthetic (include/lshkm_synth.h), resident in HBM",
-            "config": {"workload": f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128",
+            "config": {"workload": (f"C5 LSH-assign + k-means iteration (hash + assign + per-shard sums + RCCL "
+                                    f"all-reduce + finalize), K={K}, N={N} per GPU, d=128"
+                                    if args.workload == "c5" else
+                                    f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128"),
                        "N_per_gpu": N, "N_total": N_total, "d": D, "K": K, "L": L_TABLES, "k": K_FUNCS,
                        "w": W, "nb": nb, "parallelism": f"dp{world} (row shards)"},
             "roofline": {
@@ -208,6 +246,11 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample, K)
+            try:
+                line["cpu_baseline"]["all_cores"] = port_all_cores(args.cpu_port_hash_sample,
+                                                                   args.cpu_port_assign_sample * 256 // K, K)
+            except (subprocess.CalledProcessError, OSError, ValueError) as e:
+                line["cpu_baseline"]["all_cores"] = {"error": str(e)[:200]}
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

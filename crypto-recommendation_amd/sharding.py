@@ -10,9 +10,27 @@ row index. With contiguous row shards [row0, row0 + n) in rank order:
     bucket), the concatenation of the shards' members of that bucket;
   - k-means centers need the per-cluster sums: one all-reduce of K x d fp64 sums
     and K counts (fast mode; the exact-order chain would serialize the shards).
-Pure host logic (numpy + torch.distributed); the compute is the HIP library.
+Host logic (numpy + torch.distributed); the compute is the HIP library.
+Collectives: RCCL ("nccl") on GPU tensors; with the gloo backend (CPU tests,
+or several ranks sharing one GPU) device tensors are staged through host
+memory, since gloo's collectives run on host buffers.
 """
 import numpy as np
+
+
+def _dist():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist
+    return None
+
+
+def _staged(dist, t):
+    """(buffer the collective runs on, copy-back) for tensor t."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        return h, (lambda: t.copy_(h))
+    return t, (lambda: None)
 
 
 def shard_range(n_total, world, rank):
@@ -112,29 +130,98 @@ def chain_partials(local_fn, sums_like, counts_like):
     bit for bit. The last rank broadcasts the totals. ``sums_like`` /
     ``counts_like`` are receive buffers of the right shape, dtype and device.
     Point-to-point hops of K*d*8 bytes (1 MiB at K=1024, d=128) over RCCL/xGMI."""
-    import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    dist = _dist()
+    if dist is None:
         return local_fn(None, None)
     rank, world = dist.get_rank(), dist.get_world_size()
+
+    def xfer(op, t, peer):
+        b, back = _staged(dist, t)
+        if op == "recv":
+            dist.recv(b, src=peer)
+            back()
+        elif op == "send":
+            dist.send(b, dst=peer)
+        else:
+            dist.broadcast(b, src=peer)
+            back()
+
     carry_s = carry_c = None
     if rank > 0:
         carry_s, carry_c = sums_like, counts_like
-        dist.recv(carry_s, src=rank - 1)
-        dist.recv(carry_c, src=rank - 1)
+        xfer("recv", carry_s, rank - 1)
+        xfer("recv", carry_c, rank - 1)
     sums, counts = local_fn(carry_s, carry_c)
     if rank + 1 < world:
-        dist.send(sums, dst=rank + 1)
-        dist.send(counts, dst=rank + 1)
+        xfer("send", sums, rank + 1)
+        xfer("send", counts, rank + 1)
         sums, counts = sums_like, counts_like
-    dist.broadcast(sums, src=world - 1)
-    dist.broadcast(counts, src=world - 1)
+    xfer("bcast", sums, world - 1)
+    xfer("bcast", counts, world - 1)
     return sums, counts
 
 
 def allreduce_partials(sums, counts):
     """Sum the per-shard (sums, counts) over all ranks in place (RCCL on GPUs, gloo on CPU)."""
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(sums)
-        dist.all_reduce(counts)
+    dist = _dist()
+    if dist is not None:
+        for t in (sums, counts):
+            b, back = _staged(dist, t)
+            dist.all_reduce(b)
+            back()
     return sums, counts
+
+
+class ShardedLloyd:
+    """One rank's part of the C5 iteration (main.cpp:96-103 with
+    LSH hashing riding on the assignment pass): per step, on the rank's
+    resident rows,
+      lshkm_hash_assign   -- L x k hashes + bucket IDs + argmin over K centroids
+      lshkm_kmeans_partial (fast) / _partial_carry (exact) -- per-cluster sums
+      all-reduce of the K x d sums and K counts over RCCL (fast mode), or the
+        rank-to-rank carry chain (exact mode, the reference's sums bit for bit)
+      lshkm_kmeans_finalize -- means, the reference's continue test
+    and the centers are replaced when k_means would replace them
+    (update.hpp:63-80). X: this rank's rows [row0, row0 + n) of N_total."""
+
+    def __init__(self, lk, ctx, lsh, X, C0, src_rows, mode="fast", metric="euclidean", min_dist=0.0):
+        torch = ctx.torch
+        self.lk, self.ctx, self.lsh, self.X = lk, ctx, lsh, X
+        self.mode, self.metric, self.min_dist = mode, metric, float(min_dist)
+        n = X.shape[0]
+        self.K, self.d = C0.shape
+        self.C = C0.clone()
+        self.src = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
+        e = ctx.empty
+        self.tuples = e((n, lsh.L, lsh.k), torch.int32) if lsh is not None else None
+        self.bucket = e((n, lsh.L), torch.int32) if lsh is not None else None
+        self.assign = e((n,), torch.int32)
+        self.dist = e((n,), torch.float64)
+        self.sums = e((self.K, self.d), torch.float64)
+        self.counts = e((self.K,), torch.int64)
+        self.cont = True
+
+    def step(self):
+        import ctypes as C
+        lk, ctx, X = self.lk, self.ctx, self.X
+        p = lk._t_ptr
+        src = None if self.src is None else self.src.ctypes.data_as(C.c_void_p)
+        if self.lsh is not None:
+            lk._ck(lk._fn("lshkm_hash_assign", X)(self.lsh.h, p(X), X.shape[0], p(self.C), self.K, src,
+                                                  p(self.tuples), None, p(self.bucket), p(self.assign),
+                                                  p(self.dist)))
+        else:
+            lk.lloyd_assign(ctx, X, self.C, self.metric, self.src, self.assign, self.dist)
+        if self.mode == "exact":
+            def local(cs, cc):
+                return lk.kmeans_partial_carry(ctx, X, self.assign, self.K, cs, cc)
+            sums, counts = chain_partials(local, self.sums, self.counts)
+        else:
+            sums, counts = lk.kmeans_partial(ctx, X, self.assign, self.K, self.sums, self.counts)
+            allreduce_partials(sums, counts)
+        Cn, cont = lk.kmeans_finalize(ctx, sums, counts, self.C, self.metric, self.min_dist)
+        if cont:              # k_means replaces every center (update.hpp:70-79)
+            self.C = Cn
+            self.src = None   # the override applies to dataset-row centroids only
+        self.cont = cont
+        return cont

@@ -1,0 +1,66 @@
+"""One rank of the multi-rank product-path test (tests/test_gpu_multirank.py).
+
+Not a test module: launched as `python tests/mr_worker.py RANK WORLD PORT OUTDIR`
+(several ranks sharing the one MI355X over gloo, or one rank with WORLD = 1 for
+the single-process reference). Runs liblshkm on this rank's contiguous row
+shard (crypto-recommendation_amd/sharding.py): the C5 iteration (hash + assign
++ k-means update) in fast (all-reduce) and exact (carry chain) mode, and the
+sharded euclidean hypercube build; saves everything to OUTDIR/rank<R>.npz."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from amd import PKG, lshkm  # noqa: E402
+
+sys.path.insert(0, PKG)
+import sharding as sh  # noqa: E402
+
+N_TOTAL, D, L, KF, K, STEPS = 120_000, 128, 5, 4, 300, 2
+
+
+def main():
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = lshkm.Context(0)
+    row0, n = sh.shard_range(N_TOTAL, world, rank)
+    X = ctx.synth(0x5EED, n, D, row0=row0)
+    V, t, r, _ = lshkm.params_lsh_euclidean(12345, L, KF, D, 0.4)
+    lsh = lshkm.LSH(ctx, "euclidean", D, KF, L, N_TOTAL // 100, 0.4, V=V, t=t, r=r)
+    rows = sh.centroid_rows(N_TOTAL, K)
+    C0 = torch.stack([ctx.synth(0x5EED, 1, D, row0=int(rw))[0] for rw in rows]).double()
+    res = {}
+    for mode in ("fast", "exact"):
+        it = sh.ShardedLloyd(lshkm, ctx, lsh, X, C0, sh.local_src_rows(rows, row0, n), mode=mode)
+        for s in range(STEPS):
+            it.step()
+            res[f"{mode}_assign{s}"] = it.assign.cpu().numpy()
+            res[f"{mode}_dist{s}"] = it.dist.cpu().numpy()
+            res[f"{mode}_centers{s + 1}"] = it.C.cpu().numpy()
+            res[f"{mode}_cont{s}"] = np.array([it.cont])
+        res[f"{mode}_tuples"] = it.tuples.cpu().numpy()
+        res[f"{mode}_bucket"] = it.bucket.cpu().numpy()
+    Vc, tc, st = lshkm.params_cube_euclidean(777, 10, D, 2.0)
+    cube = lshkm.Cube(ctx, "euclidean", D, 10, 2.0, V=Vc, t=tc, rng_state=st)
+    sh.cube_build_sharded(lshkm, cube, X, row0)
+    f, h, b, state = cube.memo()
+    o = np.lexsort((h, f))
+    res.update(memo_f=f[o], memo_h=h[o], memo_bit=b[o], memo_state=np.array([state], np.int64),
+               vertex=cube.vertices(X).cpu().numpy(), row0=np.array([row0]))
+    np.savez(os.path.join(out, f"rank{rank}.npz"), **res)
+    ctx.sync()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    print(f"rank {rank} ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+"""The multi-rank product path on the GPU: two fresh processes
+share the one MI355X over gloo, each running liblshkm on its row shard
+(tests/mr_worker.py), against one process over all rows.
+
+  - hash tuples, bucket IDs, cluster IDs and distances: bit-exact (per row);
+  - k-means centers, fast mode (all-reduce of per-shard sums): <= 1e-13 rel;
+  - k-means centers, exact mode (rank-to-rank carry chain): bit-exact;
+  - sharded euclidean hypercube: the same coins (global first-occurrence
+    order) and vertices as the single-process build.
+The C5 bench line (bench.py --workload c5) runs the same ShardedLloyd step."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "mr_worker.py")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(world, out):
+    port = str(_free_port())
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, "-u", WORKER, str(r), str(world), port, str(out)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=240)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    return [dict(np.load(os.path.join(out, f"rank{r}.npz"))) for r in range(world)]
+
+
+def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
+    (tmp_path / "one").mkdir()
+    (tmp_path / "two").mkdir()
+    one = _run(1, tmp_path / "one")[0]
+    two = _run(2, tmp_path / "two")
+    cat = lambda key: np.concatenate([r[key] for r in two])
+    for mode in ("fast", "exact"):
+        assert np.array_equal(cat(f"{mode}_tuples"), one[f"{mode}_tuples"]), mode
+        assert np.array_equal(cat(f"{mode}_bucket"), one[f"{mode}_bucket"]), mode
+    # iteration 0 runs on the same dataset-row centroids everywhere: bit-exact
+    for mode in ("fast", "exact"):
+        assert np.array_equal(cat(f"{mode}_assign0"), one[f"{mode}_assign0"]), mode
+        assert np.array_equal(cat(f"{mode}_dist0").view(np.uint64), one[f"{mode}_dist0"].view(np.uint64)), mode
+    # exact mode: the carry chain reproduces the single pass bit for bit, so
+    # every later iteration is identical too
+    for s in range(2):
+        assert np.array_equal(cat(f"exact_assign{s}"), one[f"exact_assign{s}"]), s
+        for r in two:
+            assert np.array_equal(r[f"exact_centers{s + 1}"].view(np.uint64),
+                                  one[f"exact_centers{s + 1}"].view(np.uint64)), s
+    # fast mode: sums reassociate across the all-reduce
+    c1, c1_one = two[0]["fast_centers1"], one["fast_centers1"]
+    assert np.array_equal(c1, two[1]["fast_centers1"])       # every rank holds the same centers
+    rel = np.abs(c1 - c1_one) / np.maximum(np.abs(c1_one), 1e-300)
+    assert rel.max() <= 1e-13
+    # hypercube: same coins, same engine state, same vertices
+    for key in ("memo_f", "memo_h", "memo_bit", "memo_state"):
+        for r in two:
+            assert np.array_equal(r[key], one[key]), key
+    assert np.array_equal(cat("vertex"), one["vertex"])
