@@ -462,8 +462,9 @@ static int assign_path(int metric, int d, int K, bool f64) {
 // Segmented lists (seg_counts != NULL) come from the persistent fused form.
 static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int metric,
                         const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist,
-                        const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0) {
-    const int32_t* rows = (const int32_t*)ctx->ws_ambig.p;
+                        const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0,
+                        const int32_t* rows = nullptr) {
+    if (!rows) rows = (const int32_t*)ctx->ws_ambig.p;
     if (metric != LSHKM_METRIC_EUCLIDEAN || (!seg_counts && d > 256))
         return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist, seg_counts,
                                    seg_rows, nseg);
@@ -494,16 +495,23 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
     if (path == 0) {
         const int Kpad = (K + 63) / 64 * 64;
         const bool cosine = metric != LSHKM_METRIC_EUCLIDEAN;
+        // hi-only scoring + 3-product refinement (euclidean); LSHKM_FUSED_HI=0: the 3-product form alone
+        const char* fh = getenv("LSHKM_FUSED_HI");
+        const bool hi = !cosine && !(fh && !strcmp(fh, "0"));
+        const int64_t list_cap = N + FUSED_LIST_SLACK;
+        const int64_t part_tiles = std::max<int64_t>((N + 31) / 32, (list_cap + 31) / 32 + FUSED_MAX_SEGS);
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) ||
             (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4 + (size_t)Kpad * 8)) ||
             (rc = ctx->ws_ambig.reserve((size_t)(N + FUSED_LIST_SLACK) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
             (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)) ||
             ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8))) ||
-            (Kpad > 256 && (rc = ctx->ws_part.reserve((size_t)((N + 31) / 32) * 64 * 16))) ||
+            (Kpad > 256 && (rc = ctx->ws_part.reserve((size_t)part_tiles * 64 * 16))) ||
+            (hi && ((rc = ctx->ws_ambig2.reserve((size_t)list_cap * 4)) ||
+                    (rc = ctx->ws_seg2.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)))) ||
             (fuse_hash && !tuples && (rc = ctx->ws_tuples.reserve((size_t)std::max<int64_t>(N, 1) * lsh->proj.LK * 4))))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
-        LSHKM_HIP(hipMemsetAsync(cnt, 0, 16, s));         // [0] ambiguous rows, [1] hash fix-up rows
+        LSHKM_HIP(hipMemsetAsync(cnt, 0, 24, s));         // [0] ambiguous rows, [1] hash fix-up rows, [2] refined rows
         _Float16* Ch = (_Float16*)ctx->ws_c32.p;
         _Float16* Cl = Ch + (size_t)Kpad * 128;
         float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
@@ -517,7 +525,13 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         f.list_cap = N + FUSED_LIST_SLACK;
         f.seg_counts = (int32_t*)ctx->ws_seg.p;
         f.seg_cap = FUSED_MAX_SEGS;
-        if (Kpad > 256) { f.part = ctx->ws_part.p; f.part_bytes = (int64_t)((N + 31) / 32) * 64 * 16; }
+        if (Kpad > 256) { f.part = ctx->ws_part.p; f.part_bytes = part_tiles * 64 * 16; }
+        if (hi) {
+            f.hi = true;
+            f.list2 = (int32_t*)ctx->ws_ambig2.p;
+            f.seg_counts2 = (int32_t*)ctx->ws_seg2.p;
+            f.refined = cnt + 2;
+        }
         if (cosine) {
             f.metric = 1; f.nbv = nbv;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
@@ -533,8 +547,9 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
         if ((rc = launch_fused(s, fuse_hash, f))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
-        if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.seg_counts : nullptr,
-                               f.seg_rows, f.nseg))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.final_counts : nullptr,
+                               f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if (hi && (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_REFINED, cnt + 2))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (cosine && ((rc = launch_cos_fix_seg(s, X.f(), C, f.hfix, f.seg_counts, f.seg_rows, f.nseg, assign, dist)) ||
                        (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1)))) { LSHKM_LAUNCH_CHECK(); return rc; }

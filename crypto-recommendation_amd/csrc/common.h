@@ -57,6 +57,7 @@ enum Stat {
     STAT_KPP_CHUNKS = 2,     // k-means++ prefix-walk chunks (KPP_CHUNK rows each) ...
     STAT_KPP_SEQ = 3,        // ... of which summed element by element (binade crossings, ties)
     STAT_COS_FIX = 4,        // cosine Lloyd winners whose distance took the soft-x87 chain
+    STAT_REFINED = 5,        // rows the hi-only fused pass left to the 3-product refinement
     STAT_COUNT = 8
 };
 

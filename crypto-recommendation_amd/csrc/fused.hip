@@ -91,7 +91,8 @@ struct FusedArgs {
     const _Float16* Ch;
     const _Float16* Cl;
     const float* cnh;        // [Kpad] -||c||^2 / 2 (f32), -inf for padding rows
-    const float* cbound;     // [0] = ec (times |x|), [1] = eb (constant), [2] = range flag (bits)
+    const float* cbound;     // [0] = ec (times |x|), [1] = eb (constant), [2] = range flag (bits), [3] = max |c|,
+                             // [4] = max |c - ch|, [5] = max |ch|, [6] = max |c|^2 / 2 (all rounded up)
     const double* C64;       // [K][128] exact centroids
     int Kpad;
     // hash family (HASH only)
@@ -127,6 +128,11 @@ struct FusedArgs {
     // crosses passes in part[tile * 64 + lane]
     float4* part;
     int t0, pass_first, pass_last;
+    // LIST form (refinement of the rows a hi-only pass left uncertified): block b
+    // takes the rows list_in[b * list_seg_rows ..][0 .. list_counts[2b])
+    const int32_t* list_in;
+    const int32_t* list_counts;
+    int64_t list_seg_rows;
     unsigned long long* prof;        // LSHKM_PHASE_TIMING builds only: per-phase wave cycles
 };
 
@@ -607,8 +613,9 @@ static_assert(fp_lds_bytes(FP_KMAX, true) <= 160 * 1024, "persistent LDS image e
 // MET = 1: cosine Lloyd (HASH = false): centroids are normalised in the prep
 // (score x.c/|c|, cnh = 0), the winner distance is exact.h's certified form.
 // MP: multi-pass (K > 256) form; the single-pass instantiation compiles without
-// the pass-state code.
-template <bool HASH, int MET = 0, bool MP = false>
+// the pass-state code. LIST: the rows are block b's segment of a row list (the
+// refinement of fused_hi_kernel's uncertified rows), not a range.
+template <bool HASH, int MET = 0, bool MP = false, bool LIST = false>
 __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
@@ -663,6 +670,10 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     const _Float16* my_l = lcl + col * FU_RS + 8 * h;
     const int ntile32 = Kpad >> 5;
     const int64_t ntiles = (a.N + 31) >> 5;
+    // LIST: this block's segment of the input list
+    const int32_t* lrows = LIST ? a.list_in + (int64_t)blockIdx.x * a.list_seg_rows : nullptr;
+    const int64_t lcnt = LIST ? (int64_t)a.list_counts[2 * blockIdx.x] : 0;
+    const int64_t ptile0 = LIST ? (int64_t)blockIdx.x * ((a.list_seg_rows + 31) >> 5) : 0;   // part slots
 
 #if WAVE_OFFSET
     // Waves w and w+4 share a SIMD; starting the second half of the block late
@@ -677,9 +688,17 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     if (wave >= FP_WAVES / 2) __builtin_amdgcn_s_setprio(YOUNG_PRIO);
 #endif
     PT_DECL
-    for (int64_t tile = (int64_t)blockIdx.x * FP_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FP_WAVES) {
-        const int64_t row = tile * 32 + col;
-        const bool valid = row < a.N;
+    const int64_t tbeg = LIST ? wave : (int64_t)blockIdx.x * FP_WAVES + wave;
+    const int64_t tend = LIST ? (lcnt + 31) >> 5 : ntiles;
+    const int64_t tstep = LIST ? FP_WAVES : (int64_t)gridDim.x * FP_WAVES;
+    for (int64_t tile = tbeg; tile < tend; tile += tstep) {
+        int64_t row = tile * 32 + col;
+        bool valid = row < a.N;
+        if (LIST) {
+            valid = row < lcnt;
+            row = lrows[valid ? row : lcnt - 1];
+        }
+        const int64_t ptile = ptile0 + tile;      // pass-state slot
 
         // ---- point -> registers and the split B operand
         float xf[64];
@@ -829,7 +848,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
         int t1 = 0;
         if (MP && !a.pass_first) {
-            const float4 st = a.part[tile * 64 + lane];
+            const float4 st = a.part[ptile * 64 + lane];
             m1 = st.x; m2 = st.y; t1 = __float_as_int(st.z);
         }
         const int tg0 = MP ? a.t0 : 0;        // global index of this slice's first tile
@@ -887,7 +906,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 #endif
 #endif
         if (MP && !a.pass_last) {             // more slices to come: carry the state
-            a.part[tile * 64 + lane] = make_float4(m1, m2, __int_as_float(t1), 0.f);
+            a.part[ptile * 64 + lane] = make_float4(m1, m2, __int_as_float(t1), 0.f);
             continue;
         }
         const uint32_t l1 = __float_as_uint(m1) & 0xFu;
@@ -930,7 +949,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 if (fix) hfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
             }
         } else {
-#if FP_KEEP_X
+#if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
+        if (h == 1 && valid && cert) { a.assign[row] = I1; a.dist[row] = 0.0; }
+#elif FP_KEEP_X
         {
             // exact row still in registers (B-operand layout): lane half h owns
             // dims 16s+8h..+7; only the winner's fp64 row is loaded
@@ -1047,6 +1068,332 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     }
 }
 
+// ------------------------------------------------------------ hi-only form
+// Euclidean Lloyd (+ hashing) with ONE f16 MFMA per centroid product: the
+// score is t~ = acc(-|c|^2/2 + sum_j xh_j ch_j), the accumulator initialised
+// with the f32 -|c|^2/2 (no epilogue add), ch = f16(f32(c)), xh = f16(x).
+// Bound (rigorous, |x_j| <= 2^15, c in range): with xr = x - xh (exact in f32)
+// and cr = c - ch,
+//   |t~ - t| <= |xh||cr| + |xr||c| + 2^-24|cn| + A (|cn| + |xh||ch|),
+//   A = 130 2^-23 (<= 129 round-toward-zero additions of partial sums bounded
+//   by |cn| + sum|xh_j ch_j|), plus the terms of the 3-product form for the
+//   reference's own fp64 roundings (2^-41 (|x|^2 + |c|^2)) and the packed tile
+//   index (2^-18 (|x||c| + |cn|)); |xr| is summed per row, the centroid
+//   maxima come from the prep (cbound[3..6]). A point is certified iff
+//   M2 < M1 - 2E; the others (~3% of N(0,1) rows at K = 256) are listed for the
+//   3-product form (fused_persistent_kernel<..., LIST>), which certifies all but
+//   ~1% of those and lists the rest for the exact pass.
+// One third of the MFMA work of the 3-product form, and only the hi image of
+// the centroids in LDS: up to 512 centroids per pass (K = 1024: 2 passes).
+constexpr int FH_KMAX = 512;
+__host__ __device__ constexpr int fh_lds_bytes(int Kpad, bool hash) {
+    return 16 + Kpad * FU_RS * 2 + Kpad * 4 + (hash ? 2 * 32 * FU_RS * 2 + FP_HC_BYTES : 0);
+}
+static_assert(fh_lds_bytes(FH_KMAX, true) <= 160 * 1024, "hi-only LDS image exceeds 160 KiB");
+constexpr double FH_A = 130.0 * 0x1p-23;
+
+// hi = f16(x) of 8 values; r = x - f32(hi) (one v_fma_mix each, exact) summed
+// as r^2 into r2; LO: lo = f16(r) as well (the 3-product hash tile).
+template <bool LO>
+__device__ inline void split8_hi(const float* x, half8& hi, half8& lo, float2v& r2) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const half2v hp = {(_Float16)x[j], (_Float16)x[j + 1]};
+        hi[j] = hp.x;
+        hi[j + 1] = hp.y;
+        const float2v r = {resid_lo(x[j], hp), resid_hi(x[j + 1], hp)};
+        r2 = __builtin_elementwise_fma(r, r, r2);
+        if (LO) {
+            lo[j] = (_Float16)r.x;
+            lo[j + 1] = (_Float16)r.y;
+        }
+    }
+}
+
+template <bool HASH, bool MP = false>
+__global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int Kpad = a.Kpad;
+    int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows
+    _Float16* lch = reinterpret_cast<_Float16*>(smem + 16);
+    float* lcn = reinterpret_cast<float*>(lch + Kpad * FU_RS);
+    _Float16* lvh = reinterpret_cast<_Float16*>(lcn + Kpad);
+    _Float16* lvl = lvh + 32 * FU_RS;
+    float* lpn0 = reinterpret_cast<float*>(lvl + 32 * FU_RS);
+    float* lv10 = lpn0 + 32;
+    float* lt0 = lv10 + 32;
+    int32_t* lr0 = reinterpret_cast<int32_t*>(lt0 + 32);
+
+    for (int e = threadIdx.x; e < Kpad * 16; e += FP_THREADS) {
+        const int r = e >> 4, g = e & 15;
+        *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Ch + (size_t)r * FU_D + g * 8);
+    }
+    for (int e = threadIdx.x; e < Kpad; e += FP_THREADS) lcn[e] = a.cnh[e];
+    if (threadIdx.x < 2) lcount[threadIdx.x] = 0;
+    int32_t* ambig_seg = a.ambig + (int64_t)blockIdx.x * a.seg_rows;
+    unsigned long long* hfix_seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
+    if (HASH) {
+        for (int e = threadIdx.x; e < 32 * 16; e += FP_THREADS) {
+            const int r = e >> 4, g = e & 15;
+            *reinterpret_cast<float4*>(lvh + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vh + r * FU_D + g * 8);
+            *reinterpret_cast<float4*>(lvl + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vl + r * FU_D + g * 8);
+        }
+        if (threadIdx.x < 32) {
+            const int f = threadIdx.x;
+            const bool on = f < a.LK;
+            const double iwu = (double)(1.0f / a.w) * (1.0 + 0x1p-20);
+            lpn0[f] = on ? (float)((FU_A1H * a.pnorm[f] * (1.0 + 0x1p-20) + FU_A2 * FU_SQRT_D) * iwu * (1.0 + 0x1p-18)) : 0.f;
+            lv10[f] = on ? (float)((FU_A2 * a.v1[f] * (1.0 + 0x1p-20) + (0x1p-40 + 0x1p-23) * fabs((double)a.tv[f])) *
+                                   iwu * (1.0 + 0x1p-18)) : 0.f;
+            lt0[f] = on ? a.tv[f] : 0.f;
+            lr0[f] = on ? a.rv[f] : 0;
+        }
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = lane & 31, h = lane >> 5;
+    const float cmaxf = a.cbound[3], crf = a.cbound[4], chf = a.cbound[5], cnf = a.cbound[6];
+    const bool c_ok = __float_as_uint(a.cbound[2]) == 0u;
+    const _Float16* my_h = lch + col * FU_RS + 8 * h;
+    const int ntile32 = Kpad >> 5;
+    const int64_t ntiles = (a.N + 31) >> 5;
+    // point-independent part of the bound
+    const double Ec = (0x1p-24 + FH_A) * (double)cnf + 0x1p-41 * (double)cmaxf * (double)cmaxf + 0x1p-18 * (double)cnf;
+
+    for (int64_t tile = (int64_t)blockIdx.x * FP_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FP_WAVES) {
+        const int64_t row = tile * 32 + col;
+        const bool valid = row < a.N;
+        float xf[64];
+        {
+            const float* xr = a.X + (valid ? row : a.N - 1) * FU_D + 8 * h;
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
+                const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
+                xf[8 * s + 0] = p0.x; xf[8 * s + 1] = p0.y; xf[8 * s + 2] = p0.z; xf[8 * s + 3] = p0.w;
+                xf[8 * s + 4] = p1.x; xf[8 * s + 5] = p1.y; xf[8 * s + 6] = p1.z; xf[8 * s + 7] = p1.w;
+            }
+        }
+        half8 bh[8], bl[8];
+        float2v n2a = {0.f, 0.f}, n2b = {0.f, 0.f}, r2 = {0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            split8_hi<HASH>(xf + 8 * s, bh[s], bl[s], r2);
+#pragma unroll
+            for (int j = 0; j < 8; j += 4) {
+                const float2v u = {xf[8 * s + j], xf[8 * s + j + 1]}, v = {xf[8 * s + j + 2], xf[8 * s + j + 3]};
+                n2a = __builtin_elementwise_fma(u, u, n2a);
+                n2b = __builtin_elementwise_fma(v, v, n2b);
+            }
+        }
+        float xn2f = (n2a.x + n2a.y) + (n2b.x + n2b.y);
+        float xr2f = r2.x + r2.y;
+        xn2f += __shfl_xor(xn2f, 32);
+        xr2f += __shfl_xor(xr2f, 32);
+        // f32 sums of squares inflated by 2^-16 (> d 2^-24): upper bounds
+        const double xn2 = (double)xn2f * (1.0 + 0x1p-16);
+        const double nx = sqrt(xn2);
+        const double nxr = sqrt((double)xr2f * (1.0 + 0x1p-16)) + 0x1p-100;
+        const double nxh = nx + nxr;                            // |xh| <= |x| + |xr|
+        const bool x_ok = xn2f <= FU_RANGE * FU_RANGE;
+
+        if (HASH && (!MP || a.pass_first)) {
+            uint32_t fmask = 0;
+            float acc_hi[16];
+            {
+                const _Float16* vh_row = lvh + col * FU_RS + 8 * h;
+                const _Float16* vl_row = lvl + col * FU_RS + 8 * h;
+                floatx16 acc_lo, tot;
+#pragma unroll
+                for (int s = 0; s < 8; s++) {
+                    const half8 ah = *reinterpret_cast<const half8*>(vh_row + 16 * s);
+                    const half8 al = *reinterpret_cast<const half8*>(vl_row + 16 * s);
+                    const floatx16 z = {};
+                    const floatx16 acc_s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], z, 0, 0, 0);
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], s ? acc_lo : z, 0, 0, 0);
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc_lo, 0, 0, 0);
+                    if (s == 0) {
+                        tot = acc_s;
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 16; r += 2) {
+                            const float2v t2 = {tot[r], tot[r + 1]}, a2 = {acc_s[r], acc_s[r + 1]};
+                            const float2v u2 = t2 + a2;
+                            tot[r] = u2.x;
+                            tot[r + 1] = u2.y;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc_hi[r] = tot[r] + acc_lo[r];
+            }
+            // the floor certificate of fused_persistent_kernel (same bound)
+            const float iw = 1.0f / a.w;
+            const float nxf = (float)nx * (1.f + 0x1p-20f);
+            constexpr float G = (0x1p-22f + 0x1p-20f) * (1.f + 0x1p-18f);
+            int hc = 0;
+            asm volatile("" : "+v"(hc));
+            const float* lt = lt0 + hc;
+            const float* lP = lpn0 + hc;
+            const float* lQ = lv10 + hc;
+            const int32_t* lr = lr0 + hc;
+            if (!x_ok) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int l = 2 * g + h;
+                if (l >= a.L || !valid) continue;
+                int32_t hv[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int f = 4 * l + q;
+                    const float u = acc_hi[4 * g + q] + lt[f];
+                    const float y = u * iw;
+                    const float B = fmaf(fabsf(y), G, fmaf(nxf, lP[f], lQ[f]));
+                    const float lo = floorf(y - B), hi = floorf(y + B);
+                    hv[q] = (int32_t)lo;
+                    if (lo != hi) fmask |= 1u << f;
+                }
+                const int64_t o = row * a.L + l;
+                if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
+                uint32_t hn = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) hn += phi_term_small(hv[q], lr[4 * l + q]);
+                const uint32_t ph = phi_final(hn);
+                if (a.phi) a.phi[o] = (int32_t)ph;
+                if (a.bucket) a.bucket[o] = bucket_fast(ph, a.bdiv);
+            }
+            fmask |= __shfl_xor(fmask, 32);
+            const unsigned long long fb = __ballot(fmask != 0u && h == 1);
+            if (fb) {
+                const int leader = __builtin_ctzll(fb);
+                int base = 0;
+                if (lane == leader) base = atomicAdd(lcount + 1, __popcll(fb));
+                base = __shfl(base, leader);
+                if (fmask != 0u && h == 1)
+                    hfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = ((unsigned long long)row << 32) | fmask;
+            }
+        }
+
+        // ---- centroid tiles: 8 MFMAs each, accumulator initialised with -|c|^2/2
+        float m1 = -__builtin_inff(), m2 = -__builtin_inff();
+        int t1 = 0;
+        if (MP && !a.pass_first) {
+            const float4 st = a.part[tile * 64 + lane];
+            m1 = st.x; m2 = st.y; t1 = __float_as_int(st.z);
+        }
+        const int tg0 = MP ? a.t0 : 0;
+#if MFMA_PRIO
+        __builtin_amdgcn_s_setprio(MFMA_PRIO);
+#endif
+#pragma unroll TILE_UNROLL
+        for (int t = 0; t < ntile32; t++) {
+            const float m1_prev = m1;
+            floatx16 acc;
+            const float* cn_t = lcn + t * 32 + 4 * h;     // D rows 8g + 4h + q of registers 4g + q
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const float4 cn = *reinterpret_cast<const float4*>(cn_t + 8 * g);
+                acc[4 * g] = cn.x; acc[4 * g + 1] = cn.y; acc[4 * g + 2] = cn.z; acc[4 * g + 3] = cn.w;
+            }
+            const _Float16* arow = my_h + t * 32 * FU_RS;
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                const half8 ah = *reinterpret_cast<const half8*>(arow + 16 * s);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+            }
+            float sv[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) sv[r] = acc[r];
+            tile_epilogue(sv, m1, m2);
+            t1 = m1 != m1_prev ? t + tg0 : t1;
+        }
+#if MFMA_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+        if (MP && !a.pass_last) {
+            a.part[tile * 64 + lane] = make_float4(m1, m2, __int_as_float(t1), 0.f);
+            continue;
+        }
+        const uint32_t l1 = __float_as_uint(m1) & 0xFu;
+        const int i1 = t1 * 32 + 8 * (int)(l1 >> 2) + 4 * h + (int)(l1 & 3u);
+        const float om1 = __shfl_xor(m1, 32), om2 = __shfl_xor(m2, 32);
+        const int oi1 = __shfl_xor(i1, 32);
+        const float M2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
+        const int I1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
+        const float M1 = fmaxf(m1, om1);
+        const double E = (nxh * (double)crf + nxr * (double)cmaxf + FH_A * nxh * (double)chf + 0x1p-41 * xn2 +
+                          0x1p-18 * nx * (double)cmaxf + Ec) * (1.0 + 0x1p-20) + 1e-30;
+        const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
+
+#if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
+        if (h == 1 && valid && cert) { a.assign[row] = I1; a.dist[row] = 0.0; }
+#else
+        {
+            // winner distance in reference order (fused_persistent_kernel's chain)
+            const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
+            double acc = 0.0;
+            double2 cbuf[CHAIN_PF][4];
+#pragma unroll
+            for (int s = 0; s < CHAIN_PF; s++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) cbuf[s][j] = *reinterpret_cast<const double2*>(crow + 16 * s + 2 * j);
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                double sq[8];
+                double2 cur[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) cur[j] = cbuf[s % CHAIN_PF][j];
+                if (s + CHAIN_PF < 8) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        cbuf[s % CHAIN_PF][j] = *reinterpret_cast<const double2*>(crow + 16 * (s + CHAIN_PF) + 2 * j);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const double2 cc = cur[j];
+                    const double d0 = __dsub_rn((double)xf[8 * s + 2 * j], cc.x);
+                    const double d1 = __dsub_rn((double)xf[8 * s + 2 * j + 1], cc.y);
+                    sq[2 * j] = __dmul_rn(d0, d0);
+                    sq[2 * j + 1] = __dmul_rn(d1, d1);
+                }
+                if (h == 0) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
+                }
+                const double from0 = swap_halves(acc, h);
+                if (h == 1) {
+                    acc = from0;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
+                }
+                const double from1 = swap_halves(acc, h);
+                if (h == 0) acc = from1;
+            }
+            if (h == 1 && valid && cert) {
+                a.assign[row] = I1;
+                a.dist[row] = sqrt(acc);
+            }
+        }
+#endif
+        const bool amb = valid && !cert;
+        const unsigned long long amask = __ballot(amb && h == 1);
+        if (amb && h == 1) {
+            int base = 0;
+            const int leader = __builtin_ctzll(amask);
+            if (lane == leader) base = atomicAdd(lcount, __popcll(amask));
+            base = __shfl(base, leader);
+            ambig_seg[base + __popcll(amask & ((1ull << lane) - 1ull))] = (int32_t)row;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? a.pass_last != 0 : (HASH && a.pass_first)))) {
+        const int c = lcount[threadIdx.x];
+        a.seg_counts[2 * blockIdx.x + threadIdx.x] = c;
+        if (c) atomicAdd(threadIdx.x == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
+    }
+}
+
 // Rows listed by the persistent form with an uncertified floor: fix-up pass.
 constexpr int HF_WAVES = 4;
 constexpr int HF_SPLIT = 4;                           // blocks per list segment
@@ -1155,6 +1502,7 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
             nbv[c] = b;
         }
     }
+    double rr = 0.0, hh = 0.0;           // |c - ch|^2, |ch|^2 (the hi-only scores' bound)
     for (int j = lane; j < FU_D; j += 64) {
         const double v = c < K ? C[(size_t)c * FU_D + j] * scale : 0.0;
         const float f = (float)v;
@@ -1163,11 +1511,16 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
         Cl[(size_t)c * FU_D + j] = (_Float16)(f - (float)hv);
         s2 = fma(v, v, s2);
         s1 += fabs(v);
+        const double r = v - (double)hv;     // exact in fp64 for |v| <= 2^15
+        rr = fma(r, r, rr);
+        hh = fma((double)hv, (double)hv, hh);
         bad |= !(fabs(v) <= (double)FU_RANGE);
     }
     for (int off = 32; off >= 1; off >>= 1) {
         s2 += __shfl_xor(s2, off);
         s1 += __shfl_xor(s1, off);
+        rr += __shfl_xor(rr, off);
+        hh += __shfl_xor(hh, off);
     }
     const unsigned long long anybad = __ballot(bad);
     if (lane != 0) return;
@@ -1184,6 +1537,10 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     atomicMax(cb + 0, __float_as_uint(ec));     // positive floats order like their bits
     atomicMax(cb + 1, __float_as_uint(eb));
     atomicMax(cb + 3, __float_as_uint((float)(nc * up)));   // max |c|, rounded up
+    // hi-only scores (fused_hi_kernel): max |c - ch|, max |ch|, max |cn|, rounded up
+    atomicMax(cb + 4, __float_as_uint((float)(sqrt(rr) * (1.0 + 0x1p-30) * up)));
+    atomicMax(cb + 5, __float_as_uint((float)(sqrt(hh) * (1.0 + 0x1p-30) * up)));
+    atomicMax(cb + 6, __float_as_uint((float)(metric == 1 ? 0.0 : 0.5 * s2 * up)));
     if (anybad) atomicOr(cb + 2, 1u);
 }
 
@@ -1193,7 +1550,7 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
         set_error("launch_fused_prep: cosine needs the norm array");
         return -1;
     }
-    (void)hipMemsetAsync(cbound, 0, 16, s);
+    (void)hipMemsetAsync(cbound, 0, 32, s);
     hipLaunchKernelGGL(fused_centroid_prep, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, Ch, Cl, cnh,
                        reinterpret_cast<unsigned int*>(cbound), metric, nbv);
     return kstatus("fused_centroid_prep");
@@ -1233,6 +1590,11 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     const bool chunked = force && !strcmp(force, "chunked");
     const int npass = (f.Kpad + FP_KMAX - 1) / FP_KMAX;
     const bool multi_ok = npass == 1 || (f.part && f.part_bytes >= ((f.N + 31) / 32) * 64 * 16);
+    // LIST refinement pass state: one slot per (segment, tile) of the list
+    if (f.hi && npass > 1 && f.part_bytes < ((f.list_cap + 31) / 32 + FUSED_MAX_SEGS) * 64 * 16) {
+        set_error("launch_fused: pass-state buffer too small for the refinement");
+        return -1;
+    }
     if (f.metric == 1 && (hash || chunked || !multi_ok || !f.nbv || !f.hfix || !f.hfix_count)) {
         set_error("launch_fused: cosine runs the persistent form only (no hashing, fix-up list, pass state)");
         return -1;
@@ -1267,6 +1629,51 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         }
         if (f.metric == 1) { a.hfix = f.hfix; a.hfix_count = f.hfix_count; }
         a.part = reinterpret_cast<float4*>(f.part);
+        a.list_in = nullptr; a.list_counts = nullptr; a.list_seg_rows = 0;
+        f.final_list = f.ambig;
+        f.final_counts = f.seg_counts;
+        if (f.hi && f.metric == 0) {
+            // hi-only passes (512 centroids each), the hash fix-up, then the
+            // 3-product LIST form over the rows they listed (256 per pass)
+            if (!f.list2 || !f.seg_counts2 || !f.refined || (f.Kpad > FH_KMAX && !f.part)) {
+                set_error("launch_fused: the hi-only form needs the second list and its counters");
+                return -1;
+            }
+            const int np1 = (f.Kpad + FH_KMAX - 1) / FH_KMAX;
+            a.ambig_count = f.refined;
+            for (int p = 0; p < np1; p++) {
+                const int c0 = p * FH_KMAX;
+                a.Ch = f.Ch + (size_t)c0 * FU_D; a.cnh = f.cnh + c0;
+                a.Kpad = std::min(FH_KMAX, f.Kpad - c0);
+                a.t0 = c0 / 32; a.pass_first = p == 0; a.pass_last = p == np1 - 1;
+                const size_t lh = (size_t)fh_lds_bytes(a.Kpad, hash && p == 0);
+                if (np1 == 1) {
+                    if (hash) hipLaunchKernelGGL((fused_hi_kernel<true>), grid, block, lh, s, a);
+                    else hipLaunchKernelGGL((fused_hi_kernel<false>), grid, block, lh, s, a);
+                } else {
+                    if (hash && p == 0) hipLaunchKernelGGL((fused_hi_kernel<true, true>), grid, block, lh, s, a);
+                    else hipLaunchKernelGGL((fused_hi_kernel<false, true>), grid, block, lh, s, a);
+                }
+            }
+            if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
+            FusedArgs r = a;
+            r.list_in = f.ambig; r.list_counts = f.seg_counts; r.list_seg_rows = a.seg_rows;
+            r.ambig = f.list2; r.seg_counts = f.seg_counts2; r.ambig_count = f.ambig_count;
+            r.hfix = f.hfix; r.hfix_count = f.hfix_count;
+            r.Cl = f.Cl;
+            r.tuples = nullptr; r.phi = nullptr; r.bucket = nullptr;
+            for (int p = 0; p < npass; p++) {
+                const int c0 = p * FP_KMAX;
+                r.Ch = f.Ch + (size_t)c0 * FU_D; r.Cl = f.Cl + (size_t)c0 * FU_D; r.cnh = f.cnh + c0;
+                r.Kpad = std::min(FP_KMAX, f.Kpad - c0);
+                r.t0 = c0 / 32; r.pass_first = p == 0; r.pass_last = p == npass - 1;
+                if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 0, false, true>), grid, block, lds_nohash, s, r);
+                else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true, true>), grid, block, lds_nohash, s, r);
+            }
+            f.final_list = f.list2;
+            f.final_counts = f.seg_counts2;
+            return kstatus("fused_hi_kernel");
+        }
         // one launch per 256-centroid slice (the hashing rides on the first)
         for (int p = 0; p < npass; p++) {
             const int c0 = p * FP_KMAX;

@@ -198,6 +198,16 @@ struct FusedLaunch {
     // lane's (best, runner-up, tile) in part[] (32 B per point)
     void* part = nullptr;
     int64_t part_bytes = 0;
+    // hi-only form (euclidean): fused_hi_kernel, then the 3-product LIST form on
+    // its uncertified rows (list2 / seg_counts2: [list_cap] / [2 * seg_cap]);
+    // out: refined = rows the hi-only pass left to the 3-product form (device)
+    bool hi = false;
+    int32_t* list2 = nullptr;
+    int32_t* seg_counts2 = nullptr;
+    unsigned long long* refined = nullptr;
+    // out: the list of rows still uncertified for the exact pass
+    const int32_t* final_list = nullptr;
+    const int32_t* final_counts = nullptr;
 };
 constexpr int64_t FUSED_PART_BYTES_PER_ROW = 32;
 // List capacity the persistent form may need beyond N entries (grid <= 1024 blocks).

@@ -77,7 +77,8 @@ int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t
 /* Counters: 0 = hash values resolved by the exact soft-x87 path,
  * 1 = points whose argmin needed the exact all-centroid pass,
  * 2 = k-means++ prefix-sum chunks walked, 3 = of which summed element by element,
- * 4 = cosine Lloyd winner distances the certified fast form declined (soft-x87 chain). */
+ * 4 = cosine Lloyd winner distances the certified fast form declined (soft-x87 chain),
+ * 5 = rows the hi-only fused pass (one f16 product per score) left to the 3-product form. */
 int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);
 int lshkm_reset_stats(lshkm_ctx ctx);
 /* HIP-event timing of the dominant kernel launch (the fused hash+assign kernel)
