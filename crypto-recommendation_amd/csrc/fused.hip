@@ -1166,7 +1166,11 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
         const bool valid = row < a.N;
         float xf[64];
         {
+#if defined(ABL_L2X)   // timing experiments only: every tile reads the same 4096 rows (L2 hits)
+            const float* xr = a.X + ((valid ? row : a.N - 1) & 4095) * FU_D + 8 * h;
+#else
             const float* xr = a.X + (valid ? row : a.N - 1) * FU_D + 8 * h;
+#endif
 #pragma unroll
             for (int s = 0; s < 8; s++) {
                 const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
