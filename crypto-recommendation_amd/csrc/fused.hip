@@ -1110,8 +1110,19 @@ __device__ inline void split8_hi(const float* x, half8& hi, half8& lo, float2v& 
     }
 }
 
+// Waves per block of the hi-only form (one block per CU). Measured (fused pass,
+// N = 10M, K = 256): 8 waves (<= 256 VGPRs, no spills) 2.37 ms; 12 waves (168
+// VGPRs: ~30 spilled loop invariants) 2.74 ms; 12 waves with the row re-read
+// for the chain instead of kept (one lane per row over two tiles) 3.7 ms -- the
+// lane-per-row re-reads of the row and of the winner's fp64 row thrash L1.
+#ifndef FH_WAVES_SET
+#define FH_WAVES_SET 8
+#endif
+constexpr int FH_WAVES = FH_WAVES_SET;
+constexpr int FH_THREADS = 64 * FH_WAVES;
+
 template <bool HASH, bool MP = false>
-__global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
+__global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
     int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows
@@ -1124,16 +1135,16 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
     float* lt0 = lv10 + 32;
     int32_t* lr0 = reinterpret_cast<int32_t*>(lt0 + 32);
 
-    for (int e = threadIdx.x; e < Kpad * 16; e += FP_THREADS) {
+    for (int e = threadIdx.x; e < Kpad * 16; e += FH_THREADS) {
         const int r = e >> 4, g = e & 15;
         *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Ch + (size_t)r * FU_D + g * 8);
     }
-    for (int e = threadIdx.x; e < Kpad; e += FP_THREADS) lcn[e] = a.cnh[e];
+    for (int e = threadIdx.x; e < Kpad; e += FH_THREADS) lcn[e] = a.cnh[e];
     if (threadIdx.x < 2) lcount[threadIdx.x] = 0;
     int32_t* ambig_seg = a.ambig + (int64_t)blockIdx.x * a.seg_rows;
     unsigned long long* hfix_seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
     if (HASH) {
-        for (int e = threadIdx.x; e < 32 * 16; e += FP_THREADS) {
+        for (int e = threadIdx.x; e < 32 * 16; e += FH_THREADS) {
             const int r = e >> 4, g = e & 15;
             *reinterpret_cast<float4*>(lvh + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vh + r * FU_D + g * 8);
             *reinterpret_cast<float4*>(lvl + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Vl + r * FU_D + g * 8);
@@ -1161,7 +1172,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
     // point-independent part of the bound
     const double Ec = (0x1p-24 + FH_A) * (double)cnf + 0x1p-41 * (double)cmaxf * (double)cmaxf + 0x1p-18 * (double)cnf;
 
-    for (int64_t tile = (int64_t)blockIdx.x * FP_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FP_WAVES) {
+    for (int64_t tile = (int64_t)blockIdx.x * FH_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FH_WAVES) {
         const int64_t row = tile * 32 + col;
         const bool valid = row < a.N;
         float xf[64];
@@ -1179,44 +1190,68 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
                 xf[8 * s + 4] = p1.x; xf[8 * s + 5] = p1.y; xf[8 * s + 6] = p1.z; xf[8 * s + 7] = p1.w;
             }
         }
-        half8 bh[8], bl[8];
+        half8 bh[8];
         float2v n2a = {0.f, 0.f}, n2b = {0.f, 0.f}, r2 = {0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            split8_hi<HASH>(xf + 8 * s, bh[s], bl[s], r2);
+        // hi part of 8 values (LO: and the lo part), |x|^2 and |x - xh|^2 partial sums
+        auto split_step = [&](int s, half8& lo, auto lo_tag) {
+            split8_hi<decltype(lo_tag)::value>(xf + 8 * s, bh[s], lo, r2);
 #pragma unroll
             for (int j = 0; j < 8; j += 4) {
                 const float2v u = {xf[8 * s + j], xf[8 * s + j + 1]}, v = {xf[8 * s + j + 2], xf[8 * s + j + 3]};
                 n2a = __builtin_elementwise_fma(u, u, n2a);
                 n2b = __builtin_elementwise_fma(v, v, n2b);
             }
+        };
+        double xn2, nx, nxr, nxh;
+        bool x_ok;
+        auto finish_norms = [&]() {
+            float xn2f = (n2a.x + n2a.y) + (n2b.x + n2b.y);
+            float xr2f = r2.x + r2.y;
+            xn2f += __shfl_xor(xn2f, 32);
+            xr2f += __shfl_xor(xr2f, 32);
+            // f32 sums of squares inflated by 2^-16 (> d 2^-24): upper bounds
+            xn2 = (double)xn2f * (1.0 + 0x1p-16);
+            nx = sqrt(xn2);
+            nxr = sqrt((double)xr2f * (1.0 + 0x1p-16)) + 0x1p-100;
+            nxh = nx + nxr;                                     // |xh| <= |x| + |xr|
+            x_ok = xn2f <= FU_RANGE * FU_RANGE;
+        };
+#if defined(ABL_NOHASH)   // timing experiments only: no hash tile
+        constexpr bool hash_here = false;
+#else
+        const bool hash_here = HASH;          // <HASH, MP>: the first pass only
+#endif
+        if (!hash_here) {
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                half8 unused;
+                split_step(s, unused, std::false_type{});
+            }
+            finish_norms();
         }
-        float xn2f = (n2a.x + n2a.y) + (n2b.x + n2b.y);
-        float xr2f = r2.x + r2.y;
-        xn2f += __shfl_xor(xn2f, 32);
-        xr2f += __shfl_xor(xr2f, 32);
-        // f32 sums of squares inflated by 2^-16 (> d 2^-24): upper bounds
-        const double xn2 = (double)xn2f * (1.0 + 0x1p-16);
-        const double nx = sqrt(xn2);
-        const double nxr = sqrt((double)xr2f * (1.0 + 0x1p-16)) + 0x1p-100;
-        const double nxh = nx + nxr;                            // |xh| <= |x| + |xr|
-        const bool x_ok = xn2f <= FU_RANGE * FU_RANGE;
 
-        if (HASH && (!MP || a.pass_first)) {
+        if (hash_here) {
             uint32_t fmask = 0;
             float acc_hi[16];
             {
                 const _Float16* vh_row = lvh + col * FU_RS + 8 * h;
                 const _Float16* vl_row = lvl + col * FU_RS + 8 * h;
-                floatx16 acc_lo, tot;
+                // per 16-dim step: the lo products first, then the hi products into
+                // the same accumulator (16 roundings relative to the step's sum of
+                // |terms|, the lo parts' own roundings ~2^-11 smaller), steps added
+                // in f32 (+7): 23 -> 24 roundings, still inside FU_A1H; one
+                // accumulator fewer than the separate lo chain (fits 168 VGPRs)
+                floatx16 tot;
 #pragma unroll
                 for (int s = 0; s < 8; s++) {
+                    half8 bls;
+                    split_step(s, bls, std::true_type{});
                     const half8 ah = *reinterpret_cast<const half8*>(vh_row + 16 * s);
                     const half8 al = *reinterpret_cast<const half8*>(vl_row + 16 * s);
                     const floatx16 z = {};
-                    const floatx16 acc_s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], z, 0, 0, 0);
-                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], s ? acc_lo : z, 0, 0, 0);
-                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc_lo, 0, 0, 0);
+                    floatx16 acc_s = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], z, 0, 0, 0);
+                    acc_s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bls, acc_s, 0, 0, 0);
+                    acc_s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc_s, 0, 0, 0);
                     if (s == 0) {
                         tot = acc_s;
                     } else {
@@ -1230,8 +1265,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < 16; r++) acc_hi[r] = tot[r] + acc_lo[r];
+                for (int r = 0; r < 16; r++) acc_hi[r] = tot[r];
             }
+            finish_norms();
             // the floor certificate of fused_persistent_kernel (same bound)
             const float iw = 1.0f / a.w;
             const float nxf = (float)nx * (1.f + 0x1p-20f);
@@ -1282,7 +1318,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
         // ---- centroid tiles: 8 MFMAs each, accumulator initialised with -|c|^2/2
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
         int t1 = 0;
-        if (MP && !a.pass_first) {
+        if (MP && !HASH && !a.pass_first) {
             const float4 st = a.part[tile * 64 + lane];
             m1 = st.x; m2 = st.y; t1 = __float_as_int(st.z);
         }
@@ -1290,8 +1326,13 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
 #if MFMA_PRIO
         __builtin_amdgcn_s_setprio(MFMA_PRIO);
 #endif
+#if defined(ABL_NOCTILE)   // timing experiments only: one centroid tile
+        const int ntile_run = 1;
+#else
+        const int ntile_run = ntile32;
+#endif
 #pragma unroll TILE_UNROLL
-        for (int t = 0; t < ntile32; t++) {
+        for (int t = 0; t < ntile_run; t++) {
             const float m1_prev = m1;
             floatx16 acc;
             const float* cn_t = lcn + t * 32 + 4 * h;     // D rows 8g + 4h + q of registers 4g + q
@@ -1315,7 +1356,8 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
 #if MFMA_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
-        if (MP && !a.pass_last) {
+        // <HASH, MP> launches only the first of several passes (never the last)
+        if (MP && (HASH || !a.pass_last)) {
             a.part[tile * 64 + lane] = make_float4(m1, m2, __int_as_float(t1), 0.f);
             continue;
         }
@@ -1330,11 +1372,21 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
                           0x1p-18 * nx * (double)cmaxf + Ec) * (1.0 + 0x1p-20) + 1e-30;
         const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
 
+        const bool amb = valid && !cert;
+        const unsigned long long amask = __ballot(amb && h == 1);
+        if (amb && h == 1) {
+            int base = 0;
+            const int leader = __builtin_ctzll(amask);
+            if (lane == leader) base = atomicAdd(lcount, __popcll(amask));
+            base = __shfl(base, leader);
+            ambig_seg[base + __popcll(amask & ((1ull << lane) - 1ull))] = (int32_t)row;
+        }
 #if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
         if (h == 1 && valid && cert) { a.assign[row] = I1; a.dist[row] = 0.0; }
 #else
         {
-            // winner distance in reference order (fused_persistent_kernel's chain)
+            // winner distance in reference order from the row kept in registers:
+            // the lane halves take turns on the chain, 8 dims each
             const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
             double acc = 0.0;
             double2 cbuf[CHAIN_PF][4];
@@ -1380,18 +1432,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
             }
         }
 #endif
-        const bool amb = valid && !cert;
-        const unsigned long long amask = __ballot(amb && h == 1);
-        if (amb && h == 1) {
-            int base = 0;
-            const int leader = __builtin_ctzll(amask);
-            if (lane == leader) base = atomicAdd(lcount, __popcll(amask));
-            base = __shfl(base, leader);
-            ambig_seg[base + __popcll(amask & ((1ull << lane) - 1ull))] = (int32_t)row;
-        }
     }
     __syncthreads();
-    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? a.pass_last != 0 : (HASH && a.pass_first)))) {
+    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? (!HASH && a.pass_last != 0) : (HASH && a.pass_first)))) {
         const int c = lcount[threadIdx.x];
         a.seg_counts[2 * blockIdx.x + threadIdx.x] = c;
         if (c) atomicAdd(threadIdx.x == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
@@ -1620,6 +1663,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         const size_t lds_nohash = (size_t)fp_lds_bytes(kslice, false);
         // list segments: block b's tiles hold at most FP_WAVES * 32 * ceil(tiles / (grid * FP_WAVES)) rows
         a.seg_rows = (int64_t)FP_WAVES * 32 * ((ntiles + (int64_t)nblk * FP_WAVES - 1) / ((int64_t)nblk * FP_WAVES));
+        // the hi-only form strides by FH_WAVES tiles per block
+        a.seg_rows = std::max<int64_t>(a.seg_rows, (int64_t)FH_WAVES * 32 * ((ntiles + (int64_t)nblk * FH_WAVES - 1) /
+                                                                              ((int64_t)nblk * FH_WAVES)));
         a.seg_counts = f.seg_counts;
         if (!f.seg_counts || f.seg_cap < nblk || (int64_t)nblk * a.seg_rows > f.list_cap) {
             set_error("launch_fused: list workspace too small");
@@ -1651,12 +1697,13 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 a.Kpad = std::min(FH_KMAX, f.Kpad - c0);
                 a.t0 = c0 / 32; a.pass_first = p == 0; a.pass_last = p == np1 - 1;
                 const size_t lh = (size_t)fh_lds_bytes(a.Kpad, hash && p == 0);
+                const dim3 hblock(FH_THREADS);
                 if (np1 == 1) {
-                    if (hash) hipLaunchKernelGGL((fused_hi_kernel<true>), grid, block, lh, s, a);
-                    else hipLaunchKernelGGL((fused_hi_kernel<false>), grid, block, lh, s, a);
+                    if (hash) hipLaunchKernelGGL((fused_hi_kernel<true>), grid, hblock, lh, s, a);
+                    else hipLaunchKernelGGL((fused_hi_kernel<false>), grid, hblock, lh, s, a);
                 } else {
-                    if (hash && p == 0) hipLaunchKernelGGL((fused_hi_kernel<true, true>), grid, block, lh, s, a);
-                    else hipLaunchKernelGGL((fused_hi_kernel<false, true>), grid, block, lh, s, a);
+                    if (hash && p == 0) hipLaunchKernelGGL((fused_hi_kernel<true, true>), grid, hblock, lh, s, a);
+                    else hipLaunchKernelGGL((fused_hi_kernel<false, true>), grid, hblock, lh, s, a);
                 }
             }
             if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
