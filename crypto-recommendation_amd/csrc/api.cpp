@@ -263,7 +263,7 @@ static int kmeans_pp_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, int K, int met
         std::uniform_real_distribution<double> unit(0.0, 1.0);
         canon[i] = unit(g);
     }
-    Buf ws, dch, dcanon;
+    Buf &ws = ctx->ws_call[0], &dch = ctx->ws_call[1], &dcanon = ctx->ws_call[2];
     int rc;
     if ((rc = ws.reserve(kmeans_pp_ws_bytes(N))) || (rc = dch.reserve(sizeof(int32_t) * K)) ||
         (rc = dcanon.reserve(sizeof(double) * K)))
@@ -333,21 +333,23 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
     LSHKM_HIP(hipMemcpyAsync(t_d.p, tt.data(), LK * 4, hipMemcpyHostToDevice, s));
     LSHKM_HIP(hipMemcpyAsync(pn_d.p, pn.data(), LK * 8, hipMemcpyHostToDevice, s));
     LSHKM_HIP(hipMemcpyAsync(r_d.p, rr.data(), LK * 4, hipMemcpyHostToDevice, s));
-    // split-f16 image for the fused hash+assign kernel
+    // split-f16 image for the fused hash+assign kernel (euclidean) and the
+    // MFMA hash (either metric; cosine splits the fp64 rows of R)
     fused_ok = metric == LSHKM_METRIC_EUCLIDEAN && d == 128 && LK <= 32;
+    mfma_ok = d == 128 && LK <= 32;
     std::vector<_Float16> vh, vl;
     std::vector<double> v1;
-    if (fused_ok) {
+    if (mfma_ok) {
         vh.assign(64 * 128, (_Float16)0.f);
         vl.assign(64 * 128, (_Float16)0.f);
         v1.assign(LK, 0.0);
         for (int f = 0; f < LK; f++) {
             long double s1 = 0.0L;
             for (int j = 0; j < 128; j++) {
-                const float v = V[(size_t)f * d + j];
+                const double v = metric == LSHKM_METRIC_EUCLIDEAN ? (double)V[(size_t)f * d + j] : R[(size_t)f * d + j];
                 const _Float16 hv = (_Float16)v;
                 vh[f * 128 + j] = hv;
-                vl[f * 128 + j] = (_Float16)(v - (float)hv);
+                vl[f * 128 + j] = (_Float16)(float)(v - (double)hv);   // v - hv is exact in fp64
                 s1 += fabsl((long double)v);
             }
             v1[f] = (double)s1 * (1.0 + 0x1p-40);
@@ -370,6 +372,17 @@ HashParams ProjTable::params(int64_t nb) const {
     p.t = (const float*)t_d.p;
     p.pnorm = (const double*)pn_d.p;
     p.r = (const int32_t*)r_d.p;
+    p.w = w;
+    p.d = d; p.L = L; p.k = k; p.LK = LK; p.LKpad = LKpad;
+    p.nb = nb;
+    return p;
+}
+
+HashMfmaParams ProjTable::mfma_params(int64_t nb) const {
+    HashMfmaParams p;
+    p.Vh = vh_d.as<_Float16>(); p.Vl = vl_d.as<_Float16>();
+    p.t = (const float*)t_d.p; p.pnorm = (const double*)pn_d.p; p.v1 = (const double*)v1_d.p;
+    p.r = (const int32_t*)r_d.p; p.PT = (const double*)PT_d.p;
     p.w = w;
     p.d = d; p.L = L; p.k = k; p.LK = LK; p.LKpad = LKpad;
     p.nb = nb;
@@ -420,9 +433,8 @@ static int lsh_hash_impl(lshkm_lsh lsh, Pts X, int64_t N, int32_t* tuples, int32
     lshkm_ctx ctx = lsh->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
     const int mode = lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE;
-    const int rc = launch_proj_hash(ctx->stream, mode, X, N, lsh->proj.params(lsh->nb),
-                                    mode == HM_LSH_EUCLID ? tuples : nullptr, phi, bucket,
-                                    (unsigned long long*)ctx->stats.p);
+    const int rc = hash_rows(ctx, mode, X, N, lsh->proj, lsh->nb, mode == HM_LSH_EUCLID ? tuples : nullptr, phi, bucket,
+                             nullptr);
     if (rc) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;
 }
@@ -488,10 +500,10 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
     const int path = assign_path(metric, d, K, X.f64);
     const bool fuse_hash = lsh && path == 0 && metric == LSHKM_METRIC_EUCLIDEAN && lsh->proj.fused_ok;
     int rc;
-    if (lsh && !fuse_hash && (rc = launch_proj_hash(s, lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE,
-                                                    X, N, lsh->proj.params(lsh->nb),
-                                                    lsh->metric == LSHKM_METRIC_EUCLIDEAN ? tuples : nullptr, phi, bucket,
-                                                    (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if (lsh && !fuse_hash && (rc = hash_rows(ctx, lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE,
+                                             X, N, lsh->proj, lsh->nb,
+                                             lsh->metric == LSHKM_METRIC_EUCLIDEAN ? tuples : nullptr, phi, bucket,
+                                             nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
     if (path == 0) {
         const int Kpad = (K + 63) / 64 * 64;
         const bool cosine = metric != LSHKM_METRIC_EUCLIDEAN;

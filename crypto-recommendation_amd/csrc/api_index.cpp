@@ -14,6 +14,35 @@
 
 using namespace lshkm;
 
+// Hashing of a batch: the split-f16 MFMA kernel where it applies (fp32 rows,
+// d = 128, L*k <= 32), else the fp64 kernel (hash.hip). mm (cube euclidean):
+// the h range, into a pair the caller pre-set. LSHKM_HASH_PATH=fp64 forces the
+// fp64 kernel (tests compare the two).
+int lshkm::hash_rows(lshkm_ctx ctx, int mode, Pts X, int64_t N, const ProjTable& pj, int64_t nb, int32_t* out_h,
+                     int32_t* out_phi, int32_t* out_bucket, int32_t* mm) {
+    if (N <= 0) return 0;
+    const char* e = getenv("LSHKM_HASH_PATH");
+    const bool force64 = e && !strcmp(e, "fp64");
+    unsigned long long* stats = (unsigned long long*)ctx->stats.p;
+    int rc;
+    if (!X.f64 && pj.mfma_ok && !force64) {
+        const int64_t cap = N + FUSED_LIST_SLACK;
+        // the fix-up pass rebuilds a table's phi from the stored tuples
+        if (mode == HM_LSH_EUCLID && !out_h) {
+            if ((rc = ctx->ws_tuples.reserve((size_t)N * pj.LK * 4))) return rc;
+            out_h = ctx->ws_tuples.as<int32_t>();
+        }
+        if ((rc = ctx->ws_hfix.reserve((size_t)cap * 8)) || (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)))
+            return rc;
+        return launch_hash_mfma(ctx->stream, mode, X.f(), N, pj.mfma_params(nb), out_h, out_phi, out_bucket, mm,
+                                (unsigned long long*)ctx->ws_hfix.p, cap, (int32_t*)ctx->ws_seg.p, FUSED_MAX_SEGS * 2,
+                                stats);
+    }
+    if ((rc = launch_proj_hash(ctx->stream, mode, X, N, pj.params(nb), out_h, out_phi, out_bucket, stats))) return rc;
+    if (mode == HM_CUBE_EUCLID_H && mm) return launch_h_minmax(ctx->stream, out_h, N * pj.k, mm);
+    return 0;
+}
+
 namespace {
 
 // ctx->ws slot map
@@ -40,14 +69,16 @@ int d2h(lshkm_ctx ctx, void* dst, const void* src, size_t bytes) {
 }
 
 // Stable scatter of keys[i * kstride] in [0, nb) -> idx (row order kept) + row_ptr.
+// T bucket CSRs at once: table t's keys at keys + t (stride kstride), its
+// members at idx + t * N, its row pointers at row_ptr + t * (nb + 1).
 int build_csr(lshkm_ctx ctx, const int32_t* keys, int64_t kstride, int64_t N, int64_t nb, int32_t* idx,
-              int64_t* row_ptr) {
+              int64_t* row_ptr, int T = 1) {
     int rc;
-    if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(N, nb))) || (rc = reserve(ctx, WS_SKEYS, (size_t)N * 4)))
+    if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(N, nb, T))) || (rc = reserve(ctx, WS_SKEYS, (size_t)N * T * 4)))
         return rc;
-    if (N > 0 && (rc = stable_sort_by_key(ctx->stream, keys, kstride, nullptr, N, nb, slot<int32_t>(ctx, WS_SKEYS), idx,
-                                          ctx->ws[WS_SORT].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
-    if ((rc = launch_csr_bounds(ctx->stream, slot<int32_t>(ctx, WS_SKEYS), N, nb, row_ptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if (N > 0 && (rc = stable_sort_by_key_batched(ctx->stream, keys, kstride, 1, nullptr, 0, T, N, nb,
+                                                  slot<int32_t>(ctx, WS_SKEYS), idx, ctx->ws[WS_SORT].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if ((rc = launch_csr_bounds(ctx->stream, slot<int32_t>(ctx, WS_SKEYS), N, nb, row_ptr, T))) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;
 }
 
@@ -92,12 +123,10 @@ static int lsh_build_impl(lshkm_lsh lsh, Pts X, int64_t N) {
         return rc;
     if (lsh->metric == LSHKM_METRIC_EUCLIDEAN && (rc = lsh->tuples.reserve((size_t)std::max<int64_t>(N, 1) * L * k * 4))) return rc;
     const int mode = lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE;
-    if ((rc = launch_proj_hash(ctx->stream, mode, X, N, lsh->proj.params(nb),
-                               mode == HM_LSH_EUCLID ? lsh->tuples.as<int32_t>() : nullptr, nullptr,
-                               lsh->bucket.as<int32_t>(), (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
-    for (int l = 0; l < L; l++)
-        if ((rc = build_csr(ctx, lsh->bucket.as<int32_t>() + l, L, N, nb, lsh->idx.as<int32_t>() + (size_t)l * N,
-                            lsh->row_ptr.as<int64_t>() + (size_t)l * (nb + 1)))) return rc;
+    if ((rc = hash_rows(ctx, mode, X, N, lsh->proj, nb, mode == HM_LSH_EUCLID ? lsh->tuples.as<int32_t>() : nullptr,
+                        nullptr, lsh->bucket.as<int32_t>(), nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if ((rc = build_csr(ctx, lsh->bucket.as<int32_t>(), L, N, nb, lsh->idx.as<int32_t>(), lsh->row_ptr.as<int64_t>(), L)))
+        return rc;
     lsh->N = N;
     lsh->built = 1;
     return 0;
@@ -168,9 +197,9 @@ static int lsh_query_impl(lshkm_lsh lsh, Pts Q, int64_t nq, const int32_t* alias
         (rc = reserve(ctx, WS_SIZES, (size_t)pairs * 8)) || (rc = reserve(ctx, WS_COFF, (size_t)(pairs + 1) * 8)) ||
         (rc = reserve(ctx, WS_KCNT, (size_t)pairs * 8)) || (rc = reserve(ctx, WS_QSZ, (size_t)nq * 8)))
         return rc;
-    if (nq > 0 && (rc = launch_proj_hash(s, eu ? HM_LSH_EUCLID : HM_LSH_COSINE, Q, nq, lsh->proj.params(nb),
-                                         eu ? slot<int32_t>(ctx, WS_QTUP) : nullptr, nullptr, slot<int32_t>(ctx, WS_QBKT),
-                                         (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if (nq > 0 && (rc = hash_rows(ctx, eu ? HM_LSH_EUCLID : HM_LSH_COSINE, Q, nq, lsh->proj, nb,
+                                  eu ? slot<int32_t>(ctx, WS_QTUP) : nullptr, nullptr, slot<int32_t>(ctx, WS_QBKT),
+                                  nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
     auto run = [&](int phase, int32_t* out) {
         if (reserve_scan(ctx, scan_ws_bytes(nq * L + nq))) return LSHKM_ERR_NOMEM;
         return launch_lsh_query(s, slot<int32_t>(ctx, WS_QBKT), slot<int32_t>(ctx, WS_QTUP), alias, nq, L, k, nb,
@@ -271,11 +300,13 @@ static int cube_h_batch(lshkm_cube cube, Pts X, int64_t N, int32_t** h_out) {
     LSHKM_CHECK(N * k < (1ll << 31), LSHKM_ERR_UNSUPPORTED, "rows * k must be < 2^31");
     if ((rc = reserve(ctx, WS_H, (size_t)N * k * 4))) return rc;
     int32_t* h = slot<int32_t>(ctx, WS_H);
-    if ((rc = launch_proj_hash(s, HM_CUBE_EUCLID_H, X, N, cube->proj.params(1ll << k), h, nullptr, nullptr,
-                               (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
     const int32_t init_mm[2] = {0x7FFFFFFF, (int32_t)0x80000000};
-    LSHKM_HIP(hipMemcpyAsync(cube->mm.p, init_mm, 8, hipMemcpyHostToDevice, s));
-    if ((rc = launch_h_minmax(s, h, N * k, cube->mm.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if ((rc = ctx->pin_stage(8))) return rc;
+    std::memcpy(ctx->pinned, init_mm, 8);
+    LSHKM_HIP(hipMemcpyAsync(cube->mm.p, ctx->pinned, 8, hipMemcpyHostToDevice, s));
+    LSHKM_HIP(hipEventRecord(ctx->pinned_ev, s));
+    if ((rc = hash_rows(ctx, HM_CUBE_EUCLID_H, X, N, cube->proj, 1ll << k, h, nullptr, nullptr,
+                        cube->mm.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     int32_t mm[2];
     if ((rc = d2h(ctx, mm, cube->mm.p, 8))) return rc;
     if ((rc = cube_ensure_window(cube, mm[0], mm[1]))) return rc;
@@ -310,8 +341,10 @@ static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex
     int rc;
     if (N == 0) return 0;
     if (cube->metric == LSHKM_METRIC_COSINE) {
-        if ((rc = launch_proj_hash(s, HM_CUBE_COSINE, X, N, cube->proj.params(1ll << k), vertex, nullptr, nullptr,
-                                   (unsigned long long*)ctx->stats.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = hash_rows(ctx, HM_CUBE_COSINE, X, N, cube->proj, 1ll << k, vertex, nullptr, nullptr, nullptr))) {
+            LSHKM_LAUNCH_CHECK();
+            return rc;
+        }
         return 0;
     }
     int32_t* h = nullptr;

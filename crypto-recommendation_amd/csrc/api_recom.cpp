@@ -30,7 +30,8 @@ int lshkm_p_closest(lshkm_ctx ctx, const double* X, int64_t N, int d, const doub
     int rc;
     if ((rc = read_i64(ctx, cand_ptr + nq, &total))) return rc;
     LSHKM_CHECK(total >= 0 && (total == 0 || cand_idx), LSHKM_ERR_ARG, "bad candidate lists");
-    Buf xa, sim, key, pos, replay, count;
+    Buf &xa = ctx->ws_call[0], &sim = ctx->ws_call[1], &key = ctx->ws_call[2], &pos = ctx->ws_call[3],
+        &replay = ctx->ws_call[4], &count = ctx->ws_call[5];
     const size_t T = (size_t)(total > 0 ? total : 1);
     if ((rc = xa.reserve(sizeof(double) * N)) || (rc = sim.reserve(sizeof(double) * T)) ||
         (rc = key.reserve(sizeof(double) * T)) || (rc = pos.reserve(sizeof(int32_t) * T)) ||
@@ -43,7 +44,7 @@ int lshkm_p_closest(lshkm_ctx ctx, const double* X, int64_t N, int d, const doub
         (void)hipStreamSynchronize(ctx->stream);
         return rc;
     }
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the workspace is freed on return
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the workspace is reused by the next call
     return 0;
 }
 
@@ -59,7 +60,7 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X, const double* x_mean, int6
     int rc;
     if ((rc = read_i64(ctx, unk_ptr + nq, &total))) return rc;
     LSHKM_CHECK(total >= 0 && (total == 0 || unk_idx), LSHKM_ERR_ARG, "bad unknown-index lists");
-    Buf pred, pidx;
+    Buf &pred = ctx->ws_call[0], &pidx = ctx->ws_call[1];
     const size_t M = (size_t)(total > 0 ? total : 1);
     if ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M))) return rc;
     if ((rc = launch_rc_top_n(ctx->stream, X, x_mean, d, u_mean, nq, unk_ptr, unk_idx, nb_idx, nb_sim, nb_cnt, P, n_top,

@@ -44,7 +44,46 @@ __global__ void coin_first_kernel(const int32_t* __restrict__ h, int64_t N, int 
         const int64_t row = e / k;
         const int f = (int)(e - row * k);
         const int64_t off = (int64_t)f * hspan + (h[e] - hmin);
-        if (memo[off] < 0) atomicMin(first_row + off, (int32_t)row);
+        // read first: most (f, h) have an earlier row already (the atomics on the
+        // few popular entries otherwise serialise)
+        if (memo[off] < 0 && first_row[off] > (int32_t)row) atomicMin(first_row + off, (int32_t)row);
+    }
+}
+
+// Windows of at most CF_LDS_MAX entries: each block takes a contiguous run of
+// rows and keeps its first rows per (f, h) in LDS (entries that already have a
+// coin are marked), then merges them into first_row with one atomicMin per
+// touched entry, skipped where first_row already holds an earlier row. A fresh
+// 10M-row C4 cube: 34 ms -> well under 1 ms (every (row, f) hit one of ~400 hot
+// global entries).
+constexpr int CF_LDS_MAX = 12288;
+constexpr int32_t CF_SEEN = -1;
+__global__ __launch_bounds__(256) void coin_first_lds_kernel(const int32_t* __restrict__ h, int64_t N, int k,
+                                                             int32_t hmin, int32_t hspan, int64_t rows_per_block,
+                                                             const int32_t* __restrict__ memo,
+                                                             int32_t* __restrict__ first_row) {
+    extern __shared__ int32_t lmin[];
+    const int total = k * hspan;
+    for (int e = threadIdx.x; e < total; e += 256) lmin[e] = memo[e] < 0 ? NO_ROW : CF_SEEN;
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(N, r0 + rows_per_block);
+    // (row, f) of element e, advanced by 256 elements per step without a division
+    const int dq = 256 / k, dr = 256 - dq * k;
+    int64_t row = r0 + (int64_t)(threadIdx.x / k);
+    int f = (int)threadIdx.x - (int)(threadIdx.x / k) * k;
+    for (int64_t e = r0 * k + threadIdx.x; e < r1 * k; e += 256) {
+        const int off = f * hspan + (h[e] - hmin);
+        const int32_t cur = lmin[off];
+        if (cur != CF_SEEN && cur > (int32_t)row) atomicMin(lmin + off, (int32_t)row);
+        f += dr;
+        row += dq;
+        if (f >= k) { f -= k; row++; }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < total; e += 256) {
+        const int32_t v = lmin[e];
+        if (v != CF_SEEN && v != NO_ROW && v < first_row[e]) atomicMin(first_row + e, v);
     }
 }
 
@@ -63,31 +102,76 @@ __global__ void coin_collect_kernel(int32_t* __restrict__ first_row, int64_t tot
     }
 }
 
+// minstd_rand0: st = st * 16807 mod (2^31 - 1), reduced with 2^31 = 1 (mod M)
+// instead of a 64-bit division.
 __device__ inline uint32_t minstd_next(uint32_t& st) {
-    st = (uint32_t)(((uint64_t)st * 16807ull) % 2147483647ull);
+    const uint64_t x = (uint64_t)st * 16807ull;          // < 2^46
+    uint32_t r = (uint32_t)(x & 0x7FFFFFFFull) + (uint32_t)(x >> 31);
+    if (r >= 2147483647u) r -= 2147483647u;
+    st = r;
     return st;
 }
 
-// uniform_int_distribution<int>(1, 2) over minstd_rand0 (libstdc++-11 downscaling).
+// uniform_int_distribution<int>(1, 2) over minstd_rand0 (libstdc++-11 downscaling):
+// ret / scaling is 0 or 1 for ret < past.
 __device__ inline int coin_1_2(uint32_t& st) {
-    const uint64_t scaling = 2147483645ull / 2ull, past = 2ull * scaling;
-    uint64_t ret;
-    do { ret = (uint64_t)minstd_next(st) - 1ull; } while (ret >= past);
-    return (int)(ret / scaling) + 1;
+    constexpr uint32_t scaling = 2147483645u / 2u, past = 2u * scaling;
+    uint32_t ret;
+    do { ret = minstd_next(st) - 1u; } while (ret >= past);
+    return ret >= scaling ? 2 : 1;
 }
 
+__device__ inline uint32_t minstd_mulmod(uint32_t a, uint32_t b) {
+    const uint64_t x = (uint64_t)a * (uint64_t)b;        // < 2^62
+    uint64_t r = (x & 0x7FFFFFFFull) + (x >> 31);         // < 2^32, = x (mod 2^31 - 1)
+    r = (r & 0x7FFFFFFFull) + (r >> 31);
+    if (r >= 2147483647ull) r -= 2147483647ull;
+    return (uint32_t)r;
+}
+
+// The coins in draw order. The engine is an LCG, so draw i + 1 of a chunk is
+// state * 16807^(i+1) mod M: 64 lanes take 64 consecutive draws at once. A
+// draw that the uniform_int downscaling rejects (ret >= past: probability
+// 2^-30) would shift every later coin by one engine step; a chunk that holds
+// one is drawn again by one lane, in order.
 __global__ void coin_draw_kernel(const int32_t* __restrict__ sorted_vals, const unsigned int* __restrict__ count,
                                  int32_t hmin, int32_t hspan, int32_t* __restrict__ memo, uint32_t* __restrict__ state) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (blockIdx.x != 0) return;
+    const int lane = threadIdx.x;                       // one wave
+    constexpr uint32_t scaling = 2147483645u / 2u, past = 2u * scaling;
+    uint32_t pw = 1, b = 16807u;                        // 16807^(lane+1)
+    for (uint32_t e = (uint32_t)lane + 1u; e; e >>= 1) {
+        if (e & 1u) pw = minstd_mulmod(pw, b);
+        b = minstd_mulmod(b, b);
+    }
     uint32_t st = *state;
     const unsigned int n = *count;
-    for (unsigned int i = 0; i < n; i++) {
-        const int32_t off = sorted_vals[i];
-        const int32_t hv = hmin + (off % hspan);
-        const int c = coin_1_2(st);
-        memo[off] = (hv % c + c) % c;          // mod(hash_num, c) (utils.hpp:97-98)
+    for (unsigned int c0 = 0; c0 < n; c0 += 64) {
+        const unsigned int m = min(64u, n - c0);
+        const bool on = (unsigned int)lane < m;
+        const uint32_t u = minstd_mulmod(st, pw);
+        const bool rej = on && u - 1u >= past;
+        if (__ballot(rej)) {                             // rare: this chunk one coin at a time
+            if (lane == 0) {
+                for (unsigned int i = c0; i < n; i++) {
+                    const int32_t off = sorted_vals[i];
+                    const int32_t hv = hmin + (off % hspan);
+                    const int c = coin_1_2(st);
+                    memo[off] = (hv % c + c) % c;
+                }
+            }
+            st = __shfl(st, 0);
+            break;
+        }
+        if (on) {
+            const int c = u - 1u >= scaling ? 2 : 1;
+            const int32_t off = sorted_vals[c0 + lane];
+            const int32_t hv = hmin + (off % hspan);
+            memo[off] = (hv % c + c) % c;              // mod(hash_num, c) (utils.hpp:97-98)
+        }
+        st = __shfl(u, (int)m - 1);
     }
-    *state = st;
+    if (lane == 0) *state = st;
 }
 
 __global__ void coin_vertex_kernel(const int32_t* __restrict__ h, int64_t N, int k, int32_t hmin, int32_t hspan,
@@ -99,9 +183,49 @@ __global__ void coin_vertex_kernel(const int32_t* __restrict__ h, int64_t N, int
     }
 }
 
+// Memo windows of at most CF_LDS_MAX entries: the memo and a 256-row block of
+// h (coalesced) in LDS, then one row per thread.
+__global__ __launch_bounds__(256) void coin_vertex_lds_kernel(const int32_t* __restrict__ h, int64_t N, int k,
+                                                              int32_t hmin, int32_t hspan,
+                                                              const int32_t* __restrict__ memo,
+                                                              int32_t* __restrict__ vertex) {
+    extern __shared__ int32_t lds[];
+    int32_t* lmemo = lds;                       // [k * hspan]
+    int32_t* lh = lds + k * hspan;              // [256 * k]
+    const int total = k * hspan;
+    for (int e = threadIdx.x; e < total; e += 256) lmemo[e] = memo[e];
+    for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < N; r0 += (int64_t)gridDim.x * 256) {
+        const int nr = (int)min((int64_t)256, N - r0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < nr * k; e += 256) lh[e] = h[r0 * k + e];
+        __syncthreads();
+        if ((int)threadIdx.x < nr) {
+            int v = 0;
+            for (int f = 0; f < k; f++) v = (v << 1) + lmemo[f * hspan + (lh[threadIdx.x * k + f] - hmin)];
+            vertex[r0 + threadIdx.x] = v;
+        }
+    }
+}
+
 int launch_coin_first(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
                       const int32_t* memo, int32_t* first_row) {
     const int64_t n = N * k;
+    const int64_t total = (int64_t)k * hspan;
+    if (total <= CF_LDS_MAX) {
+        static int cus[64] = {0};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return kstatus("hipGetDevice");
+        if (dev < 64 && !cus[dev] &&
+            hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return kstatus("hipDeviceGetAttribute");
+        const int64_t ncu = dev < 64 && cus[dev] > 0 ? cus[dev] : 256;
+        // >= 2048 rows per block so the LDS table's setup and merge stay small
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(4 * ncu, (N + 2047) / 2048));
+        const int64_t rpb = (N + nblk - 1) / nblk;
+        hipLaunchKernelGGL(coin_first_lds_kernel, dim3((unsigned)nblk), dim3(256), (size_t)total * 4, s, h, N, k, hmin,
+                           hspan, rpb, memo, first_row);
+        return kstatus("cube.hip");
+    }
     hipLaunchKernelGGL(coin_first_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, h, N,
                        k, hmin, hspan, memo, first_row);
     return kstatus("cube.hip");
@@ -122,6 +246,12 @@ int launch_coin_draw(hipStream_t s, const int32_t* sorted_vals, const unsigned i
 
 int launch_coin_vertex(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
                        const int32_t* memo, int32_t* vertex) {
+    if ((int64_t)k * hspan <= CF_LDS_MAX) {
+        const size_t lds = ((size_t)k * hspan + 256 * (size_t)k) * 4;
+        hipLaunchKernelGGL(coin_vertex_lds_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 2048)), dim3(256),
+                           lds, s, h, N, k, hmin, hspan, memo, vertex);
+        return kstatus("cube.hip");
+    }
     hipLaunchKernelGGL(coin_vertex_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 8192)), dim3(256), 0, s, h, N,
                        k, hmin, hspan, memo, vertex);
     return kstatus("cube.hip");

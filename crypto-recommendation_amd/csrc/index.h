@@ -30,12 +30,23 @@ struct ProjTable {
     // split-f16 image for the fused kernel (euclidean, d == 128, L*k <= 32):
     // Vh/Vl [64][128] f16 (rows >= LK zero), v1 = ||v||_1 rounded up
     bool fused_ok = false;
+    bool mfma_ok = false;        // split image present (either metric): hash_mfma.hip
     Buf vh_d, vl_d, v1_d;
     std::vector<float> hV;
     int upload(hipStream_t s, int metric, int d, int L, int k, float w, const float* V, const float* t,
                const int32_t* r, const double* R);
     HashParams params(int64_t nb) const;
+    HashMfmaParams mfma_params(int64_t nb) const;
 };
+
+}  // namespace lshkm
+
+struct lshkm_ctx_s;
+namespace lshkm {
+// Hashing of a batch on the split-f16 MFMA kernel where it applies, else the
+// fp64 kernel (api_index.cpp).
+int hash_rows(lshkm_ctx_s* ctx, int mode, Pts X, int64_t N, const ProjTable& pj, int64_t nb, int32_t* out_h,
+              int32_t* out_phi, int32_t* out_bucket, int32_t* mm);
 
 }  // namespace lshkm
 
@@ -52,6 +63,9 @@ struct lshkm_ctx_s {
     // range assignment workspace (lshkm_range_assign)
     lshkm::Buf ws_range[12];
     lshkm::Buf ws_scan;          // multi-block scans of large query size arrays
+    // workspaces of the entry points that synchronise their stream before
+    // returning (kmeans_pp, p_closest, top_n_recom): reused across calls
+    lshkm::Buf ws_call[6];
     uint64_t ws_epoch = 0;       // bumped by every user of the ws[] slots (api_index.cpp reserve)
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
     bool timing = false;

@@ -51,6 +51,26 @@ int launch_proj_hash(hipStream_t s, int mode, Pts X, int64_t N, const HashParams
                      int32_t* out_h, int32_t* out_phi, int32_t* out_bucket,
                      unsigned long long* stats);
 
+// Split-f16 MFMA hashing (hash_mfma.hip): fp32 points, d = 128, L*k <= 32.
+struct HashMfmaParams {
+    const _Float16* Vh;   // [>= 32][128] f16 hi of the projections (rows >= LK zero)
+    const _Float16* Vl;   // lo
+    const float* t;       // [LK] (euclidean)
+    const double* pnorm;  // [LK] |v|_2 rounded up
+    const double* v1;     // [LK] |v|_1 rounded up
+    const int32_t* r;     // [LK] (LSH euclidean)
+    const double* PT;     // [d][LKpad] fp64 projections (the fix-up pass)
+    float w;
+    int d, L, k, LK, LKpad;
+    int64_t nb;
+};
+// out_h: LSH euclidean tuples [N][L*k] / cube euclidean h [N][k] / cube cosine
+// vertex [N]; mm: cube euclidean h range (atomicMin/Max into a pre-set pair).
+// list / seg_counts: per-block lists of the uncertified rows (workspace).
+int launch_hash_mfma(hipStream_t s, int mode, const float* X, int64_t N, const HashMfmaParams& p, int32_t* out_h,
+                     int32_t* out_phi, int32_t* out_bucket, int32_t* mm, unsigned long long* list, int64_t list_cap,
+                     int32_t* seg_counts, int seg_cap, unsigned long long* stats);
+
 // Lloyd assignment (assign.hip).
 struct AssignWorkspace {
     float* C32;          // [Kpad][DP]
@@ -90,10 +110,15 @@ int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_
 int launch_add_counter(hipStream_t s, unsigned long long* dst, const unsigned long long* src);
 
 // Stable bucket scatter (scatter.hip).
-size_t sort_scratch_bytes(int64_t N, int64_t range);
+size_t sort_scratch_bytes(int64_t N, int64_t range, int T = 1);
 int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
                        int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch);
-int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr);
+int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr, int T = 1);
+// T independent stable sorts in one set of launches (table t: keys + t * key_ts,
+// vals + t * val_ts; outputs at + t * N).
+int stable_sort_by_key_batched(hipStream_t s, const int32_t* keys, int64_t kstride, int64_t key_ts, const int32_t* vals,
+                               int64_t val_ts, int T, int64_t N, int64_t range, int32_t* keys_out, int32_t* vals_out,
+                               void* scratch);
 
 // Queries (query.hip).
 size_t scan_ws_bytes(int64_t M);

@@ -25,9 +25,14 @@ namespace lshkm {
 constexpr int RS_THREADS = 256;
 constexpr int RS_TILE = 4096;
 
+// Batched over T tables by blockIdx.y: table t's keys start at keys + t * k_ts,
+// its histogram at hist + t * h_ts (likewise for every kernel below).
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const int32_t* __restrict__ keys, int64_t kstride, int64_t N,
-                                                        int shift, int nbins, int nblocks, uint32_t* __restrict__ hist) {
+                                                        int shift, int nbins, int nblocks, uint32_t* __restrict__ hist,
+                                                        int64_t k_ts, int64_t h_ts) {
     __shared__ uint32_t h[256];
+    keys += blockIdx.y * k_ts;
+    hist += blockIdx.y * h_ts;
     for (int b = threadIdx.x; b < nbins; b += RS_THREADS) h[b] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * RS_TILE;
@@ -40,8 +45,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const int32_t* __restri
 }
 
 // Exclusive scan of M uint32 in place, one block of 1024 threads.
-__global__ __launch_bounds__(1024) void rs_scan(uint32_t* __restrict__ a, int64_t M) {
+__global__ __launch_bounds__(1024) void rs_scan(uint32_t* __restrict__ a, int64_t M, int64_t a_ts) {
     __shared__ uint32_t part[1024];
+    a += blockIdx.y * a_ts;
     const int t = threadIdx.x;
     const int64_t seg = (M + 1023) / 1024;
     const int64_t lo = t * seg, hi = min(M, lo + seg);
@@ -63,8 +69,11 @@ __global__ __launch_bounds__(1024) void rs_scan(uint32_t* __restrict__ a, int64_
 // N = 10M, 0.35-0.54 ms in the one-block scan): reduce-then-scan over
 // RS_SC-element chunks, in place; the chunk totals go through rs_scan.
 constexpr int RS_SC = 8192;
-__global__ __launch_bounds__(1024) void rs_chunk_sum(const uint32_t* __restrict__ a, int64_t M, uint32_t* __restrict__ part) {
+__global__ __launch_bounds__(1024) void rs_chunk_sum(const uint32_t* __restrict__ a, int64_t M, uint32_t* __restrict__ part,
+                                                     int64_t a_ts, int64_t p_ts) {
     __shared__ uint32_t red[1024];
+    a += blockIdx.y * a_ts;
+    part += blockIdx.y * p_ts;
     const int64_t base = (int64_t)blockIdx.x * RS_SC;
     uint32_t s = 0;
 #pragma unroll
@@ -80,8 +89,11 @@ __global__ __launch_bounds__(1024) void rs_chunk_sum(const uint32_t* __restrict_
     }
     if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
-__global__ __launch_bounds__(1024) void rs_chunk_scan(uint32_t* __restrict__ a, int64_t M, const uint32_t* __restrict__ off) {
+__global__ __launch_bounds__(1024) void rs_chunk_scan(uint32_t* __restrict__ a, int64_t M, const uint32_t* __restrict__ off,
+                                                      int64_t a_ts, int64_t p_ts) {
     __shared__ uint32_t sh[1024];
+    a += blockIdx.y * a_ts;
+    off += blockIdx.y * p_ts;
     const int t = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * RS_SC + t * 8;      // 8 consecutive per thread
     uint32_t v[8], s = 0;
@@ -104,8 +116,13 @@ __global__ __launch_bounds__(1024) void rs_chunk_scan(uint32_t* __restrict__ a, 
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
     const int32_t* __restrict__ keys, int64_t kstride, const int32_t* __restrict__ vals, int64_t N, int shift,
     int dbits, int nblocks, const uint32_t* __restrict__ scanned, int32_t* __restrict__ keys_out,
-    int32_t* __restrict__ vals_out) {
+    int32_t* __restrict__ vals_out, int64_t k_ts, int64_t v_ts, int64_t h_ts, int64_t o_ts) {
     __shared__ uint32_t run[256];
+    keys += blockIdx.y * k_ts;
+    if (vals) vals += blockIdx.y * v_ts;
+    scanned += blockIdx.y * h_ts;
+    keys_out += blockIdx.y * o_ts;
+    vals_out += blockIdx.y * o_ts;
     __shared__ uint32_t wcnt[4][256];
     const int nbins = 1 << dbits;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -148,7 +165,12 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
 }
 
 __global__ void rs_copy(const int32_t* __restrict__ keys, int64_t kstride, const int32_t* __restrict__ vals, int64_t N,
-                        int32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out) {
+                        int32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t k_ts, int64_t v_ts,
+                        int64_t o_ts) {
+    keys += blockIdx.y * k_ts;
+    if (vals) vals += blockIdx.y * v_ts;
+    keys_out += blockIdx.y * o_ts;
+    vals_out += blockIdx.y * o_ts;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
         keys_out[i] = keys[i * kstride];
         vals_out[i] = vals ? vals[i] : (int32_t)i;
@@ -157,6 +179,8 @@ __global__ void rs_copy(const int32_t* __restrict__ keys, int64_t kstride, const
 
 // row_ptr[b] = first position of key >= b in the sorted keys; row_ptr[nb] = N.
 __global__ void csr_bounds(const int32_t* __restrict__ skeys, int64_t N, int64_t nb, int64_t* __restrict__ row_ptr) {
+    skeys += blockIdx.y * N;
+    row_ptr += blockIdx.y * (nb + 1);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= N; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t prev = i == 0 ? -1 : (int64_t)skeys[i - 1];
         const int64_t cur = i == N ? nb : (int64_t)skeys[i];
@@ -170,62 +194,72 @@ static int key_bits(int64_t range) {
     return bits;
 }
 
-size_t sort_scratch_bytes(int64_t N, int64_t range) {
+size_t sort_scratch_bytes(int64_t N, int64_t range, int T) {
     const int bits = key_bits(range);
     const int P = (bits + 7) / 8;
     const int DB = P ? (bits + P - 1) / P : 0;
     const int64_t nblocks = (N + RS_TILE - 1) / RS_TILE;
     const int64_t M = ((int64_t)1 << DB) * nblocks;
-    return (size_t)(2 * N + 64) * 4 + (size_t)M * 4 + (size_t)((M + RS_SC - 1) / RS_SC + 2) * 4 + 256;
+    return (size_t)T * ((size_t)(2 * N + 64) * 4 + (size_t)M * 4 + (size_t)((M + RS_SC - 1) / RS_SC + 2) * 4) + 256;
 }
 
-int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
-                       int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch) {
-    if (N <= 0) return 0;
+// T independent stable sorts in one set of launches (blockIdx.y = table): table
+// t's keys at keys + t * key_ts (stride kstride), its values (or the row index
+// when vals is null) at vals + t * val_ts; outputs at keys_out / vals_out + t * N.
+int stable_sort_by_key_batched(hipStream_t s, const int32_t* keys, int64_t kstride, int64_t key_ts, const int32_t* vals,
+                               int64_t val_ts, int T, int64_t N, int64_t range, int32_t* keys_out, int32_t* vals_out,
+                               void* scratch) {
+    if (N <= 0 || T <= 0) return 0;
     const int bits = key_bits(range);
     const int64_t nblocks = (N + RS_TILE - 1) / RS_TILE;
     if (bits == 0) {
-        hipLaunchKernelGGL(rs_copy, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 4096)), dim3(256), 0, s, keys, kstride,
-                           vals, N, keys_out, vals_out);
+        hipLaunchKernelGGL(rs_copy, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 4096), (unsigned)T), dim3(256), 0,
+                           s, keys, kstride, vals, N, keys_out, vals_out, key_ts, val_ts, N);
         return kstatus("scatter.hip");
     }
     const int P = (bits + 7) / 8;
     const int DB = (bits + P - 1) / P;
     const int nbins = 1 << DB;
-    int32_t* k2 = reinterpret_cast<int32_t*>(scratch);
-    int32_t* v2 = k2 + N;
-    uint32_t* hist = reinterpret_cast<uint32_t*>(v2 + N + 64);
+    const int64_t M = (int64_t)nbins * nblocks;
+    const int64_t nch = (M + RS_SC - 1) / RS_SC;
+    int32_t* k2 = reinterpret_cast<int32_t*>(scratch);          // [T][N]
+    int32_t* v2 = k2 + (size_t)T * N;                            // [T][N] (+64)
+    uint32_t* hist = reinterpret_cast<uint32_t*>(v2 + (size_t)T * N + 64);   // [T][M]
+    uint32_t* part = hist + (size_t)T * M;                       // [T][nch + 2]
     const int32_t* kin = keys;
     const int32_t* vin = vals;
-    int64_t kst = kstride;
+    int64_t kst = kstride, kts = key_ts, vts = val_ts;
     for (int p = 0; p < P; p++) {
         const bool to_out = ((P - 1 - p) % 2) == 0;
         int32_t* ko = to_out ? keys_out : k2;
         int32_t* vo = to_out ? vals_out : v2;
         const int shift = p * DB;
-        hipLaunchKernelGGL(rs_upsweep, dim3((unsigned)nblocks), dim3(RS_THREADS), 0, s, kin, kst, N, shift, nbins,
-                           (int)nblocks, hist);
-        const int64_t M = (int64_t)nbins * nblocks;
+        hipLaunchKernelGGL(rs_upsweep, dim3((unsigned)nblocks, (unsigned)T), dim3(RS_THREADS), 0, s, kin, kst, N, shift,
+                           nbins, (int)nblocks, hist, kts, M);
         if (M <= RS_SC) {
-            hipLaunchKernelGGL(rs_scan, dim3(1), dim3(1024), 0, s, hist, M);
+            hipLaunchKernelGGL(rs_scan, dim3(1, (unsigned)T), dim3(1024), 0, s, hist, M, M);
         } else {
-            uint32_t* part = hist + M;
-            const int64_t nch = (M + RS_SC - 1) / RS_SC;
-            hipLaunchKernelGGL(rs_chunk_sum, dim3((unsigned)nch), dim3(1024), 0, s, hist, M, part);
-            hipLaunchKernelGGL(rs_scan, dim3(1), dim3(1024), 0, s, part, nch);
-            hipLaunchKernelGGL(rs_chunk_scan, dim3((unsigned)nch), dim3(1024), 0, s, hist, M, part);
+            hipLaunchKernelGGL(rs_chunk_sum, dim3((unsigned)nch, (unsigned)T), dim3(1024), 0, s, hist, M, part, M, nch + 2);
+            hipLaunchKernelGGL(rs_scan, dim3(1, (unsigned)T), dim3(1024), 0, s, part, nch, nch + 2);
+            hipLaunchKernelGGL(rs_chunk_scan, dim3((unsigned)nch, (unsigned)T), dim3(1024), 0, s, hist, M, part, M,
+                               nch + 2);
         }
-        hipLaunchKernelGGL(rs_downsweep, dim3((unsigned)nblocks), dim3(RS_THREADS), 0, s, kin, kst, vin, N, shift, DB,
-                           (int)nblocks, hist, ko, vo);
-        kin = ko; vin = vo; kst = 1;
+        hipLaunchKernelGGL(rs_downsweep, dim3((unsigned)nblocks, (unsigned)T), dim3(RS_THREADS), 0, s, kin, kst, vin, N,
+                           shift, DB, (int)nblocks, hist, ko, vo, kts, vts, M, N);
+        kin = ko; vin = vo; kst = 1; kts = N; vts = N;
     }
     return kstatus("scatter.hip");
 }
 
-int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr) {
+int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
+                       int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch) {
+    return stable_sort_by_key_batched(s, keys, kstride, 0, vals, 0, 1, N, range, keys_out, vals_out, scratch);
+}
+
+int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr, int T) {
     const int64_t threads = N + 1;
-    hipLaunchKernelGGL(csr_bounds, dim3((unsigned)std::min<int64_t>((threads + 255) / 256, 8192)), dim3(256), 0, s,
-                       sorted_keys, N, nb, row_ptr);
+    hipLaunchKernelGGL(csr_bounds, dim3((unsigned)std::min<int64_t>((threads + 255) / 256, 8192), (unsigned)T), dim3(256),
+                       0, s, sorted_keys, N, nb, row_ptr);
     return kstatus("scatter.hip");
 }
 
