@@ -154,11 +154,17 @@ __global__ __launch_bounds__(64 * HMF_W, HMF_BPC) void hash_mfma_kernel(HashMfma
         const float nxf = (float)(sqrt((double)xn2f * (1.0 + 0x1p-16)) * (1.0 + 0x1p-20));
         // value and certificate of function f = 8g + 4h + q (D register 4g + q)
         uint32_t fmask = 0;
+        // LSH euclidean with k = 4 (the reference default): table l = 2g + h is
+        // D registers 4g..4g+3 of lane half h, so tuples, phi and the bucket are
+        // written from registers (fused.hip's layout)
+        const bool k4 = MODE == HM_LSH_EUCLID && k == 4;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
+            int32_t hv4[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int f = 8 * g + 4 * h + q;
+                hv4[q] = 0;
                 if (f >= LK) continue;
                 int32_t v;
                 bool ok;
@@ -175,10 +181,24 @@ __global__ __launch_bounds__(64 * HMF_W, HMF_BPC) void hash_mfma_kernel(HashMfma
                     ok = fabsf(u) > B;
                 }
                 if (!(ok && x_ok)) fmask |= 1u << f;
-                lv[col * HMF_VS + f] = v;
+                hv4[q] = v;
+                if (!k4) lv[col * HMF_VS + f] = v;
                 if (MODE == HM_CUBE_EUCLID_H && ok && x_ok && valid) {
                     hmin = min(hmin, v);
                     hmax = max(hmax, v);
+                }
+            }
+            if (MODE == HM_LSH_EUCLID && k4) {
+                const int l = 2 * g + h;
+                if (l < L && valid) {
+                    const int64_t o = row * L + l;
+                    *reinterpret_cast<int4*>(a.out_h + o * 4) = make_int4(hv4[0], hv4[1], hv4[2], hv4[3]);
+                    uint32_t hn = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) hn += phi_term(hv4[q], lr[4 * l + q]);
+                    const uint32_t ph = phi_final(hn);
+                    if (a.out_phi) a.out_phi[o] = (int32_t)ph;
+                    if (a.out_bucket) a.out_bucket[o] = bucket_fast(ph, a.bdiv);
                 }
             }
         }
@@ -197,14 +217,14 @@ __global__ __launch_bounds__(64 * HMF_W, HMF_BPC) void hash_mfma_kernel(HashMfma
         // outputs, lanes over (point, value) pairs of the tile
         const int npts = (int)min((int64_t)32, a.N - tile * 32);
         const int64_t r0 = tile * 32;
-        if (MODE == HM_LSH_EUCLID || MODE == HM_CUBE_EUCLID_H) {
+        if ((MODE == HM_LSH_EUCLID && !k4) || MODE == HM_CUBE_EUCLID_H) {
             if (a.out_h)
                 for (int e = lane; e < npts * LK; e += 64) {
                     const int p = e / LK, f = e - p * LK;
                     a.out_h[r0 * LK + e] = lv[p * HMF_VS + f];
                 }
         }
-        if (MODE == HM_LSH_EUCLID) {
+        if (MODE == HM_LSH_EUCLID && !k4) {
             for (int e = lane; e < npts * L; e += 64) {
                 const int p = e / L, l = e - p * L;
                 uint32_t hn = 0;
