@@ -507,16 +507,16 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
     if (path == 0) {
         const int Kpad = (K + 63) / 64 * 64;
         const bool cosine = metric != LSHKM_METRIC_EUCLIDEAN;
-        // hi-only scoring + 3-product refinement (euclidean); LSHKM_FUSED_HI=0: the 3-product form alone
+        // hi-only scoring + 3-product refinement; LSHKM_FUSED_HI=0: the 3-product form alone
         const char* fh = getenv("LSHKM_FUSED_HI");
-        const bool hi = !cosine && !(fh && !strcmp(fh, "0"));
+        const bool hi = !(fh && !strcmp(fh, "0"));
         const int64_t list_cap = N + FUSED_LIST_SLACK;
         const int64_t part_tiles = std::max<int64_t>((N + 31) / 32, (list_cap + 31) / 32 + FUSED_MAX_SEGS);
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) ||
             (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4 + (size_t)Kpad * 8)) ||
             (rc = ctx->ws_ambig.reserve((size_t)(N + FUSED_LIST_SLACK) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
             (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)) ||
-            ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8))) ||
+            ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8 * (cosine && hi ? 2 : 1)))) ||
             (Kpad > 256 && (rc = ctx->ws_part.reserve((size_t)part_tiles * 64 * 16))) ||
             (hi && ((rc = ctx->ws_ambig2.reserve((size_t)list_cap * 4)) ||
                     (rc = ctx->ws_seg2.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)))) ||
@@ -547,6 +547,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if (cosine) {
             f.metric = 1; f.nbv = nbv;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
+            if (hi) f.hfix2 = f.hfix + (N + FUSED_LIST_SLACK);
         }
         if (fuse_hash) {
             const ProjTable& pj = lsh->proj;
@@ -563,8 +564,12 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
                                f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (hi && (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_REFINED, cnt + 2))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if (cosine && ((rc = launch_cos_fix_seg(s, X.f(), C, f.hfix, f.seg_counts, f.seg_rows, f.nseg, assign, dist)) ||
-                       (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1)))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if (cosine) {
+            for (int li = 0; li < f.ncos_lists; li++)
+                if ((rc = launch_cos_fix_seg(s, X.f(), C, f.cos_list[li], f.cos_counts[li], f.seg_rows, f.nseg, assign,
+                                             dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        }
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * DP * 4)) || (rc = ctx->ws_cconst.reserve((size_t)3 * Kpad * 4)) ||

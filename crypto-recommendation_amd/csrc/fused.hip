@@ -1121,8 +1121,12 @@ __device__ inline void split8_hi(const float* x, half8& hi, half8& lo, float2v& 
 constexpr int FH_WAVES = FH_WAVES_SET;
 constexpr int FH_THREADS = 64 * FH_WAVES;
 
-template <bool HASH, bool MP = false>
+// MET = 1: cosine (the prep's normalised centroid rows, score x.c^ with no
+// offset; the winner's distance by cosine_fast_nb, declines to the fix-up
+// list as in fused_persistent_kernel<., 1>). No hashing with cosine.
+template <bool HASH, bool MP = false, int MET = 0>
 __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
+    static_assert(!(HASH && MET == 1), "the hi-only cosine form does not hash");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
     int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows
@@ -1368,8 +1372,11 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
         const float M2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
         const int I1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
         const float M1 = fmaxf(m1, om1);
+        // cosine: + 2^-43 |x| for the normalisation and the reference's own q
+        // (fused_persistent_kernel's cosine bound)
         const double E = (nxh * (double)crf + nxr * (double)cmaxf + FH_A * nxh * (double)chf + 0x1p-41 * xn2 +
-                          0x1p-18 * nx * (double)cmaxf + Ec) * (1.0 + 0x1p-20) + 1e-30;
+                          0x1p-18 * nx * (double)cmaxf + (MET == 1 ? 0x1p-43 * nx : 0.0) + Ec) * (1.0 + 0x1p-20) +
+                         1e-30;
         const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
 
         const bool amb = valid && !cert;
@@ -1381,6 +1388,25 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
             base = __shfl(base, leader);
             ambig_seg[base + __popcll(amask & ((1ull << lane) - 1ull))] = (int32_t)row;
         }
+        if constexpr (MET == 1) {
+            // cosine winner: one lane per point re-reads its row (L2) and the
+            // winner's fp64 row; declined certificates -> the fix-up list
+            bool fix = false;
+            if (h == 1 && valid && cert) {
+                a.assign[row] = I1;
+                double v;
+                if (cosine_fast_nb(a.X + row * FU_D, a.C64 + (size_t)I1 * FU_D, FU_D, a.nbv[I1], v)) a.dist[row] = v;
+                else fix = true;
+            }
+            const unsigned long long fb = __ballot(fix);
+            if (fb) {
+                const int leader = __builtin_ctzll(fb);
+                int base = 0;
+                if (lane == leader) base = atomicAdd(lcount + 1, __popcll(fb));
+                base = __shfl(base, leader);
+                if (fix) hfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
+            }
+        } else {
 #if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
         if (h == 1 && valid && cert) { a.assign[row] = I1; a.dist[row] = 0.0; }
 #else
@@ -1432,9 +1458,11 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
             }
         }
 #endif
+        }
     }
     __syncthreads();
-    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? (!HASH && a.pass_last != 0) : (HASH && a.pass_first)))) {
+    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? (!HASH && a.pass_last != 0)
+                                                      : ((HASH && a.pass_first) || (MET == 1 && a.pass_last))))) {
         const int c = lcount[threadIdx.x];
         a.seg_counts[2 * blockIdx.x + threadIdx.x] = c;
         if (c) atomicAdd(threadIdx.x == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
@@ -1682,10 +1710,11 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         a.list_in = nullptr; a.list_counts = nullptr; a.list_seg_rows = 0;
         f.final_list = f.ambig;
         f.final_counts = f.seg_counts;
-        if (f.hi && f.metric == 0) {
+        if (f.hi) {
             // hi-only passes (512 centroids each), the hash fix-up, then the
             // 3-product LIST form over the rows they listed (256 per pass)
-            if (!f.list2 || !f.seg_counts2 || !f.refined || (f.Kpad > FH_KMAX && !f.part)) {
+            const bool cos = f.metric == 1;
+            if (!f.list2 || !f.seg_counts2 || !f.refined || (f.Kpad > FH_KMAX && !f.part) || (cos && !f.hfix2)) {
                 set_error("launch_fused: the hi-only form needs the second list and its counters");
                 return -1;
             }
@@ -1698,7 +1727,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 a.t0 = c0 / 32; a.pass_first = p == 0; a.pass_last = p == np1 - 1;
                 const size_t lh = (size_t)fh_lds_bytes(a.Kpad, hash && p == 0);
                 const dim3 hblock(FH_THREADS);
-                if (np1 == 1) {
+                if (cos) {
+                    if (np1 == 1) hipLaunchKernelGGL((fused_hi_kernel<false, false, 1>), grid, hblock, lh, s, a);
+                    else hipLaunchKernelGGL((fused_hi_kernel<false, true, 1>), grid, hblock, lh, s, a);
+                } else if (np1 == 1) {
                     if (hash) hipLaunchKernelGGL((fused_hi_kernel<true>), grid, hblock, lh, s, a);
                     else hipLaunchKernelGGL((fused_hi_kernel<false>), grid, hblock, lh, s, a);
                 } else {
@@ -1710,7 +1742,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             FusedArgs r = a;
             r.list_in = f.ambig; r.list_counts = f.seg_counts; r.list_seg_rows = a.seg_rows;
             r.ambig = f.list2; r.seg_counts = f.seg_counts2; r.ambig_count = f.ambig_count;
-            r.hfix = f.hfix; r.hfix_count = f.hfix_count;
+            r.hfix = cos ? f.hfix2 : f.hfix; r.hfix_count = f.hfix_count;
             r.Cl = f.Cl;
             r.tuples = nullptr; r.phi = nullptr; r.bucket = nullptr;
             for (int p = 0; p < npass; p++) {
@@ -1718,11 +1750,21 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 r.Ch = f.Ch + (size_t)c0 * FU_D; r.Cl = f.Cl + (size_t)c0 * FU_D; r.cnh = f.cnh + c0;
                 r.Kpad = std::min(FP_KMAX, f.Kpad - c0);
                 r.t0 = c0 / 32; r.pass_first = p == 0; r.pass_last = p == npass - 1;
-                if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 0, false, true>), grid, block, lds_nohash, s, r);
-                else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true, true>), grid, block, lds_nohash, s, r);
+                if (cos) {
+                    if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 1, false, true>), grid, block, lds_nohash, s, r);
+                    else hipLaunchKernelGGL((fused_persistent_kernel<false, 1, true, true>), grid, block, lds_nohash, s, r);
+                } else {
+                    if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 0, false, true>), grid, block, lds_nohash, s, r);
+                    else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true, true>), grid, block, lds_nohash, s, r);
+                }
             }
             f.final_list = f.list2;
             f.final_counts = f.seg_counts2;
+            if (cos) {
+                f.ncos_lists = 2;
+                f.cos_list[0] = f.hfix; f.cos_counts[0] = f.seg_counts;
+                f.cos_list[1] = f.hfix2; f.cos_counts[1] = f.seg_counts2;
+            }
             return kstatus("fused_hi_kernel");
         }
         // one launch per 256-centroid slice (the hashing rides on the first)
@@ -1742,6 +1784,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             }
         }
         if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
+        if (f.metric == 1) {
+            f.ncos_lists = 1;
+            f.cos_list[0] = f.hfix; f.cos_counts[0] = f.seg_counts;
+        }
         return kstatus("fused_persistent_kernel");
     }
     const dim3 grid((unsigned)((f.N + FU_PB - 1) / FU_PB)), block(FU_THREADS);

@@ -230,6 +230,13 @@ struct FusedLaunch {
     int32_t* list2 = nullptr;
     int32_t* seg_counts2 = nullptr;
     unsigned long long* refined = nullptr;
+    // hi-only cosine: the LIST form's declined winner distances go to a second
+    // fix-up list (hfix2: [list_cap] entries after the first); out: the lists
+    // for cos_fix_seg, (list, segment counts) pairs
+    unsigned long long* hfix2 = nullptr;
+    int ncos_lists = 0;
+    const unsigned long long* cos_list[2] = {nullptr, nullptr};
+    const int32_t* cos_counts[2] = {nullptr, nullptr};
     // out: the list of rows still uncertified for the exact pass
     const int32_t* final_list = nullptr;
     const int32_t* final_counts = nullptr;
