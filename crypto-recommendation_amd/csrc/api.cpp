@@ -482,10 +482,10 @@ static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int
                                    seg_rows, nseg);
     int rc;
     if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 255) / 256 * 256) * 8))) return rc;
-    // K <= 256: score every centroid in f32 first and run the exact order only on
+    // K <= 1024: score every centroid in f32 first and run the exact order only on
     // the candidates the bound leaves (LSHKM_EXACT_PASS=full: every centroid)
     const char* ep = getenv("LSHKM_EXACT_PASS");
-    if (K <= 256 && d <= 256 && !(ep && !strcmp(ep, "full")))
+    if (K <= 1024 && d <= 256 && !(ep && !strcmp(ep, "full")))
         return launch_assign_pruned_list(ctx->stream, X, d, C, K, (float*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
                                          seg_counts, seg_rows, nseg);
     return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist,

@@ -566,7 +566,6 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
 constexpr int XP_R = XP_ROWS;
 constexpr int XP_WAVES = 4;
 constexpr int XP_SPLIT = XP_SPLITS;
-constexpr int XP_L = 64 / XP_R;      // lanes per row in the candidate phase
 
 // exact_euclid with the centroid row loaded 16 values at a time (one L2 round
 // trip per 16 terms instead of one per term); x in LDS.
@@ -612,13 +611,15 @@ __global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad,
     atomicMax(chunk + 1, __float_as_uint((float)(eb * (1.0 + 0x1p-20))));
 }
 
-template <typename TX>
+// NCH = Kpad / 64 centroid chunks scored per lane (K <= 64 NCH), R rows per wave.
+template <typename TX, int NCH = 4, int R = XP_R>
 __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
     const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
     const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
     const unsigned long long* __restrict__ row_count, int64_t max_rows, int32_t* __restrict__ assign,
     double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows) {
-    __shared__ TX xs[XP_WAVES][XP_R][XB_DMAX];
+    constexpr int RL = 64 / R;           // lanes per row in the candidate phase
+    __shared__ TX xs[XP_WAVES][R][XB_DMAX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int64_t total, g0, gstride;
     if (seg_counts) {
@@ -634,15 +635,15 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         gstride = (int64_t)gridDim.x * XP_WAVES;
     }
     const float* chunkc = cconst + Kpad;
-    const int64_t ngroups = (total + XP_R - 1) / XP_R;
+    const int64_t ngroups = (total + R - 1) / R;
     for (int64_t g = g0; g < ngroups; g += gstride) {
-        const int nr = (int)min((int64_t)XP_R, total - g * XP_R);
-        int32_t myrow[XP_R];
+        const int nr = (int)min((int64_t)R, total - g * R);
+        int32_t myrow[R];
 #pragma unroll
-        for (int r = 0; r < XP_R; r++) myrow[r] = rows[g * XP_R + min(r, nr - 1)];   // pad with the last row
-        float xn2p[XP_R];
+        for (int r = 0; r < R; r++) myrow[r] = rows[g * R + min(r, nr - 1)];   // pad with the last row
+        float xn2p[R];
 #pragma unroll
-        for (int r = 0; r < XP_R; r++) {
+        for (int r = 0; r < R; r++) {
             float q = 0.f;
             for (int j = lane; j < d; j += 64) {
                 const TX v = X[(int64_t)myrow[r] * d + j];
@@ -653,40 +654,40 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         }
         wave_sync();
         // phase 1: f32 scores of centroids c = lane + 64 i
-        float acc[XP_R][4];
+        float acc[R][NCH];
 #pragma unroll
-        for (int r = 0; r < XP_R; r++)
+        for (int r = 0; r < R; r++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) acc[r][i] = 0.f;
+            for (int i = 0; i < NCH; i++) acc[r][i] = 0.f;
 #pragma unroll 8
         for (int j = 0; j < d; j++) {
-            float cv[4];
+            float cv[NCH];
 #pragma unroll
-            for (int i = 0; i < 4; i++) cv[i] = 64 * i < Kpad ? CT32[(size_t)j * Kpad + 64 * i + lane] : 0.f;
+            for (int i = 0; i < NCH; i++) cv[i] = 64 * i < Kpad ? CT32[(size_t)j * Kpad + 64 * i + lane] : 0.f;
 #pragma unroll
-            for (int r = 0; r < XP_R; r++) {
+            for (int r = 0; r < R; r++) {
                 const float xj = (float)xs[wave][r][j];
 #pragma unroll
-                for (int i = 0; i < 4; i++) acc[r][i] = fmaf(xj, cv[i], acc[r][i]);
+                for (int i = 0; i < NCH; i++) acc[r][i] = fmaf(xj, cv[i], acc[r][i]);
             }
         }
         // per row: bound, U = min (s~ + e), candidate masks (wave-uniform)
-        unsigned long long cm[XP_R][4];
-        int ncand[XP_R];
-        bool pr[XP_R];
+        unsigned long long cm[R][NCH];
+        int ncand[R];
+        bool pr[R];
 #pragma unroll
-        for (int r = 0; r < XP_R; r++) {
+        for (int r = 0; r < R; r++) {
             // |x|^2 in fp64 over the lanes' f32 partials, rounded up (as the f32 path)
             double xn2 = (double)xn2p[r];
             for (int off = 32; off >= 1; off >>= 1) xn2 += __shfl_xor(xn2, off);
             xn2 = xn2 * (sizeof(TX) == 4 ? 1.0 + 0x1p-20 : 1.0 + 0x1p-19) + (sizeof(TX) == 4 ? 0.0 : 0x1p-280);
             const float nx = (float)(sqrt(xn2) * (1.0 + 0x1p-30));
             const float ex = (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30);
-            float lo[4];
+            float lo[NCH];
             float U = __builtin_inff();
             bool finite = nx <= 3.0e38f;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
+            for (int i = 0; i < NCH; i++) {
                 const int c = lane + 64 * i;
                 lo[i] = __builtin_inff();
                 if (c < K) {
@@ -701,22 +702,22 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
             for (int off = 32; off >= 1; off >>= 1) U = fminf(U, __shfl_xor(U, off));
             ncand[r] = 0;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
+            for (int i = 0; i < NCH; i++) {
                 cm[r][i] = __ballot(lo[i] <= U);
                 ncand[r] += __popcll(cm[r][i]);
             }
             pr[r] = r < nr && __all(finite) && ncand[r] >= 1;
         }
-        // rows with <= XP_L candidates: lane XP_L r + k evaluates row r's k-th candidate
+        // rows with <= RL candidates: lane RL r + k evaluates row r's k-th candidate
         {
-            const int r = lane / XP_L, k = lane % XP_L;
+            const int r = lane / RL, k = lane % RL;
             int c = -1;
             int seen = 0;
 #pragma unroll
-            for (int rr = 0; rr < XP_R; rr++) {
-                if (rr != r || !pr[rr] || ncand[rr] > XP_L) continue;
+            for (int rr = 0; rr < R; rr++) {
+                if (rr != r || !pr[rr] || ncand[rr] > RL) continue;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
+                for (int i = 0; i < NCH; i++) {
                     const int n = __popcll(cm[rr][i]);
                     if (c < 0 && k >= seen && k < seen + n) {
                         unsigned long long m = cm[rr][i];
@@ -732,7 +733,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
                 best = exact_euclid_b16(xs[wave][r], C + (size_t)c * d, d);
                 bi = c;
             }
-            for (int off = XP_L / 2; off >= 1; off >>= 1) {   // within the row's lanes
+            for (int off = RL / 2; off >= 1; off >>= 1) {   // within the row's lanes
                 const double ob = __shfl_xor(best, off);
                 const int oi = __shfl_xor(bi, off);
                 const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
@@ -745,7 +746,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         }
         // the other rows, one at a time with the whole wave
         for (int r = 0; r < nr; r++) {
-            if (pr[r] && ncand[r] <= XP_L) continue;
+            if (pr[r] && ncand[r] <= RL) continue;
             const bool prune = pr[r] && ncand[r] <= 64;
             const TX* xr = xs[wave][r];
             double best = 0.0;
@@ -754,7 +755,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
                 // lane k takes the k-th candidate (increasing c)
                 int c = -1, seen = 0;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
+                for (int i = 0; i < NCH; i++) {
                     const int n = __popcll(cm[r][i]);
                     if (c < 0 && lane >= seen && lane < seen + n) {
                         unsigned long long m = cm[r][i];
@@ -794,7 +795,7 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
     if (max_rows <= 0) return 0;
-    if (d > XB_DMAX || K > 256 || (seg_counts && nseg <= 0)) {
+    if (d > XB_DMAX || K > 1024 || (seg_counts && nseg <= 0)) {
         set_error("launch_assign_pruned_list: unsupported shape");
         return -1;
     }
@@ -804,14 +805,20 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
     (void)hipMemsetAsync(cconst + Kpad, 0, (size_t)(Kpad / 64) * 2 * 4, s);
     hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, d, X.f64 ? 1 : 0, CT32,
                        cconst);
-    const int64_t groups = (max_rows + XP_R - 1) / XP_R;
+    // K <= 256: 8 rows per wave over 4 chunks; K <= 1024: 2 rows per wave over 16
+    const bool wide = Kpad > 256;
+    const int R = wide ? 2 : XP_R;
+    const int64_t groups = (max_rows + R - 1) / R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
-    if (X.f64)
-        hipLaunchKernelGGL(assign_pruned_kernel<double>, dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, X.d(), d, C,
-                           CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
-    else
-        hipLaunchKernelGGL(assign_pruned_kernel<float>, dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, X.f(), d, C,
-                           CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+#define XP_LAUNCH(TX, NCH, RR, XP)                                                                                   \
+    hipLaunchKernelGGL((assign_pruned_kernel<TX, NCH, RR>), dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, XP, d, \
+                       C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows)
+    if (X.f64) {
+        if (wide) XP_LAUNCH(double, 16, 2, X.d()); else XP_LAUNCH(double, 4, XP_R, X.d());
+    } else {
+        if (wide) XP_LAUNCH(float, 16, 2, X.f()); else XP_LAUNCH(float, 4, XP_R, X.f());
+    }
+#undef XP_LAUNCH
     return kstatus("assign_pruned_kernel");
 }
 

@@ -58,70 +58,63 @@ int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int6
 
 // ------------------------------------------------------------------ parallel form
 // The reference's chain s = ((0 + x_1) + x_2) + ... rounds only when a partial
-// sum is not a double. Every partial is an integer multiple of 2^q (q = the
-// lowest set bit over the chain's values) bounded by A = sum |x_i| <
-// count * 2^t (t = the highest bit position + 1), so when
-// ceil(log2 count) + t - q <= 53 no step rounds and the chain's result is the
-// exact sum -- which integer (fixed-point) arithmetic computes in any order.
-// Values are accumulated as int128 multiples of 2^-KMF (KMF = 80): every value
-// with lowest bit >= 2^-80 and magnitude < 2^46 fits (fp32 rows, and fp64 rows
-// whose values have short mantissas); a chain with anything else (huge, tiny,
-// inf, nan), whose range test fails, or whose exact sum could leave the int128
-// range (ceil(log2 count) + top bit + KMF >= 127) is flagged and recomputed by
+// sum is not a double. Every partial sum -- of the chain, or of any subset of
+// the values in any order -- is an integer multiple of 2^q (q = the lowest set
+// bit over the chain's values) bounded by A = sum |x_i| < count * 2^t (t = the
+// highest bit position + 1), so when ceil(log2 count) + t - q <= 53 every such
+// partial is a double: no step of the chain rounds, and neither does any other
+// order of fp64 additions. The chain's result is then the exact sum, which
+// plain fp64 adds compute in any order -- per lane, then by fp64 atomics into
+// the (c, j) accumulator. q and t are tracked alongside (integer min / max), and
+// a chain whose test fails (or holding inf / nan) is flagged and recomputed by
 // the sequential kernel above (km_chain_kernel).
 // Work: waves stream 512 consecutive member positions of the cluster-sorted
-// list (lane = dimension), flushing their int128 partial to the (c, j)
-// accumulator with two 64-bit atomics (the carry of the low word is exact mod
-// 2^128) whenever the cluster changes.
-constexpr int KMF = 80;
+// list (lane = dimension), flushing their partial (one fp64 atomic add, two
+// integer atomics) whenever the cluster changes.
 constexpr int KMF_CH = 512;
 constexpr int KMF_BAD = 1 << 20;     // qmin marker of a chain that needs the sequential kernel
-constexpr int KMF_TMAX = 46;         // one value < 2^46: m 2^(e + KMF) < 2^126
 
 struct KmFx {                        // per (c, j), zeroed / initialised by km_fx_init_kernel
-    unsigned long long lo;
-    long long hi;
-    int qmin;                        // lowest set-bit exponent, KMF_BAD if flagged
+    double sum;
+    int qmin;                        // lowest set-bit exponent, -KMF_BAD if flagged
     int tmax;                        // highest bit position + 1
 };
 
 __global__ void km_fx_init_kernel(KmFx* __restrict__ acc, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) { acc[i].lo = 0; acc[i].hi = 0; acc[i].qmin = 1 << 30; acc[i].tmax = -(1 << 30); }
+    if (i < n) { acc[i].sum = 0.0; acc[i].qmin = 1 << 30; acc[i].tmax = -(1 << 30); }
 }
 
-__device__ inline void km_fx_flush(KmFx* a, __int128 v, int qmin, int tmax, bool bad) {
-    const unsigned long long vlo = (unsigned long long)v;
-    const long long vhi = (long long)(v >> 64);
-    const unsigned long long old = atomicAdd(&a->lo, vlo);
-    const long long carry = (old + vlo < old) ? 1 : 0;
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a->hi), (unsigned long long)(vhi + carry));
+__device__ inline void km_fx_flush(KmFx* a, double v, int qmin, int tmax, bool bad) {
+    if (v != 0.0) atomicAdd(&a->sum, v);
     atomicMin(&a->qmin, bad ? -KMF_BAD : qmin);
     atomicMax(&a->tmax, tmax);
 }
 
-// value = (-1)^sign * m * 2^e of an fp32 / fp64 row element; false for +-0 / inf / nan
-// (inf / nan set bad)
-__device__ inline bool km_fx_split(float v, uint64_t& m, int& e, bool& neg, bool& bad) {
+// lowest set-bit exponent q and top t of a nonzero finite value; false for
+// +-0 (adds nothing: -0 + 0 = +0 either way) and inf / nan (sets bad)
+__device__ inline bool km_fx_bits(float v, int& q, int& t, bool& bad) {
     const uint32_t b = __float_as_uint(v);
     const int E = (int)((b >> 23) & 255u);
     const uint32_t f = b & 0x7FFFFFu;
     if (E == 255) { bad = true; return false; }
-    if (E == 0 && f == 0) return false;   // +-0 adds nothing (and -0 + 0 = +0 either way)
-    m = E ? (f | 0x800000u) : f;
-    e = (E ? E : 1) - 150;
-    neg = (b >> 31) != 0;
+    const uint32_t m = E ? (f | 0x800000u) : f;
+    if (m == 0) return false;
+    const int e = (E ? E : 1) - 150;
+    q = e + __builtin_ctz(m);
+    t = e + 32 - __builtin_clz(m);
     return true;
 }
-__device__ inline bool km_fx_split(double v, uint64_t& m, int& e, bool& neg, bool& bad) {
+__device__ inline bool km_fx_bits(double v, int& q, int& t, bool& bad) {
     const uint64_t b = (uint64_t)__double_as_longlong(v);
     const int E = (int)((b >> 52) & 2047u);
     const uint64_t f = b & 0xFFFFFFFFFFFFFull;
     if (E == 2047) { bad = true; return false; }
-    if (E == 0 && f == 0) return false;
-    m = E ? (f | (1ull << 52)) : f;
-    e = (E ? E : 1) - 1075;
-    neg = (b >> 63) != 0;
+    const uint64_t m = E ? (f | (1ull << 52)) : f;
+    if (m == 0) return false;
+    const int e = (E ? E : 1) - 1075;
+    q = e + __builtin_ctzll(m);
+    t = e + 64 - __builtin_clzll(m);
     return true;
 }
 
@@ -143,7 +136,7 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int
     }
     int c = lo;
     int64_t cend = crow[c + 1];
-    __int128 s = 0;
+    double s = 0.0;
     int qmin = 1 << 30, tmax = -(1 << 30);
     bool bad = false;
     for (int64_t p = p0; p < p1; p += 16) {
@@ -155,21 +148,15 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int
             if (p + u >= p1) break;
             while (p + u >= cend) {              // cluster boundary: flush, move on (skipping empty clusters)
                 if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
-                s = 0; qmin = 1 << 30; tmax = -(1 << 30); bad = false;
+                s = 0.0; qmin = 1 << 30; tmax = -(1 << 30); bad = false;
                 c++;
                 cend = crow[c + 1];
             }
-            uint64_t m;
-            int e;
-            bool neg;
-            if (!km_fx_split(v[u], m, e, neg, bad)) continue;     // value = m * 2^e
-            const int q = e + __builtin_ctzll(m), t = e + 64 - __builtin_clzll(m);
+            int q, t;
+            if (!km_fx_bits(v[u], q, t, bad)) continue;
             qmin = min(qmin, q);
             tmax = max(tmax, t);
-            if (q < -KMF || t > KMF_TMAX) { bad = true; continue; }
-            // shift out the trailing zeros first: e + KMF may be negative (q >= -KMF is not)
-            const __int128 w = (__int128)(m >> (q - e)) << (q + KMF);
-            s += neg ? -w : w;
+            s = __dadd_rn(s, (double)v[u]);     // exact whenever the chain's test passes
         }
     }
     if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
@@ -185,39 +172,26 @@ __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_
     const int c = (int)(i / d);
     const KmFx a = acc[i];
     int64_t cnt = crow[c + 1] - crow[c];
-    __int128 s = ((__int128)a.hi << 64) | (__int128)a.lo;
+    double s = a.sum;
     int qmin = a.qmin, tmax = a.tmax;
     bool ok = qmin > -KMF_BAD / 2;
     if (carry && ok) {
         const double s0 = carry[i];
         cnt += 1;
-        if (s0 != 0.0) {
-            const uint64_t b = (uint64_t)__double_as_longlong(s0);
-            const int E = (int)((b >> 52) & 2047u);
-            const uint64_t f = b & 0xFFFFFFFFFFFFFull;
-            const uint64_t m = E ? (f | (1ull << 52)) : f;
-            const int e = (E ? E : 1) - 1075;
-            const int q = e + __builtin_ctzll(m), t = e + 64 - __builtin_clzll(m);
-            if (E == 2047 || q < -KMF || t > KMF_TMAX) ok = false;
-            else {
-                qmin = min(qmin, q);
-                tmax = max(tmax, t);
-                const __int128 w = (__int128)(m >> (q - e)) << (q + KMF);
-                s += (b >> 63) ? -w : w;
-            }
+        int q, t;
+        bool bad = false;
+        if (km_fx_bits(s0, q, t, bad)) {
+            qmin = min(qmin, q);
+            tmax = max(tmax, t);
+            s = __dadd_rn(s0, s);
         }
+        if (bad) ok = false;
     }
     int lc = 0;
     while (((int64_t)1 << lc) < cnt) lc++;          // ceil(log2 count)
     if (ok && qmin <= tmax && lc + tmax - qmin > 53) ok = false;
-    // |exact sum| < count 2^tmax must stay inside the int128 accumulator
-    if (ok && qmin <= tmax && lc + tmax + KMF >= 127) ok = false;
-    if (ok) {
-        // |s| < 2^(53 + qmin + KMF): the conversion is exact, and so is the scaling
-        sums[i] = ldexp((double)s, -KMF);
-    } else {
-        atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));   // chain block (c, j/64) goes sequential
-    }
+    if (ok) sums[i] = s;
+    else atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));   // chain block (c, j/64) goes sequential
 }
 
 // The sequential chains of the flagged (c, 64-dim block)s only.

@@ -32,6 +32,18 @@ for step in "$@"; do
            > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err")
         rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    pmc5)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --pmc $c --output-format csv \
+           -d "$OUT/c5/pmc_$c" -o run -- python3 "$R/bench.py" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline \
+           > "$OUT/c5_pmc_$c.json" 2> "$OUT/c5_pmc_$c.err")
+        rc=$?; echo "pmc5 $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    prof5)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+         -d "$OUT/prof5" -o run -- python3 "$R/bench.py" --workload c5 --steps 5 --warmup 1 --no-cpu-baseline \
+         > "$OUT/bench_prof5.json" 2> "$OUT/bench_prof5.err")
+      rc=$?; echo "prof5 rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     sq)
       i=0
       for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" \

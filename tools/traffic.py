@@ -1,10 +1,12 @@
 """Per-launch HBM traffic of the fused pass from rocprofv3 PMC passes.
 
-usage: python tools/traffic.py gpurun_out/<tag> [out.json]
+usage: python tools/traffic.py gpurun_out/<tag> [out.json] [K] [workload]
 
 Reads <tag>/pmc_FETCH_SIZE/**/counter_collection.csv and pmc_WRITE_SIZE/...,
-sums the fused pass's kernels per dispatch (fused_persistent_kernel +
-hash_fixup_kernel, or fused_kernel in the chunked form) and applies the gfx950
+sums the fused pass's kernels per call (the dispatches between two
+fused_centroid_prep launches: fused_hi_kernel passes, hash_fixup_kernel, the
+3-product LIST refinement; fused_persistent_kernel / fused_kernel in the other
+forms) and applies the gfx950
 corrections of MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half the
 bytes of a wide streaming read -> x2; WRITE_SIZE is exact for 16-B stores.
 Both counters are in KiB."""
@@ -15,34 +17,32 @@ import os
 import statistics
 import sys
 
-FUSED = ("fused_persistent_kernel", "hash_fixup_kernel", "fused_kernel")
+FUSED = ("fused_hi_kernel", "fused_persistent_kernel", "hash_fixup_kernel", "fused_kernel")
 
 
 def per_launch(path, counter):
     files = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {path}")
-    by_dispatch = {}
-    names = {}
+    val, names = {}, {}
     for fn in files:
         for r in csv.DictReader(open(fn)):
             if r["Counter_Name"] != counter:
                 continue
-            k = r["Kernel_Name"]
-            if not any(f in k for f in FUSED):
-                continue
             d = int(r["Dispatch_Id"])
-            by_dispatch[d] = by_dispatch.get(d, 0.0) + float(r["Counter_Value"])
-            names[d] = k
-    # group consecutive persistent + fix-up dispatches into one fused pass
+            val[d] = val.get(d, 0.0) + float(r["Counter_Value"])
+            names[d] = r["Kernel_Name"]
+    # one call = the dispatches from a fused_centroid_prep to the next one
     passes, cur = [], None
-    for d in sorted(by_dispatch):
-        if "hash_fixup_kernel" in names[d] and cur is not None:
-            cur += by_dispatch[d]
-            passes[-1] = cur
-        else:
-            cur = by_dispatch[d]
-            passes.append(cur)
+    for d in sorted(names):
+        if "fused_centroid_prep" in names[d]:
+            if cur is not None:
+                passes.append(cur)
+            cur = 0.0
+        elif cur is not None and any(f in names[d] for f in FUSED):
+            cur += val[d]
+    if cur:
+        passes.append(cur)
     return passes
 
 
@@ -55,6 +55,8 @@ FETCH_SCALE_FUSED_PATTERN = 0.696
 def main():
     tag = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else None
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    workload = sys.argv[4] if len(sys.argv) > 4 else "c3"
     fetch = per_launch(os.path.join(tag, "pmc_FETCH_SIZE"), "FETCH_SIZE")
     write = per_launch(os.path.join(tag, "pmc_WRITE_SIZE"), "WRITE_SIZE")
     f_kib = statistics.median(fetch)
@@ -62,7 +64,7 @@ def main():
     read_b = f_kib * 1024 * 2                                    # the guide's x2 rule (upper end)
     read_cal = f_kib * 1024 / FETCH_SCALE_FUSED_PATTERN          # isolated-pattern calibration (lower end)
     res = {
-        "N": 10_000_000, "K": 256,
+        "N": 10_000_000, "K": K, "workload": workload,
         "passes_measured": [len(fetch), len(write)],
         "fetch_size_kib_raw": f_kib,
         "write_size_kib": w_kib,
@@ -74,7 +76,7 @@ def main():
                 "tools/calib_fetch.hip measured FETCH_SIZE/bytes = 0.500 for 1-KiB-per-instruction streams and "
                 "0.696 for this kernel's 2 x 16-B-per-lane point loads run alone; inside the fused pass the "
                 "ratio is lower (reads/0.696 < the 5.12 GB of X), so the x2 figure is reported. WRITE_SIZE as "
-                "counted. fused pass = fused_persistent_kernel + hash_fixup_kernel",
+                "counted. fused pass = every fused-family dispatch of one call (hi-only passes, hash fix-up, LIST refinement)",
     }
     print(json.dumps(res, indent=1))
     if out:
