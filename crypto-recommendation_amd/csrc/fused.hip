@@ -1069,9 +1069,10 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 }
 
 // ------------------------------------------------------------ hi-only form
-// Euclidean Lloyd (+ hashing) with ONE f16 MFMA per centroid product: the
+// Lloyd (+ hashing, euclidean) with ONE f16 MFMA per centroid product: the
 // score is t~ = acc(-|c|^2/2 + sum_j xh_j ch_j), the accumulator initialised
-// with the f32 -|c|^2/2 (no epilogue add), ch = f16(f32(c)), xh = f16(x).
+// with the f32 -|c|^2/2 (no epilogue add), ch = f16(f32(c)), xh = f16(x);
+// cosine (MET = 1): the normalised centroid rows, no offset.
 // Bound (rigorous, |x_j| <= 2^15, c in range): with xr = x - xh (exact in f32)
 // and cr = c - ch,
 //   |t~ - t| <= |xh||cr| + |xr||c| + 2^-24|cn| + A (|cn| + |xh||ch|),
