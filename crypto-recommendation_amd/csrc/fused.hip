@@ -1125,6 +1125,87 @@ constexpr int FH_THREADS = 64 * FH_WAVES;
 // MET = 1: cosine (the prep's normalised centroid rows, score x.c^ with no
 // offset; the winner's distance by cosine_fast_nb, declines to the fix-up
 // list as in fused_persistent_kernel<., 1>). No hashing with cosine.
+// Cosine winner distance from the row in registers, both lane halves busy.
+// Lane half h owns dims 16s + 8h..+7 (s = 0..7). Each half accumulates the
+// double products of ITS dims with IpAcc's double-double (exact.h), in its own
+// order; the reference's x87 chain runs over all 128 in order, so the error
+// term sum_k |S_k| of IpAcc is bounded by the halves' own partials: S_k =
+// A_k + B_k, A held during the other half's blocks of 8 -> ts <= ts0 + ts1 +
+// 8 (sum_s |A_end(s)| + sum_{s<7} |B_end(s)|), max |S_k| <= mx0 + mx1 (a looser
+// but rigorous radius; exact.h quot_status decides). |x|^2 is the reference's
+// sequential chain, the halves taking turns (the euclidean winner's pattern).
+// Returns 0 (certified, v = 1 - q), 1 / 2 (declined: soft-x87 fix-up).
+__device__ inline int cosine_winner_halves(const float (&xf)[64], const double* __restrict__ crow_h, double nbv, int h,
+                                           double& v) {
+    // |x|^2: the reference's sequential fp64 chain (cust_vector.hpp:139-155), halves alternating
+    double xa = 0.0;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const double xj = (double)xf[8 * s + j];
+                xa = __dadd_rn(xa, __dmul_rn(xj, xj));
+            }
+        }
+        const double from0 = swap_halves(xa, h);
+        if (h == 1) {
+            xa = from0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const double xj = (double)xf[8 * s + j];
+                xa = __dadd_rn(xa, __dmul_rn(xj, xj));
+            }
+        }
+        const double from1 = swap_halves(xa, h);
+        if (h == 0) xa = from1;
+    }
+    // the inner product, each half over its own dims
+    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0, hold = 0.0;
+    double2 cb[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 2 * j);
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        double cv[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) { cv[2 * j] = cb[j].x; cv[2 * j + 1] = cb[j].y; }
+        if (s + 1 < 8) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 16 * (s + 1) + 2 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const double pj = __dmul_rn((double)xf[8 * s + j], cv[j]);
+            const double t = __dadd_rn(sh, pj);
+            const double bb = __dsub_rn(t, sh);
+            const double e = __dadd_rn(__dsub_rn(sh, __dsub_rn(t, bb)), __dsub_rn(pj, bb));   // TwoSum
+            sh = t;
+            sl = __dadd_rn(sl, e);
+            ts = __dadd_rn(ts, fabs(t));
+            mx = fmax(mx, fabs(t));
+        }
+        hold = __dadd_rn(hold, fabs(sh));
+    }
+    // the lower half's accumulator to the upper lanes
+    const double sh0 = swap_halves(sh, h), sl0 = swap_halves(sl, h), ts0 = swap_halves(ts, h);
+    const double mx0 = swap_halves(mx, h), hold0 = swap_halves(hold, h);
+    if (h == 0) return 2;                 // the upper lanes finish
+    IpAcc ip;
+    const double t = __dadd_rn(sh0, sh);
+    const double bb = __dsub_rn(t, sh0);
+    const double e = __dadd_rn(__dsub_rn(sh0, __dsub_rn(t, bb)), __dsub_rn(sh, bb));
+    ip.sh = t;
+    ip.sl = __dadd_rn(__dadd_rn(sl0, sl), e);
+    // sum_k |S_k| bound (rounded up: + 2^-50 relative for the adds here)
+    ip.ts = __dadd_rn(__dadd_rn(ts0, ts), 8.0 * __dadd_rn(hold0, __dsub_rn(hold, fabs(sh)))) * (1.0 + 0x1p-50);
+    ip.mx = __dadd_rn(mx0, mx) * (1.0 + 0x1p-50);
+    double q, qr;
+    const int st = ip.quot_status(__dmul_rn(sqrt(xa), sqrt(nbv)), q, qr);
+    if (st == 0) v = __dsub_rn(1.0, q);
+    return st;
+}
+
 template <bool HASH, bool MP = false, int MET = 0>
 __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
     static_assert(!(HASH && MET == 1), "the hi-only cosine form does not hash");
@@ -1390,14 +1471,17 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
             ambig_seg[base + __popcll(amask & ((1ull << lane) - 1ull))] = (int32_t)row;
         }
         if constexpr (MET == 1) {
-            // cosine winner: one lane per point re-reads its row (L2) and the
-            // winner's fp64 row; declined certificates -> the fix-up list
+            // cosine winner from the row in registers, both lane halves busy;
+            // declined certificates -> the fix-up list
             bool fix = false;
-            if (h == 1 && valid && cert) {
-                a.assign[row] = I1;
-                double v;
-                if (cosine_fast_nb(a.X + row * FU_D, a.C64 + (size_t)I1 * FU_D, FU_D, a.nbv[I1], v)) a.dist[row] = v;
-                else fix = true;
+            if (valid && cert) {                          // the same on both halves of a point
+                double v = 0.0;
+                const int st = cosine_winner_halves(xf, a.C64 + (size_t)I1 * FU_D + 8 * h, a.nbv[I1], h, v);
+                if (h == 1) {
+                    a.assign[row] = I1;
+                    if (st == 0) a.dist[row] = v;
+                    else fix = true;
+                }
             }
             const unsigned long long fb = __ballot(fix);
             if (fb) {
