@@ -477,17 +477,20 @@ static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int
                         const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0,
                         const int32_t* rows = nullptr) {
     if (!rows) rows = (const int32_t*)ctx->ws_ambig.p;
-    if (metric != LSHKM_METRIC_EUCLIDEAN || (!seg_counts && d > 256))
+    // K <= 1024, d <= 256: score every centroid in f32 first and run the exact
+    // order only on the candidates the bound leaves (euclidean, and cosine on
+    // fp32 rows); LSHKM_EXACT_PASS=full: every centroid
+    const char* ep = getenv("LSHKM_EXACT_PASS");
+    const bool prune = K <= 1024 && d <= 256 && !(ep && !strcmp(ep, "full")) &&
+                       (metric == LSHKM_METRIC_EUCLIDEAN || !X.f64);
+    if (!prune && (metric != LSHKM_METRIC_EUCLIDEAN || (!seg_counts && d > 256)))
         return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist, seg_counts,
                                    seg_rows, nseg);
     int rc;
     if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 255) / 256 * 256) * 8))) return rc;
-    // K <= 1024: score every centroid in f32 first and run the exact order only on
-    // the candidates the bound leaves (LSHKM_EXACT_PASS=full: every centroid)
-    const char* ep = getenv("LSHKM_EXACT_PASS");
-    if (K <= 1024 && d <= 256 && !(ep && !strcmp(ep, "full")))
+    if (prune)
         return launch_assign_pruned_list(ctx->stream, X, d, C, K, (float*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
-                                         seg_counts, seg_rows, nseg);
+                                         seg_counts, seg_rows, nseg, metric == LSHKM_METRIC_EUCLIDEAN ? 0 : 1);
     return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
                                     seg_counts, seg_rows, nseg);
 }

@@ -586,20 +586,62 @@ __device__ inline double exact_euclid_b16(const TX* __restrict__ x, const double
     return sqrt(acc);
 }
 
+// The reference's distance of one (row, centroid) pair on the pruned pass:
+// euclidean in exact order; cosine by the soft-x87 chain (16-B loads when the
+// row length allows).
+template <int MET, typename TX>
+__device__ inline double pruned_dist(const TX* __restrict__ x, const double* __restrict__ c, int d) {
+    if constexpr (MET == 0) {
+        return exact_euclid_b16(x, c, d);
+    } else {
+        if constexpr (sizeof(TX) == 4) {
+            if ((d & 15) == 0) return exact_cosine_x87_b16(x, c, d);
+        }
+        return exact_cosine_x87(x, c, d);
+    }
+}
+
 __global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, int xf64,
-                                  float* __restrict__ CT32, float* __restrict__ cconst) {
+                                  float* __restrict__ CT32, float* __restrict__ cconst, int metric) {
     // one wave per centroid: CT32 [d][Kpad], cconst = cn2[Kpad] ++ {ec, eb}[Kpad/64]
-    // (chunk maxima by atomicMax on the bits of positive floats; zeroed first)
+    // (chunk maxima by atomicMax on the bits of positive floats; zeroed first).
+    // cosine: CT32 holds the normalised row (score -x.c^), cconst 0, or +inf for
+    // a zero / extreme-norm centroid (rows then evaluate every centroid exactly)
     const int c = blockIdx.x, lane = threadIdx.x;
+    double scale = 1.0;
+    if (metric == 1) {
+        double q = 0.0;
+        for (int j = lane; j < d; j += 64) {
+            const double v = c < K ? C[(size_t)c * d + j] : 0.0;
+            q = fma(v, v, q);
+        }
+        for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+        scale = (q >= 1e-200 && q <= 1e200) ? 1.0 / sqrt(q) : 0.0;
+        if (c < K && scale == 0.0) {
+            for (int j = lane; j < d; j += 64) CT32[(size_t)j * Kpad + c] = 0.f;
+            if (lane == 0) cconst[c] = __builtin_inff();
+            return;
+        }
+    }
     double sq = 0.0;
     for (int j = lane; j < d; j += 64) {
-        const double v = c < K ? C[(size_t)c * d + j] : 0.0;
+        const double v = c < K ? C[(size_t)c * d + j] * scale : 0.0;
         sq = fma(v, v, sq);
         CT32[(size_t)j * Kpad + c] = (float)v;
     }
     for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
     if (lane != 0) return;
     if (c >= K) { cconst[c] = __builtin_inff(); return; }
+    if (metric == 1) {
+        // |s~ - x.c^| <= (d + 2) 2^-24 |x| (f32 FMA chain, c^'s f32 rounding), and
+        // the reference's q = x.c / (|x||c|) sits within 2^-40 |x| of x.c^ / |x| . |x|
+        cconst[c] = 0.f;
+        const double ec = ((d + 2.0) * 0x1p-24 * (1.0 + 0x1p-10) + 0x1p-40 + (xf64 ? 0x1p-23 : 0.0)) * (1.0 + 0x1p-18);
+        unsigned int* chunk = reinterpret_cast<unsigned int*>(cconst + Kpad + 2 * (c / 64));
+        atomicMax(chunk, __float_as_uint((float)(ec * (1.0 + 0x1p-20))));
+        atomicMax(chunk + 1, __float_as_uint(1e-30f));
+        return;
+    }
     const double up = 1.0 + 0x1p-18;
     const double nc = sqrt(sq) * (1.0 + 0x1p-30);
     cconst[c] = (float)sq;
@@ -612,7 +654,7 @@ __global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad,
 }
 
 // NCH = Kpad / 64 centroid chunks scored per lane (K <= 64 NCH), R rows per wave.
-template <typename TX, int NCH = 4, int R = XP_R>
+template <typename TX, int NCH = 4, int R = XP_R, int MET = 0>
 __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
     const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
     const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
@@ -692,7 +734,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
                 lo[i] = __builtin_inff();
                 if (c < K) {
                     const float E = fmaf(nx, chunkc[2 * i], chunkc[2 * i + 1] + ex);
-                    const float sc = fmaf(-2.f, acc[r][i], cconst[c]);
+                    const float sc = MET == 1 ? cconst[c] - acc[r][i] : fmaf(-2.f, acc[r][i], cconst[c]);
                     lo[i] = sc - E;
                     const float hi = sc + E;
                     finite = finite && (hi - lo[i]) <= 3.0e38f;   // false for inf / nan
@@ -730,7 +772,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
             double best = 0.0;
             int bi = -1;
             if (c >= 0) {
-                best = exact_euclid_b16(xs[wave][r], C + (size_t)c * d, d);
+                best = pruned_dist<MET>(xs[wave][r], C + (size_t)c * d, d);
                 bi = c;
             }
             for (int off = RL / 2; off >= 1; off >>= 1) {   // within the row's lanes
@@ -765,12 +807,12 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
                     seen += n;
                 }
                 if (c >= 0) {
-                    best = exact_euclid_b16(xr, C + (size_t)c * d, d);
+                    best = pruned_dist<MET>(xr, C + (size_t)c * d, d);
                     bi = c;
                 }
             } else {
                 for (int c = lane; c < K; c += 64) {
-                    const double dd = exact_euclid_b16(xr, C + (size_t)c * d, d);
+                    const double dd = pruned_dist<MET>(xr, C + (size_t)c * d, d);
                     // assignment.hpp:66: the -1 sentinel takes centroid 0's distance
                     // even if NaN, which then blocks every later '<'
                     if (bi < 0 ? (dd == dd || c == 0) : dd < best) { best = dd; bi = c; }
@@ -793,7 +835,8 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
 
 int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
-                              int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
+                              int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg,
+                              int metric) {
     if (max_rows <= 0) return 0;
     if (d > XB_DMAX || K > 1024 || (seg_counts && nseg <= 0)) {
         set_error("launch_assign_pruned_list: unsupported shape");
@@ -804,19 +847,25 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
     float* cconst = ws + (size_t)d * Kpad;
     (void)hipMemsetAsync(cconst + Kpad, 0, (size_t)(Kpad / 64) * 2 * 4, s);
     hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, d, X.f64 ? 1 : 0, CT32,
-                       cconst);
+                       cconst, metric);
     // K <= 256: 8 rows per wave over 4 chunks; K <= 1024: 2 rows per wave over 16
     const bool wide = Kpad > 256;
     const int R = wide ? 2 : XP_R;
     const int64_t groups = (max_rows + R - 1) / R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
-#define XP_LAUNCH(TX, NCH, RR, XP)                                                                                   \
-    hipLaunchKernelGGL((assign_pruned_kernel<TX, NCH, RR>), dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, XP, d, \
-                       C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows)
-    if (X.f64) {
-        if (wide) XP_LAUNCH(double, 16, 2, X.d()); else XP_LAUNCH(double, 4, XP_R, X.d());
+#define XP_LAUNCH(TX, NCH, RR, MT, XP)                                                                              \
+    hipLaunchKernelGGL((assign_pruned_kernel<TX, NCH, RR, MT>), dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, XP, \
+                       d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows)
+    if (metric == 1) {
+        if (X.f64) {
+            if (wide) XP_LAUNCH(double, 16, 2, 1, X.d()); else XP_LAUNCH(double, 4, XP_R, 1, X.d());
+        } else {
+            if (wide) XP_LAUNCH(float, 16, 2, 1, X.f()); else XP_LAUNCH(float, 4, XP_R, 1, X.f());
+        }
+    } else if (X.f64) {
+        if (wide) XP_LAUNCH(double, 16, 2, 0, X.d()); else XP_LAUNCH(double, 4, XP_R, 0, X.d());
     } else {
-        if (wide) XP_LAUNCH(float, 16, 2, X.f()); else XP_LAUNCH(float, 4, XP_R, X.f());
+        if (wide) XP_LAUNCH(float, 16, 2, 0, X.f()); else XP_LAUNCH(float, 4, XP_R, 0, X.f());
     }
 #undef XP_LAUNCH
     return kstatus("assign_pruned_kernel");

@@ -49,6 +49,36 @@ __device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __re
     return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
 }
 
+// exact_cosine_x87 for an fp32 row of d % 16 == 0 (16-B aligned rows): the row
+// and the centroid loaded 16 values at a time, so the soft chain waits on one
+// round trip per 16 terms instead of one per term.
+__device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
+    sx80 ip = sx_zero();
+    double a = 0.0, b = 0.0;
+    for (int j0 = 0; j0 < d; j0 += 16) {
+        float xs[16];
+        double cs[16];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const float4 v = *reinterpret_cast<const float4*>(x + j0 + 4 * t);
+            xs[4 * t] = v.x; xs[4 * t + 1] = v.y; xs[4 * t + 2] = v.z; xs[4 * t + 3] = v.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const double2 v = *reinterpret_cast<const double2*>(c + j0 + 2 * t);
+            cs[2 * t] = v.x; cs[2 * t + 1] = v.y;
+        }
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const double xj = (double)xs[t], cj = cs[t];
+            ip = sx_add_double(ip, __dmul_rn(xj, cj));
+            a = __dadd_rn(a, __dmul_rn(xj, xj));
+            b = __dadd_rn(b, __dmul_rn(cj, cj));
+        }
+    }
+    return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
+}
+
 // Certified fast form of the x87 inner product's quotient (~12 fp64 ops per
 // element instead of a soft-x87 add). The products p_j are the reference's
 // doubles; their sum is carried exactly enough as a double-double (TwoSum),

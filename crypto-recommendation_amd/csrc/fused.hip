@@ -1893,7 +1893,7 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const float* __restric
     const unsigned long long* l = list + (int64_t)seg * seg_rows;
     for (int i = part * 256 + threadIdx.x; i < n; i += CF_SPLIT * 256) {
         const int64_t row = (int64_t)l[i];
-        dist[row] = exact_cosine_x87(X + row * FU_D, C + (size_t)assign[row] * FU_D, FU_D);
+        dist[row] = exact_cosine_x87_b16(X + row * FU_D, C + (size_t)assign[row] * FU_D, FU_D);
     }
 }
 

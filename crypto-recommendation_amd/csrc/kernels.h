@@ -103,7 +103,7 @@ int launch_assign_exact_list(hipStream_t s, Pts X, int d, const double* C, int K
 int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
-                              int64_t seg_rows = 0, int nseg = 0);
+                              int64_t seg_rows = 0, int nseg = 0, int metric = 0);
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist);
 
