@@ -501,7 +501,14 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
     hipStream_t s = ctx->stream;
     const int DP = assign_dp(d);
     const int path = assign_path(metric, d, K, X.f64);
-    const bool fuse_hash = lsh && path == 0 && metric == LSHKM_METRIC_EUCLIDEAN && lsh->proj.fused_ok;
+    // one pass for hashing + assignment: the euclidean index with euclidean
+    // Lloyd (fused_ok: d = 128, L*k <= 32), or the cosine index with cosine Lloyd
+    // on the hi-only form (k = 4)
+    const char* fh0 = getenv("LSHKM_FUSED_HI");
+    const bool hi_form = !(fh0 && !strcmp(fh0, "0"));
+    const bool fuse_hash = lsh && path == 0 && lsh->metric == metric &&
+                           (metric == LSHKM_METRIC_EUCLIDEAN ? lsh->proj.fused_ok
+                                                             : (hi_form && lsh->proj.mfma_ok && lsh->proj.k == 4));
     int rc;
     if (lsh && !fuse_hash && (rc = hash_rows(ctx, lsh->metric == LSHKM_METRIC_EUCLIDEAN ? HM_LSH_EUCLID : HM_LSH_COSINE,
                                              X, N, lsh->proj, lsh->nb,
@@ -519,14 +526,15 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4 + (size_t)Kpad * 8)) ||
             (rc = ctx->ws_ambig.reserve((size_t)(N + FUSED_LIST_SLACK) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
             (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)) ||
-            ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8 * (cosine && hi ? 2 : 1)))) ||
+            ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8 * (cosine && hi ? 3 : 1)))) ||
+            (cosine && hi && (rc = ctx->ws_seg3.reserve((size_t)FUSED_MAX_SEGS * 2 * 4))) ||
             (Kpad > 256 && (rc = ctx->ws_part.reserve((size_t)part_tiles * 64 * 16))) ||
             (hi && ((rc = ctx->ws_ambig2.reserve((size_t)list_cap * 4)) ||
                     (rc = ctx->ws_seg2.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)))) ||
-            (fuse_hash && !tuples && (rc = ctx->ws_tuples.reserve((size_t)std::max<int64_t>(N, 1) * lsh->proj.LK * 4))))
+            (fuse_hash && !cosine && !tuples && (rc = ctx->ws_tuples.reserve((size_t)std::max<int64_t>(N, 1) * lsh->proj.LK * 4))))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
-        LSHKM_HIP(hipMemsetAsync(cnt, 0, 24, s));         // [0] ambiguous rows, [1] hash fix-up rows, [2] refined rows
+        LSHKM_HIP(hipMemsetAsync(cnt, 0, 32, s));         // [0] ambiguous rows, [1] hash fix-up rows, [2] refined rows, [3] cosine declines
         _Float16* Ch = (_Float16*)ctx->ws_c32.p;
         _Float16* Cl = Ch + (size_t)Kpad * 128;
         float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
@@ -548,16 +556,23 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             f.refined = cnt + 2;
         }
         if (cosine) {
+            // ws_hfix regions: [hash fix-ups][declines of the hi-only pass][declines of the refinement]
             f.metric = 1; f.nbv = nbv;
-            f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
-            if (hi) f.hfix2 = f.hfix + (N + FUSED_LIST_SLACK);
+            f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = hi ? cnt + 1 : cnt + 3;
+            if (hi) {
+                f.cfix = f.hfix + (N + FUSED_LIST_SLACK);
+                f.cfix_counts = (int32_t*)ctx->ws_seg3.p;
+                f.cfix_count = cnt + 3;
+                f.hfix2 = f.cfix + (N + FUSED_LIST_SLACK);
+            }
         }
         if (fuse_hash) {
             const ProjTable& pj = lsh->proj;
             f.Vh = pj.vh_d.as<_Float16>(); f.Vl = pj.vl_d.as<_Float16>(); f.PT = pj.PT_d.as<double>();
             f.tv = pj.t_d.as<float>(); f.pnorm = pj.pn_d.as<double>(); f.v1 = pj.v1_d.as<double>();
             f.rv = pj.r_d.as<int32_t>(); f.w = pj.w; f.L = pj.L; f.k = pj.k; f.LK = pj.LK; f.LKpad = pj.LKpad;
-            f.nb = lsh->nb; f.tuples = tuples ? tuples : (int32_t*)ctx->ws_tuples.p; f.phi = phi; f.bucket = bucket;
+            f.nb = lsh->nb; f.phi = phi; f.bucket = bucket;
+            f.tuples = cosine ? nullptr : tuples ? tuples : (int32_t*)ctx->ws_tuples.p;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
         }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
@@ -571,7 +586,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             for (int li = 0; li < f.ncos_lists; li++)
                 if ((rc = launch_cos_fix_seg(s, X.f(), C, f.cos_list[li], f.cos_counts[li], f.seg_rows, f.nseg, assign,
                                              dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
-            if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 3))) { LSHKM_LAUNCH_CHECK(); return rc; }
         }
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;
@@ -618,13 +633,14 @@ static int lloyd_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, i
 }
 
 static int hash_assign_impl(lshkm_lsh lsh, Pts X, int64_t N, const double* C, int K, const int32_t* src_rows_host,
-                            int32_t* tuples, int32_t* phi, int32_t* bucket, int32_t* assign, double* dist) {
+                            int32_t* tuples, int32_t* phi, int32_t* bucket, int32_t* assign, double* dist,
+                            int metric = LSHKM_METRIC_EUCLIDEAN) {
     LSHKM_CHECK(lsh && (X.p || N == 0) && C && (assign || N == 0) && (dist || N == 0) && N >= 0 && K > 0, LSHKM_ERR_ARG,
                 "bad arguments");
     lshkm_ctx ctx = lsh->ctx;
     LSHKM_HIP(hipSetDevice(ctx->device));
-    return assign_impl(ctx, X, N, lsh->proj.d, C, K, LSHKM_METRIC_EUCLIDEAN, src_rows_host, assign, dist, lsh, tuples,
-                       phi, bucket);
+    LSHKM_CHECK(metric == LSHKM_METRIC_EUCLIDEAN || metric == LSHKM_METRIC_COSINE, LSHKM_ERR_ARG, "unknown metric");
+    return assign_impl(ctx, X, N, lsh->proj.d, C, K, metric, src_rows_host, assign, dist, lsh, tuples, phi, bucket);
 }
 
 static int range_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, int K, int metric,
@@ -739,6 +755,18 @@ int lshkm_hash_assign_f64(lshkm_lsh lsh, const double* X, int64_t N, const doubl
                           const int32_t* src_rows_host, int32_t* tuples, int32_t* phi, int32_t* bucket,
                           int32_t* assign, double* dist) {
     return hash_assign_impl(lsh, X, N, C, K, src_rows_host, tuples, phi, bucket, assign, dist);
+}
+
+int lshkm_hash_assign_metric(lshkm_lsh lsh, const float* X, int64_t N, const double* C, int K, int metric,
+                             const int32_t* src_rows_host, int32_t* tuples, int32_t* phi, int32_t* bucket,
+                             int32_t* assign, double* dist) {
+    return hash_assign_impl(lsh, X, N, C, K, src_rows_host, tuples, phi, bucket, assign, dist, metric);
+}
+
+int lshkm_hash_assign_metric_f64(lshkm_lsh lsh, const double* X, int64_t N, const double* C, int K, int metric,
+                                 const int32_t* src_rows_host, int32_t* tuples, int32_t* phi, int32_t* bucket,
+                                 int32_t* assign, double* dist) {
+    return hash_assign_impl(lsh, X, N, C, K, src_rows_host, tuples, phi, bucket, assign, dist, metric);
 }
 
 int lshkm_range_assign(lshkm_ctx ctx, const float* X, int64_t N, int d, const double* C, int K, int metric,

@@ -116,6 +116,11 @@ struct FusedArgs {
     unsigned long long* ambig_count;
     unsigned long long* hfix;        // persistent form: rows with an uncertified floor
     unsigned long long* hfix_count;
+    // hi-only cosine form: rows whose winner distance the certified quotient
+    // declined (cos_fix_seg pass); counts in cfix_counts[2b + 1]
+    unsigned long long* cfix;
+    int32_t* cfix_counts;
+    unsigned long long* cfix_count;
     unsigned long long* stats;
     // persistent form: block b owns ambig/hfix entries [b * seg_rows, (b+1) * seg_rows)
     // and reports their counts in seg_counts[2b] (ambiguous), seg_counts[2b+1] (fix-up)
@@ -1123,8 +1128,10 @@ constexpr int FH_WAVES = FH_WAVES_SET;
 constexpr int FH_THREADS = 64 * FH_WAVES;
 
 // MET = 1: cosine (the prep's normalised centroid rows, score x.c^ with no
-// offset; the winner's distance by cosine_fast_nb, declines to the fix-up
-// list as in fused_persistent_kernel<., 1>). No hashing with cosine.
+// offset; the winner's distance from the row in registers, declines to the
+// cfix list). HASH with MET = 1: CosineHGen signs of the L*k projections
+// (k = 4: table l = 2g + h in D registers 4g..4g+3), certified as in
+// hash_mfma.hip, g = phi = bucket; uncertified signs to the hfix list.
 // Cosine winner distance from the row in registers, both lane halves busy.
 // Lane half h owns dims 16s + 8h..+7 (s = 0..7). Each half accumulates the
 // double products of ITS dims with IpAcc's double-double (exact.h), in its own
@@ -1208,10 +1215,9 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
 
 template <bool HASH, bool MP = false, int MET = 0>
 __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
-    static_assert(!(HASH && MET == 1), "the hi-only cosine form does not hash");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
-    int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows
+    int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows, [2] cosine declines
     _Float16* lch = reinterpret_cast<_Float16*>(smem + 16);
     float* lcn = reinterpret_cast<float*>(lch + Kpad * FU_RS);
     _Float16* lvh = reinterpret_cast<_Float16*>(lcn + Kpad);
@@ -1226,9 +1232,10 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
         *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Ch + (size_t)r * FU_D + g * 8);
     }
     for (int e = threadIdx.x; e < Kpad; e += FH_THREADS) lcn[e] = a.cnh[e];
-    if (threadIdx.x < 2) lcount[threadIdx.x] = 0;
+    if (threadIdx.x < 3) lcount[threadIdx.x] = 0;
     int32_t* ambig_seg = a.ambig + (int64_t)blockIdx.x * a.seg_rows;
     unsigned long long* hfix_seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
+    unsigned long long* cfix_seg = MET == 1 ? a.cfix + (int64_t)blockIdx.x * a.seg_rows : nullptr;
     if (HASH) {
         for (int e = threadIdx.x; e < 32 * 16; e += FH_THREADS) {
             const int r = e >> 4, g = e & 15;
@@ -1238,12 +1245,15 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
         if (threadIdx.x < 32) {
             const int f = threadIdx.x;
             const bool on = f < a.LK;
-            const double iwu = (double)(1.0f / a.w) * (1.0 + 0x1p-20);
+            // euclidean: the window in units of y = (acc + t) / w; cosine: of the
+            // inner product itself (hash_mfma.hip)
+            const double iwu = MET == 1 ? 1.0 : (double)(1.0f / a.w) * (1.0 + 0x1p-20);
+            const double tf = MET == 1 || !on ? 0.0 : fabs((double)a.tv[f]);
             lpn0[f] = on ? (float)((FU_A1H * a.pnorm[f] * (1.0 + 0x1p-20) + FU_A2 * FU_SQRT_D) * iwu * (1.0 + 0x1p-18)) : 0.f;
-            lv10[f] = on ? (float)((FU_A2 * a.v1[f] * (1.0 + 0x1p-20) + (0x1p-40 + 0x1p-23) * fabs((double)a.tv[f])) *
-                                   iwu * (1.0 + 0x1p-18)) : 0.f;
-            lt0[f] = on ? a.tv[f] : 0.f;
-            lr0[f] = on ? a.rv[f] : 0;
+            lv10[f] = on ? (float)((FU_A2 * a.v1[f] * (1.0 + 0x1p-20) + (0x1p-40 + 0x1p-23) * tf) * iwu * (1.0 + 0x1p-18) +
+                                   0x1p-126) : 0.f;
+            lt0[f] = on && MET == 0 ? a.tv[f] : 0.f;
+            lr0[f] = on && MET == 0 ? a.rv[f] : 0;
         }
     }
     __syncthreads();
@@ -1355,7 +1365,7 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
             }
             finish_norms();
             // the floor certificate of fused_persistent_kernel (same bound)
-            const float iw = 1.0f / a.w;
+            const float iw = MET == 1 ? 1.f : 1.0f / a.w;
             const float nxf = (float)nx * (1.f + 0x1p-20f);
             constexpr float G = (0x1p-22f + 0x1p-20f) * (1.f + 0x1p-18f);
             int hc = 0;
@@ -1369,6 +1379,23 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
             for (int g = 0; g < 4; g++) {
                 const int l = 2 * g + h;
                 if (l >= a.L || !valid) continue;
+                const int64_t o = row * a.L + l;
+                if constexpr (MET == 1) {
+                    // CosineHGen: ip >= 0, certified when |acc~| exceeds the window;
+                    // CosineGGen: g = bits MSB first
+                    int gv = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int f = 4 * l + q;
+                        const float u = acc_hi[4 * g + q];
+                        const float B = fmaf(nxf, lP[f], lQ[f]);
+                        gv = (gv << 1) | (u >= 0.f ? 1 : 0);
+                        if (!(fabsf(u) > B)) fmask |= 1u << f;
+                    }
+                    if (a.phi) a.phi[o] = gv;
+                    if (a.bucket) a.bucket[o] = gv;
+                    continue;
+                }
                 int32_t hv[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -1380,7 +1407,6 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
                     hv[q] = (int32_t)lo;
                     if (lo != hi) fmask |= 1u << f;
                 }
-                const int64_t o = row * a.L + l;
                 if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
                 uint32_t hn = 0;
 #pragma unroll
@@ -1487,9 +1513,9 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
             if (fb) {
                 const int leader = __builtin_ctzll(fb);
                 int base = 0;
-                if (lane == leader) base = atomicAdd(lcount + 1, __popcll(fb));
+                if (lane == leader) base = atomicAdd(lcount + 2, __popcll(fb));
                 base = __shfl(base, leader);
-                if (fix) hfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
+                if (fix) cfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
             }
         } else {
 #if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
@@ -1546,11 +1572,15 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
         }
     }
     __syncthreads();
-    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? (!HASH && a.pass_last != 0)
-                                                      : ((HASH && a.pass_first) || (MET == 1 && a.pass_last))))) {
+    if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? (!HASH && a.pass_last != 0) : (HASH && a.pass_first)))) {
         const int c = lcount[threadIdx.x];
         a.seg_counts[2 * blockIdx.x + threadIdx.x] = c;
         if (c) atomicAdd(threadIdx.x == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
+    }
+    if (MET == 1 && threadIdx.x == 2 && (!MP || (!HASH && a.pass_last))) {
+        const int c = lcount[2];
+        a.cfix_counts[2 * blockIdx.x + 1] = c;
+        if (c) atomicAdd(a.cfix_count, (unsigned long long)c);
     }
 }
 
@@ -1628,6 +1658,78 @@ __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) 
             const uint32_t ph = phi_final(hn);
             if (a.phi) a.phi[row * a.L + l] = (int32_t)ph;
             if (a.bucket) a.bucket[row * a.L + l] = bucket_of(ph, a.nb);
+        }
+    }
+}
+
+// The cosine form's listed signs (CosineHGen, cosine_h_gen.hpp:67-76): the
+// flagged functions by the fp64 FMA chain over the fp64 rows of R with
+// hash.hip's bound, else the soft-x87 sign; the touched tables' g bits patched
+// in phi / bucket (the other bits are certified).
+constexpr size_t HFC_LDS = (size_t)FU_D * 32 * 8;     // R, fp64
+__global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_cos_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* pts = reinterpret_cast<double*>(smem);   // [128][LKpad]
+    const int seg = blockIdx.x / HF_SPLIT, part = blockIdx.x % HF_SPLIT;
+    const int n = a.seg_counts[2 * seg + 1];
+    if (n == 0) return;                                                 // block-uniform
+    const unsigned long long* list = a.hfix + (int64_t)seg * a.seg_rows;
+    const int LKpad = a.LKpad, k = a.k;
+    for (int e = threadIdx.x; e < FU_D * LKpad; e += 64 * HF_WAVES) pts[e] = a.PT[e];
+    __syncthreads();
+    const uint32_t kmask = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
+    for (int e = part * 64 * HF_WAVES + threadIdx.x; e < n; e += HF_SPLIT * 64 * HF_WAVES) {
+        const unsigned long long ent = list[e];
+        const int64_t row = (int64_t)(ent >> 32);
+        const uint32_t mask = (uint32_t)ent;
+        const float* xrow = a.X + row * FU_D;
+        uint32_t bits = 0;
+        for (uint32_t m = mask; m; m &= m - 1) {
+            const int f = __builtin_ctz(m);
+            double acc = 0.0, xn2 = 0.0;
+#pragma unroll 1
+            for (int c = 0; c < FU_D; c += 32) {
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const float4*>(xrow + c + 4 * u);
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float xs[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const double xj = (double)xs[q];
+                        xn2 = fma(xj, xj, xn2);
+                        acc = fma(pts[(c + 4 * u + q) * LKpad + f], xj, acc);
+                    }
+                }
+            }
+            const double P = a.pnorm[f] * sqrt(xn2) * (1.0 + 0x1p-40);
+            const double B = (double)(FU_D + 3) * 0x1p-52 * P + 0x1p-1000;
+            int bit;
+            if (acc > B && acc < 0x1p1000) bit = 1;
+            else if (acc < -B && acc > -0x1p1000) bit = 0;
+            else {
+                SxSum sx;
+                sx.init();
+                for (int j = 0; j < FU_D; j++) sx.add(__dmul_rn(pts[j * LKpad + f], (double)xrow[j]));
+                bit = sx_hash_sign(sx);
+                atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
+            }
+            bits |= (uint32_t)bit << f;
+        }
+        for (int l = 0; l < a.L; l++) {
+            if (!(mask & (kmask << (l * k)))) continue;
+            int32_t* gout = a.bucket ? a.bucket : a.phi;
+            int gv = gout[row * a.L + l];
+            for (int i = 0; i < k; i++) {
+                const int f = l * k + i;
+                if (mask & (1u << f)) {
+                    const int b = 1 << (k - 1 - i);
+                    gv = (bits >> f) & 1u ? (gv | b) : (gv & ~b);
+                }
+            }
+            if (a.phi) a.phi[row * a.L + l] = gv;
+            if (a.bucket) a.bucket[row * a.L + l] = gv;
         }
     }
 }
@@ -1727,6 +1829,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.tuples = f.tuples; a.phi = f.phi; a.bucket = f.bucket; a.assign = f.assign; a.dist = f.dist;
     a.ambig = f.ambig; a.ambig_count = f.ambig_count; a.stats = f.stats;
     a.hfix = f.hfix; a.hfix_count = f.hfix_count;
+    a.cfix = f.cfix; a.cfix_counts = f.cfix_counts; a.cfix_count = f.cfix_count;
     a.bdiv = make_bucket_div(f.nb);
     a.nbv = f.nbv;
     a.part = nullptr; a.t0 = 0; a.pass_first = 1; a.pass_last = 1;
@@ -1755,8 +1858,12 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         set_error("launch_fused: pass-state buffer too small for the refinement");
         return -1;
     }
-    if (f.metric == 1 && (hash || chunked || !multi_ok || !f.nbv || !f.hfix || !f.hfix_count)) {
-        set_error("launch_fused: cosine runs the persistent form only (no hashing, fix-up list, pass state)");
+    if (f.metric == 1 && (chunked || !multi_ok || !f.nbv || !f.hfix || !f.hfix_count || (hash && (!f.hi || f.k != 4)))) {
+        set_error("launch_fused: cosine runs the persistent form only (hashing: the hi-only form with k = 4)");
+        return -1;
+    }
+    if (f.metric == 1 && f.hi && (!f.cfix || !f.cfix_counts || !f.cfix_count)) {
+        set_error("launch_fused: the hi-only cosine form needs the decline list");
         return -1;
     }
     if (!chunked && multi_ok && (!hash || f.k == 4)) {
@@ -1786,7 +1893,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         }
         f.nseg = nblk;
         f.seg_rows = a.seg_rows;
-        if (hash && (!a.hfix || !a.hfix_count || !a.tuples || f.LKpad > 32)) {   // pts[] holds 128 x 32 projections
+        if (hash && (!a.hfix || !a.hfix_count || (f.metric == 0 && !a.tuples) || f.LKpad > 32)) {   // pts[] holds 128 x 32 projections
             set_error("launch_fused: hashing needs the fix-up list, a tuple buffer and L*k <= 32");
             return -1;
         }
@@ -1813,8 +1920,13 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 const size_t lh = (size_t)fh_lds_bytes(a.Kpad, hash && p == 0);
                 const dim3 hblock(FH_THREADS);
                 if (cos) {
-                    if (np1 == 1) hipLaunchKernelGGL((fused_hi_kernel<false, false, 1>), grid, hblock, lh, s, a);
-                    else hipLaunchKernelGGL((fused_hi_kernel<false, true, 1>), grid, hblock, lh, s, a);
+                    if (np1 == 1) {
+                        if (hash) hipLaunchKernelGGL((fused_hi_kernel<true, false, 1>), grid, hblock, lh, s, a);
+                        else hipLaunchKernelGGL((fused_hi_kernel<false, false, 1>), grid, hblock, lh, s, a);
+                    } else {
+                        if (hash && p == 0) hipLaunchKernelGGL((fused_hi_kernel<true, true, 1>), grid, hblock, lh, s, a);
+                        else hipLaunchKernelGGL((fused_hi_kernel<false, true, 1>), grid, hblock, lh, s, a);
+                    }
                 } else if (np1 == 1) {
                     if (hash) hipLaunchKernelGGL((fused_hi_kernel<true>), grid, hblock, lh, s, a);
                     else hipLaunchKernelGGL((fused_hi_kernel<false>), grid, hblock, lh, s, a);
@@ -1823,11 +1935,12 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                     else hipLaunchKernelGGL((fused_hi_kernel<false, true>), grid, hblock, lh, s, a);
                 }
             }
-            if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
+            if (hash && cos) hipLaunchKernelGGL(hash_fixup_cos_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HFC_LDS, s, a);
+            else if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
             FusedArgs r = a;
             r.list_in = f.ambig; r.list_counts = f.seg_counts; r.list_seg_rows = a.seg_rows;
             r.ambig = f.list2; r.seg_counts = f.seg_counts2; r.ambig_count = f.ambig_count;
-            r.hfix = cos ? f.hfix2 : f.hfix; r.hfix_count = f.hfix_count;
+            r.hfix = cos ? f.hfix2 : f.hfix; r.hfix_count = cos ? f.cfix_count : f.hfix_count;
             r.Cl = f.Cl;
             r.tuples = nullptr; r.phi = nullptr; r.bucket = nullptr;
             for (int p = 0; p < npass; p++) {
@@ -1847,7 +1960,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             f.final_counts = f.seg_counts2;
             if (cos) {
                 f.ncos_lists = 2;
-                f.cos_list[0] = f.hfix; f.cos_counts[0] = f.seg_counts;
+                f.cos_list[0] = f.cfix; f.cos_counts[0] = f.cfix_counts;
                 f.cos_list[1] = f.hfix2; f.cos_counts[1] = f.seg_counts2;
             }
             return kstatus("fused_hi_kernel");

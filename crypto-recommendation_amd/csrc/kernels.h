@@ -234,6 +234,11 @@ struct FusedLaunch {
     // fix-up list (hfix2: [list_cap] entries after the first); out: the lists
     // for cos_fix_seg, (list, segment counts) pairs
     unsigned long long* hfix2 = nullptr;
+    // hi-only cosine: the hi-only pass's declined winner distances ([list_cap]
+    // entries, counts in cfix_counts[2b + 1], total in cfix_count)
+    unsigned long long* cfix = nullptr;
+    int32_t* cfix_counts = nullptr;
+    unsigned long long* cfix_count = nullptr;
     int ncos_lists = 0;
     const unsigned long long* cos_list[2] = {nullptr, nullptr};
     const int32_t* cos_counts[2] = {nullptr, nullptr};

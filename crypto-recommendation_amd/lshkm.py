@@ -93,6 +93,7 @@ def lib():
             "lshkm_config_value": (i32, [C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(i32)]),
             "lshkm_config_load": (i32, [C.c_char_p, vp]),
             "lshkm_hash_assign": (i32, [vp, vp, i64, vp, i32, vp, vp, vp, vp, vp, vp]),
+            "lshkm_hash_assign_metric": (i32, [vp, vp, i64, vp, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
             "lshkm_kmeans_partial_carry": (i32, [vp, vp, i64, i32, vp, i32, vp, vp, vp, vp]),
@@ -454,18 +455,25 @@ def read_vectors(path, delimiter=",", strt_line=1, threads=0):
         lib().lshkm_vectors_free(h)
 
 
-def hash_assign(lsh, X, Cc, src_rows=None, tuples=True, phi=False, bucket=True):
-    """LSH hashing + Lloyd assignment in one pass. Returns (tuples, phi, bucket, assign, dist)."""
+def hash_assign(lsh, X, Cc, src_rows=None, tuples=True, phi=False, bucket=True, metric=None):
+    """LSH hashing + Lloyd assignment in one pass. Returns (tuples, phi, bucket, assign, dist).
+    metric None: euclidean Lloyd (lshkm_hash_assign); else the assignment metric
+    (lshkm_hash_assign_metric: a cosine index with cosine Lloyd is one pass)."""
     ctx, torch = lsh.ctx, lsh.ctx.torch
     N = X.shape[0]
-    tu = ctx.empty((N, lsh.L, lsh.k), torch.int32) if tuples else None
+    tu = ctx.empty((N, lsh.L, lsh.k), torch.int32) if (tuples and lsh.metric == EUCLIDEAN) else None
     ph = ctx.empty((N, lsh.L), torch.int32) if phi else None
     bu = ctx.empty((N, lsh.L), torch.int32) if bucket else None
     a = ctx.empty((N,), torch.int32)
     dist = ctx.empty((N,), torch.float64)
     sr = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
-    _ck(_fn("lshkm_hash_assign", X)(lsh.h, _t_ptr(X), N, _t_ptr(Cc), Cc.shape[0], _np_ptr(sr), _t_ptr(tu), _t_ptr(ph),
-                                _t_ptr(bu), _t_ptr(a), _t_ptr(dist)))
+    if metric is None:
+        _ck(_fn("lshkm_hash_assign", X)(lsh.h, _t_ptr(X), N, _t_ptr(Cc), Cc.shape[0], _np_ptr(sr), _t_ptr(tu),
+                                        _t_ptr(ph), _t_ptr(bu), _t_ptr(a), _t_ptr(dist)))
+    else:
+        _ck(_fn("lshkm_hash_assign_metric", X)(lsh.h, _t_ptr(X), N, _t_ptr(Cc), Cc.shape[0], _METRIC[metric],
+                                               _np_ptr(sr), _t_ptr(tu), _t_ptr(ph), _t_ptr(bu), _t_ptr(a),
+                                               _t_ptr(dist)))
     return tu, ph, bu, a, dist
 
 

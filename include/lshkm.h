@@ -223,6 +223,16 @@ int lshkm_hash_assign(lshkm_lsh lsh, const float* X_dev, int64_t N, const double
 int lshkm_hash_assign_f64(lshkm_lsh lsh, const double* X_dev, int64_t N, const double* C_dev, int K,
                           const int32_t* src_rows_host, int32_t* tuples_dev, int32_t* phi_dev, int32_t* bucket_dev,
                           int32_t* assign_dev, double* dist_dev);
+/* The same with the assignment metric chosen (lshkm_hash_assign is euclidean
+ * Lloyd): main.cpp's cosine flow (main.cpp:150-160, 196) hashes with the
+ * cosine family and clusters with cosineDistance. One read of X when the index
+ * metric equals the assignment metric, d = 128, L*k <= 32 (cosine: k = 4). */
+int lshkm_hash_assign_metric(lshkm_lsh lsh, const float* X_dev, int64_t N, const double* C_dev, int K, int metric,
+                             const int32_t* src_rows_host, int32_t* tuples_dev, int32_t* phi_dev, int32_t* bucket_dev,
+                             int32_t* assign_dev, double* dist_dev);
+int lshkm_hash_assign_metric_f64(lshkm_lsh lsh, const double* X_dev, int64_t N, const double* C_dev, int K,
+                                 int metric, const int32_t* src_rows_host, int32_t* tuples_dev, int32_t* phi_dev,
+                                 int32_t* bucket_dev, int32_t* assign_dev, double* dist_dev);
 /* k_means (update.hpp:37-86): exact-order per-cluster fp64 sums in row order,
  * divided by the count unless empty; *cont_host = 1 iff some center moved
  * more than min_dist. C_new_dev [K][d], counts_dev [K] (may be NULL). */

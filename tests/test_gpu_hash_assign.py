@@ -379,3 +379,56 @@ def test_multipass_persistent_k1024(ctx, metric, monkeypatch):
     oa, od = oracle.lloyd_assign(X.cpu().numpy()[sub], Cc.cpu().numpy(), metric, None)
     assert np.array_equal(a0.cpu().numpy()[sub], oa)
     assert np.array_equal(d0.cpu().numpy()[sub].view(np.uint64), od.view(np.uint64))
+
+
+@pytest.mark.parametrize("N,K,case", [(200_000, 256, "rows"), (50_000, 1000, "rows"), (30_011, 64, "special"),
+                                      (40_000, 200, "scaled")])
+def test_cosine_hash_assign_fused(ctx, N, K, case):
+    # main.cpp's cosine flow in one pass (lshkm_hash_assign_metric): CosineGGen
+    # buckets and cosine Lloyd from the hi-only kernel with the hash tile, against
+    # the two separate calls and the oracle
+    d, L, k = 128, 5, 4
+    Xh = oracle.synth(0xC0 + K, N, d).copy()
+    rng = np.random.default_rng(K)
+    if case == "special":
+        Xh[5] = 0.0                                   # zero row: NaN distances, bits of exact zeros
+        Xh[9] *= np.float32(4e4)                      # beyond the f16 range guard
+        Xh[11, :] = np.round(Xh[11, :] * 4) / 4
+    X = to_dev(ctx, Xh)
+    R, _ = lshkm.params_lsh_cosine(21, L, k, d)
+    lsh = lshkm.LSH(ctx, "cosine", d, k, L, R=R)
+    Ch = Xh[rng.choice(N, K, replace=False)].astype(np.float64)
+    if case == "scaled":
+        Ch *= rng.uniform(1e-3, 1e3, (K, 1))
+    C = to_dev(ctx, Ch)
+    ctx.reset_stats()
+    _, ph, bu, a, dist = lshkm.hash_assign(lsh, X, C, phi=True, bucket=True, metric="cosine")
+    _, ph2, bu2 = lsh.hash(X, tuples=False)
+    a2, d2 = lshkm.lloyd_assign(ctx, X, C, "cosine")
+    assert np.array_equal(ph.cpu().numpy(), ph2.cpu().numpy())
+    assert np.array_equal(bu.cpu().numpy(), bu2.cpu().numpy())
+    assert np.array_equal(a.cpu().numpy(), a2.cpu().numpy())
+    assert np.array_equal(dist.cpu().numpy().view(np.uint64), d2.cpu().numpy().view(np.uint64))
+    sub = np.random.default_rng(1).choice(N, 1200, replace=False)
+    sub = np.union1d(sub, [5, 9, 11]) if case == "special" else sub
+    og = oracle.lsh_hash_cosine(Xh[sub], R.reshape(L, k, d))
+    assert np.array_equal(bu.cpu().numpy()[sub], og)
+    oa, od = oracle.lloyd_assign(Xh[sub], Ch, "cosine", None)
+    assert np.array_equal(a.cpu().numpy()[sub], oa)
+    assert np.array_equal(dist.cpu().numpy()[sub].view(np.uint64), od.view(np.uint64))
+
+
+@pytest.mark.parametrize("name", [n for n in cases("lsh") if "_c" in n])
+def test_cosine_hash_assign_golden(ctx, name):
+    # golden lsh_c* (the reference's CosineGGen buckets) through the fused cosine pass
+    m, g = META[name], golden(name)
+    Xh = oracle.synth(m["data_seed"], m["N"], m["d"])
+    X = to_dev(ctx, Xh)
+    lsh = lshkm.LSH(ctx, "cosine", m["d"], m["k"], m["L"], R=g["R"])
+    K = min(16, m["N"])
+    Ch = Xh[:K].astype(np.float64)
+    _, _, bu, a, dist = lshkm.hash_assign(lsh, X, to_dev(ctx, Ch), bucket=True, metric="cosine")
+    assert np.array_equal(bu.cpu().numpy(), g["bucket"])
+    oa, od = oracle.lloyd_assign(Xh, Ch, "cosine", None)
+    assert np.array_equal(a.cpu().numpy(), oa)
+    assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))

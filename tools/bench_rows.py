@@ -99,9 +99,17 @@ def main():
             Xh = X[:n].cpu().numpy()
             c = (n, cpu_time(lambda: oracle.lloyd_assign(Xh, C.cpu().numpy(), "cosine", None)), f"{n} rows, K={K}")
         emit("lloyds_assignment (cosine)", "rows/s", N, t, c,
-             f"N=10M, d=128, K=256; split-f16 persistent kernel (normalised centroids), {amb:.0f} rows/call to the exact pass, "
-             f"{cfix:.0f} winner distances/call to the soft-x87 chain; "
+             f"N=10M, d=128, K=256; hi-only f16 kernel (normalised centroids), {amb:.0f} rows/call to the pruned exact "
+             f"pass, {cfix:.0f} winner distances/call to the soft-x87 chain; "
              f"exact all-K pass alone {te * 1e3:.1f} ms")
+        # main.cpp's cosine flow in one pass: CosineGGen buckets (L=5, k=4) + cosine Lloyd
+        R, _ = lshkm.params_lsh_cosine(12345, 5, 4, d)
+        lsh = lshkm.LSH(ctx, "cosine", d, 4, 5, R=R)
+        th = gpu_time(ctx, lambda: lshkm.hash_assign(lsh, X, C, tuples=False, bucket=True, metric="cosine"))
+        tsep = gpu_time(ctx, lambda: (lsh.hash(X, tuples=False, phi=False), lshkm.lloyd_assign(ctx, X, C, "cosine")))
+        emit("hash_assign (cosine LSH + cosine Lloyd)", "rows/s", N, th, None,
+             f"N=10M, d=128, L=5, k=4, K=256, one pass (lshkm_hash_assign_metric); the two separate calls "
+             f"{tsep * 1e3:.2f} ms")
         del X
 
     if "kpp" in rows:        # k_means_pp (initialization.hpp:71-156)
