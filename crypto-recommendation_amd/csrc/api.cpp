@@ -335,7 +335,11 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
     LSHKM_HIP(hipMemcpyAsync(r_d.p, rr.data(), LK * 4, hipMemcpyHostToDevice, s));
     // split-f16 image for the fused hash+assign kernel (euclidean) and the
     // MFMA hash (either metric; cosine splits the fp64 rows of R)
-    fused_ok = metric == LSHKM_METRIC_EUCLIDEAN && d == 128 && LK <= 32;
+    // the fused kernels' phi arithmetic assumes the reference's r range
+    // [0, 100] (euclidean_phi_gen.hpp:64; tile.h phi_term_small)
+    bool r_small = true;
+    for (int f = 0; f < LK; f++) r_small = r_small && rr[f] >= 0 && rr[f] <= 100;
+    fused_ok = metric == LSHKM_METRIC_EUCLIDEAN && d == 128 && LK <= 32 && r_small;
     mfma_ok = d == 128 && LK <= 32;
     std::vector<_Float16> vh, vl;
     std::vector<double> v1;

@@ -80,10 +80,12 @@ __device__ inline uint32_t phi_final(uint32_t hn) {
 __device__ inline int32_t bucket_of(uint32_t ph, int64_t nb) {
     return nb <= 0xFFFFFFFFll ? (int32_t)(ph % (uint32_t)nb) : (int32_t)ph;
 }
-// Certified hashes have |h| < 2^22 and r <= 100, so h * r does not wrap and
-// ((temp % M) + M) % M is one select.
+// Certified hashes have |h| < 2^22 and r in [0, 100] (euclidean_phi_gen.hpp:64;
+// ProjTable::r_small), so h * r does not wrap, both operands fit 24 bits (one
+// full-rate v_mul_i32_i24 instead of a quarter-rate v_mul_lo_u32) and
+// ((temp % M) + M) % M is one select. Uncertified h are rewritten by the fix-up.
 __device__ inline uint32_t phi_term_small(int32_t h, int32_t r) {
-    const int32_t p = h * r;
+    const int32_t p = __mul24(h, r);
     return p < 0 ? (uint32_t)p + PHI_M : (uint32_t)p;
 }
 __device__ inline int32_t bucket_fast(uint32_t ph, const BucketDiv& b) {

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box routine (run through gpurun from the repo root):
-#   tools/gpu_run.sh TAG [tests|bench|prof|pmc]...
+#   tools/gpu_run.sh TAG [tests|bench|benchq|prof|pmc|pmc5|prof5|sq|rows]...
 # Each GPU step has its own time limit; the script stops at the first failure.
 set -u
 TAG=${1:?tag}; shift
@@ -54,6 +54,11 @@ for step in "$@"; do
            > "$OUT/sq$i.json" 2> "$OUT/sq$i.err")
         rc=$?; echo "sq pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    rows)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv \
+         -d "$OUT/rows_prof" -o run -- python3 "$R/tools/bench_rows.py" \
+         > "$OUT/rows.jsonl" 2> "$OUT/rows.err")
+      rc=$?; echo "rows rc=$rc"; cat "$OUT/rows.jsonl"; [ $rc -eq 0 ] || { tail -5 "$OUT/rows.err"; exit $rc; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
