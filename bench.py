@@ -179,8 +179,9 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(e.item())
-    ambig = ctx.stat(lk.STAT_ASSIGN_AMBIG)
-    hexact = ctx.stat(lk.STAT_HASH_EXACT)
+    ambig = ctx.stat(lk.STAT_ASSIGN_AMBIG) // args.steps
+    hexact = ctx.stat(lk.STAT_HASH_EXACT) // args.steps
+    hfix = ctx.stat(lk.STAT_HASH_FIX) // args.steps
 
     # Dominant kernel = the fused pass (fused_persistent_kernel<true> and its
     # hash_fixup_kernel; at K > 256 one launch per 256-centroid slice): HIP
@@ -246,7 +247,8 @@ def main():
                 "mfma": {"achieved_TFs": mfma_tfs, "peak_TFs": F16_MFMA_PEAK_TFS, "frac": mfma_tfs / F16_MFMA_PEAK_TFS,
                          "flop_per_point_executed": mfma_flop_per_pt, "flop_per_point_algorithmic": flop_per_pt},
             },
-            "exactness": {"assign_ambiguous_rows": ambig, "hash_exact_fallbacks": hexact},
+            "exactness": {"per_step": True, "assign_ambiguous_rows": ambig, "hash_fixup_rows": hfix,
+                          "hash_exact_fallbacks": hexact},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample, K)

@@ -585,6 +585,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.final_counts : nullptr,
                                f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (hi && (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_REFINED, cnt + 2))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if (fuse_hash && (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_HASH_FIX, cnt + 1))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (cosine) {
             for (int li = 0; li < f.ncos_lists; li++)

@@ -1483,153 +1483,225 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
     }
 }
 
-// Rows listed by the persistent form with an uncertified floor: fix-up pass.
+// Rows listed by the fused pass with an uncertified floor (euclidean) or sign
+// (cosine): fix-up pass. Four lanes per listed row, each holding 32 contiguous
+// dims and 8 of the row's tuples (or 2 of its g values); the next row of the
+// group is loaded while the current one is computed, and the projections and
+// per-function constants sit in LDS, so the only global latency per row is
+// the prefetched one. The fp64 products are summed per lane and then across the
+// 4 lanes: hash.hip's bound covers any summation order of the 128 products
+// (depth 34 < 130); the soft-x87 fallback keeps the reference order.
 constexpr int HF_WAVES = 4;
-constexpr int HF_SPLIT = 4;                           // blocks per list segment
-constexpr size_t HF_LDS = (size_t)FU_D * 32 * 4;      // the projections, f32 (exact)
+#ifndef HF_SPLIT_SET
+#define HF_SPLIT_SET 4
+#endif
+constexpr int HF_SPLIT = HF_SPLIT_SET;                // blocks per list segment
+constexpr int HF_G = 4;                               // lanes per listed row
+constexpr int HF_SLOTS = 64 * HF_WAVES / HF_G;        // rows per block pass
+// LDS image of the projections (fp64): dim r at (r / 32) * HF_QS + (r % 32) *
+// HF_PS; the quarters skewed by 8 words so that the 4 lanes of a row, reading
+// dim 32q + j of the same function, hit different banks (LK <= 32)
+constexpr int HF_PS = 33;
+constexpr int HF_QS = 32 * HF_PS + 8;
+constexpr size_t HF_LDS = (size_t)4 * HF_QS * 8 + 32 * (8 + 8 + 4);
+__device__ inline int hf_pidx(int r) { return (r >> 5) * HF_QS + (r & 31) * HF_PS; }
 
-// fp64 projection of one row, streamed in 32-dim chunks (re-reads for a second
-// function hit L1), with the rigorous bound of hash.hip; soft-x87 fallback.
-__device__ int32_t fixup_hash(const float* xrow, const float* pts, int LKpad, int f,
-                              double tt, double ww, double pn, float w, unsigned long long* stats) {
-    double acc = 0.0, xn2 = 0.0;
-#pragma unroll 1
-    for (int c = 0; c < FU_D; c += 32) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const float4*>(xrow + c + 4 * u);
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const float xs[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int j = c + 4 * u + e;
-                const double xj = (double)xs[e];
-                xn2 = fma(xj, xj, xn2);
-                acc = fma((double)pts[j * LKpad + f], xj, acc);
-            }
-        }
-    }
-    const double P = pn * sqrt(xn2) * (1.0 + 0x1p-40);
-    const double y = (acc + tt) / ww;
-    const double B = ((double)(FU_D + 2) * 0x1p-52 * (P + fabs(tt))) / ww + fabs(y) * 0x1p-51;
-    const double lo = floor(y - B), hi = floor(y + B);
-    if (lo == hi) return (int32_t)lo;
-    sx80 s = sx_zero();
-    for (int j = 0; j < FU_D; j++) s = sx_add_double(s, __dmul_rn((double)pts[j * LKpad + f], (double)xrow[j]));
-    s = sx_add_double(s, tt);
-    atomicAdd(stats + STAT_HASH_EXACT, 1ull);
-    return (int32_t)sx_floor_i64(sx_div(s, sx_from_float(w)));
+// lane ^ 1 / lane ^ 2 within each quad by DPP quad_perm (VALU moves)
+template <int CTRL>
+__device__ inline uint32_t quad_swap(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ inline double quad_swap(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint64_t lo = quad_swap<CTRL>((uint32_t)b), hi = quad_swap<CTRL>((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)((hi << 32) | lo));
+}
+constexpr int QP_X1 = 0xB1, QP_X2 = 0x4E;   // quad_perm [1,0,3,2], [2,3,0,1]
+// sum over the 4 lanes of a row group (a quad, all active together); every
+// lane gets the same value ((v0 + v1) + (v2 + v3) in any lane's operand order)
+__device__ inline double group4_sum(double v) {
+    v += quad_swap<QP_X1>(v);
+    v += quad_swap<QP_X2>(v);
+    return v;
+}
+__device__ inline uint32_t group4_sum(uint32_t v) {
+    v += quad_swap<QP_X1>(v);
+    v += quad_swap<QP_X2>(v);
+    return v;
 }
 
-// Lane = listed row (~4% of rows at w = 0.4, mostly one function each): the row
-// is loaded into registers, the flagged functions are recomputed (the set-bit
-// loop runs the wave's max popcount, not the union), and phi / bucket of each
-// touched table are rebuilt from tuples (the other values there are certified).
-__global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* pts = reinterpret_cast<float*>(smem);     // [128][LKpad]
-    const int seg = blockIdx.x / HF_SPLIT, part = blockIdx.x % HF_SPLIT;
-    const int n = a.seg_counts[2 * seg + 1];
-    if (n == 0) return;                                                 // block-uniform
-    const unsigned long long* list = a.hfix + (int64_t)seg * a.seg_rows;
-    const int LKpad = a.LKpad;
-    for (int e = threadIdx.x; e < FU_D * LKpad; e += 64 * HF_WAVES) pts[e] = (float)a.PT[e];
-    __syncthreads();
-    const double ww = (double)a.w;
-    const uint32_t kmask = a.k >= 32 ? 0xFFFFFFFFu : ((1u << a.k) - 1u);
-    for (int e = part * 64 * HF_WAVES + threadIdx.x; e < n; e += HF_SPLIT * 64 * HF_WAVES) {
-        const unsigned long long ent = list[e];
-        const int64_t row = (int64_t)(ent >> 32);
-        const uint32_t mask = (uint32_t)ent;
-        const float* xrow = a.X + row * FU_D;
-        for (uint32_t m = mask; m; m &= m - 1) {
-            const int f = __builtin_ctz(m);
-            a.tuples[row * a.LK + f] = fixup_hash(xrow, pts, LKpad, f, (double)a.tv[f], ww, a.pnorm[f], a.w, a.stats);
-        }
-        for (int l = 0; l < a.L; l++) {
-            if (!(mask & (kmask << (l * a.k)))) continue;
-            uint32_t hn = 0;
-            for (int i = 0; i < a.k; i++) {
-                const int f = l * a.k + i;
-                hn += phi_term(a.tuples[row * a.LK + f], a.rv[f]);
-            }
-            const uint32_t ph = phi_final(hn);
-            if (a.phi) a.phi[row * a.L + l] = (int32_t)ph;
-            if (a.bucket) a.bucket[row * a.L + l] = bucket_of(ph, a.nb);
-        }
+// the rare sequential fallbacks, out of line (their registers would lower the
+// occupancy of the whole kernel)
+__device__ __noinline__ int32_t fixup_floor_x87(const float* xrow, const double* pts, int f, double tt, float w) {
+    sx80 sxs = sx_zero();
+    for (int j = 0; j < FU_D; j++) sxs = sx_add_double(sxs, __dmul_rn(pts[hf_pidx(j) + f], (double)xrow[j]));
+    sxs = sx_add_double(sxs, tt);
+    return (int32_t)sx_floor_i64(sx_div(sxs, sx_from_float(w)));
+}
+__device__ __noinline__ int fixup_sign_x87(const float* xrow, const double* pts, int f) {
+    SxSum sx;
+    sx.init();
+    for (int j = 0; j < FU_D; j++) sx.add(__dmul_rn(pts[hf_pidx(j) + f], (double)xrow[j]));
+    return sx_hash_sign(sx);
+}
+
+// One listed row as the group's lane q holds it.
+struct FixRow {
+    int64_t row;
+    uint32_t mask;
+    float x[32];       // dims [32q, 32q + 32)
+    int32_t v[8];      // euclidean: tuples [8q, 8q + 8); cosine: g of tables 2q, 2q + 1
+};
+
+template <bool COS>
+__device__ inline void fix_load(const FusedArgs& a, unsigned long long ent, int q, FixRow& r) {
+    r.row = (int64_t)(ent >> 32);
+    r.mask = (uint32_t)ent;
+    const float* xq = a.X + r.row * FU_D + 32 * q;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const float4 v = *reinterpret_cast<const float4*>(xq + 4 * u);
+        r.x[4 * u] = v.x; r.x[4 * u + 1] = v.y; r.x[4 * u + 2] = v.z; r.x[4 * u + 3] = v.w;
+    }
+    // unconditional loads (clamped indices; the extra values are never used):
+    // a load under a branch makes the compiler wait for it at the merge
+    if (COS) {
+        const int32_t* g = (a.bucket ? a.bucket : a.phi) + r.row * a.L;
+#pragma unroll
+        for (int i = 0; i < 2; i++) r.v[i] = g[min(2 * q + i, a.L - 1)];
+    } else {
+        const int32_t* t = a.tuples + r.row * a.LK;
+#pragma unroll
+        for (int i = 0; i < 8; i++) r.v[i] = t[min(8 * q + i, a.LK - 1)];
     }
 }
 
-// The cosine form's listed signs (CosineHGen, cosine_h_gen.hpp:67-76): the
-// flagged functions by the fp64 FMA chain over the fp64 rows of R with
-// hash.hip's bound, else the soft-x87 sign; the touched tables' g bits patched
-// in phi / bucket (the other bits are certified).
-constexpr size_t HFC_LDS = (size_t)FU_D * 32 * 8;     // R, fp64
-__global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_cos_kernel(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    double* pts = reinterpret_cast<double*>(smem);   // [128][LKpad]
-    const int seg = blockIdx.x / HF_SPLIT, part = blockIdx.x % HF_SPLIT;
-    const int n = a.seg_counts[2 * seg + 1];
-    if (n == 0) return;                                                 // block-uniform
-    const unsigned long long* list = a.hfix + (int64_t)seg * a.seg_rows;
-    const int LKpad = a.LKpad, k = a.k;
-    for (int e = threadIdx.x; e < FU_D * LKpad; e += 64 * HF_WAVES) pts[e] = a.PT[e];
-    __syncthreads();
-    const uint32_t kmask = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
-    for (int e = part * 64 * HF_WAVES + threadIdx.x; e < n; e += HF_SPLIT * 64 * HF_WAVES) {
-        const unsigned long long ent = list[e];
-        const int64_t row = (int64_t)(ent >> 32);
-        const uint32_t mask = (uint32_t)ent;
-        const float* xrow = a.X + row * FU_D;
-        uint32_t bits = 0;
-        for (uint32_t m = mask; m; m &= m - 1) {
-            const int f = __builtin_ctz(m);
-            double acc = 0.0, xn2 = 0.0;
-#pragma unroll 1
-            for (int c = 0; c < FU_D; c += 32) {
-                float4 v[8];
+template <bool COS>
+__device__ inline void fix_row(const FusedArgs& a, const double* pts, const double* cpn, const double* ctt,
+                               const int32_t* crv, int q, FixRow& r) {
+    double xn2 = 0.0;
 #pragma unroll
-                for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const float4*>(xrow + c + 4 * u);
+    for (int j = 0; j < 32; j++) xn2 = fma((double)r.x[j], (double)r.x[j], xn2);
+    const double nx = sqrt(group4_sum(xn2));
+    const float* xrow = a.X + r.row * FU_D;
+    const int k = a.k;
+    const double iwd = 1.0 / (double)a.w;
+    for (uint32_t m = r.mask; m; m &= m - 1) {
+        const int f = __builtin_ctz(m);
+        const double* pq = pts + q * HF_QS + f;
+        // keep the fp64 widening inside the loop (hoisted, it holds 64 VGPRs)
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const float xs[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        for (int j = 0; j < 32; j++) asm volatile("" : "+v"(r.x[j]));
+        double acc = 0.0;
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const double xj = (double)xs[q];
-                        xn2 = fma(xj, xj, xn2);
-                        acc = fma(pts[(c + 4 * u + q) * LKpad + f], xj, acc);
-                    }
-                }
-            }
-            const double P = a.pnorm[f] * sqrt(xn2) * (1.0 + 0x1p-40);
+        for (int j = 0; j < 32; j++) acc = fma(pq[j * HF_PS], (double)r.x[j], acc);
+        acc = group4_sum(acc);
+        const double P = cpn[f] * nx * (1.0 + 0x1p-40);
+        if (COS) {
             const double B = (double)(FU_D + 3) * 0x1p-52 * P + 0x1p-1000;
             int bit;
             if (acc > B && acc < 0x1p1000) bit = 1;
             else if (acc < -B && acc > -0x1p1000) bit = 0;
-            else {
-                SxSum sx;
-                sx.init();
-                for (int j = 0; j < FU_D; j++) sx.add(__dmul_rn(pts[j * LKpad + f], (double)xrow[j]));
-                bit = sx_hash_sign(sx);
-                atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
+            else {                                   // the same decision in all 4 lanes
+                bit = fixup_sign_x87(xrow, pts, f);
+                if (q == 0) atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
             }
-            bits |= (uint32_t)bit << f;
-        }
-        for (int l = 0; l < a.L; l++) {
-            if (!(mask & (kmask << (l * k)))) continue;
-            int32_t* gout = a.bucket ? a.bucket : a.phi;
-            int gv = gout[row * a.L + l];
-            for (int i = 0; i < k; i++) {
-                const int f = l * k + i;
-                if (mask & (1u << f)) {
-                    const int b = 1 << (k - 1 - i);
-                    gv = (bits >> f) & 1u ? (gv | b) : (gv & ~b);
-                }
+            // g = bits MSB first (CosineGGen): function l*k + i is bit k-1-i of table l
+            const int l = f / k, b = 1 << (k - 1 - (f - l * k));
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                if (l == 2 * q + i) r.v[i] = bit ? (r.v[i] | b) : (r.v[i] & ~b);
+        } else {
+            // y by the reciprocal (iw = RN(1/w)): three roundings of 2^-53 each
+            // relative, inside the |y| 2^-50 term
+            const double tt = ctt[f], iw = iwd;
+            const double y = (acc + tt) * iw;
+            const double B = ((double)(FU_D + 2) * 0x1p-52 * (P + fabs(tt))) * (iw * (1.0 + 0x1p-50)) +
+                             fabs(y) * 0x1p-50;
+            const double lo = floor(y - B), hi = floor(y + B);
+            int32_t hv = (int32_t)lo;
+            if (lo != hi) {                          // the same decision in all 4 lanes
+                hv = fixup_floor_x87(xrow, pts, f, tt, a.w);
+                if (q == 0) atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
             }
-            if (a.phi) a.phi[row * a.L + l] = gv;
-            if (a.bucket) a.bucket[row * a.L + l] = gv;
+#pragma unroll
+            for (int i = 0; i < 8; i++) r.v[i] = f == 8 * q + i ? hv : r.v[i];
+            if ((f >> 3) == q) a.tuples[r.row * a.LK + f] = hv;
         }
+    }
+    const uint32_t kmask = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
+    if (COS) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int l = 2 * q + i;
+            if (l < a.L && (r.mask & (kmask << (l * k)))) {
+                if (a.phi) a.phi[r.row * a.L + l] = r.v[i];
+                if (a.bucket) a.bucket[r.row * a.L + l] = r.v[i];
+            }
+        }
+        return;
+    }
+    // touched tables: phi from the lanes' partial sums of the phi terms (the
+    // uint32 sum wraps the same in any order)
+    uint32_t term[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) term[i] = 8 * q + i < a.LK ? phi_term(r.v[i], crv[8 * q + i]) : 0u;
+    for (int l = 0; l < a.L; l++) {
+        if (!(r.mask & (kmask << (l * k)))) continue;                // the same in all 4 lanes
+        uint32_t hn = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int f = 8 * q + i;
+            hn += f >= l * k && f < l * k + k ? term[i] : 0u;
+        }
+        hn = group4_sum(hn);
+        if (q == 0) {
+            const uint32_t ph = phi_final(hn);
+            if (a.phi) a.phi[r.row * a.L + l] = (int32_t)ph;
+            if (a.bucket) a.bucket[r.row * a.L + l] = bucket_fast(ph, a.bdiv);
+        }
+    }
+}
+
+template <bool COS>
+__global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double* pts = reinterpret_cast<double*>(smem);   // skewed [128][32]
+    double* cpn = pts + 4 * HF_QS;                   // [32] |p_f| (rounded up)
+    double* ctt = cpn + 32;                          // [32] t_f
+    int32_t* crv = reinterpret_cast<int32_t*>(ctt + 32);   // [32] r_f
+    const int seg = blockIdx.x / HF_SPLIT, part = blockIdx.x % HF_SPLIT;
+    const int n = a.seg_counts[2 * seg + 1];
+    if (n == 0) return;                                                 // block-uniform
+    const unsigned long long* list = a.hfix + (int64_t)seg * a.seg_rows;
+    const int LK = a.LK, LKpad = a.LKpad;
+#pragma unroll
+    for (int e = threadIdx.x; e < FU_D * 32; e += 64 * HF_WAVES) {
+        const int r = e >> 5, f = e & 31;
+        pts[hf_pidx(r) + f] = f < LK ? a.PT[r * LKpad + f] : 0.0;
+    }
+    if (threadIdx.x < 32) {
+        const int f = threadIdx.x;
+        cpn[f] = f < LK ? a.pnorm[f] : 0.0;
+        ctt[f] = !COS && f < LK ? (double)a.tv[f] : 0.0;
+        crv[f] = !COS && f < LK ? a.rv[f] : 0;
+    }
+    __syncthreads();
+    const int q = threadIdx.x & (HF_G - 1), slot = threadIdx.x / HF_G;
+    constexpr int STRIDE = HF_SPLIT * HF_SLOTS;
+    int e = part * HF_SLOTS + slot;
+    if (e >= n) return;                                                 // whole groups
+    // software pipeline: the next row (and the list entry after it) load while
+    // the current one is computed; past the end the last entry is re-loaded
+    FixRow cur, nxt;
+    fix_load<COS>(a, list[e], q, cur);
+    unsigned long long ent2 = list[min(e + STRIDE, n - 1)];
+    for (; e < n; e += STRIDE) {
+        fix_load<COS>(a, ent2, q, nxt);
+        ent2 = list[min(e + 2 * STRIDE, n - 1)];
+        fix_row<COS>(a, pts, cpn, ctt, crv, q, cur);
+        cur = nxt;
     }
 }
 
@@ -1765,6 +1837,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         set_error("launch_fused: the hi-only cosine form needs the decline list");
         return -1;
     }
+    if (hash && (f.LK > 32 || f.L * f.k != f.LK)) {              // the fix-ups hold <= 32 functions per row
+        set_error("launch_fused: hashing needs L * k <= 32");
+        return -1;
+    }
     if (!chunked && multi_ok && (!hash || f.k == 4)) {
         static int cus[64] = {0};
         int dev = 0;
@@ -1834,8 +1910,8 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                     else hipLaunchKernelGGL((fused_hi_kernel<false, true>), grid, hblock, lh, s, a);
                 }
             }
-            if (hash && cos) hipLaunchKernelGGL(hash_fixup_cos_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HFC_LDS, s, a);
-            else if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
+            if (hash && cos) hipLaunchKernelGGL(hash_fixup_kernel<true>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
+            else if (hash) hipLaunchKernelGGL(hash_fixup_kernel<false>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
             FusedArgs r = a;
             r.list_in = f.ambig; r.list_counts = f.seg_counts; r.list_seg_rows = a.seg_rows;
             r.ambig = f.list2; r.seg_counts = f.seg_counts2; r.ambig_count = f.ambig_count;
@@ -1880,7 +1956,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true>), grid, block, lds_nohash, s, a);
             }
         }
-        if (hash) hipLaunchKernelGGL(hash_fixup_kernel, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
+        if (hash) hipLaunchKernelGGL(hash_fixup_kernel<false>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
         if (f.metric == 1) {
             f.ncos_lists = 1;
             f.cos_list[0] = f.hfix; f.cos_counts[0] = f.seg_counts;

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("LSHKM_LIB") or os.path.join(_HERE, "liblshkm.so")   #
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "lshkm.h")
 
 EUCLIDEAN, COSINE = 0, 1
-STAT_HASH_EXACT, STAT_ASSIGN_AMBIG, STAT_COS_FIX, STAT_REFINED = 0, 1, 4, 5
+STAT_HASH_EXACT, STAT_ASSIGN_AMBIG, STAT_COS_FIX, STAT_REFINED, STAT_HASH_FIX = 0, 1, 4, 5, 6
 _METRIC = {"euclidean": EUCLIDEAN, "cosine": COSINE, EUCLIDEAN: EUCLIDEAN, COSINE: COSINE}
 
 _lib = None
