@@ -164,6 +164,23 @@ __device__ inline double swap_halves(double v, int h) {
     return __longlong_as_double((long long)(((uint64_t)u << 32) | l));
 }
 
+// One direction of the half swap (the chain hand-offs): take_from_lower gives
+// the upper lanes the lower half's value and leaves the lower lanes' own (the
+// first result of v_permlane32_swap(v, v)); take_from_upper the other way.
+// No select: one v_permlane32_swap per dword.
+__device__ inline double take_from_lower(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t l = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false)[0];
+    const uint32_t u = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false)[0];
+    return __longlong_as_double((long long)(((uint64_t)u << 32) | l));
+}
+__device__ inline double take_from_upper(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t l = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false)[1];
+    const uint32_t u = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false)[1];
+    return __longlong_as_double((long long)(((uint64_t)u << 32) | l));
+}
+
 // Exact (reference-order) hash of one projection from the fp32 row in HBM.
 __device__ int32_t hash_exact_row(const float* __restrict__ xrow, const double* __restrict__ PT, int LKpad, int f,
                                   float t, float w, double pn, unsigned long long* stats) {
@@ -907,14 +924,12 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
-                const double from0 = swap_halves(acc, h);
+                acc = take_from_lower(acc);
                 if (h == 1) {
-                    acc = from0;
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
-                const double from1 = swap_halves(acc, h);
-                if (h == 0) acc = from1;
+                acc = take_from_upper(acc);
             }
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
@@ -1015,16 +1030,24 @@ __host__ __device__ constexpr int fh_lds_bytes(int Kpad, bool hash) {
 static_assert(fh_lds_bytes(FH_KMAX, true) <= 160 * 1024, "hi-only LDS image exceeds 160 KiB");
 constexpr double FH_A = 130.0 * 0x1p-23;
 
-// Waves per block of the hi-only form (one block per CU). Measured (fused pass,
-// N = 10M, K = 256): 8 waves (<= 256 VGPRs, no spills) 2.37 ms; 12 waves (168
-// VGPRs: ~30 spilled loop invariants) 2.74 ms; 12 waves with the row re-read
-// for the chain instead of kept (one lane per row over two tiles) 3.7 ms -- the
-// lane-per-row re-reads of the row and of the winner's fp64 row thrash L1.
-#ifndef FH_WAVES_SET
-#define FH_WAVES_SET 8
+// Waves per block of the hi-only form (one block per CU), per instantiation.
+// Measured for the single-pass euclidean hash form (fused pass, N = 10M, K =
+// 256): 8 waves 2.37 ms; 12 waves (~30 spilled loop invariants) 2.74 ms; 12
+// waves with the row re-read for the chain instead of kept (one lane per row
+// over two tiles) 3.7 ms -- the lane-per-row re-reads of the row and of the
+// winner's fp64 row thrash L1. K = 1024 (two passes, both without spills at
+// 12 waves): first pass (hash) 1.91 -> 1.88 ms at 12 waves, second pass
+// (chain) 2.48 -> 2.59 ms -- a third wave per SIMD does not pay. FH_WAVES_SET
+// forces one count for all (experiments).
+template <bool HASH, bool MP, int MET>
+__host__ __device__ constexpr int fh_waves() {
+#ifdef FH_WAVES_SET
+    return FH_WAVES_SET;
+#else
+    return HASH && MP ? 12 : 8;
 #endif
-constexpr int FH_WAVES = FH_WAVES_SET;
-constexpr int FH_THREADS = 64 * FH_WAVES;
+}
+constexpr int FH_WAVES_MIN = 8, FH_WAVES_MAX = 12;
 
 // MET = 1: cosine (the prep's normalised centroid rows, score x.c^ with no
 // offset; the winner's distance from the row in registers, declines to the
@@ -1054,17 +1077,15 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
                 xa = __dadd_rn(xa, __dmul_rn(xj, xj));
             }
         }
-        const double from0 = swap_halves(xa, h);
+        xa = take_from_lower(xa);
         if (h == 1) {
-            xa = from0;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 const double xj = (double)xf[8 * s + j];
                 xa = __dadd_rn(xa, __dmul_rn(xj, xj));
             }
         }
-        const double from1 = swap_halves(xa, h);
-        if (h == 0) xa = from1;
+        xa = take_from_upper(xa);
     }
     // the inner product, each half over its own dims
     double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0, hold = 0.0;
@@ -1113,7 +1134,9 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
 }
 
 template <bool HASH, bool MP = false, int MET = 0>
-__global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
+__global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_kernel(FusedArgs a) {
+    constexpr int FH_WAVES = fh_waves<HASH, MP, MET>();
+    constexpr int FH_THREADS = 64 * FH_WAVES;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
     int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows, [2] cosine declines
@@ -1453,14 +1476,12 @@ __global__ __launch_bounds__(FH_THREADS, 1) void fused_hi_kernel(FusedArgs a) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
-                const double from0 = swap_halves(acc, h);
+                acc = take_from_lower(acc);
                 if (h == 1) {
-                    acc = from0;
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
-                const double from1 = swap_halves(acc, h);
-                if (h == 0) acc = from1;
+                acc = take_from_upper(acc);
             }
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
@@ -1858,9 +1879,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         const size_t lds_nohash = (size_t)fp_lds_bytes(kslice, false);
         // list segments: block b's tiles hold at most FP_WAVES * 32 * ceil(tiles / (grid * FP_WAVES)) rows
         a.seg_rows = (int64_t)FP_WAVES * 32 * ((ntiles + (int64_t)nblk * FP_WAVES - 1) / ((int64_t)nblk * FP_WAVES));
-        // the hi-only form strides by FH_WAVES tiles per block
-        a.seg_rows = std::max<int64_t>(a.seg_rows, (int64_t)FH_WAVES * 32 * ((ntiles + (int64_t)nblk * FH_WAVES - 1) /
-                                                                              ((int64_t)nblk * FH_WAVES)));
+        // the hi-only form strides by fh_waves() tiles per block (8 or 12)
+        for (const int W : {FH_WAVES_MIN, FH_WAVES_MAX})
+            a.seg_rows = std::max<int64_t>(a.seg_rows, (int64_t)W * 32 * ((ntiles + (int64_t)nblk * W - 1) / ((int64_t)nblk * W)));
         a.seg_counts = f.seg_counts;
         if (!f.seg_counts || f.seg_cap < nblk || (int64_t)nblk * a.seg_rows > f.list_cap) {
             set_error("launch_fused: list workspace too small");
@@ -1893,22 +1914,24 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 a.Kpad = std::min(FH_KMAX, f.Kpad - c0);
                 a.t0 = c0 / 32; a.pass_first = p == 0; a.pass_last = p == np1 - 1;
                 const size_t lh = (size_t)fh_lds_bytes(a.Kpad, hash && p == 0);
-                const dim3 hblock(FH_THREADS);
+#define FH_LAUNCH(H, M, C) \
+    hipLaunchKernelGGL((fused_hi_kernel<H, M, C>), grid, dim3(64 * fh_waves<H, M, C>()), lh, s, a)
                 if (cos) {
                     if (np1 == 1) {
-                        if (hash) hipLaunchKernelGGL((fused_hi_kernel<true, false, 1>), grid, hblock, lh, s, a);
-                        else hipLaunchKernelGGL((fused_hi_kernel<false, false, 1>), grid, hblock, lh, s, a);
+                        if (hash) FH_LAUNCH(true, false, 1);
+                        else FH_LAUNCH(false, false, 1);
                     } else {
-                        if (hash && p == 0) hipLaunchKernelGGL((fused_hi_kernel<true, true, 1>), grid, hblock, lh, s, a);
-                        else hipLaunchKernelGGL((fused_hi_kernel<false, true, 1>), grid, hblock, lh, s, a);
+                        if (hash && p == 0) FH_LAUNCH(true, true, 1);
+                        else FH_LAUNCH(false, true, 1);
                     }
                 } else if (np1 == 1) {
-                    if (hash) hipLaunchKernelGGL((fused_hi_kernel<true>), grid, hblock, lh, s, a);
-                    else hipLaunchKernelGGL((fused_hi_kernel<false>), grid, hblock, lh, s, a);
+                    if (hash) FH_LAUNCH(true, false, 0);
+                    else FH_LAUNCH(false, false, 0);
                 } else {
-                    if (hash && p == 0) hipLaunchKernelGGL((fused_hi_kernel<true, true>), grid, hblock, lh, s, a);
-                    else hipLaunchKernelGGL((fused_hi_kernel<false, true>), grid, hblock, lh, s, a);
+                    if (hash && p == 0) FH_LAUNCH(true, true, 0);
+                    else FH_LAUNCH(false, true, 0);
                 }
+#undef FH_LAUNCH
             }
             if (hash && cos) hipLaunchKernelGGL(hash_fixup_kernel<true>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
             else if (hash) hipLaunchKernelGGL(hash_fixup_kernel<false>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, s, a);
