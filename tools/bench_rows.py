@@ -45,8 +45,16 @@ def cpu_time(fn):
     return time.perf_counter() - t0
 
 
-def emit(row, unit, units, t_gpu, cpu=None, note=""):
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
+
+
+def emit(row, unit, units, t_gpu, cpu=None, note="", bytes_per_unit=None):
     line = {"row": row, "unit": unit, "units": units, "gpu_s": t_gpu, "gpu_rate": units / t_gpu}
+    if bytes_per_unit:
+        # algorithmic HBM bytes of the whole call (stated per unit) over its wall time
+        gbs = units * bytes_per_unit / t_gpu / 1e9
+        line["roofline"] = {"bound": "hbm", "bytes_per_unit": bytes_per_unit, "achieved": gbs,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
     if cpu:
         cu, ct, sample = cpu
         line["cpu_baseline"] = {"rate": cu / ct, "kind": "port", "cores": 1, "sample": sample}
@@ -78,7 +86,8 @@ def main():
             Xh, ah = X[:n].cpu().numpy(), asg[:n].cpu().numpy()
             c = (n, cpu_time(lambda: oracle.kmeans_update(Xh, ah, C.cpu().numpy(), "euclidean", 0.05)),
                  f"{n} rows, K={K}, d={d}")
-        emit("k_means update", "rows/s", N, t, c, "N=10M, d=128, K=256")
+        emit("k_means update", "rows/s", N, t, c, "N=10M, d=128, K=256; bytes: the row + its cluster id",
+             bytes_per_unit=4 * d + 4)
         del X
 
     if "cosine" in rows:     # lloyds_assignment, cosine metric (assignment.hpp:52-75)
@@ -101,7 +110,8 @@ def main():
         emit("lloyds_assignment (cosine)", "rows/s", N, t, c,
              f"N=10M, d=128, K=256; hi-only f16 kernel (normalised centroids), {amb:.0f} rows/call to the pruned exact "
              f"pass, {cfix:.0f} winner distances/call to the soft-x87 chain; "
-             f"exact all-K pass alone {te * 1e3:.1f} ms")
+             f"exact all-K pass alone {te * 1e3:.1f} ms; bytes: the row + cluster id and distance",
+             bytes_per_unit=4 * d + 12)
         # main.cpp's cosine flow in one pass: CosineGGen buckets (L=5, k=4) + cosine Lloyd
         R, _ = lshkm.params_lsh_cosine(12345, 5, 4, d)
         lsh = lshkm.LSH(ctx, "cosine", d, 4, 5, R=R)
@@ -109,7 +119,8 @@ def main():
         tsep = gpu_time(ctx, lambda: (lsh.hash(X, tuples=False, phi=False), lshkm.lloyd_assign(ctx, X, C, "cosine")))
         emit("hash_assign (cosine LSH + cosine Lloyd)", "rows/s", N, th, None,
              f"N=10M, d=128, L=5, k=4, K=256, one pass (lshkm_hash_assign_metric); the two separate calls "
-             f"{tsep * 1e3:.2f} ms")
+             f"{tsep * 1e3:.2f} ms; bytes: the row + cluster id, distance and 5 bucket ids",
+             bytes_per_unit=4 * d + 12 + 4 * 5)
         del X
 
     if "kpp" in rows:        # k_means_pp (initialization.hpp:71-156)
@@ -121,7 +132,9 @@ def main():
             n = 100_000
             Xh = X[:n].cpu().numpy()
             c = (n * K, cpu_time(lambda: oracle.kmeans_pp(Xh, K, "euclidean", 7)), f"{n} rows, K={K}")
-        emit("k_means_pp", "row-centroid steps/s", N * K, t, c, "N=1M, d=128, K=64, euclidean")
+        emit("k_means_pp", "row-centroid steps/s", N * K, t, c,
+             "N=1M, d=128, K=64, euclidean; bytes: one pass over the rows and D^2 per centroid",
+             bytes_per_unit=4 * d + 8)
         del X
 
     if "range" in rows:      # lsh_range_assignment (assignment.hpp:108-217)
@@ -182,7 +195,9 @@ def main():
             Xh = X[:n].cpu().numpy()
             c = (n, cpu_time(lambda: oracle.bucket_csr(oracle.lsh_hash_euclid(Xh, V, tt, np.float32(0.4), r, N // 100)[2],
                                                        N // 100)), f"{n} rows")
-        emit("create_LSH_hashtables", "rows/s", N, tb, c, "C2: N=1M, d=128, L=5, k=4, w=0.4, nb=10k")
+        emit("create_LSH_hashtables", "rows/s", N, tb, c,
+             "C2: N=1M, d=128, L=5, k=4, w=0.4, nb=10k; bytes: the row + per table its bucket key and CSR slot",
+             bytes_per_unit=4 * d + 5 * 8)
         nq = 65_536
         qrows = torch.arange(nq, device=ctx.dev) * (N // nq)
         Q = X[qrows]
@@ -206,7 +221,8 @@ def main():
         tr = gpu_time(ctx, lambda: cube.build(X), reps=3)
         emit("create_hypercube", "rows/s", N, tb, None,
              f"C4: N=10M, d=128, d'=14, w=2 (euclidean F coins), fresh cube each build; "
-             f"rebuild with the coins already drawn {tr * 1e3:.2f} ms")
+             f"rebuild with the coins already drawn {tr * 1e3:.2f} ms; bytes: the row + its vertex and CSR slot",
+             bytes_per_unit=4 * d + 8)
         nq = 65_536
         Q = X[torch.arange(nq, device=ctx.dev) * (N // nq)]
         tq = gpu_time(ctx, lambda: cube.query(Q, 14, device=True), reps=3)
