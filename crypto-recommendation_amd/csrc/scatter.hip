@@ -10,12 +10,12 @@
 // (cluster-sorted rows, update.hpp:52-56 order) and the F-coin draw order.
 //
 // Per pass (<= 8 digit bits): upsweep (block digit histograms in LDS) ->
-// one-block exclusive scan of the [digit][block] matrix -> downsweep, where a
-// block walks its 4096-key tile in rounds of 256 consecutive keys: each wave
-// finds the lanes sharing its digit with DB ballots (AND of matching bit
-// masks), ranks itself with popc(peers & lanemask_lt), publishes its per-digit
-// counts in LDS, and the block adds the counts of earlier waves and earlier
-// rounds: a stable rank without sorting inside the tile.
+// exclusive scan of the [digit][block] matrix -> downsweep, where each wave
+// ranks a contiguous quarter of the block's 4096-key tile: per 64-key round the
+// lanes sharing a digit are found with DB ballots (AND of matching bit masks),
+// rank = the wave's running count of that digit + popc(peers & lanemask_lt);
+// the block then offsets each wave by the earlier waves' totals: a stable rank
+// without sorting inside the tile.
 // HBM per pass: 4 B key read (upsweep) + 8 B read + 8 B written (downsweep).
 #include "common.h"
 #include "kernels.h"
@@ -113,54 +113,74 @@ __global__ __launch_bounds__(1024) void rs_chunk_scan(uint32_t* __restrict__ a, 
         if (base + u < M) { a[base + u] = run; run += v[u]; }
 }
 
+// Each wave ranks its own contiguous quarter of the tile (16 rounds of 64
+// keys, the keys and their ranks kept in registers) against per-wave running
+// digit counts in LDS; one barrier, the block turns the per-wave totals into
+// per-wave digit offsets (global start + earlier waves), a second barrier, and
+// every key is written. Two barriers per 4096-key tile (the round-per-256-keys
+// form needed three per round).
+constexpr int RS_R = RS_TILE / RS_THREADS;           // keys per lane
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(
     const int32_t* __restrict__ keys, int64_t kstride, const int32_t* __restrict__ vals, int64_t N, int shift,
     int dbits, int nblocks, const uint32_t* __restrict__ scanned, int32_t* __restrict__ keys_out,
     int32_t* __restrict__ vals_out, int64_t k_ts, int64_t v_ts, int64_t h_ts, int64_t o_ts) {
-    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[RS_THREADS / 64][256];
     keys += blockIdx.y * k_ts;
     if (vals) vals += blockIdx.y * v_ts;
     scanned += blockIdx.y * h_ts;
     keys_out += blockIdx.y * o_ts;
     vals_out += blockIdx.y * o_ts;
-    __shared__ uint32_t wcnt[4][256];
     const int nbins = 1 << dbits;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    for (int b = t; b < nbins; b += RS_THREADS) {
-        run[b] = scanned[(size_t)b * nblocks + blockIdx.x];
-        wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
+    for (int b = t; b < nbins; b += RS_THREADS)
+#pragma unroll
+        for (int w2 = 0; w2 < RS_THREADS / 64; w2++) wcnt[w2][b] = 0;
+    const int64_t base = (int64_t)blockIdx.x * RS_TILE + (int64_t)w * (RS_TILE / (RS_THREADS / 64));
+    int32_t kk[RS_R], vv[RS_R];
+#pragma unroll
+    for (int r = 0; r < RS_R; r++) {
+        const int64_t i = base + r * 64 + lane;
+        kk[r] = i < N ? keys[i * kstride] : 0;
+        vv[r] = i < N ? (vals ? vals[i] : (int32_t)i) : 0;
     }
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * RS_TILE;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int r = 0; r < RS_TILE / RS_THREADS; r++) {
-        const int64_t i0 = base + (int64_t)r * RS_THREADS;
-        if (i0 >= N) break;                               // uniform
-        const int64_t i = i0 + t;
-        const bool valid = i < N;
-        const int32_t key = valid ? keys[i * kstride] : 0;
-        const int digit = (key >> shift) & (nbins - 1);
+    uint32_t rk[RS_R];
+#pragma unroll
+    for (int r = 0; r < RS_R; r++) {
+        const bool valid = base + r * 64 + lane < N;
+        const int digit = (kk[r] >> shift) & (nbins - 1);
         unsigned long long peers = __ballot(valid);
         for (int b = 0; b < dbits; b++) {
             const bool bit = (digit >> b) & 1;
             const unsigned long long m = __ballot(bit);
             peers &= bit ? m : ~m;
         }
-        const int rank = __popcll(peers & lt);
-        if (valid && rank == 0) wcnt[w][digit] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = run[digit] + rank;
-            for (int w2 = 0; w2 < w; w2++) pos += wcnt[w2][digit];
-            keys_out[pos] = key;
-            vals_out[pos] = vals ? vals[i] : (int32_t)i;
+        const uint32_t before = valid ? wcnt[w][digit] : 0u;   // this wave's earlier rounds
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        rk[r] = before + below;
+        // the digit's first lane advances the wave's running count (LDS ops of
+        // one wave complete in order: every peer has read 'before')
+        if (valid && below == 0) wcnt[w][digit] = before + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    for (int b = t; b < nbins; b += RS_THREADS) {
+        uint32_t o = scanned[(size_t)b * nblocks + blockIdx.x];
+#pragma unroll
+        for (int w2 = 0; w2 < RS_THREADS / 64; w2++) {
+            const uint32_t c = wcnt[w2][b];
+            wcnt[w2][b] = o;
+            o += c;
         }
-        __syncthreads();
-        for (int b = t; b < nbins; b += RS_THREADS) {
-            run[b] += wcnt[0][b] + wcnt[1][b] + wcnt[2][b] + wcnt[3][b];
-            wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_R; r++) {
+        if (base + r * 64 + lane < N) {
+            const uint32_t pos = wcnt[w][(kk[r] >> shift) & (nbins - 1)] + rk[r];
+            keys_out[pos] = kk[r];
+            vals_out[pos] = vv[r];
         }
-        __syncthreads();
     }
 }
 
