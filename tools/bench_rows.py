@@ -203,7 +203,9 @@ def main():
         Q = X[qrows]
         alias = qrows.to(torch.int32)
         tq = gpu_time(ctx, lambda: lsh.query(Q, True, alias, device=True))
-        emit("get_LSH_filtered_combined_buckets", "queries/s", nq, tq, None, "65,536 dataset-row queries, C2 index")
+        tot = int(lsh.query(Q, True, alias, device=True)[0][-1])
+        emit("get_LSH_filtered_combined_buckets", "queries/s", nq, tq, None,
+             f"65,536 dataset-row queries, C2 index; {tot} rows returned",)
         del X
 
     if "cube" in rows:       # create_hypercube + get_hypercube_combined_buckets (C4)
@@ -226,7 +228,10 @@ def main():
         nq = 65_536
         Q = X[torch.arange(nq, device=ctx.dev) * (N // nq)]
         tq = gpu_time(ctx, lambda: cube.query(Q, 14, device=True), reps=3)
-        emit("get_hypercube_combined_buckets", "queries/s", nq, tq, None, "65,536 queries, probes=14 (Hamming<=1)")
+        tot = int(cube.query(Q, 14, device=True)[0][-1])
+        emit("get_hypercube_combined_buckets", "queries/s", nq, tq, None,
+             f"65,536 queries, probes=14 (Hamming<=1); {tot} candidate rows returned (bytes: 4 B read + 4 B "
+             f"written per candidate)", bytes_per_unit=8.0 * tot / nq)
         del X
 
     if "recom" in rows:      # get_P_closest + get_top_N_recom (crypto_rec.hpp:213-325)
