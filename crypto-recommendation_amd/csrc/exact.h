@@ -37,7 +37,7 @@ __device__ inline double one_minus(double q) { return q != q ? q : __dsub_rn(1.0
 
 // The soft-x87 form: every inner-product add emulated (~150 integer ops each).
 template <typename T, typename U>
-__device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __restrict__ c, int d) {
+__device__ inline double exact_cosine_x87_soft(const T* __restrict__ x, const U* __restrict__ c, int d) {
     sx80 ip = sx_zero();
     double a = 0.0, b = 0.0;
     for (int j = 0; j < d; j++) {
@@ -49,11 +49,32 @@ __device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __re
     return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
 }
 
+// The reference's cosine distance exactly: the x87 inner-product chain carried
+// as a double-double (softx87.h X87dd, ~30 fp64 ops per add, checked against
+// real long double on the host), the soft form only for the rare sums X87dd
+// does not decide.
+template <typename T, typename U>
+__device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __restrict__ c, int d) {
+    X87dd ip;
+    ip.init();
+    bool ok = true;
+    double a = 0.0, b = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j], cj = (double)c[j];
+        if (ok) ok = ip.add(__dmul_rn(xj, cj));
+        a = __dadd_rn(a, __dmul_rn(xj, xj));
+        b = __dadd_rn(b, __dmul_rn(cj, cj));
+    }
+    if (!ok) return exact_cosine_x87_soft(x, c, d);
+    return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
+}
+
 // exact_cosine_x87 for an fp32 row of d % 16 == 0 (16-B aligned rows): the row
-// and the centroid loaded 16 values at a time, so the soft chain waits on one
-// round trip per 16 terms instead of one per term.
+// and the centroid loaded 16 values at a time (one round trip per 16 terms).
 __device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
-    sx80 ip = sx_zero();
+    X87dd ip;
+    ip.init();
+    bool ok = true;
     double a = 0.0, b = 0.0;
     for (int j0 = 0; j0 < d; j0 += 16) {
         float xs[16];
@@ -71,12 +92,13 @@ __device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const
 #pragma unroll
         for (int t = 0; t < 16; t++) {
             const double xj = (double)xs[t], cj = cs[t];
-            ip = sx_add_double(ip, __dmul_rn(xj, cj));
+            if (ok) ok = ip.add(__dmul_rn(xj, cj));
             a = __dadd_rn(a, __dmul_rn(xj, xj));
             b = __dadd_rn(b, __dmul_rn(cj, cj));
         }
     }
-    return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
+    if (!ok) return exact_cosine_x87_soft(x, c, d);
+    return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
 }
 
 // Certified fast form of the x87 inner product's quotient (~12 fp64 ops per

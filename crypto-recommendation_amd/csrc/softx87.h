@@ -229,6 +229,61 @@ SX_HD int sx_hash_sign(const SxSum& ip) {
 }
 
 // Round to double, nearest-even (x87 FST m64 / the long double -> double cast).
+// The x87 running sum of doubles (FADD of a double operand, 64-bit
+// significand, nearest-even) carried EXACTLY as a double-double: S = h + l
+// (a 64-bit value fits in 106 bits). add(p): S <- RN64(S + p) in ~30 fp64
+// operations instead of a soft FADD: with (s, e1) = TwoSum(h, p) and (t, dl) =
+// TwoSum(l, e1), S + p = s + t + dl exactly; s lies on the 64-bit grid of the
+// result's binade E (|t + dl| << |s|), so RN64(S + p) = s + RN_grid(t + dl),
+// the grid rounding done by the magic constant 1.5 * 2^(E - 11) (whose ulp is
+// the grid spacing 2^(E - 63); ties go to even multiples, and s is an even
+// multiple, so that is the x87 tie rule), corrected when t sits exactly on a
+// midpoint and dl decides. E is the binade of fl(s + t) unless that is a power
+// of two, where the sign of S + p - 2^m decides between m and m - 1. Returns
+// false (state unspecified; the caller takes the soft form) for a zero-sum
+// with a nonzero residue or a magnitude outside [2^-899, 2^900] (incl.
+// inf / NaN products).
+struct X87dd {
+    double h, l;
+    SX_MD void init() { h = 0.0; l = 0.0; }
+    static SX_MD uint64_t bits(double v) { union { double d; uint64_t u; } c; c.d = v; return c.u; }
+    static SX_MD double from_bits(uint64_t u) { union { double d; uint64_t u; } c; c.u = u; return c.d; }
+    SX_MD bool add(double p) {
+        const double s = h + p, bb = s - h;
+        const double e1 = (h - (s - bb)) + (p - bb);
+        const double t = l + e1, b2 = t - l;
+        const double dl = (l - (t - b2)) + (e1 - b2);
+        const double u = s + t;
+        const uint64_t ub = bits(u);
+        int be = (int)((ub >> 52) & 0x7FF);
+        if (u == 0.0) {
+            if (dl != 0.0) return false;
+            h = 0.0; l = 0.0;                             // exact cancellation: +0
+            return true;
+        }
+        if (be < 124 || be > 1923) return false;
+        if ((ub & 0xFFFFFFFFFFFFFull) == 0) {            // u = +-2^m: is |S + p| below 2^m?
+            double w = (s - u) + t;                       // s - u exact (Sterbenz)
+            if (w == 0.0) w = dl;
+            if ((w < 0.0) != (u < 0.0) && w != 0.0) be -= 1;
+        }
+        const double ulp64 = from_bits((uint64_t)(be - 63) << 52);
+        const double C = from_bits(((uint64_t)(be - 11) << 52) | (1ull << 51));   // 1.5 * 2^(E - 11)
+        double r = (t + C) - C;
+        const double diff = t - r;
+        if (dl != 0.0 && (diff == 0.5 * ulp64 || diff == -0.5 * ulp64) && ((dl > 0.0) == (diff > 0.0)))
+            r += diff > 0.0 ? ulp64 : -ulp64;
+        const double nh = s + r, b3 = nh - s;
+        l = (s - (nh - b3)) + (r - b3);
+        h = nh;
+        return true;
+    }
+    // the 64-bit value as sx80 (h + l is exact in 64 bits: one exact FADD)
+    SX_MD sx80 value() const;
+};
+
+SX_MD sx80 X87dd::value() const { return sx_add_double(sx_from_double(h), l); }
+
 SX_HD double sx_to_double(sx80 v) {
     if (v.m == 0) return v.s ? -0.0 : 0.0;
     uint64_t keep = v.m >> 11, rem = v.m & 0x7FF;

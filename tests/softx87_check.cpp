@@ -107,6 +107,36 @@ int main(int argc, char** argv) {
         if (sx_hash_floor(s, (double)t, w) != want) { if (bad < 5) fprintf(stderr, "hash floor mismatch it=%ld\n", it); bad++; }
         if (sx_hash_sign(s) != (acc >= 0 ? 1 : 0)) { if (bad < 5) fprintf(stderr, "hash sign mismatch it=%ld\n", it); bad++; }
     }
+    // the double-double x87 accumulator (X87dd) against long double: random,
+    // cancelling, quantized (ties and powers of two) and wide-range terms
+    long dd_fallbacks = 0;
+    for (long it = 0; it < iters; it++) {
+        const int d = 1 + (int)(rng() % 160);
+        const int mode = (int)(rng() % 6);
+        long double acc = 0.0L;
+        X87dd x;
+        x.init();
+        bool ok = true;
+        for (int j = 0; j < d && ok; j++) {
+            double p;
+            if (mode == 0) p = (double)(float)u(rng) * (double)(float)u(rng);
+            else if (mode == 1) p = std::ldexp(u(rng), ex(rng));
+            else if (mode == 2) p = (j % 2 ? -1.0 : 1.0) * std::ldexp(1.0 + u(rng) * 1e-12, (int)(rng() % 3));
+            else if (mode == 3) p = (double)((int)(rng() % 81) - 40) / 8.0 * ((double)((int)(rng() % 81) - 40) / 8.0);
+            else if (mode == 4) p = std::ldexp(1.0, (int)(rng() % 120) - 60) * ((rng() & 1) ? 1.0 : -1.0);
+            else p = std::ldexp((double)(int64_t)(rng() % (1ull << 53)), -(int)(rng() % 106));
+            acc = acc + (long double)p;
+            ok = x.add(p);
+            if (!ok) { dd_fallbacks++; break; }
+            checks++;
+            if (!same(x.value(), acc) || (long double)x.h + (long double)x.l != acc) {
+                if (bad < 5) fprintf(stderr, "x87dd mismatch it=%ld j=%d mode=%d\n", it, j, mode);
+                bad++;
+                break;
+            }
+        }
+    }
+    printf("x87dd fallbacks=%ld\n", dd_fallbacks);
     printf("checks=%ld bad=%ld\n", checks, bad);
     return bad ? 1 : 0;
 }
