@@ -51,30 +51,27 @@ __device__ inline double exact_cosine_x87_soft(const T* __restrict__ x, const U*
 
 // The reference's cosine distance exactly: the x87 inner-product chain carried
 // as a double-double (softx87.h X87dd, ~30 fp64 ops per add, checked against
-// real long double on the host), the soft form only for the rare sums X87dd
-// does not decide.
+// real long double on the host), the soft FADD only past a sum X87dd does not
+// decide (X87acc).
 template <typename T, typename U>
 __device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __restrict__ c, int d) {
-    X87dd ip;
+    X87acc ip;
     ip.init();
-    bool ok = true;
     double a = 0.0, b = 0.0;
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], cj = (double)c[j];
-        if (ok) ok = ip.add(__dmul_rn(xj, cj));
+        ip.add(__dmul_rn(xj, cj));
         a = __dadd_rn(a, __dmul_rn(xj, xj));
         b = __dadd_rn(b, __dmul_rn(cj, cj));
     }
-    if (!ok) return exact_cosine_x87_soft(x, c, d);
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
 }
 
 // exact_cosine_x87 for an fp32 row of d % 16 == 0 (16-B aligned rows): the row
 // and the centroid loaded 16 values at a time (one round trip per 16 terms).
 __device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
-    X87dd ip;
+    X87acc ip;
     ip.init();
-    bool ok = true;
     double a = 0.0, b = 0.0;
     for (int j0 = 0; j0 < d; j0 += 16) {
         float xs[16];
@@ -92,12 +89,11 @@ __device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const
 #pragma unroll
         for (int t = 0; t < 16; t++) {
             const double xj = (double)xs[t], cj = cs[t];
-            if (ok) ok = ip.add(__dmul_rn(xj, cj));
+            ip.add(__dmul_rn(xj, cj));
             a = __dadd_rn(a, __dmul_rn(xj, xj));
             b = __dadd_rn(b, __dmul_rn(cj, cj));
         }
     }
-    if (!ok) return exact_cosine_x87_soft(x, c, d);
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
 }
 

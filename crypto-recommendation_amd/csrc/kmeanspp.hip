@@ -96,7 +96,8 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
         const int64_t n = row0 + threadIdx.x;
         const int rows = (int)(N - row0 < KPP_THREADS ? N - row0 : KPP_THREADS);
         double acc = 0.0, a = 0.0;
-        sx80 ip = sx_zero();
+        X87acc ip;
+        ip.init();
         float4 pf[KPP_V4];
         if (VEC) {
 #pragma unroll
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
                         const double df = __dsub_rn(xj, cj);
                         acc = __dadd_rn(acc, __dmul_rn(df, df));
                     } else {
-                        ip = sx_add_double(ip, __dmul_rn(xj, cj));
+                        ip.add(__dmul_rn(xj, cj));
                         a = __dadd_rn(a, __dmul_rn(xj, xj));
                     }
                 }
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
             dd = sqrt(acc);
         } else {
             const double denom = __dmul_rn(sqrt(a), sqrt(cb));
-            dd = one_minus(x87_quot(ip, denom));
+            dd = one_minus(x87_quot(ip.value(), denom));
         }
         double m = dd;
         if (it > 1) {

@@ -28,9 +28,10 @@ constexpr int RC_MAXV = 8;       // candidates per lane held in registers (n <= 
 // (xa, ub: sum of squares in dim order), long-double division, then double.
 __device__ inline double rc_cos_sim(const double* __restrict__ x, const double* __restrict__ u, int d, double xa,
                                     double ub) {
-    sx80 ip = sx_zero();
-    for (int j = 0; j < d; j++) ip = sx_add_double(ip, __dmul_rn(x[j], u[j]));
-    return x87_quot(ip, __dmul_rn(sqrt(xa), sqrt(ub)));
+    X87acc ip;
+    ip.init();
+    for (int j = 0; j < d; j++) ip.add(__dmul_rn(x[j], u[j]));
+    return x87_quot(ip.value(), __dmul_rn(sqrt(xa), sqrt(ub)));
 }
 
 __device__ inline double rc_sumsq(const double* __restrict__ x, int d) {

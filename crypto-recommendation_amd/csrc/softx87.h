@@ -284,6 +284,25 @@ struct X87dd {
 
 SX_MD sx80 X87dd::value() const { return sx_add_double(sx_from_double(h), l); }
 
+// The x87 chain for any double terms: X87dd while it decides (add leaves the
+// state untouched when it returns false), the soft FADD from that exact state
+// on. A drop-in for `sx80 ip = sx_zero(); ip = sx_add_double(ip, p);`.
+struct X87acc {
+    X87dd dd;
+    sx80 sx;
+    bool soft;
+    SX_MD void init() { dd.init(); sx = sx_zero(); soft = false; }
+    SX_MD void add(double p) {
+        if (!soft) {
+            if (dd.add(p)) return;
+            sx = dd.value();
+            soft = true;
+        }
+        sx = sx_add_double(sx, p);
+    }
+    SX_MD sx80 value() const { return soft ? sx : dd.value(); }
+};
+
 SX_HD double sx_to_double(sx80 v) {
     if (v.m == 0) return v.s ? -0.0 : 0.0;
     uint64_t keep = v.m >> 11, rem = v.m & 0x7FF;

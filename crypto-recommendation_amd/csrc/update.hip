@@ -280,15 +280,16 @@ __global__ __launch_bounds__(64) void km_finalize_kernel(const double* __restric
         }
         dist = sqrt(acc);
     } else {
-        sx80 ip = sx_zero();
+        X87acc ip;
+        ip.init();
         double x = 0.0, y = 0.0;
         for (int j = 0; j < d; j++) {
-            ip = sx_add_double(ip, __dmul_rn(a[j], b[j]));
+            ip.add(__dmul_rn(a[j], b[j]));
             x = __dadd_rn(x, __dmul_rn(a[j], a[j]));
             y = __dadd_rn(y, __dmul_rn(b[j], b[j]));
         }
         const double denom = __dmul_rn(sqrt(x), sqrt(y));
-        dist = one_minus(x87_quot(ip, denom));
+        dist = one_minus(x87_quot(ip.value(), denom));
     }
     if (dist > min_dist) atomicOr(moved, 1);
 }

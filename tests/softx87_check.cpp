@@ -136,7 +136,32 @@ int main(int argc, char** argv) {
             }
         }
     }
-    printf("x87dd fallbacks=%ld\n", dd_fallbacks);
+    // X87acc (dd, then the soft FADD from the same exact state): wide ranges
+    // that make X87dd hand over mid-chain, and cancellations to zero
+    long handovers = 0;
+    for (long it = 0; it < iters / 2; it++) {
+        const int d = 1 + (int)(rng() % 100);
+        long double acc = 0.0L;
+        X87acc x;
+        x.init();
+        for (int j = 0; j < d; j++) {
+            double p;
+            const int m = (int)(rng() % 8);
+            if (m == 0) p = std::ldexp(u(rng), (int)(rng() % 1900) - 950);
+            else if (m == 1 && j > 0) p = -(double)acc;
+            else p = (double)(float)u(rng) * (double)(float)u(rng);
+            acc = acc + (long double)p;
+            x.add(p);
+            checks++;
+            if (!same(x.value(), acc)) {
+                if (bad < 5) fprintf(stderr, "x87acc mismatch it=%ld j=%d\n", it, j);
+                bad++;
+                break;
+            }
+        }
+        handovers += x.soft ? 1 : 0;
+    }
+    printf("x87dd fallbacks=%ld x87acc handovers=%ld\n", dd_fallbacks, handovers);
     printf("checks=%ld bad=%ld\n", checks, bad);
     return bad ? 1 : 0;
 }
