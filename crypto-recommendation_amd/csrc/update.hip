@@ -162,6 +162,57 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int
     if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
 }
 
+// fp32 rows with d % 128 == 0: a wave reads whole 512-B row slices (two
+// dims per lane, float2), half the load instructions of km_fx_kernel's 256-B
+// half-rows for the same gather.
+__global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X, int d, const int32_t* __restrict__ rows,
+                                                    const int64_t* __restrict__ crow, int K, int64_t M,
+                                                    KmFx* __restrict__ acc) {
+    const int64_t p0 = (int64_t)blockIdx.x * KMF_CH;
+    if (p0 >= M) return;
+    const int64_t p1 = min(M, p0 + KMF_CH);
+    const int j = blockIdx.y * 128 + 2 * threadIdx.x;
+    const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
+    int lo = 0, hi = K;              // crow[lo] <= p0 < crow[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (crow[mid] <= p0) lo = mid; else hi = mid;
+    }
+    int c = lo;
+    int64_t cend = crow[c + 1];
+    double s0 = 0.0, s1 = 0.0;
+    int q0 = 1 << 30, t0 = -(1 << 30), q1 = 1 << 30, t1 = -(1 << 30);
+    bool bad0 = false, bad1 = false;
+    for (int64_t p = p0; p < p1; p += 16) {
+        float2 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            v[u] = p + u < p1 ? *reinterpret_cast<const float2*>(X + (int64_t)r4[p + u] * d + j) : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            if (p + u >= p1) break;
+            while (p + u >= cend) {              // cluster boundary: flush, move on (skipping empty clusters)
+                km_fx_flush(acc + (size_t)c * d + j, s0, q0, t0, bad0);
+                km_fx_flush(acc + (size_t)c * d + j + 1, s1, q1, t1, bad1);
+                s0 = s1 = 0.0; q0 = q1 = 1 << 30; t0 = t1 = -(1 << 30); bad0 = bad1 = false;
+                c++;
+                cend = crow[c + 1];
+            }
+            int q, t;
+            if (km_fx_bits(v[u].x, q, t, bad0)) {
+                q0 = min(q0, q); t0 = max(t0, t);
+                s0 = __dadd_rn(s0, (double)v[u].x);
+            }
+            if (km_fx_bits(v[u].y, q, t, bad1)) {
+                q1 = min(q1, q); t1 = max(t1, t);
+                s1 = __dadd_rn(s1, (double)v[u].y);
+            }
+        }
+    }
+    km_fx_flush(acc + (size_t)c * d + j, s0, q0, t0, bad0);
+    km_fx_flush(acc + (size_t)c * d + j + 1, s1, q1, t1, bad1);
+}
+
 // Per (c, j): the exact sum if the chain provably never rounds, else a flag for
 // the sequential kernel. carry (sharded exact mode): the chain starts from it.
 __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_t* __restrict__ crow, int K, int d,
@@ -239,6 +290,9 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
     const dim3 fgrid((unsigned)((M + KMF_CH - 1) / KMF_CH), (unsigned)jb);
     if (M > 0) {
         if (X.f64) hipLaunchKernelGGL(km_fx_kernel<double>, fgrid, dim3(64), 0, s, X.d(), d, rows, crow, K, M, acc);
+        else if (d % 128 == 0)
+            hipLaunchKernelGGL(km_fx2_kernel, dim3(fgrid.x, (unsigned)(d / 128)), dim3(64), 0, s, X.f(), d, rows, crow, K, M,
+                               acc);
         else hipLaunchKernelGGL(km_fx_kernel<float>, fgrid, dim3(64), 0, s, X.f(), d, rows, crow, K, M, acc);
     }
     hipLaunchKernelGGL(km_fx_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, crow, K, d, carry,
