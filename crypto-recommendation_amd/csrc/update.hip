@@ -165,6 +165,9 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int
 // fp32 rows with d % 128 == 0: a wave reads whole 512-B row slices (two
 // dims per lane, float2), half the load instructions of km_fx_kernel's 256-B
 // half-rows for the same gather.
+#ifndef KMF2_U
+#define KMF2_U 16       // rows in flight per wave
+#endif
 __global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                     const int64_t* __restrict__ crow, int K, int64_t M,
                                                     KmFx* __restrict__ acc) {
@@ -183,13 +186,13 @@ __global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X,
     double s0 = 0.0, s1 = 0.0;
     int q0 = 1 << 30, t0 = -(1 << 30), q1 = 1 << 30, t1 = -(1 << 30);
     bool bad0 = false, bad1 = false;
-    for (int64_t p = p0; p < p1; p += 16) {
-        float2 v[16];
+    for (int64_t p = p0; p < p1; p += KMF2_U) {
+        float2 v[KMF2_U];
 #pragma unroll
-        for (int u = 0; u < 16; u++)
+        for (int u = 0; u < KMF2_U; u++)
             v[u] = p + u < p1 ? *reinterpret_cast<const float2*>(X + (int64_t)r4[p + u] * d + j) : make_float2(0.f, 0.f);
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
+        for (int u = 0; u < KMF2_U; u++) {
             if (p + u >= p1) break;
             while (p + u >= cend) {              // cluster boundary: flush, move on (skipping empty clusters)
                 km_fx_flush(acc + (size_t)c * d + j, s0, q0, t0, bad0);
