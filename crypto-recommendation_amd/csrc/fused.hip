@@ -732,7 +732,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             const float* lP = lpn0 + hc;
             const float* lQ = lv10 + hc;
             const int32_t* lr = lr0 + hc;
-            if (!x_ok) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
+            if (!x_ok && valid) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int l = 2 * g + h;
@@ -1133,27 +1133,42 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
     return st;
 }
 
-template <bool HASH, bool MP = false, int MET = 0>
+// NIMG = 2 (512 < K <= 1024, euclidean): ONE launch for all centroids. The
+// LDS holds one 512-centroid image at a time; the block's waves each score
+// their tile against the image in LDS, the block swaps in the other image
+// (two barriers, 128 KB from L2), and the waves finish the same tile against
+// it with the row still in registers -- no second read of X and no carried
+// pass state. Images alternate A,B / B,A between rounds (one swap per round);
+// every wave runs the block's round count (tiles past the end: no valid rows).
+template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1>
 __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_kernel(FusedArgs a) {
     constexpr int FH_WAVES = fh_waves<HASH, MP, MET>();
     constexpr int FH_THREADS = 64 * FH_WAVES;
+    static_assert(NIMG == 1 || (!MP && MET == 0), "two-image form: euclidean, single launch");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
+    const int KI = NIMG == 2 ? FH_KMAX : Kpad;           // centroid rows the LDS image holds
     int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows, [2] cosine declines
     _Float16* lch = reinterpret_cast<_Float16*>(smem + 16);
-    float* lcn = reinterpret_cast<float*>(lch + Kpad * FU_RS);
-    _Float16* lvh = reinterpret_cast<_Float16*>(lcn + Kpad);
+    float* lcn = reinterpret_cast<float*>(lch + KI * FU_RS);
+    _Float16* lvh = reinterpret_cast<_Float16*>(lcn + KI);
     _Float16* lvl = lvh + 32 * FU_RS;
     float* lpn0 = reinterpret_cast<float*>(lvl + 32 * FU_RS);
     float* lv10 = lpn0 + 32;
     float* lt0 = lv10 + 32;
     int32_t* lr0 = reinterpret_cast<int32_t*>(lt0 + 32);
 
-    for (int e = threadIdx.x; e < Kpad * 16; e += FH_THREADS) {
-        const int r = e >> 4, g = e & 15;
-        *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Ch + (size_t)r * FU_D + g * 8);
-    }
-    for (int e = threadIdx.x; e < Kpad; e += FH_THREADS) lcn[e] = a.cnh[e];
+    // image img: centroid rows [img * KI, img * KI + rows) into LDS rows 0..
+    auto load_image = [&](int img) {
+        const int r0 = img * KI, nr = NIMG == 2 && img == 1 ? Kpad - FH_KMAX : KI;
+        for (int e = threadIdx.x; e < nr * 16; e += FH_THREADS) {
+            const int r = e >> 4, g = e & 15;
+            *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) =
+                *reinterpret_cast<const float4*>(a.Ch + (size_t)(r0 + r) * FU_D + g * 8);
+        }
+        for (int e = threadIdx.x; e < nr; e += FH_THREADS) lcn[e] = a.cnh[r0 + e];
+    };
+    load_image(0);
     if (threadIdx.x < 3) lcount[threadIdx.x] = 0;
     int32_t* ambig_seg = a.ambig + (int64_t)blockIdx.x * a.seg_rows;
     unsigned long long* hfix_seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
@@ -1190,7 +1205,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     // point-independent part of the bound
     const double Ec = (0x1p-24 + FH_A) * (double)cnf + 0x1p-41 * (double)cmaxf * (double)cmaxf + 0x1p-18 * (double)cnf;
 
-    for (int64_t tile = (int64_t)blockIdx.x * FH_WAVES + wave; tile < ntiles; tile += (int64_t)gridDim.x * FH_WAVES) {
+    const int64_t tstride = (int64_t)gridDim.x * FH_WAVES, tfirst = (int64_t)blockIdx.x * FH_WAVES;
+    const int64_t nround = NIMG == 2 && ntiles > tfirst ? (ntiles - tfirst + tstride - 1) / tstride : 0;
+    int64_t rd = 0;
+    for (int64_t tile = tfirst + wave; NIMG == 2 ? rd < nround : tile < ntiles; tile += tstride, rd++) {
         const int64_t row = tile * 32 + col;
         const bool valid = row < a.N;
         float xf[64];
@@ -1296,7 +1314,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             const float* lP = lpn0 + hc;
             const float* lQ = lv10 + hc;
             const int32_t* lr = lr0 + hc;
-            if (!x_ok) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
+            if (!x_ok && valid) fmask = (a.LK >= 32 ? 0xFFFFFFFFu : (1u << a.LK) - 1u);
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int l = 2 * g + h;
@@ -1365,27 +1383,41 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #else
         const int ntile_run = ntile32;
 #endif
+        auto run_tiles = [&](int ntl, int tgo) {
 #pragma unroll TILE_UNROLL
-        for (int t = 0; t < ntile_run; t++) {
-            const float m1_prev = m1;
-            floatx16 acc;
-            const float* cn_t = lcn + t * 32 + 4 * h;     // D rows 8g + 4h + q of registers 4g + q
+            for (int t = 0; t < ntl; t++) {
+                const float m1_prev = m1;
+                floatx16 acc;
+                const float* cn_t = lcn + t * 32 + 4 * h;     // D rows 8g + 4h + q of registers 4g + q
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const float4 cn = *reinterpret_cast<const float4*>(cn_t + 8 * g);
-                acc[4 * g] = cn.x; acc[4 * g + 1] = cn.y; acc[4 * g + 2] = cn.z; acc[4 * g + 3] = cn.w;
+                for (int g = 0; g < 4; g++) {
+                    const float4 cn = *reinterpret_cast<const float4*>(cn_t + 8 * g);
+                    acc[4 * g] = cn.x; acc[4 * g + 1] = cn.y; acc[4 * g + 2] = cn.z; acc[4 * g + 3] = cn.w;
+                }
+                const _Float16* arow = my_h + t * 32 * FU_RS;
+#pragma unroll
+                for (int s = 0; s < 8; s++) {
+                    const half8 ah = *reinterpret_cast<const half8*>(arow + 16 * s);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
+                }
+                float sv[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) sv[r] = acc[r];
+                tile_epilogue(sv, m1, m2);
+                t1 = m1 != m1_prev ? t + tgo : t1;
             }
-            const _Float16* arow = my_h + t * 32 * FU_RS;
-#pragma unroll
-            for (int s = 0; s < 8; s++) {
-                const half8 ah = *reinterpret_cast<const half8*>(arow + 16 * s);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc, 0, 0, 0);
-            }
-            float sv[16];
-#pragma unroll
-            for (int r = 0; r < 16; r++) sv[r] = acc[r];
-            tile_epilogue(sv, m1, m2);
-            t1 = m1 != m1_prev ? t + tg0 : t1;
+        };
+        if (NIMG == 1) {
+            run_tiles(ntile_run, tg0);
+        } else {
+            // the image in LDS at this round's start, then the other one
+            const int i0 = (int)(rd & 1);
+            const int nA = FH_KMAX / 32, nB = (Kpad - FH_KMAX) / 32;
+            run_tiles(i0 == 0 ? nA : nB, i0 * nA);
+            __syncthreads();
+            load_image(1 - i0);
+            __syncthreads();
+            run_tiles(i0 == 0 ? nB : nA, (1 - i0) * nA);
         }
 #if MFMA_PRIO
         __builtin_amdgcn_s_setprio(0);
@@ -1908,7 +1940,21 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             }
             const int np1 = (f.Kpad + FH_KMAX - 1) / FH_KMAX;
             a.ambig_count = f.refined;
-            for (int p = 0; p < np1; p++) {
+            // 512 < K <= 1024, euclidean, LSHKM_HI_TWO_IMAGE=1: one two-image launch
+            // instead of two passes with carried state. Measured at C5 (N = 10M,
+            // K = 1024): 5.09 ms vs 1.83 + 2.51 ms, HBM 8.9 GB vs 13.8 GB per call --
+            // the block-wide image swaps line the waves up and cost the MFMA/VALU
+            // overlap between them, more than the second read of X costs; opt-in.
+            const char* ti = getenv("LSHKM_HI_TWO_IMAGE");
+            const bool two_image = !cos && np1 == 2 && ti && !strcmp(ti, "1");
+            if (two_image) {
+                a.Ch = f.Ch; a.cnh = f.cnh; a.Kpad = f.Kpad;
+                a.t0 = 0; a.pass_first = 1; a.pass_last = 1;
+                const size_t lh = (size_t)fh_lds_bytes(FH_KMAX, hash);
+                if (hash) hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 2>), grid, dim3(64 * fh_waves<true, false, 0>()), lh, s, a);
+                else hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 2>), grid, dim3(64 * fh_waves<false, false, 0>()), lh, s, a);
+            }
+            for (int p = 0; p < (two_image ? 0 : np1); p++) {
                 const int c0 = p * FH_KMAX;
                 a.Ch = f.Ch + (size_t)c0 * FU_D; a.cnh = f.cnh + c0;
                 a.Kpad = std::min(FH_KMAX, f.Kpad - c0);
