@@ -381,6 +381,33 @@ def test_multipass_persistent_k1024(ctx, metric, monkeypatch):
     assert np.array_equal(d0.cpu().numpy()[sub].view(np.uint64), od.view(np.uint64))
 
 
+@pytest.mark.parametrize("hashed", [False, True])
+def test_two_image_k1000(ctx, hashed, monkeypatch):
+    # the opt-in one-launch form for 512 < K <= 1024 (LSHKM_HI_TWO_IMAGE=1): the
+    # block swaps 512-centroid images between the halves of each tile; ties
+    # across the images, a ragged second image (K = 1000) and a partial last
+    # round, bit-equal to the two-pass default (hash outputs too)
+    N, d, K, L, k = 40_011, 128, 1000, 5, 4
+    X = ctx.synth(0x21A6, N, d)
+    rng = np.random.default_rng(21)
+    rows = rng.choice(N, K, replace=False).astype(np.int64)
+    Cc = X[to_dev(ctx, rows)].double()
+    Cc[700:710] = Cc[100:110]                         # exact ties across the two images
+    V, t, r, _ = lshkm.params_lsh_euclidean(77, L, k, d, 0.4)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
+
+    def run():
+        if hashed:
+            return lshkm.hash_assign(lsh, X, Cc, tuples=True, bucket=True)
+        return lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
+    ref = [v.cpu().numpy() for v in run() if v is not None]
+    monkeypatch.setenv("LSHKM_HI_TWO_IMAGE", "1")
+    got = [v.cpu().numpy() for v in run() if v is not None]
+    assert len(ref) == len(got)
+    for a, b in zip(ref, got):
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
 @pytest.mark.parametrize("N,K,case", [(200_000, 256, "rows"), (50_000, 1000, "rows"), (30_011, 64, "special"),
                                       (40_000, 200, "scaled")])
 def test_cosine_hash_assign_fused(ctx, N, K, case):
