@@ -1367,6 +1367,12 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             }
         }
 
+        // the certificate's bound E depends on the row only: formed before the
+        // centroid tiles (its fp64 ops overlap the MFMAs). cosine: + 2^-43 |x| for the normalisation and the reference's own q
+        // (fused_persistent_kernel's cosine bound)
+        const double E = (nxh * (double)crf + nxr * (double)cmaxf + FH_A * nxh * (double)chf + 0x1p-41 * xn2 +
+                          0x1p-18 * nx * (double)cmaxf + (MET == 1 ? 0x1p-43 * nx : 0.0) + Ec) * (1.0 + 0x1p-20) +
+                         1e-30;
         // ---- centroid tiles: 8 MFMAs each, accumulator initialised with -|c|^2/2
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
         int t1 = 0;
@@ -1434,11 +1440,18 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         const float M2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
         const int I1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
         const float M1 = fmaxf(m1, om1);
-        // cosine: + 2^-43 |x| for the normalisation and the reference's own q
-        // (fused_persistent_kernel's cosine bound)
-        const double E = (nxh * (double)crf + nxr * (double)cmaxf + FH_A * nxh * (double)chf + 0x1p-41 * xn2 +
-                          0x1p-18 * nx * (double)cmaxf + (MET == 1 ? 0x1p-43 * nx : 0.0) + Ec) * (1.0 + 0x1p-20) +
-                         1e-30;
+#if !defined(ABL_NOCHAIN)
+        // the winner's fp64 row: the first loads go out before the certificate
+        // and the list append
+        const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
+        double2 cbuf[CHAIN_PF][4];
+        if (MET == 0) {
+#pragma unroll
+            for (int s = 0; s < CHAIN_PF; s++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) cbuf[s][j] = *reinterpret_cast<const double2*>(crow + 16 * s + 2 * j);
+        }
+#endif
         const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
 
         const bool amb = valid && !cert;
@@ -1478,13 +1491,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         {
             // winner distance in reference order from the row kept in registers:
             // the lane halves take turns on the chain, 8 dims each
-            const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
             double acc = 0.0;
-            double2 cbuf[CHAIN_PF][4];
-#pragma unroll
-            for (int s = 0; s < CHAIN_PF; s++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) cbuf[s][j] = *reinterpret_cast<const double2*>(crow + 16 * s + 2 * j);
 #pragma unroll
             for (int s = 0; s < 8; s++) {
                 double sq[8];
