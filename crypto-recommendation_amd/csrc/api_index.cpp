@@ -129,6 +129,7 @@ static int lsh_build_impl(lshkm_lsh lsh, Pts X, int64_t N) {
         return rc;
     lsh->N = N;
     lsh->built = 1;
+    lsh->mt0_valid = false;
     return 0;
 }
 
@@ -190,7 +191,7 @@ static int lsh_query_impl(lshkm_lsh lsh, Pts Q, int64_t nq, const int32_t* alias
                                    lsh->bucket.as<int32_t>(), lsh->row_ptr.as<int64_t>(), lsh->idx.as<int32_t>(),
                                    slot<int64_t>(ctx, WS_SIZES), slot<int64_t>(ctx, WS_COFF), slot<int32_t>(ctx, WS_KLIST),
                                    slot<int64_t>(ctx, WS_KCNT), slot<int64_t>(ctx, WS_QSZ), out_ptr, out_idx, 2,
-                                   nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                                   nullptr, lsh->mt0_valid ? lsh->mt0.as<int32_t>() : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
         return 0;
     }
     if ((rc = reserve(ctx, WS_QTUP, (size_t)pairs * k * 4)) || (rc = reserve(ctx, WS_QBKT, (size_t)pairs * 4)) ||
@@ -207,8 +208,14 @@ static int lsh_query_impl(lshkm_lsh lsh, Pts Q, int64_t nq, const int32_t* alias
                                 lsh->bucket.as<int32_t>(), lsh->row_ptr.as<int64_t>(), lsh->idx.as<int32_t>(),
                                 slot<int64_t>(ctx, WS_SIZES), slot<int64_t>(ctx, WS_COFF), slot<int32_t>(ctx, WS_KLIST),
                                 slot<int64_t>(ctx, WS_KCNT), slot<int64_t>(ctx, WS_QSZ), out_ptr, out, phase,
-                                ctx->ws_scan.as<int64_t>());
+                                ctx->ws_scan.as<int64_t>(), lsh->mt0_valid ? lsh->mt0.as<int32_t>() : nullptr);
     };
+    if (eu && filtered && !lsh->mt0_valid && lsh->N > 0) {
+        if ((rc = lsh->mt0.reserve((size_t)lsh->N * L * 4))) return rc;
+        if ((rc = launch_lsh_gather_t0(s, lsh->tuples.as<int32_t>(), lsh->idx.as<int32_t>(), lsh->N, L, k,
+                                       lsh->mt0.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        lsh->mt0_valid = true;
+    }
     if ((rc = run(0, nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
     int64_t cand = 0;
     if ((rc = d2h(ctx, &cand, slot<int64_t>(ctx, WS_COFF) + pairs, 8))) return rc;

@@ -102,6 +102,12 @@ struct lshkm_lsh_s {
     int built = 0;
     int64_t N = 0;
     lshkm::Buf tuples, bucket, row_ptr, idx;
+    // filtered queries: each table's members' first tuple value in CSR order
+    // (mt0[l * N + pos]), gathered once after a build by the first filtered
+    // query, so the marking pass reads it coalesced instead of one random
+    // tuple line per member
+    lshkm::Buf mt0;
+    bool mt0_valid = false;
     // two-phase query: the sizing call's device state, reused by the filling
     // call when nothing else touched the context's slots in between
     bool q_valid = false;

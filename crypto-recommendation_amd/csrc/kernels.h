@@ -127,7 +127,8 @@ int launch_lsh_query(hipStream_t s, const int32_t* qbucket, const int32_t* qtupl
                      int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* tuples, const int32_t* bucket,
                      const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* cand_off,
                      int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase,
-                     int64_t* scan_ws = nullptr);
+                     int64_t* scan_ws = nullptr, const int32_t* mt0 = nullptr);
+int launch_lsh_gather_t0(hipStream_t s, const int32_t* tuples, const int32_t* idx, int64_t N, int L, int k, int32_t* mt0);
 int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int32_t* masks, int S,
                       const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* slot_off,
                       int64_t* out_ptr, int32_t* out, int64_t* scan_ws = nullptr);

@@ -117,15 +117,22 @@ __device__ inline bool tuple_eq(const int32_t* __restrict__ a, const int32_t* __
     return true;
 }
 
-// One wave per (query, table).
+// Four (query, table) pairs per wave, 16 lanes each: a pair's work is a short
+// chain of dependent loads (bucket id -> bucket bounds -> member ids -> their
+// tuples), so the wave keeps four chains in flight instead of one.
+constexpr int LQ_U = 4;          // 16-member chunks per round, loads in flight together
+constexpr int LQ_G = 16;         // lanes per pair
 __global__ __launch_bounds__(256) void lq_mark(
     const int32_t* __restrict__ qbucket, const int32_t* __restrict__ qtuple, const int32_t* __restrict__ alias,
     int64_t nq, int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* __restrict__ tuples,
     const int32_t* __restrict__ bucket, const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ idx,
-    const int64_t* __restrict__ cand_off, int32_t* __restrict__ klist, int64_t* __restrict__ kcount) {
-    const int lane = threadIdx.x & 63;
-    const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (pair >= nq * L) return;
+    const int64_t* __restrict__ cand_off, int32_t* __restrict__ klist, int64_t* __restrict__ kcount,
+    const int32_t* __restrict__ mt0) {
+    const int lane = threadIdx.x & 63, gl = lane & (LQ_G - 1), grp = lane / LQ_G;
+    const int64_t pair = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LQ_G) + grp;
+    if (pair >= nq * L) return;                          // whole groups (pair is uniform in a group)
+    const unsigned long long gmask = ((1ull << LQ_G) - 1ull) << (grp * LQ_G);
+    const unsigned long long lt = (1ull << lane) - 1ull;
     const int64_t q = pair / L;
     const int l = (int)(pair - q * L);
     const int32_t* qt = nullptr;
@@ -138,24 +145,44 @@ __global__ __launch_bounds__(256) void lq_mark(
     const int64_t beg = rp[qb[l]], end = rp[qb[l] + 1];
     const int32_t* members = idx + (size_t)l * N;
     int64_t out = cand_off[pair];
-    for (int64_t p0 = beg; p0 < end; p0 += 64) {
-        const int64_t p = p0 + lane;
-        bool keep = false;
-        int32_t m = 0;
-        if (p < end) {
-            m = members[p];
-            const int32_t* mt = tuples ? tuples + (size_t)m * L * k : nullptr;
-            keep = !qt || tuple_eq(mt + l * k, qt + l * k, k);
-            for (int l2 = 0; keep && l2 < l; l2++) {
-                const bool in2 = bucket[(size_t)m * L + l2] == qb[l2] && (!qt || tuple_eq(mt + l2 * k, qt + l2 * k, k));
-                if (in2) keep = false;
-            }
+    const int32_t q0 = qt ? qt[l * k] : 0;
+    // LQ_U chunks of 16 members: the member ids, then the first tuple value of
+    // each (a random member's tuple almost always differs there), in flight
+    // together; the rest of the tuple and the earlier-table dedup only for the
+    // lanes still in; compaction in member order within the group
+    for (int64_t p0 = beg; p0 < end; p0 += LQ_G * LQ_U) {
+        int32_t m[LQ_U], t0[LQ_U];
+#pragma unroll
+        for (int u = 0; u < LQ_U; u++) {
+            const int64_t p = p0 + LQ_G * u + gl;
+            m[u] = p < end ? members[p] : 0;
         }
-        const unsigned long long bal = __ballot(keep);
-        if (keep) klist[out + __popcll(bal & ((1ull << lane) - 1ull))] = m;
-        out += __popcll(bal);
+#pragma unroll
+        for (int u = 0; u < LQ_U; u++) {
+            const int64_t p = p0 + LQ_G * u + gl;
+            t0[u] = !qt || p >= end ? 0 : mt0 ? mt0[(size_t)l * N + p] : tuples[(size_t)m[u] * L * k + l * k];
+        }
+#pragma unroll
+        for (int u = 0; u < LQ_U; u++) {
+            const int64_t p = p0 + LQ_G * u + gl;
+            bool keep = p < end && (!qt || t0[u] == q0);
+            if (keep && qt) {
+                const int32_t* mt = tuples + (size_t)m[u] * L * k;
+                keep = tuple_eq(mt + l * k + 1, qt + l * k + 1, k - 1);
+            }
+            if (keep) {
+                const int32_t* mt = tuples ? tuples + (size_t)m[u] * L * k : nullptr;
+                for (int l2 = 0; keep && l2 < l; l2++) {
+                    const bool in2 = bucket[(size_t)m[u] * L + l2] == qb[l2] && (!qt || tuple_eq(mt + l2 * k, qt + l2 * k, k));
+                    if (in2) keep = false;
+                }
+            }
+            const unsigned long long bal = __ballot(keep) & gmask;
+            if (keep) klist[out + __popcll(bal & lt)] = m[u];
+            out += __popcll(bal);
+        }
     }
-    if (lane == 0) kcount[pair] = out - cand_off[pair];
+    if (gl == 0) kcount[pair] = out - cand_off[pair];
 }
 
 __global__ void lq_qsizes(const int64_t* __restrict__ kcount, int64_t nq, int L, int64_t* __restrict__ qsz) {
@@ -194,15 +221,16 @@ int launch_lsh_query(hipStream_t s, const int32_t* qbucket, const int32_t* qtupl
                      int L, int k, int64_t nb, int filtered, int64_t N, const int32_t* tuples, const int32_t* bucket,
                      const int64_t* row_ptr, const int32_t* idx, int64_t* sizes, int64_t* cand_off,
                      int32_t* klist, int64_t* kcount, int64_t* qsz, int64_t* out_ptr, int32_t* out, int phase,
-                     int64_t* scan_ws) {
+                     int64_t* scan_ws, const int32_t* mt0) {
     const int64_t pairs = nq * L;
     if (phase == 0) {          // candidate counts -> cand_off[pairs + 1]
         hipLaunchKernelGGL(lq_sizes, dim3((unsigned)std::min<int64_t>((pairs + 255) / 256, 4096)), dim3(256), 0, s, qbucket,
                            nq, L, nb, row_ptr, sizes);
         if (launch_scan_i64(s, sizes, pairs, cand_off, scan_ws)) return -2;
     } else if (phase == 1) {   // filter + dedup + compact -> out_ptr[nq + 1]
-        hipLaunchKernelGGL(lq_mark, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, qbucket, qtuple, alias, nq, L, k,
-                           nb, filtered, N, tuples, bucket, row_ptr, idx, cand_off, klist, kcount);
+        hipLaunchKernelGGL(lq_mark, dim3((unsigned)((pairs + 4 * (64 / LQ_G) - 1) / (4 * (64 / LQ_G)))), dim3(256), 0, s,
+                           qbucket, qtuple, alias, nq, L, k,
+                           nb, filtered, N, tuples, bucket, row_ptr, idx, cand_off, klist, kcount, mt0);
         hipLaunchKernelGGL(lq_qsizes, dim3((unsigned)std::min<int64_t>((nq + 255) / 256, 4096)), dim3(256), 0, s, kcount,
                            nq, L, qsz);
         if (launch_scan_i64(s, qsz, nq, out_ptr, scan_ws)) return -2;
@@ -210,6 +238,20 @@ int launch_lsh_query(hipStream_t s, const int32_t* qbucket, const int32_t* qtupl
         hipLaunchKernelGGL(lq_merge, dim3((unsigned)((pairs + 3) / 4)), dim3(256), 0, s, cand_off, kcount, klist, nq, L,
                            out_ptr, out);
     }
+    return kstatus("query.hip");
+}
+
+// mt0[l * N + pos] = the first tuple value of table l's member at CSR position pos
+__global__ void lq_gather_t0(const int32_t* __restrict__ tuples, const int32_t* __restrict__ idx, int64_t N, int L,
+                             int k, int32_t* __restrict__ mt0) {
+    const int l = blockIdx.y;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x)
+        mt0[(size_t)l * N + p] = tuples[(size_t)idx[(size_t)l * N + p] * L * k + l * k];
+}
+int launch_lsh_gather_t0(hipStream_t s, const int32_t* tuples, const int32_t* idx, int64_t N, int L, int k, int32_t* mt0) {
+    if (N <= 0) return 0;
+    hipLaunchKernelGGL(lq_gather_t0, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 4096), (unsigned)L), dim3(256), 0, s,
+                       tuples, idx, N, L, k, mt0);
     return kstatus("query.hip");
 }
 
