@@ -579,6 +579,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             f.tuples = cosine ? nullptr : tuples ? tuples : (int32_t*)ctx->ws_tuples.p;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
         }
+        if (fuse_hash && ctx->side_init() == 0) { f.side = ctx->side_stream; f.fork = ctx->fork_ev; f.join = ctx->join_ev; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
         if ((rc = launch_fused(s, fuse_hash, f))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));

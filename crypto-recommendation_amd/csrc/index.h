@@ -71,6 +71,18 @@ struct lshkm_ctx_s {
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
     bool timing = false;
     hipEvent_t tev[2] = {nullptr, nullptr};
+    // a side stream for work independent of the main stream's next kernels
+    // (the hash fix-up beside the LIST refinement), forked / joined by events
+    hipStream_t side_stream = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    int side_init() {
+        if (side_stream) return 0;
+        if (hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking) != hipSuccess) return -2;
+        if (hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&join_ev, hipEventDisableTiming) != hipSuccess)
+            return -2;
+        return 0;
+    }
     // pinned host staging for small host->device inputs
     void* pinned = nullptr;
     size_t pinned_cap = 0;
@@ -88,6 +100,9 @@ struct lshkm_ctx_s {
     ~lshkm_ctx_s() {
         for (hipEvent_t& e : tev)
             if (e) (void)hipEventDestroy(e);
+        if (side_stream) (void)hipStreamSynchronize(side_stream), (void)hipStreamDestroy(side_stream);
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (join_ev) (void)hipEventDestroy(join_ev);
         if (pinned_ev) (void)hipEventSynchronize(pinned_ev), (void)hipEventDestroy(pinned_ev);
         if (pinned) (void)hipHostFree(pinned);
     }

@@ -180,6 +180,10 @@ int launch_rc_top_n(hipStream_t s, const double* X, const double* x_mean, int d,
 
 // Fused hash + assign on split-f16 MFMA (fused.hip), d = 128.
 struct FusedLaunch {
+    // optional side stream (+ fork / join events): the hash fix-up runs there
+    // beside the LIST refinement; joined before launch_fused returns
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     const float* X = nullptr;
     int64_t N = 0;
     const _Float16* Ch = nullptr;
