@@ -564,6 +564,10 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
 #define XP_SPLITS 4
 #endif
 constexpr int XP_R = XP_ROWS;
+#ifndef XP_WIDE_ROWS
+#define XP_WIDE_ROWS 2      // rows per wave at 256 < K <= 1024 (16 chunks of 64 centroids)
+#endif
+constexpr int XP_WR = XP_WIDE_ROWS;
 constexpr int XP_WAVES = 4;
 constexpr int XP_SPLIT = XP_SPLITS;
 
@@ -850,7 +854,7 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
                        cconst, metric);
     // K <= 256: 8 rows per wave over 4 chunks; K <= 1024: 2 rows per wave over 16
     const bool wide = Kpad > 256;
-    const int R = wide ? 2 : XP_R;
+    const int R = wide ? XP_WR : XP_R;
     const int64_t groups = (max_rows + R - 1) / R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
 #define XP_LAUNCH(TX, NCH, RR, MT, XP)                                                                              \
@@ -858,14 +862,14 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
                        d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows)
     if (metric == 1) {
         if (X.f64) {
-            if (wide) XP_LAUNCH(double, 16, 2, 1, X.d()); else XP_LAUNCH(double, 4, XP_R, 1, X.d());
+            if (wide) XP_LAUNCH(double, 16, XP_WR, 1, X.d()); else XP_LAUNCH(double, 4, XP_R, 1, X.d());
         } else {
-            if (wide) XP_LAUNCH(float, 16, 2, 1, X.f()); else XP_LAUNCH(float, 4, XP_R, 1, X.f());
+            if (wide) XP_LAUNCH(float, 16, XP_WR, 1, X.f()); else XP_LAUNCH(float, 4, XP_R, 1, X.f());
         }
     } else if (X.f64) {
-        if (wide) XP_LAUNCH(double, 16, 2, 0, X.d()); else XP_LAUNCH(double, 4, XP_R, 0, X.d());
+        if (wide) XP_LAUNCH(double, 16, XP_WR, 0, X.d()); else XP_LAUNCH(double, 4, XP_R, 0, X.d());
     } else {
-        if (wide) XP_LAUNCH(float, 16, 2, 0, X.f()); else XP_LAUNCH(float, 4, XP_R, 0, X.f());
+        if (wide) XP_LAUNCH(float, 16, XP_WR, 0, X.f()); else XP_LAUNCH(float, 4, XP_R, 0, X.f());
     }
 #undef XP_LAUNCH
     return kstatus("assign_pruned_kernel");
