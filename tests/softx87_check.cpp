@@ -1,5 +1,7 @@
 // Host check of crypto-recommendation_amd/csrc/softx87.h against the real x87
-// long double: random + adversarial sums, divisions, floors and roundings.
+// long double: random + adversarial sums, divisions, floors and roundings, and
+// the double-double x87 accumulator (X87dd / X87acc) over random, cancelling,
+// quantized (ties, powers of two) and wide-range terms.
 // Built and run by tests/test_softx87.py (CPU). Exit code 0 = all equal.
 #include <cmath>
 #include <cstdint>
