@@ -435,6 +435,9 @@ constexpr int FP_WAVES = FP_WAVES_SET ? FP_WAVES_SET : FP_KEEP_X ? 8 : 12;   // 
 #ifndef MFMA_PRIO
 #define MFMA_PRIO 1     // s_setprio inside the centroid loop (measured +1-3%)
 #endif
+#ifndef CHAIN_PRIO
+#define CHAIN_PRIO 2    // s_setprio around the hi-only kernel's winner chain (measured -0.02 ms; 0 = off)
+#endif
 #ifndef YOUNG_PRIO
 #define YOUNG_PRIO 0    // s_setprio for waves FP_WAVES/2.. for the whole loop (experiment knob)
 #endif
@@ -1491,6 +1494,9 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         {
             // winner distance in reference order from the row kept in registers:
             // the lane halves take turns on the chain, 8 dims each
+#if CHAIN_PRIO
+            __builtin_amdgcn_s_setprio(CHAIN_PRIO);
+#endif
             double acc = 0.0;
 #pragma unroll
             for (int s = 0; s < 8; s++) {
@@ -1526,6 +1532,9 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                 a.assign[row] = I1;
                 a.dist[row] = sqrt(acc);
             }
+#if CHAIN_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
         }
 #endif
         }
