@@ -336,3 +336,14 @@ def test_lsh_two_phase_reuse_guards(ctx):
     lshkm._ck(lib.lshkm_lsh_query(lsh.h, p(Q1), Q1.shape[0], None, 1, p(ptr2), p(out2), out2.shape[0], C.byref(tot)))
     ctx.sync()
     assert np.array_equal(ptr2.cpu().numpy(), want1[0]) and np.array_equal(out2.cpu().numpy()[:tot.value], want1[1])
+    # sizing into one offsets buffer, filling with a fresh one (poisoned): the
+    # fill must not trust the reuse state and must write the fresh out_ptr itself
+    ptr3 = ctx.empty((Q1.shape[0] + 1,), ctx.torch.int64)
+    lshkm._ck(lib.lshkm_lsh_query(lsh.h, p(Q1), Q1.shape[0], None, 1, p(ptr3), None, 0, C.byref(tot)))
+    ptr4 = ctx.empty((Q1.shape[0] + 1,), ctx.torch.int64)
+    ptr4.fill_(-(1 << 40))
+    out4 = ctx.empty((max(len(want1[1]), 1),), ctx.torch.int32)
+    lshkm._ck(lib.lshkm_lsh_query(lsh.h, p(Q1), Q1.shape[0], None, 1, p(ptr4), p(out4), out4.shape[0], C.byref(tot)))
+    ctx.sync()
+    assert tot.value == len(want1[1])
+    assert np.array_equal(ptr4.cpu().numpy(), want1[0]) and np.array_equal(out4.cpu().numpy()[:tot.value], want1[1])

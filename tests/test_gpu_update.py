@@ -36,7 +36,7 @@ def both(ctx, X, a, C, monkeypatch):
     return Cn, cnt
 
 
-@pytest.mark.parametrize("kind", ["synth", "fp32_full", "wide", "special", "skewed"])
+@pytest.mark.parametrize("kind", ["synth", "fp32_full", "wide", "special", "skewed", "tiny_coarse", "coarse_huge"])
 def test_parallel_sums_match_chains(ctx, kind, monkeypatch):
     rng = np.random.default_rng(11)
     N, d, K = 300_000, 72, 40
@@ -53,17 +53,29 @@ def test_parallel_sums_match_chains(ctx, kind, monkeypatch):
         Xh[::101, 7] = 1e-42                                               # denormal
         Xh[::103, 9] = -0.0
         Xh[::107, 11] = 3.0e30
+    elif kind == "tiny_coarse":
+        # columns of few-bit values far below 1 (2^-60 * {1, 3}, 2^-100): the
+        # fixed-point scaling must not shift by a negative amount
+        Xh = rng.standard_normal((N, d)).astype(np.float32)
+        Xh[:, 4] = np.ldexp(rng.choice([1.0, 3.0], N), -60).astype(np.float32)
+        Xh[:, 6] = np.float32(np.ldexp(1.0, -100))
+    elif kind == "coarse_huge":
+        # one cluster of 3/4 of the rows whose column holds 2^22: the scaled
+        # sum must not wrap in the accumulator
+        Xh = rng.standard_normal((N, d)).astype(np.float32)
+        Xh[:, 8] = np.float32(2.0 ** 22)
+        Xh[:, 10] = np.float32(2.0 ** 100)
     else:
         Xh = rng.standard_normal((N, d)).astype(np.float32)
     a = rng.integers(0, K, N).astype(np.int32)
-    if kind == "skewed":
+    if kind in ("skewed", "coarse_huge"):
         a[: N * 3 // 4] = 3                                                 # one huge cluster
         a[a == 5] = 6                                                       # an empty one
     X, A = to_dev(ctx, Xh), to_dev(ctx, a)
     C = to_dev(ctx, rng.standard_normal((K, d)))
     Cn, cnt = both(ctx, X, A, C, monkeypatch)
     sub = np.arange(N) < 60_000                                             # oracle on a prefix (its own chains)
-    if kind in ("synth", "fp32_full"):
+    if kind in ("synth", "fp32_full", "tiny_coarse", "coarse_huge"):
         Co, co, _ = oracle.kmeans_update(Xh, a, C.cpu().numpy(), "euclidean", 0.0)
         assert np.array_equal(bits(Cn), Co.view(np.uint64))
 
