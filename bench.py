@@ -6,13 +6,19 @@
   IDs) + Lloyd assignment over K=256 centroids (cluster ID + exact-order fp64
   distance). Multi-GPU: contiguous row shards, one process per GPU, no
   data-path collective (hash and assign are per point) -> weak scaling.
+  The same line carries a "c5" object (unless --no-c5): configs[4]'s full
+  iteration on the same resident shard, below.
 --workload c5 (configs[4]: 80M x 128, K=1024 over 8 GPUs = 10M per GPU): one
   step = one full iteration, sharding.ShardedLloyd: lshkm_hash_assign (K=1024)
   + lshkm_kmeans_partial + all-reduce of the K x d sums and K counts over RCCL
   + lshkm_kmeans_finalize (centers replaced as k_means does).
 Points are synthetic (include/lshkm_synth.h), generated in HBM before timing.
 
-python bench.py --gpus N --steps K --warmup W [--workload c5]   (torch.distributed.run for N>1)
+python bench.py --gpus N --steps K --warmup W [--workload c5]
+  N > 1: started under torch.distributed.run (the driver does this), or, when
+  no WORLD_SIZE is set, this script launches torch.distributed.run itself, as a
+  child process, before anything touches the GPU. --dry-run: the same launch
+  with the gloo backend and no GPU work (CPU test of the multi-rank plumbing).
 """
 import argparse
 import ctypes as C
@@ -20,6 +26,7 @@ import importlib.util
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -31,6 +38,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 D, L_TABLES, K_FUNCS, W, BUCKET_DIV, SEED_DATA, SEED_PARAMS = 128, 5, 4, 0.4, 100, 0x5EED, 12345
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 F16_MFMA_PEAK_TFS = 2500.0     # MI355X_MICROARCH.md: FP16/BF16 MFMA dense peak
+METRIC = "point hash+assign ops/sec at d=128, N=10M, K=256; 1/2/4/8 MI355X"
+# algorithmic bytes per point of the fused pass: 512 B read, 80 B
+# tuples + 20 B bucket IDs + 4 B cluster ID + 8 B distance written
+BYTES_PER_PT = 4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES + 4 + 8
 
 
 def load_module(name, fname):
@@ -96,6 +107,129 @@ def cpu_baseline(sample_hash, sample_assign, K):
     }
 
 
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a torch.distributed environment: run N ranks of this
+    script under torch.distributed.run as a child process (nothing here has
+    touched the GPU) and return its exit code."""
+    # the ranks' arguments travel in the environment: torch.distributed.run's own
+    # parser would take some of ours (--n) for abbreviations of its options
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", LSHKM_BENCH_ARGV=json.dumps(sys.argv[1:]))
+    return subprocess.call(cmd, env=env)
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed(step, steps, warmup, world, dev):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize;
+    returns the max over ranks of the elapsed seconds."""
+    def barrier():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+    for _ in range(warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier()
+    return max_over_ranks(time.perf_counter() - t0, world, dev)
+
+
+def dry_run(args, world, rank):
+    """gloo, CPU only: the rank layout, the C5 exchange (sharding.allreduce_partials
+    on K x d fp64 sums + K counts) and the max-over-ranks timing."""
+    import torch.distributed as dist
+    if "MASTER_ADDR" not in os.environ:             # a single rank started directly
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+    dev = torch.device("cpu")
+    K = args.k or 1024
+    row0, n = sharding.shard_range(args.n * world, world, rank)
+    sums = torch.full((K, D), float(rank + 1), dtype=torch.float64)
+    counts = torch.full((K,), rank + 1, dtype=torch.int64)
+
+    def step():
+        sums.fill_(float(rank + 1))
+        counts.fill_(rank + 1)
+        sharding.allreduce_partials(sums, counts)
+    elapsed = timed(step, args.steps, args.warmup, world, dev)
+    tot = world * (world + 1) // 2
+    ok = bool(torch.all(sums == float(tot)) and torch.all(counts == tot))
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (rank, row0, n))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "metric": METRIC, "n_gpus": world, "steps": args.steps,
+                          "ms_per_step": elapsed / args.steps * 1e3, "allreduce_ok": ok,
+                          "shards": [{"rank": r, "row0": a, "n": b} for r, a, b in gathered],
+                          "backend": dist.get_backend()}), flush=True)
+    dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+def fused_kernel_ms(lk, lib, ctx, step, reps):
+    """Mean time of the fused pass (the HIP events the library records around the
+    fused-family launches, on the stream they run on) over reps steps."""
+    lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 1))
+    ms = C.c_float()
+    tot = 0.0
+    for _ in range(reps):
+        step()
+        lk._ck(lib.lshkm_last_kernel_ms(ctx.h, C.byref(ms)))
+        tot += ms.value
+    lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 0))
+    return tot / reps
+
+
+def traffic_for(path, N, K, workload):
+    if os.path.exists(path):
+        with open(path) as f:
+            tj = json.load(f)
+        if tj.get("N") == N and tj.get("K") == K and tj.get("workload", "c3") == workload:
+            return tj.get("hbm_bytes_per_launch")
+    return None
+
+
+def roofline(N, K, kernel_ms, traffic, what):
+    kpad = (K + 63) // 64 * 64
+    # hi-only form: the hash tile's 3 split-f16 products (32 padded rows) + one
+    # f16 product per centroid (padded tiles); the few rows the hi-only bound
+    # leaves to the 3-product refinement are not counted
+    mfma_flop_per_pt = 2 * D * (3 * 32 + kpad)
+    flop_per_pt = 2 * D * (L_TABLES * K_FUNCS + K)
+    t = kernel_ms / 1e3
+    gbs = BYTES_PER_PT * N / t / 1e9
+    tfs = mfma_flop_per_pt * N / t / 1e12
+    return {"bound": "hbm", "kernel": what, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_point": BYTES_PER_PT, "kernel_ms": kernel_ms,
+            "mfma": {"achieved_TFs": tfs, "peak_TFs": F16_MFMA_PEAK_TFS, "frac": tfs / F16_MFMA_PEAK_TFS,
+                     "flop_per_point_executed": mfma_flop_per_pt, "flop_per_point_algorithmic": flop_per_pt}}
+
+
+FUSED_WHAT = ("fused pass = fused_hi_kernel (hash + hi-only f16 centroid scores, one read of X per 512-centroid "
+              "pass) + hash_fixup_kernel + the 3-product refinement of the rows the hi-only bound leaves")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +238,8 @@ def main():
     ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU")
     ap.add_argument("--workload", choices=["c3", "c5"], default="c3")
     ap.add_argument("--k", type=int, default=None, help="centroids (default 256 for c3, 1024 for c5)")
+    ap.add_argument("--no-c5", action="store_true", help="c3: leave out the C5 iteration object")
+    ap.add_argument("--dry-run", action="store_true", help="gloo on CPU, no GPU work (tests the rank plumbing)")
     ap.add_argument("--cpu-port-hash-sample", type=int, default=400_000)
     ap.add_argument("--cpu-port-assign-sample", type=int, default=300_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -111,15 +247,25 @@ def main():
     ap.add_argument("--cpu-assign-sample", type=int, default=12_000)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC passes (see profiles/)")
-    args = ap.parse_args()
+    ap.add_argument("--traffic-json-c5", default=os.path.join(ROOT, "profiles", "traffic_c5.json"))
+    argv = json.loads(os.environ["LSHKM_BENCH_ARGV"]) if len(sys.argv) == 1 and "LSHKM_BENCH_ARGV" in os.environ \
+        else sys.argv[1:]
+    args = ap.parse_args(argv)
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -127,7 +273,6 @@ def main():
     ctx = lk.Context(local)
     lib = lk.lib()
     N = args.n
-    K = args.k or (1024 if args.workload == "c5" else 256)
     N_total = N * world
     nb = N_total // BUCKET_DIV
 
@@ -135,132 +280,107 @@ def main():
     X = ctx.synth(SEED_DATA, N, D, row0=rank * N)
     V, t, r, _ = lk.params_lsh_euclidean(SEED_PARAMS, L_TABLES, K_FUNCS, D, W)
     lsh = lk.LSH(ctx, "euclidean", D, K_FUNCS, L_TABLES, nb, W, V=V, t=t, r=r)
-    rows = sharding.centroid_rows(N_total, K)                      # reference init: rows i*floor(N/K)
-    Cc = torch.empty((K, D), dtype=torch.float64, device=dev)
-    for i, row in enumerate(rows):                                 # centroids may live on other shards
-        Cc[i] = ctx.synth(SEED_DATA, 1, D, row0=int(row))[0].double()
-    src = sharding.local_src_rows(rows, rank * N, N)               # centroid override, shard-local
-    tuples = torch.empty((N, L_TABLES, K_FUNCS), dtype=torch.int32, device=dev)
-    bucket = torch.empty((N, L_TABLES), dtype=torch.int32, device=dev)
-    assign = torch.empty((N,), dtype=torch.int32, device=dev)
-    dist_ = torch.empty((N,), dtype=torch.float64, device=dev)
     p = lambda t_: C.c_void_p(t_.data_ptr())
-    src_p = src.ctypes.data_as(C.c_void_p)
 
-    if args.workload == "c5":
-        # one full iteration: hash + assign, per-shard sums, RCCL all-reduce, finalize
-        del tuples, bucket, assign, dist_
-        it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="fast")
+    def initial_centroids(K):
+        rows = sharding.centroid_rows(N_total, K)                  # reference init: rows i*floor(N/K)
+        Cc = torch.empty((K, D), dtype=torch.float64, device=dev)
+        for i, row in enumerate(rows):                             # centroids may live on other shards
+            Cc[i] = ctx.synth(SEED_DATA, 1, D, row0=int(row))[0].double()
+        return Cc, sharding.local_src_rows(rows, rank * N, N)      # centroid override, shard-local
 
-        def step():
-            it.step()
-    else:
+    def c3_run(K):
+        Cc, src = initial_centroids(K)
+        tuples = torch.empty((N, L_TABLES, K_FUNCS), dtype=torch.int32, device=dev)
+        bucket = torch.empty((N, L_TABLES), dtype=torch.int32, device=dev)
+        assign = torch.empty((N,), dtype=torch.int32, device=dev)
+        dist_ = torch.empty((N,), dtype=torch.float64, device=dev)
+        src_p = src.ctypes.data_as(C.c_void_p)
+
         def step():
             # one pass: tuples + bucket IDs + cluster IDs + fp64 distances (lshkm_hash_assign)
             lk._ck(lib.lshkm_hash_assign(lsh.h, p(X), N, p(Cc), K, src_p, p(tuples), None, p(bucket), p(assign),
                                          p(dist_)))
+        ctx.reset_stats()
+        elapsed = timed(step, args.steps, args.warmup, world, dev)
+        ex = {"per_step": True, "assign_ambiguous_rows": ctx.stat(lk.STAT_ASSIGN_AMBIG) // (args.steps + args.warmup),
+              "hash_fixup_rows": ctx.stat(lk.STAT_HASH_FIX) // (args.steps + args.warmup),
+              "hash_exact_fallbacks": ctx.stat(lk.STAT_HASH_EXACT) // (args.steps + args.warmup)}
+        kms = fused_kernel_ms(lk, lib, ctx, step, max(3, args.steps))
+        return elapsed, kms, ex
 
-    def barrier():
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize(dev)
+    def c5_run(K):
+        # one full iteration: hash + assign, per-shard sums, RCCL all-reduce, finalize
+        Cc, src = initial_centroids(K)
+        it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="fast")
+        elapsed = timed(it.step, args.steps, args.warmup, world, dev)
+        it.timing = True
+        kms = fused_kernel_ms(lk, lib, ctx, it.step, max(3, args.steps))
+        it.timing = False
+        xms = it.exchange_ms() if world > 1 else 0.0
+        return elapsed, kms, xms
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    ctx.reset_stats()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(e.item())
-    ambig = ctx.stat(lk.STAT_ASSIGN_AMBIG) // args.steps
-    hexact = ctx.stat(lk.STAT_HASH_EXACT) // args.steps
-    hfix = ctx.stat(lk.STAT_HASH_FIX) // args.steps
+    def c5_object(K, elapsed, kms, xms):
+        return {
+            "metric": f"C5 LSH-assign + k-means iterations: points/s (hash + assign K={K} + sums + RCCL all-reduce "
+                      f"+ finalize)",
+            "value": N_total * args.steps / elapsed, "unit": "point iteration ops/s",
+            "ms_per_step": elapsed / args.steps * 1e3, "n_gpus": world, "scaling": "weak",
+            "config": {"workload": f"C5 (BASELINE configs[4]): N={N} per GPU x {world} GPU(s), d=128, K={K}, "
+                                   f"L=5, k=4, w=0.4, RCCL all-reduce of the {K}x128 fp64 sums + {K} counts",
+                       "N_per_gpu": N, "N_total": N_total, "K": K, "parallelism": f"dp{world} (row shards)"},
+            "allreduce_ms": xms,
+            "roofline": roofline(N, K, kms, traffic_for(args.traffic_json_c5, N, K, "c5"),
+                                 FUSED_WHAT + " (K = 1024: two 512-centroid passes)"),
+        }
 
-    # Dominant kernel = the fused pass (fused_persistent_kernel<true> and its
-    # hash_fixup_kernel; at K > 256 one launch per 256-centroid slice): HIP
-    # events recorded by the library around those launches, on the stream they
-    # run on; averaged over reps steps.
-    reps = max(3, args.steps)
-    lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 1))
-    ms = C.c_float()
-    t_kernel = 0.0
-    for _ in range(reps):
-        step()
-        lk._ck(lib.lshkm_last_kernel_ms(ctx.h, C.byref(ms)))
-        t_kernel += ms.value / 1e3
-    lk._ck(lib.lshkm_ctx_enable_timing(ctx.h, 0))
-    t_kernel /= reps
-
-    # Algorithmic bytes and flops per point: 512 B read, 80 B tuples +
-    # 20 B bucket IDs + 4 B cluster ID + 8 B distance written = 624 B; 2*d*(L*k + K) flop.
-    bytes_per_pt = 4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES + 4 + 8
-    flop_per_pt = 2 * D * (L_TABLES * K_FUNCS + K)
-    kpad = (K + 63) // 64 * 64
-    # hi-only form: the hash tile's 3 split-f16 products (32 padded rows) + one
-    # f16 product per centroid (padded tiles); the ~3% of rows the hi-only bound
-    # leaves to the 3-product refinement are not counted
-    mfma_flop_per_pt = 2 * D * (3 * 32 + kpad)
-    hbm_gbs = bytes_per_pt * N / t_kernel / 1e9
-    mfma_tfs = mfma_flop_per_pt * N / t_kernel / 1e12
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if tj.get("N") == N and tj.get("K") == K and tj.get("workload", "c3") == args.workload:
-            traffic = tj.get("hbm_bytes_per_launch")
-
-    if rank == 0:
-        value = N_total * args.steps / elapsed
+    line = None
+    if args.workload == "c5":
+        K = args.k or 1024
+        el, kms, xms = c5_run(K)
+        line = c5_object(K, el, kms, xms)
+        line.update({"metric": METRIC + " (C5 workload)", "unit": "point hash+assign ops/s", "steps": args.steps,
+                     "warmup": args.warmup, "higher_is_better": True, "vs_baseline": None,
+                     "dtype": "fp32 points; split-f16 MFMA scores (f32 accumulate), fp64/x87-exact results",
+                     "data": "synthetic (include/lshkm_synth.h), resident in HBM"})
+    else:
+        K = args.k or 256
+        el, kms, ex = c3_run(K)
         line = {
-            "metric": "point hash+assign ops/sec at d=128, N=10M, K=256; 1/2/4/8 MI355X",
-            "value": value,
-            "unit": "point hash+assign ops/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
+            "metric": METRIC, "value": N_total * args.steps / el, "unit": "point hash+assign ops/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32 points; split-f16 MFMA scores (f32 accumulate), fp64/x87-exact results",
             "data": "synthetic (include/lshkm_synth.h), resident in HBM",
-            "config": {"workload": (f"C5 LSH-assign + k-means iteration (hash + assign + per-shard sums + RCCL "
-                                    f"all-reduce + finalize), K={K}, N={N} per GPU, d=128"
-                                    if args.workload == "c5" else
-                                    f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128"),
+            "config": {"workload": f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128",
                        "N_per_gpu": N, "N_total": N_total, "d": D, "K": K, "L": L_TABLES, "k": K_FUNCS,
                        "w": W, "nb": nb, "parallelism": f"dp{world} (row shards)"},
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "fused pass = fused_hi_kernel (hash + hi-only f16 centroid scores, one read of X) + "
-                          "hash_fixup_kernel + the 3-product refinement of the rows the hi-only bound leaves",
-                "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "bytes_per_point": bytes_per_pt, "kernel_ms": t_kernel * 1e3,
-                "mfma": {"achieved_TFs": mfma_tfs, "peak_TFs": F16_MFMA_PEAK_TFS, "frac": mfma_tfs / F16_MFMA_PEAK_TFS,
-                         "flop_per_point_executed": mfma_flop_per_pt, "flop_per_point_algorithmic": flop_per_pt},
-            },
-            "exactness": {"per_step": True, "assign_ambiguous_rows": ambig, "hash_fixup_rows": hfix,
-                          "hash_exact_fallbacks": hexact},
+            "roofline": roofline(N, K, kms, traffic_for(args.traffic_json, N, K, "c3"), FUSED_WHAT),
+            "exactness": ex,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample, K)
-            try:
-                line["cpu_baseline"]["all_cores"] = port_all_cores(args.cpu_port_hash_sample,
-                                                                   args.cpu_port_assign_sample * 256 // K, K)
-            except (subprocess.CalledProcessError, OSError, ValueError) as e:
-                line["cpu_baseline"]["all_cores"] = {"error": str(e)[:200]}
+        if not args.no_c5:
+            K5 = 1024
+            el5, kms5, xms5 = c5_run(K5)
+            line["c5"] = c5_object(K5, el5, kms5, xms5)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        K = line["config"]["K"]
+        line["cpu_baseline"] = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample * 256 // K, K)
+        try:
+            line["cpu_baseline"]["all_cores"] = port_all_cores(args.cpu_port_hash_sample,
+                                                               args.cpu_port_assign_sample * 256 // K, K)
+        except (subprocess.CalledProcessError, OSError, ValueError) as e:
+            line["cpu_baseline"]["all_cores"] = {"error": str(e)[:200]}
+        if "c5" in line:
+            cb = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample // 4, 1024)
+            cb["note"] = ("hash + assign only: the reference's k_means update adds ~4d flops per point, "
+                          "not timed here")
+            line["c5"]["cpu_baseline"] = cb
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

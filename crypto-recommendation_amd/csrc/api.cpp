@@ -607,8 +607,8 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
                                      assign, dist, (int32_t*)ctx->ws_ambig.p, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (metric != LSHKM_METRIC_EUCLIDEAN &&
-            (rc = launch_cos_fix(s, X, N, d, C, (const int32_t*)ctx->ws_ambig.p + N, cnt + 1, assign, dist) ||
-             launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            ((rc = launch_cos_fix(s, X, N, d, C, (const int32_t*)ctx->ws_ambig.p + N, cnt + 1, assign, dist)) ||
+             (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 1)))) { LSHKM_LAUNCH_CHECK(); return rc; }
         // ambiguous-count statistic
         if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
     } else {

@@ -2005,7 +2005,11 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             }
             if (hash && cos) hipLaunchKernelGGL(hash_fixup_kernel<true>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, hs, a);
             else if (hash) hipLaunchKernelGGL(hash_fixup_kernel<false>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, hs, a);
-            if (side && hipEventRecord(f.join, f.side) != hipSuccess) return kstatus("launch_fused (join)");
+            if (side && hipEventRecord(f.join, f.side) != hipSuccess) {
+                // never return with the fix-up unordered against later work on s
+                (void)hipStreamSynchronize(f.side);
+                return kstatus("launch_fused (join)");
+            }
             FusedArgs r = a;
             r.list_in = f.ambig; r.list_counts = f.seg_counts; r.list_seg_rows = a.seg_rows;
             r.ambig = f.list2; r.seg_counts = f.seg_counts2; r.ambig_count = f.ambig_count;
@@ -2032,7 +2036,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 f.cos_list[0] = f.cfix; f.cos_counts[0] = f.cfix_counts;
                 f.cos_list[1] = f.hfix2; f.cos_counts[1] = f.seg_counts2;
             }
-            if (side && hipStreamWaitEvent(s, f.join, 0) != hipSuccess) return kstatus("launch_fused (join)");
+            if (side && hipStreamWaitEvent(s, f.join, 0) != hipSuccess) {
+                (void)hipStreamSynchronize(f.side);
+                return kstatus("launch_fused (join)");
+            }
             return kstatus("fused_hi_kernel");
         }
         // one launch per 256-centroid slice (the hashing rides on the first)

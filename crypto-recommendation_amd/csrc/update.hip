@@ -244,6 +244,10 @@ __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_
     int lc = 0;
     while (((int64_t)1 << lc) < cnt) lc++;          // ceil(log2 count)
     if (ok && qmin <= tmax && lc + tmax - qmin > 53) ok = false;
+    // every partial sum in any order is below cnt * 2^tmax <= 2^(lc + tmax):
+    // finite only if that is <= 2^1023 (else an any-order sum may overflow where
+    // the reference's chain stays finite, e.g. [M, -M, M] with M = 1.5 * 2^1023)
+    if (ok && qmin <= tmax && lc + tmax > 1023) ok = false;
     if (ok) sums[i] = s;
     else atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));   // chain block (c, j/64) goes sequential
 }

@@ -193,13 +193,18 @@ class ShardedLloyd:
         self.C = C0.clone()
         self.src = None if src_rows is None else np.ascontiguousarray(src_rows, np.int32)
         e = ctx.empty
-        self.tuples = e((n, lsh.L, lsh.k), torch.int32) if lsh is not None else None
+        if metric not in lk._METRIC:
+            raise ValueError(f"unknown metric {metric!r}")
+        # cosine indexes have no k-tuples (CosineGGen, cosine_g_gen.hpp:58-66)
+        self.tuples = e((n, lsh.L, lsh.k), torch.int32) if lsh is not None and lsh.metric == lk.EUCLIDEAN else None
         self.bucket = e((n, lsh.L), torch.int32) if lsh is not None else None
         self.assign = e((n,), torch.int32)
         self.dist = e((n,), torch.float64)
         self.sums = e((self.K, self.d), torch.float64)
         self.counts = e((self.K,), torch.int64)
         self.cont = True
+        self.timing = False       # True: HIP events around the exchange (bench.py's breakdown)
+        self.exchange_events = []
 
     def step(self):
         import ctypes as C
@@ -207,9 +212,12 @@ class ShardedLloyd:
         p = lk._t_ptr
         src = None if self.src is None else self.src.ctypes.data_as(C.c_void_p)
         if self.lsh is not None:
-            lk._ck(lk._fn("lshkm_hash_assign", X)(self.lsh.h, p(X), X.shape[0], p(self.C), self.K, src,
-                                                  p(self.tuples), None, p(self.bucket), p(self.assign),
-                                                  p(self.dist)))
+            # the assignment metric is this iteration's (an index of either family
+            # may ride along; the cosine index + cosine Lloyd is one pass)
+            lk._ck(lk._fn("lshkm_hash_assign_metric", X)(self.lsh.h, p(X), X.shape[0], p(self.C), self.K,
+                                                         lk._METRIC[self.metric], src,
+                                                         p(self.tuples) if self.tuples is not None else None,
+                                                         None, p(self.bucket), p(self.assign), p(self.dist)))
         else:
             lk.lloyd_assign(ctx, X, self.C, self.metric, self.src, self.assign, self.dist)
         if self.mode == "exact":
@@ -218,10 +226,26 @@ class ShardedLloyd:
             sums, counts = chain_partials(local, self.sums, self.counts)
         else:
             sums, counts = lk.kmeans_partial(ctx, X, self.assign, self.K, self.sums, self.counts)
+            if self.timing:
+                ev = [ctx.torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                ev[0].record()
             allreduce_partials(sums, counts)
+            if self.timing:
+                ev[1].record()
+                self.exchange_events.append(ev)
         Cn, cont = lk.kmeans_finalize(ctx, sums, counts, self.C, self.metric, self.min_dist)
         if cont:              # k_means replaces every center (update.hpp:70-79)
             self.C = Cn
             self.src = None   # the override applies to dataset-row centroids only
         self.cont = cont
         return cont
+
+    def exchange_ms(self):
+        """Mean all-reduce time (ms) over the timed steps (torch's stream, which
+        the library context and RCCL share), then forget them."""
+        if not self.exchange_events:
+            return None
+        self.ctx.torch.cuda.synchronize(self.ctx.dev)
+        ms = sum(a.elapsed_time(b) for a, b in self.exchange_events) / len(self.exchange_events)
+        self.exchange_events = []
+        return ms

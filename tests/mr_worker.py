@@ -3,9 +3,11 @@
 Not a test module: launched as `python tests/mr_worker.py RANK WORLD PORT OUTDIR`
 (several ranks sharing the one MI355X over gloo, or one rank with WORLD = 1 for
 the single-process reference). Runs liblshkm on this rank's contiguous row
-shard (crypto-recommendation_amd/sharding.py): the C5 iteration (hash + assign
-+ k-means update) in fast (all-reduce) and exact (carry chain) mode, and the
-sharded euclidean hypercube build; saves everything to OUTDIR/rank<R>.npz."""
+shard (crypto-recommendation_amd/sharding.py): the C5 iteration at C5's K = 1024
+(hash + assign -- the hashing multi-pass fused form -- + k-means update) in fast
+(all-reduce) and exact (carry chain) mode, one cosine iteration (cosine index +
+cosine Lloyd in one pass), and the sharded euclidean hypercube build; saves
+everything to OUTDIR/rank<R>.npz."""
 import os
 import sys
 
@@ -21,7 +23,7 @@ from amd import PKG, lshkm  # noqa: E402
 sys.path.insert(0, PKG)
 import sharding as sh  # noqa: E402
 
-N_TOTAL, D, L, KF, K, STEPS = 120_000, 128, 5, 4, 300, 2
+N_TOTAL, D, L, KF, K, STEPS = 120_000, 128, 5, 4, 1024, 2
 
 
 def main():
@@ -47,6 +49,13 @@ def main():
             res[f"{mode}_cont{s}"] = np.array([it.cont])
         res[f"{mode}_tuples"] = it.tuples.cpu().numpy()
         res[f"{mode}_bucket"] = it.bucket.cpu().numpy()
+    # cosine: CosineGGen buckets + cosine Lloyd (lshkm_hash_assign_metric), fast mode
+    R, _ = lshkm.params_lsh_cosine(321, L, KF, D)
+    clsh = lshkm.LSH(ctx, "cosine", D, KF, L, R=R)
+    it = sh.ShardedLloyd(lshkm, ctx, clsh, X, C0, sh.local_src_rows(rows, row0, n), mode="fast", metric="cosine")
+    it.step()
+    res.update(cos_assign0=it.assign.cpu().numpy(), cos_dist0=it.dist.cpu().numpy(),
+               cos_bucket=it.bucket.cpu().numpy(), cos_centers1=it.C.cpu().numpy())
     Vc, tc, st = lshkm.params_cube_euclidean(777, 10, D, 2.0)
     cube = lshkm.Cube(ctx, "euclidean", D, 10, 2.0, V=Vc, t=tc, rng_state=st)
     sh.cube_build_sharded(lshkm, cube, X, row0)

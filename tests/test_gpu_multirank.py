@@ -5,8 +5,11 @@ share the one MI355X over gloo, each running liblshkm on its row shard
   - hash tuples, bucket IDs, cluster IDs and distances: bit-exact (per row);
   - k-means centers, fast mode (all-reduce of per-shard sums): <= 1e-13 rel;
   - k-means centers, exact mode (rank-to-rank carry chain): bit-exact;
+  - cosine (cosine index + cosine Lloyd in one pass, fast mode): buckets,
+    IDs, distances bit-exact, centers <= 1e-13 rel;
   - sharded euclidean hypercube: the same coins (global first-occurrence
     order) and vertices as the single-process build.
+K = 1024 with hashing: the per-shard step is C5's kernel form.
 The C5 bench line (bench.py --workload c5) runs the same ShardedLloyd step."""
 import os
 import socket
@@ -72,6 +75,13 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     assert np.array_equal(c1, two[1]["fast_centers1"])       # every rank holds the same centers
     rel = np.abs(c1 - c1_one) / np.maximum(np.abs(c1_one), 1e-300)
     assert rel.max() <= 1e-13
+    # cosine iteration: per-row outputs bit-exact, centers within the fast-mode bound
+    for key in ("cos_bucket", "cos_assign0"):
+        assert np.array_equal(cat(key), one[key]), key
+    assert np.array_equal(cat("cos_dist0").view(np.uint64), one["cos_dist0"].view(np.uint64))
+    cc, cc_one = two[0]["cos_centers1"], one["cos_centers1"]
+    assert np.array_equal(cc, two[1]["cos_centers1"])
+    assert (np.abs(cc - cc_one) / np.maximum(np.abs(cc_one), 1e-300)).max() <= 1e-13
     # hypercube: same coins, same engine state, same vertices
     for key in ("memo_f", "memo_h", "memo_bit", "memo_state"):
         for r in two:
