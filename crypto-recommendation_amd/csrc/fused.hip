@@ -1211,6 +1211,8 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     const int64_t tstride = (int64_t)gridDim.x * FH_WAVES, tfirst = (int64_t)blockIdx.x * FH_WAVES;
     const int64_t nround = NIMG == 2 && ntiles > tfirst ? (ntiles - tfirst + tstride - 1) / tstride : 0;
     int64_t rd = 0;
+    // profiling build: [0] row load + split + hash tile, [1] centroid tiles, [2] certificate + winner chain + stores
+    PT_DECL
     for (int64_t tile = tfirst + wave; NIMG == 2 ? rd < nround : tile < ntiles; tile += tstride, rd++) {
         const int64_t row = tile * 32 + col;
         const bool valid = row < a.N;
@@ -1370,6 +1372,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             }
         }
 
+        PT_MARK(0)
         // the certificate's bound E depends on the row only: formed before the
         // centroid tiles (its fp64 ops overlap the MFMAs). cosine: + 2^-43 |x| for the normalisation and the reference's own q
         // (fused_persistent_kernel's cosine bound)
@@ -1431,6 +1434,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #if MFMA_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
+        PT_MARK(1)
         // <HASH, MP> launches only the first of several passes (never the last)
         if (MP && (HASH || !a.pass_last)) {
             a.part[tile * 64 + lane] = make_float4(m1, m2, __int_as_float(t1), 0.f);
@@ -1538,7 +1542,9 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         }
 #endif
         }
+        PT_MARK(2)
     }
+    PT_FLUSH
     __syncthreads();
     if (threadIdx.x < 2 && (!MP || (threadIdx.x == 0 ? (!HASH && a.pass_last != 0) : (HASH && a.pass_first)))) {
         const int c = lcount[threadIdx.x];
@@ -1885,7 +1891,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             unsigned long long v[6];
             (void)hipMemcpyAsync(v, d, 48, hipMemcpyDeviceToHost, s);
             (void)hipStreamSynchronize(s);
-            fprintf(stderr, "PHASES load+split %llu hash %llu centroids %llu chain %llu lists %llu\n", v[0], v[1], v[2], v[3], v[4]);
+            // hi-only form: [0] load + split + hash, [1] centroid tiles, [2] certificate + chain + stores
+            // (the LIST refinement's fused_persistent_kernel adds its own phases 0-4 over its few rows)
+            fprintf(stderr, "PHASES %llu %llu %llu %llu %llu\n", v[0], v[1], v[2], v[3], v[4]);
         }
     } report{s, prof_d};
 #endif
