@@ -451,6 +451,16 @@ constexpr int FP_WAVES = FP_WAVES_SET ? FP_WAVES_SET : FP_KEEP_X ? 8 : 12;   // 
 #ifndef CHAIN_PF
 #define CHAIN_PF 1
 #endif
+#ifndef XPF
+#define XPF 0           // hi-only kernel: next tile's row loaded during the winner chain
+#endif
+// hi-only kernel's winner-row loads; ABL_CHAIN_NOLOAD (timing experiments
+// only, results invalid): values made from the row in registers instead
+#if defined(ABL_CHAIN_NOLOAD)
+#define CHAIN_LD(ptr, xi) make_double2((double)xf[(xi)] * 0.75, (double)xf[(xi) + 1] * 0.75)
+#else
+#define CHAIN_LD(ptr, xi) (*reinterpret_cast<const double2*>(ptr))
+#endif
 
 // Scores of one 32-centroid tile: t = (hi + lo) + (-|c|^2/2) on packed f32
 // (D rows of registers 4g..4g+3 are centroids 8g+4h..+3 of the tile).
@@ -899,6 +909,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             // dims 16s+8h..+7; only the winner's fp64 row is loaded
             const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
             double acc = 0.0;
+#if defined(ABL_CHAIN_TREE)
+            double tacc[4] = {0.0, 0.0, 0.0, 0.0};
+#endif
             double2 cbuf[CHAIN_PF][4];
 #pragma unroll
             for (int s = 0; s < CHAIN_PF; s++)
@@ -923,6 +936,10 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                     sq[2 * j] = __dmul_rn(d0, d0);
                     sq[2 * j + 1] = __dmul_rn(d1, d1);
                 }
+#if defined(ABL_CHAIN_TREE)   // timing experiments only: per-lane sums in any order (results invalid)
+#pragma unroll
+                for (int j = 0; j < 8; j++) tacc[j & 3] = __dadd_rn(tacc[j & 3], sq[j]);
+#else
                 if (h == 0) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
@@ -933,7 +950,12 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
                 acc = take_from_upper(acc);
+#endif
             }
+#if defined(ABL_CHAIN_TREE)
+            acc = __dadd_rn(__dadd_rn(tacc[0], tacc[1]), __dadd_rn(tacc[2], tacc[3]));
+            acc = __dadd_rn(acc, swap_halves(acc, h));
+#endif
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
                 a.dist[row] = sqrt(acc);
@@ -1212,25 +1234,41 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     const int64_t nround = NIMG == 2 && ntiles > tfirst ? (ntiles - tfirst + tstride - 1) / tstride : 0;
     int64_t rd = 0;
     // profiling build: [0] row load + split + hash tile, [1] centroid tiles, [2] certificate + winner chain + stores
-    PT_DECL
+    // this lane's 64 values of row (tile, col) in the B-operand layout (rows past
+    // the end read row N-1: their results are never stored)
+    auto load_row = [&](int64_t tl, float (&dst)[64]) {
+#if defined(ABL_XLD_COAL)   // timing experiments only: lane quads read 64 contiguous bytes (wrong layout)
+        const int64_t rr = tl * 32 + (lane >> 2);
+        const float* xr = a.X + (rr < a.N ? rr : a.N - 1) * FU_D + 4 * (lane & 3);
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * (s & 3) + 64 * (s >> 2));
+            const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * (s & 3) + 64 * (s >> 2) + 2048);
+#else
+        const int64_t rr = tl * 32 + col;
+#if defined(ABL_L2X)   // timing experiments only: every tile reads the same 4096 rows (L2 hits)
+        const float* xr = a.X + ((rr < a.N ? rr : a.N - 1) & 4095) * FU_D + 8 * h;
+#else
+        const float* xr = a.X + (rr < a.N ? rr : a.N - 1) * FU_D + 8 * h;
+#endif
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
+            const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
+#endif
+            dst[8 * s + 0] = p0.x; dst[8 * s + 1] = p0.y; dst[8 * s + 2] = p0.z; dst[8 * s + 3] = p0.w;
+            dst[8 * s + 4] = p1.x; dst[8 * s + 5] = p1.y; dst[8 * s + 6] = p1.z; dst[8 * s + 7] = p1.w;
+        }
+    };
+    // XPF: the next tile's row is loaded while this tile's winner chain waits on
+    // its fp64 centroid rows (the HBM latency hides behind the L2 round trips)
+    constexpr bool xpf = XPF && NIMG == 1;
+    float xf[64];
+    if (xpf && tfirst + wave < ntiles) load_row(tfirst + wave, xf);
     for (int64_t tile = tfirst + wave; NIMG == 2 ? rd < nround : tile < ntiles; tile += tstride, rd++) {
         const int64_t row = tile * 32 + col;
         const bool valid = row < a.N;
-        float xf[64];
-        {
-#if defined(ABL_L2X)   // timing experiments only: every tile reads the same 4096 rows (L2 hits)
-            const float* xr = a.X + ((valid ? row : a.N - 1) & 4095) * FU_D + 8 * h;
-#else
-            const float* xr = a.X + (valid ? row : a.N - 1) * FU_D + 8 * h;
-#endif
-#pragma unroll
-            for (int s = 0; s < 8; s++) {
-                const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
-                const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
-                xf[8 * s + 0] = p0.x; xf[8 * s + 1] = p0.y; xf[8 * s + 2] = p0.z; xf[8 * s + 3] = p0.w;
-                xf[8 * s + 4] = p1.x; xf[8 * s + 5] = p1.y; xf[8 * s + 6] = p1.z; xf[8 * s + 7] = p1.w;
-            }
-        }
+        if (!xpf) load_row(tile, xf);
         half8 bh[8];
         float2v n2a = {0.f, 0.f}, n2b = {0.f, 0.f}, r2 = {0.f, 0.f};
         // hi part of 8 values (LO: and the lo part), |x|^2 and |x - xh|^2 partial sums
@@ -1435,9 +1473,15 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         __builtin_amdgcn_s_setprio(0);
 #endif
         PT_MARK(1)
+        float xn[64];
+        if (xpf && tile + tstride < ntiles) load_row(tile + tstride, xn);
         // <HASH, MP> launches only the first of several passes (never the last)
         if (MP && (HASH || !a.pass_last)) {
             a.part[tile * 64 + lane] = make_float4(m1, m2, __int_as_float(t1), 0.f);
+            if (xpf) {
+#pragma unroll
+                for (int j = 0; j < 64; j++) xf[j] = xn[j];
+            }
             continue;
         }
         const uint32_t l1 = __float_as_uint(m1) & 0xFu;
@@ -1450,13 +1494,17 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #if !defined(ABL_NOCHAIN)
         // the winner's fp64 row: the first loads go out before the certificate
         // and the list append
+#if defined(ABL_CLD_COAL)   // timing experiments only: each lane quad reads 64 contiguous bytes of one row
+        const double* crow = a.C64 + (size_t)__shfl(I1, lane & ~3) * FU_D + 2 * (lane & 3);
+#else
         const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
+#endif
         double2 cbuf[CHAIN_PF][4];
         if (MET == 0) {
 #pragma unroll
             for (int s = 0; s < CHAIN_PF; s++)
 #pragma unroll
-                for (int j = 0; j < 4; j++) cbuf[s][j] = *reinterpret_cast<const double2*>(crow + 16 * s + 2 * j);
+                for (int j = 0; j < 4; j++) cbuf[s][j] = CHAIN_LD(crow + 16 * s + 2 * j, 8 * s + 2 * j);
         }
 #endif
         const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
@@ -1502,6 +1550,9 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             __builtin_amdgcn_s_setprio(CHAIN_PRIO);
 #endif
             double acc = 0.0;
+#if defined(ABL_CHAIN_TREE)
+            double tacc[4] = {0.0, 0.0, 0.0, 0.0};
+#endif
 #pragma unroll
             for (int s = 0; s < 8; s++) {
                 double sq[8];
@@ -1511,7 +1562,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                 if (s + CHAIN_PF < 8) {
 #pragma unroll
                     for (int j = 0; j < 4; j++)
-                        cbuf[s % CHAIN_PF][j] = *reinterpret_cast<const double2*>(crow + 16 * (s + CHAIN_PF) + 2 * j);
+                        cbuf[s % CHAIN_PF][j] = CHAIN_LD(crow + 16 * (s + CHAIN_PF) + 2 * j, 8 * (s + CHAIN_PF) + 2 * j);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -1521,6 +1572,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                     sq[2 * j] = __dmul_rn(d0, d0);
                     sq[2 * j + 1] = __dmul_rn(d1, d1);
                 }
+#if defined(ABL_CHAIN_TREE)   // timing experiments only: per-lane sums in any order (results invalid)
+#pragma unroll
+                for (int j = 0; j < 8; j++) tacc[j & 3] = __dadd_rn(tacc[j & 3], sq[j]);
+#else
                 if (h == 0) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
@@ -1531,7 +1586,12 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
                 acc = take_from_upper(acc);
+#endif
             }
+#if defined(ABL_CHAIN_TREE)
+            acc = __dadd_rn(__dadd_rn(tacc[0], tacc[1]), __dadd_rn(tacc[2], tacc[3]));
+            acc = __dadd_rn(acc, swap_halves(acc, h));
+#endif
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
                 a.dist[row] = sqrt(acc);
@@ -1543,6 +1603,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #endif
         }
         PT_MARK(2)
+        if (xpf) {
+#pragma unroll
+            for (int j = 0; j < 64; j++) xf[j] = xn[j];
+        }
     }
     PT_FLUSH
     __syncthreads();

@@ -4,7 +4,7 @@ reps, inputs resident in HBM), next to the CPU restatement (oracle/, one
 thread, OMP_NUM_THREADS=1, kind "port") on a bounded sample of the same
 workload, scaled to the row's unit. Prints one JSON line per row.
 
-    python tools/bench_rows.py [--rows cosine,kpp,range,sil,update,lsh,cube,recom,csv] [--no-cpu]
+    python tools/bench_rows.py [--rows cosine,kpp,range,sil,update,lsh,cube,recom,csv,f64] [--no-cpu]
 """
 import argparse
 import json
@@ -66,7 +66,7 @@ def emit(row, unit, units, t_gpu, cpu=None, note="", bytes_per_unit=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rows", default="cosine,kpp,range,sil,update,lsh,cube,recom,csv")
+    ap.add_argument("--rows", default="cosine,kpp,range,sil,update,lsh,cube,recom,csv,f64")
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
     rows = set(a.rows.split(","))
@@ -251,6 +251,57 @@ def main():
             cph, cih = cp[:q2 + 1].cpu().numpy(), ci[:int(cp[q2])].cpu().numpy()
             c = (q2, cpu_time(lambda: oracle.p_closest(Xh, Uh[:q2], cph, cih, P)), f"{q2} users x 200 candidates")
         emit("get_P_closest", "users/s", Q, t, c, f"N={N}, d={d}, {Q} users x 200 candidates, P={P}")
+
+    if "f64" in rows:        # the reference's own shapes: fp64 user vectors, d = number of coins
+        # (main.cpp:149-222 cosine LSH recommend, :240-281 clustering recommend; crypto_rec.hpp:78-140)
+        N, d, K, P, NT = 1_000_000, 100, 256, 20, 5
+        rng = np.random.default_rng(11)
+        Xh = rng.standard_normal((N, d))                  # general doubles: the _f64 entry points
+        X = torch.from_numpy(Xh).to(ctx.dev)
+        R, _ = lshkm.params_lsh_cosine(12345, 5, 4, d)
+        lsh = lshkm.LSH(ctx, "cosine", d, 4, 5, R=R)
+        tb = gpu_time(ctx, lambda: lsh.build(X))
+        emit("create_LSH_hashtables (cosine, fp64 rows)", "rows/s", N, tb, None,
+             f"N={N}, d={d} fp64 user vectors, L=5, k=4 (main.cpp:155); bytes: the fp64 row + per table its "
+             f"bucket key and CSR slot", bytes_per_unit=8 * d + 5 * 8)
+        nq = 256                                          # each cosine query unions ~5 x N/16 rows
+        qrows = torch.arange(nq, device=ctx.dev) * (N // nq)
+        Q = X[qrows]
+        alias = qrows.to(torch.int32)
+        tq = gpu_time(ctx, lambda: lsh.query(Q, True, alias, device=True), reps=3)
+        cptr, cidx = lsh.query(Q, True, alias, device=True)
+        tot = int(cptr[-1])
+        emit("get_LSH_filtered_combined_buckets (cosine, fp64 rows)", "queries/s", nq, tq, None,
+             f"{nq} dataset-row queries over N={N}; {tot} candidate rows ({tot / nq:.0f} per query); bytes: 4 B "
+             f"read + 4 B written per candidate", bytes_per_unit=8.0 * tot / nq)
+        tp = gpu_time(ctx, lambda: lshkm.p_closest(ctx, X, Q, cptr, cidx, P), reps=3)
+        emit("get_P_closest (fp64 rows)", "candidates/s", tot, tp, None,
+             f"{nq} users x {tot / nq:.0f} candidates, d={d}, P={P}; bytes: the candidate's fp64 row",
+             bytes_per_unit=8 * d + 4)
+        idx, sim, cnt = lshkm.p_closest(ctx, X, Q, cptr, cidx, P)
+        xm = X.mean(dim=1).contiguous()
+        um = xm[qrows].contiguous()
+        unk = [np.sort(rng.choice(d, 20, replace=False)).astype(np.int32) for _ in range(nq)]
+        up = torch.from_numpy(np.arange(nq + 1, dtype=np.int64) * 20).to(ctx.dev)
+        ui = torch.from_numpy(np.concatenate(unk)).to(ctx.dev)
+        tn = gpu_time(ctx, lambda: lshkm.top_n_recom(ctx, X, xm, um, up, ui, idx, sim, cnt, NT), reps=3)
+        emit("get_top_N_recom (fp64 rows)", "users/s", nq, tn, None, f"{nq} users, P={P}, 20 unknown coins each, N={NT}")
+        del lsh
+        # clustering recommendation's Lloyd + k_means on the same fp64 rows (main.cpp:248-258)
+        src = (np.arange(K) * (N // K)).astype(np.int64)
+        C = X[torch.from_numpy(src).to(ctx.dev)].clone()
+        for metric in ("euclidean", "cosine"):
+            ctx.reset_stats()
+            t = gpu_time(ctx, lambda: lshkm.lloyd_assign(ctx, X, C, metric))
+            amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG) / 6
+            emit(f"lloyds_assignment ({metric}, fp64 rows)", "rows/s", N, t, None,
+                 f"N={N}, d={d} fp64, K={K}; {amb:.0f} rows/call to the exact pass; bytes: the fp64 row + id and "
+                 f"distance", bytes_per_unit=8 * d + 12)
+        asg, _ = lshkm.lloyd_assign(ctx, X, C, "euclidean")
+        t = gpu_time(ctx, lambda: lshkm.kmeans_update(ctx, X, asg, C, "euclidean", 0.05))
+        emit("k_means update (fp64 rows)", "rows/s", N, t, None, f"N={N}, d={d} fp64, K={K}; bytes: the fp64 row + id",
+             bytes_per_unit=8 * d + 4)
+        del X
 
     if "csv" in rows:        # VectorReader (vector_reader.hpp:54-85)
         n, d = 200_000, 64
