@@ -1165,11 +1165,33 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
 // it with the row still in registers -- no second read of X and no carried
 // pass state. Images alternate A,B / B,A between rounds (one swap per round);
 // every wave runs the block's round count (tiles past the end: no valid rows).
-template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1>
+// GATH (euclidean, one pass, Kpad <= FH_GATH_KMAX): the winner rows of the
+// distance chain are gathered into a per-wave LDS ring by LDS-DMA, 8 lanes per
+// 128-B row segment (coalesced), instead of 16-B register loads from 32
+// different rows per instruction -- the vector-memory path (TA/TD/TCP) was the
+// busiest unit of the pass (TD 97 %, TA 88 % busy; 63 % of the L1 accesses
+// were these loads). Ring of two 4-KiB steps (16 dims x 32 points x 8 B).
+constexpr int FH_GATH_STEP = 32 * 16 * 8;
+constexpr int FH_GATH_WAVE = 2 * FH_GATH_STEP;
+constexpr int FH_GATH_KMAX = 256;
+__host__ __device__ constexpr int fh_gath_off(int Kpad, bool hash) { return (fh_lds_bytes(Kpad, hash) + 255) & ~255; }
+static_assert(fh_gath_off(FH_GATH_KMAX, true) + 8 * FH_GATH_WAVE <= 160 * 1024, "gather ring exceeds 160 KiB");
+
+// One LDS-DMA piece: each lane's 16 B at gsrc land at lds_dst + 16 * lane
+// (M0 written and restored in the same statement; the load is invisible to the
+// compiler's wait counting: the chain waits for it with an explicit vmcnt).
+__device__ inline void glds16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1, bool GATH = false>
 __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_kernel(FusedArgs a) {
     constexpr int FH_WAVES = fh_waves<HASH, MP, MET>();
     constexpr int FH_THREADS = 64 * FH_WAVES;
     static_assert(NIMG == 1 || (!MP && MET == 0), "two-image form: euclidean, single launch");
+    static_assert(!GATH || (!MP && MET == 0 && NIMG == 1 && FH_WAVES == 8), "gather ring: euclidean single pass");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
     const int KI = NIMG == 2 ? FH_KMAX : Kpad;           // centroid rows the LDS image holds
@@ -1499,8 +1521,27 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #else
         const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
 #endif
+        // GATH: piece u of a step holds points 8u..8u+7, lane L the 16-B chunk
+        // (L & 7) ^ swz(p) of point p = 8u + (L >> 3) (swz(p) = (p >> 1) & 7: the
+        // lanes of each ds_read_b128 group hit 16 distinct 4-bank groups)
+        const double* gsrc[4];
+        uint32_t gbase = 0;
+        if constexpr (GATH) {
+            gbase = (uint32_t)__builtin_amdgcn_readfirstlane(
+                (int)((uint32_t)(uintptr_t)(smem + fh_gath_off(Kpad, HASH)) + (uint32_t)wave * FH_GATH_WAVE));
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = 8 * u + (lane >> 3);
+                const int Ip = __shfl(I1, p);
+                gsrc[u] = a.C64 + (size_t)Ip * FU_D + 2 * ((lane & 7) ^ ((p >> 1) & 7));
+            }
+#pragma unroll
+            for (int s0 = 0; s0 < 2; s0++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) glds16(gsrc[u] + 16 * s0, gbase + s0 * FH_GATH_STEP + u * 1024);
+        }
         double2 cbuf[CHAIN_PF][4];
-        if (MET == 0) {
+        if (MET == 0 && !GATH) {
 #pragma unroll
             for (int s = 0; s < CHAIN_PF; s++)
 #pragma unroll
@@ -1553,16 +1594,49 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #if defined(ABL_CHAIN_TREE)
             double tacc[4] = {0.0, 0.0, 0.0, 0.0};
 #endif
+            // GATH: a step's values come from the ring one step early (the LDS read
+            // overlaps the previous step's chain), the ring slot is refilled two
+            // steps ahead as soon as it is read
+            double2 gnext[4];
+            auto gread = [&](int st) {
+                const char* ring = smem + fh_gath_off(Kpad, HASH) + wave * FH_GATH_WAVE + (st & 1) * FH_GATH_STEP;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    gnext[j] = *reinterpret_cast<const double2*>(ring + col * 128 + 16 * ((4 * h + j) ^ ((col >> 1) & 7)));
+            };
+            if constexpr (GATH) {
+                __builtin_amdgcn_s_waitcnt(0x0F74);                        // vmcnt(4): step 0 landed
+                asm volatile("" ::: "memory");
+                gread(0);
+            }
 #pragma unroll
             for (int s = 0; s < 8; s++) {
                 double sq[8];
                 double2 cur[4];
+                if constexpr (GATH) {
 #pragma unroll
-                for (int j = 0; j < 4; j++) cur[j] = cbuf[s % CHAIN_PF][j];
-                if (s + CHAIN_PF < 8) {
+                    for (int j = 0; j < 4; j++) cur[j] = gnext[j];
+                    if (s + 2 < 8) {
+                        __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): slot s & 1 is read
+                        asm volatile("" ::: "memory");
 #pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        cbuf[s % CHAIN_PF][j] = CHAIN_LD(crow + 16 * (s + CHAIN_PF) + 2 * j, 8 * (s + CHAIN_PF) + 2 * j);
+                        for (int u = 0; u < 4; u++)
+                            glds16(gsrc[u] + 16 * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
+                    }
+                    if (s + 1 < 8) {
+                        if (s + 2 < 8) __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): step s + 1 landed
+                        else __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
+                        asm volatile("" ::: "memory");
+                        gread(s + 1);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) cur[j] = cbuf[s % CHAIN_PF][j];
+                    if (s + CHAIN_PF < 8) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            cbuf[s % CHAIN_PF][j] = CHAIN_LD(crow + 16 * (s + CHAIN_PF) + 2 * j, 8 * (s + CHAIN_PF) + 2 * j);
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -2059,8 +2133,17 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                         else FH_LAUNCH(false, true, 1);
                     }
                 } else if (np1 == 1) {
-                    if (hash) FH_LAUNCH(true, false, 0);
-                    else FH_LAUNCH(false, false, 0);
+                    // K <= 256: the winner rows by the LDS-DMA gather (LSHKM_GATHER=0: register loads)
+                    const char* gv = getenv("LSHKM_GATHER");
+                    if (a.Kpad <= FH_GATH_KMAX && !(gv && !strcmp(gv, "0"))) {
+                        const size_t lg = (size_t)fh_gath_off(a.Kpad, hash) + 8 * FH_GATH_WAVE;
+                        if (hash) hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
+                        else hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
+                    } else if (hash) {
+                        FH_LAUNCH(true, false, 0);
+                    } else {
+                        FH_LAUNCH(false, false, 0);
+                    }
                 } else {
                     if (hash && p == 0) FH_LAUNCH(true, true, 0);
                     else FH_LAUNCH(false, true, 0);

@@ -6,7 +6,7 @@ import pytest
 
 import oracle
 from amd import lshkm
-from conftest import cases, golden, golden_meta, lloyd_input
+from conftest import case_rows, cases, golden, golden_meta, lloyd_input
 
 META = golden_meta()
 pytestmark = pytest.mark.gpu
@@ -32,6 +32,17 @@ def test_silhouette_golden(ctx, name):
     m, g = META[name], golden(name)
     X = to_dev(ctx, lloyd_input(name))
     for it in range(len(g["cont"])):
+        out, _ = lshkm.silhouette(ctx, X, to_dev(ctx, g[f"assign{it}"]), to_dev(ctx, g[f"centers{it}"]), m["metric"])
+        assert np.array_equal(bits(out), bits(g[f"sil{it}"])), (it, out, g[f"sil{it}"])
+
+
+@pytest.mark.parametrize("name", cases("range"))
+def test_silhouette_range_golden(ctx, name):
+    # the silhouettes of the reference's range assignments (lsh_/cube_range_assignment
+    # clusters, incl. "k_means_center" centroids after an update)
+    m, g = META[name], golden(name)
+    X = to_dev(ctx, np.ascontiguousarray(case_rows(name)))
+    for it in range(int(g["iters"][0])):
         out, _ = lshkm.silhouette(ctx, X, to_dev(ctx, g[f"assign{it}"]), to_dev(ctx, g[f"centers{it}"]), m["metric"])
         assert np.array_equal(bits(out), bits(g[f"sil{it}"])), (it, out, g[f"sil{it}"])
 

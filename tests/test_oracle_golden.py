@@ -198,6 +198,17 @@ def test_silhouette(name):
         assert np.array_equal(out.view(np.uint64), g[f"sil{it}"].view(np.uint64)), it
 
 
+@pytest.mark.parametrize("name", RANGE)
+def test_range_silhouette(name):
+    # silhouette_cluster of each range assignment (the reference's harness runs
+    # it on the clusters lsh_/cube_range_assignment produced), NaN bits included
+    m, g = META[name], golden(name)
+    X = case_rows(name)
+    for it in range(int(g["iters"][0])):
+        out, _ = oracle.silhouette(X, g[f"assign{it}"], g[f"centers{it}"], m["metric"])
+        assert np.array_equal(out.view(np.uint64), g[f"sil{it}"].view(np.uint64)), it
+
+
 @pytest.mark.parametrize("name", cases("chain"))
 def test_recommender_chain(name):
     # main.cpp:149-222: cosine LSH over user vectors (general doubles), filtered
