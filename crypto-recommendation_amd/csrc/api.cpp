@@ -474,6 +474,14 @@ static int assign_path(int metric, int d, int K, bool f64) {
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
+// LSHKM_DIST=fast: euclidean winner distances (d = 128 fused path) from f32(c)
+// in f32, certified to 2^-20 relative -- inside the 1e-5 the north star sets for
+// distances; cluster IDs stay bit-exact. Default: the reference-order fp64 chain.
+static bool fast_dist_on() {
+    const char* e = getenv("LSHKM_DIST");
+    return e && !strcmp(e, "fast");
+}
+
 // Exact reference-order pass over the rows listed in ws_ambig (count on device).
 // Segmented lists (seg_counts != NULL) come from the persistent fused form.
 static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int metric,
@@ -544,8 +552,19 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
         float* cnh = cbound + 8;
         double* nbv = (double*)(cnh + Kpad);               // cosine: [Kpad] sequential |c|^2 (Kpad % 64 == 0: aligned)
-        if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        // euclidean winner distances: the certified f32 form (LSHKM_DIST=fast) or the
+        // reference-order fp64 chain (default)
+        const bool fast = !cosine && fast_dist_on();
+        float* C32 = nullptr;
+        float* rn32 = nullptr;
+        if (fast) {
+            if ((rc = ctx->ws_cf32.reserve((size_t)Kpad * 128 * 4 + (size_t)Kpad * 4))) return rc;
+            C32 = (float*)ctx->ws_cf32.p;
+            rn32 = C32 + (size_t)Kpad * 128;
+        }
+        if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv, C32, rn32))) { LSHKM_LAUNCH_CHECK(); return rc; }
         FusedLaunch f;
+        f.C32 = C32; f.rn32 = rn32; f.fast_dist = fast ? 1 : 0;
         f.X = X.f(); f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C; f.Kpad = Kpad;
         f.assign = assign; f.dist = dist; f.ambig = (int32_t*)ctx->ws_ambig.p; f.ambig_count = cnt;
         f.stats = (unsigned long long*)ctx->stats.p;

@@ -107,6 +107,9 @@ struct FusedArgs {
     const int32_t* list_counts;
     int64_t list_seg_rows;
     unsigned long long* prof;        // LSHKM_PHASE_TIMING builds only: per-phase wave cycles
+    const float* C32;                // fast_dist: [Kpad][128] f32(c) and |c - f32(c)| (FusedLaunch)
+    const float* rn32;
+    int fast_dist;
 };
 
 // Profiling builds (make prof -> liblshkm_prof.so) accumulate s_memtime per
@@ -162,6 +165,11 @@ __device__ inline double swap_halves(double v, int h) {
     const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
     const uint32_t l = h ? lo[0] : lo[1], u = h ? hi[0] : hi[1];
     return __longlong_as_double((long long)(((uint64_t)u << 32) | l));
+}
+
+__device__ inline float swap_halves_f(float v, int h) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(h ? r[0] : r[1]);
 }
 
 // One direction of the half swap (the chain hand-offs): take_from_lower gives
@@ -1526,7 +1534,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         // lanes of each ds_read_b128 group hit 16 distinct 4-bank groups)
         const double* gsrc[4];
         uint32_t gbase = 0;
-        if constexpr (GATH) {
+        if (GATH && !a.fast_dist) {
             gbase = (uint32_t)__builtin_amdgcn_readfirstlane(
                 (int)((uint32_t)(uintptr_t)(smem + fh_gath_off(Kpad, HASH)) + (uint32_t)wave * FH_GATH_WAVE));
 #pragma unroll
@@ -1541,7 +1549,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                 for (int u = 0; u < 4; u++) glds16(gsrc[u] + 16 * s0, gbase + s0 * FH_GATH_STEP + u * 1024);
         }
         double2 cbuf[CHAIN_PF][4];
-        if (MET == 0 && !GATH) {
+        if (MET == 0 && !GATH && !a.fast_dist) {
 #pragma unroll
             for (int s = 0; s < CHAIN_PF; s++)
 #pragma unroll
@@ -1550,7 +1558,38 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #endif
         const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
 
-        const bool amb = valid && !cert;
+        // euclidean fast distance (a.fast_dist): the winner's distance from f32(c)
+        // in f32 with every lane busy, certified to 2^-20 relative (DESIGN.md §5:
+        // 8 accumulators per lane, <= 12 roundings per sum, plus the f32(c)
+        // residual |c - f32(c)| of the centroid); a row whose bound fails is
+        // refined like an uncertified argmin (the exact chain of the LIST form)
+        bool dok = true;
+        double fdist = 0.0;
+        if constexpr (MET == 0) {
+            if (a.fast_dist) {
+                const float* c32 = a.C32 + (size_t)I1 * FU_D + 8 * h;
+                float2v q[4] = {};
+#pragma unroll
+                for (int s = 0; s < 8; s++) {
+                    const float4 c0 = *reinterpret_cast<const float4*>(c32 + 16 * s);
+                    const float4 c1 = *reinterpret_cast<const float4*>(c32 + 16 * s + 4);
+                    const float2v cv[4] = {{c0.x, c0.y}, {c0.z, c0.w}, {c1.x, c1.y}, {c1.z, c1.w}};
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const float2v xv = {xf[8 * s + 2 * j], xf[8 * s + 2 * j + 1]};
+                        const float2v dv = xv - cv[j];
+                        q[j] = __builtin_elementwise_fma(dv, dv, q[j]);
+                    }
+                }
+                float t = ((q[0].x + q[0].y) + (q[1].x + q[1].y)) + ((q[2].x + q[2].y) + (q[3].x + q[3].y));
+                t = t + swap_halves_f(t, h);
+                const double S = (double)t, R = (double)a.rn32[I1];
+                const double B = 14.2 * 0x1p-24 * S + 2.02 * R * sqrt(S) + 2.02 * R * R + 0x1p-100;
+                dok = B <= 0x1p-19 * S;                   // false for inf / nan
+                fdist = sqrt(S);
+            }
+        }
+        const bool amb = valid && !(cert && dok);
         const unsigned long long amask = __ballot(amb && h == 1);
         if (amb && h == 1) {
             int base = 0;
@@ -1579,6 +1618,11 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                 if (lane == leader) base = atomicAdd(lcount + 2, __popcll(fb));
                 base = __shfl(base, leader);
                 if (fix) cfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
+            }
+        } else if (a.fast_dist) {
+            if (h == 1 && valid && cert && dok) {
+                a.assign[row] = I1;
+                a.dist[row] = fdist;
             }
         } else {
 #if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
@@ -1922,7 +1966,8 @@ __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) 
 // Centroids -> f16 hi/lo rows, -||c||^2/2, and the per-call bound maxima.
 __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpad, _Float16* __restrict__ Ch,
                                     _Float16* __restrict__ Cl, float* __restrict__ cnh, unsigned int* __restrict__ cb,
-                                    int metric, double* __restrict__ nbv) {
+                                    int metric, double* __restrict__ nbv, float* __restrict__ C32,
+                                    float* __restrict__ rn32) {
     const int c = blockIdx.x;            // one wave per centroid row (d = 128: 2 dims per lane)
     const int lane = threadIdx.x;
     double s2 = 0.0, s1 = 0.0;
@@ -1949,9 +1994,15 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
         }
     }
     double rr = 0.0, hh = 0.0;           // |c - ch|^2, |ch|^2 (the hi-only scores' bound)
+    double r32 = 0.0;                    // |c - f32(c)|^2 (fast distances)
     for (int j = lane; j < FU_D; j += 64) {
         const double v = c < K ? C[(size_t)c * FU_D + j] * scale : 0.0;
         const float f = (float)v;
+        if (C32) {
+            C32[(size_t)c * FU_D + j] = f;
+            const double e = v - (double)f;       // exact (or inf / nan: never certified)
+            r32 = fma(e, e, r32);
+        }
         const _Float16 hv = (_Float16)f;
         Ch[(size_t)c * FU_D + j] = hv;
         Cl[(size_t)c * FU_D + j] = (_Float16)(f - (float)hv);
@@ -1967,7 +2018,10 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
         s1 += __shfl_xor(s1, off);
         rr += __shfl_xor(rr, off);
         hh += __shfl_xor(hh, off);
+        r32 += __shfl_xor(r32, off);
     }
+    // sum of 128 non-negative fp64 values: <= 2^-46 relative rounding; rounded up
+    if (rn32 && lane == 0) rn32[c] = r32 == 0.0 ? 0.f : (float)(sqrt(r32) * (1.0 + 0x1p-40)) * (1.f + 0x1p-22f);
     const unsigned long long anybad = __ballot(bad);
     if (lane != 0) return;
     // padding rows: a finite score far below any real one (|x.c| < 2^38 under the
@@ -1991,14 +2045,18 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
 }
 
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
-                      float* cbound, int metric, double* nbv) {
+                      float* cbound, int metric, double* nbv, float* C32, float* rn32) {
     if (metric == 1 && !nbv) {
         set_error("launch_fused_prep: cosine needs the norm array");
         return -1;
     }
+    if ((C32 == nullptr) != (rn32 == nullptr)) {
+        set_error("launch_fused_prep: the fast-distance image needs both arrays");
+        return -1;
+    }
     (void)hipMemsetAsync(cbound, 0, 32, s);
     hipLaunchKernelGGL(fused_centroid_prep, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, Ch, Cl, cnh,
-                       reinterpret_cast<unsigned int*>(cbound), metric, nbv);
+                       reinterpret_cast<unsigned int*>(cbound), metric, nbv, C32, rn32);
     return kstatus("fused_centroid_prep");
 }
 
@@ -2018,6 +2076,8 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.nbv = f.nbv;
     a.part = nullptr; a.t0 = 0; a.pass_first = 1; a.pass_last = 1;
     a.prof = nullptr;
+    a.C32 = f.C32; a.rn32 = f.rn32;
+    a.fast_dist = f.fast_dist && f.metric == 0 && f.C32 && f.rn32 ? 1 : 0;
 #ifdef LSHKM_PHASE_TIMING
     static unsigned long long* prof_d = nullptr;
     if (!prof_d) (void)hipMalloc(&prof_d, 64);

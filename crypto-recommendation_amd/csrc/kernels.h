@@ -224,6 +224,12 @@ struct FusedLaunch {
     // certified form declined (cos_fix_seg pass)
     int metric = 0;
     const double* nbv = nullptr;
+    // euclidean fast distance (fast_dist): the winner's distance from f32(c) in
+    // f32, certified to 2^-20 relative (else the row is refined exactly);
+    // C32 [Kpad][128] = f32(c), rn32 [Kpad] = |c - f32(c)|_2 rounded up
+    const float* C32 = nullptr;
+    const float* rn32 = nullptr;
+    int fast_dist = 0;
     // K > 256 on the persistent form: passes over 256-centroid slices carry each
     // lane's (best, runner-up, tile) in part[] (32 B per point)
     void* part = nullptr;
@@ -256,7 +262,8 @@ constexpr int64_t FUSED_PART_BYTES_PER_ROW = 32;
 constexpr int64_t FUSED_LIST_SLACK = 32 + 1024 * 12 * 32;
 constexpr int FUSED_MAX_SEGS = 1024;
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
-                      float* cbound, int metric = 0, double* nbv = nullptr);
+                      float* cbound, int metric = 0, double* nbv = nullptr, float* C32 = nullptr,
+                      float* rn32 = nullptr);
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
 // Cosine winners listed by the persistent form (segment b: hfix[b * seg_rows ..],
 // count seg_counts[2b + 1]): soft-x87 distances.

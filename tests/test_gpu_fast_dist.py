@@ -1,0 +1,104 @@
+"""GPU parity of the fast winner distance (LSHKM_DIST=fast, euclidean, d = 128).
+
+The winner's distance is formed from f32(c) in f32 (every lane busy, no fp64
+chain) with a rigorous bound; a row whose bound exceeds 2^-20 relative is
+refined like an uncertified argmin (the exact reference-order chain). Cluster
+IDs stay bit-exact; distances are within 2^-20 relative of the reference's
+(north star: 1e-5 relative on float distances). Reference:
+lib/data_structures/cust_vector.hpp:124-136 (euclideanDistance),
+lib/clustering_phases/assignment.hpp:54-80."""
+import numpy as np
+import pytest
+
+import oracle
+from amd import lshkm
+
+pytestmark = pytest.mark.gpu
+TOL = 2.0 ** -20          # certified relative bound on every fast distance (< 1e-5, the north star's)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return lshkm.Context(0)
+
+
+@pytest.fixture
+def fast(monkeypatch):
+    monkeypatch.setenv("LSHKM_DIST", "fast")
+
+
+def to_dev(ctx, a):
+    return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+
+
+def check(a, d, oa, od):
+    assert np.array_equal(a, oa)
+    ok = od > 0
+    rel = np.abs(d[ok] - od[ok]) / od[ok]
+    assert rel.max(initial=0.0) <= TOL, rel.max()
+    assert np.all(d[~ok] == od[~ok])
+
+
+@pytest.mark.parametrize("K,centers", [(256, "rows"), (256, "f64"), (1024, "f64"), (1000, "rows")])
+def test_fast_distance_vs_oracle(ctx, fast, K, centers):
+    # the hashing fused pass (K <= 256 single pass, K > 512 two passes); dataset-row
+    # centroids (f32(c) exact) and general fp64 centroids (a residual per centroid)
+    N, d, L, k = 60_003, 128, 5, 4
+    X = ctx.synth(0xFA57 + K, N, d)
+    Xh = X.cpu().numpy()
+    V, t, r, _ = lshkm.params_lsh_euclidean(5, L, k, d, 0.4)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
+    rng = np.random.default_rng(K)
+    Ch = Xh[rng.choice(N, K, replace=False)].astype(np.float64)
+    if centers == "f64":
+        Ch = Ch * (1.0 + 1e-3 * rng.standard_normal(Ch.shape)) + 1e-6
+    Ch[7] = Ch[3]                                 # an exact tie
+    tu, _, bu, a, dist = lshkm.hash_assign(lsh, X, to_dev(ctx, Ch), tuples=True, bucket=True)
+    xt, _, xb = oracle.lsh_hash_euclid(Xh, V, t, np.float32(0.4), r, N // 100)
+    assert np.array_equal(tu.cpu().numpy(), xt) and np.array_equal(bu.cpu().numpy(), xb)
+    sub = np.random.default_rng(1).choice(N, 3000, replace=False)
+    oa, od = oracle.lloyd_assign(Xh[sub], Ch, "euclidean", None)
+    check(a.cpu().numpy()[sub], dist.cpu().numpy()[sub], oa, od)
+
+
+def test_fast_distance_fallback_rows(ctx, fast):
+    # rows at (or next to) a general fp64 centroid: the residual |c - f32(c)| is
+    # not small against the distance, the bound fails and the exact chain runs;
+    # rows beyond the f16 range and an overflowing f32 sum also go exact
+    N, d, K = 20_000, 128, 64
+    X = ctx.synth(0xFA11, N, d)
+    Xh = X.cpu().numpy().copy()
+    rng = np.random.default_rng(3)
+    Ch = Xh[rng.choice(N, K, replace=False)].astype(np.float64) * (1.0 + 2.0 ** -30)
+    Xh[:K] = Ch.astype(np.float32)                # distance ~ 2^-30 |c|: exact fallback
+    Xh[K:2 * K] = (Ch + 1e-3).astype(np.float32)
+    Xh[500] = 3.0e19                              # f32 squares overflow
+    X = to_dev(ctx, Xh)
+    ctx.reset_stats()
+    a, dist = lshkm.lloyd_assign(ctx, X, to_dev(ctx, Ch), "euclidean")
+    # listed by the hi-only pass: refined by the 3-product form (exact chain) or the exact pass
+    assert ctx.stat(lshkm.STAT_REFINED) + ctx.stat(lshkm.STAT_ASSIGN_AMBIG) >= K
+    rows = np.r_[0:3 * K, 500, np.random.default_rng(4).choice(N, 1500, replace=False)]
+    oa, od = oracle.lloyd_assign(Xh[rows], Ch, "euclidean", None)
+    ga, gd = a.cpu().numpy()[rows], dist.cpu().numpy()[rows]
+    assert np.array_equal(ga, oa)
+    # the fallback rows carry the exact chain's distance (x_j - c_j exact here: bit-exact
+    # except glibc pow vs x*x)
+    np.testing.assert_allclose(gd[:K], od[:K], rtol=1e-14, atol=0)
+    check(ga, gd, oa, od)
+
+
+def test_fast_and_exact_modes_agree_on_ids(ctx, monkeypatch):
+    # the default (reference-order fp64 chain) and the fast mode give the same
+    # cluster IDs everywhere and distances within the bound, at the C3 shape
+    N, d, K = 500_000, 128, 256
+    X = ctx.synth(0x5EED, N, d)
+    rows = (np.arange(K) * (N // K)).astype(np.int64)
+    Cc = X[to_dev(ctx, rows)].double()
+    a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows.astype(np.int32))
+    monkeypatch.setenv("LSHKM_DIST", "fast")
+    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows.astype(np.int32))
+    assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
+    check(a1.cpu().numpy(), d1.cpu().numpy(), a0.cpu().numpy(), d0.cpu().numpy())
