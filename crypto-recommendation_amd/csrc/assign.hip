@@ -138,6 +138,27 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
             }
             *reinterpret_cast<float4*>(xs + r * DS + j) = v;
         }
+    } else if (sizeof(TX) == 8 && (d & 1) == 0) {
+        // fp64 rows of even d (the recommender's user vectors, d = number of coins):
+        // 16-B loads, a row per 64-lane pass (was one 8-B load per element)
+        for (int e2 = lane; e2 < 32 * DP / 2; e2 += 64) {
+            const int r = e2 / (DP / 2), j = (e2 % (DP / 2)) * 2;
+            const int64_t row = pbase + r;
+            float2 v = make_float2(0.f, 0.f);
+            if (row < N && j < d) {
+                const double2 a = *reinterpret_cast<const double2*>(X + row * d + j);
+                v = make_float2((float)a.x, (float)a.y);
+            }
+            *reinterpret_cast<float2*>(xs + r * DS + j) = v;
+        }
+    } else if (sizeof(TX) == 4 && (d & 3) == 0) {
+        for (int e4 = lane; e4 < 32 * DP / 4; e4 += 64) {
+            const int r = e4 / (DP / 4), j = (e4 % (DP / 4)) * 4;
+            const int64_t row = pbase + r;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < N && j < d) v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + row * d + j);
+            *reinterpret_cast<float4*>(xs + r * DS + j) = v;
+        }
     } else {
         for (int e = lane; e < 32 * DP; e += 64) {
             const int r = e / DP, j = e % DP;

@@ -1295,6 +1295,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     constexpr bool xpf = XPF && NIMG == 1;
     float xf[64];
     if (xpf && tfirst + wave < ntiles) load_row(tfirst + wave, xf);
+    PT_DECL
     for (int64_t tile = tfirst + wave; NIMG == 2 ? rd < nround : tile < ntiles; tile += tstride, rd++) {
         const int64_t row = tile * 32 + col;
         const bool valid = row < a.N;
@@ -2195,10 +2196,15 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 } else if (np1 == 1) {
                     // K <= 256: the winner rows by the LDS-DMA gather (LSHKM_GATHER=0: register loads)
                     const char* gv = getenv("LSHKM_GATHER");
+#if defined(FH_WAVES_SET) && FH_WAVES_SET != 8      // experiments: the gather ring is sized for 8 waves
+                    (void)gv;
+                    if (false) {
+#else
                     if (a.Kpad <= FH_GATH_KMAX && !(gv && !strcmp(gv, "0"))) {
                         const size_t lg = (size_t)fh_gath_off(a.Kpad, hash) + 8 * FH_GATH_WAVE;
                         if (hash) hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
                         else hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
+#endif
                     } else if (hash) {
                         FH_LAUNCH(true, false, 0);
                     } else {

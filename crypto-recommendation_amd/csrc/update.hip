@@ -19,6 +19,56 @@ namespace lshkm {
 
 constexpr int KM_U = 16;
 
+// One (c, j) chain over the member rows p in [beg, end), row order: groups of
+// KM_U rows, loads issued three groups (48 rows) ahead of the adds so a lane
+// keeps ~48 row loads in flight (the chains of large clusters were latency
+// bound at 16: the k-means update of 1M fp64 rows, d = 100, K = 256 spent 5 ms
+// in the longest chain). Row indices are wave-uniform (scalar loads); positions
+// past the end re-read the last row and are not added.
+template <typename TX>
+__device__ __attribute__((always_inline)) inline double km_chain_rows(const TX* __restrict__ X, int d, int j,
+                                       const __attribute__((address_space(4))) int32_t* r4, int64_t beg, int64_t end,
+                                       double s) {
+    if (end <= beg) return s;
+    const int64_t ng = (end - beg + KM_U - 1) / KM_U;
+    TX v0[KM_U], v1[KM_U], v2[KM_U], v3[KM_U];
+    auto ld = [&](TX (&v)[KM_U], int64_t g) {
+#pragma unroll
+        for (int u = 0; u < KM_U; u++) {
+            const int64_t p = min(beg + g * KM_U + u, end - 1);
+            v[u] = X[(int64_t)r4[p] * d + j];
+        }
+    };
+    auto add = [&](const TX (&v)[KM_U], int64_t g) {
+        const int64_t p0 = beg + g * KM_U;
+        if (p0 + KM_U <= end) {
+#pragma unroll
+            for (int u = 0; u < KM_U; u++) s = __dadd_rn(s, (double)v[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < KM_U; u++)
+                if (p0 + u < end) s = __dadd_rn(s, (double)v[u]);
+        }
+    };
+    ld(v0, 0);
+    ld(v1, 1);
+    ld(v2, 2);
+    for (int64_t g = 0; g < ng; g += 4) {
+        ld(v3, g + 3);
+        add(v0, g);
+        if (g + 1 >= ng) break;
+        ld(v0, g + 4);
+        add(v1, g + 1);
+        if (g + 2 >= ng) break;
+        ld(v1, g + 5);
+        add(v2, g + 2);
+        if (g + 3 >= ng) break;
+        ld(v2, g + 6);
+        add(v3, g + 3);
+    }
+    return s;
+}
+
 template <typename TX>
 __global__ __launch_bounds__(64) void km_chain_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                      const int64_t* __restrict__ crow, int K,
@@ -31,16 +81,7 @@ __global__ __launch_bounds__(64) void km_chain_kernel(const TX* __restrict__ X, 
     if (j >= d) return;
     const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
     // exact mode across shards: the chain continues from the previous shard's running sum
-    double s = carry ? carry[(size_t)c * d + j] : 0.0;
-    int64_t p = beg;
-    for (; p + KM_U <= end; p += KM_U) {
-        TX v[KM_U];
-#pragma unroll
-        for (int u = 0; u < KM_U; u++) v[u] = X[(int64_t)r4[p + u] * d + j];
-#pragma unroll
-        for (int u = 0; u < KM_U; u++) s = __dadd_rn(s, (double)v[u]);
-    }
-    for (; p < end; p++) s = __dadd_rn(s, (double)X[(int64_t)r4[p] * d + j]);
+    const double s = km_chain_rows(X, d, j, r4, beg, end, carry ? carry[(size_t)c * d + j] : 0.0);
     sums[(size_t)c * d + j] = s;
 }
 
@@ -264,18 +305,8 @@ __global__ __launch_bounds__(64) void km_chain_flagged_kernel(const TX* __restri
     const int j = blockIdx.y * 64 + threadIdx.x;
     if (j >= d) return;
     const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
-    double s = carry ? carry[(size_t)c * d + j] : 0.0;
     const int64_t beg = crow[c], end = crow[c + 1];
-    int64_t p = beg;
-    for (; p + KM_U <= end; p += KM_U) {
-        TX v[KM_U];
-#pragma unroll
-        for (int u = 0; u < KM_U; u++) v[u] = X[(int64_t)r4[p + u] * d + j];
-#pragma unroll
-        for (int u = 0; u < KM_U; u++) s = __dadd_rn(s, (double)v[u]);
-    }
-    for (; p < end; p++) s = __dadd_rn(s, (double)X[(int64_t)r4[p] * d + j]);
-    sums[(size_t)c * d + j] = s;
+    sums[(size_t)c * d + j] = km_chain_rows(X, d, j, r4, beg, end, carry ? carry[(size_t)c * d + j] : 0.0);
 }
 
 __global__ void km_counts_kernel(const int64_t* __restrict__ crow, int K, const int64_t* __restrict__ carry_counts,
