@@ -33,10 +33,14 @@ __device__ __attribute__((always_inline)) inline double km_chain_rows(const TX* 
     const int64_t ng = (end - beg + KM_U - 1) / KM_U;
     TX v0[KM_U], v1[KM_U], v2[KM_U], v3[KM_U];
     auto ld = [&](TX (&v)[KM_U], int64_t g) {
+        const int64_t p0 = beg + g * KM_U;
+        if (p0 + KM_U <= end) {          // 16 contiguous indices: one scalar block load
+            const auto* rp = r4 + p0;
 #pragma unroll
-        for (int u = 0; u < KM_U; u++) {
-            const int64_t p = min(beg + g * KM_U + u, end - 1);
-            v[u] = X[(int64_t)r4[p] * d + j];
+            for (int u = 0; u < KM_U; u++) v[u] = X[(int64_t)rp[u] * d + j];
+        } else {
+#pragma unroll
+            for (int u = 0; u < KM_U; u++) v[u] = X[(int64_t)r4[min(p0 + u, end - 1)] * d + j];
         }
     };
     auto add = [&](const TX (&v)[KM_U], int64_t g) {
