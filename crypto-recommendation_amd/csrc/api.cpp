@@ -460,17 +460,20 @@ int lshkm_lsh_hash_f64(lshkm_lsh lsh, const double* X, int64_t N, int32_t* tuple
 // (persistent form, one launch per 256-centroid slice; cosine: normalised
 // centroids), else the f32-MFMA kernel (d <= 256), else the exact pass.
 // LSHKM_ASSIGN_PATH = "f32" / "exact" forces a path (tests compare them).
-// fp64 rows take the f32-MFMA kernel (rows rounded to f32 on load, the bound
+// Euclidean fp64 rows and fp32 rows of d < 128 dims (d <= 128, K <= 512) take
+// the hi-only form too (path 3: zero-padded dims, no LIST refinement); other
+// fp64 rows the f32-MFMA kernel (rows rounded to f32 on load, the bound
 // widened accordingly) or the exact pass.
 static int assign_path(int metric, int d, int K, bool f64) {
     const char* e = getenv("LSHKM_ASSIGN_PATH");
     if (e && !strcmp(e, "exact")) return 2;
     const bool f32 = e && !strcmp(e, "f32");
-    (void)K;
     if (d == 128 && !f32 && !f64) {
         const char* ff = getenv("LSHKM_FUSED_FORM");
         if (metric == LSHKM_METRIC_EUCLIDEAN || !(ff && !strcmp(ff, "chunked"))) return 0;
     }
+    const char* fh = getenv("LSHKM_FUSED_HI");
+    if (!f32 && metric == LSHKM_METRIC_EUCLIDEAN && d <= 128 && K <= 512 && !(fh && !strcmp(fh, "0"))) return 3;
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
@@ -526,7 +529,8 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
                                              X, N, lsh->proj, lsh->nb,
                                              lsh->metric == LSHKM_METRIC_EUCLIDEAN ? tuples : nullptr, phi, bucket,
                                              nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
-    if (path == 0) {
+    if (path == 0 || path == 3) {
+        const int rows_kind = path == 3 ? (X.f64 ? 2 : 1) : 0;
         const int Kpad = (K + 63) / 64 * 64;
         const bool cosine = metric != LSHKM_METRIC_EUCLIDEAN;
         // hi-only scoring + 3-product refinement; LSHKM_FUSED_HI=0: the 3-product form alone
@@ -554,7 +558,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         double* nbv = (double*)(cnh + Kpad);               // cosine: [Kpad] sequential |c|^2 (Kpad % 64 == 0: aligned)
         // euclidean winner distances: the certified f32 form (LSHKM_DIST=fast) or the
         // reference-order fp64 chain (default)
-        const bool fast = !cosine && fast_dist_on();
+        const bool fast = !cosine && rows_kind != 2 && fast_dist_on();
         float* C32 = nullptr;
         float* rn32 = nullptr;
         if (fast) {
@@ -562,10 +566,17 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             C32 = (float*)ctx->ws_cf32.p;
             rn32 = C32 + (size_t)Kpad * 128;
         }
-        if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv, C32, rn32))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        double* C64p = nullptr;                            // d < 128: zero-padded fp64 centroids
+        if (rows_kind != 0 && d != 128) {
+            if ((rc = ctx->ws_c64p.reserve((size_t)Kpad * 128 * 8))) return rc;
+            C64p = (double*)ctx->ws_c64p.p;
+        }
+        if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv, C32, rn32, d, C64p))) { LSHKM_LAUNCH_CHECK(); return rc; }
         FusedLaunch f;
         f.C32 = C32; f.rn32 = rn32; f.fast_dist = fast ? 1 : 0;
-        f.X = X.f(); f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C; f.Kpad = Kpad;
+        f.rows = rows_kind; f.d = d;
+        f.X = X.f64 ? nullptr : X.f(); f.X64 = X.f64 ? X.d() : nullptr;
+        f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C64p ? C64p : C; f.Kpad = Kpad;
         f.assign = assign; f.dist = dist; f.ambig = (int32_t*)ctx->ws_ambig.p; f.ambig_count = cnt;
         f.stats = (unsigned long long*)ctx->stats.p;
         f.list_cap = N + FUSED_LIST_SLACK;

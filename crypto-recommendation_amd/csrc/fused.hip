@@ -110,6 +110,10 @@ struct FusedArgs {
     const float* C32;                // fast_dist: [Kpad][128] f32(c) and |c - f32(c)| (FusedLaunch)
     const float* rn32;
     int fast_dist;
+    // general rows (fused_hi_kernel<..., ROWS = 1 / 2>): fp32 (X) or fp64 (X64)
+    // rows of d <= 128 dims, row stride d; xvec: rows 16-B aligned (vector loads)
+    const double* X64;
+    int d, xvec;
 };
 
 // Profiling builds (make prof -> liblshkm_prof.so) accumulate s_memtime per
@@ -462,6 +466,57 @@ constexpr int FP_WAVES = FP_WAVES_SET ? FP_WAVES_SET : FP_KEEP_X ? 8 : 12;   // 
 #ifndef XPF
 #define XPF 0           // hi-only kernel: next tile's row loaded during the winner chain
 #endif
+// General rows (ROWS = 1: fp32, 2: fp64; d <= 128 dims, row stride d): lane
+// half h's 64 values of row rowc in the B-operand layout (dims 16s+8h..+7),
+// zero past d; fp64 values rounded to f32 (the scores' operand; the bounds add
+// |x - f32(x)| <= 2^-24 |x|).
+template <int ROWS>
+__device__ inline void load_row_gen(const FusedArgs& a, int64_t rowc, int h, float (&dst)[64]) {
+    const int64_t ro = rowc * (int64_t)a.d;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const int j0 = 16 * s + 8 * h;
+        if (a.xvec && j0 + 8 <= a.d) {
+            if constexpr (ROWS == 1) {
+                const float4 p0 = *reinterpret_cast<const float4*>(a.X + ro + j0);
+                const float4 p1 = *reinterpret_cast<const float4*>(a.X + ro + j0 + 4);
+                dst[8 * s + 0] = p0.x; dst[8 * s + 1] = p0.y; dst[8 * s + 2] = p0.z; dst[8 * s + 3] = p0.w;
+                dst[8 * s + 4] = p1.x; dst[8 * s + 5] = p1.y; dst[8 * s + 6] = p1.z; dst[8 * s + 7] = p1.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const double2 q = *reinterpret_cast<const double2*>(a.X64 + ro + j0 + 2 * j);
+                    dst[8 * s + 2 * j] = (float)q.x;
+                    dst[8 * s + 2 * j + 1] = (float)q.y;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                float v = 0.f;
+                if (j0 + e < a.d) v = ROWS == 1 ? a.X[ro + j0 + e] : (float)a.X64[ro + j0 + e];
+                dst[8 * s + e] = v;
+            }
+        }
+    }
+}
+// fp64 rows: the exact values of 16-dim step st of lane half h (the winner chain)
+__device__ inline void load_x64_step(const FusedArgs& a, int64_t rowc, int st, int h, double2 (&o)[4]) {
+    const int64_t ro = rowc * (int64_t)a.d;
+    const int j0 = 16 * st + 8 * h;
+    if (a.xvec && j0 + 8 <= a.d) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) o[j] = *reinterpret_cast<const double2*>(a.X64 + ro + j0 + 2 * j);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            o[j] = make_double2(0.0, 0.0);
+            if (j0 + 2 * j < a.d) o[j].x = a.X64[ro + j0 + 2 * j];
+            if (j0 + 2 * j + 1 < a.d) o[j].y = a.X64[ro + j0 + 2 * j + 1];
+        }
+    }
+}
+
 // hi-only kernel's winner-row loads; ABL_CHAIN_NOLOAD (timing experiments
 // only, results invalid): values made from the row in registers instead
 #if defined(ABL_CHAIN_NOLOAD)
@@ -575,8 +630,12 @@ static_assert(fp_lds_bytes(FP_KMAX, true) <= 160 * 1024, "persistent LDS image e
 // MP: multi-pass (K > 256) form; the single-pass instantiation compiles without
 // the pass-state code. LIST: the rows are block b's segment of a row list (the
 // refinement of fused_hi_kernel's uncertified rows), not a range.
-template <bool HASH, int MET = 0, bool MP = false, bool LIST = false>
+// ROWS = 1 / 2 (LIST only): the refinement of fused_hi_kernel<..., ROWS>'s rows
+// (general rows, see there); fp64 rows add |x - f32(x)| |c| <= 2^-24 |x| |c| to E.
+template <bool HASH, int MET = 0, bool MP = false, bool LIST = false, int ROWS = 0>
 __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedArgs a) {
+    static_assert(ROWS == 0 || (LIST && !HASH && MET == 0 && FP_KEEP_X), "general rows: the euclidean LIST form");
+    static_assert(FP_KEEP_X || !LIST, "the quad-layout chain re-reads rows by tile index");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
     int* lcount = reinterpret_cast<int*>(smem);          // [0] ambiguous rows, [1] hash fix-up rows
@@ -662,7 +721,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 
         // ---- point -> registers and the split B operand
         float xf[64];
-        {
+        if constexpr (ROWS != 0) {
+            load_row_gen<ROWS>(a, valid ? row : a.N - 1, h, xf);
+        } else {
             // rows past N read row N-1 (results for them are never written)
             const float* xr = a.X + (valid ? row : a.N - 1) * FU_D + 8 * h;
 #pragma unroll
@@ -802,7 +863,8 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         // carries <= 2^-46 relative (the fp64 norm chains), and 1 - q rounds at 2^-52
         const float E = MET == 0
             ? (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2 +
-                      0x1p-18 * (nx * (double)cmaxf + 0.5 * (double)cmaxf * (double)cmaxf)) * (1.f + 0x1p-20f) + 1e-30f
+                      0x1p-18 * (nx * (double)cmaxf + 0.5 * (double)cmaxf * (double)cmaxf) +
+                      (ROWS == 2 ? 0x1p-24 * nx * (double)cmaxf : 0.0)) * (1.f + 0x1p-20f) + 1e-30f
             : (float)(nx * (double)ecf + (double)ebf + FU_A2 * x1 + 0x1p-41 * xn2 +
                       0x1p-18 * nx * (double)cmaxf + 0x1p-43 * nx) * (1.f + 0x1p-20f) + 1e-30f;
         float m1 = -__builtin_inff(), m2 = -__builtin_inff();
@@ -921,6 +983,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             double tacc[4] = {0.0, 0.0, 0.0, 0.0};
 #endif
             double2 cbuf[CHAIN_PF][4];
+            double2 xnext[4];                 // fp64 rows: the exact values, one step ahead
+            const int64_t rowc = valid ? row : a.N - 1;
+            if constexpr (ROWS == 2) load_x64_step(a, rowc, 0, h, xnext);
 #pragma unroll
             for (int s = 0; s < CHAIN_PF; s++)
 #pragma unroll
@@ -936,11 +1001,20 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                     for (int j = 0; j < 4; j++)
                         cbuf[s % CHAIN_PF][j] = *reinterpret_cast<const double2*>(crow + 16 * (s + CHAIN_PF) + 2 * j);
                 }
+                double2 xcur[4];
+                if constexpr (ROWS == 2) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) xcur[j] = xnext[j];
+                    if (s + 1 < 8) load_x64_step(a, rowc, s + 1, h, xnext);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) xcur[j] = make_double2((double)xf[8 * s + 2 * j], (double)xf[8 * s + 2 * j + 1]);
+                }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const double2 cc = cur[j];
-                    const double d0 = __dsub_rn((double)xf[8 * s + 2 * j], cc.x);
-                    const double d1 = __dsub_rn((double)xf[8 * s + 2 * j + 1], cc.y);
+                    const double d0 = __dsub_rn(xcur[j].x, cc.x);
+                    const double d1 = __dsub_rn(xcur[j].y, cc.y);
                     sq[2 * j] = __dmul_rn(d0, d0);
                     sq[2 * j + 1] = __dmul_rn(d1, d1);
                 }
@@ -1194,12 +1268,21 @@ __device__ inline void glds16(const void* gsrc, uint32_t lds_dst) {
                  : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 
-template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1, bool GATH = false>
+// ROWS = 0: fp32 rows of 128 dims (X); 1: fp32 rows of d <= 128 dims; 2: fp64
+// rows of d <= 128 dims (X64) -- euclidean Lloyd without hashing, one pass.
+// Dims d..127 are zero in the row and in the centroid images (the prep pads
+// them). fp64 rows: the scores use xh = f16(f32(x)); |x - f32(x)| <= 2^-24 |x|
+// joins |xr| in the bound; the winner chain re-reads the fp64 row (the
+// register copy is f32).
+template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1, bool GATH = false, int ROWS = 0>
 __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_kernel(FusedArgs a) {
     constexpr int FH_WAVES = fh_waves<HASH, MP, MET>();
     constexpr int FH_THREADS = 64 * FH_WAVES;
     static_assert(NIMG == 1 || (!MP && MET == 0), "two-image form: euclidean, single launch");
     static_assert(!GATH || (!MP && MET == 0 && NIMG == 1 && FH_WAVES == 8), "gather ring: euclidean single pass");
+    static_assert(ROWS == 0 || (!HASH && !MP && MET == 0 && NIMG == 1), "general rows: euclidean Lloyd, one pass");
+    // the gather's explicit vmcnt waits assume no other vector loads in the chain
+    static_assert(!(GATH && ROWS == 2), "fp64 rows re-read x in the chain: register loads of the winner rows");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
     const int KI = NIMG == 2 ? FH_KMAX : Kpad;           // centroid rows the LDS image holds
@@ -1267,6 +1350,11 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     // this lane's 64 values of row (tile, col) in the B-operand layout (rows past
     // the end read row N-1: their results are never stored)
     auto load_row = [&](int64_t tl, float (&dst)[64]) {
+        if constexpr (ROWS != 0) {
+            const int64_t rr = tl * 32 + col;
+            load_row_gen<ROWS>(a, rr < a.N ? rr : a.N - 1, h, dst);
+            return;
+        }
 #if defined(ABL_XLD_COAL)   // timing experiments only: lane quads read 64 contiguous bytes (wrong layout)
         const int64_t rr = tl * 32 + (lane >> 2);
         const float* xr = a.X + (rr < a.N ? rr : a.N - 1) * FU_D + 4 * (lane & 3);
@@ -1323,6 +1411,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             xn2 = (double)xn2f * (1.0 + 0x1p-16);
             nx = sqrt(xn2);
             nxr = sqrt((double)xr2f * (1.0 + 0x1p-16)) + 0x1p-100;
+            if (ROWS == 2) nxr += 0x1p-24 * nx * (1.0 + 0x1p-20);   // |x - f32(x)| (fp64 rows)
             nxh = nx + nxr;                                     // |xh| <= |x| + |xr|
             x_ok = xn2f <= FU_RANGE * FU_RANGE;
         };
@@ -1549,6 +1638,15 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #pragma unroll
                 for (int u = 0; u < 4; u++) glds16(gsrc[u] + 16 * s0, gbase + s0 * FH_GATH_STEP + u * 1024);
         }
+        // fp64 rows: the chain's x values re-read (mostly L2) four 16-dim steps
+        // ahead (one step ahead left the chain waiting ~8 round trips per tile)
+        constexpr int XD = 4;
+        double2 xring[XD][4];
+        const int64_t rowc = row < a.N ? row : a.N - 1;
+        if constexpr (ROWS == 2) {
+#pragma unroll
+            for (int st = 0; st < XD; st++) load_x64_step(a, rowc, st, h, xring[st]);
+        }
         double2 cbuf[CHAIN_PF][4];
         if (MET == 0 && !GATH && !a.fast_dist) {
 #pragma unroll
@@ -1683,11 +1781,20 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                             cbuf[s % CHAIN_PF][j] = CHAIN_LD(crow + 16 * (s + CHAIN_PF) + 2 * j, 8 * (s + CHAIN_PF) + 2 * j);
                     }
                 }
+                double2 xcur[4];
+                if constexpr (ROWS == 2) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) xcur[j] = xring[s % XD][j];
+                    if (s + XD < 8) load_x64_step(a, rowc, s + XD, h, xring[s % XD]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) xcur[j] = make_double2((double)xf[8 * s + 2 * j], (double)xf[8 * s + 2 * j + 1]);
+                }
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const double2 cc = cur[j];
-                    const double d0 = __dsub_rn((double)xf[8 * s + 2 * j], cc.x);
-                    const double d1 = __dsub_rn((double)xf[8 * s + 2 * j + 1], cc.y);
+                    const double d0 = __dsub_rn(xcur[j].x, cc.x);
+                    const double d1 = __dsub_rn(xcur[j].y, cc.y);
                     sq[2 * j] = __dmul_rn(d0, d0);
                     sq[2 * j + 1] = __dmul_rn(d1, d1);
                 }
@@ -1965,11 +2072,13 @@ __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) 
 
 // ------------------------------------------------------------------ preparation
 // Centroids -> f16 hi/lo rows, -||c||^2/2, and the per-call bound maxima.
+// d < 128: the rows are zero-padded to 128 dims (C64p: the padded fp64 copy the
+// winner chains read; a zero dim adds (0 - 0)^2 = +0 to a non-negative chain).
 __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpad, _Float16* __restrict__ Ch,
                                     _Float16* __restrict__ Cl, float* __restrict__ cnh, unsigned int* __restrict__ cb,
                                     int metric, double* __restrict__ nbv, float* __restrict__ C32,
-                                    float* __restrict__ rn32) {
-    const int c = blockIdx.x;            // one wave per centroid row (d = 128: 2 dims per lane)
+                                    float* __restrict__ rn32, int d, double* __restrict__ C64p) {
+    const int c = blockIdx.x;            // one wave per centroid row (2 dims per lane)
     const int lane = threadIdx.x;
     double s2 = 0.0, s1 = 0.0;
     bool bad = false;
@@ -1977,7 +2086,7 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     if (metric == 1) {
         double q = 0.0;
         for (int j = lane; j < FU_D; j += 64) {
-            const double v = c < K ? C[(size_t)c * FU_D + j] : 0.0;
+            const double v = c < K && j < d ? C[(size_t)c * d + j] : 0.0;
             q = fma(v, v, q);
         }
         for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
@@ -1987,8 +2096,8 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
         scale = (q >= 1e-200 && q <= 1e200) ? 1.0 / sqrt(q) : 0.0;
         if (lane == 0 && c < K) {
             double b = 0.0;
-            for (int j = 0; j < FU_D; j++) {
-                const double cj = C[(size_t)c * FU_D + j];
+            for (int j = 0; j < d; j++) {
+                const double cj = C[(size_t)c * d + j];
                 b = __dadd_rn(b, __dmul_rn(cj, cj));
             }
             nbv[c] = b;
@@ -1997,7 +2106,8 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     double rr = 0.0, hh = 0.0;           // |c - ch|^2, |ch|^2 (the hi-only scores' bound)
     double r32 = 0.0;                    // |c - f32(c)|^2 (fast distances)
     for (int j = lane; j < FU_D; j += 64) {
-        const double v = c < K ? C[(size_t)c * FU_D + j] * scale : 0.0;
+        const double v = c < K && j < d ? C[(size_t)c * d + j] * scale : 0.0;
+        if (C64p) C64p[(size_t)c * FU_D + j] = v;
         const float f = (float)v;
         if (C32) {
             C32[(size_t)c * FU_D + j] = f;
@@ -2046,7 +2156,11 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
 }
 
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
-                      float* cbound, int metric, double* nbv, float* C32, float* rn32) {
+                      float* cbound, int metric, double* nbv, float* C32, float* rn32, int d, double* C64p) {
+    if (d < 1 || d > FU_D || (d != FU_D && metric == 0 && !C64p)) {
+        set_error("launch_fused_prep: d <= 128, and d < 128 needs the padded centroid copy");
+        return -1;
+    }
     if (metric == 1 && !nbv) {
         set_error("launch_fused_prep: cosine needs the norm array");
         return -1;
@@ -2057,7 +2171,7 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
     }
     (void)hipMemsetAsync(cbound, 0, 32, s);
     hipLaunchKernelGGL(fused_centroid_prep, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, Ch, Cl, cnh,
-                       reinterpret_cast<unsigned int*>(cbound), metric, nbv, C32, rn32);
+                       reinterpret_cast<unsigned int*>(cbound), metric, nbv, C32, rn32, d, C64p);
     return kstatus("fused_centroid_prep");
 }
 
@@ -2078,7 +2192,15 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.part = nullptr; a.t0 = 0; a.pass_first = 1; a.pass_last = 1;
     a.prof = nullptr;
     a.C32 = f.C32; a.rn32 = f.rn32;
-    a.fast_dist = f.fast_dist && f.metric == 0 && f.C32 && f.rn32 ? 1 : 0;
+    a.fast_dist = f.fast_dist && f.metric == 0 && f.rows != 2 && f.C32 && f.rn32 ? 1 : 0;
+    a.X64 = f.X64; a.d = f.rows == 0 ? FU_D : f.d;
+    a.xvec = f.rows == 1 ? (f.d % 4 == 0 && ((uintptr_t)f.X & 15) == 0)
+                         : (f.d % 2 == 0 && ((uintptr_t)f.X64 & 15) == 0);
+    if (f.rows != 0 && (hash || f.metric != 0 || !f.hi || f.Kpad > FH_KMAX || f.d < 1 || f.d > FU_D ||
+                        (f.rows == 1 ? !f.X : (f.rows != 2 || !f.X64)))) {
+        set_error("launch_fused: general rows run the hi-only euclidean form without hashing, K <= 512, d <= 128");
+        return -1;
+    }
 #ifdef LSHKM_PHASE_TIMING
     static unsigned long long* prof_d = nullptr;
     if (!prof_d) (void)hipMalloc(&prof_d, 64);
@@ -2097,7 +2219,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     } report{s, prof_d};
 #endif
     const char* force = getenv("LSHKM_FUSED_FORM");     // "chunked" forces the streaming form (tests)
-    const bool chunked = force && !strcmp(force, "chunked");
+    const bool chunked = force && !strcmp(force, "chunked") && f.rows == 0;
     const int npass = (f.Kpad + FP_KMAX - 1) / FP_KMAX;
     const bool multi_ok = npass == 1 || (f.part && f.part_bytes >= ((f.N + 31) / 32) * 64 * 16);
     // LIST refinement pass state: one slot per (segment, tile) of the list
@@ -2169,7 +2291,27 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             // the block-wide image swaps line the waves up and cost the MFMA/VALU
             // overlap between them, more than the second read of X costs; opt-in.
             const char* ti = getenv("LSHKM_HI_TWO_IMAGE");
-            const bool two_image = !cos && np1 == 2 && ti && !strcmp(ti, "1");
+            const bool two_image = !cos && np1 == 2 && ti && !strcmp(ti, "1") && f.rows == 0;
+            if (f.rows != 0) {
+                // general rows: one hi-only pass (Kpad <= 512), then the LIST form below
+                const size_t lh = (size_t)fh_lds_bytes(f.Kpad, false);
+                const char* gv = getenv("LSHKM_GATHER");
+                const bool gath = f.rows == 1 && f.Kpad <= FH_GATH_KMAX && !(gv && !strcmp(gv, "0"));
+#if defined(FH_WAVES_SET) && FH_WAVES_SET != 8
+                if (gath) { set_error("launch_fused: gather ring needs 8 waves"); return -1; }
+#else
+                if (gath)
+                    hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, true, 1>), grid, dim3(64 * 8),
+                                       (size_t)fh_gath_off(f.Kpad, false) + 8 * FH_GATH_WAVE, s, a);
+                else
+#endif
+                if (f.rows == 1)
+                    hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 1>), grid,
+                                       dim3(64 * fh_waves<false, false, 0>()), lh, s, a);
+                else
+                    hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 2>), grid,
+                                       dim3(64 * fh_waves<false, false, 0>()), lh, s, a);
+            }
             if (two_image) {
                 a.Ch = f.Ch; a.cnh = f.cnh; a.Kpad = f.Kpad;
                 a.t0 = 0; a.pass_first = 1; a.pass_last = 1;
@@ -2177,7 +2319,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 if (hash) hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 2>), grid, dim3(64 * fh_waves<true, false, 0>()), lh, s, a);
                 else hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 2>), grid, dim3(64 * fh_waves<false, false, 0>()), lh, s, a);
             }
-            for (int p = 0; p < (two_image ? 0 : np1); p++) {
+            for (int p = 0; p < (two_image || f.rows != 0 ? 0 : np1); p++) {
                 const int c0 = p * FH_KMAX;
                 a.Ch = f.Ch + (size_t)c0 * FU_D; a.cnh = f.cnh + c0;
                 a.Kpad = std::min(FH_KMAX, f.Kpad - c0);
@@ -2245,6 +2387,12 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 if (cos) {
                     if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 1, false, true>), grid, block, lds_nohash, s, r);
                     else hipLaunchKernelGGL((fused_persistent_kernel<false, 1, true, true>), grid, block, lds_nohash, s, r);
+                } else if (f.rows == 1) {
+                    if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 0, false, true, 1>), grid, block, lds_nohash, s, r);
+                    else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true, true, 1>), grid, block, lds_nohash, s, r);
+                } else if (f.rows == 2) {
+                    if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 0, false, true, 2>), grid, block, lds_nohash, s, r);
+                    else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true, true, 2>), grid, block, lds_nohash, s, r);
                 } else {
                     if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 0, false, true>), grid, block, lds_nohash, s, r);
                     else hipLaunchKernelGGL((fused_persistent_kernel<false, 0, true, true>), grid, block, lds_nohash, s, r);

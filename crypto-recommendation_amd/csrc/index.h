@@ -58,6 +58,7 @@ struct lshkm_ctx_s {
     // assignment workspace
     lshkm::Buf ws_c32, ws_cconst, ws_ambig, ws_counter, ws_src, ws_hfix, ws_ct, ws_seg, ws_tuples, ws_part;
     lshkm::Buf ws_cf32;     // fast distances: f32(c) [Kpad][128] + |c - f32(c)| [Kpad]
+    lshkm::Buf ws_c64p;     // general rows (d < 128): the zero-padded fp64 centroids [Kpad][128]
     lshkm::Buf ws_ambig2, ws_seg2;   // the hi-only form's refinement output list
     lshkm::Buf ws_seg3;              // hi-only cosine: segment counts of the declined winner distances
     // scatter / query / update workspace (see api_index.cpp for the slot map)

@@ -230,6 +230,13 @@ struct FusedLaunch {
     const float* C32 = nullptr;
     const float* rn32 = nullptr;
     int fast_dist = 0;
+    // general rows (euclidean Lloyd, no hashing, Kpad <= 512): rows = 1: fp32
+    // rows of d <= 128 dims (X); rows = 2: fp64 rows of d <= 128 dims (X64).
+    // C64 is then the prep's [Kpad][128] zero-padded copy; the hi-only pass's
+    // uncertified rows go straight to the caller's exact pass (no LIST form)
+    int rows = 0;
+    const double* X64 = nullptr;
+    int d = 128;
     // K > 256 on the persistent form: passes over 256-centroid slices carry each
     // lane's (best, runner-up, tile) in part[] (32 B per point)
     void* part = nullptr;
@@ -263,7 +270,7 @@ constexpr int64_t FUSED_LIST_SLACK = 32 + 1024 * 12 * 32;
 constexpr int FUSED_MAX_SEGS = 1024;
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
                       float* cbound, int metric = 0, double* nbv = nullptr, float* C32 = nullptr,
-                      float* rn32 = nullptr);
+                      float* rn32 = nullptr, int d = 128, double* C64p = nullptr);
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
 // Cosine winners listed by the persistent form (segment b: hfix[b * seg_rows ..],
 // count seg_counts[2b + 1]): soft-x87 distances.

@@ -1,0 +1,102 @@
+"""GPU parity of the general-row hi-only pass (fused_hi_kernel<..., ROWS = 1 / 2>).
+
+Euclidean Lloyd on fp64 rows (the reference's own `cust_vector<double>` user
+vectors, d = number of coins) and on fp32 rows of d < 128 dims runs the
+hi-only f16 MFMA scores over zero-padded dims, the winner's reference-order
+fp64 chain (fp64 rows: re-read from the row), and the exact pass for the rows
+the bound leaves. Checked against the CPU restatement (pinned by the
+reference's fixtures, tests/test_oracle_golden.py) and bit for bit against
+the independent f32-MFMA path (LSHKM_ASSIGN_PATH=f32). Reference:
+lib/clustering_phases/assignment.hpp:54-80, cust_vector.hpp:124-136.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from amd import lshkm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return lshkm.Context(0)
+
+
+def to_dev(ctx, a):
+    return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
+
+
+def rows_f64(seed, N, d):
+    # general doubles over six orders of magnitude, exact repeats, and edge rows:
+    # beyond the f16 range, sub-f32 magnitudes, inf, nan
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((N, d)) * np.exp(rng.uniform(-3, 3, size=(N, 1)))
+    X[::97] = X[1::97][: X[::97].shape[0]]
+    X[5] = 1e-310
+    X[6, 0] = 7e4
+    X[7, -1] = np.inf
+    X[8, d // 2] = np.nan
+    return X
+
+
+def check(ctx, X, Ch, sub_n=3000, seed=0):
+    """Lloyd on the default path vs the oracle (a subset) and vs the f32-MFMA path (all rows)."""
+    import os
+    N = X.shape[0]
+    Xd, Cd = to_dev(ctx, X), to_dev(ctx, Ch)
+    a, dist = lshkm.lloyd_assign(ctx, Xd, Cd, "euclidean")
+    a, dist = a.cpu().numpy(), dist.cpu().numpy()
+    os.environ["LSHKM_ASSIGN_PATH"] = "f32"
+    try:
+        a1, d1 = lshkm.lloyd_assign(ctx, Xd, Cd, "euclidean")
+    finally:
+        del os.environ["LSHKM_ASSIGN_PATH"]
+    assert np.array_equal(a, a1.cpu().numpy())
+    assert np.array_equal(dist.view(np.uint64), d1.cpu().numpy().view(np.uint64))
+    sub = np.r_[0:10, np.random.default_rng(seed).choice(N, sub_n, replace=False)]
+    oa, od = oracle.lloyd_assign(X[sub], Ch, "euclidean", None)
+    assert np.array_equal(a[sub], oa)
+    # glibc pow vs x*x: 1 ulp on general doubles; nan rows match as nan
+    ok = np.isfinite(od)
+    np.testing.assert_allclose(dist[sub][ok], od[ok], rtol=1e-14, atol=0)
+    assert np.array_equal(np.isnan(dist[sub]), np.isnan(od))
+
+
+@pytest.mark.parametrize("d,K", [(100, 256), (100, 512), (128, 256), (37, 64), (1, 8), (100, 1), (64, 300)])
+def test_f64_rows(ctx, d, K):
+    N = 50_003
+    X = rows_f64(1000 + d + K, N, d)
+    rng = np.random.default_rng(K)
+    Ch = X[rng.choice(np.arange(20, N), K, replace=False)].copy()
+    if K > 3:
+        Ch[3] = Ch[2]                                # an exact tie: the first index wins
+    check(ctx, X, Ch)
+
+
+@pytest.mark.parametrize("d,K", [(100, 256), (64, 512), (37, 100), (127, 256)])
+def test_f32_rows_short_d(ctx, d, K):
+    N = 40_001
+    rng = np.random.default_rng(d * 7 + K)
+    X = rng.standard_normal((N, d)).astype(np.float32)
+    X[3] = 0.0
+    X[4, 0] = 1e5                                    # beyond the f16 range: the exact pass
+    Ch = X[rng.choice(np.arange(10, N), K, replace=False)].astype(np.float64)
+    Ch[1] = Ch[0]
+    Ch[5] *= 1.0 + 1e-9                              # a general double centroid
+    check(ctx, X, Ch)
+
+
+def test_f64_rows_after_update(ctx):
+    # Lloyd -> k-means update -> Lloyd on fp64 user-vector-shaped rows (main.cpp:248-258):
+    # the second assignment runs against general fp64 means
+    N, d, K = 60_000, 100, 128
+    X = rows_f64(77, N, d)
+    X[5:9] = X[10:14]                                # no inf / nan: the means stay finite
+    Xd = to_dev(ctx, X)
+    rows = (np.arange(K) * (N // K)).astype(np.int32)
+    a, _ = lshkm.lloyd_assign(ctx, Xd, to_dev(ctx, X[rows]), "euclidean", rows)
+    Cn, _, _ = lshkm.kmeans_update(ctx, Xd, a, to_dev(ctx, X[rows]), "euclidean", 0.0)
+    check(ctx, X, Cn.cpu().numpy(), sub_n=2000, seed=5)
