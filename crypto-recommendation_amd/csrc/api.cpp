@@ -561,7 +561,10 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         const bool fast = !cosine && rows_kind != 2 && fast_dist_on();
         float* C32 = nullptr;
         float* rn32 = nullptr;
-        if (fast) {
+        // the f32 image also serves the K <= 256 gather when every centroid value
+        // is an f32 (dataset rows: the first Lloyd iteration), exact as doubles
+        const char* g32e = getenv("LSHKM_GATHER32");         // "0": the fp64 winner rows always
+        if (fast || (!cosine && rows_kind != 2 && Kpad <= 256 && !(g32e && !strcmp(g32e, "0")))) {
             if ((rc = ctx->ws_cf32.reserve((size_t)Kpad * 128 * 4 + (size_t)Kpad * 4))) return rc;
             C32 = (float*)ctx->ws_cf32.p;
             rn32 = C32 + (size_t)Kpad * 128;

@@ -60,7 +60,8 @@ struct FusedArgs {
     const _Float16* Cl;
     const float* cnh;        // [Kpad] -||c||^2 / 2 (f32), -inf for padding rows
     const float* cbound;     // [0] = ec (times |x|), [1] = eb (constant), [2] = range flag (bits), [3] = max |c|,
-                             // [4] = max |c - ch|, [5] = max |ch|, [6] = max |c|^2 / 2 (all rounded up)
+                             // [4] = max |c - ch|, [5] = max |ch|, [6] = max |c|^2 / 2 (all rounded up),
+                             // [7] = nonzero if some centroid value is not an f32 (bits)
     const double* C64;       // [K][128] exact centroids
     int Kpad;
     // hash family (HASH only)
@@ -122,6 +123,10 @@ struct FusedArgs {
 #define PT_DECL unsigned long long pt_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long pt_t = __builtin_amdgcn_s_memtime();
 #define PT_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pt_acc[i] += t_ - pt_t; pt_t = t_; }
 #define PT_FLUSH if (lane == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd(a.prof + i_, pt_acc[i_]);
+#elif defined(LSHKM_ISA_MARK)       // assembly listings: region comments (tools/isa_regions.py)
+#define PT_DECL
+#define PT_MARK(i) asm volatile(";PTMARK " #i);
+#define PT_FLUSH
 #else
 #define PT_DECL
 #define PT_MARK(i)
@@ -1621,22 +1626,43 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #endif
         // GATH: piece u of a step holds points 8u..8u+7, lane L the 16-B chunk
         // (L & 7) ^ swz(p) of point p = 8u + (L >> 3) (swz(p) = (p >> 1) & 7: the
-        // lanes of each ds_read_b128 group hit 16 distinct 4-bank groups)
-        const double* gsrc[4];
+        // lanes of each ds_read_b128 group hit 16 distinct 4-bank groups).
+        // g32 (every centroid value is an f32, e.g. dataset rows: the prep's
+        // cbound[7] == 0): the f32 image C32 instead, exact as doubles -- half the
+        // bytes and two pieces per step: piece u holds points 16u..16u+15, lane L
+        // the 16-B chunk (L & 3) ^ swz32(p) of point p = 16u + (L >> 2), swz32(p) =
+        // (p >> 2) & 3 (the 16 lanes of a ds_read_b128 group on distinct banks).
+        const char* gsrc[4];
         uint32_t gbase = 0;
+        const bool g32 = GATH && a.C32 != nullptr && __float_as_uint(a.cbound[7]) == 0u;
+        const int gstep = g32 ? 64 : 128;                // bytes of one 16-dim step of a row
         if (GATH && !a.fast_dist) {
             gbase = (uint32_t)__builtin_amdgcn_readfirstlane(
                 (int)((uint32_t)(uintptr_t)(smem + fh_gath_off(Kpad, HASH)) + (uint32_t)wave * FH_GATH_WAVE));
+            if (g32) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int p = 8 * u + (lane >> 3);
-                const int Ip = __shfl(I1, p);
-                gsrc[u] = a.C64 + (size_t)Ip * FU_D + 2 * ((lane & 7) ^ ((p >> 1) & 7));
+                for (int u = 0; u < 2; u++) {
+                    const int p = 16 * u + (lane >> 2);
+                    const int Ip = __shfl(I1, p);
+                    gsrc[u] = reinterpret_cast<const char*>(a.C32 + (size_t)Ip * FU_D + 4 * ((lane & 3) ^ ((p >> 2) & 3)));
+                }
+                gsrc[2] = gsrc[3] = gsrc[0];
+#pragma unroll
+                for (int s0 = 0; s0 < 2; s0++)
+#pragma unroll
+                    for (int u = 0; u < 2; u++) glds16(gsrc[u] + gstep * s0, gbase + s0 * FH_GATH_STEP + u * 1024);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int p = 8 * u + (lane >> 3);
+                    const int Ip = __shfl(I1, p);
+                    gsrc[u] = reinterpret_cast<const char*>(a.C64 + (size_t)Ip * FU_D + 2 * ((lane & 7) ^ ((p >> 1) & 7)));
+                }
+#pragma unroll
+                for (int s0 = 0; s0 < 2; s0++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) glds16(gsrc[u] + gstep * s0, gbase + s0 * FH_GATH_STEP + u * 1024);
             }
-#pragma unroll
-            for (int s0 = 0; s0 < 2; s0++)
-#pragma unroll
-                for (int u = 0; u < 4; u++) glds16(gsrc[u] + 16 * s0, gbase + s0 * FH_GATH_STEP + u * 1024);
         }
         // fp64 rows: the chain's x values re-read (mostly L2) four 16-dim steps
         // ahead (one step ahead left the chain waiting ~8 round trips per tile)
@@ -1741,14 +1767,28 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             // overlaps the previous step's chain), the ring slot is refilled two
             // steps ahead as soon as it is read
             double2 gnext[4];
+            float4 gnext32[2];                // g32: raw f32 chunks, widened when used
             auto gread = [&](int st) {
                 const char* ring = smem + fh_gath_off(Kpad, HASH) + wave * FH_GATH_WAVE + (st & 1) * FH_GATH_STEP;
+                if (g32) {
 #pragma unroll
-                for (int j = 0; j < 4; j++)
-                    gnext[j] = *reinterpret_cast<const double2*>(ring + col * 128 + 16 * ((4 * h + j) ^ ((col >> 1) & 7)));
+                    for (int j = 0; j < 2; j++)
+                        gnext32[j] = *reinterpret_cast<const float4*>(ring + (col >> 4) * 1024 + (col & 15) * 64 +
+                                                                      16 * ((2 * h + j) ^ ((col >> 2) & 3)));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        gnext[j] = *reinterpret_cast<const double2*>(ring + col * 128 + 16 * ((4 * h + j) ^ ((col >> 1) & 7)));
+                }
+            };
+            // vmcnt(n): all but the wave's n youngest vector-memory operations done
+            // (one step's pieces: 2 for g32, else 4)
+            auto wait_step = [&]() {
+                if (g32) __builtin_amdgcn_s_waitcnt(0x0F72);               // vmcnt(2)
+                else __builtin_amdgcn_s_waitcnt(0x0F74);                   // vmcnt(4)
             };
             if constexpr (GATH) {
-                __builtin_amdgcn_s_waitcnt(0x0F74);                        // vmcnt(4): step 0 landed
+                wait_step();                                               // step 0 landed
                 asm volatile("" ::: "memory");
                 gread(0);
             }
@@ -1757,17 +1797,31 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                 double sq[8];
                 double2 cur[4];
                 if constexpr (GATH) {
+                    if (g32) {
 #pragma unroll
-                    for (int j = 0; j < 4; j++) cur[j] = gnext[j];
+                        for (int j = 0; j < 2; j++) {
+                            cur[2 * j] = make_double2((double)gnext32[j].x, (double)gnext32[j].y);
+                            cur[2 * j + 1] = make_double2((double)gnext32[j].z, (double)gnext32[j].w);
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) cur[j] = gnext[j];
+                    }
                     if (s + 2 < 8) {
                         __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): slot s & 1 is read
                         asm volatile("" ::: "memory");
+                        if (g32) {
 #pragma unroll
-                        for (int u = 0; u < 4; u++)
-                            glds16(gsrc[u] + 16 * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
+                            for (int u = 0; u < 2; u++)
+                                glds16(gsrc[u] + gstep * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
+                        } else {
+#pragma unroll
+                            for (int u = 0; u < 4; u++)
+                                glds16(gsrc[u] + gstep * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
+                        }
                     }
                     if (s + 1 < 8) {
-                        if (s + 2 < 8) __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): step s + 1 landed
+                        if (s + 2 < 8) wait_step();                        // step s + 1 landed
                         else __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
                         asm volatile("" ::: "memory");
                         gread(s + 1);
@@ -2103,12 +2157,14 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
             nbv[c] = b;
         }
     }
+    bool not32 = false;                  // some value of the row is not an f32 (cbound[7])
     double rr = 0.0, hh = 0.0;           // |c - ch|^2, |ch|^2 (the hi-only scores' bound)
     double r32 = 0.0;                    // |c - f32(c)|^2 (fast distances)
     for (int j = lane; j < FU_D; j += 64) {
         const double v = c < K && j < d ? C[(size_t)c * d + j] * scale : 0.0;
         if (C64p) C64p[(size_t)c * FU_D + j] = v;
         const float f = (float)v;
+        not32 |= c < K && (double)f != v;
         if (C32) {
             C32[(size_t)c * FU_D + j] = f;
             const double e = v - (double)f;       // exact (or inf / nan: never certified)
@@ -2134,7 +2190,9 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     // sum of 128 non-negative fp64 values: <= 2^-46 relative rounding; rounded up
     if (rn32 && lane == 0) rn32[c] = r32 == 0.0 ? 0.f : (float)(sqrt(r32) * (1.0 + 0x1p-40)) * (1.f + 0x1p-22f);
     const unsigned long long anybad = __ballot(bad);
+    const unsigned long long any_not32 = __ballot(not32);
     if (lane != 0) return;
+    if (any_not32) atomicOr(cb + 7, 1u);
     // padding rows: a finite score far below any real one (|x.c| < 2^38 under the
     // range guard), so the packed-index trick never meets an inf/nan
     if (c >= K) { cnh[c] = -0x1p100f; return; }
