@@ -135,10 +135,18 @@ int lshkm_ctx_enable_timing(lshkm_ctx ctx, int on) {
     return 0;
 }
 
+// The fused pass: from before the prep to the later of the main stream's last
+// fused launch and the side stream's hash fix-up.
 int lshkm_last_kernel_ms(lshkm_ctx ctx, float* ms) {
     LSHKM_CHECK(ctx && ms && ctx->tev[1], LSHKM_ERR_STATE, "timing not enabled");
     LSHKM_HIP(hipEventSynchronize(ctx->tev[1]));
     LSHKM_HIP(hipEventElapsedTime(ms, ctx->tev[0], ctx->tev[1]));
+    if (ctx->tev_side) {
+        float m2 = 0.f;
+        LSHKM_HIP(hipEventSynchronize(ctx->tev[2]));
+        LSHKM_HIP(hipEventElapsedTime(&m2, ctx->tev[0], ctx->tev[2]));
+        *ms = std::max(*ms, m2);
+    }
     return 0;
 }
 
@@ -612,15 +620,39 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             f.tuples = cosine ? nullptr : tuples ? tuples : (int32_t*)ctx->ws_tuples.p;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = cnt + 1;
         }
-        if (fuse_hash && ctx->side_init() == 0) { f.side = ctx->side_stream; f.fork = ctx->fork_ev; f.join = ctx->join_ev; }
+        if (fuse_hash && ctx->side_init() == 0) {
+            f.side = ctx->side_stream; f.fork = ctx->fork_ev; f.join = ctx->join_ev;
+            const char* dj = getenv("LSHKM_DEFER_JOIN");     // "0": join inside launch_fused (A/B)
+            f.defer_join = !cosine && !(dj && !strcmp(dj, "0"));   // euclidean: the exact pass also overlaps the fix-up
+            if (ctx->timing) f.side_timing = ctx->tev[2];
+        }
+        ctx->tev_side = f.side_timing != nullptr;
+        // the side stream's hash fix-up writes only tuples / phi / bucket: joined
+        // before this call's last launch, and on every error path after the fork
+        struct SideJoin {
+            lshkm_ctx c;
+            bool pending = false;
+            ~SideJoin() { if (pending) (void)hipStreamSynchronize(c->side_stream); }
+        } sj{ctx};
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
-        if ((rc = launch_fused(s, fuse_hash, f))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        rc = launch_fused(s, fuse_hash, f);
+        sj.pending = f.join_pending;
+        if (rc) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.final_counts : nullptr,
                                f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if (hi && (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_REFINED, cnt + 2))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if (fuse_hash && (rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_HASH_FIX, cnt + 1))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_ASSIGN_AMBIG, cnt))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if (sj.pending) {
+            LSHKM_HIP(hipStreamWaitEvent(s, f.join, 0));
+            sj.pending = false;
+        }
+        {
+            int di[3], n = 0;
+            const unsigned long long* sp[3];
+            if (hi) { di[n] = STAT_REFINED; sp[n++] = cnt + 2; }
+            if (fuse_hash) { di[n] = STAT_HASH_FIX; sp[n++] = cnt + 1; }
+            di[n] = STAT_ASSIGN_AMBIG; sp[n++] = cnt;
+            if ((rc = launch_add_counters(s, (unsigned long long*)ctx->stats.p, n, di, sp))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        }
         if (cosine) {
             for (int li = 0; li < f.ncos_lists; li++)
                 if ((rc = launch_cos_fix_seg(s, X.f(), C, f.cos_list[li], f.cos_counts[li], f.seg_rows, f.nseg, assign,

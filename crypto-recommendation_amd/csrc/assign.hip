@@ -983,4 +983,28 @@ int launch_add_counter(hipStream_t s, unsigned long long* dst, const unsigned lo
     return kstatus("assign.hip");
 }
 
+// stats[dst_idx[i]] += src[i] for i < n (n <= 8): the per-call statistics in one launch
+struct CounterAdds {
+    int n;
+    int dst[8];
+    const unsigned long long* src[8];
+};
+__global__ void add_counters_kernel(unsigned long long* stats, CounterAdds c) {
+    if ((int)threadIdx.x < c.n) atomicAdd(stats + c.dst[threadIdx.x], *c.src[threadIdx.x]);
+}
+
+int launch_add_counters(hipStream_t s, unsigned long long* stats, int n, const int* dst_idx,
+                        const unsigned long long* const* src) {
+    if (n <= 0) return 0;
+    if (n > 8) {
+        set_error("launch_add_counters: at most 8 counters");
+        return -1;
+    }
+    CounterAdds c;
+    c.n = n;
+    for (int i = 0; i < n; i++) { c.dst[i] = dst_idx[i]; c.src[i] = src[i]; }
+    hipLaunchKernelGGL(add_counters_kernel, dim3(1), dim3(64), 0, s, stats, c);
+    return kstatus("assign.hip");
+}
+
 }  // namespace lshkm

@@ -2426,6 +2426,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             }
             if (hash && cos) hipLaunchKernelGGL(hash_fixup_kernel<true>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, hs, a);
             else if (hash) hipLaunchKernelGGL(hash_fixup_kernel<false>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, hs, a);
+            if (side && f.side_timing && hipEventRecord(f.side_timing, f.side) != hipSuccess) {
+                (void)hipStreamSynchronize(f.side);
+                return kstatus("launch_fused (timing)");
+            }
             if (side && hipEventRecord(f.join, f.side) != hipSuccess) {
                 // never return with the fix-up unordered against later work on s
                 (void)hipStreamSynchronize(f.side);
@@ -2463,7 +2467,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 f.cos_list[0] = f.cfix; f.cos_counts[0] = f.cfix_counts;
                 f.cos_list[1] = f.hfix2; f.cos_counts[1] = f.seg_counts2;
             }
-            if (side && hipStreamWaitEvent(s, f.join, 0) != hipSuccess) {
+            if (side && f.defer_join) {
+                f.join_pending = true;          // the caller joins (after its exact pass)
+            } else if (side && hipStreamWaitEvent(s, f.join, 0) != hipSuccess) {
                 (void)hipStreamSynchronize(f.side);
                 return kstatus("launch_fused (join)");
             }

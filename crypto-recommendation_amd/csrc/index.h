@@ -72,7 +72,8 @@ struct lshkm_ctx_s {
     uint64_t ws_epoch = 0;       // bumped by every user of the ws[] slots (api_index.cpp reserve)
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
     bool timing = false;
-    hipEvent_t tev[2] = {nullptr, nullptr};
+    hipEvent_t tev[3] = {nullptr, nullptr, nullptr};   // [2]: the side stream's end (hash fix-up)
+    bool tev_side = false;       // the last timed call recorded tev[2]
     // a side stream for work independent of the main stream's next kernels
     // (the hash fix-up beside the LIST refinement), forked / joined by events
     hipStream_t side_stream = nullptr;

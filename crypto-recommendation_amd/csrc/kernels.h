@@ -108,6 +108,9 @@ int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_
                            double* dist);
 
 int launch_add_counter(hipStream_t s, unsigned long long* dst, const unsigned long long* src);
+// stats[dst_idx[i]] += *src[i], i < n <= 8, in one launch
+int launch_add_counters(hipStream_t s, unsigned long long* stats, int n, const int* dst_idx,
+                        const unsigned long long* const* src);
 
 // Stable bucket scatter (scatter.hip).
 size_t sort_scratch_bytes(int64_t N, int64_t range, int T = 1);
@@ -181,9 +184,14 @@ int launch_rc_top_n(hipStream_t s, const double* X, const double* x_mean, int d,
 // Fused hash + assign on split-f16 MFMA (fused.hip), d = 128.
 struct FusedLaunch {
     // optional side stream (+ fork / join events): the hash fix-up runs there
-    // beside the LIST refinement; joined before launch_fused returns
+    // beside the LIST refinement; joined before launch_fused returns, or, with
+    // defer_join, left to the caller (out: join_pending = the main stream must
+    // still wait on `join` -- the caller's exact pass then also overlaps it)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    bool defer_join = false;
+    bool join_pending = false;
+    hipEvent_t side_timing = nullptr;            // recorded on the side stream after the fix-up (timing)
     const float* X = nullptr;
     int64_t N = 0;
     const _Float16* Ch = nullptr;
