@@ -360,9 +360,16 @@ static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex
     unsigned int ncoins = 0;
     if ((rc = cube_unseen_impl(cube, h, N, &ncoins))) return rc;
     if (ncoins > 0) {
-        if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(ncoins, N * k)))) return rc;
-        if ((rc = stable_sort_by_key(s, slot<int32_t>(ctx, WS_SIZES), 1, slot<int32_t>(ctx, WS_COFF), ncoins, N * k,
-                                     slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT), ctx->ws[WS_SORT].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        // the draw order: keys row * k + f are distinct, so a few thousand sort in
+        // one workgroup (a multi-pass radix sort is a dozen launches)
+        if (ncoins <= 8192) {
+            if ((rc = sort_pairs_small(s, slot<int32_t>(ctx, WS_SIZES), slot<int32_t>(ctx, WS_COFF), ncoins,
+                                       slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT)))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        } else {
+            if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(ncoins, N * k)))) return rc;
+            if ((rc = stable_sort_by_key(s, slot<int32_t>(ctx, WS_SIZES), 1, slot<int32_t>(ctx, WS_COFF), ncoins, N * k,
+                                         slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT), ctx->ws[WS_SORT].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        }
         if ((rc = launch_coin_draw(s, slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>(), cube->hmin, cube->hspan,
                                    cube->memo.as<int32_t>(), cube->rng_d.as<uint32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     }

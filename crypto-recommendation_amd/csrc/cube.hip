@@ -58,6 +58,28 @@ __global__ void coin_first_kernel(const int32_t* __restrict__ h, int64_t N, int 
 // global entries).
 constexpr int CF_LDS_MAX = 12288;
 constexpr int32_t CF_SEEN = -1;
+constexpr int CF_KMAX = 32;          // functions per row held in registers (k <= 32)
+
+// This thread's row of k h values (k even: 8-byte loads, the row starts 8-B aligned).
+__device__ inline void cf_load_row(const int32_t* __restrict__ h, int64_t row, int k, int32_t (&v)[CF_KMAX]) {
+    const int32_t* p = h + row * k;
+    if ((k & 1) == 0) {
+#pragma unroll
+        for (int f = 0; f < CF_KMAX; f += 2)
+            if (f < k) {
+                const int2 w = *reinterpret_cast<const int2*>(p + f);
+                v[f] = w.x;
+                v[f + 1] = w.y;
+            }
+    } else {
+#pragma unroll
+        for (int f = 0; f < CF_KMAX; f++)
+            if (f < k) v[f] = p[f];
+    }
+}
+
+// One row per thread: its k values in registers (independent loads, a wave
+// reads 64 consecutive rows), then a read-first LDS min per (f, h).
 __global__ __launch_bounds__(256) void coin_first_lds_kernel(const int32_t* __restrict__ h, int64_t N, int k,
                                                              int32_t hmin, int32_t hspan, int64_t rows_per_block,
                                                              const int32_t* __restrict__ memo,
@@ -68,17 +90,16 @@ __global__ __launch_bounds__(256) void coin_first_lds_kernel(const int32_t* __re
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min(N, r0 + rows_per_block);
-    // (row, f) of element e, advanced by 256 elements per step without a division
-    const int dq = 256 / k, dr = 256 - dq * k;
-    int64_t row = r0 + (int64_t)(threadIdx.x / k);
-    int f = (int)threadIdx.x - (int)(threadIdx.x / k) * k;
-    for (int64_t e = r0 * k + threadIdx.x; e < r1 * k; e += 256) {
-        const int off = f * hspan + (h[e] - hmin);
-        const int32_t cur = lmin[off];
-        if (cur != CF_SEEN && cur > (int32_t)row) atomicMin(lmin + off, (int32_t)row);
-        f += dr;
-        row += dq;
-        if (f >= k) { f -= k; row++; }
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += 256) {
+        int32_t v[CF_KMAX];
+        cf_load_row(h, row, k, v);
+#pragma unroll
+        for (int f = 0; f < CF_KMAX; f++) {
+            if (f >= k) break;
+            const int off = f * hspan + (v[f] - hmin);
+            const int32_t cur = lmin[off];
+            if (cur != CF_SEEN && cur > (int32_t)row) atomicMin(lmin + off, (int32_t)row);
+        }
     }
     __syncthreads();
     for (int e = threadIdx.x; e < total; e += 256) {
@@ -183,27 +204,26 @@ __global__ void coin_vertex_kernel(const int32_t* __restrict__ h, int64_t N, int
     }
 }
 
-// Memo windows of at most CF_LDS_MAX entries: the memo and a 256-row block of
-// h (coalesced) in LDS, then one row per thread.
+// Memo windows of at most CF_LDS_MAX entries: the memo in LDS, one row per
+// thread with its k values loaded at once.
 __global__ __launch_bounds__(256) void coin_vertex_lds_kernel(const int32_t* __restrict__ h, int64_t N, int k,
                                                               int32_t hmin, int32_t hspan,
                                                               const int32_t* __restrict__ memo,
                                                               int32_t* __restrict__ vertex) {
-    extern __shared__ int32_t lds[];
-    int32_t* lmemo = lds;                       // [k * hspan]
-    int32_t* lh = lds + k * hspan;              // [256 * k]
+    extern __shared__ int32_t lmemo[];          // [k * hspan]
     const int total = k * hspan;
     for (int e = threadIdx.x; e < total; e += 256) lmemo[e] = memo[e];
-    for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < N; r0 += (int64_t)gridDim.x * 256) {
-        const int nr = (int)min((int64_t)256, N - r0);
-        __syncthreads();
-        for (int e = threadIdx.x; e < nr * k; e += 256) lh[e] = h[r0 * k + e];
-        __syncthreads();
-        if ((int)threadIdx.x < nr) {
-            int v = 0;
-            for (int f = 0; f < k; f++) v = (v << 1) + lmemo[f * hspan + (lh[threadIdx.x * k + f] - hmin)];
-            vertex[r0 + threadIdx.x] = v;
+    __syncthreads();
+    for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < N; row += (int64_t)gridDim.x * 256) {
+        int32_t v[CF_KMAX];
+        cf_load_row(h, row, k, v);
+        int x = 0;
+#pragma unroll
+        for (int f = 0; f < CF_KMAX; f++) {
+            if (f >= k) break;
+            x = (x << 1) + lmemo[f * hspan + (v[f] - hmin)];
         }
+        vertex[row] = x;
     }
 }
 
@@ -211,7 +231,7 @@ int launch_coin_first(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t
                       const int32_t* memo, int32_t* first_row) {
     const int64_t n = N * k;
     const int64_t total = (int64_t)k * hspan;
-    if (total <= CF_LDS_MAX) {
+    if (total <= CF_LDS_MAX && k <= CF_KMAX) {
         static int cus[64] = {0};
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return kstatus("hipGetDevice");
@@ -246,8 +266,8 @@ int launch_coin_draw(hipStream_t s, const int32_t* sorted_vals, const unsigned i
 
 int launch_coin_vertex(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
                        const int32_t* memo, int32_t* vertex) {
-    if ((int64_t)k * hspan <= CF_LDS_MAX) {
-        const size_t lds = ((size_t)k * hspan + 256 * (size_t)k) * 4;
+    if ((int64_t)k * hspan <= CF_LDS_MAX && k <= CF_KMAX) {
+        const size_t lds = (size_t)k * hspan * 4;
         hipLaunchKernelGGL(coin_vertex_lds_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 2048)), dim3(256),
                            lds, s, h, N, k, hmin, hspan, memo, vertex);
         return kstatus("cube.hip");

@@ -197,6 +197,55 @@ __global__ void rs_copy(const int32_t* __restrict__ keys, int64_t kstride, const
     }
 }
 
+// Small sorts (n <= SP_MAX distinct int32 keys, e.g. the few hundred unseen
+// coins of a cube build): one workgroup, a bitonic network over the keys padded
+// to a power of two in LDS -- one launch instead of a multi-pass radix sort's
+// dozen. Keys must be distinct (the order of equal keys is not kept).
+constexpr int SP_MAX = 8192;
+__global__ __launch_bounds__(1024) void sort_pairs_small_kernel(const int32_t* __restrict__ keys,
+                                                                const int32_t* __restrict__ vals, int n, int P,
+                                                                int32_t* __restrict__ keys_out,
+                                                                int32_t* __restrict__ vals_out) {
+    __shared__ int32_t sk[SP_MAX], sv[SP_MAX];
+    for (int i = threadIdx.x; i < P; i += 1024) {
+        sk[i] = i < n ? keys[i] : 0x7FFFFFFF;
+        sv[i] = i < n ? vals[i] : 0;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += 1024) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const int32_t a = sk[i], b = sk[l];
+                    const bool up = (i & k) == 0;
+                    if (up ? a > b : a < b) {
+                        sk[i] = b; sk[l] = a;
+                        const int32_t t = sv[i]; sv[i] = sv[l]; sv[l] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        keys_out[i] = sk[i];
+        vals_out[i] = sv[i];
+    }
+}
+
+int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, int64_t n, int32_t* keys_out,
+                     int32_t* vals_out) {
+    if (n <= 0) return 0;
+    if (n > SP_MAX) {
+        set_error("sort_pairs_small: too many keys");
+        return -1;
+    }
+    int P = 1;
+    while (P < n) P <<= 1;
+    hipLaunchKernelGGL(sort_pairs_small_kernel, dim3(1), dim3(1024), 0, s, keys, vals, (int)n, P, keys_out, vals_out);
+    return kstatus("scatter.hip");
+}
+
 // row_ptr[b] = first position of key >= b in the sorted keys; row_ptr[nb] = N.
 __global__ void csr_bounds(const int32_t* __restrict__ skeys, int64_t N, int64_t nb, int64_t* __restrict__ row_ptr) {
     skeys += blockIdx.y * N;
