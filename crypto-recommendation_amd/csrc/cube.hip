@@ -30,7 +30,15 @@ __global__ void h_minmax_kernel(const int32_t* __restrict__ h, int64_t n, int32_
         lo = min(lo, __shfl_xor(lo, off));
         hi = max(hi, __shfl_xor(hi, off));
     }
-    if ((threadIdx.x & 63) == 0) { atomicMin(mm, lo); atomicMax(mm + 1, hi); }
+    // one atomic pair per block (contended single-word atomics serialise)
+    __shared__ int32_t wlo[4], whi[4];
+    if ((threadIdx.x & 63) == 0) { wlo[threadIdx.x >> 6] = lo; whi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) { lo = min(lo, wlo[w]); hi = max(hi, whi[w]); }
+        atomicMin(mm, lo);
+        atomicMax(mm + 1, hi);
+    }
 }
 
 int launch_h_minmax(hipStream_t s, const int32_t* h, int64_t n, int32_t* mm_dev) {

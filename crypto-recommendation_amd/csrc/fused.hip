@@ -2126,14 +2126,15 @@ __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) 
 
 // ------------------------------------------------------------------ preparation
 // Centroids -> f16 hi/lo rows, -||c||^2/2, and the per-call bound maxima.
+constexpr int FP_PREP_WAVES = 8;     // centroids per prep block (Kpad % 64 == 0)
 // d < 128: the rows are zero-padded to 128 dims (C64p: the padded fp64 copy the
 // winner chains read; a zero dim adds (0 - 0)^2 = +0 to a non-negative chain).
 __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpad, _Float16* __restrict__ Ch,
                                     _Float16* __restrict__ Cl, float* __restrict__ cnh, unsigned int* __restrict__ cb,
                                     int metric, double* __restrict__ nbv, float* __restrict__ C32,
                                     float* __restrict__ rn32, int d, double* __restrict__ C64p) {
-    const int c = blockIdx.x;            // one wave per centroid row (2 dims per lane)
-    const int lane = threadIdx.x;
+    const int c = blockIdx.x * FP_PREP_WAVES + (threadIdx.x >> 6);   // one wave per centroid row
+    const int lane = threadIdx.x & 63;
     double s2 = 0.0, s1 = 0.0;
     bool bad = false;
     double scale = 1.0;                  // cosine: the row is normalised (score x.c/|c|)
@@ -2191,26 +2192,45 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     if (rn32 && lane == 0) rn32[c] = r32 == 0.0 ? 0.f : (float)(sqrt(r32) * (1.0 + 0x1p-40)) * (1.f + 0x1p-22f);
     const unsigned long long anybad = __ballot(bad);
     const unsigned long long any_not32 = __ballot(not32);
-    if (lane != 0) return;
-    if (any_not32) atomicOr(cb + 7, 1u);
-    // padding rows: a finite score far below any real one (|x.c| < 2^38 under the
-    // range guard), so the packed-index trick never meets an inf/nan
-    if (c >= K) { cnh[c] = -0x1p100f; return; }
-    cnh[c] = metric == 1 ? 0.f : (float)(-0.5 * s2);
-    const double up = 1.0 + 0x1p-18;
-    const double nc = sqrt(s2) * (1.0 + 0x1p-30);
-    // |t~ - t| <= (A1 + 2^-22)|x||c| + A2(|x|_1 + |c|_1) + 2^-23 |c|^2 + 2^-41 (|x|^2 + |c|^2)
-    // (cosine: no |c|^2 term in t, c = the normalised row)
-    const float ec = (float)((FU_A1 + 0x1p-22) * nc * up);
-    const float eb = (float)((FU_A2 * s1 * (1.0 + 0x1p-20) + (metric == 1 ? 0.0 : 0x1p-23 * s2) + 0x1p-41 * s2) * up);
-    atomicMax(cb + 0, __float_as_uint(ec));     // positive floats order like their bits
-    atomicMax(cb + 1, __float_as_uint(eb));
-    atomicMax(cb + 3, __float_as_uint((float)(nc * up)));   // max |c|, rounded up
-    // hi-only scores (fused_hi_kernel): max |c - ch|, max |ch|, max |cn|, rounded up
-    atomicMax(cb + 4, __float_as_uint((float)(sqrt(rr) * (1.0 + 0x1p-30) * up)));
-    atomicMax(cb + 5, __float_as_uint((float)(sqrt(hh) * (1.0 + 0x1p-30) * up)));
-    atomicMax(cb + 6, __float_as_uint((float)(metric == 1 ? 0.0 : 0.5 * s2 * up)));
-    if (anybad) atomicOr(cb + 2, 1u);
+    // per wave (centroid) the bound maxima, then one atomic per word per block:
+    // single-word atomics from every centroid serialise (~12 ns each)
+    __shared__ unsigned int wmax[FP_PREP_WAVES][8];
+    if (lane == 0) {
+        unsigned int m[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        m[7] = any_not32 ? 1u : 0u;
+        if (c >= K) {
+            // padding rows: a finite score far below any real one (|x.c| < 2^38 under
+            // the range guard), so the packed-index trick never meets an inf/nan
+            cnh[c] = -0x1p100f;
+        } else {
+            cnh[c] = metric == 1 ? 0.f : (float)(-0.5 * s2);
+            const double up = 1.0 + 0x1p-18;
+            const double nc = sqrt(s2) * (1.0 + 0x1p-30);
+            // |t~ - t| <= (A1 + 2^-22)|x||c| + A2(|x|_1 + |c|_1) + 2^-23 |c|^2 + 2^-41 (|x|^2 + |c|^2)
+            // (cosine: no |c|^2 term in t, c = the normalised row)
+            m[0] = __float_as_uint((float)((FU_A1 + 0x1p-22) * nc * up));     // positive floats order like their bits
+            m[1] = __float_as_uint((float)((FU_A2 * s1 * (1.0 + 0x1p-20) + (metric == 1 ? 0.0 : 0x1p-23 * s2) +
+                                            0x1p-41 * s2) * up));
+            m[2] = anybad ? 1u : 0u;
+            m[3] = __float_as_uint((float)(nc * up));                        // max |c|, rounded up
+            // hi-only scores (fused_hi_kernel): max |c - ch|, max |ch|, max |cn|, rounded up
+            m[4] = __float_as_uint((float)(sqrt(rr) * (1.0 + 0x1p-30) * up));
+            m[5] = __float_as_uint((float)(sqrt(hh) * (1.0 + 0x1p-30) * up));
+            m[6] = __float_as_uint((float)(metric == 1 ? 0.0 : 0.5 * s2 * up));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) wmax[threadIdx.x >> 6][i] = m[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        const int i = threadIdx.x;
+        unsigned int v = 0u;
+        for (int w = 0; w < FP_PREP_WAVES; w++) v = i == 2 || i == 7 ? (v | wmax[w][i]) : max(v, wmax[w][i]);
+        if (v) {
+            if (i == 2 || i == 7) atomicOr(cb + i, v);
+            else atomicMax(cb + i, v);
+        }
+    }
 }
 
 int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16* Ch, _Float16* Cl, float* cnh,
@@ -2228,7 +2248,11 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
         return -1;
     }
     (void)hipMemsetAsync(cbound, 0, 32, s);
-    hipLaunchKernelGGL(fused_centroid_prep, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, Ch, Cl, cnh,
+    if (Kpad % FP_PREP_WAVES) {
+        set_error("launch_fused_prep: Kpad must be a multiple of 8");
+        return -1;
+    }
+    hipLaunchKernelGGL(fused_centroid_prep, dim3((unsigned)(Kpad / FP_PREP_WAVES)), dim3(64 * FP_PREP_WAVES), 0, s, C, K, Kpad, Ch, Cl, cnh,
                        reinterpret_cast<unsigned int*>(cbound), metric, nbv, C32, rn32, d, C64p);
     return kstatus("fused_centroid_prep");
 }

@@ -34,6 +34,8 @@
 //                           integer-resolved chunks
 //   kpp_choose_kernel       the draw and the reference's binary search
 #include <climits>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "kernels.h"
@@ -75,20 +77,60 @@ __device__ inline int kpp_binade(double s) {
 constexpr int KPP_DJ = 32;
 constexpr int KPP_V4 = KPP_THREADS * KPP_DJ / 4 / KPP_THREADS;   // float4 per thread per slice (8)
 
+// The max of the minima: each block writes its own (positive doubles order as
+// their bit patterns; 0 when it has none) and kpp_max_reduce_kernel folds them
+// -- one global atomic per wave on a single word serialised at ~12 ns each
+// (15,600 waves at N = 1M: ~0.19 ms of the 0.25 ms distance pass).
+__device__ inline void kpp_block_max(double best, unsigned long long* __restrict__ bmax) {
+    __shared__ double wbest[KPP_THREADS / 64];
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double o = __shfl_xor(best, off);
+        if (o > best) best = o;
+    }
+    if ((threadIdx.x & 63) == 0) wbest[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double b = 0.0;
+        for (int w = 0; w < KPP_THREADS / 64; w++)
+            if (wbest[w] > b) b = wbest[w];
+        bmax[blockIdx.x] = (unsigned long long)__double_as_longlong(b);
+    }
+}
+
+__global__ __launch_bounds__(1024) void kpp_max_reduce_kernel(const unsigned long long* __restrict__ bmax, int nb,
+                                                              unsigned long long* __restrict__ mx_bits) {
+    __shared__ unsigned long long red[1024];
+    unsigned long long m = 0;
+    for (int i = threadIdx.x; i < nb; i += 1024) m = bmax[i] > m ? bmax[i] : m;
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off && red[threadIdx.x + off] > red[threadIdx.x]) red[threadIdx.x] = red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *mx_bits = red[0];
+}
+
 // TX: fp32 or fp64 rows (VEC only for fp32).
 template <int METRIC, bool VEC, typename TX>
 __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restrict__ X, int64_t N, int d,
                                                                const int32_t* __restrict__ chosen, int it,
                                                                double* __restrict__ mind,
-                                                               unsigned long long* __restrict__ mx_bits) {
+                                                               unsigned long long* __restrict__ bmax) {
     static_assert(!VEC || sizeof(TX) == 4, "the float4 form reads fp32 rows");
     constexpr int DJ = sizeof(TX) == 4 ? KPP_DJ : KPP_DJ / 2;     // tile <= 34 KiB either way
     __shared__ TX tile[KPP_THREADS][DJ + 1];
+    // the newest centroid's row, widened to fp64 once per block (LDS broadcast
+    // reads in the chain instead of a uniform global load per dim)
+    extern __shared__ __attribute__((aligned(8))) char kpp_dyn[];
+    TX* cs = reinterpret_cast<TX*>(kpp_dyn);            // [d] (dynamic)
     const TX* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
+    for (int j = threadIdx.x; j < d; j += KPP_THREADS) cs[j] = c[j];
+    __syncthreads();
     double cb = 0.0;                                    // cosine: sum c^2 (uniform)
     if (METRIC == 1)
         for (int j = 0; j < d; j++) {
-            const double cj = (double)c[j];
+            const double cj = (double)cs[j];
             cb = __dadd_rn(cb, __dmul_rn(cj, cj));
         }
     double best = 0.0;
@@ -137,12 +179,17 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
                 }
             }
             if (n < N) {
+#pragma unroll 8
                 for (int jj = 0; jj < dj; jj++) {
                     const double xj = (double)tile[threadIdx.x][jj];
-                    const double cj = (double)c[j0 + jj];
+                    const double cj = (double)cs[j0 + jj];
                     if (METRIC == 0) {
                         const double df = __dsub_rn(xj, cj);
+#if defined(ABL_KPP_NOCHAIN)   // timing experiments only: order-free sum (results invalid)
+                        a = fma(df, df, a);
+#else
                         acc = __dadd_rn(acc, __dmul_rn(df, df));
+#endif
                     } else {
                         ip.add(__dmul_rn(xj, cj));
                         a = __dadd_rn(a, __dmul_rn(xj, xj));
@@ -153,6 +200,9 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
         if (n >= N) continue;
         double dd;
         if (METRIC == 0) {
+#if defined(ABL_KPP_NOCHAIN)
+            acc += a;
+#endif
             dd = sqrt(acc);
         } else {
             const double denom = __dmul_rn(sqrt(a), sqrt(cb));
@@ -166,11 +216,56 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
         mind[n] = m;
         if (m > best) best = m;
     }
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double o = __shfl_xor(best, off);
-        if (o > best) best = o;
+    kpp_block_max(best, bmax);
+}
+
+// Euclidean on fp32 rows with d % 32 == 0: one row per thread straight from
+// HBM into registers (32-dim slices, the next slice's 8 float4 loads in flight
+// while the current one is summed), no LDS tile and no barriers; the centroid
+// row is an LDS broadcast. Same exact-order chain as above.
+__global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* __restrict__ X, int64_t N, int d,
+                                                                   const int32_t* __restrict__ chosen, int it,
+                                                                   double* __restrict__ mind,
+                                                                   unsigned long long* __restrict__ bmax) {
+    extern __shared__ __attribute__((aligned(8))) char kpp_dyn2[];
+    float* cs = reinterpret_cast<float*>(kpp_dyn2);     // [d]
+    const float* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
+    for (int j = threadIdx.x; j < d; j += KPP_THREADS) cs[j] = c[j];
+    __syncthreads();
+    double best = 0.0;
+    for (int64_t n = (int64_t)blockIdx.x * KPP_THREADS + threadIdx.x; n < N; n += (int64_t)gridDim.x * KPP_THREADS) {
+        const float* xr = X + n * d;
+        float4 cur[8], nxt[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) cur[u] = *reinterpret_cast<const float4*>(xr + 4 * u);
+        double acc = 0.0;
+        for (int j0 = 0; j0 < d; j0 += 32) {
+            if (j0 + 32 < d) {
+#pragma unroll
+                for (int u = 0; u < 8; u++) nxt[u] = *reinterpret_cast<const float4*>(xr + j0 + 32 + 4 * u);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const float xv[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const double df = __dsub_rn((double)xv[q], (double)cs[j0 + 4 * u + q]);
+                    acc = __dadd_rn(acc, __dmul_rn(df, df));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) cur[u] = nxt[u];
+        }
+        const double dd = sqrt(acc);
+        double m = dd;
+        if (it > 1) {
+            const double prev = mind[n];
+            if (!(dd < prev)) m = prev;
+        }
+        mind[n] = m;
+        if (m > best) best = m;
     }
-    if ((threadIdx.x & 63) == 0 && best > 0.0) atomicMax(mx_bits, (unsigned long long)__double_as_longlong(best));
+    kpp_block_max(best, bmax);
 }
 
 // --------------------------------------------------------------------- (3)
@@ -504,6 +599,7 @@ __global__ void kpp_choose_kernel(const double* __restrict__ cum, int64_t N, con
 // mode i32, and the max word.
 int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, const double* canon,
                      int32_t* chosen, void* ws, unsigned long long* stats) {
+
     const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
     char* p = (char*)ws;
     double* mind = (double*)p;                 p += sizeof(double) * N;
@@ -513,23 +609,30 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
     KppChunk* meta = (KppChunk*)p;             p += sizeof(KppChunk) * nch;
     double* cs = (double*)p;                   p += sizeof(double) * nch;
     int32_t* mode = (int32_t*)p;               p += sizeof(int32_t) * ((nch + 1) & ~1ll);
-    unsigned long long* mx = (unsigned long long*)p;
+    unsigned long long* mx = (unsigned long long*)p;   p += 64;
+    unsigned long long* bmax = (unsigned long long*)p;   // [<= 4096] per-block maxima
     const unsigned dgrid = gsz(N, KPP_THREADS, 4096);
+    const char* kr = getenv("LSHKM_KPP_DIST");           // "lds": the LDS-tile form (A/B)
+    const bool kpp_reg = !(kr && !strcmp(kr, "lds"));
     for (int it = 1; it < K; it++) {
-        if (hipMemsetAsync(mx, 0, sizeof(*mx), s) != hipSuccess) return kstatus("kmeanspp.hip");
+
         const bool vec = d % KPP_DJ == 0 && !X.f64;
         const dim3 g(dgrid), b(KPP_THREADS);
+        const size_t ld32 = (size_t)d * 4, ld64 = (size_t)d * 8;     // the centroid row in LDS
         if (X.f64) {
-            if (metric == 0) hipLaunchKernelGGL((kpp_dist_kernel<0, false, double>), g, b, 0, s, X.d(), N, d, chosen, it, mind, mx);
-            else hipLaunchKernelGGL((kpp_dist_kernel<1, false, double>), g, b, 0, s, X.d(), N, d, chosen, it, mind, mx);
-        } else if (metric == 0 && vec)
-            hipLaunchKernelGGL((kpp_dist_kernel<0, true, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
+            if (metric == 0) hipLaunchKernelGGL((kpp_dist_kernel<0, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax);
+            else hipLaunchKernelGGL((kpp_dist_kernel<1, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax);
+        } else if (metric == 0 && vec && kpp_reg)
+            hipLaunchKernelGGL(kpp_dist_reg_kernel, g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
+        else if (metric == 0 && vec)
+            hipLaunchKernelGGL((kpp_dist_kernel<0, true, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
         else if (metric == 0)
-            hipLaunchKernelGGL((kpp_dist_kernel<0, false, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
+            hipLaunchKernelGGL((kpp_dist_kernel<0, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
         else if (vec)
-            hipLaunchKernelGGL((kpp_dist_kernel<1, true, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
+            hipLaunchKernelGGL((kpp_dist_kernel<1, true, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
         else
-            hipLaunchKernelGGL((kpp_dist_kernel<1, false, float>), g, b, 0, s, X.f(), N, d, chosen, it, mind, mx);
+            hipLaunchKernelGGL((kpp_dist_kernel<1, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
+        hipLaunchKernelGGL(kpp_max_reduce_kernel, dim3(1), dim3(1024), 0, s, bmax, (int)dgrid, mx);
         hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum);
         hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, csum, nch, cstart);
         hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, cstart,
@@ -547,7 +650,7 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
 size_t kmeans_pp_ws_bytes(int64_t N) {
     const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
     return sizeof(double) * 2 * (size_t)N + (sizeof(double) * 3 + sizeof(KppChunk)) * (size_t)nch +
-           sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64;
+           sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64 + 4096 * 8;
 }
 
 }  // namespace lshkm
