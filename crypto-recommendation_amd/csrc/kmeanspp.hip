@@ -280,15 +280,21 @@ __device__ inline double block_sum_f64(double v, double* red) {
     return t;
 }
 
+// also writes q_m (one division per row for all the passes below)
 __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_sum_kernel(const double* __restrict__ mind, int64_t N,
                                                                     const unsigned long long* __restrict__ mx_bits,
-                                                                    double* __restrict__ chunk_sum) {
+                                                                    double* __restrict__ chunk_sum,
+                                                                    double* __restrict__ qbuf) {
     __shared__ double red[KPP_THREADS / 64];
     const double mx = kpp_max(mx_bits);
     const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
     double v = 0.0;
     for (int e = threadIdx.x; e < KPP_CHUNK; e += KPP_THREADS)
-        if (c0 + e < N) v += kpp_q(mind[c0 + e], mx);
+        if (c0 + e < N) {
+            const double q = kpp_q(mind[c0 + e], mx);
+            qbuf[c0 + e] = q;
+            v += q;
+        }
     const double t = block_sum_f64(v, red);
     if (threadIdx.x == 0) chunk_sum[blockIdx.x] = t;
 }
@@ -305,8 +311,13 @@ __global__ __launch_bounds__(KPP_SCAN_THREADS) void kpp_chunk_scan_kernel(const 
     for (int64_t c = lo; c < hi; c++) v += chunk_sum[c];
     part[threadIdx.x] = v;
     __syncthreads();
-    double run = 0.0;
-    for (int i = 0; i < (int)threadIdx.x; i++) run += part[i];
+    for (int off = 1; off < KPP_SCAN_THREADS; off <<= 1) {   // inclusive scan of the partials
+        const double o = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0.0;
+        __syncthreads();
+        part[threadIdx.x] += o;
+        __syncthreads();
+    }
+    double run = threadIdx.x ? part[threadIdx.x - 1] : 0.0;
     for (int64_t c = lo; c < hi; c++) {
         chunk_start[c] = run;
         run += chunk_sum[c];
@@ -330,12 +341,10 @@ struct KppChunk {
     int32_t pad;
 };
 
-__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const double* __restrict__ mind, int64_t N,
-                                                                      const unsigned long long* __restrict__ mx_bits,
+__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const double* __restrict__ qbuf, int64_t N,
                                                                       const double* __restrict__ chunk_start,
                                                                       KppChunk* __restrict__ meta) {
     __shared__ long long red[KPP_THREADS / 64];
-    const double mx = kpp_max(mx_bits);
     const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
     const double a = chunk_start[blockIdx.x];
     // a guess only; tiny or non-finite starts are left to the exact walk
@@ -344,7 +353,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const doub
     long long acc = usable ? 0 : -1;
     for (int i = threadIdx.x; i < KPP_CHUNK && acc >= 0; i += KPP_THREADS) {
         if (c0 + i >= N) break;
-        const int64_t r = kpp_units(kpp_q(mind[c0 + i], mx), e);
+        const int64_t r = kpp_units(qbuf[c0 + i], e);
         acc = r < 0 ? -1 : acc + r;
     }
     // any lane's -1 makes the chunk dirty
@@ -370,8 +379,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const doub
 // The exact walk (one wave). s is uniform across the wave. A step covers
 // 64 lanes x CPL consecutive chunks (lane-local prefix, then a wave scan of
 // the lane totals); R < 2^53 per chunk keeps every prefix below 2^62.
-__global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict__ mind, int64_t N,
-                                                       const unsigned long long* __restrict__ mx_bits,
+__global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict__ qbuf, int64_t N,
                                                        const KppChunk* __restrict__ meta, int64_t nch,
                                                        double* __restrict__ chunk_s, int32_t* __restrict__ chunk_mode,
                                                        double* __restrict__ cum, unsigned long long* __restrict__ stats) {
@@ -381,10 +389,36 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
     __shared__ double qs[KPP_CHUNK];
     __shared__ KppChunk wm[WIN];
     const int lane = threadIdx.x;
-    const double mx = kpp_max(mx_bits);
+    constexpr int EPL = KPP_CHUNK / 64;
     double s = 0.0;
     int64_t base = 0, win0 = -2 * WIN;
     unsigned long long nseq = 0;
+    // the q values of the predicted next stop chunk (a dirty chunk, or one whose
+    // successor's guessed binade differs: the running sum crosses inside it),
+    // loaded ahead
+    int64_t pf_c = -1;
+    double pf_q[EPL];
+    auto prefetch_after = [&](int64_t c) {
+        pf_c = -1;
+        for (int64_t j0 = c + 1; j0 < win0 + WIN && j0 < nch && pf_c < 0; j0 += 64) {
+            const int64_t j = j0 + lane;
+            bool st = false;
+            if (j < nch && j < win0 + WIN) {
+                const int e0 = wm[j - win0].e;
+                st = e0 == KPP_DIRTY || (j + 1 < nch && j + 1 < win0 + WIN && wm[j + 1 - win0].e != e0);
+            }
+            const unsigned long long b = __ballot(st);
+            if (b) pf_c = j0 + __ffsll((long long)b) - 1;
+        }
+        if (pf_c >= 0) {
+            const int64_t r0 = pf_c * KPP_CHUNK;
+#pragma unroll
+            for (int t = 0; t < EPL; t++) {
+                const int64_t i = r0 + lane + 64 * t;
+                pf_q[t] = i < N ? qbuf[i] : 0.0;
+            }
+        }
+    };
     while (base < nch) {
         if (base < win0 || base + STEP > win0 + WIN) {   // (re)fill the window at base
             win0 = base;
@@ -459,13 +493,19 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
         // hardware fp64 add as :122-125. Usually 2 passes.
         const int64_t r0 = c * KPP_CHUNK;
         const int n = (int)(N - r0 < KPP_CHUNK ? N - r0 : KPP_CHUNK);
-        for (int i = lane; i < n; i += 64) qs[i] = kpp_q(mind[r0 + i], mx);
+        if (c == pf_c) {
+#pragma unroll
+            for (int t = 0; t < EPL; t++)
+                if (lane + 64 * t < n) qs[lane + 64 * t] = pf_q[t];
+        } else {
+            for (int i = lane; i < n; i += 64) qs[i] = qbuf[r0 + i];
+        }
         wave_sync();
+        prefetch_after(c);
         if (lane == 0) {
             chunk_s[c] = s;
             chunk_mode[c] = 1;
         }
-        constexpr int EPL = KPP_CHUNK / 64;
         int p = 0;
         while (p < n) {
             // modes: integer units in s's binade; s == 0 (only q == 0 keeps it);
@@ -536,8 +576,7 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
 }
 
 // s_m = s_start + u * (inclusive prefix of RN_u(q)) for the integer-resolved chunks.
-__global__ __launch_bounds__(KPP_THREADS) void kpp_expand_kernel(const double* __restrict__ mind, int64_t N,
-                                                                 const unsigned long long* __restrict__ mx_bits,
+__global__ __launch_bounds__(KPP_THREADS) void kpp_expand_kernel(const double* __restrict__ qbuf, int64_t N,
                                                                  const KppChunk* __restrict__ meta,
                                                                  const double* __restrict__ chunk_s,
                                                                  const int32_t* __restrict__ chunk_mode,
@@ -545,7 +584,6 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_expand_kernel(const double* _
     constexpr int PER = KPP_CHUNK / KPP_THREADS;
     __shared__ long long wsum[KPP_THREADS / 64];
     if (chunk_mode[blockIdx.x] != 0) return;
-    const double mx = kpp_max(mx_bits);
     const int e = meta[blockIdx.x].e;
     const int64_t s_units = (int64_t)ldexp(chunk_s[blockIdx.x], 52 - e);
     const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
@@ -555,7 +593,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_expand_kernel(const double* _
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const int64_t row = c0 + threadIdx.x * PER + k;
-        r[k] = row < N ? kpp_units(kpp_q(mind[row], mx), e) : 0;
+        r[k] = row < N ? kpp_units(qbuf[row], e) : 0;
         own += r[k];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -610,7 +648,8 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
     double* cs = (double*)p;                   p += sizeof(double) * nch;
     int32_t* mode = (int32_t*)p;               p += sizeof(int32_t) * ((nch + 1) & ~1ll);
     unsigned long long* mx = (unsigned long long*)p;   p += 64;
-    unsigned long long* bmax = (unsigned long long*)p;   // [<= 4096] per-block maxima
+    unsigned long long* bmax = (unsigned long long*)p;   p += 4096 * 8;   // [<= 4096] per-block maxima
+    double* qbuf = (double*)p;                                            // [N] q_m
     const unsigned dgrid = gsz(N, KPP_THREADS, 4096);
     const char* kr = getenv("LSHKM_KPP_DIST");           // "lds": the LDS-tile form (A/B)
     const bool kpp_reg = !(kr && !strcmp(kr, "lds"));
@@ -633,13 +672,11 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
         else
             hipLaunchKernelGGL((kpp_dist_kernel<1, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
         hipLaunchKernelGGL(kpp_max_reduce_kernel, dim3(1), dim3(1024), 0, s, bmax, (int)dgrid, mx);
-        hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum);
+        hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum, qbuf);
         hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, csum, nch, cstart);
-        hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, cstart,
-                           meta);
-        hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, mind, N, mx, meta, nch, cs, mode, cum, stats);
-        hipLaunchKernelGGL(kpp_expand_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, meta, cs, mode,
-                           cum);
+        hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, cstart, meta);
+        hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, qbuf, N, meta, nch, cs, mode, cum, stats);
+        hipLaunchKernelGGL(kpp_expand_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, meta, cs, mode, cum);
         hipLaunchKernelGGL(kpp_choose_kernel, dim3(1), dim3(1), 0, s, cum, N, canon, it, chosen);
         const int rc = kstatus("kmeanspp.hip");
         if (rc) return rc;
@@ -650,7 +687,7 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
 size_t kmeans_pp_ws_bytes(int64_t N) {
     const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
     return sizeof(double) * 2 * (size_t)N + (sizeof(double) * 3 + sizeof(KppChunk)) * (size_t)nch +
-           sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64 + 4096 * 8;
+           sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64 + 4096 * 8 + sizeof(double) * (size_t)N;
 }
 
 }  // namespace lshkm
