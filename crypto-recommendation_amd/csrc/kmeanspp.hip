@@ -58,6 +58,36 @@ __device__ inline double kpp_max(const unsigned long long* mx_bits) {
     return __longlong_as_double((long long)*mx_bits);
 }
 
+// Wave-level helpers of the exact walk (one wave, every lane active): an
+// inclusive int64 scan by DPP row shifts inside each 16-lane row plus the row
+// totals by readlane (no LDS round trips, unlike __shfl_up), and reads of a
+// uniform lane.
+__device__ inline int64_t dpp_shr64(int64_t v, int k) {
+    const int lo = (int)(uint32_t)(uint64_t)v, hi = (int)(uint32_t)((uint64_t)v >> 32);
+    int rl, rh;
+    switch (k) {   // row_shr:k (0x110 + k); lanes without a source read 0 (bound_ctrl)
+        case 1: rl = __builtin_amdgcn_update_dpp(0, lo, 0x111, 0xF, 0xF, true); rh = __builtin_amdgcn_update_dpp(0, hi, 0x111, 0xF, 0xF, true); break;
+        case 2: rl = __builtin_amdgcn_update_dpp(0, lo, 0x112, 0xF, 0xF, true); rh = __builtin_amdgcn_update_dpp(0, hi, 0x112, 0xF, 0xF, true); break;
+        case 4: rl = __builtin_amdgcn_update_dpp(0, lo, 0x114, 0xF, 0xF, true); rh = __builtin_amdgcn_update_dpp(0, hi, 0x114, 0xF, 0xF, true); break;
+        default: rl = __builtin_amdgcn_update_dpp(0, lo, 0x118, 0xF, 0xF, true); rh = __builtin_amdgcn_update_dpp(0, hi, 0x118, 0xF, 0xF, true); break;
+    }
+    return (int64_t)(((uint64_t)(uint32_t)rh << 32) | (uint32_t)rl);
+}
+__device__ inline int64_t readlane64(int64_t v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ inline int64_t wave_incl_scan64(int64_t v, int lane) {
+    v += dpp_shr64(v, 1);
+    v += dpp_shr64(v, 2);
+    v += dpp_shr64(v, 4);
+    v += dpp_shr64(v, 8);
+    const int64_t t0 = readlane64(v, 15), t1 = readlane64(v, 31), t2 = readlane64(v, 47);
+    const int row = lane >> 4;
+    return v + (row > 0 ? t0 : 0) + (row > 1 ? t1 : 0) + (row > 2 ? t2 : 0);
+}
+
 // Binade exponent of a positive normal double (s in [2^e, 2^(e+1))).
 __device__ inline int kpp_binade(double s) {
     return (int)((__double_as_longlong(s) >> 52) & 0x7ff) - 1023;
@@ -419,13 +449,22 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
             }
         }
     };
+#if defined(KPP_PROF)
+    unsigned long long tp[5] = {0, 0, 0, 0, 0}, npass = 0;
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define KPP_T(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); tp[i] += t_ - tq; tq = t_; }
+#else
+#define KPP_T(i)
+#endif
     while (base < nch) {
+        KPP_T(4)
         if (base < win0 || base + STEP > win0 + WIN) {   // (re)fill the window at base
             win0 = base;
             for (int i = lane; i < WIN; i += 64)
                 if (win0 + i < nch) wm[i] = meta[win0 + i];
             wave_sync();
         }
+        KPP_T(0)
         const bool s_ok = s >= 0x1p-900 && s < 0x1p62;
         const int es = s_ok ? kpp_binade(s) : 0;
         const int64_t s_units = s_ok ? (int64_t)ldexp(s, 52 - es) : 0;
@@ -444,12 +483,7 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
             if (lbad == CPL && !(j < nch && s_ok && m.e == es)) lbad = t;
         }
         // exclusive prefix of the lane totals
-        int64_t pre = tot;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int64_t o = __shfl_up(pre, off);
-            if (lane >= off) pre += o;
-        }
-        pre -= tot;
+        int64_t pre = wave_incl_scan64(tot, lane) - tot;
         // the lane's first chunk that is wrong or would leave the binade
         int first = lbad;
         int64_t run = s_units + pre;
@@ -473,10 +507,10 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
                 }
             }
         }
-        const int fstop = fl < 64 ? __shfl(first, fl) : CPL;
+        const int fstop = fl < 64 ? __builtin_amdgcn_readlane(first, fl) : CPL;
         const int64_t c = base + (int64_t)(fl < 64 ? fl : 64) * CPL + (fl < 64 ? fstop : 0);
         // s after the resolved chunks: `run` of lane fl (or of lane 63 if none stopped)
-        const int64_t adv = __shfl(run, fl < 64 ? fl : 63);
+        const int64_t adv = readlane64(run, fl < 64 ? fl : 63);
         if (c > base) s = ldexp((double)adv, es - 52);
         if (fl == 64) {
             base += STEP;
@@ -491,6 +525,7 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
         // elements that stay in s's binade as integers (EPL per lane), then
         // adds the stopping element (binade crossing, tie, non-finite) with a
         // hardware fp64 add as :122-125. Usually 2 passes.
+        KPP_T(1)
         const int64_t r0 = c * KPP_CHUNK;
         const int n = (int)(N - r0 < KPP_CHUNK ? N - r0 : KPP_CHUNK);
         if (c == pf_c) {
@@ -502,6 +537,7 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
         }
         wave_sync();
         prefetch_after(c);
+        KPP_T(2)
         if (lane == 0) {
             chunk_s[c] = s;
             chunk_mode[c] = 1;
@@ -532,12 +568,7 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
                 if (lfirst == EPL && rr < 0) lfirst = t;
                 tot += r[t];
             }
-            int64_t pre = tot;
-            for (int off = 1; off < 64; off <<= 1) {
-                const int64_t o = __shfl_up(pre, off);
-                if (lane >= off) pre += o;
-            }
-            pre -= tot;
+            const int64_t pre = wave_incl_scan64(tot, lane) - tot;
             int first = lfirst;
             int64_t run = su + pre;
 #pragma unroll
@@ -557,18 +588,25 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
                     }
                 }
             }
-            const int fstop = fl < 64 ? __shfl(first, fl) : EPL;
+            const int fstop = fl < 64 ? __builtin_amdgcn_readlane(first, fl) : EPL;
             const int m = p + (fl < 64 ? fl : 64) * EPL + (fl < 64 ? fstop : 0);
-            if (m > p && ok) s = ldexp((double)__shfl(run, fl < 64 ? fl : 63), e - 52);
+            if (m > p && ok) s = ldexp((double)readlane64(run, fl < 64 ? fl : 63), e - 52);
             if (m >= n) break;
             s = __dadd_rn(qs[m], s);           // the reference's add (0 + q_0 = q_0 for row 0)
             if (lane == 0) cum[r0 + m] = s;
             p = m + 1;
+#if defined(KPP_PROF)
+            npass++;
+#endif
         }
         wave_sync();
+        KPP_T(3)
         base = c + 1;
         nseq++;
     }
+#if defined(KPP_PROF)
+    if (lane == 0) printf("KPPPROF %llu %llu %llu %llu %llu %llu %llu\n", tp[0], tp[1], tp[2], tp[3], tp[4], nseq, npass);
+#endif
     if (lane == 0 && stats) {
         atomicAdd(stats + STAT_KPP_CHUNKS, (unsigned long long)nch);
         atomicAdd(stats + STAT_KPP_SEQ, nseq);
