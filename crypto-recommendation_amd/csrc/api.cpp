@@ -468,8 +468,8 @@ int lshkm_lsh_hash_f64(lshkm_lsh lsh, const double* X, int64_t N, int32_t* tuple
 // (persistent form, one launch per 256-centroid slice; cosine: normalised
 // centroids), else the f32-MFMA kernel (d <= 256), else the exact pass.
 // LSHKM_ASSIGN_PATH = "f32" / "exact" forces a path (tests compare them).
-// Euclidean fp64 rows and fp32 rows of d < 128 dims (d <= 128, K <= 512) take
-// the hi-only form too (path 3: zero-padded dims, no LIST refinement); other
+// fp64 rows and fp32 rows of d < 128 dims (d <= 128, K <= 512; either metric)
+// take the hi-only form too (path 3: zero-padded dims); other
 // fp64 rows the f32-MFMA kernel (rows rounded to f32 on load, the bound
 // widened accordingly) or the exact pass.
 static int assign_path(int metric, int d, int K, bool f64) {
@@ -481,7 +481,7 @@ static int assign_path(int metric, int d, int K, bool f64) {
         if (metric == LSHKM_METRIC_EUCLIDEAN || !(ff && !strcmp(ff, "chunked"))) return 0;
     }
     const char* fh = getenv("LSHKM_FUSED_HI");
-    if (!f32 && metric == LSHKM_METRIC_EUCLIDEAN && d <= 128 && K <= 512 && !(fh && !strcmp(fh, "0"))) return 3;
+    if (!f32 && d <= 128 && K <= 512 && !(fh && !strcmp(fh, "0"))) return 3;
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
@@ -585,7 +585,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv, C32, rn32, d, C64p))) { LSHKM_LAUNCH_CHECK(); return rc; }
         FusedLaunch f;
         f.C32 = C32; f.rn32 = rn32; f.fast_dist = fast ? 1 : 0;
-        f.rows = rows_kind; f.d = d;
+        f.rows = rows_kind; f.d = d; f.Cd = C;
         f.X = X.f64 ? nullptr : X.f(); f.X64 = X.f64 ? X.d() : nullptr;
         f.N = N; f.Ch = Ch; f.Cl = Cl; f.cnh = cnh; f.cbound = cbound; f.C64 = C64p ? C64p : C; f.Kpad = Kpad;
         f.assign = assign; f.dist = dist; f.ambig = (int32_t*)ctx->ws_ambig.p; f.ambig_count = cnt;
@@ -655,7 +655,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         }
         if (cosine) {
             for (int li = 0; li < f.ncos_lists; li++)
-                if ((rc = launch_cos_fix_seg(s, X.f(), C, f.cos_list[li], f.cos_counts[li], f.seg_rows, f.nseg, assign,
+                if ((rc = launch_cos_fix_seg(s, X, d, C, f.cos_list[li], f.cos_counts[li], f.seg_rows, f.nseg, assign,
                                              dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
             if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 3))) { LSHKM_LAUNCH_CHECK(); return rc; }
         }

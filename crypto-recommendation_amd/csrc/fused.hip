@@ -115,6 +115,7 @@ struct FusedArgs {
     // rows of d <= 128 dims, row stride d; xvec: rows 16-B aligned (vector loads)
     const double* X64;
     int d, xvec;
+    const double* Cd;                // general rows: the caller's [K][d] centroids (cosine winners)
 };
 
 // Profiling builds (make prof -> liblshkm_prof.so) accumulate s_memtime per
@@ -639,7 +640,7 @@ static_assert(fp_lds_bytes(FP_KMAX, true) <= 160 * 1024, "persistent LDS image e
 // (general rows, see there); fp64 rows add |x - f32(x)| |c| <= 2^-24 |x| |c| to E.
 template <bool HASH, int MET = 0, bool MP = false, bool LIST = false, int ROWS = 0>
 __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedArgs a) {
-    static_assert(ROWS == 0 || (LIST && !HASH && MET == 0 && FP_KEEP_X), "general rows: the euclidean LIST form");
+    static_assert(ROWS == 0 || (LIST && !HASH && FP_KEEP_X), "general rows: the LIST form");
     static_assert(FP_KEEP_X || !LIST, "the quad-layout chain re-reads rows by tile index");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
@@ -964,7 +965,11 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
                 double v;
-                if (cosine_fast_nb(a.X + row * FU_D, a.C64 + (size_t)I1 * FU_D, FU_D, a.nbv[I1], v)) a.dist[row] = v;
+                bool okc;
+                if constexpr (ROWS == 1) okc = cosine_fast_nb(a.X + row * a.d, a.Cd + (size_t)I1 * a.d, a.d, a.nbv[I1], v);
+                else if constexpr (ROWS == 2) okc = cosine_fast_nb(a.X64 + row * a.d, a.Cd + (size_t)I1 * a.d, a.d, a.nbv[I1], v);
+                else okc = cosine_fast_nb(a.X + row * FU_D, a.C64 + (size_t)I1 * FU_D, FU_D, a.nbv[I1], v);
+                if (okc) a.dist[row] = v;
                 else fix = true;
             }
             const unsigned long long fb = __ballot(fix);
@@ -1285,7 +1290,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     constexpr int FH_THREADS = 64 * FH_WAVES;
     static_assert(NIMG == 1 || (!MP && MET == 0), "two-image form: euclidean, single launch");
     static_assert(!GATH || (!MP && MET == 0 && NIMG == 1 && FH_WAVES == 8), "gather ring: euclidean single pass");
-    static_assert(ROWS == 0 || (!HASH && !MP && MET == 0 && NIMG == 1), "general rows: euclidean Lloyd, one pass");
+    static_assert(ROWS == 0 || (!HASH && !MP && NIMG == 1), "general rows: Lloyd without hashing, one pass");
     // the gather's explicit vmcnt waits assume no other vector loads in the chain
     static_assert(!(GATH && ROWS == 2), "fp64 rows re-read x in the chain: register loads of the winner rows");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1669,7 +1674,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         constexpr int XD = 4;
         double2 xring[XD][4];
         const int64_t rowc = row < a.N ? row : a.N - 1;
-        if constexpr (ROWS == 2) {
+        if constexpr (ROWS == 2 && MET == 0) {
 #pragma unroll
             for (int st = 0; st < XD; st++) load_x64_step(a, rowc, st, h, xring[st]);
         }
@@ -1729,7 +1734,20 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             bool fix = false;
             if (valid && cert) {                          // the same on both halves of a point
                 double v = 0.0;
-                const int st = cosine_winner_halves(xf, a.C64 + (size_t)I1 * FU_D + 8 * h, a.nbv[I1], h, v);
+                int st;
+                if constexpr (ROWS == 0) {
+                    st = cosine_winner_halves(xf, a.C64 + (size_t)I1 * FU_D + 8 * h, a.nbv[I1], h, v);
+                } else {
+                    // general rows: one lane per point over its own row (stride d) and
+                    // the caller's centroid row
+                    st = 1;
+                    if (h == 1) {
+                        bool okc;
+                        if constexpr (ROWS == 1) okc = cosine_fast_nb(a.X + row * a.d, a.Cd + (size_t)I1 * a.d, a.d, a.nbv[I1], v);
+                        else okc = cosine_fast_nb(a.X64 + row * a.d, a.Cd + (size_t)I1 * a.d, a.d, a.nbv[I1], v);
+                        st = okc ? 0 : 1;
+                    }
+                }
                 if (h == 1) {
                     a.assign[row] = I1;
                     if (st == 0) a.dist[row] = v;
@@ -2162,8 +2180,9 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     double rr = 0.0, hh = 0.0;           // |c - ch|^2, |ch|^2 (the hi-only scores' bound)
     double r32 = 0.0;                    // |c - f32(c)|^2 (fast distances)
     for (int j = lane; j < FU_D; j += 64) {
-        const double v = c < K && j < d ? C[(size_t)c * d + j] * scale : 0.0;
-        if (C64p) C64p[(size_t)c * FU_D + j] = v;
+        const double raw = c < K && j < d ? C[(size_t)c * d + j] : 0.0;
+        const double v = raw * scale;
+        if (C64p) C64p[(size_t)c * FU_D + j] = raw;
         const float f = (float)v;
         not32 |= c < K && (double)f != v;
         if (C32) {
@@ -2278,9 +2297,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.X64 = f.X64; a.d = f.rows == 0 ? FU_D : f.d;
     a.xvec = f.rows == 1 ? (f.d % 4 == 0 && ((uintptr_t)f.X & 15) == 0)
                          : (f.d % 2 == 0 && ((uintptr_t)f.X64 & 15) == 0);
-    if (f.rows != 0 && (hash || f.metric != 0 || !f.hi || f.Kpad > FH_KMAX || f.d < 1 || f.d > FU_D ||
+    a.Cd = f.Cd;
+    if (f.rows != 0 && (hash || !f.hi || f.Kpad > FH_KMAX || f.d < 1 || f.d > FU_D || (f.metric == 1 && !f.Cd) ||
                         (f.rows == 1 ? !f.X : (f.rows != 2 || !f.X64)))) {
-        set_error("launch_fused: general rows run the hi-only euclidean form without hashing, K <= 512, d <= 128");
+        set_error("launch_fused: general rows run the hi-only form without hashing, K <= 512, d <= 128");
         return -1;
     }
 #ifdef LSHKM_PHASE_TIMING
@@ -2382,12 +2402,18 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 #if defined(FH_WAVES_SET) && FH_WAVES_SET != 8
                 if (gath) { set_error("launch_fused: gather ring needs 8 waves"); return -1; }
 #else
-                if (gath)
+                if (gath && !cos)
                     hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, true, 1>), grid, dim3(64 * 8),
                                        (size_t)fh_gath_off(f.Kpad, false) + 8 * FH_GATH_WAVE, s, a);
                 else
 #endif
-                if (f.rows == 1)
+                if (cos && f.rows == 1)
+                    hipLaunchKernelGGL((fused_hi_kernel<false, false, 1, 1, false, 1>), grid,
+                                       dim3(64 * fh_waves<false, false, 1>()), lh, s, a);
+                else if (cos)
+                    hipLaunchKernelGGL((fused_hi_kernel<false, false, 1, 1, false, 2>), grid,
+                                       dim3(64 * fh_waves<false, false, 1>()), lh, s, a);
+                else if (f.rows == 1)
                     hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 1>), grid,
                                        dim3(64 * fh_waves<false, false, 0>()), lh, s, a);
                 else
@@ -2470,7 +2496,13 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 r.Ch = f.Ch + (size_t)c0 * FU_D; r.Cl = f.Cl + (size_t)c0 * FU_D; r.cnh = f.cnh + c0;
                 r.Kpad = std::min(FP_KMAX, f.Kpad - c0);
                 r.t0 = c0 / 32; r.pass_first = p == 0; r.pass_last = p == npass - 1;
-                if (cos) {
+                if (cos && f.rows == 1) {
+                    if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 1, false, true, 1>), grid, block, lds_nohash, s, r);
+                    else hipLaunchKernelGGL((fused_persistent_kernel<false, 1, true, true, 1>), grid, block, lds_nohash, s, r);
+                } else if (cos && f.rows == 2) {
+                    if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 1, false, true, 2>), grid, block, lds_nohash, s, r);
+                    else hipLaunchKernelGGL((fused_persistent_kernel<false, 1, true, true, 2>), grid, block, lds_nohash, s, r);
+                } else if (cos) {
                     if (npass == 1) hipLaunchKernelGGL((fused_persistent_kernel<false, 1, false, true>), grid, block, lds_nohash, s, r);
                     else hipLaunchKernelGGL((fused_persistent_kernel<false, 1, true, true>), grid, block, lds_nohash, s, r);
                 } else if (f.rows == 1) {
@@ -2531,7 +2563,8 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 // Cosine winners listed by fused_persistent_kernel<false, 1>: lane per row,
 // the soft-x87 chain. Blocks own list segments (CF_SPLIT per segment).
 constexpr int CF_SPLIT = 2;
-__global__ __launch_bounds__(256) void cos_fix_seg_kernel(const float* __restrict__ X, const double* __restrict__ C,
+template <typename TX>
+__global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__ X, int d, const double* __restrict__ C,
                                                           const unsigned long long* __restrict__ list,
                                                           const int32_t* __restrict__ seg_counts, int64_t seg_rows,
                                                           const int32_t* __restrict__ assign, double* __restrict__ dist) {
@@ -2540,15 +2573,25 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const float* __restric
     const unsigned long long* l = list + (int64_t)seg * seg_rows;
     for (int i = part * 256 + threadIdx.x; i < n; i += CF_SPLIT * 256) {
         const int64_t row = (int64_t)l[i];
-        dist[row] = exact_cosine_x87_b16(X + row * FU_D, C + (size_t)assign[row] * FU_D, FU_D);
+        if constexpr (sizeof(TX) == 4) {
+            if (d == FU_D) {
+                dist[row] = exact_cosine_x87_b16(X + row * FU_D, C + (size_t)assign[row] * FU_D, FU_D);
+                continue;
+            }
+        }
+        dist[row] = exact_cosine_x87(X + row * d, C + (size_t)assign[row] * d, d);
     }
 }
 
-int launch_cos_fix_seg(hipStream_t s, const float* X, const double* C, const unsigned long long* list,
+int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, const unsigned long long* list,
                        const int32_t* seg_counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist) {
     if (nseg <= 0) return 0;
-    hipLaunchKernelGGL(cos_fix_seg_kernel, dim3((unsigned)nseg * CF_SPLIT), dim3(256), 0, s, X, C, list, seg_counts,
-                       seg_rows, assign, dist);
+    if (X.f64)
+        hipLaunchKernelGGL(cos_fix_seg_kernel<double>, dim3((unsigned)nseg * CF_SPLIT), dim3(256), 0, s, X.d(), d, C, list,
+                           seg_counts, seg_rows, assign, dist);
+    else
+        hipLaunchKernelGGL(cos_fix_seg_kernel<float>, dim3((unsigned)nseg * CF_SPLIT), dim3(256), 0, s, X.f(), d, C, list,
+                           seg_counts, seg_rows, assign, dist);
     return kstatus("cos_fix_seg_kernel");
 }
 

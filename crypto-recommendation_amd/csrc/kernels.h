@@ -248,6 +248,7 @@ struct FusedLaunch {
     int rows = 0;
     const double* X64 = nullptr;
     int d = 128;
+    const double* Cd = nullptr;                  // general rows, cosine: the caller's [K][d] centroids
     // K > 256 on the persistent form: passes over 256-centroid slices carry each
     // lane's (best, runner-up, tile) in part[] (32 B per point)
     void* part = nullptr;
@@ -285,7 +286,7 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
 // Cosine winners listed by the persistent form (segment b: hfix[b * seg_rows ..],
 // count seg_counts[2b + 1]): soft-x87 distances.
-int launch_cos_fix_seg(hipStream_t s, const float* X, const double* C, const unsigned long long* list,
+int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, const unsigned long long* list,
                        const int32_t* seg_counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist);
 
 // Range assignment (range.hip).

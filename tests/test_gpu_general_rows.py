@@ -42,22 +42,22 @@ def rows_f64(seed, N, d):
     return X
 
 
-def check(ctx, X, Ch, sub_n=3000, seed=0):
+def check(ctx, X, Ch, sub_n=3000, seed=0, metric="euclidean"):
     """Lloyd on the default path vs the oracle (a subset) and vs the f32-MFMA path (all rows)."""
     import os
     N = X.shape[0]
     Xd, Cd = to_dev(ctx, X), to_dev(ctx, Ch)
-    a, dist = lshkm.lloyd_assign(ctx, Xd, Cd, "euclidean")
+    a, dist = lshkm.lloyd_assign(ctx, Xd, Cd, metric)
     a, dist = a.cpu().numpy(), dist.cpu().numpy()
     os.environ["LSHKM_ASSIGN_PATH"] = "f32"
     try:
-        a1, d1 = lshkm.lloyd_assign(ctx, Xd, Cd, "euclidean")
+        a1, d1 = lshkm.lloyd_assign(ctx, Xd, Cd, metric)
     finally:
         del os.environ["LSHKM_ASSIGN_PATH"]
     assert np.array_equal(a, a1.cpu().numpy())
     assert np.array_equal(dist.view(np.uint64), d1.cpu().numpy().view(np.uint64))
     sub = np.r_[0:10, np.random.default_rng(seed).choice(N, sub_n, replace=False)]
-    oa, od = oracle.lloyd_assign(X[sub], Ch, "euclidean", None)
+    oa, od = oracle.lloyd_assign(X[sub], Ch, metric, None)
     assert np.array_equal(a[sub], oa)
     # glibc pow vs x*x: 1 ulp on general doubles (DESIGN.md §5); nan rows match as nan
     ok = np.isfinite(od)
@@ -100,3 +100,22 @@ def test_f64_rows_after_update(ctx):
     a, _ = lshkm.lloyd_assign(ctx, Xd, to_dev(ctx, X[rows]), "euclidean", rows)
     Cn, _, _ = lshkm.kmeans_update(ctx, Xd, a, to_dev(ctx, X[rows]), "euclidean", 0.0)
     check(ctx, X, Cn.cpu().numpy(), sub_n=2000, seed=5)
+
+
+@pytest.mark.parametrize("d,K,f64", [(100, 256, True), (100, 512, True), (37, 64, True), (100, 200, False), (64, 256, False)])
+def test_cosine_rows(ctx, d, K, f64):
+    # cosine Lloyd on the reference's user-vector shape (main.cpp:248-258 with the
+    # cosine metric of cluster.conf): zero rows (the reference's NaN distances),
+    # rows parallel to a centroid, and general doubles
+    N = 40_003
+    rng = np.random.default_rng(d * 3 + K)
+    X = rng.standard_normal((N, d)) * np.exp(rng.uniform(-2, 2, size=(N, 1)))
+    X[5] = 0.0
+    if not f64:
+        X = X.astype(np.float32)
+    Ch = X[rng.choice(np.arange(20, N), K, replace=False)].astype(np.float64)
+    Ch[2] = Ch[1] * 3.0                                   # parallel: equal cosine distance, first index wins
+    X[6] = Ch[7] * 0.5
+    if f64:
+        Ch[4] *= 1.0 + 1e-9
+    check(ctx, X, Ch, sub_n=2000, seed=d, metric="cosine")
