@@ -125,12 +125,18 @@ struct IpAcc {
     // outside the ranges the bound assumes; q meaningless)
     __device__ inline int quot_status(double denom, double& q, double& qrad) const {
         if (!(denom >= 0x1p-800 && denom < 0x1p800 && mx >= 0x1p-800 && mx < 0x1p800 && ts < 0x1p800)) return 2;
-        const double yh = sh / denom;
-        const double r = fma(-yh, denom, sh);              // exact remainder
-        const double yl = __dadd_rn(r, sl) / denom;
+        const double yh0 = sh / denom;
+        const double r = fma(-yh0, denom, sh);             // exact remainder
+        const double yl0 = __dadd_rn(r, sl) / denom;       // <= 2^-52 |yl0| off
+        // renormalised: yh = the double nearest yh0 + yl0, yl its exact rest
+        // (Fast2Sum, |yl0| << |yh0|). sl carries the partial sums' lost bits,
+        // often several ulps of the final sum: without this step the candidate
+        // yh0 is off by an ulp for ~3/4 of random rows and the check declines them.
+        const double yh = __dadd_rn(yh0, yl0);
+        const double yl = __dsub_rn(yl0, __dsub_rn(yh, yh0));
         const double ay = fabs(yh);
         if (!(ay >= 0x1p-800 && ay < 0x1p800)) return 2;
-        const double R = (__dadd_rn(ts * (0x1p-64 * (1.0 + 0x1p-30)), mx * 0x1p-88) / denom + fabs(yl) * 0x1p-51 +
+        const double R = (__dadd_rn(ts * (0x1p-64 * (1.0 + 0x1p-30)), mx * 0x1p-88) / denom + fabs(yl0) * 0x1p-51 +
                           ay * 0x1p-63) * (1.0 + 0x1p-20);
         const long long bits = __double_as_longlong(ay);
         const double up = __dsub_rn(__longlong_as_double(bits + 1), ay);   // ulp above |yh|
