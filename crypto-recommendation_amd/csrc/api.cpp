@@ -654,9 +654,8 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             if ((rc = launch_add_counters(s, (unsigned long long*)ctx->stats.p, n, di, sp))) { LSHKM_LAUNCH_CHECK(); return rc; }
         }
         if (cosine) {
-            for (int li = 0; li < f.ncos_lists; li++)
-                if ((rc = launch_cos_fix_seg(s, X, d, C, f.cos_list[li], f.cos_counts[li], f.seg_rows, f.nseg, assign,
-                                             dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            if ((rc = launch_cos_fix_seg(s, X, d, C, f.ncos_lists, f.cos_list, f.cos_counts, f.seg_rows, f.nseg, assign,
+                                         dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
             if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 3))) { LSHKM_LAUNCH_CHECK(); return rc; }
         }
     } else if (path == 1) {

@@ -67,34 +67,59 @@ __device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __re
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
 }
 
-// exact_cosine_x87 for an fp32 row of d % 16 == 0 (16-B aligned rows): the row
-// and the centroid loaded 16 values at a time (one round trip per 16 terms).
-__device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
+// exact_cosine_x87 lane per row with the next 8 terms' loads in flight while
+// the current 8 are chained (one lane's chain is ~25 dependent fp64 operations
+// per term; a load round trip per term made a lone row's chain ~45 us at
+// d = 100). VEC: fp32 row and fp64 centroid rows 16-B aligned with d % 8 == 0
+// (vector loads); otherwise element loads, the last chunk partial.
+template <bool VEC, typename T, typename U>
+__device__ inline double exact_cosine_x87_pf(const T* __restrict__ x, const U* __restrict__ c, int d) {
+    constexpr int B = 8;
     X87acc ip;
     ip.init();
     double a = 0.0, b = 0.0;
-    for (int j0 = 0; j0 < d; j0 += 16) {
-        float xs[16];
-        double cs[16];
+    T xn[B];
+    U cn[B];
+    auto load = [&](int j0) {
+        if constexpr (VEC) {
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const float4 v = *reinterpret_cast<const float4*>(x + j0 + 4 * t);
-            xs[4 * t] = v.x; xs[4 * t + 1] = v.y; xs[4 * t + 2] = v.z; xs[4 * t + 3] = v.w;
+            for (int t = 0; t < 2; t++) {
+                const float4 v = *reinterpret_cast<const float4*>(x + j0 + 4 * t);
+                xn[4 * t] = v.x; xn[4 * t + 1] = v.y; xn[4 * t + 2] = v.z; xn[4 * t + 3] = v.w;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const double2 v = *reinterpret_cast<const double2*>(c + j0 + 2 * t);
+                cn[2 * t] = v.x; cn[2 * t + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < B; t++)
+                if (j0 + t < d) { xn[t] = x[j0 + t]; cn[t] = c[j0 + t]; }
         }
+    };
+    load(0);
+    for (int j0 = 0; j0 < d; j0 += B) {
+        T xs[B];
+        U cs[B];
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const double2 v = *reinterpret_cast<const double2*>(c + j0 + 2 * t);
-            cs[2 * t] = v.x; cs[2 * t + 1] = v.y;
-        }
+        for (int t = 0; t < B; t++) { xs[t] = xn[t]; cs[t] = cn[t]; }
+        if (j0 + B < d) load(j0 + B);
 #pragma unroll
-        for (int t = 0; t < 16; t++) {
-            const double xj = (double)xs[t], cj = cs[t];
+        for (int t = 0; t < B; t++) {
+            if (!VEC && j0 + t >= d) break;
+            const double xj = (double)xs[t], cj = (double)cs[t];
             ip.add(__dmul_rn(xj, cj));
             a = __dadd_rn(a, __dmul_rn(xj, xj));
             b = __dadd_rn(b, __dmul_rn(cj, cj));
         }
     }
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
+}
+
+// fp32 rows of d % 16 == 0 (16-B aligned rows)
+__device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
+    return exact_cosine_x87_pf<true>(x, c, d);
 }
 
 // Certified fast form of the x87 inner product's quotient (~12 fp64 ops per

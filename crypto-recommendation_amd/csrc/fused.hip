@@ -1250,6 +1250,75 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
     return st;
 }
 
+// The same for fp64 rows (ROWS = 2): the exact x values re-read from the row
+// (L2) two 16-dim steps ahead (a rolled loop: unrolled, the loads of all steps
+// were hoisted and spilled), the |x|^2 chain and the halves' inner products
+// in one pass over the steps. Dims past d are zero in the row (load_x64_step)
+// and in the padded centroid copy: exact zero terms of both chains.
+__device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc, const double* __restrict__ crow_h,
+                                               double nbv, int h, double& v) {
+    double2 xn[4], xnn[4];
+    load_x64_step(a, rowc, 0, h, xn);
+    load_x64_step(a, rowc, 1, h, xnn);
+    double xa = 0.0, sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0, hold = 0.0;
+    double2 cb[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 2 * j);
+#pragma unroll 1
+    for (int s = 0; s < 8; s++) {
+        double xv[8], cv[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            xv[2 * j] = xn[j].x; xv[2 * j + 1] = xn[j].y;
+            cv[2 * j] = cb[j].x; cv[2 * j + 1] = cb[j].y;
+            xn[j] = xnn[j];
+        }
+        if (s + 2 < 8) load_x64_step(a, rowc, s + 2, h, xnn);
+        if (s + 1 < 8) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 16 * (s + 1) + 2 * j);
+        }
+        // |x|^2: the reference's sequential chain, halves alternating
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) xa = __dadd_rn(xa, __dmul_rn(xv[j], xv[j]));
+        }
+        xa = take_from_lower(xa);
+        if (h == 1) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) xa = __dadd_rn(xa, __dmul_rn(xv[j], xv[j]));
+        }
+        xa = take_from_upper(xa);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const double pj = __dmul_rn(xv[j], cv[j]);
+            const double t = __dadd_rn(sh, pj);
+            const double bb = __dsub_rn(t, sh);
+            const double e = __dadd_rn(__dsub_rn(sh, __dsub_rn(t, bb)), __dsub_rn(pj, bb));   // TwoSum
+            sh = t;
+            sl = __dadd_rn(sl, e);
+            ts = __dadd_rn(ts, fabs(t));
+            mx = fmax(mx, fabs(t));
+        }
+        hold = __dadd_rn(hold, fabs(sh));
+    }
+    const double sh0 = swap_halves(sh, h), sl0 = swap_halves(sl, h), ts0 = swap_halves(ts, h);
+    const double mx0 = swap_halves(mx, h), hold0 = swap_halves(hold, h);
+    if (h == 0) return 2;
+    IpAcc ip;
+    const double t = __dadd_rn(sh0, sh);
+    const double bb = __dsub_rn(t, sh0);
+    const double e = __dadd_rn(__dsub_rn(sh0, __dsub_rn(t, bb)), __dsub_rn(sh, bb));
+    ip.sh = t;
+    ip.sl = __dadd_rn(__dadd_rn(sl0, sl), e);
+    ip.ts = __dadd_rn(__dadd_rn(ts0, ts), 8.0 * __dadd_rn(hold0, __dsub_rn(hold, fabs(sh)))) * (1.0 + 0x1p-50);
+    ip.mx = __dadd_rn(mx0, mx) * (1.0 + 0x1p-50);
+    double q, qr;
+    const int st = ip.quot_status(__dmul_rn(sqrt(xa), sqrt(nbv)), q, qr);
+    if (st == 0) v = __dsub_rn(1.0, q);
+    return st;
+}
+
 // NIMG = 2 (512 < K <= 1024, euclidean): ONE launch for all centroids. The
 // LDS holds one 512-centroid image at a time; the block's waves each score
 // their tile against the image in LDS, the block swaps in the other image
@@ -1735,19 +1804,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             if (valid && cert) {                          // the same on both halves of a point
                 double v = 0.0;
                 int st;
-                if constexpr (ROWS == 0) {
-                    st = cosine_winner_halves(xf, a.C64 + (size_t)I1 * FU_D + 8 * h, a.nbv[I1], h, v);
-                } else {
-                    // general rows: one lane per point over its own row (stride d) and
-                    // the caller's centroid row
-                    st = 1;
-                    if (h == 1) {
-                        bool okc;
-                        if constexpr (ROWS == 1) okc = cosine_fast_nb(a.X + row * a.d, a.Cd + (size_t)I1 * a.d, a.d, a.nbv[I1], v);
-                        else okc = cosine_fast_nb(a.X64 + row * a.d, a.Cd + (size_t)I1 * a.d, a.d, a.nbv[I1], v);
-                        st = okc ? 0 : 1;
-                    }
-                }
+                // fp32 rows (ROWS = 0 / 1): the values in registers are exact (zero
+                // past d, as the padded centroid copy); fp64 rows re-read
+                if constexpr (ROWS == 2) st = cosine_winner_halves_x64(a, row, a.C64 + (size_t)I1 * FU_D + 8 * h, a.nbv[I1], h, v);
+                else st = cosine_winner_halves(xf, a.C64 + (size_t)I1 * FU_D + 8 * h, a.nbv[I1], h, v);
                 if (h == 1) {
                     a.assign[row] = I1;
                     if (st == 0) a.dist[row] = v;
@@ -2560,17 +2620,27 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     return kstatus("fused_kernel");
 }
 
-// Cosine winners listed by fused_persistent_kernel<false, 1>: lane per row,
-// the soft-x87 chain. Blocks own list segments (CF_SPLIT per segment).
-constexpr int CF_SPLIT = 2;
+// Cosine winners listed by the fused kernels: lane per row, the x87 chain
+// (exact_cosine_x87_pf). CF_SPLIT blocks per list segment; both lists of a call
+// (the hi-only pass's declines and the refinement's) in ONE launch, so the
+// short list's lone chains (~40 us of latency) overlap the long one.
+constexpr int CF_SPLIT = 8;
+struct CosLists {
+    const unsigned long long* list[2];
+    const int32_t* counts[2];
+};
 template <typename TX>
 __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__ X, int d, const double* __restrict__ C,
-                                                          const unsigned long long* __restrict__ list,
-                                                          const int32_t* __restrict__ seg_counts, int64_t seg_rows,
+                                                          CosLists cl, int nseg, int64_t seg_rows,
                                                           const int32_t* __restrict__ assign, double* __restrict__ dist) {
-    const int seg = blockIdx.x / CF_SPLIT, part = blockIdx.x % CF_SPLIT;
-    const int n = seg_counts[2 * seg + 1];
-    const unsigned long long* l = list + (int64_t)seg * seg_rows;
+    // consecutive blocks take different segments: blocks are dealt round-robin to
+    // the 8 XCDs, and a short list fills only its segment's first part (with
+    // seg = blockIdx / CF_SPLIT every busy block sat on one XCD: 4x slower)
+    const int per_list = nseg * CF_SPLIT;
+    const int li = blockIdx.x / per_list, b = blockIdx.x % per_list;
+    const int seg = b % nseg, part = b / nseg;
+    const int n = cl.counts[li][2 * seg + 1];
+    const unsigned long long* l = cl.list[li] + (int64_t)seg * seg_rows;
     for (int i = part * 256 + threadIdx.x; i < n; i += CF_SPLIT * 256) {
         const int64_t row = (int64_t)l[i];
         if constexpr (sizeof(TX) == 4) {
@@ -2579,19 +2649,21 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__
                 continue;
             }
         }
-        dist[row] = exact_cosine_x87(X + row * d, C + (size_t)assign[row] * d, d);
+        dist[row] = exact_cosine_x87_pf<false>(X + row * d, C + (size_t)assign[row] * d, d);
     }
 }
 
-int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, const unsigned long long* list,
-                       const int32_t* seg_counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist) {
-    if (nseg <= 0) return 0;
+int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, int nlists, const unsigned long long* const* lists,
+                       const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist) {
+    if (nseg <= 0 || nlists <= 0) return 0;
+    if (nlists > 2) return -1;                       // LSHKM_ERR_ARG
+    CosLists cl{};
+    for (int i = 0; i < nlists; i++) { cl.list[i] = lists[i]; cl.counts[i] = counts[i]; }
+    const dim3 grid((unsigned)(nlists * nseg * CF_SPLIT));
     if (X.f64)
-        hipLaunchKernelGGL(cos_fix_seg_kernel<double>, dim3((unsigned)nseg * CF_SPLIT), dim3(256), 0, s, X.d(), d, C, list,
-                           seg_counts, seg_rows, assign, dist);
+        hipLaunchKernelGGL(cos_fix_seg_kernel<double>, grid, dim3(256), 0, s, X.d(), d, C, cl, nseg, seg_rows, assign, dist);
     else
-        hipLaunchKernelGGL(cos_fix_seg_kernel<float>, dim3((unsigned)nseg * CF_SPLIT), dim3(256), 0, s, X.f(), d, C, list,
-                           seg_counts, seg_rows, assign, dist);
+        hipLaunchKernelGGL(cos_fix_seg_kernel<float>, grid, dim3(256), 0, s, X.f(), d, C, cl, nseg, seg_rows, assign, dist);
     return kstatus("cos_fix_seg_kernel");
 }
 

@@ -286,8 +286,8 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
 // Cosine winners listed by the persistent form (segment b: hfix[b * seg_rows ..],
 // count seg_counts[2b + 1]): soft-x87 distances.
-int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, const unsigned long long* list,
-                       const int32_t* seg_counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist);
+int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, int nlists, const unsigned long long* const* lists,
+                       const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist);
 
 // Range assignment (range.hip).
 int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0,
