@@ -373,10 +373,10 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
     int64_t nw = (int64_t)gridDim.x * 4;
     int64_t total = rows ? (int64_t)*row_count : N;
     if (seg_counts) {            // XE_SPLIT blocks per segment of the persistent fused form's list
-        const int seg = blockIdx.x / XE_SPLIT;
+        const int seg = blockIdx.x % (gridDim.x / XE_SPLIT);   // segments across XCDs (cos_fix_seg_kernel)
         rows += (int64_t)seg * seg_rows;
         total = seg_counts[2 * seg];
-        wglobal = (int64_t)(blockIdx.x % XE_SPLIT) * 4 + (threadIdx.x >> 6);
+        wglobal = (int64_t)(blockIdx.x / (gridDim.x / XE_SPLIT)) * 4 + (threadIdx.x >> 6);
         nw = XE_SPLIT * 4;
     }
     if (total > max_rows) total = max_rows;
@@ -491,7 +491,8 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int64_t total, g0, gstride;
     if (seg_counts) {            // XB_SPLIT blocks per segment (the one persistent block b wrote)
-        const int seg = blockIdx.x / XB_SPLIT, part = blockIdx.x % XB_SPLIT;
+        const int nseg = gridDim.x / XB_SPLIT;   // segments across XCDs (cos_fix_seg_kernel)
+        const int seg = blockIdx.x % nseg, part = blockIdx.x / nseg;
         rows += (int64_t)seg * seg_rows;
         total = seg_counts[2 * seg];
         g0 = (int64_t)part * XB_WAVES + wave;
@@ -690,7 +691,8 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int64_t total, g0, gstride;
     if (seg_counts) {
-        const int seg = blockIdx.x / XP_SPLIT, part = blockIdx.x % XP_SPLIT;
+        const int nseg = gridDim.x / XP_SPLIT;   // segments across XCDs (cos_fix_seg_kernel)
+        const int seg = blockIdx.x % nseg, part = blockIdx.x / nseg;
         rows += (int64_t)seg * seg_rows;
         total = seg_counts[2 * seg];
         g0 = (int64_t)part * XP_WAVES + wave;

@@ -2168,7 +2168,8 @@ __global__ __launch_bounds__(64 * HF_WAVES) void hash_fixup_kernel(FusedArgs a) 
     double* cpn = pts + 4 * HF_QS;                   // [32] |p_f| (rounded up)
     double* ctt = cpn + 32;                          // [32] t_f
     int32_t* crv = reinterpret_cast<int32_t*>(ctt + 32);   // [32] r_f
-    const int seg = blockIdx.x / HF_SPLIT, part = blockIdx.x % HF_SPLIT;
+    const int nseg = gridDim.x / HF_SPLIT;       // segments across XCDs (cos_fix_seg_kernel)
+    const int seg = blockIdx.x % nseg, part = blockIdx.x / nseg;
     const int n = a.seg_counts[2 * seg + 1];
     if (n == 0) return;                                                 // block-uniform
     const unsigned long long* list = a.hfix + (int64_t)seg * a.seg_rows;
