@@ -368,40 +368,93 @@ __device__ inline int64_t kpp_units(double q, int e) {
 struct KppChunk {
     int64_t R;     // sum of the chunk's RN_u(q) in units of 2^(e-52)
     int32_t e;     // guessed binade, or KPP_DIRTY
-    int32_t pad;
+    int32_t dual;  // 0, or 2048 + the guessed binade eg: prefix arrays in eg, eg + 1 in pa / pb
 };
+// prefix-array entries: the inclusive prefix of RN_u(q) (a tie counted as its
+// floor) | KPP_TIE if the row itself is a tie; negative from an unresolvable
+// row (non-finite, q >= 2^(e+1)) on. Prefixes stay below 512 * 2^53 = 2^62.
+constexpr int64_t KPP_TIE = 1ll << 62;
+constexpr int64_t KPP_PMASK = KPP_TIE - 1;
+constexpr int64_t KPP_POISON = INT64_MIN;
 
+// RN_u(q) in units of u = 2^(e-52) with its class: 0 resolved, 1 a tie (the
+// floor returned: the rounding depends on the running sum's parity), 2 not
+// resolvable in binade e (non-finite, q >= 2^(e+1); 0 returned).
+__device__ inline int64_t kpp_units_c(double q, int e, int& cls) {
+    if (!(q >= 0.0) || !(q < __longlong_as_double((long long)(e + 1 + 1023) << 52))) { cls = 2; return 0; }
+    const double t = ldexp(q, 52 - e);
+    const double r = floor(t);
+    const double f = t - r;
+    cls = f == 0.5 ? 1 : 0;
+    return (int64_t)r + (f > 0.5 ? 1 : 0);
+}
+
+// Chunk guesses. A chunk the running sum is predicted to cross (the next
+// chunk's approximate start lies in a higher binade, or its own sum leaves the
+// binade) or that holds a tie also gets its prefix arrays in binades e and
+// e + 1 (pa, pb), so the walk resolves it with one hardware add per crossing
+// or tie row instead of element by element. Thread t owns rows 2t, 2t+1 (row
+// order for the scans).
 __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const double* __restrict__ qbuf, int64_t N,
-                                                                      const double* __restrict__ chunk_start,
-                                                                      KppChunk* __restrict__ meta) {
+                                                                      const double* __restrict__ chunk_start, int64_t nch,
+                                                                      KppChunk* __restrict__ meta,
+                                                                      int64_t* __restrict__ pa, int64_t* __restrict__ pb) {
+    static_assert(KPP_CHUNK == 2 * KPP_THREADS, "two rows per thread");
     __shared__ long long red[KPP_THREADS / 64];
+    __shared__ int redc[KPP_THREADS / 64];
+    __shared__ long long wtot[4][KPP_THREADS / 64];
     const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
     const double a = chunk_start[blockIdx.x];
     // a guess only; tiny or non-finite starts are left to the exact walk
     const bool usable = a >= 0x1p-900 && a < 0x1p62;
     const int e = usable ? kpp_binade(a) : 0;
-    long long acc = usable ? 0 : -1;
-    for (int i = threadIdx.x; i < KPP_CHUNK && acc >= 0; i += KPP_THREADS) {
-        if (c0 + i >= N) break;
-        const int64_t r = kpp_units(qbuf[c0 + i], e);
-        acc = r < 0 ? -1 : acc + r;
-    }
-    // any lane's -1 makes the chunk dirty
-    long long v = acc;
+    const int64_t i0 = c0 + 2 * threadIdx.x;
+    const double q0 = i0 < N ? qbuf[i0] : 0.0, q1 = i0 + 1 < N ? qbuf[i0 + 1] : 0.0;
+    int ca0, ca1;
+    const int64_t ra0 = kpp_units_c(q0, e, ca0), ra1 = kpp_units_c(q1, e, ca1);
+    long long v = ra0 + ra1;
+    int cl = ca0 | ca1;
     for (int off = 32; off >= 1; off >>= 1) {
-        const long long o = __shfl_xor(v, off);
-        v = (v < 0 || o < 0) ? -1 : v + o;
+        v += __shfl_xor(v, off);
+        cl |= __shfl_xor(cl, off);
     }
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { red[w] = v; redc[w] = cl; }
     __syncthreads();
+    long long t = 0;
+    int any = 0;
+    for (int k = 0; k < KPP_THREADS / 64; k++) { t += red[k]; any |= redc[k]; }
+    const bool cross = usable && (t >= KPP_TWO53 || (blockIdx.x + 1 < nch && !(chunk_start[blockIdx.x + 1] <
+                                                                            __longlong_as_double((long long)(e + 1 + 1023) << 52))));
+    const bool arrays = usable && (cross || (any & 1));
+    if (arrays) {                                  // block-uniform
+        int cb0, cb1;
+        const int64_t rb0 = kpp_units_c(q0, e + 1, cb0), rb1 = kpp_units_c(q1, e + 1, cb1);
+        // values and unresolvable-row counts, scanned in row order
+        int64_t sa = wave_incl_scan64(ra0 + ra1, lane), sb = wave_incl_scan64(rb0 + rb1, lane);
+        int64_t sfa = wave_incl_scan64((ca0 == 2) + (ca1 == 2), lane), sfb = wave_incl_scan64((cb0 == 2) + (cb1 == 2), lane);
+        if (lane == 63) { wtot[0][w] = sa; wtot[1][w] = sb; wtot[2][w] = sfa; wtot[3][w] = sfb; }
+        __syncthreads();
+        for (int k = 0; k < w; k++) { sa += wtot[0][k]; sb += wtot[1][k]; sfa += wtot[2][k]; sfb += wtot[3][k]; }
+        // inclusive prefixes at rows 2t and 2t + 1
+        auto enc = [](int64_t p, int64_t bad, int cls) { return bad ? KPP_POISON : p | (cls == 1 ? KPP_TIE : 0); };
+        if (i0 < N) {
+            pa[i0] = enc(sa - ra1, sfa - (ca1 == 2), ca0);
+            pb[i0] = enc(sb - rb1, sfb - (cb1 == 2), cb0);
+        }
+        if (i0 + 1 < N) {
+            pa[i0 + 1] = enc(sa, sfa, ca1);
+            pb[i0 + 1] = enc(sb, sfb, cb1);
+        }
+    }
     if (threadIdx.x == 0) {
-        long long t = 0;
-        for (int w = 0; w < KPP_THREADS / 64; w++) t = (t < 0 || red[w] < 0) ? -1 : t + red[w];
         KppChunk m;
-        const bool dirty = t < 0 || t >= KPP_TWO53;     // R >= 2^53 cannot stay in the binade
+        // a tie or unresolvable row makes the chunk dirty (the walk stops
+        // there); R >= 2^53 (it leaves the binade) stops it as well
+        const bool dirty = !usable || any != 0;
         m.R = dirty ? 0 : t;
         m.e = dirty ? KPP_DIRTY : e;
-        m.pad = 0;
+        m.dual = arrays ? 2048 + e : 0;
         meta[blockIdx.x] = m;
     }
 }
@@ -411,44 +464,19 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const doub
 // the lane totals); R < 2^53 per chunk keeps every prefix below 2^62.
 __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict__ qbuf, int64_t N,
                                                        const KppChunk* __restrict__ meta, int64_t nch,
+                                                       const int64_t* __restrict__ pa, const int64_t* __restrict__ pb,
                                                        double* __restrict__ chunk_s, int32_t* __restrict__ chunk_mode,
                                                        double* __restrict__ cum, unsigned long long* __restrict__ stats) {
     constexpr int CPL = 8;                         // chunks per lane per step
     constexpr int STEP = 64 * CPL;
     constexpr int WIN = 2 * STEP;                  // chunk metadata staged in LDS (16 KB)
-    __shared__ double qs[KPP_CHUNK];
     __shared__ KppChunk wm[WIN];
+    __shared__ double qs[KPP_CHUNK];
+    __shared__ int64_t pas[KPP_CHUNK], pbs[KPP_CHUNK];
     const int lane = threadIdx.x;
-    constexpr int EPL = KPP_CHUNK / 64;
     double s = 0.0;
     int64_t base = 0, win0 = -2 * WIN;
     unsigned long long nseq = 0;
-    // the q values of the predicted next stop chunk (a dirty chunk, or one whose
-    // successor's guessed binade differs: the running sum crosses inside it),
-    // loaded ahead
-    int64_t pf_c = -1;
-    double pf_q[EPL];
-    auto prefetch_after = [&](int64_t c) {
-        pf_c = -1;
-        for (int64_t j0 = c + 1; j0 < win0 + WIN && j0 < nch && pf_c < 0; j0 += 64) {
-            const int64_t j = j0 + lane;
-            bool st = false;
-            if (j < nch && j < win0 + WIN) {
-                const int e0 = wm[j - win0].e;
-                st = e0 == KPP_DIRTY || (j + 1 < nch && j + 1 < win0 + WIN && wm[j + 1 - win0].e != e0);
-            }
-            const unsigned long long b = __ballot(st);
-            if (b) pf_c = j0 + __ffsll((long long)b) - 1;
-        }
-        if (pf_c >= 0) {
-            const int64_t r0 = pf_c * KPP_CHUNK;
-#pragma unroll
-            for (int t = 0; t < EPL; t++) {
-                const int64_t i = r0 + lane + 64 * t;
-                pf_q[t] = i < N ? qbuf[i] : 0.0;
-            }
-        }
-    };
 #if defined(KPP_PROF)
     unsigned long long tp[5] = {0, 0, 0, 0, 0}, npass = 0;
     unsigned long long tq = __builtin_amdgcn_s_memtime();
@@ -460,8 +488,16 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
         KPP_T(4)
         if (base < win0 || base + STEP > win0 + WIN) {   // (re)fill the window at base
             win0 = base;
-            for (int i = lane; i < WIN; i += 64)
-                if (win0 + i < nch) wm[i] = meta[win0 + i];
+            // all loads in flight before the LDS writes (clamped indices: a guarded
+            // load per element compiled to one round trip each)
+            KppChunk tmp[WIN / 64];
+#pragma unroll
+            for (int t = 0; t < WIN / 64; t++) {
+                const int64_t j = win0 + lane + 64 * t;
+                tmp[t] = meta[j < nch ? j : nch - 1];
+            }
+#pragma unroll
+            for (int t = 0; t < WIN / 64; t++) wm[lane + 64 * t] = tmp[t];
             wave_sync();
         }
         KPP_T(0)
@@ -521,83 +557,123 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
             base = c;
             continue;
         }
-        // Stop chunk c, walked element-wise in passes: each pass resolves the
-        // elements that stay in s's binade as integers (EPL per lane), then
-        // adds the stopping element (binade crossing, tie, non-finite) with a
-        // hardware fp64 add as :122-125. Usually 2 passes.
+        // Stop chunk c (the first, a binade crossing, a tie, a non-finite value).
+        // With prefix arrays (a predicted crossing): the rows before the crossing
+        // from pa in s's binade, the crossing row by the reference's hardware add,
+        // the rows after it from pb in the next binade, all in parallel. Any rest
+        // (no arrays, a tie, a second crossing): the reference's adds one by one
+        // (:122-125), s uniform in every lane, ~26 cycles per row.
         KPP_T(1)
         const int64_t r0 = c * KPP_CHUNK;
         const int n = (int)(N - r0 < KPP_CHUNK ? N - r0 : KPP_CHUNK);
-        if (c == pf_c) {
-#pragma unroll
-            for (int t = 0; t < EPL; t++)
-                if (lane + 64 * t < n) qs[lane + 64 * t] = pf_q[t];
-        } else {
-            for (int i = lane; i < n; i += 64) qs[i] = qbuf[r0 + i];
-        }
-        wave_sync();
-        prefetch_after(c);
-        KPP_T(2)
         if (lane == 0) {
             chunk_s[c] = s;
             chunk_mode[c] = 1;
         }
-        int p = 0;
-        while (p < n) {
-            // modes: integer units in s's binade; s == 0 (only q == 0 keeps it);
-            // s NaN (stays NaN); s == +inf (stays inf unless q is NaN)
-            const bool nan_s = s != s, inf_s = s == __longlong_as_double(0x7ff0000000000000ll);
-            const bool ok = s >= 0x1p-900 && s < 0x1p62;
-            const int e = ok ? kpp_binade(s) : 0;
-            const int64_t su = ok ? (int64_t)ldexp(s, 52 - e) : 0;
-            int64_t r[EPL];
-            int lfirst = EPL;
-            int64_t tot = 0;
+        const KppChunk mc = wm[c - win0];
+        const bool arrays = mc.dual != 0;
+        const int eg = mc.dual - 2048;
+        // lane l holds rows 8l..8l+7 of the prefix arrays in registers; q and the
+        // arrays also go to LDS for the uniform reads; every load is issued
+        // before the first use (clamped indices)
+        constexpr int EPL = KPP_CHUNK / 64;
+        int64_t PA[EPL], PB[EPL];
+        {
+            double qv[EPL];
 #pragma unroll
             for (int t = 0; t < EPL; t++) {
-                const int idx = p + lane * EPL + t;
-                int64_t rr = -1;
-                if (idx < n) {
-                    const double q = qs[idx];
-                    if (nan_s) rr = 0;
-                    else if (inf_s) rr = q == q ? 0 : -1;
-                    else if (s == 0.0) rr = q == 0.0 ? 0 : -1;
-                    else if (ok) rr = kpp_units(q, e);
-                }
-                r[t] = rr < 0 ? 0 : rr;
-                if (lfirst == EPL && rr < 0) lfirst = t;
-                tot += r[t];
+                const int i = lane * EPL + t;
+                qv[t] = qbuf[r0 + (i < n ? i : n - 1)];
             }
-            const int64_t pre = wave_incl_scan64(tot, lane) - tot;
-            int first = lfirst;
-            int64_t run = su + pre;
-#pragma unroll
-            for (int t = 0; t < EPL; t++) {
-                if (t < first && run + r[t] >= KPP_TWO53) first = t;
-                if (t < first) run += r[t];
-            }
-            const unsigned long long bad = __ballot(first < EPL);
-            const int fl = bad ? __ffsll((long long)bad) - 1 : 64;
-            if (lane <= fl) {
-                int64_t v = su + pre;
+            if (arrays) {
 #pragma unroll
                 for (int t = 0; t < EPL; t++) {
-                    if (t < first) {
-                        v += r[t];
-                        cum[r0 + p + lane * EPL + t] = ok ? ldexp((double)v, e - 52) : s;
-                    }
+                    const int i = lane * EPL + t;
+                    PA[t] = pa[r0 + (i < n ? i : n - 1)];
+                    PB[t] = pb[r0 + (i < n ? i : n - 1)];
                 }
             }
-            const int fstop = fl < 64 ? __builtin_amdgcn_readlane(first, fl) : EPL;
-            const int m = p + (fl < 64 ? fl : 64) * EPL + (fl < 64 ? fstop : 0);
-            if (m > p && ok) s = ldexp((double)readlane64(run, fl < 64 ? fl : 63), e - 52);
-            if (m >= n) break;
-            s = __dadd_rn(qs[m], s);           // the reference's add (0 + q_0 = q_0 for row 0)
-            if (lane == 0) cum[r0 + m] = s;
-            p = m + 1;
+#pragma unroll
+            for (int t = 0; t < EPL; t++) qs[lane * EPL + t] = qv[t];
+            if (arrays) {
+#pragma unroll
+                for (int t = 0; t < EPL; t++) { pas[lane * EPL + t] = PA[t]; pbs[lane * EPL + t] = PB[t]; }
+            }
+        }
+        wave_sync();
+        KPP_T(2)
+        // rows [i0, m) resolved as integers in binade E from the prefix array P
+        // (s exact, in binade E): returns m, the first row that is a tie,
+        // unresolvable or leaves the binade; s advances to row m - 1
+        auto resolve = [&](const int64_t* P, const int64_t (&PR)[EPL], int i0, int E) -> int {
+            const int64_t su = (int64_t)ldexp(s, 52 - E);
+            const int64_t base_p = i0 > 0 ? (P[i0 - 1] & KPP_PMASK) : 0;
+            int lf = EPL;
+#pragma unroll
+            for (int t = 0; t < EPL; t++) {
+                const int i = lane * EPL + t;
+                const int64_t p = PR[t];
+                if (lf == EPL && i >= i0 && i < n &&
+                    (p < 0 || (p & KPP_TIE) || su + ((p & KPP_PMASK) - base_p) >= KPP_TWO53))
+                    lf = t;
+            }
+            const unsigned long long fbits = __ballot(lf < EPL);
+            const int fl = fbits ? __ffsll((long long)fbits) - 1 : 64;
+            const int m = fl < 64 ? fl * EPL + __builtin_amdgcn_readlane(lf, fl) : n;
+            double out[EPL];
+#pragma unroll
+            for (int t = 0; t < EPL; t++) out[t] = ldexp((double)(su + ((PR[t] & KPP_PMASK) - base_p)), E - 52);
+#pragma unroll
+            for (int t = 0; t < EPL; t++) {
+                const int i = lane * EPL + t;
+                if (i >= i0 && i < m) cum[r0 + i] = out[t];
+            }
+            if (m > i0) s = ldexp((double)(su + ((P[m - 1] & KPP_PMASK) - base_p)), E - 52);
+            return m;
+        };
+        int i0 = 0;
+        while (arrays && i0 < n) {
+            if (!(s >= 0x1p-900 && s < 0x1p62)) break;
+            const int E = kpp_binade(s);
+            if (E != eg && E != eg + 1) break;
+            const int64_t* P = E == eg ? pas : pbs;
+            i0 = E == eg ? resolve(pas, PA, i0, E) : resolve(pbs, PB, i0, E);
+            if (i0 >= n || P[i0] < 0) break;         // done, or an unresolvable row: one by one from it
+            s = __dadd_rn(qs[i0], s);               // a tie or crossing row: the reference's add
+            if (lane == 0) cum[r0 + i0] = s;
+            i0++;
+        }
 #if defined(KPP_PROF)
-            npass++;
+        npass += n - i0;
+#if defined(KPP_PROF_STOPS)
+        if (lane == 0) printf("KPPSTOP %lld %d %d %d %d %d\n", (long long)c, mc.dual, mc.e, es, (int)s_ok, i0);
 #endif
+#endif
+        // the rest one by one: every lane adds and stores the same value (one
+        // line, no exec toggling), the next 16 values read ahead from LDS with
+        // uniform-address (broadcast) reads
+        constexpr int QB = 16;
+        double qn[QB];
+#pragma unroll
+        for (int t = 0; t < QB; t++) qn[t] = qs[i0 + t < n ? i0 + t : n - 1];
+        int i = i0;
+        for (; i + QB <= n; i += QB) {
+            double qv[QB];
+#pragma unroll
+            for (int t = 0; t < QB; t++) qv[t] = qn[t];
+            if (i + 2 * QB <= n) {
+#pragma unroll
+                for (int t = 0; t < QB; t++) qn[t] = qs[i + QB + t];
+            }
+#pragma unroll
+            for (int t = 0; t < QB; t++) {
+                s = __dadd_rn(qv[t], s);           // the reference's add (0 + q_0 = q_0 for row 0)
+                cum[r0 + i + t] = s;
+            }
+        }
+        for (; i < n; i++) {
+            s = __dadd_rn(qs[i], s);
+            cum[r0 + i] = s;
         }
         wave_sync();
         KPP_T(3)
@@ -687,7 +763,9 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
     int32_t* mode = (int32_t*)p;               p += sizeof(int32_t) * ((nch + 1) & ~1ll);
     unsigned long long* mx = (unsigned long long*)p;   p += 64;
     unsigned long long* bmax = (unsigned long long*)p;   p += 4096 * 8;   // [<= 4096] per-block maxima
-    double* qbuf = (double*)p;                                            // [N] q_m
+    double* qbuf = (double*)p;                 p += sizeof(double) * N;   // [N] q_m
+    int64_t* pa = (int64_t*)p;                 p += sizeof(int64_t) * N;  // crossing chunks' prefix arrays
+    int64_t* pb = (int64_t*)p;
     const unsigned dgrid = gsz(N, KPP_THREADS, 4096);
     const char* kr = getenv("LSHKM_KPP_DIST");           // "lds": the LDS-tile form (A/B)
     const bool kpp_reg = !(kr && !strcmp(kr, "lds"));
@@ -712,8 +790,8 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
         hipLaunchKernelGGL(kpp_max_reduce_kernel, dim3(1), dim3(1024), 0, s, bmax, (int)dgrid, mx);
         hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum, qbuf);
         hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, csum, nch, cstart);
-        hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, cstart, meta);
-        hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, qbuf, N, meta, nch, cs, mode, cum, stats);
+        hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, cstart, nch, meta, pa, pb);
+        hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, qbuf, N, meta, nch, pa, pb, cs, mode, cum, stats);
         hipLaunchKernelGGL(kpp_expand_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, meta, cs, mode, cum);
         hipLaunchKernelGGL(kpp_choose_kernel, dim3(1), dim3(1), 0, s, cum, N, canon, it, chosen);
         const int rc = kstatus("kmeanspp.hip");
@@ -725,7 +803,8 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
 size_t kmeans_pp_ws_bytes(int64_t N) {
     const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
     return sizeof(double) * 2 * (size_t)N + (sizeof(double) * 3 + sizeof(KppChunk)) * (size_t)nch +
-           sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64 + 4096 * 8 + sizeof(double) * (size_t)N;
+           sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64 + 4096 * 8 + sizeof(double) * (size_t)N +
+           2 * sizeof(int64_t) * (size_t)N;
 }
 
 }  // namespace lshkm
