@@ -23,16 +23,19 @@
 //   kpp_chunk_scan_kernel   approximate chunk starts (exclusive scan)
 //   kpp_chunk_units_kernel  guess each chunk's binade from its approximate
 //                           start; R = sum of RN_u(q) in units of u, or
-//                           "dirty" (tie, non-finite, crossing, tiny start)
+//                           "dirty" (tie, non-finite, tiny start); chunks
+//                           predicted to cross a binade, or holding a tie,
+//                           also get prefix arrays in binades e and e + 1
 //   kpp_chain_kernel        one wave walks the chunks with the EXACT running
 //                           s: a chunk whose guess is right (s in binade e and
-//                           s/u + R < 2^53) advances s by R*u exactly, 64
-//                           chunks per wave-wide integer scan; any other chunk
-//                           (the first, ~log2(N) binade crossings, ties) is
-//                           summed element by element with hardware fp64 adds
-//   kpp_expand_kernel       writes s_m = s_start + u * prefix for the
-//                           integer-resolved chunks
-//   kpp_choose_kernel       the draw and the reference's binary search
+//                           s/u + R < 2^53) advances s by R*u exactly, 512
+//                           chunks per wave-wide integer scan; a crossing or
+//                           tie chunk is resolved from its prefix arrays with
+//                           one hardware add per crossing / tie row; the rest
+//                           (the first chunk, unresolvable rows) by hardware
+//                           fp64 adds row by row. Then the draw and the
+//                           reference's binary search, the prefix sums formed
+//                           only for the chunk the draw lands in.
 #include <climits>
 #include <cstdlib>
 #include <cstring>
@@ -465,8 +468,9 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const doub
 __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict__ qbuf, int64_t N,
                                                        const KppChunk* __restrict__ meta, int64_t nch,
                                                        const int64_t* __restrict__ pa, const int64_t* __restrict__ pb,
-                                                       double* __restrict__ chunk_s, int32_t* __restrict__ chunk_mode,
-                                                       double* __restrict__ cum, unsigned long long* __restrict__ stats) {
+                                                       double* chunk_s, int32_t* chunk_mode,
+                                                       double* cum, const double* __restrict__ canon, int it,
+                                                       int32_t* __restrict__ chosen, unsigned long long* __restrict__ stats) {
     constexpr int CPL = 8;                         // chunks per lane per step
     constexpr int STEP = 64 * CPL;
     constexpr int WIN = 2 * STEP;                  // chunk metadata staged in LDS (16 KB)
@@ -680,6 +684,71 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
         base = c + 1;
         nseq++;
     }
+    // ---- (4) the draw (:127-149): rd = uniform_real(0, total) = canon * (total -
+    // 0) + 0, then the reference's binary search = the first row whose prefix
+    // sum reaches rd (the sums never decrease, rd <= total; a NaN total from
+    // degenerate minima gives rd NaN and row 0). The prefix sums are never
+    // materialised: the chunk by a 64-ary search over the chunk ends, then its
+    // rows (the walk wrote a stop chunk's; an integer chunk's are formed here).
+    {
+        __threadfence();                           // this wave's chunk_s / cum stores, visible to its loads
+        const double total = s;
+        const double rd = __dadd_rn(__dmul_rn(canon[it], __dsub_rn(total, 0.0)), 0.0);
+        int64_t pick = 0;
+        if (rd > qbuf[0]) {                        // cum[0] = 0 + q_0 = q_0
+            auto chunk_end = [&](int64_t cc) -> double { return cc + 1 < nch ? chunk_s[cc + 1] : total; };
+            int64_t lo = 0, hi = nch;              // the first chunk whose end reaches rd lies in [lo, hi)
+            while (hi - lo > 64) {
+                const int64_t step = (hi - lo + 63) / 64;
+                const int64_t p = lo + (int64_t)(lane + 1) * step - 1;
+                const bool ge = p >= hi - 1 || chunk_end(p) >= rd;
+                const unsigned long long b = __ballot(ge);
+                const int f = __ffsll((long long)b) - 1;          // lane 63 always qualifies
+                const int64_t nlo = f > 0 ? lo + (int64_t)f * step : lo;
+                const int64_t nhi = lo + (int64_t)(f + 1) * step;
+                lo = nlo;
+                hi = nhi < hi ? nhi : hi;
+            }
+            const bool ge = lo + lane >= hi - 1 || chunk_end(lo + lane) >= rd;
+            const int64_t cs_ = lo + (__ffsll((long long)__ballot(ge)) - 1);
+            // rows of chunk cs_
+            const int64_t r0 = cs_ * KPP_CHUNK;
+            const int n = (int)(N - r0 < KPP_CHUNK ? N - r0 : KPP_CHUNK);
+            constexpr int EPL = KPP_CHUNK / 64;
+            double v[EPL];
+            if (chunk_mode[cs_] != 0) {
+#pragma unroll
+                for (int t = 0; t < EPL; t++) {
+                    const int i = lane * EPL + t;
+                    v[t] = cum[r0 + (i < n ? i : n - 1)];
+                }
+            } else {
+                const int e = meta[cs_].e;
+                const int64_t su = (int64_t)ldexp(chunk_s[cs_], 52 - e);
+                int64_t r[EPL], own = 0;
+#pragma unroll
+                for (int t = 0; t < EPL; t++) {
+                    const int i = lane * EPL + t;
+                    r[t] = i < n ? kpp_units(qbuf[r0 + i], e) : 0;
+                    own += r[t];
+                }
+                int64_t run = su + wave_incl_scan64(own, lane) - own;
+#pragma unroll
+                for (int t = 0; t < EPL; t++) {
+                    run += r[t];
+                    v[t] = ldexp((double)run, e - 52);
+                }
+            }
+            int lf = EPL;
+#pragma unroll
+            for (int t = 0; t < EPL; t++)
+                if (lf == EPL && lane * EPL + t < n && v[t] >= rd) lf = t;
+            const unsigned long long b = __ballot(lf < EPL);
+            const int fl = b ? __ffsll((long long)b) - 1 : 63;      // b != 0: the chunk's end reaches rd
+            pick = r0 + fl * EPL + __builtin_amdgcn_readlane(lf, fl);
+        }
+        if (lane == 0) chosen[it] = (int32_t)pick;
+    }
 #if defined(KPP_PROF)
     if (lane == 0) printf("KPPPROF %llu %llu %llu %llu %llu %llu %llu\n", tp[0], tp[1], tp[2], tp[3], tp[4], nseq, npass);
 #endif
@@ -687,63 +756,6 @@ __global__ __launch_bounds__(64) void kpp_chain_kernel(const double* __restrict_
         atomicAdd(stats + STAT_KPP_CHUNKS, (unsigned long long)nch);
         atomicAdd(stats + STAT_KPP_SEQ, nseq);
     }
-}
-
-// s_m = s_start + u * (inclusive prefix of RN_u(q)) for the integer-resolved chunks.
-__global__ __launch_bounds__(KPP_THREADS) void kpp_expand_kernel(const double* __restrict__ qbuf, int64_t N,
-                                                                 const KppChunk* __restrict__ meta,
-                                                                 const double* __restrict__ chunk_s,
-                                                                 const int32_t* __restrict__ chunk_mode,
-                                                                 double* __restrict__ cum) {
-    constexpr int PER = KPP_CHUNK / KPP_THREADS;
-    __shared__ long long wsum[KPP_THREADS / 64];
-    if (chunk_mode[blockIdx.x] != 0) return;
-    const int e = meta[blockIdx.x].e;
-    const int64_t s_units = (int64_t)ldexp(chunk_s[blockIdx.x], 52 - e);
-    const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
-    // thread t owns rows c0 + t*PER .. +PER-1 (contiguous, so the scan is in row order)
-    int64_t r[PER];
-    int64_t own = 0;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int64_t row = c0 + threadIdx.x * PER + k;
-        r[k] = row < N ? kpp_units(qbuf[row], e) : 0;
-        own += r[k];
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int64_t pre = own;
-    for (int off = 1; off < 64; off <<= 1) {
-        const int64_t o = __shfl_up(pre, off);
-        if (lane >= off) pre += o;
-    }
-    if (lane == 63) wsum[w] = pre;
-    __syncthreads();
-    int64_t run = s_units + pre - own;
-    for (int i = 0; i < w; i++) run += wsum[i];
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int64_t row = c0 + threadIdx.x * PER + k;
-        run += r[k];
-        if (row < N) cum[row] = ldexp((double)run, e - 52);
-    }
-}
-
-// --------------------------------------------------------------------- (4)
-__global__ void kpp_choose_kernel(const double* __restrict__ cum, int64_t N, const double* __restrict__ canon, int it,
-                                  int32_t* __restrict__ chosen) {
-    // uniform_real_distribution<double>(0, total): canon * (b - a) + a
-    const double total = cum[N - 1];
-    const double rd = __dadd_rn(__dmul_rn(canon[it], __dsub_rn(total, 0.0)), 0.0);
-    int64_t left = 0, right = N - 1, pick = 0;
-    if (rd > cum[left]) {
-        while (right - left > 1) {
-            const int64_t m = left + (right - left) / 2;
-            if (rd <= cum[m]) right = m;
-            else left = m;
-        }
-        pick = right;
-    }
-    chosen[it] = (int32_t)pick;
 }
 
 // Runs iterations 1..K-1; chosen[0] and canon[1..K-1] are already on the device.
@@ -791,9 +803,8 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
         hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum, qbuf);
         hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, csum, nch, cstart);
         hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, cstart, nch, meta, pa, pb);
-        hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, qbuf, N, meta, nch, pa, pb, cs, mode, cum, stats);
-        hipLaunchKernelGGL(kpp_expand_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, meta, cs, mode, cum);
-        hipLaunchKernelGGL(kpp_choose_kernel, dim3(1), dim3(1), 0, s, cum, N, canon, it, chosen);
+        hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, qbuf, N, meta, nch, pa, pb, cs, mode, cum, canon, it,
+                           chosen, stats);
         const int rc = kstatus("kmeanspp.hip");
         if (rc) return rc;
     }
