@@ -19,8 +19,9 @@
 // in one binade [2^e, 2^(e+1)) every s is a multiple of u = 2^(e-52), so
 // RN(s + q) = s + u * RN_u(q) unless q is a tie (q/u = k + 1/2) — the chain is
 // an integer prefix sum there. Rows are cut into chunks of KPP_CHUNK:
-//   kpp_chunk_sum_kernel    approximate chunk sums (any order)
-//   kpp_chunk_scan_kernel   approximate chunk starts (exclusive scan)
+//   kpp_scan_kernel         the max of the minima; approximate chunk sums (the
+//                           distance pass's sum m^2 per 256 rows / max^2) and
+//                           their exclusive scan: approximate chunk starts
 //   kpp_chunk_units_kernel  guess each chunk's binade from its approximate
 //                           start; R = sum of RN_u(q) in units of u, or
 //                           "dirty" (tie, non-finite, tiny start); chunks
@@ -130,18 +131,19 @@ __device__ inline void kpp_block_max(double best, unsigned long long* __restrict
     }
 }
 
-__global__ __launch_bounds__(1024) void kpp_max_reduce_kernel(const unsigned long long* __restrict__ bmax, int nb,
-                                                              unsigned long long* __restrict__ mx_bits) {
-    __shared__ unsigned long long red[1024];
-    unsigned long long m = 0;
-    for (int i = threadIdx.x; i < nb; i += 1024) m = bmax[i] > m ? bmax[i] : m;
-    red[threadIdx.x] = m;
+// Sum of the block's m^2 (any order: only the chunk guesses use it) for its
+// 256-row group g. Every thread of the block calls it.
+__device__ inline void kpp_group_sum(double v, double* __restrict__ gsum, int64_t g) {
+    __shared__ double wsum[KPP_THREADS / 64];
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
     __syncthreads();
-    for (int off = 512; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off && red[threadIdx.x + off] > red[threadIdx.x]) red[threadIdx.x] = red[threadIdx.x + off];
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < KPP_THREADS / 64; w++) t += wsum[w];
+        gsum[g] = t;
     }
-    if (threadIdx.x == 0) *mx_bits = red[0];
+    __syncthreads();
 }
 
 // TX: fp32 or fp64 rows (VEC only for fp32).
@@ -149,7 +151,8 @@ template <int METRIC, bool VEC, typename TX>
 __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restrict__ X, int64_t N, int d,
                                                                const int32_t* __restrict__ chosen, int it,
                                                                double* __restrict__ mind,
-                                                               unsigned long long* __restrict__ bmax) {
+                                                               unsigned long long* __restrict__ bmax,
+                                                               double* __restrict__ gsum) {
     static_assert(!VEC || sizeof(TX) == 4, "the float4 form reads fp32 rows");
     constexpr int DJ = sizeof(TX) == 4 ? KPP_DJ : KPP_DJ / 2;     // tile <= 34 KiB either way
     __shared__ TX tile[KPP_THREADS][DJ + 1];
@@ -230,7 +233,8 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
                 }
             }
         }
-        if (n >= N) continue;
+        double m = 0.0;
+        if (n < N) {
         double dd;
         if (METRIC == 0) {
 #if defined(ABL_KPP_NOCHAIN)
@@ -241,13 +245,15 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
             const double denom = __dmul_rn(sqrt(a), sqrt(cb));
             dd = one_minus(x87_quot(ip.value(), denom));
         }
-        double m = dd;
+        m = dd;
         if (it > 1) {
             const double prev = mind[n];
             if (!(dd < prev)) m = prev;
         }
         mind[n] = m;
         if (m > best) best = m;
+        }
+        kpp_group_sum(m * m, gsum, row0 / KPP_THREADS);
     }
     kpp_block_max(best, bmax);
 }
@@ -259,14 +265,18 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
 __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* __restrict__ X, int64_t N, int d,
                                                                    const int32_t* __restrict__ chosen, int it,
                                                                    double* __restrict__ mind,
-                                                                   unsigned long long* __restrict__ bmax) {
+                                                                   unsigned long long* __restrict__ bmax,
+                                                                   double* __restrict__ gsum) {
     extern __shared__ __attribute__((aligned(8))) char kpp_dyn2[];
     float* cs = reinterpret_cast<float*>(kpp_dyn2);     // [d]
     const float* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
     for (int j = threadIdx.x; j < d; j += KPP_THREADS) cs[j] = c[j];
     __syncthreads();
     double best = 0.0;
-    for (int64_t n = (int64_t)blockIdx.x * KPP_THREADS + threadIdx.x; n < N; n += (int64_t)gridDim.x * KPP_THREADS) {
+    for (int64_t row0 = (int64_t)blockIdx.x * KPP_THREADS; row0 < N; row0 += (int64_t)gridDim.x * KPP_THREADS) {
+        const int64_t n = row0 + threadIdx.x;
+        double m = 0.0;
+        if (n < N) {
         const float* xr = X + n * d;
         float4 cur[8], nxt[8];
 #pragma unroll
@@ -290,58 +300,50 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* 
             for (int u = 0; u < 8; u++) cur[u] = nxt[u];
         }
         const double dd = sqrt(acc);
-        double m = dd;
+        m = dd;
         if (it > 1) {
             const double prev = mind[n];
             if (!(dd < prev)) m = prev;
         }
         mind[n] = m;
         if (m > best) best = m;
+        }
+        kpp_group_sum(m * m, gsum, row0 / KPP_THREADS);
     }
     kpp_block_max(best, bmax);
 }
 
 // --------------------------------------------------------------------- (3)
-__device__ inline double block_sum_f64(double v, double* red) {
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    double t = 0.0;
-    for (int i = 0; i < KPP_THREADS / 64; i++) t += red[i];
-    return t;
-}
-
-// also writes q_m (one division per row for all the passes below)
-__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_sum_kernel(const double* __restrict__ mind, int64_t N,
-                                                                    const unsigned long long* __restrict__ mx_bits,
-                                                                    double* __restrict__ chunk_sum,
-                                                                    double* __restrict__ qbuf) {
-    __shared__ double red[KPP_THREADS / 64];
-    const double mx = kpp_max(mx_bits);
-    const int64_t c0 = (int64_t)blockIdx.x * KPP_CHUNK;
-    double v = 0.0;
-    for (int e = threadIdx.x; e < KPP_CHUNK; e += KPP_THREADS)
-        if (c0 + e < N) {
-            const double q = kpp_q(mind[c0 + e], mx);
-            qbuf[c0 + e] = q;
-            v += q;
-        }
-    const double t = block_sum_f64(v, red);
-    if (threadIdx.x == 0) chunk_sum[blockIdx.x] = t;
-}
-
-// Exclusive scan of the approximate chunk sums (one block; order irrelevant).
+// One block: the max of the minima (from the per-block maxima, written to
+// mx_bits for the exact q_m), then the approximate chunk sums sum m^2 / max^2
+// (two 256-row groups per chunk) and their exclusive scan (order irrelevant:
+// guesses only).
 constexpr int KPP_SCAN_THREADS = 1024;
+static_assert(KPP_CHUNK == 2 * KPP_THREADS, "two row groups per chunk");
 
-__global__ __launch_bounds__(KPP_SCAN_THREADS) void kpp_chunk_scan_kernel(const double* __restrict__ chunk_sum,
-                                                                          int64_t nch, double* __restrict__ chunk_start) {
+__global__ __launch_bounds__(KPP_SCAN_THREADS) void kpp_scan_kernel(const unsigned long long* __restrict__ bmax, int nb,
+                                                                    const double* __restrict__ gsum, int64_t ngroups,
+                                                                    int64_t nch, unsigned long long* __restrict__ mx_bits,
+                                                                    double* __restrict__ chunk_start) {
+    __shared__ unsigned long long redm[KPP_SCAN_THREADS];
     __shared__ double part[KPP_SCAN_THREADS];
+    unsigned long long mb = 0;
+    for (int i = threadIdx.x; i < nb; i += KPP_SCAN_THREADS) mb = bmax[i] > mb ? bmax[i] : mb;
+    redm[threadIdx.x] = mb;
+    __syncthreads();
+    for (int off = KPP_SCAN_THREADS / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off && redm[threadIdx.x + off] > redm[threadIdx.x]) redm[threadIdx.x] = redm[threadIdx.x + off];
+        __syncthreads();
+    }
+    const unsigned long long mxb = redm[0];
+    if (threadIdx.x == 0) *mx_bits = mxb;
+    const double mx = __longlong_as_double((long long)mxb);
+    const double inv = 1.0 / (mx * mx);
+    auto csum = [&](int64_t c) { return (gsum[2 * c] + (2 * c + 1 < ngroups ? gsum[2 * c + 1] : 0.0)) * inv; };
     const int64_t per = (nch + KPP_SCAN_THREADS - 1) / KPP_SCAN_THREADS;
     const int64_t lo = threadIdx.x * per, hi = lo + per < nch ? lo + per : nch;
     double v = 0.0;
-    for (int64_t c = lo; c < hi; c++) v += chunk_sum[c];
+    for (int64_t c = lo; c < hi; c++) v += csum(c);
     part[threadIdx.x] = v;
     __syncthreads();
     for (int off = 1; off < KPP_SCAN_THREADS; off <<= 1) {   // inclusive scan of the partials
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(KPP_SCAN_THREADS) void kpp_chunk_scan_kernel(const 
     double run = threadIdx.x ? part[threadIdx.x - 1] : 0.0;
     for (int64_t c = lo; c < hi; c++) {
         chunk_start[c] = run;
-        run += chunk_sum[c];
+        run += csum(c);
     }
 }
 
@@ -398,7 +400,9 @@ __device__ inline int64_t kpp_units_c(double q, int e, int& cls) {
 // e + 1 (pa, pb), so the walk resolves it with one hardware add per crossing
 // or tie row instead of element by element. Thread t owns rows 2t, 2t+1 (row
 // order for the scans).
-__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const double* __restrict__ qbuf, int64_t N,
+__global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const double* __restrict__ mind, int64_t N,
+                                                                      const unsigned long long* __restrict__ mx_bits,
+                                                                      double* __restrict__ qbuf,
                                                                       const double* __restrict__ chunk_start, int64_t nch,
                                                                       KppChunk* __restrict__ meta,
                                                                       int64_t* __restrict__ pa, int64_t* __restrict__ pb) {
@@ -412,7 +416,11 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_chunk_units_kernel(const doub
     const bool usable = a >= 0x1p-900 && a < 0x1p62;
     const int e = usable ? kpp_binade(a) : 0;
     const int64_t i0 = c0 + 2 * threadIdx.x;
-    const double q0 = i0 < N ? qbuf[i0] : 0.0, q1 = i0 + 1 < N ? qbuf[i0 + 1] : 0.0;
+    // q_m = (min_m / max)^2 (:121-124), stored for the walk
+    const double mx = kpp_max(mx_bits);
+    const double q0 = i0 < N ? kpp_q(mind[i0], mx) : 0.0, q1 = i0 + 1 < N ? kpp_q(mind[i0 + 1], mx) : 0.0;
+    if (i0 < N) qbuf[i0] = q0;
+    if (i0 + 1 < N) qbuf[i0 + 1] = q1;
     int ca0, ca1;
     const int64_t ra0 = kpp_units_c(q0, e, ca0), ra1 = kpp_units_c(q1, e, ca1);
     long long v = ra0 + ra1;
@@ -768,7 +776,8 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
     char* p = (char*)ws;
     double* mind = (double*)p;                 p += sizeof(double) * N;
     double* cum = (double*)p;                  p += sizeof(double) * N;
-    double* csum = (double*)p;                 p += sizeof(double) * nch;
+    const int64_t ngroups = (N + KPP_THREADS - 1) / KPP_THREADS;
+    double* gsum = (double*)p;                 p += sizeof(double) * ((ngroups + 1) & ~1ll);   // per 256-row group sum m^2
     double* cstart = (double*)p;               p += sizeof(double) * nch;
     KppChunk* meta = (KppChunk*)p;             p += sizeof(KppChunk) * nch;
     double* cs = (double*)p;                   p += sizeof(double) * nch;
@@ -787,22 +796,21 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
         const dim3 g(dgrid), b(KPP_THREADS);
         const size_t ld32 = (size_t)d * 4, ld64 = (size_t)d * 8;     // the centroid row in LDS
         if (X.f64) {
-            if (metric == 0) hipLaunchKernelGGL((kpp_dist_kernel<0, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax);
-            else hipLaunchKernelGGL((kpp_dist_kernel<1, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax);
+            if (metric == 0) hipLaunchKernelGGL((kpp_dist_kernel<0, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax, gsum);
+            else hipLaunchKernelGGL((kpp_dist_kernel<1, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax, gsum);
         } else if (metric == 0 && vec && kpp_reg)
-            hipLaunchKernelGGL(kpp_dist_reg_kernel, g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
+            hipLaunchKernelGGL(kpp_dist_reg_kernel, g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
         else if (metric == 0 && vec)
-            hipLaunchKernelGGL((kpp_dist_kernel<0, true, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
+            hipLaunchKernelGGL((kpp_dist_kernel<0, true, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
         else if (metric == 0)
-            hipLaunchKernelGGL((kpp_dist_kernel<0, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
+            hipLaunchKernelGGL((kpp_dist_kernel<0, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
         else if (vec)
-            hipLaunchKernelGGL((kpp_dist_kernel<1, true, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
+            hipLaunchKernelGGL((kpp_dist_kernel<1, true, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
         else
-            hipLaunchKernelGGL((kpp_dist_kernel<1, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax);
-        hipLaunchKernelGGL(kpp_max_reduce_kernel, dim3(1), dim3(1024), 0, s, bmax, (int)dgrid, mx);
-        hipLaunchKernelGGL(kpp_chunk_sum_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, csum, qbuf);
-        hipLaunchKernelGGL(kpp_chunk_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, csum, nch, cstart);
-        hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, qbuf, N, cstart, nch, meta, pa, pb);
+            hipLaunchKernelGGL((kpp_dist_kernel<1, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
+        hipLaunchKernelGGL(kpp_scan_kernel, dim3(1), dim3(KPP_SCAN_THREADS), 0, s, bmax, (int)dgrid, gsum, ngroups, nch, mx, cstart);
+        hipLaunchKernelGGL(kpp_chunk_units_kernel, dim3((unsigned)nch), dim3(KPP_THREADS), 0, s, mind, N, mx, qbuf, cstart, nch, meta,
+                           pa, pb);
         hipLaunchKernelGGL(kpp_chain_kernel, dim3(1), dim3(64), 0, s, qbuf, N, meta, nch, pa, pb, cs, mode, cum, canon, it,
                            chosen, stats);
         const int rc = kstatus("kmeanspp.hip");
@@ -813,7 +821,9 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
 
 size_t kmeans_pp_ws_bytes(int64_t N) {
     const int64_t nch = (N + KPP_CHUNK - 1) / KPP_CHUNK;
-    return sizeof(double) * 2 * (size_t)N + (sizeof(double) * 3 + sizeof(KppChunk)) * (size_t)nch +
+    const int64_t ngroups = (N + KPP_THREADS - 1) / KPP_THREADS;
+    return sizeof(double) * 2 * (size_t)N + sizeof(double) * (size_t)((ngroups + 1) & ~1ll) +
+           (sizeof(double) * 2 + sizeof(KppChunk)) * (size_t)nch +
            sizeof(int32_t) * (size_t)((nch + 1) & ~1ll) + 64 + 4096 * 8 + sizeof(double) * (size_t)N +
            2 * sizeof(int64_t) * (size_t)N;
 }
