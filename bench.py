@@ -39,6 +39,9 @@ D, L_TABLES, K_FUNCS, W, BUCKET_DIV, SEED_DATA, SEED_PARAMS = 128, 5, 4, 0.4, 10
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 F16_MFMA_PEAK_TFS = 2500.0     # MI355X_MICROARCH.md: FP16/BF16 MFMA dense peak
 METRIC = "point hash+assign ops/sec at d=128, N=10M, K=256; 1/2/4/8 MI355X"
+DTYPE = ("fp32 points; split-f16 MFMA scores (f32 accumulate); tuples, bucket IDs and cluster IDs bit-exact "
+         "(x87-exact hashing, certified argmin); distances: certified f32, <= 2^-20 relative to the reference's "
+         "fp64 (north star: 1e-5), LSHKM_DIST=exact for the reference-order fp64 chain (exactness.exact_distances)")
 # algorithmic bytes per point of the fused pass: 512 B read, 80 B
 # tuples + 20 B bucket IDs + 4 B cluster ID + 8 B distance written
 BYTES_PER_PT = 4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES + 4 + 8
@@ -239,6 +242,8 @@ def main():
     ap.add_argument("--workload", choices=["c3", "c5"], default="c3")
     ap.add_argument("--k", type=int, default=None, help="centroids (default 256 for c3, 1024 for c5)")
     ap.add_argument("--no-c5", action="store_true", help="c3: leave out the C5 iteration object")
+    ap.add_argument("--no-exact-dist-line", dest="exact_dist_line", action="store_false",
+                    help="c3: leave out the timing with bit-exact (fp64 chain) distances")
     ap.add_argument("--dry-run", action="store_true", help="gloo on CPU, no GPU work (tests the rank plumbing)")
     ap.add_argument("--cpu-port-hash-sample", type=int, default=400_000)
     ap.add_argument("--cpu-port-assign-sample", type=int, default=300_000)
@@ -298,7 +303,7 @@ def main():
         src_p = src.ctypes.data_as(C.c_void_p)
 
         def step():
-            # one pass: tuples + bucket IDs + cluster IDs + fp64 distances (lshkm_hash_assign)
+            # one pass: tuples + bucket IDs + cluster IDs + distances (lshkm_hash_assign)
             lk._ck(lib.lshkm_hash_assign(lsh.h, p(X), N, p(Cc), K, src_p, p(tuples), None, p(bucket), p(assign),
                                          p(dist_)))
         ctx.reset_stats()
@@ -307,6 +312,17 @@ def main():
               "hash_fixup_rows": ctx.stat(lk.STAT_HASH_FIX) // (args.steps + args.warmup),
               "hash_exact_fallbacks": ctx.stat(lk.STAT_HASH_EXACT) // (args.steps + args.warmup)}
         kms = fused_kernel_ms(lk, lib, ctx, step, max(3, args.steps))
+        if args.exact_dist_line:
+            # the same step with every distance from the reference-order fp64 chain
+            os.environ["LSHKM_DIST"] = "exact"
+            try:
+                el_x = timed(step, args.steps, args.warmup, world, dev)
+                kms_x = fused_kernel_ms(lk, lib, ctx, step, max(3, args.steps))
+            finally:
+                os.environ.pop("LSHKM_DIST", None)
+            ex["exact_distances"] = {"note": "LSHKM_DIST=exact: bit-exact distances (the reference's fp64 chain)",
+                                     "value": N_total * args.steps / el_x, "ms_per_step": el_x / args.steps * 1e3,
+                                     "kernel_ms": kms_x, "frac": 624.0 * N / (kms_x * 1e-3) / 8e12}
         return elapsed, kms, ex
 
     def c5_run(K):
@@ -341,7 +357,7 @@ def main():
         line = c5_object(K, el, kms, xms)
         line.update({"metric": METRIC + " (C5 workload)", "unit": "point hash+assign ops/s", "steps": args.steps,
                      "warmup": args.warmup, "higher_is_better": True, "vs_baseline": None,
-                     "dtype": "fp32 points; split-f16 MFMA scores (f32 accumulate), fp64/x87-exact results",
+                     "dtype": DTYPE,
                      "data": "synthetic (include/lshkm_synth.h), resident in HBM"})
     else:
         K = args.k or 256
@@ -350,7 +366,7 @@ def main():
             "metric": METRIC, "value": N_total * args.steps / el, "unit": "point hash+assign ops/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32 points; split-f16 MFMA scores (f32 accumulate), fp64/x87-exact results",
+            "dtype": DTYPE,
             "data": "synthetic (include/lshkm_synth.h), resident in HBM",
             "config": {"workload": f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128",
                        "N_per_gpu": N, "N_total": N_total, "d": D, "K": K, "L": L_TABLES, "k": K_FUNCS,

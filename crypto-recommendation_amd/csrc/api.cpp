@@ -485,12 +485,14 @@ static int assign_path(int metric, int d, int K, bool f64) {
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
-// LSHKM_DIST=fast: euclidean winner distances (d = 128 fused path) from f32(c)
-// in f32, certified to 2^-20 relative -- inside the 1e-5 the north star sets for
-// distances; cluster IDs stay bit-exact. Default: the reference-order fp64 chain.
+// Euclidean winner distances of the hi-only pass (fp32 rows): from f32(c) in
+// f32, certified to 2^-20 relative -- inside the 1e-5 relative the north star
+// sets for float distances; cluster IDs stay bit-exact, and a row whose bound
+// fails gets the reference-order fp64 chain. LSHKM_DIST=exact: the
+// reference-order fp64 chain for every row (bit-exact distances).
 static bool fast_dist_on() {
     const char* e = getenv("LSHKM_DIST");
-    return e && !strcmp(e, "fast");
+    return !(e && !strcmp(e, "exact"));
 }
 
 // Exact reference-order pass over the rows listed in ws_ambig (count on device).
@@ -564,8 +566,8 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
         float* cnh = cbound + 8;
         double* nbv = (double*)(cnh + Kpad);               // cosine: [Kpad] sequential |c|^2 (Kpad % 64 == 0: aligned)
-        // euclidean winner distances: the certified f32 form (LSHKM_DIST=fast) or the
-        // reference-order fp64 chain (default)
+        // euclidean winner distances: the certified f32 form (default) or the
+        // reference-order fp64 chain (LSHKM_DIST=exact)
         const bool fast = !cosine && rows_kind != 2 && fast_dist_on();
         float* C32 = nullptr;
         float* rn32 = nullptr;

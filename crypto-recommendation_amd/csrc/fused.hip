@@ -1353,7 +1353,11 @@ __device__ inline void glds16(const void* gsrc, uint32_t lds_dst) {
 // them). fp64 rows: the scores use xh = f16(f32(x)); |x - f32(x)| <= 2^-24 |x|
 // joins |xr| in the bound; the winner chain re-reads the fp64 row (the
 // register copy is f32).
-template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1, bool GATH = false, int ROWS = 0>
+// FAST (euclidean, one pass, fp32 rows): the certified f32 winner distance
+// compiled in (no fp64 chain state). Its f32 centroid rows are register loads:
+// through the gather ring (GATH) each 16-dim step waits on its DMA, and the
+// short f32 sum cannot hide that (fused pass 2.21 vs 2.14 ms at C3).
+template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1, bool GATH = false, int ROWS = 0, bool FAST = false>
 __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_kernel(FusedArgs a) {
     constexpr int FH_WAVES = fh_waves<HASH, MP, MET>();
     constexpr int FH_THREADS = 64 * FH_WAVES;
@@ -1362,8 +1366,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     static_assert(ROWS == 0 || (!HASH && !MP && NIMG == 1), "general rows: Lloyd without hashing, one pass");
     // the gather's explicit vmcnt waits assume no other vector loads in the chain
     static_assert(!(GATH && ROWS == 2), "fp64 rows re-read x in the chain: register loads of the winner rows");
+    static_assert(!FAST || (MET == 0 && ROWS != 2 && !MP && NIMG == 1 && !GATH), "fast distance: euclidean single pass, fp32 rows");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
+    const bool fastd = FAST || a.fast_dist != 0;
     const int KI = NIMG == 2 ? FH_KMAX : Kpad;           // centroid rows the LDS image holds
     int* lcount = reinterpret_cast<int*>(smem);          // [0] uncertified rows, [1] hash fix-up rows, [2] cosine declines
     _Float16* lch = reinterpret_cast<_Float16*>(smem + 16);
@@ -1710,7 +1716,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         uint32_t gbase = 0;
         const bool g32 = GATH && a.C32 != nullptr && __float_as_uint(a.cbound[7]) == 0u;
         const int gstep = g32 ? 64 : 128;                // bytes of one 16-dim step of a row
-        if (GATH && !a.fast_dist) {
+        if (GATH && !fastd) {
             gbase = (uint32_t)__builtin_amdgcn_readfirstlane(
                 (int)((uint32_t)(uintptr_t)(smem + fh_gath_off(Kpad, HASH)) + (uint32_t)wave * FH_GATH_WAVE));
             if (g32) {
@@ -1738,6 +1744,50 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                     for (int u = 0; u < 4; u++) glds16(gsrc[u] + gstep * s0, gbase + s0 * FH_GATH_STEP + u * 1024);
             }
         }
+        // GATH: a step's values come from the ring one step early (the LDS read
+        // overlaps the previous step's chain), the ring slot is refilled two
+        // steps ahead as soon as it is read
+        double2 gnext[4];
+        float4 gnext32[2];                    // g32: raw f32 chunks, widened when used
+        auto gread = [&](int st) {
+            const char* ring = smem + fh_gath_off(Kpad, HASH) + wave * FH_GATH_WAVE + (st & 1) * FH_GATH_STEP;
+            if (g32) {
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    gnext32[j] = *reinterpret_cast<const float4*>(ring + (col >> 4) * 1024 + (col & 15) * 64 +
+                                                                  16 * ((2 * h + j) ^ ((col >> 2) & 3)));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    gnext[j] = *reinterpret_cast<const double2*>(ring + col * 128 + 16 * ((4 * h + j) ^ ((col >> 1) & 7)));
+            }
+        };
+        // vmcnt(n): all but the wave's n youngest vector-memory operations done
+        // (one step's pieces: 2 for g32, else 4)
+        auto wait_step = [&]() {
+            if (g32) __builtin_amdgcn_s_waitcnt(0x0F72);                   // vmcnt(2)
+            else __builtin_amdgcn_s_waitcnt(0x0F74);                       // vmcnt(4)
+        };
+        // ring step s consumed: slot s & 1 refilled with step s + 2, step s + 1 read
+        auto ring_advance = [&](int s) {
+            if (s + 2 < 8) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);                        // lgkmcnt(0): slot s & 1 is read
+                asm volatile("" ::: "memory");
+                if (g32) {
+#pragma unroll
+                    for (int u = 0; u < 2; u++) glds16(gsrc[u] + gstep * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) glds16(gsrc[u] + gstep * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
+                }
+            }
+            if (s + 1 < 8) {
+                if (s + 2 < 8) wait_step();                                // step s + 1 landed
+                else __builtin_amdgcn_s_waitcnt(0x0F70);                    // vmcnt(0)
+                asm volatile("" ::: "memory");
+                gread(s + 1);
+            }
+        };
         // fp64 rows: the chain's x values re-read (mostly L2) four 16-dim steps
         // ahead (one step ahead left the chain waiting ~8 round trips per tile)
         constexpr int XD = 4;
@@ -1748,7 +1798,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
             for (int st = 0; st < XD; st++) load_x64_step(a, rowc, st, h, xring[st]);
         }
         double2 cbuf[CHAIN_PF][4];
-        if (MET == 0 && !GATH && !a.fast_dist) {
+        if (MET == 0 && !GATH && !fastd) {
 #pragma unroll
             for (int s = 0; s < CHAIN_PF; s++)
 #pragma unroll
@@ -1757,7 +1807,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #endif
         const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
 
-        // euclidean fast distance (a.fast_dist): the winner's distance from f32(c)
+        // euclidean fast distance (fastd): the winner's distance from f32(c)
         // in f32 with every lane busy, certified to 2^-20 relative (DESIGN.md §5:
         // 8 accumulators per lane, <= 12 roundings per sum, plus the f32(c)
         // residual |c - f32(c)| of the centroid); a row whose bound fails is
@@ -1765,7 +1815,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         bool dok = true;
         double fdist = 0.0;
         if constexpr (MET == 0) {
-            if (a.fast_dist) {
+            if (fastd) {
                 const float* c32 = a.C32 + (size_t)I1 * FU_D + 8 * h;
                 float2v q[4] = {};
 #pragma unroll
@@ -1822,7 +1872,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                 base = __shfl(base, leader);
                 if (fix) cfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
             }
-        } else if (a.fast_dist) {
+        } else if (fastd) {
             if (h == 1 && valid && cert && dok) {
                 a.assign[row] = I1;
                 a.dist[row] = fdist;
@@ -1841,30 +1891,6 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #if defined(ABL_CHAIN_TREE)
             double tacc[4] = {0.0, 0.0, 0.0, 0.0};
 #endif
-            // GATH: a step's values come from the ring one step early (the LDS read
-            // overlaps the previous step's chain), the ring slot is refilled two
-            // steps ahead as soon as it is read
-            double2 gnext[4];
-            float4 gnext32[2];                // g32: raw f32 chunks, widened when used
-            auto gread = [&](int st) {
-                const char* ring = smem + fh_gath_off(Kpad, HASH) + wave * FH_GATH_WAVE + (st & 1) * FH_GATH_STEP;
-                if (g32) {
-#pragma unroll
-                    for (int j = 0; j < 2; j++)
-                        gnext32[j] = *reinterpret_cast<const float4*>(ring + (col >> 4) * 1024 + (col & 15) * 64 +
-                                                                      16 * ((2 * h + j) ^ ((col >> 2) & 3)));
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        gnext[j] = *reinterpret_cast<const double2*>(ring + col * 128 + 16 * ((4 * h + j) ^ ((col >> 1) & 7)));
-                }
-            };
-            // vmcnt(n): all but the wave's n youngest vector-memory operations done
-            // (one step's pieces: 2 for g32, else 4)
-            auto wait_step = [&]() {
-                if (g32) __builtin_amdgcn_s_waitcnt(0x0F72);               // vmcnt(2)
-                else __builtin_amdgcn_s_waitcnt(0x0F74);                   // vmcnt(4)
-            };
             if constexpr (GATH) {
                 wait_step();                                               // step 0 landed
                 asm volatile("" ::: "memory");
@@ -1885,25 +1911,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
 #pragma unroll
                         for (int j = 0; j < 4; j++) cur[j] = gnext[j];
                     }
-                    if (s + 2 < 8) {
-                        __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): slot s & 1 is read
-                        asm volatile("" ::: "memory");
-                        if (g32) {
-#pragma unroll
-                            for (int u = 0; u < 2; u++)
-                                glds16(gsrc[u] + gstep * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
-                        } else {
-#pragma unroll
-                            for (int u = 0; u < 4; u++)
-                                glds16(gsrc[u] + gstep * (s + 2), gbase + (s & 1) * FH_GATH_STEP + u * 1024);
-                        }
-                    }
-                    if (s + 1 < 8) {
-                        if (s + 2 < 8) wait_step();                        // step s + 1 landed
-                        else __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
-                        asm volatile("" ::: "memory");
-                        gread(s + 1);
-                    }
+                    ring_advance(s);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; j++) cur[j] = cbuf[s % CHAIN_PF][j];
@@ -2463,7 +2471,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 #if defined(FH_WAVES_SET) && FH_WAVES_SET != 8
                 if (gath) { set_error("launch_fused: gather ring needs 8 waves"); return -1; }
 #else
-                if (gath && !cos)
+                if (!cos && a.fast_dist)
+                    hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 1, true>), grid, dim3(64 * 8), lh, s, a);
+                else if (gath && !cos)
                     hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, true, 1>), grid, dim3(64 * 8),
                                        (size_t)fh_gath_off(f.Kpad, false) + 8 * FH_GATH_WAVE, s, a);
                 else
@@ -2513,7 +2523,13 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 #else
                     if (a.Kpad <= FH_GATH_KMAX && !(gv && !strcmp(gv, "0"))) {
                         const size_t lg = (size_t)fh_gath_off(a.Kpad, hash) + 8 * FH_GATH_WAVE;
-                        if (hash) hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
+                        // the certified f32 winner distance (a.fast_dist) compiled in
+                        if (hash && a.fast_dist)
+                            hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);
+                        else if (a.fast_dist)
+                            hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);
+                        else if (hash)
+                            hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
                         else hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
 #endif
                     } else if (hash) {

@@ -76,3 +76,41 @@ def cases(kind):
 @pytest.fixture(scope="session")
 def meta():
     return golden_meta()
+
+
+# Distances of the euclidean hi-only pass: the product default is the certified
+# f32 winner distance (<= 2^-20 relative: the north star asks 1e-5 relative on
+# float distances; cluster IDs and bucket IDs stay bit-exact); LSHKM_DIST=exact
+# gives the reference-order fp64 chain, bit for bit. Tests that compare
+# distances bit for bit run in exact mode; tests taking `dist_mode` run both.
+DIST_TOL = 2.0 ** -20
+
+
+@pytest.fixture(autouse=True)
+def _dist_env(request, monkeypatch):
+    if "dist_mode" not in request.fixturenames:
+        monkeypatch.setenv("LSHKM_DIST", "exact")
+
+
+@pytest.fixture(params=["default", "exact"])
+def dist_mode(request, monkeypatch):
+    if request.param == "exact":
+        monkeypatch.setenv("LSHKM_DIST", "exact")
+    else:
+        monkeypatch.delenv("LSHKM_DIST", raising=False)
+    return request.param
+
+
+def assert_dist(got, want, mode):
+    """exact: bit for bit; default: within DIST_TOL relative where the reference's
+    distance is finite and non-zero, bit for bit elsewhere (0, inf, NaN)."""
+    got = np.ascontiguousarray(got, np.float64)
+    want = np.ascontiguousarray(want, np.float64)
+    assert got.shape == want.shape
+    if mode == "exact":
+        assert np.array_equal(got.view(np.uint64), want.view(np.uint64)), np.nonzero(got != want)[0][:10]
+        return
+    fin = np.isfinite(want) & (want != 0.0)
+    assert np.array_equal(got[~fin].view(np.uint64), want[~fin].view(np.uint64))
+    rel = np.abs(got[fin] - want[fin]) / np.abs(want[fin])
+    assert rel.max(initial=0.0) <= DIST_TOL, rel.max(initial=0.0)

@@ -22,6 +22,7 @@ import pytest
 
 import oracle
 from amd import lshkm
+from conftest import assert_dist
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -53,13 +54,13 @@ def near_tie_rows(ctx, X, Cc, rel=1e-4, chunk=1 << 18):
     return torch.cat(out).cpu().numpy()
 
 
-def check_lloyd_rows(Xh, Cc_h, rows, ga, gd, src):
+def check_lloyd_rows(Xh, Cc_h, rows, ga, gd, src, mode="exact"):
     """Oracle Lloyd on the listed rows; centroid-override rows are (c, 0)."""
     over = {int(r): c for c, r in enumerate(src) if r >= 0} if src is not None else {}
     plain = np.array([r for r in rows if int(r) not in over], np.int64)
     oa, od = oracle.lloyd_assign(Xh[plain], Cc_h, "euclidean", None)
     assert np.array_equal(ga[plain], oa), np.nonzero(ga[plain] != oa)[0][:10]
-    assert np.array_equal(gd[plain].view(np.uint64), od.view(np.uint64))
+    assert_dist(gd[plain], od, mode)
     for r, c in over.items():
         assert ga[r] == c and gd[r] == 0.0
 
@@ -71,7 +72,7 @@ def check_hash_all(Xh, tu, bu, V, t, w, r, nb, chunk=1_000_000):
         assert np.array_equal(bu[lo:lo + chunk], xb), lo
 
 
-def test_c5_hash_assign_k1024_vs_oracle(ctx):
+def test_c5_hash_assign_k1024_vs_oracle(ctx, dist_mode):
     # the C5 shard's exact call shape at 200,003 rows (ragged last tile): K = 1024
     # dataset-row centroids, 24 of them exact duplicates across the 512-centroid
     # pass boundary (the first index must win) and 8 within the second pass
@@ -99,12 +100,12 @@ def test_c5_hash_assign_k1024_vs_oracle(ctx):
     assert dup.sum() > 1000 and not np.isin(ga, np.r_[600:624, 1000:1008]).any()
     sample = np.random.default_rng(6).choice(N, 6000, replace=False)
     check_lloyd_rows(Xh, Cc.cpu().numpy(), np.union1d(np.union1d(near, sample), np.nonzero(dup)[0][:3000]),
-                     ga, gd, src)
+                     ga, gd, src, dist_mode)
     assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0          # the tie rows reached the exact pass
 
 
 @pytest.mark.parametrize("metric", ["euclidean", "cosine"])
-def test_c5_shapes_two_passes_ragged(ctx, metric):
+def test_c5_shapes_two_passes_ragged(ctx, metric, dist_mode):
     # K = 1000 (ragged second pass of 488), N not a multiple of 32: the hashing
     # multi-pass form against the unhashed path and the oracle on a sample
     N, d, L, k, K = 70_001, 128, 5, 4, 1000
@@ -127,10 +128,10 @@ def test_c5_shapes_two_passes_ragged(ctx, metric):
     sub = np.random.default_rng(2).choice(N, 1500, replace=False)
     oa, od = oracle.lloyd_assign(X.cpu().numpy()[sub], Cc.cpu().numpy(), metric, None)
     assert np.array_equal(a.cpu().numpy()[sub], oa)
-    assert np.array_equal(dist.cpu().numpy()[sub].view(np.uint64), od.view(np.uint64))
+    assert_dist(dist.cpu().numpy()[sub], od, "exact" if metric == "cosine" else dist_mode)
 
 
-def test_c3_bench_call_full_size(ctx):
+def test_c3_bench_call_full_size(ctx, dist_mode):
     # bench.py's timed call at N = 10M, K = 256 (centroids = rows i * floor(N/K),
     # with the override): every row's tuples and buckets; Lloyd on every near-tie
     # row and a 50K sample
@@ -158,7 +159,7 @@ def test_c3_bench_call_full_size(ctx):
     Xh = X.cpu().numpy()
     check_hash_all(Xh, tu_h, bu_h, V, t, w, r, N // 100)
     sample = np.random.default_rng(10).choice(N, 50_000, replace=False)
-    check_lloyd_rows(Xh, Cc.cpu().numpy(), np.union1d(near, sample), ga, gd, src)
+    check_lloyd_rows(Xh, Cc.cpu().numpy(), np.union1d(near, sample), ga, gd, src, dist_mode)
 
 
 def test_c4_cube_full_size(ctx):
