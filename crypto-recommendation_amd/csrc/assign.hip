@@ -710,14 +710,27 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         int32_t myrow[R];
 #pragma unroll
         for (int r = 0; r < R; r++) myrow[r] = rows[g * R + min(r, nr - 1)];   // pad with the last row
+        // every row value of the group in flight at once (d <= XB_DMAX: at most
+        // XB_DMAX / 64 per lane and row), then staged in LDS
         float xn2p[R];
+        TX xv[R][XB_DMAX / 64];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int u = 0; u < XB_DMAX / 64; u++) {
+                const int j = lane + 64 * u;
+                xv[r][u] = j < d ? X[(int64_t)myrow[r] * d + j] : TX(0);
+            }
 #pragma unroll
         for (int r = 0; r < R; r++) {
             float q = 0.f;
-            for (int j = lane; j < d; j += 64) {
-                const TX v = X[(int64_t)myrow[r] * d + j];
-                xs[wave][r][j] = v;
-                q = fmaf((float)v, (float)v, q);
+#pragma unroll
+            for (int u = 0; u < XB_DMAX / 64; u++) {
+                const int j = lane + 64 * u;
+                if (j < d) {
+                    xs[wave][r][j] = xv[r][u];
+                    q = fmaf((float)xv[r][u], (float)xv[r][u], q);
+                }
             }
             xn2p[r] = q;
         }
@@ -728,11 +741,16 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
         for (int r = 0; r < R; r++)
 #pragma unroll
             for (int i = 0; i < NCH; i++) acc[r][i] = 0.f;
+        // chunks past Kpad read chunk 0 (their scores are never used): the loads
+        // carry no branch, so the unrolled iterations' loads issue together
+        int coff[NCH];
+#pragma unroll
+        for (int i = 0; i < NCH; i++) coff[i] = (64 * i < Kpad ? 64 * i : 0) + lane;
 #pragma unroll 8
         for (int j = 0; j < d; j++) {
             float cv[NCH];
 #pragma unroll
-            for (int i = 0; i < NCH; i++) cv[i] = 64 * i < Kpad ? CT32[(size_t)j * Kpad + 64 * i + lane] : 0.f;
+            for (int i = 0; i < NCH; i++) cv[i] = CT32[(size_t)j * Kpad + coff[i]];
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 const float xj = (float)xs[wave][r][j];

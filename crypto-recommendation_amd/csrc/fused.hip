@@ -655,11 +655,27 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
     float* lt0 = lv10 + 32;
     int32_t* lr0 = reinterpret_cast<int32_t*>(lt0 + 32);
 
-    // ---- prologue: the block's resident image (once per block)
-    for (int e = threadIdx.x; e < Kpad * 16; e += FP_THREADS) {
-        const int r = e >> 4, g = e & 15;
-        *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Ch + (size_t)r * FU_D + g * 8);
-        *reinterpret_cast<float4*>(lcl + r * FU_RS + g * 8) = *reinterpret_cast<const float4*>(a.Cl + (size_t)r * FU_D + g * 8);
+    // ---- prologue: the block's resident image (once per block), FP_CU granules
+    // per thread in flight at once (a plain copy loop waited on every load)
+    constexpr int FP_CU = 4;
+    for (int e0 = 0; e0 < Kpad * 16; e0 += FP_THREADS * FP_CU) {
+        float4 vh[FP_CU], vl[FP_CU];
+#pragma unroll
+        for (int u = 0; u < FP_CU; u++) {
+            // past the end: granule 0 again (the same bytes rewritten), so neither
+            // the loads nor the stores carry a branch and the loads issue together
+            const int e = e0 + u * FP_THREADS + (int)threadIdx.x < Kpad * 16 ? e0 + u * FP_THREADS + (int)threadIdx.x : 0;
+            const int r = e >> 4, g = e & 15;
+            vh[u] = *reinterpret_cast<const float4*>(a.Ch + (size_t)r * FU_D + g * 8);
+            vl[u] = *reinterpret_cast<const float4*>(a.Cl + (size_t)r * FU_D + g * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < FP_CU; u++) {
+            const int e = e0 + u * FP_THREADS + (int)threadIdx.x < Kpad * 16 ? e0 + u * FP_THREADS + (int)threadIdx.x : 0;
+            const int r = e >> 4, g = e & 15;
+            *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) = vh[u];
+            *reinterpret_cast<float4*>(lcl + r * FU_RS + g * 8) = vl[u];
+        }
     }
     for (int e = threadIdx.x; e < Kpad; e += FP_THREADS) lcn[e] = a.cnh[e];
     if (threadIdx.x < 2) lcount[threadIdx.x] = 0;
@@ -1384,10 +1400,22 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     // image img: centroid rows [img * KI, img * KI + rows) into LDS rows 0..
     auto load_image = [&](int img) {
         const int r0 = img * KI, nr = NIMG == 2 && img == 1 ? Kpad - FH_KMAX : KI;
-        for (int e = threadIdx.x; e < nr * 16; e += FH_THREADS) {
-            const int r = e >> 4, g = e & 15;
-            *reinterpret_cast<float4*>(lch + r * FU_RS + g * 8) =
-                *reinterpret_cast<const float4*>(a.Ch + (size_t)(r0 + r) * FU_D + g * 8);
+        // FH_CU granules per thread in flight at once (a plain copy loop waited on every load)
+        constexpr int FH_CU = 8;
+        for (int e0 = 0; e0 < nr * 16; e0 += FH_THREADS * FH_CU) {
+            float4 v[FH_CU];
+#pragma unroll
+            for (int u = 0; u < FH_CU; u++) {
+                // past the end: granule 0 again (the same bytes rewritten), so neither
+                // the loads nor the stores carry a branch and the loads issue together
+                const int e = e0 + u * FH_THREADS + (int)threadIdx.x < nr * 16 ? e0 + u * FH_THREADS + (int)threadIdx.x : 0;
+                v[u] = *reinterpret_cast<const float4*>(a.Ch + (size_t)(r0 + (e >> 4)) * FU_D + (e & 15) * 8);
+            }
+#pragma unroll
+            for (int u = 0; u < FH_CU; u++) {
+                const int e = e0 + u * FH_THREADS + (int)threadIdx.x < nr * 16 ? e0 + u * FH_THREADS + (int)threadIdx.x : 0;
+                *reinterpret_cast<float4*>(lch + (e >> 4) * FU_RS + (e & 15) * 8) = v[u];
+            }
         }
         for (int e = threadIdx.x; e < nr; e += FH_THREADS) lcn[e] = a.cnh[r0 + e];
     };
