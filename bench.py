@@ -236,8 +236,8 @@ FUSED_WHAT = ("fused pass = fused_hi_kernel (hash + hi-only f16 centroid scores,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=10_000_000, help="points per GPU")
     ap.add_argument("--workload", choices=["c3", "c5"], default="c3")
     ap.add_argument("--k", type=int, default=None, help="centroids (default 256 for c3, 1024 for c5)")

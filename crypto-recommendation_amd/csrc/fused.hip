@@ -1369,7 +1369,7 @@ __device__ inline void glds16(const void* gsrc, uint32_t lds_dst) {
 // them). fp64 rows: the scores use xh = f16(f32(x)); |x - f32(x)| <= 2^-24 |x|
 // joins |xr| in the bound; the winner chain re-reads the fp64 row (the
 // register copy is f32).
-// FAST (euclidean, one pass, fp32 rows): the certified f32 winner distance
+// FAST (euclidean, fp32 rows; the last pass when K > 512): the certified f32 winner distance
 // compiled in (no fp64 chain state). Its f32 centroid rows are register loads:
 // through the gather ring (GATH) each 16-dim step waits on its DMA, and the
 // short f32 sum cannot hide that (fused pass 2.21 vs 2.14 ms at C3).
@@ -1382,7 +1382,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
     static_assert(ROWS == 0 || (!HASH && !MP && NIMG == 1), "general rows: Lloyd without hashing, one pass");
     // the gather's explicit vmcnt waits assume no other vector loads in the chain
     static_assert(!(GATH && ROWS == 2), "fp64 rows re-read x in the chain: register loads of the winner rows");
-    static_assert(!FAST || (MET == 0 && ROWS != 2 && !MP && NIMG == 1 && !GATH), "fast distance: euclidean single pass, fp32 rows");
+    static_assert(!FAST || (MET == 0 && ROWS != 2 && NIMG == 1 && !GATH), "fast distance: euclidean, fp32 rows");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int Kpad = a.Kpad;
     const bool fastd = FAST || a.fast_dist != 0;
@@ -2567,6 +2567,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                     }
                 } else {
                     if (hash && p == 0) FH_LAUNCH(true, true, 0);
+                    else if (a.fast_dist && a.pass_last)   // the winner's distance: certified f32, compiled in
+                        hipLaunchKernelGGL((fused_hi_kernel<false, true, 0, 1, false, 0, true>), grid,
+                                           dim3(64 * fh_waves<false, true, 0>()), lh, s, a);
                     else FH_LAUNCH(false, true, 0);
                 }
 #undef FH_LAUNCH
