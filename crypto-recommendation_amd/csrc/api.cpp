@@ -683,13 +683,24 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
     }
     if (src_rows_host) {
         if ((rc = ctx->ws_src.reserve((size_t)K * 4))) return rc;
-        // Stage through a pinned buffer so the caller's array may be freed at
-        // once and no stream sync is needed; the previous copy from the pinned
-        // buffer must have landed before we overwrite it.
-        if ((rc = ctx->pin_stage((size_t)K * 4))) return rc;
-        std::memcpy(ctx->pinned, src_rows_host, (size_t)K * 4);
-        LSHKM_HIP(hipMemcpyAsync(ctx->ws_src.p, ctx->pinned, (size_t)K * 4, hipMemcpyHostToDevice, s));
-        LSHKM_HIP(hipEventRecord(ctx->pinned_ev, s));
+        // The same rows as the previous override already sit in ws_src (Lloyd
+        // iterations and the bench pass one array repeatedly): no copy. A small
+        // host->device copy blocked the host until the stream drained, so every
+        // call waited for the previous one's tail: 2.05 ms of host enqueue per call vs 0.05).
+        const bool same = ctx->src_cache_dev == ctx->ws_src.p && ctx->src_cache_cap == ctx->ws_src.cap &&
+                          ctx->src_cache.size() == (size_t)K &&
+                          std::memcmp(ctx->src_cache.data(), src_rows_host, (size_t)K * 4) == 0;
+        if (!same) {
+            // Stage through a pinned buffer so the caller's array may be freed at
+            // once and no stream sync is needed (a ring of buffers, index.h).
+            if ((rc = ctx->pin_stage((size_t)K * 4))) return rc;
+            std::memcpy(ctx->pinned, src_rows_host, (size_t)K * 4);
+            LSHKM_HIP(hipMemcpyAsync(ctx->ws_src.p, ctx->pinned, (size_t)K * 4, hipMemcpyHostToDevice, s));
+            LSHKM_HIP(hipEventRecord(ctx->pinned_ev, s));
+            ctx->src_cache.assign(src_rows_host, src_rows_host + K);
+            ctx->src_cache_dev = ctx->ws_src.p;
+            ctx->src_cache_cap = ctx->ws_src.cap;
+        }
         if ((rc = launch_assign_override(s, (const int32_t*)ctx->ws_src.p, K, N, assign, dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
     }
     return 0;
@@ -797,6 +808,7 @@ static int range_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, i
     // the centroid override (assignment.hpp:125-127, :143-145)
     if (src_rows_host) {
         if ((rc = ctx->ws_src.reserve((size_t)K * 4))) return rc;
+        ctx->src_cache_dev = nullptr;            // ws_src overwritten outside the cache
         LSHKM_HIP(hipMemcpyAsync(ctx->ws_src.p, src_rows_host, (size_t)K * 4, hipMemcpyHostToDevice, s));
         if ((rc = launch_assign_override(s, (const int32_t*)ctx->ws_src.p, K, N, assign, dist))) return rc;
         LSHKM_HIP(hipStreamSynchronize(s));     // the host arrays may be freed on return

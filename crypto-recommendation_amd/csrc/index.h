@@ -86,18 +86,38 @@ struct lshkm_ctx_s {
             return -2;
         return 0;
     }
-    // pinned host staging for small host->device inputs
+    // pinned host staging for small host->device inputs: a ring of PIN_SLOTS
+    // buffers, each reused only after the copy from it PIN_SLOTS stagings ago
+    // has landed (one slot made every call wait for the previous call's tail:
+    // the host then re-fed an idle GPU). Callers fill `pinned`, copy from it and
+    // record `pinned_ev` on their stream.
+    static constexpr int PIN_SLOTS = 4;
+    void* pin_buf[PIN_SLOTS] = {};
+    size_t pin_cap[PIN_SLOTS] = {};
+    hipEvent_t pin_ev[PIN_SLOTS] = {};
+    bool pin_used[PIN_SLOTS] = {};
+    int pin_cur = -1;
     void* pinned = nullptr;
-    size_t pinned_cap = 0;
     hipEvent_t pinned_ev = nullptr;
+    // the centroid-override rows last copied into ws_src (valid while ws_src
+    // keeps that allocation): a repeated override needs no copy
+    std::vector<int32_t> src_cache;
+    void* src_cache_dev = nullptr;
+    size_t src_cache_cap = 0;
     int pin_stage(size_t bytes) {
-        if (pinned_ev) (void)hipEventSynchronize(pinned_ev);
-        else if (hipEventCreateWithFlags(&pinned_ev, hipEventDisableTiming) != hipSuccess) return -2;
-        if (bytes <= pinned_cap) return 0;
-        if (pinned) (void)hipHostFree(pinned);
-        pinned = nullptr; pinned_cap = 0;
-        if (hipHostMalloc(&pinned, bytes, hipHostMallocDefault) != hipSuccess) return -3;
-        pinned_cap = bytes;
+        const int i = (pin_cur + 1) % PIN_SLOTS;
+        if (!pin_ev[i] && hipEventCreateWithFlags(&pin_ev[i], hipEventDisableTiming) != hipSuccess) return -2;
+        if (pin_used[i]) (void)hipEventSynchronize(pin_ev[i]);
+        if (bytes > pin_cap[i]) {
+            if (pin_buf[i]) (void)hipHostFree(pin_buf[i]);
+            pin_buf[i] = nullptr; pin_cap[i] = 0;
+            if (hipHostMalloc(&pin_buf[i], bytes, hipHostMallocDefault) != hipSuccess) return -3;
+            pin_cap[i] = bytes;
+        }
+        pin_cur = i;
+        pin_used[i] = true;              // the caller records pin_ev[i] after its copy
+        pinned = pin_buf[i];
+        pinned_ev = pin_ev[i];
         return 0;
     }
     ~lshkm_ctx_s() {
@@ -106,8 +126,10 @@ struct lshkm_ctx_s {
         if (side_stream) (void)hipStreamSynchronize(side_stream), (void)hipStreamDestroy(side_stream);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         if (join_ev) (void)hipEventDestroy(join_ev);
-        if (pinned_ev) (void)hipEventSynchronize(pinned_ev), (void)hipEventDestroy(pinned_ev);
-        if (pinned) (void)hipHostFree(pinned);
+        for (int i = 0; i < PIN_SLOTS; i++) {
+            if (pin_ev[i]) (void)hipEventSynchronize(pin_ev[i]), (void)hipEventDestroy(pin_ev[i]);
+            if (pin_buf[i]) (void)hipHostFree(pin_buf[i]);
+        }
     }
 };
 

@@ -463,3 +463,18 @@ def test_cosine_hash_assign_golden(ctx, name):
     oa, od = oracle.lloyd_assign(Xh, Ch, "cosine", None)
     assert np.array_equal(a.cpu().numpy(), oa)
     assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
+
+
+def test_override_rows_change_between_calls(ctx):
+    # the override rows are cached on the device while unchanged (api.cpp): a
+    # call with other rows (same K) must override those, and a repeat the first
+    N, d, K = 20_000, 128, 64
+    X = ctx.synth(0x0F0, N, d)
+    ra = (np.arange(K) * 300).astype(np.int32)
+    rb = ra + 7
+    Cc = X[ctx.torch.from_numpy(ra.astype(np.int64)).to(ctx.dev)].double()
+    for src in (ra, rb, rb.copy(), ra):
+        a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", src)
+        oa, od = oracle.lloyd_assign(X.cpu().numpy(), Cc.cpu().numpy(), "euclidean", src)
+        assert np.array_equal(a.cpu().numpy(), oa)
+        assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
