@@ -41,7 +41,8 @@ F16_MFMA_PEAK_TFS = 2500.0     # MI355X_MICROARCH.md: FP16/BF16 MFMA dense peak
 METRIC = "point hash+assign ops/sec at d=128, N=10M, K=256; 1/2/4/8 MI355X"
 DTYPE = ("fp32 points; split-f16 MFMA scores (f32 accumulate); tuples, bucket IDs and cluster IDs bit-exact "
          "(x87-exact hashing, certified argmin); distances: certified f32, <= 2^-20 relative to the reference's "
-         "fp64 (north star: 1e-5), LSHKM_DIST=exact for the reference-order fp64 chain (exactness.exact_distances)")
+         "fp64 (north star: 1e-5; the context's default LSHKM_DIST_CERTIFIED mode), LSHKM_DIST_EXACT for the "
+         "reference-order fp64 chain (exactness.exact_distances)")
 # algorithmic bytes per point of the fused pass: 512 B read, 80 B
 # tuples + 20 B bucket IDs + 4 B cluster ID + 8 B distance written
 BYTES_PER_PT = 4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES + 4 + 8
@@ -108,6 +109,22 @@ def cpu_baseline(sample_hash, sample_assign, K):
                   f"1 thread, {platform.processor() or platform.machine()}; hash {res['hash_s']:.2f}s, "
                   f"assign {res['assign_s']:.2f}s",
     }
+
+
+def attach_cpu_baseline(line, args, K):
+    """line["cpu_baseline"] (+ line["c5"]["cpu_baseline"]): the reference's CPU
+    path on a bounded sample, 1 thread, plus the C restatement on all cores."""
+    line["cpu_baseline"] = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample * 256 // K, K)
+    try:
+        line["cpu_baseline"]["all_cores"] = port_all_cores(args.cpu_port_hash_sample,
+                                                           args.cpu_port_assign_sample * 256 // K, K)
+    except (subprocess.CalledProcessError, OSError, ValueError) as e:
+        line["cpu_baseline"]["all_cores"] = {"error": str(e)[:200]}
+    if "c5" in line:
+        cb = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample // 4, 1024)
+        cb["note"] = ("hash + assign only: the reference's k_means update adds ~4d flops per point, "
+                      "not timed here")
+        line["c5"]["cpu_baseline"] = cb
 
 
 def free_port():
@@ -181,11 +198,15 @@ def dry_run(args, world, rank):
     ok = bool(torch.all(sums == float(tot)) and torch.all(counts == tot))
     gathered = [None] * world
     dist.all_gather_object(gathered, (rank, row0, n))
+    dist.barrier()
     if rank == 0:
-        print(json.dumps({"dry_run": True, "metric": METRIC, "n_gpus": world, "steps": args.steps,
-                          "ms_per_step": elapsed / args.steps * 1e3, "allreduce_ok": ok,
-                          "shards": [{"rank": r, "row0": a, "n": b} for r, a, b in gathered],
-                          "backend": dist.get_backend()}), flush=True)
+        line = {"dry_run": True, "metric": METRIC, "n_gpus": world, "world_size": world, "steps": args.steps,
+                "ms_per_step": elapsed / args.steps * 1e3, "allreduce_ok": ok,
+                "shards": [{"rank": r, "row0": a, "n": b} for r, a, b in gathered],
+                "backend": dist.get_backend()}
+        if not args.no_cpu_baseline:
+            attach_cpu_baseline(line, args, args.k or 256)
+        print(json.dumps(line), flush=True)
     dist.destroy_process_group()
     return 0 if ok else 1
 
@@ -229,8 +250,9 @@ def roofline(N, K, kernel_ms, traffic, what):
                      "flop_per_point_executed": mfma_flop_per_pt, "flop_per_point_algorithmic": flop_per_pt}}
 
 
-FUSED_WHAT = ("fused pass = fused_hi_kernel (hash + hi-only f16 centroid scores, one read of X per 512-centroid "
-              "pass) + hash_fixup_kernel + the 3-product refinement of the rows the hi-only bound leaves")
+FUSED_WHAT = ("fused pass = fused_centroid_prep + fused_hi_kernel (hash + hi-only f16 centroid scores, one read of X "
+              "per 512-centroid pass) + hash_fixup_kernel (side stream) + the 3-product refinement of the rows the "
+              "hi-only bound leaves")
 
 
 def main():
@@ -266,11 +288,14 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.dry_run:
         return dry_run(args, world, rank)
+    backend = "none (single process)"
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         assert dist.get_world_size() == args.gpus
+        backend = dist.get_backend()
+        assert backend == "nccl", backend          # RCCL on ROCm
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -314,13 +339,14 @@ def main():
         kms = fused_kernel_ms(lk, lib, ctx, step, max(3, args.steps))
         if args.exact_dist_line:
             # the same step with every distance from the reference-order fp64 chain
-            os.environ["LSHKM_DIST"] = "exact"
+            ctx.set_dist_mode("exact")
             try:
                 el_x = timed(step, args.steps, args.warmup, world, dev)
                 kms_x = fused_kernel_ms(lk, lib, ctx, step, max(3, args.steps))
             finally:
-                os.environ.pop("LSHKM_DIST", None)
-            ex["exact_distances"] = {"note": "LSHKM_DIST=exact: bit-exact distances (the reference's fp64 chain)",
+                ctx.set_dist_mode("certified")
+            ex["exact_distances"] = {"note": "lshkm_ctx_set_dist_mode(LSHKM_DIST_EXACT): bit-exact distances "
+                                             "(the reference's fp64 chain)",
                                      "value": N_total * args.steps / el_x, "ms_per_step": el_x / args.steps * 1e3,
                                      "kernel_ms": kms_x, "frac": 624.0 * N / (kms_x * 1e-3) / 8e12}
         return elapsed, kms, ex
@@ -333,19 +359,22 @@ def main():
         it.timing = True
         kms = fused_kernel_ms(lk, lib, ctx, it.step, max(3, args.steps))
         it.timing = False
-        xms = it.exchange_ms() if world > 1 else 0.0
+        xms = it.exchange_ms() if world > 1 else None
         return elapsed, kms, xms
 
     def c5_object(K, elapsed, kms, xms):
+        coll = (f"RCCL all-reduce ({backend}) of the {K}x128 fp64 sums + {K} counts" if world > 1
+                else "none (N = 1: a single shard, no collective)")
         return {
-            "metric": f"C5 LSH-assign + k-means iterations: points/s (hash + assign K={K} + sums + RCCL all-reduce "
-                      f"+ finalize)",
+            "metric": f"C5 LSH-assign + k-means iterations: points/s (hash + assign K={K} + sums + "
+                      f"{'RCCL all-reduce' if world > 1 else 'no collective at N = 1'} + finalize)",
             "value": N_total * args.steps / elapsed, "unit": "point iteration ops/s",
             "ms_per_step": elapsed / args.steps * 1e3, "n_gpus": world, "scaling": "weak",
             "config": {"workload": f"C5 (BASELINE configs[4]): N={N} per GPU x {world} GPU(s), d=128, K={K}, "
-                                   f"L=5, k=4, w=0.4, RCCL all-reduce of the {K}x128 fp64 sums + {K} counts",
+                                   f"L=5, k=4, w=0.4, exchange: {coll}",
                        "N_per_gpu": N, "N_total": N_total, "K": K, "parallelism": f"dp{world} (row shards)"},
-            "allreduce_ms": xms,
+            "allreduce": coll,
+            "allreduce_ms": xms if world > 1 else None,
             "roofline": roofline(N, K, kms, traffic_for(args.traffic_json_c5, N, K, "c5"),
                                  FUSED_WHAT + " (K = 1024: two 512-centroid passes)"),
         }
@@ -378,19 +407,14 @@ def main():
             K5 = 1024
             el5, kms5, xms5 = c5_run(K5)
             line["c5"] = c5_object(K5, el5, kms5, xms5)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        K = line["config"]["K"]
-        line["cpu_baseline"] = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample * 256 // K, K)
-        try:
-            line["cpu_baseline"]["all_cores"] = port_all_cores(args.cpu_port_hash_sample,
-                                                               args.cpu_port_assign_sample * 256 // K, K)
-        except (subprocess.CalledProcessError, OSError, ValueError) as e:
-            line["cpu_baseline"]["all_cores"] = {"error": str(e)[:200]}
-        if "c5" in line:
-            cb = cpu_baseline(args.cpu_hash_sample, args.cpu_assign_sample // 4, 1024)
-            cb["note"] = ("hash + assign only: the reference's k_means update adds ~4d flops per point, "
-                          "not timed here")
-            line["c5"]["cpu_baseline"] = cb
+    line["world_size"] = world
+    line["backend"] = backend
+    if world > 1:
+        torch.distributed.barrier()       # every rank's timed work is done before the CPU baseline runs
+    if rank == 0 and not args.no_cpu_baseline:
+        # the reference's CPU path on this host, in the same run (rank 0 only; at
+        # N > 1 after the final barrier, so no rank's timing overlaps it)
+        attach_cpu_baseline(line, args, line["config"]["K"])
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -67,6 +67,20 @@ int lshkm_ctx_set_stream(lshkm_ctx ctx, void* s) {
     return 0;
 }
 
+int lshkm_ctx_set_dist_mode(lshkm_ctx ctx, int mode) {
+    LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
+    LSHKM_CHECK(mode == LSHKM_DIST_CERTIFIED || mode == LSHKM_DIST_EXACT, LSHKM_ERR_ARG,
+                "unknown distance mode (LSHKM_DIST_CERTIFIED or LSHKM_DIST_EXACT)");
+    ctx->dist_mode = mode;
+    return 0;
+}
+
+int lshkm_ctx_get_dist_mode(lshkm_ctx ctx, int* mode) {
+    LSHKM_CHECK(ctx && mode, LSHKM_ERR_ARG, "bad arguments");
+    *mode = ctx->dist_mode;
+    return 0;
+}
+
 int lshkm_ctx_sync(lshkm_ctx ctx) {
     LSHKM_CHECK(ctx, LSHKM_ERR_ARG, "ctx is NULL");
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
@@ -485,14 +499,19 @@ static int assign_path(int metric, int d, int K, bool f64) {
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
-// Euclidean winner distances of the hi-only pass (fp32 rows): from f32(c) in
-// f32, certified to 2^-20 relative -- inside the 1e-5 relative the north star
-// sets for float distances; cluster IDs stay bit-exact, and a row whose bound
-// fails gets the reference-order fp64 chain. LSHKM_DIST=exact: the
-// reference-order fp64 chain for every row (bit-exact distances).
-static bool fast_dist_on() {
+// Euclidean winner distances of the hi-only pass (fp32 rows), per context
+// (lshkm_ctx_set_dist_mode): LSHKM_DIST_CERTIFIED (default) takes them from
+// f32(c) in f32, certified to 2^-20 relative -- inside the 1e-5 relative the
+// north star sets for float distances; cluster IDs stay bit-exact, and a row
+// whose bound fails gets the reference-order fp64 chain. LSHKM_DIST_EXACT: the
+// reference-order fp64 chain for every row (bit-exact distances). The
+// environment variable LSHKM_DIST=exact|certified overrides the context's mode
+// (experiments and A/B timing only).
+static bool fast_dist_on(const lshkm_ctx_s* ctx) {
     const char* e = getenv("LSHKM_DIST");
-    return !(e && !strcmp(e, "exact"));
+    if (e && !strcmp(e, "exact")) return false;
+    if (e && (!strcmp(e, "certified") || !strcmp(e, "fast"))) return true;
+    return ctx->dist_mode == LSHKM_DIST_CERTIFIED;
 }
 
 // Exact reference-order pass over the rows listed in ws_ambig (count on device).
@@ -568,7 +587,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         double* nbv = (double*)(cnh + Kpad);               // cosine: [Kpad] sequential |c|^2 (Kpad % 64 == 0: aligned)
         // euclidean winner distances: the certified f32 form (default) or the
         // reference-order fp64 chain (LSHKM_DIST=exact)
-        const bool fast = !cosine && rows_kind != 2 && fast_dist_on();
+        const bool fast = !cosine && rows_kind != 2 && fast_dist_on(ctx);
         float* C32 = nullptr;
         float* rn32 = nullptr;
         // the f32 image also serves the K <= 256 gather when every centroid value
@@ -584,6 +603,8 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             if ((rc = ctx->ws_c64p.reserve((size_t)Kpad * 128 * 8))) return rc;
             C64p = (double*)ctx->ws_c64p.p;
         }
+        // the timed fused pass starts before the centroid prep
+        if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
         if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv, C32, rn32, d, C64p))) { LSHKM_LAUNCH_CHECK(); return rc; }
         FusedLaunch f;
         f.C32 = C32; f.rn32 = rn32; f.fast_dist = fast ? 1 : 0;
@@ -628,7 +649,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             f.defer_join = !cosine && !(dj && !strcmp(dj, "0"));   // euclidean: the exact pass also overlaps the fix-up
             if (ctx->timing) f.side_timing = ctx->tev[2];
         }
-        ctx->tev_side = f.side_timing != nullptr;
+        ctx->tev_side = false;
         // the side stream's hash fix-up writes only tuples / phi / bucket: joined
         // before this call's last launch, and on every error path after the fork
         struct SideJoin {
@@ -636,9 +657,9 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             bool pending = false;
             ~SideJoin() { if (pending) (void)hipStreamSynchronize(c->side_stream); }
         } sj{ctx};
-        if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
         rc = launch_fused(s, fuse_hash, f);
         sj.pending = f.join_pending;
+        ctx->tev_side = f.side_timed;      // only a launch that recorded tev[2] extends the pass
         if (rc) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.final_counts : nullptr,
@@ -799,9 +820,13 @@ static int range_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, i
             int32_t* ar = (int32_t*)(dr + U);
             if ((rc = launch_range_gather(s, X, d, list, (int64_t)U, w[7].p))) return rc;
             const Pts Xr = X.f64 ? Pts(w[7].as<double>()) : Pts(w[7].as<float>());
-            if ((rc = assign_impl(ctx, Xr, (int64_t)U, d, C, K, metric, nullptr, ar, dr, nullptr, nullptr, nullptr,
-                                  nullptr)))
-                return rc;
+            // the range pass's distances are the exact chain; the leftover rows
+            // get the same (a range assignment is exact-order in either mode)
+            const int mode = ctx->dist_mode;
+            ctx->dist_mode = LSHKM_DIST_EXACT;
+            rc = assign_impl(ctx, Xr, (int64_t)U, d, C, K, metric, nullptr, ar, dr, nullptr, nullptr, nullptr, nullptr);
+            ctx->dist_mode = mode;
+            if (rc) return rc;
             if ((rc = launch_range_scatter(s, list, (int64_t)U, ar, dr, assign, dist))) return rc;
         }
     }

@@ -2375,6 +2375,7 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
 
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     f.nseg = 0;
+    f.side_timed = false;
     if (f.N <= 0) return 0;
     FusedArgs a;
     a.X = f.X; a.N = f.N;
@@ -2584,9 +2585,12 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             }
             if (hash && cos) hipLaunchKernelGGL(hash_fixup_kernel<true>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, hs, a);
             else if (hash) hipLaunchKernelGGL(hash_fixup_kernel<false>, dim3((unsigned)nblk * HF_SPLIT), dim3(64 * HF_WAVES), HF_LDS, hs, a);
-            if (side && f.side_timing && hipEventRecord(f.side_timing, f.side) != hipSuccess) {
-                (void)hipStreamSynchronize(f.side);
-                return kstatus("launch_fused (timing)");
+            if (side && f.side_timing) {
+                if (hipEventRecord(f.side_timing, f.side) != hipSuccess) {
+                    (void)hipStreamSynchronize(f.side);
+                    return kstatus("launch_fused (timing)");
+                }
+                f.side_timed = true;
             }
             if (side && hipEventRecord(f.join, f.side) != hipSuccess) {
                 // never return with the fix-up unordered against later work on s

@@ -52,6 +52,8 @@ int hash_rows(lshkm_ctx_s* ctx, int mode, Pts X, int64_t N, const ProjTable& pj,
 
 struct lshkm_ctx_s {
     int device = 0;
+    // LSHKM_DIST_CERTIFIED (default) / LSHKM_DIST_EXACT: lshkm_ctx_set_dist_mode
+    int dist_mode = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     lshkm::Buf stats;            // STAT_COUNT x u64

@@ -195,6 +195,7 @@ struct FusedLaunch {
     bool defer_join = false;
     bool join_pending = false;
     hipEvent_t side_timing = nullptr;            // recorded on the side stream after the fix-up (timing)
+    bool side_timed = false;                     // out: side_timing was recorded by this launch
     const float* X = nullptr;
     int64_t N = 0;
     const _Float16* Ch = nullptr;

@@ -22,6 +22,9 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "lshkm.h")
 EUCLIDEAN, COSINE = 0, 1
 STAT_HASH_EXACT, STAT_ASSIGN_AMBIG, STAT_COS_FIX, STAT_REFINED, STAT_HASH_FIX = 0, 1, 4, 5, 6
 _METRIC = {"euclidean": EUCLIDEAN, "cosine": COSINE, EUCLIDEAN: EUCLIDEAN, COSINE: COSINE}
+DIST_CERTIFIED, DIST_EXACT = 0, 1
+_DIST = {"certified": DIST_CERTIFIED, "default": DIST_CERTIFIED, "exact": DIST_EXACT,
+         DIST_CERTIFIED: DIST_CERTIFIED, DIST_EXACT: DIST_EXACT}
 
 _lib = None
 
@@ -49,6 +52,8 @@ def lib():
             "lshkm_version": (C.c_char_p, []),
             "lshkm_ctx_create": (i32, [i32, C.POINTER(vp)]),
             "lshkm_ctx_set_stream": (i32, [vp, vp]),
+            "lshkm_ctx_set_dist_mode": (i32, [vp, i32]),
+            "lshkm_ctx_get_dist_mode": (i32, [vp, C.POINTER(i32)]),
             "lshkm_ctx_sync": (i32, [vp]),
             "lshkm_ctx_destroy": (i32, [vp]),
             "lshkm_dev_alloc": (i32, [vp, i64, C.POINTER(vp)]),
@@ -179,6 +184,17 @@ class Context:
         self.h = h
         if use_torch_stream:
             _ck(lib().lshkm_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)))
+
+    def set_dist_mode(self, mode):
+        """The context's distance contract (lshkm_ctx_set_dist_mode): "certified"
+        (the default: euclidean winner distances within 2^-20 relative) or
+        "exact" (the reference's fp64 chain for every distance)."""
+        _ck(lib().lshkm_ctx_set_dist_mode(self.h, _DIST[mode]))
+
+    def dist_mode(self):
+        m = C.c_int()
+        _ck(lib().lshkm_ctx_get_dist_mode(self.h, C.byref(m)))
+        return "exact" if m.value == DIST_EXACT else "certified"
 
     def sync(self):
         _ck(lib().lshkm_ctx_sync(self.h))

@@ -30,8 +30,22 @@
  *     holds general doubles, e.g. the recommender's user vectors,
  *     crypto_rec.hpp:78-140). Centroids are fp64 rows, K x d.
  *   - Bit-exact with the reference: tuples, phi, bucket IDs, bucket member
- *     order, query results, hypercube vertices, probe order, cluster IDs.
- *     Distances: exact-order fp64 (see DESIGN.md for the pow(x,2) note).
+ *     order, query results, hypercube vertices, probe order, cluster IDs,
+ *     k-means centers and counts, chosen k-means++ rows, recommendations.
+ *   - Distances (the `dist` output of the Lloyd / hash+assign entry points)
+ *     follow the context's distance mode (lshkm_ctx_set_dist_mode):
+ *       LSHKM_DIST_CERTIFIED (the default): euclidean winner distances may come
+ *         from a certified f32 evaluation, within 2^-20 relative of the
+ *         reference's fp64 value (the north star's tolerance is 1e-5); a row
+ *         whose bound fails gets the reference-order chain. Zero, inf and NaN
+ *         distances are reproduced bit for bit. Cluster IDs are unaffected.
+ *       LSHKM_DIST_EXACT: every distance is the reference's sequential fp64
+ *         chain sqrt(sum_j (x_j - c_j)^2), j ascending -- bit-exact while the
+ *         centroids are fp32 values (dataset rows, the first Lloyd iteration);
+ *         after an update within 1.4e-16 relative (the reference's glibc
+ *         pow(x, 2) vs x*x).
+ *     Cosine distances, range-assignment distances, silhouettes, similarities
+ *     and every other output are exact-order in both modes.
  *   - One handle per thread; calls on a handle are serialised on its stream.
  */
 #ifndef LSHKM_H
@@ -53,6 +67,9 @@ extern "C" {
 #define LSHKM_METRIC_EUCLIDEAN 0
 #define LSHKM_METRIC_COSINE 1
 
+#define LSHKM_DIST_CERTIFIED 0   /* euclidean winner distances within 2^-20 relative (default) */
+#define LSHKM_DIST_EXACT 1       /* the reference's fp64 chain for every distance */
+
 typedef struct lshkm_ctx_s* lshkm_ctx;
 typedef struct lshkm_lsh_s* lshkm_lsh;
 typedef struct lshkm_cube_s* lshkm_cube;
@@ -65,6 +82,13 @@ int lshkm_ctx_create(int device, lshkm_ctx* out);
 /* Run on a caller-owned hipStream_t (e.g. torch's current stream), used
  * verbatim: NULL is the default (null) stream. A new context uses its own stream. */
 int lshkm_ctx_set_stream(lshkm_ctx ctx, void* hip_stream);
+/* Distance contract of the context (see Conventions): LSHKM_DIST_CERTIFIED
+ * (the default of a new context) or LSHKM_DIST_EXACT (the reference's
+ * euclideanDistance, cust_vector.hpp:124-136, for every row; a few percent
+ * slower at d = 128). The environment variable LSHKM_DIST=exact|certified
+ * overrides it for experiments. */
+int lshkm_ctx_set_dist_mode(lshkm_ctx ctx, int mode);
+int lshkm_ctx_get_dist_mode(lshkm_ctx ctx, int* mode_host);
 int lshkm_ctx_sync(lshkm_ctx ctx);
 int lshkm_ctx_destroy(lshkm_ctx ctx);
 /* Device memory for callers without HIP headers (the C++ shim

@@ -73,11 +73,17 @@ inline void check(int rc) {
 }
 
 // ------------------------------------------------------------ context / memory
+// The shim is a zero-change drop-in for the reference's semantics, so its
+// contexts run in LSHKM_DIST_EXACT mode: every distance a CustVector receives
+// (setCluster, assignment.hpp:73-76) is the reference's fp64 chain.
+// set_distance_mode(LSHKM_DIST_CERTIFIED) opts the calling thread into the
+// faster certified distances (<= 2^-20 relative; cluster IDs unchanged).
 class Context {
 public:
     Context() {
         const char* env = std::getenv("LSHKM_DEVICE");
         check(lshkm_ctx_create(env ? std::atoi(env) : 0, &h_));
+        check(lshkm_ctx_set_dist_mode(h_, LSHKM_DIST_EXACT));
     }
     ~Context() { lshkm_ctx_destroy(h_); }
     Context(const Context&) = delete;
@@ -92,6 +98,10 @@ inline lshkm_ctx context() {
     static thread_local Context c;
     return c.get();
 }
+
+// LSHKM_DIST_EXACT (the shim's default) or LSHKM_DIST_CERTIFIED for the
+// calling thread's context.
+inline void set_distance_mode(int mode) { check(lshkm_ctx_set_dist_mode(context(), mode)); }
 
 // Device allocation owned by the calling thread's context.
 class DevMem {

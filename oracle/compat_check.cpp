@@ -44,6 +44,8 @@ system_clock::time_point system_clock::now() noexcept {
 typedef CustVector<double> Vec;
 
 static int g_bad = 0;
+static bool g_f64 = false;         // the components are general doubles
+static bool g_certified = false;   // the shim runs in LSHKM_DIST_CERTIFIED mode
 static std::map<std::string, long> g_stat;   // coverage: how much each check exercised
 static void fail(const std::string& what) {
     if (g_bad++ < 20) std::printf("MISMATCH %s\n", what.c_str());
@@ -234,13 +236,34 @@ static void check_kmeans(std::vector<Vec>& data, const std::string& metric, int 
     for (int it = 0; it < 4; it++) {
         lloyds_assignment(a, ca, metric);
         lshkm_compat::lloyds_assignment(b, cb, metric);
+        // the distance contract of the shim's mode (lshkm.h Conventions):
+        //   exact: the reference's fp64 chain -- bit for bit where every squared
+        //     square is exact in fp64 (fp32 rows against fp32-valued
+        //     centroids), else the glibc pow(x, 2) vs x*x ulp:
+        //     <= 1e-15 relative;
+        //   certified (euclidean only; cosine stays exact-order): <= 2^-20
+        //     relative, bit for bit at 0 / inf / NaN.
+        bool sq_exact = !g_f64;
+        for (int c = 0; c < K && sq_exact; c++)
+            for (double v : *ca[c]->getDimensions()) sq_exact = sq_exact && (double)(float)v == v;
+        const double tol = (g_certified && metric == "euclidean") ? std::ldexp(1.0, -20) : (sq_exact ? 0.0 : 1e-15);
         int nd = 0;
+        double worst = 0.0;
         for (int i = 0; i < N; i++) {
             if (a[i].getCluster() != b[i].getCluster()) fail(tag + "cluster of row " + std::to_string(i));
             const double da = a[i].getDistFromCentroid(), db = b[i].getDistFromCentroid();
-            if (std::fabs(da - db) > 1e-12 * std::fabs(da)) nd++;
+            if (!(da != 0.0 && std::isfinite(da))) {
+                if (std::memcmp(&da, &db, sizeof da)) nd++;
+                continue;
+            }
+            const double rel = std::fabs(da - db) / std::fabs(da);
+            worst = std::max(worst, rel);
+            if (!(rel <= tol)) nd++;
         }
-        if (nd) fail(tag + std::to_string(nd) + " distances beyond 1e-12 rel, iteration " + std::to_string(it));
+        if (nd)
+            fail(tag + std::to_string(nd) + " distances beyond " + std::to_string(tol) + " rel (worst " +
+                 std::to_string(worst) + "), iteration " + std::to_string(it));
+        if (tol == 0.0) g_stat["kmeans_" + metric + "_bitexact_iterations"]++;
         const bool ra = k_means(a, ca, metric, 1e-9), rb = lshkm_compat::k_means(b, cb, metric, 1e-9);
         if (ra != rb) fail(tag + "k_means return, iteration " + std::to_string(it));
         for (int c = 0; c < K; c++) {
@@ -259,14 +282,21 @@ static void check_kmeans(std::vector<Vec>& data, const std::string& metric, int 
 
 int main(int argc, char** argv) {
     if (argc < 5) {
-        std::fprintf(stderr, "usage: compat_check SEED N d K [f64]\n");
+        std::fprintf(stderr, "usage: compat_check SEED N d K [f64] [exact|certified]\n");
         return 2;
     }
     g_seed = std::atoll(argv[1]);
     const int N = std::atoi(argv[2]), d = std::atoi(argv[3]), K = std::atoi(argv[4]);
-    const bool f64 = argc > 5 && std::string(argv[5]) == "f64";
-    std::vector<Vec> data = make_data((uint64_t)g_seed, N, d, f64);
+    for (int i = 5; i < argc; i++) {
+        const std::string a = argv[i];
+        if (a == "f64") g_f64 = true;
+        else if (a == "certified") g_certified = true;
+        else if (a != "exact") { std::fprintf(stderr, "unknown option %s\n", argv[i]); return 2; }
+    }
+    std::vector<Vec> data = make_data((uint64_t)g_seed, N, d, g_f64);
     try {
+        // the shim's default is LSHKM_DIST_EXACT; "certified" opts in
+        if (g_certified) lshkm_compat::set_distance_mode(LSHKM_DIST_CERTIFIED);
         check_lsh(data, "euclidean", 4, 5, 50, 4.0);
         check_lsh(data, "cosine", 6, 3, 8, 4.0);
         check_cube(data, "euclidean", 8, 2.0);
@@ -285,7 +315,7 @@ int main(int argc, char** argv) {
         std::printf("compat FAILED: %d mismatches\n", g_bad);
         return 1;
     }
-    std::printf("compat ok N=%d d=%d K=%d", N, d, K);
+    std::printf("compat ok N=%d d=%d K=%d mode=%s", N, d, K, g_certified ? "certified" : "exact");
     for (const auto& e : g_stat) std::printf(" %s=%ld", e.first.c_str(), e.second);
     std::printf("\n");
     return 0;

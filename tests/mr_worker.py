@@ -1,13 +1,14 @@
 """One rank of the multi-rank product-path test (tests/test_gpu_multirank.py).
 
-Not a test module: launched as `python tests/mr_worker.py RANK WORLD PORT OUTDIR`
+Not a test module: launched as `python tests/mr_worker.py RANK WORLD PORT OUTDIR DIST`
 (several ranks sharing the one MI355X over gloo, or one rank with WORLD = 1 for
 the single-process reference). Runs liblshkm on this rank's contiguous row
 shard (crypto-recommendation_amd/sharding.py): the C5 iteration at C5's K = 1024
 (hash + assign -- the hashing multi-pass fused form -- + k-means update) in fast
 (all-reduce) and exact (carry chain) mode, one cosine iteration (cosine index +
 cosine Lloyd in one pass), and the sharded euclidean hypercube build; saves
-everything to OUTDIR/rank<R>.npz."""
+everything to OUTDIR/rank<R>.npz. DIST: the context's distance mode
+("certified", the default, or "exact"; lshkm_ctx_set_dist_mode)."""
 import os
 import sys
 
@@ -28,10 +29,13 @@ N_TOTAL, D, L, KF, K, STEPS = 120_000, 128, 5, 4, 1024, 2
 
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    dist_mode = sys.argv[5] if len(sys.argv) > 5 else "certified"
     if world > 1:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = lshkm.Context(0)
+    ctx.set_dist_mode(dist_mode)
+    assert ctx.dist_mode() == dist_mode
     row0, n = sh.shard_range(N_TOTAL, world, rank)
     X = ctx.synth(0x5EED, n, D, row0=row0)
     V, t, r, _ = lshkm.params_lsh_euclidean(12345, L, KF, D, 0.4)
@@ -62,7 +66,8 @@ def main():
     f, h, b, state = cube.memo()
     o = np.lexsort((h, f))
     res.update(memo_f=f[o], memo_h=h[o], memo_bit=b[o], memo_state=np.array([state], np.int64),
-               vertex=cube.vertices(X).cpu().numpy(), row0=np.array([row0]))
+               vertex=cube.vertices(X).cpu().numpy(), row0=np.array([row0]),
+               dist_mode=np.array([dist_mode]))
     np.savez(os.path.join(out, f"rank{rank}.npz"), **res)
     ctx.sync()
     if world > 1:

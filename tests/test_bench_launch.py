@@ -26,8 +26,14 @@ def _bench(*argv):
 
 @pytest.mark.parametrize("n", [1, 2, 3])
 def test_bench_spawns_ranks(n):
-    res = _bench("--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1", "--n", "1000", "--k", "64")
-    assert res["dry_run"] and res["n_gpus"] == n and res["backend"] == "gloo"
+    res = _bench("--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1", "--n", "1000", "--k", "64",
+                 "--cpu-hash-sample", "2000", "--cpu-assign-sample", "400", "--cpu-port-hash-sample", "2000",
+                 "--cpu-port-assign-sample", "400")
+    assert res["dry_run"] and res["n_gpus"] == n and res["world_size"] == n and res["backend"] == "gloo"
+    # rank 0 times the reference's CPU path in the same run at every N (after the final barrier)
+    cb = res["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("reference", "port"), cb
+    assert "all_cores" in cb
     assert res["allreduce_ok"]
     assert [s["rank"] for s in res["shards"]] == list(range(n))
     assert sum(s["n"] for s in res["shards"]) == 1000 * n

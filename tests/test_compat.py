@@ -54,18 +54,27 @@ def test_shim_compiles_against_reference_headers(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["exact", "certified"])
 @pytest.mark.parametrize("args", [("7", "2000", "128", "16"), ("11", "900", "17", "5"),
                                   ("13", "1500", "100", "12", "f64")])
-def test_shim_matches_reference_functions(args):
+def test_shim_matches_reference_functions(args, mode):
+    # exact: the shim's default (LSHKM_DIST_EXACT) -- distances bit for bit where
+    # the squares are exact in fp64, else within the pow(x, 2) ulp; certified:
+    # lshkm_compat::set_distance_mode(LSHKM_DIST_CERTIFIED), euclidean distances
+    # within 2^-20 relative. Everything else bit for bit in both.
     if not os.path.exists(CHECK):
         pytest.skip("oracle/_ref/compat_check not built (needs the reference sources at build time)")
-    r = subprocess.run([CHECK, *args], capture_output=True, text=True, timeout=600)
+    env = {k: v for k, v in os.environ.items() if k != "LSHKM_DIST"}   # the ABI mode alone decides
+    r = subprocess.run([CHECK, *args, mode], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0 and "compat ok" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
     # the comparison exercised something: non-empty filtered unions and probe
     # lists, and k_means replaced its centers at least once
     stats = dict(kv.split("=") for kv in r.stdout.split("compat ok")[1].split() if "=" in kv)
+    assert stats["mode"] == mode
+    if mode == "exact" and "f64" not in args:
+        assert int(stats["kmeans_euclidean_bitexact_iterations"]) >= 1, stats
     for key in ("lsh_euclidean_filtered_rows", "lsh_cosine_filtered_rows", "cube_euclidean_probe_rows",
-                "cube_cosine_probe_rows"):
+                "cube_cosine_probe_rows", "cluster_recom_users"):
         assert int(stats[key]) > 0, (key, stats)
     assert int(stats["kmeans_euclidean_iterations"]) >= 2 and int(stats["kmeans_cosine_iterations"]) >= 2, stats
     assert int(stats["recom_users"]) >= 30, stats

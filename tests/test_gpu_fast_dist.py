@@ -1,4 +1,5 @@
-"""GPU parity of the fast winner distance (LSHKM_DIST=fast, euclidean, d = 128).
+"""GPU parity of the certified winner distance (LSHKM_DIST_CERTIFIED, the
+default distance mode of a context; euclidean, d = 128).
 
 The winner's distance is formed from f32(c) in f32 (every lane busy, no fp64
 chain) with a rigorous bound; a row whose bound exceeds 2^-20 relative is
@@ -25,8 +26,10 @@ def ctx():
 
 
 @pytest.fixture
-def fast(monkeypatch):
-    monkeypatch.setenv("LSHKM_DIST", "fast")
+def fast(ctx):
+    ctx.set_dist_mode("certified")      # the shipped default, set explicitly
+    yield
+    ctx.set_dist_mode("certified")
 
 
 def to_dev(ctx, a):
@@ -90,15 +93,19 @@ def test_fast_distance_fallback_rows(ctx, fast):
     check(ga, gd, oa, od)
 
 
-def test_fast_and_exact_modes_agree_on_ids(ctx, monkeypatch):
-    # the default (reference-order fp64 chain) and the fast mode give the same
-    # cluster IDs everywhere and distances within the bound, at the C3 shape
+def test_fast_and_exact_modes_agree_on_ids(ctx):
+    # LSHKM_DIST_EXACT (the reference-order fp64 chain) and LSHKM_DIST_CERTIFIED
+    # (the default) give the same cluster IDs everywhere and distances within the
+    # bound, at the C3 shape
     N, d, K = 500_000, 128, 256
     X = ctx.synth(0x5EED, N, d)
     rows = (np.arange(K) * (N // K)).astype(np.int64)
     Cc = X[to_dev(ctx, rows)].double()
-    a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows.astype(np.int32))
-    monkeypatch.setenv("LSHKM_DIST", "fast")
+    ctx.set_dist_mode("exact")
+    try:
+        a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows.astype(np.int32))
+    finally:
+        ctx.set_dist_mode("certified")
     a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows.astype(np.int32))
     assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
     check(a1.cpu().numpy(), d1.cpu().numpy(), a0.cpu().numpy(), d0.cpu().numpy())

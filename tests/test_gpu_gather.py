@@ -10,6 +10,7 @@ import pytest
 
 import oracle
 from amd import lshkm
+from conftest import assert_dist_tol
 
 pytestmark = pytest.mark.gpu
 
@@ -37,6 +38,8 @@ def run(ctx, monkeypatch, X, C, env, lsh=None):
 
 @pytest.mark.parametrize("K,general,hashing", [(256, False, True), (256, True, True), (200, False, False), (64, True, False)])
 def test_gather_modes_agree(ctx, monkeypatch, K, general, hashing):
+    # the gather feeds the exact winner chain: the LSHKM_DIST_EXACT contract
+    ctx.set_dist_mode("exact")
     N, d = 300_007, 128
     X = ctx.synth(0x6A7 + K, N, d)
     Xh = X.cpu().numpy()
@@ -59,7 +62,5 @@ def test_gather_modes_agree(ctx, monkeypatch, K, general, hashing):
     oa, od = oracle.lloyd_assign(Xh[sub], Ch, "euclidean", None)
     a, dist = ref[-2], ref[-1]
     assert np.array_equal(a[sub], oa)
-    if general:
-        np.testing.assert_allclose(dist[sub], od, rtol=1e-14, atol=0)
-    else:
-        assert np.array_equal(dist[sub].view(np.uint64), od.view(np.uint64))
+    assert_dist_tol(dist[sub], od, "exact", 1e-14 if general else 0.0)
+    ctx.set_dist_mode("certified")

@@ -6,7 +6,7 @@ import pytest
 
 import oracle
 from amd import lshkm
-from conftest import assert_dist, cases, golden, golden_meta, lloyd_input
+from conftest import assert_dist, assert_dist_tol, cases, golden, golden_meta, lloyd_input
 
 META = golden_meta()
 pytestmark = pytest.mark.gpu
@@ -100,9 +100,9 @@ def test_lloyd_golden(ctx, name, dist_mode):
         a, dist = lshkm.lloyd_assign(ctx, X, Cc, m["metric"], src)
         assert np.array_equal(a.cpu().numpy(), g[f"assign{it}"]), it
         gd, rd = dist.cpu().numpy(), g[f"dist{it}"]
-        if dist_mode == "default" and m["metric"] == "euclidean":
+        if dist_mode == "certified" and m["metric"] == "euclidean":
             # the certified f32 winner distance (conftest.DIST_TOL)
-            assert_dist(gd, rd, "default")
+            assert_dist(gd, rd, "certified")
             continue
         fp32_centers = np.array_equal(g[f"centers{it}"], g[f"centers{it}"].astype(np.float32).astype(np.float64))
         if fp32_centers or m["metric"] == "cosine" and it == 0:
@@ -135,19 +135,19 @@ def test_lloyd_large_vs_oracle(ctx, dist_mode):
     assert np.all(gd[over] == 0.0)
 
 
-def test_lloyd_general_fp64_centroids(ctx):
-    # centroids that are not fp32 values (after an update): distances keep exact-order fp64
+def test_lloyd_general_fp64_centroids(ctx, dist_mode):
+    # centroids that are not fp32 values (after an update): exact mode keeps the
+    # exact-order fp64 chain (within the pow(x,2) ulp), certified mode 2^-20
     N, d, K = 20_000, 128, 64
     X = ctx.synth(3, N, d)
     Cc = X[:K].double() * (1 + 1e-3) + 1e-5
     a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
     oa, od = oracle.lloyd_assign(X.cpu().numpy(), Cc.cpu().numpy(), "euclidean", None)
     assert np.array_equal(a.cpu().numpy(), oa)
-    rel = np.abs(dist.cpu().numpy() - od) / np.maximum(od, 1e-300)
-    assert rel.max() <= 1e-15          # tolerance note: pow(x,2) vs x*x, DESIGN.md
+    assert_dist_tol(dist.cpu().numpy(), od, dist_mode, 1e-15)   # pow(x,2) vs x*x, DESIGN.md §5
 
 
-def test_lloyd_ties_and_duplicates(ctx):
+def test_lloyd_ties_and_duplicates(ctx, dist_mode):
     N, d, K = 5000, 32, 16
     X = ctx.synth(11, N, d)
     rows = np.array([0, 1, 1, 2, 3, 3, 3, 4, 5, 6, 7, 8, 9, 9, 10, 11], np.int32)
@@ -156,7 +156,7 @@ def test_lloyd_ties_and_duplicates(ctx):
     a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", rows)
     oa, od = oracle.lloyd_assign(X.cpu().numpy(), Cc.cpu().numpy(), "euclidean", rows)
     assert np.array_equal(a.cpu().numpy(), oa)
-    assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
+    assert_dist(dist.cpu().numpy(), od, dist_mode)
     assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0
 
 
@@ -190,7 +190,7 @@ def test_hash_assign_fused_vs_oracle(ctx, form, monkeypatch, dist_mode):
 
 
 @pytest.mark.parametrize("path", ["f32", "exact"])
-def test_assign_paths_agree(ctx, path, monkeypatch):
+def test_assign_paths_agree(ctx, path, monkeypatch, dist_mode):
     N, d, K = 30_000, 128, 64
     X = ctx.synth(21, N, d)
     Cc = X[:K].double() * 1.0001
@@ -198,7 +198,8 @@ def test_assign_paths_agree(ctx, path, monkeypatch):
     monkeypatch.setenv("LSHKM_ASSIGN_PATH", path)
     a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
     assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
-    assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
+    # the f32-MFMA and exact paths always give the exact-order distance
+    assert_dist(d0.cpu().numpy(), d1.cpu().numpy(), dist_mode)
 
 
 @pytest.mark.parametrize("d,K,case", [(128, 256, "rows"), (100, 64, "rows"), (16, 1, "rows"), (256, 300, "scaled"),
@@ -244,7 +245,7 @@ def test_cosine_mfma_vs_exact(ctx, d, K, case, monkeypatch):
 
 @pytest.mark.parametrize("N,K,L,k", [(1, 1, 1, 4), (65, 64, 8, 4), (4099, 300, 8, 4), (777, 256, 3, 3),
                                      (2048, 200, 2, 4), (1500, 256, 7, 2)])
-def test_hash_assign_shapes(ctx, N, K, L, k):
+def test_hash_assign_shapes(ctx, N, K, L, k, dist_mode):
     # persistent form (K <= 256, k = 4) and the chunked form (K > 256 or k != 4)
     d = 128
     Xh = oracle.synth(31 + N, N, d)
@@ -261,12 +262,12 @@ def test_hash_assign_shapes(ctx, N, K, L, k):
     assert np.array_equal(bu.cpu().numpy(), xb)
     oa, od = oracle.lloyd_assign(Xh, Ch, "euclidean", None)
     assert np.array_equal(a.cpu().numpy(), oa)
-    # centroids are not fp32-valued: glibc pow vs x*x may differ in the last bit (DESIGN.md §4)
-    np.testing.assert_allclose(dist.cpu().numpy(), od, rtol=1e-14, atol=0)
+    # centroids are not fp32-valued: glibc pow vs x*x may differ in the last bit (DESIGN.md §5)
+    assert_dist_tol(dist.cpu().numpy(), od, dist_mode, 1e-14)
 
 
 @pytest.mark.parametrize("form", ["persistent", "chunked"])
-def test_fused_range_guard(ctx, form, monkeypatch):
+def test_fused_range_guard(ctx, form, monkeypatch, dist_mode):
     # values beyond the f16 range must never be certified by the split path
     # (in the persistent form every function of such a row goes through the fix-up pass)
     if form == "chunked":
@@ -284,17 +285,17 @@ def test_fused_range_guard(ctx, form, monkeypatch):
     oa, od = oracle.lloyd_assign(Xh, Xh[:K].astype(np.float64), "euclidean", None)
     assert np.array_equal(tu.cpu().numpy(), xt) and np.array_equal(bu.cpu().numpy(), xb)
     assert np.array_equal(a.cpu().numpy(), oa)
-    assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
+    assert_dist(dist.cpu().numpy(), od, dist_mode if form == "persistent" else "exact")
     # and centroids beyond the range
     Cbig = Cc.clone(); Cbig[2, 0] = 5.0e4
     a2, d2 = lshkm.lloyd_assign(ctx, X, Cbig, "euclidean")
     oa2, od2 = oracle.lloyd_assign(Xh, Cbig.cpu().numpy(), "euclidean", None)
     assert np.array_equal(a2.cpu().numpy(), oa2)
-    assert np.array_equal(d2.cpu().numpy().view(np.uint64), od2.view(np.uint64))
+    assert_dist(d2.cpu().numpy(), od2, dist_mode)
 
 
 @pytest.mark.parametrize("case", ["ties", "near", "nonfinite"])
-def test_pruned_exact_pass(ctx, case, monkeypatch):
+def test_pruned_exact_pass(ctx, case, monkeypatch, dist_mode):
     # the listed-row pass (f32 candidate pruning + exact order on the candidates)
     # against the every-centroid pass and the oracle: duplicate centroids (exact
     # ties, first index must win), near-duplicates (many candidates), and rows
@@ -322,7 +323,7 @@ def test_pruned_exact_pass(ctx, case, monkeypatch):
     sub = np.random.default_rng(4).choice(N, 3000, replace=False)
     oa, od = oracle.lloyd_assign(Xh[sub], Ch, "euclidean", None)
     assert np.array_equal(a.cpu().numpy()[sub], oa)
-    np.testing.assert_allclose(dist.cpu().numpy()[sub], od, rtol=1e-14, atol=0)
+    assert_dist_tol(dist.cpu().numpy()[sub], od, dist_mode, 1e-14)   # "near": non-fp32 centroids
 
 
 @pytest.mark.parametrize("d", [64, 128])
@@ -361,7 +362,7 @@ def test_cosine_certified_quotient_adversarial(ctx, case, d, monkeypatch):
 
 
 @pytest.mark.parametrize("metric", ["euclidean", "cosine"])
-def test_multipass_persistent_k1024(ctx, metric, monkeypatch):
+def test_multipass_persistent_k1024(ctx, metric, monkeypatch, dist_mode):
     # K > 256 on the persistent form: one launch per 256-centroid slice with the
     # per-lane (best, runner-up, tile) carried across launches; duplicates in
     # different slices (exact ties: the first index must win) and a ragged last
@@ -377,16 +378,17 @@ def test_multipass_persistent_k1024(ctx, metric, monkeypatch):
     a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, metric)
     monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
     a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, metric)
+    mode = dist_mode if metric == "euclidean" else "exact"      # cosine distances are exact-order in both
     assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
-    assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
+    assert_dist(d0.cpu().numpy(), d1.cpu().numpy(), mode)
     sub = np.random.default_rng(2).choice(N, 600, replace=False)
     oa, od = oracle.lloyd_assign(X.cpu().numpy()[sub], Cc.cpu().numpy(), metric, None)
     assert np.array_equal(a0.cpu().numpy()[sub], oa)
-    assert np.array_equal(d0.cpu().numpy()[sub].view(np.uint64), od.view(np.uint64))
+    assert_dist(d0.cpu().numpy()[sub], od, mode)
 
 
 @pytest.mark.parametrize("hashed", [False, True])
-def test_two_image_k1000(ctx, hashed, monkeypatch):
+def test_two_image_k1000(ctx, hashed, monkeypatch, dist_mode):
     # the opt-in one-launch form for 512 < K <= 1024 (LSHKM_HI_TWO_IMAGE=1): the
     # block swaps 512-centroid images between the halves of each tile; ties
     # across the images, a ragged second image (K = 1000) and a partial last
@@ -408,8 +410,9 @@ def test_two_image_k1000(ctx, hashed, monkeypatch):
     monkeypatch.setenv("LSHKM_HI_TWO_IMAGE", "1")
     got = [v.cpu().numpy() for v in run() if v is not None]
     assert len(ref) == len(got)
-    for a, b in zip(ref, got):
+    for a, b in zip(ref[:-1], got[:-1]):                 # tuples / buckets / cluster IDs
         assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+    assert_dist(got[-1], ref[-1], dist_mode, both_certified=True)
 
 
 @pytest.mark.parametrize("N,K,case", [(200_000, 256, "rows"), (50_000, 1000, "rows"), (30_011, 64, "special"),
@@ -465,7 +468,7 @@ def test_cosine_hash_assign_golden(ctx, name):
     assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
 
 
-def test_override_rows_change_between_calls(ctx):
+def test_override_rows_change_between_calls(ctx, dist_mode):
     # the override rows are cached on the device while unchanged (api.cpp): a
     # call with other rows (same K) must override those, and a repeat the first
     N, d, K = 20_000, 128, 64
@@ -477,4 +480,4 @@ def test_override_rows_change_between_calls(ctx):
         a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean", src)
         oa, od = oracle.lloyd_assign(X.cpu().numpy(), Cc.cpu().numpy(), "euclidean", src)
         assert np.array_equal(a.cpu().numpy(), oa)
-        assert np.array_equal(dist.cpu().numpy().view(np.uint64), od.view(np.uint64))
+        assert_dist(dist.cpu().numpy(), od, dist_mode)

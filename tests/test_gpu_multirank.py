@@ -2,7 +2,9 @@
 share the one MI355X over gloo, each running liblshkm on its row shard
 (tests/mr_worker.py), against one process over all rows.
 
-  - hash tuples, bucket IDs, cluster IDs and distances: bit-exact (per row);
+  - hash tuples, bucket IDs, cluster IDs and distances: bit-exact (per row),
+    in both distance modes of the context (certified: the shipped default;
+    exact), and the iteration-0 distances against the oracle per the mode;
   - k-means centers, fast mode (all-reduce of per-shard sums): <= 1e-13 rel;
   - k-means centers, exact mode (rank-to-rank carry chain): bit-exact;
   - cosine (cosine index + cosine Lloyd in one pass, fast mode): buckets,
@@ -32,10 +34,11 @@ def _free_port():
     return p
 
 
-def _run(world, out):
+def _run(world, out, dist_mode):
     port = str(_free_port())
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    procs = [subprocess.Popen([sys.executable, "-u", WORKER, str(r), str(world), port, str(out)], env=env,
+    env = {k: v for k, v in os.environ.items() if k != "LSHKM_DIST"}      # the ABI mode alone decides
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    procs = [subprocess.Popen([sys.executable, "-u", WORKER, str(r), str(world), port, str(out), dist_mode], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
     logs = []
     for p in procs:
@@ -50,11 +53,13 @@ def _run(world, out):
     return [dict(np.load(os.path.join(out, f"rank{r}.npz"))) for r in range(world)]
 
 
-def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
+@pytest.mark.parametrize("dist_mode", ["certified", "exact"])
+def test_two_ranks_on_one_gpu_match_single_process(tmp_path, dist_mode):
     (tmp_path / "one").mkdir()
     (tmp_path / "two").mkdir()
-    one = _run(1, tmp_path / "one")[0]
-    two = _run(2, tmp_path / "two")
+    one = _run(1, tmp_path / "one", dist_mode)[0]
+    two = _run(2, tmp_path / "two", dist_mode)
+    assert all(str(r["dist_mode"][0]) == dist_mode for r in two + [one])
     cat = lambda key: np.concatenate([r[key] for r in two])
     for mode in ("fast", "exact"):
         assert np.array_equal(cat(f"{mode}_tuples"), one[f"{mode}_tuples"]), mode
@@ -82,6 +87,20 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     cc, cc_one = two[0]["cos_centers1"], one["cos_centers1"]
     assert np.array_equal(cc, two[1]["cos_centers1"])
     assert (np.abs(cc - cc_one) / np.maximum(np.abs(cc_one), 1e-300)).max() <= 1e-13
+    # iteration 0 against the oracle: IDs bit-exact, distances per the mode's
+    # contract (a sample of rows; centroid-override rows are (c, 0))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from conftest import assert_dist
+    sys.path.insert(0, os.path.join(ROOT, "crypto-recommendation_amd"))
+    import sharding as sh
+    N, K = 120_000, 1024
+    rows = sh.centroid_rows(N, K)
+    Xall = oracle.synth(0x5EED, N, 128)
+    sub = np.setdiff1d(np.random.default_rng(8).choice(N, 2000, replace=False), rows)
+    oa, od = oracle.lloyd_assign(Xall[sub], Xall[rows].astype(np.float64), "euclidean", None)
+    assert np.array_equal(cat("fast_assign0")[sub], oa)
+    assert_dist(cat("fast_dist0")[sub], od, dist_mode)
     # hypercube: same coins, same engine state, same vertices
     for key in ("memo_f", "memo_h", "memo_bit", "memo_state"):
         for r in two:
