@@ -2,7 +2,9 @@
 // get_P_closest and get_top_N_recom (lib/crypto_rec.hpp:213-325).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <vector>
 
 #include "../../include/lshkm.h"
 #include "common.h"
@@ -70,6 +72,72 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X, const double* x_mean, int6
     }
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     return 0;
+}
+
+}  // extern "C"
+
+// get_top_N_recom(neighbors, user, N), crypto_rec.hpp:327-345, over whole
+// clusters (main.cpp:260-269, :353-373). The cluster sizes come to the host
+// once to size the per-wave similarity scratch (waves x largest cluster).
+static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_t N, int d, const int64_t* crow,
+                              const int32_t* crows, int K, Pts U, const double* u_mean, int64_t nq,
+                              const int32_t* ucl, const int64_t* unk_ptr, const int32_t* unk_idx, int n_top,
+                              int32_t* out) {
+    LSHKM_CHECK(ctx && X.p && x_mean && crow && U.p && u_mean && ucl && unk_ptr && out && N >= 1 && d >= 1 &&
+                    K >= 1 && nq >= 0 && n_top >= 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    if (nq == 0 || n_top == 0) return 0;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    std::vector<int64_t> hc((size_t)K + 1);
+    int64_t total = 0;
+    LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    int64_t maxn = 0;
+    bool ok = hc[0] == 0;
+    for (int c = 0; c < K && ok; c++) {
+        ok = hc[c + 1] >= hc[c];
+        maxn = std::max<int64_t>(maxn, hc[c + 1] - hc[c]);
+    }
+    LSHKM_CHECK(ok && hc[K] <= N && (hc[K] == 0 || crows), LSHKM_ERR_ARG,
+                "bad cluster CSR (crow must start at 0, not decrease, and hold at most N members)");
+    LSHKM_CHECK(maxn < (1ll << 31), LSHKM_ERR_ARG, "a cluster of 2^31 members or more");
+    LSHKM_CHECK(total >= 0 && (total == 0 || unk_idx), LSHKM_ERR_ARG, "bad unknown-index lists");
+    // one wave per user in flight; the scratch row of a wave holds one cluster's
+    // similarities (at most 1 GiB of scratch: fewer waves for huge clusters)
+    const int64_t row = std::max<int64_t>(maxn, 1);
+    int64_t nw = std::min<int64_t>(nq, 8192);
+    nw = std::min<int64_t>(nw, std::max<int64_t>((int64_t)RC_CLUSTER_WAVES_PER_BLOCK, (1ll << 30) / (row * 8)));
+    nw = (nw + RC_CLUSTER_WAVES_PER_BLOCK - 1) / RC_CLUSTER_WAVES_PER_BLOCK * RC_CLUSTER_WAVES_PER_BLOCK;
+    Buf &scratch = ctx->ws_call[0], &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
+    const size_t M = (size_t)(total > 0 ? total : 1);
+    int rc;
+    if ((rc = scratch.reserve(sizeof(double) * (size_t)nw * row)) || (rc = pred.reserve(sizeof(double) * M)) ||
+        (rc = pidx.reserve(sizeof(int32_t) * M)))
+        return rc;
+    if ((rc = launch_rc_cluster_top_n(ctx->stream, X, x_mean, d, crow, crows, K, U, u_mean, nq, ucl, unk_ptr, unk_idx,
+                                      n_top, scratch.as<double>(), row, (int)nw, pred.as<double>(), pidx.as<int32_t>(),
+                                      out, (unsigned long long*)ctx->stats.p + STAT_REC_SOFT))) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return rc;
+    }
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the workspace is reused by the next call
+    return 0;
+}
+
+extern "C" {
+
+int lshkm_cluster_top_n(lshkm_ctx ctx, const float* X, const double* x_mean, int64_t N, int d, const int64_t* crow,
+                        const int32_t* crows, int K, const float* U, const double* u_mean, int64_t nq,
+                        const int32_t* ucl, const int64_t* unk_ptr, const int32_t* unk_idx, int n_top, int32_t* out) {
+    return cluster_top_n_impl(ctx, X, x_mean, N, d, crow, crows, K, U, u_mean, nq, ucl, unk_ptr, unk_idx, n_top, out);
+}
+
+int lshkm_cluster_top_n_f64(lshkm_ctx ctx, const double* X, const double* x_mean, int64_t N, int d,
+                            const int64_t* crow, const int32_t* crows, int K, const double* U, const double* u_mean,
+                            int64_t nq, const int32_t* ucl, const int64_t* unk_ptr, const int32_t* unk_idx, int n_top,
+                            int32_t* out) {
+    return cluster_top_n_impl(ctx, X, x_mean, N, d, crow, crows, K, U, u_mean, nq, ucl, unk_ptr, unk_idx, n_top, out);
 }
 
 }  // extern "C"

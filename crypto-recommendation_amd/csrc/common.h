@@ -59,6 +59,7 @@ enum Stat {
     STAT_COS_FIX = 4,        // cosine Lloyd winners whose distance took the soft-x87 chain
     STAT_REFINED = 5,        // rows the hi-only fused pass left to the 3-product refinement
     STAT_HASH_FIX = 6,       // rows the fused pass listed for the hash fix-up (an uncertified floor / sign)
+    STAT_REC_SOFT = 7,       // clustering-recommender similarities decided by the x87 chain (IpAcc declined)
     STAT_COUNT = 8
 };
 

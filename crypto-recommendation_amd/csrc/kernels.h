@@ -176,6 +176,12 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
 
 // Recommend step (recom.hip): fp64 rows, per-user candidate CSR.
 int launch_rc_norms(hipStream_t s, const double* X, int64_t N, int d, double* xa);
+int launch_rc_cluster_top_n(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow,
+                            const int32_t* crows, int K, Pts U, const double* u_mean, int64_t nq, const int32_t* ucl,
+                            const int64_t* unk_ptr, const int32_t* unk_idx, int n_top, double* scratch,
+                            int64_t scratch_row, int nwaves, double* pred, int32_t* pidx, int32_t* out,
+                            unsigned long long* soft_count);
+constexpr int RC_CLUSTER_WAVES_PER_BLOCK = 4;     // rc_cluster_top_n_kernel: waves per block (RC_WAVES)
 int launch_rc_p_closest(hipStream_t s, const double* X, const double* xa, int d, const double* U, int64_t nq,
                         const int64_t* cand_ptr, const int32_t* cand_idx, int P, double* sim, double* key,
                         int32_t* pos, int32_t* out_idx, double* out_sim, int32_t* out_cnt, int32_t* replay,

@@ -281,6 +281,213 @@ __global__ __launch_bounds__(64 * RC_WAVES) void rc_top_n_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// The clustering recommenders' get_top_N_recom(neighbors, user, N) -- the
+// 3-argument overload (crypto_rec.hpp:327-345) over the user's whole cluster
+// (main.cpp:260-269 Part A: the user's own cluster; :353-373 Part B: the
+// cluster of the nearest centroid). One wave per user:
+//   phase 1: cosineSimilarity(member, user) of every member, lane per member,
+//     certified by IpAcc (exact.h; ~3% decline), the declined members queued
+//     in LDS and run through the X87acc chain 64 at a time (all lanes busy),
+//     sims into the wave's scratch row in member order;
+//   phase 2: get_predicted_user_sim (:280-306): lane per unknown index (CR_MI
+//     per lane), the member loop in order, 64 members per chunk read coalesced
+//     (sim, mean, row id) and broadcast by readlane, the row values of the next
+//     8 members loaded ahead of the dependent fp64 chains;
+//   the Lomuto quicksort of the predictions (lane 0, :341) and the first n_top,
+//   0-padded (:343). Users of an empty cluster get -1 (main.cpp skips them).
+constexpr int CR_MI = 4;          // unknown indexes per lane per pass (256 per pass)
+constexpr int CR_Q = 128;         // LDS queue of declined members per wave
+
+__device__ inline double cr_rl(double v, int t) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), t);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), t);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <typename T>
+__device__ inline double cr_sumsq(const T* __restrict__ x, int d) {
+    double a = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double v = (double)x[j];
+        a = __dadd_rn(a, __dmul_rn(v, v));
+    }
+    return a;
+}
+
+// IpAcc certificate of cosineSimilarity(x, u) (cust_vector.hpp:158-174);
+// false: the x87 chain must decide (declined, or a zero denominator)
+template <typename T>
+__device__ inline bool cr_sim_cert(const T* __restrict__ x, const T* __restrict__ u, int d, double ub, double& s,
+                                   double& denom) {
+    IpAcc ip;
+    double xa = 0.0;
+    for (int j = 0; j < d; j++) {
+        const double xj = (double)x[j], uj = (double)u[j];
+        ip.add(__dmul_rn(xj, uj));
+        xa = __dadd_rn(xa, __dmul_rn(xj, xj));
+    }
+    denom = __dmul_rn(sqrt(xa), sqrt(ub));
+    double qr;
+    return ip.quot_status(denom, s, qr) == 0;
+}
+
+template <typename T>
+__device__ inline double cr_sim_x87(const T* __restrict__ x, const T* __restrict__ u, int d, double denom) {
+    X87acc ip;
+    ip.init();
+    for (int j = 0; j < d; j++) ip.add(__dmul_rn((double)x[j], (double)u[j]));
+    return x87_quot(ip.value(), denom);
+}
+
+template <typename T>
+__global__ __launch_bounds__(64 * RC_WAVES) void rc_cluster_top_n_kernel(
+    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const int64_t* __restrict__ crow,
+    const int32_t* __restrict__ crows, int K, const T* __restrict__ U, const double* __restrict__ u_mean, int64_t nq,
+    const int32_t* __restrict__ ucl, const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx,
+    int n_top, double* __restrict__ scratch, int64_t scratch_row, double* __restrict__ pred, int32_t* __restrict__ pidx,
+    int32_t* __restrict__ out, unsigned long long* __restrict__ soft_count) {
+    __shared__ int32_t queue[RC_WAVES][CR_Q];
+    __shared__ double qden[RC_WAVES][CR_Q];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t w0 = (int64_t)blockIdx.x * RC_WAVES + wv;
+    const int64_t nw = (int64_t)gridDim.x * RC_WAVES;
+    double* sim = scratch + w0 * scratch_row;       // this wave's similarities, member order
+    unsigned long long soft = 0;
+    for (int64_t q = w0; q < nq; q += nw) {
+        const int c = ucl[q];
+        const int64_t base = (c >= 0 && c < K) ? crow[c] : 0;
+        const int n = (c >= 0 && c < K) ? (int)(crow[c + 1] - base) : 0;
+        if (n == 0) {                                   // main.cpp:262 / :366 skip the user
+            for (int i = lane; i < n_top; i += 64) out[q * n_top + i] = -1;
+            continue;
+        }
+        const int64_t o = unk_ptr[q];
+        const int m = (int)(unk_ptr[q + 1] - o);
+        const T* u = U + q * d;
+        if (m > 0) {
+            // phase 1: similarities in member order
+            const double ub = cr_sumsq(u, d);
+            int nqd = 0;                                // queued declines
+            auto drain = [&](int cnt) {                 // the x87 chain for queue[0 .. cnt)
+                if (lane < cnt) {
+                    const int i = queue[wv][lane];
+                    sim[i] = cr_sim_x87(X + (int64_t)crows[base + i] * d, u, d, qden[wv][lane]);
+                }
+                soft += (unsigned long long)cnt;
+            };
+            for (int b = 0; b < n; b += 64) {
+                const int i = b + lane;
+                bool dec = false;
+                double s = 0.0, den = 0.0;
+                if (i < n) {
+                    dec = !cr_sim_cert(X + (int64_t)crows[base + i] * d, u, d, ub, s, den);
+                    if (!dec) sim[i] = s;
+                }
+                const unsigned long long mask = __ballot(dec);
+                const int pos = nqd + __popcll(mask & ((1ull << lane) - 1ull));
+                if (dec) { queue[wv][pos] = i; qden[wv][pos] = den; }
+                nqd += __popcll(mask);
+                wave_sync();
+                if (nqd >= 64) {
+                    drain(64);
+                    const int rest = nqd - 64;
+                    int32_t qi = 0; double qd = 0.0;
+                    if (lane < rest) { qi = queue[wv][64 + lane]; qd = qden[wv][64 + lane]; }
+                    wave_sync();
+                    if (lane < rest) { queue[wv][lane] = qi; qden[wv][lane] = qd; }
+                    nqd = rest;
+                    wave_sync();
+                }
+            }
+            if (nqd > 0) drain(nqd);
+            __threadfence_block();
+            wave_sync();
+            // phase 2: get_predicted_user_sim, CR_MI * 64 unknown indexes per pass
+            const double um = u_mean[q];
+            for (int g0 = 0; g0 < m; g0 += 64 * CR_MI) {
+                int idx[CR_MI];
+                bool ok[CR_MI];
+                double acc[CR_MI];
+#pragma unroll
+                for (int k = 0; k < CR_MI; k++) {
+                    const int e = g0 + lane + 64 * k;
+                    ok[k] = e < m;
+                    idx[k] = ok[k] ? unk_idx[o + e] : 0;
+                    acc[k] = 0.0;
+                }
+                double abs_sum = 0.0;
+                for (int b = 0; b < n; b += 64) {
+                    const int cnt = n - b < 64 ? n - b : 64;
+                    int32_t r = 0;
+                    double sv = 0.0, mv = 0.0;
+                    if (lane < cnt) {
+                        r = crows[base + b + lane];
+                        sv = sim[b + lane];
+                        mv = x_mean[r];
+                    }
+                    for (int t0 = 0; t0 < cnt; t0 += 8) {
+                        double xv[8][CR_MI];
+#pragma unroll
+                        for (int tt = 0; tt < 8; tt++) {
+                            const int64_t rr = (int64_t)__builtin_amdgcn_readlane(r, t0 + tt);
+#pragma unroll
+                            for (int k = 0; k < CR_MI; k++)
+                                xv[tt][k] = (t0 + tt < cnt && ok[k]) ? (double)X[rr * d + idx[k]] : 0.0;
+                        }
+#pragma unroll
+                        for (int tt = 0; tt < 8; tt++) {
+                            if (t0 + tt >= cnt) break;
+                            const double cs = cr_rl(sv, t0 + tt), nm = cr_rl(mv, t0 + tt);
+                            abs_sum = __dadd_rn(abs_sum, fabs(cs));
+#pragma unroll
+                            for (int k = 0; k < CR_MI; k++)
+                                acc[k] = __dadd_rn(acc[k], __dmul_rn(cs, __dsub_rn(xv[tt][k], nm)));
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < CR_MI; k++)
+                    if (ok[k]) {
+                        const int e = g0 + lane + 64 * k;
+                        pred[o + e] = __dadd_rn(__ddiv_rn(acc[k], abs_sum), um);
+                        pidx[o + e] = idx[k];
+                    }
+            }
+            __threadfence_block();
+            wave_sync();
+        }
+        if (lane == 0) {
+            if (m > 0) lomuto_sort(pred + o, pidx + o, m);
+            for (int i = 0; i < n_top; i++) out[q * n_top + i] = i < m ? pidx[o + i] : 0;
+        }
+        wave_sync();
+    }
+    if (soft_count) {
+        // one atomic per wave
+        if (lane == 0 && soft) atomicAdd(soft_count, soft);
+    }
+}
+
+int launch_rc_cluster_top_n(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow,
+                            const int32_t* crows, int K, Pts U, const double* u_mean, int64_t nq, const int32_t* ucl,
+                            const int64_t* unk_ptr, const int32_t* unk_idx, int n_top, double* scratch,
+                            int64_t scratch_row, int nwaves, double* pred, int32_t* pidx, int32_t* out,
+                            unsigned long long* soft_count) {
+    if (nq <= 0) return 0;
+    const unsigned grid = (unsigned)((nwaves + RC_WAVES - 1) / RC_WAVES);
+    if (X.f64)
+        hipLaunchKernelGGL(rc_cluster_top_n_kernel<double>, dim3(grid), dim3(64 * RC_WAVES), 0, s, X.d(), x_mean, d,
+                           crow, crows, K, U.d(), u_mean, nq, ucl, unk_ptr, unk_idx, n_top, scratch, scratch_row, pred,
+                           pidx, out, soft_count);
+    else
+        hipLaunchKernelGGL(rc_cluster_top_n_kernel<float>, dim3(grid), dim3(64 * RC_WAVES), 0, s, X.f(), x_mean, d,
+                           crow, crows, K, U.f(), u_mean, nq, ucl, unk_ptr, unk_idx, n_top, scratch, scratch_row, pred,
+                           pidx, out, soft_count);
+    return kstatus("rc_cluster_top_n_kernel");
+}
+
 int launch_rc_norms(hipStream_t s, const double* X, int64_t N, int d, double* xa) {
     hipLaunchKernelGGL(rc_norm_kernel, dim3(gsz(N, 256, 4096)), dim3(256), 0, s, X, N, d, xa);
     return kstatus("recom.hip");

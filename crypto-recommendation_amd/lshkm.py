@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("LSHKM_LIB") or os.path.join(_HERE, "liblshkm.so")   #
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "lshkm.h")
 
 EUCLIDEAN, COSINE = 0, 1
-STAT_HASH_EXACT, STAT_ASSIGN_AMBIG, STAT_COS_FIX, STAT_REFINED, STAT_HASH_FIX = 0, 1, 4, 5, 6
+STAT_HASH_EXACT, STAT_ASSIGN_AMBIG, STAT_COS_FIX, STAT_REFINED, STAT_HASH_FIX, STAT_REC_SOFT = 0, 1, 4, 5, 6, 7
 _METRIC = {"euclidean": EUCLIDEAN, "cosine": COSINE, EUCLIDEAN: EUCLIDEAN, COSINE: COSINE}
 DIST_CERTIFIED, DIST_EXACT = 0, 1
 _DIST = {"certified": DIST_CERTIFIED, "default": DIST_CERTIFIED, "exact": DIST_EXACT,
@@ -107,6 +107,7 @@ def lib():
             "lshkm_rand_selection": (i32, [u64, i64, i32, vp]),
             "lshkm_p_closest": (i32, [vp, vp, i64, i32, vp, i64, vp, vp, i32, vp, vp, vp]),
             "lshkm_top_n_recom": (i32, [vp, vp, vp, i64, i32, vp, i64, vp, vp, vp, vp, vp, i32, i32, vp]),
+            "lshkm_cluster_top_n": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, vp, vp, i64, vp, vp, vp, i32, vp]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
             "lshkm_clusters": (i32, [vp, vp, i64, i32, vp, vp]),
         }
@@ -592,6 +593,24 @@ def top_n_recom(ctx, X, x_mean, u_mean, unk_ptr, unk_idx, nb_idx, nb_sim, nb_cnt
     _ck(lib().lshkm_top_n_recom(ctx.h, _t_ptr(X), _t_ptr(x_mean), N, d, _t_ptr(u_mean), nq, _t_ptr(unk_ptr),
                                 _t_ptr(unk_idx) if unk_idx.numel() else None, _t_ptr(nb_idx), _t_ptr(nb_sim),
                                 _t_ptr(nb_cnt), P, n_top, _t_ptr(out)))
+    return out
+
+
+def cluster_top_n(ctx, X, x_mean, crow, crows, U, u_mean, ucl, unk_ptr, unk_idx, n_top):
+    """get_top_N_recom(neighbors, user, N) (crypto_rec.hpp:327-345) for every user
+    of U, its neighbours = the members of cluster ucl[q] (crow [K+1] int64 /
+    crows int32, lshkm_clusters' CSR), as main.cpp:260-269 / :353-373 call it.
+    X [N][d] / U [nq][d] rows of one dtype (fp32 or fp64), means fp64, all device
+    tensors. Returns [nq][n_top] int32 (0-padded; -1 rows: empty cluster)."""
+    torch = ctx.torch
+    N, d = X.shape
+    nq = U.shape[0]
+    K = crow.shape[0] - 1
+    out = ctx.empty((nq, n_top), torch.int32)
+    _ck(_fn("lshkm_cluster_top_n", X)(ctx.h, _t_ptr(X), _t_ptr(x_mean), N, d, _t_ptr(crow),
+                                      _t_ptr(crows) if crows.numel() else None, K, _t_ptr(U), _t_ptr(u_mean), nq,
+                                      _t_ptr(ucl), _t_ptr(unk_ptr), _t_ptr(unk_idx) if unk_idx.numel() else None,
+                                      n_top, _t_ptr(out)))
     return out
 
 

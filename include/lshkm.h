@@ -102,7 +102,9 @@ int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t
  * 1 = points whose argmin needed the exact all-centroid pass,
  * 2 = k-means++ prefix-sum chunks walked, 3 = of which summed element by element,
  * 4 = cosine Lloyd winner distances the certified fast form declined (soft-x87 chain),
- * 5 = rows the hi-only fused pass (one f16 product per score) left to the 3-product form. */
+ * 5 = rows the hi-only fused pass (one f16 product per score) left to the 3-product form,
+ * 6 = rows the fused pass listed for the hash fix-up,
+ * 7 = clustering-recommender similarities decided by the x87 chain (lshkm_cluster_top_n). */
 int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);
 int lshkm_reset_stats(lshkm_ctx ctx);
 /* HIP-event timing of the dominant kernel launch (the fused hash+assign kernel)
@@ -366,6 +368,33 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X_dev, const double* x_mean_d
                       const double* u_mean_dev, int64_t nq, const int64_t* unk_ptr_dev, const int32_t* unk_idx_dev,
                       const int32_t* nb_idx_dev, const double* nb_sim_dev, const int32_t* nb_cnt_dev, int P,
                       int n_top, int32_t* out_dev);
+
+/* get_top_N_recom(neighbors, user, N) -- the 3-argument overload
+ * (crypto_rec.hpp:327-345) -- as the clustering recommenders call it:
+ * main.cpp:260-269 (Part A: user q's own cluster) and :353-373 (Part B: the
+ * cluster of the user's nearest centroid, i.e. lshkm_lloyd_assign of the users
+ * without the override). User q's neighbours are the members of cluster
+ * ucl_dev[q], crows_dev[crow_dev[c] .. crow_dev[c+1]) in member order (what
+ * lshkm_clusters returns: separate_clusters_from_input, utils.hpp:150-158);
+ * similarities = cosineSimilarity(member, user) in that order (x87-exact,
+ * cust_vector.hpp:158-174); predictions = get_predicted_user_sim over all of
+ * them (:280-306; x_mean_dev [N] / u_mean_dev [nq] = getKnownMean, unk_* = CSR
+ * of each user's ascending unknown indexes, values in [0, d)); the reference's
+ * quicksort of the predictions (:234-277, ties / NaNs included); out_dev
+ * [nq][n_top] = the first n_top unknown indexes, 0-padded like vector::resize.
+ * Users whose cluster is empty (or ucl outside [0, K)) get -1 in every slot:
+ * main.cpp skips them (:262, :366). X_dev [N][d] pool rows and U_dev [nq][d]
+ * users share the element type (for Part A pass the same rows twice). Counter
+ * 7 counts the similarities the x87 chain decided. Bit-exact when the squares of
+ * the components are exact in fp64 (pow(x, 2)). */
+int lshkm_cluster_top_n(lshkm_ctx ctx, const float* X_dev, const double* x_mean_dev, int64_t N, int d,
+                        const int64_t* crow_dev, const int32_t* crows_dev, int K, const float* U_dev,
+                        const double* u_mean_dev, int64_t nq, const int32_t* ucl_dev, const int64_t* unk_ptr_dev,
+                        const int32_t* unk_idx_dev, int n_top, int32_t* out_dev);
+int lshkm_cluster_top_n_f64(lshkm_ctx ctx, const double* X_dev, const double* x_mean_dev, int64_t N, int d,
+                            const int64_t* crow_dev, const int32_t* crows_dev, int K, const double* U_dev,
+                            const double* u_mean_dev, int64_t nq, const int32_t* ucl_dev, const int64_t* unk_ptr_dev,
+                            const int32_t* unk_idx_dev, int n_top, int32_t* out_dev);
 
 /* ------------------------------------------------------------ input formats
  * Host only (no device needed). VectorReader<double>::read

@@ -18,6 +18,8 @@
  *   k_means                 lib/clustering_phases/update.hpp:37-86
  *   k_means_pp              lib/clustering_phases/initialization.hpp:71-156
  *   rand_selection          lib/clustering_phases/initialization.hpp:39-69
+ *   get_P_closest           lib/crypto_rec.hpp:213-231
+ *   get_top_N_recom (both overloads)  lib/crypto_rec.hpp:309-345
  *
  * Same signatures, same return values and the same ownership as the
  * reference: the hashtables are real CustHashtable objects (the caller deletes
@@ -615,6 +617,48 @@ std::vector<int> get_top_N_recom(std::vector<CustVector<T>*>& neighbors, CustVec
     download(o.data(), od, N);
     for (int i = 0; i < N; i++) out[i] = o[i];
     return out;
+}
+
+// get_top_N_recom(neighbors, user, N) -- the 3-argument overload
+// (crypto_rec.hpp:327-345) the clustering recommenders call with a whole
+// cluster (main.cpp:266, :370): similarities to every neighbour in order,
+// predictions over all of them, the quicksort, first N (0-padded).
+template <typename T>
+std::vector<int> get_top_N_recom(std::vector<CustVector<T>*>& neighbors, CustVector<T>& user, int N) {
+    static_assert(std::is_same<T, double>::value, "lshkm_compat::get_top_N_recom matches CustVector<double> only");
+    const size_t n = neighbors.size(), d = user.getDimensions()->size();
+    if (N <= 0) return std::vector<int>();
+    // no neighbours: every prediction is 0/0 (the 4-argument path computes the
+    // same sums over an empty list)
+    if (n == 0) return lshkm_compat::get_top_N_recom<T>(neighbors, user, N, std::vector<double>());
+    std::vector<double> X(n * d), xm(n);
+    for (size_t i = 0; i < n; i++) {
+        const std::vector<T>& x = *neighbors[i]->getDimensions();
+        if (x.size() != d) throw std::invalid_argument("lshkm_compat: neighbour dimension mismatch");
+        for (size_t j = 0; j < d; j++) X[i * d + j] = x[j];
+        xm[i] = neighbors[i]->getKnownMean();
+    }
+    // the neighbours as one cluster of an n-row pool, in their order
+    std::vector<int64_t> crow = {0, (int64_t)n};
+    std::vector<int32_t> crows(n), ucl = {0};
+    for (size_t i = 0; i < n; i++) crows[i] = (int32_t)i;
+    const std::vector<int> unk = user.getUnknownIndexes();
+    for (int e : unk)
+        if (e < 0 || (size_t)e >= d) throw std::out_of_range("lshkm_compat: unknown index outside the vector");
+    std::vector<int64_t> up = {0, (int64_t)unk.size()};
+    std::vector<int32_t> ui(unk.begin(), unk.end());
+    if (ui.empty()) ui.push_back(0);
+    const double um = user.getKnownMean();
+    DevMem Xd = upload(X.data(), X.size()), xmd = upload(xm.data(), n), Ud = upload(user.getDimensions()->data(), d);
+    DevMem umd = upload(&um, 1), crd = upload(crow.data(), 2), crsd = upload(crows.data(), n), ucd = upload(ucl.data(), 1);
+    DevMem upd = upload(up.data(), 2), uid = upload(ui.data(), ui.size());
+    DevMem od(sizeof(int32_t) * N);
+    check(lshkm_cluster_top_n_f64(context(), Xd.as<double>(), xmd.as<double>(), (int64_t)n, (int)d, crd.as<int64_t>(),
+                                  crsd.as<int32_t>(), 1, Ud.as<double>(), umd.as<double>(), 1, ucd.as<int32_t>(),
+                                  upd.as<int64_t>(), uid.as<int32_t>(), N, od.as<int32_t>()));
+    std::vector<int32_t> o(N);
+    download(o.data(), od, N);
+    return std::vector<int>(o.begin(), o.end());
 }
 
 }  // namespace lshkm_compat

@@ -216,6 +216,39 @@ static void check_chain(std::vector<Vec>& data, int k, int L, int P) {
     for (auto t : gpu) delete t;
 }
 
+// main.cpp:240-269 (the clustering recommender, Part A): users clustered by the
+// reference's own lloyds_assignment, then get_top_N_recom(neighbors, user, 5) --
+// the 3-argument overload -- over each user's whole cluster; plus the
+// reference's function on an empty list (0/0 predictions) and N past the count.
+static void check_cluster_recom(std::vector<Vec>& data, int K) {
+    std::vector<Vec> users;
+    users.reserve(data.size());
+    for (size_t i = 0; i < data.size(); i++) {
+        std::set<int> unk;
+        const int d = (int)data[i].getDimensions()->size();
+        for (int j = 0; j < d; j++)
+            if ((j * 3 + (int)i) % 5 == 0) unk.insert(j);
+        users.emplace_back("c" + std::to_string(i), *data[i].getDimensions(), unk, ((int)(i % 13) - 6) / 4.0);
+    }
+    users[3] = Vec("zero", std::vector<double>(data[0].getDimensions()->size(), 0.0), std::set<int>{1, 2}, 0.5);
+    const int N = (int)users.size();
+    std::vector<Vec*> cents;
+    for (int c = 0; c < K; c++) cents.push_back(&users[(size_t)c * (N / K)]);
+    lloyds_assignment(users, cents, std::string("euclidean"));
+    std::vector<std::vector<Vec*>> clusters = separate_clusters_from_input(users, K);
+    const std::string tag = "cluster recom ";
+    for (int q = 0; q < N; q += 5) {
+        std::vector<Vec*> na = clusters[users[q].getCluster()], nb = na;
+        const int nt = q % 3 == 0 ? 5 : (q % 3 == 1 ? 2 : 40);      // 40: past the unknown count (0-padded)
+        if (get_top_N_recom(na, users[q], nt) != lshkm_compat::get_top_N_recom(nb, users[q], nt))
+            fail(tag + "top-N, user " + std::to_string(q));
+        g_stat["cluster_recom_users"]++;
+    }
+    std::vector<Vec*> none_a, none_b;
+    if (get_top_N_recom(none_a, users[1], 5) != lshkm_compat::get_top_N_recom(none_b, users[1], 5))
+        fail(tag + "empty neighbour list");
+}
+
 static void check_init(std::vector<Vec>& data, const std::string& metric, int K) {
     g_seed += 303;
     const std::string tag = "init/" + metric + " ";
@@ -306,6 +339,7 @@ int main(int argc, char** argv) {
         check_init(data, "euclidean", K);
         check_init(data, "cosine", K);
         check_recom(data, 10);
+        check_cluster_recom(data, K);
         check_chain(data, 4, 5, 20);
     } catch (const std::exception& e) {
         std::printf("EXCEPTION %s\n", e.what());

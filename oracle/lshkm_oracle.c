@@ -569,6 +569,54 @@ void or_top_n_recom(int d, const double* X, const double* x_mean, int64_t nq, co
     }
 }
 
+/* get_top_N_recom(neighbors, user, N) -- the 3-argument overload
+ * (crypto_rec.hpp:327-345) -- as the clustering recommenders call it
+ * (main.cpp:260-269 with the user's own cluster, :353-373 with the cluster of
+ * the user's nearest centroid). User q's neighbours are the members of cluster
+ * ucl[q], crows[crow[c] .. crow[c+1]) in member order (separate_clusters_from_input,
+ * utils.hpp:150-158); similarities cosineSimilarity(member, user) in that order
+ * (:330-332); get_predicted_user_sim over all of them (:280-306); the
+ * quicksort of the unknown indexes' predictions (:341); first N, 0-padded
+ * (:343). Users of an empty cluster are skipped by main.cpp (:262, :366): -1
+ * in every slot. out [nq][N]. */
+void or_cluster_top_n(int d, const double* X, const double* x_mean, const int64_t* crow, const int32_t* crows,
+                      int64_t nq, const double* U, const double* u_mean, const int32_t* ucl,
+                      const int64_t* unk_ptr, const int32_t* unk_idx, int N, int32_t* out) {
+    for (int64_t q = 0; q < nq; q++) {
+        const int c = ucl[q];
+        const int64_t b = crow[c];
+        const int n = (int)(crow[c + 1] - b);
+        if (n == 0) {
+            for (int i = 0; i < N; i++) out[q * N + i] = -1;
+            continue;
+        }
+        const double* u = U + (size_t)q * d;
+        double* sim = (double*)malloc(sizeof(double) * (size_t)n);
+        for (int i = 0; i < n; i++) sim[i] = cos_sim_f64(X + (size_t)crows[b + i] * d, u, d);
+        const int64_t o = unk_ptr[q];
+        const int m = (int)(unk_ptr[q + 1] - o);
+        double* pred = (double*)malloc(sizeof(double) * (size_t)(m > 0 ? m : 1));
+        int32_t* ix = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m > 0 ? m : 1));
+        for (int e = 0; e < m; e++) {
+            const int index = unk_idx[o + e];
+            double main_sum = 0, abs_sum = 0;
+            for (int i = 0; i < n; i++) {
+                const double cs = sim[i];
+                abs_sum = abs_sum + fabs(cs);
+                const int32_t r = crows[b + i];
+                main_sum = main_sum + (cs * (X[(size_t)r * d + index] - x_mean[r]));
+            }
+            double p = main_sum / abs_sum;
+            p = p + u_mean[q];
+            pred[e] = p;
+            ix[e] = index;
+        }
+        lomuto_desc(pred, ix, 0, m - 1);
+        for (int i = 0; i < N; i++) out[q * N + i] = i < m ? ix[i] : 0;
+        free(sim); free(pred); free(ix);
+    }
+}
+
 void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out) {
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < rows; i++)

@@ -96,6 +96,17 @@ void or_silhouette(int64_t N, int d, int K, const double* X, const int32_t* assi
 void or_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows);
 void or_kmeans_pp(int64_t N, int d, int K, const double* X, int metric, uint64_t seed, int32_t* rows);
 
+/* ---- recommendation (crypto_rec.hpp:213-345) */
+void or_p_closest(int d, const double* X, int64_t nq, const double* U, const int64_t* cand_ptr,
+                  const int32_t* cand_idx, int P, int32_t* out_idx, double* out_sim, int32_t* out_cnt);
+void or_top_n_recom(int d, const double* X, const double* x_mean, int64_t nq, const double* U,
+                    const double* u_mean, const int64_t* unk_ptr, const int32_t* unk_idx, const int32_t* nb_idx,
+                    const double* nb_sim, const int32_t* nb_cnt, int P, int N, int32_t* out);
+/* the 3-argument get_top_N_recom over each user's whole cluster (:327-345) */
+void or_cluster_top_n(int d, const double* X, const double* x_mean, const int64_t* crow, const int32_t* crows,
+                      int64_t nq, const double* U, const double* u_mean, const int32_t* ucl,
+                      const int64_t* unk_ptr, const int32_t* unk_idx, int N, int32_t* out);
+
 /* ---- synthetic points (include/lshkm_synth.h) */
 void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out);
 

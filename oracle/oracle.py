@@ -59,6 +59,8 @@ def lib():
             "or_p_closest": (None, [C.c_int, f64p, C.c_int64, f64p, i64p, i32p, C.c_int, i32p, f64p, i32p]),
             "or_top_n_recom": (None, [C.c_int, f64p, f64p, C.c_int64, f64p, f64p, i64p, i32p, i32p, f64p, i32p,
                                       C.c_int, C.c_int, i32p]),
+            "or_cluster_top_n": (None, [C.c_int, f64p, f64p, i64p, i32p, C.c_int64, f64p, f64p, i32p, i64p, i32p,
+                                        C.c_int, i32p]),
             "or_synth": (None, [C.c_uint64, C.c_int64, C.c_int64, C.c_int, f32p]),
         }
         for name, (res, args) in sig.items():
@@ -274,3 +276,29 @@ def top_n_recom(X, x_mean, U, u_mean, unk_ptr, unk_idx, nb_idx, nb_sim, nb_cnt, 
                          np.ascontiguousarray(nb_idx, np.int32), np.ascontiguousarray(nb_sim, np.float64),
                          np.ascontiguousarray(nb_cnt, np.int32), P, N, out)
     return out
+
+
+def cluster_top_n(X, x_mean, crow, crows, U, u_mean, ucl, unk_ptr, unk_idx, N):
+    """get_top_N_recom(neighbors, user, N) (crypto_rec.hpp:327-345) with each user's
+    neighbours = the members of cluster ucl[q] (crows[crow[c]:crow[c+1]], member
+    order), as main.cpp:260-269 / :353-373 call it: [Q][N], 0-padded; -1 rows for
+    users of an empty cluster (main.cpp skips them)."""
+    X = np.ascontiguousarray(X, np.float64); U = np.ascontiguousarray(U, np.float64)
+    Q, d = U.shape
+    out = np.zeros((Q, N), np.int32)
+    ui = np.ascontiguousarray(unk_idx, np.int32)
+    cr = np.ascontiguousarray(crows, np.int32)
+    lib().or_cluster_top_n(d, X, np.ascontiguousarray(x_mean, np.float64), np.ascontiguousarray(crow, np.int64),
+                           cr if len(cr) else np.zeros(1, np.int32), Q, U, np.ascontiguousarray(u_mean, np.float64),
+                           np.ascontiguousarray(ucl, np.int32), np.ascontiguousarray(unk_ptr, np.int64),
+                           ui if len(ui) else np.zeros(1, np.int32), N, out)
+    return out
+
+
+def clusters_csr(assign, K):
+    """separate_clusters_from_input (utils.hpp:150-158): (crow [K+1], rows) in row order."""
+    assign = np.asarray(assign, np.int64)
+    order = np.argsort(assign, kind="stable").astype(np.int32)
+    crow = np.zeros(K + 1, np.int64)
+    np.add.at(crow, assign + 1, 1)
+    return np.cumsum(crow), order

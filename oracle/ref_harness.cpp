@@ -705,8 +705,124 @@ static int mode_chain(int argc, char** argv) {
     return 0;
 }
 
+// -------------------------------------------------------------- crec mode
+// crec DIR N F d K iters min_dist seedA seedB NTA NTB — the two clustering
+// recommenders of main.cpp, as written:
+//   Part A (main.cpp:240-273): rand_selection over the user vectors, Lloyd +
+//     k_means (euclidean) until converged or `iters`, separate_clusters_from_input,
+//     then per user get_top_N_recom(clusters[user.getCluster()], user, NTA) -- the
+//     3-argument overload (crypto_rec.hpp:327-345);
+//   Part B (main.cpp:334-381): k_means_pp over the "fake" user vectors, the same
+//     loop on them, then per user the nearest centroid by the inline argmin
+//     (:356-364) and get_top_N_recom(clusters[argmin], user, NTB), skipping empty
+//     clusters.
+// DIR holds users.f64 [N][d], umean.f64, uunk_ptr.i64 / uunk_idx.i32 and
+// fake.f64 [F][d], fmean.f64, funk_ptr.i64 / funk_idx.i32 (means, unknown sets).
+// Outputs: A_rows [K], A_assign [N], A_iters, A_centers [K][d], A_top [N][NTA];
+// B_rows [K], B_assign [F], B_iters, B_centers [K][d], B_ucl [N], B_top [N][NTB]
+// (-1 rows for skipped users).
+static std::vector<Vec> read_vecs(const std::string& dir, const std::string& pre, int N, int d, const std::string& id) {
+    std::vector<double> x = read_raw<double>(dir + "/" + pre + ".f64", (size_t)N * d);
+    const std::string a = pre.substr(0, 1);
+    std::vector<double> m = read_raw<double>(dir + "/" + a + "mean.f64", N);
+    std::vector<int64_t> up = read_raw<int64_t>(dir + "/" + a + "unk_ptr.i64", N + 1);
+    std::vector<int32_t> ui = read_raw<int32_t>(dir + "/" + a + "unk_idx.i32", (size_t)up[N]);
+    std::vector<Vec> v;
+    v.reserve(N);
+    for (int i = 0; i < N; i++)
+        v.emplace_back(id + std::to_string(i), std::vector<double>(x.begin() + (size_t)i * d, x.begin() + (size_t)(i + 1) * d),
+                       std::set<int>(ui.begin() + up[i], ui.begin() + up[i + 1]), m[i]);
+    return v;
+}
+
+static int mode_crec(int argc, char** argv) {
+    if (argc < 12) { fprintf(stderr, "usage: crec DIR N F d K iters min_dist seedA seedB NTA NTB\n"); return 2; }
+    std::string dir = argv[1];
+    int N = atoi(argv[2]), F = atoi(argv[3]), d = atoi(argv[4]), K = atoi(argv[5]), iters = atoi(argv[6]);
+    double min_dist = atof(argv[7]);
+    long long seedA = atoll(argv[8]), seedB = atoll(argv[9]);
+    int NTA = atoi(argv[10]), NTB = atoi(argv[11]);
+    std::vector<Vec> users = read_vecs(dir, "users", N, d, "u");
+    std::vector<Vec> fake = read_vecs(dir, "fake", F, d, "f");
+    const std::string metric = "euclidean";
+    auto centers_of = [&](std::vector<Vec*>& cs) {
+        std::vector<double> o;
+        for (auto c : cs) o.insert(o.end(), c->getDimensions()->begin(), c->getDimensions()->end());
+        return o;
+    };
+    {   // Part A
+        g_seed = seedA;
+        std::vector<Vec*> centroids = rand_selection(users, K);
+        std::vector<int32_t> rows;
+        for (auto p : centroids) rows.push_back((int32_t)(p - users.data()));
+        int it = 0;
+        bool cont = true;
+        while (cont && it < iters) {
+            lloyds_assignment(users, centroids, metric);
+            cont = k_means(users, centroids, metric, min_dist);
+            it++;
+        }
+        std::vector<std::vector<Vec*>> clusters = separate_clusters_from_input(users, (int)centroids.size());
+        std::vector<int32_t> assign(N), top((size_t)N * NTA, -1);
+        for (int i = 0; i < N; i++) assign[i] = users[i].getCluster();
+        for (int i = 0; i < N; i++) {
+            std::vector<Vec*> neighbors = clusters[users[i].getCluster()];
+            if (neighbors.empty()) continue;
+            std::vector<int> t = get_top_N_recom(neighbors, users[i], NTA);
+            for (int j = 0; j < NTA; j++) top[(size_t)i * NTA + j] = t[j];
+        }
+        std::vector<int32_t> nit(1, it);
+        write_npy(dir + "/A_rows.npy", rows, {rows.size()});
+        write_npy(dir + "/A_assign.npy", assign, {(size_t)N});
+        write_npy(dir + "/A_iters.npy", nit, {1});
+        write_npy(dir + "/A_centers.npy", centers_of(centroids), {(size_t)K, (size_t)d});
+        write_npy(dir + "/A_top.npy", top, {(size_t)N, (size_t)NTA});
+        for (auto c : centroids) if (c->getId() == "k_means_center") delete c;
+    }
+    {   // Part B
+        g_seed = seedB;
+        std::vector<Vec*> centroids = k_means_pp(fake, K, metric);
+        std::vector<int32_t> rows;
+        for (auto p : centroids) rows.push_back((int32_t)(p - fake.data()));
+        int it = 0;
+        bool cont = true;
+        while (cont && it < iters) {
+            lloyds_assignment(fake, centroids, metric);
+            cont = k_means(fake, centroids, metric, min_dist);
+            it++;
+        }
+        std::vector<std::vector<Vec*>> clusters = separate_clusters_from_input(fake, (int)centroids.size());
+        std::vector<int32_t> assign(F), ucl(N), top((size_t)N * NTB, -1);
+        for (int i = 0; i < F; i++) assign[i] = fake[i].getCluster();
+        for (int i = 0; i < N; i++) {
+            Vec& user = users[i];
+            double mind = user.euclideanDistance(centroids[0]);
+            int mi = 0;
+            for (int c = 1; c < (int)centroids.size(); c++) {
+                double cur = user.euclideanDistance(centroids[c]);
+                if (cur < mind) { mind = cur; mi = c; }
+            }
+            ucl[i] = mi;
+            std::vector<Vec*> neighbors = clusters[mi];
+            if (neighbors.empty()) continue;
+            std::vector<int> t = get_top_N_recom(neighbors, user, NTB);
+            for (int j = 0; j < NTB; j++) top[(size_t)i * NTB + j] = t[j];
+        }
+        std::vector<int32_t> nit(1, it);
+        write_npy(dir + "/B_rows.npy", rows, {rows.size()});
+        write_npy(dir + "/B_assign.npy", assign, {(size_t)F});
+        write_npy(dir + "/B_iters.npy", nit, {1});
+        write_npy(dir + "/B_centers.npy", centers_of(centroids), {(size_t)K, (size_t)d});
+        write_npy(dir + "/B_ucl.npy", ucl, {(size_t)N});
+        write_npy(dir + "/B_top.npy", top, {(size_t)N, (size_t)NTB});
+        for (auto c : centroids) if (c->getId() == "k_means_center") delete c;
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { fprintf(stderr, "usage: ref_harness {lsh|cube|lloyd|kmeanspp|bench} ...\n"); return 2; }
+    if (std::string(argv[1]) == "crec") return mode_crec(argc - 1, argv + 1);
     std::string m = argv[1];
     if (m == "lsh") return mode_lsh(argc - 1, argv + 1);
     if (m == "cube") return mode_cube(argc - 1, argv + 1);

@@ -14,7 +14,7 @@ fp64 cases (kind f64_*, chain, c1 with "f64": true) run on general doubles shape
 like the recommender's user vectors (user_vectors below); their inputs ARE
 stored (x64 / q64 / pool ... arrays), as fixtures.
 
-Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,range,csv,conf,c1,recom,f64,chain]
+Usage: python tests/golden/make_golden.py [--only lsh,cube,lloyd,kmeanspp,range,csv,conf,c1,recom,f64,chain,crec]
 (--only regenerates those kinds and keeps the other cases' entries.)
 """
 import json
@@ -261,6 +261,20 @@ CHAIN_CASES = [
     ("chain_a_k6", 400, 400, 60, 6, 3, 0.4, 853, 10, 5, 1, 8103),
 ]
 
+# main.cpp's clustering recommenders (Part A: rand_selection + Lloyd/k_means on the
+# user vectors, each user's own cluster; Part B: k_means_pp + Lloyd/k_means on
+# the "fake" user vectors, each user's nearest centroid), both with the
+# 3-argument get_top_N_recom (crypto_rec.hpp:327-345):
+# name, N users, F fake users, d, K, iters, min_dist, seedA, seedB, NTA, NTB, data seed, fake dup
+# (fake dup g: each distinct fake user appears g times in a row -- more
+# centroids than distinct points: k_means_pp's all-zero minima, duplicate
+# centroids, empty clusters)
+CREC_CASES = [
+    ("crec_a", 600, 500, 100, 12, 5, 0.0, 861, 862, 5, 2, 8201, 1),
+    ("crec_b", 300, 60, 60, 30, 4, 0.0, 863, 864, 5, 2, 8202, 3),      # 20 distinct fake users, K = 30
+    ("crec_c", 500, 400, 24, 8, 30, 0.05, 865, 866, 7, 3, 8203, 1),    # converges before the iteration cap
+]
+
 
 def run(args):
     subprocess.run([HARNESS] + [str(a) for a in args], check=True)
@@ -430,6 +444,24 @@ def main(only=None):
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
             meta[name] = dict(kind="chain", N=N, Q=N if self_ else Q, d=d, k=k, L=L, w=w, seed=seed, P=P, NTOP=NT,
                               self=bool(self_), data_seed=dseed)
+        for (name, N, F, d, K, iters, md, sa, sb, nta, ntb, dseed, dup) in (CREC_CASES if want("crec") else []):
+            out = os.path.join(tmp, name); os.makedirs(out)
+            users, uunk, umean = user_vectors(dseed, N, d)
+            fake, funk, fmean = user_vectors(dseed + 1, F // dup, d)
+            fake, fmean = np.repeat(fake, dup, axis=0), np.repeat(fmean, dup)
+            funk = [u for u in funk for _ in range(dup)]
+            inp = dict(users=users, umean=umean, fake=fake, fmean=fmean)
+            inp["uunk_ptr"], inp["uunk_idx"] = csr_of(uunk)
+            inp["funk_ptr"], inp["funk_idx"] = csr_of(funk)
+            ext = dict(users="f64", umean="f64", fake="f64", fmean="f64", uunk_ptr="i64", uunk_idx="i32",
+                       funk_ptr="i64", funk_idx="i32")
+            for kk, v in inp.items():
+                v.tofile(os.path.join(out, f"{kk}.{ext[kk]}"))
+            run(["crec", out, N, F, d, K, iters, repr(md), sa, sb, nta, ntb])
+            res = load_dir(out); res.update(inp)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **res)
+            meta[name] = dict(kind="crec", N=N, F=F, d=d, K=K, iters=iters, min_dist=md, seedA=sa, seedB=sb,
+                              NTA=nta, NTB=ntb, data_seed=dseed, fake_dup=dup)
         for name, text in (CONF_CASES.items() if want("conf") else []):
             path = os.path.join(iodir, name + ".conf")
             with open(path, "w", newline="") as f:

@@ -43,6 +43,8 @@ def test_shim_compiles_against_reference_headers(tmp_path):
         "    CustVector<double>&, int);\n"
         "template std::vector<int> lshkm_compat::get_top_N_recom<double>(std::vector<CustVector<double>*>&,\n"
         "    CustVector<double>&, int, std::vector<double>);\n"
+        "template std::vector<int> lshkm_compat::get_top_N_recom<double>(std::vector<CustVector<double>*>&,\n"
+        "    CustVector<double>&, int);\n"
         "template class lshkm_compat::GpuLshGenerator<float>;\n"
         "template class lshkm_compat::GpuCubeGenerator<int>;\n")
     r = subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Wno-unused-function", "-I", REF_LIB,

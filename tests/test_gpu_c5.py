@@ -16,6 +16,7 @@ The near-tie screen is an fp64 GEMM (torch, test-side only): rows whose two
 smallest squared distances lie within 1e-4 relative are exactly the rows the
 kernel's certificate has to work for (refinement list, exact pass)."""
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -160,6 +161,93 @@ def test_c3_bench_call_full_size(ctx, dist_mode):
     check_hash_all(Xh, tu_h, bu_h, V, t, w, r, N // 100)
     sample = np.random.default_rng(10).choice(N, 50_000, replace=False)
     check_lloyd_rows(Xh, Cc.cpu().numpy(), np.union1d(near, sample), ga, gd, src, dist_mode)
+
+
+def _sharding():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("lshkm_sharding", os.path.join(ROOT, "crypto-recommendation_amd",
+                                                                                "sharding.py"))
+    sh = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sh)
+    return sh
+
+
+def progress(msg):
+    # long full-size tests: a line on the real stderr now and then (a GPU-box
+    # run is taken for hung after minutes without output)
+    print(f"[test_gpu_c5] {msg}", file=sys.__stderr__, flush=True)
+
+
+@pytest.mark.timeout(420)
+def test_c5_shard_full_size(ctx):
+    # C5's per-GPU shard exactly as bench.py times it (N = 10M rows, K = 1024
+    # centroids = rows i * floor(80M / 1024) of the 80M-row job that fall in
+    # shard 0 plus the other shards' rows, L = 5, k = 4, w = 0.4, nb = 80M / 100):
+    #  - lshkm_hash_assign in both distance modes of the context: every row's
+    #    tuples and buckets vs the oracle; Lloyd (IDs, distances per the mode's
+    #    contract) on every near-tie row plus a 50K sample; IDs identical across
+    #    the modes;
+    #  - one sharding.ShardedLloyd iteration at world size 1, fast (all-reduce)
+    #    and carry (exact chain) mode: counts and centers bit-exact vs the oracle's
+    #    k_means on the same assignment (update.hpp:37-86).
+    sh = _sharding()
+    torch = ctx.torch
+    N, d, L, k, K, w, world = 10_000_000, 128, 5, 4, 1024, 0.4, 8
+    N_total = N * world
+    X = ctx.synth(SEED_DATA, N, d)                       # shard 0 of the 80M-row job
+    V, t, r, _ = lshkm.params_lsh_euclidean(SEED_PARAMS, L, k, d, w)
+    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N_total // 100, w, V=V, t=t, r=r)
+    rows = sh.centroid_rows(N_total, K)
+    Cc = torch.stack([ctx.synth(SEED_DATA, 1, d, row0=int(rw))[0] for rw in rows]).double()
+    src = sh.local_src_rows(rows, 0, N)
+    assert (src >= 0).sum() == K // world                # the shard's own centroid rows are overridden
+    out = {}
+    for mode in ("certified", "exact"):
+        ctx.set_dist_mode(mode)
+        try:
+            ctx.reset_stats()
+            tu, _, bu, a, dist = lshkm.hash_assign(lsh, X, Cc, src, tuples=True, bucket=True)
+            ctx.sync()
+            assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0 and ctx.stat(lshkm.STAT_HASH_FIX) > 0
+        finally:
+            ctx.set_dist_mode("certified")
+        out[mode] = (tu.cpu().numpy(), bu.cpu().numpy(), a.cpu().numpy(), dist.cpu().numpy())
+        del tu, bu, a, dist
+    for i in range(3):
+        assert np.array_equal(out["certified"][i], out["exact"][i]), i      # tuples, buckets, IDs
+    progress("hash_assign done in both modes")
+    near = near_tie_rows(ctx, X, Cc)
+    Xh = X.cpu().numpy()
+    check_hash_all(Xh, out["exact"][0], out["exact"][1], V, t, w, r, N_total // 100)
+    progress("tuples / buckets of every row match the oracle")
+    sample = np.random.default_rng(11).choice(N, 50_000, replace=False)
+    chk = np.union1d(near, sample)
+    over = {int(rw): c for c, rw in enumerate(src) if rw >= 0}
+    plain = np.array([rw for rw in chk if int(rw) not in over], np.int64)
+    oa, od = oracle.lloyd_assign(Xh[plain], Cc.cpu().numpy(), "euclidean", None)
+    for mode in ("certified", "exact"):
+        ga, gd = out[mode][2], out[mode][3]
+        assert np.array_equal(ga[plain], oa), (mode, np.nonzero(ga[plain] != oa)[0][:10])
+        assert_dist(gd[plain], od, mode)
+        for rw, c in over.items():
+            assert ga[rw] == c and gd[rw] == 0.0
+    assign_h = out["exact"][2]
+    del out
+    progress(f"Lloyd of {len(plain)} rows (near ties + sample) matches the oracle")
+    # one C5 iteration at world size 1 (the all-reduce is a no-op, the carry
+    # chain has no predecessor): the update must be the reference's k_means
+    X64 = oracle.rows64(Xh)
+    del Xh
+    Cn_o, cnt_o, cont_o = oracle.kmeans_update(X64, assign_h, Cc.cpu().numpy(), "euclidean", 0.0)
+    del X64
+    for kmode in ("fast", "exact"):
+        it = sh.ShardedLloyd(lshkm, ctx, lsh, X, Cc, src, mode=kmode)
+        cont = it.step()
+        ctx.sync()
+        assert np.array_equal(it.assign.cpu().numpy(), assign_h), kmode
+        assert np.array_equal(it.counts.cpu().numpy(), cnt_o), kmode
+        assert cont == cont_o
+        assert np.array_equal(it.C.cpu().numpy().view(np.uint64), Cn_o.view(np.uint64)), kmode
 
 
 def test_c4_cube_full_size(ctx):

@@ -235,3 +235,49 @@ def test_recommender_chain(name):
     top = oracle.top_n_recom(pool, g["pmean"], users, um, up, ui, idx_, sim, cnt, m["NTOP"])
     has = cnt > 0
     assert np.array_equal(top[has], g["top"][has])
+
+
+def crec_flow(X, K, iters, min_dist, rows, src_override=True):
+    """main.cpp:248-254 / :340-347: Lloyd + k_means from dataset-row centroids
+    until k_means reports no move or `iters`; returns (assign, centers, iterations)."""
+    C = X[rows].astype(np.float64)
+    it, cont, a = 0, True, None
+    while cont and it < iters:
+        a, _ = oracle.lloyd_assign(X, C, "euclidean", rows.astype(np.int32) if (it == 0 and src_override) else None)
+        Cn, _, cont = oracle.kmeans_update(X, a, C, "euclidean", min_dist)
+        C = Cn if cont else C
+        it += 1
+    return a, C, it
+
+
+@pytest.mark.parametrize("name", cases("crec"))
+def test_clustering_recommenders(name):
+    # main.cpp's clustering recommenders on user-vector doubles, both parts, with
+    # the 3-argument get_top_N_recom (crypto_rec.hpp:327-345) over whole clusters
+    m, g = META[name], golden(name)
+    K = m["K"]
+    users, fake = g["users"], g["fake"]
+    # Part A (main.cpp:240-273): rand_selection, Lloyd/k_means, each user's own cluster
+    rows = oracle.rand_selection(m["N"], K, m["seedA"])
+    assert np.array_equal(rows, g["A_rows"])
+    a, C, it = crec_flow(users, K, m["iters"], m["min_dist"], rows)
+    assert it == int(g["A_iters"][0]) and np.array_equal(a, g["A_assign"])
+    assert np.array_equal(C.view(np.uint64), g["A_centers"].view(np.uint64))
+    crow, crows = oracle.clusters_csr(a, K)
+    top = oracle.cluster_top_n(users, g["umean"], crow, crows, users, g["umean"], a, g["uunk_ptr"], g["uunk_idx"],
+                               m["NTA"])
+    assert np.array_equal(top, g["A_top"])
+    # Part B (main.cpp:334-381): k_means_pp over the fake users, the nearest
+    # centroid of each user (the inline argmin :356-364 is lloyds_assignment's rule
+    # without the override), recommendations from that cluster; empty ones skipped
+    rows = oracle.kmeans_pp(fake, K, "euclidean", m["seedB"])
+    assert np.array_equal(rows, g["B_rows"])
+    a, C, it = crec_flow(fake, K, m["iters"], m["min_dist"], rows)
+    assert it == int(g["B_iters"][0]) and np.array_equal(a, g["B_assign"])
+    assert np.array_equal(C.view(np.uint64), g["B_centers"].view(np.uint64))
+    ucl, _ = oracle.lloyd_assign(users, C, "euclidean", None)
+    assert np.array_equal(ucl, g["B_ucl"])
+    crow, crows = oracle.clusters_csr(a, K)
+    top = oracle.cluster_top_n(fake, g["fmean"], crow, crows, users, g["umean"], ucl, g["uunk_ptr"], g["uunk_idx"],
+                               m["NTB"])
+    assert np.array_equal(top, g["B_top"])
