@@ -125,7 +125,114 @@ static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     return 0;
 }
 
+// Host view of the cluster CSR: every user's member count on this shard and
+// the prefix offsets of its similarities.
+static int shard_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
+                         std::vector<int64_t>& soff) {
+    std::vector<int64_t> hc((size_t)K + 1);
+    std::vector<int32_t> hu((size_t)nq);
+    LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipMemcpyAsync(hu.data(), ucl, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    bool ok = hc[0] == 0;
+    for (int c = 0; c < K && ok; c++) ok = hc[c + 1] >= hc[c];
+    LSHKM_CHECK(ok && hc[K] <= N, LSHKM_ERR_ARG, "bad cluster CSR");
+    soff.assign((size_t)nq + 1, 0);
+    for (int64_t q = 0; q < nq; q++) {
+        const int c = hu[q];
+        const int64_t n = (c >= 0 && c < K) ? hc[c + 1] - hc[c] : 0;
+        LSHKM_CHECK(n < (1ll << 31), LSHKM_ERR_ARG, "a cluster of 2^31 members or more");
+        soff[q + 1] = soff[q] + n;
+    }
+    return 0;
+}
+
+static int cluster_sims_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64_t* crow, const int32_t* crows, int K,
+                             Pts U, int64_t nq, const int32_t* ucl, const int64_t* unk_ptr, int64_t* soff_dev,
+                             double* sims, int64_t cap, int64_t* total_host) {
+    LSHKM_CHECK(ctx && X.p && crow && U.p && ucl && unk_ptr && soff_dev && total_host && N >= 1 && d >= 1 && K >= 1 &&
+                    nq >= 0 && cap >= 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    std::vector<int64_t> soff;
+    int rc;
+    if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff))) return rc;
+    *total_host = soff[nq];
+    LSHKM_HIP(hipMemcpyAsync(soff_dev, soff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, ctx->stream));
+    if (sims && soff[nq] <= cap && soff[nq] > 0) {
+        LSHKM_CHECK(crows, LSHKM_ERR_ARG, "crows is NULL");
+        if ((rc = launch_rc_shard_sims(ctx->stream, X, d, crow, crows, K, U, nq, ucl, unk_ptr, soff_dev, sims,
+                                       (unsigned long long*)ctx->stats.p + STAT_REC_SOFT)))
+            return rc;
+    }
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // soff (host vector) is copied before return
+    return 0;
+}
+
+static int cluster_chain_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_t N, int d, const int64_t* crow,
+                              const int32_t* crows, int K, int64_t nq, const int32_t* ucl, const double* u_mean,
+                              const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* soff, const double* sims,
+                              const double* carry_main, const double* carry_abs, const int64_t* carry_cnt,
+                              double* main_out, double* abs_out, int64_t* cnt_out, int n_top, int32_t* out) {
+    LSHKM_CHECK(ctx && X.p && x_mean && crow && ucl && u_mean && unk_ptr && soff && N >= 1 && d >= 1 && K >= 1 &&
+                    nq >= 0 && n_top >= 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK((carry_main == nullptr) == (carry_abs == nullptr) && (carry_abs == nullptr) == (carry_cnt == nullptr),
+                LSHKM_ERR_ARG, "carry_main / carry_abs / carry_cnt: all or none");
+    LSHKM_CHECK(out || (main_out && abs_out && cnt_out), LSHKM_ERR_ARG, "either the carry outputs or out");
+    if (nq == 0) return 0;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int64_t total = 0;
+    LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    LSHKM_CHECK(total >= 0 && (total == 0 || unk_idx), LSHKM_ERR_ARG, "bad unknown-index lists");
+    Buf &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
+    const size_t M = (size_t)(total > 0 ? total : 1);
+    int rc;
+    if (out && ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M)))) return rc;
+    if ((rc = launch_rc_shard_chain(ctx->stream, X, x_mean, d, crow, crows, K, nq, ucl, u_mean, unk_ptr, unk_idx, soff,
+                                    sims, carry_main, carry_abs, carry_cnt, out ? nullptr : main_out,
+                                    out ? nullptr : abs_out, out ? nullptr : cnt_out, n_top, pred.as<double>(),
+                                    pidx.as<int32_t>(), out))) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return rc;
+    }
+    if (out) LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // pred / pidx workspace reused by the next call
+    return 0;
+}
+
 extern "C" {
+
+int lshkm_cluster_sims(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow, const int32_t* crows,
+                       int K, const float* U, int64_t nq, const int32_t* ucl, const int64_t* unk_ptr,
+                       int64_t* soff, double* sims, int64_t cap, int64_t* total) {
+    return cluster_sims_impl(ctx, X, N, d, crow, crows, K, U, nq, ucl, unk_ptr, soff, sims, cap, total);
+}
+
+int lshkm_cluster_sims_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int64_t* crow,
+                           const int32_t* crows, int K, const double* U, int64_t nq, const int32_t* ucl,
+                           const int64_t* unk_ptr, int64_t* soff, double* sims, int64_t cap, int64_t* total) {
+    return cluster_sims_impl(ctx, X, N, d, crow, crows, K, U, nq, ucl, unk_ptr, soff, sims, cap, total);
+}
+
+int lshkm_cluster_chain(lshkm_ctx ctx, const float* X, const double* x_mean, int64_t N, int d, const int64_t* crow,
+                        const int32_t* crows, int K, int64_t nq, const int32_t* ucl, const double* u_mean,
+                        const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* soff, const double* sims,
+                        const double* carry_main, const double* carry_abs, const int64_t* carry_cnt,
+                        double* main_out, double* abs_out, int64_t* cnt_out, int n_top, int32_t* out) {
+    return cluster_chain_impl(ctx, X, x_mean, N, d, crow, crows, K, nq, ucl, u_mean, unk_ptr, unk_idx, soff, sims,
+                              carry_main, carry_abs, carry_cnt, main_out, abs_out, cnt_out, n_top, out);
+}
+
+int lshkm_cluster_chain_f64(lshkm_ctx ctx, const double* X, const double* x_mean, int64_t N, int d,
+                            const int64_t* crow, const int32_t* crows, int K, int64_t nq, const int32_t* ucl,
+                            const double* u_mean, const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* soff,
+                            const double* sims, const double* carry_main, const double* carry_abs,
+                            const int64_t* carry_cnt, double* main_out, double* abs_out, int64_t* cnt_out, int n_top,
+                            int32_t* out) {
+    return cluster_chain_impl(ctx, X, x_mean, N, d, crow, crows, K, nq, ucl, u_mean, unk_ptr, unk_idx, soff, sims,
+                              carry_main, carry_abs, carry_cnt, main_out, abs_out, cnt_out, n_top, out);
+}
 
 int lshkm_cluster_top_n(lshkm_ctx ctx, const float* X, const double* x_mean, int64_t N, int d, const int64_t* crow,
                         const int32_t* crows, int K, const float* U, const double* u_mean, int64_t nq,

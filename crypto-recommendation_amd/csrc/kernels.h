@@ -182,6 +182,14 @@ int launch_rc_cluster_top_n(hipStream_t s, Pts X, const double* x_mean, int d, c
                             int64_t scratch_row, int nwaves, double* pred, int32_t* pidx, int32_t* out,
                             unsigned long long* soft_count);
 constexpr int RC_CLUSTER_WAVES_PER_BLOCK = 4;     // rc_cluster_top_n_kernel: waves per block (RC_WAVES)
+int launch_rc_shard_sims(hipStream_t s, Pts X, int d, const int64_t* crow, const int32_t* crows, int K, Pts U,
+                         int64_t nq, const int32_t* ucl, const int64_t* unk_ptr, const int64_t* soff, double* sims,
+                         unsigned long long* soft_count);
+int launch_rc_shard_chain(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
+                          int K, int64_t nq, const int32_t* ucl, const double* u_mean, const int64_t* unk_ptr,
+                          const int32_t* unk_idx, const int64_t* soff, const double* sims, const double* carry_main,
+                          const double* carry_abs, const int64_t* carry_cnt, double* main_out, double* abs_out,
+                          int64_t* cnt_out, int n_top, double* pred, int32_t* pidx, int32_t* out);
 int launch_rc_p_closest(hipStream_t s, const double* X, const double* xa, int d, const double* U, int64_t nq,
                         const int64_t* cand_ptr, const int32_t* cand_idx, int P, double* sim, double* key,
                         int32_t* pos, int32_t* out_idx, double* out_sim, int32_t* out_cnt, int32_t* replay,

@@ -341,6 +341,138 @@ __device__ inline double cr_sim_x87(const T* __restrict__ x, const T* __restrict
     return x87_quot(ip.value(), denom);
 }
 
+// Phase 1 for one user: sim[i] = cosineSimilarity(member i, user) for the n
+// members mem[0 .. n) (dataset rows), in member order. Declined certificates
+// are queued (queue / qden: this wave's CR_Q LDS slots) and decided by the x87
+// chain 64 at a time. Counts the x87-chain members in `soft`.
+template <typename T>
+__device__ inline void cr_sims(const T* __restrict__ X, const int32_t* __restrict__ mem, int n, const T* __restrict__ u,
+                               int d, double* __restrict__ sim, int32_t* queue, double* qden, int lane,
+                               unsigned long long& soft) {
+    const double ub = cr_sumsq(u, d);
+    int nqd = 0;                                    // queued declines
+    auto drain = [&](int cnt) {                     // the x87 chain for queue[0 .. cnt)
+        if (lane < cnt) {
+            const int i = queue[lane];
+            sim[i] = cr_sim_x87(X + (int64_t)mem[i] * d, u, d, qden[lane]);
+        }
+        soft += (unsigned long long)cnt;
+    };
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        bool dec = false;
+        double s = 0.0, den = 0.0;
+        if (i < n) {
+            dec = !cr_sim_cert(X + (int64_t)mem[i] * d, u, d, ub, s, den);
+            if (!dec) sim[i] = s;
+        }
+        const unsigned long long mask = __ballot(dec);
+        const int pos = nqd + __popcll(mask & ((1ull << lane) - 1ull));
+        if (dec) { queue[pos] = i; qden[pos] = den; }
+        nqd += __popcll(mask);
+        wave_sync();
+        if (nqd >= 64) {
+            drain(64);
+            const int rest = nqd - 64;
+            int32_t qi = 0; double qd = 0.0;
+            if (lane < rest) { qi = queue[64 + lane]; qd = qden[64 + lane]; }
+            wave_sync();
+            if (lane < rest) { queue[lane] = qi; qden[lane] = qd; }
+            nqd = rest;
+            wave_sync();
+        }
+    }
+    if (nqd > 0) drain(nqd);
+    __threadfence_block();
+    wave_sync();
+}
+
+// Phase 2 for one user (get_predicted_user_sim, crypto_rec.hpp:285-303): over
+// the members mem[0 .. n) in order, abs_sum += |sim| and, per unknown index e
+// (uidx[0 .. m)), main_sum[e] += sim * (x[index] - mean), every sum continuing
+// from its carry (main_in / abs_in: 0 for the first shard). Writes the running
+// sums (main_out[e], *abs_out by lane 0) or, with pred != NULL, the
+// predictions main / abs + um and the index list.
+template <typename T>
+__device__ inline void cr_chains(const T* __restrict__ X, const double* __restrict__ x_mean,
+                                 const int32_t* __restrict__ mem, int n, int d, const double* __restrict__ sim,
+                                 const int32_t* __restrict__ uidx, int m, const double* __restrict__ main_in,
+                                 double abs_in, double* __restrict__ main_out, double* __restrict__ abs_out, double um,
+                                 double* __restrict__ pred, int32_t* __restrict__ pidx, int lane) {
+    for (int g0 = 0; g0 < m; g0 += 64 * CR_MI) {
+        int idx[CR_MI];
+        bool ok[CR_MI];
+        double acc[CR_MI];
+#pragma unroll
+        for (int k = 0; k < CR_MI; k++) {
+            const int e = g0 + lane + 64 * k;
+            ok[k] = e < m;
+            idx[k] = ok[k] ? uidx[e] : 0;
+            acc[k] = ok[k] && main_in ? main_in[e] : 0.0;
+        }
+        double abs_sum = abs_in;
+        for (int b = 0; b < n; b += 64) {
+            const int cnt = n - b < 64 ? n - b : 64;
+            int32_t r = 0;
+            double sv = 0.0, mv = 0.0;
+            if (lane < cnt) {
+                r = mem[b + lane];
+                sv = sim[b + lane];
+                mv = x_mean[r];
+            }
+            for (int t0 = 0; t0 < cnt; t0 += 8) {
+                double xv[8][CR_MI];
+#pragma unroll
+                for (int tt = 0; tt < 8; tt++) {
+                    const int64_t rr = (int64_t)__builtin_amdgcn_readlane(r, t0 + tt);
+#pragma unroll
+                    for (int k = 0; k < CR_MI; k++)
+                        xv[tt][k] = (t0 + tt < cnt && ok[k]) ? (double)X[rr * d + idx[k]] : 0.0;
+                }
+#pragma unroll
+                for (int tt = 0; tt < 8; tt++) {
+                    if (t0 + tt >= cnt) break;
+                    const double cs = cr_rl(sv, t0 + tt), nm = cr_rl(mv, t0 + tt);
+                    abs_sum = __dadd_rn(abs_sum, fabs(cs));
+#pragma unroll
+                    for (int k = 0; k < CR_MI; k++)
+                        acc[k] = __dadd_rn(acc[k], __dmul_rn(cs, __dsub_rn(xv[tt][k], nm)));
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CR_MI; k++)
+            if (ok[k]) {
+                const int e = g0 + lane + 64 * k;
+                if (pred) {
+                    pred[e] = __dadd_rn(__ddiv_rn(acc[k], abs_sum), um);    // crypto_rec.hpp:299-302
+                    pidx[e] = idx[k];
+                } else {
+                    main_out[e] = acc[k];
+                }
+            }
+        if (!pred && g0 == 0 && lane == 0) *abs_out = abs_sum;
+    }
+    if (!pred && m == 0 && lane == 0) {
+        // no unknown index: only the |sim| chain (its count decides "skipped")
+        double abs_sum = abs_in;
+        for (int i = 0; i < n; i++) abs_sum = __dadd_rn(abs_sum, fabs(sim[i]));
+        *abs_out = abs_sum;
+    }
+    __threadfence_block();
+    wave_sync();
+}
+
+// Lane 0: the reference's quicksort of the predictions (:341) and the first
+// n_top unknown indexes, 0-padded (:343).
+__device__ inline void cr_top(double* pred, int32_t* pidx, int m, int n_top, int32_t* out, int lane) {
+    if (lane == 0) {
+        if (m > 0) lomuto_sort(pred, pidx, m);
+        for (int i = 0; i < n_top; i++) out[i] = i < m ? pidx[i] : 0;
+    }
+    wave_sync();
+}
+
 template <typename T>
 __global__ __launch_bounds__(64 * RC_WAVES) void rc_cluster_top_n_kernel(
     const T* __restrict__ X, const double* __restrict__ x_mean, int d, const int64_t* __restrict__ crow,
@@ -365,108 +497,88 @@ __global__ __launch_bounds__(64 * RC_WAVES) void rc_cluster_top_n_kernel(
         }
         const int64_t o = unk_ptr[q];
         const int m = (int)(unk_ptr[q + 1] - o);
-        const T* u = U + q * d;
         if (m > 0) {
-            // phase 1: similarities in member order
-            const double ub = cr_sumsq(u, d);
-            int nqd = 0;                                // queued declines
-            auto drain = [&](int cnt) {                 // the x87 chain for queue[0 .. cnt)
-                if (lane < cnt) {
-                    const int i = queue[wv][lane];
-                    sim[i] = cr_sim_x87(X + (int64_t)crows[base + i] * d, u, d, qden[wv][lane]);
-                }
-                soft += (unsigned long long)cnt;
-            };
-            for (int b = 0; b < n; b += 64) {
-                const int i = b + lane;
-                bool dec = false;
-                double s = 0.0, den = 0.0;
-                if (i < n) {
-                    dec = !cr_sim_cert(X + (int64_t)crows[base + i] * d, u, d, ub, s, den);
-                    if (!dec) sim[i] = s;
-                }
-                const unsigned long long mask = __ballot(dec);
-                const int pos = nqd + __popcll(mask & ((1ull << lane) - 1ull));
-                if (dec) { queue[wv][pos] = i; qden[wv][pos] = den; }
-                nqd += __popcll(mask);
-                wave_sync();
-                if (nqd >= 64) {
-                    drain(64);
-                    const int rest = nqd - 64;
-                    int32_t qi = 0; double qd = 0.0;
-                    if (lane < rest) { qi = queue[wv][64 + lane]; qd = qden[wv][64 + lane]; }
-                    wave_sync();
-                    if (lane < rest) { queue[wv][lane] = qi; qden[wv][lane] = qd; }
-                    nqd = rest;
-                    wave_sync();
-                }
-            }
-            if (nqd > 0) drain(nqd);
-            __threadfence_block();
-            wave_sync();
-            // phase 2: get_predicted_user_sim, CR_MI * 64 unknown indexes per pass
-            const double um = u_mean[q];
-            for (int g0 = 0; g0 < m; g0 += 64 * CR_MI) {
-                int idx[CR_MI];
-                bool ok[CR_MI];
-                double acc[CR_MI];
-#pragma unroll
-                for (int k = 0; k < CR_MI; k++) {
-                    const int e = g0 + lane + 64 * k;
-                    ok[k] = e < m;
-                    idx[k] = ok[k] ? unk_idx[o + e] : 0;
-                    acc[k] = 0.0;
-                }
-                double abs_sum = 0.0;
-                for (int b = 0; b < n; b += 64) {
-                    const int cnt = n - b < 64 ? n - b : 64;
-                    int32_t r = 0;
-                    double sv = 0.0, mv = 0.0;
-                    if (lane < cnt) {
-                        r = crows[base + b + lane];
-                        sv = sim[b + lane];
-                        mv = x_mean[r];
-                    }
-                    for (int t0 = 0; t0 < cnt; t0 += 8) {
-                        double xv[8][CR_MI];
-#pragma unroll
-                        for (int tt = 0; tt < 8; tt++) {
-                            const int64_t rr = (int64_t)__builtin_amdgcn_readlane(r, t0 + tt);
-#pragma unroll
-                            for (int k = 0; k < CR_MI; k++)
-                                xv[tt][k] = (t0 + tt < cnt && ok[k]) ? (double)X[rr * d + idx[k]] : 0.0;
-                        }
-#pragma unroll
-                        for (int tt = 0; tt < 8; tt++) {
-                            if (t0 + tt >= cnt) break;
-                            const double cs = cr_rl(sv, t0 + tt), nm = cr_rl(mv, t0 + tt);
-                            abs_sum = __dadd_rn(abs_sum, fabs(cs));
-#pragma unroll
-                            for (int k = 0; k < CR_MI; k++)
-                                acc[k] = __dadd_rn(acc[k], __dmul_rn(cs, __dsub_rn(xv[tt][k], nm)));
-                        }
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < CR_MI; k++)
-                    if (ok[k]) {
-                        const int e = g0 + lane + 64 * k;
-                        pred[o + e] = __dadd_rn(__ddiv_rn(acc[k], abs_sum), um);
-                        pidx[o + e] = idx[k];
-                    }
-            }
-            __threadfence_block();
-            wave_sync();
+            const T* u = U + q * d;
+            cr_sims(X, crows + base, n, u, d, sim, queue[wv], qden[wv], lane, soft);
+            cr_chains(X, x_mean, crows + base, n, d, sim, unk_idx + o, m, (const double*)nullptr, 0.0,
+                      (double*)nullptr, (double*)nullptr, u_mean[q], pred + o, pidx + o, lane);
         }
-        if (lane == 0) {
-            if (m > 0) lomuto_sort(pred + o, pidx + o, m);
-            for (int i = 0; i < n_top; i++) out[q * n_top + i] = i < m ? pidx[o + i] : 0;
-        }
-        wave_sync();
+        cr_top(pred + o, pidx + o, m, n_top, out + q * n_top, lane);
     }
-    if (soft_count) {
-        // one atomic per wave
-        if (lane == 0 && soft) atomicAdd(soft_count, soft);
+    if (soft_count && lane == 0 && soft) atomicAdd(soft_count, soft);     // one atomic per wave
+}
+
+// Sharded form, phase 1: every user's similarities to THIS shard's members of
+// its cluster into sims[soff[q] .. soff[q+1]) (member order).
+template <typename T>
+__global__ __launch_bounds__(64 * RC_WAVES) void rc_shard_sims_kernel(
+    const T* __restrict__ X, int d, const int64_t* __restrict__ crow, const int32_t* __restrict__ crows, int K,
+    const T* __restrict__ U, int64_t nq, const int32_t* __restrict__ ucl, const int64_t* __restrict__ unk_ptr,
+    const int64_t* __restrict__ soff, double* __restrict__ sims, unsigned long long* __restrict__ soft_count) {
+    __shared__ int32_t queue[RC_WAVES][CR_Q];
+    __shared__ double qden[RC_WAVES][CR_Q];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long soft = 0;
+    for (int64_t q = (int64_t)blockIdx.x * RC_WAVES + wv; q < nq; q += (int64_t)gridDim.x * RC_WAVES) {
+        const int c = ucl[q];
+        const int64_t base = (c >= 0 && c < K) ? crow[c] : 0;
+        const int n = (c >= 0 && c < K) ? (int)(crow[c + 1] - base) : 0;
+        if (n > 0) cr_sims(X, crows + base, n, U + q * d, d, sims + soff[q], queue[wv], qden[wv], lane, soft);
+    }
+    if (soft_count && lane == 0 && soft) atomicAdd(soft_count, soft);
+}
+
+// Sharded form, phase 2: the chains over this shard's members, continued from
+// the carry (carry_main [total unknowns], carry_abs / carry_cnt [nq]; NULL on
+// the first shard); the running sums out, or (out != NULL) the final step.
+template <typename T>
+__global__ __launch_bounds__(64 * RC_WAVES) void rc_shard_chain_kernel(
+    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const int64_t* __restrict__ crow,
+    const int32_t* __restrict__ crows, int K, int64_t nq, const int32_t* __restrict__ ucl,
+    const double* __restrict__ u_mean, const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx,
+    const int64_t* __restrict__ soff, const double* __restrict__ sims, const double* __restrict__ carry_main,
+    const double* __restrict__ carry_abs, const int64_t* __restrict__ carry_cnt, double* __restrict__ main_out,
+    double* __restrict__ abs_out, int64_t* __restrict__ cnt_out, int n_top, double* __restrict__ pred,
+    int32_t* __restrict__ pidx, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int64_t q = (int64_t)blockIdx.x * RC_WAVES + wv; q < nq; q += (int64_t)gridDim.x * RC_WAVES) {
+        const int c = ucl[q];
+        const int64_t base = (c >= 0 && c < K) ? crow[c] : 0;
+        const int n = (c >= 0 && c < K) ? (int)(crow[c + 1] - base) : 0;
+        const int64_t o = unk_ptr[q];
+        const int m = (int)(unk_ptr[q + 1] - o);
+        const int64_t total = (carry_cnt ? carry_cnt[q] : 0) + n;
+        const double* min = carry_main ? carry_main + o : nullptr;
+        const double ain = carry_abs ? carry_abs[q] : 0.0;
+        if (!out) {                                     // pass the running sums on
+            if (n > 0) {
+                cr_chains(X, x_mean, crows + base, n, d, sims + soff[q], unk_idx + o, m, min, ain, main_out + o,
+                          abs_out + q, u_mean[q], (double*)nullptr, (int32_t*)nullptr, lane);
+            } else {                                    // no member here: the carry unchanged
+                for (int e = lane; e < m; e += 64) main_out[o + e] = min ? min[e] : 0.0;
+                if (lane == 0) abs_out[q] = ain;
+            }
+            if (lane == 0) cnt_out[q] = total;
+            continue;
+        }
+        if (total == 0) {                               // an empty cluster on every shard: skipped
+            for (int i = lane; i < n_top; i += 64) out[q * n_top + i] = -1;
+            continue;
+        }
+        if (m > 0) {
+            if (n > 0) {
+                cr_chains(X, x_mean, crows + base, n, d, sims + soff[q], unk_idx + o, m, min, ain, (double*)nullptr,
+                          (double*)nullptr, u_mean[q], pred + o, pidx + o, lane);
+            } else {
+                for (int e = lane; e < m; e += 64) {
+                    pred[o + e] = __dadd_rn(__ddiv_rn(min ? min[e] : 0.0, ain), u_mean[q]);
+                    pidx[o + e] = unk_idx[o + e];
+                }
+                __threadfence_block();
+                wave_sync();
+            }
+        }
+        cr_top(pred + o, pidx + o, m, n_top, out + q * n_top, lane);
     }
 }
 
@@ -486,6 +598,38 @@ int launch_rc_cluster_top_n(hipStream_t s, Pts X, const double* x_mean, int d, c
                            crow, crows, K, U.f(), u_mean, nq, ucl, unk_ptr, unk_idx, n_top, scratch, scratch_row, pred,
                            pidx, out, soft_count);
     return kstatus("rc_cluster_top_n_kernel");
+}
+
+int launch_rc_shard_sims(hipStream_t s, Pts X, int d, const int64_t* crow, const int32_t* crows, int K, Pts U,
+                        int64_t nq, const int32_t* ucl, const int64_t* unk_ptr, const int64_t* soff, double* sims,
+                        unsigned long long* soft_count) {
+    if (nq <= 0) return 0;
+    const dim3 grid(gsz(nq, RC_WAVES, 2048));
+    if (X.f64)
+        hipLaunchKernelGGL(rc_shard_sims_kernel<double>, grid, dim3(64 * RC_WAVES), 0, s, X.d(), d, crow, crows, K,
+                           U.d(), nq, ucl, unk_ptr, soff, sims, soft_count);
+    else
+        hipLaunchKernelGGL(rc_shard_sims_kernel<float>, grid, dim3(64 * RC_WAVES), 0, s, X.f(), d, crow, crows, K,
+                           U.f(), nq, ucl, unk_ptr, soff, sims, soft_count);
+    return kstatus("rc_shard_sims_kernel");
+}
+
+int launch_rc_shard_chain(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
+                          int K, int64_t nq, const int32_t* ucl, const double* u_mean, const int64_t* unk_ptr,
+                          const int32_t* unk_idx, const int64_t* soff, const double* sims, const double* carry_main,
+                          const double* carry_abs, const int64_t* carry_cnt, double* main_out, double* abs_out,
+                          int64_t* cnt_out, int n_top, double* pred, int32_t* pidx, int32_t* out) {
+    if (nq <= 0) return 0;
+    const dim3 grid(gsz(nq, RC_WAVES, 2048));
+    if (X.f64)
+        hipLaunchKernelGGL(rc_shard_chain_kernel<double>, grid, dim3(64 * RC_WAVES), 0, s, X.d(), x_mean, d, crow,
+                           crows, K, nq, ucl, u_mean, unk_ptr, unk_idx, soff, sims, carry_main, carry_abs, carry_cnt,
+                           main_out, abs_out, cnt_out, n_top, pred, pidx, out);
+    else
+        hipLaunchKernelGGL(rc_shard_chain_kernel<float>, grid, dim3(64 * RC_WAVES), 0, s, X.f(), x_mean, d, crow,
+                           crows, K, nq, ucl, u_mean, unk_ptr, unk_idx, soff, sims, carry_main, carry_abs, carry_cnt,
+                           main_out, abs_out, cnt_out, n_top, pred, pidx, out);
+    return kstatus("rc_shard_chain_kernel");
 }
 
 int launch_rc_norms(hipStream_t s, const double* X, int64_t N, int d, double* xa) {

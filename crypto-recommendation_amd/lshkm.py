@@ -108,6 +108,10 @@ def lib():
             "lshkm_p_closest": (i32, [vp, vp, i64, i32, vp, i64, vp, vp, i32, vp, vp, vp]),
             "lshkm_top_n_recom": (i32, [vp, vp, vp, i64, i32, vp, i64, vp, vp, vp, vp, vp, i32, i32, vp]),
             "lshkm_cluster_top_n": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, vp, vp, i64, vp, vp, vp, i32, vp]),
+            "lshkm_cluster_sims": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, i64, vp, vp, vp, vp, i64,
+                                         C.POINTER(i64)]),
+            "lshkm_cluster_chain": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                          vp, vp, vp, vp, i32, vp]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
             "lshkm_clusters": (i32, [vp, vp, i64, i32, vp, vp]),
         }
@@ -612,6 +616,54 @@ def cluster_top_n(ctx, X, x_mean, crow, crows, U, u_mean, ucl, unk_ptr, unk_idx,
                                       _t_ptr(ucl), _t_ptr(unk_ptr), _t_ptr(unk_idx) if unk_idx.numel() else None,
                                       n_top, _t_ptr(out)))
     return out
+
+
+def cluster_sims(ctx, X, crow, crows, U, ucl, unk_ptr):
+    """Sharded clustering recommender, phase 1 (lshkm_cluster_sims): every user's
+    similarities to this shard's members of its cluster. Returns (soff [nq+1]
+    int64, sims fp64) device tensors."""
+    torch = ctx.torch
+    N, d = X.shape
+    nq = U.shape[0]
+    K = crow.shape[0] - 1
+    soff = ctx.empty((nq + 1,), torch.int64)
+    total = C.c_int64()
+    fn = _fn("lshkm_cluster_sims", X)
+    cr = _t_ptr(crows) if crows.numel() else None
+    _ck(fn(ctx.h, _t_ptr(X), N, d, _t_ptr(crow), cr, K, _t_ptr(U), nq, _t_ptr(ucl), _t_ptr(unk_ptr), _t_ptr(soff),
+           None, 0, C.byref(total)))
+    sims = ctx.empty((max(total.value, 1),), torch.float64)
+    _ck(fn(ctx.h, _t_ptr(X), N, d, _t_ptr(crow), cr, K, _t_ptr(U), nq, _t_ptr(ucl), _t_ptr(unk_ptr), _t_ptr(soff),
+           _t_ptr(sims), total.value, C.byref(total)))
+    return soff, sims
+
+
+def cluster_chain(ctx, X, x_mean, crow, crows, ucl, u_mean, unk_ptr, unk_idx, soff, sims, carry=None, n_top=None,
+                  carry_out=None):
+    """Sharded clustering recommender, phase 2 (lshkm_cluster_chain): the
+    prediction sums over this shard's members continued from `carry` (main, abs,
+    cnt) or None on the first shard. n_top None: returns the running sums
+    (main [total unknowns], abs [nq], cnt [nq]; into carry_out when given);
+    else the final [nq][n_top] int32 recommendations."""
+    torch = ctx.torch
+    N, d = X.shape
+    nq = ucl.shape[0]
+    K = crow.shape[0] - 1
+    M = unk_idx.shape[0]
+    cm, ca, cc = carry if carry is not None else (None, None, None)
+    out = outs = None
+    if n_top is None:
+        outs = carry_out if carry_out is not None else (ctx.empty((max(M, 1),), torch.float64),
+                                                        ctx.empty((nq,), torch.float64), ctx.empty((nq,), torch.int64))
+    else:
+        out = ctx.empty((nq, n_top), torch.int32)
+    om, oa, oc = outs if outs is not None else (None, None, None)
+    _ck(_fn("lshkm_cluster_chain", X)(ctx.h, _t_ptr(X), _t_ptr(x_mean), N, d, _t_ptr(crow),
+                                      _t_ptr(crows) if crows.numel() else None, K, nq, _t_ptr(ucl), _t_ptr(u_mean),
+                                      _t_ptr(unk_ptr), _t_ptr(unk_idx) if M else None, _t_ptr(soff), _t_ptr(sims),
+                                      _t_ptr(cm), _t_ptr(ca), _t_ptr(cc), _t_ptr(om), _t_ptr(oa), _t_ptr(oc),
+                                      0 if n_top is None else n_top, _t_ptr(out)))
+    return outs if n_top is None else out
 
 
 # ------------------------------------------------- reference-named mirrors

@@ -172,6 +172,99 @@ def allreduce_partials(sums, counts):
     return sums, counts
 
 
+def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, unk_idx, n_top, timing=None):
+    """The clustering recommender over row shards (main.cpp:260-269 on the
+    sharded rows; get_top_N_recom's 3-argument overload, crypto_rec.hpp:327-345).
+
+    A cluster's members lie on every rank, in row order = rank order, and the
+    reference sums get_predicted_user_sim's terms over them in that order. Every
+    rank holds the same query users (U rows, u_mean, their global clusters ucl,
+    the unknown-index CSR) and its own rows (X, x_mean, assign):
+      1. lshkm_clusters of the local assignment -> the local cluster CSR;
+      2. lshkm_cluster_sims: every user's similarities to the local members of
+         its cluster -- the bulk of the work, all ranks at once;
+      3. lshkm_cluster_chain in rank order: rank r receives the running sums
+         (one fp64 per (user, unknown index) + |sim| sum + member count per user)
+         from rank r-1 over RCCL point-to-point, continues them over its
+         members, and sends them on; the last rank finalizes (quicksort, first
+         n_top) and broadcasts the [nq][n_top] result.
+    Bit for bit lshkm_cluster_top_n over the concatenated rows. Returns the
+    result on every rank (device tensor). timing: optional list that receives
+    (ms of phases 1, 2+3) from CUDA events."""
+    torch = ctx.torch
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timing is not None else None
+    if ev:
+        ev[0].record()
+    crow, crows = lk.clusters(ctx, assign, K)
+    soff, sims = lk.cluster_sims(ctx, X, crow, crows, U, ucl, unk_ptr)
+    if ev:
+        ev[1].record()
+    dist = _dist()
+    args = (ctx, X, x_mean, crow, crows, ucl, u_mean, unk_ptr, unk_idx, soff, sims)
+    if dist is None:
+        out = lk.cluster_chain(*args, carry=None, n_top=n_top)
+    else:
+        rank, world = dist.get_rank(), dist.get_world_size()
+        nq, M = ucl.shape[0], unk_idx.shape[0]
+        carry = None
+        if rank > 0:
+            carry = (ctx.empty((max(M, 1),), torch.float64), ctx.empty((nq,), torch.float64),
+                     ctx.empty((nq,), torch.int64))
+            for t in carry:
+                b, back = _staged(dist, t)
+                dist.recv(b, src=rank - 1)
+                back()
+        if rank + 1 < world:
+            outs = lk.cluster_chain(*args, carry=carry, n_top=None)
+            for t in outs:
+                b, _ = _staged(dist, t)
+                dist.send(b, dst=rank + 1)
+            out = ctx.empty((nq, n_top), torch.int32)
+        else:
+            out = lk.cluster_chain(*args, carry=carry, n_top=n_top)
+        b, back = _staged(dist, out)
+        dist.broadcast(b, src=world - 1)
+        back()
+    if ev:
+        ev[2].record()
+        torch.cuda.synchronize(ctx.dev)
+        timing.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
+    return out
+
+
+def synth_recom_users(ctx, n_total, Q, d, seed):
+    """The C5 recommend step's query users (bench / tests): Q rows spread over
+    the whole job (rows i * floor(N / Q)), their known means (0: synthetic rows
+    carry no ratings) and unknown sets {j : (7j + row) % 16 == 0}. Returns
+    (rows numpy, U, u_mean, unk_ptr, unk_idx) device tensors, equal on every rank."""
+    torch = ctx.torch
+    rows = np.arange(Q, dtype=np.int64) * (n_total // Q)
+    U = torch.stack([ctx.synth(seed, 1, d, row0=int(r))[0] for r in rows])
+    u_mean = torch.zeros((Q,), dtype=torch.float64, device=ctx.dev)
+    sets = [np.nonzero((7 * np.arange(d) + int(r)) % 16 == 0)[0].astype(np.int32) for r in rows]
+    unk_ptr = torch.from_numpy(np.cumsum([0] + [len(s) for s in sets]).astype(np.int64)).to(ctx.dev)
+    unk_idx = torch.from_numpy(np.concatenate(sets)).to(ctx.dev)
+    return rows, U, u_mean, unk_ptr, unk_idx
+
+
+def user_clusters(ctx, rows, assign_local, row0, n):
+    """The users' clusters (main.cpp:261: user.getCluster()): the owning rank's
+    assignment of each user row, all-reduced (one int32 per user)."""
+    torch = ctx.torch
+    Q = len(rows)
+    ucl = torch.zeros((Q,), dtype=torch.int32, device=ctx.dev)
+    mine = (rows >= row0) & (rows < row0 + n)
+    if mine.any():
+        loc = torch.from_numpy(rows[mine] - row0).to(ctx.dev)
+        ucl[torch.from_numpy(np.nonzero(mine)[0]).to(ctx.dev)] = assign_local[loc]
+    dist = _dist()
+    if dist is not None:
+        b, back = _staged(dist, ucl)
+        dist.all_reduce(b)
+        back()
+    return ucl
+
+
 class ShardedLloyd:
     """One rank's part of the C5 iteration (main.cpp:96-103 with
     LSH hashing riding on the assignment pass): per step, on the rank's
@@ -205,6 +298,7 @@ class ShardedLloyd:
         self.cont = True
         self.timing = False       # True: HIP events around the exchange (bench.py's breakdown)
         self.exchange_events = []
+        self.recom = None         # enable_recommend(): the C5 recommend step after each update
 
     def step(self):
         import ctypes as C
@@ -233,12 +327,39 @@ class ShardedLloyd:
             if self.timing:
                 ev[1].record()
                 self.exchange_events.append(ev)
+        self.last_sums, self.last_counts = sums, counts     # this iteration's totals (either mode)
         Cn, cont = lk.kmeans_finalize(ctx, sums, counts, self.C, self.metric, self.min_dist)
         if cont:              # k_means replaces every center (update.hpp:70-79)
             self.C = Cn
             self.src = None   # the override applies to dataset-row centroids only
         self.cont = cont
+        if self.recom is not None:
+            self.recommend()
         return cont
+
+    def enable_recommend(self, n_total, row0, Q, n_top=5, seed=0x5EED, x_mean=None):
+        """Add the "k-means recommend" step of C5 (BASELINE configs[4]) to every
+        iteration: Q query users spread over the whole job (synth_recom_users)
+        get get_top_N_recom over their whole clusters (recommend_sharded). The
+        users' clusters are this iteration's assignment (main.cpp:261)."""
+        torch = self.ctx.torch
+        n = self.X.shape[0]
+        if x_mean is None:
+            x_mean = torch.zeros((n,), dtype=torch.float64, device=self.ctx.dev)
+        rows, U, um, up, ui = synth_recom_users(self.ctx, n_total, Q, self.d, seed)
+        self.recom = dict(row0=row0, n_top=n_top, x_mean=x_mean, rows=rows, U=U, u_mean=um, unk_ptr=up, unk_idx=ui)
+        self.recom_out = None
+        self.recom_ucl = None
+        self.recom_timing = None      # a list: (phase-1 ms, phase-2 ms) per step
+
+    def recommend(self):
+        r = self.recom
+        ucl = user_clusters(self.ctx, r["rows"], self.assign, r["row0"], self.X.shape[0])
+        self.recom_ucl = ucl
+        self.recom_out = recommend_sharded(self.lk, self.ctx, self.X, r["x_mean"], self.assign, self.K, r["U"],
+                                           r["u_mean"], ucl, r["unk_ptr"], r["unk_idx"], r["n_top"],
+                                           timing=self.recom_timing)
+        return self.recom_out
 
     def exchange_ms(self):
         """Mean all-reduce time (ms) over the timed steps (torch's stream, which

@@ -396,6 +396,48 @@ int lshkm_cluster_top_n_f64(lshkm_ctx ctx, const double* X_dev, const double* x_
                             const double* u_mean_dev, int64_t nq, const int32_t* ucl_dev, const int64_t* unk_ptr_dev,
                             const int32_t* unk_idx_dev, int n_top, int32_t* out_dev);
 
+/* The same over row shards (the C5 recommend step): a cluster's
+ * members lie on every rank, in row order = rank order, and
+ * get_predicted_user_sim's sums (crypto_rec.hpp:285-303) run over them in that
+ * order -- so the sums pass from rank to rank (point-to-point, like the exact
+ * k-means carry). Every rank holds the same nq query users (U_dev rows,
+ * u_mean, ucl = their global cluster IDs, the unknown lists) and the CSR of
+ * its own rows' clusters (lshkm_clusters of its assignment: local row ids).
+ * lshkm_cluster_sims: each user's similarities to this rank's members of its
+ *   cluster, the bulk of the work and independent of the other ranks:
+ *   soff_dev [nq+1] <- offsets; sims_dev [cap] <- the similarities in member
+ *   order when *total_host <= cap (call with sims_dev = NULL to size).
+ * lshkm_cluster_chain: the prediction sums continued over this rank's members
+ *   from the previous rank's carry (carry_* all NULL on rank 0): carry_main /
+ *   main_out [total unknown indexes] (per unknown index, unk_ptr order),
+ *   carry_abs / abs_out and carry_cnt / cnt_out [nq] (sum |sim|, members so
+ *   far); send the outputs to the next rank. The last rank passes out_dev
+ *   [nq][n_top] instead (main_out etc. may be NULL): the predictions, the
+ *   quicksort and the first n_top as lshkm_cluster_top_n, -1 for users whose
+ *   cluster is empty on every rank. Chained over the ranks in row order this is
+ *   lshkm_cluster_top_n over the concatenated rows, bit for bit. */
+int lshkm_cluster_sims(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                       const int32_t* crows_dev, int K, const float* U_dev, int64_t nq, const int32_t* ucl_dev,
+                       const int64_t* unk_ptr_dev, int64_t* soff_dev, double* sims_dev, int64_t cap,
+                       int64_t* total_host);
+int lshkm_cluster_sims_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                           const int32_t* crows_dev, int K, const double* U_dev, int64_t nq, const int32_t* ucl_dev,
+                           const int64_t* unk_ptr_dev, int64_t* soff_dev, double* sims_dev, int64_t cap,
+                           int64_t* total_host);
+int lshkm_cluster_chain(lshkm_ctx ctx, const float* X_dev, const double* x_mean_dev, int64_t N, int d,
+                        const int64_t* crow_dev, const int32_t* crows_dev, int K, int64_t nq, const int32_t* ucl_dev,
+                        const double* u_mean_dev, const int64_t* unk_ptr_dev, const int32_t* unk_idx_dev,
+                        const int64_t* soff_dev, const double* sims_dev, const double* carry_main_dev,
+                        const double* carry_abs_dev, const int64_t* carry_cnt_dev, double* main_out_dev,
+                        double* abs_out_dev, int64_t* cnt_out_dev, int n_top, int32_t* out_dev);
+int lshkm_cluster_chain_f64(lshkm_ctx ctx, const double* X_dev, const double* x_mean_dev, int64_t N, int d,
+                            const int64_t* crow_dev, const int32_t* crows_dev, int K, int64_t nq,
+                            const int32_t* ucl_dev, const double* u_mean_dev, const int64_t* unk_ptr_dev,
+                            const int32_t* unk_idx_dev, const int64_t* soff_dev, const double* sims_dev,
+                            const double* carry_main_dev, const double* carry_abs_dev, const int64_t* carry_cnt_dev,
+                            double* main_out_dev, double* abs_out_dev, int64_t* cnt_out_dev, int n_top,
+                            int32_t* out_dev);
+
 /* ------------------------------------------------------------ input formats
  * Host only (no device needed). VectorReader<double>::read
  * (vector_reader.hpp:54-85): lines 1..strt_line-1 kept as metadata, then one

@@ -45,8 +45,15 @@ def main():
     res = {}
     for mode in ("fast", "exact"):
         it = sh.ShardedLloyd(lshkm, ctx, lsh, X, C0, sh.local_src_rows(rows, row0, n), mode=mode)
+        if mode == "fast":
+            # C5's recommend step: 96 users over the whole job, their whole clusters
+            # (the prediction sums carried rank to rank, sharding.recommend_sharded)
+            it.enable_recommend(N_TOTAL, row0, Q=96, n_top=5)
         for s in range(STEPS):
             it.step()
+            if mode == "fast":
+                res[f"recom{s}"] = it.recom_out.cpu().numpy()
+                res[f"recom_ucl{s}"] = it.recom_ucl.cpu().numpy()
             res[f"{mode}_assign{s}"] = it.assign.cpu().numpy()
             res[f"{mode}_dist{s}"] = it.dist.cpu().numpy()
             res[f"{mode}_centers{s + 1}"] = it.C.cpu().numpy()

@@ -245,7 +245,7 @@ def test_c5_shard_full_size(ctx):
         cont = it.step()
         ctx.sync()
         assert np.array_equal(it.assign.cpu().numpy(), assign_h), kmode
-        assert np.array_equal(it.counts.cpu().numpy(), cnt_o), kmode
+        assert np.array_equal(it.last_counts.cpu().numpy(), cnt_o), kmode
         assert cont == cont_o
         assert np.array_equal(it.C.cpu().numpy().view(np.uint64), Cn_o.view(np.uint64)), kmode
 

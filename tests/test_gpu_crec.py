@@ -157,3 +157,47 @@ def test_cluster_top_n_device_csr_from_lshkm_clusters(ctx):
     want = oracle.cluster_top_n(Xh, xm, crow.cpu().numpy(), crows.cpu().numpy(), Xh[q], xm[q], a.cpu().numpy()[q],
                                 up, ui, 5)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("kind", ["f32", "f64"])
+def test_shard_carry_chain_equals_single_pass(ctx, kind):
+    # the sharded form (lshkm_cluster_sims + lshkm_cluster_chain) on
+    # one GPU: the rows cut into 3 contiguous shards, each shard's local cluster
+    # CSR, the prediction sums carried shard to shard in row order -- bit for bit
+    # lshkm_cluster_top_n over all rows (and the oracle); a cluster empty on some
+    # shards, empty on all shards, and members only on the last shard
+    rng = np.random.default_rng(17 if kind == "f32" else 18)
+    N, d, K, nq, NT = 24_000, 64, 20, 500, 5
+    X = rng.standard_normal((N, d))
+    X = X.astype(np.float32) if kind == "f32" else np.round(X * 2**18) / 2**18
+    xm = (rng.integers(-8, 9, size=N) / 8.0).astype(np.float64)
+    assign = rng.integers(0, K, size=N).astype(np.int32)
+    assign[assign == 19] = 18                          # cluster 19 empty everywhere
+    assign[:16_000][assign[:16_000] == 17] = 16        # cluster 17 only on the last shard
+    assign[8_000:16_000][assign[8_000:16_000] == 15] = 14   # cluster 15 absent from the middle shard
+    users = rng.choice(N, nq, replace=False)
+    U = X[users].copy()
+    um = (rng.integers(-8, 9, size=nq) / 8.0).astype(np.float64)
+    ucl = assign[users].copy()
+    ucl[::23] = 19
+    ucl[1::29] = 17
+    up, ui = unknown_sets(rng, nq, d)
+    crow, crows = oracle.clusters_csr(assign, K)
+    want = oracle.cluster_top_n(X, xm, crow, crows, U, um, ucl, up, ui, NT)
+    Ud, umd, ucd, upd, uid = dev(ctx, U), dev(ctx, um), dev(ctx, ucl), dev(ctx, up), dev(ctx, ui)
+    single = lshkm.cluster_top_n(ctx, dev(ctx, X), dev(ctx, xm), dev(ctx, crow), dev(ctx, crows), Ud, umd, ucd, upd,
+                                 uid, NT).cpu().numpy()
+    assert np.array_equal(single, want)
+    carry, bounds = None, [0, 8_000, 16_000, N]
+    for s in range(3):
+        lo, hi = bounds[s], bounds[s + 1]
+        Xs = dev(ctx, X[lo:hi])
+        lcrow, lrows = oracle.clusters_csr(assign[lo:hi], K)
+        a = (ctx, Xs, dev(ctx, xm[lo:hi]), dev(ctx, lcrow), dev(ctx, lrows), ucd, umd, upd, uid)
+        soff, sims = lshkm.cluster_sims(ctx, Xs, dev(ctx, lcrow), dev(ctx, lrows), Ud, ucd, upd)
+        if s < 2:
+            carry = lshkm.cluster_chain(*a, soff, sims, carry=carry, n_top=None)
+        else:
+            got = lshkm.cluster_chain(*a, soff, sims, carry=carry, n_top=NT).cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
+    assert (want[:, 0] == -1).any()

@@ -101,6 +101,21 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path, dist_mode):
     oa, od = oracle.lloyd_assign(Xall[sub], Xall[rows].astype(np.float64), "euclidean", None)
     assert np.array_equal(cat("fast_assign0")[sub], oa)
     assert_dist(cat("fast_dist0")[sub], od, dist_mode)
+    # the C5 recommend step (recommend_sharded: the prediction sums carried from
+    # rank to rank): every rank holds the single process's result, which is the
+    # oracle's get_top_N_recom over the users' whole clusters
+    for s in range(2):
+        for r in two:
+            assert np.array_equal(r[f"recom_ucl{s}"], one[f"recom_ucl{s}"]), s
+            assert np.array_equal(r[f"recom{s}"], one[f"recom{s}"]), s
+    qrows = np.arange(96, dtype=np.int64) * (N // 96)
+    sets = [np.nonzero((7 * np.arange(128) + int(r)) % 16 == 0)[0].astype(np.int32) for r in qrows]
+    up = np.cumsum([0] + [len(x) for x in sets]).astype(np.int64)
+    crow, crows = oracle.clusters_csr(one["fast_assign1"], K)
+    want = oracle.cluster_top_n(Xall, np.zeros(N), crow, crows, Xall[qrows], np.zeros(96), one["recom_ucl1"], up,
+                                np.concatenate(sets), 5)
+    assert np.array_equal(one["recom_ucl1"], one["fast_assign1"][qrows])
+    assert np.array_equal(one["recom1"], want)
     # hypercube: same coins, same engine state, same vertices
     for key in ("memo_f", "memo_h", "memo_bit", "memo_state"):
         for r in two:
