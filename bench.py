@@ -11,7 +11,11 @@
 --workload c5 (configs[4]: 80M x 128, K=1024 over 8 GPUs = 10M per GPU): one
   step = one full iteration, sharding.ShardedLloyd: lshkm_hash_assign (K=1024)
   + lshkm_kmeans_partial + all-reduce of the K x d sums and K counts over RCCL
-  + lshkm_kmeans_finalize (centers replaced as k_means does).
+  + lshkm_kmeans_finalize (centers replaced as k_means does) + the recommend
+  step ("k-means recommend"): --recom-users Q query users (rows spread over the
+  whole job) get get_top_N_recom over their whole clusters (crypto_rec.hpp:
+  327-345): similarities on every rank, prediction sums carried rank to rank
+  over RCCL point-to-point (sharding.recommend_sharded).
 Points are synthetic (include/lshkm_synth.h), generated in HBM before timing.
 
 python bench.py --gpus N --steps K --warmup W [--workload c5]
@@ -264,6 +268,8 @@ def main():
     ap.add_argument("--workload", choices=["c3", "c5"], default="c3")
     ap.add_argument("--k", type=int, default=None, help="centroids (default 256 for c3, 1024 for c5)")
     ap.add_argument("--no-c5", action="store_true", help="c3: leave out the C5 iteration object")
+    ap.add_argument("--recom-users", type=int, default=1024,
+                    help="C5: query users per iteration of the recommend step (0: no recommend step)")
     ap.add_argument("--no-exact-dist-line", dest="exact_dist_line", action="store_false",
                     help="c3: leave out the timing with bit-exact (fp64 chain) distances")
     ap.add_argument("--dry-run", action="store_true", help="gloo on CPU, no GPU work (tests the rank plumbing)")
@@ -352,22 +358,47 @@ def main():
         return elapsed, kms, ex
 
     def c5_run(K):
-        # one full iteration: hash + assign, per-shard sums, RCCL all-reduce, finalize
+        # one full iteration: hash + assign, per-shard sums, RCCL all-reduce,
+        # finalize, and the recommend step (get_top_N_recom over the whole
+        # clusters of Q query users, the prediction sums carried rank to rank)
         Cc, src = initial_centroids(K)
         it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="fast")
+        if args.recom_users > 0:
+            it.enable_recommend(N_total, rank * N, Q=args.recom_users, n_top=5)
         elapsed = timed(it.step, args.steps, args.warmup, world, dev)
         it.timing = True
         kms = fused_kernel_ms(lk, lib, ctx, it.step, max(3, args.steps))
         it.timing = False
         xms = it.exchange_ms() if world > 1 else None
-        return elapsed, kms, xms
+        rec = None
+        if args.recom_users > 0:
+            it.recom_timing = []
+            for _ in range(3):
+                it.step()
+            ph1 = sorted(a for a, _ in it.recom_timing)[1]
+            ph2 = sorted(b for _, b in it.recom_timing)[1]
+            it.recom_timing = None
+            ucl = it.recom_ucl.cpu().numpy()
+            counts = it.last_counts.cpu().numpy()
+            sims = int(counts[ucl].sum())
+            rec = {"what": "get_top_N_recom(neighbors, user, 5) over the user's whole cluster (crypto_rec.hpp:327-345, "
+                           "main.cpp:260-269): x87-exact cosine similarities to every member on every rank "
+                           "(lshkm_cluster_sims), then the prediction sums carried rank to rank in row order "
+                           "(lshkm_cluster_chain, RCCL point-to-point) and the quicksort",
+                   "users_per_step": args.recom_users, "n_top": 5,
+                   "users": "rows i * floor(N_total / Q) of the whole job (their clusters span every shard)",
+                   "similarities_per_step": sims, "sims_ms": ph1, "chain_ms": ph2,
+                   "users_per_s": args.recom_users / ((ph1 + ph2) / 1e3),
+                   "similarities_per_s": sims / ((ph1 + ph2) / 1e3)}
+        return elapsed, kms, xms, rec
 
-    def c5_object(K, elapsed, kms, xms):
+    def c5_object(K, elapsed, kms, xms, rec=None):
         coll = (f"RCCL all-reduce ({backend}) of the {K}x128 fp64 sums + {K} counts" if world > 1
                 else "none (N = 1: a single shard, no collective)")
         return {
-            "metric": f"C5 LSH-assign + k-means iterations: points/s (hash + assign K={K} + sums + "
-                      f"{'RCCL all-reduce' if world > 1 else 'no collective at N = 1'} + finalize)",
+            "metric": f"C5 LSH-assign + k-means recommend iterations: points/s (hash + assign K={K} + sums + "
+                      f"{'RCCL all-reduce' if world > 1 else 'no collective at N = 1'} + finalize"
+                      + (f" + recommend for {args.recom_users} users)" if args.recom_users > 0 else ")"),
             "value": N_total * args.steps / elapsed, "unit": "point iteration ops/s",
             "ms_per_step": elapsed / args.steps * 1e3, "n_gpus": world, "scaling": "weak",
             "config": {"workload": f"C5 (BASELINE configs[4]): N={N} per GPU x {world} GPU(s), d=128, K={K}, "
@@ -375,6 +406,7 @@ def main():
                        "N_per_gpu": N, "N_total": N_total, "K": K, "parallelism": f"dp{world} (row shards)"},
             "allreduce": coll,
             "allreduce_ms": xms if world > 1 else None,
+            "recommend": rec,
             "roofline": roofline(N, K, kms, traffic_for(args.traffic_json_c5, N, K, "c5"),
                                  FUSED_WHAT + " (K = 1024: two 512-centroid passes)"),
         }
@@ -382,8 +414,8 @@ def main():
     line = None
     if args.workload == "c5":
         K = args.k or 1024
-        el, kms, xms = c5_run(K)
-        line = c5_object(K, el, kms, xms)
+        el, kms, xms, rec = c5_run(K)
+        line = c5_object(K, el, kms, xms, rec)
         line.update({"metric": METRIC + " (C5 workload)", "unit": "point hash+assign ops/s", "steps": args.steps,
                      "warmup": args.warmup, "higher_is_better": True, "vs_baseline": None,
                      "dtype": DTYPE,
@@ -405,8 +437,8 @@ def main():
         }
         if not args.no_c5:
             K5 = 1024
-            el5, kms5, xms5 = c5_run(K5)
-            line["c5"] = c5_object(K5, el5, kms5, xms5)
+            el5, kms5, xms5, rec5 = c5_run(K5)
+            line["c5"] = c5_object(K5, el5, kms5, xms5, rec5)
     line["world_size"] = world
     line["backend"] = backend
     if world > 1:
