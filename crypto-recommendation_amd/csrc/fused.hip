@@ -472,6 +472,21 @@ constexpr int FP_WAVES = FP_WAVES_SET ? FP_WAVES_SET : FP_KEEP_X ? 8 : 12;   // 
 #ifndef XPF
 #define XPF 0           // hi-only kernel: next tile's row loaded during the winner chain
 #endif
+// NO_XF (the hashing FAST kernel): the row's f32 copy dies after the split; the
+// certified distance is formed from its f16 hi + lo parts (kept instead, half
+// the registers), the residual |x - hi - lo| <= 2^-22 |x| + 2^-25 per value
+// joining the centroid's in the bound. HASH_LDS_FENCE: the hash tile's A
+// operands read per 16-dim step (the compiler otherwise hoists all 16 LDS reads
+// and holds 64 registers through the split).
+#ifndef NO_XF
+#define NO_XF 0
+#endif
+#ifndef HASH_LDS_FENCE
+#define HASH_LDS_FENCE 0
+#endif
+#ifndef FH_WAVES_HFAST
+#define FH_WAVES_HFAST 8      // waves of the hashing single-pass FAST kernel (12: needs <= 168 VGPRs)
+#endif
 // General rows (ROWS = 1: fp32, 2: fp64; d <= 128 dims, row stride d): lane
 // half h's 64 values of row rowc in the B-operand layout (dims 16s+8h..+7),
 // zero past d; fp64 values rounded to f32 (the scores' operand; the bounds add
@@ -1172,12 +1187,15 @@ constexpr double FH_A = 130.0 * 0x1p-23;
 // 12 waves): first pass (hash) 1.91 -> 1.88 ms at 12 waves, second pass
 // (chain) 2.48 -> 2.59 ms -- a third wave per SIMD does not pay. FH_WAVES_SET
 // forces one count for all (experiments).
-template <bool HASH, bool MP, int MET>
+#ifndef FH_WAVES_MPFAST
+#define FH_WAVES_MPFAST 8     // the last pass of the multi-pass form with the certified distance (A/B knob)
+#endif
+template <bool HASH, bool MP, int MET, bool FAST = false>
 __host__ __device__ constexpr int fh_waves() {
 #ifdef FH_WAVES_SET
     return FH_WAVES_SET;
 #else
-    return HASH && MP ? 12 : 8;
+    return HASH && MP ? 12 : (MP && FAST ? FH_WAVES_MPFAST : (HASH && FAST ? FH_WAVES_HFAST : 8));
 #endif
 }
 constexpr int FH_WAVES_MIN = 8, FH_WAVES_MAX = 12;
@@ -1374,8 +1392,8 @@ __device__ inline void glds16(const void* gsrc, uint32_t lds_dst) {
 // through the gather ring (GATH) each 16-dim step waits on its DMA, and the
 // short f32 sum cannot hide that (fused pass 2.21 vs 2.14 ms at C3).
 template <bool HASH, bool MP = false, int MET = 0, int NIMG = 1, bool GATH = false, int ROWS = 0, bool FAST = false>
-__global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_kernel(FusedArgs a) {
-    constexpr int FH_WAVES = fh_waves<HASH, MP, MET>();
+__global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fused_hi_kernel(FusedArgs a) {
+    constexpr int FH_WAVES = fh_waves<HASH, MP, MET, FAST>();
     constexpr int FH_THREADS = 64 * FH_WAVES;
     static_assert(NIMG == 1 || (!MP && MET == 0), "two-image form: euclidean, single launch");
     static_assert(!GATH || (!MP && MET == 0 && NIMG == 1 && FH_WAVES == 8), "gather ring: euclidean single pass");
@@ -1502,6 +1520,8 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
         const bool valid = row < a.N;
         if (!xpf) load_row(tile, xf);
         half8 bh[8];
+        constexpr bool noxf = NO_XF && FAST && HASH && MET == 0 && ROWS == 0 && NIMG == 1 && !GATH;
+        half8 blk[noxf ? 8 : 1];              // NO_XF: the lo halves, kept for the distance
         float2v n2a = {0.f, 0.f}, n2b = {0.f, 0.f}, r2 = {0.f, 0.f};
         // hi part of 8 values (LO: and the lo part), |x|^2 and |x - xh|^2 partial sums
         auto split_step = [&](int s, half8& lo, auto lo_tag) {
@@ -1558,6 +1578,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                 for (int s = 0; s < 8; s++) {
                     half8 bls;
                     split_step(s, bls, std::true_type{});
+                    if constexpr (noxf) blk[s] = bls;
+#if HASH_LDS_FENCE
+                    asm volatile("" ::: "memory");
+#endif
                     const half8 ah = *reinterpret_cast<const half8*>(vh_row + 16 * s);
                     const half8 al = *reinterpret_cast<const half8*>(vl_row + 16 * s);
                     const floatx16 z = {};
@@ -1853,14 +1877,29 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET>()), 1) void fused_hi_
                     const float2v cv[4] = {{c0.x, c0.y}, {c0.z, c0.w}, {c1.x, c1.y}, {c1.z, c1.w}};
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        const float2v xv = {xf[8 * s + 2 * j], xf[8 * s + 2 * j + 1]};
-                        const float2v dv = xv - cv[j];
+                        float2v dv;
+                        if constexpr (noxf) {
+                            // (hi - c) + lo, two f32 roundings (in the bound below)
+                            const half2v hp = {bh[s][2 * j], bh[s][2 * j + 1]};
+                            const half2v lp = {blk[s][2 * j], blk[s][2 * j + 1]};
+                            dv = float2v{mix_add_lo(lp, mix_sub_lo(hp, cv[j].x)), mix_add_hi(lp, mix_sub_hi(hp, cv[j].y))};
+                        } else {
+                            const float2v xv = {xf[8 * s + 2 * j], xf[8 * s + 2 * j + 1]};
+                            dv = xv - cv[j];
+                        }
                         q[j] = __builtin_elementwise_fma(dv, dv, q[j]);
                     }
                 }
                 float t = ((q[0].x + q[0].y) + (q[1].x + q[1].y)) + ((q[2].x + q[2].y) + (q[3].x + q[3].y));
                 t = t + swap_halves_f(t, h);
-                const double S = (double)t, R = (double)a.rn32[I1];
+                const double S = (double)t;
+                double R = (double)a.rn32[I1];
+                if constexpr (noxf) {
+                    // |x - hi - lo| (<= 2^-22 |x| + 2^-25 per value) and the extra
+                    // rounding of hi - c (<= 2^-24 |hi - c| <= 2^-24 (|b| + |lo|))
+                    R = (R + 0x1p-22 * (1.0 + 0x1p-10) * nx + 0x1p-21 +
+                         0x1p-23 * (sqrt(S) * (1.0 + 0x1p-20) + 0x1p-11 * nx + 0x1p-20)) * (1.0 + 0x1p-20);
+                }
                 const double B = 14.2 * 0x1p-24 * S + 2.02 * R * sqrt(S) + 2.02 * R * R + 0x1p-100;
                 dok = B <= 0x1p-19 * S;                   // false for inf / nan
                 fdist = sqrt(S);
@@ -2570,7 +2609,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                     if (hash && p == 0) FH_LAUNCH(true, true, 0);
                     else if (a.fast_dist && a.pass_last)   // the winner's distance: certified f32, compiled in
                         hipLaunchKernelGGL((fused_hi_kernel<false, true, 0, 1, false, 0, true>), grid,
-                                           dim3(64 * fh_waves<false, true, 0>()), lh, s, a);
+                                           dim3(64 * fh_waves<false, true, 0, true>()), lh, s, a);
                     else FH_LAUNCH(false, true, 0);
                 }
 #undef FH_LAUNCH

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from amd import lshkm  # noqa: E402
 
-N, D, K, L, KF = int(os.environ.get("TF_N", 10_000_000)), 128, 256, 5, 4
+N, D, K, L, KF = int(os.environ.get("TF_N", 10_000_000)), 128, int(os.environ.get("TF_K", 256)), 5, 4
 ctx = lshkm.Context(0)
 lib = lshkm.lib()
 X = ctx.synth(0x5EED, N, D)
