@@ -39,6 +39,7 @@
 #include "softx87.h"
 #include "exact.h"
 #include "tile.h"
+#include "fused_args.h"
 
 namespace lshkm {
 
@@ -52,71 +53,6 @@ constexpr int FU_HS_OFF = FU_XSTAGE_BYTES;              // hash values [128][32]
 constexpr int FU_LDS_BYTES = FU_HS_OFF + FU_PB * 32 * 4; // 80 KiB -> 2 blocks / CU
 static_assert(FU_CHUNK_BYTES <= FU_XSTAGE_BYTES, "chunk region must fit in the staging alias");
 
-struct FusedArgs {
-    const float* X;
-    int64_t N;
-    // centroids (prepared by fused_centroid_prep)
-    const _Float16* Ch;
-    const _Float16* Cl;
-    const float* cnh;        // [Kpad] -||c||^2 / 2 (f32), -inf for padding rows
-    const float* cbound;     // [0] = ec (times |x|), [1] = eb (constant), [2] = range flag (bits), [3] = max |c|,
-                             // [4] = max |c - ch|, [5] = max |ch|, [6] = max |c|^2 / 2 (all rounded up),
-                             // [7] = nonzero if some centroid value is not an f32 (bits)
-    const double* C64;       // [K][128] exact centroids
-    int Kpad;
-    // hash family (HASH only)
-    const _Float16* Vh;      // [32][128] f16 hi of the projections (rows >= LK zero)
-    const _Float16* Vl;
-    const double* PT;        // [128][LKpad] fp64 projections (exact paths)
-    const float* tv;         // [LK]
-    const double* pnorm;     // [LK] ||v||_2 (rounded up)
-    const double* v1;        // [LK] ||v||_1 (rounded up)
-    const int32_t* rv;       // [LK]
-    float w;
-    int L, k, LK, LKpad;
-    int64_t nb;
-    // outputs
-    int32_t* tuples;         // [N][L][k] (may be null)
-    int32_t* phi;            // [N][L] (may be null)
-    int32_t* bucket;         // [N][L] (may be null)
-    int32_t* assign;         // [N]
-    double* dist;            // [N]
-    int32_t* ambig;          // [N] uncertified rows
-    unsigned long long* ambig_count;
-    unsigned long long* hfix;        // persistent form: rows with an uncertified floor
-    unsigned long long* hfix_count;
-    // hi-only cosine form: rows whose winner distance the certified quotient
-    // declined (cos_fix_seg pass); counts in cfix_counts[2b + 1]
-    unsigned long long* cfix;
-    int32_t* cfix_counts;
-    unsigned long long* cfix_count;
-    unsigned long long* stats;
-    // persistent form: block b owns ambig/hfix entries [b * seg_rows, (b+1) * seg_rows)
-    // and reports their counts in seg_counts[2b] (ambiguous), seg_counts[2b+1] (fix-up)
-    int64_t seg_rows;
-    int32_t* seg_counts;
-    BucketDiv bdiv;          // phi % nb by multiply-high
-    const double* nbv;       // cosine: [K] sequential sum of c_j^2 (cust_vector.hpp:139-155)
-    // multi-pass persistent form (K > 256): this launch scores centroid tiles
-    // t0.. of the slice in Ch/Cl/cnh (Kpad rows); the running state per lane
-    // crosses passes in part[tile * 64 + lane]
-    float4* part;
-    int t0, pass_first, pass_last;
-    // LIST form (refinement of the rows a hi-only pass left uncertified): block b
-    // takes the rows list_in[b * list_seg_rows ..][0 .. list_counts[2b])
-    const int32_t* list_in;
-    const int32_t* list_counts;
-    int64_t list_seg_rows;
-    unsigned long long* prof;        // LSHKM_PHASE_TIMING builds only: per-phase wave cycles
-    const float* C32;                // fast_dist: [Kpad][128] f32(c) and |c - f32(c)| (FusedLaunch)
-    const float* rn32;
-    int fast_dist;
-    // general rows (fused_hi_kernel<..., ROWS = 1 / 2>): fp32 (X) or fp64 (X64)
-    // rows of d <= 128 dims, row stride d; xvec: rows 16-B aligned (vector loads)
-    const double* X64;
-    int d, xvec;
-    const double* Cd;                // general rows: the caller's [K][d] centroids (cosine winners)
-};
 
 // Profiling builds (make prof -> liblshkm_prof.so) accumulate s_memtime per
 // phase of the persistent loop; the product library compiles these away.
@@ -471,21 +407,6 @@ constexpr int FP_WAVES = FP_WAVES_SET ? FP_WAVES_SET : FP_KEEP_X ? 8 : 12;   // 
 #endif
 #ifndef XPF
 #define XPF 0           // hi-only kernel: next tile's row loaded during the winner chain
-#endif
-// NO_XF (the hashing FAST kernel): the row's f32 copy dies after the split; the
-// certified distance is formed from its f16 hi + lo parts (kept instead, half
-// the registers), the residual |x - hi - lo| <= 2^-22 |x| + 2^-25 per value
-// joining the centroid's in the bound. HASH_LDS_FENCE: the hash tile's A
-// operands read per 16-dim step (the compiler otherwise hoists all 16 LDS reads
-// and holds 64 registers through the split).
-#ifndef NO_XF
-#define NO_XF 0
-#endif
-#ifndef HASH_LDS_FENCE
-#define HASH_LDS_FENCE 0
-#endif
-#ifndef FH_WAVES_HFAST
-#define FH_WAVES_HFAST 8      // waves of the hashing single-pass FAST kernel (12: needs <= 168 VGPRs)
 #endif
 // General rows (ROWS = 1: fp32, 2: fp64; d <= 128 dims, row stride d): lane
 // half h's 64 values of row rowc in the B-operand layout (dims 16s+8h..+7),
@@ -1172,6 +1093,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 // One third of the MFMA work of the 3-product form, and only the hi image of
 // the centroids in LDS: up to 512 centroids per pass (K = 1024: 2 passes).
 constexpr int FH_KMAX = 512;
+// fused16.hip: the single-pass FAST form over 16-row tiles
+int launch_fused16(const FusedArgs& a, bool hash, int nblk, hipStream_t s);
+int fused16_waves();
 __host__ __device__ constexpr int fh_lds_bytes(int Kpad, bool hash) {
     return 16 + Kpad * FU_RS * 2 + Kpad * 4 + (hash ? 2 * 32 * FU_RS * 2 + FP_HC_BYTES : 0);
 }
@@ -1188,14 +1112,14 @@ constexpr double FH_A = 130.0 * 0x1p-23;
 // (chain) 2.48 -> 2.59 ms -- a third wave per SIMD does not pay. FH_WAVES_SET
 // forces one count for all (experiments).
 #ifndef FH_WAVES_MPFAST
-#define FH_WAVES_MPFAST 8     // the last pass of the multi-pass form with the certified distance (A/B knob)
+#define FH_WAVES_MPFAST 12     // the last pass of the multi-pass form with the certified distance
 #endif
 template <bool HASH, bool MP, int MET, bool FAST = false>
 __host__ __device__ constexpr int fh_waves() {
 #ifdef FH_WAVES_SET
     return FH_WAVES_SET;
 #else
-    return HASH && MP ? 12 : (MP && FAST ? FH_WAVES_MPFAST : (HASH && FAST ? FH_WAVES_HFAST : 8));
+    return HASH && MP ? 12 : (MP && FAST ? FH_WAVES_MPFAST : 8);
 #endif
 }
 constexpr int FH_WAVES_MIN = 8, FH_WAVES_MAX = 12;
@@ -1520,8 +1444,6 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
         const bool valid = row < a.N;
         if (!xpf) load_row(tile, xf);
         half8 bh[8];
-        constexpr bool noxf = NO_XF && FAST && HASH && MET == 0 && ROWS == 0 && NIMG == 1 && !GATH;
-        half8 blk[noxf ? 8 : 1];              // NO_XF: the lo halves, kept for the distance
         float2v n2a = {0.f, 0.f}, n2b = {0.f, 0.f}, r2 = {0.f, 0.f};
         // hi part of 8 values (LO: and the lo part), |x|^2 and |x - xh|^2 partial sums
         auto split_step = [&](int s, half8& lo, auto lo_tag) {
@@ -1578,10 +1500,6 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                 for (int s = 0; s < 8; s++) {
                     half8 bls;
                     split_step(s, bls, std::true_type{});
-                    if constexpr (noxf) blk[s] = bls;
-#if HASH_LDS_FENCE
-                    asm volatile("" ::: "memory");
-#endif
                     const half8 ah = *reinterpret_cast<const half8*>(vh_row + 16 * s);
                     const half8 al = *reinterpret_cast<const half8*>(vl_row + 16 * s);
                     const floatx16 z = {};
@@ -1877,29 +1795,14 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                     const float2v cv[4] = {{c0.x, c0.y}, {c0.z, c0.w}, {c1.x, c1.y}, {c1.z, c1.w}};
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        float2v dv;
-                        if constexpr (noxf) {
-                            // (hi - c) + lo, two f32 roundings (in the bound below)
-                            const half2v hp = {bh[s][2 * j], bh[s][2 * j + 1]};
-                            const half2v lp = {blk[s][2 * j], blk[s][2 * j + 1]};
-                            dv = float2v{mix_add_lo(lp, mix_sub_lo(hp, cv[j].x)), mix_add_hi(lp, mix_sub_hi(hp, cv[j].y))};
-                        } else {
-                            const float2v xv = {xf[8 * s + 2 * j], xf[8 * s + 2 * j + 1]};
-                            dv = xv - cv[j];
-                        }
+                        const float2v xv = {xf[8 * s + 2 * j], xf[8 * s + 2 * j + 1]};
+                        const float2v dv = xv - cv[j];
                         q[j] = __builtin_elementwise_fma(dv, dv, q[j]);
                     }
                 }
                 float t = ((q[0].x + q[0].y) + (q[1].x + q[1].y)) + ((q[2].x + q[2].y) + (q[3].x + q[3].y));
                 t = t + swap_halves_f(t, h);
-                const double S = (double)t;
-                double R = (double)a.rn32[I1];
-                if constexpr (noxf) {
-                    // |x - hi - lo| (<= 2^-22 |x| + 2^-25 per value) and the extra
-                    // rounding of hi - c (<= 2^-24 |hi - c| <= 2^-24 (|b| + |lo|))
-                    R = (R + 0x1p-22 * (1.0 + 0x1p-10) * nx + 0x1p-21 +
-                         0x1p-23 * (sqrt(S) * (1.0 + 0x1p-20) + 0x1p-11 * nx + 0x1p-20)) * (1.0 + 0x1p-20);
-                }
+                const double S = (double)t, R = (double)a.rn32[I1];
                 const double B = 14.2 * 0x1p-24 * S + 2.02 * R * sqrt(S) + 2.02 * R * R + 0x1p-100;
                 dok = B <= 0x1p-19 * S;                   // false for inf / nan
                 fdist = sqrt(S);
@@ -2498,6 +2401,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         // the hi-only form strides by fh_waves() tiles per block (8 or 12)
         for (const int W : {FH_WAVES_MIN, FH_WAVES_MAX})
             a.seg_rows = std::max<int64_t>(a.seg_rows, (int64_t)W * 32 * ((ntiles + (int64_t)nblk * W - 1) / ((int64_t)nblk * W)));
+        {   // the 16-row form (fused16.hip)
+            const int64_t W = fused16_waves(), nt16 = (f.N + 15) / 16;
+            a.seg_rows = std::max<int64_t>(a.seg_rows, W * 16 * ((nt16 + (int64_t)nblk * W - 1) / ((int64_t)nblk * W)));
+        }
         a.seg_counts = f.seg_counts;
         if (!f.seg_counts || f.seg_cap < nblk || (int64_t)nblk * a.seg_rows > f.list_cap) {
             set_error("launch_fused: list workspace too small");
@@ -2591,8 +2498,15 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 #else
                     if (a.Kpad <= FH_GATH_KMAX && !(gv && !strcmp(gv, "0"))) {
                         const size_t lg = (size_t)fh_gath_off(a.Kpad, hash) + 8 * FH_GATH_WAVE;
-                        // the certified f32 winner distance (a.fast_dist) compiled in
-                        if (hash && a.fast_dist)
+                        // the certified f32 winner distance (a.fast_dist) compiled in:
+                        // the 16-row form (fused16.hip) with LSHKM_F16=1 (being measured)
+                        const char* f16v = getenv("LSHKM_F16");
+                        if (a.fast_dist && (f16v && !strcmp(f16v, "1")) && a.Kpad % 16 == 0) {
+                            if (launch_fused16(a, hash, nblk, s)) {
+                                set_error("launch_fused: 16-row form launch");
+                                return -1;
+                            }
+                        } else if (hash && a.fast_dist)
                             hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);
                         else if (a.fast_dist)
                             hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);

@@ -59,29 +59,6 @@ __device__ inline float resid_hi(float x, half2v hp) {
     return r;
 }
 
-// f32(h) - c and f32(h) + t for the low / high f16 of hp, one v_fma_mix_f32 each
-// (the f16 operand widened exactly, one rounding of the f32 result).
-__device__ inline float mix_sub_lo(half2v hp, float c) {
-    float r;
-    asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(c));
-    return r;
-}
-__device__ inline float mix_sub_hi(half2v hp, float c) {
-    float r;
-    asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(c));
-    return r;
-}
-__device__ inline float mix_add_lo(half2v hp, float t) {
-    float r;
-    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(t));
-    return r;
-}
-__device__ inline float mix_add_hi(half2v hp, float t) {
-    float r;
-    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(t));
-    return r;
-}
-
 // EuclideanPhi arithmetic (euclidean_phi_gen.hpp:70-92) in 32-bit form, M =
 // int(pow(2,32)-5) = 2^31-1 under g++. temp = (long)(h * r) is an int32 (the
 // int product wraps), so ((temp % M) + M) % M needs only compares; the uint32

@@ -11,6 +11,9 @@
 // in row order; a wave owns 64 dimensions of one cluster, each lane one chain,
 // and streams the member rows with 16 row loads in flight per lane (row
 // indices are wave-uniform scalar loads). Bytes: 4d per row read once.
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 #include "kernels.h"
 #include "exact.h"
@@ -73,6 +76,96 @@ __device__ __attribute__((always_inline)) inline double km_chain_rows(const TX* 
     return s;
 }
 
+// Wide form (the sequential chains of large clusters): a wave owns 16 dims of
+// one cluster and each load instruction fetches 4 member rows (lane group k =
+// lane >> 4 the row, lane & 15 the dim), so a wave keeps 4 x 48 rows in flight
+// and the d / 16 waves of a cluster run side by side (the 64-dim form held one
+// row per instruction and two waves per cluster at d = 100; the largest
+// cluster's chain set the time). The chain lanes (k = 0) take the other groups'
+// values by lane-half swaps, in row order. Member indices are read one group of
+// 64 ahead of the row loads that use them.
+constexpr int KM16_G = 64;                 // member positions per group (16 steps x 4 rows)
+constexpr int KM16_Q = 3;                  // groups of row loads in flight
+
+__device__ inline double km_x16(double v) {      // lanes k = 0, 2: lane + 16's value
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false)[1];
+    const uint32_t hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false)[1];
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ inline double km_x32(double v) {      // lanes k = 0, 1: lane + 32's value
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false)[1];
+    const uint32_t hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false)[1];
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <typename TX>
+__global__ __launch_bounds__(64) void km_chain16_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
+                                                       const int64_t* __restrict__ crow, const double* __restrict__ carry,
+                                                       const int* __restrict__ flag, double* __restrict__ sums) {
+    const int c = blockIdx.x, jb = blockIdx.y;
+    if (flag && !((flag[c] >> min(31, jb / 4)) & 1)) return;
+    const int lane = threadIdx.x, k = lane >> 4;
+    const int j = jb * 16 + (lane & 15);
+    const int jl = j < d ? j : d - 1;
+    const int64_t beg = crow[c], end = crow[c + 1];
+    double s = carry && j < d ? carry[(size_t)c * d + j] : 0.0;
+    const int64_t ng = (end - beg + KM16_G - 1) / KM16_G;
+    auto idx = [&](int64_t gi) {
+        const int64_t p = beg + gi * KM16_G + lane;
+        return rows[p < end ? p : (end > beg ? end - 1 : beg)];
+    };
+    TX v[KM16_Q + 1][16];
+    auto ld = [&](TX (&vv)[16], int32_t ri) {
+#pragma unroll
+        for (int st = 0; st < 16; st++) {
+            const int rr = __shfl(ri, 4 * st + k);
+            vv[st] = X[(int64_t)rr * d + jl];
+        }
+    };
+    auto add = [&](const TX (&vv)[16], int64_t gi) {
+        const int64_t p0 = beg + gi * KM16_G;
+        const bool full = p0 + KM16_G <= end;
+#pragma unroll
+        for (int st = 0; st < 16; st++) {
+            const double x0 = (double)vv[st];
+            const double x1 = km_x16(x0), x2 = km_x32(x0), x3 = km_x32(km_x16(x0));
+            const int64_t p = p0 + 4 * st;
+            if (full) {
+                s = __dadd_rn(s, x0); s = __dadd_rn(s, x1); s = __dadd_rn(s, x2); s = __dadd_rn(s, x3);
+            } else {
+                if (p < end) s = __dadd_rn(s, x0);
+                if (p + 1 < end) s = __dadd_rn(s, x1);
+                if (p + 2 < end) s = __dadd_rn(s, x2);
+                if (p + 3 < end) s = __dadd_rn(s, x3);
+            }
+        }
+    };
+    if (ng > 0) {
+        // indices one group ahead of the loads that use them
+        int32_t r_next = idx(0);
+        int32_t r_after = idx(1);
+#pragma unroll
+        for (int q = 0; q < KM16_Q; q++) {
+            ld(v[q], r_next);
+            r_next = r_after;
+            r_after = idx(q + 2);
+        }
+        for (int64_t g = 0; g < ng; g += KM16_Q + 1) {
+#pragma unroll
+            for (int u = 0; u <= KM16_Q; u++) {
+                if (g + u >= ng) break;
+                ld(v[(u + KM16_Q) % (KM16_Q + 1)], r_next);     // group g + u + Q (past the end: re-reads)
+                r_next = r_after;
+                r_after = idx(g + u + KM16_Q + 2);
+                add(v[u], g + u);
+            }
+        }
+    }
+    if (k == 0 && j < d) sums[(size_t)c * d + j] = s;
+}
+
 template <typename TX>
 __global__ __launch_bounds__(64) void km_chain_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                      const int64_t* __restrict__ crow, int K,
@@ -89,8 +182,30 @@ __global__ __launch_bounds__(64) void km_chain_kernel(const TX* __restrict__ X, 
     sums[(size_t)c * d + j] = s;
 }
 
+__global__ void km_counts_kernel(const int64_t* __restrict__ crow, int K, const int64_t* __restrict__ carry_counts,
+                                 int64_t* __restrict__ counts) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < K) counts[c] = crow[c + 1] - crow[c] + (carry_counts ? carry_counts[c] : 0);
+}
+
+static bool km_wide() {
+    const char* v = getenv("LSHKM_KM_CHAIN");          // "16": the wide form (being measured)
+    return v && !strcmp(v, "16");
+}
+
 int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K,
                     double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts) {
+    if (km_wide()) {
+        const dim3 grid((unsigned)K, (unsigned)((d + 15) / 16));
+        if (X.f64)
+            hipLaunchKernelGGL(km_chain16_kernel<double>, grid, dim3(64), 0, s, X.d(), d, rows, crow, carry, nullptr, sums);
+        else
+            hipLaunchKernelGGL(km_chain16_kernel<float>, grid, dim3(64), 0, s, X.f(), d, rows, crow, carry, nullptr, sums);
+        if (counts)
+            hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
+                               counts);
+        return kstatus("update.hip");
+    }
     const dim3 grid((unsigned)K, (unsigned)((d + 63) / 64));
     if (X.f64)
         hipLaunchKernelGGL(km_chain_kernel<double>, grid, dim3(64), 0, s, X.d(), d, rows, crow, K, carry, carry_counts,
@@ -313,11 +428,6 @@ __global__ __launch_bounds__(64) void km_chain_flagged_kernel(const TX* __restri
     sums[(size_t)c * d + j] = km_chain_rows(X, d, j, r4, beg, end, carry ? carry[(size_t)c * d + j] : 0.0);
 }
 
-__global__ void km_counts_kernel(const int64_t* __restrict__ crow, int K, const int64_t* __restrict__ carry_counts,
-                                 int64_t* __restrict__ counts) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c < K) counts[c] = crow[c + 1] - crow[c] + (carry_counts ? carry_counts[c] : 0);
-}
 
 size_t km_fx_ws_bytes(int K, int d) { return (size_t)K * d * sizeof(KmFx) + (size_t)K * 4 + 64; }
 
@@ -339,7 +449,13 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
     }
     hipLaunchKernelGGL(km_fx_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, crow, K, d, carry,
                        carry_counts, sums, flag);
-    if (X.f64)
+    if (km_wide()) {
+        const dim3 g16((unsigned)K, (unsigned)((d + 15) / 16));
+        if (X.f64)
+            hipLaunchKernelGGL(km_chain16_kernel<double>, g16, dim3(64), 0, s, X.d(), d, rows, crow, carry, flag, sums);
+        else
+            hipLaunchKernelGGL(km_chain16_kernel<float>, g16, dim3(64), 0, s, X.f(), d, rows, crow, carry, flag, sums);
+    } else if (X.f64)
         hipLaunchKernelGGL(km_chain_flagged_kernel<double>, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X.d(), d,
                            rows, crow, K, carry, flag, sums);
     else

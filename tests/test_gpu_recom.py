@@ -38,14 +38,15 @@ def test_recommend_golden(ctx, name):
                                  g["cand_ptr"], g["cand_idx"], m["P"], m["NTOP"])
     assert np.array_equal(cnt, g["pc_cnt"])
     has = cnt > 0                     # main.cpp:161 skips users without neighbours
-    if m["values"] == "dyadic":       # squares exact: pow(x, 2) == x * x, bit-exact everywhere
-        assert np.array_equal(idx, g["pc_idx"])
-        assert np.array_equal(sim.view(np.uint64), g["pc_sim"].view(np.uint64))
-        assert np.array_equal(top[has], g["top"][has])
-    else:                             # general doubles: glibc pow(x, 2) may differ from x * x by an ulp
-        assert np.allclose(sim, g["pc_sim"], rtol=1e-13, atol=1e-15, equal_nan=True)
-        agree = (idx == g["pc_idx"]).all(axis=1) & (top == g["top"]).all(axis=1)
-        assert agree[has].mean() >= 0.95, agree[has].mean()
+    # bit-exact in both value kinds: on the general-double case glibc's pow(x, 2)
+    # rounds like x * x for every value in the fixture (the oracle reproduces it
+    # bit for bit, tests/test_oracle_golden.py::test_recommend_step); where the two
+    # could differ by an ulp in general is DESIGN.md §5's caveat, not this input
+    agree = (idx == g["pc_idx"]).all(axis=1) & (top == g["top"]).all(axis=1)
+    print(f"{name} ({m['values']}): users agreeing {agree[has].mean():.4f} of {int(has.sum())}")
+    assert np.array_equal(idx, g["pc_idx"])
+    assert np.array_equal(sim.view(np.uint64), g["pc_sim"].view(np.uint64))
+    assert np.array_equal(top[has], g["top"][has])
 
 
 @pytest.mark.parametrize("N,d,nq,P,NT,levels,seed", [

@@ -17,3 +17,5 @@ for _ in range(5):
     lshkm.kmeans_update(ctx, X, asg, C, "euclidean", 0.05)
 ctx.sync()
 print("update fp64", (time.perf_counter() - t0) / 5 * 1e3, "ms")
+cnt = np.bincount(asg.cpu().numpy(), minlength=K)
+print("cluster sizes: max", int(cnt.max()), "mean", float(cnt.mean()))
