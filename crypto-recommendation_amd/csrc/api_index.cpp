@@ -74,6 +74,16 @@ int d2h(lshkm_ctx ctx, void* dst, const void* src, size_t bytes) {
 int build_csr(lshkm_ctx ctx, const int32_t* keys, int64_t kstride, int64_t N, int64_t nb, int32_t* idx,
               int64_t* row_ptr, int T = 1) {
     int rc;
+    // one-pass form for key ranges that fit an LDS counter image (LSHKM_CSR=onepass; being measured)
+    const char* cv = getenv("LSHKM_CSR");
+    if (nb <= 32768 && (cv && !strcmp(cv, "onepass"))) {
+        if ((rc = reserve(ctx, WS_SORT, csr1_scratch_bytes(N, nb, T)))) return rc;
+        if ((rc = csr_build_onepass(ctx->stream, keys, kstride, 1, T, N, nb, idx, row_ptr, ctx->ws[WS_SORT].p))) {
+            LSHKM_LAUNCH_CHECK();
+            return rc;
+        }
+        return 0;
+    }
     if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(N, nb, T))) || (rc = reserve(ctx, WS_SKEYS, (size_t)N * T * 4)))
         return rc;
     if (N > 0 && (rc = stable_sort_by_key_batched(ctx->stream, keys, kstride, 1, nullptr, 0, T, N, nb,

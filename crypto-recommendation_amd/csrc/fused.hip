@@ -1094,7 +1094,11 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 // the centroids in LDS: up to 512 centroids per pass (K = 1024: 2 passes).
 constexpr int FH_KMAX = 512;
 // fused16.hip: the single-pass FAST form over 16-row tiles
-int launch_fused16(const FusedArgs& a, bool hash, int nblk, hipStream_t s);
+int launch_fused16(const FusedArgs& a, bool hash, bool mp, int nblk, hipStream_t s);
+static bool fused16_on() {
+    const char* v = getenv("LSHKM_F16");
+    return v && !strcmp(v, "1");
+}
 int fused16_waves();
 __host__ __device__ constexpr int fh_lds_bytes(int Kpad, bool hash) {
     return 16 + Kpad * FU_RS * 2 + Kpad * 4 + (hash ? 2 * 32 * FU_RS * 2 + FP_HC_BYTES : 0);
@@ -2500,9 +2504,8 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                         const size_t lg = (size_t)fh_gath_off(a.Kpad, hash) + 8 * FH_GATH_WAVE;
                         // the certified f32 winner distance (a.fast_dist) compiled in:
                         // the 16-row form (fused16.hip) with LSHKM_F16=1 (being measured)
-                        const char* f16v = getenv("LSHKM_F16");
-                        if (a.fast_dist && (f16v && !strcmp(f16v, "1")) && a.Kpad % 16 == 0) {
-                            if (launch_fused16(a, hash, nblk, s)) {
+                        if (a.fast_dist && fused16_on() && a.Kpad % 16 == 0) {
+                            if (launch_fused16(a, hash, false, nblk, s)) {
                                 set_error("launch_fused: 16-row form launch");
                                 return -1;
                             }
@@ -2518,6 +2521,12 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                         FH_LAUNCH(true, false, 0);
                     } else {
                         FH_LAUNCH(false, false, 0);
+                    }
+                } else if (a.fast_dist && fused16_on()) {
+                    // the 16-row form for every slice (its own pass state layout)
+                    if (launch_fused16(a, hash && p == 0, true, nblk, s)) {
+                        set_error("launch_fused: 16-row form launch");
+                        return -1;
                     }
                 } else {
                     if (hash && p == 0) FH_LAUNCH(true, true, 0);

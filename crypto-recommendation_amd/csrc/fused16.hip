@@ -92,7 +92,11 @@ __device__ inline float vmax3_16(float a, float b, float c) {
     return r;
 }
 
-template <bool HASH>
+// MP (K > 512): one launch per 512-centroid slice a.Ch / a.cnh (slice offset
+// 32 a.t0); hashing rides on the first, the certificate and the outputs on the
+// last; between launches each row's merged (best, runner-up, index) crosses in
+// a.part[row] (16 B).
+template <bool HASH, bool MP>
 __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a) {
     constexpr int NT = 64 * F16_WAVES;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -163,6 +167,8 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
     int32_t* ambig_seg = a.ambig + (int64_t)blockIdx.x * a.seg_rows;
     unsigned long long* hfix_seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
     const int64_t tstride = (int64_t)gridDim.x * F16_WAVES;
+    const bool first = !MP || a.pass_first != 0, last = !MP || a.pass_last != 0;
+    const int c0 = MP ? 32 * a.t0 : 0;
 
     for (int64_t tile = (int64_t)blockIdx.x * F16_WAVES + wave; tile < ntiles; tile += tstride) {
         const int64_t row = tile * 16 + p;
@@ -327,7 +333,7 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
             t1 = m1 != m1p ? t : t1;
         }
         // best and runner-up over the row's 4 lane groups (lowest index on ties)
-        int i1 = t1 * 16 + 4 * g + (int)(__float_as_uint(m1) & 3u);
+        int i1 = c0 + t1 * 16 + 4 * g + (int)(__float_as_uint(m1) & 3u);
         {
             const float om1 = __uint_as_float(x16_u(__float_as_uint(m1), g));
             const float om2 = __uint_as_float(x16_u(__float_as_uint(m2), g));
@@ -343,6 +349,18 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
             m2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
             i1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
             m1 = fmaxf(m1, om1);
+        }
+        if (MP && !first) {      // the earlier slices' state (lower indices: it wins ties)
+            const float4 st = reinterpret_cast<const float4*>(a.part)[valid ? row : a.N - 1];
+            const float om1 = st.x, om2 = st.y;
+            const int oi1 = __float_as_int(st.z);
+            m2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
+            i1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
+            m1 = fmaxf(m1, om1);
+        }
+        if (MP && !last) {
+            if (g == 0 && valid) reinterpret_cast<float4*>(a.part)[row] = make_float4(m1, m2, __int_as_float(i1), 0.f);
+            continue;
         }
         const bool cert = x_ok && c_ok && ((double)m2 < (double)m1 - 2.0 * E);
 
@@ -380,7 +398,7 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
         }
     }
     __syncthreads();
-    if (tid < 2 && (tid == 0 || HASH)) {
+    if (tid < 2 && (tid == 0 ? last : HASH)) {
         const int c = lcount[tid];
         a.seg_counts[2 * blockIdx.x + tid] = c;
         if (c) atomicAdd(tid == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
@@ -389,12 +407,22 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
 
 int fused16_waves() { return F16_WAVES; }
 
-// One launch over all rows (Kpad <= 512, euclidean, fp32 rows of 128 dims).
-int launch_fused16(const FusedArgs& a, bool hash, int nblk, hipStream_t s) {
-    if (a.Kpad > 512 || (a.Kpad & 15) || !a.C32 || !a.rn32 || (hash && (a.k != 4 || a.LK > 32))) return -1;
+// One launch over all rows for a slice of Kpad <= 512 centroids (euclidean,
+// fp32 rows of 128 dims); mp: one of several slices (a.t0, a.pass_first,
+// a.pass_last, a.part set by the caller; hash only with the first).
+int launch_fused16(const FusedArgs& a, bool hash, bool mp, int nblk, hipStream_t s) {
+    if (a.Kpad > 512 || (a.Kpad & 15) || !a.C32 || !a.rn32 || (hash && (a.k != 4 || a.LK > 32)) ||
+        (mp && (!a.part || (hash && !a.pass_first))))
+        return -1;
     const size_t lds = (size_t)f16_lds_bytes(a.Kpad, hash);
-    if (hash) hipLaunchKernelGGL(fused16_kernel<true>, dim3((unsigned)nblk), dim3(64 * F16_WAVES), lds, s, a);
-    else hipLaunchKernelGGL(fused16_kernel<false>, dim3((unsigned)nblk), dim3(64 * F16_WAVES), lds, s, a);
+    const dim3 grid((unsigned)nblk), block(64 * F16_WAVES);
+    if (mp) {
+        if (hash) hipLaunchKernelGGL((fused16_kernel<true, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((fused16_kernel<false, true>), grid, block, lds, s, a);
+    } else {
+        if (hash) hipLaunchKernelGGL((fused16_kernel<true, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((fused16_kernel<false, false>), grid, block, lds, s, a);
+    }
     return 0;
 }
 

@@ -120,6 +120,11 @@ int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, in
 int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
                        int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch);
 int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr, int T = 1);
+// One-pass stable CSR (nb <= 32768): T tables' keys at keys + t * k_ts (stride
+// kstride); idx [T][N] row ids in bucket order, row_ptr [T][nb + 1].
+size_t csr1_scratch_bytes(int64_t N, int64_t nb, int T);
+int csr_build_onepass(hipStream_t s, const int32_t* keys, int64_t kstride, int64_t k_ts, int T, int64_t N, int64_t nb,
+                      int32_t* idx, int64_t* row_ptr, void* scratch);
 // T independent stable sorts in one set of launches (table t: keys + t * key_ts,
 // vals + t * val_ts; outputs at + t * N).
 int stable_sort_by_key_batched(hipStream_t s, const int32_t* keys, int64_t kstride, int64_t key_ts, const int32_t* vals,
