@@ -365,6 +365,7 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
     mfma_ok = d == 128 && LK <= 32;
     std::vector<_Float16> vh, vl;
     std::vector<double> v1;
+    std::vector<float> v32;
     if (mfma_ok) {
         vh.assign(64 * 128, (_Float16)0.f);
         vl.assign(64 * 128, (_Float16)0.f);
@@ -385,6 +386,13 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
         LSHKM_HIP(hipMemcpyAsync(vh_d.p, vh.data(), vh.size() * 2, hipMemcpyHostToDevice, s));
         LSHKM_HIP(hipMemcpyAsync(vl_d.p, vl.data(), vl.size() * 2, hipMemcpyHostToDevice, s));
         LSHKM_HIP(hipMemcpyAsync(v1_d.p, v1.data(), LK * 8, hipMemcpyHostToDevice, s));
+        if (metric == LSHKM_METRIC_EUCLIDEAN) {
+            v32.assign(32 * 128, 0.f);
+            for (int f = 0; f < LK; f++)
+                for (int j = 0; j < 128; j++) v32[f * 128 + j] = V[(size_t)f * d + j];
+            if ((rc = v32_d.reserve(v32.size() * 4))) return rc;
+            LSHKM_HIP(hipMemcpyAsync(v32_d.p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice, s));
+        }
     }
     LSHKM_HIP(hipStreamSynchronize(s));   // host vectors go out of scope
     // host copies kept for introspection
@@ -637,6 +645,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if (fuse_hash) {
             const ProjTable& pj = lsh->proj;
             f.Vh = pj.vh_d.as<_Float16>(); f.Vl = pj.vl_d.as<_Float16>(); f.PT = pj.PT_d.as<double>();
+            f.V32 = pj.v32_d.as<float>();
             f.tv = pj.t_d.as<float>(); f.pnorm = pj.pn_d.as<double>(); f.v1 = pj.v1_d.as<double>();
             f.rv = pj.r_d.as<int32_t>(); f.w = pj.w; f.L = pj.L; f.k = pj.k; f.LK = pj.LK; f.LKpad = pj.LKpad;
             f.nb = lsh->nb; f.phi = phi; f.bucket = bucket;

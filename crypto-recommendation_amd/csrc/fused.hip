@@ -2326,7 +2326,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     FusedArgs a;
     a.X = f.X; a.N = f.N;
     a.Ch = f.Ch; a.Cl = f.Cl; a.cnh = f.cnh; a.cbound = f.cbound; a.C64 = f.C64; a.Kpad = f.Kpad;
-    a.Vh = f.Vh; a.Vl = f.Vl; a.PT = f.PT; a.tv = f.tv; a.pnorm = f.pnorm; a.v1 = f.v1; a.rv = f.rv;
+    a.Vh = f.Vh; a.Vl = f.Vl; a.V32 = f.V32; a.PT = f.PT; a.tv = f.tv; a.pnorm = f.pnorm; a.v1 = f.v1; a.rv = f.rv;
     a.w = f.w; a.L = f.L; a.k = f.k; a.LK = f.LK; a.LKpad = f.LKpad; a.nb = f.nb;
     a.tuples = f.tuples; a.phi = f.phi; a.bucket = f.bucket; a.assign = f.assign; a.dist = f.dist;
     a.ambig = f.ambig; a.ambig_count = f.ambig_count; a.stats = f.stats;

@@ -52,6 +52,9 @@ constexpr int F16_WAVES = F16_WAVES_SET;
 #ifndef F16_FLOOR_SB
 #define F16_FLOOR_SB 1
 #endif
+#ifndef F16_H64
+#define F16_H64 0       // the f32 hash window's rejects refined in fp64 inside the pass
+#endif
 #ifndef F16_HASH_SB
 #define F16_HASH_SB 1
 #endif
@@ -85,6 +88,17 @@ __device__ inline uint32_t or4g(uint32_t v) {
     const uint32_t s = a[0] | a[1];
     const auto b = __builtin_amdgcn_permlane32_swap(s, s, false, false);
     return b[0] | b[1];
+}
+// fp64 sum over the row's 4 lane groups (the same value in all 4 lanes)
+__device__ inline double sum4g_d(double v, int g) {
+    const uint64_t u = __double_as_longlong(v);
+    const double o1 = __longlong_as_double((long long)(((uint64_t)x16_u((uint32_t)(u >> 32), g) << 32) |
+                                                       x16_u((uint32_t)u, g)));
+    const double s = v + o1;
+    const uint64_t w = __double_as_longlong(s);
+    const double o2 = __longlong_as_double((long long)(((uint64_t)x32_u((uint32_t)(w >> 32), g) << 32) |
+                                                       x32_u((uint32_t)w, g)));
+    return s + o2;
 }
 __device__ inline float vmax3_16(float a, float b, float c) {
     float r;
@@ -251,17 +265,18 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
 #pragma unroll
             for (int b = 0; b < 2; b++) {
                 const int l = 4 * b + g;
-                if (l >= a.L || !valid) continue;
+                const bool on = l < a.L && valid;
+                const int lc = on ? l : 0;
                 const floatx4 hv4 = b ? hs1 : hs0;
-                const float4 tq = *reinterpret_cast<const float4*>(lt0 + 4 * l);
-                const float4 pq = *reinterpret_cast<const float4*>(lpn0 + 4 * l);
-                const float4 qq = *reinterpret_cast<const float4*>(lv10 + 4 * l);
-                const int4 rq = *reinterpret_cast<const int4*>(lr0 + 4 * l);
+                const float4 tq = *reinterpret_cast<const float4*>(lt0 + 4 * lc);
+                const float4 pq = *reinterpret_cast<const float4*>(lpn0 + 4 * lc);
+                const float4 qq = *reinterpret_cast<const float4*>(lv10 + 4 * lc);
+                const int4 rq = *reinterpret_cast<const int4*>(lr0 + 4 * lc);
                 const float tv[4] = {tq.x, tq.y, tq.z, tq.w}, pv[4] = {pq.x, pq.y, pq.z, pq.w};
                 const float qv[4] = {qq.x, qq.y, qq.z, qq.w};
                 const int32_t rv[4] = {rq.x, rq.y, rq.z, rq.w};
                 int32_t hv[4];
-                uint32_t hn = 0;
+                uint32_t fl = 0;                      // this table's uncertified functions
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const float u = hv4[q] + tv[q];
@@ -269,14 +284,55 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
                     const float B = fmaf(fabsf(y), G, fmaf(nxf, pv[q], qv[q]));
                     const float lo = floorf(y - B), hi = floorf(y + B);
                     hv[q] = (int32_t)lo;
-                    if (lo != hi) fmask |= 1u << (4 * l + q);
-                    hn += phi_term_small(hv[q], rv[q]);
+                    if (lo != hi) fl |= 1u << q;
                 }
-                const int64_t o = row * a.L + l;
-                if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
-                const uint32_t ph = phi_final(hn);
-                if (a.phi) a.phi[o] = (int32_t)ph;
-                if (a.bucket) a.bucket[o] = bucket_fast(ph, a.bdiv);
+                if (!on) fl = 0;
+#if F16_H64
+                // the f32 window's rejects redone in fp64 inside the pass (fix_row's
+                // bound, hash_fixup_kernel): the row's 4 lanes form v_f . x over
+                // their 32 dims (exact f32 products, 4 fp64 chains of 32 fma and
+                // two adds), so only floors within ~2^-44 of an integer are listed
+                uint32_t rm = x_ok ? or4g(fl << (4 * g)) : 0u;   // the same in the row's 4 lanes
+                while (rm) {
+                    const int fi = __builtin_ctz(rm);
+                    rm &= rm - 1;
+                    const int f = 16 * b + fi;
+                    const float* vr = a.V32 + f * FU_D + 8 * g;
+                    double acc = 0.0;
+#pragma unroll
+                    for (int s = 0; s < 4; s++) {
+                        const float4 v0 = *reinterpret_cast<const float4*>(vr + 32 * s);
+                        const float4 v1 = *reinterpret_cast<const float4*>(vr + 32 * s + 4);
+                        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                        for (int j = 0; j < 8; j++) acc = fma((double)vv[j], (double)xf[8 * s + j], acc);
+                    }
+                    acc = sum4g_d(acc, g);
+                    const double P = a.pnorm[f] * nx * (1.0 + 0x1p-40);
+                    const double tt = (double)a.tv[f], iwd = 1.0 / (double)a.w;
+                    const double y = (acc + tt) * iwd;
+                    const double B = ((double)(FU_D + 2) * 0x1p-52 * (P + fabs(tt))) * (iwd * (1.0 + 0x1p-50)) +
+                                     fabs(y) * 0x1p-50;
+                    const double lo = floor(y - B), hi = floor(y + B);
+                    if (lo == hi && (fi >> 2) == g) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++)
+                            if (q == (fi & 3)) hv[q] = (int32_t)lo;
+                        fl &= ~(1u << (fi & 3));
+                    }
+                }
+#endif
+                fmask |= fl << (4 * l);
+                if (on) {
+                    uint32_t hn = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) hn += phi_term_small(hv[q], rv[q]);
+                    const int64_t o = row * a.L + l;
+                    if (a.tuples) *reinterpret_cast<int4*>(a.tuples + o * 4) = make_int4(hv[0], hv[1], hv[2], hv[3]);
+                    const uint32_t ph = phi_final(hn);
+                    if (a.phi) a.phi[o] = (int32_t)ph;
+                    if (a.bucket) a.bucket[o] = bucket_fast(ph, a.bdiv);
+                }
 #if F16_FLOOR_SB
                 __builtin_amdgcn_sched_barrier(0);    // one table's constants live at a time
 #endif
@@ -411,7 +467,7 @@ int fused16_waves() { return F16_WAVES; }
 // fp32 rows of 128 dims); mp: one of several slices (a.t0, a.pass_first,
 // a.pass_last, a.part set by the caller; hash only with the first).
 int launch_fused16(const FusedArgs& a, bool hash, bool mp, int nblk, hipStream_t s) {
-    if (a.Kpad > 512 || (a.Kpad & 15) || !a.C32 || !a.rn32 || (hash && (a.k != 4 || a.LK > 32)) ||
+    if (a.Kpad > 512 || (a.Kpad & 15) || !a.C32 || !a.rn32 || (hash && (a.k != 4 || a.LK > 32 || (F16_H64 && !a.V32))) ||
         (mp && (!a.part || (hash && !a.pass_first))))
         return -1;
     const size_t lds = (size_t)f16_lds_bytes(a.Kpad, hash);

@@ -23,6 +23,7 @@ struct FusedArgs {
     // hash family (HASH only)
     const _Float16* Vh;      // [32][128] f16 hi of the projections (rows >= LK zero)
     const _Float16* Vl;
+    const float* V32;        // [32][128] f32 projections, euclidean (rows >= LK zero)
     const double* PT;        // [128][LKpad] fp64 projections (exact paths)
     const float* tv;         // [LK]
     const double* pnorm;     // [LK] ||v||_2 (rounded up)

@@ -32,6 +32,7 @@ struct ProjTable {
     bool fused_ok = false;
     bool mfma_ok = false;        // split image present (either metric): hash_mfma.hip
     Buf vh_d, vl_d, v1_d;
+    Buf v32_d;     // euclidean: [32][128] f32 projections (rows >= LK zero), the fused in-pass fp64 refinement
     std::vector<float> hV;
     int upload(hipStream_t s, int metric, int d, int L, int k, float w, const float* V, const float* t,
                const int32_t* r, const double* R);

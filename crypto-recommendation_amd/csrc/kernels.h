@@ -225,6 +225,7 @@ struct FusedLaunch {
     int Kpad = 0;
     const _Float16* Vh = nullptr;
     const _Float16* Vl = nullptr;
+    const float* V32 = nullptr;     // euclidean: [32][128] f32 projections (16-row form's in-pass refinement)
     const double* PT = nullptr;
     const float* tv = nullptr;
     const double* pnorm = nullptr;

@@ -13,6 +13,6 @@ for rep in 1 2; do
     if [ "$v" = base ]; then lib=crypto-recommendation_amd/liblshkm.so; else lib=crypto-recommendation_amd/liblshkm_$v.so; fi
     tagf=$(echo "$vv" | tr '@=' '__')
     env LSHKM_LIB=$PWD/$lib $ev timeout -k 10 120 python tools/time_fused.py > "$OUT/$tagf.$rep.txt" 2>&1 || { tail -3 "$OUT/$tagf.$rep.txt"; exit 1; }
-    echo "$vv: $(tail -1 "$OUT/$tagf.$rep.txt" | cut -d: -f2 | cut -c1-60)"
+    echo "$vv: $(tail -1 "$OUT/$tagf.$rep.txt" | cut -d: -f2- | cut -c1-150)"
   done
 done
