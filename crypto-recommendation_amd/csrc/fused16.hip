@@ -44,7 +44,10 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int F16_WAVES = F16_WAVES_SET;
 #ifndef F16_TU
-#define F16_TU 1        // centroid tiles per loop iteration
+#define F16_TU 1        // centroid tiles per loop iteration (run-time tile count)
+#endif
+#ifndef F16_FIXNT
+#define F16_FIXNT 1     // K = 256 / 512-centroid slices: the tile count compiled in
 #endif
 #ifndef F16_APF
 #define F16_APF 0       // A-operand reads one tile ahead
@@ -110,7 +113,9 @@ __device__ inline float vmax3_16(float a, float b, float c) {
 // 32 a.t0); hashing rides on the first, the certificate and the outputs on the
 // last; between launches each row's merged (best, runner-up, index) crosses in
 // a.part[row] (16 B).
-template <bool HASH, bool MP>
+// NTL: centroid tiles compiled in (16: K = 256, 32: a 512-centroid slice; the
+// LDS offsets of the unrolled tile loop become immediates), 0: Kpad / 16 at run time
+template <bool HASH, bool MP, int NTL>
 __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a) {
     constexpr int NT = 64 * F16_WAVES;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -171,7 +176,7 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
     const int p = lane & 15, g = lane >> 4;
     const float cmaxf = a.cbound[3], crf = a.cbound[4], chf = a.cbound[5], cnf = a.cbound[6];
     const bool c_ok = __float_as_uint(a.cbound[2]) == 0u;
-    const int ntl = Kpad >> 4;
+    const int ntl = NTL ? NTL : Kpad >> 4;
     const int64_t ntiles = (a.N + 15) >> 4;
     const double Ec = (0x1p-24 + F16_FH_A) * (double)cnf + 0x1p-41 * (double)cmaxf * (double)cmaxf + 0x1p-18 * (double)cnf;
     // this lane's A-operand offsets (row p of a 16-row block, chunk 4s + g)
@@ -362,8 +367,9 @@ __global__ __launch_bounds__(64 * F16_WAVES, 1) void fused16_kernel(FusedArgs a)
 #pragma unroll
         for (int s = 0; s < 4; s++) ab[s] = *reinterpret_cast<const half8*>(lch + ao[s]);
 #endif
-#pragma unroll F16_TU
-        for (int t = 0; t < ntl; t++) {
+        constexpr int UNR = NTL ? NTL : F16_TU;
+#pragma unroll UNR
+        for (int t = 0; t < (NTL ? NTL : ntl); t++) {
             const float m1p = m1;
             floatx4 acc = *reinterpret_cast<const floatx4*>(lcn + 16 * t + 4 * g);
 #if F16_APF
@@ -472,13 +478,22 @@ int launch_fused16(const FusedArgs& a, bool hash, bool mp, int nblk, hipStream_t
         return -1;
     const size_t lds = (size_t)f16_lds_bytes(a.Kpad, hash);
     const dim3 grid((unsigned)nblk), block(64 * F16_WAVES);
+#define F16_LAUNCH(H, M, T) hipLaunchKernelGGL((fused16_kernel<H, M, T>), grid, block, lds, s, a)
+#define F16_BY_NT(H, M)                                      \
+    do {                                                     \
+        if (F16_FIXNT && a.Kpad == 256) F16_LAUNCH(H, M, 16); \
+        else if (F16_FIXNT && a.Kpad == 512) F16_LAUNCH(H, M, 32); \
+        else F16_LAUNCH(H, M, 0);                            \
+    } while (0)
     if (mp) {
-        if (hash) hipLaunchKernelGGL((fused16_kernel<true, true>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((fused16_kernel<false, true>), grid, block, lds, s, a);
+        if (hash) F16_BY_NT(true, true);
+        else F16_BY_NT(false, true);
     } else {
-        if (hash) hipLaunchKernelGGL((fused16_kernel<true, false>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((fused16_kernel<false, false>), grid, block, lds, s, a);
+        if (hash) F16_BY_NT(true, false);
+        else F16_BY_NT(false, false);
     }
+#undef F16_BY_NT
+#undef F16_LAUNCH
     return 0;
 }
 

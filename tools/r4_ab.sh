@@ -19,5 +19,5 @@ LSHKM_CSR=onepass LSHKM_KM_CHAIN=16 timeout -k 10 300 python tools/bench_rows.py
 cut -c1-220 "$OUT/rows.jsonl"
 LSHKM_CSR=radix timeout -k 10 300 python tools/bench_rows.py --rows lsh,cube --no-cpu > "$OUT/rows_radix.jsonl" 2> "$OUT/rows_radix.err" || { tail -5 "$OUT/rows_radix.err"; exit 1; }
 cut -c1-220 "$OUT/rows_radix.jsonl"
-bash tools/variants.sh "${TAG}_c3" base base@LSHKM_F16=1 h64@LSHKM_F16=1 w12@LSHKM_F16=1 apf16@LSHKM_F16=1 apf12@LSHKM_F16=1 || exit 1
-TF_K=1024 bash tools/variants.sh "${TAG}_c5" base base@LSHKM_F16=1 h64@LSHKM_F16=1 w12@LSHKM_F16=1 apf12@LSHKM_F16=1 || exit 1
+bash tools/variants.sh "${TAG}_c3" base base@LSHKM_F16=1 h64@LSHKM_F16=1 w12@LSHKM_F16=1 nt0@LSHKM_F16=1 || exit 1
+TF_K=1024 bash tools/variants.sh "${TAG}_c5" base base@LSHKM_F16=1 h64@LSHKM_F16=1 w12@LSHKM_F16=1 nt0@LSHKM_F16=1 || exit 1
