@@ -580,6 +580,14 @@ static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign
     // Parallel exact sums (fixed point where the chain provably never rounds);
     // LSHKM_KM_PATH=chain runs every (c, j) chain sequentially.
     const char* kp = getenv("LSHKM_KM_PATH");
+    // fp64 rows: binade segments (LSHKM_KM_PATH=seg; being measured)
+    if (X.f64 && kp && !strcmp(kp, "seg")) {
+        const size_t wsb = km_seg_ws_bytes(N, K, d);
+        if ((rc = ctx->ws_range[11].reserve(wsb))) return rc;
+        if ((rc = launch_km_sums_seg(ctx->stream, X.d(), d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K,
+                                     N, sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        return 0;
+    }
     if (!(kp && !strcmp(kp, "chain"))) {
         if ((rc = ctx->ws_range[11].reserve(km_fx_ws_bytes(K, d)))) return rc;
         if ((rc = launch_km_sums_fx(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, N,

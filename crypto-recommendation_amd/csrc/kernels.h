@@ -164,6 +164,11 @@ int launch_memo_scatter(hipStream_t s, const int32_t* off, const int32_t* bit, i
 int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K,
                     double* sums, int64_t* counts, const double* carry = nullptr,
                     const int64_t* carry_counts = nullptr);
+// fp64 rows: the same sums by binade segments (kmseg.h; ws: km_seg_ws_bytes).
+size_t km_seg_ws_bytes(int64_t M, int K, int d);
+int launch_km_sums_seg(hipStream_t s, const double* X, int d, const int32_t* rows, const int64_t* crow, int K,
+                       int64_t M, double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts,
+                       void* ws);
 // Same sums, parallel: exact int128 fixed-point sums wherever the sequential
 // chain provably never rounds, the sequential chain elsewhere (ws: km_fx_ws_bytes).
 size_t km_fx_ws_bytes(int K, int d);

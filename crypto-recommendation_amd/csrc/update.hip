@@ -17,6 +17,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "exact.h"
+#include "kmseg.h"
 
 namespace lshkm {
 
@@ -465,6 +466,201 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
         hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
                            counts);
     return kstatus("update.hip (fixed point)");
+}
+
+// ------------------------------------------------------------------ segmented form
+// fp64 rows (general doubles: the fixed-point test above fails for almost every
+// chain, and the sequential chain of the largest cluster set the time). Every
+// (c, j) chain is cut into pairs (512-position window x cluster) and each pair
+// into binade segments (kmseg.h), four launches:
+//   A ks_sum: the pair sums (any order; only to predict binades)
+//   B ks_scan: the approximate sum at each pair's start, per chain
+//   C ks_seg: the segment records of every pair (<= KS_R, else the pair is walked)
+//   D ks_compose: one lane per chain applies the records in order (real adds
+//     where a summary does not apply), so the critical path is the number of
+//     segments of the longest chain, not its length.
+// A and C stream the member rows (lane = dimension, 512-B row slices); pair
+// (w, c) has index w + c (windows and clusters advance monotonically together).
+constexpr int KS_U = 16;           // member rows in flight per wave
+
+__device__ inline int ks_first_cluster(const int64_t* __restrict__ crow, int K, int64_t p0) {
+    int lo = 0, hi = K;            // crow[lo] <= p0 < crow[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (crow[mid] <= p0) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Walk window w's positions (lane j); f(p, x) per position, close(c) when
+// cluster c's part of the window ends (only for clusters with positions in it),
+// open(c, p) when it starts.
+template <typename Open, typename Step, typename Close>
+__device__ __attribute__((always_inline)) inline void ks_walk(const double* __restrict__ X, int d, int jl,
+                                                              const int32_t* __restrict__ rows,
+                                                              const int64_t* __restrict__ crow, int K, int64_t M,
+                                                              int64_t p0, Open&& open, Step&& step, Close&& close) {
+    const int64_t p1 = min(M, p0 + KS_W);
+    const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
+    int c = ks_first_cluster(crow, K, p0);
+    int64_t cend = crow[c + 1];
+    open(c, p0);
+    for (int64_t p = p0; p < p1; p += KS_U) {
+        double v[KS_U];
+        if (p + KS_U <= p1) {
+#pragma unroll
+            for (int u = 0; u < KS_U; u++) v[u] = X[(int64_t)r4[p + u] * d + jl];
+        } else {
+#pragma unroll
+            for (int u = 0; u < KS_U; u++) v[u] = X[(int64_t)r4[min(p + u, p1 - 1)] * d + jl];
+        }
+#pragma unroll
+        for (int u = 0; u < KS_U; u++) {
+            if (p + u >= p1) break;
+            if (p + u >= cend) {                     // wave-uniform
+                close(c);
+                do {
+                    c++;
+                    cend = crow[c + 1];
+                } while (p + u >= cend);             // empty clusters have no pair here
+                open(c, p + u);
+            }
+            step(p + u, v[u]);
+        }
+    }
+    close(c);
+}
+
+__global__ __launch_bounds__(64) void ks_sum_kernel(const double* __restrict__ X, int d, const int32_t* __restrict__ rows,
+                                                    const int64_t* __restrict__ crow, int K, int64_t M,
+                                                    double* __restrict__ psum) {
+    const int w = blockIdx.x;
+    const int j = blockIdx.y * 64 + threadIdx.x;
+    const bool on = j < d;
+    double s = 0.0;
+    ks_walk(X, d, on ? j : d - 1, rows, crow, K, M, (int64_t)w * KS_W,
+            [&](int, int64_t) { s = 0.0; },
+            [&](int64_t, double x) { s += x; },
+            [&](int c) { if (on) psum[(size_t)(w + c) * d + j] = s; });
+}
+
+__global__ __launch_bounds__(64) void ks_scan_kernel(const double* __restrict__ psum, const int64_t* __restrict__ crow,
+                                                     int K, int d, const double* __restrict__ carry,
+                                                     double* __restrict__ sin) {
+    const int c = blockIdx.x;
+    const int j = blockIdx.y * 64 + threadIdx.x;
+    const int64_t beg = crow[c], end = crow[c + 1];
+    if (j >= d || beg == end) return;
+    double run = carry ? carry[(size_t)c * d + j] : 0.0;
+    for (int64_t w = beg / KS_W; w <= (end - 1) / KS_W; w++) {
+        const size_t o = (size_t)(w + c) * d + j;
+        sin[o] = run;
+        run += psum[o];
+    }
+}
+
+__global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X, int d, const int32_t* __restrict__ rows,
+                                                    const int64_t* __restrict__ crow, int K, int64_t M,
+                                                    const double* __restrict__ sin, int32_t* __restrict__ cnt,
+                                                    KsRec* __restrict__ rec) {
+    const int w = blockIdx.x;
+    const int j = blockIdx.y * 64 + threadIdx.x;
+    const bool on = j < d;
+    const int64_t p0 = (int64_t)w * KS_W;
+    double st = 0.0;
+    KsSeg g;
+    bool open = false;
+    int nr = 0;
+    KsRec* rp = rec;
+    auto emit = [&](const KsSeg& gg) {
+        if (on && nr < KS_R) rp[nr] = ks_record(gg);
+        nr++;
+    };
+    ks_walk(X, d, on ? j : d - 1, rows, crow, K, M, p0,
+            [&](int c, int64_t) {
+                const size_t o = (size_t)(w + c) * d + j;
+                st = on ? sin[o] : 0.0;
+                open = false;
+                nr = 0;
+                rp = rec + o * KS_R;
+            },
+            [&](int64_t p, double x) {
+                st += x;
+                ks_feed(g, open, x, st, (int)(p - p0), emit);
+            },
+            [&](int c) {
+                if (open) emit(g);
+                if (on) cnt[(size_t)(w + c) * d + j] = nr;
+            });
+}
+
+__global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict__ X, int d,
+                                                        const int32_t* __restrict__ rows,
+                                                        const int64_t* __restrict__ crow, int K,
+                                                        const double* __restrict__ carry,
+                                                        const int32_t* __restrict__ cnt, const KsRec* __restrict__ rec,
+                                                        double* __restrict__ sums) {
+    const int c = blockIdx.x;
+    const int j = blockIdx.y * 64 + threadIdx.x;
+    if (j >= d) return;
+    const int64_t beg = crow[c], end = crow[c + 1];
+    double s = carry ? carry[(size_t)c * d + j] : 0.0;
+    if (beg < end) {
+        for (int64_t w = beg / KS_W; w <= (end - 1) / KS_W; w++) {
+            const size_t o = (size_t)(w + c) * d + j;
+            const int n = cnt[o];
+            const int64_t wb = w * KS_W;
+            if (n > KS_R) {                              // dense pair: the plain chain
+                const int64_t q1 = min(end, wb + KS_W);
+                for (int64_t p = max(beg, wb); p < q1; p++) s = __dadd_rn(s, X[(int64_t)rows[p] * d + j]);
+                continue;
+            }
+            const KsRec* r = rec + o * KS_R;
+            KsRec nx = n > 0 ? r[0] : KsRec{};
+            for (int i = 0; i < n; i++) {
+                const KsRec cur = nx;
+                if (i + 1 < n) nx = r[i + 1];            // the next record in flight
+                if (!ks_apply(s, cur)) {
+                    const int b = ks_rec_b(cur);
+                    for (int q = ks_rec_a(cur) + 1; q <= b; q++) s = __dadd_rn(s, X[(int64_t)rows[wb + q] * d + j]);
+                }
+            }
+        }
+    }
+    sums[(size_t)c * d + j] = s;
+}
+
+static int64_t ks_pairs(int64_t M, int K) { return (M + KS_W - 1) / KS_W + K; }
+
+size_t km_seg_ws_bytes(int64_t M, int K, int d) {
+    const size_t pd = (size_t)ks_pairs(M, K) * d;
+    return pd * (8 + 8 + 4) + 64 + pd * KS_R * sizeof(KsRec);
+}
+
+// Exact-order sums of fp64 rows by segments (sums, counts as launch_km_chain).
+int launch_km_sums_seg(hipStream_t s, const double* X, int d, const int32_t* rows, const int64_t* crow, int K,
+                       int64_t M, double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts,
+                       void* ws) {
+    const size_t pd = (size_t)ks_pairs(M, K) * d;
+    char* b = reinterpret_cast<char*>(ws);
+    KsRec* rec = reinterpret_cast<KsRec*>(b);                 // 16-B aligned first
+    double* psum = reinterpret_cast<double*>(b + pd * KS_R * sizeof(KsRec));
+    double* sin = psum + pd;
+    int32_t* cnt = reinterpret_cast<int32_t*>(sin + pd);
+    const int jb = (d + 63) / 64;
+    const int64_t W = (M + KS_W - 1) / KS_W;
+    if (W > 0) {
+        hipLaunchKernelGGL(ks_sum_kernel, dim3((unsigned)W, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, M, psum);
+        hipLaunchKernelGGL(ks_scan_kernel, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, psum, crow, K, d, carry, sin);
+        hipLaunchKernelGGL(ks_seg_kernel, dim3((unsigned)W, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, M, sin,
+                           cnt, rec);
+    }
+    hipLaunchKernelGGL(ks_compose_kernel, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, carry, cnt,
+                       rec, sums);
+    if (counts)
+        hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
+                           counts);
+    return kstatus("update.hip (segmented)");
 }
 
 // One wave per cluster: divide (unless empty), then the reference's movement

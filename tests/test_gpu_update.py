@@ -93,3 +93,67 @@ def test_parallel_sums_carry_mode(ctx):
         cs, cc = lshkm.kmeans_partial_carry(ctx, X[lo:hi], A[lo:hi], K, cs, cc)
     whole_s, whole_c = lshkm.kmeans_partial_carry(ctx, X, A, K)
     assert np.array_equal(bits(cs), bits(whole_s)) and np.array_equal(cc.cpu().numpy(), whole_c.cpu().numpy())
+
+
+@pytest.mark.parametrize("kind", ["walk", "drift", "ties", "wide", "special", "skewed"])
+@pytest.mark.parametrize("path", ["seg", "fx"])
+def test_f64_segmented_sums_match_chains(ctx, kind, path, monkeypatch):
+    # fp64 rows (the reference's user vectors): the binade-segment form (kmseg.h,
+    # LSHKM_KM_PATH=seg) and the fixed-point + sequential form against the
+    # sequential chains, bit for bit, incl. ties in the grid (dyadic values near
+    # 2^50), inf / nan / overflow, denormals, -0, one huge and one empty cluster
+    rng = np.random.default_rng(23)
+    N, d, K = 120_000, 70, 24
+    if kind == "walk":
+        Xh = rng.standard_normal((N, d))
+    elif kind == "drift":
+        Xh = 0.3 + rng.standard_normal((N, d))
+    elif kind == "ties":
+        Xh = np.ldexp(np.round(rng.standard_normal((N, d)) * 64), -7)
+        Xh[:, 0] += 2.0 ** 44                                               # coarse grid, many exact ties
+        Xh[:, 1] = 2 * rng.integers(0, 8, N) + 1.0
+    elif kind == "wide":
+        Xh = rng.standard_normal((N, d)) * 10.0 ** rng.integers(-200, 200, (N, d))
+    elif kind == "special":
+        Xh = rng.standard_normal((N, d))
+        Xh[::9973, 3] = np.inf
+        Xh[::7919, 5] = np.nan
+        Xh[::101, 7] = 1e-310
+        Xh[::103, 9] = -0.0
+        Xh[::1511, 11] = 1.5e308                                            # chains overflow to inf
+    else:
+        Xh = rng.standard_normal((N, d)) * np.exp(rng.uniform(-3, 3, size=(N, 1)))
+    a = rng.integers(0, K, N).astype(np.int32)
+    if kind in ("skewed", "walk"):
+        a[: N * 3 // 4] = 3                                                 # one huge cluster
+        a[a == 5] = 6                                                       # an empty one
+    X, A = to_dev(ctx, Xh), to_dev(ctx, a)
+    C = to_dev(ctx, rng.standard_normal((K, d)))
+    monkeypatch.setenv("LSHKM_KM_PATH", path)
+    Cn, cnt, _ = lshkm.kmeans_update(ctx, X, A, C, "euclidean", 0.0)
+    monkeypatch.setenv("LSHKM_KM_PATH", "chain")
+    Cs, cs, _ = lshkm.kmeans_update(ctx, X, A, C, "euclidean", 0.0)
+    monkeypatch.delenv("LSHKM_KM_PATH")
+    assert np.array_equal(cnt.cpu().numpy(), cs.cpu().numpy())
+    assert np.array_equal(bits(Cn), bits(Cs))
+    if kind in ("walk", "ties"):
+        Co, _, _ = oracle.kmeans_update(Xh, a, C.cpu().numpy(), "euclidean", 0.0)
+        assert np.array_equal(bits(Cn), Co.view(np.uint64))
+
+
+@pytest.mark.parametrize("path", ["seg", "chain"])
+def test_f64_segmented_carry_mode(ctx, path, monkeypatch):
+    # sharded exact mode on fp64 rows: chains continue shard to shard (the carry
+    # is each segmented chain's start value)
+    rng = np.random.default_rng(4)
+    N, d, K = 150_000, 33, 12
+    Xh = rng.standard_normal((N, d)) + 0.1
+    a = rng.integers(0, K, N).astype(np.int32)
+    X, A = to_dev(ctx, Xh), to_dev(ctx, a)
+    monkeypatch.setenv("LSHKM_KM_PATH", path)
+    cs = cc = None
+    for lo, hi in ((0, 40_000), (40_000, 100_001), (100_001, N)):
+        cs, cc = lshkm.kmeans_partial_carry(ctx, X[lo:hi], A[lo:hi], K, cs, cc)
+    monkeypatch.setenv("LSHKM_KM_PATH", "chain")
+    whole_s, whole_c = lshkm.kmeans_partial_carry(ctx, X, A, K)
+    assert np.array_equal(bits(cs), bits(whole_s)) and np.array_equal(cc.cpu().numpy(), whole_c.cpu().numpy())

@@ -92,6 +92,16 @@ def test_softx87_matches_long_double(tmp_path):
     assert "bad=0" in out.stdout
 
 
+def test_kmseg_matches_chain(tmp_path):
+    # the binade-segment evaluation of the fp64 chain (csrc/kmseg.h) vs the plain chain
+    exe = tmp_path / "kmseg_check"
+    subprocess.run(["g++", "-O1", "-std=c++14", "-o", str(exe), os.path.join(ROOT, "tests", "kmseg_check.cpp")],
+                   check=True)
+    out = subprocess.run([str(exe), "30"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad=0" in out.stdout
+
+
 def test_no_gpu_means_loud_failure():
     import torch
     if torch.cuda.is_available():

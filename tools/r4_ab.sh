@@ -13,6 +13,7 @@ rc=$?; tail -3 "$OUT/tests.log"; [ $rc -eq 0 ] || { grep -E "^E |Error" "$OUT/te
 LSHKM_LIB=$PWD/crypto-recommendation_amd/liblshkm_h64.so LSHKM_F16=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_fast_dist.py \
   tests/test_gpu_hash_assign.py tests/test_gpu_c5.py -k "not full_size" -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/tests_h64.log" 2>&1
 rc=$?; tail -3 "$OUT/tests_h64.log"; [ $rc -eq 0 ] || { grep -E "^E |Error" "$OUT/tests_h64.log" | head -20; exit $rc; }
+LSHKM_KM_PATH=seg timeout -k 10 120 python tools/time_update64.py || exit 1
 LSHKM_KM_CHAIN=16 timeout -k 10 120 python tools/time_update64.py || exit 1
 timeout -k 10 120 python tools/time_update64.py || exit 1
 LSHKM_CSR=onepass LSHKM_KM_CHAIN=16 timeout -k 10 300 python tools/bench_rows.py --rows lsh,cube,update --no-cpu > "$OUT/rows.jsonl" 2> "$OUT/rows.err" || { tail -5 "$OUT/rows.err"; exit 1; }
