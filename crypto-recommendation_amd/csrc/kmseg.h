@@ -3,7 +3,7 @@
 // cust_vector.hpp:177-184) evaluated in segments, bit for bit.
 //
 // While the partial sums stay inside one binade [2^E, 2^(E+1)) of one sign,
-// they are integer multiples S of G = 2^(E-52) with 2^52 < |S| < 2^53, and one
+// they are integer multiples S of G = 2^(E-52) with 2^52 <= |S| < 2^53, and one
 // step is S_i = S_{i-1} + m_i, m_i = x_i / G rounded to the nearest integer
 // (ties to the even S_i) -- an integer that does not depend on S_{i-1} except
 // through its parity at a tie. A segment [a, b] is therefore summarised
@@ -36,15 +36,18 @@ namespace lshkm {
 constexpr int KS_W = 512;          // member positions per window (pair = window x cluster)
 constexpr int KS_R = 32;           // segment records per (pair, dim); more: the pair is walked
 
-// One segment. meta: bits 0-15 dM = M1 - M0 (int16), 16-27 biased exponent
-// (0: a single real add, no summary), bit 28 negative, 32-41 first offset a,
-// 42-51 last offset b (in the window).
+// One segment, as the composition applies it: s = fl(s + xa); the summary
+// holds iff L <= s <= H (a range inside the predicted binade, folding in the
+// prefix checks for every S_a -- the union over both parities); then s += d0
+// or d1 by the parity of S_a (the last significand bit of s). s + d is exact:
+// (S_a + M) G is a double of the same binade. Single-step segments: L = -inf,
+// H = +inf, d = -0.0 (s + -0.0 == s, signed zeros included). meta: bits 0-9
+// first offset a, 10-19 last offset b (in the window).
 struct KsRec {
     double xa;
-    int64_t m0;        // M for an even S_a
-    int64_t lo, hi;    // prefix-sum range over both parities
-    uint64_t meta;
-    uint64_t pad;      // 48 B: three 16-B loads
+    double L, H;
+    double d0, d1;     // M G for an even / odd S_a
+    uint64_t meta;     // 48 B: three 16-B loads
 };
 
 KS_HD uint64_t ks_bits(double v) {
@@ -62,46 +65,46 @@ KS_HD int ks_key(double s) {
     return be | (int)((b >> 63) << 11);
 }
 
+// Integer-valued doubles throughout: m_i and the prefix sums P are exact while
+// |P| < 2^53; a segment whose prefix ever leaves that range has |lo| or |hi|
+// >= 2^52 and can never pass its check, so rounding beyond it is harmless.
 struct KsSeg {
     int key;           // 0: single-step segment
     int a, n;          // first offset, steps after the first
     double xa;
-    int64_t p0, p1, lo, hi;
+    double p0, p1, lo, hi;
 };
 
 KS_HD void ks_open(KsSeg& g, int key, int a, double xa) {
     g.key = key; g.a = a; g.n = 0; g.xa = xa;
-    g.p0 = 0; g.p1 = 0; g.lo = 0; g.hi = 0;
+    g.p0 = 0.0; g.p1 = 0.0; g.lo = 0.0; g.hi = 0.0;
 }
 
+KS_HD bool ks_even(double v) { return v - 2.0 * floor(0.5 * v) == 0.0; }   // v integer-valued, |v| < 2^53
+
 // One step x after the segment's first: false if x / G is not a usable integer
-// candidate (|x / G| >= 2^54, inf / nan) -- the caller then breaks the segment.
+// candidate (|x / G| >= 2^52, inf / nan) -- the caller then breaks the segment.
 KS_HD bool ks_step(KsSeg& g, double x) {
     const int E = (g.key & 2047) - 1023;
     const double y = ldexp(x, 52 - E);                // exact (power-of-two scaling)
     const double a = fabs(y);
-    if (!(a < 0x1p54)) return false;
+    if (!(a < 0x1p52)) return false;
     const double na = floor(a);
     const double fa = a - na;                         // exact: a >= 0
-    const int64_t ni = (int64_t)na;
-    const bool neg = y < 0.0;
-    const int64_t c_lo = neg ? -ni : ni;              // toward zero
-    const int64_t c_hi = neg ? -ni - 1 : ni + 1;      // away from zero
-    int64_t m0, m1;
+    const double c_lo = copysign(na, y);              // toward zero
+    const double c_hi = copysign(na + 1.0, y);        // away from zero
+    double m0, m1;
     if (fa < 0.5) { m0 = c_lo; m1 = c_lo; }
     else if (fa > 0.5) { m0 = c_hi; m1 = c_hi; }
     else {                                            // tie: the candidate giving an even S
-        m0 = ((g.p0 + c_lo) & 1) == 0 ? c_lo : c_hi;          // S_a even
-        m1 = ((g.p1 + 1 + c_lo) & 1) == 0 ? c_lo : c_hi;      // S_a odd
+        m0 = ks_even(g.p0 + c_lo) ? c_lo : c_hi;            // S_a even
+        m1 = ks_even(g.p1 + 1.0 + c_lo) ? c_lo : c_hi;      // S_a odd
     }
     g.p0 += m0;
     g.p1 += m1;
-    const int64_t mn = g.p0 < g.p1 ? g.p0 : g.p1, mx = g.p0 < g.p1 ? g.p1 : g.p0;
-    if (g.n == 0) { g.lo = mn; g.hi = mx; }
-    else {
-        g.lo = mn < g.lo ? mn : g.lo;
-        g.hi = mx > g.hi ? mx : g.hi;
-    }
+    const double mn = fmin(g.p0, g.p1), mx = fmax(g.p0, g.p1);
+    g.lo = g.n ? fmin(g.lo, mn) : mn;
+    g.hi = g.n ? fmax(g.hi, mx) : mx;
     g.n++;
     return true;
 }
@@ -122,19 +125,31 @@ KS_HD void ks_feed(KsSeg& g, bool& open, double x, double st, int o, Emit&& emit
 KS_HD KsRec ks_record(const KsSeg& g) {
     KsRec r;
     r.xa = g.xa;
-    r.m0 = g.p0;
-    r.lo = g.lo;
-    r.hi = g.hi;
-    const int64_t dm = g.p1 - g.p0;                   // |dm| <= number of ties < KS_W
-    const int be = g.n ? (g.key & 2047) : 0;
-    r.pad = 0;
-    r.meta = (uint64_t)(uint16_t)(int16_t)dm | ((uint64_t)be << 16) | ((uint64_t)((g.key >> 11) & 1) << 28) |
-             ((uint64_t)g.a << 32) | ((uint64_t)(g.a + g.n) << 42);
+    r.meta = (uint64_t)g.a | ((uint64_t)(g.a + g.n) << 10);
+    if (g.n == 0) {
+        r.L = -INFINITY; r.H = INFINITY; r.d0 = -0.0; r.d1 = -0.0;
+        return r;
+    }
+    const int E = (g.key & 2047) - 1023;
+    const bool neg = (g.key >> 11) & 1;
+    double Lv, Hv;                                    // bounds on S_a (integers)
+    if (!(fabs(g.lo) < 0x1p52 && fabs(g.hi) < 0x1p52)) { Lv = 1.0; Hv = 0.0; }
+    else if (!neg) {      // 2^52 + 1 <= S_a + P <= 2^53 - 1 for every prefix P
+        Lv = fmax(0x1p52 + 1.0 - g.lo, 0x1p52);
+        Hv = fmin(0x1p53 - 1.0 - g.hi, 0x1p53 - 1.0);
+    } else {              // -2^53 + 1 <= S_a + P <= -2^52 - 1
+        Lv = fmax(-0x1p53 + 1.0 - g.lo, -0x1p53 + 1.0);
+        Hv = fmin(-0x1p52 - 1.0 - g.hi, -0x1p52);
+    }
+    if (Lv > Hv) { r.L = INFINITY; r.H = -INFINITY; }
+    else { r.L = ldexp(Lv, E - 52); r.H = ldexp(Hv, E - 52); }
+    r.d0 = ldexp(g.p0, E - 52);
+    r.d1 = ldexp(g.p1, E - 52);
     return r;
 }
 
-KS_HD int ks_rec_a(const KsRec& r) { return (int)((r.meta >> 32) & 1023u); }
-KS_HD int ks_rec_b(const KsRec& r) { return (int)((r.meta >> 42) & 1023u); }
+KS_HD int ks_rec_a(const KsRec& r) { return (int)(r.meta & 1023u); }
+KS_HD int ks_rec_b(const KsRec& r) { return (int)((r.meta >> 10) & 1023u); }
 
 // Apply a record to the running sum s (the real first add included). false:
 // the summary does not apply -- s holds fl(s_{a-1} + x_a) and the caller adds
@@ -146,19 +161,8 @@ KS_HD int ks_rec_b(const KsRec& r) { return (int)((r.meta >> 42) & 1023u); }
 #endif
 KS_HD bool ks_apply(double& s, const KsRec& r) {
     s = KS_ADD(s, r.xa);
-    const int be = (int)((r.meta >> 16) & 2047u);
-    if (be == 0) return true;                         // single step
-    const uint64_t b = ks_bits(s);
-    const int neg = (int)((r.meta >> 28) & 1u);
-    if ((int)((b >> 52) & 2047u) != be || (int)(b >> 63) != neg) return false;
-    const int E = be - 1023;
-    const int64_t S = (int64_t)ldexp(s, 52 - E);      // exact: |S| in [2^52, 2^53)
-    const int64_t dm = (int64_t)(int16_t)(uint16_t)(r.meta & 0xFFFFu);
-    const int64_t M = (S & 1) ? r.m0 + dm : r.m0;
-    constexpr int64_t B0 = (int64_t)1 << 52, B1 = (int64_t)1 << 53;
-    const bool ok = neg ? (S + r.hi <= -B0 - 1 && S + r.lo >= -B1 + 1) : (S + r.lo >= B0 + 1 && S + r.hi <= B1 - 1);
-    if (!ok) return false;
-    s = ldexp((double)(S + M), E - 52);               // exact: |S + M| < 2^53
+    if (!(s >= r.L && s <= r.H)) return false;        // nan: false
+    s = KS_ADD(s, (ks_bits(s) & 1u) ? r.d1 : r.d0);  // exact
     return true;
 }
 

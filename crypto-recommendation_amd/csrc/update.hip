@@ -190,8 +190,11 @@ __global__ void km_counts_kernel(const int64_t* __restrict__ crow, int K, const 
 }
 
 static bool km_wide() {
-    const char* v = getenv("LSHKM_KM_CHAIN");          // "16": the wide form (being measured)
-    return v && !strcmp(v, "16");
+    // the wide form (16 dims per wave, 4 member rows per load) by default: the
+    // fp64 update of 1M x 100 rows, K = 256, 3.44 -> 2.68 ms; LSHKM_KM_CHAIN=64:
+    // the 64-dim form
+    const char* v = getenv("LSHKM_KM_CHAIN");
+    return !(v && !strcmp(v, "64"));
 }
 
 int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K,
@@ -476,7 +479,7 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
 //   A ks_sum: the pair sums (any order; only to predict binades)
 //   B ks_scan: the approximate sum at each pair's start, per chain
 //   C ks_seg: the segment records of every pair (<= KS_R, else the pair is walked)
-//   D ks_compose: one lane per chain applies the records in order (real adds
+//   D ks_compose: one wave per chain applies the records in order (real adds
 //     where a summary does not apply), so the critical path is the number of
 //     segments of the longest chain, not its length.
 // A and C stream the member rows (lane = dimension, 512-B row slices); pair
@@ -594,40 +597,81 @@ __global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X
             });
 }
 
+// D: one wave per chain. A pair's records (or, for a dense pair / a segment
+// whose summary does not apply, its member values) are loaded by the lanes at
+// once -- lane i holds record i -- and applied in order from the lanes by
+// readlane, so the dependent chain waits on no memory load; the next pair's
+// count and records are in flight meanwhile.
+__device__ inline double ks_rl(double v, int i) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, i);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), i);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ inline int64_t ks_rl(int64_t v, int i) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, i);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), i);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// positions [q0, q1) of the chain's member list added to s in order (<= 512)
+__device__ inline double ks_walk_values(double s, const double* __restrict__ X, int d, int j,
+                                        const int32_t* __restrict__ rows, int64_t q0, int64_t q1) {
+    const int lane = threadIdx.x;
+    for (int64_t q = q0; q < q1; q += 64) {
+        const int m = (int)min<int64_t>(64, q1 - q);
+        const double v = lane < m ? X[(int64_t)rows[q + lane] * d + j] : 0.0;
+        for (int i = 0; i < m; i++) s = __dadd_rn(s, ks_rl(v, i));
+    }
+    return s;
+}
+
 __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict__ X, int d,
                                                         const int32_t* __restrict__ rows,
                                                         const int64_t* __restrict__ crow, int K,
                                                         const double* __restrict__ carry,
                                                         const int32_t* __restrict__ cnt, const KsRec* __restrict__ rec,
                                                         double* __restrict__ sums) {
-    const int c = blockIdx.x;
-    const int j = blockIdx.y * 64 + threadIdx.x;
-    if (j >= d) return;
+    const int j = blockIdx.x, c = blockIdx.y;
+    const int lane = threadIdx.x;
     const int64_t beg = crow[c], end = crow[c + 1];
     double s = carry ? carry[(size_t)c * d + j] : 0.0;
     if (beg < end) {
-        for (int64_t w = beg / KS_W; w <= (end - 1) / KS_W; w++) {
+        const int64_t w0 = beg / KS_W, w1 = (end - 1) / KS_W;
+        auto load = [&](int64_t w, int& n, KsRec& r) {
             const size_t o = (size_t)(w + c) * d + j;
-            const int n = cnt[o];
+            n = cnt[o];
+            if (lane < n && n <= KS_R) r = rec[o * KS_R + lane];
+        };
+        int n_nx = 0;
+        KsRec r_nx = {};
+        load(w0, n_nx, r_nx);
+        for (int64_t w = w0; w <= w1; w++) {
+            const int n = n_nx;
+            const KsRec r = r_nx;
+            if (w < w1) load(w + 1, n_nx, r_nx);
             const int64_t wb = w * KS_W;
             if (n > KS_R) {                              // dense pair: the plain chain
-                const int64_t q1 = min(end, wb + KS_W);
-                for (int64_t p = max(beg, wb); p < q1; p++) s = __dadd_rn(s, X[(int64_t)rows[p] * d + j]);
+                s = ks_walk_values(s, X, d, j, rows, max(beg, wb), min(end, wb + KS_W));
                 continue;
             }
-            const KsRec* r = rec + o * KS_R;
-            KsRec nx = n > 0 ? r[0] : KsRec{};
+#pragma unroll 2
             for (int i = 0; i < n; i++) {
-                const KsRec cur = nx;
-                if (i + 1 < n) nx = r[i + 1];            // the next record in flight
-                if (!ks_apply(s, cur)) {
-                    const int b = ks_rec_b(cur);
-                    for (int q = ks_rec_a(cur) + 1; q <= b; q++) s = __dadd_rn(s, X[(int64_t)rows[wb + q] * d + j]);
+                KsRec ri;
+                ri.xa = ks_rl(r.xa, i);
+                ri.L = ks_rl(r.L, i);
+                ri.H = ks_rl(r.H, i);
+                ri.d0 = ks_rl(r.d0, i);
+                ri.d1 = ks_rl(r.d1, i);
+                ri.meta = (uint64_t)ks_rl((int64_t)r.meta, i);
+                if (!ks_apply(s, ri)) {
+                    const int a = ks_rec_a(ri), b = ks_rec_b(ri);
+                    s = ks_walk_values(s, X, d, j, rows, wb + a + 1, wb + b + 1);
                 }
             }
         }
     }
-    sums[(size_t)c * d + j] = s;
+    if (lane == 0) sums[(size_t)c * d + j] = s;
 }
 
 static int64_t ks_pairs(int64_t M, int K) { return (M + KS_W - 1) / KS_W + K; }
@@ -655,7 +699,7 @@ int launch_km_sums_seg(hipStream_t s, const double* X, int d, const int32_t* row
         hipLaunchKernelGGL(ks_seg_kernel, dim3((unsigned)W, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, M, sin,
                            cnt, rec);
     }
-    hipLaunchKernelGGL(ks_compose_kernel, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, carry, cnt,
+    hipLaunchKernelGGL(ks_compose_kernel, dim3((unsigned)d, (unsigned)K), dim3(64), 0, s, X, d, rows, crow, K, carry, cnt,
                        rec, sums);
     if (counts)
         hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
