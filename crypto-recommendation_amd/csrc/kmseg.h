@@ -68,45 +68,53 @@ KS_HD int ks_key(double s) {
 // Integer-valued doubles throughout: m_i and the prefix sums P are exact while
 // |P| < 2^53; a segment whose prefix ever leaves that range has |lo| or |hi|
 // >= 2^52 and can never pass its check, so rounding beyond it is harmless.
+// par0 / par1: the parity of S_{i-1} in the even / odd S_a scenario.
 struct KsSeg {
     int key;           // 0: single-step segment
     int a, n;          // first offset, steps after the first
+    int par0, par1;
     double xa;
     double p0, p1, lo, hi;
 };
 
 KS_HD void ks_open(KsSeg& g, int key, int a, double xa) {
     g.key = key; g.a = a; g.n = 0; g.xa = xa;
-    g.p0 = 0.0; g.p1 = 0.0; g.lo = 0.0; g.hi = 0.0;
+    g.par0 = 0; g.par1 = 1;
+    g.p0 = 0.0; g.p1 = 0.0; g.lo = INFINITY; g.hi = -INFINITY;
 }
 
-KS_HD bool ks_even(double v) { return v - 2.0 * floor(0.5 * v) == 0.0; }   // v integer-valued, |v| < 2^53
-
-// One step x after the segment's first: false if x / G is not a usable integer
-// candidate (|x / G| >= 2^52, inf / nan) -- the caller then breaks the segment.
-KS_HD bool ks_step(KsSeg& g, double x) {
-    const int E = (g.key & 2047) - 1023;
+// The step's integer m, branch-free: r = x / G rounded to nearest-even by the
+// 1.5 * 2^52 shifter (its last significand bit is r's parity); at a tie
+// (|x / G - r| = 1/2) the reference rounds to the even S_i, so the scenario
+// whose S_{i-1} is odd takes the other candidate 2 x / G - r. After a tie S_i
+// is even in both scenarios.
+struct KsStep {
+    double r, alt;
+    bool tie, ok;
+    int pr;
+};
+KS_HD KsStep ks_step_m(double x, int key) {
+    KsStep t;
+    const int E = (key & 2047) - 1023;
     const double y = ldexp(x, 52 - E);                // exact (power-of-two scaling)
-    const double a = fabs(y);
-    if (!(a < 0x1p52)) return false;
-    const double na = floor(a);
-    const double fa = a - na;                         // exact: a >= 0
-    const double c_lo = copysign(na, y);              // toward zero
-    const double c_hi = copysign(na + 1.0, y);        // away from zero
-    double m0, m1;
-    if (fa < 0.5) { m0 = c_lo; m1 = c_lo; }
-    else if (fa > 0.5) { m0 = c_hi; m1 = c_hi; }
-    else {                                            // tie: the candidate giving an even S
-        m0 = ks_even(g.p0 + c_lo) ? c_lo : c_hi;            // S_a even
-        m1 = ks_even(g.p1 + 1.0 + c_lo) ? c_lo : c_hi;      // S_a odd
-    }
+    t.ok = fabs(y) < 0x1p51;                           // false for inf / nan
+    const double u = y + 0x1.8p52;
+    t.r = u - 0x1.8p52;
+    t.pr = (int)(ks_bits(u) & 1u);
+    t.tie = fabs(y - t.r) == 0.5;
+    t.alt = 2.0 * y - t.r;                            // exact: an integer next to r
+    return t;
+}
+KS_HD void ks_commit(KsSeg& g, const KsStep& t) {
+    const double m0 = (t.tie && g.par0) ? t.alt : t.r;
+    const double m1 = (t.tie && g.par1) ? t.alt : t.r;
+    g.par0 = t.tie ? 0 : (g.par0 ^ t.pr);
+    g.par1 = t.tie ? 0 : (g.par1 ^ t.pr);
     g.p0 += m0;
     g.p1 += m1;
-    const double mn = fmin(g.p0, g.p1), mx = fmax(g.p0, g.p1);
-    g.lo = g.n ? fmin(g.lo, mn) : mn;
-    g.hi = g.n ? fmax(g.hi, mx) : mx;
+    g.lo = fmin(g.lo, fmin(g.p0, g.p1));
+    g.hi = fmax(g.hi, fmax(g.p0, g.p1));
     g.n++;
-    return true;
 }
 
 // Segmentation of one pair's positions: x at offset o, st the approximate
@@ -116,7 +124,11 @@ KS_HD bool ks_step(KsSeg& g, double x) {
 template <typename Emit>
 KS_HD void ks_feed(KsSeg& g, bool& open, double x, double st, int o, Emit&& emit) {
     const int key = ks_key(st);
-    if (open && key != 0 && key == g.key && ks_step(g, x)) return;
+    const KsStep t = ks_step_m(x, g.key);
+    if (open && key != 0 && key == g.key && t.ok) {
+        ks_commit(g, t);
+        return;
+    }
     if (open) emit(g);
     ks_open(g, key, o, x);
     open = true;

@@ -508,15 +508,30 @@ __device__ __attribute__((always_inline)) inline void ks_walk(const double* __re
     int c = ks_first_cluster(crow, K, p0);
     int64_t cend = crow[c + 1];
     open(c, p0);
-    for (int64_t p = p0; p < p1; p += KS_U) {
-        double v[KS_U];
+    // pipeline: the member indices two blocks ahead (scalar loads), the row
+    // values one block ahead; past the end, the last position again (every
+    // block issues the same loads, so the waits count exactly)
+    auto ld_idx = [&](int64_t p, int32_t (&ix)[KS_U]) {
         if (p + KS_U <= p1) {
 #pragma unroll
-            for (int u = 0; u < KS_U; u++) v[u] = X[(int64_t)r4[p + u] * d + jl];
+            for (int u = 0; u < KS_U; u++) ix[u] = r4[p + u];
         } else {
 #pragma unroll
-            for (int u = 0; u < KS_U; u++) v[u] = X[(int64_t)r4[min(p + u, p1 - 1)] * d + jl];
+            for (int u = 0; u < KS_U; u++) ix[u] = r4[min(p + u, p1 - 1)];
         }
+    };
+    auto ld_val = [&](const int32_t (&ix)[KS_U], double (&v)[KS_U]) {
+#pragma unroll
+        for (int u = 0; u < KS_U; u++) v[u] = X[(int64_t)ix[u] * d + jl];
+    };
+    int32_t ia[KS_U], ib[KS_U];
+    double va[KS_U], vb[KS_U];
+    ld_idx(p0, ia);
+    ld_val(ia, va);
+    ld_idx(p0 + KS_U, ib);
+    for (int64_t p = p0; p < p1; p += KS_U) {
+        ld_val(ib, vb);
+        ld_idx(p + 2 * KS_U, ia);
 #pragma unroll
         for (int u = 0; u < KS_U; u++) {
             if (p + u >= p1) break;
@@ -528,8 +543,10 @@ __device__ __attribute__((always_inline)) inline void ks_walk(const double* __re
                 } while (p + u >= cend);             // empty clusters have no pair here
                 open(c, p + u);
             }
-            step(p + u, v[u]);
+            step(p + u, va[u]);
         }
+#pragma unroll
+        for (int u = 0; u < KS_U; u++) { va[u] = vb[u]; ib[u] = ia[u]; }
     }
     close(c);
 }
@@ -583,6 +600,7 @@ __global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X
             [&](int c, int64_t) {
                 const size_t o = (size_t)(w + c) * d + j;
                 st = on ? sin[o] : 0.0;
+                asm volatile("" : "+v"(st));      // waited here, not at every step after this branch
                 open = false;
                 nr = 0;
                 rp = rec + o * KS_R;
@@ -614,17 +632,16 @@ __device__ inline int64_t ks_rl(int64_t v, int i) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// positions [q0, q1) of the chain's member list added to s in order (<= 512)
-__device__ inline double ks_walk_values(double s, const double* __restrict__ X, int d, int j,
-                                        const int32_t* __restrict__ rows, int64_t q0, int64_t q1) {
-    const int lane = threadIdx.x;
-    for (int64_t q = q0; q < q1; q += 64) {
-        const int m = (int)min<int64_t>(64, q1 - q);
-        const double v = lane < m ? X[(int64_t)rows[q + lane] * d + j] : 0.0;
-        for (int i = 0; i < m; i++) s = __dadd_rn(s, ks_rl(v, i));
-    }
-    return s;
-}
+// Pair pipeline: while pair w is applied, pair w+1's records -- or, for a
+// dense pair, its member values (lane i: positions i, i+64, ...) -- and pair
+// w+2's count and member row indices are in flight (row indices always: the
+// values need them one pair ahead, and a failed summary reads from them).
+struct KsPair {
+    int n;
+    int32_t idx[KS_W / 64];
+    double v[KS_W / 64];
+    KsRec r;
+};
 
 __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict__ X, int d,
                                                         const int32_t* __restrict__ rows,
@@ -638,37 +655,85 @@ __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict
     double s = carry ? carry[(size_t)c * d + j] : 0.0;
     if (beg < end) {
         const int64_t w0 = beg / KS_W, w1 = (end - 1) / KS_W;
-        auto load = [&](int64_t w, int& n, KsRec& r) {
-            const size_t o = (size_t)(w + c) * d + j;
-            n = cnt[o];
-            if (lane < n && n <= KS_R) r = rec[o * KS_R + lane];
-        };
-        int n_nx = 0;
-        KsRec r_nx = {};
-        load(w0, n_nx, r_nx);
-        for (int64_t w = w0; w <= w1; w++) {
-            const int n = n_nx;
-            const KsRec r = r_nx;
-            if (w < w1) load(w + 1, n_nx, r_nx);
+        auto load_meta = [&](int64_t w, KsPair& P) {      // count and row indices
+            if (w > w1) return;
+            P.n = cnt[(size_t)(w + c) * d + j];
             const int64_t wb = w * KS_W;
-            if (n > KS_R) {                              // dense pair: the plain chain
-                s = ks_walk_values(s, X, d, j, rows, max(beg, wb), min(end, wb + KS_W));
-                continue;
+#pragma unroll
+            for (int k = 0; k < KS_W / 64; k++) {
+                const int64_t q = min(max(wb + 64 * k + lane, beg), end - 1);
+                P.idx[k] = rows[q];
             }
-#pragma unroll 2
-            for (int i = 0; i < n; i++) {
-                KsRec ri;
-                ri.xa = ks_rl(r.xa, i);
-                ri.L = ks_rl(r.L, i);
-                ri.H = ks_rl(r.H, i);
-                ri.d0 = ks_rl(r.d0, i);
-                ri.d1 = ks_rl(r.d1, i);
-                ri.meta = (uint64_t)ks_rl((int64_t)r.meta, i);
-                if (!ks_apply(s, ri)) {
-                    const int a = ks_rec_a(ri), b = ks_rec_b(ri);
-                    s = ks_walk_values(s, X, d, j, rows, wb + a + 1, wb + b + 1);
+        };
+        auto load_body = [&](int64_t w, KsPair& P) {      // records or values
+            if (w > w1) return;
+            if (P.n <= KS_R) {
+                if (lane < P.n) P.r = rec[((size_t)(w + c) * d + j) * KS_R + lane];
+            } else {
+#pragma unroll
+                for (int k = 0; k < KS_W / 64; k++) P.v[k] = X[(int64_t)P.idx[k] * d + j];
+            }
+        };
+        KsPair A, B, Cn;
+        load_meta(w0, A);
+        load_body(w0, A);
+        load_meta(w0 + 1, B);
+        for (int64_t w = w0; w <= w1; w++) {
+            // pair w's registers are complete before the next loads issue, so
+            // nothing below waits on those (vmcnt counts in order)
+            asm volatile("" : "+v"(A.r.xa), "+v"(A.r.L), "+v"(A.r.H), "+v"(A.r.d0), "+v"(A.r.d1), "+v"(A.r.meta));
+#pragma unroll
+            for (int k = 0; k < KS_W / 64; k++) asm volatile("" : "+v"(A.v[k]), "+v"(A.idx[k]));
+            load_meta(w + 2, Cn);
+            load_body(w + 1, B);
+            const int64_t wb = w * KS_W;
+            const int o0 = (int)(max(beg, wb) - wb), o1 = (int)(min(end, wb + KS_W) - wb);   // valid offsets
+            if (A.n > KS_R) {                            // dense pair: the plain chain
+#pragma unroll
+                for (int k = 0; k < KS_W / 64; k++) {
+                    const int i0 = max(0, o0 - 64 * k), i1 = min(64, o1 - 64 * k);
+                    if (i0 == 0 && i1 == 64) {
+#pragma unroll
+                        for (int i = 0; i < 64; i++) s = __dadd_rn(s, ks_rl(A.v[k], i));
+                    } else {
+                        for (int i = i0; i < i1; i++) s = __dadd_rn(s, ks_rl(A.v[k], i));
+                    }
+                }
+            } else {
+                // records in order; the loop itself holds no memory load (a load
+                // inside would make every record wait for the prefetches), a
+                // record whose summary does not apply leaves it for the fix below
+                int i = 0;
+                while (i < A.n) {
+                    int fa = -1, fb = -1;
+                    for (; i < A.n; i++) {
+                        KsRec ri;
+                        ri.xa = ks_rl(A.r.xa, i);
+                        ri.L = ks_rl(A.r.L, i);
+                        ri.H = ks_rl(A.r.H, i);
+                        ri.d0 = ks_rl(A.r.d0, i);
+                        ri.d1 = ks_rl(A.r.d1, i);
+                        if (!ks_apply(s, ri)) {
+                            ri.meta = (uint64_t)ks_rl((int64_t)A.r.meta, i);
+                            fa = ks_rec_a(ri);
+                            fb = ks_rec_b(ri);
+                            i++;
+                            break;
+                        }
+                    }
+                    // positions fa+1 .. fb with real adds
+                    for (int k = (fa + 1) / 64; fa >= 0 && k <= fb / 64; k++) {
+                        int32_t ix = A.idx[0];
+#pragma unroll
+                        for (int u = 1; u < KS_W / 64; u++) ix = u == k ? A.idx[u] : ix;   // registers, no scratch
+                        const double v = X[(int64_t)ix * d + j];
+                        const int i0 = max(0, fa + 1 - 64 * k), i1 = min(64, fb + 1 - 64 * k);
+                        for (int q = i0; q < i1; q++) s = __dadd_rn(s, ks_rl(v, q));
+                    }
                 }
             }
+            A = B;
+            B = Cn;
         }
     }
     if (lane == 0) sums[(size_t)c * d + j] = s;
