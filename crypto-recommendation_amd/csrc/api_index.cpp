@@ -580,8 +580,10 @@ static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign
     // Parallel exact sums (fixed point where the chain provably never rounds);
     // LSHKM_KM_PATH=chain runs every (c, j) chain sequentially.
     const char* kp = getenv("LSHKM_KM_PATH");
-    // fp64 rows: binade segments (LSHKM_KM_PATH=seg; being measured)
-    if (X.f64 && kp && !strcmp(kp, "seg")) {
+    // fp64 rows: binade segments (update.hip / kmseg.h; the fp64 update of 1M x
+    // 100 rows, K = 256: 1.09 ms vs 2.68 ms for fixed point + the wide chains);
+    // LSHKM_KM_PATH=fx: the fixed-point form, =chain: every chain sequential
+    if (X.f64 && !(kp && (!strcmp(kp, "fx") || !strcmp(kp, "chain")))) {
         const size_t wsb = km_seg_ws_bytes(N, K, d);
         if ((rc = ctx->ws_range[11].reserve(wsb))) return rc;
         if ((rc = launch_km_sums_seg(ctx->stream, X.d(), d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K,

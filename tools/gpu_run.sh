@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box routine (run through gpurun from the repo root):
-#   tools/gpu_run.sh TAG [tests|bench|benchq|prof|pmc|pmc5|prof5|sq|rows]...
+#   tools/gpu_run.sh TAG [tests|smoke|bench|benchq|prof|pmc|pmc5|prof5|sq|rows]...
 # Each GPU step has its own time limit; the script stops at the first failure.
 set -u
 TAG=${1:?tag}; shift
@@ -13,6 +13,9 @@ for step in "$@"; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
       rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { echo "tests rc=$rc"; exit $rc; } ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      rc=$?; tail -2 "$OUT/smoke.log"; [ $rc -eq 0 ] || { echo "smoke rc=$rc"; exit $rc; } ;;
     bench)
       timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
       rc=$?; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; } ;;
