@@ -76,6 +76,20 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X, const double* x_mean, int6
 
 }  // extern "C"
 
+static int terms_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
+                         const int64_t* unk_ptr, std::vector<int64_t>& soff, std::vector<int64_t>& hup,
+                         std::vector<int64_t>& toff);
+static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_t N, int d, const int64_t* crow,
+                              const int32_t* crows, int K, Pts U, int64_t nq, const int32_t* ucl,
+                              const int64_t* unk_ptr, const int32_t* unk_idx, int64_t* soff_dev, int64_t* toff_dev,
+                              double* sims, double* terms, int64_t cap, int64_t tcap, int64_t* total_host,
+                              int64_t* tterms_host);
+static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, const int64_t* unk_ptr,
+                            const int32_t* unk_idx, const int64_t* soff, const int64_t* toff, const double* sims,
+                            const double* terms, const double* carry_main, const double* carry_abs,
+                            const int64_t* carry_cnt, double* main_out, double* abs_out, int64_t* cnt_out, int n_top,
+                            int32_t* out);
+
 // get_top_N_recom(neighbors, user, N), crypto_rec.hpp:327-345, over whole
 // clusters (main.cpp:260-269, :353-373). The cluster sizes come to the host
 // once to size the per-wave similarity scratch (waves x largest cluster).
@@ -88,6 +102,29 @@ static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
                 LSHKM_ERR_ARG, "bad arguments");
     if (nq == 0 || n_top == 0) return 0;
     LSHKM_HIP(hipSetDevice(ctx->device));
+    {   // the terms form (recom.hip) when the rows stage and the terms fit 2 GiB
+        const int64_t rb = (int64_t)d * (X.f64 ? 8 : 4);
+        if (rb % 8 == 0 && rb <= 1016) {
+            std::vector<int64_t> soff, hup, toff;
+            int rc;
+            if ((rc = terms_offsets(ctx, crow, K, N, ucl, nq, unk_ptr, soff, hup, toff))) return rc;
+            if (toff[nq] <= (1ll << 28)) {
+                Buf &bs = ctx->ws_call[0], &bt = ctx->ws_call[5], &bso = ctx->ws_call[6], &bto = ctx->ws_call[7];
+                if ((rc = bs.reserve(8 * (size_t)std::max<int64_t>(soff[nq], 1))) ||
+                    (rc = bt.reserve(8 * (size_t)std::max<int64_t>(toff[nq], 1))) ||
+                    (rc = bso.reserve(8 * (size_t)(nq + 1))) || (rc = bto.reserve(8 * (size_t)(nq + 1))))
+                    return rc;
+                int64_t tot = 0, tt = 0;
+                if ((rc = cluster_terms_impl(ctx, X, x_mean, N, d, crow, crows, K, U, nq, ucl, unk_ptr, unk_idx,
+                                             bso.as<int64_t>(), bto.as<int64_t>(), bs.as<double>(), bt.as<double>(),
+                                             soff[nq], toff[nq], &tot, &tt)))
+                    return rc;
+                return chain_terms_impl(ctx, nq, u_mean, unk_ptr, unk_idx, bso.as<int64_t>(), bto.as<int64_t>(),
+                                        bs.as<double>(), bt.as<double>(), nullptr, nullptr, nullptr, nullptr, nullptr,
+                                        nullptr, n_top, out);
+            }
+        }
+    }
     std::vector<int64_t> hc((size_t)K + 1);
     int64_t total = 0;
     LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
@@ -201,6 +238,116 @@ static int cluster_chain_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     return 0;
 }
 
+// ----------------------------------------------------------- terms form
+// Host offsets of the terms form: soff (members per user on this shard), the
+// unknown-index CSR (hup) and toff (terms per user: members x unknown indexes).
+static int terms_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
+                         const int64_t* unk_ptr, std::vector<int64_t>& soff, std::vector<int64_t>& hup,
+                         std::vector<int64_t>& toff) {
+    int rc;
+    if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff))) return rc;
+    hup.assign((size_t)nq + 1, 0);
+    LSHKM_HIP(hipMemcpyAsync(hup.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    toff.assign((size_t)nq + 1, 0);
+    bool ok = hup[0] == 0;
+    for (int64_t q = 0; q < nq && ok; q++) {
+        ok = hup[q + 1] >= hup[q];
+        toff[q + 1] = toff[q] + (soff[q + 1] - soff[q]) * (hup[q + 1] - hup[q]);
+    }
+    LSHKM_CHECK(ok, LSHKM_ERR_ARG, "bad unknown-index lists (unk_ptr must start at 0 and not decrease)");
+    return 0;
+}
+
+// The (user, unknown index) slots of rc_chain_terms_kernel (e = -1: a user
+// without unknown indexes), uploaded to ws_call[3] / [4].
+static int chain_slots(lshkm_ctx ctx, const int64_t* unk_ptr, int64_t nq, int64_t* nslot) {
+    std::vector<int64_t> hup((size_t)nq + 1);
+    LSHKM_HIP(hipMemcpyAsync(hup.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<int32_t> sq, se;
+    for (int64_t q = 0; q < nq; q++) {
+        const int64_t m = hup[q + 1] - hup[q];
+        LSHKM_CHECK(m >= 0 && m < (1ll << 31), LSHKM_ERR_ARG, "bad unknown-index lists");
+        if (m == 0) { sq.push_back((int32_t)q); se.push_back(-1); }
+        for (int64_t e = 0; e < m; e++) { sq.push_back((int32_t)q); se.push_back((int32_t)e); }
+    }
+    *nslot = (int64_t)sq.size();
+    int rc;
+    if ((rc = ctx->ws_call[3].reserve(4 * sq.size() + 4)) || (rc = ctx->ws_call[4].reserve(4 * se.size() + 4))) return rc;
+    if (!sq.empty()) {
+        LSHKM_HIP(hipMemcpyAsync(ctx->ws_call[3].p, sq.data(), 4 * sq.size(), hipMemcpyHostToDevice, ctx->stream));
+        LSHKM_HIP(hipMemcpyAsync(ctx->ws_call[4].p, se.data(), 4 * se.size(), hipMemcpyHostToDevice, ctx->stream));
+    }
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host vectors go out of scope
+    return 0;
+}
+
+static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_t N, int d, const int64_t* crow,
+                              const int32_t* crows, int K, Pts U, int64_t nq, const int32_t* ucl,
+                              const int64_t* unk_ptr, const int32_t* unk_idx, int64_t* soff_dev, int64_t* toff_dev,
+                              double* sims, double* terms, int64_t cap, int64_t tcap, int64_t* total_host,
+                              int64_t* tterms_host) {
+    LSHKM_CHECK(ctx && X.p && x_mean && crow && U.p && ucl && unk_ptr && soff_dev && toff_dev && total_host &&
+                    tterms_host && N >= 1 && d >= 1 && K >= 1 && nq >= 0 && cap >= 0 && tcap >= 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(((int64_t)d * (X.f64 ? 8 : 4)) % 8 == 0 && (int64_t)d * (X.f64 ? 8 : 4) <= 1016, LSHKM_ERR_ARG,
+                "the terms form stages rows of a multiple of 8 B up to 1016 B (use lshkm_cluster_sims)");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    std::vector<int64_t> soff, hup, toff;
+    int rc;
+    if ((rc = terms_offsets(ctx, crow, K, N, ucl, nq, unk_ptr, soff, hup, toff))) return rc;
+    *total_host = soff[nq];
+    *tterms_host = toff[nq];
+    LSHKM_CHECK(toff[nq] == 0 || unk_idx, LSHKM_ERR_ARG, "unk_idx is NULL");
+    LSHKM_HIP(hipMemcpyAsync(soff_dev, soff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, ctx->stream));
+    LSHKM_HIP(hipMemcpyAsync(toff_dev, toff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, ctx->stream));
+    if (sims && terms && soff[nq] <= cap && toff[nq] <= tcap && soff[nq] > 0) {
+        LSHKM_CHECK(crows, LSHKM_ERR_ARG, "crows is NULL");
+        if ((rc = launch_rc_terms(ctx->stream, X, x_mean, d, crow, crows, K, U, nq, ucl, soff_dev, soff[nq], unk_ptr,
+                                  unk_idx, toff_dev, sims, terms, (unsigned long long*)ctx->stats.p + STAT_REC_SOFT)))
+            return rc;
+    }
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host offsets are copied before return
+    return 0;
+}
+
+static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, const int64_t* unk_ptr,
+                            const int32_t* unk_idx, const int64_t* soff, const int64_t* toff, const double* sims,
+                            const double* terms, const double* carry_main, const double* carry_abs,
+                            const int64_t* carry_cnt, double* main_out, double* abs_out, int64_t* cnt_out, int n_top,
+                            int32_t* out) {
+    LSHKM_CHECK(ctx && u_mean && unk_ptr && soff && toff && nq >= 0 && n_top >= 0, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK((carry_main == nullptr) == (carry_abs == nullptr) && (carry_abs == nullptr) == (carry_cnt == nullptr),
+                LSHKM_ERR_ARG, "carry_main / carry_abs / carry_cnt: all or none");
+    LSHKM_CHECK(out || (main_out && abs_out && cnt_out), LSHKM_ERR_ARG, "either the carry outputs or out");
+    if (nq == 0) return 0;
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int64_t nslot = 0, total = 0;
+    int rc;
+    if ((rc = chain_slots(ctx, unk_ptr, nq, &nslot))) return rc;
+    LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    LSHKM_CHECK(total == 0 || unk_idx, LSHKM_ERR_ARG, "unk_idx is NULL");
+    Buf &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
+    const size_t M = (size_t)(total > 0 ? total : 1);
+    if (out && ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M)))) return rc;
+    if ((rc = launch_rc_chain_terms(ctx->stream, nslot, ctx->ws_call[3].as<int32_t>(), ctx->ws_call[4].as<int32_t>(),
+                                    soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
+                                    out ? nullptr : main_out, out ? nullptr : abs_out, out ? nullptr : cnt_out,
+                                    out ? pred.as<double>() : nullptr))) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return rc;
+    }
+    if (out && (rc = launch_rc_top(ctx->stream, nq, soff, carry_cnt, unk_ptr, unk_idx, pred.as<double>(),
+                                   pidx.as<int32_t>(), n_top, out))) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return rc;
+    }
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the slot / pred workspace is reused by the next call
+    return 0;
+}
+
 extern "C" {
 
 int lshkm_cluster_sims(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow, const int32_t* crows,
@@ -232,6 +379,32 @@ int lshkm_cluster_chain_f64(lshkm_ctx ctx, const double* X, const double* x_mean
                             int32_t* out) {
     return cluster_chain_impl(ctx, X, x_mean, N, d, crow, crows, K, nq, ucl, u_mean, unk_ptr, unk_idx, soff, sims,
                               carry_main, carry_abs, carry_cnt, main_out, abs_out, cnt_out, n_top, out);
+}
+
+int lshkm_cluster_terms(lshkm_ctx ctx, const float* X, const double* x_mean, int64_t N, int d, const int64_t* crow,
+                        const int32_t* crows, int K, const float* U, int64_t nq, const int32_t* ucl,
+                        const int64_t* unk_ptr, const int32_t* unk_idx, int64_t* soff, int64_t* toff, double* sims,
+                        double* terms, int64_t cap, int64_t tcap, int64_t* total, int64_t* tterms) {
+    return cluster_terms_impl(ctx, X, x_mean, N, d, crow, crows, K, U, nq, ucl, unk_ptr, unk_idx, soff, toff, sims,
+                              terms, cap, tcap, total, tterms);
+}
+
+int lshkm_cluster_terms_f64(lshkm_ctx ctx, const double* X, const double* x_mean, int64_t N, int d,
+                            const int64_t* crow, const int32_t* crows, int K, const double* U, int64_t nq,
+                            const int32_t* ucl, const int64_t* unk_ptr, const int32_t* unk_idx, int64_t* soff,
+                            int64_t* toff, double* sims, double* terms, int64_t cap, int64_t tcap, int64_t* total,
+                            int64_t* tterms) {
+    return cluster_terms_impl(ctx, X, x_mean, N, d, crow, crows, K, U, nq, ucl, unk_ptr, unk_idx, soff, toff, sims,
+                              terms, cap, tcap, total, tterms);
+}
+
+int lshkm_cluster_chain_terms(lshkm_ctx ctx, int64_t nq, const double* u_mean, const int64_t* unk_ptr,
+                              const int32_t* unk_idx, const int64_t* soff, const int64_t* toff, const double* sims,
+                              const double* terms, const double* carry_main, const double* carry_abs,
+                              const int64_t* carry_cnt, double* main_out, double* abs_out, int64_t* cnt_out,
+                              int n_top, int32_t* out) {
+    return chain_terms_impl(ctx, nq, u_mean, unk_ptr, unk_idx, soff, toff, sims, terms, carry_main, carry_abs,
+                            carry_cnt, main_out, abs_out, cnt_out, n_top, out);
 }
 
 int lshkm_cluster_top_n(lshkm_ctx ctx, const float* X, const double* x_mean, int64_t N, int d, const int64_t* crow,

@@ -71,7 +71,7 @@ struct lshkm_ctx_s {
     lshkm::Buf ws_scan;          // multi-block scans of large query size arrays
     // workspaces of the entry points that synchronise their stream before
     // returning (kmeans_pp, p_closest, top_n_recom): reused across calls
-    lshkm::Buf ws_call[6];
+    lshkm::Buf ws_call[10];
     uint64_t ws_epoch = 0;       // bumped by every user of the ws[] slots (api_index.cpp reserve)
     // optional HIP-event timing of the dominant kernel launch (lshkm_last_kernel_ms)
     bool timing = false;

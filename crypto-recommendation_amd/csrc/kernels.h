@@ -191,6 +191,21 @@ int launch_rc_cluster_top_n(hipStream_t s, Pts X, const double* x_mean, int d, c
                             const int64_t* unk_ptr, const int32_t* unk_idx, int n_top, double* scratch,
                             int64_t scratch_row, int nwaves, double* pred, int32_t* pidx, int32_t* out,
                             unsigned long long* soft_count);
+// The terms form of the clustering recommender (recom.hip): similarities and
+// the per-(member, unknown index) terms of every user at once, then the chains
+// one thread per (user, unknown index), then the quicksort per user.
+int rc_terms_stride8(int d, int elem);
+int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
+                    int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
+                    const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
+                    unsigned long long* soft_count);
+int launch_rc_chain_terms(hipStream_t s, int64_t nslot, const int32_t* slot_q, const int32_t* slot_e,
+                          const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff, const double* sims,
+                          const double* terms, const double* carry_main, const double* carry_abs,
+                          const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,
+                          int64_t* cnt_out, double* pred);
+int launch_rc_top(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* carry_cnt, const int64_t* unk_ptr,
+                  const int32_t* unk_idx, double* pred, int32_t* pidx, int n_top, int32_t* out);
 constexpr int RC_CLUSTER_WAVES_PER_BLOCK = 4;     // rc_cluster_top_n_kernel: waves per block (RC_WAVES)
 int launch_rc_shard_sims(hipStream_t s, Pts X, int d, const int64_t* crow, const int32_t* crows, int K, Pts U,
                          int64_t nq, const int32_t* ucl, const int64_t* unk_ptr, const int64_t* soff, double* sims,

@@ -632,6 +632,211 @@ int launch_rc_shard_chain(hipStream_t s, Pts X, const double* x_mean, int d, con
     return kstatus("rc_shard_chain_kernel");
 }
 
+// ------------------------------------------------- terms form (round 4)
+// The clustering recommender as two data-parallel phases instead of one wave
+// per user (which walked ~10K members with lane-per-member row loads touching
+// 64 lines per instruction, then the chains with 8 lanes of 64 busy):
+//   rc_terms_kernel: every (user, member) pair at once -- members flattened
+//     over users, 64 per wave; the 64 member rows staged through LDS by
+//     coalesced row loads, then per lane cosineSimilarity (IpAcc certificate,
+//     the x87 chain where it declines) and the terms of
+//     get_predicted_user_sim's main sums, t = sim * (x[index] - mean)
+//     (crypto_rec.hpp:296), one fp64 per (member, unknown index);
+//   rc_chain_terms_kernel: one thread per (user, unknown index) adds its terms
+//     and the |sim| in member order (the reference's sequential chains,
+//     :290-296), 32 values in flight, continued from / into the rank carry;
+//   rc_top_kernel: one thread per user, the division, the quicksort and the
+//     first N (:299-302, :341-343).
+constexpr int CT_STAGE = 64;      // member rows staged per wave
+
+template <typename T>
+__global__ __launch_bounds__(64) void rc_terms_kernel(
+    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const int64_t* __restrict__ crow,
+    const int32_t* __restrict__ crows, int K, const T* __restrict__ U, int64_t nq, const int32_t* __restrict__ ucl,
+    const int64_t* __restrict__ soff, const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx,
+    const int64_t* __restrict__ toff, double* __restrict__ sims, double* __restrict__ terms, int stride8,
+    unsigned long long* __restrict__ soft_count) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x;
+    const int64_t total = soff[nq];
+    const int nunit = (int)((int64_t)d * (int64_t)sizeof(T) / 8);      // 8-B units per row (d * sizeof(T) % 8 == 0)
+    uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
+    const T* myrow = reinterpret_cast<const T*>(stage + (size_t)lane * stride8);
+    unsigned long long soft = 0;
+    for (int64_t g0 = (int64_t)blockIdx.x * CT_STAGE; g0 < total; g0 += (int64_t)gridDim.x * CT_STAGE) {
+        const int64_t g = min(g0 + lane, total - 1);
+        const bool on = g0 + lane < total;
+        int lo = 0, hi = (int)nq;                   // soff[lo] <= g < soff[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (soff[mid] <= g) lo = mid; else hi = mid;
+        }
+        const int q = lo;
+        const int64_t i = g - soff[q];
+        const int c = ucl[q];
+        const int32_t r = crows[crow[c] + i];
+        // stage the wave's member rows: row t by all lanes, 8 B per lane
+        __syncthreads();
+        for (int t = 0; t < CT_STAGE; t++) {
+            const int rt = __builtin_amdgcn_readlane(r, t);
+            const uint64_t* src = reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d);
+            for (int u = lane; u < nunit; u += 64) stage[(size_t)t * stride8 + u] = src[u];
+        }
+        __syncthreads();
+        const T* u = U + (int64_t)q * d;
+        double ub = 0.0, xa = 0.0;
+        IpAcc ip;
+        for (int j = 0; j < d; j++) {
+            const double xj = (double)myrow[j], uj = (double)u[j];
+            ub = __dadd_rn(ub, __dmul_rn(uj, uj));
+            ip.add(__dmul_rn(xj, uj));
+            xa = __dadd_rn(xa, __dmul_rn(xj, xj));
+        }
+        const double denom = __dmul_rn(sqrt(xa), sqrt(ub));
+        double sv, qr;
+        if (ip.quot_status(denom, sv, qr) != 0) {   // declined (rare): the x87 chain
+            sv = cr_sim_x87(myrow, u, d, denom);
+            soft += on ? 1 : 0;
+        }
+        if (!on) continue;
+        sims[g] = sv;
+        if (terms) {
+            const int64_t o = unk_ptr[q];
+            const int m = (int)(unk_ptr[q + 1] - o);
+            const int64_t n = soff[q + 1] - soff[q];
+            const double mean = x_mean[r];
+            double* tq = terms + toff[q] + i;
+            for (int e = 0; e < m; e++)
+                tq[(int64_t)e * n] = __dmul_rn(sv, __dsub_rn((double)myrow[unk_idx[o + e]], mean));
+        }
+    }
+    if (soft_count && soft) atomicAdd(soft_count, soft);
+}
+
+// slot = (user q, unknown index e); e = -1: a user without unknown indexes (its
+// |sim| sum and count only). carry_*: the previous rank's sums (NULL: first);
+// pred == NULL: the running sums out, else the predictions.
+__global__ __launch_bounds__(64) void rc_chain_terms_kernel(
+    int64_t nslot, const int32_t* __restrict__ slot_q, const int32_t* __restrict__ slot_e,
+    const int64_t* __restrict__ soff, const int64_t* __restrict__ unk_ptr, const int64_t* __restrict__ toff,
+    const double* __restrict__ sims, const double* __restrict__ terms, const double* __restrict__ carry_main,
+    const double* __restrict__ carry_abs, const int64_t* __restrict__ carry_cnt, const double* __restrict__ u_mean,
+    double* __restrict__ main_out, double* __restrict__ abs_out, int64_t* __restrict__ cnt_out,
+    double* __restrict__ pred) {
+    constexpr int B = 16;
+    const int64_t L = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (L >= nslot) return;
+    const int q = slot_q[L], e = slot_e[L];
+    const int64_t b0 = soff[q], n = soff[q + 1] - b0;
+    const int64_t ui = unk_ptr[q] + (e < 0 ? 0 : e);
+    const double* sp = sims + b0;
+    const double* tp = terms + toff[q] + (e < 0 ? 0 : (int64_t)e * n);
+    double acc = (carry_main && e >= 0) ? carry_main[ui] : 0.0;
+    double as = carry_abs ? carry_abs[q] : 0.0;
+    const bool te = e >= 0;
+    double sa[B], ta[B], sb[B], tb[B];
+    auto ld = [&](int64_t i0, double (&sv)[B], double (&tv)[B]) {
+#pragma unroll
+        for (int k = 0; k < B; k++) {
+            const int64_t ii = min(i0 + k, n - 1);
+            sv[k] = sp[ii];
+            tv[k] = te ? tp[ii] : 0.0;
+        }
+    };
+    if (n > 0) {
+        ld(0, sa, ta);
+        for (int64_t i0 = 0; i0 < n; i0 += 2 * B) {
+            ld(i0 + B, sb, tb);
+#pragma unroll
+            for (int k = 0; k < B; k++)
+                if (i0 + k < n) {
+                    as = __dadd_rn(as, fabs(sa[k]));
+                    acc = __dadd_rn(acc, ta[k]);
+                }
+            ld(i0 + 2 * B, sa, ta);
+#pragma unroll
+            for (int k = 0; k < B; k++)
+                if (i0 + B + k < n) {
+                    as = __dadd_rn(as, fabs(sb[k]));
+                    acc = __dadd_rn(acc, tb[k]);
+                }
+        }
+    }
+    if (pred) {
+        if (te) pred[ui] = __dadd_rn(__ddiv_rn(acc, as), u_mean[q]);      // crypto_rec.hpp:299-302
+        return;
+    }
+    if (te) main_out[ui] = acc;
+    if (e <= 0) {
+        abs_out[q] = as;
+        cnt_out[q] = (carry_cnt ? carry_cnt[q] : 0) + n;
+    }
+}
+
+// One thread per user: the quicksort of its predictions (:341) and the first
+// n_top unknown indexes, 0-padded (:343); -1 rows for users whose cluster is
+// empty on every rank (main.cpp:262 / :366 skip them).
+__global__ __launch_bounds__(64) void rc_top_kernel(int64_t nq, const int64_t* __restrict__ soff,
+                                                    const int64_t* __restrict__ carry_cnt,
+                                                    const int64_t* __restrict__ unk_ptr,
+                                                    const int32_t* __restrict__ unk_idx, double* __restrict__ pred,
+                                                    int32_t* __restrict__ pidx, int n_top, int32_t* __restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (q >= nq) return;
+    const int64_t cnt = (carry_cnt ? carry_cnt[q] : 0) + soff[q + 1] - soff[q];
+    if (cnt == 0) {
+        for (int i = 0; i < n_top; i++) out[q * n_top + i] = -1;
+        return;
+    }
+    const int64_t o = unk_ptr[q];
+    const int m = (int)(unk_ptr[q + 1] - o);
+    for (int e = 0; e < m; e++) pidx[o + e] = unk_idx[o + e];
+    if (m > 0) lomuto_sort(pred + o, pidx + o, m);
+    for (int i = 0; i < n_top; i++) out[q * n_top + i] = i < m ? pidx[o + i] : 0;
+}
+
+int rc_terms_stride8(int d, int elem) { return (int)(((int64_t)d * elem + 7) / 8) + 1; }
+
+int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
+                    int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
+                    const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
+                    unsigned long long* soft_count) {
+    if (nq <= 0 || total <= 0) return 0;
+    const int elem = X.f64 ? 8 : 4;
+    if (((int64_t)d * elem) % 8 != 0) return -1;
+    const int stride8 = rc_terms_stride8(d, elem);
+    const size_t lds = (size_t)CT_STAGE * stride8 * 8;
+    if (lds > 64 * 1024) return -1;
+    const dim3 grid(gsz(total, CT_STAGE, 8192));
+    if (X.f64)
+        hipLaunchKernelGGL(rc_terms_kernel<double>, grid, dim3(64), lds, s, X.d(), x_mean, d, crow, crows, K, U.d(), nq,
+                           ucl, soff, unk_ptr, unk_idx, toff, sims, terms, stride8, soft_count);
+    else
+        hipLaunchKernelGGL(rc_terms_kernel<float>, grid, dim3(64), lds, s, X.f(), x_mean, d, crow, crows, K, U.f(), nq,
+                           ucl, soff, unk_ptr, unk_idx, toff, sims, terms, stride8, soft_count);
+    return kstatus("rc_terms_kernel");
+}
+
+int launch_rc_chain_terms(hipStream_t s, int64_t nslot, const int32_t* slot_q, const int32_t* slot_e,
+                          const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff, const double* sims,
+                          const double* terms, const double* carry_main, const double* carry_abs,
+                          const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,
+                          int64_t* cnt_out, double* pred) {
+    if (nslot <= 0) return 0;
+    hipLaunchKernelGGL(rc_chain_terms_kernel, dim3((unsigned)((nslot + 63) / 64)), dim3(64), 0, s, nslot, slot_q, slot_e,
+                       soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean, main_out, abs_out,
+                       cnt_out, pred);
+    return kstatus("rc_chain_terms_kernel");
+}
+
+int launch_rc_top(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* carry_cnt, const int64_t* unk_ptr,
+                  const int32_t* unk_idx, double* pred, int32_t* pidx, int n_top, int32_t* out) {
+    if (nq <= 0) return 0;
+    hipLaunchKernelGGL(rc_top_kernel, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, s, nq, soff, carry_cnt, unk_ptr,
+                       unk_idx, pred, pidx, n_top, out);
+    return kstatus("rc_top_kernel");
+}
+
 int launch_rc_norms(hipStream_t s, const double* X, int64_t N, int d, double* xa) {
     hipLaunchKernelGGL(rc_norm_kernel, dim3(gsz(N, 256, 4096)), dim3(256), 0, s, X, N, d, xa);
     return kstatus("recom.hip");

@@ -112,6 +112,10 @@ def lib():
                                          C.POINTER(i64)]),
             "lshkm_cluster_chain": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, vp,
                                           vp, vp, vp, vp, i32, vp]),
+            "lshkm_cluster_terms": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp, vp,
+                                          i64, i64, C.POINTER(i64), C.POINTER(i64)]),
+            "lshkm_cluster_chain_terms": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32,
+                                                vp]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
             "lshkm_clusters": (i32, [vp, vp, i64, i32, vp, vp]),
         }
@@ -663,6 +667,50 @@ def cluster_chain(ctx, X, x_mean, crow, crows, ucl, u_mean, unk_ptr, unk_idx, so
                                       _t_ptr(unk_ptr), _t_ptr(unk_idx) if M else None, _t_ptr(soff), _t_ptr(sims),
                                       _t_ptr(cm), _t_ptr(ca), _t_ptr(cc), _t_ptr(om), _t_ptr(oa), _t_ptr(oc),
                                       0 if n_top is None else n_top, _t_ptr(out)))
+    return outs if n_top is None else out
+
+
+def cluster_terms(ctx, X, x_mean, crow, crows, U, ucl, unk_ptr, unk_idx):
+    """Sharded clustering recommender, phase 1 in the terms form
+    (lshkm_cluster_terms): every user's similarities to this shard's members of
+    its cluster and its get_predicted_user_sim terms. Returns (soff, toff, sims,
+    terms) device tensors."""
+    torch = ctx.torch
+    N, d = X.shape
+    nq = U.shape[0]
+    K = crow.shape[0] - 1
+    soff = ctx.empty((nq + 1,), torch.int64)
+    toff = ctx.empty((nq + 1,), torch.int64)
+    total, tt = C.c_int64(), C.c_int64()
+    fn = _fn("lshkm_cluster_terms", X)
+    cr = _t_ptr(crows) if crows.numel() else None
+    ui = _t_ptr(unk_idx) if unk_idx.numel() else None
+    args = (ctx.h, _t_ptr(X), _t_ptr(x_mean), N, d, _t_ptr(crow), cr, K, _t_ptr(U), nq, _t_ptr(ucl), _t_ptr(unk_ptr),
+            ui, _t_ptr(soff), _t_ptr(toff))
+    _ck(fn(*args, None, None, 0, 0, C.byref(total), C.byref(tt)))
+    sims = ctx.empty((max(total.value, 1),), torch.float64)
+    terms = ctx.empty((max(tt.value, 1),), torch.float64)
+    _ck(fn(*args, _t_ptr(sims), _t_ptr(terms), total.value, tt.value, C.byref(total), C.byref(tt)))
+    return soff, toff, sims, terms
+
+
+def cluster_chain_terms(ctx, u_mean, unk_ptr, unk_idx, soff, toff, sims, terms, carry=None, n_top=None):
+    """Sharded clustering recommender, phase 2 in the terms form
+    (lshkm_cluster_chain_terms): as cluster_chain, from cluster_terms' output."""
+    torch = ctx.torch
+    nq = u_mean.shape[0]
+    M = unk_idx.shape[0]
+    cm, ca, cc = carry if carry is not None else (None, None, None)
+    out = outs = None
+    if n_top is None:
+        outs = (ctx.empty((max(M, 1),), torch.float64), ctx.empty((nq,), torch.float64), ctx.empty((nq,), torch.int64))
+    else:
+        out = ctx.empty((nq, n_top), torch.int32)
+    om, oa, oc = outs if outs is not None else (None, None, None)
+    _ck(lib().lshkm_cluster_chain_terms(ctx.h, nq, _t_ptr(u_mean), _t_ptr(unk_ptr), _t_ptr(unk_idx) if M else None,
+                                        _t_ptr(soff), _t_ptr(toff), _t_ptr(sims), _t_ptr(terms), _t_ptr(cm),
+                                        _t_ptr(ca), _t_ptr(cc), _t_ptr(om), _t_ptr(oa), _t_ptr(oc),
+                                        0 if n_top is None else n_top, _t_ptr(out)))
     return outs if n_top is None else out
 
 

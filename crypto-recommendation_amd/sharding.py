@@ -181,9 +181,10 @@ def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, un
     rank holds the same query users (U rows, u_mean, their global clusters ucl,
     the unknown-index CSR) and its own rows (X, x_mean, assign):
       1. lshkm_clusters of the local assignment -> the local cluster CSR;
-      2. lshkm_cluster_sims: every user's similarities to the local members of
-         its cluster -- the bulk of the work, all ranks at once;
-      3. lshkm_cluster_chain in rank order: rank r receives the running sums
+      2. lshkm_cluster_terms: every user's similarities to the local members of
+         its cluster and its prediction terms sim * (x[index] - mean) -- the
+         bulk of the work, all ranks at once;
+      3. lshkm_cluster_chain_terms in rank order: rank r receives the running sums
          (one fp64 per (user, unknown index) + |sim| sum + member count per user)
          from rank r-1 over RCCL point-to-point, continues them over its
          members, and sends them on; the last rank finalizes (quicksort, first
@@ -196,13 +197,14 @@ def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, un
     if ev:
         ev[0].record()
     crow, crows = lk.clusters(ctx, assign, K)
-    soff, sims = lk.cluster_sims(ctx, X, crow, crows, U, ucl, unk_ptr)
+    soff, toff, sims, terms = lk.cluster_terms(ctx, X, x_mean, crow, crows, U, ucl, unk_ptr, unk_idx)
     if ev:
         ev[1].record()
     dist = _dist()
-    args = (ctx, X, x_mean, crow, crows, ucl, u_mean, unk_ptr, unk_idx, soff, sims)
+    args = (ctx, u_mean, unk_ptr, unk_idx, soff, toff, sims, terms)
+    chain = lk.cluster_chain_terms
     if dist is None:
-        out = lk.cluster_chain(*args, carry=None, n_top=n_top)
+        out = chain(*args, carry=None, n_top=n_top)
     else:
         rank, world = dist.get_rank(), dist.get_world_size()
         nq, M = ucl.shape[0], unk_idx.shape[0]
@@ -215,13 +217,13 @@ def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, un
                 dist.recv(b, src=rank - 1)
                 back()
         if rank + 1 < world:
-            outs = lk.cluster_chain(*args, carry=carry, n_top=None)
+            outs = chain(*args, carry=carry, n_top=None)
             for t in outs:
                 b, _ = _staged(dist, t)
                 dist.send(b, dst=rank + 1)
             out = ctx.empty((nq, n_top), torch.int32)
         else:
-            out = lk.cluster_chain(*args, carry=carry, n_top=n_top)
+            out = chain(*args, carry=carry, n_top=n_top)
         b, back = _staged(dist, out)
         dist.broadcast(b, src=world - 1)
         back()

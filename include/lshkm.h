@@ -438,6 +438,33 @@ int lshkm_cluster_chain_f64(lshkm_ctx ctx, const double* X_dev, const double* x_
                             double* main_out_dev, double* abs_out_dev, int64_t* cnt_out_dev, int n_top,
                             int32_t* out_dev);
 
+/* The terms form of the same two phases (what sharding.recommend_sharded and
+ * lshkm_cluster_top_n run): phase 1 also forms get_predicted_user_sim's terms
+ * sim_i * (x_i[index] - mean_i) (crypto_rec.hpp:296) while the member rows are
+ * on chip, so the rank-to-rank chain reads no rows.
+ * lshkm_cluster_terms: soff_dev / toff_dev [nq+1] <- the offsets of each user's
+ *   similarities (member order) and terms (unknown-index-major: toff[q] +
+ *   e * n_q + i); sims_dev [cap] / terms_dev [tcap] filled when the totals
+ *   (*total_host, *tterms_host) fit (NULL to size). Rows of d * sizeof(elem) a
+ *   multiple of 8 B and at most 1016 B (else LSHKM_ERR_ARG: the form above).
+ * lshkm_cluster_chain_terms: lshkm_cluster_chain from them (same carry and
+ *   outputs). */
+int lshkm_cluster_terms(lshkm_ctx ctx, const float* X_dev, const double* x_mean_dev, int64_t N, int d,
+                        const int64_t* crow_dev, const int32_t* crows_dev, int K, const float* U_dev, int64_t nq,
+                        const int32_t* ucl_dev, const int64_t* unk_ptr_dev, const int32_t* unk_idx_dev,
+                        int64_t* soff_dev, int64_t* toff_dev, double* sims_dev, double* terms_dev, int64_t cap,
+                        int64_t tcap, int64_t* total_host, int64_t* tterms_host);
+int lshkm_cluster_terms_f64(lshkm_ctx ctx, const double* X_dev, const double* x_mean_dev, int64_t N, int d,
+                            const int64_t* crow_dev, const int32_t* crows_dev, int K, const double* U_dev, int64_t nq,
+                            const int32_t* ucl_dev, const int64_t* unk_ptr_dev, const int32_t* unk_idx_dev,
+                            int64_t* soff_dev, int64_t* toff_dev, double* sims_dev, double* terms_dev, int64_t cap,
+                            int64_t tcap, int64_t* total_host, int64_t* tterms_host);
+int lshkm_cluster_chain_terms(lshkm_ctx ctx, int64_t nq, const double* u_mean_dev, const int64_t* unk_ptr_dev,
+                              const int32_t* unk_idx_dev, const int64_t* soff_dev, const int64_t* toff_dev,
+                              const double* sims_dev, const double* terms_dev, const double* carry_main_dev,
+                              const double* carry_abs_dev, const int64_t* carry_cnt_dev, double* main_out_dev,
+                              double* abs_out_dev, int64_t* cnt_out_dev, int n_top, int32_t* out_dev);
+
 /* ------------------------------------------------------------ input formats
  * Host only (no device needed). VectorReader<double>::read
  * (vector_reader.hpp:54-85): lines 1..strt_line-1 kept as metadata, then one

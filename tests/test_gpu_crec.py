@@ -201,3 +201,44 @@ def test_shard_carry_chain_equals_single_pass(ctx, kind):
             got = lshkm.cluster_chain(*a, soff, sims, carry=carry, n_top=NT).cpu().numpy()
     assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
     assert (want[:, 0] == -1).any()
+
+
+@pytest.mark.parametrize("kind", ["f32", "f64"])
+def test_shard_carry_terms_form(ctx, kind):
+    # the terms form (lshkm_cluster_terms + lshkm_cluster_chain_terms, what
+    # sharding.recommend_sharded runs): the same 3 shards, the carry passed shard
+    # to shard -- bit for bit the oracle and the sims form; users without unknown
+    # indexes and users of clusters empty on every shard included
+    rng = np.random.default_rng(27 if kind == "f32" else 28)
+    N, d, K, nq, NT = 21_000, 100 if kind == "f64" else 128, 16, 400, 6
+    X = rng.standard_normal((N, d))
+    X = X.astype(np.float32) if kind == "f32" else X * np.exp(rng.uniform(-2, 2, size=(N, 1)))
+    xm = rng.standard_normal(N) * 0.3
+    assign = rng.integers(0, K, size=N).astype(np.int32)
+    assign[assign == 15] = 14                          # cluster 15 empty everywhere
+    assign[:14_000][assign[:14_000] == 13] = 12        # cluster 13 only on the last shard
+    users = rng.choice(N, nq, replace=False)
+    U = X[users].copy()
+    um = rng.standard_normal(nq) * 0.2
+    ucl = assign[users].copy()
+    ucl[::31] = 15
+    ucl[1::37] = 13
+    up, ui = unknown_sets(rng, nq, d)
+    up = up.copy()
+    crow, crows = oracle.clusters_csr(assign, K)
+    want = oracle.cluster_top_n(X, xm, crow, crows, U, um, ucl, up, ui, NT)
+    Ud, umd, ucd, upd, uid = dev(ctx, U), dev(ctx, um), dev(ctx, ucl), dev(ctx, up), dev(ctx, ui)
+    carry, bounds = None, [0, 7_000, 14_000, N]
+    for s in range(3):
+        lo, hi = bounds[s], bounds[s + 1]
+        Xs = dev(ctx, X[lo:hi])
+        lcrow, lrows = oracle.clusters_csr(assign[lo:hi], K)
+        soff, toff, sims, terms = lshkm.cluster_terms(ctx, Xs, dev(ctx, xm[lo:hi]), dev(ctx, lcrow), dev(ctx, lrows),
+                                                      Ud, ucd, upd, uid)
+        a = (ctx, umd, upd, uid, soff, toff, sims, terms)
+        if s < 2:
+            carry = lshkm.cluster_chain_terms(*a, carry=carry, n_top=None)
+        else:
+            got = lshkm.cluster_chain_terms(*a, carry=carry, n_top=NT).cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
+    assert (want[:, 0] == -1).any()
