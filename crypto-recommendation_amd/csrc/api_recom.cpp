@@ -304,8 +304,14 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     LSHKM_HIP(hipMemcpyAsync(toff_dev, toff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, ctx->stream));
     if (sims && terms && soff[nq] <= cap && toff[nq] <= tcap && soff[nq] > 0) {
         LSHKM_CHECK(crows, LSHKM_ERR_ARG, "crows is NULL");
+        Buf& map = ctx->ws_call[8];                  // member -> (user, row); the declined-member list + count
+        if ((rc = map.reserve(16 * (size_t)soff[nq] + 16))) return rc;
+        int32_t* mq = map.as<int32_t>();
+        int64_t* fl = reinterpret_cast<int64_t*>(map.as<char>() + 8 * (size_t)soff[nq]);
         if ((rc = launch_rc_terms(ctx->stream, X, x_mean, d, crow, crows, K, U, nq, ucl, soff_dev, soff[nq], unk_ptr,
-                                  unk_idx, toff_dev, sims, terms, (unsigned long long*)ctx->stats.p + STAT_REC_SOFT)))
+                                  unk_idx, toff_dev, sims, terms, mq, mq + soff[nq], fl,
+                                  reinterpret_cast<unsigned long long*>(fl + soff[nq]),
+                                  (unsigned long long*)ctx->stats.p + STAT_REC_SOFT)))
             return rc;
     }
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host offsets are copied before return

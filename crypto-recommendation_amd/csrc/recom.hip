@@ -638,79 +638,243 @@ int launch_rc_shard_chain(hipStream_t s, Pts X, const double* x_mean, int d, con
 // 64 lines per instruction, then the chains with 8 lanes of 64 busy):
 //   rc_terms_kernel: every (user, member) pair at once -- members flattened
 //     over users, 64 per wave; the 64 member rows staged through LDS by
-//     coalesced row loads, then per lane cosineSimilarity (IpAcc certificate,
-//     the x87 chain where it declines) and the terms of
+//     coalesced row loads, then per lane cosineSimilarity (IpAcc certificate;
+//     declined ones listed for rc_terms_fix_kernel's x87 chain) and the terms of
 //     get_predicted_user_sim's main sums, t = sim * (x[index] - mean)
 //     (crypto_rec.hpp:296), one fp64 per (member, unknown index);
 //   rc_chain_terms_kernel: one thread per (user, unknown index) adds its terms
 //     and the |sim| in member order (the reference's sequential chains,
-//     :290-296), 32 values in flight, continued from / into the rank carry;
+//     :290-296), 64 values in flight, continued from / into the rank carry;
 //   rc_top_kernel: one thread per user, the division, the quicksort and the
 //     first N (:299-302, :341-343).
 constexpr int CT_STAGE = 64;      // member rows staged per wave
 
+// The certified similarity of the lane's staged row (8-B units, in dim order)
+// against user row u8 (LDS when the wave's members share one user, else the
+// lane's own global row); ok = false where the certificate declines.
 template <typename T>
-__global__ __launch_bounds__(64) void rc_terms_kernel(
-    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const int64_t* __restrict__ crow,
-    const int32_t* __restrict__ crows, int K, const T* __restrict__ U, int64_t nq, const int32_t* __restrict__ ucl,
-    const int64_t* __restrict__ soff, const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx,
-    const int64_t* __restrict__ toff, double* __restrict__ sims, double* __restrict__ terms, int stride8,
-    unsigned long long* __restrict__ soft_count) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x;
-    const int64_t total = soff[nq];
-    const int nunit = (int)((int64_t)d * (int64_t)sizeof(T) / 8);      // 8-B units per row (d * sizeof(T) % 8 == 0)
-    uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
-    const T* myrow = reinterpret_cast<const T*>(stage + (size_t)lane * stride8);
-    unsigned long long soft = 0;
-    for (int64_t g0 = (int64_t)blockIdx.x * CT_STAGE; g0 < total; g0 += (int64_t)gridDim.x * CT_STAGE) {
-        const int64_t g = min(g0 + lane, total - 1);
-        const bool on = g0 + lane < total;
-        int lo = 0, hi = (int)nq;                   // soff[lo] <= g < soff[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (soff[mid] <= g) lo = mid; else hi = mid;
-        }
-        const int q = lo;
-        const int64_t i = g - soff[q];
-        const int c = ucl[q];
-        const int32_t r = crows[crow[c] + i];
-        // stage the wave's member rows: row t by all lanes, 8 B per lane
-        __syncthreads();
-        for (int t = 0; t < CT_STAGE; t++) {
-            const int rt = __builtin_amdgcn_readlane(r, t);
-            const uint64_t* src = reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d);
-            for (int u = lane; u < nunit; u += 64) stage[(size_t)t * stride8 + u] = src[u];
-        }
-        __syncthreads();
-        const T* u = U + (int64_t)q * d;
-        double ub = 0.0, xa = 0.0;
-        IpAcc ip;
-        for (int j = 0; j < d; j++) {
-            const double xj = (double)myrow[j], uj = (double)u[j];
+__device__ inline double ct_sim(const uint64_t* myrow8, const uint64_t* u8, int nunit, bool& ok) {
+    constexpr int PER = 8 / (int)sizeof(T);
+    double ub = 0.0, xa = 0.0;
+    IpAcc ip;
+    auto step = [&](uint64_t xw, uint64_t uw) {
+        T xv[PER], uv[PER];
+        memcpy(xv, &xw, 8);
+        memcpy(uv, &uw, 8);
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const double xj = (double)xv[k], uj = (double)uv[k];
             ub = __dadd_rn(ub, __dmul_rn(uj, uj));
             ip.add(__dmul_rn(xj, uj));
             xa = __dadd_rn(xa, __dmul_rn(xj, xj));
         }
-        const double denom = __dmul_rn(sqrt(xa), sqrt(ub));
-        double sv, qr;
-        if (ip.quot_status(denom, sv, qr) != 0) {   // declined (rare): the x87 chain
-            sv = cr_sim_x87(myrow, u, d, denom);
-            soft += on ? 1 : 0;
+    };
+    int w = 0;
+    for (; w + 4 <= nunit; w += 4) {                // four units' reads in flight
+        uint64_t xw[4], uw[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { xw[k] = myrow8[w + k]; uw[k] = u8[w + k]; }
+#pragma unroll
+        for (int k = 0; k < 4; k++) step(xw[k], uw[k]);
+    }
+    for (; w < nunit; w++) step(myrow8[w], u8[w]);
+    const double denom = __dmul_rn(sqrt(xa), sqrt(ub));
+    double sv, qr;
+    ok = ip.quot_status(denom, sv, qr) == 0;        // declined: rc_terms_fix_kernel decides
+    return sv;
+}
+
+// Member g's user and dataset row (the flattened pair space of rc_terms_kernel).
+__global__ __launch_bounds__(256) void rc_member_map_kernel(int64_t nq, const int64_t* __restrict__ soff,
+                                                            const int32_t* __restrict__ ucl,
+                                                            const int64_t* __restrict__ crow,
+                                                            const int32_t* __restrict__ crows,
+                                                            int32_t* __restrict__ mem_q, int32_t* __restrict__ mem_r) {
+    for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int64_t b = soff[q], n = soff[q + 1] - b;
+        if (n == 0) continue;
+        const int32_t* cr = crows + crow[ucl[q]];
+        for (int64_t i = threadIdx.x; i < n; i += 256) {
+            mem_q[b + i] = (int32_t)q;
+            mem_r[b + i] = cr[i];
         }
-        if (!on) continue;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void rc_terms_kernel(
+    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const T* __restrict__ U, int64_t total,
+    const int32_t* __restrict__ mem_q, const int32_t* __restrict__ mem_r, const int64_t* __restrict__ soff,
+    const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx, const int64_t* __restrict__ toff,
+    double* __restrict__ sims, double* __restrict__ terms, int stride8, int64_t* __restrict__ fix_list,
+    unsigned long long* __restrict__ fix_count) {
+    constexpr int SB = 16;                          // rows per staging batch (loads in flight)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x;
+    const int nunit = (int)((int64_t)d * (int64_t)sizeof(T) / 8);      // 8-B units per row (d * sizeof(T) % 8 == 0)
+    uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* ustage = stage + (size_t)CT_STAGE * stride8;
+    const uint64_t* myrow8 = stage + (size_t)lane * stride8;
+    int64_t g0 = (int64_t)blockIdx.x * CT_STAGE;
+    const int64_t gstep = (int64_t)gridDim.x * CT_STAGE;
+    // pipeline: the member map two chunks ahead; for rows of at most 64 units
+    // (fp32 d <= 128) the next chunk's rows in registers (unit `lane` of each)
+    // while this chunk is computed
+    auto map_at = [&](int64_t gg, int& qq, int32_t& rr) {
+        const int64_t x = min(gg + lane, total - 1);
+        qq = mem_q[x];
+        rr = mem_r[x];
+    };
+    const bool pfok = nunit <= 64;
+    uint64_t pf[CT_STAGE];
+    auto issue_pf = [&](int32_t rr) {
+#pragma unroll
+        for (int t = 0; t < CT_STAGE; t++) {
+            const int rt = __builtin_amdgcn_readlane(rr, t);
+            pf[t] = lane < nunit ? reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d)[lane] : 0ull;
+        }
+    };
+    int qA = 0, qB = 0;
+    int32_t rA = 0, rB = 0;
+    if (g0 < total) map_at(g0, qA, rA);
+    if (g0 + gstep < total) map_at(g0 + gstep, qB, rB);
+    if (pfok && g0 < total) issue_pf(rA);
+    for (; g0 < total; g0 += gstep) {
+        const int64_t g = min(g0 + lane, total - 1);
+        const bool on = g0 + lane < total;
+        const int q = qA;
+        const int32_t r = rA;
+        const int64_t i = g - soff[q];
+        const int q0 = __builtin_amdgcn_readfirstlane(q);
+        const bool one = __ballot(q != q0) == 0ull;
+        // stage the wave's member rows (and the user row when there is one user):
+        // from the prefetch registers, or in batches of SB rows with every load of
+        // a batch in flight before its LDS writes
+        __syncthreads();
+        if (pfok) {
+#pragma unroll
+            for (int t = 0; t < CT_STAGE; t++)
+                if (lane < nunit) stage[(size_t)t * stride8 + lane] = pf[t];
+            if (g0 + gstep < total) issue_pf(rB);
+        } else {
+            for (int t0 = 0; t0 < CT_STAGE; t0 += SB) {
+                for (int u0 = 0; u0 < nunit; u0 += 64) {
+                    const bool uon = u0 + lane < nunit;
+                    uint64_t v[SB];
+#pragma unroll
+                    for (int k = 0; k < SB; k++) {
+                        const int rt = __builtin_amdgcn_readlane(r, t0 + k);
+                        v[k] = uon ? reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d)[u0 + lane] : 0ull;
+                    }
+#pragma unroll
+                    for (int k = 0; k < SB; k++)
+                        if (uon) stage[(size_t)(t0 + k) * stride8 + u0 + lane] = v[k];
+                }
+            }
+        }
+        qA = qB;
+        rA = rB;
+        if (g0 + 2 * gstep < total) map_at(g0 + 2 * gstep, qB, rB);
+        if (one)
+            for (int u0 = lane; u0 < nunit; u0 += 64)
+                ustage[u0] = reinterpret_cast<const uint64_t*>(U + (int64_t)q0 * d)[u0];
+        __syncthreads();
+        const T* u = U + (int64_t)q * d;
+        bool ok;
+        const double sv = ct_sim<T>(myrow8, one ? ustage : reinterpret_cast<const uint64_t*>(u), nunit, ok);
+        // declined certificates (~12% of random pairs: cancelling inner products
+        // widen the bound) to the list of rc_terms_fix_kernel, which runs the x87
+        // chain with every lane busy (inline it cost each wave the chain's full
+        // length for a few lanes)
+        const unsigned long long dm = __ballot(on && !ok);
+        if (dm) {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(fix_count, (unsigned long long)__popcll(dm));
+            base = __shfl(base, 0);
+            if (on && !ok) fix_list[base + __popcll(dm & ((1ull << lane) - 1ull))] = g;
+        }
+        if (!on || !ok) continue;
         sims[g] = sv;
         if (terms) {
             const int64_t o = unk_ptr[q];
             const int m = (int)(unk_ptr[q + 1] - o);
             const int64_t n = soff[q + 1] - soff[q];
             const double mean = x_mean[r];
+            const T* xr = reinterpret_cast<const T*>(myrow8);
             double* tq = terms + toff[q] + i;
             for (int e = 0; e < m; e++)
-                tq[(int64_t)e * n] = __dmul_rn(sv, __dsub_rn((double)myrow[unk_idx[o + e]], mean));
+                tq[(int64_t)e * n] = __dmul_rn(sv, __dsub_rn((double)xr[unk_idx[o + e]], mean));
         }
     }
-    if (soft_count && soft) atomicAdd(soft_count, soft);
+}
+
+// The listed members: cosineSimilarity by the x87 chain (softx87.h X87acc),
+// lane per member, 64 members per wave with their rows and their users' rows
+// staged through LDS (coalesced row loads, as rc_terms_kernel), then the terms;
+// soft_count += the list length.
+template <typename T>
+__global__ __launch_bounds__(64) void rc_terms_fix_kernel(
+    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const T* __restrict__ U,
+    const int32_t* __restrict__ mem_q, const int32_t* __restrict__ mem_r, const int64_t* __restrict__ soff,
+    const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx, const int64_t* __restrict__ toff,
+    double* __restrict__ sims, double* __restrict__ terms, const int64_t* __restrict__ fix_list,
+    const unsigned long long* __restrict__ fix_count, int stride8, unsigned long long* __restrict__ soft_count) {
+    constexpr int SB = 16;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x;
+    const int nunit = (int)((int64_t)d * (int64_t)sizeof(T) / 8);
+    uint64_t* xs = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* us = xs + (size_t)CT_STAGE * stride8;
+    const T* myx = reinterpret_cast<const T*>(xs + (size_t)lane * stride8);
+    const T* myu = reinterpret_cast<const T*>(us + (size_t)lane * stride8);
+    const int64_t nfix = (int64_t)*fix_count;
+    if (blockIdx.x == 0 && lane == 0 && soft_count && nfix) atomicAdd(soft_count, (unsigned long long)nfix);
+    for (int64_t k0 = (int64_t)blockIdx.x * CT_STAGE; k0 < nfix; k0 += (int64_t)gridDim.x * CT_STAGE) {
+        const bool on = k0 + lane < nfix;
+        const int64_t g = fix_list[min(k0 + lane, nfix - 1)];
+        const int q = mem_q[g];
+        const int32_t r = mem_r[g];
+        __syncthreads();
+        for (int t0 = 0; t0 < CT_STAGE; t0 += SB) {
+            for (int u0 = 0; u0 < nunit; u0 += 64) {
+                const bool uon = u0 + lane < nunit;
+                uint64_t vx[SB], vu[SB];
+#pragma unroll
+                for (int k = 0; k < SB; k++) {
+                    const int rt = __builtin_amdgcn_readlane(r, t0 + k), qt = __builtin_amdgcn_readlane(q, t0 + k);
+                    vx[k] = uon ? reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d)[u0 + lane] : 0ull;
+                    vu[k] = uon ? reinterpret_cast<const uint64_t*>(U + (int64_t)qt * d)[u0 + lane] : 0ull;
+                }
+#pragma unroll
+                for (int k = 0; k < SB; k++)
+                    if (uon) {
+                        xs[(size_t)(t0 + k) * stride8 + u0 + lane] = vx[k];
+                        us[(size_t)(t0 + k) * stride8 + u0 + lane] = vu[k];
+                    }
+            }
+        }
+        __syncthreads();
+        double xa = 0.0, ub = 0.0;
+        X87acc ip;
+        ip.init();
+        for (int j = 0; j < d; j++) {
+            const double xj = (double)myx[j], uj = (double)myu[j];
+            ip.add(__dmul_rn(xj, uj));
+            xa = __dadd_rn(xa, __dmul_rn(xj, xj));
+            ub = __dadd_rn(ub, __dmul_rn(uj, uj));
+        }
+        const double sv = x87_quot(ip.value(), __dmul_rn(sqrt(xa), sqrt(ub)));
+        if (!on) continue;
+        sims[g] = sv;
+        if (terms) {
+            const int64_t o = unk_ptr[q];
+            const int m = (int)(unk_ptr[q + 1] - o);
+            const int64_t n = soff[q + 1] - soff[q], i = g - soff[q];
+            const double mean = x_mean[r];
+            double* tq = terms + toff[q] + i;
+            for (int e = 0; e < m; e++) tq[(int64_t)e * n] = __dmul_rn(sv, __dsub_rn((double)myx[unk_idx[o + e]], mean));
+        }
+    }
 }
 
 // slot = (user q, unknown index e); e = -1: a user without unknown indexes (its
@@ -723,7 +887,7 @@ __global__ __launch_bounds__(64) void rc_chain_terms_kernel(
     const double* __restrict__ carry_abs, const int64_t* __restrict__ carry_cnt, const double* __restrict__ u_mean,
     double* __restrict__ main_out, double* __restrict__ abs_out, int64_t* __restrict__ cnt_out,
     double* __restrict__ pred) {
-    constexpr int B = 16;
+    constexpr int B = 32;                           // values per buffer; two buffers in flight
     const int64_t L = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (L >= nslot) return;
     const int q = slot_q[L], e = slot_e[L];
@@ -800,20 +964,34 @@ int rc_terms_stride8(int d, int elem) { return (int)(((int64_t)d * elem + 7) / 8
 int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
                     int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
                     const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
+                    int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
                     unsigned long long* soft_count) {
+    (void)K;
     if (nq <= 0 || total <= 0) return 0;
     const int elem = X.f64 ? 8 : 4;
     if (((int64_t)d * elem) % 8 != 0) return -1;
     const int stride8 = rc_terms_stride8(d, elem);
-    const size_t lds = (size_t)CT_STAGE * stride8 * 8;
-    if (lds > 64 * 1024) return -1;
-    const dim3 grid(gsz(total, CT_STAGE, 8192));
+    const size_t lds = (size_t)(CT_STAGE + 1) * stride8 * 8;
+    if (2 * lds > 160 * 1024) return -1;
+    hipLaunchKernelGGL(rc_member_map_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0, s, nq, soff, ucl,
+                       crow, crows, mem_q, mem_r);
+    const dim3 grid(gsz(total, CT_STAGE, 4096));
+    if (hipMemsetAsync(fix_count, 0, 8, s) != hipSuccess) return kstatus("rc_terms (memset)");
     if (X.f64)
-        hipLaunchKernelGGL(rc_terms_kernel<double>, grid, dim3(64), lds, s, X.d(), x_mean, d, crow, crows, K, U.d(), nq,
-                           ucl, soff, unk_ptr, unk_idx, toff, sims, terms, stride8, soft_count);
+        hipLaunchKernelGGL(rc_terms_kernel<double>, grid, dim3(64), lds, s, X.d(), x_mean, d, U.d(), total, mem_q, mem_r,
+                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count);
     else
-        hipLaunchKernelGGL(rc_terms_kernel<float>, grid, dim3(64), lds, s, X.f(), x_mean, d, crow, crows, K, U.f(), nq,
-                           ucl, soff, unk_ptr, unk_idx, toff, sims, terms, stride8, soft_count);
+        hipLaunchKernelGGL(rc_terms_kernel<float>, grid, dim3(64), lds, s, X.f(), x_mean, d, U.f(), total, mem_q, mem_r,
+                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count);
+    // the list length is on the device: a grid for up to ~1/4 of the pairs, looping beyond
+    const dim3 fgrid(gsz(total / 4 + 1, CT_STAGE, 2048));
+    const size_t flds = 2 * lds;
+    if (X.f64)
+        hipLaunchKernelGGL(rc_terms_fix_kernel<double>, fgrid, dim3(64), flds, s, X.d(), x_mean, d, U.d(), mem_q, mem_r,
+                           soff, unk_ptr, unk_idx, toff, sims, terms, fix_list, fix_count, stride8, soft_count);
+    else
+        hipLaunchKernelGGL(rc_terms_fix_kernel<float>, fgrid, dim3(64), flds, s, X.f(), x_mean, d, U.f(), mem_q, mem_r,
+                           soff, unk_ptr, unk_idx, toff, sims, terms, fix_list, fix_count, stride8, soft_count);
     return kstatus("rc_terms_kernel");
 }
 
