@@ -878,6 +878,185 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
     }
 }
 
+// 256 < K <= 1024: XPW_R rows per wave -- the centroid columns stream from L2
+// once per XPW_R rows (at 2 rows per wave the C5 pass read ~36 GB of L2 for
+// 140K listed rows) -- and the candidates of each row selected and evaluated in
+// turn by the whole wave (per-row masks only: no [rows][chunks] mask array).
+#ifndef XPW_ROWS
+#define XPW_ROWS 4       // C5 whole call: 2 rows per wave (segmented) 5.46-5.51 ms; flat 2 / 4 / 8: 4.97 / 4.82-4.91 / 4.95-5.08
+#endif
+#ifndef XPW_OFF
+#define XPW_OFF 0       // 1: the 2-rows-per-wave form (A/B)
+#endif
+constexpr int XPW_MAXSEG = 4096;
+template <typename TX, int MET = 0>
+__global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_wide_kernel(
+    const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
+    const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
+    const unsigned long long* __restrict__ row_count, int64_t max_rows, int32_t* __restrict__ assign,
+    double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows, int nseg) {
+    constexpr int R = XPW_ROWS, NCH = 16;
+    __shared__ TX xs[XP_WAVES][R][XB_DMAX];
+    __shared__ int gpre[XPW_MAXSEG + 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // segmented lists (one per fused block): the groups of every segment in one
+    // flat index space, so the waves share the work whatever the segments' sizes
+    // (per-segment waves left the pass waiting on the fullest segments)
+    int64_t ngroups;
+    if (seg_counts) {
+        for (int sg = threadIdx.x; sg < nseg; sg += 64 * XP_WAVES) gpre[sg + 1] = (seg_counts[2 * sg] + R - 1) / R;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            gpre[0] = 0;
+            for (int sg = 0; sg < nseg; sg++) gpre[sg + 1] += gpre[sg];
+        }
+        __syncthreads();
+        ngroups = gpre[nseg];
+    } else {
+        int64_t total = (int64_t)*row_count;
+        if (total > max_rows) total = max_rows;
+        ngroups = (total + R - 1) / R;
+    }
+    const float* chunkc = cconst + Kpad;
+    const int64_t g0 = (int64_t)blockIdx.x * XP_WAVES + wave, gstride = (int64_t)gridDim.x * XP_WAVES;
+    for (int64_t g = g0; g < ngroups; g += gstride) {
+        const int32_t* grows;
+        int64_t gbase, cnt;
+        if (seg_counts) {
+            int lo = 0, hi = nseg;                  // gpre[lo] <= g < gpre[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (gpre[mid] <= g) lo = mid; else hi = mid;
+            }
+            grows = rows + (int64_t)lo * seg_rows;
+            gbase = (g - gpre[lo]) * R;
+            cnt = seg_counts[2 * lo];
+        } else {
+            grows = rows;
+            gbase = g * R;
+            cnt = min((int64_t)*row_count, max_rows);
+        }
+        const int nr = (int)min((int64_t)R, cnt - gbase);
+        int32_t myrow[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) myrow[r] = grows[gbase + min(r, nr - 1)];   // pad with the last row
+        float xn2p[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            TX xv[XB_DMAX / 64];
+#pragma unroll
+            for (int u = 0; u < XB_DMAX / 64; u++) {
+                const int j = lane + 64 * u;
+                xv[u] = j < d ? X[(int64_t)myrow[r] * d + j] : TX(0);
+            }
+            float q = 0.f;
+#pragma unroll
+            for (int u = 0; u < XB_DMAX / 64; u++) {
+                const int j = lane + 64 * u;
+                if (j < d) {
+                    xs[wave][r][j] = xv[u];
+                    q = fmaf((float)xv[u], (float)xv[u], q);
+                }
+            }
+            xn2p[r] = q;
+        }
+        wave_sync();
+        float acc[R][NCH];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int i = 0; i < NCH; i++) acc[r][i] = 0.f;
+        int coff[NCH];
+#pragma unroll
+        for (int i = 0; i < NCH; i++) coff[i] = (64 * i < Kpad ? 64 * i : 0) + lane;
+#pragma unroll 2
+        for (int j = 0; j < d; j++) {
+            float cv[NCH];
+#pragma unroll
+            for (int i = 0; i < NCH; i++) cv[i] = CT32[(size_t)j * Kpad + coff[i]];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const float xj = (float)xs[wave][r][j];
+#pragma unroll
+                for (int i = 0; i < NCH; i++) acc[r][i] = fmaf(xj, cv[i], acc[r][i]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (r >= nr) break;                     // wave-uniform
+            double xn2 = (double)xn2p[r];
+            for (int off = 32; off >= 1; off >>= 1) xn2 += __shfl_xor(xn2, off);
+            xn2 = xn2 * (sizeof(TX) == 4 ? 1.0 + 0x1p-20 : 1.0 + 0x1p-19) + (sizeof(TX) == 4 ? 0.0 : 0x1p-280);
+            const float nx = (float)(sqrt(xn2) * (1.0 + 0x1p-30));
+            const float ex = (float)(0x1p-40 * xn2 * (1.0 + 0x1p-18) + 1e-30);
+            float lo[NCH];
+            float U = __builtin_inff();
+            bool finite = nx <= 3.0e38f;
+#pragma unroll
+            for (int i = 0; i < NCH; i++) {
+                const int c = lane + 64 * i;
+                lo[i] = __builtin_inff();
+                if (c < K) {
+                    const float E = fmaf(nx, chunkc[2 * i], chunkc[2 * i + 1] + ex);
+                    const float sc = MET == 1 ? cconst[c] - acc[r][i] : fmaf(-2.f, acc[r][i], cconst[c]);
+                    lo[i] = sc - E;
+                    const float hi = sc + E;
+                    finite = finite && (hi - lo[i]) <= 3.0e38f;   // false for inf / nan
+                    U = fminf(U, hi);
+                }
+            }
+            for (int off = 32; off >= 1; off >>= 1) U = fminf(U, __shfl_xor(U, off));
+            unsigned long long cm[NCH];
+            int ncand = 0;
+#pragma unroll
+            for (int i = 0; i < NCH; i++) {
+                cm[i] = __ballot(lo[i] <= U);
+                ncand += __popcll(cm[i]);
+            }
+            const bool prune = __all(finite) && ncand >= 1 && ncand <= 64;
+            const TX* xr = xs[wave][r];
+            double best = 0.0;
+            int bi = -1;
+            if (prune) {
+                // lane k takes the k-th candidate (increasing c)
+                int c = -1, seen = 0;
+#pragma unroll
+                for (int i = 0; i < NCH; i++) {
+                    const int n = __popcll(cm[i]);
+                    if (c < 0 && lane >= seen && lane < seen + n) {
+                        unsigned long long m = cm[i];
+                        for (int t = lane - seen; t > 0; t--) m &= m - 1;
+                        c = 64 * i + __builtin_ctzll(m);
+                    }
+                    seen += n;
+                }
+                if (c >= 0) {
+                    best = pruned_dist<MET>(xr, C + (size_t)c * d, d);
+                    bi = c;
+                }
+            } else {
+                for (int c = lane; c < K; c += 64) {
+                    const double dd = pruned_dist<MET>(xr, C + (size_t)c * d, d);
+                    // assignment.hpp:66: the -1 sentinel takes centroid 0's distance
+                    // even if NaN, which then blocks every later '<'
+                    if (bi < 0 ? (dd == dd || c == 0) : dd < best) { best = dd; bi = c; }
+                }
+            }
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double ob = __shfl_xor(best, off);
+                const int oi = __shfl_xor(bi, off);
+                const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
+                if (take) { best = ob; bi = oi; }
+            }
+            if (lane == 0) {
+                assign[myrow[r]] = bi < 0 ? 0 : bi;
+                dist[myrow[r]] = bi < 0 ? -1.0 : best;
+            }
+        }
+        wave_sync();
+    }
+}
+
 int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg,
@@ -895,13 +1074,23 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
                        cconst, metric);
     // K <= 256: 8 rows per wave over 4 chunks; K <= 1024: 2 rows per wave over 16
     const bool wide = Kpad > 256;
-    const int R = wide ? XP_WR : XP_R;
+    const int R = wide ? (XPW_OFF ? XP_WR : XPW_ROWS) : XP_R;
     const int64_t groups = (max_rows + R - 1) / R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
 #define XP_LAUNCH(TX, NCH, RR, MT, XP)                                                                              \
     hipLaunchKernelGGL((assign_pruned_kernel<TX, NCH, RR, MT>), dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, XP, \
                        d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows)
-    if (metric == 1) {
+#define XPW_LAUNCH(TX, MT, XP)                                                                                   \
+    hipLaunchKernelGGL((assign_pruned_wide_kernel<TX, MT>), dim3((unsigned)wblocks), dim3(64 * XP_WAVES), 0, s, XP, d, \
+                       C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, nseg)
+    const int64_t wblocks = std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 1024);
+    if (wide && !XPW_OFF && (!seg_counts || nseg <= XPW_MAXSEG)) {
+        if (metric == 1) {
+            if (X.f64) XPW_LAUNCH(double, 1, X.d()); else XPW_LAUNCH(float, 1, X.f());
+        } else {
+            if (X.f64) XPW_LAUNCH(double, 0, X.d()); else XPW_LAUNCH(float, 0, X.f());
+        }
+    } else if (metric == 1) {
         if (X.f64) {
             if (wide) XP_LAUNCH(double, 16, XP_WR, 1, X.d()); else XP_LAUNCH(double, 4, XP_R, 1, X.d());
         } else {
@@ -913,6 +1102,7 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
         if (wide) XP_LAUNCH(float, 16, XP_WR, 0, X.f()); else XP_LAUNCH(float, 4, XP_R, 0, X.f());
     }
 #undef XP_LAUNCH
+#undef XPW_LAUNCH
     return kstatus("assign_pruned_kernel");
 }
 
