@@ -889,13 +889,15 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
 #define XPW_OFF 0       // 1: the 2-rows-per-wave form (A/B)
 #endif
 constexpr int XPW_MAXSEG = 4096;
-template <typename TX, int MET = 0>
+#ifndef XPN_FLAT
+#define XPN_FLAT 0      // K <= 256 through the flat form as well (being measured)
+#endif
+template <typename TX, int MET = 0, int NCH = 16, int R = XPW_ROWS>
 __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_wide_kernel(
     const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
     const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
     const unsigned long long* __restrict__ row_count, int64_t max_rows, int32_t* __restrict__ assign,
     double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows, int nseg) {
-    constexpr int R = XPW_ROWS, NCH = 16;
     __shared__ TX xs[XP_WAVES][R][XB_DMAX];
     __shared__ int gpre[XPW_MAXSEG + 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1074,21 +1076,27 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
                        cconst, metric);
     // K <= 256: 8 rows per wave over 4 chunks; K <= 1024: 2 rows per wave over 16
     const bool wide = Kpad > 256;
-    const int R = wide ? (XPW_OFF ? XP_WR : XPW_ROWS) : XP_R;
+    const int R = wide ? (XPW_OFF ? XP_WR : XPW_ROWS) : XP_R;     // groups of R rows
     const int64_t groups = (max_rows + R - 1) / R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
 #define XP_LAUNCH(TX, NCH, RR, MT, XP)                                                                              \
     hipLaunchKernelGGL((assign_pruned_kernel<TX, NCH, RR, MT>), dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, XP, \
                        d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows)
-#define XPW_LAUNCH(TX, MT, XP)                                                                                   \
-    hipLaunchKernelGGL((assign_pruned_wide_kernel<TX, MT>), dim3((unsigned)wblocks), dim3(64 * XP_WAVES), 0, s, XP, d, \
-                       C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, nseg)
+#define XPW_LAUNCH(TX, MT, NC, RW, XP)                                                                           \
+    hipLaunchKernelGGL((assign_pruned_wide_kernel<TX, MT, NC, RW>), dim3((unsigned)wblocks), dim3(64 * XP_WAVES), 0, s, \
+                       XP, d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, nseg)
     const int64_t wblocks = std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 1024);
     if (wide && !XPW_OFF && (!seg_counts || nseg <= XPW_MAXSEG)) {
         if (metric == 1) {
-            if (X.f64) XPW_LAUNCH(double, 1, X.d()); else XPW_LAUNCH(float, 1, X.f());
+            if (X.f64) XPW_LAUNCH(double, 1, 16, XPW_ROWS, X.d()); else XPW_LAUNCH(float, 1, 16, XPW_ROWS, X.f());
         } else {
-            if (X.f64) XPW_LAUNCH(double, 0, X.d()); else XPW_LAUNCH(float, 0, X.f());
+            if (X.f64) XPW_LAUNCH(double, 0, 16, XPW_ROWS, X.d()); else XPW_LAUNCH(float, 0, 16, XPW_ROWS, X.f());
+        }
+    } else if (!wide && XPN_FLAT && (!seg_counts || nseg <= XPW_MAXSEG)) {
+        if (metric == 1) {
+            if (X.f64) XPW_LAUNCH(double, 1, 4, XP_R, X.d()); else XPW_LAUNCH(float, 1, 4, XP_R, X.f());
+        } else {
+            if (X.f64) XPW_LAUNCH(double, 0, 4, XP_R, X.d()); else XPW_LAUNCH(float, 0, 4, XP_R, X.f());
         }
     } else if (metric == 1) {
         if (X.f64) {
