@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box routine (run through gpurun from the repo root):
-#   tools/gpu_run.sh TAG [tests|smoke|bench|benchq|prof|pmc|pmc5|prof5|sq|rows]...
+#   tools/gpu_run.sh TAG [tests|smoke|bench|benchq|prof|pmc|pmc5|prof5|sq|sq5|rows]...
 # Each GPU step has its own time limit; the script stops at the first failure.
 set -u
 TAG=${1:?tag}; shift
@@ -56,6 +56,16 @@ for step in "$@"; do
            -d "$OUT/sq$i" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-c5 --no-exact-dist-line \
            > "$OUT/sq$i.json" 2> "$OUT/sq$i.err")
         rc=$?; echo "sq pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    sq5)
+      i=0
+      for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" \
+                 "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_SALU"; do
+        i=$((i+1))
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --pmc $set --output-format csv \
+           -d "$OUT/c5sq$i" -o run -- python3 "$R/bench.py" --workload c5 --steps 2 --warmup 1 --no-cpu-baseline \
+           > "$OUT/c5sq$i.json" 2> "$OUT/c5sq$i.err")
+        rc=$?; echo "sq5 pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
     rows)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv \
