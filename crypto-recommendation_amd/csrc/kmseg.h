@@ -33,16 +33,22 @@
 
 namespace lshkm {
 
-constexpr int KS_W = 512;          // member positions per window (pair = window x cluster)
-constexpr int KS_R = 32;           // segment records per (pair, dim); more: the pair is walked
+#ifndef KS_WINDOW
+#define KS_WINDOW 512
+#endif
+#ifndef KS_RECORDS
+#define KS_RECORDS 32
+#endif
+constexpr int KS_W = KS_WINDOW;    // member positions per window (pair = window x cluster)
+constexpr int KS_R = KS_RECORDS;   // segment records per (pair, dim); more: the pair is walked
 
 // One segment, as the composition applies it: s = fl(s + xa); the summary
 // holds iff L <= s <= H (a range inside the predicted binade, folding in the
 // prefix checks for every S_a -- the union over both parities); then s += d0
 // or d1 by the parity of S_a (the last significand bit of s). s + d is exact:
 // (S_a + M) G is a double of the same binade. Single-step segments: L = -inf,
-// H = +inf, d = -0.0 (s + -0.0 == s, signed zeros included). meta: bits 0-9
-// first offset a, 10-19 last offset b (in the window).
+// H = +inf, d = -0.0 (s + -0.0 == s, signed zeros included). meta: bits 0-15
+// first offset a, 16-31 last offset b (in the window).
 struct KsRec {
     double xa;
     double L, H;
@@ -137,7 +143,7 @@ KS_HD void ks_feed(KsSeg& g, bool& open, double x, double st, int o, Emit&& emit
 KS_HD KsRec ks_record(const KsSeg& g) {
     KsRec r;
     r.xa = g.xa;
-    r.meta = (uint64_t)g.a | ((uint64_t)(g.a + g.n) << 10);
+    r.meta = (uint64_t)g.a | ((uint64_t)(g.a + g.n) << 16);
     if (g.n == 0) {
         r.L = -INFINITY; r.H = INFINITY; r.d0 = -0.0; r.d1 = -0.0;
         return r;
@@ -160,8 +166,8 @@ KS_HD KsRec ks_record(const KsSeg& g) {
     return r;
 }
 
-KS_HD int ks_rec_a(const KsRec& r) { return (int)(r.meta & 1023u); }
-KS_HD int ks_rec_b(const KsRec& r) { return (int)((r.meta >> 10) & 1023u); }
+KS_HD int ks_rec_a(const KsRec& r) { return (int)(r.meta & 0xFFFFu); }
+KS_HD int ks_rec_b(const KsRec& r) { return (int)((r.meta >> 16) & 0xFFFFu); }
 
 // Apply a record to the running sum s (the real first add included). false:
 // the summary does not apply -- s holds fl(s_{a-1} + x_a) and the caller adds
