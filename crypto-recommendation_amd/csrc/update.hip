@@ -503,21 +503,23 @@ __device__ __attribute__((always_inline)) inline void ks_walk(const double* __re
                                                               const int32_t* __restrict__ rows,
                                                               const int64_t* __restrict__ crow, int K, int64_t M,
                                                               int64_t p0, Open&& open, Step&& step, Close&& close) {
-    const int64_t p1 = min(M, p0 + KS_W);
-    const __attribute__((address_space(4))) int32_t* r4 = (const __attribute__((address_space(4))) int32_t*)rows;
+    // positions as 32-bit offsets o = p - p0 in [0, n): scalar compares, no 64-bit VALU ones
+    const int n = (int)(min(M, p0 + KS_W) - p0);
+    const __attribute__((address_space(4))) int32_t* r4 =
+        (const __attribute__((address_space(4))) int32_t*)rows + p0;
     int c = ks_first_cluster(crow, K, p0);
-    int64_t cend = crow[c + 1];
+    int oend = (int)min(crow[c + 1] - p0, (int64_t)n);          // this cluster's part ends here
     open(c, p0);
     // pipeline: the member indices two blocks ahead (scalar loads), the row
     // values one block ahead; past the end, the last position again (every
     // block issues the same loads, so the waits count exactly)
-    auto ld_idx = [&](int64_t p, int32_t (&ix)[KS_U]) {
-        if (p + KS_U <= p1) {
+    auto ld_idx = [&](int o, int32_t (&ix)[KS_U]) {
+        if (o + KS_U <= n) {
 #pragma unroll
-            for (int u = 0; u < KS_U; u++) ix[u] = r4[p + u];
+            for (int u = 0; u < KS_U; u++) ix[u] = r4[o + u];
         } else {
 #pragma unroll
-            for (int u = 0; u < KS_U; u++) ix[u] = r4[min(p + u, p1 - 1)];
+            for (int u = 0; u < KS_U; u++) ix[u] = r4[min(o + u, n - 1)];
         }
     };
     auto ld_val = [&](const int32_t (&ix)[KS_U], double (&v)[KS_U]) {
@@ -526,24 +528,24 @@ __device__ __attribute__((always_inline)) inline void ks_walk(const double* __re
     };
     int32_t ia[KS_U], ib[KS_U];
     double va[KS_U], vb[KS_U];
-    ld_idx(p0, ia);
+    ld_idx(0, ia);
     ld_val(ia, va);
-    ld_idx(p0 + KS_U, ib);
-    for (int64_t p = p0; p < p1; p += KS_U) {
+    ld_idx(KS_U, ib);
+    for (int o = 0; o < n; o += KS_U) {
         ld_val(ib, vb);
-        ld_idx(p + 2 * KS_U, ia);
+        ld_idx(o + 2 * KS_U, ia);
 #pragma unroll
         for (int u = 0; u < KS_U; u++) {
-            if (p + u >= p1) break;
-            if (p + u >= cend) {                     // wave-uniform
+            if (o + u >= n) break;
+            if (o + u >= oend) {                     // wave-uniform
                 close(c);
                 do {
                     c++;
-                    cend = crow[c + 1];
-                } while (p + u >= cend);             // empty clusters have no pair here
-                open(c, p + u);
+                    oend = (int)min(crow[c + 1] - p0, (int64_t)n);
+                } while (o + u >= oend);             // empty clusters have no pair here
+                open(c, p0 + o + u);
             }
-            step(p + u, va[u]);
+            step(o + u, va[u]);
         }
 #pragma unroll
         for (int u = 0; u < KS_U; u++) { va[u] = vb[u]; ib[u] = ia[u]; }
@@ -560,7 +562,7 @@ __global__ __launch_bounds__(64) void ks_sum_kernel(const double* __restrict__ X
     double s = 0.0;
     ks_walk(X, d, on ? j : d - 1, rows, crow, K, M, (int64_t)w * KS_W,
             [&](int, int64_t) { s = 0.0; },
-            [&](int64_t, double x) { s += x; },
+            [&](int, double x) { s += x; },
             [&](int c) { if (on) psum[(size_t)(w + c) * d + j] = s; });
 }
 
@@ -582,7 +584,7 @@ __global__ __launch_bounds__(64) void ks_scan_kernel(const double* __restrict__ 
 __global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                     const int64_t* __restrict__ crow, int K, int64_t M,
                                                     const double* __restrict__ sin, int32_t* __restrict__ cnt,
-                                                    KsRec* __restrict__ rec) {
+                                                    KsRaw* __restrict__ rec) {
     const int w = blockIdx.x;
     const int j = blockIdx.y * 64 + threadIdx.x;
     const bool on = j < d;
@@ -591,9 +593,9 @@ __global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X
     KsSeg g;
     bool open = false;
     int nr = 0;
-    KsRec* rp = rec;
+    KsRaw* rp = rec;
     auto emit = [&](const KsSeg& gg) {
-        if (on && nr < KS_R) rp[nr] = ks_record(gg);
+        if (on && nr < KS_R) rp[nr] = ks_raw(gg);
         nr++;
     };
     ks_walk(X, d, on ? j : d - 1, rows, crow, K, M, p0,
@@ -605,9 +607,9 @@ __global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X
                 nr = 0;
                 rp = rec + o * KS_R;
             },
-            [&](int64_t p, double x) {
+            [&](int o, double x) {
                 st += x;
-                ks_feed(g, open, x, st, (int)(p - p0), emit);
+                ks_feed(g, open, x, st, o, emit);
             },
             [&](int c) {
                 if (open) emit(g);
@@ -615,11 +617,15 @@ __global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X
             });
 }
 
-// D: one wave per chain. A pair's records (or, for a dense pair / a segment
-// whose summary does not apply, its member values) are loaded by the lanes at
-// once -- lane i holds record i -- and applied in order from the lanes by
-// readlane, so the dependent chain waits on no memory load; the next pair's
-// count and records are in flight meanwhile.
+// D: one wave per chain. A pair's records (or, for a dense pair, its member
+// values) are loaded by the lanes at once -- lane i holds record i, its bounds
+// formed in every lane at once -- and applied in order by passing the running
+// sum from lane to lane (DPP wave_shr:1: lane i applies record i to what lane
+// i-1 produced), so the dependent chain waits on no memory load and reads no
+// record through a scalar register; the next pair's count and records are in
+// flight meanwhile. Each lane keeps the sum it received; one check over the
+// lanes after the pass finds the first record whose summary does not apply,
+// whose positions are then walked with real adds before the pass resumes.
 __device__ inline double ks_rl(double v, int i) {
     const uint64_t b = (uint64_t)__double_as_longlong(v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, i);
@@ -632,6 +638,20 @@ __device__ inline int64_t ks_rl(int64_t v, int i) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// Lane form of ks_apply for the pass: every lane applies its record to its own
+// sum (the result where the summary does not apply is unused).
+__device__ inline double ks_apply_t(double s, const KsRec& r) {
+    const double t = __dadd_rn(s, r.xa);
+    const double t2 = __dadd_rn(t, r.d);
+    return (t >= r.L && t <= r.H) ? t2 : t;
+}
+__device__ inline int ks_rec_a(uint64_t meta, int i) {
+    return (int)((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)meta, i) & 0xFFFFu);
+}
+__device__ inline int ks_rec_b(uint64_t meta, int i) {
+    return (int)(((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)meta, i) >> 16) & 0xFFFFu);
+}
+
 // Pair pipeline: while pair w is applied, pair w+1's records -- or, for a
 // dense pair, its member values (lane i: positions i, i+64, ...) -- and pair
 // w+2's count and member row indices are in flight (row indices always: the
@@ -640,14 +660,20 @@ struct KsPair {
     int n;
     int32_t idx[KS_W / 64];
     double v[KS_W / 64];
-    KsRec r;
+    KsRaw r;
 };
+__device__ inline double ks_shr1(double v) {          // lane l <- lane l-1
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 
 __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict__ X, int d,
                                                         const int32_t* __restrict__ rows,
                                                         const int64_t* __restrict__ crow, int K,
                                                         const double* __restrict__ carry,
-                                                        const int32_t* __restrict__ cnt, const KsRec* __restrict__ rec,
+                                                        const int32_t* __restrict__ cnt, const KsRaw* __restrict__ rec,
                                                         double* __restrict__ sums) {
     const int j = blockIdx.x, c = blockIdx.y;
     const int lane = threadIdx.x;
@@ -681,7 +707,7 @@ __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict
         for (int64_t w = w0; w <= w1; w++) {
             // pair w's registers are complete before the next loads issue, so
             // nothing below waits on those (vmcnt counts in order)
-            asm volatile("" : "+v"(A.r.xa), "+v"(A.r.L), "+v"(A.r.H), "+v"(A.r.d0), "+v"(A.r.d1), "+v"(A.r.meta));
+            asm volatile("" : "+v"(A.r.xa), "+v"(A.r.p), "+v"(A.r.lo), "+v"(A.r.hi), "+v"(A.r.meta));
 #pragma unroll
             for (int k = 0; k < KS_W / 64; k++) asm volatile("" : "+v"(A.v[k]), "+v"(A.idx[k]));
             load_meta(w + 2, Cn);
@@ -700,36 +726,38 @@ __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict
                     }
                 }
             } else {
-                // records in order; the loop itself holds no memory load (a load
-                // inside would make every record wait for the prefetches), a
-                // record whose summary does not apply leaves it for the fix below
-                int i = 0;
-                while (i < A.n) {
-                    int fa = -1, fb = -1;
-                    for (; i < A.n; i++) {
-                        KsRec ri;
-                        ri.xa = ks_rl(A.r.xa, i);
-                        ri.L = ks_rl(A.r.L, i);
-                        ri.H = ks_rl(A.r.H, i);
-                        ri.d0 = ks_rl(A.r.d0, i);
-                        ri.d1 = ks_rl(A.r.d1, i);
-                        if (!ks_apply(s, ri)) {
-                            ri.meta = (uint64_t)ks_rl((int64_t)A.r.meta, i);
-                            fa = ks_rec_a(ri);
-                            fb = ks_rec_b(ri);
-                            i++;
-                            break;
-                        }
+                const KsRec R = ks_finish(A.r);
+                int i0 = 0;
+                while (i0 < A.n) {
+                    // records i0 .. n-1 by the pass; sin: the sum lane i received
+                    double sv = s, sin = s, t = s;
+                    for (int i = i0; i < A.n; i++) {
+                        sin = lane == i ? sv : sin;
+                        t = ks_apply_t(sv, R);
+                        sv = ks_shr1(t);
                     }
-                    // positions fa+1 .. fb with real adds
-                    for (int k = (fa + 1) / 64; fa >= 0 && k <= fb / 64; k++) {
+                    // the first record whose summary does not apply (the lanes past it
+                    // worked from a wrong sum; they are redone)
+                    double ta = __dadd_rn(sin, R.xa);
+                    const bool bad = lane >= i0 && lane < A.n && !(ta >= R.L && ta <= R.H);
+                    const unsigned long long fb = __ballot(bad);
+                    if (!fb) {
+                        s = ks_rl(t, A.n - 1);
+                        break;
+                    }
+                    const int f = __builtin_ctzll(fb);
+                    s = ks_rl(ta, f);                            // the record's real first add
+                    const int fa = ks_rec_a(R.meta, f), fb2 = ks_rec_b(R.meta, f);
+                    // positions fa+1 .. fb2 with real adds
+                    for (int k = (fa + 1) / 64; k <= fb2 / 64; k++) {
                         int32_t ix = A.idx[0];
 #pragma unroll
                         for (int u = 1; u < KS_W / 64; u++) ix = u == k ? A.idx[u] : ix;   // registers, no scratch
                         const double v = X[(int64_t)ix * d + j];
-                        const int i0 = max(0, fa + 1 - 64 * k), i1 = min(64, fb + 1 - 64 * k);
-                        for (int q = i0; q < i1; q++) s = __dadd_rn(s, ks_rl(v, q));
+                        const int q0 = max(0, fa + 1 - 64 * k), q1 = min(64, fb2 + 1 - 64 * k);
+                        for (int q = q0; q < q1; q++) s = __dadd_rn(s, ks_rl(v, q));
                     }
+                    i0 = f + 1;
                 }
             }
             A = B;
@@ -743,7 +771,7 @@ static int64_t ks_pairs(int64_t M, int K) { return (M + KS_W - 1) / KS_W + K; }
 
 size_t km_seg_ws_bytes(int64_t M, int K, int d) {
     const size_t pd = (size_t)ks_pairs(M, K) * d;
-    return pd * (8 + 8 + 4) + 64 + pd * KS_R * sizeof(KsRec);
+    return pd * (8 + 8 + 4) + 64 + pd * KS_R * sizeof(KsRaw);
 }
 
 // Exact-order sums of fp64 rows by segments (sums, counts as launch_km_chain).
@@ -752,8 +780,8 @@ int launch_km_sums_seg(hipStream_t s, const double* X, int d, const int32_t* row
                        void* ws) {
     const size_t pd = (size_t)ks_pairs(M, K) * d;
     char* b = reinterpret_cast<char*>(ws);
-    KsRec* rec = reinterpret_cast<KsRec*>(b);                 // 16-B aligned first
-    double* psum = reinterpret_cast<double*>(b + pd * KS_R * sizeof(KsRec));
+    KsRaw* rec = reinterpret_cast<KsRaw*>(b);                 // 16-B aligned first
+    double* psum = reinterpret_cast<double*>(b + pd * KS_R * sizeof(KsRaw));
     double* sin = psum + pd;
     int32_t* cnt = reinterpret_cast<int32_t*>(sin + pd);
     const int jb = (d + 63) / 64;
