@@ -484,7 +484,10 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
 //     segments of the longest chain, not its length.
 // A and C stream the member rows (lane = dimension, 512-B row slices); pair
 // (w, c) has index w + c (windows and clusters advance monotonically together).
-constexpr int KS_U = 16;           // member rows in flight per wave
+constexpr int KS_USUM = 16;        // member rows in flight per wave: pass A
+#ifndef KS_USEG
+#define KS_USEG 16                 // pass C (its per-step state holds more registers)
+#endif
 
 __device__ inline int ks_first_cluster(const int64_t* __restrict__ crow, int K, int64_t p0) {
     int lo = 0, hi = K;            // crow[lo] <= p0 < crow[hi]
@@ -498,7 +501,7 @@ __device__ inline int ks_first_cluster(const int64_t* __restrict__ crow, int K, 
 // Walk window w's positions (lane j); f(p, x) per position, close(c) when
 // cluster c's part of the window ends (only for clusters with positions in it),
 // open(c, p) when it starts.
-template <typename Open, typename Step, typename Close>
+template <int KS_U, typename Open, typename Step, typename Close>
 __device__ __attribute__((always_inline)) inline void ks_walk(const double* __restrict__ X, int d, int jl,
                                                               const int32_t* __restrict__ rows,
                                                               const int64_t* __restrict__ crow, int K, int64_t M,
@@ -560,7 +563,7 @@ __global__ __launch_bounds__(64) void ks_sum_kernel(const double* __restrict__ X
     const int j = blockIdx.y * 64 + threadIdx.x;
     const bool on = j < d;
     double s = 0.0;
-    ks_walk(X, d, on ? j : d - 1, rows, crow, K, M, (int64_t)w * KS_W,
+    ks_walk<KS_USUM>(X, d, on ? j : d - 1, rows, crow, K, M, (int64_t)w * KS_W,
             [&](int, int64_t) { s = 0.0; },
             [&](int, double x) { s += x; },
             [&](int c) { if (on) psum[(size_t)(w + c) * d + j] = s; });
@@ -598,7 +601,7 @@ __global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X
         if (on && nr < KS_R) rp[nr] = ks_raw(gg);
         nr++;
     };
-    ks_walk(X, d, on ? j : d - 1, rows, crow, K, M, p0,
+    ks_walk<KS_USEG>(X, d, on ? j : d - 1, rows, crow, K, M, p0,
             [&](int c, int64_t) {
                 const size_t o = (size_t)(w + c) * d + j;
                 st = on ? sin[o] : 0.0;
