@@ -113,16 +113,24 @@ KS_HD void ks_commit(KsSeg& g, const KsStep& t) {
 // partial sum after it. The segment continues while the predicted key holds
 // and the step has a summary; otherwise the open segment is emitted and a new
 // one starts at o (its first step is the real add of the composition).
+// Branch-free except for the emit (a store): both outcomes are formed and
+// selected, so lanes that continue and lanes that start a segment run the same
+// instructions (the segment pass runs one lane per dimension).
 template <typename Emit>
 KS_HD void ks_feed(KsSeg& g, bool& open, double x, double st, int o, Emit&& emit) {
     const int key = ks_key(st);
     const KsStep t = ks_step_m(x, g.sh);
-    if (open && key != 0 && key == g.key && t.ok) {
-        ks_commit(g, t);
-        return;
-    }
-    if (open) emit(g);
-    ks_open(g, key, o, x);
+    const bool cont = open && key != 0 && key == g.key && t.ok;
+    if (open && !cont) emit(g);
+    const double p = g.p + t.r;
+    g.p = cont ? p : 0.0;
+    g.lo = cont ? fmin(g.lo, p) : INFINITY;
+    g.hi = cont ? fmax(g.hi, p) : -INFINITY;
+    g.n = cont ? g.n + 1 : 0;
+    g.a = cont ? g.a : o;
+    g.xa = cont ? g.xa : x;
+    g.sh = cont ? g.sh : 52 - ((key & 2047) - 1023);
+    g.key = cont ? g.key : key;
     open = true;
 }
 
