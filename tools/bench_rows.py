@@ -1,6 +1,8 @@
 """Timings of the SURVEY §8 rows beside the headline (one MI355X): each row's
-device call at a production-like size (HIP-synchronised wall time, median of
-reps, inputs resident in HBM), next to the CPU restatement (oracle/, one
+device call at a production-like size, inputs resident in HBM: "gpu_s" is the
+time per call with calls back to back (HIP events on the library's stream, as
+bench.py times its steps), "call_s" the median of single calls between host
+syncs (host launch and sync latency included) -- next to the CPU restatement (oracle/, one
 thread, OMP_NUM_THREADS=1, kind "port") on a bounded sample of the same
 workload, scaled to the row's unit. Prints one JSON line per row.
 
@@ -25,6 +27,13 @@ import oracle  # noqa: E402
 from amd import lshkm  # noqa: E402
 
 
+class GpuTime(float):
+    """Seconds per call, back to back (HIP events on the library's stream around
+    reps calls, as bench.py times its steps); .call: the median of single calls
+    each bracketed by host syncs (host launch and sync latency included)."""
+    call = None
+
+
 def gpu_time(ctx, fn, reps=5):
     fn()
     ctx.sync()
@@ -36,7 +45,17 @@ def gpu_time(ctx, fn, reps=5):
         ctx.sync()
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
-    return float(np.median(ts))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    ctx.sync()
+    torch.cuda.synchronize()
+    t = GpuTime(e0.elapsed_time(e1) / 1e3 / reps)
+    t.call = float(np.median(ts))
+    return t
 
 
 def cpu_time(fn):
@@ -49,9 +68,11 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
 
 
 def emit(row, unit, units, t_gpu, cpu=None, note="", bytes_per_unit=None):
-    line = {"row": row, "unit": unit, "units": units, "gpu_s": t_gpu, "gpu_rate": units / t_gpu}
+    line = {"row": row, "unit": unit, "units": units, "gpu_s": float(t_gpu), "gpu_rate": units / t_gpu}
+    if getattr(t_gpu, "call", None) is not None:
+        line["call_s"] = t_gpu.call          # one call between host syncs
     if bytes_per_unit:
-        # algorithmic HBM bytes of the whole call (stated per unit) over its wall time
+        # algorithmic HBM bytes of the whole call (stated per unit) over its time per call
         gbs = units * bytes_per_unit / t_gpu / 1e9
         line["roofline"] = {"bound": "hbm", "bytes_per_unit": bytes_per_unit, "achieved": gbs,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
