@@ -638,6 +638,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         }
     }
     __syncthreads();
+#if defined(ABL_LIST_PROLOGUE)   // timing experiments only: the LIST form stops after its image load
+    if (LIST) return;
+#endif
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = lane & 31, h = lane >> 5;
@@ -2101,7 +2104,9 @@ __device__ inline void fix_row(const FusedArgs& a, const double* pts, const doub
             const double lo = floor(y - B), hi = floor(y + B);
             int32_t hv = (int32_t)lo;
             if (lo != hi) {                          // the same decision in all 4 lanes
+#if !defined(ABL_HF_NOX87)   // timing experiments only: the provisional value kept
                 hv = fixup_floor_x87(xrow, pts, f, tt, a.w);
+#endif
                 if (q == 0) atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
             }
 #pragma unroll

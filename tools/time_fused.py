@@ -44,5 +44,5 @@ for _ in range(5):
 t1.record()
 torch.cuda.synchronize()
 print(f"{os.path.basename(os.environ.get('LSHKM_LIB', 'liblshkm.so'))}: fused pass {np.median(ts):.3f} ms, "
-      f"whole call {t0.elapsed_time(t1) / 5:.3f} ms, ambiguous {ctx.stat(lshkm.STAT_ASSIGN_AMBIG) // 5}, hash fix-up rows {ctx.stat(lshkm.STAT_HASH_FIX) // 5}, "
+      f"whole call {t0.elapsed_time(t1) / 5:.3f} ms, ambiguous {ctx.stat(lshkm.STAT_ASSIGN_AMBIG) // 5}, hash fix-up rows {ctx.stat(lshkm.STAT_HASH_FIX) // 5}, soft-x87 hash values {ctx.stat(lshkm.STAT_HASH_EXACT) // 5}, "
       f"checksum {int(assign.sum().item())} {float(dist.sum().item()):.6f}", flush=True)
