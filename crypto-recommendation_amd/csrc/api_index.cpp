@@ -581,7 +581,7 @@ static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign
     // LSHKM_KM_PATH=chain runs every (c, j) chain sequentially.
     const char* kp = getenv("LSHKM_KM_PATH");
     // fp64 rows: binade segments (update.hip / kmseg.h; the fp64 update of 1M x
-    // 100 rows, K = 256: 1.09 ms vs 2.68 ms for fixed point + the wide chains);
+    // 100 rows, K = 256: 0.93 ms vs 2.68 ms for fixed point + the wide chains);
     // LSHKM_KM_PATH=fx: the fixed-point form, =chain: every chain sequential
     if (X.f64 && !(kp && (!strcmp(kp, "fx") || !strcmp(kp, "chain")))) {
         const size_t wsb = km_seg_ws_bytes(N, K, d);
