@@ -365,7 +365,6 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
     mfma_ok = d == 128 && LK <= 32;
     std::vector<_Float16> vh, vl;
     std::vector<double> v1;
-    std::vector<float> v32;
     if (mfma_ok) {
         vh.assign(64 * 128, (_Float16)0.f);
         vl.assign(64 * 128, (_Float16)0.f);
@@ -386,13 +385,6 @@ int ProjTable::upload(hipStream_t s, int metric_, int d_, int L_, int k_, float 
         LSHKM_HIP(hipMemcpyAsync(vh_d.p, vh.data(), vh.size() * 2, hipMemcpyHostToDevice, s));
         LSHKM_HIP(hipMemcpyAsync(vl_d.p, vl.data(), vl.size() * 2, hipMemcpyHostToDevice, s));
         LSHKM_HIP(hipMemcpyAsync(v1_d.p, v1.data(), LK * 8, hipMemcpyHostToDevice, s));
-        if (metric == LSHKM_METRIC_EUCLIDEAN) {
-            v32.assign(32 * 128, 0.f);
-            for (int f = 0; f < LK; f++)
-                for (int j = 0; j < 128; j++) v32[f * 128 + j] = V[(size_t)f * d + j];
-            if ((rc = v32_d.reserve(v32.size() * 4))) return rc;
-            LSHKM_HIP(hipMemcpyAsync(v32_d.p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice, s));
-        }
     }
     LSHKM_HIP(hipStreamSynchronize(s));   // host vectors go out of scope
     // host copies kept for introspection
@@ -495,15 +487,12 @@ int lshkm_lsh_hash_f64(lshkm_lsh lsh, const double* X, int64_t N, int32_t* tuple
 // fp64 rows the f32-MFMA kernel (rows rounded to f32 on load, the bound
 // widened accordingly) or the exact pass.
 static int assign_path(int metric, int d, int K, bool f64) {
-    const char* e = getenv("LSHKM_ASSIGN_PATH");
-    if (e && !strcmp(e, "exact")) return 2;
-    const bool f32 = e && !strcmp(e, "f32");
+    if (test_switch("LSHKM_ASSIGN_PATH", "exact")) return 2;
+    const bool f32 = test_switch("LSHKM_ASSIGN_PATH", "f32");
     if (d == 128 && !f32 && !f64) {
-        const char* ff = getenv("LSHKM_FUSED_FORM");
-        if (metric == LSHKM_METRIC_EUCLIDEAN || !(ff && !strcmp(ff, "chunked"))) return 0;
+        if (metric == LSHKM_METRIC_EUCLIDEAN || !test_switch("LSHKM_FUSED_FORM", "chunked")) return 0;
     }
-    const char* fh = getenv("LSHKM_FUSED_HI");
-    if (!f32 && d <= 128 && K <= 512 && !(fh && !strcmp(fh, "0"))) return 3;
+    if (!f32 && d <= 128 && K <= 512 && !test_switch("LSHKM_FUSED_HI", "0")) return 3;
     return assign_dp(d) > 0 ? 1 : 2;
 }
 
@@ -512,13 +501,9 @@ static int assign_path(int metric, int d, int K, bool f64) {
 // f32(c) in f32, certified to 2^-20 relative -- inside the 1e-5 relative the
 // north star sets for float distances; cluster IDs stay bit-exact, and a row
 // whose bound fails gets the reference-order fp64 chain. LSHKM_DIST_EXACT: the
-// reference-order fp64 chain for every row (bit-exact distances). The
-// environment variable LSHKM_DIST=exact|certified overrides the context's mode
-// (experiments and A/B timing only).
+// reference-order fp64 chain for every row (bit-exact distances). The context's
+// mode alone decides (no environment override in the product library).
 static bool fast_dist_on(const lshkm_ctx_s* ctx) {
-    const char* e = getenv("LSHKM_DIST");
-    if (e && !strcmp(e, "exact")) return false;
-    if (e && (!strcmp(e, "certified") || !strcmp(e, "fast"))) return true;
     return ctx->dist_mode == LSHKM_DIST_CERTIFIED;
 }
 
@@ -532,8 +517,7 @@ static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int
     // K <= 1024, d <= 256: score every centroid in f32 first and run the exact
     // order only on the candidates the bound leaves (euclidean, and cosine on
     // fp32 rows); LSHKM_EXACT_PASS=full: every centroid
-    const char* ep = getenv("LSHKM_EXACT_PASS");
-    const bool prune = K <= 1024 && d <= 256 && !(ep && !strcmp(ep, "full")) &&
+    const bool prune = K <= 1024 && d <= 256 && !test_switch("LSHKM_EXACT_PASS", "full") &&
                        (metric == LSHKM_METRIC_EUCLIDEAN || !X.f64);
     if (!prune && (metric != LSHKM_METRIC_EUCLIDEAN || (!seg_counts && d > 256)))
         return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist, seg_counts,
@@ -556,8 +540,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
     // one pass for hashing + assignment: the euclidean index with euclidean
     // Lloyd (fused_ok: d = 128, L*k <= 32), or the cosine index with cosine Lloyd
     // on the hi-only form (k = 4)
-    const char* fh0 = getenv("LSHKM_FUSED_HI");
-    const bool hi_form = !(fh0 && !strcmp(fh0, "0"));
+    const bool hi_form = !test_switch("LSHKM_FUSED_HI", "0");
     const bool fuse_hash = lsh && path == 0 && lsh->metric == metric &&
                            (metric == LSHKM_METRIC_EUCLIDEAN ? lsh->proj.fused_ok
                                                              : (hi_form && lsh->proj.mfma_ok && lsh->proj.k == 4));
@@ -570,38 +553,43 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         const int rows_kind = path == 3 ? (X.f64 ? 2 : 1) : 0;
         const int Kpad = (K + 63) / 64 * 64;
         const bool cosine = metric != LSHKM_METRIC_EUCLIDEAN;
-        // hi-only scoring + 3-product refinement; LSHKM_FUSED_HI=0: the 3-product form alone
-        const char* fh = getenv("LSHKM_FUSED_HI");
-        const bool hi = !(fh && !strcmp(fh, "0"));
+        // hi-only scoring + 3-product refinement; test switch LSHKM_FUSED_HI=0: the 3-product form alone
+        const bool hi = hi_form;
+        // euclidean winner distances: the certified f32 form (default) or the
+        // reference-order fp64 chain (LSHKM_DIST_EXACT)
+        const bool fast = !cosine && rows_kind != 2 && fast_dist_on(ctx);
+        // exact distances of the hi-only pass: rows whose chain met an inexact
+        // square (glibc's pow(x, 2) may differ from x*x) are listed for the fix-up
+        const bool pwfix = !cosine && hi && !fast;
+        // ws_hfix regions: [hash fix-ups] then, cosine: [declines of the hi-only
+        // pass][declines of the refinement]; euclidean exact: [pow fix-ups]
+        const int nfix_regions = 1 + (cosine && hi ? 2 : 0) + (pwfix ? 1 : 0);
         const int64_t list_cap = N + FUSED_LIST_SLACK;
         const int64_t part_tiles = std::max<int64_t>((N + 31) / 32, (list_cap + 31) / 32 + FUSED_MAX_SEGS);
         if ((rc = ctx->ws_c32.reserve((size_t)Kpad * 128 * 2 * 2)) ||
             (rc = ctx->ws_cconst.reserve((size_t)(Kpad + 8) * 4 + (size_t)Kpad * 8)) ||
             (rc = ctx->ws_ambig.reserve((size_t)(N + FUSED_LIST_SLACK) * 4)) || (rc = ctx->ws_counter.reserve(64)) ||
             (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)) ||
-            ((fuse_hash || cosine) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8 * (cosine && hi ? 3 : 1)))) ||
-            (cosine && hi && (rc = ctx->ws_seg3.reserve((size_t)FUSED_MAX_SEGS * 2 * 4))) ||
+            ((fuse_hash || cosine || pwfix) && (rc = ctx->ws_hfix.reserve((size_t)(N + FUSED_LIST_SLACK) * 8 * nfix_regions))) ||
+            (((cosine && hi) || pwfix) && (rc = ctx->ws_seg3.reserve((size_t)FUSED_MAX_SEGS * 2 * 4))) ||
             (Kpad > 256 && (rc = ctx->ws_part.reserve((size_t)part_tiles * 64 * 16))) ||
             (hi && ((rc = ctx->ws_ambig2.reserve((size_t)list_cap * 4)) ||
                     (rc = ctx->ws_seg2.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)))) ||
             (fuse_hash && !cosine && !tuples && (rc = ctx->ws_tuples.reserve((size_t)std::max<int64_t>(N, 1) * lsh->proj.LK * 4))))
             return rc;
         unsigned long long* cnt = (unsigned long long*)ctx->ws_counter.p;
-        LSHKM_HIP(hipMemsetAsync(cnt, 0, 32, s));         // [0] ambiguous rows, [1] hash fix-up rows, [2] refined rows, [3] cosine declines
+        LSHKM_HIP(hipMemsetAsync(cnt, 0, 32, s));         // [0] ambiguous rows, [1] hash fix-up rows, [2] refined rows, [3] cosine declines / pow fix-ups
         _Float16* Ch = (_Float16*)ctx->ws_c32.p;
         _Float16* Cl = Ch + (size_t)Kpad * 128;
         float* cbound = (float*)ctx->ws_cconst.p;          // 4 floats, then cnh[Kpad]
         float* cnh = cbound + 8;
         double* nbv = (double*)(cnh + Kpad);               // cosine: [Kpad] sequential |c|^2 (Kpad % 64 == 0: aligned)
-        // euclidean winner distances: the certified f32 form (default) or the
-        // reference-order fp64 chain (LSHKM_DIST=exact)
-        const bool fast = !cosine && rows_kind != 2 && fast_dist_on(ctx);
         float* C32 = nullptr;
         float* rn32 = nullptr;
         // the f32 image also serves the K <= 256 gather when every centroid value
         // is an f32 (dataset rows: the first Lloyd iteration), exact as doubles
-        const char* g32e = getenv("LSHKM_GATHER32");         // "0": the fp64 winner rows always
-        if (fast || (!cosine && rows_kind != 2 && Kpad <= 256 && !(g32e && !strcmp(g32e, "0")))) {
+        // (test switch LSHKM_GATHER32=0: the fp64 winner rows always)
+        if (fast || (!cosine && rows_kind != 2 && Kpad <= 256 && !test_switch("LSHKM_GATHER32", "0"))) {
             if ((rc = ctx->ws_cf32.reserve((size_t)Kpad * 128 * 4 + (size_t)Kpad * 4))) return rc;
             C32 = (float*)ctx->ws_cf32.p;
             rn32 = C32 + (size_t)Kpad * 128;
@@ -631,8 +619,17 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             f.seg_counts2 = (int32_t*)ctx->ws_seg2.p;
             f.refined = cnt + 2;
         }
+        if (pwfix) {
+            f.cfix = (unsigned long long*)ctx->ws_hfix.p + (N + FUSED_LIST_SLACK);
+            f.cfix_counts = (int32_t*)ctx->ws_seg3.p;
+            f.cfix_count = cnt + 3;
+        }
+        if (cosine && rows_kind == 2) {
+            if ((rc = ctx->ws_xn2.reserve((size_t)std::max<int64_t>(N, 1) * 8))) return rc;
+            if ((rc = launch_row_sumsq(s, X.d(), N, d, (double*)ctx->ws_xn2.p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            f.xn2 = (const double*)ctx->ws_xn2.p;
+        }
         if (cosine) {
-            // ws_hfix regions: [hash fix-ups][declines of the hi-only pass][declines of the refinement]
             f.metric = 1; f.nbv = nbv;
             f.hfix = (unsigned long long*)ctx->ws_hfix.p; f.hfix_count = hi ? cnt + 1 : cnt + 3;
             if (hi) {
@@ -645,7 +642,6 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if (fuse_hash) {
             const ProjTable& pj = lsh->proj;
             f.Vh = pj.vh_d.as<_Float16>(); f.Vl = pj.vl_d.as<_Float16>(); f.PT = pj.PT_d.as<double>();
-            f.V32 = pj.v32_d.as<float>();
             f.tv = pj.t_d.as<float>(); f.pnorm = pj.pn_d.as<double>(); f.v1 = pj.v1_d.as<double>();
             f.rv = pj.r_d.as<int32_t>(); f.w = pj.w; f.L = pj.L; f.k = pj.k; f.LK = pj.LK; f.LKpad = pj.LKpad;
             f.nb = lsh->nb; f.phi = phi; f.bucket = bucket;
@@ -654,8 +650,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         }
         if (fuse_hash && ctx->side_init() == 0) {
             f.side = ctx->side_stream; f.fork = ctx->fork_ev; f.join = ctx->join_ev;
-            const char* dj = getenv("LSHKM_DEFER_JOIN");     // "0": join inside launch_fused (A/B)
-            f.defer_join = !cosine && !(dj && !strcmp(dj, "0"));   // euclidean: the exact pass also overlaps the fix-up
+            f.defer_join = !cosine;        // euclidean: the exact pass also overlaps the fix-up
             if (ctx->timing) f.side_timing = ctx->tev[2];
         }
         ctx->tev_side = false;
@@ -685,10 +680,10 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
             di[n] = STAT_ASSIGN_AMBIG; sp[n++] = cnt;
             if ((rc = launch_add_counters(s, (unsigned long long*)ctx->stats.p, n, di, sp))) { LSHKM_LAUNCH_CHECK(); return rc; }
         }
-        if (cosine) {
+        if (cosine || pwfix) {
             if ((rc = launch_cos_fix_seg(s, X, d, C, f.ncos_lists, f.cos_list, f.cos_counts, f.seg_rows, f.nseg, assign,
-                                         dist))) { LSHKM_LAUNCH_CHECK(); return rc; }
-            if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + STAT_COS_FIX, cnt + 3))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                                         dist, cosine ? 1 : 0))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + (cosine ? STAT_COS_FIX : STAT_POW_FIX), cnt + 3))) { LSHKM_LAUNCH_CHECK(); return rc; }
         }
     } else if (path == 1) {
         const int Kpad = (K + 63) / 64 * 64;

@@ -21,8 +21,7 @@ using namespace lshkm;
 int lshkm::hash_rows(lshkm_ctx ctx, int mode, Pts X, int64_t N, const ProjTable& pj, int64_t nb, int32_t* out_h,
                      int32_t* out_phi, int32_t* out_bucket, int32_t* mm) {
     if (N <= 0) return 0;
-    const char* e = getenv("LSHKM_HASH_PATH");
-    const bool force64 = e && !strcmp(e, "fp64");
+    const bool force64 = test_switch("LSHKM_HASH_PATH", "fp64");
     unsigned long long* stats = (unsigned long long*)ctx->stats.p;
     int rc;
     if (!X.f64 && pj.mfma_ok && !force64) {
@@ -74,16 +73,6 @@ int d2h(lshkm_ctx ctx, void* dst, const void* src, size_t bytes) {
 int build_csr(lshkm_ctx ctx, const int32_t* keys, int64_t kstride, int64_t N, int64_t nb, int32_t* idx,
               int64_t* row_ptr, int T = 1) {
     int rc;
-    // one-pass form for key ranges that fit an LDS counter image (LSHKM_CSR=onepass; being measured)
-    const char* cv = getenv("LSHKM_CSR");
-    if (nb <= 32768 && (cv && !strcmp(cv, "onepass"))) {
-        if ((rc = reserve(ctx, WS_SORT, csr1_scratch_bytes(N, nb, T)))) return rc;
-        if ((rc = csr_build_onepass(ctx->stream, keys, kstride, 1, T, N, nb, idx, row_ptr, ctx->ws[WS_SORT].p))) {
-            LSHKM_LAUNCH_CHECK();
-            return rc;
-        }
-        return 0;
-    }
     if ((rc = reserve(ctx, WS_SORT, sort_scratch_bytes(N, nb, T))) || (rc = reserve(ctx, WS_SKEYS, (size_t)N * T * 4)))
         return rc;
     if (N > 0 && (rc = stable_sort_by_key_batched(ctx->stream, keys, kstride, 1, nullptr, 0, T, N, nb,
@@ -578,19 +567,24 @@ static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign
         return rc;
     if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
     // Parallel exact sums (fixed point where the chain provably never rounds);
-    // LSHKM_KM_PATH=chain runs every (c, j) chain sequentially.
-    const char* kp = getenv("LSHKM_KM_PATH");
+    // test switch LSHKM_KM_PATH=chain runs every (c, j) chain sequentially.
+    const bool force_chain = test_switch("LSHKM_KM_PATH", "chain");
     // fp64 rows: binade segments (update.hip / kmseg.h; the fp64 update of 1M x
     // 100 rows, K = 256: 0.93 ms vs 2.68 ms for fixed point + the wide chains);
-    // LSHKM_KM_PATH=fx: the fixed-point form, =chain: every chain sequential
-    if (X.f64 && !(kp && (!strcmp(kp, "fx") || !strcmp(kp, "chain")))) {
+    // test switch LSHKM_KM_PATH=fx: the fixed-point form. The segment workspace
+    // is ~5 B per row element plus 2.5 KB per (cluster, dim): past KM_SEG_WS_CAP
+    // (or when it cannot be reserved, or K exceeds the composition grid's y
+    // limit) the fixed-point form runs instead -- the same exact sums.
+    if (X.f64 && !force_chain && !test_switch("LSHKM_KM_PATH", "fx") && K <= 65535) {
         const size_t wsb = km_seg_ws_bytes(N, K, d);
-        if ((rc = ctx->ws_range[11].reserve(wsb))) return rc;
-        if ((rc = launch_km_sums_seg(ctx->stream, X.d(), d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K,
-                                     N, sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        return 0;
+        if (wsb <= KM_SEG_WS_CAP && ctx->ws_range[11].reserve(wsb) == 0) {
+            if ((rc = launch_km_sums_seg(ctx->stream, X.d(), d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW),
+                                         K, N, sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            return 0;
+        }
+        (void)hipGetLastError();          // a failed reservation leaves no sticky error
     }
-    if (!(kp && !strcmp(kp, "chain"))) {
+    if (!force_chain) {
         if ((rc = ctx->ws_range[11].reserve(km_fx_ws_bytes(K, d)))) return rc;
         if ((rc = launch_km_sums_fx(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, N,
                                     sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
             if (s < d) {
                 const double xv = sizeof(TX) == 4 ? (double)b[s] : (double)xrow[s];
                 const double df = __dsub_rn(xv, crow[s]);
-                accd = __dadd_rn(accd, __dmul_rn(df, df));
+                accd = __dadd_rn(accd, gp_sq(df));
             }
     }
     const double part = __shfl_xor(accd, 32);
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(AS_THREADS, 2) void assign_mfma_kernel(
                 if (H + s < d) {
                     const double xv = sizeof(TX) == 4 ? (double)b[s] : (double)xrow[H + s];
                     const double df = __dsub_rn(xv, crow[H + s]);
-                    a2 = __dadd_rn(a2, __dmul_rn(df, df));
+                    a2 = __dadd_rn(a2, gp_sq(df));
                 }
             assign[row] = ni1;
             dist[row] = sqrt(a2);
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(64 * XB_WAVES) void assign_exact_batch_kernel(
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         const double df = __dsub_rn(xj, cv[i]);
-                        acc[r][i] = __dadd_rn(acc[r][i], __dmul_rn(df, df));
+                        acc[r][i] = __dadd_rn(acc[r][i], gp_sq(df));
                     }
                 }
             }
@@ -606,7 +606,7 @@ __device__ inline double exact_euclid_b16(const TX* __restrict__ x, const double
         for (int t = 0; t < 16; t++)
             if (j0 + t < d) {
                 const double df = __dsub_rn((double)x[j0 + t], cv[t]);
-                acc = __dadd_rn(acc, __dmul_rn(df, df));
+                acc = __dadd_rn(acc, gp_sq(df));
             }
     }
     return sqrt(acc);
@@ -885,13 +885,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
 #ifndef XPW_ROWS
 #define XPW_ROWS 4       // C5 whole call: 2 rows per wave (segmented) 5.46-5.51 ms; flat 2 / 4 / 8: 4.97 / 4.82-4.91 / 4.95-5.08
 #endif
-#ifndef XPW_OFF
-#define XPW_OFF 0       // 1: the 2-rows-per-wave form (A/B)
-#endif
 constexpr int XPW_MAXSEG = 4096;
-#ifndef XPN_FLAT
-#define XPN_FLAT 0      // K <= 256 through the flat form as well (being measured)
-#endif
 template <typename TX, int MET = 0, int NCH = 16, int R = XPW_ROWS>
 __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_wide_kernel(
     const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
@@ -1076,7 +1070,8 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
                        cconst, metric);
     // K <= 256: 8 rows per wave over 4 chunks; K <= 1024: 2 rows per wave over 16
     const bool wide = Kpad > 256;
-    const int R = wide ? (XPW_OFF ? XP_WR : XPW_ROWS) : XP_R;     // groups of R rows
+    const bool flat = wide && (!seg_counts || nseg <= XPW_MAXSEG);
+    const int R = wide ? (flat ? XPW_ROWS : XP_WR) : XP_R;     // groups of R rows
     const int64_t groups = (max_rows + R - 1) / R;
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
 #define XP_LAUNCH(TX, NCH, RR, MT, XP)                                                                              \
@@ -1086,17 +1081,11 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
     hipLaunchKernelGGL((assign_pruned_wide_kernel<TX, MT, NC, RW>), dim3((unsigned)wblocks), dim3(64 * XP_WAVES), 0, s, \
                        XP, d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, nseg)
     const int64_t wblocks = std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 1024);
-    if (wide && !XPW_OFF && (!seg_counts || nseg <= XPW_MAXSEG)) {
+    if (flat) {
         if (metric == 1) {
             if (X.f64) XPW_LAUNCH(double, 1, 16, XPW_ROWS, X.d()); else XPW_LAUNCH(float, 1, 16, XPW_ROWS, X.f());
         } else {
             if (X.f64) XPW_LAUNCH(double, 0, 16, XPW_ROWS, X.d()); else XPW_LAUNCH(float, 0, 16, XPW_ROWS, X.f());
-        }
-    } else if (!wide && XPN_FLAT && (!seg_counts || nseg <= XPW_MAXSEG)) {
-        if (metric == 1) {
-            if (X.f64) XPW_LAUNCH(double, 1, 4, XP_R, X.d()); else XPW_LAUNCH(float, 1, 4, XP_R, X.f());
-        } else {
-            if (X.f64) XPW_LAUNCH(double, 0, 4, XP_R, X.d()); else XPW_LAUNCH(float, 0, 4, XP_R, X.f());
         }
     } else if (metric == 1) {
         if (X.f64) {

@@ -3,8 +3,27 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#ifdef LSHKM_TEST_SWITCHES
+#include <cstdlib>
+#include <cstring>
+#endif
 
 namespace lshkm {
+
+// Path switches for the tests' A/B comparisons (one kernel path forced against
+// another, bit for bit). Compiled only into the test build liblshkm_test.so
+// (-DLSHKM_TEST_SWITCHES, `make test`); the product library liblshkm.so reads
+// no environment and always takes the default paths.
+inline bool test_switch(const char* name, const char* value) {
+#ifdef LSHKM_TEST_SWITCHES
+    const char* e = std::getenv(name);
+    return e && !std::strcmp(e, value);
+#else
+    (void)name;
+    (void)value;
+    return false;
+#endif
+}
 
 // Thread-local last error, surfaced through lshkm_last_error().
 void set_error(const std::string& msg);
@@ -60,7 +79,8 @@ enum Stat {
     STAT_REFINED = 5,        // rows the hi-only fused pass left to the 3-product refinement
     STAT_HASH_FIX = 6,       // rows the fused pass listed for the hash fix-up (an uncertified floor / sign)
     STAT_REC_SOFT = 7,       // clustering-recommender similarities decided by the x87 chain (IpAcc declined)
-    STAT_COUNT = 8
+    STAT_POW_FIX = 8,        // euclidean winner distances redone with glibc's pow(x, 2) (an inexact square)
+    STAT_COUNT = 9
 };
 
 constexpr int WAVE = 64;

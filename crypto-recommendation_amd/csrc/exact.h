@@ -5,18 +5,26 @@
 //   cosineDistance     lib/data_structures/cust_vector.hpp:139-155
 //     1 - (long double) inner product / (sqrt(sum x^2) * sqrt(sum c^2))
 // `this` is the point x (fp32 or fp64 values), `in` the centroid c (fp64).
-// pow(v, 2) is v*v here (identical whenever v is a difference of
-// fp32 values, i.e. for every dataset-row centroid of fp32 data; within an ulp
-// otherwise). No FMA contraction.
+// pow(v, 2) is gp_sq(v) (gpow2.h): glibc's own result, bit for bit. No FMA
+// contraction.
 #pragma once
 #include "softx87.h"
+#include "gpow2.h"
+
+// pow(v, 2) of a value stored as T: an fp32 value squares exactly in fp64
+// (48 significant bits, no underflow), so only fp64 values need gp_sq.
+template <typename T>
+__device__ inline double sq_of(double v) {
+    if constexpr (sizeof(T) == 4) return __dmul_rn(v, v);
+    else return gp_sq(v);
+}
 
 template <typename T>
 __device__ inline double exact_euclid(const T* __restrict__ x, const double* __restrict__ c, int d) {
     double acc = 0.0;
     for (int j = 0; j < d; j++) {
         const double df = __dsub_rn((double)x[j], c[j]);
-        acc = __dadd_rn(acc, __dmul_rn(df, df));
+        acc = __dadd_rn(acc, gp_sq(df));
     }
     return sqrt(acc);
 }
@@ -43,8 +51,8 @@ __device__ inline double exact_cosine_x87_soft(const T* __restrict__ x, const U*
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], cj = (double)c[j];
         ip = sx_add_double(ip, __dmul_rn(xj, cj));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(cj, cj));
+        a = __dadd_rn(a, sq_of<T>(xj));
+        b = __dadd_rn(b, sq_of<U>(cj));
     }
     return one_minus(x87_quot(ip, __dmul_rn(sqrt(a), sqrt(b))));
 }
@@ -61,8 +69,8 @@ __device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __re
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], cj = (double)c[j];
         ip.add(__dmul_rn(xj, cj));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(cj, cj));
+        a = __dadd_rn(a, sq_of<T>(xj));
+        b = __dadd_rn(b, sq_of<U>(cj));
     }
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
 }
@@ -110,11 +118,53 @@ __device__ inline double exact_cosine_x87_pf(const T* __restrict__ x, const U* _
             if (!VEC && j0 + t >= d) break;
             const double xj = (double)xs[t], cj = (double)cs[t];
             ip.add(__dmul_rn(xj, cj));
-            a = __dadd_rn(a, __dmul_rn(xj, xj));
-            b = __dadd_rn(b, __dmul_rn(cj, cj));
+            a = __dadd_rn(a, sq_of<T>(xj));
+            b = __dadd_rn(b, sq_of<U>(cj));
         }
     }
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
+}
+
+// The reference's euclidean distance lane per row with the next 8 terms' loads
+// in flight (the pow fix-up list of the hi-only pass; VEC as above).
+template <bool VEC, typename T, typename U>
+__device__ inline double exact_euclid_pf(const T* __restrict__ x, const U* __restrict__ c, int d) {
+    constexpr int B = 8;
+    double acc = 0.0;
+    T xn[B];
+    U cn[B];
+    auto load = [&](int j0) {
+        if constexpr (VEC) {
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                const float4 v = *reinterpret_cast<const float4*>(x + j0 + 4 * t);
+                xn[4 * t] = v.x; xn[4 * t + 1] = v.y; xn[4 * t + 2] = v.z; xn[4 * t + 3] = v.w;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const double2 v = *reinterpret_cast<const double2*>(c + j0 + 2 * t);
+                cn[2 * t] = v.x; cn[2 * t + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < B; t++)
+                if (j0 + t < d) { xn[t] = x[j0 + t]; cn[t] = c[j0 + t]; }
+        }
+    };
+    load(0);
+    for (int j0 = 0; j0 < d; j0 += B) {
+        T xs[B];
+        U cs[B];
+#pragma unroll
+        for (int t = 0; t < B; t++) { xs[t] = xn[t]; cs[t] = cn[t]; }
+        if (j0 + B < d) load(j0 + B);
+#pragma unroll
+        for (int t = 0; t < B; t++) {
+            if (!VEC && j0 + t >= d) break;
+            acc = __dadd_rn(acc, gp_sq(__dsub_rn((double)xs[t], (double)cs[t])));
+        }
+    }
+    return sqrt(acc);
 }
 
 // fp32 rows of d % 16 == 0 (16-B aligned rows)
@@ -191,8 +241,8 @@ __device__ inline int cosine_interval(const T* __restrict__ x, const U* __restri
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], cj = (double)c[j];
         ip.add(__dmul_rn(xj, cj));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(cj, cj));
+        a = __dadd_rn(a, sq_of<T>(xj));
+        b = __dadd_rn(b, sq_of<U>(cj));
     }
     double q = 0.0, qr = 0.0;
     const int st = ip.quot_status(__dmul_rn(sqrt(a), sqrt(b)), q, qr);
@@ -208,8 +258,8 @@ __device__ inline bool cosine_fast(const T* __restrict__ x, const U* __restrict_
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], cj = (double)c[j];
         ip.add(__dmul_rn(xj, cj));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
-        b = __dadd_rn(b, __dmul_rn(cj, cj));
+        a = __dadd_rn(a, sq_of<T>(xj));
+        b = __dadd_rn(b, sq_of<U>(cj));
     }
     double q;
     if (!ip.quot(__dmul_rn(sqrt(a), sqrt(b)), q)) return false;
@@ -226,7 +276,7 @@ __device__ inline bool cosine_fast_nb(const T* __restrict__ x, const U* __restri
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j];
         ip.add(__dmul_rn(xj, (double)c[j]));
-        a = __dadd_rn(a, __dmul_rn(xj, xj));
+        a = __dadd_rn(a, sq_of<T>(xj));
     }
     double q;
     if (!ip.quot(__dmul_rn(sqrt(a), sqrt(nbv)), q)) return false;
@@ -251,7 +301,7 @@ __device__ inline double exact_dist(const T* __restrict__ x, const U* __restrict
         double acc = 0.0;
         for (int j = 0; j < d; j++) {
             const double df = __dsub_rn((double)x[j], (double)c[j]);
-            acc = __dadd_rn(acc, __dmul_rn(df, df));
+            acc = __dadd_rn(acc, gp_sq(df));
         }
         return sqrt(acc);
     }

@@ -179,12 +179,8 @@ __device__ inline void tile_mfma(const _Float16* ah_row, const _Float16* al_row,
         const half8 ah = *reinterpret_cast<const half8*>(ah_row + 16 * s);
         const half8 al = *reinterpret_cast<const half8*>(al_row + 16 * s);
         acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc_hi, 0, 0, 0);
-#ifndef ABL_NOLO   // timing experiments only: results are wrong without the lo products
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc_lo, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc_lo, 0, 0, 0);
-#else
-        (void)al;
-#endif
     }
 }
 
@@ -315,7 +311,7 @@ __global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
         const double* crow = a.C64 + (size_t)I1 * FU_D;
         for (int j = 0; j < FU_D / 2; j++) {
             const double df = __dsub_rn((double)xrow[j], crow[j]);
-            accd = __dadd_rn(accd, __dmul_rn(df, df));
+            accd = __dadd_rn(accd, gp_sq(df));
         }
     }
     const double part = __shfl_xor(accd, 32);
@@ -325,7 +321,7 @@ __global__ __launch_bounds__(FU_THREADS, 2) void fused_kernel(FusedArgs a) {
             const double* crow = a.C64 + (size_t)I1 * FU_D;
             for (int j = FU_D / 2; j < FU_D; j++) {
                 const double df = __dsub_rn((double)xrow[j], crow[j]);
-                s2 = __dadd_rn(s2, __dmul_rn(df, df));
+                s2 = __dadd_rn(s2, gp_sq(df));
             }
             a.assign[row] = I1;
             a.dist[row] = sqrt(s2);
@@ -459,13 +455,8 @@ __device__ inline void load_x64_step(const FusedArgs& a, int64_t rowc, int st, i
     }
 }
 
-// hi-only kernel's winner-row loads; ABL_CHAIN_NOLOAD (timing experiments
-// only, results invalid): values made from the row in registers instead
-#if defined(ABL_CHAIN_NOLOAD)
-#define CHAIN_LD(ptr, xi) make_double2((double)xf[(xi)] * 0.75, (double)xf[(xi) + 1] * 0.75)
-#else
+// hi-only kernel's winner-row loads
 #define CHAIN_LD(ptr, xi) (*reinterpret_cast<const double2*>(ptr))
-#endif
 
 // Scores of one 32-centroid tile: t = (hi + lo) + (-|c|^2/2) on packed f32
 // (D rows of registers 4g..4g+3 are centroids 8g+4h..+3 of the tile).
@@ -638,9 +629,6 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
         }
     }
     __syncthreads();
-#if defined(ABL_LIST_PROLOGUE)   // timing experiments only: the LIST form stops after its image load
-    if (LIST) return;
-#endif
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = lane & 31, h = lane >> 5;
@@ -936,17 +924,12 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 if (fix) hfix_seg[base + __popcll(fb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
             }
         } else {
-#if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
-        if (h == 1 && valid && cert) { a.assign[row] = I1; a.dist[row] = 0.0; }
-#elif FP_KEEP_X
+#if FP_KEEP_X
         {
             // exact row still in registers (B-operand layout): lane half h owns
             // dims 16s+8h..+7; only the winner's fp64 row is loaded
             const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
             double acc = 0.0;
-#if defined(ABL_CHAIN_TREE)
-            double tacc[4] = {0.0, 0.0, 0.0, 0.0};
-#endif
             double2 cbuf[CHAIN_PF][4];
             double2 xnext[4];                 // fp64 rows: the exact values, one step ahead
             const int64_t rowc = valid ? row : a.N - 1;
@@ -980,13 +963,9 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                     const double2 cc = cur[j];
                     const double d0 = __dsub_rn(xcur[j].x, cc.x);
                     const double d1 = __dsub_rn(xcur[j].y, cc.y);
-                    sq[2 * j] = __dmul_rn(d0, d0);
-                    sq[2 * j + 1] = __dmul_rn(d1, d1);
+                    sq[2 * j] = gp_sq(d0);
+                    sq[2 * j + 1] = gp_sq(d1);
                 }
-#if defined(ABL_CHAIN_TREE)   // timing experiments only: per-lane sums in any order (results invalid)
-#pragma unroll
-                for (int j = 0; j < 8; j++) tacc[j & 3] = __dadd_rn(tacc[j & 3], sq[j]);
-#else
                 if (h == 0) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
@@ -997,12 +976,7 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
                 acc = take_from_upper(acc);
-#endif
             }
-#if defined(ABL_CHAIN_TREE)
-            acc = __dadd_rn(__dadd_rn(tacc[0], tacc[1]), __dadd_rn(tacc[2], tacc[3]));
-            acc = __dadd_rn(acc, swap_halves(acc, h));
-#endif
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
                 a.dist[row] = sqrt(acc);
@@ -1027,10 +1001,10 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                 const double2 c1 = *reinterpret_cast<const double2*>(cq + 4 * u + 2);
                 const double d0 = __dsub_rn((double)xv.x, c0.x), d1 = __dsub_rn((double)xv.y, c0.y);
                 const double d2 = __dsub_rn((double)xv.z, c1.x), d3 = __dsub_rn((double)xv.w, c1.y);
-                sq[4 * u] = __dmul_rn(d0, d0);
-                sq[4 * u + 1] = __dmul_rn(d1, d1);
-                sq[4 * u + 2] = __dmul_rn(d2, d2);
-                sq[4 * u + 3] = __dmul_rn(d3, d3);
+                sq[4 * u] = gp_sq(d0);
+                sq[4 * u + 1] = gp_sq(d1);
+                sq[4 * u + 2] = gp_sq(d2);
+                sq[4 * u + 3] = gp_sq(d3);
             }
             double acc = 0.0;
 #pragma unroll
@@ -1096,13 +1070,6 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
 // One third of the MFMA work of the 3-product form, and only the hi image of
 // the centroids in LDS: up to 512 centroids per pass (K = 1024: 2 passes).
 constexpr int FH_KMAX = 512;
-// fused16.hip: the single-pass FAST form over 16-row tiles
-int launch_fused16(const FusedArgs& a, bool hash, bool mp, int nblk, hipStream_t s);
-static bool fused16_on() {
-    const char* v = getenv("LSHKM_F16");
-    return v && !strcmp(v, "1");
-}
-int fused16_waves();
 __host__ __device__ constexpr int fh_lds_bytes(int Kpad, bool hash) {
     return 16 + Kpad * FU_RS * 2 + Kpad * 4 + (hash ? 2 * 32 * FU_RS * 2 + FP_HC_BYTES : 0);
 }
@@ -1217,15 +1184,16 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
 
 // The same for fp64 rows (ROWS = 2): the exact x values re-read from the row
 // (L2) two 16-dim steps ahead (a rolled loop: unrolled, the loads of all steps
-// were hoisted and spilled), the |x|^2 chain and the halves' inner products
-// in one pass over the steps. Dims past d are zero in the row (load_x64_step)
-// and in the padded centroid copy: exact zero terms of both chains.
+// were hoisted and spilled) for the halves' inner products. Dims past d are
+// zero in the row (load_x64_step) and in the padded centroid copy: exact zero
+// terms. |x|^2 of a general double row needs glibc's pow(x, 2) per term
+// (gpow2.h): the row's sequential sum comes precomputed (a.xn2, row_sumsq).
 __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc, const double* __restrict__ crow_h,
                                                double nbv, int h, double& v) {
     double2 xn[4], xnn[4];
     load_x64_step(a, rowc, 0, h, xn);
     load_x64_step(a, rowc, 1, h, xnn);
-    double xa = 0.0, sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0, hold = 0.0;
+    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0, hold = 0.0;
     double2 cb[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 2 * j);
@@ -1243,17 +1211,6 @@ __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc,
 #pragma unroll
             for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 16 * (s + 1) + 2 * j);
         }
-        // |x|^2: the reference's sequential chain, halves alternating
-        if (h == 0) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) xa = __dadd_rn(xa, __dmul_rn(xv[j], xv[j]));
-        }
-        xa = take_from_lower(xa);
-        if (h == 1) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) xa = __dadd_rn(xa, __dmul_rn(xv[j], xv[j]));
-        }
-        xa = take_from_upper(xa);
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const double pj = __dmul_rn(xv[j], cv[j]);
@@ -1270,6 +1227,7 @@ __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc,
     const double sh0 = swap_halves(sh, h), sl0 = swap_halves(sl, h), ts0 = swap_halves(ts, h);
     const double mx0 = swap_halves(mx, h), hold0 = swap_halves(hold, h);
     if (h == 0) return 2;
+    const double xa = a.xn2[rowc];
     IpAcc ip;
     const double t = __dadd_rn(sh0, sh);
     const double bb = __dsub_rn(t, sh0);
@@ -1372,7 +1330,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
     if (threadIdx.x < 3) lcount[threadIdx.x] = 0;
     int32_t* ambig_seg = a.ambig + (int64_t)blockIdx.x * a.seg_rows;
     unsigned long long* hfix_seg = a.hfix + (int64_t)blockIdx.x * a.seg_rows;
-    unsigned long long* cfix_seg = MET == 1 ? a.cfix + (int64_t)blockIdx.x * a.seg_rows : nullptr;
+    unsigned long long* cfix_seg = a.cfix ? a.cfix + (int64_t)blockIdx.x * a.seg_rows : nullptr;
     if (HASH) {
         for (int e = threadIdx.x; e < 32 * 16; e += FH_THREADS) {
             const int r = e >> 4, g = e & 15;
@@ -1417,25 +1375,12 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
             load_row_gen<ROWS>(a, rr < a.N ? rr : a.N - 1, h, dst);
             return;
         }
-#if defined(ABL_XLD_COAL)   // timing experiments only: lane quads read 64 contiguous bytes (wrong layout)
-        const int64_t rr = tl * 32 + (lane >> 2);
-        const float* xr = a.X + (rr < a.N ? rr : a.N - 1) * FU_D + 4 * (lane & 3);
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * (s & 3) + 64 * (s >> 2));
-            const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * (s & 3) + 64 * (s >> 2) + 2048);
-#else
         const int64_t rr = tl * 32 + col;
-#if defined(ABL_L2X)   // timing experiments only: every tile reads the same 4096 rows (L2 hits)
-        const float* xr = a.X + ((rr < a.N ? rr : a.N - 1) & 4095) * FU_D + 8 * h;
-#else
         const float* xr = a.X + (rr < a.N ? rr : a.N - 1) * FU_D + 8 * h;
-#endif
 #pragma unroll
         for (int s = 0; s < 8; s++) {
             const float4 p0 = *reinterpret_cast<const float4*>(xr + 16 * s);
             const float4 p1 = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
-#endif
             dst[8 * s + 0] = p0.x; dst[8 * s + 1] = p0.y; dst[8 * s + 2] = p0.z; dst[8 * s + 3] = p0.w;
             dst[8 * s + 4] = p1.x; dst[8 * s + 5] = p1.y; dst[8 * s + 6] = p1.z; dst[8 * s + 7] = p1.w;
         }
@@ -1477,11 +1422,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
             nxh = nx + nxr;                                     // |xh| <= |x| + |xr|
             x_ok = xn2f <= FU_RANGE * FU_RANGE;
         };
-#if defined(ABL_NOHASH)   // timing experiments only: no hash tile
-        constexpr bool hash_here = false;
-#else
         const bool hash_here = HASH;          // <HASH, MP>: the first pass only
-#endif
         if (!hash_here) {
 #pragma unroll
             for (int s = 0; s < 8; s++) {
@@ -1610,11 +1551,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
 #if MFMA_PRIO
         __builtin_amdgcn_s_setprio(MFMA_PRIO);
 #endif
-#if defined(ABL_NOCTILE)   // timing experiments only: one centroid tile
-        const int ntile_run = 1;
-#else
         const int ntile_run = ntile32;
-#endif
         auto run_tiles = [&](int ntl, int tgo) {
 #pragma unroll TILE_UNROLL
             for (int t = 0; t < ntl; t++) {
@@ -1673,14 +1610,9 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
         const float M2 = fmaxf(fmaxf(m2, om2), fminf(m1, om1));
         const int I1 = (om1 > m1 || (om1 == m1 && oi1 < i1)) ? oi1 : i1;
         const float M1 = fmaxf(m1, om1);
-#if !defined(ABL_NOCHAIN)
         // the winner's fp64 row: the first loads go out before the certificate
         // and the list append
-#if defined(ABL_CLD_COAL)   // timing experiments only: each lane quad reads 64 contiguous bytes of one row
-        const double* crow = a.C64 + (size_t)__shfl(I1, lane & ~3) * FU_D + 2 * (lane & 3);
-#else
         const double* crow = a.C64 + (size_t)I1 * FU_D + 8 * h;
-#endif
         // GATH: piece u of a step holds points 8u..8u+7, lane L the 16-B chunk
         // (L & 7) ^ swz(p) of point p = 8u + (L >> 3) (swz(p) = (p >> 1) & 7: the
         // lanes of each ds_read_b128 group hit 16 distinct 4-bank groups).
@@ -1781,7 +1713,6 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
 #pragma unroll
                 for (int j = 0; j < 4; j++) cbuf[s][j] = CHAIN_LD(crow + 16 * s + 2 * j, 8 * s + 2 * j);
         }
-#endif
         const bool cert = x_ok && c_ok && ((double)M2 < (double)M1 - 2.0 * E);
 
         // euclidean fast distance (fastd): the winner's distance from f32(c)
@@ -1855,9 +1786,6 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                 a.dist[row] = fdist;
             }
         } else {
-#if defined(ABL_NOCHAIN)   // timing experiments only: no winner distance
-        if (h == 1 && valid && cert) { a.assign[row] = I1; a.dist[row] = 0.0; }
-#else
         {
             // winner distance in reference order from the row kept in registers:
             // the lane halves take turns on the chain, 8 dims each
@@ -1865,9 +1793,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
             __builtin_amdgcn_s_setprio(CHAIN_PRIO);
 #endif
             double acc = 0.0;
-#if defined(ABL_CHAIN_TREE)
-            double tacc[4] = {0.0, 0.0, 0.0, 0.0};
-#endif
+            bool pw_hard = false;
             if constexpr (GATH) {
                 wait_step();                                               // step 0 landed
                 asm volatile("" ::: "memory");
@@ -1914,11 +1840,12 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                     const double d1 = __dsub_rn(xcur[j].y, cc.y);
                     sq[2 * j] = __dmul_rn(d0, d0);
                     sq[2 * j + 1] = __dmul_rn(d1, d1);
+                    // the reference squares with glibc pow: x*x is its value when
+                    // the square is exact; otherwise the row's distance is redone
+                    // by the fix-up (gpow2.h) -- no row of dataset-row centroids
+                    // of the synthetic data, every row after an update
+                    pw_hard |= !gp_sq_is(d0, sq[2 * j]) || !gp_sq_is(d1, sq[2 * j + 1]);
                 }
-#if defined(ABL_CHAIN_TREE)   // timing experiments only: per-lane sums in any order (results invalid)
-#pragma unroll
-                for (int j = 0; j < 8; j++) tacc[j & 3] = __dadd_rn(tacc[j & 3], sq[j]);
-#else
                 if (h == 0) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
@@ -1929,21 +1856,26 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                     for (int j = 0; j < 8; j++) acc = __dadd_rn(acc, sq[j]);
                 }
                 acc = take_from_upper(acc);
-#endif
             }
-#if defined(ABL_CHAIN_TREE)
-            acc = __dadd_rn(__dadd_rn(tacc[0], tacc[1]), __dadd_rn(tacc[2], tacc[3]));
-            acc = __dadd_rn(acc, swap_halves(acc, h));
-#endif
+            const bool hard = pw_hard || __shfl_xor((int)pw_hard, 32) != 0;
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
-                a.dist[row] = sqrt(acc);
+                if (!hard) a.dist[row] = sqrt(acc);
+            }
+            // the pow fix-up list (cfix, counts in slot 2): certified winners
+            // whose chain met an inexact square
+            const unsigned long long pb = __ballot(h == 1 && valid && cert && hard);
+            if (pb) {
+                const int leader = __builtin_ctzll(pb);
+                int base = 0;
+                if (lane == leader) base = atomicAdd(lcount + 2, __popcll(pb));
+                base = __shfl(base, leader);
+                if (h == 1 && valid && cert && hard) cfix_seg[base + __popcll(pb & ((1ull << lane) - 1ull))] = (unsigned long long)row;
             }
 #if CHAIN_PRIO
             __builtin_amdgcn_s_setprio(0);
 #endif
         }
-#endif
         }
         PT_MARK(2)
         if (xpf) {
@@ -1958,7 +1890,8 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
         a.seg_counts[2 * blockIdx.x + threadIdx.x] = c;
         if (c) atomicAdd(threadIdx.x == 0 ? a.ambig_count : a.hfix_count, (unsigned long long)c);
     }
-    if (MET == 1 && threadIdx.x == 2 && (!MP || (!HASH && a.pass_last))) {
+    // slot 2: cosine declines / euclidean pow fix-ups (exact distances)
+    if ((MET == 1 || !fastd) && threadIdx.x == 2 && (!MP || (!HASH && a.pass_last))) {
         const int c = lcount[2];
         a.cfix_counts[2 * blockIdx.x + 1] = c;
         if (c) atomicAdd(a.cfix_count, (unsigned long long)c);
@@ -2104,9 +2037,7 @@ __device__ inline void fix_row(const FusedArgs& a, const double* pts, const doub
             const double lo = floor(y - B), hi = floor(y + B);
             int32_t hv = (int32_t)lo;
             if (lo != hi) {                          // the same decision in all 4 lanes
-#if !defined(ABL_HF_NOX87)   // timing experiments only: the provisional value kept
                 hv = fixup_floor_x87(xrow, pts, f, tt, a.w);
-#endif
                 if (q == 0) atomicAdd(a.stats + STAT_HASH_EXACT, 1ull);
             }
 #pragma unroll
@@ -2219,7 +2150,7 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
             double b = 0.0;
             for (int j = 0; j < d; j++) {
                 const double cj = C[(size_t)c * d + j];
-                b = __dadd_rn(b, __dmul_rn(cj, cj));
+                b = __dadd_rn(b, gp_sq(cj));
             }
             nbv[c] = b;
         }
@@ -2331,7 +2262,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     FusedArgs a;
     a.X = f.X; a.N = f.N;
     a.Ch = f.Ch; a.Cl = f.Cl; a.cnh = f.cnh; a.cbound = f.cbound; a.C64 = f.C64; a.Kpad = f.Kpad;
-    a.Vh = f.Vh; a.Vl = f.Vl; a.V32 = f.V32; a.PT = f.PT; a.tv = f.tv; a.pnorm = f.pnorm; a.v1 = f.v1; a.rv = f.rv;
+    a.Vh = f.Vh; a.Vl = f.Vl; a.PT = f.PT; a.tv = f.tv; a.pnorm = f.pnorm; a.v1 = f.v1; a.rv = f.rv;
     a.w = f.w; a.L = f.L; a.k = f.k; a.LK = f.LK; a.LKpad = f.LKpad; a.nb = f.nb;
     a.tuples = f.tuples; a.phi = f.phi; a.bucket = f.bucket; a.assign = f.assign; a.dist = f.dist;
     a.ambig = f.ambig; a.ambig_count = f.ambig_count; a.stats = f.stats;
@@ -2343,7 +2274,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     a.prof = nullptr;
     a.C32 = f.C32; a.rn32 = f.rn32;
     a.fast_dist = f.fast_dist && f.metric == 0 && f.rows != 2 && f.C32 && f.rn32 ? 1 : 0;
-    a.X64 = f.X64; a.d = f.rows == 0 ? FU_D : f.d;
+    a.X64 = f.X64; a.d = f.rows == 0 ? FU_D : f.d; a.xn2 = f.xn2;
     a.xvec = f.rows == 1 ? (f.d % 4 == 0 && ((uintptr_t)f.X & 15) == 0)
                          : (f.d % 2 == 0 && ((uintptr_t)f.X64 & 15) == 0);
     a.Cd = f.Cd;
@@ -2369,8 +2300,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         }
     } report{s, prof_d};
 #endif
-    const char* force = getenv("LSHKM_FUSED_FORM");     // "chunked" forces the streaming form (tests)
-    const bool chunked = force && !strcmp(force, "chunked") && f.rows == 0;
+    const bool chunked = test_switch("LSHKM_FUSED_FORM", "chunked") && f.rows == 0;   // the streaming form (tests)
     const int npass = (f.Kpad + FP_KMAX - 1) / FP_KMAX;
     const bool multi_ok = npass == 1 || (f.part && f.part_bytes >= ((f.N + 31) / 32) * 64 * 16);
     // LIST refinement pass state: one slot per (segment, tile) of the list
@@ -2382,8 +2312,12 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         set_error("launch_fused: cosine runs the persistent form only (hashing: the hi-only form with k = 4)");
         return -1;
     }
-    if (f.metric == 1 && f.hi && (!f.cfix || !f.cfix_counts || !f.cfix_count)) {
-        set_error("launch_fused: the hi-only cosine form needs the decline list");
+    if (f.metric == 1 && f.rows == 2 && !f.xn2) {
+        set_error("launch_fused: cosine on fp64 rows needs the rows' sums of squares");
+        return -1;
+    }
+    if (f.hi && (f.metric == 1 || !a.fast_dist) && (!f.cfix || !f.cfix_counts || !f.cfix_count)) {
+        set_error("launch_fused: the hi-only cosine form needs the decline list, the exact euclidean one the pow fix-up list");
         return -1;
     }
     if (hash && (f.LK > 32 || f.L * f.k != f.LK)) {              // the fix-ups hold <= 32 functions per row
@@ -2410,10 +2344,6 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
         // the hi-only form strides by fh_waves() tiles per block (8 or 12)
         for (const int W : {FH_WAVES_MIN, FH_WAVES_MAX})
             a.seg_rows = std::max<int64_t>(a.seg_rows, (int64_t)W * 32 * ((ntiles + (int64_t)nblk * W - 1) / ((int64_t)nblk * W)));
-        {   // the 16-row form (fused16.hip)
-            const int64_t W = fused16_waves(), nt16 = (f.N + 15) / 16;
-            a.seg_rows = std::max<int64_t>(a.seg_rows, W * 16 * ((nt16 + (int64_t)nblk * W - 1) / ((int64_t)nblk * W)));
-        }
         a.seg_counts = f.seg_counts;
         if (!f.seg_counts || f.seg_cap < nblk || (int64_t)nblk * a.seg_rows > f.list_cap) {
             set_error("launch_fused: list workspace too small");
@@ -2445,13 +2375,11 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             // K = 1024): 5.09 ms vs 1.83 + 2.51 ms, HBM 8.9 GB vs 13.8 GB per call --
             // the block-wide image swaps line the waves up and cost the MFMA/VALU
             // overlap between them, more than the second read of X costs; opt-in.
-            const char* ti = getenv("LSHKM_HI_TWO_IMAGE");
-            const bool two_image = !cos && np1 == 2 && ti && !strcmp(ti, "1") && f.rows == 0;
+            const bool two_image = !cos && np1 == 2 && test_switch("LSHKM_HI_TWO_IMAGE", "1") && f.rows == 0;
             if (f.rows != 0) {
                 // general rows: one hi-only pass (Kpad <= 512), then the LIST form below
                 const size_t lh = (size_t)fh_lds_bytes(f.Kpad, false);
-                const char* gv = getenv("LSHKM_GATHER");
-                const bool gath = f.rows == 1 && f.Kpad <= FH_GATH_KMAX && !(gv && !strcmp(gv, "0"));
+                const bool gath = f.rows == 1 && f.Kpad <= FH_GATH_KMAX && !test_switch("LSHKM_GATHER", "0");
 #if defined(FH_WAVES_SET) && FH_WAVES_SET != 8
                 if (gath) { set_error("launch_fused: gather ring needs 8 waves"); return -1; }
 #else
@@ -2500,21 +2428,13 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                     }
                 } else if (np1 == 1) {
                     // K <= 256: the winner rows by the LDS-DMA gather (LSHKM_GATHER=0: register loads)
-                    const char* gv = getenv("LSHKM_GATHER");
 #if defined(FH_WAVES_SET) && FH_WAVES_SET != 8      // experiments: the gather ring is sized for 8 waves
-                    (void)gv;
                     if (false) {
 #else
-                    if (a.Kpad <= FH_GATH_KMAX && !(gv && !strcmp(gv, "0"))) {
+                    if (a.Kpad <= FH_GATH_KMAX && !test_switch("LSHKM_GATHER", "0")) {
                         const size_t lg = (size_t)fh_gath_off(a.Kpad, hash) + 8 * FH_GATH_WAVE;
-                        // the certified f32 winner distance (a.fast_dist) compiled in:
-                        // the 16-row form (fused16.hip) with LSHKM_F16=1 (being measured)
-                        if (a.fast_dist && fused16_on() && a.Kpad % 16 == 0) {
-                            if (launch_fused16(a, hash, false, nblk, s)) {
-                                set_error("launch_fused: 16-row form launch");
-                                return -1;
-                            }
-                        } else if (hash && a.fast_dist)
+                        // the certified f32 winner distance (a.fast_dist) compiled in
+                        if (hash && a.fast_dist)
                             hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);
                         else if (a.fast_dist)
                             hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);
@@ -2526,12 +2446,6 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                         FH_LAUNCH(true, false, 0);
                     } else {
                         FH_LAUNCH(false, false, 0);
-                    }
-                } else if (a.fast_dist && fused16_on()) {
-                    // the 16-row form for every slice (its own pass state layout)
-                    if (launch_fused16(a, hash && p == 0, true, nblk, s)) {
-                        set_error("launch_fused: 16-row form launch");
-                        return -1;
                     }
                 } else {
                     if (hash && p == 0) FH_LAUNCH(true, true, 0);
@@ -2597,6 +2511,10 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
             }
             f.final_list = f.list2;
             f.final_counts = f.seg_counts2;
+            if (!cos && !a.fast_dist && f.cfix) {      // the hi-only pass's pow fix-ups (exact distances)
+                f.ncos_lists = 1;
+                f.cos_list[0] = f.cfix; f.cos_counts[0] = f.cfix_counts;
+            }
             if (cos) {
                 f.ncos_lists = 2;
                 f.cos_list[0] = f.cfix; f.cos_counts[0] = f.cfix_counts;
@@ -2639,16 +2557,19 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     return kstatus("fused_kernel");
 }
 
-// Cosine winners listed by the fused kernels: lane per row, the x87 chain
-// (exact_cosine_x87_pf). CF_SPLIT blocks per list segment; both lists of a call
-// (the hi-only pass's declines and the refinement's) in ONE launch, so the
-// short list's lone chains (~40 us of latency) overlap the long one.
+// Winners listed by the fused kernels for their distance alone: lane per row.
+// Cosine (MET = 1): the certificate declined, the x87 chain decides
+// (exact_cosine_x87_pf). Euclidean (MET = 0, exact distances): a square of the
+// chain was inexact, so glibc's pow(x, 2) may differ from x*x -- the chain
+// again with gp_sq (exact_euclid_pf). CF_SPLIT blocks per list segment; both
+// lists of a call (the hi-only pass's and the refinement's) in ONE launch, so
+// the short list's lone chains (~40 us of latency) overlap the long one.
 constexpr int CF_SPLIT = 8;
 struct CosLists {
     const unsigned long long* list[2];
     const int32_t* counts[2];
 };
-template <typename TX>
+template <typename TX, int MET>
 __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__ X, int d, const double* __restrict__ C,
                                                           CosLists cl, int nseg, int64_t seg_rows,
                                                           const int32_t* __restrict__ assign, double* __restrict__ dist) {
@@ -2660,29 +2581,63 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__
     const int seg = b % nseg, part = b / nseg;
     const int n = cl.counts[li][2 * seg + 1];
     const unsigned long long* l = cl.list[li] + (int64_t)seg * seg_rows;
+    const bool vec = sizeof(TX) == 4 && d % 8 == 0 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)C & 15) == 0;
     for (int i = part * 256 + threadIdx.x; i < n; i += CF_SPLIT * 256) {
         const int64_t row = (int64_t)l[i];
-        if constexpr (sizeof(TX) == 4) {
-            if (d == FU_D) {
-                dist[row] = exact_cosine_x87_b16(X + row * FU_D, C + (size_t)assign[row] * FU_D, FU_D);
+        const TX* xr = X + row * d;
+        const double* cr = C + (size_t)assign[row] * d;
+        if constexpr (MET == 1) {
+            if (sizeof(TX) == 4 && d == FU_D) {
+                dist[row] = exact_cosine_x87_b16(reinterpret_cast<const float*>(xr), cr, FU_D);
                 continue;
             }
+            dist[row] = exact_cosine_x87_pf<false>(xr, cr, d);
+        } else {
+            if constexpr (sizeof(TX) == 4) {
+                if (vec) {
+                    dist[row] = exact_euclid_pf<true>(xr, cr, d);
+                    continue;
+                }
+            }
+            dist[row] = exact_euclid_pf<false>(xr, cr, d);
         }
-        dist[row] = exact_cosine_x87_pf<false>(X + row * d, C + (size_t)assign[row] * d, d);
     }
 }
 
+// out[i] = the reference's sum_j pow(x_ij, 2), j ascending (the |x|^2 of
+// cosineDistance, cust_vector.hpp:148-151) for fp64 rows, lane per row.
+__global__ __launch_bounds__(256) void row_sumsq_kernel(const double* __restrict__ X, int64_t N, int d,
+                                                         double* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256) {
+        const double* x = X + i * d;
+        double a = 0.0;
+        for (int j = 0; j < d; j++) a = __dadd_rn(a, gp_sq(x[j]));
+        out[i] = a;
+    }
+}
+
+int launch_row_sumsq(hipStream_t s, const double* X, int64_t N, int d, double* out) {
+    if (N <= 0) return 0;
+    const unsigned grid = (unsigned)std::min<int64_t>((N + 255) / 256, 4096);
+    hipLaunchKernelGGL(row_sumsq_kernel, dim3(grid), dim3(256), 0, s, X, N, d, out);
+    return kstatus("row_sumsq_kernel");
+}
+
 int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, int nlists, const unsigned long long* const* lists,
-                       const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist) {
+                       const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist,
+                       int metric) {
     if (nseg <= 0 || nlists <= 0) return 0;
     if (nlists > 2) return -1;                       // LSHKM_ERR_ARG
     CosLists cl{};
     for (int i = 0; i < nlists; i++) { cl.list[i] = lists[i]; cl.counts[i] = counts[i]; }
     const dim3 grid((unsigned)(nlists * nseg * CF_SPLIT));
-    if (X.f64)
-        hipLaunchKernelGGL(cos_fix_seg_kernel<double>, grid, dim3(256), 0, s, X.d(), d, C, cl, nseg, seg_rows, assign, dist);
-    else
-        hipLaunchKernelGGL(cos_fix_seg_kernel<float>, grid, dim3(256), 0, s, X.f(), d, C, cl, nseg, seg_rows, assign, dist);
+#define CF_LAUNCH(TX, M, XP) hipLaunchKernelGGL((cos_fix_seg_kernel<TX, M>), grid, dim3(256), 0, s, XP, d, C, cl, nseg, seg_rows, assign, dist)
+    if (metric == 1) {
+        if (X.f64) CF_LAUNCH(double, 1, X.d()); else CF_LAUNCH(float, 1, X.f());
+    } else {
+        if (X.f64) CF_LAUNCH(double, 0, X.d()); else CF_LAUNCH(float, 0, X.f());
+    }
+#undef CF_LAUNCH
     return kstatus("cos_fix_seg_kernel");
 }
 

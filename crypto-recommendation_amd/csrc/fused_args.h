@@ -1,5 +1,5 @@
 // fused_args.h — the argument block of the fused hash + assign kernels
-// (fused.hip: persistent and hi-only forms; fused16.hip: the 16-row-tile form).
+// (fused.hip: the persistent and hi-only forms).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -23,7 +23,6 @@ struct FusedArgs {
     // hash family (HASH only)
     const _Float16* Vh;      // [32][128] f16 hi of the projections (rows >= LK zero)
     const _Float16* Vl;
-    const float* V32;        // [32][128] f32 projections, euclidean (rows >= LK zero)
     const double* PT;        // [128][LKpad] fp64 projections (exact paths)
     const float* tv;         // [LK]
     const double* pnorm;     // [LK] ||v||_2 (rounded up)
@@ -54,6 +53,7 @@ struct FusedArgs {
     int32_t* seg_counts;
     BucketDiv bdiv;          // phi % nb by multiply-high
     const double* nbv;       // cosine: [K] sequential sum of c_j^2 (cust_vector.hpp:139-155)
+    const double* xn2;       // cosine, fp64 rows: [N] the rows' sequential sum of pow(x_j, 2)
     // multi-pass persistent form (K > 256): this launch scores centroid tiles
     // t0.. of the slice in Ch/Cl/cnh (Kpad rows); the running state per lane
     // crosses passes in part[tile * 64 + lane]

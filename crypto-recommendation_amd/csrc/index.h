@@ -32,7 +32,6 @@ struct ProjTable {
     bool fused_ok = false;
     bool mfma_ok = false;        // split image present (either metric): hash_mfma.hip
     Buf vh_d, vl_d, v1_d;
-    Buf v32_d;     // euclidean: [32][128] f32 projections (rows >= LK zero), the fused in-pass fp64 refinement
     std::vector<float> hV;
     int upload(hipStream_t s, int metric, int d, int L, int k, float w, const float* V, const float* t,
                const int32_t* r, const double* R);
@@ -63,7 +62,8 @@ struct lshkm_ctx_s {
     lshkm::Buf ws_cf32;     // fast distances: f32(c) [Kpad][128] + |c - f32(c)| [Kpad]
     lshkm::Buf ws_c64p;     // general rows (d < 128): the zero-padded fp64 centroids [Kpad][128]
     lshkm::Buf ws_ambig2, ws_seg2;   // the hi-only form's refinement output list
-    lshkm::Buf ws_seg3;              // hi-only cosine: segment counts of the declined winner distances
+    lshkm::Buf ws_seg3;              // hi-only cosine: segment counts of the declined winner distances (euclidean exact: of the pow fix-ups)
+    lshkm::Buf ws_xn2;               // cosine on fp64 rows: [N] sum_j pow(x_j, 2)
     // scatter / query / update workspace (see api_index.cpp for the slot map)
     lshkm::Buf ws[16];
     // range assignment workspace (lshkm_range_assign)

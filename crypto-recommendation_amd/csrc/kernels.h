@@ -120,11 +120,6 @@ int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, in
 int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
                        int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch);
 int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr, int T = 1);
-// One-pass stable CSR (nb <= 32768): T tables' keys at keys + t * k_ts (stride
-// kstride); idx [T][N] row ids in bucket order, row_ptr [T][nb + 1].
-size_t csr1_scratch_bytes(int64_t N, int64_t nb, int T);
-int csr_build_onepass(hipStream_t s, const int32_t* keys, int64_t kstride, int64_t k_ts, int T, int64_t N, int64_t nb,
-                      int32_t* idx, int64_t* row_ptr, void* scratch);
 // T independent stable sorts in one set of launches (table t: keys + t * key_ts,
 // vals + t * val_ts; outputs at + t * N).
 int stable_sort_by_key_batched(hipStream_t s, const int32_t* keys, int64_t kstride, int64_t key_ts, const int32_t* vals,
@@ -166,6 +161,8 @@ int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int6
                     const int64_t* carry_counts = nullptr);
 // fp64 rows: the same sums by binade segments (kmseg.h; ws: km_seg_ws_bytes).
 size_t km_seg_ws_bytes(int64_t M, int K, int d);
+// above this the update takes the fixed-point form instead (same exact sums)
+constexpr size_t KM_SEG_WS_CAP = (size_t)8 << 30;
 int launch_km_sums_seg(hipStream_t s, const double* X, int d, const int32_t* rows, const int64_t* crow, int K,
                        int64_t M, double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts,
                        void* ws);
@@ -246,7 +243,6 @@ struct FusedLaunch {
     int Kpad = 0;
     const _Float16* Vh = nullptr;
     const _Float16* Vl = nullptr;
-    const float* V32 = nullptr;     // euclidean: [32][128] f32 projections (16-row form's in-pass refinement)
     const double* PT = nullptr;
     const float* tv = nullptr;
     const double* pnorm = nullptr;
@@ -277,6 +273,7 @@ struct FusedLaunch {
     // certified form declined (cos_fix_seg pass)
     int metric = 0;
     const double* nbv = nullptr;
+    const double* xn2 = nullptr;    // cosine, fp64 rows: [N] sum_j pow(x_j, 2) (launch_row_sumsq)
     // euclidean fast distance (fast_dist): the winner's distance from f32(c) in
     // f32, certified to 2^-20 relative (else the row is refined exactly);
     // C32 [Kpad][128] = f32(c), rn32 [Kpad] = |c - f32(c)|_2 rounded up
@@ -326,10 +323,14 @@ int launch_fused_prep(hipStream_t s, const double* C, int K, int Kpad, _Float16*
                       float* cbound, int metric = 0, double* nbv = nullptr, float* C32 = nullptr,
                       float* rn32 = nullptr, int d = 128, double* C64p = nullptr);
 int launch_fused(hipStream_t s, bool hash, FusedLaunch& f);
-// Cosine winners listed by the persistent form (segment b: hfix[b * seg_rows ..],
-// count seg_counts[2b + 1]): soft-x87 distances.
+// out[i] = sum_j pow(x_ij, 2) in j order (glibc's pow, gpow2.h), fp64 rows
+int launch_row_sumsq(hipStream_t s, const double* X, int64_t N, int d, double* out);
+// Winners listed by the fused kernels for their distance alone (segment b:
+// list[b * seg_rows ..], count counts[2b + 1]): metric 1 the soft-x87 cosine,
+// metric 0 the euclidean chain with glibc's pow(x, 2) (gpow2.h).
 int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, int nlists, const unsigned long long* const* lists,
-                       const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist);
+                       const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist,
+                       int metric);
 
 // Range assignment (range.hip).
 int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0,

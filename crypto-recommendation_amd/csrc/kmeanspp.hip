@@ -167,7 +167,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
     if (METRIC == 1)
         for (int j = 0; j < d; j++) {
             const double cj = (double)cs[j];
-            cb = __dadd_rn(cb, __dmul_rn(cj, cj));
+            cb = __dadd_rn(cb, sq_of<TX>(cj));
         }
     double best = 0.0;
     for (int64_t row0 = (int64_t)blockIdx.x * KPP_THREADS; row0 < N; row0 += (int64_t)gridDim.x * KPP_THREADS) {
@@ -221,14 +221,10 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
                     const double cj = (double)cs[j0 + jj];
                     if (METRIC == 0) {
                         const double df = __dsub_rn(xj, cj);
-#if defined(ABL_KPP_NOCHAIN)   // timing experiments only: order-free sum (results invalid)
-                        a = fma(df, df, a);
-#else
-                        acc = __dadd_rn(acc, __dmul_rn(df, df));
-#endif
+                        acc = __dadd_rn(acc, gp_sq(df));
                     } else {
                         ip.add(__dmul_rn(xj, cj));
-                        a = __dadd_rn(a, __dmul_rn(xj, xj));
+                        a = __dadd_rn(a, sq_of<TX>(xj));
                     }
                 }
             }
@@ -237,9 +233,6 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
         if (n < N) {
         double dd;
         if (METRIC == 0) {
-#if defined(ABL_KPP_NOCHAIN)
-            acc += a;
-#endif
             dd = sqrt(acc);
         } else {
             const double denom = __dmul_rn(sqrt(a), sqrt(cb));
@@ -293,7 +286,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* 
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const double df = __dsub_rn((double)xv[q], (double)cs[j0 + 4 * u + q]);
-                    acc = __dadd_rn(acc, __dmul_rn(df, df));
+                    acc = __dadd_rn(acc, gp_sq(df));
                 }
             }
 #pragma unroll
@@ -788,8 +781,6 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
     int64_t* pa = (int64_t*)p;                 p += sizeof(int64_t) * N;  // crossing chunks' prefix arrays
     int64_t* pb = (int64_t*)p;
     const unsigned dgrid = gsz(N, KPP_THREADS, 4096);
-    const char* kr = getenv("LSHKM_KPP_DIST");           // "lds": the LDS-tile form (A/B)
-    const bool kpp_reg = !(kr && !strcmp(kr, "lds"));
     for (int it = 1; it < K; it++) {
 
         const bool vec = d % KPP_DJ == 0 && !X.f64;
@@ -798,10 +789,8 @@ int launch_kmeans_pp(hipStream_t s, Pts X, int64_t N, int d, int K, int metric, 
         if (X.f64) {
             if (metric == 0) hipLaunchKernelGGL((kpp_dist_kernel<0, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax, gsum);
             else hipLaunchKernelGGL((kpp_dist_kernel<1, false, double>), g, b, ld64, s, X.d(), N, d, chosen, it, mind, bmax, gsum);
-        } else if (metric == 0 && vec && kpp_reg)
+        } else if (metric == 0 && vec)
             hipLaunchKernelGGL(kpp_dist_reg_kernel, g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
-        else if (metric == 0 && vec)
-            hipLaunchKernelGGL((kpp_dist_kernel<0, true, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
         else if (metric == 0)
             hipLaunchKernelGGL((kpp_dist_kernel<0, false, float>), g, b, ld32, s, X.f(), N, d, chosen, it, mind, bmax, gsum);
         else if (vec)

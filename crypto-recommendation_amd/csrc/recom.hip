@@ -36,7 +36,7 @@ __device__ inline double rc_cos_sim(const double* __restrict__ x, const double* 
 
 __device__ inline double rc_sumsq(const double* __restrict__ x, int d) {
     double a = 0.0;
-    for (int j = 0; j < d; j++) a = __dadd_rn(a, __dmul_rn(x[j], x[j]));
+    for (int j = 0; j < d; j++) a = __dadd_rn(a, gp_sq(x[j]));
     return a;
 }
 
@@ -311,7 +311,7 @@ __device__ inline double cr_sumsq(const T* __restrict__ x, int d) {
     double a = 0.0;
     for (int j = 0; j < d; j++) {
         const double v = (double)x[j];
-        a = __dadd_rn(a, __dmul_rn(v, v));
+        a = __dadd_rn(a, sq_of<T>(v));
     }
     return a;
 }
@@ -326,7 +326,7 @@ __device__ inline bool cr_sim_cert(const T* __restrict__ x, const T* __restrict_
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], uj = (double)u[j];
         ip.add(__dmul_rn(xj, uj));
-        xa = __dadd_rn(xa, __dmul_rn(xj, xj));
+        xa = __dadd_rn(xa, sq_of<T>(xj));
     }
     denom = __dmul_rn(sqrt(xa), sqrt(ub));
     double qr;
@@ -664,9 +664,9 @@ __device__ inline double ct_sim(const uint64_t* myrow8, const uint64_t* u8, int 
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const double xj = (double)xv[k], uj = (double)uv[k];
-            ub = __dadd_rn(ub, __dmul_rn(uj, uj));
+            ub = __dadd_rn(ub, sq_of<T>(uj));
             ip.add(__dmul_rn(xj, uj));
-            xa = __dadd_rn(xa, __dmul_rn(xj, xj));
+            xa = __dadd_rn(xa, sq_of<T>(xj));
         }
     };
     int w = 0;
@@ -860,8 +860,8 @@ __global__ __launch_bounds__(64) void rc_terms_fix_kernel(
         for (int j = 0; j < d; j++) {
             const double xj = (double)myx[j], uj = (double)myu[j];
             ip.add(__dmul_rn(xj, uj));
-            xa = __dadd_rn(xa, __dmul_rn(xj, xj));
-            ub = __dadd_rn(ub, __dmul_rn(uj, uj));
+            xa = __dadd_rn(xa, sq_of<T>(xj));
+            ub = __dadd_rn(ub, sq_of<T>(uj));
         }
         const double sv = x87_quot(ip.value(), __dmul_rn(sqrt(xa), sqrt(ub)));
         if (!on) continue;

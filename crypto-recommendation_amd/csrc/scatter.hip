@@ -334,162 +334,4 @@ int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int6
     return kstatus("scatter.hip");
 }
 
-
-// ---------------------------------------------------------------- one-pass CSR
-// Stable bucket CSR for key ranges nb <= C1_MAXNB without a multi-pass sort:
-// the rows are cut into B contiguous blocks per table;
-//   c1_hist_kernel      per block, an LDS histogram of its keys -> hist[t][b][bin]
-//   c1_colscan_kernel   per bin, the exclusive prefix over the blocks (in place)
-//                       and the bin's total
-//   c1_start_kernel     per table, the exclusive scan of the totals: the bins'
-//                       starts = row_ptr (and row_ptr[nb] = N)
-//   c1_place_kernel     one wave per block walks its rows in order, 64 at a time:
-//                       peers of equal key by ballots, position = the bin's
-//                       running slot (LDS, from start + the block prefix) + the
-//                       lanes of that key below; the key's first lane advances it
-// Row order inside a bin is block order then row order in the block: the
-// insertion order of CustHashtable / VectorBucket (stable, as the radix form).
-// Four launches per build (the two 7-bit radix passes and the bounds pass took
-// eleven); HBM: the keys twice, the row ids once, the hist matrix (T B nb
-// counters) three times.
-constexpr int C1_MAXNB = 32768;
-constexpr int C1_COLB = 16;            // column loads in flight per bin
-
-__global__ __launch_bounds__(1024) void c1_hist_kernel(const int32_t* __restrict__ keys, int64_t kstride, int64_t k_ts,
-                                                       int64_t N, int nb, int64_t R, int B, uint32_t* __restrict__ hist) {
-    extern __shared__ uint32_t c1h[];
-    const int t = blockIdx.y, b = blockIdx.x;
-    keys += t * k_ts;
-    for (int i = threadIdx.x; i < nb; i += 1024) c1h[i] = 0;
-    __syncthreads();
-    const int64_t r0 = (int64_t)b * R, r1 = min(N, r0 + R);
-    for (int64_t i = r0 + threadIdx.x; i < r1; i += 1024) {
-        const uint32_t k = (uint32_t)keys[i * kstride];
-        if (k < (uint32_t)nb) atomicAdd(&c1h[k], 1u);
-    }
-    __syncthreads();
-    uint32_t* out = hist + ((size_t)t * B + b) * nb;
-    for (int i = threadIdx.x; i < nb; i += 1024) out[i] = c1h[i];
-}
-
-__global__ __launch_bounds__(256) void c1_colscan_kernel(uint32_t* __restrict__ hist, int nb, int B,
-                                                         uint32_t* __restrict__ total) {
-    const int t = blockIdx.y;
-    const int bin = blockIdx.x * 256 + threadIdx.x;
-    if (bin >= nb) return;
-    uint32_t* h = hist + (size_t)t * B * nb + bin;
-    uint32_t run = 0;
-    for (int b0 = 0; b0 < B; b0 += C1_COLB) {
-        uint32_t v[C1_COLB];
-#pragma unroll
-        for (int u = 0; u < C1_COLB; u++) v[u] = b0 + u < B ? h[(size_t)(b0 + u) * nb] : 0u;
-#pragma unroll
-        for (int u = 0; u < C1_COLB; u++)
-            if (b0 + u < B) { h[(size_t)(b0 + u) * nb] = run; run += v[u]; }
-    }
-    total[(size_t)t * nb + bin] = run;
-}
-
-__global__ __launch_bounds__(1024) void c1_start_kernel(uint32_t* __restrict__ total, int nb, int64_t N,
-                                                        int64_t* __restrict__ row_ptr) {
-    __shared__ uint32_t part[1024];
-    const int t = blockIdx.x, tid = threadIdx.x;
-    uint32_t* a = total + (size_t)t * nb;
-    int64_t* rp = row_ptr + (size_t)t * (nb + 1);
-    const int seg = (nb + 1023) / 1024;
-    const int lo = tid * seg, hi = min(nb, lo + seg);
-    uint32_t sum = 0;
-    for (int i = lo; i < hi; i++) sum += a[i];
-    part[tid] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = tid >= off ? part[tid - off] : 0u;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    uint32_t run = tid ? part[tid - 1] : 0u;
-    for (int i = lo; i < hi; i++) {
-        const uint32_t v = a[i];
-        a[i] = run;
-        rp[i] = run;
-        run += v;
-    }
-    if (tid == 0) rp[nb] = N;
-}
-
-__global__ __launch_bounds__(64) void c1_place_kernel(const int32_t* __restrict__ keys, int64_t kstride, int64_t k_ts,
-                                                      int64_t N, int nb, int nbits, int64_t R, int B,
-                                                      const uint32_t* __restrict__ hist, const uint32_t* __restrict__ start,
-                                                      int32_t* __restrict__ idx) {
-    extern __shared__ uint32_t run[];
-    const int t = blockIdx.y, b = blockIdx.x, lane = threadIdx.x;
-    keys += t * k_ts;
-    idx += (size_t)t * N;
-    const uint32_t* hb = hist + ((size_t)t * B + b) * nb;
-    const uint32_t* st = start + (size_t)t * nb;
-    for (int i = lane; i < nb; i += 64) run[i] = st[i] + hb[i];
-    __syncthreads();
-    const int64_t r0 = (int64_t)b * R, r1 = min(N, r0 + R);
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    int32_t knext = r0 + lane < r1 ? keys[(r0 + lane) * kstride] : 0;
-    for (int64_t c = r0; c < r1; c += 64) {
-        const int64_t row = c + lane;
-        const bool valid = row < r1;
-        const int32_t key = knext;
-        knext = row + 64 < r1 ? keys[(row + 64) * kstride] : 0;
-        const bool ok = valid && (uint32_t)key < (uint32_t)nb;
-        unsigned long long peers = __ballot(ok);
-        for (int bt = 0; bt < nbits; bt++) {
-            const bool bit = (key >> bt) & 1;
-            const unsigned long long m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
-        if (ok) {
-            const uint32_t below = (uint32_t)__popcll(peers & lt);
-            const uint32_t base = run[key];
-            idx[base + below] = (int32_t)row;
-            // LDS operations of one wave complete in order: every peer has read base
-            if (below == 0) run[key] = base + (uint32_t)__popcll(peers);
-        }
-    }
-}
-
-size_t csr1_scratch_bytes(int64_t N, int64_t nb, int T) {
-    if (nb > C1_MAXNB || nb <= 0) return 0;
-    int64_t B = std::max<int64_t>(1, (N + 24575) / 24576);
-    B = std::min<int64_t>(B, std::max<int64_t>(1, ((int64_t)1 << 24) / ((int64_t)T * nb)));
-    B = std::min<int64_t>(B, 4096);
-    return (size_t)T * ((size_t)B * nb + nb) * 4 + 256;
-}
-
-int csr_build_onepass(hipStream_t s, const int32_t* keys, int64_t kstride, int64_t k_ts, int T, int64_t N, int64_t nb,
-                      int32_t* idx, int64_t* row_ptr, void* scratch) {
-    if (nb > C1_MAXNB || nb <= 0 || T <= 0) {
-        set_error("csr_build_onepass: key range out of bounds");
-        return -1;
-    }
-    int64_t B = std::max<int64_t>(1, (N + 24575) / 24576);
-    B = std::min<int64_t>(B, std::max<int64_t>(1, ((int64_t)1 << 24) / ((int64_t)T * nb)));
-    B = std::min<int64_t>(B, 4096);
-    const int64_t R = std::max<int64_t>(1, (N + B - 1) / B);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);            // [T][B][nb]
-    uint32_t* total = hist + (size_t)T * B * nb;                      // [T][nb]
-    int nbits = 0;
-    while (((int64_t)1 << nbits) < nb) nbits++;
-    const size_t lds = (size_t)nb * 4;
-    if (N > 0)
-        hipLaunchKernelGGL(c1_hist_kernel, dim3((unsigned)B, (unsigned)T), dim3(1024), lds, s, keys, kstride, k_ts, N,
-                           (int)nb, R, (int)B, hist);
-    else
-        (void)hipMemsetAsync(hist, 0, (size_t)T * B * nb * 4, s);
-    hipLaunchKernelGGL(c1_colscan_kernel, dim3((unsigned)((nb + 255) / 256), (unsigned)T), dim3(256), 0, s, hist, (int)nb,
-                       (int)B, total);
-    hipLaunchKernelGGL(c1_start_kernel, dim3((unsigned)T), dim3(1024), 0, s, total, (int)nb, N, row_ptr);
-    if (N > 0)
-        hipLaunchKernelGGL(c1_place_kernel, dim3((unsigned)B, (unsigned)T), dim3(64), lds, s, keys, kstride, k_ts, N,
-                           (int)nb, nbits, R, (int)B, hist, total, idx);
-    return kstatus("scatter.hip (one-pass CSR)");
-}
-
 }  // namespace lshkm

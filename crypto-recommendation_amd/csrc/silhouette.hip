@@ -60,13 +60,13 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const double df = __dsub_rn(a[u], b[u]);
-                acc = __dadd_rn(acc, __dmul_rn(df, df));
+                acc = __dadd_rn(acc, gp_sq(df));
             }
         }
     }
     for (; k < d; k++) {
         const double df = __dsub_rn((double)xi[k], (double)xj[k]);
-        acc = __dadd_rn(acc, __dmul_rn(df, df));
+        acc = __dadd_rn(acc, gp_sq(df));
     }
     return sqrt(acc);
 }
@@ -103,8 +103,8 @@ __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restri
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const double du = __dsub_rn(u[e], b[e]), dv = __dsub_rn(v[e], b[e]);
-            aa = __dadd_rn(aa, __dmul_rn(du, du));
-            ab = __dadd_rn(ab, __dmul_rn(dv, dv));
+            aa = __dadd_rn(aa, gp_sq(du));
+            ab = __dadd_rn(ab, gp_sq(dv));
         }
     }
     da = sqrt(aa);

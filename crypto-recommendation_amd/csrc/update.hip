@@ -193,8 +193,7 @@ static bool km_wide() {
     // the wide form (16 dims per wave, 4 member rows per load) by default: the
     // fp64 update of 1M x 100 rows, K = 256, 3.44 -> 2.68 ms; LSHKM_KM_CHAIN=64:
     // the 64-dim form
-    const char* v = getenv("LSHKM_KM_CHAIN");
-    return !(v && !strcmp(v, "64"));
+    return !test_switch("LSHKM_KM_CHAIN", "64");
 }
 
 int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K,
@@ -824,7 +823,7 @@ __global__ __launch_bounds__(64) void km_finalize_kernel(const double* __restric
         double acc = 0.0;
         for (int j = 0; j < d; j++) {
             const double df = __dsub_rn(a[j], b[j]);
-            acc = __dadd_rn(acc, __dmul_rn(df, df));
+            acc = __dadd_rn(acc, gp_sq(df));
         }
         dist = sqrt(acc);
     } else {
@@ -833,8 +832,8 @@ __global__ __launch_bounds__(64) void km_finalize_kernel(const double* __restric
         double x = 0.0, y = 0.0;
         for (int j = 0; j < d; j++) {
             ip.add(__dmul_rn(a[j], b[j]));
-            x = __dadd_rn(x, __dmul_rn(a[j], a[j]));
-            y = __dadd_rn(y, __dmul_rn(b[j], b[j]));
+            x = __dadd_rn(x, gp_sq(a[j]));
+            y = __dadd_rn(y, gp_sq(b[j]));
         }
         const double denom = __dmul_rn(sqrt(x), sqrt(y));
         dist = one_minus(x87_quot(ip.value(), denom));

@@ -21,6 +21,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "lshkm.h")
 
 EUCLIDEAN, COSINE = 0, 1
 STAT_HASH_EXACT, STAT_ASSIGN_AMBIG, STAT_COS_FIX, STAT_REFINED, STAT_HASH_FIX, STAT_REC_SOFT = 0, 1, 4, 5, 6, 7
+STAT_POW_FIX = 8
 _METRIC = {"euclidean": EUCLIDEAN, "cosine": COSINE, EUCLIDEAN: EUCLIDEAN, COSINE: COSINE}
 DIST_CERTIFIED, DIST_EXACT = 0, 1
 _DIST = {"certified": DIST_CERTIFIED, "default": DIST_CERTIFIED, "exact": DIST_EXACT,
@@ -31,6 +32,15 @@ _lib = None
 
 class LshkmError(RuntimeError):
     pass
+
+
+def pow_selfcheck():
+    """Host only: the device's restatement of glibc's pow(x, 2) against this
+    process's pow on discriminating inputs (lshkm_pow_selfcheck); returns
+    (mismatches, tested)."""
+    m, t = C.c_int64(), C.c_int64()
+    _ck(lib().lshkm_pow_selfcheck(C.byref(m), C.byref(t)))
+    return m.value, t.value
 
 
 def declared_symbols():
@@ -50,6 +60,8 @@ def lib():
         sigs = {
             "lshkm_last_error": (C.c_char_p, []),
             "lshkm_version": (C.c_char_p, []),
+            "lshkm_pow2": (i32, [vp, vp, i64, vp]),
+            "lshkm_pow_selfcheck": (i32, [C.POINTER(i64), C.POINTER(i64)]),
             "lshkm_ctx_create": (i32, [i32, C.POINTER(vp)]),
             "lshkm_ctx_set_stream": (i32, [vp, vp]),
             "lshkm_ctx_set_dist_mode": (i32, [vp, i32]),
@@ -199,6 +211,15 @@ class Context:
         (the default: euclidean winner distances within 2^-20 relative) or
         "exact" (the reference's fp64 chain for every distance)."""
         _ck(lib().lshkm_ctx_set_dist_mode(self.h, _DIST[mode]))
+
+    def pow2(self, x):
+        """pow(x, 2) as the reference's glibc computes it (lshkm_pow2), for a
+        float64 device tensor."""
+        x = x.contiguous()
+        assert x.dtype == self.torch.float64 and x.device.type == "cuda"
+        out = self.torch.empty_like(x)
+        _ck(lib().lshkm_pow2(self.h, C.c_void_p(x.data_ptr()), x.numel(), C.c_void_p(out.data_ptr())))
+        return out
 
     def dist_mode(self):
         m = C.c_int()

@@ -40,12 +40,17 @@
  *         whose bound fails gets the reference-order chain. Zero, inf and NaN
  *         distances are reproduced bit for bit. Cluster IDs are unaffected.
  *       LSHKM_DIST_EXACT: every distance is the reference's sequential fp64
- *         chain sqrt(sum_j (x_j - c_j)^2), j ascending -- bit-exact while the
- *         centroids are fp32 values (dataset rows, the first Lloyd iteration);
- *         after an update within 1.4e-16 relative (the reference's glibc
- *         pow(x, 2) vs x*x).
+ *         chain sqrt(sum_j pow(x_j - c_j, 2)), j ascending, bit for bit --
+ *         for dataset-row centroids and for general fp64 centroids after an
+ *         update alike.
  *     Cosine distances, range-assignment distances, silhouettes, similarities
  *     and every other output are exact-order in both modes.
+ *   - Every square the reference takes is glibc's pow(x, 2) (cust_vector.hpp:
+ *     132, 149-150, 168-169), which is not x*x for ~0.085 % of general doubles
+ *     (and for many exact ties): the device evaluates glibc 2.35's own
+ *     algorithm (the x86-64 __pow_fma variant, csrc/gpow2.h) wherever x*x is
+ *     not provably the same value. lshkm_pow_selfcheck() compares that
+ *     restatement with the running process's pow.
  *   - One handle per thread; calls on a handle are serialised on its stream.
  */
 #ifndef LSHKM_H
@@ -78,6 +83,16 @@ typedef struct lshkm_vectors_s* lshkm_vectors;
 /* ------------------------------------------------------------------ context */
 const char* lshkm_last_error(void);
 const char* lshkm_version(void);
+/* pow(x, 2) as the reference computes it (glibc's pow, cust_vector.hpp:132):
+ * out_dev[i] for x_dev[i], i < n, on the device (csrc/gpow2.h). */
+int lshkm_pow2(lshkm_ctx ctx, const double* x_dev, int64_t n, double* out_dev);
+/* Host-only (no GPU): compares the device's restatement of glibc's pow(x, 2)
+ * (the same code, compiled for the host) with this process's own pow on a
+ * fixed set of inputs whose squares lie near rounding midpoints (the inputs
+ * that tell pow from x*x) plus exact ties and special ranges; *mismatches_host
+ * = how many differ (0 when the process's libm is the one the restatement
+ * follows), *tested_host = inputs tried. */
+int lshkm_pow_selfcheck(int64_t* mismatches_host, int64_t* tested_host);
 int lshkm_ctx_create(int device, lshkm_ctx* out);
 /* Run on a caller-owned hipStream_t (e.g. torch's current stream), used
  * verbatim: NULL is the default (null) stream. A new context uses its own stream. */
@@ -104,7 +119,9 @@ int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t
  * 4 = cosine Lloyd winner distances the certified fast form declined (soft-x87 chain),
  * 5 = rows the hi-only fused pass (one f16 product per score) left to the 3-product form,
  * 6 = rows the fused pass listed for the hash fix-up,
- * 7 = clustering-recommender similarities decided by the x87 chain (lshkm_cluster_top_n). */
+ * 7 = clustering-recommender similarities decided by the x87 chain (lshkm_cluster_top_n),
+ * 8 = euclidean winner distances (LSHKM_DIST_EXACT, hi-only pass) whose chain met an
+ *     inexact square and were redone with glibc's pow(x, 2) (gpow2.h). */
 int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);
 int lshkm_reset_stats(lshkm_ctx ctx);
 /* HIP-event timing of the dominant kernel launch (the fused hash+assign kernel)

@@ -718,9 +718,13 @@ static int mode_chain(int argc, char** argv) {
 //     clusters.
 // DIR holds users.f64 [N][d], umean.f64, uunk_ptr.i64 / uunk_idx.i32 and
 // fake.f64 [F][d], fmean.f64, funk_ptr.i64 / funk_idx.i32 (means, unknown sets).
-// Outputs: A_rows [K], A_assign [N], A_iters, A_centers [K][d], A_top [N][NTA];
-// B_rows [K], B_assign [F], B_iters, B_centers [K][d], B_ucl [N], B_top [N][NTB]
-// (-1 rows for skipped users).
+// Outputs: A_rows [K], A_assign [N], A_iters, A_centers [K][d], A_top [N][NTA],
+// A_dist [N] (dist_from_centroid after the last Lloyd: fp64 means after the
+// first update), A_sim_ptr [N+1] / A_sims (cosineSimilarity(member, user) over
+// the user's cluster in member order, as the 3-argument get_top_N_recom forms
+// them), A_pred (get_predicted_user_sim at the user's unknown indexes, ascending);
+// B_rows [K], B_assign [F], B_iters, B_centers [K][d], B_ucl [N], B_top [N][NTB],
+// B_dist [F] (-1 rows for skipped users).
 static std::vector<Vec> read_vecs(const std::string& dir, const std::string& pre, int N, int d, const std::string& id) {
     std::vector<double> x = read_raw<double>(dir + "/" + pre + ".f64", (size_t)N * d);
     const std::string a = pre.substr(0, 1);
@@ -764,13 +768,28 @@ static int mode_crec(int argc, char** argv) {
         }
         std::vector<std::vector<Vec*>> clusters = separate_clusters_from_input(users, (int)centroids.size());
         std::vector<int32_t> assign(N), top((size_t)N * NTA, -1);
+        std::vector<double> dist(N), sims, pred;
+        std::vector<int64_t> sim_ptr(1, 0);
         for (int i = 0; i < N; i++) assign[i] = users[i].getCluster();
+        for (int i = 0; i < N; i++) dist[i] = users[i].getDistFromCentroid();
         for (int i = 0; i < N; i++) {
             std::vector<Vec*> neighbors = clusters[users[i].getCluster()];
-            if (neighbors.empty()) continue;
-            std::vector<int> t = get_top_N_recom(neighbors, users[i], NTA);
-            for (int j = 0; j < NTA; j++) top[(size_t)i * NTA + j] = t[j];
+            if (!neighbors.empty()) {
+                std::vector<int> t = get_top_N_recom(neighbors, users[i], NTA);
+                for (int j = 0; j < NTA; j++) top[(size_t)i * NTA + j] = t[j];
+            }
+            // the similarities and predictions get_top_N_recom formed (crypto_rec.hpp:327-345)
+            std::vector<double> s(neighbors.size());
+            for (size_t k = 0; k < neighbors.size(); k++) s[k] = neighbors[k]->cosineSimilarity(&users[i]);
+            sims.insert(sims.end(), s.begin(), s.end());
+            sim_ptr.push_back((int64_t)sims.size());
+            std::vector<double> p = get_predicted_user_sim(neighbors, users[i], s);
+            for (int idx : users[i].getUnknownIndexes()) pred.push_back(p[idx]);
         }
+        write_npy(dir + "/A_dist.npy", dist, {(size_t)N});
+        write_npy(dir + "/A_sim_ptr.npy", sim_ptr, {sim_ptr.size()});
+        write_npy(dir + "/A_sims.npy", sims, {sims.size()});
+        write_npy(dir + "/A_pred.npy", pred, {pred.size()});
         std::vector<int32_t> nit(1, it);
         write_npy(dir + "/A_rows.npy", rows, {rows.size()});
         write_npy(dir + "/A_assign.npy", assign, {(size_t)N});
@@ -793,7 +812,10 @@ static int mode_crec(int argc, char** argv) {
         }
         std::vector<std::vector<Vec*>> clusters = separate_clusters_from_input(fake, (int)centroids.size());
         std::vector<int32_t> assign(F), ucl(N), top((size_t)N * NTB, -1);
+        std::vector<double> fdist(F);
         for (int i = 0; i < F; i++) assign[i] = fake[i].getCluster();
+        for (int i = 0; i < F; i++) fdist[i] = fake[i].getDistFromCentroid();
+        write_npy(dir + "/B_dist.npy", fdist, {(size_t)F});
         for (int i = 0; i < N; i++) {
             Vec& user = users[i];
             double mind = user.euclideanDistance(centroids[0]);

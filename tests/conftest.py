@@ -84,8 +84,9 @@ def meta():
 # asks 1e-5 relative on float distances; cluster IDs and bucket IDs stay
 # bit-exact) or, when set, LSHKM_DIST_EXACT (the reference-order fp64 chain, bit
 # for bit). Tests taking `dist_mode` run both modes on their module's `ctx`; the
-# rest run the shipped default. The LSHKM_DIST environment override is cleared
-# for every test, so the ABI alone decides.
+# rest run the shipped default. (The product library reads no environment; the
+# LSHKM_DIST override exists only in the test build and is cleared for every
+# test, so the ABI alone decides there too.)
 DIST_TOL = 2.0 ** -20
 
 
@@ -96,10 +97,29 @@ def _no_dist_env(monkeypatch):
 
 @pytest.fixture(params=["certified", "exact"])
 def dist_mode(request):
-    ctx = request.getfixturevalue("ctx")
-    ctx.set_dist_mode(request.param)
+    ctxs = [request.getfixturevalue("ctx")]
+    if "sctx" in request.fixturenames:
+        ctxs.append(request.getfixturevalue("sctx"))
+    for c in ctxs:
+        c.set_dist_mode(request.param)
     yield request.param
-    ctx.set_dist_mode("certified")
+    for c in ctxs:
+        c.set_dist_mode("certified")
+
+
+@pytest.fixture(scope="session")
+def sw():
+    """The test build's binding (amd.switched()): forced kernel paths."""
+    import amd
+    return amd.switched()
+
+
+@pytest.fixture(scope="module")
+def sctx(sw):
+    """A context of the test build (its handles are its own)."""
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    return sw.Context(0)
 
 
 def assert_dist(got, want, mode, both_certified=False):
@@ -120,13 +140,3 @@ def assert_dist(got, want, mode, both_certified=False):
     assert rel.max(initial=0.0) <= tol, rel.max(initial=0.0)
 
 
-def assert_dist_tol(got, want, mode, rtol):
-    """General (non-fp32) centroids: the exact mode's pow(x, 2) tolerance `rtol`
-    (DESIGN.md §5), or the certified mode's DIST_TOL, whichever is larger."""
-    got = np.ascontiguousarray(got, np.float64)
-    want = np.ascontiguousarray(want, np.float64)
-    fin = np.isfinite(want) & (want != 0.0)
-    assert np.array_equal(got[~fin].view(np.uint64), want[~fin].view(np.uint64))
-    tol = max(rtol, DIST_TOL) if mode != "exact" else rtol
-    rel = np.abs(got[fin] - want[fin]) / np.abs(want[fin])
-    assert rel.max(initial=0.0) <= tol, rel.max(initial=0.0)

@@ -273,7 +273,27 @@ CREC_CASES = [
     ("crec_a", 600, 500, 100, 12, 5, 0.0, 861, 862, 5, 2, 8201, 1),
     ("crec_b", 300, 60, 60, 30, 4, 0.0, 863, 864, 5, 2, 8202, 3),      # 20 distinct fake users, K = 30
     ("crec_c", 500, 400, 24, 8, 30, 0.05, 865, 866, 7, 3, 8203, 1),    # converges before the iteration cap
+    # user vectors scaled per user by 16 exp(U(-0.3, 0.3)) and rounded to 2^-24
+    # (25-28 significant bits): many squares are exact ties, which glibc's
+    # pow(x, 2) rounds unlike x*x, so the norms differ on >= 1 % of the users
+    # (checked below; plain general doubles absorb the last-bit differences of
+    # their squares in the sums almost always)
+    ("crec_pw", 1000, 600, 100, 16, 4, 0.0, 867, 868, 5, 3, 8204, 1),
 ]
+CREC_GENERAL = {"crec_pw"}
+
+
+def pow_norm_disagreement(X):
+    """Fraction of rows whose sequential sum of pow(x, 2) differs from the sum of x*x."""
+    import math
+    n = 0
+    for x in X:
+        a = b = 0.0
+        for v in x:
+            a = a + math.pow(float(v), 2)
+            b = b + float(v) * float(v)
+        n += a != b
+    return n / max(len(X), 1)
 
 
 def run(args):
@@ -448,6 +468,15 @@ def main(only=None):
             out = os.path.join(tmp, name); os.makedirs(out)
             users, uunk, umean = user_vectors(dseed, N, d)
             fake, funk, fmean = user_vectors(dseed + 1, F // dup, d)
+            if name in CREC_GENERAL:
+                rs = np.random.RandomState(dseed + 2)
+                su, sf = 16.0 * np.exp(rs.uniform(-0.3, 0.3, N)), 16.0 * np.exp(rs.uniform(-0.3, 0.3, len(fake)))
+                q = lambda v: np.round(v * 2.0 ** 24) / 2.0 ** 24
+                users, umean = q(users * su[:, None]), q(umean * su)
+                fake, fmean = q(fake * sf[:, None]), q(fmean * sf)
+                fr = pow_norm_disagreement(users)
+                assert fr >= 0.01, fr
+                print(f"{name}: pow(x, 2) vs x*x differ on {100 * fr:.1f} % of the user norms")
             fake, fmean = np.repeat(fake, dup, axis=0), np.repeat(fmean, dup)
             funk = [u for u in funk for _ in range(dup)]
             inp = dict(users=users, umean=umean, fake=fake, fmean=fmean)

@@ -60,8 +60,8 @@ def test_shim_compiles_against_reference_headers(tmp_path):
 @pytest.mark.parametrize("args", [("7", "2000", "128", "16"), ("11", "900", "17", "5"),
                                   ("13", "1500", "100", "12", "f64")])
 def test_shim_matches_reference_functions(args, mode):
-    # exact: the shim's default (LSHKM_DIST_EXACT) -- distances bit for bit where
-    # the squares are exact in fp64, else within the pow(x, 2) ulp; certified:
+    # exact: the shim's default (LSHKM_DIST_EXACT) -- distances bit for bit, after
+    # updates too (glibc's pow(x, 2), csrc/gpow2.h); certified:
     # lshkm_compat::set_distance_mode(LSHKM_DIST_CERTIFIED), euclidean distances
     # within 2^-20 relative. Everything else bit for bit in both.
     if not os.path.exists(CHECK):
@@ -73,8 +73,8 @@ def test_shim_matches_reference_functions(args, mode):
     # lists, and k_means replaced its centers at least once
     stats = dict(kv.split("=") for kv in r.stdout.split("compat ok")[1].split() if "=" in kv)
     assert stats["mode"] == mode
-    if mode == "exact" and "f64" not in args:
-        assert int(stats["kmeans_euclidean_bitexact_iterations"]) >= 1, stats
+    if mode == "exact":
+        assert int(stats["kmeans_euclidean_bitexact_iterations"]) == int(stats["kmeans_euclidean_iterations"]), stats
     for key in ("lsh_euclidean_filtered_rows", "lsh_cosine_filtered_rows", "cube_euclidean_probe_rows",
                 "cube_cosine_probe_rows", "cluster_recom_users"):
         assert int(stats[key]) > 0, (key, stats)

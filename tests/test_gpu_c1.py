@@ -38,10 +38,9 @@ def test_c1_matches_reference(ctx, name, tmp_path):
     it = int(g["iters"][0])
     assert res["iters"] == it and res["cont"] == bool(g["cont"][0])
     assert np.array_equal(res["assign"], g[f"assign{it - 1}"])
-    # the last iteration's centroids are k-means means (fp64): distances within
-    # the pow(x,2) ulp note of DESIGN.md §5 after the first update
+    # the last iteration's centroids are k-means means (general fp64): the
+    # reference's distances bit for bit (glibc's pow(x, 2), csrc/gpow2.h)
     want = g[f"dist{it - 1}"]
-    rel = np.abs(res["dist"] - want) / np.maximum(np.abs(want), 1e-300)
-    assert rel.max() <= 1e-14
+    assert np.array_equal(res["dist"].view(np.uint64), want.view(np.uint64))
     # centers after the last k_means (replaced iff it continued): bit-exact sums
     assert np.array_equal(res["centers"].view(np.uint64), g[f"centers{it}"].view(np.uint64))

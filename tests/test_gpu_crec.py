@@ -41,36 +41,79 @@ def kmeans_loop(ctx, X, rows, K, iters, min_dist):
     """main.cpp:248-254 / :342-347 on the device: Lloyd + k_means from dataset-row
     centroids (the override in the first iteration) until no move or `iters`."""
     C = X[dev(ctx, rows.astype(np.int64))].clone()
-    it, cont, a = 0, True, None
+    it, cont, a, dist = 0, True, None, None
     while cont and it < iters:
-        a, _ = lshkm.lloyd_assign(ctx, X, C, "euclidean", rows.astype(np.int32) if it == 0 else None)
+        a, dist = lshkm.lloyd_assign(ctx, X, C, "euclidean", rows.astype(np.int32) if it == 0 else None)
         Cn, _, cont = lshkm.kmeans_update(ctx, X, a, C, "euclidean", min_dist)
         C = Cn if cont else C
         it += 1
-    return a, C, it
+    return a, C, it, dist
+
+
+def bits_equal(got, want):
+    got, want = np.ascontiguousarray(got, np.float64), np.ascontiguousarray(want, np.float64)
+    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
+    return bad.size == 0, bad[:8]
 
 
 @pytest.mark.parametrize("name", cases("crec"))
 def test_clustering_recommenders_golden(ctx, name):
+    # main.cpp's two clustering recommenders on user vectors (fp64), against the
+    # reference's own run: cluster IDs, centers, the last Lloyd's distances (the
+    # LSHKM_DIST_EXACT contract: fp64 means after the first update, glibc's
+    # pow(x, 2) per square), every similarity, every prediction and the
+    # recommendations, bit for bit. crec_pw's values are tie-heavy, so x*x and
+    # pow(x, 2) differ on 2 % of its user norms.
     m, g = META[name], golden(name)
     K = m["K"]
     users, fake = dev(ctx, g["users"]), dev(ctx, g["fake"])
     um, fm = dev(ctx, g["umean"]), dev(ctx, g["fmean"])
     up, ui = dev(ctx, g["uunk_ptr"]), dev(ctx, g["uunk_idx"])
-    # Part A: the user vectors clustered, each user's own cluster
-    rows = lshkm.rand_selection_rows(m["N"], K, m["seedA"])
-    assert np.array_equal(rows, g["A_rows"])
-    a, C, it = kmeans_loop(ctx, users, rows, K, m["iters"], m["min_dist"])
-    assert it == int(g["A_iters"][0])
-    assert np.array_equal(a.cpu().numpy(), g["A_assign"])
-    assert np.array_equal(C.cpu().numpy().view(np.uint64), g["A_centers"].view(np.uint64))
+    ctx.set_dist_mode("exact")
+    try:
+        # Part A: the user vectors clustered, each user's own cluster
+        rows = lshkm.rand_selection_rows(m["N"], K, m["seedA"])
+        assert np.array_equal(rows, g["A_rows"])
+        a, C, it, dist = kmeans_loop(ctx, users, rows, K, m["iters"], m["min_dist"])
+        assert it == int(g["A_iters"][0])
+        assert np.array_equal(a.cpu().numpy(), g["A_assign"])
+        assert np.array_equal(C.cpu().numpy().view(np.uint64), g["A_centers"].view(np.uint64))
+        ok, bad = bits_equal(dist.cpu().numpy(), g["A_dist"])
+        assert ok, ("A_dist", bad)
+    finally:
+        ctx.set_dist_mode("certified")
     crow, crows = lshkm.clusters(ctx, a, K)
     top = lshkm.cluster_top_n(ctx, users, um, crow, crows, users, um, a, up, ui, m["NTA"]).cpu().numpy()
     assert np.array_equal(top, g["A_top"]), np.nonzero((top != g["A_top"]).any(1))[0][:10]
+    # the similarities and the predictions themselves, both sharded forms (one shard)
+    soff, sims = lshkm.cluster_sims(ctx, users, crow, crows, users, a, up)
+    assert np.array_equal(soff.cpu().numpy(), g["A_sim_ptr"])
+    ok, bad = bits_equal(sims.cpu().numpy()[:len(g["A_sims"])], g["A_sims"])
+    assert ok, ("A_sims", bad)
+    main_s, abs_s, _ = lshkm.cluster_chain(ctx, users, um, crow, crows, a, um, up, ui, soff, sims)
+    soff2, toff, sims2, terms = lshkm.cluster_terms(ctx, users, um, crow, crows, users, a, up, ui)
+    ok, bad = bits_equal(sims2.cpu().numpy()[:len(g["A_sims"])], g["A_sims"])
+    assert ok, ("A_sims (terms form)", bad)
+    main_t, abs_t, _ = lshkm.cluster_chain_terms(ctx, um, up, ui, soff2, toff, sims2, terms)
+    uptr = g["uunk_ptr"]
+    owner = np.repeat(np.arange(m["N"]), np.diff(uptr))          # the user of each unknown index
+    for main_, abs_ in ((main_s, abs_s), (main_t, abs_t)):
+        # get_predicted_user_sim (crypto_rec.hpp:297-298): main / abs, then + the user's mean
+        mn, ab = main_.cpu().numpy()[:len(owner)], abs_.cpu().numpy()
+        with np.errstate(divide="ignore", invalid="ignore"):
+            pred = mn / ab[owner] + g["umean"][owner]
+        ok, bad = bits_equal(pred, g["A_pred"])
+        assert ok, ("A_pred", bad)
     # Part B: the fake users clustered from k-means++, each user's nearest centroid
     rows = lshkm.kmeans_pp_rows(ctx, fake, K, "euclidean", m["seedB"])
     assert np.array_equal(rows, g["B_rows"])
-    a, C, it = kmeans_loop(ctx, fake, rows, K, m["iters"], m["min_dist"])
+    ctx.set_dist_mode("exact")
+    try:
+        a, C, it, dist = kmeans_loop(ctx, fake, rows, K, m["iters"], m["min_dist"])
+        ok, bad = bits_equal(dist.cpu().numpy(), g["B_dist"])
+        assert ok, ("B_dist", bad)
+    finally:
+        ctx.set_dist_mode("certified")
     assert it == int(g["B_iters"][0])
     assert np.array_equal(a.cpu().numpy(), g["B_assign"])
     assert np.array_equal(C.cpu().numpy().view(np.uint64), g["B_centers"].view(np.uint64))
@@ -101,7 +144,8 @@ def unknown_sets(rng, nq, d, big_every=0):
 
 @pytest.mark.parametrize("N,d,K,nq,NT,kind,seed", [
     (60_000, 128, 96, 1500, 5, "f32", 1),          # the C5 shape class: fp32 rows, d = 128
-    (20_000, 100, 40, 800, 5, "f64", 2),           # user-vector doubles (pow(x,2) == x*x holds here)
+    (20_000, 100, 40, 800, 5, "f64", 2),           # user-vector doubles (pow(x, 2) != x*x on ~8 % of norms)
+    (20_000, 100, 40, 800, 5, "f64q", 5),          # 20-bit quantized doubles: exact squares
     (8_000, 24, 12, 600, 7, "dyadic", 3),          # k/8 values: exact ties in the predictions
     (4_000, 300, 10, 120, 4, "f32", 4),            # d = 300: unknown sets > 256 (two prediction passes)
 ])
@@ -109,9 +153,10 @@ def test_cluster_top_n_vs_oracle(ctx, N, d, K, nq, NT, kind, seed):
     rng = np.random.default_rng(seed)
     if kind == "dyadic":
         X = rng.integers(-6, 7, size=(N, d)).astype(np.float64) / 8.0
-    elif kind == "f64":
+    elif kind in ("f64", "f64q"):
         X = rng.standard_normal((N, d)) * np.exp(rng.uniform(-1, 1, size=(N, 1)))
-        X = np.round(X * 2**20) / 2**20                        # squares exact in fp64 (pow(x,2) == x*x)
+        if kind == "f64q":
+            X = np.round(X * 2**20) / 2**20                    # squares exact in fp64 (pow(x,2) == x*x)
     else:
         X = rng.standard_normal((N, d)).astype(np.float32)
     X[5] = 0.0                                                 # a zero member: NaN similarity

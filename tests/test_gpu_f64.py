@@ -9,9 +9,9 @@ user_vectors, kinds f64_* and chain; inputs stored in the fixtures).
 Bit-exact: tuples, phi, bucket IDs, bucket member order, query results,
 hypercube vertices and coins, probe lists, cluster IDs, k-means centers (from
 the same assignment), k-means++ rows, neighbour lists and recommendations.
-Distances: exact-order fp64 with x*x for the reference's glibc pow(x, 2),
-which differs by <= 1 ulp on some general doubles: within
-1e-14 relative here (the north star allows 1e-5), and most are bit-equal.
+Distances, silhouettes and similarities: bit-exact too -- every square is
+glibc's pow(x, 2) (csrc/gpow2.h), which differs from x*x on ~0.085 % of
+general doubles.
 """
 import numpy as np
 import pytest
@@ -22,7 +22,6 @@ from conftest import case_queries, case_rows, cases, golden, golden_meta
 
 META = golden_meta()
 pytestmark = pytest.mark.gpu
-DIST_RTOL = 1e-14
 
 
 @pytest.fixture(scope="module")
@@ -36,14 +35,12 @@ def to_dev(ctx, a):
     return ctx.torch.from_numpy(np.ascontiguousarray(a)).to(ctx.dev)
 
 
-def assert_close_f64(got, want, rtol=DIST_RTOL):
-    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
-    both_nan = np.isnan(got) & np.isnan(want)
-    assert np.array_equal(np.isnan(got), np.isnan(want))
-    g, w = got[~both_nan], want[~both_nan]
-    rel = np.abs(g - w) / np.maximum(np.abs(w), 1e-300)
-    assert rel.max(initial=0.0) <= rtol, rel.max()
-    return float(np.mean(g.view(np.uint64) == w.view(np.uint64))) if g.size else 1.0
+def assert_close_f64(got, want):
+    """Bit for bit, NaN payloads included."""
+    got, want = np.ascontiguousarray(got, np.float64), np.ascontiguousarray(want, np.float64)
+    assert got.shape == want.shape
+    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
+    assert bad.size == 0, (bad[:8], got[bad[:4]], want[bad[:4]])
 
 
 def make_lsh(ctx, m, g):
@@ -111,26 +108,31 @@ def test_f64_cube(ctx, name):
 
 @pytest.mark.parametrize("path", ["auto", "exact"])
 @pytest.mark.parametrize("name", cases("f64_lloyd"))
-def test_f64_lloyd_update_silhouette(ctx, name, path, monkeypatch):
+def test_f64_lloyd_update_silhouette(ctx, sctx, sw, name, path, monkeypatch):
+    M, c = (lshkm, ctx) if path == "auto" else (sw, sctx)
     if path == "exact":
         monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
+    c.set_dist_mode("exact")           # the reference's distances, bit for bit
     m, g = META[name], golden(name)
     X = to_dev(ctx, case_rows(name))
     C = to_dev(ctx, g["centers0"])
     src = g["src_rows"]
-    for it in range(len(g["cont"])):
-        a, dist = lshkm.lloyd_assign(ctx, X, C, m["metric"], src if it == 0 else None)
-        a = a.cpu().numpy()
-        assert np.array_equal(a, g[f"assign{it}"]), it
-        assert_close_f64(dist.cpu().numpy(), g[f"dist{it}"])
-        sil, _ = lshkm.silhouette(ctx, X, to_dev(ctx, a), C, m["metric"])
-        assert_close_f64(sil, g[f"sil{it}"], 1e-12)
-        Cn, cnt, cont = lshkm.kmeans_update(ctx, X, to_dev(ctx, a), C, m["metric"], m["min_dist"])
-        assert cont == bool(g["cont"][it])
-        C = Cn if cont else C
-        # the reference's sequential fp64 chains over the same members: bit-exact
-        assert np.array_equal(C.cpu().numpy().view(np.uint64), g[f"centers{it + 1}"].view(np.uint64)), it
-        assert np.array_equal(cnt.cpu().numpy(), np.bincount(a, minlength=m["K"]))
+    try:
+        for it in range(len(g["cont"])):
+            a, dist = M.lloyd_assign(c, X, C, m["metric"], src if it == 0 else None)
+            a = a.cpu().numpy()
+            assert np.array_equal(a, g[f"assign{it}"]), it
+            assert_close_f64(dist.cpu().numpy(), g[f"dist{it}"])
+            sil, _ = M.silhouette(c, X, to_dev(ctx, a), C, m["metric"])
+            assert_close_f64(sil, g[f"sil{it}"])
+            Cn, cnt, cont = M.kmeans_update(c, X, to_dev(ctx, a), C, m["metric"], m["min_dist"])
+            assert cont == bool(g["cont"][it])
+            C = Cn if cont else C
+            # the reference's sequential fp64 chains over the same members: bit-exact
+            assert np.array_equal(C.cpu().numpy().view(np.uint64), g[f"centers{it + 1}"].view(np.uint64)), it
+            assert np.array_equal(cnt.cpu().numpy(), np.bincount(a, minlength=m["K"]))
+    finally:
+        c.set_dist_mode("certified")
 
 
 @pytest.mark.parametrize("name", cases("f64_kmeanspp"))

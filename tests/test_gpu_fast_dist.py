@@ -87,9 +87,8 @@ def test_fast_distance_fallback_rows(ctx, fast):
     oa, od = oracle.lloyd_assign(Xh[rows], Ch, "euclidean", None)
     ga, gd = a.cpu().numpy()[rows], dist.cpu().numpy()[rows]
     assert np.array_equal(ga, oa)
-    # the fallback rows carry the exact chain's distance (x_j - c_j exact here: bit-exact
-    # except glibc pow vs x*x)
-    np.testing.assert_allclose(gd[:K], od[:K], rtol=1e-14, atol=0)
+    # the fallback rows carry the exact chain's distance, bit for bit
+    assert np.array_equal(gd[:K].view(np.uint64), od[:K].view(np.uint64))
     check(ga, gd, oa, od)
 
 

@@ -14,7 +14,7 @@ import pytest
 
 import oracle
 from amd import lshkm
-from conftest import assert_dist, assert_dist_tol
+from conftest import assert_dist, assert_dist
 
 pytestmark = pytest.mark.gpu
 
@@ -43,47 +43,55 @@ def rows_f64(seed, N, d):
     return X
 
 
-def check(ctx, X, Ch, sub_n=3000, seed=0, metric="euclidean", mode="exact"):
+@pytest.fixture(scope="module")
+def alt(sw, sctx):
+    return sw, sctx
+
+
+def check(ctx, alt, X, Ch, sub_n=3000, seed=0, metric="euclidean", mode="exact"):
     """Lloyd on the default path vs the oracle (a subset) and vs the f32-MFMA path
-    (all rows; that path's distances are always the exact-order chain). mode: the
-    context's distance mode -- "certified" applies to euclidean fp32 rows only
-    (fp64 rows and cosine keep the exact chain)."""
+    forced in the test build (all rows; that path's distances are always the
+    exact-order chain). mode: the context's distance mode -- "certified" applies
+    to euclidean fp32 rows only (fp64 rows and cosine keep the exact chain)."""
     if metric != "euclidean" or X.dtype == np.float64:
         mode = "exact"
     import os
+    sw, sctx = alt
     N = X.shape[0]
     Xd, Cd = to_dev(ctx, X), to_dev(ctx, Ch)
     a, dist = lshkm.lloyd_assign(ctx, Xd, Cd, metric)
     a, dist = a.cpu().numpy(), dist.cpu().numpy()
     os.environ["LSHKM_ASSIGN_PATH"] = "f32"
     try:
-        a1, d1 = lshkm.lloyd_assign(ctx, Xd, Cd, metric)
+        sctx.set_dist_mode(ctx.dist_mode())
+        a1, d1 = sw.lloyd_assign(sctx, Xd, Cd, metric)
     finally:
         del os.environ["LSHKM_ASSIGN_PATH"]
+        sctx.set_dist_mode("certified")
     assert np.array_equal(a, a1.cpu().numpy())
     assert_dist(dist, d1.cpu().numpy(), mode)
     sub = np.r_[0:10, np.random.default_rng(seed).choice(N, sub_n, replace=False)]
     oa, od = oracle.lloyd_assign(X[sub], Ch, metric, None)
     assert np.array_equal(a[sub], oa)
-    # glibc pow vs x*x: 1 ulp on general doubles (DESIGN.md §5); nan rows match as nan
+    # general doubles: glibc's pow(x, 2) per square (DESIGN.md §5); nan rows match as nan
     ok = np.isfinite(od)
-    assert_dist_tol(dist[sub][ok], od[ok], mode, 1e-14)
+    assert_dist(dist[sub][ok], od[ok], mode)
     assert np.array_equal(np.isnan(dist[sub]), np.isnan(od))
 
 
 @pytest.mark.parametrize("d,K", [(100, 256), (100, 512), (128, 256), (37, 64), (1, 8), (100, 1), (64, 300)])
-def test_f64_rows(ctx, d, K):
+def test_f64_rows(ctx, alt, d, K):
     N = 50_003
     X = rows_f64(1000 + d + K, N, d)
     rng = np.random.default_rng(K)
     Ch = X[rng.choice(np.arange(20, N), K, replace=False)].copy()
     if K > 3:
         Ch[3] = Ch[2]                                # an exact tie: the first index wins
-    check(ctx, X, Ch)
+    check(ctx, alt, X, Ch)
 
 
 @pytest.mark.parametrize("d,K", [(100, 256), (64, 512), (37, 100), (127, 256)])
-def test_f32_rows_short_d(ctx, d, K, dist_mode):
+def test_f32_rows_short_d(ctx, alt, d, K, dist_mode):
     N = 40_001
     rng = np.random.default_rng(d * 7 + K)
     X = rng.standard_normal((N, d)).astype(np.float32)
@@ -92,10 +100,10 @@ def test_f32_rows_short_d(ctx, d, K, dist_mode):
     Ch = X[rng.choice(np.arange(10, N), K, replace=False)].astype(np.float64)
     Ch[1] = Ch[0]
     Ch[5] *= 1.0 + 1e-9                              # a general double centroid
-    check(ctx, X, Ch, mode=dist_mode)
+    check(ctx, alt, X, Ch, mode=dist_mode)
 
 
-def test_f64_rows_after_update(ctx):
+def test_f64_rows_after_update(ctx, alt):
     # Lloyd -> k-means update -> Lloyd on fp64 user-vector-shaped rows (main.cpp:248-258):
     # the second assignment runs against general fp64 means
     N, d, K = 60_000, 100, 128
@@ -105,11 +113,11 @@ def test_f64_rows_after_update(ctx):
     rows = (np.arange(K) * (N // K)).astype(np.int32)
     a, _ = lshkm.lloyd_assign(ctx, Xd, to_dev(ctx, X[rows]), "euclidean", rows)
     Cn, _, _ = lshkm.kmeans_update(ctx, Xd, a, to_dev(ctx, X[rows]), "euclidean", 0.0)
-    check(ctx, X, Cn.cpu().numpy(), sub_n=2000, seed=5)
+    check(ctx, alt, X, Cn.cpu().numpy(), sub_n=2000, seed=5)
 
 
 @pytest.mark.parametrize("d,K,f64", [(100, 256, True), (100, 512, True), (37, 64, True), (100, 200, False), (64, 256, False)])
-def test_cosine_rows(ctx, d, K, f64):
+def test_cosine_rows(ctx, alt, d, K, f64):
     # cosine Lloyd on the reference's user-vector shape (main.cpp:248-258 with the
     # cosine metric of cluster.conf): zero rows (the reference's NaN distances),
     # rows parallel to a centroid, and general doubles
@@ -124,4 +132,4 @@ def test_cosine_rows(ctx, d, K, f64):
     X[6] = Ch[7] * 0.5
     if f64:
         Ch[4] *= 1.0 + 1e-9
-    check(ctx, X, Ch, sub_n=2000, seed=d, metric="cosine")
+    check(ctx, alt, X, Ch, sub_n=2000, seed=d, metric="cosine")

@@ -6,7 +6,7 @@ import pytest
 
 import oracle
 from amd import lshkm
-from conftest import assert_dist, assert_dist_tol, cases, golden, golden_meta, lloyd_input
+from conftest import assert_dist, cases, golden, golden_meta, lloyd_input
 
 META = golden_meta()
 pytestmark = pytest.mark.gpu
@@ -104,19 +104,9 @@ def test_lloyd_golden(ctx, name, dist_mode):
             # the certified f32 winner distance (conftest.DIST_TOL)
             assert_dist(gd, rd, "certified")
             continue
-        fp32_centers = np.array_equal(g[f"centers{it}"], g[f"centers{it}"].astype(np.float32).astype(np.float64))
-        if fp32_centers or m["metric"] == "cosine" and it == 0:
-            # (x_j - c_j) is exact, so glibc pow(x,2) == x*x: bit-exact
-            assert np.array_equal(gd.view(np.uint64), rd.view(np.uint64)), it
-        else:
-            # General fp64 centroids: glibc pow(x,2) may differ from x*x by 1 ulp per
-            # term (DESIGN.md "Distances"); north-star tolerance is 1e-5 relative.
-            nan = np.isnan(rd)            # zero rows under cosine: the x86 default NaN, bit for bit
-            assert np.array_equal(gd[nan].view(np.uint64), rd[nan].view(np.uint64)), it
-            gd, rd = gd[~nan], rd[~nan]
-            rel = np.abs(gd - rd) / np.maximum(np.abs(rd), 1e-300)
-            assert rel.max(initial=0.0) <= 1e-14, (it, rel.max())
-            assert np.mean(gd != rd) < 0.05, it
+        # bit for bit, general fp64 centroids after an update included (glibc's
+        # pow(x, 2), csrc/gpow2.h); zero rows under cosine: the x86 default NaN
+        assert np.array_equal(gd.view(np.uint64), rd.view(np.uint64)), (it, np.nonzero(gd != rd)[0][:8])
 
 
 def test_lloyd_large_vs_oracle(ctx, dist_mode):
@@ -137,14 +127,18 @@ def test_lloyd_large_vs_oracle(ctx, dist_mode):
 
 def test_lloyd_general_fp64_centroids(ctx, dist_mode):
     # centroids that are not fp32 values (after an update): exact mode keeps the
-    # exact-order fp64 chain (within the pow(x,2) ulp), certified mode 2^-20
+    # reference's chain bit for bit -- every (x_j - c_j) is a general double, so
+    # glibc's pow(x, 2) differs from x*x on some of its squares -- certified 2^-20
     N, d, K = 20_000, 128, 64
     X = ctx.synth(3, N, d)
     Cc = X[:K].double() * (1 + 1e-3) + 1e-5
+    ctx.reset_stats()
     a, dist = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
     oa, od = oracle.lloyd_assign(X.cpu().numpy(), Cc.cpu().numpy(), "euclidean", None)
     assert np.array_equal(a.cpu().numpy(), oa)
-    assert_dist_tol(dist.cpu().numpy(), od, dist_mode, 1e-15)   # pow(x,2) vs x*x, DESIGN.md §5
+    assert_dist(dist.cpu().numpy(), od, dist_mode)
+    if dist_mode == "exact":
+        assert ctx.stat(lshkm.STAT_POW_FIX) > 0.5 * N         # the pow fix-up list ran
 
 
 def test_lloyd_ties_and_duplicates(ctx, dist_mode):
@@ -161,19 +155,21 @@ def test_lloyd_ties_and_duplicates(ctx, dist_mode):
 
 
 @pytest.mark.parametrize("form", ["persistent", "chunked"])
-def test_hash_assign_fused_vs_oracle(ctx, form, monkeypatch, dist_mode):
+def test_hash_assign_fused_vs_oracle(ctx, sctx, sw, form, monkeypatch, dist_mode):
     # the headline path: one pass over the rows (split-f16 MFMA), at 200k rows
-    # (ragged: not a multiple of the 32-row tile); both kernel forms
+    # (ragged: not a multiple of the 32-row tile); both kernel forms (chunked:
+    # forced in the test build)
+    M, c = (lshkm, ctx) if form == "persistent" else (sw, sctx)
     if form == "chunked":
         monkeypatch.setenv("LSHKM_FUSED_FORM", "chunked")
     N, d, L, k, K = 200_003, 128, 5, 4, 256
     V, t, r, _ = lshkm.params_lsh_euclidean(12345, L, k, d, 0.4)
     X = ctx.synth(0x5EED, N, d)
-    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
+    lsh = M.LSH(c, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
     rows = (np.arange(K) * (N // K)).astype(np.int32)
     Cc = X[to_dev(ctx, rows.astype(np.int64))].double()
-    ctx.reset_stats()
-    tu, ph, bu, a, dist = lshkm.hash_assign(lsh, X, Cc, rows, tuples=True, phi=True, bucket=True)
+    c.reset_stats()
+    tu, ph, bu, a, dist = M.hash_assign(lsh, X, Cc, rows, tuples=True, phi=True, bucket=True)
     Xh = X.cpu().numpy()
     xt, xp, xb = oracle.lsh_hash_euclid(Xh, V, t, np.float32(0.4), r, N // 100)
     assert np.array_equal(tu.cpu().numpy(), xt)
@@ -185,18 +181,18 @@ def test_hash_assign_fused_vs_oracle(ctx, form, monkeypatch, dist_mode):
     ga, gd = a.cpu().numpy()[sub], dist.cpu().numpy()[sub]
     assert np.array_equal(ga[~over], oa[~over])
     assert_dist(gd[~over], od[~over], dist_mode if form == "persistent" else "exact")
-    amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG)
+    amb = c.stat(lshkm.STAT_ASSIGN_AMBIG)
     assert amb < 0.05 * N, amb          # the bound is certifying the vast majority
 
 
 @pytest.mark.parametrize("path", ["f32", "exact"])
-def test_assign_paths_agree(ctx, path, monkeypatch, dist_mode):
+def test_assign_paths_agree(ctx, sctx, sw, path, monkeypatch, dist_mode):
     N, d, K = 30_000, 128, 64
     X = ctx.synth(21, N, d)
     Cc = X[:K].double() * 1.0001
     a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
     monkeypatch.setenv("LSHKM_ASSIGN_PATH", path)
-    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
+    a1, d1 = sw.lloyd_assign(sctx, X, Cc, "euclidean")
     assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
     # the f32-MFMA and exact paths always give the exact-order distance
     assert_dist(d0.cpu().numpy(), d1.cpu().numpy(), dist_mode)
@@ -205,7 +201,7 @@ def test_assign_paths_agree(ctx, path, monkeypatch, dist_mode):
 @pytest.mark.parametrize("d,K,case", [(128, 256, "rows"), (100, 64, "rows"), (16, 1, "rows"), (256, 300, "scaled"),
                                       (64, 40, "dups"), (32, 20, "zero_c0"), (32, 20, "zero_c5"),
                                       (48, 30, "special")])
-def test_cosine_mfma_vs_exact(ctx, d, K, case, monkeypatch):
+def test_cosine_mfma_vs_exact(ctx, sctx, sw, d, K, case, monkeypatch):
     # cosine Lloyd: the certified f32-MFMA path (-x.c/|c| scores) must agree bit
     # for bit with the exact all-centroid pass and with the oracle (assignment.hpp:52-75)
     N = 20_011
@@ -230,7 +226,7 @@ def test_cosine_mfma_vs_exact(ctx, d, K, case, monkeypatch):
     a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
     amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG)
     monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
-    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
+    a1, d1 = sw.lloyd_assign(sctx, X, Cc, "cosine")
     assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
     assert np.array_equal(d0.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
     sub = np.random.default_rng(7).choice(N, 1500, replace=False)
@@ -262,14 +258,15 @@ def test_hash_assign_shapes(ctx, N, K, L, k, dist_mode):
     assert np.array_equal(bu.cpu().numpy(), xb)
     oa, od = oracle.lloyd_assign(Xh, Ch, "euclidean", None)
     assert np.array_equal(a.cpu().numpy(), oa)
-    # centroids are not fp32-valued: glibc pow vs x*x may differ in the last bit
-    assert_dist_tol(dist.cpu().numpy(), od, dist_mode, 1e-14)
+    # centroids are not fp32-valued: glibc's pow(x, 2), bit for bit in exact mode
+    assert_dist(dist.cpu().numpy(), od, dist_mode)
 
 
 @pytest.mark.parametrize("form", ["persistent", "chunked"])
-def test_fused_range_guard(ctx, form, monkeypatch, dist_mode):
+def test_fused_range_guard(ctx, sctx, sw, form, monkeypatch, dist_mode):
     # values beyond the f16 range must never be certified by the split path
     # (in the persistent form every function of such a row goes through the fix-up pass)
+    M, c = (lshkm, ctx) if form == "persistent" else (sw, sctx)
     if form == "chunked":
         monkeypatch.setenv("LSHKM_FUSED_FORM", "chunked")
     N, d, K, L, k = 3000, 128, 16, 5, 4
@@ -278,9 +275,9 @@ def test_fused_range_guard(ctx, form, monkeypatch, dist_mode):
     Xh[5, :] = 7.0e4
     X = to_dev(ctx, Xh)
     V, t, r, _ = lshkm.params_lsh_euclidean(3, L, k, d, 4.0)
-    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, 30, 4.0, V=V, t=t, r=r)
+    lsh = M.LSH(c, "euclidean", d, k, L, 30, 4.0, V=V, t=t, r=r)
     Cc = to_dev(ctx, Xh[:K].astype(np.float64))
-    tu, _, bu, a, dist = lshkm.hash_assign(lsh, X, Cc, None)
+    tu, _, bu, a, dist = M.hash_assign(lsh, X, Cc, None)
     xt, _, xb = oracle.lsh_hash_euclid(Xh, V, t, np.float32(4.0), r, 30)
     oa, od = oracle.lloyd_assign(Xh, Xh[:K].astype(np.float64), "euclidean", None)
     assert np.array_equal(tu.cpu().numpy(), xt) and np.array_equal(bu.cpu().numpy(), xb)
@@ -288,14 +285,14 @@ def test_fused_range_guard(ctx, form, monkeypatch, dist_mode):
     assert_dist(dist.cpu().numpy(), od, dist_mode if form == "persistent" else "exact")
     # and centroids beyond the range
     Cbig = Cc.clone(); Cbig[2, 0] = 5.0e4
-    a2, d2 = lshkm.lloyd_assign(ctx, X, Cbig, "euclidean")
+    a2, d2 = M.lloyd_assign(c, X, Cbig, "euclidean")
     oa2, od2 = oracle.lloyd_assign(Xh, Cbig.cpu().numpy(), "euclidean", None)
     assert np.array_equal(a2.cpu().numpy(), oa2)
     assert_dist(d2.cpu().numpy(), od2, dist_mode)
 
 
 @pytest.mark.parametrize("case", ["ties", "near", "nonfinite"])
-def test_pruned_exact_pass(ctx, case, monkeypatch, dist_mode):
+def test_pruned_exact_pass(ctx, sctx, sw, case, monkeypatch, dist_mode):
     # the listed-row pass (f32 candidate pruning + exact order on the candidates)
     # against the every-centroid pass and the oracle: duplicate centroids (exact
     # ties, first index must win), near-duplicates (many candidates), and rows
@@ -317,18 +314,18 @@ def test_pruned_exact_pass(ctx, case, monkeypatch, dist_mode):
     a, dist = lshkm.lloyd_assign(ctx, X, C, "euclidean")
     assert ctx.stat(lshkm.STAT_ASSIGN_AMBIG) > 0
     monkeypatch.setenv("LSHKM_EXACT_PASS", "full")
-    a1, d1 = lshkm.lloyd_assign(ctx, X, C, "euclidean")
+    a1, d1 = sw.lloyd_assign(sctx, X, C, "euclidean")
     assert np.array_equal(a.cpu().numpy(), a1.cpu().numpy())
     assert np.array_equal(dist.cpu().numpy().view(np.uint64), d1.cpu().numpy().view(np.uint64))
     sub = np.random.default_rng(4).choice(N, 3000, replace=False)
     oa, od = oracle.lloyd_assign(Xh[sub], Ch, "euclidean", None)
     assert np.array_equal(a.cpu().numpy()[sub], oa)
-    assert_dist_tol(dist.cpu().numpy()[sub], od, dist_mode, 1e-14)   # "near": non-fp32 centroids
+    assert_dist(dist.cpu().numpy()[sub], od, dist_mode)     # "near": non-fp32 centroids, bit for bit
 
 
 @pytest.mark.parametrize("d", [64, 128])
 @pytest.mark.parametrize("case", ["near_parallel", "near_orthogonal", "cancelling"])
-def test_cosine_certified_quotient_adversarial(ctx, case, d, monkeypatch):
+def test_cosine_certified_quotient_adversarial(ctx, sctx, sw, case, d, monkeypatch):
     # exact.h IpAcc: the double-double inner product with the bounded x87
     # rounding must give the soft-x87 bits or decline; every row is checked
     # against the oracle (real long double) on both assignment paths (d = 128:
@@ -354,7 +351,7 @@ def test_cosine_certified_quotient_adversarial(ctx, case, d, monkeypatch):
     Cc = to_dev(ctx, np.ascontiguousarray(Ch))
     a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
     monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
-    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, "cosine")
+    a1, d1 = sw.lloyd_assign(sctx, X, Cc, "cosine")
     oa, od = oracle.lloyd_assign(X.cpu().numpy(), Ch, "cosine", None)
     for a, dd in ((a0, d0), (a1, d1)):
         assert np.array_equal(a.cpu().numpy(), oa)
@@ -362,7 +359,7 @@ def test_cosine_certified_quotient_adversarial(ctx, case, d, monkeypatch):
 
 
 @pytest.mark.parametrize("metric", ["euclidean", "cosine"])
-def test_multipass_persistent_k1024(ctx, metric, monkeypatch, dist_mode):
+def test_multipass_persistent_k1024(ctx, sctx, sw, metric, monkeypatch, dist_mode):
     # K > 256 on the persistent form: one launch per 256-centroid slice with the
     # per-lane (best, runner-up, tile) carried across launches; duplicates in
     # different slices (exact ties: the first index must win) and a ragged last
@@ -377,7 +374,7 @@ def test_multipass_persistent_k1024(ctx, metric, monkeypatch, dist_mode):
     ctx.reset_stats()
     a0, d0 = lshkm.lloyd_assign(ctx, X, Cc, metric)
     monkeypatch.setenv("LSHKM_ASSIGN_PATH", "exact")
-    a1, d1 = lshkm.lloyd_assign(ctx, X, Cc, metric)
+    a1, d1 = sw.lloyd_assign(sctx, X, Cc, metric)
     mode = dist_mode if metric == "euclidean" else "exact"      # cosine distances are exact-order in both
     assert np.array_equal(a0.cpu().numpy(), a1.cpu().numpy())
     assert_dist(d0.cpu().numpy(), d1.cpu().numpy(), mode)
@@ -388,7 +385,7 @@ def test_multipass_persistent_k1024(ctx, metric, monkeypatch, dist_mode):
 
 
 @pytest.mark.parametrize("hashed", [False, True])
-def test_two_image_k1000(ctx, hashed, monkeypatch, dist_mode):
+def test_two_image_k1000(ctx, sctx, sw, hashed, monkeypatch, dist_mode):
     # the opt-in one-launch form for 512 < K <= 1024 (LSHKM_HI_TWO_IMAGE=1): the
     # block swaps 512-centroid images between the halves of each tile; ties
     # across the images, a ragged second image (K = 1000) and a partial last
@@ -400,15 +397,15 @@ def test_two_image_k1000(ctx, hashed, monkeypatch, dist_mode):
     Cc = X[to_dev(ctx, rows)].double()
     Cc[700:710] = Cc[100:110]                         # exact ties across the two images
     V, t, r, _ = lshkm.params_lsh_euclidean(77, L, k, d, 0.4)
-    lsh = lshkm.LSH(ctx, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
 
-    def run():
+    def run(M, c):
         if hashed:
-            return lshkm.hash_assign(lsh, X, Cc, tuples=True, bucket=True)
-        return lshkm.lloyd_assign(ctx, X, Cc, "euclidean")
-    ref = [v.cpu().numpy() for v in run() if v is not None]
+            lsh = M.LSH(c, "euclidean", d, k, L, N // 100, 0.4, V=V, t=t, r=r)
+            return M.hash_assign(lsh, X, Cc, tuples=True, bucket=True)
+        return M.lloyd_assign(c, X, Cc, "euclidean")
+    ref = [v.cpu().numpy() for v in run(lshkm, ctx) if v is not None]
     monkeypatch.setenv("LSHKM_HI_TWO_IMAGE", "1")
-    got = [v.cpu().numpy() for v in run() if v is not None]
+    got = [v.cpu().numpy() for v in run(sw, sctx) if v is not None]
     assert len(ref) == len(got)
     for a, b in zip(ref[:-1], got[:-1]):                 # tuples / buckets / cluster IDs
         assert np.array_equal(a.view(np.uint8), b.view(np.uint8))

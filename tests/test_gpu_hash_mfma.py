@@ -46,6 +46,7 @@ def rows(n, seed, special=True):
 
 
 class fp64_path:
+    """The fp64 hash kernel forced in the test build (LSHKM_HASH_PATH=fp64)."""
     def __enter__(self):
         self.old = os.environ.get("LSHKM_HASH_PATH")
         os.environ["LSHKM_HASH_PATH"] = "fp64"
@@ -64,20 +65,20 @@ def host(t):
 @pytest.mark.parametrize("metric,w,L,k", [("euclidean", 0.4, 5, 4), ("euclidean", 0.01, 5, 4),
                                           ("euclidean", 4.0, 3, 7), ("euclidean", 1.0, 2, 16), ("euclidean", 1.0, 1, 30),
                                           ("cosine", 0.0, 5, 4), ("cosine", 0.0, 4, 8)])
-def test_lsh_hash_mfma_vs_fp64_and_oracle(ctx, metric, w, L, k):
+def test_lsh_hash_mfma_vs_fp64_and_oracle(ctx, sctx, sw, metric, w, L, k):
     N = 50_000 + 17                                 # ragged last tile
     Xh = rows(N, 77)
     X = to_dev(ctx, Xh)
     if metric == "euclidean":
         V, t, r, _ = lshkm.params_lsh_euclidean(123, L, k, D, w)
-        lsh = lshkm.LSH(ctx, metric, D, k, L, N // 100, w, V=V, t=t, r=r)
+        mk = lambda M, c: M.LSH(c, metric, D, k, L, N // 100, w, V=V, t=t, r=r)
     else:
         R, _ = lshkm.params_lsh_cosine(123, L, k, D)
-        lsh = lshkm.LSH(ctx, metric, D, k, L, R=R)
+        mk = lambda M, c: M.LSH(c, metric, D, k, L, R=R)
     ctx.reset_stats()
-    a = [host(v) for v in lsh.hash(X)]
+    a = [host(v) for v in mk(lshkm, ctx).hash(X)]
     with fp64_path():
-        b = [host(v) for v in lsh.hash(X)]
+        b = [host(v) for v in mk(sw, sctx).hash(X)]
     for u, v in zip(a, b):
         assert (u is None) == (v is None)
         if u is not None:
@@ -94,21 +95,21 @@ def test_lsh_hash_mfma_vs_fp64_and_oracle(ctx, metric, w, L, k):
 
 
 @pytest.mark.parametrize("metric", ["euclidean", "cosine"])
-def test_lsh_build_query_mfma_vs_fp64(ctx, metric):
+def test_lsh_build_query_mfma_vs_fp64(ctx, sctx, sw, metric):
     N = 200_000
     X = ctx.synth(0x5EED, N, D)
     if metric == "euclidean":
         V, t, r, _ = lshkm.params_lsh_euclidean(9, 5, 4, D, 0.4)
-        mk = lambda: lshkm.LSH(ctx, metric, D, 4, 5, N // 100, 0.4, V=V, t=t, r=r)
+        mk = lambda M, c: M.LSH(c, metric, D, 4, 5, N // 100, 0.4, V=V, t=t, r=r)
     else:
         R, _ = lshkm.params_lsh_cosine(9, 5, 4, D)
-        mk = lambda: lshkm.LSH(ctx, metric, D, 4, 5, R=R)
+        mk = lambda M, c: M.LSH(c, metric, D, 4, 5, R=R)
     Q = to_dev(ctx, rows(3000, 5))
-    l1 = mk()
+    l1 = mk(lshkm, ctx)
     l1.build(X)
     q1 = l1.query(Q, filtered=metric == "euclidean")
     with fp64_path():
-        l2 = mk()
+        l2 = mk(sw, sctx)
         l2.build(X)
         q2 = l2.query(Q, filtered=metric == "euclidean")
     for tb in range(5):
@@ -119,7 +120,7 @@ def test_lsh_build_query_mfma_vs_fp64(ctx, metric):
 
 
 @pytest.mark.parametrize("metric,k,w", [("euclidean", 14, 2.0), ("euclidean", 12, 0.05), ("cosine", 14, 0.0)])
-def test_cube_mfma_vs_fp64_and_oracle(ctx, metric, k, w):
+def test_cube_mfma_vs_fp64_and_oracle(ctx, sctx, sw, metric, k, w):
     N = 300_000
     Xh = rows(N, 31, special=metric == "cosine")
     if metric == "euclidean":                      # the coin memo needs finite, moderate h values
@@ -127,14 +128,14 @@ def test_cube_mfma_vs_fp64_and_oracle(ctx, metric, k, w):
     X = to_dev(ctx, Xh)
     if metric == "euclidean":
         V, t, st = lshkm.params_cube_euclidean(4242, k, D, w)
-        mk = lambda: lshkm.Cube(ctx, metric, D, k, w, V=V, t=t, rng_state=st)
+        mk = lambda M, c: M.Cube(c, metric, D, k, w, V=V, t=t, rng_state=st)
     else:
         R, st = lshkm.params_cube_cosine(4242, k, D)
-        mk = lambda: lshkm.Cube(ctx, metric, D, k, R=R)
-    c1 = mk()
+        mk = lambda M, c: M.Cube(c, metric, D, k, R=R)
+    c1 = mk(lshkm, ctx)
     c1.build(X)
     with fp64_path():
-        c2 = mk()
+        c2 = mk(sw, sctx)
         c2.build(X)
     p1, i1 = c1.buckets()
     p2, i2 = c2.buckets()
@@ -152,7 +153,7 @@ def test_cube_mfma_vs_fp64_and_oracle(ctx, metric, k, w):
     assert np.array_equal(p1, orp[0]) and np.array_equal(i1, oidx[0])
 
 
-def test_hash_mfma_fixup_counts(ctx):
+def test_hash_mfma_fixup_counts(ctx, sctx, sw):
     # tiny w lists most rows for the fix-up pass; the soft-x87 path runs on the
     # rows whose fp64 bound cannot decide either (exact ties on grid rows)
     N = 20_000
@@ -161,6 +162,7 @@ def test_hash_mfma_fixup_counts(ctx):
     lsh = lshkm.LSH(ctx, "euclidean", D, 4, 5, 1000, 0.001, V=V, t=t, r=r)
     a = [host(v) for v in lsh.hash(to_dev(ctx, Xh))]
     with fp64_path():
-        b = [host(v) for v in lsh.hash(to_dev(ctx, Xh))]
+        lsh2 = sw.LSH(sctx, "euclidean", D, 4, 5, 1000, 0.001, V=V, t=t, r=r)
+        b = [host(v) for v in lsh2.hash(to_dev(ctx, Xh))]
     for u, v in zip(a, b):
         assert np.array_equal(u, v)

@@ -27,17 +27,20 @@ def bits(t):
     return t.cpu().numpy().view(np.uint64)
 
 
-def both(ctx, X, a, C, monkeypatch):
+def both(ctx, X, a, C, monkeypatch, alt):
+    # the product's parallel exact sums vs every (c, j) chain run sequentially
+    # (forced in the test build)
+    sw, sctx = alt
     Cn, cnt, cont = lshkm.kmeans_update(ctx, X, a, C, "euclidean", 0.0)
     monkeypatch.setenv("LSHKM_KM_PATH", "chain")
-    Cs, cs, conts = lshkm.kmeans_update(ctx, X, a, C, "euclidean", 0.0)
+    Cs, cs, conts = sw.kmeans_update(sctx, X, a, C, "euclidean", 0.0)
     monkeypatch.delenv("LSHKM_KM_PATH")
     assert np.array_equal(bits(Cn), bits(Cs)) and np.array_equal(cnt.cpu().numpy(), cs.cpu().numpy()) and cont == conts
     return Cn, cnt
 
 
 @pytest.mark.parametrize("kind", ["synth", "fp32_full", "wide", "special", "skewed", "tiny_coarse", "coarse_huge"])
-def test_parallel_sums_match_chains(ctx, kind, monkeypatch):
+def test_parallel_sums_match_chains(ctx, sctx, sw, kind, monkeypatch):
     rng = np.random.default_rng(11)
     N, d, K = 300_000, 72, 40
     if kind == "synth":
@@ -73,7 +76,7 @@ def test_parallel_sums_match_chains(ctx, kind, monkeypatch):
         a[a == 5] = 6                                                       # an empty one
     X, A = to_dev(ctx, Xh), to_dev(ctx, a)
     C = to_dev(ctx, rng.standard_normal((K, d)))
-    Cn, cnt = both(ctx, X, A, C, monkeypatch)
+    Cn, cnt = both(ctx, X, A, C, monkeypatch, (sw, sctx))
     sub = np.arange(N) < 60_000                                             # oracle on a prefix (its own chains)
     if kind in ("synth", "fp32_full", "tiny_coarse", "coarse_huge"):
         Co, co, _ = oracle.kmeans_update(Xh, a, C.cpu().numpy(), "euclidean", 0.0)
@@ -97,7 +100,7 @@ def test_parallel_sums_carry_mode(ctx):
 
 @pytest.mark.parametrize("kind", ["walk", "drift", "ties", "wide", "special", "skewed"])
 @pytest.mark.parametrize("path", ["seg", "fx"])
-def test_f64_segmented_sums_match_chains(ctx, kind, path, monkeypatch):
+def test_f64_segmented_sums_match_chains(ctx, sctx, sw, kind, path, monkeypatch):
     # fp64 rows (the reference's user vectors): the binade-segment form (kmseg.h,
     # LSHKM_KM_PATH=seg) and the fixed-point + sequential form against the
     # sequential chains, bit for bit, incl. ties in the grid (dyadic values near
@@ -129,20 +132,25 @@ def test_f64_segmented_sums_match_chains(ctx, kind, path, monkeypatch):
         a[a == 5] = 6                                                       # an empty one
     X, A = to_dev(ctx, Xh), to_dev(ctx, a)
     C = to_dev(ctx, rng.standard_normal((K, d)))
-    monkeypatch.setenv("LSHKM_KM_PATH", path)
-    Cn, cnt, _ = lshkm.kmeans_update(ctx, X, A, C, "euclidean", 0.0)
+    if path == "seg":                                   # the product default for fp64 rows
+        Cn, cnt, _ = lshkm.kmeans_update(ctx, X, A, C, "euclidean", 0.0)
+    else:
+        monkeypatch.setenv("LSHKM_KM_PATH", path)
+        Cn, cnt, _ = sw.kmeans_update(sctx, X, A, C, "euclidean", 0.0)
+    # reference runs: the sequential chains in their older 64-dim form, and the oracle
     monkeypatch.setenv("LSHKM_KM_PATH", "chain")
-    Cs, cs, _ = lshkm.kmeans_update(ctx, X, A, C, "euclidean", 0.0)
+    monkeypatch.setenv("LSHKM_KM_CHAIN", "64")
+    Cs, cs, _ = sw.kmeans_update(sctx, X, A, C, "euclidean", 0.0)
     monkeypatch.delenv("LSHKM_KM_PATH")
+    monkeypatch.delenv("LSHKM_KM_CHAIN")
     assert np.array_equal(cnt.cpu().numpy(), cs.cpu().numpy())
     assert np.array_equal(bits(Cn), bits(Cs))
-    if kind in ("walk", "ties"):
-        Co, _, _ = oracle.kmeans_update(Xh, a, C.cpu().numpy(), "euclidean", 0.0)
-        assert np.array_equal(bits(Cn), Co.view(np.uint64))
+    Co, _, _ = oracle.kmeans_update(Xh, a, C.cpu().numpy(), "euclidean", 0.0)
+    assert np.array_equal(bits(Cn), Co.view(np.uint64))
 
 
 @pytest.mark.parametrize("path", ["seg", "chain"])
-def test_f64_segmented_carry_mode(ctx, path, monkeypatch):
+def test_f64_segmented_carry_mode(ctx, sctx, sw, path, monkeypatch):
     # sharded exact mode on fp64 rows: chains continue shard to shard (the carry
     # is each segmented chain's start value)
     rng = np.random.default_rng(4)
@@ -150,10 +158,11 @@ def test_f64_segmented_carry_mode(ctx, path, monkeypatch):
     Xh = rng.standard_normal((N, d)) + 0.1
     a = rng.integers(0, K, N).astype(np.int32)
     X, A = to_dev(ctx, Xh), to_dev(ctx, a)
+    M, c = (lshkm, ctx) if path == "seg" else (sw, sctx)
     monkeypatch.setenv("LSHKM_KM_PATH", path)
     cs = cc = None
     for lo, hi in ((0, 40_000), (40_000, 100_001), (100_001, N)):
-        cs, cc = lshkm.kmeans_partial_carry(ctx, X[lo:hi], A[lo:hi], K, cs, cc)
+        cs, cc = M.kmeans_partial_carry(c, X[lo:hi], A[lo:hi], K, cs, cc)
     monkeypatch.setenv("LSHKM_KM_PATH", "chain")
-    whole_s, whole_c = lshkm.kmeans_partial_carry(ctx, X, A, K)
+    whole_s, whole_c = sw.kmeans_partial_carry(sctx, X, A, K)
     assert np.array_equal(bits(cs), bits(whole_s)) and np.array_equal(cc.cpu().numpy(), whole_c.cpu().numpy())

@@ -1,8 +1,9 @@
 """CPU-side checks of the product's host code (no GPU needed):
 the C-ABI library loads and exports every symbol include/lshkm.h declares,
 the host parameter generation reproduces the reference's RNG draws bit for
-bit, and the soft-x87 emulation used by the kernels' exact paths agrees with
-real x87 long double."""
+bit, the soft-x87 emulation used by the kernels' exact paths agrees with
+real x87 long double, and the restatement of glibc's pow(x, 2) (csrc/gpow2.h)
+agrees with this process's pow."""
 import os
 import subprocess
 
@@ -100,6 +101,38 @@ def test_kmseg_matches_chain(tmp_path):
     out = subprocess.run([str(exe), "30"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "bad=0" in out.stdout
+
+
+def test_pow2_restatement_matches_glibc(tmp_path):
+    # csrc/gpow2.h (glibc 2.35 __pow_fma, operation for operation) vs the real
+    # pow on 7 x 4M inputs: any bit pattern, [0.5, 4), exact ties, the special
+    # ranges, random exponents, squares within 2^-8 ulp of a midpoint (a fifth
+    # of which differ from x*x) and exact squares of every exponent
+    exe = tmp_path / "pow2_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "pow2_check.cpp"), "-lm"], check=True)
+    out = subprocess.run([str(exe), "4"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "total mismatches 0" in out.stdout
+    differ = int(out.stdout.split("pow != x*x on ")[-1].split()[0])
+    assert differ > 100_000, out.stdout            # the inputs do tell pow from x*x
+
+
+def test_pow_selfcheck_in_library():
+    # the library's own host-side check against the process's pow (lshkm_pow_selfcheck)
+    bad, tested = lshkm.pow_selfcheck()
+    assert bad == 0 and tested >= 6000, (bad, tested)
+
+
+def test_release_library_reads_no_environment():
+    # the product library takes no path switches from the environment: no getenv
+    # import at all (the A/B switches live in liblshkm_test.so only)
+    syms = subprocess.run(["nm", "-D", "--undefined-only", os.path.join(PKG, "liblshkm.so")], capture_output=True,
+                          text=True, check=True).stdout
+    assert " getenv" not in syms and "secure_getenv" not in syms, [l for l in syms.splitlines() if "getenv" in l]
+    test_syms = subprocess.run(["nm", "-D", "--undefined-only", os.path.join(PKG, "liblshkm_test.so")],
+                               capture_output=True, text=True, check=True).stdout
+    assert " getenv" in test_syms
 
 
 def test_no_gpu_means_loud_failure():
