@@ -382,9 +382,10 @@ def main():
             counts = it.last_counts.cpu().numpy()
             sims = int(counts[ucl].sum())
             rec = {"what": "get_top_N_recom(neighbors, user, 5) over the user's whole cluster (crypto_rec.hpp:327-345, "
-                           "main.cpp:260-269): x87-exact cosine similarities to every member on every rank "
-                           "(lshkm_cluster_sims), then the prediction sums carried rank to rank in row order "
-                           "(lshkm_cluster_chain, RCCL point-to-point) and the quicksort",
+                           "main.cpp:260-269): x87-exact cosine similarities to every member and the "
+                           "get_predicted_user_sim terms on every rank (lshkm_cluster_terms), then the prediction "
+                           "sums carried rank to rank in row order (lshkm_cluster_chain_terms, RCCL point-to-point) "
+                           "and the quicksort",
                    "users_per_step": args.recom_users, "n_top": 5,
                    "users": "rows i * floor(N_total / Q) of the whole job (their clusters span every shard)",
                    "similarities_per_step": sims, "sims_ms": ph1, "chain_ms": ph2,

@@ -531,9 +531,11 @@ static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int
                                     seg_counts, seg_rows, nseg);
 }
 
+// force_exact: exact distances whatever the context's mode (range
+// assignment's leftover rows: a range assignment is exact-order in either mode)
 static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, int K, int metric,
                        const int32_t* src_rows_host, int32_t* assign, double* dist, lshkm_lsh lsh, int32_t* tuples,
-                       int32_t* phi, int32_t* bucket) {
+                       int32_t* phi, int32_t* bucket, bool force_exact = false) {
     hipStream_t s = ctx->stream;
     const int DP = assign_dp(d);
     const int path = assign_path(metric, d, K, X.f64);
@@ -557,7 +559,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         const bool hi = hi_form;
         // euclidean winner distances: the certified f32 form (default) or the
         // reference-order fp64 chain (LSHKM_DIST_EXACT)
-        const bool fast = !cosine && rows_kind != 2 && fast_dist_on(ctx);
+        const bool fast = !cosine && rows_kind != 2 && !force_exact && fast_dist_on(ctx);
         // exact distances of the hi-only pass: rows whose chain met an inexact
         // square (glibc's pow(x, 2) may differ from x*x) are listed for the fix-up
         const bool pwfix = !cosine && hi && !fast;
@@ -826,10 +828,8 @@ static int range_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, i
             const Pts Xr = X.f64 ? Pts(w[7].as<double>()) : Pts(w[7].as<float>());
             // the range pass's distances are the exact chain; the leftover rows
             // get the same (a range assignment is exact-order in either mode)
-            const int mode = ctx->dist_mode;
-            ctx->dist_mode = LSHKM_DIST_EXACT;
-            rc = assign_impl(ctx, Xr, (int64_t)U, d, C, K, metric, nullptr, ar, dr, nullptr, nullptr, nullptr, nullptr);
-            ctx->dist_mode = mode;
+            rc = assign_impl(ctx, Xr, (int64_t)U, d, C, K, metric, nullptr, ar, dr, nullptr, nullptr, nullptr, nullptr,
+                             true);
             if (rc) return rc;
             if ((rc = launch_range_scatter(s, list, (int64_t)U, ar, dr, assign, dist))) return rc;
         }

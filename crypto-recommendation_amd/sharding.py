@@ -197,12 +197,21 @@ def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, un
     if ev:
         ev[0].record()
     crow, crows = lk.clusters(ctx, assign, K)
-    soff, toff, sims, terms = lk.cluster_terms(ctx, X, x_mean, crow, crows, U, ucl, unk_ptr, unk_idx)
+    # the terms form stages rows of <= 1016 B in 8-B units (lshkm_cluster_terms):
+    # other rows (fp32 of odd d, fp64 of d >= 128) take the sims form, the same
+    # rank-to-rank chain over lshkm_cluster_sims + lshkm_cluster_chain
+    rb = X.shape[1] * X.element_size()
+    if rb % 8 == 0 and rb <= 1016:
+        soff, toff, sims, terms = lk.cluster_terms(ctx, X, x_mean, crow, crows, U, ucl, unk_ptr, unk_idx)
+        args = (ctx, u_mean, unk_ptr, unk_idx, soff, toff, sims, terms)
+        chain = lk.cluster_chain_terms
+    else:
+        soff, sims = lk.cluster_sims(ctx, X, crow, crows, U, ucl, unk_ptr)
+        args = (ctx, X, x_mean, crow, crows, ucl, u_mean, unk_ptr, unk_idx, soff, sims)
+        chain = lk.cluster_chain
     if ev:
         ev[1].record()
     dist = _dist()
-    args = (ctx, u_mean, unk_ptr, unk_idx, soff, toff, sims, terms)
-    chain = lk.cluster_chain_terms
     if dist is None:
         out = chain(*args, carry=None, n_top=n_top)
     else:

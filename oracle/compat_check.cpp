@@ -244,6 +244,31 @@ static void check_cluster_recom(std::vector<Vec>& data, int K) {
             fail(tag + "top-N, user " + std::to_string(q));
         g_stat["cluster_recom_users"]++;
     }
+    // main.cpp:260-269 shaped: every user once through the shim, each call with
+    // a fresh copy of its cluster (the shim's cluster cache uploads a cluster
+    // once, later calls compare it); timed per user
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int q = 0; q < N; q++) {
+        std::vector<Vec*> nb = clusters[users[q].getCluster()];
+        (void)lshkm_compat::get_top_N_recom(nb, users[q], 5);
+    }
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    g_stat["cluster_recom_shim_us_per_user"] = (long)(us / N + 0.5);
+    g_stat["cluster_recom_cache_hits"] = (long)lshkm_compat::cluster_cache().hits;
+    // a member changed in place: its cluster's cached copy must not be used
+    {
+        const int q = 7, c = users[q].getCluster();
+        std::vector<double>& x = *clusters[c][0]->getDimensions();
+        const double keep = x[0];
+        x[0] = keep * 3.0 + 1.0;
+        std::vector<Vec*> na = clusters[c], nb = na;
+        if (get_top_N_recom(na, users[q], 5) != lshkm_compat::get_top_N_recom(nb, users[q], 5))
+            fail(tag + "top-N after a member changed");
+        x[0] = keep;
+        std::vector<Vec*> na2 = clusters[c], nb2 = na2;
+        if (get_top_N_recom(na2, users[q], 5) != lshkm_compat::get_top_N_recom(nb2, users[q], 5))
+            fail(tag + "top-N after the member was restored");
+    }
     std::vector<Vec*> none_a, none_b;
     if (get_top_N_recom(none_a, users[1], 5) != lshkm_compat::get_top_N_recom(none_b, users[1], 5))
         fail(tag + "empty neighbour list");

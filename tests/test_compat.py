@@ -80,4 +80,7 @@ def test_shim_matches_reference_functions(args, mode):
         assert int(stats[key]) > 0, (key, stats)
     assert int(stats["kmeans_euclidean_iterations"]) >= 2 and int(stats["kmeans_cosine_iterations"]) >= 2, stats
     assert int(stats["recom_users"]) >= 30, stats
+    # the per-user shim calls reused the cached clusters (main.cpp-shaped timing in the log)
+    assert int(stats["cluster_recom_cache_hits"]) > 0, stats
+    print("shim get_top_N_recom (3-argument, per user):", stats["cluster_recom_shim_us_per_user"], "us")
     assert int(stats["chain_users"]) >= 100, stats

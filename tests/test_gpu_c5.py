@@ -189,7 +189,11 @@ def test_c5_shard_full_size(ctx):
     #    the modes;
     #  - one sharding.ShardedLloyd iteration at world size 1, fast (all-reduce)
     #    and carry (exact chain) mode: counts and centers bit-exact vs the oracle's
-    #    k_means on the same assignment (update.hpp:37-86).
+    #    k_means on the same assignment (update.hpp:37-86);
+    #  - the recommend step of that iteration as bench.py times it (1,024 users
+    #    spread over the job, get_top_N_recom over their whole clusters of the
+    #    10M rows, main.cpp:260-269): every user's recommendations vs the
+    #    oracle's cluster_top_n (crypto_rec.hpp:327-345).
     sh = _sharding()
     torch = ctx.torch
     N, d, L, k, K, w, world = 10_000_000, 128, 5, 4, 1024, 0.4, 8
@@ -239,15 +243,30 @@ def test_c5_shard_full_size(ctx):
     X64 = oracle.rows64(Xh)
     del Xh
     Cn_o, cnt_o, cont_o = oracle.kmeans_update(X64, assign_h, Cc.cpu().numpy(), "euclidean", 0.0)
-    del X64
     for kmode in ("fast", "exact"):
         it = sh.ShardedLloyd(lshkm, ctx, lsh, X, Cc, src, mode=kmode)
+        if kmode == "fast":
+            # bench.py at one GPU: the job is this shard (users = rows i * floor(N / 1024))
+            it.enable_recommend(N, 0, Q=1024, n_top=5)
         cont = it.step()
         ctx.sync()
         assert np.array_equal(it.assign.cpu().numpy(), assign_h), kmode
         assert np.array_equal(it.last_counts.cpu().numpy(), cnt_o), kmode
         assert cont == cont_o
         assert np.array_equal(it.C.cpu().numpy().view(np.uint64), Cn_o.view(np.uint64)), kmode
+        if kmode == "fast":
+            r = it.recom
+            ucl = it.recom_ucl.cpu().numpy()
+            assert np.array_equal(ucl, assign_h[r["rows"]])
+            crow, crows = oracle.clusters_csr(assign_h, K)
+            want = oracle.cluster_top_n(X64, np.zeros(N), crow, crows, r["U"].cpu().numpy().astype(np.float64),
+                                        r["u_mean"].cpu().numpy(), ucl, r["unk_ptr"].cpu().numpy(),
+                                        r["unk_idx"].cpu().numpy(), 5)
+            got = it.recom_out.cpu().numpy()
+            bad = np.nonzero((got != want).any(1))[0]
+            assert len(bad) == 0, (len(bad), bad[:10])
+            progress("recommend step of 1,024 users over the 10M rows matches the oracle")
+    del X64
 
 
 def test_c4_cube_full_size(ctx):

@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 import oracle
-from amd import lshkm
+from amd import PKG, lshkm
 from conftest import cases, golden, golden_meta
 
 META = golden_meta()
@@ -287,3 +287,30 @@ def test_shard_carry_terms_form(ctx, kind):
             got = lshkm.cluster_chain_terms(*a, carry=carry, n_top=NT).cpu().numpy()
     assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
     assert (want[:, 0] == -1).any()
+
+
+@pytest.mark.parametrize("kind,d", [("f64", 128), ("f32", 37), ("f32", 64)])
+def test_recommend_sharded_row_shapes(ctx, kind, d):
+    # sharding.recommend_sharded at world size 1 on rows the terms form does not
+    # stage (fp64 of d >= 128, fp32 of odd d: the sims form) and on one it does
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("sharding_t", os.path.join(PKG, "sharding.py"))
+    sh = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sh)
+    rng = np.random.default_rng(d)
+    N, K, nq, NT = 9_000, 12, 300, 4
+    X = rng.standard_normal((N, d))
+    X = X.astype(np.float32) if kind == "f32" else X * np.exp(rng.uniform(-1, 1, size=(N, 1)))
+    xm = rng.standard_normal(N) * 0.3
+    assign = rng.integers(0, K, size=N).astype(np.int32)
+    users = rng.choice(N, nq, replace=False)
+    U = X[users].copy()
+    um = rng.standard_normal(nq) * 0.2
+    ucl = assign[users].copy()
+    up, ui = unknown_sets(rng, nq, d)
+    crow, crows = oracle.clusters_csr(assign, K)
+    want = oracle.cluster_top_n(X, xm, crow, crows, U, um, ucl, up, ui, NT)
+    got = sh.recommend_sharded(lshkm, ctx, dev(ctx, X), dev(ctx, xm), dev(ctx, assign), K, dev(ctx, U), dev(ctx, um),
+                               dev(ctx, ucl), dev(ctx, up), dev(ctx, ui), NT).cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
