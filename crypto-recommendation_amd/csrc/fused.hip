@@ -1857,7 +1857,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                 }
                 acc = take_from_upper(acc);
             }
-            const bool hard = pw_hard || __shfl_xor((int)pw_hard, 32) != 0;
+            // the shuffle outside the ||: evaluated only where pw_hard is false, it
+            // would read the other half's lane while that lane is masked off
+            const int pw_other = __shfl_xor((int)pw_hard, 32);
+            const bool hard = pw_hard || pw_other != 0;
             if (h == 1 && valid && cert) {
                 a.assign[row] = I1;
                 if (!hard) a.dist[row] = sqrt(acc);
