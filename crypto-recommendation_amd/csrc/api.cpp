@@ -512,7 +512,7 @@ static bool fast_dist_on(const lshkm_ctx_s* ctx) {
 static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int metric,
                         const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist,
                         const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0,
-                        const int32_t* rows = nullptr) {
+                        const int32_t* rows = nullptr, bool exact_dist = true) {
     if (!rows) rows = (const int32_t*)ctx->ws_ambig.p;
     // K <= 1024, d <= 256: score every centroid in f32 first and run the exact
     // order only on the candidates the bound leaves (euclidean, and cosine on
@@ -526,7 +526,8 @@ static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int
     if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 255) / 256 * 256) * 8))) return rc;
     if (prune)
         return launch_assign_pruned_list(ctx->stream, X, d, C, K, (float*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
-                                         seg_counts, seg_rows, nseg, metric == LSHKM_METRIC_EUCLIDEAN ? 0 : 1);
+                                         seg_counts, seg_rows, nseg, metric == LSHKM_METRIC_EUCLIDEAN ? 0 : 1,
+                                         exact_dist ? 1 : 0);
     return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
                                     seg_counts, seg_rows, nseg);
 }
@@ -669,7 +670,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if (rc) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.final_counts : nullptr,
-                               f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                               f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr, !fast))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (sj.pending) {
             LSHKM_HIP(hipStreamWaitEvent(s, f.join, 0));
             sj.pending = false;

@@ -593,10 +593,38 @@ constexpr int XP_WR = XP_WIDE_ROWS;
 constexpr int XP_WAVES = 4;
 constexpr int XP_SPLIT = XP_SPLITS;
 
-// exact_euclid with the centroid row loaded 16 values at a time (one L2 round
-// trip per 16 terms instead of one per term); x in LDS.
+// The reference's distance of one (row, centroid) pair on the pruned pass:
+// euclidean in exact order; cosine by the soft-x87 chain (16-B loads when the
+// row length allows).
+// The reference's euclidean chain with glibc's pow per square, a rolled loop
+// inlined where it is used: the kernels' rare exact paths (a call would raise
+// the whole kernel to the calling convention's 256 VGPRs).
 template <typename TX>
-__device__ inline double exact_euclid_b16(const TX* __restrict__ x, const double* __restrict__ c, int d) {
+__device__ __attribute__((always_inline)) inline double exact_euclid_rolled(const TX* __restrict__ x,
+                                                                            const double* __restrict__ c, int d) {
+    double acc = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < d; j++) acc = __dadd_rn(acc, gp_sq(__dsub_rn((double)x[j], c[j])));
+    return sqrt(acc);
+}
+
+template <int MET, typename TX>
+__device__ inline double pruned_dist(const TX* __restrict__ x, const double* __restrict__ c, int d) {
+    if constexpr (MET == 0) {
+        return exact_euclid_rolled(x, c, d);
+    } else {
+        if constexpr (sizeof(TX) == 4) {
+            if ((d & 15) == 0) return exact_cosine_x87_b16(x, c, d);
+        }
+        return exact_cosine_x87(x, c, d);
+    }
+}
+
+// The squared euclidean chain of one (row, centroid) pair in the reference's
+// order with x*x squares: the reference's value unless pw.hard() afterwards
+// (some square pow(x, 2) may round differently, gpow2.h).
+template <typename TX>
+__device__ inline double euclid_sumsq_mul(const TX* __restrict__ x, const double* __restrict__ c, int d, PwAcc& pw) {
     double acc = 0.0;
     for (int j0 = 0; j0 < d; j0 += 16) {
         double cv[16];
@@ -606,25 +634,70 @@ __device__ inline double exact_euclid_b16(const TX* __restrict__ x, const double
         for (int t = 0; t < 16; t++)
             if (j0 + t < d) {
                 const double df = __dsub_rn((double)x[j0 + t], cv[t]);
-                acc = __dadd_rn(acc, gp_sq(df));
+                const double p = __dmul_rn(df, df);
+                pw.add<true>(df);
+                acc = __dadd_rn(acc, p);
             }
     }
-    return sqrt(acc);
+    return acc;
 }
 
-// The reference's distance of one (row, centroid) pair on the pruned pass:
-// euclidean in exact order; cosine by the soft-x87 chain (16-B loads when the
-// row length allows).
-template <int MET, typename TX>
-__device__ inline double pruned_dist(const TX* __restrict__ x, const double* __restrict__ c, int d) {
-    if constexpr (MET == 0) {
-        return exact_euclid_b16(x, c, d);
-    } else {
-        if constexpr (sizeof(TX) == 4) {
-            if ((d & 15) == 0) return exact_cosine_x87_b16(x, c, d);
-        }
-        return exact_cosine_x87(x, c, d);
+// (best, bi) over a group of G lanes (xor offsets < G): the smallest value, the
+// first index on ties (assignment.hpp:66-69 strict '<' in index order); bi < 0:
+// no candidate in the lane.
+template <int G>
+__device__ inline void group_argmin(double& best, int& bi) {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) {
+        const double ob = __shfl_xor(best, off);
+        const int oi = __shfl_xor(bi, off);
+        const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
+        if (take) { best = ob; bi = oi; }
     }
+}
+template <int G>
+__device__ inline double group_min(double v) {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    return v;
+}
+
+// The pruned pass's euclidean pick among a group's candidates (lane: centroid c,
+// or c < 0). The chains run with x*x squares; where one of the group holds a
+// square pow may round differently (PwAcc), each chain is within 2^-43 of the
+// reference's (both sums' roundings, <= gamma_255 of the non-negative terms, plus
+// one ulp per square), so the x*x winner stands when every other candidate's sum
+// exceeds its own by 2^-41 relative -- the reference's sums then order the same
+// way and their square roots are distinct doubles. Otherwise every chain is
+// redone with pow (gp_sq). exact_dist (LSHKM_DIST_EXACT): the winner's distance
+// from its pow chain; certified mode keeps the x*x one (2^-44 relative).
+template <int G, typename TX>
+__device__ inline void pruned_pick_euclid(const TX* __restrict__ xr, const double* __restrict__ C, int d, int c,
+                                          bool exact_dist, double& best, int& bi) {
+    PwAcc pw;
+    const double S = c >= 0 ? euclid_sumsq_mul(xr, C + (size_t)c * d, d, pw) : 0.0;
+    const bool hard = c >= 0 && pw.hard();
+    best = c >= 0 ? sqrt(S) : 0.0;
+    bi = c;
+    group_argmin<G>(best, bi);
+    int anyh = hard ? 1 : 0;
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) anyh |= __shfl_xor(anyh, off);
+    if (!anyh) return;                                           // every chain is pow's
+    const double S1 = group_min<G>(c >= 0 && c == bi ? S : __builtin_inf());
+    const double S2 = group_min<G>(c >= 0 && c != bi ? S : __builtin_inf());
+    if (S2 != __builtin_inf() && !(S2 - S1 > 0x1p-41 * S2)) {      // S2 = inf: the lone candidate
+        // too close to call: the reference's chains
+        best = c >= 0 ? exact_euclid_rolled(xr, C + (size_t)c * d, d) : 0.0;
+        bi = c;
+        group_argmin<G>(best, bi);
+        return;
+    }
+    if (!exact_dist) return;
+    const int w = bi;
+    double v = __builtin_inf();
+    if (c == w) v = hard ? exact_euclid_rolled(xr, C + (size_t)c * d, d) : best;
+    best = group_min<G>(v);
 }
 
 __global__ void exact_prep_kernel(const double* __restrict__ C, int K, int Kpad, int d, int xf64,
@@ -685,7 +758,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
     const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
     const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
     const unsigned long long* __restrict__ row_count, int64_t max_rows, int32_t* __restrict__ assign,
-    double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows) {
+    double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows, int exact_dist) {
     constexpr int RL = 64 / R;           // lanes per row in the candidate phase
     __shared__ TX xs[XP_WAVES][R][XB_DMAX];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -816,15 +889,14 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
             }
             double best = 0.0;
             int bi = -1;
-            if (c >= 0) {
-                best = pruned_dist<MET>(xs[wave][r], C + (size_t)c * d, d);
-                bi = c;
-            }
-            for (int off = RL / 2; off >= 1; off >>= 1) {   // within the row's lanes
-                const double ob = __shfl_xor(best, off);
-                const int oi = __shfl_xor(bi, off);
-                const bool take = oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi));
-                if (take) { best = ob; bi = oi; }
+            if constexpr (MET == 0) {
+                pruned_pick_euclid<RL>(xs[wave][r], C, d, c, exact_dist != 0, best, bi);   // within the row's lanes
+            } else {
+                if (c >= 0) {
+                    best = pruned_dist<MET>(xs[wave][r], C + (size_t)c * d, d);
+                    bi = c;
+                }
+                group_argmin<RL>(best, bi);
             }
             if (k == 0 && bi >= 0) {
                 assign[myrow[r]] = bi;
@@ -851,7 +923,9 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_kernel(
                     }
                     seen += n;
                 }
-                if (c >= 0) {
+                if constexpr (MET == 0) {
+                    pruned_pick_euclid<64>(xr, C, d, c, exact_dist != 0, best, bi);
+                } else if (c >= 0) {
                     best = pruned_dist<MET>(xr, C + (size_t)c * d, d);
                     bi = c;
                 }
@@ -891,7 +965,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_wide_kernel(
     const TX* __restrict__ X, int d, const double* __restrict__ C, const float* __restrict__ CT32,
     const float* __restrict__ cconst, int K, int Kpad, const int32_t* __restrict__ rows,
     const unsigned long long* __restrict__ row_count, int64_t max_rows, int32_t* __restrict__ assign,
-    double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows, int nseg) {
+    double* __restrict__ dist, const int32_t* __restrict__ seg_counts, int64_t seg_rows, int nseg, int exact_dist) {
     __shared__ TX xs[XP_WAVES][R][XB_DMAX];
     __shared__ int gpre[XPW_MAXSEG + 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1026,7 +1100,9 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_wide_kernel(
                     }
                     seen += n;
                 }
-                if (c >= 0) {
+                if constexpr (MET == 0) {
+                    pruned_pick_euclid<64>(xr, C, d, c, exact_dist != 0, best, bi);
+                } else if (c >= 0) {
                     best = pruned_dist<MET>(xr, C + (size_t)c * d, d);
                     bi = c;
                 }
@@ -1056,7 +1132,7 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_wide_kernel(
 int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg,
-                              int metric) {
+                              int metric, int exact_dist) {
     if (max_rows <= 0) return 0;
     if (d > XB_DMAX || K > 1024 || (seg_counts && nseg <= 0)) {
         set_error("launch_assign_pruned_list: unsupported shape");
@@ -1076,10 +1152,11 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
     const int64_t blocks = seg_counts ? (int64_t)nseg * XP_SPLIT : std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 2048);
 #define XP_LAUNCH(TX, NCH, RR, MT, XP)                                                                              \
     hipLaunchKernelGGL((assign_pruned_kernel<TX, NCH, RR, MT>), dim3((unsigned)blocks), dim3(64 * XP_WAVES), 0, s, XP, \
-                       d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows)
+                       d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, exact_dist)
 #define XPW_LAUNCH(TX, MT, NC, RW, XP)                                                                           \
     hipLaunchKernelGGL((assign_pruned_wide_kernel<TX, MT, NC, RW>), dim3((unsigned)wblocks), dim3(64 * XP_WAVES), 0, s, \
-                       XP, d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, nseg)
+                       XP, d, C, CT32, cconst, K, Kpad, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, nseg, \
+                       exact_dist)
     const int64_t wblocks = std::min<int64_t>((groups + XP_WAVES - 1) / XP_WAVES, 1024);
     if (flat) {
         if (metric == 1) {

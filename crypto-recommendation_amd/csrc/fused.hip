@@ -963,8 +963,10 @@ __global__ __launch_bounds__(FP_THREADS, 1) void fused_persistent_kernel(FusedAr
                     const double2 cc = cur[j];
                     const double d0 = __dsub_rn(xcur[j].x, cc.x);
                     const double d1 = __dsub_rn(xcur[j].y, cc.y);
-                    sq[2 * j] = gp_sq(d0);
-                    sq[2 * j + 1] = gp_sq(d1);
+                    // LSHKM_DIST_CERTIFIED: x*x (the chain within 2^-44 of the
+                    // reference's, inside the 2^-20 contract); exact: glibc's pow
+                    sq[2 * j] = a.fast_dist ? __dmul_rn(d0, d0) : gp_sq(d0);
+                    sq[2 * j + 1] = a.fast_dist ? __dmul_rn(d1, d1) : gp_sq(d1);
                 }
                 if (h == 0) {
 #pragma unroll
@@ -1623,7 +1625,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
         // (p >> 2) & 3 (the 16 lanes of a ds_read_b128 group on distinct banks).
         const char* gsrc[4];
         uint32_t gbase = 0;
-        const bool g32 = GATH && a.C32 != nullptr && __float_as_uint(a.cbound[7]) == 0u;
+        const bool g32 = GATH && a.C32 != nullptr && (__float_as_uint(a.cbound[7]) & 1u) == 0u;
         const int gstep = g32 ? 64 : 128;                // bytes of one 16-dim step of a row
         if (GATH && !fastd) {
             gbase = (uint32_t)__builtin_amdgcn_readfirstlane(
@@ -1793,7 +1795,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
             __builtin_amdgcn_s_setprio(CHAIN_PRIO);
 #endif
             double acc = 0.0;
-            bool pw_hard = false;
+            PwAcc pw;
             if constexpr (GATH) {
                 wait_step();                                               // step 0 landed
                 asm volatile("" ::: "memory");
@@ -1842,9 +1844,10 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                     sq[2 * j + 1] = __dmul_rn(d1, d1);
                     // the reference squares with glibc pow: x*x is its value when
                     // the square is exact; otherwise the row's distance is redone
-                    // by the fix-up (gpow2.h) -- no row of dataset-row centroids
-                    // of the synthetic data, every row after an update
-                    pw_hard |= !gp_sq_is(d0, sq[2 * j]) || !gp_sq_is(d1, sq[2 * j + 1]);
+                    // by the fix-up (gpow2.h PwAcc: differences of <= 26 bits, and
+                    // for fp64 rows no tiny ones)
+                    pw.add<ROWS == 2>(d0);
+                    pw.add<ROWS == 2>(d1);
                 }
                 if (h == 0) {
 #pragma unroll
@@ -1857,6 +1860,9 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
                 }
                 acc = take_from_upper(acc);
             }
+            // fp32 rows: a difference 0 < |x - c| < 2^-460 needs such a centroid
+            // value (x has >= 2^-149 magnitude or is zero), flagged by the prep
+            const bool pw_hard = pw.hard() || (ROWS != 2 && (__float_as_uint(a.cbound[7]) & 2u) != 0u);
             // the shuffle outside the ||: evaluated only where pw_hard is false, it
             // would read the other half's lane while that lane is masked off
             const int pw_other = __shfl_xor((int)pw_hard, 32);
@@ -2158,7 +2164,8 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
             nbv[c] = b;
         }
     }
-    bool not32 = false;                  // some value of the row is not an f32 (cbound[7])
+    bool not32 = false;                  // some value of the row is not an f32 (cbound[7] bit 0)
+    bool tiny = false;                   // some 0 < |c_j| < 2^-460 (cbound[7] bit 1: PwAcc)
     double rr = 0.0, hh = 0.0;           // |c - ch|^2, |ch|^2 (the hi-only scores' bound)
     double r32 = 0.0;                    // |c - f32(c)|^2 (fast distances)
     for (int j = lane; j < FU_D; j += 64) {
@@ -2167,6 +2174,7 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
         if (C64p) C64p[(size_t)c * FU_D + j] = raw;
         const float f = (float)v;
         not32 |= c < K && (double)f != v;
+        tiny |= c < K && fabs(raw) < 0x1p-460 && raw != 0.0;
         if (C32) {
             C32[(size_t)c * FU_D + j] = f;
             const double e = v - (double)f;       // exact (or inf / nan: never certified)
@@ -2193,12 +2201,13 @@ __global__ void fused_centroid_prep(const double* __restrict__ C, int K, int Kpa
     if (rn32 && lane == 0) rn32[c] = r32 == 0.0 ? 0.f : (float)(sqrt(r32) * (1.0 + 0x1p-40)) * (1.f + 0x1p-22f);
     const unsigned long long anybad = __ballot(bad);
     const unsigned long long any_not32 = __ballot(not32);
+    const unsigned long long any_tiny = __ballot(tiny);
     // per wave (centroid) the bound maxima, then one atomic per word per block:
     // single-word atomics from every centroid serialise (~12 ns each)
     __shared__ unsigned int wmax[FP_PREP_WAVES][8];
     if (lane == 0) {
         unsigned int m[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        m[7] = any_not32 ? 1u : 0u;
+        m[7] = (any_not32 ? 1u : 0u) | (any_tiny ? 2u : 0u);
         if (c >= K) {
             // padding rows: a finite score far below any real one (|x.c| < 2^38 under
             // the range guard), so the packed-index trick never meets an inf/nan

@@ -36,10 +36,12 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define GP_HD __host__ __device__ inline
+#define GP_HDM __host__ __device__ inline
 static __device__ __constant__ const double gp_log_tab_d[128][3] = GP_LOG_TAB_INIT;
 static __device__ __constant__ const uint64_t gp_exp_tab_d[256] = GP_EXP_TAB_INIT;
 #else
 #define GP_HD static inline
+#define GP_HDM inline
 #endif
 static const double gp_log_tab_h[128][3] = GP_LOG_TAB_INIT;
 static const uint64_t gp_exp_tab_h[256] = GP_EXP_TAB_INIT;
@@ -186,6 +188,26 @@ GP_HD double gp_pow2_emul(double x) {
 GP_HD bool gp_sq_is(double x, double p) {
     return (fma(x, x, -p) == 0.0 && fabs(x) >= 0x1p-460) || x == 0.0;
 }
+
+// A sufficient test over a whole chain, without branches or fp64 work: x*x is
+// pow(x, 2) whenever x has at most 26 significant bits (its square then fits
+// the 53-bit significand: pow returns a representable x^2 exactly) and x^2 is
+// not subnormal, so the chain ORs the low 32 bits of every x and checks the low
+// 27 mantissa bits once (one v_or per square, two with v_or3). Zero, inf and
+// nan have no such bits (their pow is x*x). TINY: the caller cannot rule out
+// 0 < |x| < 2^-460 (a square near the subnormal range). hard() is false only
+// if every square of the chain is certainly pow's value; a true hard() only
+// costs a redo (x of 27 bits can still square exactly).
+struct PwAcc {
+    uint32_t lo = 0u;
+    bool tiny = false;
+    template <bool TINY>
+    GP_HDM void add(double x) {
+        lo |= (uint32_t)gp_bits(x);
+        if (TINY) tiny = tiny | ((fabs(x) < 0x1p-460) & (x != 0.0));
+    }
+    GP_HDM bool hard() const { return (lo & 0x07FFFFFFu) != 0u || tiny; }
+};
 
 // pow(x, 2) as the reference computes it: x*x unless x^2 might sit near a
 // rounding midpoint (see the file comment), then the restatement.

@@ -98,12 +98,14 @@ int launch_assign_exact_list(hipStream_t s, Pts X, int d, const double* C, int K
                              const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                              int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
                              int64_t seg_rows = 0, int nseg = 0);
-// Euclidean, listed rows, K <= 256: f32 candidate pruning, then exact order on
+// Euclidean, listed rows, K <= 1024: f32 candidate pruning, then exact order on
 // the candidates only (ws: d * ceil64(K) + ceil64(K) + ceil64(K)/32 floats).
+// exact_dist = 0 (LSHKM_DIST_CERTIFIED): a winner distance may come from the
+// x*x chain (<= 2^-44 relative); cluster IDs are the reference's either way.
 int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
-                              int64_t seg_rows = 0, int nseg = 0, int metric = 0);
+                              int64_t seg_rows = 0, int nseg = 0, int metric = 0, int exact_dist = 1);
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist);
 
