@@ -259,30 +259,6 @@ static int terms_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, c
     return 0;
 }
 
-// The (user, unknown index) slots of rc_chain_terms_kernel (e = -1: a user
-// without unknown indexes), uploaded to ws_call[3] / [4].
-static int chain_slots(lshkm_ctx ctx, const int64_t* unk_ptr, int64_t nq, int64_t* nslot) {
-    std::vector<int64_t> hup((size_t)nq + 1);
-    LSHKM_HIP(hipMemcpyAsync(hup.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
-    std::vector<int32_t> sq, se;
-    for (int64_t q = 0; q < nq; q++) {
-        const int64_t m = hup[q + 1] - hup[q];
-        LSHKM_CHECK(m >= 0 && m < (1ll << 31), LSHKM_ERR_ARG, "bad unknown-index lists");
-        if (m == 0) { sq.push_back((int32_t)q); se.push_back(-1); }
-        for (int64_t e = 0; e < m; e++) { sq.push_back((int32_t)q); se.push_back((int32_t)e); }
-    }
-    *nslot = (int64_t)sq.size();
-    int rc;
-    if ((rc = ctx->ws_call[3].reserve(4 * sq.size() + 4)) || (rc = ctx->ws_call[4].reserve(4 * se.size() + 4))) return rc;
-    if (!sq.empty()) {
-        LSHKM_HIP(hipMemcpyAsync(ctx->ws_call[3].p, sq.data(), 4 * sq.size(), hipMemcpyHostToDevice, ctx->stream));
-        LSHKM_HIP(hipMemcpyAsync(ctx->ws_call[4].p, se.data(), 4 * se.size(), hipMemcpyHostToDevice, ctx->stream));
-    }
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host vectors go out of scope
-    return 0;
-}
-
 static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_t N, int d, const int64_t* crow,
                               const int32_t* crows, int K, Pts U, int64_t nq, const int32_t* ucl,
                               const int64_t* unk_ptr, const int32_t* unk_idx, int64_t* soff_dev, int64_t* toff_dev,
@@ -305,13 +281,14 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     if (sims && terms && soff[nq] <= cap && toff[nq] <= tcap && soff[nq] > 0) {
         LSHKM_CHECK(crows, LSHKM_ERR_ARG, "crows is NULL");
         Buf& map = ctx->ws_call[8];                  // member -> (user, row); the declined-member list + count
-        if ((rc = map.reserve(16 * (size_t)soff[nq] + 16))) return rc;
+        if ((rc = map.reserve(16 * (size_t)soff[nq] + 16 + 8 * (size_t)nq))) return rc;
         int32_t* mq = map.as<int32_t>();
         int64_t* fl = reinterpret_cast<int64_t*>(map.as<char>() + 8 * (size_t)soff[nq]);
+        double* unorm = reinterpret_cast<double*>(fl + soff[nq] + 1);     // the users' |u|^2
         if ((rc = launch_rc_terms(ctx->stream, X, x_mean, d, crow, crows, K, U, nq, ucl, soff_dev, soff[nq], unk_ptr,
                                   unk_idx, toff_dev, sims, terms, mq, mq + soff[nq], fl,
                                   reinterpret_cast<unsigned long long*>(fl + soff[nq]),
-                                  (unsigned long long*)ctx->stats.p + STAT_REC_SOFT)))
+                                  (unsigned long long*)ctx->stats.p + STAT_REC_SOFT, unorm)))
             return rc;
     }
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host offsets are copied before return
@@ -329,17 +306,15 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
     LSHKM_CHECK(out || (main_out && abs_out && cnt_out), LSHKM_ERR_ARG, "either the carry outputs or out");
     if (nq == 0) return 0;
     LSHKM_HIP(hipSetDevice(ctx->device));
-    int64_t nslot = 0, total = 0;
+    int64_t total = 0;
     int rc;
-    if ((rc = chain_slots(ctx, unk_ptr, nq, &nslot))) return rc;
     LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     LSHKM_CHECK(total == 0 || unk_idx, LSHKM_ERR_ARG, "unk_idx is NULL");
     Buf &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
     const size_t M = (size_t)(total > 0 ? total : 1);
     if (out && ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M)))) return rc;
-    if ((rc = launch_rc_chain_terms(ctx->stream, nslot, ctx->ws_call[3].as<int32_t>(), ctx->ws_call[4].as<int32_t>(),
-                                    soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
+    if ((rc = launch_rc_chain_terms(ctx->stream, nq, soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
                                     out ? nullptr : main_out, out ? nullptr : abs_out, out ? nullptr : cnt_out,
                                     out ? pred.as<double>() : nullptr))) {
         (void)hipStreamSynchronize(ctx->stream);

@@ -192,16 +192,15 @@ int launch_rc_cluster_top_n(hipStream_t s, Pts X, const double* x_mean, int d, c
                             unsigned long long* soft_count);
 // The terms form of the clustering recommender (recom.hip): similarities and
 // the per-(member, unknown index) terms of every user at once, then the chains
-// one thread per (user, unknown index), then the quicksort per user.
+// one wave per user (its chains lane by lane), then the quicksort per user.
 int rc_terms_stride8(int d, int elem);
 int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
                     int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
                     const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
                     int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
-                    unsigned long long* soft_count);
-int launch_rc_chain_terms(hipStream_t s, int64_t nslot, const int32_t* slot_q, const int32_t* slot_e,
-                          const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff, const double* sims,
-                          const double* terms, const double* carry_main, const double* carry_abs,
+                    unsigned long long* soft_count, double* unorm);
+int launch_rc_chain_terms(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff,
+                          const double* sims, const double* terms, const double* carry_main, const double* carry_abs,
                           const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,
                           int64_t* cnt_out, double* pred);
 int launch_rc_top(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* carry_cnt, const int64_t* unk_ptr,

@@ -652,10 +652,13 @@ constexpr int CT_STAGE = 64;      // member rows staged per wave
 // The certified similarity of the lane's staged row (8-B units, in dim order)
 // against user row u8 (LDS when the wave's members share one user, else the
 // lane's own global row); ok = false where the certificate declines.
+// ub: the user's sum_j pow(u_j, 2) (rc_user_norm_kernel: the same chain, once
+// per user instead of once per member). Called with u8 in LDS or in global
+// memory, never a generic pointer (flat loads wait on both counters).
 template <typename T>
-__device__ inline double ct_sim(const uint64_t* myrow8, const uint64_t* u8, int nunit, bool& ok) {
+__device__ inline double ct_sim(const uint64_t* myrow8, const uint64_t* u8, int nunit, double ub, bool& ok) {
     constexpr int PER = 8 / (int)sizeof(T);
-    double ub = 0.0, xa = 0.0;
+    double xa = 0.0;
     IpAcc ip;
     auto step = [&](uint64_t xw, uint64_t uw) {
         T xv[PER], uv[PER];
@@ -664,7 +667,6 @@ __device__ inline double ct_sim(const uint64_t* myrow8, const uint64_t* u8, int 
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const double xj = (double)xv[k], uj = (double)uv[k];
-            ub = __dadd_rn(ub, sq_of<T>(uj));
             ip.add(__dmul_rn(xj, uj));
             xa = __dadd_rn(xa, sq_of<T>(xj));
         }
@@ -682,6 +684,18 @@ __device__ inline double ct_sim(const uint64_t* myrow8, const uint64_t* u8, int 
     double sv, qr;
     ok = ip.quot_status(denom, sv, qr) == 0;        // declined: rc_terms_fix_kernel decides
     return sv;
+}
+
+// The users' sum_j pow(u_j, 2) in j order (cosineSimilarity's |u|^2,
+// cust_vector.hpp:166-170), lane per user.
+template <typename T>
+__global__ __launch_bounds__(256) void rc_user_norm_kernel(const T* __restrict__ U, int64_t nq, int d,
+                                                           double* __restrict__ ub) {
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+        double b = 0.0;
+        for (int j = 0; j < d; j++) b = __dadd_rn(b, sq_of<T>((double)U[q * d + j]));
+        ub[q] = b;
+    }
 }
 
 // Member g's user and dataset row (the flattened pair space of rc_terms_kernel).
@@ -707,7 +721,7 @@ __global__ __launch_bounds__(64) void rc_terms_kernel(
     const int32_t* __restrict__ mem_q, const int32_t* __restrict__ mem_r, const int64_t* __restrict__ soff,
     const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx, const int64_t* __restrict__ toff,
     double* __restrict__ sims, double* __restrict__ terms, int stride8, int64_t* __restrict__ fix_list,
-    unsigned long long* __restrict__ fix_count) {
+    unsigned long long* __restrict__ fix_count, const double* __restrict__ unorm) {
     constexpr int SB = 16;                          // rows per staging batch (loads in flight)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x;
@@ -781,7 +795,9 @@ __global__ __launch_bounds__(64) void rc_terms_kernel(
         __syncthreads();
         const T* u = U + (int64_t)q * d;
         bool ok;
-        const double sv = ct_sim<T>(myrow8, one ? ustage : reinterpret_cast<const uint64_t*>(u), nunit, ok);
+        double sv;
+        if (one) sv = ct_sim<T>(myrow8, ustage, nunit, unorm[q0], ok);            // wave-uniform
+        else sv = ct_sim<T>(myrow8, reinterpret_cast<const uint64_t*>(u), nunit, unorm[q], ok);
         // declined certificates (~12% of random pairs: cancelling inner products
         // widen the bound) to the list of rc_terms_fix_kernel, which runs the x87
         // chain with every lane busy (inline it cost each wave the chain's full
@@ -798,12 +814,10 @@ __global__ __launch_bounds__(64) void rc_terms_kernel(
         if (terms) {
             const int64_t o = unk_ptr[q];
             const int m = (int)(unk_ptr[q + 1] - o);
-            const int64_t n = soff[q + 1] - soff[q];
             const double mean = x_mean[r];
             const T* xr = reinterpret_cast<const T*>(myrow8);
-            double* tq = terms + toff[q] + i;
-            for (int e = 0; e < m; e++)
-                tq[(int64_t)e * n] = __dmul_rn(sv, __dsub_rn((double)xr[unk_idx[o + e]], mean));
+            double* tq = terms + toff[q] + i * m;           // member-major: the pair's m terms together
+            for (int e = 0; e < m; e++) tq[e] = __dmul_rn(sv, __dsub_rn((double)xr[unk_idx[o + e]], mean));
         }
     }
 }
@@ -818,7 +832,8 @@ __global__ __launch_bounds__(64) void rc_terms_fix_kernel(
     const int32_t* __restrict__ mem_q, const int32_t* __restrict__ mem_r, const int64_t* __restrict__ soff,
     const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx, const int64_t* __restrict__ toff,
     double* __restrict__ sims, double* __restrict__ terms, const int64_t* __restrict__ fix_list,
-    const unsigned long long* __restrict__ fix_count, int stride8, unsigned long long* __restrict__ soft_count) {
+    const unsigned long long* __restrict__ fix_count, int stride8, unsigned long long* __restrict__ soft_count,
+    const double* __restrict__ unorm) {
     constexpr int SB = 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x;
@@ -854,14 +869,14 @@ __global__ __launch_bounds__(64) void rc_terms_fix_kernel(
             }
         }
         __syncthreads();
-        double xa = 0.0, ub = 0.0;
+        double xa = 0.0;
+        const double ub = unorm[q];
         X87acc ip;
         ip.init();
         for (int j = 0; j < d; j++) {
             const double xj = (double)myx[j], uj = (double)myu[j];
             ip.add(__dmul_rn(xj, uj));
             xa = __dadd_rn(xa, sq_of<T>(xj));
-            ub = __dadd_rn(ub, sq_of<T>(uj));
         }
         const double sv = x87_quot(ip.value(), __dmul_rn(sqrt(xa), sqrt(ub)));
         if (!on) continue;
@@ -869,71 +884,107 @@ __global__ __launch_bounds__(64) void rc_terms_fix_kernel(
         if (terms) {
             const int64_t o = unk_ptr[q];
             const int m = (int)(unk_ptr[q + 1] - o);
-            const int64_t n = soff[q + 1] - soff[q], i = g - soff[q];
+            const int64_t i = g - soff[q];
             const double mean = x_mean[r];
-            double* tq = terms + toff[q] + i;
-            for (int e = 0; e < m; e++) tq[(int64_t)e * n] = __dmul_rn(sv, __dsub_rn((double)myx[unk_idx[o + e]], mean));
+            double* tq = terms + toff[q] + i * m;
+            for (int e = 0; e < m; e++) tq[e] = __dmul_rn(sv, __dsub_rn((double)myx[unk_idx[o + e]], mean));
         }
     }
 }
 
-// slot = (user q, unknown index e); e = -1: a user without unknown indexes (its
-// |sim| sum and count only). carry_*: the previous rank's sums (NULL: first);
-// pred == NULL: the running sums out, else the predictions.
-__global__ __launch_bounds__(64) void rc_chain_terms_kernel(
-    int64_t nslot, const int32_t* __restrict__ slot_q, const int32_t* __restrict__ slot_e,
-    const int64_t* __restrict__ soff, const int64_t* __restrict__ unk_ptr, const int64_t* __restrict__ toff,
-    const double* __restrict__ sims, const double* __restrict__ terms, const double* __restrict__ carry_main,
-    const double* __restrict__ carry_abs, const int64_t* __restrict__ carry_cnt, const double* __restrict__ u_mean,
-    double* __restrict__ main_out, double* __restrict__ abs_out, int64_t* __restrict__ cnt_out,
-    double* __restrict__ pred) {
-    constexpr int B = 32;                           // values per buffer; two buffers in flight
-    const int64_t L = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (L >= nslot) return;
-    const int q = slot_q[L], e = slot_e[L];
-    const int64_t b0 = soff[q], n = soff[q + 1] - b0;
-    const int64_t ui = unk_ptr[q] + (e < 0 ? 0 : e);
-    const double* sp = sims + b0;
-    const double* tp = terms + toff[q] + (e < 0 ? 0 : (int64_t)e * n);
-    double acc = (carry_main && e >= 0) ? carry_main[ui] : 0.0;
-    double as = carry_abs ? carry_abs[q] : 0.0;
-    const bool te = e >= 0;
-    double sa[B], ta[B], sb[B], tb[B];
-    auto ld = [&](int64_t i0, double (&sv)[B], double (&tv)[B]) {
+// One wave per user q: its get_predicted_user_sim chains (crypto_rec.hpp:290-296)
+// -- per unknown index e, main_e = sum_i sim_i * (x_i[e] - mean_i), and the
+// |sim| sum -- each one sequential fp64 adds in member order, as the
+// reference's. The wave streams 64 members at a time (the sims coalesced, the
+// block's terms member-major: 64 x m contiguous doubles per user), transposes
+// the block through LDS, and lane k adds chain k's 64 values in order (lane
+// RC_CH: the |sim| chain), the next block's loads in flight meanwhile (the
+// round-4 form, one thread per chain reading its own stream, waited on ~20K
+// dependent loads per thread with 128 waves on the chip). Users with more than
+// RC_CH unknown indexes run their chains in groups (|sim| with the first).
+// carry_*: the previous rank's sums (NULL: first rank); pred == NULL: the
+// running sums out, else the predictions (:299-302).
+constexpr int RC_CH = 8;                  // chains per group
+constexpr int RC_LS = 65;                 // LDS row stride (doubles; reads run to t0 + 15 <= 63)
+constexpr int RC_PF = 4;                  // blocks of 64 members in flight
+__global__ __launch_bounds__(64) void rc_chain_user_kernel(
+    int64_t nq, const int64_t* __restrict__ soff, const int64_t* __restrict__ unk_ptr,
+    const int64_t* __restrict__ toff, const double* __restrict__ sims, const double* __restrict__ terms,
+    const double* __restrict__ carry_main, const double* __restrict__ carry_abs,
+    const int64_t* __restrict__ carry_cnt, const double* __restrict__ u_mean, double* __restrict__ main_out,
+    double* __restrict__ abs_out, int64_t* __restrict__ cnt_out, double* __restrict__ pred) {
+    __shared__ double blk[(RC_CH + 1) * RC_LS];
+    __shared__ double as_sh;
+    const int lane = threadIdx.x;
+    for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int64_t b0 = soff[q], n = soff[q + 1] - b0;
+        const int64_t u0 = unk_ptr[q];
+        const int m = (int)(unk_ptr[q + 1] - u0);
+        const double* sp = sims + b0;
+        const double* tq = terms + toff[q];
+        for (int c0 = 0; c0 < (m > 0 ? m : 1); c0 += RC_CH) {
+            const int nc = min(RC_CH, m - c0);                 // chains of this group (<= 0: none)
+            const bool first = c0 == 0;
+            const bool mine = lane < nc;
+            const bool absl = lane == RC_CH && first;
+            double acc = 0.0;
+            if (mine) acc = carry_main ? carry_main[u0 + c0 + lane] : 0.0;
+            if (absl) acc = carry_abs ? carry_abs[q] : 0.0;
+            // v[k]: chain c0 + k's value of member i0 + lane (k < nc); v[RC_CH]: its sim
+            auto load_blk = [&](int64_t i0, double (&v)[RC_CH + 1]) {
+                const int64_t i = min(i0 + lane, n - 1);
 #pragma unroll
-        for (int k = 0; k < B; k++) {
-            const int64_t ii = min(i0 + k, n - 1);
-            sv[k] = sp[ii];
-            tv[k] = te ? tp[ii] : 0.0;
-        }
-    };
-    if (n > 0) {
-        ld(0, sa, ta);
-        for (int64_t i0 = 0; i0 < n; i0 += 2 * B) {
-            ld(i0 + B, sb, tb);
+                for (int k = 0; k < RC_CH; k++) v[k] = k < nc ? tq[i * m + c0 + k] : 0.0;
+                v[RC_CH] = first ? sp[i] : 0.0;
+            };
+            if (n > 0) {
+                // a ring of RC_PF blocks in flight (one block's adds take ~0.5 us,
+                // a load round trip several); the LDS reads of a chain in
+                // batches of 16 ahead of their dependent adds
+                double ring[RC_PF][RC_CH + 1];
 #pragma unroll
-            for (int k = 0; k < B; k++)
-                if (i0 + k < n) {
-                    as = __dadd_rn(as, fabs(sa[k]));
-                    acc = __dadd_rn(acc, ta[k]);
+                for (int p = 0; p < RC_PF; p++)
+                    if ((int64_t)p * 64 < n) load_blk((int64_t)p * 64, ring[p]);
+                for (int64_t i0 = 0; i0 < n; i0 += 64 * RC_PF) {
+#pragma unroll
+                    for (int p = 0; p < RC_PF; p++) {
+                        const int64_t ib = i0 + (int64_t)p * 64;
+                        if (ib >= n) break;                       // wave-uniform
+#pragma unroll
+                        for (int k = 0; k <= RC_CH; k++) blk[k * RC_LS + lane] = ring[p][k];
+                        __syncthreads();
+                        if (ib + 64 * RC_PF < n) load_blk(ib + 64 * RC_PF, ring[p]);
+                        const int cnt = (int)min((int64_t)64, n - ib);
+                        if (mine || absl) {
+                            const double* row = blk + lane * RC_LS;
+                            for (int t0 = 0; t0 < cnt; t0 += 16) {
+                                double v[16];
+#pragma unroll
+                                for (int k = 0; k < 16; k++) v[k] = row[t0 + k];   // < RC_LS: in the row
+#pragma unroll
+                                for (int k = 0; k < 16; k++)
+                                    if (t0 + k < cnt) acc = __dadd_rn(acc, mine ? v[k] : fabs(v[k]));
+                            }
+                        }
+                        __syncthreads();
+                    }
                 }
-            ld(i0 + 2 * B, sa, ta);
-#pragma unroll
-            for (int k = 0; k < B; k++)
-                if (i0 + B + k < n) {
-                    as = __dadd_rn(as, fabs(sb[k]));
-                    acc = __dadd_rn(acc, tb[k]);
+            }
+            // the |sim| sum to every lane (each prediction divides by it)
+            if (absl) as_sh = acc;
+            __syncthreads();
+            const double as = as_sh;
+            if (pred) {
+                if (mine) pred[u0 + c0 + lane] = __dadd_rn(__ddiv_rn(acc, as), u_mean[q]);
+            } else {
+                if (mine) main_out[u0 + c0 + lane] = acc;
+                if (absl) {
+                    abs_out[q] = acc;
+                    cnt_out[q] = (carry_cnt ? carry_cnt[q] : 0) + n;
                 }
+            }
+            __syncthreads();
         }
-    }
-    if (pred) {
-        if (te) pred[ui] = __dadd_rn(__ddiv_rn(acc, as), u_mean[q]);      // crypto_rec.hpp:299-302
-        return;
-    }
-    if (te) main_out[ui] = acc;
-    if (e <= 0) {
-        abs_out[q] = as;
-        cnt_out[q] = (carry_cnt ? carry_cnt[q] : 0) + n;
     }
 }
 
@@ -965,8 +1016,7 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
                     int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
                     const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
                     int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
-                    unsigned long long* soft_count) {
-    (void)K;
+                    unsigned long long* soft_count, double* unorm) {
     if (nq <= 0 || total <= 0) return 0;
     const int elem = X.f64 ? 8 : 4;
     if (((int64_t)d * elem) % 8 != 0) return -1;
@@ -975,36 +1025,39 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
     if (2 * lds > 160 * 1024) return -1;
     hipLaunchKernelGGL(rc_member_map_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0, s, nq, soff, ucl,
                        crow, crows, mem_q, mem_r);
+    if (X.f64)
+        hipLaunchKernelGGL(rc_user_norm_kernel<double>, dim3(gsz(nq, 256, 1024)), dim3(256), 0, s, U.d(), nq, d, unorm);
+    else
+        hipLaunchKernelGGL(rc_user_norm_kernel<float>, dim3(gsz(nq, 256, 1024)), dim3(256), 0, s, U.f(), nq, d, unorm);
     const dim3 grid(gsz(total, CT_STAGE, 4096));
     if (hipMemsetAsync(fix_count, 0, 8, s) != hipSuccess) return kstatus("rc_terms (memset)");
     if (X.f64)
         hipLaunchKernelGGL(rc_terms_kernel<double>, grid, dim3(64), lds, s, X.d(), x_mean, d, U.d(), total, mem_q, mem_r,
-                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count);
+                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
     else
         hipLaunchKernelGGL(rc_terms_kernel<float>, grid, dim3(64), lds, s, X.f(), x_mean, d, U.f(), total, mem_q, mem_r,
-                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count);
+                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
     // the list length is on the device: a grid for up to ~1/4 of the pairs, looping beyond
     const dim3 fgrid(gsz(total / 4 + 1, CT_STAGE, 2048));
     const size_t flds = 2 * lds;
     if (X.f64)
         hipLaunchKernelGGL(rc_terms_fix_kernel<double>, fgrid, dim3(64), flds, s, X.d(), x_mean, d, U.d(), mem_q, mem_r,
-                           soff, unk_ptr, unk_idx, toff, sims, terms, fix_list, fix_count, stride8, soft_count);
+                           soff, unk_ptr, unk_idx, toff, sims, terms, fix_list, fix_count, stride8, soft_count, unorm);
     else
         hipLaunchKernelGGL(rc_terms_fix_kernel<float>, fgrid, dim3(64), flds, s, X.f(), x_mean, d, U.f(), mem_q, mem_r,
-                           soff, unk_ptr, unk_idx, toff, sims, terms, fix_list, fix_count, stride8, soft_count);
+                           soff, unk_ptr, unk_idx, toff, sims, terms, fix_list, fix_count, stride8, soft_count, unorm);
     return kstatus("rc_terms_kernel");
 }
 
-int launch_rc_chain_terms(hipStream_t s, int64_t nslot, const int32_t* slot_q, const int32_t* slot_e,
-                          const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff, const double* sims,
-                          const double* terms, const double* carry_main, const double* carry_abs,
+int launch_rc_chain_terms(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff,
+                          const double* sims, const double* terms, const double* carry_main, const double* carry_abs,
                           const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,
                           int64_t* cnt_out, double* pred) {
-    if (nslot <= 0) return 0;
-    hipLaunchKernelGGL(rc_chain_terms_kernel, dim3((unsigned)((nslot + 63) / 64)), dim3(64), 0, s, nslot, slot_q, slot_e,
-                       soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean, main_out, abs_out,
-                       cnt_out, pred);
-    return kstatus("rc_chain_terms_kernel");
+    if (nq <= 0) return 0;
+    hipLaunchKernelGGL(rc_chain_user_kernel, dim3((unsigned)std::min<int64_t>(nq, 65536)), dim3(64), 0, s, nq, soff,
+                       unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean, main_out, abs_out, cnt_out,
+                       pred);
+    return kstatus("rc_chain_user_kernel");
 }
 
 int launch_rc_top(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* carry_cnt, const int64_t* unk_ptr,

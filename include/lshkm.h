@@ -460,8 +460,8 @@ int lshkm_cluster_chain_f64(lshkm_ctx ctx, const double* X_dev, const double* x_
  * sim_i * (x_i[index] - mean_i) (crypto_rec.hpp:296) while the member rows are
  * on chip, so the rank-to-rank chain reads no rows.
  * lshkm_cluster_terms: soff_dev / toff_dev [nq+1] <- the offsets of each user's
- *   similarities (member order) and terms (unknown-index-major: toff[q] +
- *   e * n_q + i); sims_dev [cap] / terms_dev [tcap] filled when the totals
+ *   similarities (member order) and terms (member-major: toff[q] + i * m_q + e,
+ *   m_q = the user's unknown indexes); sims_dev [cap] / terms_dev [tcap] filled when the totals
  *   (*total_host, *tterms_host) fit (NULL to size). Rows of d * sizeof(elem) a
  *   multiple of 8 B and at most 1016 B (else LSHKM_ERR_ARG: the form above).
  * lshkm_cluster_chain_terms: lshkm_cluster_chain from them (same carry and
