@@ -507,18 +507,32 @@ static bool fast_dist_on(const lshkm_ctx_s* ctx) {
     return ctx->dist_mode == LSHKM_DIST_CERTIFIED;
 }
 
+// K <= 1024, d <= 256: the exact pass scores every centroid in f32 first and
+// runs the exact order only on the candidates the bound leaves (euclidean, and
+// cosine on fp32 rows); LSHKM_EXACT_PASS=full: every centroid
+static bool exact_pruned(Pts X, int d, int K, int metric) {
+    return K <= 1024 && d <= 256 && !test_switch("LSHKM_EXACT_PASS", "full") &&
+           (metric == LSHKM_METRIC_EUCLIDEAN || !X.f64);
+}
+
+// The pruned pass's centroid prep ahead of the fused pass (ws_ct): the listed
+// rows' pass then starts as soon as the refinement ends.
+static int exact_listed_prep(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int metric) {
+    int rc;
+    if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 255) / 256 * 256) * 8))) return rc;
+    return launch_assign_pruned_prep(ctx->stream, X.f64, d, C, K, (float*)ctx->ws_ct.p,
+                                     metric == LSHKM_METRIC_EUCLIDEAN ? 0 : 1);
+}
+
 // Exact reference-order pass over the rows listed in ws_ambig (count on device).
 // Segmented lists (seg_counts != NULL) come from the persistent fused form.
+// prepped: exact_listed_prep ran for these centroids on this stream.
 static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int metric,
                         const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist,
                         const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0,
-                        const int32_t* rows = nullptr, bool exact_dist = true) {
+                        const int32_t* rows = nullptr, bool exact_dist = true, bool prepped = false) {
     if (!rows) rows = (const int32_t*)ctx->ws_ambig.p;
-    // K <= 1024, d <= 256: score every centroid in f32 first and run the exact
-    // order only on the candidates the bound leaves (euclidean, and cosine on
-    // fp32 rows); LSHKM_EXACT_PASS=full: every centroid
-    const bool prune = K <= 1024 && d <= 256 && !test_switch("LSHKM_EXACT_PASS", "full") &&
-                       (metric == LSHKM_METRIC_EUCLIDEAN || !X.f64);
+    const bool prune = exact_pruned(X, d, K, metric);
     if (!prune && (metric != LSHKM_METRIC_EUCLIDEAN || (!seg_counts && d > 256)))
         return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist, seg_counts,
                                    seg_rows, nseg);
@@ -527,7 +541,7 @@ static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int
     if (prune)
         return launch_assign_pruned_list(ctx->stream, X, d, C, K, (float*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
                                          seg_counts, seg_rows, nseg, metric == LSHKM_METRIC_EUCLIDEAN ? 0 : 1,
-                                         exact_dist ? 1 : 0);
+                                         exact_dist ? 1 : 0, prepped);
     return launch_assign_exact_list(ctx->stream, X, d, C, K, (double*)ctx->ws_ct.p, rows, cnt, N, assign, dist,
                                     seg_counts, seg_rows, nseg);
 }
@@ -605,6 +619,8 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         // the timed fused pass starts before the centroid prep
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[0], s));
         if ((rc = launch_fused_prep(s, C, K, Kpad, Ch, Cl, cnh, cbound, cosine ? 1 : 0, nbv, C32, rn32, d, C64p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        const bool xprep = exact_pruned(X, d, K, metric);
+        if (xprep && (rc = exact_listed_prep(ctx, X, d, C, K, metric))) { LSHKM_LAUNCH_CHECK(); return rc; }
         FusedLaunch f;
         f.C32 = C32; f.rn32 = rn32; f.fast_dist = fast ? 1 : 0;
         f.rows = rows_kind; f.d = d; f.Cd = C;
@@ -670,7 +686,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if (rc) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.final_counts : nullptr,
-                               f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr, !fast))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                               f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr, !fast, xprep))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (sj.pending) {
             LSHKM_HIP(hipStreamWaitEvent(s, f.join, 0));
             sj.pending = false;

@@ -560,12 +560,22 @@ int lshkm_cube_get_memo(lshkm_cube cube, int32_t* f, int32_t* h, int32_t* bit, i
 }
 
 // ------------------------------------------------------------------- k-means
+// csr_crow / csr_rows: the cluster CSR of this assignment from lshkm_clusters
+// (the caller's; NULL: built here into the context's slots).
 static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign, int K, double* sums,
-                   int64_t* counts, const double* carry = nullptr, const int64_t* carry_counts = nullptr) {
+                   int64_t* counts, const double* carry = nullptr, const int64_t* carry_counts = nullptr,
+                   const int64_t* csr_crow = nullptr, const int32_t* csr_rows = nullptr) {
     int rc;
-    if ((rc = reserve(ctx, WS_ROWS, (size_t)std::max<int64_t>(N, 1) * 4)) || (rc = reserve(ctx, WS_CROW, (size_t)(K + 1) * 8)))
-        return rc;
-    if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
+    const int32_t* rows_p = csr_rows;
+    const int64_t* crow_p = csr_crow;
+    if (!crow_p) {
+        if ((rc = reserve(ctx, WS_ROWS, (size_t)std::max<int64_t>(N, 1) * 4)) ||
+            (rc = reserve(ctx, WS_CROW, (size_t)(K + 1) * 8)))
+            return rc;
+        if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
+        rows_p = slot<int32_t>(ctx, WS_ROWS);
+        crow_p = slot<int64_t>(ctx, WS_CROW);
+    }
     // Parallel exact sums (fixed point where the chain provably never rounds);
     // test switch LSHKM_KM_PATH=chain runs every (c, j) chain sequentially.
     const bool force_chain = test_switch("LSHKM_KM_PATH", "chain");
@@ -578,7 +588,7 @@ static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign
     if (X.f64 && !force_chain && !test_switch("LSHKM_KM_PATH", "fx") && K <= 65535) {
         const size_t wsb = km_seg_ws_bytes(N, K, d);
         if (wsb <= KM_SEG_WS_CAP && ctx->ws_range[11].reserve(wsb) == 0) {
-            if ((rc = launch_km_sums_seg(ctx->stream, X.d(), d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW),
+            if ((rc = launch_km_sums_seg(ctx->stream, X.d(), d, rows_p, crow_p,
                                          K, N, sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
             return 0;
         }
@@ -586,11 +596,11 @@ static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign
     }
     if (!force_chain) {
         if ((rc = ctx->ws_range[11].reserve(km_fx_ws_bytes(K, d)))) return rc;
-        if ((rc = launch_km_sums_fx(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, N,
+        if ((rc = launch_km_sums_fx(ctx->stream, X, d, rows_p, crow_p, K, N,
                                     sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
         return 0;
     }
-    if ((rc = launch_km_chain(ctx->stream, X, d, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, sums, counts,
+    if ((rc = launch_km_chain(ctx->stream, X, d, rows_p, crow_p, K, sums, counts,
                               carry, carry_counts))) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;
 }
@@ -657,6 +667,25 @@ int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X, int64_t N, int d, const 
 int lshkm_kmeans_partial_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int32_t* assign, int K,
                              double* sums, int64_t* counts) {
     return kmeans_partial_impl(ctx, X, N, d, assign, K, sums, counts);
+}
+
+static int kmeans_partial_csr_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64_t* crow, const int32_t* rows,
+                                   int K, double* sums, int64_t* counts) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && crow && (rows || N == 0) && sums && counts && N >= 0 && N < (1ll << 31) &&
+                    d > 0 && K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    return km_sums(ctx, X, N, d, nullptr, K, sums, counts, nullptr, nullptr, crow, rows);
+}
+
+int lshkm_kmeans_partial_csr(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow, const int32_t* rows,
+                             int K, double* sums, int64_t* counts) {
+    return kmeans_partial_csr_impl(ctx, X, N, d, crow, rows, K, sums, counts);
+}
+
+int lshkm_kmeans_partial_csr_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int64_t* crow,
+                                 const int32_t* rows, int K, double* sums, int64_t* counts) {
+    return kmeans_partial_csr_impl(ctx, X, N, d, crow, rows, K, sums, counts);
 }
 
 int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X, int64_t N, int d, const int32_t* assign, int K,

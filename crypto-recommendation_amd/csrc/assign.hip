@@ -1129,10 +1129,23 @@ __global__ __launch_bounds__(64 * XP_WAVES) void assign_pruned_wide_kernel(
     }
 }
 
+int launch_assign_pruned_prep(hipStream_t s, bool xf64, int d, const double* C, int K, float* ws, int metric) {
+    if (d > XB_DMAX || K > 1024) {
+        set_error("launch_assign_pruned_prep: unsupported shape");
+        return -1;
+    }
+    const int Kpad = (K + 63) / 64 * 64;
+    float* cconst = ws + (size_t)d * Kpad;
+    if (hipMemsetAsync(cconst + Kpad, 0, (size_t)(Kpad / 64) * 2 * 4, s) != hipSuccess) return kstatus("pruned prep");
+    hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, d, xf64 ? 1 : 0, ws, cconst,
+                       metric);
+    return kstatus("exact_prep_kernel");
+}
+
 int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg,
-                              int metric, int exact_dist) {
+                              int metric, int exact_dist, bool prepped) {
     if (max_rows <= 0) return 0;
     if (d > XB_DMAX || K > 1024 || (seg_counts && nseg <= 0)) {
         set_error("launch_assign_pruned_list: unsupported shape");
@@ -1141,9 +1154,10 @@ int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int 
     const int Kpad = (K + 63) / 64 * 64;
     float* CT32 = ws;
     float* cconst = ws + (size_t)d * Kpad;
-    (void)hipMemsetAsync(cconst + Kpad, 0, (size_t)(Kpad / 64) * 2 * 4, s);
-    hipLaunchKernelGGL(exact_prep_kernel, dim3((unsigned)Kpad), dim3(64), 0, s, C, K, Kpad, d, X.f64 ? 1 : 0, CT32,
-                       cconst, metric);
+    if (!prepped) {
+        int rc = launch_assign_pruned_prep(s, X.f64, d, C, K, ws, metric);
+        if (rc) return rc;
+    }
     // K <= 256: 8 rows per wave over 4 chunks; K <= 1024: 2 rows per wave over 16
     const bool wide = Kpad > 256;
     const bool flat = wide && (!seg_counts || nseg <= XPW_MAXSEG);

@@ -105,7 +105,12 @@ int launch_assign_exact_list(hipStream_t s, Pts X, int d, const double* C, int K
 int launch_assign_pruned_list(hipStream_t s, Pts X, int d, const double* C, int K, float* ws,
                               const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
                               int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
-                              int64_t seg_rows = 0, int nseg = 0, int metric = 0, int exact_dist = 1);
+                              int64_t seg_rows = 0, int nseg = 0, int metric = 0, int exact_dist = 1,
+                              bool prepped = false);
+// The centroid-only part of the pruned pass (f32 transposed centroids, |c|^2,
+// the chunk bounds into ws): launched before the fused pass, off its tail;
+// then launch_assign_pruned_list(..., prepped = true).
+int launch_assign_pruned_prep(hipStream_t s, bool xf64, int d, const double* C, int K, float* ws, int metric);
 int launch_assign_override(hipStream_t s, const int32_t* src_rows, int K, int64_t N, int32_t* assign,
                            double* dist);
 

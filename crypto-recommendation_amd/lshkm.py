@@ -114,6 +114,7 @@ def lib():
             "lshkm_kmeans_update": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, f64, vp, vp, C.POINTER(i32)]),
             "lshkm_kmeans_partial": (i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
             "lshkm_kmeans_partial_carry": (i32, [vp, vp, i64, i32, vp, i32, vp, vp, vp, vp]),
+            "lshkm_kmeans_partial_csr": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp]),
             "lshkm_kmeans_finalize": (i32, [vp, vp, vp, i32, i32, vp, i32, f64, vp, C.POINTER(i32)]),
             "lshkm_kmeans_pp": (i32, [vp, vp, i64, i32, i32, i32, u64, vp]),
             "lshkm_rand_selection": (i32, [u64, i64, i32, vp]),
@@ -536,12 +537,18 @@ def kmeans_update(ctx, X, assign, C_old, metric="euclidean", min_dist=0.0):
     return Cn, cnt, bool(cont.value)
 
 
-def kmeans_partial(ctx, X, assign, K, sums=None, counts=None):
+def kmeans_partial(ctx, X, assign, K, sums=None, counts=None, csr=None):
+    """Per-shard exact sums (lshkm_kmeans_partial); csr = (crow, rows) of this
+    assignment from clusters(): lshkm_kmeans_partial_csr, no second sort."""
     torch = ctx.torch
     N, d = X.shape
     sums = ctx.empty((K, d), torch.float64) if sums is None else sums
     counts = ctx.empty((K,), torch.int64) if counts is None else counts
-    _ck(_fn("lshkm_kmeans_partial", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K, _t_ptr(sums), _t_ptr(counts)))
+    if csr is not None:
+        _ck(_fn("lshkm_kmeans_partial_csr", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(csr[0]), _t_ptr(csr[1]), K, _t_ptr(sums),
+                                               _t_ptr(counts)))
+    else:
+        _ck(_fn("lshkm_kmeans_partial", X)(ctx.h, _t_ptr(X), N, d, _t_ptr(assign), K, _t_ptr(sums), _t_ptr(counts)))
     return sums, counts
 
 

@@ -172,7 +172,7 @@ def allreduce_partials(sums, counts):
     return sums, counts
 
 
-def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, unk_idx, n_top, timing=None):
+def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, unk_idx, n_top, timing=None, csr=None):
     """The clustering recommender over row shards (main.cpp:260-269 on the
     sharded rows; get_top_N_recom's 3-argument overload, crypto_rec.hpp:327-345).
 
@@ -191,12 +191,13 @@ def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, un
          n_top) and broadcasts the [nq][n_top] result.
     Bit for bit lshkm_cluster_top_n over the concatenated rows. Returns the
     result on every rank (device tensor). timing: optional list that receives
-    (ms of phases 1, 2+3) from CUDA events."""
+    (ms of phases 1, 2+3) from CUDA events. csr: (crow, crows) of this
+    assignment when the caller built it already (ShardedLloyd's sums)."""
     torch = ctx.torch
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timing is not None else None
     if ev:
         ev[0].record()
-    crow, crows = lk.clusters(ctx, assign, K)
+    crow, crows = csr if csr is not None else lk.clusters(ctx, assign, K)
     # the terms form stages rows of <= 1016 B in 8-B units (lshkm_cluster_terms):
     # other rows (fp32 of odd d, fp64 of d >= 128) take the sims form, the same
     # rank-to-rank chain over lshkm_cluster_sims + lshkm_cluster_chain
@@ -310,6 +311,7 @@ class ShardedLloyd:
         self.timing = False       # True: HIP events around the exchange (bench.py's breakdown)
         self.exchange_events = []
         self.recom = None         # enable_recommend(): the C5 recommend step after each update
+        self.csr = None           # (crow, crows) of this iteration's assignment (recommend runs)
 
     def step(self):
         import ctypes as C
@@ -330,7 +332,10 @@ class ShardedLloyd:
                 return lk.kmeans_partial_carry(ctx, X, self.assign, self.K, cs, cc)
             sums, counts = chain_partials(local, self.sums, self.counts)
         else:
-            sums, counts = lk.kmeans_partial(ctx, X, self.assign, self.K, self.sums, self.counts)
+            # with the recommend step, the cluster CSR of this assignment is built
+            # once and serves both the sums and the recommender
+            self.csr = lk.clusters(ctx, self.assign, self.K) if self.recom is not None else None
+            sums, counts = lk.kmeans_partial(ctx, X, self.assign, self.K, self.sums, self.counts, csr=self.csr)
             if self.timing:
                 ev = [ctx.torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 ev[0].record()
@@ -369,7 +374,7 @@ class ShardedLloyd:
         self.recom_ucl = ucl
         self.recom_out = recommend_sharded(self.lk, self.ctx, self.X, r["x_mean"], self.assign, self.K, r["U"],
                                            r["u_mean"], ucl, r["unk_ptr"], r["unk_idx"], r["n_top"],
-                                           timing=self.recom_timing)
+                                           timing=self.recom_timing, csr=getattr(self, "csr", None))
         return self.recom_out
 
     def exchange_ms(self):

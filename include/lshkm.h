@@ -292,6 +292,14 @@ int lshkm_kmeans_partial(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, co
                          int K, double* sums_dev, int64_t* counts_dev);
 int lshkm_kmeans_partial_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int32_t* assign_dev,
                              int K, double* sums_dev, int64_t* counts_dev);
+/* lshkm_kmeans_partial over the cluster CSR lshkm_clusters returned for the
+ * same assignment (crow_dev [K+1], rows_dev [N]): the same sums without a
+ * second sort when the caller needs the CSR anyway (the C5 iteration's
+ * recommend step, main.cpp:261 over separate_clusters_from_input). */
+int lshkm_kmeans_partial_csr(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                             const int32_t* rows_dev, int K, double* sums_dev, int64_t* counts_dev);
+int lshkm_kmeans_partial_csr_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                                 const int32_t* rows_dev, int K, double* sums_dev, int64_t* counts_dev);
 /* Sharded update (exact mode): the per-(c, j) chains continue from
  * carry_sums_dev / carry_counts_dev (the previous shard's result, or NULL for
  * the first shard), so passing the carry shard to shard in row order gives the

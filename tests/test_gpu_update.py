@@ -166,3 +166,21 @@ def test_f64_segmented_carry_mode(ctx, sctx, sw, path, monkeypatch):
     monkeypatch.setenv("LSHKM_KM_PATH", "chain")
     whole_s, whole_c = sw.kmeans_partial_carry(sctx, X, A, K)
     assert np.array_equal(bits(cs), bits(whole_s)) and np.array_equal(cc.cpu().numpy(), whole_c.cpu().numpy())
+
+
+@pytest.mark.parametrize("kind", ["f32", "f64"])
+def test_partial_over_given_csr(ctx, kind):
+    # lshkm_kmeans_partial_csr (the C5 iteration shares lshkm_clusters' CSR with
+    # the recommend step) == lshkm_kmeans_partial bit for bit, empty clusters
+    # included; the f64 rows take the binade-segment sums
+    rng = np.random.default_rng(31 if kind == "f32" else 32)
+    N, d, K = 200_003, 40, 97
+    Xh = rng.standard_normal((N, d))
+    Xh = Xh.astype(np.float32) if kind == "f32" else Xh * np.exp(rng.uniform(-3, 3, size=(N, 1)))
+    A = rng.integers(0, K, size=N).astype(np.int32)
+    A[A == 5] = 6                                            # cluster 5 empty
+    X, a = to_dev(ctx, Xh), to_dev(ctx, A)
+    s0, c0 = lshkm.kmeans_partial(ctx, X, a, K)
+    csr = lshkm.clusters(ctx, a, K)
+    s1, c1 = lshkm.kmeans_partial(ctx, X, a, K, csr=csr)
+    assert np.array_equal(bits(s0), bits(s1)) and np.array_equal(c0.cpu().numpy(), c1.cpu().numpy())
