@@ -1108,11 +1108,14 @@ constexpr int FH_WAVES_MIN = 8, FH_WAVES_MAX = 12;
 // Cosine winner distance from the row in registers, both lane halves busy.
 // Lane half h owns dims 16s + 8h..+7 (s = 0..7). Each half accumulates the
 // double products of ITS dims with IpAcc's double-double (exact.h), in its own
-// order; the reference's x87 chain runs over all 128 in order, so the error
-// term sum_k |S_k| of IpAcc is bounded by the halves' own partials: S_k =
-// A_k + B_k, A held during the other half's blocks of 8 -> ts <= ts0 + ts1 +
-// 8 (sum_s |A_end(s)| + sum_{s<7} |B_end(s)|), max |S_k| <= mx0 + mx1 (a looser
-// but rigorous radius; exact.h quot_status decides). |x|^2 is the reference's
+// order; the reference's x87 chain runs over all 128 in order (block 2s = half
+// 0's step s, block 2s + 1 = half 1's), so its partial sums are S_k = A_k +
+// B_end(s-1) in half 0's block s and S_k = B_k + A_end(s) in half 1's. The
+// halves trade their running sums after every step: half 0 adds |A_k + B_end(s-1)|
+// exactly as the reference's partial sum, half 1 |B_k + A_end(s-1)| plus
+// 8 |A_end(s) - A_end(s-1)| (the block it runs one step behind) -- the round-4
+// bound 8 (sum |A_end| + sum |B_end|) roughly doubled sum_k |S_k| and declined
+// 9.3 % of the C3 winners. max |S_k| <= mx0 + mx1 (exact.h quot_status decides). |x|^2 is the reference's
 // sequential chain, the halves taking turns (the euclidean winner's pattern).
 // Returns 0 (certified, v = 1 - q), 1 / 2 (declined: soft-x87 fix-up).
 __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* __restrict__ crow_h, double nbv, int h,
@@ -1139,7 +1142,8 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
         xa = take_from_upper(xa);
     }
     // the inner product, each half over its own dims
-    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0, hold = 0.0;
+    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0;
+    double off = 0.0;                     // half 0: B_end(s-1); half 1: A_end(s-1)
     double2 cb[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 2 * j);
@@ -1160,14 +1164,18 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
             const double e = __dadd_rn(__dsub_rn(sh, __dsub_rn(t, bb)), __dsub_rn(pj, bb));   // TwoSum
             sh = t;
             sl = __dadd_rn(sl, e);
-            ts = __dadd_rn(ts, fabs(t));
+            ts = __dadd_rn(ts, fabs(__dadd_rn(t, off)));
             mx = fmax(mx, fabs(t));
         }
-        hold = __dadd_rn(hold, fabs(sh));
+        // trade the running sums: half 0 takes B_end(s), half 1 A_end(s) (and
+        // charges the block it ran behind: 8 |A_end(s) - A_end(s-1)|)
+        const double other = swap_halves(sh, h);
+        if (h == 1) ts = __dadd_rn(ts, 8.0 * fabs(__dsub_rn(other, off)));
+        off = other;
     }
     // the lower half's accumulator to the upper lanes
     const double sh0 = swap_halves(sh, h), sl0 = swap_halves(sl, h), ts0 = swap_halves(ts, h);
-    const double mx0 = swap_halves(mx, h), hold0 = swap_halves(hold, h);
+    const double mx0 = swap_halves(mx, h);
     if (h == 0) return 2;                 // the upper lanes finish
     IpAcc ip;
     const double t = __dadd_rn(sh0, sh);
@@ -1175,8 +1183,12 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
     const double e = __dadd_rn(__dsub_rn(sh0, __dsub_rn(t, bb)), __dsub_rn(sh, bb));
     ip.sh = t;
     ip.sl = __dadd_rn(__dadd_rn(sl0, sl), e);
-    // sum_k |S_k| bound (rounded up: + 2^-50 relative for the adds here)
-    ip.ts = __dadd_rn(__dadd_rn(ts0, ts), 8.0 * __dadd_rn(hold0, __dsub_rn(hold, fabs(sh)))) * (1.0 + 0x1p-50);
+    // sum_k |S_k| bound, rounded up: + 2^-47 relative for the roundings of
+    // |A_k + B_end| and of the sums here; the partial sums stand in for the
+    // exact ones (their TwoSum rests: |sl| <= 64 2^-53 max|t| per half, over 128
+    // terms and the offsets <= 2^-38 (mx0 + mx1), absolute: a cancelling
+    // A_k + B_end must not hide them)
+    ip.ts = __dadd_rn(__dadd_rn(ts0, ts) * (1.0 + 0x1p-47), 0x1p-37 * __dadd_rn(mx0, mx));
     ip.mx = __dadd_rn(mx0, mx) * (1.0 + 0x1p-50);
     double q, qr;
     const int st = ip.quot_status(__dmul_rn(sqrt(xa), sqrt(nbv)), q, qr);
@@ -1195,7 +1207,8 @@ __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc,
     double2 xn[4], xnn[4];
     load_x64_step(a, rowc, 0, h, xn);
     load_x64_step(a, rowc, 1, h, xnn);
-    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0, hold = 0.0;
+    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0;
+    double off = 0.0;                     // as cosine_winner_halves
     double2 cb[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) cb[j] = *reinterpret_cast<const double2*>(crow_h + 2 * j);
@@ -1221,13 +1234,15 @@ __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc,
             const double e = __dadd_rn(__dsub_rn(sh, __dsub_rn(t, bb)), __dsub_rn(pj, bb));   // TwoSum
             sh = t;
             sl = __dadd_rn(sl, e);
-            ts = __dadd_rn(ts, fabs(t));
+            ts = __dadd_rn(ts, fabs(__dadd_rn(t, off)));
             mx = fmax(mx, fabs(t));
         }
-        hold = __dadd_rn(hold, fabs(sh));
+        const double other = swap_halves(sh, h);
+        if (h == 1) ts = __dadd_rn(ts, 8.0 * fabs(__dsub_rn(other, off)));
+        off = other;
     }
     const double sh0 = swap_halves(sh, h), sl0 = swap_halves(sl, h), ts0 = swap_halves(ts, h);
-    const double mx0 = swap_halves(mx, h), hold0 = swap_halves(hold, h);
+    const double mx0 = swap_halves(mx, h);
     if (h == 0) return 2;
     const double xa = a.xn2[rowc];
     IpAcc ip;
@@ -1236,7 +1251,7 @@ __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc,
     const double e = __dadd_rn(__dsub_rn(sh0, __dsub_rn(t, bb)), __dsub_rn(sh, bb));
     ip.sh = t;
     ip.sl = __dadd_rn(__dadd_rn(sl0, sl), e);
-    ip.ts = __dadd_rn(__dadd_rn(ts0, ts), 8.0 * __dadd_rn(hold0, __dsub_rn(hold, fabs(sh)))) * (1.0 + 0x1p-50);
+    ip.ts = __dadd_rn(__dadd_rn(ts0, ts) * (1.0 + 0x1p-47), 0x1p-37 * __dadd_rn(mx0, mx));   // as above
     ip.mx = __dadd_rn(mx0, mx) * (1.0 + 0x1p-50);
     double q, qr;
     const int st = ip.quot_status(__dmul_rn(sqrt(xa), sqrt(nbv)), q, qr);
