@@ -167,6 +167,89 @@ __device__ inline double exact_euclid_pf(const T* __restrict__ x, const U* __res
     return sqrt(acc);
 }
 
+// The fix-up chains above with the whole wave in step (every lane calls them;
+// a lane without a row repeats another's): each 8 terms' squares go through
+// gp_sq_wave (sq: wave-private LDS), so the wave evaluates
+// glibc's restatement for the few squares that need it in one batch instead of
+// serialising one lane's restatement after another (a wave of lane chains
+// holds one such square in nearly every term). sq: 64 * 8 doubles (euclidean,
+// cosine on fp32 rows) or 64 * 16 (cosine on fp64 rows).
+template <bool VEC, typename T, typename U>
+__device__ inline void pf_load8(const T* __restrict__ x, const U* __restrict__ c, int j0, int d, T (&xn)[8],
+                                U (&cn)[8]) {
+    if constexpr (VEC) {
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const float4 v = *reinterpret_cast<const float4*>(x + j0 + 4 * t);
+            xn[4 * t] = v.x; xn[4 * t + 1] = v.y; xn[4 * t + 2] = v.z; xn[4 * t + 3] = v.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const double2 v = *reinterpret_cast<const double2*>(c + j0 + 2 * t);
+            cn[2 * t] = v.x; cn[2 * t + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            xn[t] = j0 + t < d ? x[j0 + t] : (T)0;
+            cn[t] = j0 + t < d ? c[j0 + t] : (U)0;
+        }
+    }
+}
+
+template <bool VEC, typename T, typename U>
+__device__ inline double exact_euclid_wave(const T* __restrict__ x, const U* __restrict__ c, int d, double* sq) {
+    double acc = 0.0;
+    T xn[8];
+    U cn[8];
+    pf_load8<VEC>(x, c, 0, d, xn, cn);
+    for (int j0 = 0; j0 < d; j0 += 8) {
+        double df[8], p[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) df[t] = __dsub_rn((double)xn[t], (double)cn[t]);
+        if (j0 + 8 < d) pf_load8<VEC>(x, c, j0 + 8, d, xn, cn);
+        gp_sq_wave<8>(df, p, sq);
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (!VEC && j0 + t >= d) break;
+            acc = __dadd_rn(acc, p[t]);
+        }
+    }
+    return sqrt(acc);
+}
+
+template <bool VEC, typename T, typename U>
+__device__ inline double exact_cosine_x87_wave(const T* __restrict__ x, const U* __restrict__ c, int d, double* sq) {
+    static_assert(sizeof(U) == 8, "fp64 centroids");
+    constexpr int NS = sizeof(T) == 8 ? 16 : 8;         // squares through gp_sq_wave per 8 terms
+    X87acc ip;
+    ip.init();
+    double a = 0.0, b = 0.0;
+    T xn[8];
+    U cn[8];
+    pf_load8<VEC>(x, c, 0, d, xn, cn);
+    for (int j0 = 0; j0 < d; j0 += 8) {
+        double xv[8], cv[8], v[NS], p[NS];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            xv[t] = (double)xn[t];
+            cv[t] = (double)cn[t];
+            v[t] = cv[t];
+            if constexpr (NS == 16) v[8 + t] = xv[t];
+        }
+        if (j0 + 8 < d) pf_load8<VEC>(x, c, j0 + 8, d, xn, cn);
+        gp_sq_wave<NS>(v, p, sq);
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            if (!VEC && j0 + t >= d) break;
+            ip.add(__dmul_rn(xv[t], cv[t]));
+            a = __dadd_rn(a, NS == 16 ? p[8 + t] : __dmul_rn(xv[t], xv[t]));
+            b = __dadd_rn(b, p[t]);
+        }
+    }
+    return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
+}
+
 // fp32 rows of d % 16 == 0 (16-B aligned rows)
 __device__ inline double exact_cosine_x87_b16(const float* __restrict__ x, const double* __restrict__ c, int d) {
     return exact_cosine_x87_pf<true>(x, c, d);

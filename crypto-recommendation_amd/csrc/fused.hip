@@ -2586,9 +2586,9 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
 
 // Winners listed by the fused kernels for their distance alone: lane per row.
 // Cosine (MET = 1): the certificate declined, the x87 chain decides
-// (exact_cosine_x87_pf). Euclidean (MET = 0, exact distances): a square of the
-// chain was inexact, so glibc's pow(x, 2) may differ from x*x -- the chain
-// again with gp_sq (exact_euclid_pf). CF_SPLIT blocks per list segment; both
+// (exact_cosine_x87_wave). Euclidean (MET = 0, exact distances): a square of
+// the chain was inexact, so glibc's pow(x, 2) may differ from x*x -- the chain
+// again with glibc's pow (exact_euclid_wave). CF_SPLIT blocks per list segment; both
 // lists of a call (the hi-only pass's and the refinement's) in ONE launch, so
 // the short list's lone chains (~40 us of latency) overlap the long one.
 constexpr int CF_SPLIT = 8;
@@ -2609,25 +2609,26 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__
     const int n = cl.counts[li][2 * seg + 1];
     const unsigned long long* l = cl.list[li] + (int64_t)seg * seg_rows;
     const bool vec = sizeof(TX) == 4 && d % 8 == 0 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)C & 15) == 0;
-    for (int i = part * 256 + threadIdx.x; i < n; i += CF_SPLIT * 256) {
-        const int64_t row = (int64_t)l[i];
+    __shared__ double sqs[4][64 * 16];                   // gp_sq_wave: 64 * NV per wave
+    double* sq = sqs[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    // wave-uniform trip count (the chains run the whole wave in step); a lane
+    // past the list end repeats the wave's first row and writes nothing
+    for (int i0 = part * 256 + (threadIdx.x & ~63); i0 < n; i0 += CF_SPLIT * 256) {
+        const int i = i0 + lane;
+        const bool live = i < n;
+        const int64_t row = (int64_t)l[live ? i : i0];
         const TX* xr = X + row * d;
         const double* cr = C + (size_t)assign[row] * d;
+        double v;
         if constexpr (MET == 1) {
-            if (sizeof(TX) == 4 && d == FU_D) {
-                dist[row] = exact_cosine_x87_b16(reinterpret_cast<const float*>(xr), cr, FU_D);
-                continue;
-            }
-            dist[row] = exact_cosine_x87_pf<false>(xr, cr, d);
+            if (vec) v = exact_cosine_x87_wave<sizeof(TX) == 4>(xr, cr, d, sq);
+            else v = exact_cosine_x87_wave<false>(xr, cr, d, sq);
         } else {
-            if constexpr (sizeof(TX) == 4) {
-                if (vec) {
-                    dist[row] = exact_euclid_pf<true>(xr, cr, d);
-                    continue;
-                }
-            }
-            dist[row] = exact_euclid_pf<false>(xr, cr, d);
+            if (vec) v = exact_euclid_wave<sizeof(TX) == 4>(xr, cr, d, sq);
+            else v = exact_euclid_wave<false>(xr, cr, d, sq);
         }
+        if (live) dist[row] = v;
     }
 }
 
@@ -2635,11 +2636,24 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__
 // cosineDistance, cust_vector.hpp:148-151) for fp64 rows, lane per row.
 __global__ __launch_bounds__(256) void row_sumsq_kernel(const double* __restrict__ X, int64_t N, int d,
                                                          double* __restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256) {
-        const double* x = X + i * d;
+    __shared__ double sqs[4][64 * 8];                    // gp_sq_wave: 64 * NV per wave
+    double* sq = sqs[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    // wave-uniform trip count: lanes past N repeat row N - 1 and write nothing
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); i0 < N; i0 += (int64_t)gridDim.x * 256) {
+        const int64_t i = i0 + lane;
+        const double* x = X + (i < N ? i : N - 1) * d;
         double a = 0.0;
-        for (int j = 0; j < d; j++) a = __dadd_rn(a, gp_sq(x[j]));
-        out[i] = a;
+        for (int j0 = 0; j0 < d; j0 += 8) {
+            double v[8], p[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) v[t] = j0 + t < d ? x[j0 + t] : 0.0;
+            gp_sq_wave<8>(v, p, sq);
+#pragma unroll
+            for (int t = 0; t < 8; t++)
+                if (j0 + t < d) a = __dadd_rn(a, p[t]);
+        }
+        if (i < N) out[i] = a;
     }
 }
 

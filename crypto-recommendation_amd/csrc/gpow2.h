@@ -209,19 +209,72 @@ struct PwAcc {
     GP_HDM bool hard() const { return (lo & 0x07FFFFFFu) != 0u || tiny; }
 };
 
+// True when p = x*x might not be pow(x, 2): |x| outside [2^-40, 2^40) (x != 0),
+// x^2 just below a power of two, or x^2 within 2^-5 ulp of a rounding midpoint
+// (see the file comment). The midpoint test without the ulp: with x^2 = p + e
+// exactly, fma(e, K, p) for K = 16/15 (1 + 2^-40) rounds back to p iff |e K|
+// <= ulp/2, i.e. |e| < 15/32 ulp: more than 1/32 ulp from the midpoint (an
+// exact square, e = 0, always passes). ~9 VALU per square.
+GP_HD bool gp_sq_slow(double x, double p) {
+    const double e = fma(x, x, -p);                        // x^2 = p + e exactly
+    const double r = fma(e, 0x1.1111111112223p+0, p);      // K rounded up
+    const double ax = fabs(x);
+    const uint32_t hp = (uint32_t)(gp_bits(p) >> 32);
+    const bool out = !(ax >= 0x1p-40 && ax < 0x1p40);      // nan too
+    const bool pow2_below = (hp & 0xFFFFFu) == 0u && e < 0.0;   // ulp below p is ulp/2: restate
+    return (r != p || out || pow2_below) && x != 0.0;
+}
+
 // pow(x, 2) as the reference computes it: x*x unless x^2 might sit near a
 // rounding midpoint (see the file comment), then the restatement.
 GP_HD double gp_sq(double x) {
     const double p = x * x;
-    if (gp_sq_is(x, p)) return p;                          // exact square
-    const double ax = fabs(x);
-    if (ax >= 0x1p-40 && ax <= 0x1p40) {
-        const double e = fma(x, x, -p);                    // x^2 = p + e exactly
-        const uint64_t pb = gp_bits(p);
-        const double u = gp_dbl(pb & 0x7ff0000000000000ull) * 0x1p-52;   // ulp above p
-        // at a power of two with x^2 below it the midpoint is u/4 away: restate
-        const bool pow2_below = (pb & 0x000fffffffffffffull) == 0 && e < 0.0;
-        if (!pow2_below && fabs(fabs(e) - 0.5 * u) > 0x1p-5 * u) return p;
-    }
-    return gp_pow2_emul(x);
+    return gp_sq_slow(x, p) ? gp_pow2_emul(x) : p;
 }
+
+#if defined(__HIPCC__)
+// NV squares per lane for a whole wave: p[j] = pow(x[j], 2). The few squares
+// that need the restatement (~4 % of differences of fp32 values, ~6 % of
+// general doubles) are packed from all lanes into lds (64 * NV doubles,
+// wave-private; slots by ballot prefix counts, no scan) and evaluated 64 at a
+// time, one per lane: a lane-per-chain gp_sq makes the wave run the
+// restatement for nearly every term (a 64-lane wave almost always holds one
+// such square). All 64 lanes must call it together.
+template <int NV>
+__device__ inline void gp_sq_wave(const double (&x)[NV], double (&p)[NV], double* lds) {
+    static_assert(NV <= 32, "lds holds 64 * NV doubles");
+    bool sl[NV];
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        p[j] = __dmul_rn(x[j], x[j]);
+        sl[j] = gp_sq_slow(x[j], p[j]);
+        any = any || sl[j];
+    }
+    if (__ballot(any) == 0ull) return;
+    int pos[NV];
+    int total = 0;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        const unsigned long long m = __ballot(sl[j]);
+        pos[j] = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        total += __popcll(m);
+        if (sl[j]) lds[pos[j]] = x[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int lane = (int)__lane_id();
+    for (int b = 0; b < total; b += 64)
+        if (b + lane < total) lds[b + lane] = gp_pow2_emul(lds[b + lane]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < NV; j++)
+        if (sl[j]) p[j] = lds[pos[j]];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");     // the next call's deposits come after these reads
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#endif

@@ -156,6 +156,8 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
     static_assert(!VEC || sizeof(TX) == 4, "the float4 form reads fp32 rows");
     constexpr int DJ = sizeof(TX) == 4 ? KPP_DJ : KPP_DJ / 2;     // tile <= 34 KiB either way
     __shared__ TX tile[KPP_THREADS][DJ + 1];
+    __shared__ double sqs[METRIC == 0 ? KPP_THREADS / 64 : 1][64 * 8];   // gp_sq_wave: 64 * 8 per wave
+    double* sqb = sqs[METRIC == 0 ? threadIdx.x >> 6 : 0];
     // the newest centroid's row, widened to fp64 once per block (LDS broadcast
     // reads in the chain instead of a uniform global load per dim)
     extern __shared__ __attribute__((aligned(8))) char kpp_dyn[];
@@ -214,18 +216,34 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
                         pf[k] = *reinterpret_cast<const float4*>(X + (row0 + r) * d + j0 + DJ + part * 4);
                 }
             }
-            if (n < N) {
+            if (METRIC == 0) {
+                // the whole block (rows past N too: their sums are dropped), the
+                // squares through gp_sq_wave (glibc's pow batched over the wave)
+                int jj = 0;
+#pragma unroll 1
+                for (; jj + 8 <= dj; jj += 8) {
+                    double df[8], p[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        df[q] = __dsub_rn((double)tile[threadIdx.x][jj + q], (double)cs[j0 + jj + q]);
+                    gp_sq_wave<8>(df, p, sqb);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) acc = __dadd_rn(acc, p[q]);
+                }
+#pragma unroll 1
+                for (; jj < dj; jj++) {
+                    const double df[1] = {__dsub_rn((double)tile[threadIdx.x][jj], (double)cs[j0 + jj])};
+                    double p[1];
+                    gp_sq_wave<1>(df, p, sqb);
+                    acc = __dadd_rn(acc, p[0]);
+                }
+            } else if (n < N) {
 #pragma unroll 8
                 for (int jj = 0; jj < dj; jj++) {
                     const double xj = (double)tile[threadIdx.x][jj];
                     const double cj = (double)cs[j0 + jj];
-                    if (METRIC == 0) {
-                        const double df = __dsub_rn(xj, cj);
-                        acc = __dadd_rn(acc, gp_sq(df));
-                    } else {
-                        ip.add(__dmul_rn(xj, cj));
-                        a = __dadd_rn(a, sq_of<TX>(xj));
-                    }
+                    ip.add(__dmul_rn(xj, cj));
+                    a = __dadd_rn(a, sq_of<TX>(xj));
                 }
             }
         }
@@ -265,12 +283,14 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* 
     const float* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
     for (int j = threadIdx.x; j < d; j += KPP_THREADS) cs[j] = c[j];
     __syncthreads();
+    __shared__ double sqs[KPP_THREADS / 64][64 * 16];   // gp_sq_wave: 64 * 16 per wave
+    double* sqb = sqs[threadIdx.x >> 6];
     double best = 0.0;
     for (int64_t row0 = (int64_t)blockIdx.x * KPP_THREADS; row0 < N; row0 += (int64_t)gridDim.x * KPP_THREADS) {
         const int64_t n = row0 + threadIdx.x;
-        double m = 0.0;
-        if (n < N) {
-        const float* xr = X + n * d;
+        // the whole block runs the chain (rows past N repeat row N - 1, dropped):
+        // the squares go through gp_sq_wave, glibc's pow batched over the wave
+        const float* xr = X + (n < N ? n : N - 1) * d;
         float4 cur[8], nxt[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) cur[u] = *reinterpret_cast<const float4*>(xr + 4 * u);
@@ -281,25 +301,33 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* 
                 for (int u = 0; u < 8; u++) nxt[u] = *reinterpret_cast<const float4*>(xr + j0 + 32 + 4 * u);
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const float xv[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+            for (int h = 0; h < 2; h++) {
+                double df[16], p[16];
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const double df = __dsub_rn((double)xv[q], (double)cs[j0 + 4 * u + q]);
-                    acc = __dadd_rn(acc, gp_sq(df));
+                for (int u = 0; u < 4; u++) {
+                    const float4 v = cur[4 * h + u];
+                    const float xv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        df[4 * u + q] = __dsub_rn((double)xv[q], (double)cs[j0 + 16 * h + 4 * u + q]);
                 }
+                gp_sq_wave<16>(df, p, sqb);
+#pragma unroll
+                for (int q = 0; q < 16; q++) acc = __dadd_rn(acc, p[q]);
             }
 #pragma unroll
             for (int u = 0; u < 8; u++) cur[u] = nxt[u];
         }
-        const double dd = sqrt(acc);
-        m = dd;
-        if (it > 1) {
-            const double prev = mind[n];
-            if (!(dd < prev)) m = prev;
-        }
-        mind[n] = m;
-        if (m > best) best = m;
+        double m = 0.0;
+        if (n < N) {
+            const double dd = sqrt(acc);
+            m = dd;
+            if (it > 1) {
+                const double prev = mind[n];
+                if (!(dd < prev)) m = prev;
+            }
+            mind[n] = m;
+            if (m > best) best = m;
         }
         kpp_group_sum(m * m, gsum, row0 / KPP_THREADS);
     }

@@ -46,65 +46,113 @@ __global__ void sil_near_kernel(const double* __restrict__ C, int K, int d, int 
 constexpr int SP_WAVES = 4;
 constexpr int SIL_DMAX = 512;
 
-// x_i (LDS) vs x_j (global), rows of fp32 or fp64: the exact.h order, 4-wide loads
+// x_i (LDS) vs x_j (global), rows of fp32 or fp64: the exact.h order, 4-wide
+// loads. The whole wave calls it: the squares go through gp_sq_wave (sq: 64 *
+// 16 doubles of wave-private LDS; glibc's pow restated for the few squares
+// that need it, batched over the wave -- per lane, a wave paid it in nearly
+// every term).
 template <typename TX>
-__device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restrict__ xj, int d) {
+__device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restrict__ xj, int d, double* sq) {
     double acc = 0.0;
     int k = 0;
     if ((d & 3) == 0) {
-#pragma unroll 4
-        for (; k < d; k += 4) {
-            double a[4], b[4];
+#pragma unroll 1
+        for (; k + 8 <= d; k += 8) {
+            double a[4], b[4], df[8], p[8];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                ld4d(xi + k + 4 * h, a);
+                ld4d(xj + k + 4 * h, b);
+#pragma unroll
+                for (int u = 0; u < 4; u++) df[4 * h + u] = __dsub_rn(a[u], b[u]);
+            }
+            gp_sq_wave<8>(df, p, sq);
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc = __dadd_rn(acc, p[u]);
+        }
+        if (k < d) {                                        // d % 8 == 4
+            double a[4], b[4], df[4], p[4];
             ld4d(xi + k, a);
             ld4d(xj + k, b);
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const double df = __dsub_rn(a[u], b[u]);
-                acc = __dadd_rn(acc, gp_sq(df));
-            }
+            for (int u = 0; u < 4; u++) df[u] = __dsub_rn(a[u], b[u]);
+            gp_sq_wave<4>(df, p, sq);
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc = __dadd_rn(acc, p[u]);
+            k += 4;
         }
     }
+#pragma unroll 1
     for (; k < d; k++) {
-        const double df = __dsub_rn((double)xi[k], (double)xj[k]);
-        acc = __dadd_rn(acc, gp_sq(df));
+        const double df[1] = {__dsub_rn((double)xi[k], (double)xj[k])};
+        double p[1];
+        gp_sq_wave<1>(df, p, sq);
+        acc = __dadd_rn(acc, p[0]);
     }
     return sqrt(acc);
 }
 
-// sum_{j in [j0, j1)} d(x_i, x_rows[j]) in j order (wave-uniform result)
+// sum_{j in [j0, j1)} d(x_i, x_rows[j]) in j order (wave-uniform result);
+// lanes past j1 repeat the last member so the whole wave stays in step
 template <typename TX>
 __device__ inline double sil_segment(const TX* __restrict__ xi, const TX* __restrict__ X, int d, int metric,
-                                     const int32_t* __restrict__ rows, int64_t j0, int64_t j1, int lane) {
+                                     const int32_t* __restrict__ rows, int64_t j0, int64_t j1, int lane,
+                                     double* sq) {
     double acc = 0.0;
     for (int64_t jb = j0; jb < j1; jb += 64) {
-        const int64_t j = jb + lane;
-        double dj = 0.0;
-        if (j < j1) {
-            const TX* xj = X + (size_t)rows[j] * d;
-            dj = metric == 0 ? sil_euclid(xi, xj, d) : exact_dist(xi, xj, d, metric);
-        }
+        const int64_t j = min<int64_t>(jb + lane, j1 - 1);
+        const TX* xj = X + (size_t)rows[j] * d;
+        const double dj = metric == 0 ? sil_euclid(xi, xj, d, sq) : exact_dist(xi, xj, d, metric);
         const int n = (int)min<int64_t>(64, j1 - jb);
         for (int t = 0; t < n; t++) acc = __dadd_rn(acc, __shfl(dj, t));
     }
     return acc;
 }
 
-// Two members (same cluster) against the same x_j: each x_j load serves both.
+// Two members (same cluster) against the same x_j: each x_j load serves both
+// (d % 4 == 0).
 template <typename TX>
 __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restrict__ xb,
-                                   const TX* __restrict__ xj, int d, double& da, double& db) {
+                                   const TX* __restrict__ xj, int d, double& da, double& db, double* sq) {
     double aa = 0.0, ab = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < d; k += 4) {
-        double b[4], u[4], v[4];
+    int k = 0;
+#pragma unroll 1
+    for (; k + 8 <= d; k += 8) {
+        double df[16], p[16];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            double b[4], u[4], v[4];
+            ld4d(xj + k + 4 * h, b);
+            ld4d(xa + k + 4 * h, u);
+            ld4d(xb + k + 4 * h, v);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                df[8 * h + 2 * e] = __dsub_rn(u[e], b[e]);
+                df[8 * h + 2 * e + 1] = __dsub_rn(v[e], b[e]);
+            }
+        }
+        gp_sq_wave<16>(df, p, sq);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            aa = __dadd_rn(aa, p[2 * e]);
+            ab = __dadd_rn(ab, p[2 * e + 1]);
+        }
+    }
+    if (k < d) {                                            // d % 8 == 4
+        double b[4], u[4], v[4], df[8], p[8];
         ld4d(xj + k, b);
         ld4d(xa + k, u);
         ld4d(xb + k, v);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-            const double du = __dsub_rn(u[e], b[e]), dv = __dsub_rn(v[e], b[e]);
-            aa = __dadd_rn(aa, gp_sq(du));
-            ab = __dadd_rn(ab, gp_sq(dv));
+            df[2 * e] = __dsub_rn(u[e], b[e]);
+            df[2 * e + 1] = __dsub_rn(v[e], b[e]);
+        }
+        gp_sq_wave<8>(df, p, sq);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            aa = __dadd_rn(aa, p[2 * e]);
+            ab = __dadd_rn(ab, p[2 * e + 1]);
         }
     }
     da = sqrt(aa);
@@ -114,12 +162,12 @@ __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restri
 template <typename TX>
 __device__ inline void sil_segment2(const TX* __restrict__ xa, const TX* __restrict__ xb,
                                     const TX* __restrict__ X, int d, const int32_t* __restrict__ rows, int64_t j0,
-                                    int64_t j1, int lane, double& sa, double& sb) {
+                                    int64_t j1, int lane, double& sa, double& sb, double* sq) {
     double acc_a = 0.0, acc_b = 0.0;
     for (int64_t jb = j0; jb < j1; jb += 64) {
-        const int64_t j = jb + lane;
-        double da = 0.0, db = 0.0;
-        if (j < j1) sil_euclid2(xa, xb, X + (size_t)rows[j] * d, d, da, db);
+        const int64_t j = min<int64_t>(jb + lane, j1 - 1);
+        double da, db;
+        sil_euclid2(xa, xb, X + (size_t)rows[j] * d, d, da, db, sq);
         const int n = (int)min<int64_t>(64, j1 - jb);
         for (int t = 0; t < n; t++) {
             acc_a = __dadd_rn(acc_a, __shfl(da, t));
@@ -145,7 +193,9 @@ __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
     const TX* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows, const int64_t* __restrict__ crow,
     const int32_t* __restrict__ assign, const int32_t* __restrict__ near, int64_t N, double* __restrict__ s_out) {
     __shared__ __attribute__((aligned(16))) TX xs[SP_WAVES][2][SIL_DMAX];
+    __shared__ double sqs[SP_WAVES][64 * 16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double* sq = sqs[wave];
     TX* xa = xs[wave][0];
     TX* xb = xs[wave][1];
     // a wave takes members p, p + 1 (cluster-sorted): one pass over the x_j when
@@ -169,8 +219,8 @@ __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
             const int nc = near[ca];
             const int64_t n0 = crow[nc], n1 = crow[nc + 1];
             double a0, a1, b0, b1;
-            sil_segment2(xa, xb, X, d, rows, c0, c1, lane, a0, a1);
-            sil_segment2(xa, xb, X, d, rows, n0, n1, lane, b0, b1);
+            sil_segment2(xa, xb, X, d, rows, c0, c1, lane, a0, a1, sq);
+            sil_segment2(xa, xb, X, d, rows, n0, n1, lane, b0, b1, sq);
             if (lane == 0) {
                 s_out[ra] = sil_value(a0, b0, c0, c1, n0, n1);
                 s_out[rb] = sil_value(a1, b1, c0, c1, n0, n1);
@@ -181,10 +231,10 @@ __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
             const TX* xi = m ? xb : xa;
             const int c = m ? cb : ca;
             const int64_t c0 = crow[c], c1 = crow[c + 1];
-            const double a = sil_segment(xi, X, d, metric, rows, c0, c1, lane);
+            const double a = sil_segment(xi, X, d, metric, rows, c0, c1, lane, sq);
             const int nc = near[c];
             const int64_t n0 = crow[nc], n1 = crow[nc + 1];
-            const double b = sil_segment(xi, X, d, metric, rows, n0, n1, lane);
+            const double b = sil_segment(xi, X, d, metric, rows, n0, n1, lane, sq);
             if (lane == 0) s_out[m ? rb : ra] = sil_value(a, b, c0, c1, n0, n1);
         }
     }

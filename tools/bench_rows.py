@@ -55,6 +55,7 @@ def gpu_time(ctx, fn, reps=5):
     torch.cuda.synchronize()
     t = GpuTime(e0.elapsed_time(e1) / 1e3 / reps)
     t.call = float(np.median(ts))
+    t.calls = 2 * reps + 1          # fn's calls here (stat counters divide by it)
     return t
 
 
@@ -118,8 +119,8 @@ def main():
         C = X[torch.from_numpy(src).to(ctx.dev)].double()
         ctx.reset_stats()
         t = gpu_time(ctx, lambda: lshkm.lloyd_assign(ctx, X, C, "cosine"))
-        amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG) / 6
-        cfix = ctx.stat(lshkm.STAT_COS_FIX) / 6
+        amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG) / t.calls
+        cfix = ctx.stat(lshkm.STAT_COS_FIX) / t.calls
         os.environ["LSHKM_ASSIGN_PATH"] = "exact"
         te = gpu_time(ctx, lambda: lshkm.lloyd_assign(ctx, X, C, "cosine"), reps=1)
         del os.environ["LSHKM_ASSIGN_PATH"]
@@ -318,7 +319,7 @@ def main():
         for metric in ("euclidean", "cosine"):
             ctx.reset_stats()
             t = gpu_time(ctx, lambda: lshkm.lloyd_assign(ctx, X, C, metric))
-            amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG) / 6
+            amb = ctx.stat(lshkm.STAT_ASSIGN_AMBIG) / t.calls
             emit(f"lloyds_assignment ({metric}, fp64 rows)", "rows/s", N, t, None,
                  f"N={N}, d={d} fp64, K={K}; {amb:.0f} rows/call to the exact pass; bytes: the fp64 row + id and "
                  f"distance", bytes_per_unit=8 * d + 12)
