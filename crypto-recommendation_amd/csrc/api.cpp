@@ -530,12 +530,13 @@ static int exact_listed_prep(lshkm_ctx ctx, Pts X, int d, const double* C, int K
 static int exact_listed(lshkm_ctx ctx, Pts X, int d, const double* C, int K, int metric,
                         const unsigned long long* cnt, int64_t N, int32_t* assign, double* dist,
                         const int32_t* seg_counts = nullptr, int64_t seg_rows = 0, int nseg = 0,
-                        const int32_t* rows = nullptr, bool exact_dist = true, bool prepped = false) {
+                        const int32_t* rows = nullptr, bool exact_dist = true, bool prepped = false,
+                        const double* xn2 = nullptr, const double* nbv = nullptr) {
     if (!rows) rows = (const int32_t*)ctx->ws_ambig.p;
     const bool prune = exact_pruned(X, d, K, metric);
     if (!prune && (metric != LSHKM_METRIC_EUCLIDEAN || (!seg_counts && d > 256)))
         return launch_assign_exact(ctx->stream, X, N, d, C, K, metric, rows, cnt, N, assign, dist, seg_counts,
-                                   seg_rows, nseg);
+                                   seg_rows, nseg, xn2, nbv);
     int rc;
     if ((rc = ctx->ws_ct.reserve((size_t)d * ((K + 255) / 256 * 256) * 8))) return rc;
     if (prune)
@@ -686,7 +687,8 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         if (rc) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (ctx->timing) LSHKM_HIP(hipEventRecord(ctx->tev[1], s));
         if ((rc = exact_listed(ctx, X, d, C, K, metric, cnt, N, assign, dist, f.nseg ? f.final_counts : nullptr,
-                               f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr, !fast, xprep))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                               f.seg_rows, f.nseg, f.nseg ? f.final_list : nullptr, !fast, xprep,
+                               cosine ? f.xn2 : nullptr, cosine ? nbv : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
         if (sj.pending) {
             LSHKM_HIP(hipStreamWaitEvent(s, f.join, 0));
             sj.pending = false;

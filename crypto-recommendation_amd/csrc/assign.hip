@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
     const TX* __restrict__ X, int64_t N, int d, const double* __restrict__ C, int K, int metric,
     const int32_t* __restrict__ rows, const unsigned long long* __restrict__ row_count, int64_t max_rows,
     int32_t* __restrict__ assign, double* __restrict__ dist, const int32_t* __restrict__ seg_counts,
-    int64_t seg_rows) {
+    int64_t seg_rows, const double* __restrict__ xn2, const double* __restrict__ nbv) {
     const int lane = threadIdx.x & 63;
     int64_t wglobal = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     int64_t nw = (int64_t)gridDim.x * 4;
@@ -384,6 +384,9 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
         const int64_t row = rows ? rows[it] : it;
         const TX* x = X + row * d;
         double best = 0.0; int bi = -1;
+        // cosine: the row's / centroids' sums of squares precomputed (row_sumsq,
+        // the prep's nbv; glibc pow per square, the same for every pair) when given
+        const double xa = metric == 1 && xn2 ? xn2[row] : -1.0;
         if (metric == 1 && K <= 64 * XC_MAXV) {
             // cosine: certified values (exact.h cosine_interval) for every
             // centroid, the soft-x87 chain only for those whose interval can
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
                 const int c = lane + 64 * k;
                 st[k] = 0; v[k] = 0.0; rad[k] = 0.0;
                 if (c < K) {
-                    st[k] = cosine_interval(x, C + (size_t)c * d, d, v[k], rad[k]);
+                    st[k] = cosine_interval(x, C + (size_t)c * d, d, v[k], rad[k], xa, nbv ? nbv[c] : -1.0);
                     unknown |= st[k] == 2;
                     if (st[k] != 2) U = fmin(U, v[k] + rad[k]);
                 }
@@ -409,7 +412,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
                 for (int k = 0; k < XC_MAXV; k++) {
                     const int c = lane + 64 * k;
                     if (c < K && v[k] - rad[k] <= U) {     // non-candidates are strictly above the minimum
-                        const double dd = st[k] == 0 ? v[k] : exact_cosine_x87(x, C + (size_t)c * d, d);
+                        const double dd = st[k] == 0 ? v[k] : exact_cosine_x87(x, C + (size_t)c * d, d, xa, nbv ? nbv[c] : -1.0);
                         if (bi < 0 || dd < best) { best = dd; bi = c; }
                     }
                 }
@@ -427,7 +430,8 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
             }
         }
         for (int c = lane; c < K; c += 64) {
-            const double dd = metric == 0 ? exact_euclid(x, C + (size_t)c * d, d) : exact_cosine(x, C + (size_t)c * d, d);
+            const double dd = metric == 0 ? exact_euclid(x, C + (size_t)c * d, d)
+                                          : exact_cosine_x87(x, C + (size_t)c * d, d, xa, nbv ? nbv[c] : -1.0);
             // assignment.hpp:66: the -1 sentinel takes centroid 0's distance even
             // if NaN (a zero vector under cosine), which then blocks every later
             // '<'; any other NaN is never taken
@@ -449,7 +453,8 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(
 
 int launch_assign_exact(hipStream_t s, Pts X, int64_t N, int d, const double* C, int K, int metric,
                         const int32_t* rows, const unsigned long long* row_count, int64_t max_rows,
-                        int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg) {
+                        int32_t* assign, double* dist, const int32_t* seg_counts, int64_t seg_rows, int nseg,
+                        const double* xn2, const double* nbv) {
     if (max_rows <= 0) return 0;
     // rows == NULL: every row (fallback path); else a device-counted list that is
     // usually ~0.3% of the rows: one block per CU, waves loop over the list.
@@ -457,10 +462,10 @@ int launch_assign_exact(hipStream_t s, Pts X, int64_t N, int d, const double* C,
     if (blocks <= 0) return 0;
     if (X.f64)
         hipLaunchKernelGGL(assign_exact_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s, X.d(), N, d, C, K,
-                           metric, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+                           metric, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, xn2, nbv);
     else
         hipLaunchKernelGGL(assign_exact_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, X.f(), N, d, C, K,
-                           metric, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows);
+                           metric, rows, row_count, max_rows, assign, dist, seg_counts, seg_rows, xn2, nbv);
     return kstatus("assign.hip");
 }
 

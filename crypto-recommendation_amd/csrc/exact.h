@@ -61,17 +61,22 @@ __device__ inline double exact_cosine_x87_soft(const T* __restrict__ x, const U*
 // as a double-double (softx87.h X87dd, ~30 fp64 ops per add, checked against
 // real long double on the host), the soft FADD only past a sum X87dd does not
 // decide (X87acc).
+// xa / cb as cosine_interval's.
 template <typename T, typename U>
-__device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __restrict__ c, int d) {
+__device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __restrict__ c, int d, double xa = -1.0,
+                                          double cb = -1.0) {
     X87acc ip;
     ip.init();
     double a = 0.0, b = 0.0;
+    const bool fa = xa < 0.0, fb = cb < 0.0;
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], cj = (double)c[j];
         ip.add(__dmul_rn(xj, cj));
-        a = __dadd_rn(a, sq_of<T>(xj));
-        b = __dadd_rn(b, sq_of<U>(cj));
+        if (fa) a = __dadd_rn(a, sq_of<T>(xj));
+        if (fb) b = __dadd_rn(b, sq_of<U>(cj));
     }
+    if (!fa) a = xa;
+    if (!fb) b = cb;
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
 }
 
@@ -316,17 +321,22 @@ struct IpAcc {
 
 // Cosine distance with its certificate status (IpAcc::quot_status): 0 = v is
 // the reference's value, 1 = the reference's value lies within v +- rad,
-// 2 = unknown.
+// 2 = unknown. xa / cb: the row's / centroid's sequential sum of squares when
+// the caller has it (row_sumsq, the prep's nbv), else < 0: formed here.
 template <typename T, typename U>
-__device__ inline int cosine_interval(const T* __restrict__ x, const U* __restrict__ c, int d, double& v, double& rad) {
+__device__ inline int cosine_interval(const T* __restrict__ x, const U* __restrict__ c, int d, double& v, double& rad,
+                                      double xa = -1.0, double cb = -1.0) {
     IpAcc ip;
     double a = 0.0, b = 0.0;
+    const bool fa = xa < 0.0, fb = cb < 0.0;
     for (int j = 0; j < d; j++) {
         const double xj = (double)x[j], cj = (double)c[j];
         ip.add(__dmul_rn(xj, cj));
-        a = __dadd_rn(a, sq_of<T>(xj));
-        b = __dadd_rn(b, sq_of<U>(cj));
+        if (fa) a = __dadd_rn(a, sq_of<T>(xj));
+        if (fb) b = __dadd_rn(b, sq_of<U>(cj));
     }
+    if (!fa) a = xa;
+    if (!fb) b = cb;
     double q = 0.0, qr = 0.0;
     const int st = ip.quot_status(__dmul_rn(sqrt(a), sqrt(b)), q, qr);
     v = __dsub_rn(1.0, q);

@@ -1811,6 +1811,13 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
 #endif
             double acc = 0.0;
             PwAcc pw;
+            // fp64 rows: glibc's pow in the chain itself when the launch gave the
+            // LDS for it (gp_sq_wave; every difference of general doubles has
+            // more than 26 bits, so the PwAcc test would list every row)
+            double* pwl = nullptr;
+            if constexpr (ROWS == 2) {
+                if (a.pw_lds) pwl = reinterpret_cast<double*>(smem + a.pw_lds) + wave * 512;
+            }
             if constexpr (GATH) {
                 wait_step();                                               // step 0 landed
                 asm volatile("" ::: "memory");
@@ -1850,19 +1857,25 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
 #pragma unroll
                     for (int j = 0; j < 4; j++) xcur[j] = make_double2((double)xf[8 * s + 2 * j], (double)xf[8 * s + 2 * j + 1]);
                 }
+                double dv[8];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const double2 cc = cur[j];
-                    const double d0 = __dsub_rn(xcur[j].x, cc.x);
-                    const double d1 = __dsub_rn(xcur[j].y, cc.y);
-                    sq[2 * j] = __dmul_rn(d0, d0);
-                    sq[2 * j + 1] = __dmul_rn(d1, d1);
-                    // the reference squares with glibc pow: x*x is its value when
-                    // the square is exact; otherwise the row's distance is redone
-                    // by the fix-up (gpow2.h PwAcc: differences of <= 26 bits, and
-                    // for fp64 rows no tiny ones)
-                    pw.add<ROWS == 2>(d0);
-                    pw.add<ROWS == 2>(d1);
+                    dv[2 * j] = __dsub_rn(xcur[j].x, cc.x);
+                    dv[2 * j + 1] = __dsub_rn(xcur[j].y, cc.y);
+                }
+                if (ROWS == 2 && pwl) {
+                    gp_sq_wave<8>(dv, sq, pwl);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        sq[j] = __dmul_rn(dv[j], dv[j]);
+                        // the reference squares with glibc pow: x*x is its value when
+                        // the square is exact; otherwise the row's distance is redone
+                        // by the fix-up (gpow2.h PwAcc: differences of <= 26 bits, and
+                        // for fp64 rows no tiny ones)
+                        pw.add<ROWS == 2>(dv[j]);
+                    }
                 }
                 if (h == 0) {
 #pragma unroll
@@ -1877,7 +1890,7 @@ __global__ __launch_bounds__((64 * fh_waves<HASH, MP, MET, FAST>()), 1) void fus
             }
             // fp32 rows: a difference 0 < |x - c| < 2^-460 needs such a centroid
             // value (x has >= 2^-149 magnitude or is zero), flagged by the prep
-            const bool pw_hard = pw.hard() || (ROWS != 2 && (__float_as_uint(a.cbound[7]) & 2u) != 0u);
+            const bool pw_hard = pwl == nullptr && (pw.hard() || (ROWS != 2 && (__float_as_uint(a.cbound[7]) & 2u) != 0u));
             // the shuffle outside the ||: evaluated only where pw_hard is false, it
             // would read the other half's lane while that lane is masked off
             const int pw_other = __shfl_xor((int)pw_hard, 32);
@@ -2287,6 +2300,7 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
     f.side_timed = false;
     if (f.N <= 0) return 0;
     FusedArgs a;
+    a.pw_lds = 0;
     a.X = f.X; a.N = f.N;
     a.Ch = f.Ch; a.Cl = f.Cl; a.cnh = f.cnh; a.cbound = f.cbound; a.C64 = f.C64; a.Kpad = f.Kpad;
     a.Vh = f.Vh; a.Vl = f.Vl; a.PT = f.PT; a.tv = f.tv; a.pnorm = f.pnorm; a.v1 = f.v1; a.rv = f.rv;
@@ -2426,9 +2440,15 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                 else if (f.rows == 1)
                     hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 1>), grid,
                                        dim3(64 * fh_waves<false, false, 0>()), lh, s, a);
-                else
+                else {
+                    // the chain's pow buffers after the image when they fit (Kpad <= 448)
+                    constexpr int PW_BYTES = fh_waves<false, false, 0>() * 512 * 8;
+                    const size_t off = (lh + 255) & ~(size_t)255;
+                    const bool pw = off + PW_BYTES <= 160 * 1024;
+                    a.pw_lds = pw ? (int)off : 0;
                     hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 2>), grid,
-                                       dim3(64 * fh_waves<false, false, 0>()), lh, s, a);
+                                       dim3(64 * fh_waves<false, false, 0>()), pw ? off + PW_BYTES : lh, s, a);
+                }
             }
             if (two_image) {
                 a.Ch = f.Ch; a.cnh = f.cnh; a.Kpad = f.Kpad;
@@ -2633,25 +2653,73 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__
 }
 
 // out[i] = the reference's sum_j pow(x_ij, 2), j ascending (the |x|^2 of
-// cosineDistance, cust_vector.hpp:148-151) for fp64 rows, lane per row.
+// cosineDistance, cust_vector.hpp:148-151) for fp64 rows, lane per row. A wave
+// takes 64 rows; VEC (d even, rows 16-B aligned): each 8-dim step of the 64
+// rows is loaded as 16-B pieces, four lanes per row's 64 contiguous bytes, and
+// transposed through LDS (a lane-per-row load touches 64 lines per instruction).
+constexpr int RSQ_S = 10;                                // LDS row stride (doubles)
+template <bool VEC>
 __global__ __launch_bounds__(256) void row_sumsq_kernel(const double* __restrict__ X, int64_t N, int d,
                                                          double* __restrict__ out) {
     __shared__ double sqs[4][64 * 8];                    // gp_sq_wave: 64 * NV per wave
+    __shared__ __attribute__((aligned(16))) double tr[4][64 * RSQ_S];
     double* sq = sqs[threadIdx.x >> 6];
+    double* t = tr[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     // wave-uniform trip count: lanes past N repeat row N - 1 and write nothing
     for (int64_t i0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); i0 < N; i0 += (int64_t)gridDim.x * 256) {
         const int64_t i = i0 + lane;
-        const double* x = X + (i < N ? i : N - 1) * d;
         double a = 0.0;
-        for (int j0 = 0; j0 < d; j0 += 8) {
-            double v[8], p[8];
+        if constexpr (VEC) {
+            double2 pc[4], pn[4];
+            auto load = [&](int j0, double2 (&dst)[4]) {
 #pragma unroll
-            for (int t = 0; t < 8; t++) v[t] = j0 + t < d ? x[j0 + t] : 0.0;
-            gp_sq_wave<8>(v, p, sq);
+                for (int k = 0; k < 4; k++) {
+                    const int q = 64 * k + lane, r = q >> 2, part = q & 3;
+                    const int64_t rr = i0 + r < N ? i0 + r : N - 1;
+                    const int j = j0 + 2 * part;
+                    dst[k] = j < d ? *reinterpret_cast<const double2*>(X + rr * d + j) : make_double2(0.0, 0.0);
+                }
+            };
+            load(0, pn);
+            for (int j0 = 0; j0 < d; j0 += 8) {
 #pragma unroll
-            for (int t = 0; t < 8; t++)
-                if (j0 + t < d) a = __dadd_rn(a, p[t]);
+                for (int k = 0; k < 4; k++) pc[k] = pn[k];
+                if (j0 + 8 < d) load(j0 + 8, pn);               // the next step in flight
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int q = 64 * k + lane;
+                    *reinterpret_cast<double2*>(t + (q >> 2) * RSQ_S + 2 * (q & 3)) = pc[k];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                double v[8], p[8];
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    const double2 w = *reinterpret_cast<const double2*>(t + lane * RSQ_S + 2 * h);
+                    v[2 * h] = w.x;
+                    v[2 * h + 1] = w.y;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                gp_sq_wave<8>(v, p, sq);
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (j0 + u < d) a = __dadd_rn(a, p[u]);
+            }
+        } else {
+            const double* x = X + (i < N ? i : N - 1) * d;
+            for (int j0 = 0; j0 < d; j0 += 8) {
+                double v[8], p[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = j0 + u < d ? x[j0 + u] : 0.0;
+                gp_sq_wave<8>(v, p, sq);
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (j0 + u < d) a = __dadd_rn(a, p[u]);
+            }
         }
         if (i < N) out[i] = a;
     }
@@ -2660,7 +2728,8 @@ __global__ __launch_bounds__(256) void row_sumsq_kernel(const double* __restrict
 int launch_row_sumsq(hipStream_t s, const double* X, int64_t N, int d, double* out) {
     if (N <= 0) return 0;
     const unsigned grid = (unsigned)std::min<int64_t>((N + 255) / 256, 4096);
-    hipLaunchKernelGGL(row_sumsq_kernel, dim3(grid), dim3(256), 0, s, X, N, d, out);
+    if (d % 2 == 0 && ((uintptr_t)X & 15) == 0) hipLaunchKernelGGL(row_sumsq_kernel<true>, dim3(grid), dim3(256), 0, s, X, N, d, out);
+    else hipLaunchKernelGGL(row_sumsq_kernel<false>, dim3(grid), dim3(256), 0, s, X, N, d, out);
     return kstatus("row_sumsq_kernel");
 }
 

@@ -73,6 +73,8 @@ struct FusedArgs {
     const double* X64;
     int d, xvec;
     const double* Cd;                // general rows: the caller's [K][d] centroids (cosine winners)
+    int pw_lds;                      // fp64 rows, exact distances: LDS byte offset of the chain's
+                                     // gp_sq_wave buffers (4 KiB per wave), 0: PwAcc + fix-up list
 };
 
 }  // namespace lshkm

@@ -91,7 +91,7 @@ int launch_cos_fix(hipStream_t s, Pts X, int64_t N, int d, const double* C, cons
 int launch_assign_exact(hipStream_t s, Pts X, int64_t N, int d, const double* C, int K,
                         int metric, const int32_t* rows, const unsigned long long* row_count,
                         int64_t max_rows, int32_t* assign, double* dist, const int32_t* seg_counts = nullptr,
-                        int64_t seg_rows = 0, int nseg = 0);
+                        int64_t seg_rows = 0, int nseg = 0, const double* xn2 = nullptr, const double* nbv = nullptr);
 // Euclidean, listed rows, batched (CT: d * ceil64(K) doubles of workspace).
 // Segmented form (seg_counts != NULL): segment b = rows[b * seg_rows ...], count seg_counts[2b].
 int launch_assign_exact_list(hipStream_t s, Pts X, int d, const double* C, int K, double* CT,
