@@ -269,10 +269,13 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
     kpp_block_max(best, bmax);
 }
 
-// Euclidean on fp32 rows with d % 32 == 0: one row per thread straight from
-// HBM into registers (32-dim slices, the next slice's 8 float4 loads in flight
-// while the current one is summed), no LDS tile and no barriers; the centroid
-// row is an LDS broadcast. Same exact-order chain as above.
+// Euclidean on fp32 rows with d % 32 == 0 (16-B aligned rows): each wave takes
+// 64 consecutive rows and reads them 16 dims at a time as 16-B pieces, four
+// lanes per row's 64 contiguous bytes (a row per lane touched 64 lines per
+// load instruction), transposed through LDS with the next step's loads in
+// flight; the squares go through gp_sq_wave (glibc's pow batched over the
+// wave). The centroid row is an LDS broadcast. Same exact-order chain as above.
+constexpr int KR_S = 20;                                 // LDS row stride of the transpose (floats)
 __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* __restrict__ X, int64_t N, int d,
                                                                    const int32_t* __restrict__ chosen, int it,
                                                                    double* __restrict__ mind,
@@ -280,43 +283,56 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* 
                                                                    double* __restrict__ gsum) {
     extern __shared__ __attribute__((aligned(8))) char kpp_dyn2[];
     float* cs = reinterpret_cast<float*>(kpp_dyn2);     // [d]
+    __shared__ double sqs[KPP_THREADS / 64][64 * 16];   // gp_sq_wave: 64 * 16 per wave
+    __shared__ __attribute__((aligned(16))) float trs[KPP_THREADS / 64][64 * KR_S];
     const float* __restrict__ c = X + (int64_t)chosen[it - 1] * d;
     for (int j = threadIdx.x; j < d; j += KPP_THREADS) cs[j] = c[j];
     __syncthreads();
-    __shared__ double sqs[KPP_THREADS / 64][64 * 16];   // gp_sq_wave: 64 * 16 per wave
-    double* sqb = sqs[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double* sqb = sqs[w];
+    float* tr = trs[w];
     double best = 0.0;
     for (int64_t row0 = (int64_t)blockIdx.x * KPP_THREADS; row0 < N; row0 += (int64_t)gridDim.x * KPP_THREADS) {
-        const int64_t n = row0 + threadIdx.x;
-        // the whole block runs the chain (rows past N repeat row N - 1, dropped):
-        // the squares go through gp_sq_wave, glibc's pow batched over the wave
-        const float* xr = X + (n < N ? n : N - 1) * d;
-        float4 cur[8], nxt[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) cur[u] = *reinterpret_cast<const float4*>(xr + 4 * u);
+        const int64_t wr0 = row0 + 64 * w;             // this wave's rows wr0 .. wr0 + 63 (past N: row N - 1, dropped)
+        const int64_t n = wr0 + lane;
+        // this lane's 4 pieces: rows wr0 + q / 4 (q = 64 k + lane), dims 4 (q % 4) of each 16-dim step
+        const int64_t r0 = wr0 + (lane >> 2), rlast = N - 1;
+        const float* s0 = X + (r0 < N ? r0 : rlast) * d + 4 * (lane & 3);
+        const float* s1 = X + (r0 + 16 < N ? r0 + 16 : rlast) * d + 4 * (lane & 3);
+        const float* s2 = X + (r0 + 32 < N ? r0 + 32 : rlast) * d + 4 * (lane & 3);
+        const float* s3 = X + (r0 + 48 < N ? r0 + 48 : rlast) * d + 4 * (lane & 3);
+        float* t0 = tr + (lane >> 2) * KR_S + 4 * (lane & 3);
+        float4 n0 = *reinterpret_cast<const float4*>(s0), n1 = *reinterpret_cast<const float4*>(s1);
+        float4 n2 = *reinterpret_cast<const float4*>(s2), n3 = *reinterpret_cast<const float4*>(s3);
         double acc = 0.0;
-        for (int j0 = 0; j0 < d; j0 += 32) {
-            if (j0 + 32 < d) {
+        for (int j0 = 0; j0 < d; j0 += 16) {
+            const float4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+            const int jn = j0 + 16 < d ? j0 + 16 : j0;     // the last step reloads its own (no branch)
+            n0 = *reinterpret_cast<const float4*>(s0 + jn);
+            n1 = *reinterpret_cast<const float4*>(s1 + jn);
+            n2 = *reinterpret_cast<const float4*>(s2 + jn);
+            n3 = *reinterpret_cast<const float4*>(s3 + jn);
+            *reinterpret_cast<float4*>(t0) = c0;
+            *reinterpret_cast<float4*>(t0 + 16 * KR_S) = c1;
+            *reinterpret_cast<float4*>(t0 + 32 * KR_S) = c2;
+            *reinterpret_cast<float4*>(t0 + 48 * KR_S) = c3;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double df[16], p[16];
 #pragma unroll
-                for (int u = 0; u < 8; u++) nxt[u] = *reinterpret_cast<const float4*>(xr + j0 + 32 + 4 * u);
+            for (int h = 0; h < 4; h++) {
+                const float4 v = *reinterpret_cast<const float4*>(tr + lane * KR_S + 4 * h);
+                const float xv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) df[4 * h + u] = __dsub_rn((double)xv[u], (double)cs[j0 + 4 * h + u]);
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            gp_sq_wave<16>(df, p, sqb);
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                double df[16], p[16];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const float4 v = cur[4 * h + u];
-                    const float xv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        df[4 * u + q] = __dsub_rn((double)xv[q], (double)cs[j0 + 16 * h + 4 * u + q]);
-                }
-                gp_sq_wave<16>(df, p, sqb);
-#pragma unroll
-                for (int q = 0; q < 16; q++) acc = __dadd_rn(acc, p[q]);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) cur[u] = nxt[u];
+            for (int u = 0; u < 16; u++) acc = __dadd_rn(acc, p[u]);
         }
         double m = 0.0;
         if (n < N) {
