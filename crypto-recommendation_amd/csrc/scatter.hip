@@ -71,6 +71,10 @@ __global__ __launch_bounds__(1024) void rs_scan(uint32_t* __restrict__ a, int64_
 // N = 10M, 0.35-0.54 ms in the one-block scan): reduce-then-scan over
 // RS_SC-element chunks, in place; the chunk totals go through rs_scan.
 constexpr int RS_SC = 8192;
+// up to this many counters the one-block scan (1024 threads, <= 64 each) beats
+// the reduce-then-scan trio's two extra launches (the C2 build: 7-bit digits x
+// 245 tiles x 5 tables)
+constexpr int64_t RS_ONE_SCAN = 65536;
 __global__ __launch_bounds__(1024) void rs_chunk_sum(const uint32_t* __restrict__ a, int64_t M, uint32_t* __restrict__ part,
                                                      int64_t a_ts, int64_t p_ts) {
     __shared__ uint32_t red[1024];
@@ -307,7 +311,7 @@ int stable_sort_by_key_batched(hipStream_t s, const int32_t* keys, int64_t kstri
         const int shift = p * DB;
         hipLaunchKernelGGL(rs_upsweep, dim3((unsigned)nblocks, (unsigned)T), dim3(RS_THREADS), 0, s, kin, kst, N, shift,
                            nbins, (int)nblocks, hist, kts, M);
-        if (M <= RS_SC) {
+        if (M <= RS_ONE_SCAN) {
             hipLaunchKernelGGL(rs_scan, dim3(1, (unsigned)T), dim3(1024), 0, s, hist, M, M);
         } else {
             hipLaunchKernelGGL(rs_chunk_sum, dim3((unsigned)nch, (unsigned)T), dim3(1024), 0, s, hist, M, part, M, nch + 2);
