@@ -703,7 +703,7 @@ static int assign_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const double* C, 
         }
         if (cosine || pwfix) {
             if ((rc = launch_cos_fix_seg(s, X, d, C, f.ncos_lists, f.cos_list, f.cos_counts, f.seg_rows, f.nseg, assign,
-                                         dist, cosine ? 1 : 0))) { LSHKM_LAUNCH_CHECK(); return rc; }
+                                         dist, cosine ? 1 : 0, cosine ? f.xn2 : nullptr, cosine ? nbv : nullptr))) { LSHKM_LAUNCH_CHECK(); return rc; }
             if ((rc = launch_add_counter(s, (unsigned long long*)ctx->stats.p + (cosine ? STAT_COS_FIX : STAT_POW_FIX), cnt + 3))) { LSHKM_LAUNCH_CHECK(); return rc; }
         }
     } else if (path == 1) {

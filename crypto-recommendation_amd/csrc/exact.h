@@ -85,12 +85,15 @@ __device__ inline double exact_cosine_x87(const T* __restrict__ x, const U* __re
 // per term; a load round trip per term made a lone row's chain ~45 us at
 // d = 100). VEC: fp32 row and fp64 centroid rows 16-B aligned with d % 8 == 0
 // (vector loads); otherwise element loads, the last chunk partial.
+// xa / cb as cosine_interval's (precomputed sums of squares, else < 0).
 template <bool VEC, typename T, typename U>
-__device__ inline double exact_cosine_x87_pf(const T* __restrict__ x, const U* __restrict__ c, int d) {
+__device__ inline double exact_cosine_x87_pf(const T* __restrict__ x, const U* __restrict__ c, int d, double xa = -1.0,
+                                             double cb = -1.0) {
     constexpr int B = 8;
     X87acc ip;
     ip.init();
     double a = 0.0, b = 0.0;
+    const bool fa = xa < 0.0, fb = cb < 0.0;
     T xn[B];
     U cn[B];
     auto load = [&](int j0) {
@@ -123,10 +126,12 @@ __device__ inline double exact_cosine_x87_pf(const T* __restrict__ x, const U* _
             if (!VEC && j0 + t >= d) break;
             const double xj = (double)xs[t], cj = (double)cs[t];
             ip.add(__dmul_rn(xj, cj));
-            a = __dadd_rn(a, sq_of<T>(xj));
-            b = __dadd_rn(b, sq_of<U>(cj));
+            if (fa) a = __dadd_rn(a, sq_of<T>(xj));
+            if (fb) b = __dadd_rn(b, sq_of<U>(cj));
         }
     }
+    if (!fa) a = xa;
+    if (!fb) b = cb;
     return one_minus(x87_quot(ip.value(), __dmul_rn(sqrt(a), sqrt(b))));
 }
 

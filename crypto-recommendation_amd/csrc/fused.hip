@@ -2619,7 +2619,8 @@ struct CosLists {
 template <typename TX, int MET>
 __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__ X, int d, const double* __restrict__ C,
                                                           CosLists cl, int nseg, int64_t seg_rows,
-                                                          const int32_t* __restrict__ assign, double* __restrict__ dist) {
+                                                          const int32_t* __restrict__ assign, double* __restrict__ dist,
+                                                          const double* __restrict__ xn2, const double* __restrict__ nbv) {
     // consecutive blocks take different segments: blocks are dealt round-robin to
     // the 8 XCDs, and a short list fills only its segment's first part (with
     // seg = blockIdx / CF_SPLIT every busy block sat on one XCD: 4x slower)
@@ -2642,8 +2643,17 @@ __global__ __launch_bounds__(256) void cos_fix_seg_kernel(const TX* __restrict__
         const double* cr = C + (size_t)assign[row] * d;
         double v;
         if constexpr (MET == 1) {
-            if (vec) v = exact_cosine_x87_wave<sizeof(TX) == 4>(xr, cr, d, sq);
-            else v = exact_cosine_x87_wave<false>(xr, cr, d, sq);
+            // the sums of squares precomputed (the prep's nbv; fp64 rows: row_sumsq)
+            // when the launch has them: no squares left in the chain
+            if (nbv && (sizeof(TX) == 4 || xn2)) {
+                const double xa = sizeof(TX) == 4 ? -1.0 : xn2[row], cb = nbv[assign[row]];
+                if (vec) v = exact_cosine_x87_pf<sizeof(TX) == 4>(xr, cr, d, xa, cb);
+                else v = exact_cosine_x87_pf<false>(xr, cr, d, xa, cb);
+            } else if (vec) {
+                v = exact_cosine_x87_wave<sizeof(TX) == 4>(xr, cr, d, sq);
+            } else {
+                v = exact_cosine_x87_wave<false>(xr, cr, d, sq);
+            }
         } else {
             if (vec) v = exact_euclid_wave<sizeof(TX) == 4>(xr, cr, d, sq);
             else v = exact_euclid_wave<false>(xr, cr, d, sq);
@@ -2735,13 +2745,13 @@ int launch_row_sumsq(hipStream_t s, const double* X, int64_t N, int d, double* o
 
 int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, int nlists, const unsigned long long* const* lists,
                        const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist,
-                       int metric) {
+                       int metric, const double* xn2, const double* nbv) {
     if (nseg <= 0 || nlists <= 0) return 0;
     if (nlists > 2) return -1;                       // LSHKM_ERR_ARG
     CosLists cl{};
     for (int i = 0; i < nlists; i++) { cl.list[i] = lists[i]; cl.counts[i] = counts[i]; }
     const dim3 grid((unsigned)(nlists * nseg * CF_SPLIT));
-#define CF_LAUNCH(TX, M, XP) hipLaunchKernelGGL((cos_fix_seg_kernel<TX, M>), grid, dim3(256), 0, s, XP, d, C, cl, nseg, seg_rows, assign, dist)
+#define CF_LAUNCH(TX, M, XP) hipLaunchKernelGGL((cos_fix_seg_kernel<TX, M>), grid, dim3(256), 0, s, XP, d, C, cl, nseg, seg_rows, assign, dist, xn2, nbv)
     if (metric == 1) {
         if (X.f64) CF_LAUNCH(double, 1, X.d()); else CF_LAUNCH(float, 1, X.f());
     } else {

@@ -336,7 +336,7 @@ int launch_row_sumsq(hipStream_t s, const double* X, int64_t N, int d, double* o
 // metric 0 the euclidean chain with glibc's pow(x, 2) (gpow2.h).
 int launch_cos_fix_seg(hipStream_t s, Pts X, int d, const double* C, int nlists, const unsigned long long* const* lists,
                        const int32_t* const* counts, int64_t seg_rows, int nseg, const int32_t* assign, double* dist,
-                       int metric);
+                       int metric, const double* xn2 = nullptr, const double* nbv = nullptr);
 
 // Range assignment (range.hip).
 int launch_range_radius(hipStream_t s, const double* C, int K, int d, int metric, double* r0,
