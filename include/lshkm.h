@@ -100,8 +100,8 @@ int lshkm_ctx_set_stream(lshkm_ctx ctx, void* hip_stream);
 /* Distance contract of the context (see Conventions): LSHKM_DIST_CERTIFIED
  * (the default of a new context) or LSHKM_DIST_EXACT (the reference's
  * euclideanDistance, cust_vector.hpp:124-136, for every row; a few percent
- * slower at d = 128). The environment variable LSHKM_DIST=exact|certified
- * overrides it for experiments. */
+ * slower at d = 128). The context's mode alone decides (no environment
+ * override in this library). */
 int lshkm_ctx_set_dist_mode(lshkm_ctx ctx, int mode);
 int lshkm_ctx_get_dist_mode(lshkm_ctx ctx, int* mode_host);
 int lshkm_ctx_sync(lshkm_ctx ctx);
@@ -378,8 +378,8 @@ int lshkm_rand_selection(uint64_t seed, int64_t N, int K, int32_t* rows_host);
  * (parallel_quickSort, :234-277, ties and NaNs included); first P kept.
  * Rows are fp64 (X_dev [N][d] neighbour pool, U_dev [nq][d] users).
  * out_idx_dev / out_sim_dev [nq][P] (-1 / 0 past the count), out_cnt_dev [nq]
- * = min(P, neighbours). Bit-exact when the squares of the components are exact
- * in fp64 (the reference's pow(x, 2)); otherwise within an ulp. */
+ * = min(P, neighbours). Bit-exact on any doubles (the norms' squares are
+ * glibc's pow(x, 2)). */
 int lshkm_p_closest(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const double* U_dev, int64_t nq,
                     const int64_t* cand_ptr_dev, const int32_t* cand_idx_dev, int P, int32_t* out_idx_dev,
                     double* out_sim_dev, int32_t* out_cnt_dev);
@@ -410,8 +410,8 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X_dev, const double* x_mean_d
  * Users whose cluster is empty (or ucl outside [0, K)) get -1 in every slot:
  * main.cpp skips them (:262, :366). X_dev [N][d] pool rows and U_dev [nq][d]
  * users share the element type (for Part A pass the same rows twice). Counter
- * 7 counts the similarities the x87 chain decided. Bit-exact when the squares of
- * the components are exact in fp64 (pow(x, 2)). */
+ * 7 counts the similarities the x87 chain decided. Bit-exact on any rows (the
+ * norms' squares are glibc's pow(x, 2)). */
 int lshkm_cluster_top_n(lshkm_ctx ctx, const float* X_dev, const double* x_mean_dev, int64_t N, int d,
                         const int64_t* crow_dev, const int32_t* crows_dev, int K, const float* U_dev,
                         const double* u_mean_dev, int64_t nq, const int32_t* ucl_dev, const int64_t* unk_ptr_dev,
