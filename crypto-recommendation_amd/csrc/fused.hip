@@ -1100,6 +1100,35 @@ __host__ __device__ constexpr int fh_waves() {
 }
 constexpr int FH_WAVES_MIN = 8, FH_WAVES_MAX = 12;
 
+// The upper half's finish of the cosine winner certificate (IpAcc, exact.h):
+// the halves' double-double sums joined by one TwoSum; sum_k |S_k| bound
+// rounded up (+ 2^-47 relative for the roundings of |A_k + B_end| and of the
+// sums here; the partial sums stand in for the exact ones: their TwoSum rests,
+// |sl| <= 64 2^-53 max|t| per half, and the offsets, <= 2^-38 max|t|, charged
+// absolutely -- a cancelling A_k + B_end must not hide them). max |t| of both
+// halves' running sums <= sum_j |p_j| <= (1 + 2^-53) |x| |c| (Cauchy-Schwarz):
+// mb = 2 sqrt(xa nbv) (1 + 2^-40) bounds the pair of them without a per-term
+// max; sum |S_k| >= 2^-790 stands in for quot_status's lower range check on
+// the partial sums themselves (max |S_k| >= that / 128).
+__device__ inline int cosine_halves_finish(double sh0, double sl0, double ts0, double sh, double sl, double ts,
+                                           double xa, double nbv, double& v) {
+    const double mb = 2.0 * sqrt(__dmul_rn(xa, nbv)) * (1.0 + 0x1p-40);
+    const double tsum = __dadd_rn(ts0, ts);
+    if (!(tsum >= 0x1p-790)) return 2;
+    IpAcc ip;
+    const double t = __dadd_rn(sh0, sh);
+    const double bb = __dsub_rn(t, sh0);
+    const double e = __dadd_rn(__dsub_rn(sh0, __dsub_rn(t, bb)), __dsub_rn(sh, bb));
+    ip.sh = t;
+    ip.sl = __dadd_rn(__dadd_rn(sl0, sl), e);
+    ip.ts = __dadd_rn(tsum * (1.0 + 0x1p-47), 0x1p-37 * mb);
+    ip.mx = mb;
+    double q, qr;
+    const int st = ip.quot_status(__dmul_rn(sqrt(xa), sqrt(nbv)), q, qr);
+    if (st == 0) v = __dsub_rn(1.0, q);
+    return st;
+}
+
 // MET = 1: cosine (the prep's normalised centroid rows, score x.c^ with no
 // offset; the winner's distance from the row in registers, declines to the
 // cfix list). HASH with MET = 1: CosineHGen signs of the L*k projections
@@ -1115,8 +1144,9 @@ constexpr int FH_WAVES_MIN = 8, FH_WAVES_MAX = 12;
 // exactly as the reference's partial sum, half 1 |B_k + A_end(s-1)| plus
 // 8 |A_end(s) - A_end(s-1)| (the block it runs one step behind) -- the round-4
 // bound 8 (sum |A_end| + sum |B_end|) roughly doubled sum_k |S_k| and declined
-// 9.3 % of the C3 winners. max |S_k| <= mx0 + mx1 (exact.h quot_status decides). |x|^2 is the reference's
-// sequential chain, the halves taking turns (the euclidean winner's pattern).
+// 9.3 % of the C3 winners. max |S_k| from the norms (cosine_halves_finish;
+// exact.h quot_status decides). |x|^2 is the reference's sequential chain, the
+// halves taking turns (the euclidean winner's pattern).
 // Returns 0 (certified, v = 1 - q), 1 / 2 (declined: soft-x87 fix-up).
 __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* __restrict__ crow_h, double nbv, int h,
                                            double& v) {
@@ -1142,7 +1172,7 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
         xa = take_from_upper(xa);
     }
     // the inner product, each half over its own dims
-    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0;
+    double sh = 0.0, sl = 0.0, ts = 0.0;
     double off = 0.0;                     // half 0: B_end(s-1); half 1: A_end(s-1)
     double2 cb[4];
 #pragma unroll
@@ -1165,7 +1195,6 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
             sh = t;
             sl = __dadd_rn(sl, e);
             ts = __dadd_rn(ts, fabs(__dadd_rn(t, off)));
-            mx = fmax(mx, fabs(t));
         }
         // trade the running sums: half 0 takes B_end(s), half 1 A_end(s) (and
         // charges the block it ran behind: 8 |A_end(s) - A_end(s-1)|)
@@ -1175,25 +1204,8 @@ __device__ inline int cosine_winner_halves(const float (&xf)[64], const double* 
     }
     // the lower half's accumulator to the upper lanes
     const double sh0 = swap_halves(sh, h), sl0 = swap_halves(sl, h), ts0 = swap_halves(ts, h);
-    const double mx0 = swap_halves(mx, h);
     if (h == 0) return 2;                 // the upper lanes finish
-    IpAcc ip;
-    const double t = __dadd_rn(sh0, sh);
-    const double bb = __dsub_rn(t, sh0);
-    const double e = __dadd_rn(__dsub_rn(sh0, __dsub_rn(t, bb)), __dsub_rn(sh, bb));
-    ip.sh = t;
-    ip.sl = __dadd_rn(__dadd_rn(sl0, sl), e);
-    // sum_k |S_k| bound, rounded up: + 2^-47 relative for the roundings of
-    // |A_k + B_end| and of the sums here; the partial sums stand in for the
-    // exact ones (their TwoSum rests: |sl| <= 64 2^-53 max|t| per half, over 128
-    // terms and the offsets <= 2^-38 (mx0 + mx1), absolute: a cancelling
-    // A_k + B_end must not hide them)
-    ip.ts = __dadd_rn(__dadd_rn(ts0, ts) * (1.0 + 0x1p-47), 0x1p-37 * __dadd_rn(mx0, mx));
-    ip.mx = __dadd_rn(mx0, mx) * (1.0 + 0x1p-50);
-    double q, qr;
-    const int st = ip.quot_status(__dmul_rn(sqrt(xa), sqrt(nbv)), q, qr);
-    if (st == 0) v = __dsub_rn(1.0, q);
-    return st;
+    return cosine_halves_finish(sh0, sl0, ts0, sh, sl, ts, xa, nbv, v);
 }
 
 // The same for fp64 rows (ROWS = 2): the exact x values re-read from the row
@@ -1207,7 +1219,7 @@ __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc,
     double2 xn[4], xnn[4];
     load_x64_step(a, rowc, 0, h, xn);
     load_x64_step(a, rowc, 1, h, xnn);
-    double sh = 0.0, sl = 0.0, ts = 0.0, mx = 0.0;
+    double sh = 0.0, sl = 0.0, ts = 0.0;
     double off = 0.0;                     // as cosine_winner_halves
     double2 cb[4];
 #pragma unroll
@@ -1235,28 +1247,14 @@ __device__ inline int cosine_winner_halves_x64(const FusedArgs& a, int64_t rowc,
             sh = t;
             sl = __dadd_rn(sl, e);
             ts = __dadd_rn(ts, fabs(__dadd_rn(t, off)));
-            mx = fmax(mx, fabs(t));
         }
         const double other = swap_halves(sh, h);
         if (h == 1) ts = __dadd_rn(ts, 8.0 * fabs(__dsub_rn(other, off)));
         off = other;
     }
     const double sh0 = swap_halves(sh, h), sl0 = swap_halves(sl, h), ts0 = swap_halves(ts, h);
-    const double mx0 = swap_halves(mx, h);
     if (h == 0) return 2;
-    const double xa = a.xn2[rowc];
-    IpAcc ip;
-    const double t = __dadd_rn(sh0, sh);
-    const double bb = __dsub_rn(t, sh0);
-    const double e = __dadd_rn(__dsub_rn(sh0, __dsub_rn(t, bb)), __dsub_rn(sh, bb));
-    ip.sh = t;
-    ip.sl = __dadd_rn(__dadd_rn(sl0, sl), e);
-    ip.ts = __dadd_rn(__dadd_rn(ts0, ts) * (1.0 + 0x1p-47), 0x1p-37 * __dadd_rn(mx0, mx));   // as above
-    ip.mx = __dadd_rn(mx0, mx) * (1.0 + 0x1p-50);
-    double q, qr;
-    const int st = ip.quot_status(__dmul_rn(sqrt(xa), sqrt(nbv)), q, qr);
-    if (st == 0) v = __dsub_rn(1.0, q);
-    return st;
+    return cosine_halves_finish(sh0, sl0, ts0, sh, sl, ts, a.xn2[rowc], nbv, v);
 }
 
 // NIMG = 2 (512 < K <= 1024, euclidean): ONE launch for all centroids. The
