@@ -78,7 +78,7 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X, const double* x_mean, int6
 
 static int terms_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
                          const int64_t* unk_ptr, std::vector<int64_t>& soff, std::vector<int64_t>& hup,
-                         std::vector<int64_t>& toff);
+                         std::vector<int64_t>& toff, std::vector<int32_t>* hu_out = nullptr);
 static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_t N, int d, const int64_t* crow,
                               const int32_t* crows, int K, Pts U, int64_t nq, const int32_t* ucl,
                               const int64_t* unk_ptr, const int32_t* unk_idx, int64_t* soff_dev, int64_t* toff_dev,
@@ -165,7 +165,7 @@ static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
 // Host view of the cluster CSR: every user's member count on this shard and
 // the prefix offsets of its similarities.
 static int shard_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
-                         std::vector<int64_t>& soff) {
+                         std::vector<int64_t>& soff, std::vector<int32_t>* hu_out = nullptr) {
     std::vector<int64_t> hc((size_t)K + 1);
     std::vector<int32_t> hu((size_t)nq);
     LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
@@ -181,6 +181,7 @@ static int shard_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, c
         LSHKM_CHECK(n < (1ll << 31), LSHKM_ERR_ARG, "a cluster of 2^31 members or more");
         soff[q + 1] = soff[q] + n;
     }
+    if (hu_out) hu_out->swap(hu);
     return 0;
 }
 
@@ -243,9 +244,9 @@ static int cluster_chain_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
 // unknown-index CSR (hup) and toff (terms per user: members x unknown indexes).
 static int terms_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
                          const int64_t* unk_ptr, std::vector<int64_t>& soff, std::vector<int64_t>& hup,
-                         std::vector<int64_t>& toff) {
+                         std::vector<int64_t>& toff, std::vector<int32_t>* hu_out) {
     int rc;
-    if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff))) return rc;
+    if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff, hu_out))) return rc;
     hup.assign((size_t)nq + 1, 0);
     LSHKM_HIP(hipMemcpyAsync(hup.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
@@ -271,8 +272,9 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
                 "the terms form stages rows of a multiple of 8 B up to 1016 B (use lshkm_cluster_sims)");
     LSHKM_HIP(hipSetDevice(ctx->device));
     std::vector<int64_t> soff, hup, toff;
+    std::vector<int32_t> hu;                       // the users' clusters (host)
     int rc;
-    if ((rc = terms_offsets(ctx, crow, K, N, ucl, nq, unk_ptr, soff, hup, toff))) return rc;
+    if ((rc = terms_offsets(ctx, crow, K, N, ucl, nq, unk_ptr, soff, hup, toff, &hu))) return rc;
     *total_host = soff[nq];
     *tterms_host = toff[nq];
     LSHKM_CHECK(toff[nq] == 0 || unk_idx, LSHKM_ERR_ARG, "unk_idx is NULL");
@@ -285,10 +287,43 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
         int32_t* mq = map.as<int32_t>();
         int64_t* fl = reinterpret_cast<int64_t*>(map.as<char>() + 8 * (size_t)soff[nq]);
         double* unorm = reinterpret_cast<double*>(fl + soff[nq] + 1);     // the users' |u|^2
+        // cluster-major work list: the users of each cluster (ascending) and the
+        // 64-member chunks of the cluster's rows on this shard, each staged once
+        // for all of them (rc_terms_cl_kernel)
+        std::vector<int32_t> byc;
+        byc.reserve((size_t)nq);
+        for (int64_t q = 0; q < nq; q++)
+            if (soff[q + 1] > soff[q]) byc.push_back((int32_t)q);
+        std::stable_sort(byc.begin(), byc.end(), [&](int32_t a, int32_t b) { return hu[a] < hu[b]; });
+        // one host buffer, one copy: ioff [G + 1] | gcl [G] | gptr [G + 1] | gusr
+        std::vector<int32_t> gcl, gptr(1, 0), ioff(1, 0);
+        for (size_t k = 0; k < byc.size(); k++) {
+            const int32_t q = byc[k];
+            if (k == 0 || hu[q] != hu[byc[k - 1]]) {
+                if (k) gptr.push_back((int32_t)k);
+                gcl.push_back(hu[q]);
+                const int64_t n = soff[q + 1] - soff[q];
+                ioff.push_back(ioff.back() + (int32_t)((n + 63) / 64));
+            }
+        }
+        gptr.push_back((int32_t)byc.size());
+        const size_t nG = gcl.size();
+        std::vector<int32_t> pack;
+        pack.reserve(3 * nG + 2 + byc.size());
+        pack.insert(pack.end(), ioff.begin(), ioff.end());
+        pack.insert(pack.end(), gcl.begin(), gcl.end());
+        pack.insert(pack.end(), gptr.begin(), gptr.end());
+        pack.insert(pack.end(), byc.begin(), byc.end());
+        Buf& gb = ctx->ws_call[9];
+        if ((rc = gb.reserve(4 * std::max<size_t>(pack.size(), 1)))) return rc;
+        int32_t* dp = gb.as<int32_t>();
+        if (!pack.empty())
+            LSHKM_HIP(hipMemcpyAsync(dp, pack.data(), 4 * pack.size(), hipMemcpyHostToDevice, ctx->stream));
+        const RcGroups groups{dp, (int)nG, nG ? (int64_t)ioff.back() : 0, dp + nG + 1, dp + 2 * nG + 1, dp + 3 * nG + 2};
         if ((rc = launch_rc_terms(ctx->stream, X, x_mean, d, crow, crows, K, U, nq, ucl, soff_dev, soff[nq], unk_ptr,
                                   unk_idx, toff_dev, sims, terms, mq, mq + soff[nq], fl,
                                   reinterpret_cast<unsigned long long*>(fl + soff[nq]),
-                                  (unsigned long long*)ctx->stats.p + STAT_REC_SOFT, unorm)))
+                                  (unsigned long long*)ctx->stats.p + STAT_REC_SOFT, unorm, &groups)))
             return rc;
     }
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host offsets are copied before return

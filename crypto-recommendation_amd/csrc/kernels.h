@@ -199,11 +199,22 @@ int launch_rc_cluster_top_n(hipStream_t s, Pts X, const double* x_mean, int d, c
 // the per-(member, unknown index) terms of every user at once, then the chains
 // one wave per user (its chains lane by lane), then the quicksort per user.
 int rc_terms_stride8(int d, int elem);
+// Cluster-major work list of the terms form (rc_terms_cl_kernel): group g =
+// the users gusr[gptr[g] .. gptr[g + 1]) of cluster gcl[g]; its 64-member
+// chunks are the items ioff[g] .. ioff[g + 1] - 1 (nitems = ioff[ngroups]).
+struct RcGroups {
+    const int32_t* ioff;
+    int ngroups;
+    int64_t nitems;
+    const int32_t* gcl;
+    const int32_t* gptr;
+    const int32_t* gusr;
+};
 int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
                     int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
                     const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
                     int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
-                    unsigned long long* soft_count, double* unorm);
+                    unsigned long long* soft_count, double* unorm, const RcGroups* groups);
 int launch_rc_chain_terms(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff,
                           const double* sims, const double* terms, const double* carry_main, const double* carry_abs,
                           const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,

@@ -636,12 +636,8 @@ int launch_rc_shard_chain(hipStream_t s, Pts X, const double* x_mean, int d, con
 // The clustering recommender as two data-parallel phases instead of one wave
 // per user (which walked ~10K members with lane-per-member row loads touching
 // 64 lines per instruction, then the chains with 8 lanes of 64 busy):
-//   rc_terms_kernel: every (user, member) pair at once -- members flattened
-//     over users, 64 per wave; the 64 member rows staged through LDS by
-//     coalesced row loads, then per lane cosineSimilarity (IpAcc certificate;
-//     declined ones listed for rc_terms_fix_kernel's x87 chain) and the terms of
-//     get_predicted_user_sim's main sums, t = sim * (x[index] - mean)
-//     (crypto_rec.hpp:296), one fp64 per (member, unknown index);
+//   rc_terms_cl_kernel: every (user, member) pair at once, 64 members of a
+//     cluster per wave for all of the cluster's users (below);
 //   rc_chain_terms_kernel: one thread per (user, unknown index) adds its terms
 //     and the |sim| in member order (the reference's sequential chains,
 //     :290-296), 64 values in flight, continued from / into the rank carry;
@@ -698,7 +694,7 @@ __global__ __launch_bounds__(256) void rc_user_norm_kernel(const T* __restrict__
     }
 }
 
-// Member g's user and dataset row (the flattened pair space of rc_terms_kernel).
+// Member g's user and dataset row (the pair space g = soff[q] + i; rc_terms_fix_kernel's lookups).
 __global__ __launch_bounds__(256) void rc_member_map_kernel(int64_t nq, const int64_t* __restrict__ soff,
                                                             const int32_t* __restrict__ ucl,
                                                             const int64_t* __restrict__ crow,
@@ -715,30 +711,49 @@ __global__ __launch_bounds__(256) void rc_member_map_kernel(int64_t nq, const in
     }
 }
 
+// rc_terms_cl_kernel: a wave takes 64 members of one cluster, stages their
+// rows through LDS by coalesced row loads (the next item's rows in registers
+// while this one is computed) once for every user of that cluster on this
+// shard -- users sharing a cluster read its rows once, not once each (~1.6
+// users per distinct cluster at C5: 38 % fewer row bytes than one pass per
+// (user, member) pair); per user and lane: cosineSimilarity (IpAcc
+// certificate; declined ones listed for rc_terms_fix_kernel's x87 chain) and
+// the terms of get_predicted_user_sim's main sums, t = sim * (x[index] - mean)
+// (crypto_rec.hpp:296), one fp64 per (member, unknown index), at the pair
+// index soff[q] + i (i = the member's index in its cluster).
+// Item it: the 64-member chunk it - ioff[g] of group g (ioff[g] <= it <
+// ioff[g + 1], a binary search over the G + 1 offsets); group g: cluster gcl[g],
+// users gusr[gptr[g] .. gptr[g + 1]).
 template <typename T>
-__global__ __launch_bounds__(64) void rc_terms_kernel(
-    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const T* __restrict__ U, int64_t total,
-    const int32_t* __restrict__ mem_q, const int32_t* __restrict__ mem_r, const int64_t* __restrict__ soff,
-    const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx, const int64_t* __restrict__ toff,
-    double* __restrict__ sims, double* __restrict__ terms, int stride8, int64_t* __restrict__ fix_list,
-    unsigned long long* __restrict__ fix_count, const double* __restrict__ unorm) {
+__global__ __launch_bounds__(64) void rc_terms_cl_kernel(
+    const T* __restrict__ X, const double* __restrict__ x_mean, int d, const T* __restrict__ U,
+    const int32_t* __restrict__ ioff, int ngroups, int64_t nitems, const int32_t* __restrict__ gcl, const int32_t* __restrict__ gptr,
+    const int32_t* __restrict__ gusr, const int64_t* __restrict__ crow, const int32_t* __restrict__ crows,
+    const int64_t* __restrict__ soff, const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx,
+    const int64_t* __restrict__ toff, double* __restrict__ sims, double* __restrict__ terms, int stride8,
+    int64_t* __restrict__ fix_list, unsigned long long* __restrict__ fix_count, const double* __restrict__ unorm) {
     constexpr int SB = 16;                          // rows per staging batch (loads in flight)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x;
-    const int nunit = (int)((int64_t)d * (int64_t)sizeof(T) / 8);      // 8-B units per row (d * sizeof(T) % 8 == 0)
+    const int nunit = (int)((int64_t)d * (int64_t)sizeof(T) / 8);
     uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
     uint64_t* ustage = stage + (size_t)CT_STAGE * stride8;
     const uint64_t* myrow8 = stage + (size_t)lane * stride8;
-    int64_t g0 = (int64_t)blockIdx.x * CT_STAGE;
-    const int64_t gstep = (int64_t)gridDim.x * CT_STAGE;
-    // pipeline: the member map two chunks ahead; for rows of at most 64 units
-    // (fp32 d <= 128) the next chunk's rows in registers (unit `lane` of each)
-    // while this chunk is computed
-    auto map_at = [&](int64_t gg, int& qq, int32_t& rr) {
-        const int64_t x = min(gg + lane, total - 1);
-        qq = mem_q[x];
-        rr = mem_r[x];
+    // item it's group, first member, cluster size and this lane's member row
+    auto item_at = [&](int64_t it_, int& grp_, int& i0_, int64_t& n_, int32_t& r_) {
+        int lo = 0, hi = ngroups;                    // the last g with ioff[g] <= it_
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (ioff[mid] <= it_) lo = mid; else hi = mid;
+        }
+        grp_ = lo;
+        i0_ = (int)(it_ - ioff[lo]) * CT_STAGE;
+        const int64_t cb_ = crow[gcl[grp_]];
+        n_ = crow[gcl[grp_] + 1] - cb_;
+        r_ = crows[cb_ + (i0_ + lane < n_ ? i0_ + lane : n_ - 1)];
     };
+    // rows of at most 64 units (fp32 d <= 128): the next item's rows in
+    // registers (unit `lane` of each) while this item's users are computed
     const bool pfok = nunit <= 64;
     uint64_t pf[CT_STAGE];
     auto issue_pf = [&](int32_t rr) {
@@ -748,28 +763,23 @@ __global__ __launch_bounds__(64) void rc_terms_kernel(
             pf[t] = lane < nunit ? reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d)[lane] : 0ull;
         }
     };
-    int qA = 0, qB = 0;
-    int32_t rA = 0, rB = 0;
-    if (g0 < total) map_at(g0, qA, rA);
-    if (g0 + gstep < total) map_at(g0 + gstep, qB, rB);
-    if (pfok && g0 < total) issue_pf(rA);
-    for (; g0 < total; g0 += gstep) {
-        const int64_t g = min(g0 + lane, total - 1);
-        const bool on = g0 + lane < total;
-        const int q = qA;
-        const int32_t r = rA;
-        const int64_t i = g - soff[q];
-        const int q0 = __builtin_amdgcn_readfirstlane(q);
-        const bool one = __ballot(q != q0) == 0ull;
-        // stage the wave's member rows (and the user row when there is one user):
-        // from the prefetch registers, or in batches of SB rows with every load of
-        // a batch in flight before its LDS writes
-        __syncthreads();
+    int gN = 0, iN = 0;
+    int64_t nN = 0;
+    int32_t rN = 0;
+    if (blockIdx.x < nitems) {
+        item_at(blockIdx.x, gN, iN, nN, rN);
+        if (pfok) issue_pf(rN);
+    }
+    for (int64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const int grp = gN, i0 = iN;
+        const int64_t n = nN;
+        const int32_t r = rN;
+        const bool on = i0 + lane < n;
+        __syncthreads();                            // the previous item's reads of the stage are done
         if (pfok) {
 #pragma unroll
             for (int t = 0; t < CT_STAGE; t++)
                 if (lane < nunit) stage[(size_t)t * stride8 + lane] = pf[t];
-            if (g0 + gstep < total) issue_pf(rB);
         } else {
             for (int t0 = 0; t0 < CT_STAGE; t0 += SB) {
                 for (int u0 = 0; u0 < nunit; u0 += 64) {
@@ -786,45 +796,45 @@ __global__ __launch_bounds__(64) void rc_terms_kernel(
                 }
             }
         }
-        qA = qB;
-        rA = rB;
-        if (g0 + 2 * gstep < total) map_at(g0 + 2 * gstep, qB, rB);
-        if (one)
-            for (int u0 = lane; u0 < nunit; u0 += 64)
-                ustage[u0] = reinterpret_cast<const uint64_t*>(U + (int64_t)q0 * d)[u0];
-        __syncthreads();
-        const T* u = U + (int64_t)q * d;
-        bool ok;
-        double sv;
-        if (one) sv = ct_sim<T>(myrow8, ustage, nunit, unorm[q0], ok);            // wave-uniform
-        else sv = ct_sim<T>(myrow8, reinterpret_cast<const uint64_t*>(u), nunit, unorm[q], ok);
-        // declined certificates (~12% of random pairs: cancelling inner products
-        // widen the bound) to the list of rc_terms_fix_kernel, which runs the x87
-        // chain with every lane busy (inline it cost each wave the chain's full
-        // length for a few lanes)
-        const unsigned long long dm = __ballot(on && !ok);
-        if (dm) {
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(fix_count, (unsigned long long)__popcll(dm));
-            base = __shfl(base, 0);
-            if (on && !ok) fix_list[base + __popcll(dm & ((1ull << lane) - 1ull))] = g;
+        if (it + gridDim.x < nitems) {
+            item_at(it + gridDim.x, gN, iN, nN, rN);
+            if (pfok) issue_pf(rN);
         }
-        if (!on || !ok) continue;
-        sims[g] = sv;
-        if (terms) {
-            const int64_t o = unk_ptr[q];
-            const int m = (int)(unk_ptr[q + 1] - o);
-            const double mean = x_mean[r];
-            const T* xr = reinterpret_cast<const T*>(myrow8);
-            double* tq = terms + toff[q] + i * m;           // member-major: the pair's m terms together
-            for (int e = 0; e < m; e++) tq[e] = __dmul_rn(sv, __dsub_rn((double)xr[unk_idx[o + e]], mean));
+        const double mean = x_mean[r];
+        const T* xr = reinterpret_cast<const T*>(myrow8);
+        for (int k = gptr[grp]; k < gptr[grp + 1]; k++) {
+            const int q = gusr[k];
+            __syncthreads();                        // the stage landed / the previous user's row is read
+            for (int u0 = lane; u0 < nunit; u0 += 64)
+                ustage[u0] = reinterpret_cast<const uint64_t*>(U + (int64_t)q * d)[u0];
+            __syncthreads();
+            bool ok;
+            const double sv = ct_sim<T>(myrow8, ustage, nunit, unorm[q], ok);
+            const int64_t i = i0 + lane;
+            const int64_t g = soff[q] + i;
+            const unsigned long long dm = __ballot(on && !ok);
+            if (dm) {
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(fix_count, (unsigned long long)__popcll(dm));
+                base = __shfl(base, 0);
+                if (on && !ok) fix_list[base + __popcll(dm & ((1ull << lane) - 1ull))] = g;
+            }
+            if (on && ok) {
+                sims[g] = sv;
+                if (terms) {
+                    const int64_t o = unk_ptr[q];
+                    const int m = (int)(unk_ptr[q + 1] - o);
+                    double* tq = terms + toff[q] + i * m;       // member-major: the pair's m terms together
+                    for (int e = 0; e < m; e++) tq[e] = __dmul_rn(sv, __dsub_rn((double)xr[unk_idx[o + e]], mean));
+                }
+            }
         }
     }
 }
 
 // The listed members: cosineSimilarity by the x87 chain (softx87.h X87acc),
 // lane per member, 64 members per wave with their rows and their users' rows
-// staged through LDS (coalesced row loads, as rc_terms_kernel), then the terms;
+// staged through LDS (coalesced row loads, as rc_terms_cl_kernel), then the terms;
 // soft_count += the list length.
 template <typename T>
 __global__ __launch_bounds__(64) void rc_terms_fix_kernel(
@@ -1016,7 +1026,7 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
                     int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
                     const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
                     int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
-                    unsigned long long* soft_count, double* unorm) {
+                    unsigned long long* soft_count, double* unorm, const RcGroups* groups) {
     if (nq <= 0 || total <= 0) return 0;
     const int elem = X.f64 ? 8 : 4;
     if (((int64_t)d * elem) % 8 != 0) return -1;
@@ -1029,14 +1039,17 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
         hipLaunchKernelGGL(rc_user_norm_kernel<double>, dim3(gsz(nq, 256, 1024)), dim3(256), 0, s, U.d(), nq, d, unorm);
     else
         hipLaunchKernelGGL(rc_user_norm_kernel<float>, dim3(gsz(nq, 256, 1024)), dim3(256), 0, s, U.f(), nq, d, unorm);
-    const dim3 grid(gsz(total, CT_STAGE, 4096));
     if (hipMemsetAsync(fix_count, 0, 8, s) != hipSuccess) return kstatus("rc_terms (memset)");
+    if (!groups || groups->nitems <= 0) return -1;
+    const dim3 cgrid((unsigned)std::min<int64_t>(groups->nitems, 65536));
     if (X.f64)
-        hipLaunchKernelGGL(rc_terms_kernel<double>, grid, dim3(64), lds, s, X.d(), x_mean, d, U.d(), total, mem_q, mem_r,
-                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
+        hipLaunchKernelGGL(rc_terms_cl_kernel<double>, cgrid, dim3(64), lds, s, X.d(), x_mean, d, U.d(), groups->ioff,
+                           groups->ngroups, groups->nitems, groups->gcl, groups->gptr, groups->gusr, crow, crows, soff,
+                           unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
     else
-        hipLaunchKernelGGL(rc_terms_kernel<float>, grid, dim3(64), lds, s, X.f(), x_mean, d, U.f(), total, mem_q, mem_r,
-                           soff, unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
+        hipLaunchKernelGGL(rc_terms_cl_kernel<float>, cgrid, dim3(64), lds, s, X.f(), x_mean, d, U.f(), groups->ioff,
+                           groups->ngroups, groups->nitems, groups->gcl, groups->gptr, groups->gusr, crow, crows, soff,
+                           unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
     // the list length is on the device: a grid for up to ~1/4 of the pairs, looping beyond
     const dim3 fgrid(gsz(total / 4 + 1, CT_STAGE, 2048));
     const size_t flds = 2 * lds;
@@ -1046,7 +1059,7 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
     else
         hipLaunchKernelGGL(rc_terms_fix_kernel<float>, fgrid, dim3(64), flds, s, X.f(), x_mean, d, U.f(), mem_q, mem_r,
                            soff, unk_ptr, unk_idx, toff, sims, terms, fix_list, fix_count, stride8, soft_count, unorm);
-    return kstatus("rc_terms_kernel");
+    return kstatus("rc_terms_cl_kernel");
 }
 
 int launch_rc_chain_terms(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff,
