@@ -321,7 +321,8 @@ static int cube_h_batch(lshkm_cube cube, Pts X, int64_t N, int32_t** h_out) {
 }
 
 // First occurrence of every (f, h) of the batch that has no coin yet, as
-// (key = row * k + f, memo offset) pairs in WS_SIZES / WS_COFF; count in *n.
+// (key = row * k + f, memo offset) pairs in WS_SIZES / WS_COFF; count in
+// cube->cnt on the device and, when n is given, in *n.
 static int cube_unseen_impl(lshkm_cube cube, const int32_t* h, int64_t N, unsigned int* n) {
     lshkm_ctx ctx = cube->ctx;
     hipStream_t s = ctx->stream;
@@ -337,7 +338,7 @@ static int cube_unseen_impl(lshkm_cube cube, const int32_t* h, int64_t N, unsign
         return rc;
     if ((rc = launch_coin_collect(s, cube->first_row.as<int32_t>(), total, k, cube->hspan, slot<int32_t>(ctx, WS_SIZES),
                                   slot<int32_t>(ctx, WS_COFF), cube->cnt.as<unsigned int>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
-    return d2h(ctx, n, cube->cnt.p, 4);
+    return n ? d2h(ctx, n, cube->cnt.p, 4) : 0;
 }
 
 static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex) {
@@ -356,6 +357,18 @@ static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex
     int32_t* h = nullptr;
     if ((rc = cube_h_batch(cube, X, N, &h))) return rc;
     // first occurrence of each unseen (f, h), then the draw in (row, f) order
+    const int64_t bound = std::min<int64_t>((int64_t)k * cube->hspan, N * k);
+    if (bound <= 8192) {
+        // the count cannot pass the one-workgroup sort's limit: it stays on the
+        // device (sort and draw read it there), no host round trip
+        if ((rc = cube_unseen_impl(cube, h, N, nullptr))) return rc;
+        if ((rc = sort_pairs_small(s, slot<int32_t>(ctx, WS_SIZES), slot<int32_t>(ctx, WS_COFF), 0,
+                                   slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>())) ||
+            (rc = launch_coin_draw(s, slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>(), cube->hmin, cube->hspan,
+                                   cube->memo.as<int32_t>(), cube->rng_d.as<uint32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = launch_coin_vertex(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), vertex))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        return 0;
+    }
     unsigned int ncoins = 0;
     if ((rc = cube_unseen_impl(cube, h, N, &ncoins))) return rc;
     if (ncoins > 0) {

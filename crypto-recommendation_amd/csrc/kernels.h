@@ -122,8 +122,9 @@ int launch_add_counters(hipStream_t s, unsigned long long* stats, int n, const i
 // Stable bucket scatter (scatter.hip).
 size_t sort_scratch_bytes(int64_t N, int64_t range, int T = 1);
 // Distinct int32 keys, n <= 8192: one-workgroup bitonic sort of (key, val) pairs.
+// n_dev: the count is read on the device instead (the caller bounds it by 8192).
 int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, int64_t n, int32_t* keys_out,
-                     int32_t* vals_out);
+                     int32_t* vals_out, const unsigned int* n_dev = nullptr);
 int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,
                        int64_t range, int32_t* keys_out, int32_t* vals_out, void* scratch);
 int launch_csr_bounds(hipStream_t s, const int32_t* sorted_keys, int64_t N, int64_t nb, int64_t* row_ptr, int T = 1);

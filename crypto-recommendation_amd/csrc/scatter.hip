@@ -210,9 +210,14 @@ __global__ void rs_copy(const int32_t* __restrict__ keys, int64_t kstride, const
 constexpr int SP_MAX = 8192;
 __global__ __launch_bounds__(1024) void sort_pairs_small_kernel(const int32_t* __restrict__ keys,
                                                                 const int32_t* __restrict__ vals, int n, int P,
+                                                                const unsigned int* __restrict__ n_dev,
                                                                 int32_t* __restrict__ keys_out,
                                                                 int32_t* __restrict__ vals_out) {
     __shared__ int32_t sk[SP_MAX], sv[SP_MAX];
+    if (n_dev) {                        // count left on the device (<= SP_MAX by the caller's bound)
+        n = (int)min(*n_dev, (unsigned int)SP_MAX);
+        for (P = 1; P < n; P <<= 1) {}
+    }
     for (int i = threadIdx.x; i < P; i += 1024) {
         sk[i] = i < n ? keys[i] : 0x7FFFFFFF;
         sv[i] = i < n ? vals[i] : 0;
@@ -240,7 +245,11 @@ __global__ __launch_bounds__(1024) void sort_pairs_small_kernel(const int32_t* _
 }
 
 int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, int64_t n, int32_t* keys_out,
-                     int32_t* vals_out) {
+                     int32_t* vals_out, const unsigned int* n_dev) {
+    if (n_dev) {
+        hipLaunchKernelGGL(sort_pairs_small_kernel, dim3(1), dim3(1024), 0, s, keys, vals, 0, 1, n_dev, keys_out, vals_out);
+        return kstatus("scatter.hip");
+    }
     if (n <= 0) return 0;
     if (n > SP_MAX) {
         set_error("sort_pairs_small: too many keys");
@@ -248,7 +257,7 @@ int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, in
     }
     int P = 1;
     while (P < n) P <<= 1;
-    hipLaunchKernelGGL(sort_pairs_small_kernel, dim3(1), dim3(1024), 0, s, keys, vals, (int)n, P, keys_out, vals_out);
+    hipLaunchKernelGGL(sort_pairs_small_kernel, dim3(1), dim3(1024), 0, s, keys, vals, (int)n, P, nullptr, keys_out, vals_out);
     return kstatus("scatter.hip");
 }
 
