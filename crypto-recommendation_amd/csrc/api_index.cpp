@@ -19,7 +19,9 @@ using namespace lshkm;
 // the h range, into a pair the caller pre-set. LSHKM_HASH_PATH=fp64 forces the
 // fp64 kernel (tests compare the two).
 int lshkm::hash_rows(lshkm_ctx ctx, int mode, Pts X, int64_t N, const ProjTable& pj, int64_t nb, int32_t* out_h,
-                     int32_t* out_phi, int32_t* out_bucket, int32_t* mm) {
+                     int32_t* out_phi, int32_t* out_bucket, int32_t* mm, bool* h16) {
+    const bool want16 = h16 && *h16;
+    if (h16) *h16 = false;
     if (N <= 0) return 0;
     const bool force64 = test_switch("LSHKM_HASH_PATH", "fp64");
     unsigned long long* stats = (unsigned long long*)ctx->stats.p;
@@ -33,9 +35,13 @@ int lshkm::hash_rows(lshkm_ctx ctx, int mode, Pts X, int64_t N, const ProjTable&
         }
         if ((rc = ctx->ws_hfix.reserve((size_t)cap * 8)) || (rc = ctx->ws_seg.reserve((size_t)FUSED_MAX_SEGS * 2 * 4)))
             return rc;
-        return launch_hash_mfma(ctx->stream, mode, X.f(), N, pj.mfma_params(nb), out_h, out_phi, out_bucket, mm,
-                                (unsigned long long*)ctx->ws_hfix.p, cap, (int32_t*)ctx->ws_seg.p, FUSED_MAX_SEGS * 2,
-                                stats);
+        const bool w16 = want16 && mode == HM_CUBE_EUCLID_H;
+        if ((rc = launch_hash_mfma(ctx->stream, mode, X.f(), N, pj.mfma_params(nb), out_h, out_phi, out_bucket, mm,
+                                   (unsigned long long*)ctx->ws_hfix.p, cap, (int32_t*)ctx->ws_seg.p, FUSED_MAX_SEGS * 2,
+                                   stats, w16)))
+            return rc;
+        if (h16) *h16 = w16;
+        return 0;
     }
     if ((rc = launch_proj_hash(ctx->stream, mode, X, N, pj.params(nb), out_h, out_phi, out_bucket, stats))) return rc;
     if (mode == HM_CUBE_EUCLID_H && mm) return launch_h_minmax(ctx->stream, out_h, N * pj.k, mm);
@@ -298,39 +304,47 @@ static int cube_ensure_window(lshkm_cube cube, int32_t lo_h, int32_t hi_h) {
 }
 
 // h of a batch (EuclideanH, k per row) into WS_H, and the memo window over it.
-static int cube_h_batch(lshkm_cube cube, Pts X, int64_t N, int32_t** h_out) {
+// h is int16 (*h16) when the MFMA kernel wrote it and the range fits, else
+// int32 (the batch is hashed again when the int16 values saturated).
+static int cube_h_batch(lshkm_cube cube, Pts X, int64_t N, const void** h_out, bool* h16) {
     lshkm_ctx ctx = cube->ctx;
     hipStream_t s = ctx->stream;
     const int k = cube->k;
     int rc;
     LSHKM_CHECK(N * k < (1ll << 31), LSHKM_ERR_UNSUPPORTED, "rows * k must be < 2^31");
-    if ((rc = reserve(ctx, WS_H, (size_t)N * k * 4))) return rc;
+    if ((rc = reserve(ctx, WS_H, (size_t)N * k * 4 + 16))) return rc;   // + the staged loads' slack (cube.hip)
     int32_t* h = slot<int32_t>(ctx, WS_H);
     const int32_t init_mm[2] = {0x7FFFFFFF, (int32_t)0x80000000};
-    if ((rc = ctx->pin_stage(8))) return rc;
-    std::memcpy(ctx->pinned, init_mm, 8);
-    LSHKM_HIP(hipMemcpyAsync(cube->mm.p, ctx->pinned, 8, hipMemcpyHostToDevice, s));
-    LSHKM_HIP(hipEventRecord(ctx->pinned_ev, s));
-    if ((rc = hash_rows(ctx, HM_CUBE_EUCLID_H, X, N, cube->proj, 1ll << k, h, nullptr, nullptr,
-                        cube->mm.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     int32_t mm[2];
-    if ((rc = d2h(ctx, mm, cube->mm.p, 8))) return rc;
+    bool narrow = true;
+    for (int pass = 0; pass < 2; pass++) {
+        if ((rc = ctx->pin_stage(8))) return rc;
+        std::memcpy(ctx->pinned, init_mm, 8);
+        LSHKM_HIP(hipMemcpyAsync(cube->mm.p, ctx->pinned, 8, hipMemcpyHostToDevice, s));
+        LSHKM_HIP(hipEventRecord(ctx->pinned_ev, s));
+        if ((rc = hash_rows(ctx, HM_CUBE_EUCLID_H, X, N, cube->proj, 1ll << k, h, nullptr, nullptr,
+                            cube->mm.as<int32_t>(), &narrow))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = d2h(ctx, mm, cube->mm.p, 8))) return rc;
+        if (!narrow || (mm[0] >= -32768 && mm[1] <= 32767)) break;
+        narrow = false;                      // saturated: hash again as int32
+    }
     if ((rc = cube_ensure_window(cube, mm[0], mm[1]))) return rc;
     *h_out = h;
+    *h16 = narrow;
     return 0;
 }
 
 // First occurrence of every (f, h) of the batch that has no coin yet, as
 // (key = row * k + f, memo offset) pairs in WS_SIZES / WS_COFF; count in
 // cube->cnt on the device and, when n is given, in *n.
-static int cube_unseen_impl(lshkm_cube cube, const int32_t* h, int64_t N, unsigned int* n) {
+static int cube_unseen_impl(lshkm_cube cube, const void* h, bool h16, int64_t N, unsigned int* n) {
     lshkm_ctx ctx = cube->ctx;
     hipStream_t s = ctx->stream;
     const int k = cube->k;
     int rc;
     const int64_t total = (int64_t)k * cube->hspan;
     LSHKM_HIP(hipMemsetAsync(cube->first_row.p, 0x7F, (size_t)total * 4, s));
-    if ((rc = launch_coin_first(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), cube->first_row.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if ((rc = launch_coin_first(s, h, h16, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), cube->first_row.as<int32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     LSHKM_HIP(hipMemsetAsync(cube->cnt.p, 0, 4, s));
     const int64_t maxe = std::min<int64_t>(total, N * k);
     if ((rc = reserve(ctx, WS_SIZES, (size_t)maxe * 4)) || (rc = reserve(ctx, WS_COFF, (size_t)maxe * 4)) ||
@@ -354,23 +368,24 @@ static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex
         }
         return 0;
     }
-    int32_t* h = nullptr;
-    if ((rc = cube_h_batch(cube, X, N, &h))) return rc;
+    const void* h = nullptr;
+    bool h16 = false;
+    if ((rc = cube_h_batch(cube, X, N, &h, &h16))) return rc;
     // first occurrence of each unseen (f, h), then the draw in (row, f) order
     const int64_t bound = std::min<int64_t>((int64_t)k * cube->hspan, N * k);
     if (bound <= 8192) {
         // the count cannot pass the one-workgroup sort's limit: it stays on the
         // device (sort and draw read it there), no host round trip
-        if ((rc = cube_unseen_impl(cube, h, N, nullptr))) return rc;
+        if ((rc = cube_unseen_impl(cube, h, h16, N, nullptr))) return rc;
         if ((rc = sort_pairs_small(s, slot<int32_t>(ctx, WS_SIZES), slot<int32_t>(ctx, WS_COFF), 0,
                                    slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>())) ||
             (rc = launch_coin_draw(s, slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>(), cube->hmin, cube->hspan,
                                    cube->memo.as<int32_t>(), cube->rng_d.as<uint32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
-        if ((rc = launch_coin_vertex(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), vertex))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        if ((rc = launch_coin_vertex(s, h, h16, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), vertex))) { LSHKM_LAUNCH_CHECK(); return rc; }
         return 0;
     }
     unsigned int ncoins = 0;
-    if ((rc = cube_unseen_impl(cube, h, N, &ncoins))) return rc;
+    if ((rc = cube_unseen_impl(cube, h, h16, N, &ncoins))) return rc;
     if (ncoins > 0) {
         // the draw order: keys row * k + f are distinct, so a few thousand sort in
         // one workgroup (a multi-pass radix sort is a dozen launches)
@@ -385,7 +400,7 @@ static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex
         if ((rc = launch_coin_draw(s, slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>(), cube->hmin, cube->hspan,
                                    cube->memo.as<int32_t>(), cube->rng_d.as<uint32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }
     }
-    if ((rc = launch_coin_vertex(s, h, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), vertex))) { LSHKM_LAUNCH_CHECK(); return rc; }
+    if ((rc = launch_coin_vertex(s, h, h16, N, k, cube->hmin, cube->hspan, cube->memo.as<int32_t>(), vertex))) { LSHKM_LAUNCH_CHECK(); return rc; }
     return 0;
 }
 
@@ -400,10 +415,11 @@ static int cube_unseen_api(lshkm_cube cube, Pts X, int64_t N, int32_t* f_host, i
     *count_host = 0;
     if (N == 0) return 0;
     int rc;
-    int32_t* h = nullptr;
-    if ((rc = cube_h_batch(cube, X, N, &h))) return rc;
+    const void* h = nullptr;
+    bool h16 = false;
+    if ((rc = cube_h_batch(cube, X, N, &h, &h16))) return rc;
     unsigned int n = 0;
-    if ((rc = cube_unseen_impl(cube, h, N, &n))) return rc;
+    if ((rc = cube_unseen_impl(cube, h, h16, N, &n))) return rc;
     *count_host = n;
     if (n == 0 || (int64_t)n > cap) return 0;
     std::vector<int32_t> keys(n), offs(n);

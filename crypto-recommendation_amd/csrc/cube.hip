@@ -46,12 +46,13 @@ int launch_h_minmax(hipStream_t s, const int32_t* h, int64_t n, int32_t* mm_dev)
     return kstatus("cube.hip");
 }
 
-__global__ void coin_first_kernel(const int32_t* __restrict__ h, int64_t N, int k, int32_t hmin, int32_t hspan,
+template <typename T>
+__global__ void coin_first_kernel(const T* __restrict__ h, int64_t N, int k, int32_t hmin, int32_t hspan,
                                   const int32_t* __restrict__ memo, int32_t* __restrict__ first_row) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N * k; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t row = e / k;
         const int f = (int)(e - row * k);
-        const int64_t off = (int64_t)f * hspan + (h[e] - hmin);
+        const int64_t off = (int64_t)f * hspan + ((int32_t)h[e] - hmin);
         // read first: most (f, h) have an earlier row already (the atomics on the
         // few popular entries otherwise serialise)
         if (memo[off] < 0 && first_row[off] > (int32_t)row) atomicMin(first_row + off, (int32_t)row);
@@ -68,27 +69,81 @@ constexpr int CF_LDS_MAX = 12288;
 constexpr int32_t CF_SEEN = -1;
 constexpr int CF_KMAX = 32;          // functions per row held in registers (k <= 32)
 
-// This thread's row of k h values (k even: 8-byte loads, the row starts 8-B aligned).
-__device__ inline void cf_load_row(const int32_t* __restrict__ h, int64_t row, int k, int32_t (&v)[CF_KMAX]) {
-    const int32_t* p = h + row * k;
-    if ((k & 1) == 0) {
-#pragma unroll
-        for (int f = 0; f < CF_KMAX; f += 2)
-            if (f < k) {
-                const int2 w = *reinterpret_cast<const int2*>(p + f);
-                v[f] = w.x;
-                v[f + 1] = w.y;
-            }
-    } else {
-#pragma unroll
-        for (int f = 0; f < CF_KMAX; f++)
-            if (f < k) v[f] = p[f];
+// A wave's 64 consecutive rows of h are contiguous and 16-B aligned (chunks
+// start at multiples of 64 rows): cf_fetch issues their coalesced 16-byte
+// loads, cf_stash puts them in the wave's LDS buffer and reads this lane's row
+// back (lane-per-row global loads touch ~k lines per instruction). The last chunk may read up to
+// 15 B past the rows (WS_H keeps that slack).
+// PF: 16-B pieces per lane, ceil(k * sizeof(T) / 16) (1, 2, 4 or 8). The
+// loads are unconditional (clamped to the chunk's last piece) so the pieces
+// stay in registers.
+// (named registers, not an array: a loop-carried int4 array goes to scratch)
+struct CfPre {
+    int4 p0, p1, p2, p3, p4, p5, p6, p7;
+};
+template <typename T, int PF>
+__device__ inline CfPre cf_fetch(const T* __restrict__ h, int64_t row0, int nrows, int k, int lane) {
+    CfPre pre;
+    const int q = (nrows * k * (int)sizeof(T) + 15) >> 4;
+    const int4* src = reinterpret_cast<const int4*>(h + row0 * k);
+    pre.p0 = src[min(lane, q - 1)];
+    if constexpr (PF > 1) pre.p1 = src[min(lane + 64, q - 1)];
+    if constexpr (PF > 2) { pre.p2 = src[min(lane + 128, q - 1)]; pre.p3 = src[min(lane + 192, q - 1)]; }
+    if constexpr (PF > 4) {
+        pre.p4 = src[min(lane + 256, q - 1)]; pre.p5 = src[min(lane + 320, q - 1)];
+        pre.p6 = src[min(lane + 384, q - 1)]; pre.p7 = src[min(lane + 448, q - 1)];
     }
+    return pre;
+}
+template <typename T, int PF>
+__device__ inline void cf_stash(const CfPre pre, int nrows, int k, int32_t* __restrict__ buf, int lane,
+                                int32_t (&v)[CF_KMAX]) {
+    const int q = (nrows * k * (int)sizeof(T) + 15) >> 4;
+    int4* b4 = reinterpret_cast<int4*>(buf);
+    if (lane < q) b4[lane] = pre.p0;
+    if constexpr (PF > 1) { if (lane + 64 < q) b4[lane + 64] = pre.p1; }
+    if constexpr (PF > 2) {
+        if (lane + 128 < q) b4[lane + 128] = pre.p2;
+        if (lane + 192 < q) b4[lane + 192] = pre.p3;
+    }
+    if constexpr (PF > 4) {
+        if (lane + 256 < q) b4[lane + 256] = pre.p4;
+        if (lane + 320 < q) b4[lane + 320] = pre.p5;
+        if (lane + 384 < q) b4[lane + 384] = pre.p6;
+        if (lane + 448 < q) b4[lane + 448] = pre.p7;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    {   // lanes past nrows read stale buffer words (never used)
+        if (sizeof(T) == 2 && (k & 1)) {
+            const int16_t* p = reinterpret_cast<const int16_t*>(buf) + lane * k;
+#pragma unroll
+            for (int f = 0; f < CF_KMAX; f++)
+                if (f < k) v[f] = p[f];
+        } else if (sizeof(T) == 2) {
+            const int32_t* p = buf + lane * (k >> 1);
+#pragma unroll
+            for (int f = 0; f < CF_KMAX; f += 2)
+                if (f < k) {
+                    const int32_t w = p[f >> 1];
+                    v[f] = (int32_t)(int16_t)(w & 0xFFFF);
+                    v[f + 1] = w >> 16;
+                }
+        } else {
+            const int32_t* p = buf + lane * k;
+#pragma unroll
+            for (int f = 0; f < CF_KMAX; f++)
+                if (f < k) v[f] = p[f];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// One row per thread: its k values in registers (independent loads, a wave
-// reads 64 consecutive rows), then a read-first LDS min per (f, h).
-__global__ __launch_bounds__(256) void coin_first_lds_kernel(const int32_t* __restrict__ h, int64_t N, int k,
+// One row per lane (a wave takes 64 consecutive rows, staged through LDS),
+// then a read-first LDS min per (f, h).
+template <typename T, int PF>
+__global__ __launch_bounds__(256) void coin_first_lds_kernel(const T* __restrict__ h, int64_t N, int k,
                                                              int32_t hmin, int32_t hspan, int64_t rows_per_block,
                                                              const int32_t* __restrict__ memo,
                                                              int32_t* __restrict__ first_row) {
@@ -98,9 +153,15 @@ __global__ __launch_bounds__(256) void coin_first_lds_kernel(const int32_t* __re
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min(N, r0 + rows_per_block);
-    for (int64_t row = r0 + threadIdx.x; row < r1; row += 256) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // chunk starts are 64-row aligned (rows_per_block is a multiple of 64)
+    int32_t* stage = lmin + ((total + 3) & ~3) + wave * (64 * k * (int)sizeof(T) / 4);
+    for (int64_t c0 = r0 + 64 * wave; c0 < r1; c0 += 256) {
+        const int64_t row = c0 + lane;
+        const int nrows = (int)min((int64_t)64, r1 - c0);
         int32_t v[CF_KMAX];
-        cf_load_row(h, row, k, v);
+        cf_stash<T, PF>(cf_fetch<T, PF>(h, c0, nrows, k, lane), nrows, k, stage, lane, v);
+        if (row >= r1) continue;
 #pragma unroll
         for (int f = 0; f < CF_KMAX; f++) {
             if (f >= k) break;
@@ -203,28 +264,35 @@ __global__ void coin_draw_kernel(const int32_t* __restrict__ sorted_vals, const 
     if (lane == 0) *state = st;
 }
 
-__global__ void coin_vertex_kernel(const int32_t* __restrict__ h, int64_t N, int k, int32_t hmin, int32_t hspan,
+template <typename T>
+__global__ void coin_vertex_kernel(const T* __restrict__ h, int64_t N, int k, int32_t hmin, int32_t hspan,
                                    const int32_t* __restrict__ memo, int32_t* __restrict__ vertex) {
     for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < N; row += (int64_t)gridDim.x * blockDim.x) {
         int v = 0;
-        for (int f = 0; f < k; f++) v = (v << 1) + memo[(size_t)f * hspan + (h[row * k + f] - hmin)];
+        for (int f = 0; f < k; f++) v = (v << 1) + memo[(size_t)f * hspan + ((int32_t)h[row * k + f] - hmin)];
         vertex[row] = v;
     }
 }
 
 // Memo windows of at most CF_LDS_MAX entries: the memo in LDS, one row per
-// thread with its k values loaded at once.
-__global__ __launch_bounds__(256) void coin_vertex_lds_kernel(const int32_t* __restrict__ h, int64_t N, int k,
+// lane from the staged rows.
+template <typename T, int PF>
+__global__ __launch_bounds__(256) void coin_vertex_lds_kernel(const T* __restrict__ h, int64_t N, int k,
                                                               int32_t hmin, int32_t hspan,
                                                               const int32_t* __restrict__ memo,
                                                               int32_t* __restrict__ vertex) {
-    extern __shared__ int32_t lmemo[];          // [k * hspan]
+    extern __shared__ int32_t lmemo[];          // [k * hspan], then the per-wave row stages
     const int total = k * hspan;
     for (int e = threadIdx.x; e < total; e += 256) lmemo[e] = memo[e];
     __syncthreads();
-    for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < N; row += (int64_t)gridDim.x * 256) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int32_t* stage = lmemo + ((total + 3) & ~3) + wave * (64 * k * (int)sizeof(T) / 4);
+    for (int64_t c0 = (int64_t)blockIdx.x * 256 + 64 * wave; c0 < N; c0 += (int64_t)gridDim.x * 256) {
+        const int64_t row = c0 + lane;
+        const int nrows = (int)min((int64_t)64, N - c0);
         int32_t v[CF_KMAX];
-        cf_load_row(h, row, k, v);
+        cf_stash<T, PF>(cf_fetch<T, PF>(h, c0, nrows, k, lane), nrows, k, stage, lane, v);
+        if (row >= N) continue;
         int x = 0;
 #pragma unroll
         for (int f = 0; f < CF_KMAX; f++) {
@@ -235,8 +303,9 @@ __global__ __launch_bounds__(256) void coin_vertex_lds_kernel(const int32_t* __r
     }
 }
 
-int launch_coin_first(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
-                      const int32_t* memo, int32_t* first_row) {
+template <typename T>
+static int launch_coin_first_t(hipStream_t s, const T* h, int64_t N, int k, int32_t hmin, int32_t hspan,
+                               const int32_t* memo, int32_t* first_row) {
     const int64_t n = N * k;
     const int64_t total = (int64_t)k * hspan;
     if (total <= CF_LDS_MAX && k <= CF_KMAX) {
@@ -249,14 +318,23 @@ int launch_coin_first(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t
         const int64_t ncu = dev < 64 && cus[dev] > 0 ? cus[dev] : 256;
         // >= 2048 rows per block so the LDS table's setup and merge stay small
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(4 * ncu, (N + 2047) / 2048));
-        const int64_t rpb = (N + nblk - 1) / nblk;
-        hipLaunchKernelGGL(coin_first_lds_kernel, dim3((unsigned)nblk), dim3(256), (size_t)total * 4, s, h, N, k, hmin,
-                           hspan, rpb, memo, first_row);
+        const int64_t rpb = ((N + nblk - 1) / nblk + 63) & ~(int64_t)63;
+        const size_t lds = (size_t)((total + 3) & ~3) * 4 + 4 * 64 * (size_t)k * sizeof(T);
+        const int pf = (k * (int)sizeof(T) + 15) / 16;
+#define CF_FIRST(P) hipLaunchKernelGGL((coin_first_lds_kernel<T, P>), dim3((unsigned)nblk), dim3(256), lds, s, h, N, k, hmin, hspan, rpb, memo, first_row)
+        if (pf <= 1) CF_FIRST(1); else if (pf <= 2) CF_FIRST(2); else if (pf <= 4) CF_FIRST(4); else CF_FIRST(8);
+#undef CF_FIRST
         return kstatus("cube.hip");
     }
-    hipLaunchKernelGGL(coin_first_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, h, N,
-                       k, hmin, hspan, memo, first_row);
+    hipLaunchKernelGGL(coin_first_kernel<T>, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, h,
+                       N, k, hmin, hspan, memo, first_row);
     return kstatus("cube.hip");
+}
+
+int launch_coin_first(hipStream_t s, const void* h, bool h16, int64_t N, int k, int32_t hmin, int32_t hspan,
+                      const int32_t* memo, int32_t* first_row) {
+    return h16 ? launch_coin_first_t(s, static_cast<const int16_t*>(h), N, k, hmin, hspan, memo, first_row)
+               : launch_coin_first_t(s, static_cast<const int32_t*>(h), N, k, hmin, hspan, memo, first_row);
 }
 
 int launch_coin_collect(hipStream_t s, int32_t* first_row, int64_t total, int k, int32_t hspan, int32_t* keys,
@@ -272,17 +350,27 @@ int launch_coin_draw(hipStream_t s, const int32_t* sorted_vals, const unsigned i
     return kstatus("cube.hip");
 }
 
-int launch_coin_vertex(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
-                       const int32_t* memo, int32_t* vertex) {
+template <typename T>
+static int launch_coin_vertex_t(hipStream_t s, const T* h, int64_t N, int k, int32_t hmin, int32_t hspan,
+                                const int32_t* memo, int32_t* vertex) {
     if ((int64_t)k * hspan <= CF_LDS_MAX && k <= CF_KMAX) {
-        const size_t lds = (size_t)k * hspan * 4;
-        hipLaunchKernelGGL(coin_vertex_lds_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 2048)), dim3(256),
-                           lds, s, h, N, k, hmin, hspan, memo, vertex);
+        const size_t lds = (size_t)((k * hspan + 3) & ~3) * 4 + 4 * 64 * (size_t)k * sizeof(T);
+        const int pf = (k * (int)sizeof(T) + 15) / 16;
+        const dim3 grid((unsigned)std::min<int64_t>((N + 255) / 256, 2048));
+#define CF_VTX(P) hipLaunchKernelGGL((coin_vertex_lds_kernel<T, P>), grid, dim3(256), lds, s, h, N, k, hmin, hspan, memo, vertex)
+        if (pf <= 1) CF_VTX(1); else if (pf <= 2) CF_VTX(2); else if (pf <= 4) CF_VTX(4); else CF_VTX(8);
+#undef CF_VTX
         return kstatus("cube.hip");
     }
-    hipLaunchKernelGGL(coin_vertex_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 8192)), dim3(256), 0, s, h, N,
-                       k, hmin, hspan, memo, vertex);
+    hipLaunchKernelGGL(coin_vertex_kernel<T>, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 8192)), dim3(256), 0, s, h,
+                       N, k, hmin, hspan, memo, vertex);
     return kstatus("cube.hip");
+}
+
+int launch_coin_vertex(hipStream_t s, const void* h, bool h16, int64_t N, int k, int32_t hmin, int32_t hspan,
+                       const int32_t* memo, int32_t* vertex) {
+    return h16 ? launch_coin_vertex_t(s, static_cast<const int16_t*>(h), N, k, hmin, hspan, memo, vertex)
+               : launch_coin_vertex_t(s, static_cast<const int32_t*>(h), N, k, hmin, hspan, memo, vertex);
 }
 
 // Imported coins (sharded builds): memo[off[i]] = bit[i].

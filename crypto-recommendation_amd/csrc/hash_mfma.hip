@@ -48,6 +48,7 @@ struct HashMfmaArgs {
     int L, k, LK, LKpad;
     BucketDiv bdiv;
     int32_t* out_h;          // LSH euclidean: tuples [N][LK]; cube euclidean: h [N][k]; cube cosine: vertex [N]
+    int h16;                 // cube euclidean: h as int16 (saturated; the range in mm is the true one)
     int32_t* out_phi;        // LSH: [N][L] (may be null)
     int32_t* out_bucket;     // LSH: [N][L] (may be null)
     int32_t* mm;             // cube euclidean: [0] min h, [1] max h (atomics; pre-set by the caller)
@@ -56,6 +57,10 @@ struct HashMfmaArgs {
     int64_t seg_rows;
     unsigned long long* stats;
 };
+
+// int16 h (cube euclidean): values outside the range saturate; the caller sees
+// the true range in mm and hashes again as int32 then.
+__device__ inline int16_t h_sat16(int32_t v) { return (int16_t)min(32767, max(-32768, v)); }
 
 template <int MODE>
 __global__ __launch_bounds__(64 * HMF_W, HMF_BPC) void hash_mfma_kernel(HashMfmaArgs a) {
@@ -218,11 +223,18 @@ __global__ __launch_bounds__(64 * HMF_W, HMF_BPC) void hash_mfma_kernel(HashMfma
         const int npts = (int)min((int64_t)32, a.N - tile * 32);
         const int64_t r0 = tile * 32;
         if ((MODE == HM_LSH_EUCLID && !k4) || MODE == HM_CUBE_EUCLID_H) {
-            if (a.out_h)
+            if (MODE == HM_CUBE_EUCLID_H && a.h16) {
+                int16_t* o16 = reinterpret_cast<int16_t*>(a.out_h) + r0 * LK;
+                for (int e = lane; e < npts * LK; e += 64) {
+                    const int p = e / LK, f = e - p * LK;
+                    o16[e] = h_sat16(lv[p * HMF_VS + f]);
+                }
+            } else if (a.out_h) {
                 for (int e = lane; e < npts * LK; e += 64) {
                     const int p = e / LK, f = e - p * LK;
                     a.out_h[r0 * LK + e] = lv[p * HMF_VS + f];
                 }
+            }
         }
         if (MODE == HM_LSH_EUCLID && !k4) {
             for (int e = lane; e < npts * L; e += 64) {
@@ -337,7 +349,10 @@ __global__ __launch_bounds__(HMF_FIX_THREADS) void hash_mfma_fix_kernel(HashMfma
             const int32_t v = hmf_exact<EUCLID>(xrow, pt, a.LKpad, f, EUCLID ? (double)a.tv[f] : 0.0, a.w,
                                                 a.pnorm[f], a.stats);
             if (MODE == HM_LSH_EUCLID || MODE == HM_CUBE_EUCLID_H) {
-                if (a.out_h) a.out_h[row * LK + f] = v;
+                if (MODE == HM_CUBE_EUCLID_H && a.h16)
+                    reinterpret_cast<int16_t*>(a.out_h)[row * LK + f] = h_sat16(v);
+                else if (a.out_h)
+                    a.out_h[row * LK + f] = v;
                 if (MODE == HM_CUBE_EUCLID_H) { atomicMin(a.mm, v); atomicMax(a.mm + 1, v); }
             }
             bits |= (uint32_t)v << f;
@@ -382,7 +397,7 @@ __global__ __launch_bounds__(HMF_FIX_THREADS) void hash_mfma_fix_kernel(HashMfma
 
 int launch_hash_mfma(hipStream_t s, int mode, const float* X, int64_t N, const HashMfmaParams& p, int32_t* out_h,
                      int32_t* out_phi, int32_t* out_bucket, int32_t* mm, unsigned long long* list, int64_t list_cap,
-                     int32_t* seg_counts, int seg_cap, unsigned long long* stats) {
+                     int32_t* seg_counts, int seg_cap, unsigned long long* stats, int h16) {
     if (N <= 0) return 0;
     if (p.d != FU_D || p.LK > 32 || p.LK < 1 || !p.Vh || !p.Vl || !list || !seg_counts) {
         set_error("launch_hash_mfma: needs d = 128, 1 <= L*k <= 32 and the split image");
@@ -399,7 +414,7 @@ int launch_hash_mfma(hipStream_t s, int mode, const float* X, int64_t N, const H
     HashMfmaArgs a;
     a.X = X; a.N = N; a.Vh = p.Vh; a.Vl = p.Vl; a.tv = p.t; a.pnorm = p.pnorm; a.v1 = p.v1; a.rv = p.r; a.PT = p.PT;
     a.w = p.w; a.L = p.L; a.k = p.k; a.LK = p.LK; a.LKpad = p.LKpad; a.bdiv = make_bucket_div(p.nb);
-    a.out_h = out_h; a.out_phi = out_phi; a.out_bucket = out_bucket; a.mm = mm;
+    a.out_h = out_h; a.h16 = mode == HM_CUBE_EUCLID_H && h16; a.out_phi = out_phi; a.out_bucket = out_bucket; a.mm = mm;
     a.list = list; a.seg_counts = seg_counts; a.stats = stats;
     a.seg_rows = (int64_t)HMF_W * 32 * ((ntiles + (int64_t)nblk * HMF_W - 1) / ((int64_t)nblk * HMF_W));
     if (nblk > seg_cap || (int64_t)nblk * a.seg_rows > list_cap) {

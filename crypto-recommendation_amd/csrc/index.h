@@ -45,8 +45,10 @@ struct lshkm_ctx_s;
 namespace lshkm {
 // Hashing of a batch on the split-f16 MFMA kernel where it applies, else the
 // fp64 kernel (api_index.cpp).
+// h16 (cube euclidean): in, int16 h wanted; out, whether int16 was written
+// (only the MFMA kernel writes it).
 int hash_rows(lshkm_ctx_s* ctx, int mode, Pts X, int64_t N, const ProjTable& pj, int64_t nb, int32_t* out_h,
-              int32_t* out_phi, int32_t* out_bucket, int32_t* mm);
+              int32_t* out_phi, int32_t* out_bucket, int32_t* mm, bool* h16 = nullptr);
 
 }  // namespace lshkm
 

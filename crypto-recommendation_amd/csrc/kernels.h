@@ -69,7 +69,7 @@ struct HashMfmaParams {
 // list / seg_counts: per-block lists of the uncertified rows (workspace).
 int launch_hash_mfma(hipStream_t s, int mode, const float* X, int64_t N, const HashMfmaParams& p, int32_t* out_h,
                      int32_t* out_phi, int32_t* out_bucket, int32_t* mm, unsigned long long* list, int64_t list_cap,
-                     int32_t* seg_counts, int seg_cap, unsigned long long* stats);
+                     int32_t* seg_counts, int seg_cap, unsigned long long* stats, int h16 = 0);
 
 // Lloyd assignment (assign.hip).
 struct AssignWorkspace {
@@ -149,13 +149,14 @@ int launch_cube_query(hipStream_t s, const int32_t* qvert, int64_t nq, const int
 
 // Hypercube coins (cube.hip).
 int launch_h_minmax(hipStream_t s, const int32_t* h, int64_t n, int32_t* mm_dev);
-int launch_coin_first(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
+// h: int32 [N][k], or int16 when h16 (the hash kernel's narrow output).
+int launch_coin_first(hipStream_t s, const void* h, bool h16, int64_t N, int k, int32_t hmin, int32_t hspan,
                       const int32_t* memo, int32_t* first_row);
 int launch_coin_collect(hipStream_t s, int32_t* first_row, int64_t total, int k, int32_t hspan, int32_t* keys,
                         int32_t* vals, unsigned int* count);
 int launch_coin_draw(hipStream_t s, const int32_t* sorted_vals, const unsigned int* count, int32_t hmin, int32_t hspan,
                      int32_t* memo, uint32_t* state);
-int launch_coin_vertex(hipStream_t s, const int32_t* h, int64_t N, int k, int32_t hmin, int32_t hspan,
+int launch_coin_vertex(hipStream_t s, const void* h, bool h16, int64_t N, int k, int32_t hmin, int32_t hspan,
                        const int32_t* memo, int32_t* vertex);
 int launch_memo_rehome(hipStream_t s, const int32_t* old_memo, int32_t old_min, int32_t old_span, int32_t* new_memo,
                        int32_t new_min, int32_t new_span, int k);

@@ -153,6 +153,40 @@ def test_cube_large_and_continued_coins_vs_oracle(ctx):
         assert np.array_equal(out[ptr[q]:ptr[q + 1]], exp), q
 
 
+@pytest.mark.parametrize("k,N", [(7, 5001), (13, 777), (14, 64 * 300 + 63), (3, 1)])
+def test_cube_narrow_h_odd_shapes_vs_oracle(ctx, k, N):
+    # int16 h with odd k / ragged row counts through the staged row loads
+    d, w = 128, 2.0
+    V, t, st = lshkm.params_cube_euclidean(k * 31 + N, k, d, w)
+    Xh = oracle.synth(N + k, N, d)
+    cube = lshkm.Cube(ctx, "euclidean", d, k, w, V=V, t=t, rng_state=st)
+    cube.build(to_dev(ctx, Xh))
+    memo = oracle.CoinMemo(k, st)
+    ov, _ = memo.apply(oracle.cube_h(Xh, V, t, np.float32(w)))
+    rp, idx = cube.buckets()
+    orp, oidx = oracle.bucket_csr(ov[:, None], 1 << k)
+    assert np.array_equal(rp, orp[0]) and np.array_equal(idx, oidx[0])
+    assert cube.memo()[3] == memo.state.value
+
+
+def test_cube_wide_h_range_vs_oracle(ctx):
+    # h beyond int16 (w = 1e-4): the narrow h output saturates, the batch is
+    # hashed again as int32; vertices, buckets and the coin stream stay exact
+    N, d, k, w = 3000, 128, 6, 1e-4
+    V, t, st = lshkm.params_cube_euclidean(77, k, d, w)
+    Xh = oracle.synth(0xB16, N, d)
+    cube = lshkm.Cube(ctx, "euclidean", d, k, w, V=V, t=t, rng_state=st)
+    cube.build(to_dev(ctx, Xh))
+    hh = oracle.cube_h(Xh, V, t, np.float32(w))
+    assert np.abs(hh).max() > 32767
+    memo = oracle.CoinMemo(k, st, hmin=int(hh.min()), hspan=int(hh.max() - hh.min()) + 1)
+    ov, _ = memo.apply(hh)
+    rp, idx = cube.buckets()
+    orp, oidx = oracle.bucket_csr(ov[:, None], 1 << k)
+    assert np.array_equal(rp, orp[0]) and np.array_equal(idx, oidx[0])
+    assert cube.memo()[3] == memo.state.value
+
+
 def test_cube_sharded_build_matches_single(ctx):
     # shards export unseen (f, h), merge in global first-occurrence
     # order, draw on the host, import, build -> per-shard vertices, memo and
