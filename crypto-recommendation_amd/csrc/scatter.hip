@@ -46,24 +46,59 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const int32_t* __restri
     for (int b = threadIdx.x; b < nbins; b += RS_THREADS) hist[(size_t)b * nblocks + blockIdx.x] = h[b];
 }
 
-// Exclusive scan of M uint32 in place, one block of 1024 threads.
+// Exclusive scan of M uint32 in place, one block of 1024 threads: thread t
+// owns the contiguous segment [t * seg, (t + 1) * seg). For seg <= 64 (M <=
+// 65536) the segment is loaded into registers with all its loads in flight at
+// once (a loop of dependent-looking loads ran ~60 serial trips: 44 us for the
+// C2 build's 31K counters); the 1024 partials are scanned per wave by shuffles,
+// then across the 16 waves.
+constexpr int RS_SEG = 64;
+__device__ inline uint32_t rs_block_exclusive(uint32_t s, uint32_t* wsum) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o);
+        if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    if (t < 64) {
+        const uint32_t x = t < 16 ? wsum[t] : 0u;
+        uint32_t y = x;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t u = __shfl_up(y, o);
+            if (lane >= o) y += u;
+        }
+        if (t < 16) wsum[16 + t] = y - x;              // exclusive wave offsets
+    }
+    __syncthreads();
+    return wsum[16 + w] + inc - s;
+}
 __global__ __launch_bounds__(1024) void rs_scan(uint32_t* __restrict__ a, int64_t M, int64_t a_ts) {
-    __shared__ uint32_t part[1024];
+    __shared__ uint32_t wsum[32];
     a += blockIdx.y * a_ts;
     const int t = threadIdx.x;
     const int64_t seg = (M + 1023) / 1024;
     const int64_t lo = t * seg, hi = min(M, lo + seg);
+    if (seg <= RS_SEG) {                               // block-uniform
+        uint32_t v[RS_SEG];
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < RS_SEG; j++) {
+            v[j] = lo + j < hi ? a[lo + j] : 0u;
+            s += v[j];
+        }
+        uint32_t run = rs_block_exclusive(s, wsum);
+#pragma unroll
+        for (int j = 0; j < RS_SEG; j++)
+            if (lo + j < hi) { a[lo + j] = run; run += v[j]; }
+        return;
+    }
     uint32_t s = 0;
     for (int64_t i = lo; i < hi; i++) s += a[i];
-    part[t] = s;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {          // Hillis-Steele over the 1024 partials
-        const uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = t ? part[t - 1] : 0u;
+    uint32_t run = rs_block_exclusive(s, wsum);
     for (int64_t i = lo; i < hi; i++) { const uint32_t v = a[i]; a[i] = run; run += v; }
 }
 
@@ -97,7 +132,7 @@ __global__ __launch_bounds__(1024) void rs_chunk_sum(const uint32_t* __restrict_
 }
 __global__ __launch_bounds__(1024) void rs_chunk_scan(uint32_t* __restrict__ a, int64_t M, const uint32_t* __restrict__ off,
                                                       int64_t a_ts, int64_t p_ts) {
-    __shared__ uint32_t sh[1024];
+    __shared__ uint32_t wsum[32];
     a += blockIdx.y * a_ts;
     off += blockIdx.y * p_ts;
     const int t = threadIdx.x;
@@ -105,15 +140,7 @@ __global__ __launch_bounds__(1024) void rs_chunk_scan(uint32_t* __restrict__ a, 
     uint32_t v[8], s = 0;
 #pragma unroll
     for (int u = 0; u < 8; u++) { v[u] = base + u < M ? a[base + u] : 0u; s += v[u]; }
-    sh[t] = s;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const uint32_t w = t >= o ? sh[t - o] : 0u;
-        __syncthreads();
-        sh[t] += w;
-        __syncthreads();
-    }
-    uint32_t run = off[blockIdx.x] + (t ? sh[t - 1] : 0u);
+    uint32_t run = off[blockIdx.x] + rs_block_exclusive(s, wsum);
 #pragma unroll
     for (int u = 0; u < 8; u++)
         if (base + u < M) { a[base + u] = run; run += v[u]; }
