@@ -46,13 +46,14 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const int32_t* __restri
     for (int b = threadIdx.x; b < nbins; b += RS_THREADS) hist[(size_t)b * nblocks + blockIdx.x] = h[b];
 }
 
-// Exclusive scan of M uint32 in place, one block of 1024 threads: thread t
-// owns the contiguous segment [t * seg, (t + 1) * seg). For seg <= 64 (M <=
-// 65536) the segment is loaded into registers with all its loads in flight at
-// once (a loop of dependent-looking loads ran ~60 serial trips: 44 us for the
-// C2 build's 31K counters); the 1024 partials are scanned per wave by shuffles,
-// then across the 16 waves.
-constexpr int RS_SEG = 64;
+// Exclusive scan of M uint32 in place, one block of 1024 threads. For M <=
+// 32768 the array is read as rows of 1024 (thread t: column t, all its loads
+// in flight, each instruction coalesced): every row is scanned per wave by
+// shuffles, the (row, wave) totals get one block scan, and the results are
+// written back the same way. (A thread-per-contiguous-segment form touches 64
+// cache lines per load instruction on the handful of CUs a few-table scan
+// uses: 27-44 us for the C2 build's 5 x 31K counters.)
+constexpr int RS_SEG = 32;
 __device__ inline uint32_t rs_block_exclusive(uint32_t s, uint32_t* wsum) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t inc = s;
@@ -74,42 +75,60 @@ __device__ inline uint32_t rs_block_exclusive(uint32_t s, uint32_t* wsum) {
         if (t < 16) wsum[16 + t] = y - x;              // exclusive wave offsets
     }
     __syncthreads();
-    return wsum[16 + w] + inc - s;
+    const uint32_t r = wsum[16 + w] + inc - s;
+    __syncthreads();                                   // wsum reusable on return
+    return r;
 }
 __global__ __launch_bounds__(1024) void rs_scan(uint32_t* __restrict__ a, int64_t M, int64_t a_ts) {
     __shared__ uint32_t wsum[32];
+    __shared__ uint32_t rw[RS_SEG * 16];               // (row, wave) offsets
     a += blockIdx.y * a_ts;
-    const int t = threadIdx.x;
-    const int64_t seg = (M + 1023) / 1024;
-    const int64_t lo = t * seg, hi = min(M, lo + seg);
-    if (seg <= RS_SEG) {                               // block-uniform
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (M <= (int64_t)RS_SEG * 1024) {                 // block-uniform
+        const int rows = (int)((M + 1023) >> 10);
         uint32_t v[RS_SEG];
-        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < RS_SEG; j++) v[j] = j < rows && ((int64_t)j << 10) + t < M ? a[((int64_t)j << 10) + t] : 0u;
+        // per row: wave-exclusive prefix in v[j], the wave's row total to rw
+#pragma unroll
+        for (int j = 0; j < RS_SEG; j++) {               // branch-free: v stays in registers
+            uint32_t inc = v[j];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(inc, o);
+                if (lane >= o) inc += u;
+            }
+            if (lane == 63 && j < rows) rw[j * 16 + w] = inc;
+            v[j] = inc - v[j];
+        }
+        __syncthreads();
+        const uint32_t tot = t < rows * 16 ? rw[t] : 0u;
+        const uint32_t ex = rs_block_exclusive(tot, wsum);
+        if (t < rows * 16) rw[t] = ex;
+        __syncthreads();
 #pragma unroll
         for (int j = 0; j < RS_SEG; j++) {
-            v[j] = lo + j < hi ? a[lo + j] : 0u;
-            s += v[j];
+            const int64_t i = ((int64_t)j << 10) + t;
+            if (j < rows && i < M) a[i] = rw[j * 16 + w] + v[j];
         }
-        uint32_t run = rs_block_exclusive(s, wsum);
-#pragma unroll
-        for (int j = 0; j < RS_SEG; j++)
-            if (lo + j < hi) { a[lo + j] = run; run += v[j]; }
         return;
     }
+    const int64_t seg = (M + 1023) / 1024;
+    const int64_t lo = t * seg, hi = min(M, lo + seg);
     uint32_t s = 0;
     for (int64_t i = lo; i < hi; i++) s += a[i];
     uint32_t run = rs_block_exclusive(s, wsum);
-    for (int64_t i = lo; i < hi; i++) { const uint32_t v = a[i]; a[i] = run; run += v; }
+    for (int64_t i = lo; i < hi; i++) { const uint32_t x = a[i]; a[i] = run; run += x; }
 }
 
 // Large histograms (the cube's 2^7 bins x N / 4096 tiles: 312K counters at
 // N = 10M, 0.35-0.54 ms in the one-block scan): reduce-then-scan over
 // RS_SC-element chunks, in place; the chunk totals go through rs_scan.
 constexpr int RS_SC = 8192;
-// up to this many counters the one-block scan (1024 threads, <= 64 each) beats
-// the reduce-then-scan trio's two extra launches (the C2 build: 7-bit digits x
-// 245 tiles x 5 tables)
-constexpr int64_t RS_ONE_SCAN = 65536;
+// up to this many counters the one-block scan (32 coalesced rows of 1024)
+// beats the reduce-then-scan trio's two extra launches (the C2 build: 7-bit
+// digits x 245 tiles x 5 tables)
+constexpr int64_t RS_ONE_SCAN = 32768;
 __global__ __launch_bounds__(1024) void rs_chunk_sum(const uint32_t* __restrict__ a, int64_t M, uint32_t* __restrict__ part,
                                                      int64_t a_ts, int64_t p_ts) {
     __shared__ uint32_t red[1024];
