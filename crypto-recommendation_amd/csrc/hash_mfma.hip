@@ -28,7 +28,11 @@
 namespace lshkm {
 
 constexpr int HMF_W = 4;        // waves per block
-constexpr int HMF_BPC = 4;      // blocks per CU (<= 128 VGPRs, 139 KiB of LDS)
+// blocks per CU: 2 (~160 VGPRs) so a wave's 16 row loads can all be in flight
+// before its first MFMA (at 4 blocks the 128-VGPR cap made the scheduler issue
+// them pair by pair next to each step: 8 serial trips per tile; C4 build 1.87
+// -> 1.76 ms, C2 0.353 -> 0.337 ms)
+constexpr int HMF_BPC = 2;
 constexpr int HMF_VS = 33;      // per-wave value tile [32 points][33] int32
 constexpr int hmf_lds_bytes() {
     return 2 * 32 * FU_RS * 2 + 4 * 32 * 4 + HMF_W * 32 * HMF_VS * 4 + 16;
@@ -122,6 +126,7 @@ __global__ __launch_bounds__(64 * HMF_W, HMF_BPC) void hash_mfma_kernel(HashMfma
                 xf[8 * s + 4] = p1.x; xf[8 * s + 5] = p1.y; xf[8 * s + 6] = p1.z; xf[8 * s + 7] = p1.w;
             }
         }
+        __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads ahead of the MFMA steps
         float2v n2a = {0.f, 0.f}, n2b = {0.f, 0.f}, r2 = {0.f, 0.f};
         floatx16 tot;
 #pragma unroll
