@@ -43,6 +43,9 @@ const char* lshkm_version(void) { return "lshkm-gfx950 0.1"; }
 
 int lshkm_ctx_create(int device, lshkm_ctx* out) {
     LSHKM_CHECK(out, LSHKM_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    // the pow contract (gpow2.h), once per process, before any device work
+    if (const int rc = pow_contract_check()) return rc;
     int n = 0;
     LSHKM_HIP(hipGetDeviceCount(&n));
     LSHKM_CHECK(device >= 0 && device < n, LSHKM_ERR_ARG, "device out of range");

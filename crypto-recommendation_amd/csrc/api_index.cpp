@@ -377,7 +377,7 @@ static int cube_vertices_impl(lshkm_cube cube, Pts X, int64_t N, int32_t* vertex
         // the count cannot pass the one-workgroup sort's limit: it stays on the
         // device (sort and draw read it there), no host round trip
         if ((rc = cube_unseen_impl(cube, h, h16, N, nullptr))) return rc;
-        if ((rc = sort_pairs_small(s, slot<int32_t>(ctx, WS_SIZES), slot<int32_t>(ctx, WS_COFF), 0,
+        if ((rc = sort_pairs_small(s, slot<int32_t>(ctx, WS_SIZES), slot<int32_t>(ctx, WS_COFF), bound,
                                    slot<int32_t>(ctx, WS_KLIST), slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>())) ||
             (rc = launch_coin_draw(s, slot<int32_t>(ctx, WS_KCNT), cube->cnt.as<unsigned int>(), cube->hmin, cube->hspan,
                                    cube->memo.as<int32_t>(), cube->rng_d.as<uint32_t>()))) { LSHKM_LAUNCH_CHECK(); return rc; }

@@ -19,6 +19,27 @@ static int read_i64(lshkm_ctx ctx, const int64_t* dev, int64_t* host) {
     return 0;
 }
 
+// Host vectors handed to hipMemcpyAsync must outlive the copy: declared after
+// them, this waits for the stream on every exit path (its destructor runs
+// before theirs).
+struct StreamSyncOnExit {
+    hipStream_t s;
+    ~StreamSyncOnExit() { (void)hipStreamSynchronize(s); }
+};
+
+// The users' clusters on the host, each in [0, K): the reference indexes
+// clusters[user.getCluster()] (main.cpp:261, :366), so an ID outside the
+// clusters is a caller error here, not an empty neighbourhood.
+static int read_ucl(lshkm_ctx ctx, const int32_t* ucl, int64_t nq, int K, std::vector<int32_t>& hu) {
+    hu.resize((size_t)nq);
+    if (nq == 0) return 0;
+    LSHKM_HIP(hipMemcpyAsync(hu.data(), ucl, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    for (int64_t q = 0; q < nq; q++)
+        LSHKM_CHECK(hu[q] >= 0 && hu[q] < K, LSHKM_ERR_ARG, "ucl holds a cluster ID outside [0, K)");
+    return 0;
+}
+
 extern "C" {
 
 int lshkm_p_closest(lshkm_ctx ctx, const double* X, int64_t N, int d, const double* U, int64_t nq,
@@ -126,7 +147,12 @@ static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
         }
     }
     std::vector<int64_t> hc((size_t)K + 1);
+    std::vector<int32_t> hu;
     int64_t total = 0;
+    {
+        int rc;
+        if ((rc = read_ucl(ctx, ucl, nq, K, hu))) return rc;
+    }
     LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
@@ -167,17 +193,17 @@ static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
 static int shard_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
                          std::vector<int64_t>& soff, std::vector<int32_t>* hu_out = nullptr) {
     std::vector<int64_t> hc((size_t)K + 1);
-    std::vector<int32_t> hu((size_t)nq);
+    std::vector<int32_t> hu;
+    int rc;
+    if ((rc = read_ucl(ctx, ucl, nq, K, hu))) return rc;
     LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipMemcpyAsync(hu.data(), ucl, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     bool ok = hc[0] == 0;
     for (int c = 0; c < K && ok; c++) ok = hc[c + 1] >= hc[c];
     LSHKM_CHECK(ok && hc[K] <= N, LSHKM_ERR_ARG, "bad cluster CSR");
     soff.assign((size_t)nq + 1, 0);
     for (int64_t q = 0; q < nq; q++) {
-        const int c = hu[q];
-        const int64_t n = (c >= 0 && c < K) ? hc[c + 1] - hc[c] : 0;
+        const int64_t n = hc[hu[q] + 1] - hc[hu[q]];
         LSHKM_CHECK(n < (1ll << 31), LSHKM_ERR_ARG, "a cluster of 2^31 members or more");
         soff[q + 1] = soff[q] + n;
     }
@@ -193,6 +219,7 @@ static int cluster_sims_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_HIP(hipSetDevice(ctx->device));
     std::vector<int64_t> soff;
+    const StreamSyncOnExit sync_guard{ctx->stream};   // soff is copied before return
     int rc;
     if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff))) return rc;
     *total_host = soff[nq];
@@ -203,7 +230,7 @@ static int cluster_sims_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64
                                        (unsigned long long*)ctx->stats.p + STAT_REC_SOFT)))
             return rc;
     }
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // soff (host vector) is copied before return
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     return 0;
 }
 
@@ -221,12 +248,14 @@ static int cluster_chain_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     if (nq == 0) return 0;
     LSHKM_HIP(hipSetDevice(ctx->device));
     int64_t total = 0;
+    int rc;
+    std::vector<int32_t> hu;
+    if ((rc = read_ucl(ctx, ucl, nq, K, hu))) return rc;
     LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     LSHKM_CHECK(total >= 0 && (total == 0 || unk_idx), LSHKM_ERR_ARG, "bad unknown-index lists");
     Buf &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
     const size_t M = (size_t)(total > 0 ? total : 1);
-    int rc;
     if (out && ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M)))) return rc;
     if ((rc = launch_rc_shard_chain(ctx->stream, X, x_mean, d, crow, crows, K, nq, ucl, u_mean, unk_ptr, unk_idx, soff,
                                     sims, carry_main, carry_abs, carry_cnt, out ? nullptr : main_out,
@@ -273,6 +302,8 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     LSHKM_HIP(hipSetDevice(ctx->device));
     std::vector<int64_t> soff, hup, toff;
     std::vector<int32_t> hu;                       // the users' clusters (host)
+    std::vector<int32_t> pack;                     // the cluster-major work list (host side of its copy)
+    const StreamSyncOnExit sync_guard{ctx->stream};   // the host vectors are copied before return
     int rc;
     if ((rc = terms_offsets(ctx, crow, K, N, ucl, nq, unk_ptr, soff, hup, toff, &hu))) return rc;
     *total_host = soff[nq];
@@ -308,7 +339,6 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
         }
         gptr.push_back((int32_t)byc.size());
         const size_t nG = gcl.size();
-        std::vector<int32_t> pack;
         pack.reserve(3 * nG + 2 + byc.size());
         pack.insert(pack.end(), ioff.begin(), ioff.end());
         pack.insert(pack.end(), gcl.begin(), gcl.end());
@@ -326,7 +356,7 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
                                   (unsigned long long*)ctx->stats.p + STAT_REC_SOFT, unorm, &groups)))
             return rc;
     }
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the host offsets are copied before return
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     return 0;
 }
 

@@ -23,9 +23,11 @@
 // general doubles, none of the exactly-representable squares; measured worst
 // case of the algorithm: 0.0085 ulp, tests/pow2_check.cpp).
 // Checked on the host against the process's real pow on ~2e9 inputs, near
-// midpoints, ties, subnormals and the special ranges (tests/pow2_check.cpp), and
-// at run time by lshkm_pow_selfcheck() (api.cpp) against the running process's
-// pow; the device path against host pow by tests/test_gpu_pow2.py.
+// midpoints, ties, subnormals and the special ranges (tests/pow2_check.cpp); at
+// run time, once per process, lshkm_ctx_create runs lshkm_pow_selfcheck()
+// (pow2.hip) against the running process's pow and refuses to create a context
+// (LSHKM_ERR_UNSUPPORTED) when they differ; the device path against host pow by
+// tests/test_gpu_pow2.py.
 #pragma once
 #include <stdint.h>
 #include <string.h>

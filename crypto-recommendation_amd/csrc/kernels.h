@@ -122,7 +122,12 @@ int launch_add_counters(hipStream_t s, unsigned long long* stats, int n, const i
 // Stable bucket scatter (scatter.hip).
 size_t sort_scratch_bytes(int64_t N, int64_t range, int T = 1);
 // Distinct int32 keys, n <= 8192: one-workgroup bitonic sort of (key, val) pairs.
-// n_dev: the count is read on the device instead (the caller bounds it by 8192).
+// n_dev: the count is read on the device instead; n is then the caller's bound on
+// it (refused past 8192).
+// The pow contract (pow2.hip): lshkm_pow_selfcheck once per process; 0, or
+// LSHKM_ERR_UNSUPPORTED with the error set when this process's pow differs.
+int pow_contract_check();
+
 int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, int64_t n, int32_t* keys_out,
                      int32_t* vals_out, const unsigned int* n_dev = nullptr);
 int stable_sort_by_key(hipStream_t s, const int32_t* keys, int64_t kstride, const int32_t* vals, int64_t N,

@@ -6,6 +6,8 @@
 
 #include <cmath>
 #include <cstdint>
+#include <mutex>
+#include <string>
 
 #include "../../include/lshkm.h"
 #include "common.h"
@@ -31,6 +33,30 @@ using namespace lshkm;
 
 // the process's pow, called for real (never folded to x*x)
 static double (*volatile g_libm_pow)(double, double) = pow;
+
+// Test build only (LSHKM_POW_HOST=rn): stand in for a host whose libm squares
+// correctly rounded (another glibc variant, musl, ...), to exercise the
+// refusal path of lshkm_ctx_create.
+static double pow_rn(double x, double y) { return y == 2.0 ? x * x : pow(x, y); }
+
+namespace lshkm {
+// The pow contract, checked once per process (lshkm_ctx_create): 0 when the
+// restatement matches this process's pow on the self-check's inputs.
+int pow_contract_check() {
+    static std::once_flag once;
+    static int64_t bad = -1, tested = 0;
+    std::call_once(once, [] {
+        if (test_switch("LSHKM_POW_HOST", "rn")) g_libm_pow = pow_rn;
+        if (lshkm_pow_selfcheck(&bad, &tested) != 0) bad = -1;
+    });
+    if (bad == 0) return 0;
+    set_error("this process's pow(x, 2) differs from the device restatement of glibc 2.35's __pow_fma on " +
+              std::to_string(bad) + " of " + std::to_string(tested) +
+              " self-check inputs (lshkm_pow_selfcheck): the reference's distances and similarities on this host "
+              "cannot be reproduced bit for bit (csrc/gpow2.h)");
+    return LSHKM_ERR_UNSUPPORTED;
+}
+}  // namespace lshkm
 
 extern "C" {
 

@@ -14,6 +14,7 @@
 // the first P+1 are equal (a tie touching the first P positions), hands the user
 // to lomuto_sort, which replays the reference's quicksort exactly (one lane per
 // user; disjoint subarrays, so the order they are sorted in does not matter).
+#include "../../include/lshkm.h"
 #include "common.h"
 #include "kernels.h"
 #include "exact.h"
@@ -1029,10 +1030,17 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
                     unsigned long long* soft_count, double* unorm, const RcGroups* groups) {
     if (nq <= 0 || total <= 0) return 0;
     const int elem = X.f64 ? 8 : 4;
-    if (((int64_t)d * elem) % 8 != 0) return -1;
     const int stride8 = rc_terms_stride8(d, elem);
     const size_t lds = (size_t)(CT_STAGE + 1) * stride8 * 8;
-    if (2 * lds > 160 * 1024) return -1;
+    // every check before the first launch: a refused call enqueues nothing
+    if (((int64_t)d * elem) % 8 != 0 || 2 * lds > 160 * 1024) {
+        set_error("launch_rc_terms: rows must be a multiple of 8 B and stage in LDS");
+        return LSHKM_ERR_ARG;
+    }
+    if (!groups || groups->nitems <= 0) {
+        set_error("launch_rc_terms: empty cluster-major work list for a nonzero member total");
+        return LSHKM_ERR_ARG;
+    }
     hipLaunchKernelGGL(rc_member_map_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0, s, nq, soff, ucl,
                        crow, crows, mem_q, mem_r);
     if (X.f64)
@@ -1040,7 +1048,6 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
     else
         hipLaunchKernelGGL(rc_user_norm_kernel<float>, dim3(gsz(nq, 256, 1024)), dim3(256), 0, s, U.f(), nq, d, unorm);
     if (hipMemsetAsync(fix_count, 0, 8, s) != hipSuccess) return kstatus("rc_terms (memset)");
-    if (!groups || groups->nitems <= 0) return -1;
     const dim3 cgrid((unsigned)std::min<int64_t>(groups->nitems, 65536));
     if (X.f64)
         hipLaunchKernelGGL(rc_terms_cl_kernel<double>, cgrid, dim3(64), lds, s, X.d(), x_mean, d, U.d(), groups->ioff,

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(1024) void sort_pairs_small_kernel(const int32_t* _
                                                                 int32_t* __restrict__ keys_out,
                                                                 int32_t* __restrict__ vals_out) {
     __shared__ int32_t sk[SP_MAX], sv[SP_MAX];
-    if (n_dev) {                        // count left on the device (<= SP_MAX by the caller's bound)
+    if (n_dev) {                        // count left on the device (<= SP_MAX: the host checks the caller's bound)
         n = (int)min(*n_dev, (unsigned int)SP_MAX);
         for (P = 1; P < n; P <<= 1) {}
     }
@@ -290,9 +290,15 @@ __global__ __launch_bounds__(1024) void sort_pairs_small_kernel(const int32_t* _
     }
 }
 
+// n_dev: the count is read on the device; n is then the caller's upper bound on
+// it, checked here (a count past SP_MAX would drop keys silently).
 int sort_pairs_small(hipStream_t s, const int32_t* keys, const int32_t* vals, int64_t n, int32_t* keys_out,
                      int32_t* vals_out, const unsigned int* n_dev) {
     if (n_dev) {
+        if (n > SP_MAX) {
+            set_error("sort_pairs_small: the device count's bound exceeds the one-workgroup sort");
+            return -1;
+        }
         hipLaunchKernelGGL(sort_pairs_small_kernel, dim3(1), dim3(1024), 0, s, keys, vals, 0, 1, n_dev, keys_out, vals_out);
         return kstatus("scatter.hip");
     }

@@ -50,7 +50,10 @@
  *     (and for many exact ties): the device evaluates glibc 2.35's own
  *     algorithm (the x86-64 __pow_fma variant, csrc/gpow2.h) wherever x*x is
  *     not provably the same value. lshkm_pow_selfcheck() compares that
- *     restatement with the running process's pow.
+ *     restatement with the running process's pow; lshkm_ctx_create runs it
+ *     once per process and refuses (LSHKM_ERR_UNSUPPORTED, see
+ *     lshkm_last_error) on a host whose pow differs, since the reference's
+ *     own results on that host could not be reproduced bit for bit.
  *   - One handle per thread; calls on a handle are serialised on its stream.
  */
 #ifndef LSHKM_H
@@ -93,6 +96,9 @@ int lshkm_pow2(lshkm_ctx ctx, const double* x_dev, int64_t n, double* out_dev);
  * = how many differ (0 when the process's libm is the one the restatement
  * follows), *tested_host = inputs tried. */
 int lshkm_pow_selfcheck(int64_t* mismatches_host, int64_t* tested_host);
+/* A context on `device` (gfx950). Fails with LSHKM_ERR_UNSUPPORTED, before any
+ * device work, when this process's pow(x, 2) differs from the restatement
+ * (the pow contract above; checked once per process). */
 int lshkm_ctx_create(int device, lshkm_ctx* out);
 /* Run on a caller-owned hipStream_t (e.g. torch's current stream), used
  * verbatim: NULL is the default (null) stream. A new context uses its own stream. */
@@ -407,8 +413,9 @@ int lshkm_top_n_recom(lshkm_ctx ctx, const double* X_dev, const double* x_mean_d
  * of each user's ascending unknown indexes, values in [0, d)); the reference's
  * quicksort of the predictions (:234-277, ties / NaNs included); out_dev
  * [nq][n_top] = the first n_top unknown indexes, 0-padded like vector::resize.
- * Users whose cluster is empty (or ucl outside [0, K)) get -1 in every slot:
- * main.cpp skips them (:262, :366). X_dev [N][d] pool rows and U_dev [nq][d]
+ * Users whose cluster is empty get -1 in every slot: main.cpp skips them
+ * (:262, :366). A ucl outside [0, K) is LSHKM_ERR_ARG (the reference indexes
+ * clusters[ucl] unchecked; the same holds for the sharded entry points below). X_dev [N][d] pool rows and U_dev [nq][d]
  * users share the element type (for Part A pass the same rows twice). Counter
  * 7 counts the similarities the x87 chain decided. Bit-exact on any rows (the
  * norms' squares are glibc's pow(x, 2)). */

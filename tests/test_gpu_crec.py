@@ -314,3 +314,34 @@ def test_recommend_sharded_row_shapes(ctx, kind, d):
     got = sh.recommend_sharded(lshkm, ctx, dev(ctx, X), dev(ctx, xm), dev(ctx, assign), K, dev(ctx, U), dev(ctx, um),
                                dev(ctx, ucl), dev(ctx, up), dev(ctx, ui), NT).cpu().numpy()
     assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
+
+
+@pytest.mark.parametrize("bad_cl", [-1, 12, 17])
+def test_cluster_ids_outside_k_are_refused(ctx, bad_cl):
+    # the reference indexes clusters[user.getCluster()] unchecked (main.cpp:261,
+    # :366): a ucl outside [0, K) is LSHKM_ERR_ARG in every entry point that
+    # takes one (the single-pass top-N, and the sharded sims / terms phases)
+    N, d, K, nq = 2_000, 128, 12, 40
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((N, d)).astype(np.float32)
+    assign = rng.integers(0, K, size=N).astype(np.int32)
+    crow, crows = oracle.clusters_csr(assign, K)
+    users = rng.choice(N, nq, replace=False)
+    ucl = assign[users].copy()
+    ucl[7] = bad_cl
+    up, ui = unknown_sets(rng, nq, d)
+    Xd, xm = dev(ctx, X), dev(ctx, np.zeros(N))
+    args = (dev(ctx, crow), dev(ctx, crows))
+    with pytest.raises(lshkm.LshkmError, match=r"outside \[0, K\)"):
+        lshkm.cluster_top_n(ctx, Xd, xm, *args, dev(ctx, X[users]), dev(ctx, np.zeros(nq)), dev(ctx, ucl),
+                            dev(ctx, up), dev(ctx, ui), 5)
+    with pytest.raises(lshkm.LshkmError, match=r"outside \[0, K\)"):
+        lshkm.cluster_terms(ctx, Xd, xm, *args, dev(ctx, X[users]), dev(ctx, ucl), dev(ctx, up), dev(ctx, ui))
+    with pytest.raises(lshkm.LshkmError, match=r"outside \[0, K\)"):
+        lshkm.cluster_sims(ctx, Xd, *args, dev(ctx, X[users]), dev(ctx, ucl), dev(ctx, up))
+    # the context stays usable: the same call with the IDs in range matches the oracle
+    ucl[7] = 0
+    want = oracle.cluster_top_n(X, np.zeros(N), crow, crows, X[users], np.zeros(nq), ucl, up, ui, 5)
+    got = lshkm.cluster_top_n(ctx, Xd, xm, *args, dev(ctx, X[users]), dev(ctx, np.zeros(nq)), dev(ctx, ucl),
+                              dev(ctx, up), dev(ctx, ui), 5).cpu().numpy()
+    assert np.array_equal(got, want)

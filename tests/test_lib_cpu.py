@@ -141,3 +141,42 @@ def test_no_gpu_means_loud_failure():
         pytest.skip("a GPU is present")
     with pytest.raises(Exception):
         lshkm.Context(0)
+
+
+_CTX_PROBE = r"""
+import ctypes, sys
+L = ctypes.CDLL(sys.argv[1])
+L.lshkm_last_error.restype = ctypes.c_char_p
+h = ctypes.c_void_p()
+rc = L.lshkm_ctx_create(0, ctypes.byref(h))
+print(rc, L.lshkm_last_error().decode())
+if rc == 0:
+    L.lshkm_ctx_destroy(h)
+"""
+
+
+def _ctx_create_in_child(libname, env_extra):
+    env = dict(os.environ)
+    env.update(env_extra)
+    out = subprocess.run([os.sys.executable, "-c", _CTX_PROBE, os.path.join(PKG, libname)], capture_output=True,
+                         text=True, env=env, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    rc, msg = out.stdout.strip().split(" ", 1) if " " in out.stdout.strip() else (out.stdout.strip(), "")
+    return int(rc), msg
+
+
+def test_ctx_create_enforces_pow_contract():
+    # lshkm_ctx_create runs lshkm_pow_selfcheck once per process, before any
+    # device work, and refuses on a host whose pow(x, 2) is not the one the
+    # device restates (gpow2.h). The test build's LSHKM_POW_HOST=rn stands in
+    # for such a host (a correctly rounded square): refused with
+    # LSHKM_ERR_UNSUPPORTED and the mismatch count, GPU or not.
+    rc, msg = _ctx_create_in_child("liblshkm_test.so", {"LSHKM_POW_HOST": "rn"})
+    assert rc == -4 and "pow(x, 2) differs" in msg, (rc, msg)
+    bad = int(msg.split(" on ")[1].split(" of ")[0])
+    assert bad > 100, msg                          # the self-check's inputs tell pow from x*x
+    # this image's libm: the contract holds; the context then fails only for want
+    # of a GPU here (or succeeds on the GPU box)
+    for lib in ("liblshkm.so", "liblshkm_test.so"):
+        rc, msg = _ctx_create_in_child(lib, {"LSHKM_POW_HOST": "rn"} if lib == "liblshkm.so" else {})
+        assert "pow" not in msg, (lib, rc, msg)    # the product library reads no switch
