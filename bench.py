@@ -50,6 +50,9 @@ DTYPE = ("fp32 points; split-f16 MFMA scores (f32 accumulate); tuples, bucket ID
 # algorithmic bytes per point of the fused pass: 512 B read, 80 B
 # tuples + 20 B bucket IDs + 4 B cluster ID + 8 B distance written
 BYTES_PER_PT = 4 * D + 4 * L_TABLES * K_FUNCS + 4 * L_TABLES + 4 + 8
+DATA = {"grid": "synthetic (include/lshkm_synth.h grid generator: Irwin-Hall(4) on a 2^-15 grid), resident in HBM",
+        "normal": "synthetic (include/lshkm_synth.h normal generator: Irwin-Hall(12), full fp32 mantissas), "
+                  "resident in HBM"}
 
 
 def load_module(name, fname):
@@ -268,6 +271,11 @@ def main():
     ap.add_argument("--workload", choices=["c3", "c5"], default="c3")
     ap.add_argument("--k", type=int, default=None, help="centroids (default 256 for c3, 1024 for c5)")
     ap.add_argument("--no-c5", action="store_true", help="c3: leave out the C5 iteration object")
+    ap.add_argument("--data", choices=["grid", "normal"], default="grid",
+                    help="the rows: include/lshkm_synth.h's 2^-15 grid generator (default) or its full-mantissa "
+                         "normal generator (SURVEY.md §8d)")
+    ap.add_argument("--no-normal-leg", dest="normal_leg", action="store_false",
+                    help="c3 on grid data: leave out the normal_data object (C3 + C5 on full-mantissa rows)")
     ap.add_argument("--recom-users", type=int, default=1024,
                     help="C5: query users per iteration of the recommend step (0: no recommend step)")
     ap.add_argument("--no-exact-dist-line", dest="exact_dist_line", action="store_false",
@@ -313,20 +321,20 @@ def main():
     nb = N_total // BUCKET_DIV
 
     # Resident shard + parameters (untimed).
-    X = ctx.synth(SEED_DATA, N, D, row0=rank * N)
+    X = ctx.synth(SEED_DATA, N, D, row0=rank * N, kind=args.data)
     V, t, r, _ = lk.params_lsh_euclidean(SEED_PARAMS, L_TABLES, K_FUNCS, D, W)
     lsh = lk.LSH(ctx, "euclidean", D, K_FUNCS, L_TABLES, nb, W, V=V, t=t, r=r)
     p = lambda t_: C.c_void_p(t_.data_ptr())
 
-    def initial_centroids(K):
+    def initial_centroids(K, kind):
         rows = sharding.centroid_rows(N_total, K)                  # reference init: rows i*floor(N/K)
         Cc = torch.empty((K, D), dtype=torch.float64, device=dev)
         for i, row in enumerate(rows):                             # centroids may live on other shards
-            Cc[i] = ctx.synth(SEED_DATA, 1, D, row0=int(row))[0].double()
+            Cc[i] = ctx.synth(SEED_DATA, 1, D, row0=int(row), kind=kind)[0].double()
         return Cc, sharding.local_src_rows(rows, rank * N, N)      # centroid override, shard-local
 
-    def c3_run(K):
-        Cc, src = initial_centroids(K)
+    def c3_run(K, X=X, kind=args.data, steps=args.steps, warmup=args.warmup):
+        Cc, src = initial_centroids(K, kind)
         tuples = torch.empty((N, L_TABLES, K_FUNCS), dtype=torch.int32, device=dev)
         bucket = torch.empty((N, L_TABLES), dtype=torch.int32, device=dev)
         assign = torch.empty((N,), dtype=torch.int32, device=dev)
@@ -338,36 +346,42 @@ def main():
             lk._ck(lib.lshkm_hash_assign(lsh.h, p(X), N, p(Cc), K, src_p, p(tuples), None, p(bucket), p(assign),
                                          p(dist_)))
         ctx.reset_stats()
-        elapsed = timed(step, args.steps, args.warmup, world, dev)
-        ex = {"per_step": True, "assign_ambiguous_rows": ctx.stat(lk.STAT_ASSIGN_AMBIG) // (args.steps + args.warmup),
-              "hash_fixup_rows": ctx.stat(lk.STAT_HASH_FIX) // (args.steps + args.warmup),
-              "hash_exact_fallbacks": ctx.stat(lk.STAT_HASH_EXACT) // (args.steps + args.warmup)}
-        kms = fused_kernel_ms(lk, lib, ctx, step, max(3, args.steps))
+        elapsed = timed(step, steps, warmup, world, dev)
+        ex = {"per_step": True, "assign_ambiguous_rows": ctx.stat(lk.STAT_ASSIGN_AMBIG) // (steps + warmup),
+              "hash_fixup_rows": ctx.stat(lk.STAT_HASH_FIX) // (steps + warmup),
+              "hash_exact_fallbacks": ctx.stat(lk.STAT_HASH_EXACT) // (steps + warmup),
+              "refined_rows": ctx.stat(lk.STAT_REFINED) // (steps + warmup)}
+        kms = fused_kernel_ms(lk, lib, ctx, step, max(3, steps))
         if args.exact_dist_line:
             # the same step with every distance from the reference-order fp64 chain
             ctx.set_dist_mode("exact")
             try:
-                el_x = timed(step, args.steps, args.warmup, world, dev)
-                kms_x = fused_kernel_ms(lk, lib, ctx, step, max(3, args.steps))
+                ctx.reset_stats()
+                el_x = timed(step, steps, warmup, world, dev)
+                pow_fix = ctx.stat(lk.STAT_POW_FIX) // (steps + warmup)
+                kms_x = fused_kernel_ms(lk, lib, ctx, step, max(3, steps))
             finally:
                 ctx.set_dist_mode("certified")
             ex["exact_distances"] = {"note": "lshkm_ctx_set_dist_mode(LSHKM_DIST_EXACT): bit-exact distances "
                                              "(the reference's fp64 chain)",
-                                     "value": N_total * args.steps / el_x, "ms_per_step": el_x / args.steps * 1e3,
-                                     "kernel_ms": kms_x, "frac": 624.0 * N / (kms_x * 1e-3) / 8e12}
+                                     "value": N_total * steps / el_x, "ms_per_step": el_x / steps * 1e3,
+                                     "kernel_ms": kms_x, "frac": 624.0 * N / (kms_x * 1e-3) / 8e12,
+                                     "pow_fix_rows": pow_fix}
         return elapsed, kms, ex
 
-    def c5_run(K):
+    def c5_run(K, X=X, kind=args.data, steps=args.steps, warmup=args.warmup):
         # one full iteration: hash + assign, per-shard sums, RCCL all-reduce,
         # finalize, and the recommend step (get_top_N_recom over the whole
         # clusters of Q query users, the prediction sums carried rank to rank)
-        Cc, src = initial_centroids(K)
-        it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="fast")
+        Cc, src = initial_centroids(K, kind)
+        it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="certified")
         if args.recom_users > 0:
             it.enable_recommend(N_total, rank * N, Q=args.recom_users, n_top=5)
-        elapsed = timed(it.step, args.steps, args.warmup, world, dev)
+        ctx.reset_stats()
+        elapsed = timed(it.step, steps, warmup, world, dev)
+        it.km_seq_chains = ctx.stat(lk.STAT_KM_SEQ) // (steps + warmup)
         it.timing = True
-        kms = fused_kernel_ms(lk, lib, ctx, it.step, max(3, args.steps))
+        kms = fused_kernel_ms(lk, lib, ctx, it.step, max(3, steps))
         it.timing = False
         xms = it.exchange_ms() if world > 1 else None
         rec = None
@@ -391,23 +405,26 @@ def main():
                    "similarities_per_step": sims, "sims_ms": ph1, "chain_ms": ph2,
                    "users_per_s": args.recom_users / ((ph1 + ph2) / 1e3),
                    "similarities_per_s": sims / ((ph1 + ph2) / 1e3)}
+        rec = rec or {}
+        rec["km_sequential_chains"] = it.km_seq_chains
         return elapsed, kms, xms, rec
 
-    def c5_object(K, elapsed, kms, xms, rec=None):
+    def c5_object(K, elapsed, kms, xms, rec=None, steps=args.steps):
         coll = (f"RCCL all-reduce ({backend}) of the {K}x128 fp64 sums + {K} counts" if world > 1
                 else "none (N = 1: a single shard, no collective)")
         return {
             "metric": f"C5 LSH-assign + k-means recommend iterations: points/s (hash + assign K={K} + sums + "
                       f"{'RCCL all-reduce' if world > 1 else 'no collective at N = 1'} + finalize"
                       + (f" + recommend for {args.recom_users} users)" if args.recom_users > 0 else ")"),
-            "value": N_total * args.steps / elapsed, "unit": "point iteration ops/s",
-            "ms_per_step": elapsed / args.steps * 1e3, "n_gpus": world, "scaling": "weak",
+            "value": N_total * steps / elapsed, "unit": "point iteration ops/s",
+            "ms_per_step": elapsed / steps * 1e3, "n_gpus": world, "scaling": "weak",
             "config": {"workload": f"C5 (BASELINE configs[4]): N={N} per GPU x {world} GPU(s), d=128, K={K}, "
                                    f"L=5, k=4, w=0.4, exchange: {coll}",
                        "N_per_gpu": N, "N_total": N_total, "K": K, "parallelism": f"dp{world} (row shards)"},
             "allreduce": coll,
             "allreduce_ms": xms if world > 1 else None,
-            "recommend": rec,
+            "km_sequential_chains": (rec or {}).pop("km_sequential_chains", None),
+            "recommend": rec or None,
             "roofline": roofline(N, K, kms, traffic_for(args.traffic_json_c5, N, K, "c5"),
                                  FUSED_WHAT + " (K = 1024: two 512-centroid passes)"),
         }
@@ -420,7 +437,7 @@ def main():
         line.update({"metric": METRIC + " (C5 workload)", "unit": "point hash+assign ops/s", "steps": args.steps,
                      "warmup": args.warmup, "higher_is_better": True, "vs_baseline": None,
                      "dtype": DTYPE,
-                     "data": "synthetic (include/lshkm_synth.h), resident in HBM"})
+                     "data": DATA[args.data]})
     else:
         K = args.k or 256
         el, kms, ex = c3_run(K)
@@ -429,7 +446,7 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": DTYPE,
-            "data": "synthetic (include/lshkm_synth.h), resident in HBM",
+            "data": DATA[args.data],
             "config": {"workload": f"C3 Lloyd K={K} + C2 LSH L=5 k=4 hashing, N={N} per GPU, d=128",
                        "N_per_gpu": N, "N_total": N_total, "d": D, "K": K, "L": L_TABLES, "k": K_FUNCS,
                        "w": W, "nb": nb, "parallelism": f"dp{world} (row shards)"},
@@ -440,6 +457,21 @@ def main():
             K5 = 1024
             el5, kms5, xms5, rec5 = c5_run(K5)
             line["c5"] = c5_object(K5, el5, kms5, xms5, rec5)
+        if args.data == "grid" and args.normal_leg:
+            # the same C3 step and C5 iteration on full-mantissa rows (SURVEY.md
+            # §8d's N(0,1) data): the certificates' and exact chains' rates there
+            Xn = ctx.synth(SEED_DATA, N, D, row0=rank * N, kind="normal")
+            ns, nw = max(5, args.steps // 2), max(5, args.warmup // 3)
+            el_n, kms_n, ex_n = c3_run(K, X=Xn, kind="normal", steps=ns, warmup=nw)
+            nd = {"data": DATA["normal"], "steps": ns, "warmup": nw,
+                  "c3": {"value": N_total * ns / el_n, "ms_per_step": el_n / ns * 1e3, "kernel_ms": kms_n,
+                         "frac": BYTES_PER_PT * N / (kms_n * 1e-3) / (HBM_PEAK_GBS * 1e9), "exactness": ex_n}}
+            if not args.no_c5:
+                el5, kms5, xms5, rec5 = c5_run(1024, X=Xn, kind="normal", steps=ns, warmup=nw)
+                nd["c5"] = c5_object(1024, el5, kms5, xms5, rec5, steps=ns)
+                nd["c5"].pop("roofline")
+                nd["c5"]["kernel_ms"] = kms5
+            line["normal_data"] = nd
     line["world_size"] = world
     line["backend"] = backend
     if world > 1:

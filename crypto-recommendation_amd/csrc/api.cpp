@@ -926,4 +926,12 @@ int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d,
     return rc;
 }
 
+int lshkm_synth_normal(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X) {
+    LSHKM_CHECK(ctx && (X || rows == 0) && rows >= 0 && d > 0, LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc = launch_synth(ctx->stream, seed, row0, rows, d, X, 1);
+    if (rc) { LSHKM_LAUNCH_CHECK(); }
+    return rc;
+}
+
 }  // extern "C"

@@ -617,16 +617,31 @@ static int km_sums(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t* assign
     if (X.f64 && !force_chain && !test_switch("LSHKM_KM_PATH", "fx") && K <= 65535) {
         const size_t wsb = km_seg_ws_bytes(N, K, d);
         if (wsb <= KM_SEG_WS_CAP && ctx->ws_range[11].reserve(wsb) == 0) {
-            if ((rc = launch_km_sums_seg(ctx->stream, X.d(), d, rows_p, crow_p,
-                                         K, N, sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+            if ((rc = launch_km_sums_seg(ctx->stream, X, d, rows_p, crow_p, K, N, sums, counts, carry, carry_counts,
+                                         ctx->ws_range[11].p))) {
+                LSHKM_LAUNCH_CHECK();
+                return rc;
+            }
             return 0;
         }
         (void)hipGetLastError();          // a failed reservation leaves no sticky error
     }
     if (!force_chain) {
         if ((rc = ctx->ws_range[11].reserve(km_fx_ws_bytes(K, d)))) return rc;
-        if ((rc = launch_km_sums_fx(ctx->stream, X, d, rows_p, crow_p, K, N,
-                                    sums, counts, carry, carry_counts, ctx->ws_range[11].p))) { LSHKM_LAUNCH_CHECK(); return rc; }
+        // the chains the never-rounds test flags: by segments (fp32 rows of
+        // general values: ~5 % of the chains of 10K N(0,1) values, most of 40K),
+        // sequential where the segment workspace does not fit
+        void* seg_ws = nullptr;
+        if (!X.f64 && K <= 65535) {
+            const size_t wsb = km_seg_ws_bytes(N, K, d);
+            if (wsb <= KM_SEG_WS_CAP && ctx->ws_km_seg.reserve(wsb) == 0) seg_ws = ctx->ws_km_seg.p;
+            else (void)hipGetLastError();
+        }
+        if ((rc = launch_km_sums_fx(ctx->stream, X, d, rows_p, crow_p, K, N, sums, counts, carry, carry_counts,
+                                    ctx->ws_range[11].p, (unsigned long long*)ctx->stats.p + STAT_KM_SEQ, seg_ws))) {
+            LSHKM_LAUNCH_CHECK();
+            return rc;
+        }
         return 0;
     }
     if ((rc = launch_km_chain(ctx->stream, X, d, rows_p, crow_p, K, sums, counts,
@@ -726,6 +741,117 @@ int lshkm_kmeans_partial_carry_f64(lshkm_ctx ctx, const double* X, int64_t N, in
                                    const double* carry_sums, const int64_t* carry_counts, double* sums,
                                    int64_t* counts) {
     return kmeans_partial_carry_impl(ctx, X, N, d, assign, K, carry_sums, carry_counts, sums, counts);
+}
+
+// ------------------------------------------------------- sharded k-means sums
+static int shard_begin_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64_t* crow, const int32_t* rows, int K,
+                            double* sums, double* asum, int32_t* qt, int64_t* counts) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && crow && (rows || N == 0) && sums && asum && qt && counts && N >= 0 &&
+                    N < (1ll << 31) && d > 0 && K > 0,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = ctx->ws_range[11].reserve(km_fx_ws_bytes(K, d)))) return rc;
+    if ((rc = launch_km_shard_begin(ctx->stream, X, d, rows, crow, K, N, sums, asum, qt, counts, ctx->ws_range[11].p))) {
+        LSHKM_LAUNCH_CHECK();
+        return rc;
+    }
+    return 0;
+}
+
+static int shard_prepare_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64_t* crow, const int32_t* rows, int K,
+                              const double* start, const int32_t* flag, void* ws, int64_t ws_bytes) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && crow && (rows || N == 0) && start && flag && ws && N >= 0 &&
+                    N < (1ll << 31) && d > 0 && K > 0 && K <= 65535,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(ws_bytes >= (int64_t)km_shard_ws_bytes(N, K, d), LSHKM_ERR_ARG,
+                "workspace smaller than lshkm_kmeans_shard_ws_bytes");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = launch_km_shard_prepare(ctx->stream, X, d, rows, crow, K, N, start, flag, ws))) {
+        LSHKM_LAUNCH_CHECK();
+        return rc;
+    }
+    return 0;
+}
+
+static int shard_chain_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64_t* crow, const int32_t* rows, int K,
+                            const int32_t* flag, const uint8_t* mask, const double* carry, void* ws, int64_t ws_bytes,
+                            double* sums) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && crow && (rows || N == 0) && flag && mask && ws && sums && N >= 0 &&
+                    N < (1ll << 31) && d > 0 && K > 0 && K <= 65535,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_CHECK(ws_bytes >= (int64_t)km_shard_ws_bytes(N, K, d), LSHKM_ERR_ARG,
+                "workspace smaller than lshkm_kmeans_shard_ws_bytes");
+    LSHKM_CHECK(carry != sums, LSHKM_ERR_ARG, "sums must not alias carry");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = launch_km_shard_chain(ctx->stream, X, d, rows, crow, K, N, flag, mask, carry, ws, sums))) {
+        LSHKM_LAUNCH_CHECK();
+        return rc;
+    }
+    return 0;
+}
+
+int lshkm_kmeans_shard_begin(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow, const int32_t* rows,
+                             int K, double* sums, double* asum, int32_t* qt, int64_t* counts) {
+    return shard_begin_impl(ctx, X, N, d, crow, rows, K, sums, asum, qt, counts);
+}
+
+int lshkm_kmeans_shard_begin_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int64_t* crow,
+                                 const int32_t* rows, int K, double* sums, double* asum, int32_t* qt, int64_t* counts) {
+    return shard_begin_impl(ctx, X, N, d, crow, rows, K, sums, asum, qt, counts);
+}
+
+int lshkm_kmeans_shard_certify(lshkm_ctx ctx, int K, int d, int world, int rank, const double* gathered,
+                               const double* asum, const int32_t* qt, const int64_t* counts, double* sums_out,
+                               double* start, int32_t* flag, uint8_t* mask, int64_t* n_flagged) {
+    LSHKM_CHECK(ctx && K > 0 && d > 0 && world >= 1 && rank >= 0 && rank < world && gathered && asum && qt && counts &&
+                    sums_out && flag && mask && n_flagged,
+                LSHKM_ERR_ARG, "bad arguments");
+    LSHKM_HIP(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = reserve(ctx, WS_FLAG, 64))) return rc;
+    unsigned long long* nf = slot<unsigned long long>(ctx, WS_FLAG);
+    if ((rc = launch_km_shard_certify(ctx->stream, gathered, world, rank, asum, qt, counts, K, d, sums_out, start, flag,
+                                      mask, nf))) {
+        LSHKM_LAUNCH_CHECK();
+        return rc;
+    }
+    unsigned long long h = 0;
+    if ((rc = d2h(ctx, &h, nf, 8))) return rc;
+    *n_flagged = (int64_t)h;
+    return 0;
+}
+
+int lshkm_kmeans_shard_ws_bytes(int64_t N, int K, int d, int64_t* bytes) {
+    LSHKM_CHECK(bytes && N >= 0 && K > 0 && d > 0, LSHKM_ERR_ARG, "bad arguments");
+    *bytes = (int64_t)km_shard_ws_bytes(N, K, d);
+    return 0;
+}
+
+int lshkm_kmeans_shard_prepare(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow,
+                               const int32_t* rows, int K, const double* start, const int32_t* flag, void* ws,
+                               int64_t ws_bytes) {
+    return shard_prepare_impl(ctx, X, N, d, crow, rows, K, start, flag, ws, ws_bytes);
+}
+
+int lshkm_kmeans_shard_prepare_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int64_t* crow,
+                                   const int32_t* rows, int K, const double* start, const int32_t* flag, void* ws,
+                                   int64_t ws_bytes) {
+    return shard_prepare_impl(ctx, X, N, d, crow, rows, K, start, flag, ws, ws_bytes);
+}
+
+int lshkm_kmeans_shard_chain(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow, const int32_t* rows,
+                             int K, const int32_t* flag, const uint8_t* mask, const double* carry, void* ws,
+                             int64_t ws_bytes, double* sums) {
+    return shard_chain_impl(ctx, X, N, d, crow, rows, K, flag, mask, carry, ws, ws_bytes, sums);
+}
+
+int lshkm_kmeans_shard_chain_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int64_t* crow,
+                                 const int32_t* rows, int K, const int32_t* flag, const uint8_t* mask,
+                                 const double* carry, void* ws, int64_t ws_bytes, double* sums) {
+    return shard_chain_impl(ctx, X, N, d, crow, rows, K, flag, mask, carry, ws, ws_bytes, sums);
 }
 
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums, const int64_t* counts, int K, int d, const double* C_old,

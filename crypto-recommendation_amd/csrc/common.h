@@ -80,7 +80,8 @@ enum Stat {
     STAT_HASH_FIX = 6,       // rows the fused pass listed for the hash fix-up (an uncertified floor / sign)
     STAT_REC_SOFT = 7,       // clustering-recommender similarities decided by the x87 chain (IpAcc declined)
     STAT_POW_FIX = 8,        // euclidean winner distances redone with glibc's pow(x, 2) (an inexact square)
-    STAT_COUNT = 9
+    STAT_KM_SEQ = 9,         // k-means (cluster, dim) sums whose never-rounds test failed (sequential / segment chain)
+    STAT_COUNT = 10
 };
 
 constexpr int WAVE = 64;

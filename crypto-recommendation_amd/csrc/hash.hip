@@ -244,18 +244,23 @@ int launch_proj_hash(hipStream_t s, int mode, Pts X, int64_t N, const HashParams
 }
 
 // ------------------------------------------------------------ synthetic data
+template <bool NORMAL>
 __global__ void synth_kernel(uint64_t seed, int64_t row0, int64_t total, int d, float* X) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = e / d, c = e - r * d;
-        X[e] = lshkm_synth_value(seed, (uint64_t)(row0 + r), (uint64_t)d, (uint64_t)c);
+        X[e] = NORMAL ? lshkm_synth_normal_value(seed, (uint64_t)(row0 + r), (uint64_t)d, (uint64_t)c)
+                      : lshkm_synth_value(seed, (uint64_t)(row0 + r), (uint64_t)d, (uint64_t)c);
     }
 }
 
-int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X) {
+int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X, int kind) {
     const int64_t total = rows * d;
     if (total <= 0) return 0;
     const int64_t blocks = min((total + 255) / 256, (int64_t)256 * 64);
-    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, seed, row0, total, d, X);
+    if (kind == 1)
+        hipLaunchKernelGGL(synth_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, seed, row0, total, d, X);
+    else
+        hipLaunchKernelGGL(synth_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, seed, row0, total, d, X);
     return kstatus("hash.hip");
 }
 

@@ -173,18 +173,34 @@ int launch_memo_scatter(hipStream_t s, const int32_t* off, const int32_t* bit, i
 int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K,
                     double* sums, int64_t* counts, const double* carry = nullptr,
                     const int64_t* carry_counts = nullptr);
-// fp64 rows: the same sums by binade segments (kmseg.h; ws: km_seg_ws_bytes).
+// The same sums by binade segments (kmseg.h; ws: km_seg_ws_bytes): every chain
+// of fp64 rows; flag != NULL: only the flagged (cluster, 64-dim block) chains.
 size_t km_seg_ws_bytes(int64_t M, int K, int d);
 // above this the update takes the fixed-point form instead (same exact sums)
 constexpr size_t KM_SEG_WS_CAP = (size_t)8 << 30;
-int launch_km_sums_seg(hipStream_t s, const double* X, int d, const int32_t* rows, const int64_t* crow, int K,
-                       int64_t M, double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts,
-                       void* ws);
-// Same sums, parallel: exact int128 fixed-point sums wherever the sequential
-// chain provably never rounds, the sequential chain elsewhere (ws: km_fx_ws_bytes).
+int launch_km_sums_seg(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                       double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws,
+                       const int* flag = nullptr);
+// Same sums, parallel: plain fp64 adds in any order wherever the sequential
+// chain provably never rounds (km_cert), the rounding chains by segments
+// (seg_ws: km_seg_ws_bytes) or, without seg_ws, by the sequential kernel
+// (ws: km_fx_ws_bytes). stat: counts the chains the test flags.
 size_t km_fx_ws_bytes(int K, int d);
 int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
-                      double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws);
+                      double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws,
+                      unsigned long long* stat = nullptr, void* seg_ws = nullptr);
+// Sharded form (lshkm_kmeans_shard_*): begin (ws: km_shard_ws_bytes), certify,
+// prepare / chain (the flagged chains' records and their composition).
+size_t km_shard_ws_bytes(int64_t M, int K, int d);
+int launch_km_shard_begin(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                          double* sums, double* asum, int32_t* qt, int64_t* counts, void* ws);
+int launch_km_shard_certify(hipStream_t s, const double* gathered, int world, int rank, const double* asum,
+                            const int32_t* qt, const int64_t* counts, int K, int d, double* sums_out, double* start,
+                            int* flag, uint8_t* mask, unsigned long long* nflag);
+int launch_km_shard_prepare(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                            const double* start, const int* flag, void* ws);
+int launch_km_shard_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                          const int* flag, const uint8_t* mask, const double* carry, void* ws, double* sums);
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
 
@@ -380,6 +396,6 @@ int launch_sil_sum(hipStream_t s, const double* sv, const int32_t* rows, const i
                    double* raw, double* out);
 
 // Synthetic data.
-int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X);
+int launch_synth(hipStream_t s, uint64_t seed, int64_t row0, int64_t rows, int d, float* X, int kind = 0);
 
 }  // namespace lshkm

@@ -11,6 +11,7 @@
 // in row order; a wave owns 64 dimensions of one cluster, each lane one chain,
 // and streams the member rows with 16 row loads in flight per lane (row
 // indices are wave-uniform scalar loads). Bytes: 4d per row read once.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -104,7 +105,8 @@ __device__ inline double km_x32(double v) {      // lanes k = 0, 1: lane + 32's 
 template <typename TX>
 __global__ __launch_bounds__(64) void km_chain16_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                        const int64_t* __restrict__ crow, const double* __restrict__ carry,
-                                                       const int* __restrict__ flag, double* __restrict__ sums) {
+                                                       const int* __restrict__ flag, double* __restrict__ sums,
+                                                       const uint8_t* __restrict__ mask) {
     const int c = blockIdx.x, jb = blockIdx.y;
     if (flag && !((flag[c] >> min(31, jb / 4)) & 1)) return;
     const int lane = threadIdx.x, k = lane >> 4;
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(64) void km_chain16_kernel(const TX* __restrict__ X
             }
         }
     }
-    if (k == 0 && j < d) sums[(size_t)c * d + j] = s;
+    if (k == 0 && j < d && (!mask || mask[(size_t)c * d + j])) sums[(size_t)c * d + j] = s;
 }
 
 template <typename TX>
@@ -201,9 +203,9 @@ int launch_km_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int6
     if (km_wide()) {
         const dim3 grid((unsigned)K, (unsigned)((d + 15) / 16));
         if (X.f64)
-            hipLaunchKernelGGL(km_chain16_kernel<double>, grid, dim3(64), 0, s, X.d(), d, rows, crow, carry, nullptr, sums);
+            hipLaunchKernelGGL(km_chain16_kernel<double>, grid, dim3(64), 0, s, X.d(), d, rows, crow, carry, nullptr, sums, nullptr);
         else
-            hipLaunchKernelGGL(km_chain16_kernel<float>, grid, dim3(64), 0, s, X.f(), d, rows, crow, carry, nullptr, sums);
+            hipLaunchKernelGGL(km_chain16_kernel<float>, grid, dim3(64), 0, s, X.f(), d, rows, crow, carry, nullptr, sums, nullptr);
         if (counts)
             hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
                                counts);
@@ -239,19 +241,42 @@ constexpr int KMF_BAD = 1 << 20;     // qmin marker of a chain that needs the se
 
 struct KmFx {                        // per (c, j), zeroed / initialised by km_fx_init_kernel
     double sum;
+    double asum;                     // sum of |x| (rounded: <= (1 + n 2^-53) times the true one)
     int qmin;                        // lowest set-bit exponent, -KMF_BAD if flagged
     int tmax;                        // highest bit position + 1
 };
 
 __global__ void km_fx_init_kernel(KmFx* __restrict__ acc, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) { acc[i].sum = 0.0; acc[i].qmin = 1 << 30; acc[i].tmax = -(1 << 30); }
+    if (i < n) { acc[i].sum = 0.0; acc[i].asum = 0.0; acc[i].qmin = 1 << 30; acc[i].tmax = -(1 << 30); }
 }
 
-__device__ inline void km_fx_flush(KmFx* a, double v, int qmin, int tmax, bool bad) {
+__device__ inline void km_fx_flush(KmFx* a, double v, double av, int qmin, int tmax, bool bad) {
     if (v != 0.0) atomicAdd(&a->sum, v);
+    if (av != 0.0) atomicAdd(&a->asum, av);
     atomicMin(&a->qmin, bad ? -KMF_BAD : qmin);
     atomicMax(&a->tmax, tmax);
+}
+
+// The never-rounds test of one (c, j): its cnt values are integer multiples of
+// 2^qmin below 2^tmax in magnitude, and their |x| sum to asum (fp64-rounded in
+// any order: within a factor 1 + cnt 2^-53 <= 1 + 2^-22 of the true sum for
+// cnt < 2^31). Every partial sum of any subset, in any order, is a multiple of
+// 2^qmin no larger in magnitude than the true sum of |x|: a double when that is
+// below 2^(53 + qmin). The count form (cnt 2^tmax) is the coarser bound of the
+// same kind; the |x| form passes on far more general fp32 chains (N(0,1) rows:
+// ~95 % vs ~64 % of the chains of 10K values).
+__device__ inline bool km_cert(int qmin, int tmax, int64_t cnt, double asum) {
+    if (qmin <= -KMF_BAD / 2) return false;        // inf / nan among the values
+    if (qmin > tmax) return true;                  // no nonzero value: the sum is +0
+    int lc = 0;
+    while (((int64_t)1 << lc) < cnt) lc++;         // ceil(log2 count)
+    // every partial below cnt 2^tmax <= 2^(lc + tmax): finite only if that is <=
+    // 2^1023 (else an any-order sum may overflow where the reference's chain stays
+    // finite, e.g. [M, -M, M] with M = 1.5 * 2^1023)
+    if (lc + tmax - qmin <= 53 && lc + tmax <= 1023) return true;
+    // the |x| bound (an overflowed asum is inf and fails; 2^(53 + qmin) may be inf)
+    return asum * (1.0 + 0x1p-20) < ldexp(1.0, min(53 + qmin, 1024));
 }
 
 // lowest set-bit exponent q and top t of a nonzero finite value; false for
@@ -299,7 +324,7 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int
     }
     int c = lo;
     int64_t cend = crow[c + 1];
-    double s = 0.0;
+    double s = 0.0, as = 0.0;
     int qmin = 1 << 30, tmax = -(1 << 30);
     bool bad = false;
     for (int64_t p = p0; p < p1; p += 16) {
@@ -310,8 +335,8 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int
         for (int u = 0; u < 16; u++) {
             if (p + u >= p1) break;
             while (p + u >= cend) {              // cluster boundary: flush, move on (skipping empty clusters)
-                if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
-                s = 0.0; qmin = 1 << 30; tmax = -(1 << 30); bad = false;
+                if (on) km_fx_flush(acc + (size_t)c * d + j, s, as, qmin, tmax, bad);
+                s = 0.0; as = 0.0; qmin = 1 << 30; tmax = -(1 << 30); bad = false;
                 c++;
                 cend = crow[c + 1];
             }
@@ -320,9 +345,10 @@ __global__ __launch_bounds__(64) void km_fx_kernel(const TX* __restrict__ X, int
             qmin = min(qmin, q);
             tmax = max(tmax, t);
             s = __dadd_rn(s, (double)v[u]);     // exact whenever the chain's test passes
+            as = __dadd_rn(as, fabs((double)v[u]));
         }
     }
-    if (on) km_fx_flush(acc + (size_t)c * d + j, s, qmin, tmax, bad);
+    if (on) km_fx_flush(acc + (size_t)c * d + j, s, as, qmin, tmax, bad);
 }
 
 // fp32 rows with d % 128 == 0: a wave reads whole 512-B row slices (two
@@ -346,7 +372,7 @@ __global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X,
     }
     int c = lo;
     int64_t cend = crow[c + 1];
-    double s0 = 0.0, s1 = 0.0;
+    double s0 = 0.0, s1 = 0.0, a0 = 0.0, a1 = 0.0;
     int q0 = 1 << 30, t0 = -(1 << 30), q1 = 1 << 30, t1 = -(1 << 30);
     bool bad0 = false, bad1 = false;
     for (int64_t p = p0; p < p1; p += KMF2_U) {
@@ -358,9 +384,9 @@ __global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X,
         for (int u = 0; u < KMF2_U; u++) {
             if (p + u >= p1) break;
             while (p + u >= cend) {              // cluster boundary: flush, move on (skipping empty clusters)
-                km_fx_flush(acc + (size_t)c * d + j, s0, q0, t0, bad0);
-                km_fx_flush(acc + (size_t)c * d + j + 1, s1, q1, t1, bad1);
-                s0 = s1 = 0.0; q0 = q1 = 1 << 30; t0 = t1 = -(1 << 30); bad0 = bad1 = false;
+                km_fx_flush(acc + (size_t)c * d + j, s0, a0, q0, t0, bad0);
+                km_fx_flush(acc + (size_t)c * d + j + 1, s1, a1, q1, t1, bad1);
+                s0 = s1 = a0 = a1 = 0.0; q0 = q1 = 1 << 30; t0 = t1 = -(1 << 30); bad0 = bad1 = false;
                 c++;
                 cend = crow[c + 1];
             }
@@ -368,31 +394,34 @@ __global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X,
             if (km_fx_bits(v[u].x, q, t, bad0)) {
                 q0 = min(q0, q); t0 = max(t0, t);
                 s0 = __dadd_rn(s0, (double)v[u].x);
+                a0 = __dadd_rn(a0, (double)fabsf(v[u].x));
             }
             if (km_fx_bits(v[u].y, q, t, bad1)) {
                 q1 = min(q1, q); t1 = max(t1, t);
                 s1 = __dadd_rn(s1, (double)v[u].y);
+                a1 = __dadd_rn(a1, (double)fabsf(v[u].y));
             }
         }
     }
-    km_fx_flush(acc + (size_t)c * d + j, s0, q0, t0, bad0);
-    km_fx_flush(acc + (size_t)c * d + j + 1, s1, q1, t1, bad1);
+    km_fx_flush(acc + (size_t)c * d + j, s0, a0, q0, t0, bad0);
+    km_fx_flush(acc + (size_t)c * d + j + 1, s1, a1, q1, t1, bad1);
 }
 
 // Per (c, j): the exact sum if the chain provably never rounds, else a flag for
 // the sequential kernel. carry (sharded exact mode): the chain starts from it.
 __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_t* __restrict__ crow, int K, int d,
                                       const double* __restrict__ carry, const int64_t* __restrict__ carry_counts,
-                                      double* __restrict__ sums, int* __restrict__ flag) {
+                                      double* __restrict__ sums, int* __restrict__ flag,
+                                      unsigned long long* __restrict__ stat) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)K * d) return;
     const int c = (int)(i / d);
     const KmFx a = acc[i];
     int64_t cnt = crow[c + 1] - crow[c];
-    double s = a.sum;
+    double s = a.sum, as = a.asum;
     int qmin = a.qmin, tmax = a.tmax;
     bool ok = qmin > -KMF_BAD / 2;
-    if (carry && ok) {
+    if (carry && ok) {                  // the carried running sum is one more value of the chain
         const double s0 = carry[i];
         cnt += 1;
         int q, t;
@@ -401,18 +430,17 @@ __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_
             qmin = min(qmin, q);
             tmax = max(tmax, t);
             s = __dadd_rn(s0, s);
+            as = __dadd_rn(as, fabs(s0));
         }
         if (bad) ok = false;
     }
-    int lc = 0;
-    while (((int64_t)1 << lc) < cnt) lc++;          // ceil(log2 count)
-    if (ok && qmin <= tmax && lc + tmax - qmin > 53) ok = false;
-    // every partial sum in any order is below cnt * 2^tmax <= 2^(lc + tmax):
-    // finite only if that is <= 2^1023 (else an any-order sum may overflow where
-    // the reference's chain stays finite, e.g. [M, -M, M] with M = 1.5 * 2^1023)
-    if (ok && qmin <= tmax && lc + tmax > 1023) ok = false;
+    ok = ok && km_cert(qmin, tmax, cnt, as);
     if (ok) sums[i] = s;
     else atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));   // chain block (c, j/64) goes sequential
+    if (stat) {
+        const unsigned long long nb = __ballot(!ok);
+        if (nb && (threadIdx.x & 63) == __builtin_ctzll(nb)) atomicAdd(stat, (unsigned long long)__popcll(nb));
+    }
 }
 
 // The sequential chains of the flagged (c, 64-dim block)s only.
@@ -434,8 +462,13 @@ __global__ __launch_bounds__(64) void km_chain_flagged_kernel(const TX* __restri
 
 size_t km_fx_ws_bytes(int K, int d) { return (size_t)K * d * sizeof(KmFx) + (size_t)K * 4 + 64; }
 
+int launch_km_sums_seg(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                       double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws,
+                       const int* flag);
+
 int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
-                      double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws) {
+                      double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws,
+                      unsigned long long* stat, void* seg_ws) {
     KmFx* acc = reinterpret_cast<KmFx*>(ws);
     int* flag = reinterpret_cast<int*>(acc + (size_t)K * d);
     const int64_t n = (int64_t)K * d;
@@ -451,13 +484,19 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
         else hipLaunchKernelGGL(km_fx_kernel<float>, fgrid, dim3(64), 0, s, X.f(), d, rows, crow, K, M, acc);
     }
     hipLaunchKernelGGL(km_fx_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, crow, K, d, carry,
-                       carry_counts, sums, flag);
-    if (km_wide()) {
+                       carry_counts, sums, flag, stat);
+    if (seg_ws && !test_switch("LSHKM_KM_FLAGGED", "chain")) {
+        // the flagged chains by binade segments (every window of theirs in
+        // parallel; the sequential form's time was set by the longest chain:
+        // 20 ms for a 206K-member cluster of full-mantissa rows)
+        if (const int rc = launch_km_sums_seg(s, X, d, rows, crow, K, M, sums, nullptr, carry, nullptr, seg_ws, flag))
+            return rc;
+    } else if (km_wide()) {
         const dim3 g16((unsigned)K, (unsigned)((d + 15) / 16));
         if (X.f64)
-            hipLaunchKernelGGL(km_chain16_kernel<double>, g16, dim3(64), 0, s, X.d(), d, rows, crow, carry, flag, sums);
+            hipLaunchKernelGGL(km_chain16_kernel<double>, g16, dim3(64), 0, s, X.d(), d, rows, crow, carry, flag, sums, nullptr);
         else
-            hipLaunchKernelGGL(km_chain16_kernel<float>, g16, dim3(64), 0, s, X.f(), d, rows, crow, carry, flag, sums);
+            hipLaunchKernelGGL(km_chain16_kernel<float>, g16, dim3(64), 0, s, X.f(), d, rows, crow, carry, flag, sums, nullptr);
     } else if (X.f64)
         hipLaunchKernelGGL(km_chain_flagged_kernel<double>, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, X.d(), d,
                            rows, crow, K, carry, flag, sums);
@@ -500,8 +539,8 @@ __device__ inline int ks_first_cluster(const int64_t* __restrict__ crow, int K, 
 // Walk window w's positions (lane j); f(p, x) per position, close(c) when
 // cluster c's part of the window ends (only for clusters with positions in it),
 // open(c, p) when it starts.
-template <int KS_U, typename Open, typename Step, typename Close>
-__device__ __attribute__((always_inline)) inline void ks_walk(const double* __restrict__ X, int d, int jl,
+template <int KS_U, typename TX, typename Open, typename Step, typename Close>
+__device__ __attribute__((always_inline)) inline void ks_walk(const TX* __restrict__ X, int d, int jl,
                                                               const int32_t* __restrict__ rows,
                                                               const int64_t* __restrict__ crow, int K, int64_t M,
                                                               int64_t p0, Open&& open, Step&& step, Close&& close) {
@@ -526,7 +565,7 @@ __device__ __attribute__((always_inline)) inline void ks_walk(const double* __re
     };
     auto ld_val = [&](const int32_t (&ix)[KS_U], double (&v)[KS_U]) {
 #pragma unroll
-        for (int u = 0; u < KS_U; u++) v[u] = X[(int64_t)ix[u] * d + jl];
+        for (int u = 0; u < KS_U; u++) v[u] = (double)X[(int64_t)ix[u] * d + jl];
     };
     int32_t ia[KS_U], ib[KS_U];
     double va[KS_U], vb[KS_U];
@@ -555,10 +594,25 @@ __device__ __attribute__((always_inline)) inline void ks_walk(const double* __re
     close(c);
 }
 
-__global__ __launch_bounds__(64) void ks_sum_kernel(const double* __restrict__ X, int d, const int32_t* __restrict__ rows,
+// flag (fp32 chains the never-rounds test flags; the sharded form): only the
+// windows holding a flagged (cluster, 64-dim block) chain run; NULL: every one.
+__device__ inline bool ks_window_flagged(const int* __restrict__ flag, const int64_t* __restrict__ crow, int K,
+                                         int64_t M, int64_t p0) {
+    if (!flag) return true;
+    const int c0 = ks_first_cluster(crow, K, p0);
+    const int c1 = ks_first_cluster(crow, K, min(M, p0 + KS_W) - 1);
+    const int bit = min(31, (int)blockIdx.y);
+    int any = 0;
+    for (int c = c0; c <= c1; c++) any |= (flag[c] >> bit) & 1;
+    return any != 0;
+}
+
+template <typename TX>
+__global__ __launch_bounds__(64) void ks_sum_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                     const int64_t* __restrict__ crow, int K, int64_t M,
-                                                    double* __restrict__ psum) {
+                                                    double* __restrict__ psum, const int* __restrict__ flag) {
     const int w = blockIdx.x;
+    if (!ks_window_flagged(flag, crow, K, M, (int64_t)w * KS_W)) return;
     const int j = blockIdx.y * 64 + threadIdx.x;
     const bool on = j < d;
     double s = 0.0;
@@ -570,8 +624,9 @@ __global__ __launch_bounds__(64) void ks_sum_kernel(const double* __restrict__ X
 
 __global__ __launch_bounds__(64) void ks_scan_kernel(const double* __restrict__ psum, const int64_t* __restrict__ crow,
                                                      int K, int d, const double* __restrict__ carry,
-                                                     double* __restrict__ sin) {
+                                                     double* __restrict__ sin, const int* __restrict__ flag) {
     const int c = blockIdx.x;
+    if (flag && !((flag[c] >> min(31, (int)blockIdx.y)) & 1)) return;
     const int j = blockIdx.y * 64 + threadIdx.x;
     const int64_t beg = crow[c], end = crow[c + 1];
     if (j >= d || beg == end) return;
@@ -583,11 +638,13 @@ __global__ __launch_bounds__(64) void ks_scan_kernel(const double* __restrict__ 
     }
 }
 
-__global__ __launch_bounds__(64) void ks_seg_kernel(const double* __restrict__ X, int d, const int32_t* __restrict__ rows,
+template <typename TX>
+__global__ __launch_bounds__(64) void ks_seg_kernel(const TX* __restrict__ X, int d, const int32_t* __restrict__ rows,
                                                     const int64_t* __restrict__ crow, int K, int64_t M,
                                                     const double* __restrict__ sin, int32_t* __restrict__ cnt,
-                                                    KsRaw* __restrict__ rec) {
+                                                    KsRaw* __restrict__ rec, const int* __restrict__ flag) {
     const int w = blockIdx.x;
+    if (!ks_window_flagged(flag, crow, K, M, (int64_t)w * KS_W)) return;
     const int j = blockIdx.y * 64 + threadIdx.x;
     const bool on = j < d;
     const int64_t p0 = (int64_t)w * KS_W;
@@ -671,14 +728,17 @@ __device__ inline double ks_shr1(double v) {          // lane l <- lane l-1
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
-__global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict__ X, int d,
+template <typename TX>
+__global__ __launch_bounds__(64) void ks_compose_kernel(const TX* __restrict__ X, int d,
                                                         const int32_t* __restrict__ rows,
                                                         const int64_t* __restrict__ crow, int K,
                                                         const double* __restrict__ carry,
                                                         const int32_t* __restrict__ cnt, const KsRaw* __restrict__ rec,
-                                                        double* __restrict__ sums) {
+                                                        double* __restrict__ sums, const int* __restrict__ flag,
+                                                        const uint8_t* __restrict__ mask) {
     const int j = blockIdx.x, c = blockIdx.y;
     const int lane = threadIdx.x;
+    if (flag && !((flag[c] >> min(31, j / 64)) & 1)) return;          // the flagged chains only
     const int64_t beg = crow[c], end = crow[c + 1];
     double s = carry ? carry[(size_t)c * d + j] : 0.0;
     if (beg < end) {
@@ -699,7 +759,7 @@ __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict
                 if (lane < P.n) P.r = rec[((size_t)(w + c) * d + j) * KS_R + lane];
             } else {
 #pragma unroll
-                for (int k = 0; k < KS_W / 64; k++) P.v[k] = X[(int64_t)P.idx[k] * d + j];
+                for (int k = 0; k < KS_W / 64; k++) P.v[k] = (double)X[(int64_t)P.idx[k] * d + j];
             }
         };
         KsPair A, B, Cn;
@@ -755,7 +815,7 @@ __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict
                         int32_t ix = A.idx[0];
 #pragma unroll
                         for (int u = 1; u < KS_W / 64; u++) ix = u == k ? A.idx[u] : ix;   // registers, no scratch
-                        const double v = X[(int64_t)ix * d + j];
+                        const double v = (double)X[(int64_t)ix * d + j];
                         const int q0 = max(0, fa + 1 - 64 * k), q1 = min(64, fb2 + 1 - 64 * k);
                         for (int q = q0; q < q1; q++) s = __dadd_rn(s, ks_rl(v, q));
                     }
@@ -766,7 +826,7 @@ __global__ __launch_bounds__(64) void ks_compose_kernel(const double* __restrict
             B = Cn;
         }
     }
-    if (lane == 0) sums[(size_t)c * d + j] = s;
+    if (lane == 0 && (!mask || mask[(size_t)c * d + j])) sums[(size_t)c * d + j] = s;
 }
 
 static int64_t ks_pairs(int64_t M, int K) { return (M + KS_W - 1) / KS_W + K; }
@@ -776,30 +836,166 @@ size_t km_seg_ws_bytes(int64_t M, int K, int d) {
     return pd * (8 + 8 + 4) + 64 + pd * KS_R * sizeof(KsRaw);
 }
 
-// Exact-order sums of fp64 rows by segments (sums, counts as launch_km_chain).
-int launch_km_sums_seg(hipStream_t s, const double* X, int d, const int32_t* rows, const int64_t* crow, int K,
-                       int64_t M, double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts,
-                       void* ws) {
-    const size_t pd = (size_t)ks_pairs(M, K) * d;
-    char* b = reinterpret_cast<char*>(ws);
-    KsRaw* rec = reinterpret_cast<KsRaw*>(b);                 // 16-B aligned first
-    double* psum = reinterpret_cast<double*>(b + pd * KS_R * sizeof(KsRaw));
-    double* sin = psum + pd;
-    int32_t* cnt = reinterpret_cast<int32_t*>(sin + pd);
+// The segment workspace: records | pair sums | pair starts | record counts.
+struct KsWs {
+    KsRaw* rec;
+    double *psum, *sin;
+    int32_t* cnt;
+    KsWs(void* ws, int64_t M, int K, int d) {
+        const size_t pd = (size_t)ks_pairs(M, K) * d;
+        char* b = reinterpret_cast<char*>(ws);
+        rec = reinterpret_cast<KsRaw*>(b);                 // 16-B aligned first
+        psum = reinterpret_cast<double*>(b + pd * KS_R * sizeof(KsRaw));
+        sin = psum + pd;
+        cnt = reinterpret_cast<int32_t*>(sin + pd);
+    }
+};
+
+// Passes A-C: the pair sums, the pairs' approximate starts (from `start`, the
+// chains' approximate start values; NULL: 0) and the segment records. flag:
+// only the flagged (cluster, 64-dim block) chains (NULL: all).
+template <typename TX>
+static void km_seg_records(hipStream_t s, const TX* X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                           const double* start, const int* flag, const KsWs& w) {
     const int jb = (d + 63) / 64;
     const int64_t W = (M + KS_W - 1) / KS_W;
-    if (W > 0) {
-        hipLaunchKernelGGL(ks_sum_kernel, dim3((unsigned)W, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, M, psum);
-        hipLaunchKernelGGL(ks_scan_kernel, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, psum, crow, K, d, carry, sin);
-        hipLaunchKernelGGL(ks_seg_kernel, dim3((unsigned)W, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, M, sin,
-                           cnt, rec);
+    if (W <= 0) return;
+    hipLaunchKernelGGL(ks_sum_kernel<TX>, dim3((unsigned)W, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, M, w.psum,
+                       flag);
+    hipLaunchKernelGGL(ks_scan_kernel, dim3((unsigned)K, (unsigned)jb), dim3(64), 0, s, w.psum, crow, K, d, start, w.sin,
+                       flag);
+    hipLaunchKernelGGL(ks_seg_kernel<TX>, dim3((unsigned)W, (unsigned)jb), dim3(64), 0, s, X, d, rows, crow, K, M, w.sin,
+                       w.cnt, w.rec, flag);
+}
+
+// Pass D: the chains composed from `carry` (NULL: from 0); flag: only the
+// flagged chains; mask: written only where set (NULL: every dim of them).
+template <typename TX>
+static void km_seg_compose(hipStream_t s, const TX* X, int d, const int32_t* rows, const int64_t* crow, int K,
+                           const double* carry, const int* flag, const uint8_t* mask, const KsWs& w, double* sums) {
+    hipLaunchKernelGGL(ks_compose_kernel<TX>, dim3((unsigned)d, (unsigned)K), dim3(64), 0, s, X, d, rows, crow, K, carry,
+                       w.cnt, w.rec, sums, flag, mask);
+}
+
+// Exact-order sums by segments (sums, counts as launch_km_chain): every chain
+// of fp64 rows; with flag, only the chains the never-rounds test flagged (fp32
+// rows, after launch_km_sums_fx has written the others).
+int launch_km_sums_seg(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                       double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws,
+                       const int* flag) {
+    const KsWs w(ws, M, K, d);
+    if (X.f64) {
+        km_seg_records(s, X.d(), d, rows, crow, K, M, carry, flag, w);
+        km_seg_compose(s, X.d(), d, rows, crow, K, carry, flag, nullptr, w, sums);
+    } else {
+        km_seg_records(s, X.f(), d, rows, crow, K, M, carry, flag, w);
+        km_seg_compose(s, X.f(), d, rows, crow, K, carry, flag, nullptr, w, sums);
     }
-    hipLaunchKernelGGL(ks_compose_kernel, dim3((unsigned)d, (unsigned)K), dim3(64), 0, s, X, d, rows, crow, K, carry, cnt,
-                       rec, sums);
     if (counts)
         hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, carry_counts,
                            counts);
     return kstatus("update.hip (segmented)");
+}
+
+// ------------------------------------------------------------------ sharded form
+// The reference's chain over row shards (lshkm_kmeans_shard_*, include/lshkm.h):
+// every rank forms its partial sums by the parallel form above and reports its
+// values' q / t / sum |x|; after the exchange (partial sums gathered, q MIN, t
+// MAX, |x| sums and counts SUM) the never-rounds test runs on the GLOBAL values.
+// Where it passes, every partial sum of any subset of the chain's values, in
+// any order, is a double: each rank's partial is exact, and so is the total of
+// the gathered partials -- the chain's own result, whatever the order. Only the
+// chains that fail it need the rank-to-rank carry, and of those only the
+// composition of their segment records runs in rank order: the records are
+// formed on all ranks at once from each chain's approximate start on the rank
+// (the sum of the lower ranks' partials).
+__global__ void km_shard_split_kernel(const KmFx* __restrict__ acc, int64_t n, double* __restrict__ sums,
+                                      double* __restrict__ asum, int32_t* __restrict__ qt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const KmFx a = acc[i];
+    sums[i] = a.sum;
+    asum[i] = a.asum;
+    qt[i] = a.qmin;
+    qt[n + i] = -a.tmax;              // one MIN all-reduce for both
+}
+
+__global__ void km_shard_certify_kernel(const double* __restrict__ gathered, int world, int rank,
+                                        const double* __restrict__ asum, const int32_t* __restrict__ qt,
+                                        const int64_t* __restrict__ counts, int K, int d,
+                                        double* __restrict__ sums_out, double* __restrict__ start,
+                                        int* __restrict__ flag, uint8_t* __restrict__ mask,
+                                        unsigned long long* __restrict__ nflag) {
+    const int64_t n = (int64_t)K * d;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int c = (int)(i / d);
+    double tot = 0.0, pre = 0.0;
+    for (int r = 0; r < world; r++) {            // rank order (any order is exact where the test passes)
+        if (r == rank) pre = tot;
+        tot = __dadd_rn(tot, gathered[(size_t)r * n + i]);
+    }
+    const bool ok = km_cert(qt[i], -qt[n + i], counts[c], asum[i]);
+    if (start) start[i] = pre;
+    sums_out[i] = tot;                           // the chain's value where ok; the carry replaces the rest
+    mask[i] = ok ? 0 : 1;
+    if (!ok) atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));
+    const unsigned long long nb = __ballot(!ok);
+    if (nb && (threadIdx.x & 63) == __builtin_ctzll(nb)) atomicAdd(nflag, (unsigned long long)__popcll(nb));
+}
+
+int launch_km_shard_begin(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                          double* sums, double* asum, int32_t* qt, int64_t* counts, void* ws) {
+    KmFx* acc = reinterpret_cast<KmFx*>(ws);
+    const int64_t n = (int64_t)K * d;
+    hipLaunchKernelGGL(km_fx_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, n);
+    const int jb = (d + 63) / 64;
+    const dim3 fgrid((unsigned)((M + KMF_CH - 1) / KMF_CH), (unsigned)jb);
+    if (M > 0) {
+        if (X.f64) hipLaunchKernelGGL(km_fx_kernel<double>, fgrid, dim3(64), 0, s, X.d(), d, rows, crow, K, M, acc);
+        else if (d % 128 == 0)
+            hipLaunchKernelGGL(km_fx2_kernel, dim3(fgrid.x, (unsigned)(d / 128)), dim3(64), 0, s, X.f(), d, rows, crow, K, M,
+                               acc);
+        else hipLaunchKernelGGL(km_fx_kernel<float>, fgrid, dim3(64), 0, s, X.f(), d, rows, crow, K, M, acc);
+    }
+    hipLaunchKernelGGL(km_shard_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, n, sums, asum, qt);
+    hipLaunchKernelGGL(km_counts_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, crow, K, nullptr, counts);
+    return kstatus("update.hip (shard begin)");
+}
+
+int launch_km_shard_certify(hipStream_t s, const double* gathered, int world, int rank, const double* asum,
+                            const int32_t* qt, const int64_t* counts, int K, int d, double* sums_out, double* start,
+                            int* flag, uint8_t* mask, unsigned long long* nflag) {
+    const int64_t n = (int64_t)K * d;
+    if (hipMemsetAsync(flag, 0, (size_t)K * 4, s) != hipSuccess || hipMemsetAsync(nflag, 0, 8, s) != hipSuccess)
+        return kstatus("update.hip (shard certify memset)");
+    hipLaunchKernelGGL(km_shard_certify_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gathered, world, rank,
+                       asum, qt, counts, K, d, sums_out, start, flag, mask, nflag);
+    return kstatus("update.hip (shard certify)");
+}
+
+size_t km_shard_ws_bytes(int64_t M, int K, int d) {
+    return std::max((size_t)K * d * sizeof(KmFx) + 64, km_seg_ws_bytes(M, K, d));
+}
+
+// The flagged chains' segment records from their approximate starts on this
+// rank (passes A-C, carry-free: all ranks at once).
+int launch_km_shard_prepare(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                            const double* start, const int* flag, void* ws) {
+    const KsWs w(ws, M, K, d);
+    if (X.f64) km_seg_records(s, X.d(), d, rows, crow, K, M, start, flag, w);
+    else km_seg_records(s, X.f(), d, rows, crow, K, M, start, flag, w);
+    return kstatus("update.hip (shard prepare)");
+}
+
+// The flagged chains composed over this rank's rows from `carry` (the previous
+// rank's running sums; NULL on the first rank: from 0), written where mask is set.
+int launch_km_shard_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
+                          const int* flag, const uint8_t* mask, const double* carry, void* ws, double* sums) {
+    const KsWs w(ws, M, K, d);
+    if (X.f64) km_seg_compose(s, X.d(), d, rows, crow, K, carry, flag, mask, w, sums);
+    else km_seg_compose(s, X.f(), d, rows, crow, K, carry, flag, mask, w, sums);
+    return kstatus("update.hip (shard chain)");
 }
 
 // One wave per cluster: divide (unless empty), then the reference's movement

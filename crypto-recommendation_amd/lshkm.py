@@ -22,6 +22,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "lshkm.h")
 EUCLIDEAN, COSINE = 0, 1
 STAT_HASH_EXACT, STAT_ASSIGN_AMBIG, STAT_COS_FIX, STAT_REFINED, STAT_HASH_FIX, STAT_REC_SOFT = 0, 1, 4, 5, 6, 7
 STAT_POW_FIX = 8
+STAT_KM_SEQ = 9
 _METRIC = {"euclidean": EUCLIDEAN, "cosine": COSINE, EUCLIDEAN: EUCLIDEAN, COSINE: COSINE}
 DIST_CERTIFIED, DIST_EXACT = 0, 1
 _DIST = {"certified": DIST_CERTIFIED, "default": DIST_CERTIFIED, "exact": DIST_EXACT,
@@ -116,6 +117,12 @@ def lib():
             "lshkm_kmeans_partial_carry": (i32, [vp, vp, i64, i32, vp, i32, vp, vp, vp, vp]),
             "lshkm_kmeans_partial_csr": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp]),
             "lshkm_kmeans_finalize": (i32, [vp, vp, vp, i32, i32, vp, i32, f64, vp, C.POINTER(i32)]),
+            "lshkm_kmeans_shard_begin": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, vp]),
+            "lshkm_kmeans_shard_certify": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                 C.POINTER(i64)]),
+            "lshkm_kmeans_shard_ws_bytes": (i32, [i64, i32, i32, C.POINTER(i64)]),
+            "lshkm_kmeans_shard_prepare": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, i64]),
+            "lshkm_kmeans_shard_chain": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, vp, i64, vp]),
             "lshkm_kmeans_pp": (i32, [vp, vp, i64, i32, i32, i32, u64, vp]),
             "lshkm_rand_selection": (i32, [u64, i64, i32, vp]),
             "lshkm_p_closest": (i32, [vp, vp, i64, i32, vp, i64, vp, vp, i32, vp, vp, vp]),
@@ -130,6 +137,7 @@ def lib():
             "lshkm_cluster_chain_terms": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32,
                                                 vp]),
             "lshkm_synth": (i32, [vp, u64, i64, i64, i32, vp]),
+            "lshkm_synth_normal": (i32, [vp, u64, i64, i64, i32, vp]),
             "lshkm_clusters": (i32, [vp, vp, i64, i32, vp, vp]),
         }
         for name, (res, args) in sigs.items():
@@ -252,9 +260,12 @@ class Context:
     def empty(self, shape, dtype):
         return self.torch.empty(shape, dtype=dtype, device=self.dev)
 
-    def synth(self, seed, rows, d, row0=0):
+    def synth(self, seed, rows, d, row0=0, kind="grid"):
+        """include/lshkm_synth.h rows on the device: kind "grid" (the default,
+        2^-15 grid) or "normal" (Irwin-Hall(12), full fp32 mantissas)."""
         X = self.empty((rows, d), self.torch.float32)
-        _ck(lib().lshkm_synth(self.h, seed, row0, rows, d, _t_ptr(X)))
+        fn = {"grid": lib().lshkm_synth, "normal": lib().lshkm_synth_normal}[kind]
+        _ck(fn(self.h, seed, row0, rows, d, _t_ptr(X)))
         return X
 
 
@@ -564,6 +575,62 @@ def kmeans_partial_carry(ctx, X, assign, K, carry_sums=None, carry_counts=None):
                                          _t_ptr(carry_counts) if carry_counts is not None else None,
                                          _t_ptr(sums), _t_ptr(counts)))
     return sums, counts
+
+
+class ShardSums:
+    """One rank's part of the sharded exact k-means sums (lshkm_kmeans_shard_*,
+    include/lshkm.h): X this rank's rows, csr = (crow, rows) of its assignment
+    (clusters()). sharding.kmeans_sums_sharded runs the exchange between the
+    calls; every method works on device tensors."""
+
+    def __init__(self, ctx, X, csr, K):
+        self.ctx, self.X, self.csr, self.K = ctx, X, csr, K
+        self.N, self.d = X.shape
+        self.ws = None
+
+    def empty(self, shape, dtype):
+        return self.ctx.empty(shape, dtype)
+
+    def begin(self):
+        """-> (sums [K][d], asum [K][d], qt [2][K][d] int32, counts [K]): this rank's partials."""
+        torch, K, d = self.ctx.torch, self.K, self.d
+        sums, asum = self.empty((K, d), torch.float64), self.empty((K, d), torch.float64)
+        qt, counts = self.empty((2, K, d), torch.int32), self.empty((K,), torch.int64)
+        _ck(_fn("lshkm_kmeans_shard_begin", self.X)(self.ctx.h, _t_ptr(self.X), self.N, d, _t_ptr(self.csr[0]),
+                                                    _t_ptr(self.csr[1]), K, _t_ptr(sums), _t_ptr(asum), _t_ptr(qt),
+                                                    _t_ptr(counts)))
+        return sums, asum, qt, counts
+
+    def certify(self, gathered, asum, qt, counts, world, rank):
+        """-> (sums_out, start, flag, mask, n_flagged) from the exchanged values."""
+        torch, K, d = self.ctx.torch, self.K, self.d
+        out, start = self.empty((K, d), torch.float64), self.empty((K, d), torch.float64)
+        flag, mask = self.empty((K,), torch.int32), self.empty((K, d), torch.uint8)
+        nf = C.c_int64()
+        _ck(lib().lshkm_kmeans_shard_certify(self.ctx.h, K, d, world, rank, _t_ptr(gathered), _t_ptr(asum),
+                                             _t_ptr(qt), _t_ptr(counts), _t_ptr(out), _t_ptr(start), _t_ptr(flag),
+                                             _t_ptr(mask), C.byref(nf)))
+        return out, start, flag, mask, int(nf.value)
+
+    def _ws(self):
+        nb = C.c_int64()
+        _ck(lib().lshkm_kmeans_shard_ws_bytes(self.N, self.K, self.d, C.byref(nb)))
+        if self.ws is None or self.ws.numel() < nb.value:
+            self.ws = self.empty((int(nb.value),), self.ctx.torch.uint8)
+        return self.ws
+
+    def prepare(self, start, flag):
+        ws = self._ws()
+        _ck(_fn("lshkm_kmeans_shard_prepare", self.X)(self.ctx.h, _t_ptr(self.X), self.N, self.d, _t_ptr(self.csr[0]),
+                                                      _t_ptr(self.csr[1]), self.K, _t_ptr(start), _t_ptr(flag),
+                                                      _t_ptr(ws), ws.numel()))
+
+    def chain(self, flag, mask, carry, sums):
+        ws = self._ws()
+        _ck(_fn("lshkm_kmeans_shard_chain", self.X)(self.ctx.h, _t_ptr(self.X), self.N, self.d, _t_ptr(self.csr[0]),
+                                                    _t_ptr(self.csr[1]), self.K, _t_ptr(flag), _t_ptr(mask),
+                                                    _t_ptr(carry) if carry is not None else None, _t_ptr(ws),
+                                                    ws.numel(), _t_ptr(sums)))
 
 
 def kmeans_finalize(ctx, sums, counts, C_old, metric="euclidean", min_dist=0.0):

@@ -8,8 +8,11 @@ row index. With contiguous row shards [row0, row0 + n) in rank order:
     per-shard results in shard order;
   - a hypercube query's result is, slot by slot (main bucket, then each probe
     bucket), the concatenation of the shards' members of that bucket;
-  - k-means centers need the per-cluster sums: one all-reduce of K x d fp64 sums
-    and K counts (fast mode; the exact-order chain would serialize the shards).
+  - k-means centers need the per-cluster sums, which the reference forms as ONE
+    sequential chain per (cluster, dim) in row order: kmeans_sums_sharded gets
+    that chain's value bit for bit from one all-gather of the K x d partial sums
+    plus three all-reduces, wherever the chain provably never rounds (the global
+    never-rounds test), and carries only the other chains rank to rank.
 Host logic (numpy + torch.distributed); the compute is the HIP library.
 Collectives: RCCL ("nccl") on GPU tensors; with the gloo backend (CPU tests,
 or several ranks sharing one GPU) device tensors are staged through host
@@ -161,6 +164,73 @@ def chain_partials(local_fn, sums_like, counts_like):
     return sums, counts
 
 
+def _all_gather_rows(dist, t):
+    """[world, *t.shape] tensor of every rank's t, in rank order, on t's device."""
+    world = dist.get_world_size()
+    if t.is_cuda and dist.get_backend() != "gloo":
+        out = t.new_empty((world,) + tuple(t.shape))
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+    h = t.cpu()
+    parts = [h.new_empty(h.shape) for _ in range(world)]
+    dist.all_gather(parts, h)
+    import torch
+    return torch.stack(parts).to(t.device)
+
+
+def kmeans_sums_sharded(ops, timing=None):
+    """The reference's k-means sums (update.hpp:45-58: one sequential fp64 chain
+    per (cluster, dim) over ALL rows in row order) from row shards, bit for bit,
+    at all-reduce cost (lshkm_kmeans_shard_*, include/lshkm.h):
+      1. ops.begin(): this rank's partial sums (any order), sums of |x|, the
+         values' lowest / top bit positions, counts;
+      2. all-gather the partial sums; all-reduce |x| sums and counts (SUM) and
+         the bit positions (MIN) -- 1 + 3 collectives of ~K*d*8 bytes;
+      3. ops.certify(): the never-rounds test on the GLOBAL values. Where it
+         holds (every chain of the 2^-15-grid bench data; ~95 % of the chains of
+         10K N(0,1) fp32 values), any order of fp64 adds is exact: the gathered
+         partials' total IS the chain. The rest are flagged, identically on
+         every rank;
+      4. only if some chain is flagged: ops.prepare() forms their segment
+         records on every rank at once, then ops.chain() composes them in rank
+         order from the previous rank's running sums (point-to-point), and the
+         last rank broadcasts the result.
+    ops: lshkm.ShardSums (or a restatement with the same methods). Returns
+    (sums, counts): the chains' values and the global counts, on every rank.
+    timing: optional dict that receives the flagged-chain count."""
+    dist = _dist()
+    world, rank = (dist.get_world_size(), dist.get_rank()) if dist is not None else (1, 0)
+    sums, asum, qt, counts = ops.begin()
+    if dist is not None:
+        gathered = _all_gather_rows(dist, sums)
+        for t, op in ((asum, dist.ReduceOp.SUM), (counts, dist.ReduceOp.SUM), (qt, dist.ReduceOp.MIN)):
+            b, back = _staged(dist, t)
+            dist.all_reduce(b, op=op)
+            back()
+    else:
+        gathered = sums.reshape((1,) + tuple(sums.shape))
+    out, start, flag, mask, n_flagged = ops.certify(gathered, asum, qt, counts, world, rank)
+    if timing is not None:
+        timing["flagged"] = n_flagged
+    if n_flagged:
+        ops.prepare(start, flag)            # carry-free: every rank at once
+        carry = None
+        if rank > 0:
+            carry = ops.empty(tuple(out.shape), out.dtype)
+            b, back = _staged(dist, carry)
+            dist.recv(b, src=rank - 1)
+            back()
+        ops.chain(flag, mask, carry, out)
+        if dist is not None:
+            if rank + 1 < world:
+                b, _ = _staged(dist, out)
+                dist.send(b, dst=rank + 1)
+            b, back = _staged(dist, out)
+            dist.broadcast(b, src=world - 1)
+            back()
+    return out, counts
+
+
 def allreduce_partials(sums, counts):
     """Sum the per-shard (sums, counts) over all ranks in place (RCCL on GPUs, gloo on CPU)."""
     dist = _dist()
@@ -282,16 +352,22 @@ class ShardedLloyd:
     LSH hashing riding on the assignment pass): per step, on the rank's
     resident rows,
       lshkm_hash_assign   -- L x k hashes + bucket IDs + argmin over K centroids
-      lshkm_kmeans_partial (fast) / _partial_carry (exact) -- per-cluster sums
-      all-reduce of the K x d sums and K counts over RCCL (fast mode), or the
-        rank-to-rank carry chain (exact mode, the reference's sums bit for bit)
+      lshkm_clusters      -- the cluster CSR (shared with the recommend step)
+      the k-means sums    -- mode "certified" (default): kmeans_sums_sharded,
+        the reference's chains bit for bit at all-reduce cost over RCCL; mode
+        "carry": every chain carried rank to rank (lshkm_kmeans_partial_carry,
+        the shards' updates in series; kept as the cross-check)
       lshkm_kmeans_finalize -- means, the reference's continue test
     and the centers are replaced when k_means would replace them
     (update.hpp:63-80). X: this rank's rows [row0, row0 + n) of N_total."""
 
-    def __init__(self, lk, ctx, lsh, X, C0, src_rows, mode="fast", metric="euclidean", min_dist=0.0):
+    MODES = ("certified", "carry")
+
+    def __init__(self, lk, ctx, lsh, X, C0, src_rows, mode="certified", metric="euclidean", min_dist=0.0):
         torch = ctx.torch
         self.lk, self.ctx, self.lsh, self.X = lk, ctx, lsh, X
+        if mode not in self.MODES:
+            raise ValueError(f"unknown mode {mode!r} (one of {self.MODES})")
         self.mode, self.metric, self.min_dist = mode, metric, float(min_dist)
         n = X.shape[0]
         self.K, self.d = C0.shape
@@ -308,7 +384,8 @@ class ShardedLloyd:
         self.sums = e((self.K, self.d), torch.float64)
         self.counts = e((self.K,), torch.int64)
         self.cont = True
-        self.timing = False       # True: HIP events around the exchange (bench.py's breakdown)
+        self.timing = False       # True: HIP events around the sums + exchange (bench.py's breakdown)
+        self.flagged = 0          # chains the last step's global never-rounds test flagged
         self.exchange_events = []
         self.recom = None         # enable_recommend(): the C5 recommend step after each update
         self.csr = None           # (crow, crows) of this iteration's assignment (recommend runs)
@@ -327,19 +404,20 @@ class ShardedLloyd:
                                                          None, p(self.bucket), p(self.assign), p(self.dist)))
         else:
             lk.lloyd_assign(ctx, X, self.C, self.metric, self.src, self.assign, self.dist)
-        if self.mode == "exact":
+        if self.mode == "carry":
             def local(cs, cc):
                 return lk.kmeans_partial_carry(ctx, X, self.assign, self.K, cs, cc)
             sums, counts = chain_partials(local, self.sums, self.counts)
-        else:
-            # with the recommend step, the cluster CSR of this assignment is built
-            # once and serves both the sums and the recommender
             self.csr = lk.clusters(ctx, self.assign, self.K) if self.recom is not None else None
-            sums, counts = lk.kmeans_partial(ctx, X, self.assign, self.K, self.sums, self.counts, csr=self.csr)
+        else:
+            # the cluster CSR of this assignment serves the sums and the recommender
+            self.csr = lk.clusters(ctx, self.assign, self.K)
             if self.timing:
                 ev = [ctx.torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 ev[0].record()
-            allreduce_partials(sums, counts)
+            info = {}
+            sums, counts = kmeans_sums_sharded(lk.ShardSums(ctx, X, self.csr, self.K), timing=info)
+            self.flagged = info.get("flagged", 0)
             if self.timing:
                 ev[1].record()
                 self.exchange_events.append(ev)
@@ -378,8 +456,9 @@ class ShardedLloyd:
         return self.recom_out
 
     def exchange_ms(self):
-        """Mean all-reduce time (ms) over the timed steps (torch's stream, which
-        the library context and RCCL share), then forget them."""
+        """Mean time (ms) of the sums and their exchange (kmeans_sums_sharded)
+        over the timed steps (torch's stream, which the library context and RCCL
+        share), then forget them."""
         if not self.exchange_events:
             return None
         self.ctx.torch.cuda.synchronize(self.ctx.dev)

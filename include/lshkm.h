@@ -127,7 +127,9 @@ int lshkm_memcpy_d2h(lshkm_ctx ctx, void* dst_host, const void* src_dev, int64_t
  * 6 = rows the fused pass listed for the hash fix-up,
  * 7 = clustering-recommender similarities decided by the x87 chain (lshkm_cluster_top_n),
  * 8 = euclidean winner distances (LSHKM_DIST_EXACT, hi-only pass) whose chain met an
- *     inexact square and were redone with glibc's pow(x, 2) (gpow2.h). */
+ *     inexact square and were redone with glibc's pow(x, 2) (gpow2.h),
+ * 9 = k-means (cluster, dim) sums of fp32 rows whose never-rounds test failed,
+ *     i.e. that took a rounding-aware chain instead of plain fp64 adds. */
 int lshkm_get_stat(lshkm_ctx ctx, int which, int64_t* value_host);
 int lshkm_reset_stats(lshkm_ctx ctx);
 /* HIP-event timing of the dominant kernel launch (the fused hash+assign kernel)
@@ -316,6 +318,57 @@ int lshkm_kmeans_partial_carry(lshkm_ctx ctx, const float* X_dev, int64_t N, int
 int lshkm_kmeans_partial_carry_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d,
                                    const int32_t* assign_dev, int K, const double* carry_sums_dev,
                                    const int64_t* carry_counts_dev, double* sums_dev, int64_t* counts_dev);
+/* Sharded update, bit-exact at all-reduce cost (the reference's
+ * one sequential chain per (c, j), update.hpp:45-58, over row shards in rank
+ * order). crow_dev / rows_dev: this rank's cluster CSR (lshkm_clusters).
+ *  1. lshkm_kmeans_shard_begin: this rank's per-(c, j) partial sums (any
+ *     order) sums_dev [K][d], the sums of |x| asum_dev [K][d], qt_dev [2][K][d]
+ *     int32 (the lowest set-bit exponent of the values, then minus the top
+ *     bit position), counts_dev [K].
+ *  2. exchange: all-gather sums_dev in rank order into gathered [world][K][d];
+ *     all-reduce asum_dev and counts_dev (SUM) and qt_dev (MIN).
+ *  3. lshkm_kmeans_shard_certify (identical on every rank): per (c, j) the
+ *     never-rounds test on the global values. Where it holds, every partial sum
+ *     of any subset of the chain's values in any order is a double, so the
+ *     total of the gathered partials IS the reference's chain: sums_out_dev.
+ *     Elsewhere mask_dev [K][d] = 1 and flag_dev [K] has bit min(31, j / 64)
+ *     set; start_dev [K][d] (may be NULL) = the chain's approximate value
+ *     before this rank's rows (the lower ranks' partials); *n_flagged_host =
+ *     the number of (c, j) masked (the same on every rank).
+ *  4. only when *n_flagged_host > 0: lshkm_kmeans_shard_prepare (the masked
+ *     chains' binade-segment records from start_dev; all ranks at once), then
+ *     in rank order lshkm_kmeans_shard_chain: the masked chains continued over
+ *     this rank's rows from the previous rank's sums_out (carry_dev; NULL on
+ *     rank 0), written into sums_dev where mask_dev is set; send sums_dev on.
+ *     The last rank's sums_dev holds every chain's result: broadcast it.
+ * ws_dev (prepare / chain; the same buffer for both): at least
+ * lshkm_kmeans_shard_ws_bytes bytes, holding the records between the calls.
+ * Then lshkm_kmeans_finalize on the totals and the all-reduced counts. One
+ * rank (world 1) is the single-GPU update. sharding.kmeans_sums_sharded runs
+ * the protocol over torch.distributed (RCCL on GPUs). */
+int lshkm_kmeans_shard_begin(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                             const int32_t* rows_dev, int K, double* sums_dev, double* asum_dev, int32_t* qt_dev,
+                             int64_t* counts_dev);
+int lshkm_kmeans_shard_begin_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                                 const int32_t* rows_dev, int K, double* sums_dev, double* asum_dev, int32_t* qt_dev,
+                                 int64_t* counts_dev);
+int lshkm_kmeans_shard_certify(lshkm_ctx ctx, int K, int d, int world, int rank, const double* gathered_dev,
+                               const double* asum_dev, const int32_t* qt_dev, const int64_t* counts_dev,
+                               double* sums_out_dev, double* start_dev, int32_t* flag_dev, uint8_t* mask_dev,
+                               int64_t* n_flagged_host);
+int lshkm_kmeans_shard_ws_bytes(int64_t N, int K, int d, int64_t* bytes_host);
+int lshkm_kmeans_shard_prepare(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                               const int32_t* rows_dev, int K, const double* start_dev, const int32_t* flag_dev,
+                               void* ws_dev, int64_t ws_bytes);
+int lshkm_kmeans_shard_prepare_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                                   const int32_t* rows_dev, int K, const double* start_dev, const int32_t* flag_dev,
+                                   void* ws_dev, int64_t ws_bytes);
+int lshkm_kmeans_shard_chain(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                             const int32_t* rows_dev, int K, const int32_t* flag_dev, const uint8_t* mask_dev,
+                             const double* carry_dev, void* ws_dev, int64_t ws_bytes, double* sums_dev);
+int lshkm_kmeans_shard_chain_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int64_t* crow_dev,
+                                 const int32_t* rows_dev, int K, const int32_t* flag_dev, const uint8_t* mask_dev,
+                                 const double* carry_dev, void* ws_dev, int64_t ws_bytes, double* sums_dev);
 int lshkm_kmeans_finalize(lshkm_ctx ctx, const double* sums_dev, const int64_t* counts_dev, int K, int d,
                           const double* C_old_dev, int metric, double min_dist, double* C_new_dev,
                           int* cont_host);
@@ -542,6 +595,9 @@ int lshkm_config_load(const char* path, lshkm_config* out);
 /* ------------------------------------------------------------ synthetic data */
 /* include/lshkm_synth.h generator, rows [row0, row0+rows) into X_dev. */
 int lshkm_synth(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X_dev);
+/* The "normal" generator of include/lshkm_synth.h (Irwin-Hall(12), full fp32
+ * mantissas; SURVEY.md §8d's N(0,1) rows), rows [row0, row0+rows) into X_dev. */
+int lshkm_synth_normal(lshkm_ctx ctx, uint64_t seed, int64_t row0, int64_t rows, int d, float* X_dev);
 
 #ifdef __cplusplus
 }

@@ -40,4 +40,26 @@ LSHKM_HD float lshkm_synth_value(uint64_t seed, uint64_t row, uint64_t d, uint64
     return (float)s * (1.0f / 32768.0f);
 }
 
+/*
+ * The "normal" generator (fp32 i.i.d. N(0,1) rows, full
+ * mantissas): Irwin-Hall(12) -- the sum of twelve uniforms minus 6, mean 0,
+ * variance exactly 1, the classic normal approximation (tails end at +-6) --
+ * over 40-bit uniforms, so the sum is an integer of ~44 bits:
+ *
+ *   base = seed * 0x9E3779B97F4A7C15 + (row * d + col) * 12        (mod 2^64)
+ *   S    = sum_{k<12} (splitmix64(base + k) >> 24)  -  6 * 2^40
+ *   x    = (float)S * 2^-40          (one correctly rounded int64 -> fp32)
+ *
+ * Every value with |x| >= 2^-20 has a full 24-bit mantissa (the grid generator
+ * above has <= 18 significant bits), so differences, squares and the f16
+ * hi/lo splits are those of general fp32 data. Integer-only up to the one
+ * rounding: gcc, numpy and the device give the same bits.
+ */
+LSHKM_HD float lshkm_synth_normal_value(uint64_t seed, uint64_t row, uint64_t d, uint64_t col) {
+    const uint64_t base = seed * 0x9E3779B97F4A7C15ull + (row * d + col) * 12ull;
+    int64_t s = -(int64_t)(6ull << 40);
+    for (int k = 0; k < 12; k++) s += (int64_t)(lshkm_splitmix64(base + (uint64_t)k) >> 24);
+    return (float)s * (1.0f / 1099511627776.0f);     /* 2^-40, exact */
+}
+
 #endif /* LSHKM_SYNTH_H */

@@ -626,6 +626,13 @@ void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out) {
         for (int j = 0; j < d; j++) out[i * d + j] = lshkm_synth_value(seed, (uint64_t)(row0 + i), (uint64_t)d, (uint64_t)j);
 }
 
+void or_synth_normal(uint64_t seed, int64_t row0, int64_t rows, int d, float* out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < rows; i++)
+        for (int j = 0; j < d; j++)
+            out[i * d + j] = lshkm_synth_normal_value(seed, (uint64_t)(row0 + i), (uint64_t)d, (uint64_t)j);
+}
+
 /* ---------------------------------------------------------- range assignment */
 
 /* find_min_vector_distance (utils.hpp:161-178) over the centroid rows: pairs

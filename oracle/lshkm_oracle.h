@@ -109,6 +109,7 @@ void or_cluster_top_n(int d, const double* X, const double* x_mean, const int64_
 
 /* ---- synthetic points (include/lshkm_synth.h) */
 void or_synth(uint64_t seed, int64_t row0, int64_t rows, int d, float* out);
+void or_synth_normal(uint64_t seed, int64_t row0, int64_t rows, int d, float* out);
 
 #ifdef __cplusplus
 }

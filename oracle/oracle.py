@@ -62,6 +62,7 @@ def lib():
             "or_cluster_top_n": (None, [C.c_int, f64p, f64p, i64p, i32p, C.c_int64, f64p, f64p, i32p, i64p, i32p,
                                         C.c_int, i32p]),
             "or_synth": (None, [C.c_uint64, C.c_int64, C.c_int64, C.c_int, f32p]),
+            "or_synth_normal": (None, [C.c_uint64, C.c_int64, C.c_int64, C.c_int, f32p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -80,10 +81,30 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
-def synth(seed, rows, d, row0=0):
+def synth(seed, rows, d, row0=0, kind="grid"):
+    """include/lshkm_synth.h: kind "grid" (Irwin-Hall(4) on a 2^-15 grid) or
+    "normal" (Irwin-Hall(12), full fp32 mantissas)."""
     out = np.empty((rows, d), np.float32)
-    lib().or_synth(seed, row0, rows, d, out)
+    (lib().or_synth_normal if kind == "normal" else lib().or_synth)(seed, row0, rows, d, out)
     return out
+
+
+def synth_normal_np(seed, rows, d, row0=0):
+    """The "normal" generator restated in numpy (uint64 arithmetic), a second
+    producer of the same bits."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        e = (np.arange(rows, dtype=np.uint64)[:, None] + np.uint64(row0)) * np.uint64(d) + np.arange(d, dtype=np.uint64)
+        base = np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + e * np.uint64(12)
+        s = np.full(base.shape, -(6 << 40), np.int64)
+        for k in range(12):
+            x = base + np.uint64(k) + np.uint64(0x9E3779B97F4A7C15)
+            x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            x = x ^ (x >> np.uint64(31))
+            s += (x >> np.uint64(24)).astype(np.int64)
+    del M
+    return (s.astype(np.float32) * np.float32(2.0 ** -40)).astype(np.float32)
 
 
 def gen_lsh_euclid(seed, L, k, d, w):

@@ -4,11 +4,16 @@ Not a test module: launched as `python tests/mr_worker.py RANK WORLD PORT OUTDIR
 (several ranks sharing the one MI355X over gloo, or one rank with WORLD = 1 for
 the single-process reference). Runs liblshkm on this rank's contiguous row
 shard (crypto-recommendation_amd/sharding.py): the C5 iteration at C5's K = 1024
-(hash + assign -- the hashing multi-pass fused form -- + k-means update) in fast
-(all-reduce) and exact (carry chain) mode, one cosine iteration (cosine index +
-cosine Lloyd in one pass), and the sharded euclidean hypercube build; saves
-everything to OUTDIR/rank<R>.npz. DIST: the context's distance mode
-("certified", the default, or "exact"; lshkm_ctx_set_dist_mode)."""
+(hash + assign -- the hashing multi-pass fused form -- + k-means update) in the
+certified mode (kmeans_sums_sharded: the global never-rounds test, only flagged
+chains carried) and the carry mode (every chain carried rank to rank), three
+Lloyd + k-means iterations each on general rows -- full-mantissa fp32
+(include/lshkm_synth.h "normal"), fp32 rows of a wide dynamic range (chains
+that round, so the carry runs), fp64 doubles (segment records on every rank,
+composition in rank order) -- one cosine iteration (cosine index + cosine Lloyd
+in one pass), and the sharded euclidean hypercube build; saves everything to
+OUTDIR/rank<R>.npz. DIST: the context's distance mode ("certified", the
+default, or "exact"; lshkm_ctx_set_dist_mode)."""
 import os
 import sys
 
@@ -24,7 +29,20 @@ from amd import PKG, lshkm  # noqa: E402
 sys.path.insert(0, PKG)
 import sharding as sh  # noqa: E402
 
-N_TOTAL, D, L, KF, K, STEPS = 120_000, 128, 5, 4, 1024, 2
+N_TOTAL, D, L, KF, K, STEPS = 120_000, 128, 5, 4, 1024, 3
+
+
+def general_rows(kind, row0, n):
+    """This rank's rows of a general-row leg (deterministic over the whole job)."""
+    rng = np.random.default_rng({"wide": 41, "f64": 42}[kind])
+    if kind == "wide":
+        # per-element scales 10^-8 .. 10^5 mix magnitudes inside every chain:
+        # the chains round, the global test flags them and the carry runs
+        X = rng.standard_normal((N_TOTAL, 96)) * 10.0 ** rng.integers(-8, 6, size=(N_TOTAL, 96))
+        X = X.astype(np.float32)
+    else:
+        X = rng.standard_normal((N_TOTAL, 100)) * np.exp(rng.uniform(-2, 2, size=(N_TOTAL, 1)))
+    return np.ascontiguousarray(X[row0:row0 + n])
 
 
 def main():
@@ -43,15 +61,15 @@ def main():
     rows = sh.centroid_rows(N_TOTAL, K)
     C0 = torch.stack([ctx.synth(0x5EED, 1, D, row0=int(rw))[0] for rw in rows]).double()
     res = {}
-    for mode in ("fast", "exact"):
+    for mode in ("certified", "carry"):
         it = sh.ShardedLloyd(lshkm, ctx, lsh, X, C0, sh.local_src_rows(rows, row0, n), mode=mode)
-        if mode == "fast":
+        if mode == "certified":
             # C5's recommend step: 96 users over the whole job, their whole clusters
             # (the prediction sums carried rank to rank, sharding.recommend_sharded)
             it.enable_recommend(N_TOTAL, row0, Q=96, n_top=5)
         for s in range(STEPS):
             it.step()
-            if mode == "fast":
+            if mode == "certified":
                 res[f"recom{s}"] = it.recom_out.cpu().numpy()
                 res[f"recom_ucl{s}"] = it.recom_ucl.cpu().numpy()
             res[f"{mode}_assign{s}"] = it.assign.cpu().numpy()
@@ -60,10 +78,30 @@ def main():
             res[f"{mode}_cont{s}"] = np.array([it.cont])
         res[f"{mode}_tuples"] = it.tuples.cpu().numpy()
         res[f"{mode}_bucket"] = it.bucket.cpu().numpy()
+    # general rows: 3 Lloyd + k-means iterations per leg, both modes
+    for leg, Kg in (("normal", 64), ("wide", 48), ("f64", 32)):
+        if leg == "normal":
+            Xg = ctx.synth(0x5EED, n, D, row0=row0, kind="normal")
+            full = ctx.synth(0x5EED, N_TOTAL, D, kind="normal")
+        else:
+            Xg = ctx.torch.from_numpy(general_rows(leg, row0, n)).to(ctx.dev)
+            full = ctx.torch.from_numpy(general_rows(leg, 0, N_TOTAL)).to(ctx.dev)
+        grows = sh.centroid_rows(N_TOTAL, Kg)
+        Cg = full[ctx.torch.from_numpy(grows).to(ctx.dev)].double()
+        del full
+        for mode in ("certified", "carry"):
+            it = sh.ShardedLloyd(lshkm, ctx, None, Xg, Cg, sh.local_src_rows(grows, row0, n), mode=mode)
+            for s in range(STEPS):
+                it.step()
+                res[f"{leg}_{mode}_assign{s}"] = it.assign.cpu().numpy()
+                res[f"{leg}_{mode}_centers{s + 1}"] = it.C.cpu().numpy()
+                res[f"{leg}_{mode}_cont{s}"] = np.array([it.cont])
+                if mode == "certified":
+                    res[f"{leg}_flagged{s}"] = np.array([it.flagged])
     # cosine: CosineGGen buckets + cosine Lloyd (lshkm_hash_assign_metric), fast mode
     R, _ = lshkm.params_lsh_cosine(321, L, KF, D)
     clsh = lshkm.LSH(ctx, "cosine", D, KF, L, R=R)
-    it = sh.ShardedLloyd(lshkm, ctx, clsh, X, C0, sh.local_src_rows(rows, row0, n), mode="fast", metric="cosine")
+    it = sh.ShardedLloyd(lshkm, ctx, clsh, X, C0, sh.local_src_rows(rows, row0, n), mode="certified", metric="cosine")
     it.step()
     res.update(cos_assign0=it.assign.cpu().numpy(), cos_dist0=it.dist.cpu().numpy(),
                cos_bucket=it.bucket.cpu().numpy(), cos_centers1=it.C.cpu().numpy())

@@ -243,9 +243,9 @@ def test_c5_shard_full_size(ctx):
     X64 = oracle.rows64(Xh)
     del Xh
     Cn_o, cnt_o, cont_o = oracle.kmeans_update(X64, assign_h, Cc.cpu().numpy(), "euclidean", 0.0)
-    for kmode in ("fast", "exact"):
+    for kmode in ("certified", "carry"):
         it = sh.ShardedLloyd(lshkm, ctx, lsh, X, Cc, src, mode=kmode)
-        if kmode == "fast":
+        if kmode == "certified":
             # bench.py at one GPU: the job is this shard (users = rows i * floor(N / 1024))
             it.enable_recommend(N, 0, Q=1024, n_top=5)
         cont = it.step()
@@ -254,7 +254,7 @@ def test_c5_shard_full_size(ctx):
         assert np.array_equal(it.last_counts.cpu().numpy(), cnt_o), kmode
         assert cont == cont_o
         assert np.array_equal(it.C.cpu().numpy().view(np.uint64), Cn_o.view(np.uint64)), kmode
-        if kmode == "fast":
+        if kmode == "certified":
             r = it.recom
             ucl = it.recom_ucl.cpu().numpy()
             assert np.array_equal(ucl, assign_h[r["rows"]])

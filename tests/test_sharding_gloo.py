@@ -166,3 +166,55 @@ def test_shard_ranges_cover_rows():
         assert spans[0][0] == 0 and sum(n for _, n in spans) == n_total
         for (a0, an), (b0, _) in zip(spans, spans[1:]):
             assert a0 + an == b0
+
+
+def _certified_worker(rank, world, port, kind, N, d, K, out_path):
+    """kmeans_sums_sharded (the certified all-reduce: global never-rounds test,
+    only flagged chains carried) with the numpy restatement of the per-rank
+    calls (tests/km_shard_np.py)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    oracle, sh = _imports()
+    from km_shard_np import NumpyShardSums
+    Xall, a_all = _general_rows(oracle, kind, N, d, K)
+    row0, n = sh.shard_range(N, world, rank)
+    info = {}
+    sums, cnt = sh.kmeans_sums_sharded(NumpyShardSums(Xall[row0:row0 + n], a_all[row0:row0 + n], K), timing=info)
+    np.savez(out_path + f".{rank}.npz", sums=sums.numpy(), cnt=cnt.numpy(), flagged=info["flagged"])
+    dist.destroy_process_group()
+
+
+def _general_rows(oracle, kind, N, d, K):
+    rng = np.random.default_rng(77)
+    if kind == "grid":
+        X = oracle.synth(0x5EED ^ 5, N, d)                          # every chain passes the test
+    elif kind == "normal":
+        X = oracle.synth(0x5EED ^ 5, N, d, kind="normal")
+    elif kind == "wide":
+        X = (rng.standard_normal((N, d)) * 10.0 ** rng.integers(-9, 7, size=(N, d))).astype(np.float32)
+    else:                                                           # fp64 doubles
+        X = rng.standard_normal((N, d)) * np.exp(rng.uniform(-3, 3, size=(N, 1)))
+    a = (np.arange(N) * 7919 + 13) % K
+    a[: N // 3] = 2                                                 # one big cluster
+    a[a == 4] = 5                                                   # an empty one
+    return X, a
+
+
+@pytest.mark.parametrize("kind", ["grid", "normal", "wide", "f64"])
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_certified_sharded_sums_match_sequential(kind, world, tmp_path):
+    N, d, K = 3001, 70, 9
+    out = str(tmp_path / "cert")
+    mp.spawn(_certified_worker, args=(world, _free_port(), kind, N, d, K, out), nprocs=world, join=True)
+    oracle, _ = _imports()
+    Xall, a_all = _general_rows(oracle, kind, N, d, K)
+    es, ec = _seq_partials(Xall.astype(np.float64), a_all, K)
+    res = [np.load(out + f".{r}.npz") for r in range(world)]
+    for r in res:                                                   # every rank: the sequential chain, bit for bit
+        assert np.array_equal(r["cnt"], ec)
+        assert np.array_equal(r["sums"].view(np.uint64), es.view(np.uint64))
+        assert int(r["flagged"]) == int(res[0]["flagged"])
+    if kind == "grid":
+        assert int(res[0]["flagged"]) == 0
+    if kind in ("wide", "f64"):
+        assert int(res[0]["flagged"]) > 0                           # the carry ran

@@ -15,7 +15,7 @@ lsh = lk.LSH(ctx, 'euclidean', D, 4, 5, N // 100, 0.4, V=V, t=t, r=r)
 rows = sh.centroid_rows(N, K)
 Cc = torch.empty((K, D), dtype=torch.float64, device=dev)
 for i, row in enumerate(rows): Cc[i] = ctx.synth(0x5EED, 1, D, row0=int(row))[0].double()
-it = sh.ShardedLloyd(lk, ctx, lsh, X, Cc, sh.local_src_rows(rows, 0, N), mode='fast')
+it = sh.ShardedLloyd(lk, ctx, lsh, X, Cc, sh.local_src_rows(rows, 0, N), mode='certified')
 it.enable_recommend(N, 0, Q=1024, n_top=5)
 it.recom_timing = []
 for s in range(5):

@@ -13,6 +13,17 @@ for step in "$@"; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1
       rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { echo "tests rc=$rc"; exit $rc; } ;;
+    pyt)
+      # a subset: TESTS="tests/test_a.py tests/test_b.py::name" tools/gpu_run.sh TAG pyt
+      timeout -k 10 900 python -u -m pytest ${TESTS:?TESTS} -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pyt.log" 2>&1
+      rc=$?; tail -3 "$OUT/pyt.log"; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" "$OUT/pyt.log" | head -20; echo "pyt rc=$rc"; exit $rc; } ;;
+    profn)
+      # kernel stats of the C3 step and the C5 iteration on full-mantissa rows
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+         -d "$OUT/profn" -o run -- python3 "$R/bench.py" --data normal --steps 5 --warmup 2 --no-cpu-baseline \
+         --no-exact-dist-line > "$OUT/bench_profn.json" 2> "$OUT/bench_profn.err")
+      rc=$?; echo "profn rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      find "$OUT/profn" -name '*kernel_stats.csv' -exec head -14 {} \; ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       rc=$?; tail -2 "$OUT/smoke.log"; [ $rc -eq 0 ] || { echo "smoke rc=$rc"; exit $rc; } ;;
