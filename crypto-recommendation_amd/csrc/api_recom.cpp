@@ -379,9 +379,41 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
     Buf &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
     const size_t M = (size_t)(total > 0 ? total : 1);
     if (out && ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M)))) return rc;
+    // users whose cluster holds >= RC_LONG_MIN members here: their chains by
+    // binade segments (the offsets come to the host to find them)
+    std::vector<int64_t> hs((size_t)nq + 1), ht((size_t)nq + 1), hu((size_t)nq + 1);
+    LSHKM_HIP(hipMemcpyAsync(hs.data(), soff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipMemcpyAsync(ht.data(), toff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipMemcpyAsync(hu.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<RcLongUser> lus;
+    int64_t maxn = 0, maxm = 1;
+    for (int64_t q = 0; q < nq; q++) {
+        const int64_t n = hs[q + 1] - hs[q];
+        if (n < RC_LONG_MIN) continue;
+        const int m = (int)(hu[q + 1] - hu[q]);
+        lus.push_back(RcLongUser{q, n, hs[q], ht[q], hu[q], m});
+        maxn = std::max(maxn, n);
+        maxm = std::max<int64_t>(maxm, m);
+    }
+    RcLong lng{};
+    if (!lus.empty()) {
+        const size_t wsb = (seg_columns_ws_bytes(maxn, (int)maxm) + 255) / 256 * 256;
+        const size_t nb = wsb + (size_t)maxn * 4 + 16 + (size_t)maxm * 8 + 8 + (size_t)maxn * 8 + 64;
+        if ((rc = ctx->ws_long.reserve(nb))) return rc;
+        char* b = ctx->ws_long.as<char>();
+        lng.ws = b;
+        lng.absv = reinterpret_cast<double*>(b + wsb);
+        lng.sums = lng.absv + maxn;
+        lng.asum = lng.sums + maxm;
+        lng.crow = reinterpret_cast<int64_t*>(lng.asum + 1);
+        lng.iota = reinterpret_cast<int32_t*>(lng.crow + 2);
+        lng.users = lus.data();
+        lng.nlong = (int64_t)lus.size();
+    }
     if ((rc = launch_rc_chain_terms(ctx->stream, nq, soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
                                     out ? nullptr : main_out, out ? nullptr : abs_out, out ? nullptr : cnt_out,
-                                    out ? pred.as<double>() : nullptr))) {
+                                    out ? pred.as<double>() : nullptr, lus.empty() ? nullptr : &lng))) {
         (void)hipStreamSynchronize(ctx->stream);
         return rc;
     }

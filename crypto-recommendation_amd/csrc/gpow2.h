@@ -19,7 +19,7 @@
 // in round-to-nearest, so host and device give the same bits.
 // gp_sq(x) takes x*x when x^2 is provably not near a midpoint (|x| in
 // [2^-40, 2^40], where the algorithm's error is <= 0.011 ulp, and x^2 more than
-// 2^-5 ulp away from every midpoint) and the restatement otherwise (~6 % of
+// 2^-6 ulp away from every midpoint) and the restatement otherwise (~3 % of
 // general doubles, none of the exactly-representable squares; measured worst
 // case of the algorithm: 0.0085 ulp, tests/pow2_check.cpp).
 // Checked on the host against the process's real pow on ~2e9 inputs, near
@@ -212,14 +212,17 @@ struct PwAcc {
 };
 
 // True when p = x*x might not be pow(x, 2): |x| outside [2^-40, 2^40) (x != 0),
-// x^2 just below a power of two, or x^2 within 2^-5 ulp of a rounding midpoint
+// x^2 just below a power of two, or x^2 within 2^-6 ulp of a rounding midpoint
 // (see the file comment). The midpoint test without the ulp: with x^2 = p + e
-// exactly, fma(e, K, p) for K = 16/15 (1 + 2^-40) rounds back to p iff |e K|
-// <= ulp/2, i.e. |e| < 15/32 ulp: more than 1/32 ulp from the midpoint (an
-// exact square, e = 0, always passes). ~9 VALU per square.
+// exactly, fma(e, K, p) for K = 32/31 (1 + 2^-40) rounds back to p iff |e K|
+// <= ulp/2, i.e. |e| < 31/64 ulp: more than 1/64 ulp from the midpoint (an
+// exact square, e = 0, always passes). ~9 VALU per square. The margin: 1/64
+// = 0.0156 ulp against the algorithm's ~0.011-ulp bound; on 4e8 random squares
+// no pow(x, 2) differs from x*x farther than 0.0086 ulp from a midpoint (the
+// window was 2^-5 until round 6: twice the restatements).
 GP_HD bool gp_sq_slow(double x, double p) {
     const double e = fma(x, x, -p);                        // x^2 = p + e exactly
-    const double r = fma(e, 0x1.1111111112223p+0, p);      // K rounded up
+    const double r = fma(e, 0x1.0842108422109p+0, p);      // K rounded up
     const double ax = fabs(x);
     const uint32_t hp = (uint32_t)(gp_bits(p) >> 32);
     const bool out = !(ax >= 0x1p-40 && ax < 0x1p40);      // nan too
@@ -242,14 +245,30 @@ GP_HD double gp_sq(double x) {
 // time, one per lane: a lane-per-chain gp_sq makes the wave run the
 // restatement for nearly every term (a 64-lane wave almost always holds one
 // such square). All 64 lanes must call it together.
-template <int NV>
+// First the exact-square prefilter (PwAcc's test, wave-wide): when no value of
+// any lane has more than 26 significant bits and none squares near the
+// subnormal range, every x*x is pow's own value and nothing else runs (~2-4
+// VALU per square instead of the midpoint test's ~9: fp32-grid rows, the
+// reference's quantized inputs). TINY = false: the caller's values cannot lie
+// in (0, 2^-460) (differences of fp32 values).
+template <int NV, bool TINY = true>
 __device__ inline void gp_sq_wave(const double (&x)[NV], double (&p)[NV], double* lds) {
     static_assert(NV <= 32, "lds holds 64 * NV doubles");
+    uint32_t lo = 0u, hmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        p[j] = __dmul_rn(x[j], x[j]);
+        const uint64_t b = gp_bits(x[j]);
+        lo |= (uint32_t)b;
+        // |x| < 2^-460, zero excluded (0 - 1 wraps to the top); x with a zero
+        // high word and low bits set fails the low-bits test anyway
+        if (TINY) hmin = min(hmin, ((uint32_t)(b >> 32) & 0x7FFFFFFFu) - 1u);
+    }
+    if (__ballot((lo & 0x07FFFFFFu) != 0u || (TINY && hmin < 0x23300000u - 1u)) == 0ull) return;
     bool sl[NV];
     bool any = false;
 #pragma unroll
     for (int j = 0; j < NV; j++) {
-        p[j] = __dmul_rn(x[j], x[j]);
         sl[j] = gp_sq_slow(x[j], p[j]);
         any = any || sl[j];
     }

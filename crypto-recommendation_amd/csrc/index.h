@@ -70,6 +70,7 @@ struct lshkm_ctx_s {
     lshkm::Buf ws[16];
     // range assignment workspace (lshkm_range_assign)
     lshkm::Buf ws_range[12];
+    lshkm::Buf ws_long;          // the recommender's chains of huge clusters (RcLong)
     lshkm::Buf ws_km_seg;        // k-means: the segment records of the chains the never-rounds test flags (fp32 rows)
     lshkm::Buf ws_scan;          // multi-block scans of large query size arrays
     // workspaces of the entry points that synchronise their stream before

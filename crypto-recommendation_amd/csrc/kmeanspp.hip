@@ -226,7 +226,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
 #pragma unroll
                     for (int q = 0; q < 8; q++)
                         df[q] = __dsub_rn((double)tile[threadIdx.x][jj + q], (double)cs[j0 + jj + q]);
-                    gp_sq_wave<8>(df, p, sqb);
+                    gp_sq_wave<8, sizeof(TX) == 8>(df, p, sqb);
 #pragma unroll
                     for (int q = 0; q < 8; q++) acc = __dadd_rn(acc, p[q]);
                 }
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_kernel(const TX* __restr
                 for (; jj < dj; jj++) {
                     const double df[1] = {__dsub_rn((double)tile[threadIdx.x][jj], (double)cs[j0 + jj])};
                     double p[1];
-                    gp_sq_wave<1>(df, p, sqb);
+                    gp_sq_wave<1, sizeof(TX) == 8>(df, p, sqb);
                     acc = __dadd_rn(acc, p[0]);
                 }
             } else if (n < N) {
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(KPP_THREADS) void kpp_dist_reg_kernel(const float* 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            gp_sq_wave<16>(df, p, sqb);
+            gp_sq_wave<16, false>(df, p, sqb);
 #pragma unroll
             for (int u = 0; u < 16; u++) acc = __dadd_rn(acc, p[u]);
         }

@@ -14,6 +14,8 @@
 // the first P+1 are equal (a tie touching the first P positions), hands the user
 // to lomuto_sort, which replays the reference's quicksort exactly (one lane per
 // user; disjoint subarrays, so the order they are sorted in does not matter).
+#include <climits>
+
 #include "../../include/lshkm.h"
 #include "common.h"
 #include "kernels.h"
@@ -923,12 +925,13 @@ __global__ __launch_bounds__(64) void rc_chain_user_kernel(
     const int64_t* __restrict__ toff, const double* __restrict__ sims, const double* __restrict__ terms,
     const double* __restrict__ carry_main, const double* __restrict__ carry_abs,
     const int64_t* __restrict__ carry_cnt, const double* __restrict__ u_mean, double* __restrict__ main_out,
-    double* __restrict__ abs_out, int64_t* __restrict__ cnt_out, double* __restrict__ pred) {
+    double* __restrict__ abs_out, int64_t* __restrict__ cnt_out, double* __restrict__ pred, int64_t long_min) {
     __shared__ double blk[(RC_CH + 1) * RC_LS];
     __shared__ double as_sh;
     const int lane = threadIdx.x;
     for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
         const int64_t b0 = soff[q], n = soff[q + 1] - b0;
+        if (n >= long_min) continue;                   // a huge cluster: the segmented chains (rc_long_*)
         const int64_t u0 = unk_ptr[q];
         const int m = (int)(unk_ptr[q + 1] - u0);
         const double* sp = sims + b0;
@@ -996,6 +999,33 @@ __global__ __launch_bounds__(64) void rc_chain_user_kernel(
             }
             __syncthreads();
         }
+    }
+}
+
+// A user of a huge cluster (n >= RC_LONG_MIN members on this shard): its chains
+// were evaluated by binade segments (launch_seg_columns: the terms block [n][m]
+// -> sums [m], the |sim| copy [n][1] -> its sum); the same outputs as
+// rc_chain_user_kernel from them.
+__global__ void rc_abs_kernel(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = fabs(v[i]);
+}
+
+__global__ void rc_long_finish_kernel(int64_t q, int64_t n, const int64_t* __restrict__ unk_ptr,
+                                      const double* __restrict__ sums, const double* __restrict__ asum,
+                                      const int64_t* __restrict__ carry_cnt, const double* __restrict__ u_mean,
+                                      double* __restrict__ main_out, double* __restrict__ abs_out,
+                                      int64_t* __restrict__ cnt_out, double* __restrict__ pred) {
+    const int64_t u0 = unk_ptr[q];
+    const int m = (int)(unk_ptr[q + 1] - u0);
+    const double as = asum[0];
+    for (int e = threadIdx.x; e < m; e += blockDim.x) {
+        if (pred) pred[u0 + e] = __dadd_rn(__ddiv_rn(sums[e], as), u_mean[q]);
+        else main_out[u0 + e] = sums[e];
+    }
+    if (!pred && threadIdx.x == 0) {
+        abs_out[q] = as;
+        cnt_out[q] = (carry_cnt ? carry_cnt[q] : 0) + n;
     }
 }
 
@@ -1072,11 +1102,32 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
 int launch_rc_chain_terms(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff,
                           const double* sims, const double* terms, const double* carry_main, const double* carry_abs,
                           const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,
-                          int64_t* cnt_out, double* pred) {
+                          int64_t* cnt_out, double* pred, const RcLong* lng) {
     if (nq <= 0) return 0;
+    // the users of huge clusters first, by segments (their chain would be one
+    // wave's ~n dependent adds: 4.9 ms for the 206,926 members of the first C5
+    // iteration's largest cluster)
+    const int64_t long_min = lng && lng->nlong > 0 ? RC_LONG_MIN : INT64_MAX;
+    if (lng) {
+        for (int64_t k = 0; k < lng->nlong; k++) {
+            const RcLongUser& u = lng->users[k];
+            int rc;
+            if ((rc = launch_seg_iota(s, lng->iota, u.n, lng->crow))) return rc;
+            if (u.m > 0 &&
+                (rc = launch_seg_columns(s, terms + u.toff, u.n, u.m, lng->iota, lng->crow,
+                                         carry_main ? carry_main + u.u0 : nullptr, lng->sums, lng->ws)))
+                return rc;
+            hipLaunchKernelGGL(rc_abs_kernel, dim3(gsz(u.n, 256, 1024)), dim3(256), 0, s, sims + u.b0, u.n, lng->absv);
+            if ((rc = launch_seg_columns(s, lng->absv, u.n, 1, lng->iota, lng->crow, carry_abs ? carry_abs + u.q : nullptr,
+                                         lng->asum, lng->ws)))
+                return rc;
+            hipLaunchKernelGGL(rc_long_finish_kernel, dim3(1), dim3(64), 0, s, u.q, u.n, unk_ptr, lng->sums, lng->asum,
+                               carry_cnt, u_mean, main_out, abs_out, cnt_out, pred);
+        }
+    }
     hipLaunchKernelGGL(rc_chain_user_kernel, dim3((unsigned)std::min<int64_t>(nq, 65536)), dim3(64), 0, s, nq, soff,
                        unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean, main_out, abs_out, cnt_out,
-                       pred);
+                       pred, long_min);
     return kstatus("rc_chain_user_kernel");
 }
 

@@ -66,7 +66,7 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
 #pragma unroll
                 for (int u = 0; u < 4; u++) df[4 * h + u] = __dsub_rn(a[u], b[u]);
             }
-            gp_sq_wave<8>(df, p, sq);
+            gp_sq_wave<8, sizeof(TX) == 8>(df, p, sq);
 #pragma unroll
             for (int u = 0; u < 8; u++) acc = __dadd_rn(acc, p[u]);
         }
@@ -76,7 +76,7 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
             ld4d(xj + k, b);
 #pragma unroll
             for (int u = 0; u < 4; u++) df[u] = __dsub_rn(a[u], b[u]);
-            gp_sq_wave<4>(df, p, sq);
+            gp_sq_wave<4, sizeof(TX) == 8>(df, p, sq);
 #pragma unroll
             for (int u = 0; u < 4; u++) acc = __dadd_rn(acc, p[u]);
             k += 4;
@@ -86,7 +86,7 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
     for (; k < d; k++) {
         const double df[1] = {__dsub_rn((double)xi[k], (double)xj[k])};
         double p[1];
-        gp_sq_wave<1>(df, p, sq);
+        gp_sq_wave<1, sizeof(TX) == 8>(df, p, sq);
         acc = __dadd_rn(acc, p[0]);
     }
     return sqrt(acc);
@@ -131,7 +131,7 @@ __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restri
                 df[8 * h + 2 * e + 1] = __dsub_rn(v[e], b[e]);
             }
         }
-        gp_sq_wave<16>(df, p, sq);
+        gp_sq_wave<16, sizeof(TX) == 8>(df, p, sq);
 #pragma unroll
         for (int e = 0; e < 8; e++) {
             aa = __dadd_rn(aa, p[2 * e]);
@@ -148,7 +148,7 @@ __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restri
             df[2 * e] = __dsub_rn(u[e], b[e]);
             df[2 * e + 1] = __dsub_rn(v[e], b[e]);
         }
-        gp_sq_wave<8>(df, p, sq);
+        gp_sq_wave<8, sizeof(TX) == 8>(df, p, sq);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             aa = __dadd_rn(aa, p[2 * e]);

@@ -897,6 +897,33 @@ int launch_km_sums_seg(hipStream_t s, Pts X, int d, const int32_t* rows, const i
     return kstatus("update.hip (segmented)");
 }
 
+// ------------------------------------------------------------------ long chains
+// Column sums of a row-major [n][m] fp64 block V, each column one sequential
+// chain in row order from carry (NULL: 0) -- the same segmented evaluation
+// with the rows as one "cluster" (iota: 0..n-1, crow: {0, n}). The clustering
+// recommender's prediction chains of a huge cluster (recom.hip) take it.
+__global__ void seg_iota_kernel(int32_t* __restrict__ iota, int64_t n, int64_t* __restrict__ crow) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        iota[i] = (int32_t)i;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { crow[0] = 0; crow[1] = n; }
+}
+
+size_t seg_columns_ws_bytes(int64_t n, int m) { return km_seg_ws_bytes(n, 1, m); }
+
+int launch_seg_iota(hipStream_t s, int32_t* iota, int64_t n, int64_t* crow) {
+    hipLaunchKernelGGL(seg_iota_kernel, dim3(gsz(n, 256, 4096)), dim3(256), 0, s, iota, n, crow);
+    return kstatus("update.hip (iota)");
+}
+
+int launch_seg_columns(hipStream_t s, const double* V, int64_t n, int m, const int32_t* iota, const int64_t* crow,
+                       const double* carry, double* out, void* ws) {
+    if (n <= 0 || m <= 0) return 0;
+    const KsWs w(ws, n, 1, m);
+    km_seg_records(s, V, m, iota, crow, 1, n, carry, nullptr, w);
+    km_seg_compose(s, V, m, iota, crow, 1, carry, nullptr, nullptr, w, out);
+    return kstatus("update.hip (column chains)");
+}
+
 // ------------------------------------------------------------------ sharded form
 // The reference's chain over row shards (lshkm_kmeans_shard_*, include/lshkm.h):
 // every rank forms its partial sums by the parallel form above and reports its

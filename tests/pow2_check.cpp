@@ -4,7 +4,8 @@
 //   pow2_check <millions of random samples per set>
 // Sets: uniform 64-bit patterns (every exponent, subnormals, inf, nan),
 // [0.5, 4) dense, squares within 2^-8 ulp of a midpoint (the discriminating
-// ones: ~20 % of them differ from x*x), 27-bit mantissas (exact ties), and
+// ones: ~20 % of them differ from x*x; and 2^-8 .. 2^-4 ulp away, across the
+// 2^-6 window of gp_sq), 27-bit mantissas (exact ties), and
 // exact squares across every exponent (<= 26-bit mantissas), and sweeps
 // across the special ranges (subnormal / overflowing squares,
 // |2 ln x| < 2^-54, the exp specialcase range 2^+-369, the gp_sq filter edges).
@@ -56,19 +57,22 @@ static double gen(int set, uint64_t i) {
 int main(int argc, char** argv) {
     const long n = (argc > 1 ? atol(argv[1]) : 10) * 1000000L;
     long bad = 0, nearmid = 0, differ = 0;
-    for (int set = 0; set < 7; set++) {
+    for (int set = 0; set < 8; set++) {
         long sbad = 0, sdiff = 0, snear = 0;
 #pragma omp parallel for reduction(+ : sbad, sdiff, snear) schedule(static)
         for (long i = 0; i < n; i++) {
             double x;
-            if (set == 5) {                                              // near midpoints
-                uint64_t j = (uint64_t)i * 64;
+            if (set == 5 || set == 7) {      // near midpoints (5: within 2^-8 ulp; 7: 2^-8 .. 2^-4
+                                             // ulp away, across gp_sq's 2^-6 window edge)
+                uint64_t j = (uint64_t)i * 64 + (set == 7 ? (1ull << 50) : 0);
+                const double lo = set == 5 ? 0.0 : 0x1p-8, hi = set == 5 ? 0x1p-8 : 0x1p-4;
                 for (;; j++) {
                     x = gen(j & 1 ? 1 : 4, j + 0x51ed);
                     const double p = x * x, e = fma(x, x, -p);
                     if (!(fabs(x) >= 0x1p-500 && fabs(x) <= 0x1p500)) continue;
                     const double u = gp_dbl(gp_bits(p) & 0x7ff0000000000000ull) * 0x1p-52;
-                    if (fabs(fabs(e) - 0.5 * u) <= 0x1p-8 * u) break;
+                    const double dm = fabs(fabs(e) - 0.5 * u);
+                    if (dm >= lo * u && dm <= hi * u) break;
                 }
                 snear++;
             } else {

@@ -316,6 +316,49 @@ def test_recommend_sharded_row_shapes(ctx, kind, d):
     assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
 
 
+@pytest.mark.parametrize("kind", ["f32", "f64"])
+def test_huge_cluster_chains_by_segments(ctx, kind):
+    # users of a cluster with >= RC_LONG_MIN (16,384) members on a shard take
+    # their prediction chains by binade segments (launch_seg_columns; the first
+    # C5 iteration's 206,926-member cluster) instead of one wave's sequential
+    # adds: single pass and 3 shards with the carry, bit for bit the oracle;
+    # users without unknown indexes and users of small clusters beside them
+    rng = np.random.default_rng(41 if kind == "f32" else 42)
+    N, d, K, nq, NT = 80_000, 64 if kind == "f32" else 100, 6, 90, 5
+    X = rng.standard_normal((N, d))
+    X = X.astype(np.float32) if kind == "f32" else X * np.exp(rng.uniform(-2, 2, size=(N, 1)))
+    xm = rng.standard_normal(N) * 0.3
+    assign = rng.integers(1, K, size=N).astype(np.int32)
+    assign[rng.random(N) < 0.75] = 0                          # ~60K members: ~20K on each shard
+    users = rng.choice(N, nq, replace=False)
+    U = X[users].copy()
+    um = rng.standard_normal(nq) * 0.2
+    ucl = assign[users].copy()
+    ucl[::3] = 0
+    up, ui = unknown_sets(rng, nq, d)
+    crow, crows = oracle.clusters_csr(assign, K)
+    assert crow[1] - crow[0] > 3 * 16_384
+    want = oracle.cluster_top_n(X, xm, crow, crows, U, um, ucl, up, ui, NT)
+    Ud, umd, ucd, upd, uid = dev(ctx, U), dev(ctx, um), dev(ctx, ucl), dev(ctx, up), dev(ctx, ui)
+    single = lshkm.cluster_top_n(ctx, dev(ctx, X), dev(ctx, xm), dev(ctx, crow), dev(ctx, crows), Ud, umd, ucd, upd,
+                                 uid, NT).cpu().numpy()
+    assert np.array_equal(single, want), np.nonzero((single != want).any(1))[0][:10]
+    carry, bounds = None, [0, 26_000, 53_000, N]
+    for s in range(3):
+        lo, hi = bounds[s], bounds[s + 1]
+        Xs = dev(ctx, X[lo:hi])
+        lcrow, lrows = oracle.clusters_csr(assign[lo:hi], K)
+        assert lcrow[1] - lcrow[0] >= 16_384
+        soff, toff, sims, terms = lshkm.cluster_terms(ctx, Xs, dev(ctx, xm[lo:hi]), dev(ctx, lcrow), dev(ctx, lrows),
+                                                      Ud, ucd, upd, uid)
+        a = (ctx, umd, upd, uid, soff, toff, sims, terms)
+        if s < 2:
+            carry = lshkm.cluster_chain_terms(*a, carry=carry, n_top=None)
+        else:
+            got = lshkm.cluster_chain_terms(*a, carry=carry, n_top=NT).cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero((got != want).any(1))[0][:10]
+
+
 @pytest.mark.parametrize("bad_cl", [-1, 12, 17])
 def test_cluster_ids_outside_k_are_refused(ctx, bad_cl):
     # the reference indexes clusters[user.getCluster()] unchecked (main.cpp:261,
