@@ -377,13 +377,11 @@ def main():
         it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="certified")
         if args.recom_users > 0:
             it.enable_recommend(N_total, rank * N, Q=args.recom_users, n_top=5)
-        ctx.reset_stats()
         elapsed = timed(it.step, steps, warmup, world, dev)
-        it.km_seq_chains = ctx.stat(lk.STAT_KM_SEQ) // (steps + warmup)
         it.timing = True
         kms = fused_kernel_ms(lk, lib, ctx, it.step, max(3, steps))
         it.timing = False
-        xms = it.exchange_ms() if world > 1 else None
+        xms = it.exchange_ms()
         rec = None
         if args.recom_users > 0:
             it.recom_timing = []
@@ -406,15 +404,17 @@ def main():
                    "users_per_s": args.recom_users / ((ph1 + ph2) / 1e3),
                    "similarities_per_s": sims / ((ph1 + ph2) / 1e3)}
         rec = rec or {}
-        rec["km_sequential_chains"] = it.km_seq_chains
+        rec["km_flagged_chains"] = it.flagged       # the last step's: carried rank to rank (segments)
         return elapsed, kms, xms, rec
 
     def c5_object(K, elapsed, kms, xms, rec=None, steps=args.steps):
-        coll = (f"RCCL all-reduce ({backend}) of the {K}x128 fp64 sums + {K} counts" if world > 1
+        coll = (f"sharding.kmeans_sums_sharded over RCCL ({backend}): all-gather of the {K}x128 fp64 partial sums, "
+                f"all-reduces of the |x| sums, bit positions and {K} counts; the chains the global never-rounds "
+                f"test flags carried rank to rank" if world > 1
                 else "none (N = 1: a single shard, no collective)")
         return {
             "metric": f"C5 LSH-assign + k-means recommend iterations: points/s (hash + assign K={K} + sums + "
-                      f"{'RCCL all-reduce' if world > 1 else 'no collective at N = 1'} + finalize"
+                      f"{'RCCL exchange' if world > 1 else 'no collective at N = 1'} + finalize"
                       + (f" + recommend for {args.recom_users} users)" if args.recom_users > 0 else ")"),
             "value": N_total * steps / elapsed, "unit": "point iteration ops/s",
             "ms_per_step": elapsed / steps * 1e3, "n_gpus": world, "scaling": "weak",
@@ -422,8 +422,8 @@ def main():
                                    f"L=5, k=4, w=0.4, exchange: {coll}",
                        "N_per_gpu": N, "N_total": N_total, "K": K, "parallelism": f"dp{world} (row shards)"},
             "allreduce": coll,
-            "allreduce_ms": xms if world > 1 else None,
-            "km_sequential_chains": (rec or {}).pop("km_sequential_chains", None),
+            "km_sums_exchange_ms": xms,         # the sums + their exchange + certificate (HIP events)
+            "km_flagged_chains": (rec or {}).pop("km_flagged_chains", None),
             "recommend": rec or None,
             "roofline": roofline(N, K, kms, traffic_for(args.traffic_json_c5, N, K, "c5"),
                                  FUSED_WHAT + " (K = 1024: two 512-centroid passes)"),

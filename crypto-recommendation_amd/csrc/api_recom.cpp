@@ -380,40 +380,69 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
     const size_t M = (size_t)(total > 0 ? total : 1);
     if (out && ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M)))) return rc;
     // users whose cluster holds >= RC_LONG_MIN members here: their chains by
-    // binade segments (the offsets come to the host to find them)
+    // binade segments (the offsets come to the host to find them), in batches of
+    // at most ~1 GiB of packed values
     std::vector<int64_t> hs((size_t)nq + 1), ht((size_t)nq + 1), hu((size_t)nq + 1);
     LSHKM_HIP(hipMemcpyAsync(hs.data(), soff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipMemcpyAsync(ht.data(), toff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipMemcpyAsync(hu.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     std::vector<RcLongUser> lus;
-    int64_t maxn = 0, maxm = 1;
     for (int64_t q = 0; q < nq; q++) {
         const int64_t n = hs[q + 1] - hs[q];
-        if (n < RC_LONG_MIN) continue;
-        const int m = (int)(hu[q + 1] - hu[q]);
-        lus.push_back(RcLongUser{q, n, hs[q], ht[q], hu[q], m});
-        maxn = std::max(maxn, n);
-        maxm = std::max<int64_t>(maxm, m);
+        if (n >= RC_LONG_MIN) lus.push_back(RcLongUser{q, n, hs[q], ht[q], hu[q], hu[q + 1] - hu[q], 0, 0});
     }
-    RcLong lng{};
-    if (!lus.empty()) {
-        const size_t wsb = (seg_columns_ws_bytes(maxn, (int)maxm) + 255) / 256 * 256;
-        const size_t nb = wsb + (size_t)maxn * 4 + 16 + (size_t)maxm * 8 + 8 + (size_t)maxn * 8 + 64;
+    std::vector<int64_t> hcrow;
+    const StreamSyncOnExit sync_guard{ctx->stream};     // lus / hcrow are copied before return
+    const int64_t long_min = lus.empty() ? INT64_MAX : RC_LONG_MIN;
+    for (size_t k0 = 0; k0 < lus.size();) {
+        // a batch: users k0 .. k1-1, D = their max m + 1, rows * D * 8 <= 1 GiB (one user at least)
+        size_t k1 = k0;
+        int64_t rows = 0, D = 1;
+        while (k1 < lus.size()) {
+            const int64_t D2 = std::max<int64_t>(D, lus[k1].m + 1), rows2 = rows + lus[k1].n;
+            if (k1 > k0 && (rows2 * D2 * 8 > (1ll << 30) || rows2 >= (1ll << 31))) break;
+            D = D2;
+            rows = rows2;
+            k1++;
+        }
+        const int64_t nl = (int64_t)(k1 - k0);
+        hcrow.assign(1, 0);
+        for (size_t k = k0; k < k1; k++) {
+            lus[k].off = hcrow.back();
+            hcrow.push_back(hcrow.back() + lus[k].n);
+        }
+        const size_t wsb = (seg_columns_ws_bytes(rows, (int)nl, (int)D) + 255) / 256 * 256;
+        const size_t vb = (size_t)rows * D * 8, cb = (size_t)nl * D * 8;
+        const size_t tb = (size_t)nl * sizeof(RcLongUser), rb = (size_t)(nl + 1) * 8;
+        const size_t nb = wsb + vb + 2 * cb + tb + rb + (size_t)rows * 4 + 256;
         if ((rc = ctx->ws_long.reserve(nb))) return rc;
         char* b = ctx->ws_long.as<char>();
-        lng.ws = b;
-        lng.absv = reinterpret_cast<double*>(b + wsb);
-        lng.sums = lng.absv + maxn;
-        lng.asum = lng.sums + maxm;
-        lng.crow = reinterpret_cast<int64_t*>(lng.asum + 1);
-        lng.iota = reinterpret_cast<int32_t*>(lng.crow + 2);
-        lng.users = lus.data();
-        lng.nlong = (int64_t)lus.size();
+        RcLong L{};
+        L.ws = b;
+        L.V = reinterpret_cast<double*>(b + wsb);
+        L.carry = L.V + (size_t)rows * D;
+        L.sums = L.carry + (size_t)nl * D;
+        RcLongUser* tab = reinterpret_cast<RcLongUser*>(L.sums + (size_t)nl * D);
+        int64_t* crow = reinterpret_cast<int64_t*>(tab + nl);
+        L.iota = reinterpret_cast<int32_t*>(crow + nl + 1);
+        L.tab = tab;
+        L.crow = crow;
+        L.nlong = nl;
+        L.rows = rows;
+        L.D = (int)D;
+        LSHKM_HIP(hipMemcpyAsync(tab, lus.data() + k0, tb, hipMemcpyHostToDevice, ctx->stream));
+        LSHKM_HIP(hipMemcpyAsync(crow, hcrow.data(), rb, hipMemcpyHostToDevice, ctx->stream));
+        if ((rc = launch_rc_long(ctx->stream, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
+                                 out ? nullptr : main_out, out ? nullptr : abs_out, out ? nullptr : cnt_out,
+                                 out ? pred.as<double>() : nullptr, L)))
+            return rc;
+        LSHKM_HIP(hipStreamSynchronize(ctx->stream));      // the next batch reuses the workspace and hcrow
+        k0 = k1;
     }
     if ((rc = launch_rc_chain_terms(ctx->stream, nq, soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
                                     out ? nullptr : main_out, out ? nullptr : abs_out, out ? nullptr : cnt_out,
-                                    out ? pred.as<double>() : nullptr, lus.empty() ? nullptr : &lng))) {
+                                    out ? pred.as<double>() : nullptr, long_min))) {
         (void)hipStreamSynchronize(ctx->stream);
         return rc;
     }

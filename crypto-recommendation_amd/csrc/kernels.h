@@ -1,5 +1,6 @@
 // kernels.h — launchers of the gfx950 kernels (host-callable, stream-ordered).
 #pragma once
+#include <climits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -201,12 +202,13 @@ int launch_km_shard_prepare(hipStream_t s, Pts X, int d, const int32_t* rows, co
                             const double* start, const int* flag, void* ws);
 int launch_km_shard_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
                           const int* flag, const uint8_t* mask, const double* carry, void* ws, double* sums);
-// Column chains of a row-major [n][m] fp64 block (row order, from carry; iota /
-// crow from launch_seg_iota; ws: seg_columns_ws_bytes) by binade segments.
-size_t seg_columns_ws_bytes(int64_t n, int m);
-int launch_seg_iota(hipStream_t s, int32_t* iota, int64_t n, int64_t* crow);
-int launch_seg_columns(hipStream_t s, const double* V, int64_t n, int m, const int32_t* iota, const int64_t* crow,
-                       const double* carry, double* out, void* ws);
+// Column chains of K row blocks [crow[k], crow[k+1]) of a row-major [n][m]
+// fp64 matrix (row order, from carry [K][m] or 0; iota from launch_seg_iota;
+// ws: seg_columns_ws_bytes) by binade segments -> out [K][m].
+size_t seg_columns_ws_bytes(int64_t n, int K, int m);
+int launch_seg_iota(hipStream_t s, int32_t* iota, int64_t n);
+int launch_seg_columns(hipStream_t s, const double* V, int64_t n, int K, int m, const int32_t* iota,
+                       const int64_t* crow, const double* carry, double* out, void* ws);
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
 
@@ -245,27 +247,31 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
                     int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
                     unsigned long long* soft_count, double* unorm, const RcGroups* groups);
 // Users whose cluster holds >= RC_LONG_MIN members on this shard: their
-// prediction chains by binade segments (launch_seg_columns) instead of one
-// wave's sequential adds. users: host list; the buffers are device workspace
-// (iota [max n] int32, crow [2], sums [max m], asum [1], absv [max n], ws:
-// seg_columns_ws_bytes(max n, max(max m, 1))).
+// prediction chains by binade segments (launch_seg_columns, all such users in
+// one set of launches) instead of one wave's sequential adds. Device
+// workspace: tab [nlong] RcLongUser, crow [nlong + 1] (row offsets in V), V
+// [rows][D] (D = max m + 1: each user's terms, zero-padded, then |sim|),
+// iota [rows], carry / sums [nlong][D], ws (seg_columns_ws_bytes).
 constexpr int64_t RC_LONG_MIN = 16384;
 struct RcLongUser {
-    int64_t q, n, b0, toff, u0;
-    int m;
+    int64_t q, n, b0, toff, u0, m, off, pad;
 };
 struct RcLong {
-    const RcLongUser* users;
-    int64_t nlong;
+    const RcLongUser* tab;
+    int64_t nlong, rows;
+    int D;
+    const int64_t* crow;
+    double *V, *carry, *sums;
     int32_t* iota;
-    int64_t* crow;
-    double *sums, *asum, *absv;
     void* ws;
 };
 int launch_rc_chain_terms(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff,
                           const double* sims, const double* terms, const double* carry_main, const double* carry_abs,
                           const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,
-                          int64_t* cnt_out, double* pred, const RcLong* lng = nullptr);
+                          int64_t* cnt_out, double* pred, int64_t long_min = INT64_MAX);
+int launch_rc_long(hipStream_t s, const double* sims, const double* terms, const double* carry_main,
+                   const double* carry_abs, const int64_t* carry_cnt, const double* u_mean, double* main_out,
+                   double* abs_out, int64_t* cnt_out, double* pred, const RcLong& lng);
 int launch_rc_top(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* carry_cnt, const int64_t* unk_ptr,
                   const int32_t* unk_idx, double* pred, int32_t* pidx, int n_top, int32_t* out);
 constexpr int RC_CLUSTER_WAVES_PER_BLOCK = 4;     // rc_cluster_top_n_kernel: waves per block (RC_WAVES)

@@ -1006,26 +1006,45 @@ __global__ __launch_bounds__(64) void rc_chain_user_kernel(
 // were evaluated by binade segments (launch_seg_columns: the terms block [n][m]
 // -> sums [m], the |sim| copy [n][1] -> its sum); the same outputs as
 // rc_chain_user_kernel from them.
-__global__ void rc_abs_kernel(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = fabs(v[i]);
+// V [rows][D]: user k's member r at row off_k + r -- its m_k terms, zeros, then
+// |sim| in column D - 1 (blockIdx.y = k)
+__global__ void rc_long_pack_kernel(const RcLongUser* __restrict__ tab, int D, const double* __restrict__ sims,
+                                    const double* __restrict__ terms, double* __restrict__ V) {
+    const RcLongUser u = tab[blockIdx.y];
+    const int64_t tot = u.n * D;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / D;
+        const int e = (int)(i - r * D);
+        const double v = e < u.m ? terms[u.toff + r * u.m + e] : (e == D - 1 ? fabs(sims[u.b0 + r]) : 0.0);
+        V[(u.off + r) * D + e] = v;
+    }
 }
 
-__global__ void rc_long_finish_kernel(int64_t q, int64_t n, const int64_t* __restrict__ unk_ptr,
-                                      const double* __restrict__ sums, const double* __restrict__ asum,
+__global__ void rc_long_carry_kernel(const RcLongUser* __restrict__ tab, int64_t nlong, int D,
+                                     const double* __restrict__ carry_main, const double* __restrict__ carry_abs,
+                                     double* __restrict__ carry) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlong * D) return;
+    const RcLongUser u = tab[i / D];
+    const int e = (int)(i % D);
+    carry[i] = e < u.m ? carry_main[u.u0 + e] : (e == D - 1 ? carry_abs[u.q] : 0.0);
+}
+
+// user k = blockIdx.x: rc_chain_user_kernel's outputs from its column sums
+__global__ void rc_long_finish_kernel(const RcLongUser* __restrict__ tab, int D, const double* __restrict__ sums,
                                       const int64_t* __restrict__ carry_cnt, const double* __restrict__ u_mean,
                                       double* __restrict__ main_out, double* __restrict__ abs_out,
                                       int64_t* __restrict__ cnt_out, double* __restrict__ pred) {
-    const int64_t u0 = unk_ptr[q];
-    const int m = (int)(unk_ptr[q + 1] - u0);
-    const double as = asum[0];
-    for (int e = threadIdx.x; e < m; e += blockDim.x) {
-        if (pred) pred[u0 + e] = __dadd_rn(__ddiv_rn(sums[e], as), u_mean[q]);
-        else main_out[u0 + e] = sums[e];
+    const RcLongUser u = tab[blockIdx.x];
+    const double* sk = sums + (size_t)blockIdx.x * D;
+    const double as = sk[D - 1];
+    for (int e = threadIdx.x; e < u.m; e += blockDim.x) {
+        if (pred) pred[u.u0 + e] = __dadd_rn(__ddiv_rn(sk[e], as), u_mean[u.q]);
+        else main_out[u.u0 + e] = sk[e];
     }
     if (!pred && threadIdx.x == 0) {
-        abs_out[q] = as;
-        cnt_out[q] = (carry_cnt ? carry_cnt[q] : 0) + n;
+        abs_out[u.q] = as;
+        cnt_out[u.q] = (carry_cnt ? carry_cnt[u.q] : 0) + u.n;
     }
 }
 
@@ -1102,33 +1121,37 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
 int launch_rc_chain_terms(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* unk_ptr, const int64_t* toff,
                           const double* sims, const double* terms, const double* carry_main, const double* carry_abs,
                           const int64_t* carry_cnt, const double* u_mean, double* main_out, double* abs_out,
-                          int64_t* cnt_out, double* pred, const RcLong* lng) {
+                          int64_t* cnt_out, double* pred, int64_t long_min) {
     if (nq <= 0) return 0;
-    // the users of huge clusters first, by segments (their chain would be one
-    // wave's ~n dependent adds: 4.9 ms for the 206,926 members of the first C5
-    // iteration's largest cluster)
-    const int64_t long_min = lng && lng->nlong > 0 ? RC_LONG_MIN : INT64_MAX;
-    if (lng) {
-        for (int64_t k = 0; k < lng->nlong; k++) {
-            const RcLongUser& u = lng->users[k];
-            int rc;
-            if ((rc = launch_seg_iota(s, lng->iota, u.n, lng->crow))) return rc;
-            if (u.m > 0 &&
-                (rc = launch_seg_columns(s, terms + u.toff, u.n, u.m, lng->iota, lng->crow,
-                                         carry_main ? carry_main + u.u0 : nullptr, lng->sums, lng->ws)))
-                return rc;
-            hipLaunchKernelGGL(rc_abs_kernel, dim3(gsz(u.n, 256, 1024)), dim3(256), 0, s, sims + u.b0, u.n, lng->absv);
-            if ((rc = launch_seg_columns(s, lng->absv, u.n, 1, lng->iota, lng->crow, carry_abs ? carry_abs + u.q : nullptr,
-                                         lng->asum, lng->ws)))
-                return rc;
-            hipLaunchKernelGGL(rc_long_finish_kernel, dim3(1), dim3(64), 0, s, u.q, u.n, unk_ptr, lng->sums, lng->asum,
-                               carry_cnt, u_mean, main_out, abs_out, cnt_out, pred);
-        }
-    }
     hipLaunchKernelGGL(rc_chain_user_kernel, dim3((unsigned)std::min<int64_t>(nq, 65536)), dim3(64), 0, s, nq, soff,
                        unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean, main_out, abs_out, cnt_out,
                        pred, long_min);
     return kstatus("rc_chain_user_kernel");
+}
+
+// The users of huge clusters (lng: one batch of them), by segments: their chain
+// would be one wave's ~n dependent adds (4.9 ms for the 206,926 members of the
+// first C5 iteration's largest cluster).
+int launch_rc_long(hipStream_t s, const double* sims, const double* terms, const double* carry_main,
+                   const double* carry_abs, const int64_t* carry_cnt, const double* u_mean, double* main_out,
+                   double* abs_out, int64_t* cnt_out, double* pred, const RcLong& L) {
+    const RcLong* lng = &L;
+    {
+        int rc;
+        const int D = lng->D;
+        hipLaunchKernelGGL(rc_long_pack_kernel, dim3(gsz(lng->rows * D / lng->nlong, 256, 2048), (unsigned)lng->nlong),
+                           dim3(256), 0, s, lng->tab, D, sims, terms, lng->V);
+        if (carry_main)
+            hipLaunchKernelGGL(rc_long_carry_kernel, dim3(gsz(lng->nlong * D, 256, 65535)), dim3(256), 0, s, lng->tab,
+                               lng->nlong, D, carry_main, carry_abs, lng->carry);
+        if ((rc = launch_seg_iota(s, lng->iota, lng->rows)) ||
+            (rc = launch_seg_columns(s, lng->V, lng->rows, (int)lng->nlong, D, lng->iota, lng->crow,
+                                     carry_main ? lng->carry : nullptr, lng->sums, lng->ws)))
+            return rc;
+        hipLaunchKernelGGL(rc_long_finish_kernel, dim3((unsigned)lng->nlong), dim3(64), 0, s, lng->tab, D, lng->sums,
+                           carry_cnt, u_mean, main_out, abs_out, cnt_out, pred);
+    }
+    return kstatus("rc_long");
 }
 
 int launch_rc_top(hipStream_t s, int64_t nq, const int64_t* soff, const int64_t* carry_cnt, const int64_t* unk_ptr,

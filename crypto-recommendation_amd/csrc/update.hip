@@ -631,10 +631,19 @@ __global__ __launch_bounds__(64) void ks_scan_kernel(const double* __restrict__ 
     const int64_t beg = crow[c], end = crow[c + 1];
     if (j >= d || beg == end) return;
     double run = carry ? carry[(size_t)c * d + j] : 0.0;
-    for (int64_t w = beg / KS_W; w <= (end - 1) / KS_W; w++) {
-        const size_t o = (size_t)(w + c) * d + j;
-        sin[o] = run;
-        run += psum[o];
+    // 16 pairs' sums loaded at once, then their (approximate) running sums: the
+    // loads do not depend on the chain (a chain of 400 pairs waited on each)
+    const int64_t w0 = beg / KS_W, w1 = (end - 1) / KS_W;
+    for (int64_t wb = w0; wb <= w1; wb += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = wb + u <= w1 ? psum[(size_t)(wb + u + c) * d + j] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            if (wb + u > w1) break;
+            sin[(size_t)(wb + u + c) * d + j] = run;
+            run += v[u];
+        }
     }
 }
 
@@ -902,25 +911,26 @@ int launch_km_sums_seg(hipStream_t s, Pts X, int d, const int32_t* rows, const i
 // chain in row order from carry (NULL: 0) -- the same segmented evaluation
 // with the rows as one "cluster" (iota: 0..n-1, crow: {0, n}). The clustering
 // recommender's prediction chains of a huge cluster (recom.hip) take it.
-__global__ void seg_iota_kernel(int32_t* __restrict__ iota, int64_t n, int64_t* __restrict__ crow) {
+__global__ void seg_iota_kernel(int32_t* __restrict__ iota, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         iota[i] = (int32_t)i;
-    if (blockIdx.x == 0 && threadIdx.x == 0) { crow[0] = 0; crow[1] = n; }
 }
 
-size_t seg_columns_ws_bytes(int64_t n, int m) { return km_seg_ws_bytes(n, 1, m); }
+size_t seg_columns_ws_bytes(int64_t n, int K, int m) { return km_seg_ws_bytes(n, K, m); }
 
-int launch_seg_iota(hipStream_t s, int32_t* iota, int64_t n, int64_t* crow) {
-    hipLaunchKernelGGL(seg_iota_kernel, dim3(gsz(n, 256, 4096)), dim3(256), 0, s, iota, n, crow);
+int launch_seg_iota(hipStream_t s, int32_t* iota, int64_t n) {
+    hipLaunchKernelGGL(seg_iota_kernel, dim3(gsz(n, 256, 4096)), dim3(256), 0, s, iota, n);
     return kstatus("update.hip (iota)");
 }
 
-int launch_seg_columns(hipStream_t s, const double* V, int64_t n, int m, const int32_t* iota, const int64_t* crow,
-                       const double* carry, double* out, void* ws) {
-    if (n <= 0 || m <= 0) return 0;
-    const KsWs w(ws, n, 1, m);
-    km_seg_records(s, V, m, iota, crow, 1, n, carry, nullptr, w);
-    km_seg_compose(s, V, m, iota, crow, 1, carry, nullptr, nullptr, w, out);
+// K blocks of rows [crow[k], crow[k+1]) of V [n][m], each column of each block
+// one chain from carry[k][e] (NULL: 0) into out [K][m].
+int launch_seg_columns(hipStream_t s, const double* V, int64_t n, int K, int m, const int32_t* iota,
+                       const int64_t* crow, const double* carry, double* out, void* ws) {
+    if (n <= 0 || m <= 0 || K <= 0) return 0;
+    const KsWs w(ws, n, K, m);
+    km_seg_records(s, V, m, iota, crow, K, n, carry, nullptr, w);
+    km_seg_compose(s, V, m, iota, crow, K, carry, nullptr, nullptr, w, out);
     return kstatus("update.hip (column chains)");
 }
 
