@@ -897,8 +897,17 @@ static int silhouette_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int32_t
     // separate_clusters_from_input (utils.hpp:150-158): members in row order
     if ((rc = build_csr(ctx, assign, 1, N, K, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW)))) return rc;
     if ((rc = launch_sil_near(s, C, K, d, metric, near))) return rc;
+    // rows on a grid of <= 26 bits (every difference squares exactly): x*x for
+    // pow(x, 2) without the per-square test (grid_exact_squares)
+    bool exsq = false;
+    if (metric == LSHKM_METRIC_EUCLIDEAN) {
+        int qt[3];
+        if ((rc = reserve(ctx, WS_FLAG, 64)) || (rc = launch_grid_bits(s, X, N * d, slot<int>(ctx, WS_FLAG)))) return rc;
+        if ((rc = d2h(ctx, qt, ctx->ws[WS_FLAG].p, sizeof qt))) return rc;
+        exsq = grid_exact_squares(qt);
+    }
     if ((rc = launch_sil_points(s, X, d, metric, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), assign, near,
-                                N, sv)))
+                                N, sv, exsq)))
         return rc;
     if ((rc = launch_sil_sum(s, sv, slot<int32_t>(ctx, WS_ROWS), slot<int64_t>(ctx, WS_CROW), K, N, raw, out))) return rc;
     return d2h(ctx, out_host, out, (size_t)(K + 1) * 8);

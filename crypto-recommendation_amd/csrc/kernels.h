@@ -209,6 +209,11 @@ size_t seg_columns_ws_bytes(int64_t n, int K, int m);
 int launch_seg_iota(hipStream_t s, int32_t* iota, int64_t n);
 int launch_seg_columns(hipStream_t s, const double* V, int64_t n, int K, int m, const int32_t* iota,
                        const int64_t* crow, const double* carry, double* out, void* ws);
+// Grid test of a matrix's values (update.hip): qt [3] device ints; after the
+// copy back, grid_exact_squares says whether every difference of two values
+// squares exactly with pow(x, 2) == x*x.
+int launch_grid_bits(hipStream_t s, Pts X, int64_t n, int* qt);
+bool grid_exact_squares(const int* qt_host);
 int launch_km_finalize(hipStream_t s, const double* sums, const int64_t* counts, int K, int d, const double* C_old,
                        int metric, double min_dist, double* C_new, int* moved);
 
@@ -421,7 +426,7 @@ int launch_range_scatter(hipStream_t s, const int32_t* list, int64_t M, const in
 // Silhouette (silhouette.hip).
 int launch_sil_near(hipStream_t s, const double* C, int K, int d, int metric, int32_t* near);
 int launch_sil_points(hipStream_t s, Pts X, int d, int metric, const int32_t* rows, const int64_t* crow,
-                      const int32_t* assign, const int32_t* near, int64_t N, double* s_out);
+                      const int32_t* assign, const int32_t* near, int64_t N, double* s_out, bool exsq = false);
 int launch_sil_sum(hipStream_t s, const double* sv, const int32_t* rows, const int64_t* crow, int K, int64_t N,
                    double* raw, double* out);
 

@@ -51,7 +51,7 @@ constexpr int SIL_DMAX = 512;
 // 16 doubles of wave-private LDS; glibc's pow restated for the few squares
 // that need it, batched over the wave -- per lane, a wave paid it in nearly
 // every term).
-template <typename TX>
+template <typename TX, bool EXSQ>
 __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restrict__ xj, int d, double* sq) {
     double acc = 0.0;
     int k = 0;
@@ -66,7 +66,7 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
 #pragma unroll
                 for (int u = 0; u < 4; u++) df[4 * h + u] = __dsub_rn(a[u], b[u]);
             }
-            gp_sq_wave<8, sizeof(TX) == 8>(df, p, sq);
+            gp_sq_wave<8, sizeof(TX) == 8, EXSQ>(df, p, sq);
 #pragma unroll
             for (int u = 0; u < 8; u++) acc = __dadd_rn(acc, p[u]);
         }
@@ -76,7 +76,7 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
             ld4d(xj + k, b);
 #pragma unroll
             for (int u = 0; u < 4; u++) df[u] = __dsub_rn(a[u], b[u]);
-            gp_sq_wave<4, sizeof(TX) == 8>(df, p, sq);
+            gp_sq_wave<4, sizeof(TX) == 8, EXSQ>(df, p, sq);
 #pragma unroll
             for (int u = 0; u < 4; u++) acc = __dadd_rn(acc, p[u]);
             k += 4;
@@ -86,7 +86,7 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
     for (; k < d; k++) {
         const double df[1] = {__dsub_rn((double)xi[k], (double)xj[k])};
         double p[1];
-        gp_sq_wave<1, sizeof(TX) == 8>(df, p, sq);
+        gp_sq_wave<1, sizeof(TX) == 8, EXSQ>(df, p, sq);
         acc = __dadd_rn(acc, p[0]);
     }
     return sqrt(acc);
@@ -94,7 +94,7 @@ __device__ inline double sil_euclid(const TX* __restrict__ xi, const TX* __restr
 
 // sum_{j in [j0, j1)} d(x_i, x_rows[j]) in j order (wave-uniform result);
 // lanes past j1 repeat the last member so the whole wave stays in step
-template <typename TX>
+template <typename TX, bool EXSQ>
 __device__ inline double sil_segment(const TX* __restrict__ xi, const TX* __restrict__ X, int d, int metric,
                                      const int32_t* __restrict__ rows, int64_t j0, int64_t j1, int lane,
                                      double* sq) {
@@ -102,7 +102,7 @@ __device__ inline double sil_segment(const TX* __restrict__ xi, const TX* __rest
     for (int64_t jb = j0; jb < j1; jb += 64) {
         const int64_t j = min<int64_t>(jb + lane, j1 - 1);
         const TX* xj = X + (size_t)rows[j] * d;
-        const double dj = metric == 0 ? sil_euclid(xi, xj, d, sq) : exact_dist(xi, xj, d, metric);
+        const double dj = metric == 0 ? sil_euclid<TX, EXSQ>(xi, xj, d, sq) : exact_dist(xi, xj, d, metric);
         const int n = (int)min<int64_t>(64, j1 - jb);
         for (int t = 0; t < n; t++) acc = __dadd_rn(acc, __shfl(dj, t));
     }
@@ -111,7 +111,7 @@ __device__ inline double sil_segment(const TX* __restrict__ xi, const TX* __rest
 
 // Two members (same cluster) against the same x_j: each x_j load serves both
 // (d % 4 == 0).
-template <typename TX>
+template <typename TX, bool EXSQ>
 __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restrict__ xb,
                                    const TX* __restrict__ xj, int d, double& da, double& db, double* sq) {
     double aa = 0.0, ab = 0.0;
@@ -131,7 +131,7 @@ __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restri
                 df[8 * h + 2 * e + 1] = __dsub_rn(v[e], b[e]);
             }
         }
-        gp_sq_wave<16, sizeof(TX) == 8>(df, p, sq);
+        gp_sq_wave<16, sizeof(TX) == 8, EXSQ>(df, p, sq);
 #pragma unroll
         for (int e = 0; e < 8; e++) {
             aa = __dadd_rn(aa, p[2 * e]);
@@ -148,7 +148,7 @@ __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restri
             df[2 * e] = __dsub_rn(u[e], b[e]);
             df[2 * e + 1] = __dsub_rn(v[e], b[e]);
         }
-        gp_sq_wave<8, sizeof(TX) == 8>(df, p, sq);
+        gp_sq_wave<8, sizeof(TX) == 8, EXSQ>(df, p, sq);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             aa = __dadd_rn(aa, p[2 * e]);
@@ -159,7 +159,7 @@ __device__ inline void sil_euclid2(const TX* __restrict__ xa, const TX* __restri
     db = sqrt(ab);
 }
 
-template <typename TX>
+template <typename TX, bool EXSQ>
 __device__ inline void sil_segment2(const TX* __restrict__ xa, const TX* __restrict__ xb,
                                     const TX* __restrict__ X, int d, const int32_t* __restrict__ rows, int64_t j0,
                                     int64_t j1, int lane, double& sa, double& sb, double* sq) {
@@ -167,7 +167,7 @@ __device__ inline void sil_segment2(const TX* __restrict__ xa, const TX* __restr
     for (int64_t jb = j0; jb < j1; jb += 64) {
         const int64_t j = min<int64_t>(jb + lane, j1 - 1);
         double da, db;
-        sil_euclid2(xa, xb, X + (size_t)rows[j] * d, d, da, db, sq);
+        sil_euclid2<TX, EXSQ>(xa, xb, X + (size_t)rows[j] * d, d, da, db, sq);
         const int n = (int)min<int64_t>(64, j1 - jb);
         for (int t = 0; t < n; t++) {
             acc_a = __dadd_rn(acc_a, __shfl(da, t));
@@ -188,7 +188,9 @@ __device__ inline double sil_value(double a, double b, int64_t c0, int64_t c1, i
     return x86_nan(__ddiv_rn(__dsub_rn(b, a), mx));
 }
 
-template <typename TX>
+// EXSQ: every difference of the rows squares exactly (data_grid_exact): x*x
+// for pow(x, 2) without the per-square test.
+template <typename TX, bool EXSQ>
 __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
     const TX* __restrict__ X, int d, int metric, const int32_t* __restrict__ rows, const int64_t* __restrict__ crow,
     const int32_t* __restrict__ assign, const int32_t* __restrict__ near, int64_t N, double* __restrict__ s_out) {
@@ -219,8 +221,8 @@ __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
             const int nc = near[ca];
             const int64_t n0 = crow[nc], n1 = crow[nc + 1];
             double a0, a1, b0, b1;
-            sil_segment2(xa, xb, X, d, rows, c0, c1, lane, a0, a1, sq);
-            sil_segment2(xa, xb, X, d, rows, n0, n1, lane, b0, b1, sq);
+            sil_segment2<TX, EXSQ>(xa, xb, X, d, rows, c0, c1, lane, a0, a1, sq);
+            sil_segment2<TX, EXSQ>(xa, xb, X, d, rows, n0, n1, lane, b0, b1, sq);
             if (lane == 0) {
                 s_out[ra] = sil_value(a0, b0, c0, c1, n0, n1);
                 s_out[rb] = sil_value(a1, b1, c0, c1, n0, n1);
@@ -231,10 +233,10 @@ __global__ __launch_bounds__(64 * SP_WAVES) void sil_point_kernel(
             const TX* xi = m ? xb : xa;
             const int c = m ? cb : ca;
             const int64_t c0 = crow[c], c1 = crow[c + 1];
-            const double a = sil_segment(xi, X, d, metric, rows, c0, c1, lane, sq);
+            const double a = sil_segment<TX, EXSQ>(xi, X, d, metric, rows, c0, c1, lane, sq);
             const int nc = near[c];
             const int64_t n0 = crow[nc], n1 = crow[nc + 1];
-            const double b = sil_segment(xi, X, d, metric, rows, n0, n1, lane, sq);
+            const double b = sil_segment<TX, EXSQ>(xi, X, d, metric, rows, n0, n1, lane, sq);
             if (lane == 0) s_out[m ? rb : ra] = sil_value(a, b, c0, c1, n0, n1);
         }
     }
@@ -293,22 +295,26 @@ int launch_sil_near(hipStream_t s, const double* C, int K, int d, int metric, in
 
 template <typename TX>
 static int sil_points_tx(hipStream_t s, const TX* X, int d, int metric, const int32_t* rows, const int64_t* crow,
-                         const int32_t* assign, const int32_t* near, int64_t N, double* s_out) {
+                         const int32_t* assign, const int32_t* near, int64_t N, double* s_out, bool exsq) {
     if (d > SIL_DMAX) {
         hipLaunchKernelGGL(sil_point_thread_kernel<TX>, dim3(gsz(N, 256, 16384)), dim3(256), 0, s, X, d, metric, rows,
                            crow, assign, near, N, s_out);
         return kstatus("sil_point_thread_kernel");
     }
-    hipLaunchKernelGGL(sil_point_kernel<TX>, dim3(gsz((N + 1) / 2, SP_WAVES, 16384)), dim3(64 * SP_WAVES), 0, s, X, d,
-                       metric, rows, crow, assign, near, N, s_out);
+    if (exsq)
+        hipLaunchKernelGGL((sil_point_kernel<TX, true>), dim3(gsz((N + 1) / 2, SP_WAVES, 16384)), dim3(64 * SP_WAVES), 0,
+                           s, X, d, metric, rows, crow, assign, near, N, s_out);
+    else
+        hipLaunchKernelGGL((sil_point_kernel<TX, false>), dim3(gsz((N + 1) / 2, SP_WAVES, 16384)), dim3(64 * SP_WAVES), 0,
+                           s, X, d, metric, rows, crow, assign, near, N, s_out);
     return kstatus("sil_point_kernel");
 }
 
 int launch_sil_points(hipStream_t s, Pts X, int d, int metric, const int32_t* rows, const int64_t* crow,
-                      const int32_t* assign, const int32_t* near, int64_t N, double* s_out) {
+                      const int32_t* assign, const int32_t* near, int64_t N, double* s_out, bool exsq) {
     if (N == 0) return 0;
-    return X.f64 ? sil_points_tx(s, X.d(), d, metric, rows, crow, assign, near, N, s_out)
-                 : sil_points_tx(s, X.f(), d, metric, rows, crow, assign, near, N, s_out);
+    return X.f64 ? sil_points_tx(s, X.d(), d, metric, rows, crow, assign, near, N, s_out, exsq)
+                 : sil_points_tx(s, X.f(), d, metric, rows, crow, assign, near, N, s_out, exsq);
 }
 
 int launch_sil_sum(hipStream_t s, const double* sv, const int32_t* rows, const int64_t* crow, int K, int64_t N,

@@ -906,6 +906,51 @@ int launch_km_sums_seg(hipStream_t s, Pts X, int d, const int32_t* rows, const i
     return kstatus("update.hip (segmented)");
 }
 
+// ------------------------------------------------------------------ grid test
+// Whether every difference of two values of X squares exactly in fp64 and
+// pow(x, 2) of it is x*x (gpow2.h): all finite values are multiples of 2^q below
+// 2^t with t - q <= 25 (a difference then has <= 26 significant bits) and q >=
+// -460 (no square near the subnormal range). qt: [q min, t max, bad].
+__global__ void grid_bits_init_kernel(int* qt) {
+    qt[0] = 1 << 30;
+    qt[1] = -(1 << 30);
+    qt[2] = 0;
+}
+template <typename TX>
+__global__ __launch_bounds__(256) void grid_bits_kernel(const TX* __restrict__ X, int64_t n, int* __restrict__ qt) {
+    int q = 1 << 30, t = -(1 << 30);
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        int qi, ti;
+        if (km_fx_bits(X[i], qi, ti, bad)) {
+            q = min(q, qi);
+            t = max(t, ti);
+        }
+    }
+    // wave reductions, then one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) {
+        q = min(q, __shfl_xor(q, o));
+        t = max(t, __shfl_xor(t, o));
+    }
+    const bool anybad = __ballot(bad) != 0ull;
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(qt, q);
+        atomicMax(qt + 1, t);
+        if (anybad) atomicOr(qt + 2, 1);
+    }
+}
+int launch_grid_bits(hipStream_t s, Pts X, int64_t n, int* qt) {
+    hipLaunchKernelGGL(grid_bits_init_kernel, dim3(1), dim3(1), 0, s, qt);
+    if (n > 0) {
+        if (X.f64) hipLaunchKernelGGL(grid_bits_kernel<double>, dim3(gsz(n, 256, 4096)), dim3(256), 0, s, X.d(), n, qt);
+        else hipLaunchKernelGGL(grid_bits_kernel<float>, dim3(gsz(n, 256, 4096)), dim3(256), 0, s, X.f(), n, qt);
+    }
+    return kstatus("update.hip (grid bits)");
+}
+bool grid_exact_squares(const int* qt_host) {
+    return qt_host[2] == 0 && (qt_host[0] > qt_host[1] || (qt_host[1] - qt_host[0] <= 25 && qt_host[0] >= -460));
+}
+
 // ------------------------------------------------------------------ long chains
 // Column sums of a row-major [n][m] fp64 block V, each column one sequential
 // chain in row order from carry (NULL: 0) -- the same segmented evaluation

@@ -47,14 +47,18 @@ def test_silhouette_range_golden(ctx, name):
         assert np.array_equal(bits(out), bits(g[f"sil{it}"])), (it, out, g[f"sil{it}"])
 
 
-@pytest.mark.parametrize("N,d,K,metric,zero_every", [
-    (20_000, 128, 16, "euclidean", 0),
-    (30_000, 16, 64, "euclidean", 0),
-    (12_000, 64, 12, "cosine", 101),       # zero rows: NaN distances
-    (5_000, 8, 300, "euclidean", 0),       # many small (and some empty) clusters
+@pytest.mark.parametrize("N,d,K,metric,zero_every,kind", [
+    (20_000, 128, 16, "euclidean", 0, "grid"),     # every square exact: the x*x form (grid test)
+    (30_000, 16, 64, "euclidean", 0, "grid"),
+    (12_000, 64, 12, "cosine", 101, "grid"),       # zero rows: NaN distances
+    (5_000, 8, 300, "euclidean", 0, "grid"),       # many small (and some empty) clusters
+    (12_000, 128, 10, "euclidean", 0, "normal"),   # full mantissas: glibc's pow where x*x may differ
+    (6_000, 40, 24, "euclidean", 0, "wide"),       # a grid wider than 26 bits (x*x exact for most, not all)
 ])
-def test_silhouette_vs_oracle(ctx, N, d, K, metric, zero_every):
-    Xh = oracle.synth(900 + d, N, d)
+def test_silhouette_vs_oracle(ctx, N, d, K, metric, zero_every, kind):
+    Xh = oracle.synth(900 + d, N, d, kind="normal" if kind == "normal" else "grid")
+    if kind == "wide":
+        Xh[::7, 3] *= np.float32(2.0 ** 12)                 # spans 2^-15 .. 2^15: differences of up to 31 bits
     if zero_every:
         Xh[3::zero_every] = 0.0
     src = (np.arange(K) * (N // K)).astype(np.int32)
