@@ -1091,11 +1091,14 @@ constexpr double FH_A = 130.0 * 0x1p-23;
 #define FH_WAVES_MPFAST 12     // the last pass of the multi-pass form with the certified distance
 #endif
 template <bool HASH, bool MP, int MET, bool FAST = false>
+#ifndef FH_FAST_WAVES
+#define FH_FAST_WAVES 8     // the single-pass FAST form (the headline kernel)
+#endif
 __host__ __device__ constexpr int fh_waves() {
 #ifdef FH_WAVES_SET
     return FH_WAVES_SET;
 #else
-    return HASH && MP ? 12 : (MP && FAST ? FH_WAVES_MPFAST : 8);
+    return HASH && MP ? 12 : (MP && FAST ? FH_WAVES_MPFAST : (FAST && !MP ? FH_FAST_WAVES : 8));
 #endif
 }
 constexpr int FH_WAVES_MIN = 8, FH_WAVES_MAX = 12;
@@ -2480,9 +2483,11 @@ int launch_fused(hipStream_t s, bool hash, FusedLaunch& f) {
                         const size_t lg = (size_t)fh_gath_off(a.Kpad, hash) + 8 * FH_GATH_WAVE;
                         // the certified f32 winner distance (a.fast_dist) compiled in
                         if (hash && a.fast_dist)
-                            hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);
+                            hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, false, 0, true>), grid,
+                                               dim3(64 * fh_waves<true, false, 0, true>()), lh, s, a);
                         else if (a.fast_dist)
-                            hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 0, true>), grid, dim3(64 * 8), lh, s, a);
+                            hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, false, 0, true>), grid,
+                                               dim3(64 * fh_waves<false, false, 0, true>()), lh, s, a);
                         else if (hash)
                             hipLaunchKernelGGL((fused_hi_kernel<true, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);
                         else hipLaunchKernelGGL((fused_hi_kernel<false, false, 0, 1, true>), grid, dim3(64 * 8), lg, s, a);

@@ -35,14 +35,14 @@ for step in "$@"; do
       rc=$?; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit $rc; } ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
-         -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-c5 \
+         -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-c5 --no-normal-leg \
          > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err")
       rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
       find "$OUT/prof" -name '*kernel_stats.csv' -exec head -8 {} \; ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --pmc $c --output-format csv \
-           -d "$OUT/pmc_$c" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-c5 --no-exact-dist-line \
+           -d "$OUT/pmc_$c" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-c5 --no-exact-dist-line --no-normal-leg \
            > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err")
         rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
@@ -64,7 +64,7 @@ for step in "$@"; do
                  "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_SALU"; do
         i=$((i+1))
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --pmc $set --output-format csv \
-           -d "$OUT/sq$i" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-c5 --no-exact-dist-line \
+           -d "$OUT/sq$i" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-c5 --no-exact-dist-line --no-normal-leg \
            > "$OUT/sq$i.json" 2> "$OUT/sq$i.err")
         rc=$?; echo "sq pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
       done ;;
