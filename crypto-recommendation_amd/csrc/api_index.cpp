@@ -760,15 +760,16 @@ static int shard_begin_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64_
 }
 
 static int shard_prepare_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64_t* crow, const int32_t* rows, int K,
-                              const double* start, const int32_t* flag, void* ws, int64_t ws_bytes) {
-    LSHKM_CHECK(ctx && (X.p || N == 0) && crow && (rows || N == 0) && start && flag && ws && N >= 0 &&
+                              const double* start, const int32_t* flag, const uint8_t* mask, void* ws,
+                              int64_t ws_bytes) {
+    LSHKM_CHECK(ctx && (X.p || N == 0) && crow && (rows || N == 0) && start && flag && mask && ws && N >= 0 &&
                     N < (1ll << 31) && d > 0 && K > 0 && K <= 65535,
                 LSHKM_ERR_ARG, "bad arguments");
     LSHKM_CHECK(ws_bytes >= (int64_t)km_shard_ws_bytes(N, K, d), LSHKM_ERR_ARG,
                 "workspace smaller than lshkm_kmeans_shard_ws_bytes");
     LSHKM_HIP(hipSetDevice(ctx->device));
     int rc;
-    if ((rc = launch_km_shard_prepare(ctx->stream, X, d, rows, crow, K, N, start, flag, ws))) {
+    if ((rc = launch_km_shard_prepare(ctx->stream, X, d, rows, crow, K, N, start, flag, mask, ws))) {
         LSHKM_LAUNCH_CHECK();
         return rc;
     }
@@ -831,15 +832,15 @@ int lshkm_kmeans_shard_ws_bytes(int64_t N, int K, int d, int64_t* bytes) {
 }
 
 int lshkm_kmeans_shard_prepare(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow,
-                               const int32_t* rows, int K, const double* start, const int32_t* flag, void* ws,
-                               int64_t ws_bytes) {
-    return shard_prepare_impl(ctx, X, N, d, crow, rows, K, start, flag, ws, ws_bytes);
+                               const int32_t* rows, int K, const double* start, const int32_t* flag,
+                               const uint8_t* mask, void* ws, int64_t ws_bytes) {
+    return shard_prepare_impl(ctx, X, N, d, crow, rows, K, start, flag, mask, ws, ws_bytes);
 }
 
 int lshkm_kmeans_shard_prepare_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const int64_t* crow,
-                                   const int32_t* rows, int K, const double* start, const int32_t* flag, void* ws,
-                                   int64_t ws_bytes) {
-    return shard_prepare_impl(ctx, X, N, d, crow, rows, K, start, flag, ws, ws_bytes);
+                                   const int32_t* rows, int K, const double* start, const int32_t* flag,
+                                   const uint8_t* mask, void* ws, int64_t ws_bytes) {
+    return shard_prepare_impl(ctx, X, N, d, crow, rows, K, start, flag, mask, ws, ws_bytes);
 }
 
 int lshkm_kmeans_shard_chain(lshkm_ctx ctx, const float* X, int64_t N, int d, const int64_t* crow, const int32_t* rows,

@@ -199,7 +199,7 @@ int launch_km_shard_certify(hipStream_t s, const double* gathered, int world, in
                             const int32_t* qt, const int64_t* counts, int K, int d, double* sums_out, double* start,
                             int* flag, uint8_t* mask, unsigned long long* nflag);
 int launch_km_shard_prepare(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
-                            const double* start, const int* flag, void* ws);
+                            const double* start, const int* flag, const uint8_t* mask, void* ws);
 int launch_km_shard_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
                           const int* flag, const uint8_t* mask, const double* carry, void* ws, double* sums);
 // Column chains of K row blocks [crow[k], crow[k+1]) of a row-major [n][m]

@@ -407,12 +407,66 @@ __global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X,
     km_fx_flush(acc + (size_t)c * d + j + 1, s1, a1, q1, t1, bad1);
 }
 
+// The flagged chains of at most KM_LANE_MAX members (global count): one lane
+// each, the reference's sequential adds in member order from carry (NULL: 0).
+// Per step a lane issues the values of one block of KML_B member positions
+// (their indices were loaded the step before) and the indices of the next, so
+// one round trip covers both; lanes of one cluster (consecutive list entries)
+// share the index loads and read neighbouring dims of the same rows. Far
+// cheaper than the segment passes when few chains are flagged (0.8 % of the C5
+// chains on full-mantissa rows: their 64-dim blocks touch ~40 % of the windows).
+constexpr int64_t KM_LANE_MAX = 32768;
+constexpr int KML_B = 32;
+template <typename TX>
+__global__ __launch_bounds__(256) void km_chain_lanes_kernel(const TX* __restrict__ X, int d,
+                                                            const int32_t* __restrict__ rows,
+                                                            const int64_t* __restrict__ crow,
+                                                            const int32_t* __restrict__ list,
+                                                            const unsigned int* __restrict__ count,
+                                                            const double* __restrict__ carry, double* __restrict__ sums) {
+    const int64_t nl = (int64_t)*count;
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nl; t += (int64_t)gridDim.x * 256) {
+        const int32_t i = list[t];
+        const int c = i / d, j = i - c * d;
+        const int64_t beg = crow[c], end = crow[c + 1];
+        double s = carry ? carry[i] : 0.0;
+        int32_t ix[KML_B];
+#pragma unroll
+        for (int u = 0; u < KML_B; u++) ix[u] = rows[min(beg + u, end - 1)];
+        for (int64_t p0 = beg; p0 < end; p0 += KML_B) {
+            TX v[KML_B];
+#pragma unroll
+            for (int u = 0; u < KML_B; u++) v[u] = X[(int64_t)ix[u] * d + j];
+            const int64_t pn = p0 + KML_B;
+#pragma unroll
+            for (int u = 0; u < KML_B; u++) ix[u] = rows[min(pn + u, end - 1)];
+#pragma unroll
+            for (int u = 0; u < KML_B; u++)
+                if (p0 + u < end) s = __dadd_rn(s, (double)v[u]);
+        }
+        sums[i] = s;
+    }
+}
+
+// Append entry i to the lane list (order kept within a wave: ballot prefix,
+// one atomic per wave).
+__device__ inline void km_lane_append(bool want, int32_t i, int32_t* __restrict__ list, unsigned int* __restrict__ cnt) {
+    const unsigned long long m = __ballot(want);
+    if (!m) return;
+    const int lane = (int)(threadIdx.x & 63), leader = __builtin_ctzll(m);
+    unsigned int base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (unsigned int)__popcll(m));
+    base = __shfl(base, leader);
+    if (want) list[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+}
+
 // Per (c, j): the exact sum if the chain provably never rounds, else a flag for
 // the sequential kernel. carry (sharded exact mode): the chain starts from it.
 __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_t* __restrict__ crow, int K, int d,
                                       const double* __restrict__ carry, const int64_t* __restrict__ carry_counts,
                                       double* __restrict__ sums, int* __restrict__ flag,
-                                      unsigned long long* __restrict__ stat) {
+                                      unsigned long long* __restrict__ stat, int32_t* __restrict__ lanes,
+                                      unsigned int* __restrict__ lane_cnt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)K * d) return;
     const int c = (int)(i / d);
@@ -435,8 +489,12 @@ __global__ void km_fx_finalize_kernel(const KmFx* __restrict__ acc, const int64_
         if (bad) ok = false;
     }
     ok = ok && km_cert(qmin, tmax, cnt, as);
+    // a flagged chain: one lane of km_chain_lanes_kernel when it is short (and
+    // a lane list is given), else its (c, 64-dim block) to the block kernels
+    const bool lane_chain = !ok && lanes && cnt <= KM_LANE_MAX;
     if (ok) sums[i] = s;
-    else atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));   // chain block (c, j/64) goes sequential
+    else if (!lane_chain) atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));
+    if (lanes) km_lane_append(lane_chain, (int32_t)i, lanes, lane_cnt);
     if (stat) {
         const unsigned long long nb = __ballot(!ok);
         if (nb && (threadIdx.x & 63) == __builtin_ctzll(nb)) atomicAdd(stat, (unsigned long long)__popcll(nb));
@@ -460,7 +518,7 @@ __global__ __launch_bounds__(64) void km_chain_flagged_kernel(const TX* __restri
 }
 
 
-size_t km_fx_ws_bytes(int K, int d) { return (size_t)K * d * sizeof(KmFx) + (size_t)K * 4 + 64; }
+size_t km_fx_ws_bytes(int K, int d) { return (size_t)K * d * sizeof(KmFx) + (size_t)K * 4 + 64 + (size_t)K * d * 4 + 64; }
 
 int launch_km_sums_seg(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
                        double* sums, int64_t* counts, const double* carry, const int64_t* carry_counts, void* ws,
@@ -471,8 +529,10 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
                       unsigned long long* stat, void* seg_ws) {
     KmFx* acc = reinterpret_cast<KmFx*>(ws);
     int* flag = reinterpret_cast<int*>(acc + (size_t)K * d);
+    unsigned int* lane_cnt = reinterpret_cast<unsigned int*>(flag + K);
+    int32_t* lanes = reinterpret_cast<int32_t*>(lane_cnt + 16);
     const int64_t n = (int64_t)K * d;
-    (void)hipMemsetAsync(flag, 0, (size_t)K * 4, s);
+    (void)hipMemsetAsync(flag, 0, (size_t)K * 4 + 64, s);      // the flags and the lane count
     hipLaunchKernelGGL(km_fx_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, n);
     const int jb = (d + 63) / 64;
     const dim3 fgrid((unsigned)((M + KMF_CH - 1) / KMF_CH), (unsigned)jb);
@@ -483,8 +543,19 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
                                acc);
         else hipLaunchKernelGGL(km_fx_kernel<float>, fgrid, dim3(64), 0, s, X.f(), d, rows, crow, K, M, acc);
     }
+    // the lane form for short flagged chains where the segment form would run
+    // (test switch LSHKM_KM_LANES=0: every flagged chain to the block kernels)
+    const bool use_lanes = seg_ws && !test_switch("LSHKM_KM_FLAGGED", "chain") && !test_switch("LSHKM_KM_LANES", "0");
     hipLaunchKernelGGL(km_fx_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, crow, K, d, carry,
-                       carry_counts, sums, flag, stat);
+                       carry_counts, sums, flag, stat, use_lanes ? lanes : nullptr, lane_cnt);
+    if (use_lanes) {
+        if (X.f64)
+            hipLaunchKernelGGL(km_chain_lanes_kernel<double>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.d(), d, rows, crow,
+                               lanes, lane_cnt, carry, sums);
+        else
+            hipLaunchKernelGGL(km_chain_lanes_kernel<float>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.f(), d, rows, crow,
+                               lanes, lane_cnt, carry, sums);
+    }
     if (seg_ws && !test_switch("LSHKM_KM_FLAGGED", "chain")) {
         // the flagged chains by binade segments (every window of theirs in
         // parallel; the sequential form's time was set by the longest chain:
@@ -835,7 +906,7 @@ __global__ __launch_bounds__(64) void ks_compose_kernel(const TX* __restrict__ X
             B = Cn;
         }
     }
-    if (lane == 0 && (!mask || mask[(size_t)c * d + j])) sums[(size_t)c * d + j] = s;
+    if (lane == 0 && (!mask || mask[(size_t)c * d + j] == 1)) sums[(size_t)c * d + j] = s;
 }
 
 static int64_t ks_pairs(int64_t M, int K) { return (M + KS_W - 1) / KS_W + K; }
@@ -1018,17 +1089,18 @@ __global__ void km_shard_certify_kernel(const double* __restrict__ gathered, int
         tot = __dadd_rn(tot, gathered[(size_t)r * n + i]);
     }
     const bool ok = km_cert(qt[i], -qt[n + i], counts[c], asum[i]);
+    const bool lane_chain = !ok && counts[c] <= KM_LANE_MAX;     // the global count: the same split on every rank
     if (start) start[i] = pre;
     sums_out[i] = tot;                           // the chain's value where ok; the carry replaces the rest
-    mask[i] = ok ? 0 : 1;
-    if (!ok) atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));
+    mask[i] = ok ? 0 : (lane_chain ? 2 : 1);     // 1: segment records, 2: one lane (km_chain_lanes_kernel)
+    if (!ok && !lane_chain) atomicOr(flag + c, 1 << min(31, (int)(i % d) / 64));
     const unsigned long long nb = __ballot(!ok);
     if (nb && (threadIdx.x & 63) == __builtin_ctzll(nb)) atomicAdd(nflag, (unsigned long long)__popcll(nb));
 }
 
 int launch_km_shard_begin(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
                           double* sums, double* asum, int32_t* qt, int64_t* counts, void* ws) {
-    KmFx* acc = reinterpret_cast<KmFx*>(ws);
+    KmFx* acc = reinterpret_cast<KmFx*>(ws);      // the context's k-means workspace (km_fx_ws_bytes)
     const int64_t n = (int64_t)K * d;
     hipLaunchKernelGGL(km_fx_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, acc, n);
     const int jb = (d + 63) / 64;
@@ -1056,15 +1128,31 @@ int launch_km_shard_certify(hipStream_t s, const double* gathered, int world, in
     return kstatus("update.hip (shard certify)");
 }
 
+// [lane count (64 B) | lane list (K * d int32), 256-B aligned] then the
+// begin pass's accumulators or the segment records
+static size_t km_shard_lane_bytes(int K, int d) { return ((size_t)K * d * 4 + 64 + 255) / 256 * 256; }
 size_t km_shard_ws_bytes(int64_t M, int K, int d) {
-    return std::max((size_t)K * d * sizeof(KmFx) + 64, km_seg_ws_bytes(M, K, d));
+    return km_shard_lane_bytes(K, d) + std::max((size_t)K * d * sizeof(KmFx) + 64, km_seg_ws_bytes(M, K, d));
+}
+
+__global__ void km_lane_list_kernel(const uint8_t* __restrict__ mask, int64_t n, int32_t* __restrict__ list,
+                                    unsigned int* __restrict__ cnt) {
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = b + threadIdx.x;
+        km_lane_append(i < n && mask[i] == 2, (int32_t)i, list, cnt);
+    }
 }
 
 // The flagged chains' segment records from their approximate starts on this
 // rank (passes A-C, carry-free: all ranks at once).
 int launch_km_shard_prepare(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
-                            const double* start, const int* flag, void* ws) {
-    const KsWs w(ws, M, K, d);
+                            const double* start, const int* flag, const uint8_t* mask, void* ws) {
+    unsigned int* lane_cnt = reinterpret_cast<unsigned int*>(ws);
+    int32_t* lanes = reinterpret_cast<int32_t*>(lane_cnt + 16);
+    const int64_t n = (int64_t)K * d;
+    if (hipMemsetAsync(lane_cnt, 0, 64, s) != hipSuccess) return kstatus("update.hip (shard prepare memset)");
+    hipLaunchKernelGGL(km_lane_list_kernel, dim3(gsz(n, 256, 4096)), dim3(256), 0, s, mask, n, lanes, lane_cnt);
+    const KsWs w(reinterpret_cast<char*>(ws) + km_shard_lane_bytes(K, d), M, K, d);
     if (X.f64) km_seg_records(s, X.d(), d, rows, crow, K, M, start, flag, w);
     else km_seg_records(s, X.f(), d, rows, crow, K, M, start, flag, w);
     return kstatus("update.hip (shard prepare)");
@@ -1074,9 +1162,20 @@ int launch_km_shard_prepare(hipStream_t s, Pts X, int d, const int32_t* rows, co
 // rank's running sums; NULL on the first rank: from 0), written where mask is set.
 int launch_km_shard_chain(hipStream_t s, Pts X, int d, const int32_t* rows, const int64_t* crow, int K, int64_t M,
                           const int* flag, const uint8_t* mask, const double* carry, void* ws, double* sums) {
-    const KsWs w(ws, M, K, d);
-    if (X.f64) km_seg_compose(s, X.d(), d, rows, crow, K, carry, flag, mask, w, sums);
-    else km_seg_compose(s, X.f(), d, rows, crow, K, carry, flag, mask, w, sums);
+    const unsigned int* lane_cnt = reinterpret_cast<const unsigned int*>(ws);
+    const int32_t* lanes = reinterpret_cast<const int32_t*>(lane_cnt + 16);
+    const int64_t n = (int64_t)K * d;
+    const KsWs w(reinterpret_cast<char*>(ws) + km_shard_lane_bytes(K, d), M, K, d);
+    // mask 1: the segment composition (flag bits), mask 2: one lane per chain
+    if (X.f64) {
+        km_seg_compose(s, X.d(), d, rows, crow, K, carry, flag, mask, w, sums);
+        hipLaunchKernelGGL(km_chain_lanes_kernel<double>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.d(), d, rows, crow,
+                           lanes, lane_cnt, carry, sums);
+    } else {
+        km_seg_compose(s, X.f(), d, rows, crow, K, carry, flag, mask, w, sums);
+        hipLaunchKernelGGL(km_chain_lanes_kernel<float>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.f(), d, rows, crow,
+                           lanes, lane_cnt, carry, sums);
+    }
     return kstatus("update.hip (shard chain)");
 }
 

@@ -121,7 +121,7 @@ def lib():
             "lshkm_kmeans_shard_certify": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp,
                                                  C.POINTER(i64)]),
             "lshkm_kmeans_shard_ws_bytes": (i32, [i64, i32, i32, C.POINTER(i64)]),
-            "lshkm_kmeans_shard_prepare": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, i64]),
+            "lshkm_kmeans_shard_prepare": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, vp, i64]),
             "lshkm_kmeans_shard_chain": (i32, [vp, vp, i64, i32, vp, vp, i32, vp, vp, vp, vp, i64, vp]),
             "lshkm_kmeans_pp": (i32, [vp, vp, i64, i32, i32, i32, u64, vp]),
             "lshkm_rand_selection": (i32, [u64, i64, i32, vp]),
@@ -619,11 +619,11 @@ class ShardSums:
             self.ws = self.empty((int(nb.value),), self.ctx.torch.uint8)
         return self.ws
 
-    def prepare(self, start, flag):
+    def prepare(self, start, flag, mask):
         ws = self._ws()
         _ck(_fn("lshkm_kmeans_shard_prepare", self.X)(self.ctx.h, _t_ptr(self.X), self.N, self.d, _t_ptr(self.csr[0]),
                                                       _t_ptr(self.csr[1]), self.K, _t_ptr(start), _t_ptr(flag),
-                                                      _t_ptr(ws), ws.numel()))
+                                                      _t_ptr(mask), _t_ptr(ws), ws.numel()))
 
     def chain(self, flag, mask, carry, sums):
         ws = self._ws()

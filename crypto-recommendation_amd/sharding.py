@@ -213,7 +213,7 @@ def kmeans_sums_sharded(ops, timing=None):
     if timing is not None:
         timing["flagged"] = n_flagged
     if n_flagged:
-        ops.prepare(start, flag)            # carry-free: every rank at once
+        ops.prepare(start, flag, mask)      # carry-free: every rank at once
         carry = None
         if rank > 0:
             carry = ops.empty(tuple(out.shape), out.dtype)

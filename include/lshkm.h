@@ -331,12 +331,15 @@ int lshkm_kmeans_partial_carry_f64(lshkm_ctx ctx, const double* X_dev, int64_t N
  *     never-rounds test on the global values. Where it holds, every partial sum
  *     of any subset of the chain's values in any order is a double, so the
  *     total of the gathered partials IS the reference's chain: sums_out_dev.
- *     Elsewhere mask_dev [K][d] = 1 and flag_dev [K] has bit min(31, j / 64)
- *     set; start_dev [K][d] (may be NULL) = the chain's approximate value
+ *     Elsewhere mask_dev [K][d] != 0: 2 for a chain of at most 32,768 values
+ *     in all (one lane each in the chain phase), else 1 and flag_dev [K] has
+ *     bit min(31, j / 64) set (segment records); start_dev [K][d] (may be
+ *     NULL) = the chain's approximate value
  *     before this rank's rows (the lower ranks' partials); *n_flagged_host =
  *     the number of (c, j) masked (the same on every rank).
- *  4. only when *n_flagged_host > 0: lshkm_kmeans_shard_prepare (the masked
- *     chains' binade-segment records from start_dev; all ranks at once), then
+ *  4. only when *n_flagged_host > 0: lshkm_kmeans_shard_prepare (the lane
+ *     list and the masked chains' binade-segment records from start_dev; all
+ *     ranks at once), then
  *     in rank order lshkm_kmeans_shard_chain: the masked chains continued over
  *     this rank's rows from the previous rank's sums_out (carry_dev; NULL on
  *     rank 0), written into sums_dev where mask_dev is set; send sums_dev on.
@@ -359,10 +362,10 @@ int lshkm_kmeans_shard_certify(lshkm_ctx ctx, int K, int d, int world, int rank,
 int lshkm_kmeans_shard_ws_bytes(int64_t N, int K, int d, int64_t* bytes_host);
 int lshkm_kmeans_shard_prepare(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int64_t* crow_dev,
                                const int32_t* rows_dev, int K, const double* start_dev, const int32_t* flag_dev,
-                               void* ws_dev, int64_t ws_bytes);
+                               const uint8_t* mask_dev, void* ws_dev, int64_t ws_bytes);
 int lshkm_kmeans_shard_prepare_f64(lshkm_ctx ctx, const double* X_dev, int64_t N, int d, const int64_t* crow_dev,
                                    const int32_t* rows_dev, int K, const double* start_dev, const int32_t* flag_dev,
-                                   void* ws_dev, int64_t ws_bytes);
+                                   const uint8_t* mask_dev, void* ws_dev, int64_t ws_bytes);
 int lshkm_kmeans_shard_chain(lshkm_ctx ctx, const float* X_dev, int64_t N, int d, const int64_t* crow_dev,
                              const int32_t* rows_dev, int K, const int32_t* flag_dev, const uint8_t* mask_dev,
                              const double* carry_dev, void* ws_dev, int64_t ws_bytes, double* sums_dev);

@@ -85,14 +85,15 @@ class NumpyShardSums:
             tot = tot + g[r]
         qt = qt.numpy().astype(np.int64)
         ok = km_cert(qt[0], -qt[1], counts.numpy(), asum.numpy())
-        mask = (~ok).astype(np.uint8)
+        lane = ~ok & (counts.numpy()[:, None] <= 32768)           # one lane each (km_chain_lanes_kernel)
+        mask = np.where(ok, 0, np.where(lane, 2, 1)).astype(np.uint8)
         flag = np.zeros(self.K, np.int32)
-        for c, j in zip(*np.nonzero(~ok)):
+        for c, j in zip(*np.nonzero(mask == 1)):
             flag[c] |= np.int32(1 << min(31, j // 64))
         return (torch.from_numpy(tot), torch.from_numpy(pre), torch.from_numpy(flag), torch.from_numpy(mask),
                 int((~ok).sum()))
 
-    def prepare(self, start, flag):
+    def prepare(self, start, flag, mask):
         pass                                                 # the segment records: a device-side speedup only
 
     def chain(self, flag, mask, carry, sums):
