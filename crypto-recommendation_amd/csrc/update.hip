@@ -407,44 +407,50 @@ __global__ __launch_bounds__(64) void km_fx2_kernel(const float* __restrict__ X,
     km_fx_flush(acc + (size_t)c * d + j + 1, s1, a1, q1, t1, bad1);
 }
 
-// The flagged chains of at most KM_LANE_MAX members (global count): one lane
-// each, the reference's sequential adds in member order from carry (NULL: 0).
-// Per step a lane issues the values of one block of KML_B member positions
-// (their indices were loaded the step before) and the indices of the next, so
-// one round trip covers both; lanes of one cluster (consecutive list entries)
-// share the index loads and read neighbouring dims of the same rows. Far
-// cheaper than the segment passes when few chains are flagged (0.8 % of the C5
-// chains on full-mantissa rows: their 64-dim blocks touch ~40 % of the windows).
+// The flagged chains of at most KM_LANE_MAX members (global count): one wave
+// each (a lane list entry), the reference's sequential adds in member order
+// from carry (NULL: 0). Lane u loads member position p0 + u of a 64-position
+// block (the member indices coalesced, the values one per row), two blocks
+// ahead of the adds; lane 0 adds the block's 64 values in order (readlane).
+// A lane per chain left the few flagged chains of a call on a handful of CUs
+// (1,016 chains: 4 blocks of 256, 7 ms); a wave per chain spreads them.
+// Far cheaper than the segment passes when few chains are flagged (0.8 % of
+// the C5 chains on full-mantissa rows: their 64-dim blocks touch ~40 % of the
+// windows).
 constexpr int64_t KM_LANE_MAX = 32768;
-constexpr int KML_B = 32;
+__device__ inline double ks_rl(double v, int i);
 template <typename TX>
-__global__ __launch_bounds__(256) void km_chain_lanes_kernel(const TX* __restrict__ X, int d,
-                                                            const int32_t* __restrict__ rows,
-                                                            const int64_t* __restrict__ crow,
-                                                            const int32_t* __restrict__ list,
-                                                            const unsigned int* __restrict__ count,
-                                                            const double* __restrict__ carry, double* __restrict__ sums) {
+__global__ __launch_bounds__(64) void km_chain_lanes_kernel(const TX* __restrict__ X, int d,
+                                                           const int32_t* __restrict__ rows,
+                                                           const int64_t* __restrict__ crow,
+                                                           const int32_t* __restrict__ list,
+                                                           const unsigned int* __restrict__ count,
+                                                           const double* __restrict__ carry, double* __restrict__ sums) {
     const int64_t nl = (int64_t)*count;
-    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nl; t += (int64_t)gridDim.x * 256) {
+    const int lane = threadIdx.x;
+    for (int64_t t = blockIdx.x; t < nl; t += gridDim.x) {
         const int32_t i = list[t];
         const int c = i / d, j = i - c * d;
         const int64_t beg = crow[c], end = crow[c + 1];
         double s = carry ? carry[i] : 0.0;
-        int32_t ix[KML_B];
-#pragma unroll
-        for (int u = 0; u < KML_B; u++) ix[u] = rows[min(beg + u, end - 1)];
-        for (int64_t p0 = beg; p0 < end; p0 += KML_B) {
-            TX v[KML_B];
-#pragma unroll
-            for (int u = 0; u < KML_B; u++) v[u] = X[(int64_t)ix[u] * d + j];
-            const int64_t pn = p0 + KML_B;
-#pragma unroll
-            for (int u = 0; u < KML_B; u++) ix[u] = rows[min(pn + u, end - 1)];
-#pragma unroll
-            for (int u = 0; u < KML_B; u++)
-                if (p0 + u < end) s = __dadd_rn(s, (double)v[u]);
+        auto ld = [&](int64_t p0) -> double {
+            const int64_t p = min(p0 + lane, end - 1);
+            return end > beg ? (double)X[(int64_t)rows[p] * d + j] : 0.0;
+        };
+        double v0 = ld(beg), v1 = ld(beg + 64);
+        for (int64_t p0 = beg; p0 < end; p0 += 64) {
+            const double v = v0;
+            v0 = v1;
+            v1 = ld(p0 + 128);
+            const int n = (int)min((int64_t)64, end - p0);
+            if (n == 64) {
+#pragma unroll 16
+                for (int u = 0; u < 64; u++) s = __dadd_rn(s, ks_rl(v, u));
+            } else {
+                for (int u = 0; u < n; u++) s = __dadd_rn(s, ks_rl(v, u));
+            }
         }
-        sums[i] = s;
+        if (lane == 0) sums[i] = s;
     }
 }
 
@@ -550,10 +556,10 @@ int launch_km_sums_fx(hipStream_t s, Pts X, int d, const int32_t* rows, const in
                        carry_counts, sums, flag, stat, use_lanes ? lanes : nullptr, lane_cnt);
     if (use_lanes) {
         if (X.f64)
-            hipLaunchKernelGGL(km_chain_lanes_kernel<double>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.d(), d, rows, crow,
+            hipLaunchKernelGGL(km_chain_lanes_kernel<double>, dim3(gsz(n, 1, 8192)), dim3(64), 0, s, X.d(), d, rows, crow,
                                lanes, lane_cnt, carry, sums);
         else
-            hipLaunchKernelGGL(km_chain_lanes_kernel<float>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.f(), d, rows, crow,
+            hipLaunchKernelGGL(km_chain_lanes_kernel<float>, dim3(gsz(n, 1, 8192)), dim3(64), 0, s, X.f(), d, rows, crow,
                                lanes, lane_cnt, carry, sums);
     }
     if (seg_ws && !test_switch("LSHKM_KM_FLAGGED", "chain")) {
@@ -1169,11 +1175,11 @@ int launch_km_shard_chain(hipStream_t s, Pts X, int d, const int32_t* rows, cons
     // mask 1: the segment composition (flag bits), mask 2: one lane per chain
     if (X.f64) {
         km_seg_compose(s, X.d(), d, rows, crow, K, carry, flag, mask, w, sums);
-        hipLaunchKernelGGL(km_chain_lanes_kernel<double>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.d(), d, rows, crow,
+        hipLaunchKernelGGL(km_chain_lanes_kernel<double>, dim3(gsz(n, 1, 8192)), dim3(64), 0, s, X.d(), d, rows, crow,
                            lanes, lane_cnt, carry, sums);
     } else {
         km_seg_compose(s, X.f(), d, rows, crow, K, carry, flag, mask, w, sums);
-        hipLaunchKernelGGL(km_chain_lanes_kernel<float>, dim3(gsz(n, 256, 1024)), dim3(256), 0, s, X.f(), d, rows, crow,
+        hipLaunchKernelGGL(km_chain_lanes_kernel<float>, dim3(gsz(n, 1, 8192)), dim3(64), 0, s, X.f(), d, rows, crow,
                            lanes, lane_cnt, carry, sums);
     }
     return kstatus("update.hip (shard chain)");
