@@ -314,10 +314,13 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     if (sims && terms && soff[nq] <= cap && toff[nq] <= tcap && soff[nq] > 0) {
         LSHKM_CHECK(crows, LSHKM_ERR_ARG, "crows is NULL");
         Buf& map = ctx->ws_call[8];                  // member -> (user, row); the declined-member list + count
-        if ((rc = map.reserve(16 * (size_t)soff[nq] + 16 + 8 * (size_t)nq))) return rc;
+        // mq | mr | the declined list | its count | unorm | the blocks' private lists | their capacities and counts
+        if ((rc = map.reserve(24 * (size_t)soff[nq] + 16 + 8 * (size_t)nq + 16 * (size_t)RC_TERMS_GMAX))) return rc;
         int32_t* mq = map.as<int32_t>();
         int64_t* fl = reinterpret_cast<int64_t*>(map.as<char>() + 8 * (size_t)soff[nq]);
         double* unorm = reinterpret_cast<double*>(fl + soff[nq] + 1);     // the users' |u|^2
+        int64_t* fregion = reinterpret_cast<int64_t*>(unorm + nq);
+        int64_t* faux = fregion + soff[nq];
         // cluster-major work list: the users of each cluster (ascending) and the
         // 64-member chunks of the cluster's rows on this shard, each staged once
         // for all of them (rc_terms_cl_kernel)
@@ -345,15 +348,20 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
         pack.insert(pack.end(), gptr.begin(), gptr.end());
         pack.insert(pack.end(), byc.begin(), byc.end());
         Buf& gb = ctx->ws_call[9];
-        if ((rc = gb.reserve(4 * std::max<size_t>(pack.size(), 1)))) return rc;
+        const int64_t nitems = nG ? (int64_t)ioff.back() : 0;
+        // the item and user records after the list
+        const size_t item_off = (4 * std::max<size_t>(pack.size(), 1) + 255) / 256 * 256;
+        const size_t user_off = item_off + (RC_ITEM_BYTES * (size_t)std::max<int64_t>(nitems, 1) + 255) / 256 * 256;
+        if ((rc = gb.reserve(user_off + RC_USER_BYTES * std::max<size_t>(byc.size(), 1)))) return rc;
         int32_t* dp = gb.as<int32_t>();
         if (!pack.empty())
             LSHKM_HIP(hipMemcpyAsync(dp, pack.data(), 4 * pack.size(), hipMemcpyHostToDevice, ctx->stream));
-        const RcGroups groups{dp, (int)nG, nG ? (int64_t)ioff.back() : 0, dp + nG + 1, dp + 2 * nG + 1, dp + 3 * nG + 2};
+        const RcGroups groups{dp, (int)nG, nitems, dp + nG + 1, dp + 2 * nG + 1, dp + 3 * nG + 2, gb.as<char>() + item_off,
+                              (int64_t)byc.size(), gb.as<char>() + user_off};
         if ((rc = launch_rc_terms(ctx->stream, X, x_mean, d, crow, crows, K, U, nq, ucl, soff_dev, soff[nq], unk_ptr,
                                   unk_idx, toff_dev, sims, terms, mq, mq + soff[nq], fl,
                                   reinterpret_cast<unsigned long long*>(fl + soff[nq]),
-                                  (unsigned long long*)ctx->stats.p + STAT_REC_SOFT, unorm, &groups)))
+                                  (unsigned long long*)ctx->stats.p + STAT_REC_SOFT, unorm, &groups, fregion, faux)))
             return rc;
     }
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));

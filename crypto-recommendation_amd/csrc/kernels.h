@@ -245,12 +245,19 @@ struct RcGroups {
     const int32_t* gcl;
     const int32_t* gptr;
     const int32_t* gusr;
+    void* items;              // nitems x 32 B (16-B aligned): the per-item records (rc_item_meta_kernel)
+    int64_t nusers;           // gptr[ngroups]: the work list's users
+    void* users;              // nusers x 48 B (16-B aligned): the per-user records (rc_user_meta_kernel)
 };
+constexpr size_t RC_ITEM_BYTES = 32, RC_USER_BYTES = 48;
 int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int64_t* crow, const int32_t* crows,
                     int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
                     const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
                     int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
-                    unsigned long long* soft_count, double* unorm, const RcGroups* groups);
+                    unsigned long long* soft_count, double* unorm, const RcGroups* groups, int64_t* fix_region,
+                    int64_t* fix_aux);
+// fix_region: total entries (the terms blocks' private decline lists); fix_aux: 2 x RC_TERMS_GMAX
+constexpr int RC_TERMS_GMAX = 8192;
 // Users whose cluster holds >= RC_LONG_MIN members on this shard: their
 // prediction chains by binade segments (launch_seg_columns, all such users in
 // one set of launches) instead of one wave's sequential adds. Device

@@ -715,74 +715,213 @@ __global__ __launch_bounds__(256) void rc_member_map_kernel(int64_t nq, const in
 }
 
 // rc_terms_cl_kernel: a wave takes 64 members of one cluster, stages their
-// rows through LDS by coalesced row loads (the next item's rows in registers
-// while this one is computed) once for every user of that cluster on this
-// shard -- users sharing a cluster read its rows once, not once each (~1.6
-// users per distinct cluster at C5: 38 % fewer row bytes than one pass per
-// (user, member) pair); per user and lane: cosineSimilarity (IpAcc
+// rows through LDS by coalesced row loads once for every user of that cluster
+// on this shard -- users sharing a cluster read its rows once, not once each
+// (~1.6 users per distinct cluster at C5: 38 % fewer row bytes than one pass
+// per (user, member) pair); per user and lane: cosineSimilarity (IpAcc
 // certificate; declined ones listed for rc_terms_fix_kernel's x87 chain) and
 // the terms of get_predicted_user_sim's main sums, t = sim * (x[index] - mean)
 // (crypto_rec.hpp:296), one fp64 per (member, unknown index), at the pair
 // index soff[q] + i (i = the member's index in its cluster).
-// Item it: the 64-member chunk it - ioff[g] of group g (ioff[g] <= it <
-// ioff[g + 1], a binary search over the G + 1 offsets); group g: cluster gcl[g],
-// users gusr[gptr[g] .. gptr[g + 1]).
+// Item it: rc_item_meta_kernel's record (its group's cluster chunk and users);
+// user k of the work list: rc_user_meta_kernel's record (its pair and term
+// offsets, unknown indexes and |u|^2).
+// Rows of at most 64 units (fp32 d <= 128) run as a software pipeline over the
+// wave's items it_j = blockIdx.x + j * gridDim.x: every global load an item
+// consumes is issued while the item before it is computed -- its member rows
+// (unit `lane` of each), its mean values, its first CT_UMAX users' rows and
+// unknown-index lists and its user records -- and the rest one or two items
+// earlier (member row indexes, user records, item records). The vector memory
+// counter retires in order, so a load issued after the next item's rows and
+// consumed by this item would wait on all of them: the round-5 form issued
+// this item's user rows and means after the next item's row loads and waited
+// on those (45 % of its cycles waiting, profiles/round5_sq_c5_terms_v1.txt).
+// Users past the first CT_UMAX of a group, or with more than 64 unknown
+// indexes, take direct loads (correct, not pipelined).
+constexpr int CT_UMAX = 4;        // users per item staged ahead
+struct RcItem {
+    int64_t mem0;      // crows index of the item's first member
+    int32_t cnt;       // members in the item (1..64)
+    int32_t i0;        // index of its first member in the cluster
+    int32_t kb, ke;    // the group's users: work-list positions kb .. ke
+    int32_t pad0, pad1;
+};
+static_assert(sizeof(RcItem) == 32, "RcItem: two 16-B loads");
+struct RcUser {
+    int64_t soff, toff, o;   // pair offset, term offset, unk_idx offset
+    double unorm;            // sum_j pow(u_j, 2)
+    int32_t q, m;            // user index, unknown indexes
+    int64_t pad;
+};
+static_assert(sizeof(RcUser) == 48, "RcUser: three 16-B loads");
+
+__global__ __launch_bounds__(256) void rc_item_meta_kernel(const int32_t* __restrict__ ioff, int ngroups, int64_t nitems,
+                                                           const int32_t* __restrict__ gcl,
+                                                           const int32_t* __restrict__ gptr,
+                                                           const int64_t* __restrict__ crow, RcItem* __restrict__ items) {
+    for (int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x; it < nitems; it += (int64_t)gridDim.x * 256) {
+        int lo = 0, hi = ngroups;                    // the last g with ioff[g] <= it
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (ioff[mid] <= it) lo = mid; else hi = mid;
+        }
+        const int i0 = (int)(it - ioff[lo]) * CT_STAGE;
+        const int64_t cb = crow[gcl[lo]], n = crow[gcl[lo] + 1] - cb;
+        RcItem m;
+        m.mem0 = cb + i0;
+        m.cnt = (int32_t)(n - i0 < CT_STAGE ? n - i0 : CT_STAGE);
+        m.i0 = i0;
+        m.kb = gptr[lo];
+        m.ke = gptr[lo + 1];
+        m.pad0 = m.pad1 = 0;
+        items[it] = m;
+    }
+}
+
+__global__ __launch_bounds__(256) void rc_user_meta_kernel(const int32_t* __restrict__ gusr, int64_t nusers,
+                                                           const int64_t* __restrict__ soff,
+                                                           const int64_t* __restrict__ toff,
+                                                           const int64_t* __restrict__ unk_ptr,
+                                                           const double* __restrict__ unorm, RcUser* __restrict__ users) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nusers; k += (int64_t)gridDim.x * 256) {
+        const int q = gusr[k];
+        RcUser u;
+        u.soff = soff[q];
+        u.toff = toff[q];
+        u.o = unk_ptr[q];
+        u.m = (int32_t)(unk_ptr[q + 1] - u.o);
+        u.unorm = unorm[q];
+        u.q = q;
+        u.pad = 0;
+        users[k] = u;
+    }
+}
+
+// ct_sim with the row reads one 4-unit block ahead of the arithmetic (the
+// round-5 loop waited on each block's LDS reads), and the member's |x|^2 taken
+// from the item's first user (XA) instead of recomputed per user.
+template <typename T, bool XA>
+__device__ inline double ct_sim_pl(const uint64_t* myrow8, const uint64_t* u8, int nunit, double ub, double& xa,
+                                   bool& ok) {
+    constexpr int PER = 8 / (int)sizeof(T);
+    double xs = 0.0;
+    IpAcc ip;
+    auto step = [&](uint64_t xw, uint64_t uw) {
+        T xv[PER], uv[PER];
+        memcpy(xv, &xw, 8);
+        memcpy(uv, &uw, 8);
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const double xj = (double)xv[k], uj = (double)uv[k];
+            ip.add(__dmul_rn(xj, uj));
+            if (XA) xs = __dadd_rn(xs, sq_of<T>(xj));
+        }
+    };
+    int w = 0;
+    if (nunit >= 4) {
+        uint64_t xc[4], uc[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { xc[k] = myrow8[k]; uc[k] = u8[k]; }
+        for (; w + 8 <= nunit; w += 4) {
+            uint64_t xn[4], un[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) { xn[k] = myrow8[w + 4 + k]; un[k] = u8[w + 4 + k]; }
+#pragma unroll
+            for (int k = 0; k < 4; k++) step(xc[k], uc[k]);
+#pragma unroll
+            for (int k = 0; k < 4; k++) { xc[k] = xn[k]; uc[k] = un[k]; }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) step(xc[k], uc[k]);
+        w += 4;
+    }
+    for (; w < nunit; w++) step(myrow8[w], u8[w]);
+    if (XA) xa = xs;
+    const double denom = __dmul_rn(sqrt(xa), sqrt(ub));
+    double sv, qr;
+    ok = ip.quot_status(denom, sv, qr) == 0;        // declined: rc_terms_fix_kernel decides
+    return sv;
+}
+
+__device__ inline int64_t rl64(int64_t v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, l);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ inline double rld(double v, int l) { return __longlong_as_double(rl64(__double_as_longlong(v), l)); }
+
 template <typename T>
 __global__ __launch_bounds__(64) void rc_terms_cl_kernel(
     const T* __restrict__ X, const double* __restrict__ x_mean, int d, const T* __restrict__ U,
-    const int32_t* __restrict__ ioff, int ngroups, int64_t nitems, const int32_t* __restrict__ gcl, const int32_t* __restrict__ gptr,
-    const int32_t* __restrict__ gusr, const int64_t* __restrict__ crow, const int32_t* __restrict__ crows,
-    const int64_t* __restrict__ soff, const int64_t* __restrict__ unk_ptr, const int32_t* __restrict__ unk_idx,
-    const int64_t* __restrict__ toff, double* __restrict__ sims, double* __restrict__ terms, int stride8,
-    int64_t* __restrict__ fix_list, unsigned long long* __restrict__ fix_count, const double* __restrict__ unorm) {
+    const RcItem* __restrict__ items, int64_t nitems, const RcUser* __restrict__ users,
+    const int32_t* __restrict__ crows, const int32_t* __restrict__ unk_idx, double* __restrict__ sims,
+    double* __restrict__ terms, int stride8, int64_t* __restrict__ fix_region, const int64_t* __restrict__ fix_cap,
+    int64_t* __restrict__ fix_cnt) {
     constexpr int SB = 16;                          // rows per staging batch (loads in flight)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x;
     const int nunit = (int)((int64_t)d * (int64_t)sizeof(T) / 8);
     uint64_t* stage = reinterpret_cast<uint64_t*>(smem);
-    uint64_t* ustage = stage + (size_t)CT_STAGE * stride8;
+    uint64_t* ustage = stage + (size_t)CT_STAGE * stride8;      // CT_UMAX + 1 user rows
     const uint64_t* myrow8 = stage + (size_t)lane * stride8;
-    // item it's group, first member, cluster size and this lane's member row
-    auto item_at = [&](int64_t it_, int& grp_, int& i0_, int64_t& n_, int32_t& r_) {
-        int lo = 0, hi = ngroups;                    // the last g with ioff[g] <= it_
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (ioff[mid] <= it_) lo = mid; else hi = mid;
-        }
-        grp_ = lo;
-        i0_ = (int)(it_ - ioff[lo]) * CT_STAGE;
-        const int64_t cb_ = crow[gcl[grp_]];
-        n_ = crow[gcl[grp_] + 1] - cb_;
-        r_ = crows[cb_ + (i0_ + lane < n_ ? i0_ + lane : n_ - 1)];
-    };
-    // rows of at most 64 units (fp32 d <= 128): the next item's rows in
-    // registers (unit `lane` of each) while this item's users are computed
+    const int64_t G = gridDim.x;
     const bool pfok = nunit <= 64;
+    const int ul = lane < nunit ? lane : nunit - 1;              // this lane's unit (clamped: no branch per load)
+    auto meta = [&](int64_t it_) { return items[it_ < nitems ? it_ : nitems - 1]; };
+    auto member_row = [&](const RcItem& m) { return crows[m.mem0 + (lane < m.cnt ? lane : m.cnt - 1)]; };
+    // lane u: the record of the item's user u (clamped to its last)
+    auto user_rec = [&](const RcItem& m) { return users[m.kb + (lane < m.ke - m.kb ? lane : m.ke - m.kb - 1)]; };
     uint64_t pf[CT_STAGE];
     auto issue_pf = [&](int32_t rr) {
 #pragma unroll
         for (int t = 0; t < CT_STAGE; t++) {
             const int rt = __builtin_amdgcn_readlane(rr, t);
-            pf[t] = lane < nunit ? reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d)[lane] : 0ull;
+            pf[t] = reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d)[ul];
         }
     };
-    int gN = 0, iN = 0;
-    int64_t nN = 0;
-    int32_t rN = 0;
-    if (blockIdx.x < nitems) {
-        item_at(blockIdx.x, gN, iN, nN, rN);
-        if (pfok) issue_pf(rN);
-    }
-    for (int64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const int grp = gN, i0 = iN;
-        const int64_t n = nN;
-        const int32_t r = rN;
-        const bool on = i0 + lane < n;
+    // the first CT_UMAX users' rows (unit `lane`) and unknown-index lists (lane e: index e)
+    uint64_t up0[CT_UMAX], up1[CT_UMAX];
+    int32_t ux0[CT_UMAX], ux1[CT_UMAX];
+    auto issue_users = [&](const RcItem& m, const RcUser& ur, uint64_t (&up)[CT_UMAX], int32_t (&ux)[CT_UMAX]) {
+#pragma unroll
+        for (int u = 0; u < CT_UMAX; u++) {
+            const int uu = u < m.ke - m.kb ? u : 0;
+            const int q = __builtin_amdgcn_readlane(ur.q, uu);
+            const int mm = __builtin_amdgcn_readlane(ur.m, uu);
+            const int64_t o = rl64(ur.o, uu);
+            if (pfok) up[u] = reinterpret_cast<const uint64_t*>(U + (int64_t)q * d)[ul];
+            ux[u] = terms && mm > 0 ? unk_idx[o + (lane < mm ? lane : mm - 1)] : 0;
+        }
+    };
+    const int64_t it0 = blockIdx.x;
+    if (it0 >= nitems) return;
+    // this block's private decline list: fix_region[rbase ..), its capacity the
+    // pairs of its items (rc_block_cap_kernel) -- no shared counter: one atomic
+    // per (item, user) pass on a single word serialised at ~12 ns each, ~1.9 ms
+    // over the ~160K passes of a C5 call, was the round-5 kernel's floor
+    int64_t rbase = 0;
+    for (int b = lane; b < (int)blockIdx.x; b += 64) rbase += fix_cap[b];
+    for (int off = 32; off >= 1; off >>= 1) rbase += __shfl_xor(rbase, off);
+    int64_t nloc = 0;
+    // pipeline fill: item 0's loads, then item 1's that the loop expects in flight
+    RcItem m0 = meta(it0), m1 = meta(it0 + G), m2 = meta(it0 + 2 * G);
+    int32_t r0 = member_row(m0), r1 = member_row(m1);
+    RcUser ub0 = user_rec(m0), ub1 = user_rec(m1);
+    if (pfok) issue_pf(r0);
+    issue_users(m0, ub0, up0, ux0);
+    double mean0 = x_mean[r0];
+    for (int64_t it = it0; it < nitems; it += G) {
+        const bool on = lane < m0.cnt;
+        const bool more = it + G < nitems;
+        const int nu = m0.ke - m0.kb;
         __syncthreads();                            // the previous item's reads of the stage are done
         if (pfok) {
 #pragma unroll
             for (int t = 0; t < CT_STAGE; t++)
                 if (lane < nunit) stage[(size_t)t * stride8 + lane] = pf[t];
+#pragma unroll
+            for (int u = 0; u < CT_UMAX; u++)
+                if (u < nu && lane < nunit) ustage[(size_t)u * stride8 + lane] = up0[u];
         } else {
             for (int t0 = 0; t0 < CT_STAGE; t0 += SB) {
                 for (int u0 = 0; u0 < nunit; u0 += 64) {
@@ -790,7 +929,7 @@ __global__ __launch_bounds__(64) void rc_terms_cl_kernel(
                     uint64_t v[SB];
 #pragma unroll
                     for (int k = 0; k < SB; k++) {
-                        const int rt = __builtin_amdgcn_readlane(r, t0 + k);
+                        const int rt = __builtin_amdgcn_readlane(r0, t0 + k);
                         v[k] = uon ? reinterpret_cast<const uint64_t*>(X + (int64_t)rt * d)[u0 + lane] : 0ull;
                     }
 #pragma unroll
@@ -799,40 +938,113 @@ __global__ __launch_bounds__(64) void rc_terms_cl_kernel(
                 }
             }
         }
-        if (it + gridDim.x < nitems) {
-            item_at(it + gridDim.x, gN, iN, nN, rN);
-            if (pfok) issue_pf(rN);
-        }
-        const double mean = x_mean[r];
+        // loads for the items ahead (consumed an item or more later; see above)
+        if (pfok && more) issue_pf(r1);
+        if (more) issue_users(m1, ub1, up1, ux1);
+        const double mean1 = x_mean[r1];
+        const int32_t r2 = member_row(m2);
+        const RcUser ub2 = user_rec(m2);
+        const RcItem m3 = meta(it + 3 * G);
         const T* xr = reinterpret_cast<const T*>(myrow8);
-        for (int k = gptr[grp]; k < gptr[grp + 1]; k++) {
-            const int q = gusr[k];
-            __syncthreads();                        // the stage landed / the previous user's row is read
-            for (int u0 = lane; u0 < nunit; u0 += 64)
-                ustage[u0] = reinterpret_cast<const uint64_t*>(U + (int64_t)q * d)[u0];
+        double xa = 0.0;
+        for (int u = 0; u < nu; u++) {
+            const int q = __builtin_amdgcn_readlane(ub0.q, u < 64 ? u : 0);
+            const uint64_t* urow = ustage + (size_t)(pfok && u < CT_UMAX ? u : CT_UMAX) * stride8;
+            int64_t soffq, toffq, o;
+            double unq;
+            int m;
+            if (u < 64) {
+                soffq = rl64(ub0.soff, u); toffq = rl64(ub0.toff, u); o = rl64(ub0.o, u);
+                unq = rld(ub0.unorm, u); m = __builtin_amdgcn_readlane(ub0.m, u);
+            } else {
+                const RcUser r = users[m0.kb + u];
+                soffq = r.soff; toffq = r.toff; o = r.o; unq = r.unorm; m = r.m;
+            }
+            const int qq = u < 64 ? q : users[m0.kb + u].q;
+            if (u >= CT_UMAX || !pfok) {            // direct: the row into the spare slot
+                __syncthreads();
+                for (int u0 = lane; u0 < nunit; u0 += 64)
+                    ustage[(size_t)CT_UMAX * stride8 + u0] = reinterpret_cast<const uint64_t*>(U + (int64_t)qq * d)[u0];
+            }
             __syncthreads();
             bool ok;
-            const double sv = ct_sim<T>(myrow8, ustage, nunit, unorm[q], ok);
-            const int64_t i = i0 + lane;
-            const int64_t g = soff[q] + i;
+            const double sv = u == 0 ? ct_sim_pl<T, true>(myrow8, urow, nunit, unq, xa, ok)
+                                     : ct_sim_pl<T, false>(myrow8, urow, nunit, unq, xa, ok);
+            const int64_t i = m0.i0 + lane;
+            const int64_t g = soffq + i;
             const unsigned long long dm = __ballot(on && !ok);
-            if (dm) {
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(fix_count, (unsigned long long)__popcll(dm));
-                base = __shfl(base, 0);
-                if (on && !ok) fix_list[base + __popcll(dm & ((1ull << lane) - 1ull))] = g;
-            }
-            if (on && ok) {
-                sims[g] = sv;
-                if (terms) {
-                    const int64_t o = unk_ptr[q];
-                    const int m = (int)(unk_ptr[q + 1] - o);
-                    double* tq = terms + toff[q] + i * m;       // member-major: the pair's m terms together
-                    for (int e = 0; e < m; e++) tq[e] = __dmul_rn(sv, __dsub_rn((double)xr[unk_idx[o + e]], mean));
+            if (on && !ok) fix_region[rbase + nloc + __popcll(dm & ((1ull << lane) - 1ull))] = g;
+            nloc += __popcll(dm);
+            const bool wr = on && ok;
+            if (wr) sims[g] = sv;
+            if (terms) {
+                // the index list is read across lanes (readlane ignores EXEC, so
+                // every lane's copy is selected and read in uniform control flow;
+                // only the stores are predicated)
+                double* tq = terms + toffq + i * m;             // member-major: the pair's m terms together
+                int32_t uxv = ux0[0];
+#pragma unroll
+                for (int uu = 1; uu < CT_UMAX; uu++)
+                    if (uu == u) uxv = ux0[uu];
+                if (u < CT_UMAX && m <= 64) {
+                    for (int e = 0; e < m; e++) {
+                        const double t = __dmul_rn(sv, __dsub_rn((double)xr[__builtin_amdgcn_readlane(uxv, e)], mean0));
+                        if (wr) tq[e] = t;
+                    }
+                } else {
+                    for (int e = 0; e < m; e++) {
+                        const double t = __dmul_rn(sv, __dsub_rn((double)xr[unk_idx[o + e]], mean0));
+                        if (wr) tq[e] = t;
+                    }
                 }
             }
         }
+        m0 = m1; m1 = m2; m2 = m3;
+        r0 = r1; r1 = r2;
+        ub0 = ub1; ub1 = ub2;
+        mean0 = mean1;
+#pragma unroll
+        for (int u = 0; u < CT_UMAX; u++) { up0[u] = up1[u]; ux0[u] = ux1[u]; }
     }
+    if (lane == 0) fix_cnt[blockIdx.x] = nloc;
+}
+
+// Block b of the terms grid (G blocks): the pairs of its items it = b, b + G, ...
+// -- the capacity of its private decline list.
+__global__ __launch_bounds__(256) void rc_block_cap_kernel(const RcItem* __restrict__ items, int64_t nitems, int G,
+                                                           int64_t* __restrict__ cap) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= G) return;
+    int64_t c = 0;
+    for (int64_t it = b; it < nitems; it += G) {
+        const RcItem m = items[it];
+        c += (int64_t)m.cnt * (m.ke - m.kb);
+    }
+    cap[b] = c;
+}
+
+// The blocks' private lists into one dense list in block order (fix_list,
+// *fix_count), for rc_terms_fix_kernel: block b (one wave) copies its count.
+__global__ __launch_bounds__(64) void rc_fix_gather_kernel(const int64_t* __restrict__ cap,
+                                                           const int64_t* __restrict__ cnt, int G,
+                                                           const int64_t* __restrict__ region,
+                                                           int64_t* __restrict__ fix_list,
+                                                           unsigned long long* __restrict__ fix_count) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    int64_t rs = 0, ds = 0, tot = 0;
+    for (int k = lane; k < G; k += 64) {
+        const int64_t c = cnt[k];
+        if (k < b) { rs += cap[k]; ds += c; }
+        tot += c;
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        rs += __shfl_xor(rs, off);
+        ds += __shfl_xor(ds, off);
+        tot += __shfl_xor(tot, off);
+    }
+    if (b == 0 && lane == 0) *fix_count = (unsigned long long)tot;
+    const int64_t n = cnt[b];
+    for (int64_t i = lane; i < n; i += 64) fix_list[ds + i] = region[rs + i];
 }
 
 // The listed members: cosineSimilarity by the x87 chain (softx87.h X87acc),
@@ -1076,18 +1288,21 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
                     int K, Pts U, int64_t nq, const int32_t* ucl, const int64_t* soff, int64_t total,
                     const int64_t* unk_ptr, const int32_t* unk_idx, const int64_t* toff, double* sims, double* terms,
                     int32_t* mem_q, int32_t* mem_r, int64_t* fix_list, unsigned long long* fix_count,
-                    unsigned long long* soft_count, double* unorm, const RcGroups* groups) {
+                    unsigned long long* soft_count, double* unorm, const RcGroups* groups, int64_t* fix_region,
+                    int64_t* fix_aux) {
     if (nq <= 0 || total <= 0) return 0;
     const int elem = X.f64 ? 8 : 4;
     const int stride8 = rc_terms_stride8(d, elem);
     const size_t lds = (size_t)(CT_STAGE + 1) * stride8 * 8;
+    const size_t lds_cl = (size_t)(CT_STAGE + CT_UMAX + 1) * stride8 * 8;   // rows | the users' rows | a spare
     // every check before the first launch: a refused call enqueues nothing
-    if (((int64_t)d * elem) % 8 != 0 || 2 * lds > 160 * 1024) {
+    if (((int64_t)d * elem) % 8 != 0 || 2 * lds > 160 * 1024 || lds_cl > 160 * 1024) {
         set_error("launch_rc_terms: rows must be a multiple of 8 B and stage in LDS");
         return LSHKM_ERR_ARG;
     }
-    if (!groups || groups->nitems <= 0) {
-        set_error("launch_rc_terms: empty cluster-major work list for a nonzero member total");
+    if (!groups || groups->nitems <= 0 || groups->nusers <= 0 || !groups->items || !groups->users ||
+        ((uintptr_t)groups->items & 15) != 0 || ((uintptr_t)groups->users & 15) != 0 || !fix_region || !fix_aux) {
+        set_error("launch_rc_terms: empty cluster-major work list (or no 16-B aligned item records) for a nonzero member total");
         return LSHKM_ERR_ARG;
     }
     hipLaunchKernelGGL(rc_member_map_kernel, dim3((unsigned)std::min<int64_t>(nq, 4096)), dim3(256), 0, s, nq, soff, ucl,
@@ -1096,16 +1311,38 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
         hipLaunchKernelGGL(rc_user_norm_kernel<double>, dim3(gsz(nq, 256, 1024)), dim3(256), 0, s, U.d(), nq, d, unorm);
     else
         hipLaunchKernelGGL(rc_user_norm_kernel<float>, dim3(gsz(nq, 256, 1024)), dim3(256), 0, s, U.f(), nq, d, unorm);
-    if (hipMemsetAsync(fix_count, 0, 8, s) != hipSuccess) return kstatus("rc_terms (memset)");
-    const dim3 cgrid((unsigned)std::min<int64_t>(groups->nitems, 65536));
+    // persistent: the resident waves (LDS-limited) times 2, each walking its
+    // items as a pipeline (a grid of 65,536 one-item blocks would pay the
+    // pipeline's fill per block)
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kstatus("launch_rc_terms (device)");
+    if (dev < 64 && !cus[dev] &&
+        hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return kstatus("launch_rc_terms (CU count)");
+    const int64_t per_cu = std::max<int64_t>(1, (int64_t)(160 * 1024) / (int64_t)lds_cl);
+    const int64_t resident = (dev < 64 && cus[dev] > 0 ? cus[dev] : 256) * per_cu;
+    const dim3 cgrid((unsigned)std::min<int64_t>(
+        {groups->nitems, (int64_t)RC_TERMS_GMAX, test_switch("LSHKM_TERMS_GRID", "r4") ? 4 * resident : 2 * resident}));
+    RcItem* items = reinterpret_cast<RcItem*>(groups->items);
+    RcUser* users = reinterpret_cast<RcUser*>(groups->users);
+    hipLaunchKernelGGL(rc_item_meta_kernel, dim3(gsz(groups->nitems, 256, 4096)), dim3(256), 0, s, groups->ioff,
+                       groups->ngroups, groups->nitems, groups->gcl, groups->gptr, crow, items);
+    hipLaunchKernelGGL(rc_user_meta_kernel, dim3(gsz(groups->nusers, 256, 1024)), dim3(256), 0, s, groups->gusr,
+                       groups->nusers, soff, toff, unk_ptr, unorm, users);
+    const int G = (int)cgrid.x;
+    int64_t* fcap = fix_aux;
+    int64_t* fcnt = fix_aux + RC_TERMS_GMAX;
+    hipLaunchKernelGGL(rc_block_cap_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, s, items, groups->nitems, G,
+                       fcap);
     if (X.f64)
-        hipLaunchKernelGGL(rc_terms_cl_kernel<double>, cgrid, dim3(64), lds, s, X.d(), x_mean, d, U.d(), groups->ioff,
-                           groups->ngroups, groups->nitems, groups->gcl, groups->gptr, groups->gusr, crow, crows, soff,
-                           unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
+        hipLaunchKernelGGL(rc_terms_cl_kernel<double>, cgrid, dim3(64), lds_cl, s, X.d(), x_mean, d, U.d(), items,
+                           groups->nitems, users, crows, unk_idx, sims, terms, stride8, fix_region, fcap, fcnt);
     else
-        hipLaunchKernelGGL(rc_terms_cl_kernel<float>, cgrid, dim3(64), lds, s, X.f(), x_mean, d, U.f(), groups->ioff,
-                           groups->ngroups, groups->nitems, groups->gcl, groups->gptr, groups->gusr, crow, crows, soff,
-                           unk_ptr, unk_idx, toff, sims, terms, stride8, fix_list, fix_count, unorm);
+        hipLaunchKernelGGL(rc_terms_cl_kernel<float>, cgrid, dim3(64), lds_cl, s, X.f(), x_mean, d, U.f(), items,
+                           groups->nitems, users, crows, unk_idx, sims, terms, stride8, fix_region, fcap, fcnt);
+    hipLaunchKernelGGL(rc_fix_gather_kernel, dim3((unsigned)G), dim3(64), 0, s, fcap, fcnt, G, fix_region, fix_list,
+                       fix_count);
     // the list length is on the device: a grid for up to ~1/4 of the pairs, looping beyond
     const dim3 fgrid(gsz(total / 4 + 1, CT_STAGE, 2048));
     const size_t flds = 2 * lds;
