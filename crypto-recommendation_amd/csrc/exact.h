@@ -291,7 +291,9 @@ struct IpAcc {
     // double(ip87 / (long double)denom): 0 = certified (q exact), 1 = not
     // certified but |q - double(ip87 / denom)| <= qrad, 2 = declined (a quantity
     // outside the ranges the bound assumes; q meaningless)
-    __device__ inline int quot_status(double denom, double& q, double& qrad) const {
+    // exact: the caller certified that the x87 chain never rounded (ip_never_rounds):
+    // then ip87 == sh + sl exactly and only the quotient's own roundings remain in R
+    __device__ inline int quot_status(double denom, double& q, double& qrad, bool exact = false) const {
         if (!(denom >= 0x1p-800 && denom < 0x1p800 && mx >= 0x1p-800 && mx < 0x1p800 && ts < 0x1p800)) return 2;
         const double yh0 = sh / denom;
         const double r = fma(-yh0, denom, sh);             // exact remainder
@@ -304,8 +306,8 @@ struct IpAcc {
         const double yl = __dsub_rn(yl0, __dsub_rn(yh, yh0));
         const double ay = fabs(yh);
         if (!(ay >= 0x1p-800 && ay < 0x1p800)) return 2;
-        const double R = (__dadd_rn(ts * (0x1p-64 * (1.0 + 0x1p-30)), mx * 0x1p-88) / denom + fabs(yl0) * 0x1p-51 +
-                          ay * 0x1p-63) * (1.0 + 0x1p-20);
+        const double R = ((exact ? 0.0 : __dadd_rn(ts * (0x1p-64 * (1.0 + 0x1p-30)), mx * 0x1p-88) / denom) +
+                          fabs(yl0) * 0x1p-51 + ay * 0x1p-63) * (1.0 + 0x1p-20);
         const long long bits = __double_as_longlong(ay);
         const double up = __dsub_rn(__longlong_as_double(bits + 1), ay);   // ulp above |yh|
         const double dn = __dsub_rn(ay, __longlong_as_double(bits - 1));   // ulp below (half at a power of 2)
@@ -323,6 +325,37 @@ struct IpAcc {
         return quot_status(denom, q, qr) == 0;
     }
 };
+
+// Exponent of the lowest set bit of a nonzero value (LOWBIT_NONE for zero); for
+// subnormals one below (the implicit bit counted): a lower bound, which is all
+// ip_never_rounds needs.
+constexpr int LOWBIT_NONE = 1 << 20;
+__device__ inline int lowbit_exp(float x) {
+    const uint32_t b = __float_as_uint(x);
+    const int e = (int)((b >> 23) & 0xffu);
+    return (b & 0x7fffffffu) == 0u ? LOWBIT_NONE : e - 150 + (int)__builtin_ctz(b | 0x800000u);
+}
+__device__ inline int lowbit_exp(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const int e = (int)((b >> 52) & 0x7ffu);
+    return (b << 1) == 0ull ? LOWBIT_NONE : e - 1075 + (int)__builtin_ctzll(b | (1ull << 52));
+}
+// The x87 chain of IpAcc's products never rounded: every product p_j is a
+// multiple of 2^qlow (qlow = lowbit(x) + lowbit(u) bounds lowbit(RN(x_j u_j))
+// from below: a product rounds onto a grid no finer than its factors' joint
+// one), and every exact partial sum S_k lies below 2^T (|S_k| <= mx (1 +
+// 2^-40): mx is the largest double partial sum, off the exact one by the
+// double-double rest) -- so each S_k has at most T - qlow <= 64 significant
+// bits and every FADD of the chain is exact. The double-double then carries
+// the same exact sums: the TwoSum rests are multiples of 2^qlow below
+// 2^(T - 53), and their running sum needs at most T - 46 - qlow <= 18 bits.
+__device__ inline bool ip_never_rounds(double mx, int qlow) {
+    if (qlow >= LOWBIT_NONE) return true;                 // an all-zero row: every product 0
+    if (!(mx > 0.0)) return mx == 0.0;
+    if (!(mx < 0x1p1000)) return false;
+    const int T = ilogb(mx * (1.0 + 0x1p-40)) + 1;
+    return T - qlow <= 64;
+}
 
 // Cosine distance with its certificate status (IpAcc::quot_status): 0 = v is
 // the reference's value, 1 = the reference's value lies within v +- rad,

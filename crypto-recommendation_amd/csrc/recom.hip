@@ -751,7 +751,7 @@ struct RcUser {
     int64_t soff, toff, o;   // pair offset, term offset, unk_idx offset
     double unorm;            // sum_j pow(u_j, 2)
     int32_t q, m;            // user index, unknown indexes
-    int64_t pad;
+    int32_t qlow, pad;       // min_j lowbit_exp(u_j) (exact.h; LOWBIT_NONE: an all-zero row)
 };
 static_assert(sizeof(RcUser) == 48, "RcUser: three 16-B loads");
 
@@ -778,7 +778,9 @@ __global__ __launch_bounds__(256) void rc_item_meta_kernel(const int32_t* __rest
     }
 }
 
-__global__ __launch_bounds__(256) void rc_user_meta_kernel(const int32_t* __restrict__ gusr, int64_t nusers,
+template <typename T>
+__global__ __launch_bounds__(256) void rc_user_meta_kernel(const T* __restrict__ U, int d,
+                                                           const int32_t* __restrict__ gusr, int64_t nusers,
                                                            const int64_t* __restrict__ soff,
                                                            const int64_t* __restrict__ toff,
                                                            const int64_t* __restrict__ unk_ptr,
@@ -792,6 +794,9 @@ __global__ __launch_bounds__(256) void rc_user_meta_kernel(const int32_t* __rest
         u.m = (int32_t)(unk_ptr[q + 1] - u.o);
         u.unorm = unorm[q];
         u.q = q;
+        int ql = LOWBIT_NONE;
+        for (int j = 0; j < d; j++) ql = min(ql, lowbit_exp(U[(int64_t)q * d + j]));
+        u.qlow = ql;
         u.pad = 0;
         users[k] = u;
     }
@@ -800,11 +805,16 @@ __global__ __launch_bounds__(256) void rc_user_meta_kernel(const int32_t* __rest
 // ct_sim with the row reads one 4-unit block ahead of the arithmetic (the
 // round-5 loop waited on each block's LDS reads), and the member's |x|^2 taken
 // from the item's first user (XA) instead of recomputed per user.
+// The member's lowest-bit bound qx (XA pass, with |x|^2) and the user's qu
+// certify a never-rounding x87 chain (exact.h ip_never_rounds): then the
+// quotient's status drops the chain's rounding bound, which alone declined
+// ~6-12 % of pairs (a 2^-58 relative R against a 2^-53 half ulp).
 template <typename T, bool XA>
 __device__ inline double ct_sim_pl(const uint64_t* myrow8, const uint64_t* u8, int nunit, double ub, double& xa,
-                                   bool& ok) {
+                                   int& qx, int qu, bool& ok) {
     constexpr int PER = 8 / (int)sizeof(T);
     double xs = 0.0;
+    int ql = LOWBIT_NONE;
     IpAcc ip;
     auto step = [&](uint64_t xw, uint64_t uw) {
         T xv[PER], uv[PER];
@@ -814,7 +824,10 @@ __device__ inline double ct_sim_pl(const uint64_t* myrow8, const uint64_t* u8, i
         for (int k = 0; k < PER; k++) {
             const double xj = (double)xv[k], uj = (double)uv[k];
             ip.add(__dmul_rn(xj, uj));
-            if (XA) xs = __dadd_rn(xs, sq_of<T>(xj));
+            if (XA) {
+                xs = __dadd_rn(xs, sq_of<T>(xj));
+                ql = min(ql, lowbit_exp(xv[k]));
+            }
         }
     };
     int w = 0;
@@ -836,10 +849,14 @@ __device__ inline double ct_sim_pl(const uint64_t* myrow8, const uint64_t* u8, i
         w += 4;
     }
     for (; w < nunit; w++) step(myrow8[w], u8[w]);
-    if (XA) xa = xs;
+    if (XA) {
+        xa = xs;
+        qx = ql;
+    }
     const double denom = __dmul_rn(sqrt(xa), sqrt(ub));
     double sv, qr;
-    ok = ip.quot_status(denom, sv, qr) == 0;        // declined: rc_terms_fix_kernel decides
+    const bool exact = ip_never_rounds(ip.mx, min(qx, LOWBIT_NONE) + min(qu, LOWBIT_NONE));
+    ok = ip.quot_status(denom, sv, qr, exact) == 0;     // declined: rc_terms_fix_kernel decides
     return sv;
 }
 
@@ -947,18 +964,20 @@ __global__ __launch_bounds__(64) void rc_terms_cl_kernel(
         const RcItem m3 = meta(it + 3 * G);
         const T* xr = reinterpret_cast<const T*>(myrow8);
         double xa = 0.0;
+        int qx = LOWBIT_NONE;
         for (int u = 0; u < nu; u++) {
             const int q = __builtin_amdgcn_readlane(ub0.q, u < 64 ? u : 0);
             const uint64_t* urow = ustage + (size_t)(pfok && u < CT_UMAX ? u : CT_UMAX) * stride8;
             int64_t soffq, toffq, o;
             double unq;
-            int m;
+            int m, qu;
             if (u < 64) {
                 soffq = rl64(ub0.soff, u); toffq = rl64(ub0.toff, u); o = rl64(ub0.o, u);
                 unq = rld(ub0.unorm, u); m = __builtin_amdgcn_readlane(ub0.m, u);
+                qu = __builtin_amdgcn_readlane(ub0.qlow, u);
             } else {
                 const RcUser r = users[m0.kb + u];
-                soffq = r.soff; toffq = r.toff; o = r.o; unq = r.unorm; m = r.m;
+                soffq = r.soff; toffq = r.toff; o = r.o; unq = r.unorm; m = r.m; qu = r.qlow;
             }
             const int qq = u < 64 ? q : users[m0.kb + u].q;
             if (u >= CT_UMAX || !pfok) {            // direct: the row into the spare slot
@@ -968,8 +987,8 @@ __global__ __launch_bounds__(64) void rc_terms_cl_kernel(
             }
             __syncthreads();
             bool ok;
-            const double sv = u == 0 ? ct_sim_pl<T, true>(myrow8, urow, nunit, unq, xa, ok)
-                                     : ct_sim_pl<T, false>(myrow8, urow, nunit, unq, xa, ok);
+            const double sv = u == 0 ? ct_sim_pl<T, true>(myrow8, urow, nunit, unq, xa, qx, qu, ok)
+                                     : ct_sim_pl<T, false>(myrow8, urow, nunit, unq, xa, qx, qu, ok);
             const int64_t i = m0.i0 + lane;
             const int64_t g = soffq + i;
             const unsigned long long dm = __ballot(on && !ok);
@@ -1328,8 +1347,12 @@ int launch_rc_terms(hipStream_t s, Pts X, const double* x_mean, int d, const int
     RcUser* users = reinterpret_cast<RcUser*>(groups->users);
     hipLaunchKernelGGL(rc_item_meta_kernel, dim3(gsz(groups->nitems, 256, 4096)), dim3(256), 0, s, groups->ioff,
                        groups->ngroups, groups->nitems, groups->gcl, groups->gptr, crow, items);
-    hipLaunchKernelGGL(rc_user_meta_kernel, dim3(gsz(groups->nusers, 256, 1024)), dim3(256), 0, s, groups->gusr,
-                       groups->nusers, soff, toff, unk_ptr, unorm, users);
+    if (X.f64)
+        hipLaunchKernelGGL(rc_user_meta_kernel<double>, dim3(gsz(groups->nusers, 256, 1024)), dim3(256), 0, s, U.d(), d,
+                           groups->gusr, groups->nusers, soff, toff, unk_ptr, unorm, users);
+    else
+        hipLaunchKernelGGL(rc_user_meta_kernel<float>, dim3(gsz(groups->nusers, 256, 1024)), dim3(256), 0, s, U.f(), d,
+                           groups->gusr, groups->nusers, soff, toff, unk_ptr, unorm, users);
     const int G = (int)cgrid.x;
     int64_t* fcap = fix_aux;
     int64_t* fcnt = fix_aux + RC_TERMS_GMAX;

@@ -388,3 +388,61 @@ def test_cluster_ids_outside_k_are_refused(ctx, bad_cl):
     got = lshkm.cluster_top_n(ctx, Xd, xm, *args, dev(ctx, X[users]), dev(ctx, np.zeros(nq)), dev(ctx, ucl),
                               dev(ctx, up), dev(ctx, ui), 5).cpu().numpy()
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("kind", ["grid", "normal", "wide", "zeros"])
+def test_terms_never_rounding_chain_certificate(ctx, kind):
+    # lshkm_cluster_terms certifies a similarity without the x87 chain's rounding
+    # bound when the chain provably never rounds (csrc/exact.h ip_never_rounds:
+    # every partial sum of the products fits 64 bits); lshkm_cluster_sims keeps
+    # the bounded form. Both must give the reference's x87 similarity bit for bit
+    # (cust_vector.hpp:139-155) -- checked against each other on every pair and
+    # against the oracle's x87 (get_P_closest's sims, crypto_rec.hpp:213-231) on
+    # a sample of users. grid / normal rows certify; wide-range rows (values
+    # 1e-8 .. 1e5 in one row) do not and keep the bounded form; zero entries
+    # carry no low bit.
+    N, d, K, nq = 20_000, 128, 8, 24
+    rng = np.random.default_rng(11)
+    if kind in ("grid", "normal"):
+        X = ctx.synth(0x5EED, N, d, kind=kind).cpu().numpy()
+    elif kind == "wide":
+        X = (rng.standard_normal((N, d)) * 10.0 ** rng.uniform(-8, 5, size=(N, d))).astype(np.float32)
+    else:
+        X = rng.standard_normal((N, d)).astype(np.float32)
+        X[rng.random((N, d)) < 0.3] = 0.0
+    assign = rng.integers(0, K, size=N).astype(np.int32)
+    crow, crows = oracle.clusters_csr(assign, K)
+    users = rng.choice(N, nq, replace=False)
+    U = X[users].copy()
+    ucl = assign[users].copy()
+    up, ui = unknown_sets(rng, nq, d)
+    xm = np.zeros(N, np.float64)
+    Xd, Ud = dev(ctx, X), dev(ctx, U)
+    args = (dev(ctx, crow), dev(ctx, crows))
+    ctx.reset_stats()
+    soff_s, sims_s = lshkm.cluster_sims(ctx, Xd, *args, Ud, dev(ctx, ucl), dev(ctx, up))
+    soft_sims = ctx.stat(lshkm.STAT_REC_SOFT)
+    ctx.reset_stats()
+    soff_t, toff, sims_t, terms = lshkm.cluster_terms(ctx, Xd, dev(ctx, xm), *args, Ud, dev(ctx, ucl), dev(ctx, up),
+                                                       dev(ctx, ui))
+    soft_terms = ctx.stat(lshkm.STAT_REC_SOFT)
+    soff = soff_s.cpu().numpy()
+    assert np.array_equal(soff, soff_t.cpu().numpy())
+    a, b = sims_s.cpu().numpy()[:soff[-1]], sims_t.cpu().numpy()[:soff[-1]]
+    ok, bad = bits_equal(b, a)
+    assert ok, (kind, bad)
+    pairs = int(soff[-1])
+    # grid rows (18 significant bits) always certify; full mantissas often do
+    # (the bound min_j lowbit(x_j) + min_j lowbit(u_j) is coarse): 12 % -> 6 %
+    if kind == "grid":
+        assert soft_sims > pairs // 50 and soft_terms < pairs // 200, (soft_sims, soft_terms, pairs)
+    elif kind == "normal":
+        assert soft_terms < 0.7 * soft_sims, (soft_sims, soft_terms, pairs)
+    for q in range(0, nq, 6):                                  # the oracle's x87 on a sample
+        mem = crows[crow[ucl[q]]:crow[ucl[q] + 1]]
+        _, osim, ocnt = oracle.p_closest(X, U[q:q + 1], np.array([0, len(mem)], np.int64), mem.astype(np.int32),
+                                         len(mem))
+        got = np.sort(b[soff[q]:soff[q + 1]])
+        want = np.sort(osim[0, :ocnt[0]])
+        ok, bad = bits_equal(got, want)
+        assert ok, (kind, q, bad)
