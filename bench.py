@@ -377,7 +377,11 @@ def main():
         it = sharding.ShardedLloyd(lk, ctx, lsh, X, Cc, src, mode="certified")
         if args.recom_users > 0:
             it.enable_recommend(N_total, rank * N, Q=args.recom_users, n_top=5)
+        ctx.reset_stats()
         elapsed = timed(it.step, steps, warmup, world, dev)
+        ex = {"per_step": True, "assign_ambiguous_rows": ctx.stat(lk.STAT_ASSIGN_AMBIG) // (steps + warmup),
+              "hash_fixup_rows": ctx.stat(lk.STAT_HASH_FIX) // (steps + warmup),
+              "refined_rows": ctx.stat(lk.STAT_REFINED) // (steps + warmup)}
         it.timing = True
         kms = fused_kernel_ms(lk, lib, ctx, it.step, max(3, steps))
         it.timing = False
@@ -405,6 +409,7 @@ def main():
                    "similarities_per_s": sims / ((ph1 + ph2) / 1e3)}
         rec = rec or {}
         rec["km_flagged_chains"] = it.flagged       # the last step's: carried rank to rank (segments)
+        rec["exactness"] = ex
         return elapsed, kms, xms, rec
 
     def c5_object(K, elapsed, kms, xms, rec=None, steps=args.steps):
@@ -424,6 +429,7 @@ def main():
             "allreduce": coll,
             "km_sums_exchange_ms": xms,         # the sums + their exchange + certificate (HIP events)
             "km_flagged_chains": (rec or {}).pop("km_flagged_chains", None),
+            "exactness": (rec or {}).pop("exactness", None),
             "recommend": rec or None,
             "roofline": roofline(N, K, kms, traffic_for(args.traffic_json_c5, N, K, "c5"),
                                  FUSED_WHAT + " (K = 1024: two 512-centroid passes)"),

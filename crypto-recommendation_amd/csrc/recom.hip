@@ -809,26 +809,88 @@ __global__ __launch_bounds__(256) void rc_user_meta_kernel(const T* __restrict__
 // certify a never-rounding x87 chain (exact.h ip_never_rounds): then the
 // quotient's status drops the chain's rounding bound, which alone declined
 // ~6-12 % of pairs (a 2^-58 relative R against a 2^-53 half ulp).
+// Plain fp64 chain (ct_exact53): when every partial sum of the products is a
+// multiple of 2^(qx + qu) below 2^T with T - (qx + qu) <= 53 -- T from the
+// Cauchy-Schwarz bound sqrt(xa ub) >= sum_j |x_j u_j| >= max_k |S_k| -- every
+// add of the chain is exact in fp64 as it is in the x87 chain: the sum is
+// exact in one fma per element (fp32 rows: the products are exact doubles)
+// instead of IpAcc's TwoSum (~10 fp64 ops), and it is ip87 itself.
+template <typename T>
+__device__ inline bool ct_exact53(double xa, double ub, int qx, int qu, double& bnd) {
+    // fp64 rows: the rounded products |RN(x u)| <= |x u| (1 + 2^-53)
+    bnd = sqrt(xa) * sqrt(ub) * (1.0 + 0x1p-40);
+    if (qx >= LOWBIT_NONE || qu >= LOWBIT_NONE) return true;     // a zero row: every product 0
+    if (!(bnd > 0.0 && bnd < 0x1p1000)) return false;
+    return ilogb(bnd) + 1 - (qx + qu) <= 53;
+}
+
 template <typename T, bool XA>
 __device__ inline double ct_sim_pl(const uint64_t* myrow8, const uint64_t* u8, int nunit, double ub, double& xa,
                                    int& qx, int qu, bool& ok) {
     constexpr int PER = 8 / (int)sizeof(T);
-    double xs = 0.0;
-    int ql = LOWBIT_NONE;
+    if (XA) {
+        // the member's sum_j pow(x_j, 2) in j order and its lowest set bit, once per member
+        double xs = 0.0;
+        int ql = LOWBIT_NONE;
+        auto xstep = [&](uint64_t xw) {
+            T xv[PER];
+            memcpy(xv, &xw, 8);
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
+                xs = __dadd_rn(xs, sq_of<T>((double)xv[k]));
+                ql = min(ql, lowbit_exp(xv[k]));
+            }
+        };
+        int w = 0;
+        for (; w + 4 <= nunit; w += 4) {
+            uint64_t xw[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) xw[k] = myrow8[w + k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) xstep(xw[k]);
+        }
+        for (; w < nunit; w++) xstep(myrow8[w]);
+        xa = xs;
+        qx = ql;
+    }
+    const double denom = __dmul_rn(sqrt(xa), sqrt(ub));
+    double bnd;
+    double sv = 0.0, qr;
+    if (ct_exact53<T>(xa, ub, qx, qu, bnd)) {
+        double s = 0.0;
+        auto step = [&](uint64_t xw, uint64_t uw) {
+            T xv[PER], uv[PER];
+            memcpy(xv, &xw, 8);
+            memcpy(uv, &uw, 8);
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
+                const double xj = (double)xv[k], uj = (double)uv[k];
+                if constexpr (sizeof(T) == 4) s = fma(xj, uj, s);          // exact product, exact sum
+                else s = __dadd_rn(s, __dmul_rn(xj, uj));                  // the reference's rounded product
+            }
+        };
+        int w = 0;
+        for (; w + 4 <= nunit; w += 4) {
+            uint64_t xw[4], uw[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) { xw[k] = myrow8[w + k]; uw[k] = u8[w + k]; }
+#pragma unroll
+            for (int k = 0; k < 4; k++) step(xw[k], uw[k]);
+        }
+        for (; w < nunit; w++) step(myrow8[w], u8[w]);
+        IpAcc ip;
+        ip.sh = s;
+        ip.mx = bnd;
+        ok = ip.quot_status(denom, sv, qr, true) == 0;
+        return sv;
+    }
     IpAcc ip;
     auto step = [&](uint64_t xw, uint64_t uw) {
         T xv[PER], uv[PER];
         memcpy(xv, &xw, 8);
         memcpy(uv, &uw, 8);
 #pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const double xj = (double)xv[k], uj = (double)uv[k];
-            ip.add(__dmul_rn(xj, uj));
-            if (XA) {
-                xs = __dadd_rn(xs, sq_of<T>(xj));
-                ql = min(ql, lowbit_exp(xv[k]));
-            }
-        }
+        for (int k = 0; k < PER; k++) ip.add(__dmul_rn((double)xv[k], (double)uv[k]));
     };
     int w = 0;
     if (nunit >= 4) {
@@ -849,12 +911,6 @@ __device__ inline double ct_sim_pl(const uint64_t* myrow8, const uint64_t* u8, i
         w += 4;
     }
     for (; w < nunit; w++) step(myrow8[w], u8[w]);
-    if (XA) {
-        xa = xs;
-        qx = ql;
-    }
-    const double denom = __dmul_rn(sqrt(xa), sqrt(ub));
-    double sv, qr;
     const bool exact = ip_never_rounds(ip.mx, min(qx, LOWBIT_NONE) + min(qu, LOWBIT_NONE));
     ok = ip.quot_status(denom, sv, qr, exact) == 0;     // declined: rc_terms_fix_kernel decides
     return sv;
