@@ -190,14 +190,23 @@ static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
 
 // Host view of the cluster CSR: every user's member count on this shard and
 // the prefix offsets of its similarities.
+// unk_ptr / hup (optional): the unknown-index CSR offsets, read in the same
+// batch of copies (one stream synchronisation for all three)
 static int shard_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, const int32_t* ucl, int64_t nq,
-                         std::vector<int64_t>& soff, std::vector<int32_t>* hu_out = nullptr) {
+                         std::vector<int64_t>& soff, std::vector<int32_t>* hu_out = nullptr,
+                         const int64_t* unk_ptr = nullptr, std::vector<int64_t>* hup = nullptr) {
     std::vector<int64_t> hc((size_t)K + 1);
-    std::vector<int32_t> hu;
-    int rc;
-    if ((rc = read_ucl(ctx, ucl, nq, K, hu))) return rc;
-    LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<int32_t> hu((size_t)nq);
+    if (hup) hup->assign((size_t)nq + 1, 0);
+    {
+        const StreamSyncOnExit sync_guard{ctx->stream};   // every copy lands before the host reads it
+        if (nq > 0) LSHKM_HIP(hipMemcpyAsync(hu.data(), ucl, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+        LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
+        if (hup)
+            LSHKM_HIP(hipMemcpyAsync(hup->data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    for (int64_t q = 0; q < nq; q++)
+        LSHKM_CHECK(hu[q] >= 0 && hu[q] < K, LSHKM_ERR_ARG, "ucl holds a cluster ID outside [0, K)");
     bool ok = hc[0] == 0;
     for (int c = 0; c < K && ok; c++) ok = hc[c + 1] >= hc[c];
     LSHKM_CHECK(ok && hc[K] <= N, LSHKM_ERR_ARG, "bad cluster CSR");
@@ -275,10 +284,7 @@ static int terms_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, c
                          const int64_t* unk_ptr, std::vector<int64_t>& soff, std::vector<int64_t>& hup,
                          std::vector<int64_t>& toff, std::vector<int32_t>* hu_out) {
     int rc;
-    if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff, hu_out))) return rc;
-    hup.assign((size_t)nq + 1, 0);
-    LSHKM_HIP(hipMemcpyAsync(hup.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff, hu_out, unk_ptr, &hup))) return rc;
     toff.assign((size_t)nq + 1, 0);
     bool ok = hup[0] == 0;
     for (int64_t q = 0; q < nq && ok; q++) {
@@ -379,22 +385,23 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
     LSHKM_CHECK(out || (main_out && abs_out && cnt_out), LSHKM_ERR_ARG, "either the carry outputs or out");
     if (nq == 0) return 0;
     LSHKM_HIP(hipSetDevice(ctx->device));
-    int64_t total = 0;
     int rc;
-    LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    // users whose cluster holds >= RC_LONG_MIN members here: their chains by
+    // binade segments (the offsets come to the host to find them), in batches of
+    // at most ~1 GiB of packed values; the unknown-index total is hu[nq] (one
+    // batch of copies, one synchronisation)
+    std::vector<int64_t> hs((size_t)nq + 1), ht((size_t)nq + 1), hu((size_t)nq + 1);
+    {
+        const StreamSyncOnExit sync_guard{ctx->stream};
+        LSHKM_HIP(hipMemcpyAsync(hs.data(), soff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+        LSHKM_HIP(hipMemcpyAsync(ht.data(), toff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+        LSHKM_HIP(hipMemcpyAsync(hu.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    const int64_t total = hu[nq];
     LSHKM_CHECK(total == 0 || unk_idx, LSHKM_ERR_ARG, "unk_idx is NULL");
     Buf &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
     const size_t M = (size_t)(total > 0 ? total : 1);
     if (out && ((rc = pred.reserve(sizeof(double) * M)) || (rc = pidx.reserve(sizeof(int32_t) * M)))) return rc;
-    // users whose cluster holds >= RC_LONG_MIN members here: their chains by
-    // binade segments (the offsets come to the host to find them), in batches of
-    // at most ~1 GiB of packed values
-    std::vector<int64_t> hs((size_t)nq + 1), ht((size_t)nq + 1), hu((size_t)nq + 1);
-    LSHKM_HIP(hipMemcpyAsync(hs.data(), soff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipMemcpyAsync(ht.data(), toff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipMemcpyAsync(hu.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
     std::vector<RcLongUser> lus;
     for (int64_t q = 0; q < nq; q++) {
         const int64_t n = hs[q + 1] - hs[q];

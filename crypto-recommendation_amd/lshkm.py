@@ -782,10 +782,25 @@ def cluster_terms(ctx, X, x_mean, crow, crows, U, ucl, unk_ptr, unk_idx):
     ui = _t_ptr(unk_idx) if unk_idx.numel() else None
     args = (ctx.h, _t_ptr(X), _t_ptr(x_mean), N, d, _t_ptr(crow), cr, K, _t_ptr(U), nq, _t_ptr(ucl), _t_ptr(unk_ptr),
             ui, _t_ptr(soff), _t_ptr(toff))
-    _ck(fn(*args, None, None, 0, 0, C.byref(total), C.byref(tt)))
+    # one call when buffers of the previous call's sizes (+1/8) hold this call's
+    # output: the library computes only when both totals fit and reports them
+    # either way; else a second call into buffers of the reported sizes
+    cache = ctx.__dict__.setdefault("_terms_sizes", {})
+    key = (str(X.device), X.dtype, nq)
+    if key in cache:
+        cs, ct = cache[key]
+        sims = ctx.empty((cs + cs // 8 + 1,), torch.float64)
+        terms = ctx.empty((ct + ct // 8 + 1,), torch.float64)
+        _ck(fn(*args, _t_ptr(sims), _t_ptr(terms), sims.numel(), terms.numel(), C.byref(total), C.byref(tt)))
+        if total.value <= sims.numel() and tt.value <= terms.numel():
+            cache[key] = (total.value, tt.value)
+            return soff, toff, sims[:max(total.value, 1)], terms[:max(tt.value, 1)]
+    else:
+        _ck(fn(*args, None, None, 0, 0, C.byref(total), C.byref(tt)))
     sims = ctx.empty((max(total.value, 1),), torch.float64)
     terms = ctx.empty((max(tt.value, 1),), torch.float64)
     _ck(fn(*args, _t_ptr(sims), _t_ptr(terms), total.value, tt.value, C.byref(total), C.byref(tt)))
+    cache[key] = (total.value, tt.value)
     return soff, toff, sims, terms
 
 

@@ -329,17 +329,31 @@ def synth_recom_users(ctx, n_total, Q, d, seed):
     return rows, U, u_mean, unk_ptr, unk_idx
 
 
-def user_clusters(ctx, rows, assign_local, row0, n):
+def user_cluster_index(ctx, rows, row0, n):
+    """(positions, local rows) of the users this rank owns, device tensors (or
+    None when it owns none): user_clusters' gather, formed once per user set."""
+    mine = (rows >= row0) & (rows < row0 + n)
+    if not mine.any():
+        return None
+    torch = ctx.torch
+    return (torch.from_numpy(np.nonzero(mine)[0]).to(ctx.dev),
+            torch.from_numpy(rows[mine] - row0).to(ctx.dev))
+
+
+def user_clusters(ctx, rows, assign_local, row0, n, index=False):
     """The users' clusters (main.cpp:261: user.getCluster()): the owning rank's
-    assignment of each user row, all-reduced (one int32 per user)."""
+    assignment of each user row, all-reduced (one int32 per user). index: a
+    user_cluster_index result for these rows (False: formed here)."""
     torch = ctx.torch
     Q = len(rows)
-    ucl = torch.zeros((Q,), dtype=torch.int32, device=ctx.dev)
-    mine = (rows >= row0) & (rows < row0 + n)
-    if mine.any():
-        loc = torch.from_numpy(rows[mine] - row0).to(ctx.dev)
-        ucl[torch.from_numpy(np.nonzero(mine)[0]).to(ctx.dev)] = assign_local[loc]
+    if index is False:
+        index = user_cluster_index(ctx, rows, row0, n)
     dist = _dist()
+    if dist is None and index is not None and index[0].numel() == Q:
+        return assign_local.index_select(0, index[1])        # every user local: one gather
+    ucl = torch.zeros((Q,), dtype=torch.int32, device=ctx.dev)
+    if index is not None:
+        ucl[index[0]] = assign_local[index[1]]
     if dist is not None:
         b, back = _staged(dist, ucl)
         dist.all_reduce(b)
@@ -441,14 +455,15 @@ class ShardedLloyd:
         if x_mean is None:
             x_mean = torch.zeros((n,), dtype=torch.float64, device=self.ctx.dev)
         rows, U, um, up, ui = synth_recom_users(self.ctx, n_total, Q, self.d, seed)
-        self.recom = dict(row0=row0, n_top=n_top, x_mean=x_mean, rows=rows, U=U, u_mean=um, unk_ptr=up, unk_idx=ui)
+        self.recom = dict(row0=row0, n_top=n_top, x_mean=x_mean, rows=rows, U=U, u_mean=um, unk_ptr=up, unk_idx=ui,
+                          index=user_cluster_index(self.ctx, rows, row0, n))
         self.recom_out = None
         self.recom_ucl = None
         self.recom_timing = None      # a list: (phase-1 ms, phase-2 ms) per step
 
     def recommend(self):
         r = self.recom
-        ucl = user_clusters(self.ctx, r["rows"], self.assign, r["row0"], self.X.shape[0])
+        ucl = user_clusters(self.ctx, r["rows"], self.assign, r["row0"], self.X.shape[0], index=r["index"])
         self.recom_ucl = ucl
         self.recom_out = recommend_sharded(self.lk, self.ctx, self.X, r["x_mean"], self.assign, self.K, r["U"],
                                            r["u_mean"], ucl, r["unk_ptr"], r["unk_idx"], r["n_top"],
