@@ -67,10 +67,56 @@ int reserve_scan(lshkm_ctx ctx, size_t bytes) {
     return ctx->ws_scan.reserve(bytes);
 }
 
-int d2h(lshkm_ctx ctx, void* dst, const void* src, size_t bytes) {
-    LSHKM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+// batches beyond this go straight to their (pageable) destinations
+constexpr size_t PIN_BATCH_MAX = (size_t)16 << 20;
+
+int d2h_batch_impl(lshkm_ctx ctx, const D2H* r, int n) {
+    size_t tot = 0;
+    for (int i = 0; i < n; i++) tot += (r[i].bytes + 255) & ~(size_t)255;
+    if (tot > PIN_BATCH_MAX || lshkm_ctx_s::pin_grow(ctx->rb_buf, ctx->rb_cap, tot)) {
+        for (int i = 0; i < n; i++)
+            if (r[i].bytes) LSHKM_HIP(hipMemcpyAsync(r[i].dst, r[i].src, r[i].bytes, hipMemcpyDeviceToHost, ctx->stream));
+        LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+        return 0;
+    }
+    char* b = static_cast<char*>(ctx->rb_buf);
+    size_t off = 0;
+    for (int i = 0; i < n; i++) {
+        if (r[i].bytes) LSHKM_HIP(hipMemcpyAsync(b + off, r[i].src, r[i].bytes, hipMemcpyDeviceToHost, ctx->stream));
+        off += (r[i].bytes + 255) & ~(size_t)255;
+    }
     LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    off = 0;
+    for (int i = 0; i < n; i++) {
+        if (r[i].bytes) std::memcpy(r[i].dst, b + off, r[i].bytes);
+        off += (r[i].bytes + 255) & ~(size_t)255;
+    }
     return 0;
+}
+
+int h2d_batch_impl(lshkm_ctx ctx, const H2D* r, int n) {
+    size_t tot = 0;
+    for (int i = 0; i < n; i++) tot += (r[i].bytes + 255) & ~(size_t)255;
+    if (tot > PIN_BATCH_MAX || lshkm_ctx_s::pin_grow(ctx->ub_buf, ctx->ub_cap, tot)) {
+        for (int i = 0; i < n; i++)
+            if (r[i].bytes) LSHKM_HIP(hipMemcpyAsync(r[i].dst, r[i].src, r[i].bytes, hipMemcpyHostToDevice, ctx->stream));
+        return 0;
+    }
+    char* b = static_cast<char*>(ctx->ub_buf);
+    size_t off = 0;
+    for (int i = 0; i < n; i++) {
+        if (r[i].bytes) {
+            std::memcpy(b + off, r[i].src, r[i].bytes);
+            LSHKM_HIP(hipMemcpyAsync(r[i].dst, b + off, r[i].bytes, hipMemcpyHostToDevice, ctx->stream));
+        }
+        off += (r[i].bytes + 255) & ~(size_t)255;
+    }
+    return 0;
+}
+
+int d2h(lshkm_ctx ctx, void* dst, const void* src, size_t bytes) {
+    const D2H r{dst, src, bytes};
+    return d2h_batch_impl(ctx, &r, 1);
 }
 
 // Stable scatter of keys[i * kstride] in [0, nb) -> idx (row order kept) + row_ptr.
@@ -925,3 +971,8 @@ int lshkm_silhouette_f64(lshkm_ctx ctx, const double* X, int64_t N, int d, const
 }
 
 }  // extern "C"
+
+namespace lshkm {
+int d2h_batch(lshkm_ctx_s* ctx, const D2H* r, int n) { return d2h_batch_impl(ctx, r, n); }
+int h2d_batch(lshkm_ctx_s* ctx, const H2D* r, int n) { return h2d_batch_impl(ctx, r, n); }
+}  // namespace lshkm

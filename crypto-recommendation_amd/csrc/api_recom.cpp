@@ -14,9 +14,8 @@
 using namespace lshkm;
 
 static int read_i64(lshkm_ctx ctx, const int64_t* dev, int64_t* host) {
-    LSHKM_HIP(hipMemcpyAsync(host, dev, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
-    return 0;
+    const D2H r{host, dev, sizeof(int64_t)};
+    return d2h_batch(ctx, &r, 1);
 }
 
 // Host vectors handed to hipMemcpyAsync must outlive the copy: declared after
@@ -33,8 +32,9 @@ struct StreamSyncOnExit {
 static int read_ucl(lshkm_ctx ctx, const int32_t* ucl, int64_t nq, int K, std::vector<int32_t>& hu) {
     hu.resize((size_t)nq);
     if (nq == 0) return 0;
-    LSHKM_HIP(hipMemcpyAsync(hu.data(), ucl, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    const D2H r{hu.data(), ucl, sizeof(int32_t) * nq};
+    int rc;
+    if ((rc = d2h_batch(ctx, &r, 1))) return rc;
     for (int64_t q = 0; q < nq; q++)
         LSHKM_CHECK(hu[q] >= 0 && hu[q] < K, LSHKM_ERR_ARG, "ucl holds a cluster ID outside [0, K)");
     return 0;
@@ -153,9 +153,11 @@ static int cluster_top_n_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
         int rc;
         if ((rc = read_ucl(ctx, ucl, nq, K, hu))) return rc;
     }
-    LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    {
+        const D2H rd[2] = {{hc.data(), crow, sizeof(int64_t) * (K + 1)}, {&total, unk_ptr + nq, sizeof(int64_t)}};
+        int rc;
+        if ((rc = d2h_batch(ctx, rd, 2))) return rc;
+    }
     int64_t maxn = 0;
     bool ok = hc[0] == 0;
     for (int c = 0; c < K && ok; c++) {
@@ -198,13 +200,11 @@ static int shard_offsets(lshkm_ctx ctx, const int64_t* crow, int K, int64_t N, c
     std::vector<int64_t> hc((size_t)K + 1);
     std::vector<int32_t> hu((size_t)nq);
     if (hup) hup->assign((size_t)nq + 1, 0);
-    {
-        const StreamSyncOnExit sync_guard{ctx->stream};   // every copy lands before the host reads it
-        if (nq > 0) LSHKM_HIP(hipMemcpyAsync(hu.data(), ucl, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
-        LSHKM_HIP(hipMemcpyAsync(hc.data(), crow, sizeof(int64_t) * (K + 1), hipMemcpyDeviceToHost, ctx->stream));
-        if (hup)
-            LSHKM_HIP(hipMemcpyAsync(hup->data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-    }
+    const D2H rd[3] = {{hc.data(), crow, sizeof(int64_t) * (K + 1)},
+                       {hu.data(), ucl, sizeof(int32_t) * nq},
+                       {hup ? hup->data() : nullptr, unk_ptr, hup ? sizeof(int64_t) * (nq + 1) : 0}};
+    int rc;
+    if ((rc = d2h_batch(ctx, rd, 3))) return rc;
     for (int64_t q = 0; q < nq; q++)
         LSHKM_CHECK(hu[q] >= 0 && hu[q] < K, LSHKM_ERR_ARG, "ucl holds a cluster ID outside [0, K)");
     bool ok = hc[0] == 0;
@@ -232,7 +232,8 @@ static int cluster_sims_impl(lshkm_ctx ctx, Pts X, int64_t N, int d, const int64
     int rc;
     if ((rc = shard_offsets(ctx, crow, K, N, ucl, nq, soff))) return rc;
     *total_host = soff[nq];
-    LSHKM_HIP(hipMemcpyAsync(soff_dev, soff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, ctx->stream));
+    const H2D up{soff_dev, soff.data(), sizeof(int64_t) * (nq + 1)};
+    if ((rc = h2d_batch(ctx, &up, 1))) return rc;
     if (sims && soff[nq] <= cap && soff[nq] > 0) {
         LSHKM_CHECK(crows, LSHKM_ERR_ARG, "crows is NULL");
         if ((rc = launch_rc_shard_sims(ctx->stream, X, d, crow, crows, K, U, nq, ucl, unk_ptr, soff_dev, sims,
@@ -260,8 +261,7 @@ static int cluster_chain_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     int rc;
     std::vector<int32_t> hu;
     if ((rc = read_ucl(ctx, ucl, nq, K, hu))) return rc;
-    LSHKM_HIP(hipMemcpyAsync(&total, unk_ptr + nq, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = read_i64(ctx, unk_ptr + nq, &total))) return rc;
     LSHKM_CHECK(total >= 0 && (total == 0 || unk_idx), LSHKM_ERR_ARG, "bad unknown-index lists");
     Buf &pred = ctx->ws_call[1], &pidx = ctx->ws_call[2];
     const size_t M = (size_t)(total > 0 ? total : 1);
@@ -315,9 +315,11 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     *total_host = soff[nq];
     *tterms_host = toff[nq];
     LSHKM_CHECK(toff[nq] == 0 || unk_idx, LSHKM_ERR_ARG, "unk_idx is NULL");
-    LSHKM_HIP(hipMemcpyAsync(soff_dev, soff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, ctx->stream));
-    LSHKM_HIP(hipMemcpyAsync(toff_dev, toff.data(), sizeof(int64_t) * (nq + 1), hipMemcpyHostToDevice, ctx->stream));
-    if (sims && terms && soff[nq] <= cap && toff[nq] <= tcap && soff[nq] > 0) {
+    const H2D offs[2] = {{soff_dev, soff.data(), sizeof(int64_t) * (nq + 1)},
+                         {toff_dev, toff.data(), sizeof(int64_t) * (nq + 1)}};
+    if (!(sims && terms && soff[nq] <= cap && toff[nq] <= tcap && soff[nq] > 0)) {
+        if ((rc = h2d_batch(ctx, offs, 2))) return rc;
+    } else {
         LSHKM_CHECK(crows, LSHKM_ERR_ARG, "crows is NULL");
         Buf& map = ctx->ws_call[8];                  // member -> (user, row); the declined-member list + count
         // mq | mr | the declined list | its count | unorm | the blocks' private lists | their capacities and counts
@@ -360,8 +362,8 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
         const size_t user_off = item_off + (RC_ITEM_BYTES * (size_t)std::max<int64_t>(nitems, 1) + 255) / 256 * 256;
         if ((rc = gb.reserve(user_off + RC_USER_BYTES * std::max<size_t>(byc.size(), 1)))) return rc;
         int32_t* dp = gb.as<int32_t>();
-        if (!pack.empty())
-            LSHKM_HIP(hipMemcpyAsync(dp, pack.data(), 4 * pack.size(), hipMemcpyHostToDevice, ctx->stream));
+        const H2D up[3] = {offs[0], offs[1], {dp, pack.data(), 4 * pack.size()}};
+        if ((rc = h2d_batch(ctx, up, 3))) return rc;
         const RcGroups groups{dp, (int)nG, nitems, dp + nG + 1, dp + 2 * nG + 1, dp + 3 * nG + 2, gb.as<char>() + item_off,
                               (int64_t)byc.size(), gb.as<char>() + user_off};
         if ((rc = launch_rc_terms(ctx->stream, X, x_mean, d, crow, crows, K, U, nq, ucl, soff_dev, soff[nq], unk_ptr,
@@ -392,10 +394,10 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
     // batch of copies, one synchronisation)
     std::vector<int64_t> hs((size_t)nq + 1), ht((size_t)nq + 1), hu((size_t)nq + 1);
     {
-        const StreamSyncOnExit sync_guard{ctx->stream};
-        LSHKM_HIP(hipMemcpyAsync(hs.data(), soff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-        LSHKM_HIP(hipMemcpyAsync(ht.data(), toff, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
-        LSHKM_HIP(hipMemcpyAsync(hu.data(), unk_ptr, sizeof(int64_t) * (nq + 1), hipMemcpyDeviceToHost, ctx->stream));
+        const D2H rd[3] = {{hs.data(), soff, sizeof(int64_t) * (nq + 1)},
+                           {ht.data(), toff, sizeof(int64_t) * (nq + 1)},
+                           {hu.data(), unk_ptr, sizeof(int64_t) * (nq + 1)}};
+        if ((rc = d2h_batch(ctx, rd, 3))) return rc;
     }
     const int64_t total = hu[nq];
     LSHKM_CHECK(total == 0 || unk_idx, LSHKM_ERR_ARG, "unk_idx is NULL");
@@ -446,8 +448,8 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
         L.nlong = nl;
         L.rows = rows;
         L.D = (int)D;
-        LSHKM_HIP(hipMemcpyAsync(tab, lus.data() + k0, tb, hipMemcpyHostToDevice, ctx->stream));
-        LSHKM_HIP(hipMemcpyAsync(crow, hcrow.data(), rb, hipMemcpyHostToDevice, ctx->stream));
+        const H2D up[2] = {{tab, lus.data() + k0, tb}, {crow, hcrow.data(), rb}};
+        if ((rc = h2d_batch(ctx, up, 2))) return rc;
         if ((rc = launch_rc_long(ctx->stream, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
                                  out ? nullptr : main_out, out ? nullptr : abs_out, out ? nullptr : cnt_out,
                                  out ? pred.as<double>() : nullptr, L)))

@@ -1,5 +1,6 @@
 // index.h — handle types behind the opaque C ABI pointers.
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -127,7 +128,28 @@ struct lshkm_ctx_s {
         pinned_ev = pin_ev[i];
         return 0;
     }
+    // pinned host buffers of the entry points that synchronise their stream
+    // before returning: rb_buf receives device->host reads (d2h_batch: async
+    // copies, one synchronisation per batch -- into pageable memory every copy
+    // was its own blocking round trip, ~20 us each), ub_buf stages host->device
+    // uploads (h2d_batch; reused only after the calling entry point's sync)
+    void* rb_buf = nullptr;
+    size_t rb_cap = 0;
+    void* ub_buf = nullptr;
+    size_t ub_cap = 0;
+    static int pin_grow(void*& b, size_t& cap, size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (b) (void)hipHostFree(b);
+        b = nullptr;
+        cap = 0;
+        const size_t nb = std::max<size_t>(bytes, 64 << 10);
+        if (hipHostMalloc(&b, nb, hipHostMallocDefault) != hipSuccess) return -3;
+        cap = nb;
+        return 0;
+    }
     ~lshkm_ctx_s() {
+        if (rb_buf) (void)hipHostFree(rb_buf);
+        if (ub_buf) (void)hipHostFree(ub_buf);
         for (hipEvent_t& e : tev)
             if (e) (void)hipEventDestroy(e);
         if (side_stream) (void)hipStreamSynchronize(side_stream), (void)hipStreamDestroy(side_stream);
@@ -139,6 +161,17 @@ struct lshkm_ctx_s {
         }
     }
 };
+
+namespace lshkm {
+// Device->host reads / host->device uploads in one batch (api_index.cpp):
+// d2h_batch returns after every read landed in its destination; h2d_batch only
+// issues the copies (from ctx->ub_buf: the caller synchronises its stream
+// before it returns, and before any later h2d_batch of the same call).
+struct D2H { void* dst; const void* src; size_t bytes; };
+struct H2D { void* dst; const void* src; size_t bytes; };
+int d2h_batch(lshkm_ctx_s* ctx, const D2H* r, int n);
+int h2d_batch(lshkm_ctx_s* ctx, const H2D* r, int n);
+}  // namespace lshkm
 
 struct lshkm_lsh_s {
     lshkm_ctx_s* ctx = nullptr;
