@@ -97,9 +97,16 @@ int d2h_batch_impl(lshkm_ctx ctx, const D2H* r, int n) {
 int h2d_batch_impl(lshkm_ctx ctx, const H2D* r, int n) {
     size_t tot = 0;
     for (int i = 0; i < n; i++) tot += (r[i].bytes + 255) & ~(size_t)255;
-    if (tot > PIN_BATCH_MAX || lshkm_ctx_s::pin_grow(ctx->ub_buf, ctx->ub_cap, tot)) {
+    if (ctx->ub_pending) {                           // the previous batch's copies still read ub_buf
+        LSHKM_HIP(hipEventSynchronize(ctx->ub_ev));
+        ctx->ub_pending = false;
+    }
+    if (!ctx->ub_ev && hipEventCreateWithFlags(&ctx->ub_ev, hipEventDisableTiming) != hipSuccess) ctx->ub_ev = nullptr;
+    if (!ctx->ub_ev || tot > PIN_BATCH_MAX || lshkm_ctx_s::pin_grow(ctx->ub_buf, ctx->ub_cap, tot)) {
+        // pageable sources: copied before return (the caller's buffers may go)
         for (int i = 0; i < n; i++)
             if (r[i].bytes) LSHKM_HIP(hipMemcpyAsync(r[i].dst, r[i].src, r[i].bytes, hipMemcpyHostToDevice, ctx->stream));
+        LSHKM_HIP(hipStreamSynchronize(ctx->stream));
         return 0;
     }
     char* b = static_cast<char*>(ctx->ub_buf);
@@ -111,6 +118,8 @@ int h2d_batch_impl(lshkm_ctx ctx, const H2D* r, int n) {
         }
         off += (r[i].bytes + 255) & ~(size_t)255;
     }
+    LSHKM_HIP(hipEventRecord(ctx->ub_ev, ctx->stream));
+    ctx->ub_pending = true;
     return 0;
 }
 

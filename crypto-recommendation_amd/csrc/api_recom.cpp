@@ -308,8 +308,7 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
     LSHKM_HIP(hipSetDevice(ctx->device));
     std::vector<int64_t> soff, hup, toff;
     std::vector<int32_t> hu;                       // the users' clusters (host)
-    std::vector<int32_t> pack;                     // the cluster-major work list (host side of its copy)
-    const StreamSyncOnExit sync_guard{ctx->stream};   // the host vectors are copied before return
+    std::vector<int32_t> pack;                     // the cluster-major work list (staged by h2d_batch)
     int rc;
     if ((rc = terms_offsets(ctx, crow, K, N, ucl, nq, unk_ptr, soff, hup, toff, &hu))) return rc;
     *total_host = soff[nq];
@@ -372,7 +371,8 @@ static int cluster_terms_impl(lshkm_ctx ctx, Pts X, const double* x_mean, int64_
                                   (unsigned long long*)ctx->stats.p + STAT_REC_SOFT, unorm, &groups, fregion, faux)))
             return rc;
     }
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));
+    // no host synchronisation: the uploads are staged (h2d_batch), the outputs
+    // and the workspaces are ordered on the stream
     return 0;
 }
 
@@ -409,8 +409,7 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
         const int64_t n = hs[q + 1] - hs[q];
         if (n >= RC_LONG_MIN) lus.push_back(RcLongUser{q, n, hs[q], ht[q], hu[q], hu[q + 1] - hu[q], 0, 0});
     }
-    std::vector<int64_t> hcrow;
-    const StreamSyncOnExit sync_guard{ctx->stream};     // lus / hcrow are copied before return
+    std::vector<int64_t> hcrow;                         // staged by h2d_batch with the user table
     const int64_t long_min = lus.empty() ? INT64_MAX : RC_LONG_MIN;
     for (size_t k0 = 0; k0 < lus.size();) {
         // a batch: users k0 .. k1-1, D = their max m + 1, rows * D * 8 <= 1 GiB (one user at least)
@@ -454,7 +453,8 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
                                  out ? nullptr : main_out, out ? nullptr : abs_out, out ? nullptr : cnt_out,
                                  out ? pred.as<double>() : nullptr, L)))
             return rc;
-        LSHKM_HIP(hipStreamSynchronize(ctx->stream));      // the next batch reuses the workspace and hcrow
+        // a further batch may grow ws_long: not while this one's kernels run
+        if (k1 < lus.size()) LSHKM_HIP(hipStreamSynchronize(ctx->stream));
         k0 = k1;
     }
     if ((rc = launch_rc_chain_terms(ctx->stream, nq, soff, unk_ptr, toff, sims, terms, carry_main, carry_abs, carry_cnt, u_mean,
@@ -468,7 +468,8 @@ static int chain_terms_impl(lshkm_ctx ctx, int64_t nq, const double* u_mean, con
         (void)hipStreamSynchronize(ctx->stream);
         return rc;
     }
-    LSHKM_HIP(hipStreamSynchronize(ctx->stream));   // the slot / pred workspace is reused by the next call
+    // no host synchronisation: the pred / pidx workspace's next user is ordered
+    // on the same stream (a reserve that grows it frees through hipFree)
     return 0;
 }
 

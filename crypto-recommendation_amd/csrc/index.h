@@ -137,6 +137,8 @@ struct lshkm_ctx_s {
     size_t rb_cap = 0;
     void* ub_buf = nullptr;
     size_t ub_cap = 0;
+    hipEvent_t ub_ev = nullptr;      // recorded after each upload batch: ub_buf is rewritten only after it
+    bool ub_pending = false;
     static int pin_grow(void*& b, size_t& cap, size_t bytes) {
         if (bytes <= cap) return 0;
         if (b) (void)hipHostFree(b);
@@ -149,6 +151,10 @@ struct lshkm_ctx_s {
     }
     ~lshkm_ctx_s() {
         if (rb_buf) (void)hipHostFree(rb_buf);
+        if (ub_ev) {
+            if (ub_pending) (void)hipEventSynchronize(ub_ev);
+            (void)hipEventDestroy(ub_ev);
+        }
         if (ub_buf) (void)hipHostFree(ub_buf);
         for (hipEvent_t& e : tev)
             if (e) (void)hipEventDestroy(e);
@@ -164,9 +170,10 @@ struct lshkm_ctx_s {
 
 namespace lshkm {
 // Device->host reads / host->device uploads in one batch (api_index.cpp):
-// d2h_batch returns after every read landed in its destination; h2d_batch only
-// issues the copies (from ctx->ub_buf: the caller synchronises its stream
-// before it returns, and before any later h2d_batch of the same call).
+// d2h_batch returns after every read landed in its destination; h2d_batch
+// stages the sources in ctx->ub_buf and only issues the copies (the host
+// buffers may go at once; the next batch waits for this one's copies before it
+// rewrites ub_buf).
 struct D2H { void* dst; const void* src; size_t bytes; };
 struct H2D { void* dst; const void* src; size_t bytes; };
 int d2h_batch(lshkm_ctx_s* ctx, const D2H* r, int n);
