@@ -2033,10 +2033,13 @@ __device__ inline void fix_load(const FusedArgs& a, unsigned long long ent, int 
 template <bool COS>
 __device__ inline void fix_row(const FusedArgs& a, const double* pts, const double* cpn, const double* ctt,
                                const int32_t* crv, int q, FixRow& r) {
-    double xn2 = 0.0;
+    // four independent accumulators per lane (the fp64 FMA chains of 32 left the
+    // waves issue-stalled on their dependencies, 39 % of their cycles): nx only
+    // bounds, and the dot product's bound covers any summation order (depth 12 here)
+    double xq[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int j = 0; j < 32; j++) xn2 = fma((double)r.x[j], (double)r.x[j], xn2);
-    const double nx = sqrt(group4_sum(xn2));
+    for (int j = 0; j < 32; j++) xq[j & 3] = fma((double)r.x[j], (double)r.x[j], xq[j & 3]);
+    const double nx = sqrt(group4_sum((xq[0] + xq[1]) + (xq[2] + xq[3])));
     const float* xrow = a.X + r.row * FU_D;
     const int k = a.k;
     const double iwd = 1.0 / (double)a.w;
@@ -2046,10 +2049,10 @@ __device__ inline void fix_row(const FusedArgs& a, const double* pts, const doub
         // keep the fp64 widening inside the loop (hoisted, it holds 64 VGPRs)
 #pragma unroll
         for (int j = 0; j < 32; j++) asm volatile("" : "+v"(r.x[j]));
-        double acc = 0.0;
+        double aq[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int j = 0; j < 32; j++) acc = fma(pq[j * HF_PS], (double)r.x[j], acc);
-        acc = group4_sum(acc);
+        for (int j = 0; j < 32; j++) aq[j & 3] = fma(pq[j * HF_PS], (double)r.x[j], aq[j & 3]);
+        const double acc = group4_sum((aq[0] + aq[1]) + (aq[2] + aq[3]));
         const double P = cpn[f] * nx * (1.0 + 0x1p-40);
         if (COS) {
             const double B = (double)(FU_D + 3) * 0x1p-52 * P + 0x1p-1000;
