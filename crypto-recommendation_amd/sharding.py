@@ -242,6 +242,54 @@ def allreduce_partials(sums, counts):
     return sums, counts
 
 
+def recommend_terms(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, unk_idx, csr=None):
+    """Phase 1 of recommend_sharded (steps 1-2 below): this rank's similarities
+    and prediction terms, all ranks at once. Returns the state recommend_chain
+    continues from."""
+    crow, crows = csr if csr is not None else lk.clusters(ctx, assign, K)
+    # the terms form stages rows of <= 1016 B in 8-B units (lshkm_cluster_terms):
+    # other rows (fp32 of odd d, fp64 of d >= 128) take the sims form, the same
+    # rank-to-rank chain over lshkm_cluster_sims + lshkm_cluster_chain
+    rb = X.shape[1] * X.element_size()
+    if rb % 8 == 0 and rb <= 1016:
+        soff, toff, sims, terms = lk.cluster_terms(ctx, X, x_mean, crow, crows, U, ucl, unk_ptr, unk_idx)
+        return (lk.cluster_chain_terms, (ctx, u_mean, unk_ptr, unk_idx, soff, toff, sims, terms), ucl, unk_idx)
+    soff, sims = lk.cluster_sims(ctx, X, crow, crows, U, ucl, unk_ptr)
+    return (lk.cluster_chain, (ctx, X, x_mean, crow, crows, ucl, u_mean, unk_ptr, unk_idx, soff, sims), ucl, unk_idx)
+
+
+def recommend_chain(ctx, state, n_top):
+    """Phase 2 of recommend_sharded (step 3 below): the prediction sums carried
+    rank to rank from recommend_terms' state; the result on every rank."""
+    torch = ctx.torch
+    chain, args, ucl, unk_idx = state
+    dist = _dist()
+    if dist is None:
+        return chain(*args, carry=None, n_top=n_top)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    nq, M = ucl.shape[0], unk_idx.shape[0]
+    carry = None
+    if rank > 0:
+        carry = (ctx.empty((max(M, 1),), torch.float64), ctx.empty((nq,), torch.float64),
+                 ctx.empty((nq,), torch.int64))
+        for t in carry:
+            b, back = _staged(dist, t)
+            dist.recv(b, src=rank - 1)
+            back()
+    if rank + 1 < world:
+        outs = chain(*args, carry=carry, n_top=None)
+        for t in outs:
+            b, _ = _staged(dist, t)
+            dist.send(b, dst=rank + 1)
+        out = ctx.empty((nq, n_top), torch.int32)
+    else:
+        out = chain(*args, carry=carry, n_top=n_top)
+    b, back = _staged(dist, out)
+    dist.broadcast(b, src=world - 1)
+    back()
+    return out
+
+
 def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, unk_idx, n_top, timing=None, csr=None):
     """The clustering recommender over row shards (main.cpp:260-269 on the
     sharded rows; get_top_N_recom's 3-argument overload, crypto_rec.hpp:327-345).
@@ -267,46 +315,10 @@ def recommend_sharded(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, un
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timing is not None else None
     if ev:
         ev[0].record()
-    crow, crows = csr if csr is not None else lk.clusters(ctx, assign, K)
-    # the terms form stages rows of <= 1016 B in 8-B units (lshkm_cluster_terms):
-    # other rows (fp32 of odd d, fp64 of d >= 128) take the sims form, the same
-    # rank-to-rank chain over lshkm_cluster_sims + lshkm_cluster_chain
-    rb = X.shape[1] * X.element_size()
-    if rb % 8 == 0 and rb <= 1016:
-        soff, toff, sims, terms = lk.cluster_terms(ctx, X, x_mean, crow, crows, U, ucl, unk_ptr, unk_idx)
-        args = (ctx, u_mean, unk_ptr, unk_idx, soff, toff, sims, terms)
-        chain = lk.cluster_chain_terms
-    else:
-        soff, sims = lk.cluster_sims(ctx, X, crow, crows, U, ucl, unk_ptr)
-        args = (ctx, X, x_mean, crow, crows, ucl, u_mean, unk_ptr, unk_idx, soff, sims)
-        chain = lk.cluster_chain
+    state = recommend_terms(lk, ctx, X, x_mean, assign, K, U, u_mean, ucl, unk_ptr, unk_idx, csr=csr)
     if ev:
         ev[1].record()
-    dist = _dist()
-    if dist is None:
-        out = chain(*args, carry=None, n_top=n_top)
-    else:
-        rank, world = dist.get_rank(), dist.get_world_size()
-        nq, M = ucl.shape[0], unk_idx.shape[0]
-        carry = None
-        if rank > 0:
-            carry = (ctx.empty((max(M, 1),), torch.float64), ctx.empty((nq,), torch.float64),
-                     ctx.empty((nq,), torch.int64))
-            for t in carry:
-                b, back = _staged(dist, t)
-                dist.recv(b, src=rank - 1)
-                back()
-        if rank + 1 < world:
-            outs = chain(*args, carry=carry, n_top=None)
-            for t in outs:
-                b, _ = _staged(dist, t)
-                dist.send(b, dst=rank + 1)
-            out = ctx.empty((nq, n_top), torch.int32)
-        else:
-            out = chain(*args, carry=carry, n_top=n_top)
-        b, back = _staged(dist, out)
-        dist.broadcast(b, src=world - 1)
-        back()
+    out = recommend_chain(ctx, state, n_top)
     if ev:
         ev[2].record()
         torch.cuda.synchronize(ctx.dev)
@@ -403,6 +415,8 @@ class ShardedLloyd:
         self.exchange_events = []
         self.recom = None         # enable_recommend(): the C5 recommend step after each update
         self.csr = None           # (crow, crows) of this iteration's assignment (recommend runs)
+        self._rstream = None      # device rows: the recommend phase's stream (enable_recommend)
+        self.rctx = None
 
     def step(self):
         import ctypes as C
@@ -418,14 +432,26 @@ class ShardedLloyd:
                                                          None, p(self.bucket), p(self.assign), p(self.dist)))
         else:
             lk.lloyd_assign(ctx, X, self.C, self.metric, self.src, self.assign, self.dist)
+        # the recommend phase on its own stream (device rows): its similarities
+        # and terms depend only on this assignment, so they run beside the
+        # k-means sums, and each phase's host synchronisations wait for its own
+        # stream only; the chain follows the finalize, and the stream joins
+        # torch's before the step returns (host order keeps the ranks'
+        # collectives in one order)
+        rs = self._rstream if self.recom is not None else None
+        rstate = None
+        # the cluster CSR of this assignment serves the sums and the recommender
+        self.csr = lk.clusters(ctx, self.assign, self.K) if self.mode != "carry" or self.recom is not None else None
+        if rs is not None:
+            torch = ctx.torch
+            rs.wait_stream(torch.cuda.current_stream(ctx.dev))
+            with torch.cuda.stream(rs):
+                rstate = self._recommend_begin()
         if self.mode == "carry":
             def local(cs, cc):
                 return lk.kmeans_partial_carry(ctx, X, self.assign, self.K, cs, cc)
             sums, counts = chain_partials(local, self.sums, self.counts)
-            self.csr = lk.clusters(ctx, self.assign, self.K) if self.recom is not None else None
         else:
-            # the cluster CSR of this assignment serves the sums and the recommender
-            self.csr = lk.clusters(ctx, self.assign, self.K)
             if self.timing:
                 ev = [ctx.torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 ev[0].record()
@@ -441,7 +467,12 @@ class ShardedLloyd:
             self.C = Cn
             self.src = None   # the override applies to dataset-row centroids only
         self.cont = cont
-        if self.recom is not None:
+        if rs is not None:
+            torch = ctx.torch
+            with torch.cuda.stream(rs):
+                self._recommend_end(rstate)
+            torch.cuda.current_stream(ctx.dev).wait_stream(rs)
+        elif self.recom is not None:
             self.recommend()
         return cont
 
@@ -457,9 +488,40 @@ class ShardedLloyd:
         rows, U, um, up, ui = synth_recom_users(self.ctx, n_total, Q, self.d, seed)
         self.recom = dict(row0=row0, n_top=n_top, x_mean=x_mean, rows=rows, U=U, u_mean=um, unk_ptr=up, unk_idx=ui,
                           index=user_cluster_index(self.ctx, rows, row0, n))
+        if self.X.is_cuda and self._rstream is None:
+            # the recommend phase's stream and a library context on it (its own
+            # workspaces: the two phases run at once)
+            import ctypes as C
+            self._rstream = torch.cuda.Stream(device=self.ctx.dev)
+            self.rctx = self.lk.Context(self.ctx.device, use_torch_stream=False)
+            self.lk._ck(self.lk.lib().lshkm_ctx_set_stream(self.rctx.h, C.c_void_p(self._rstream.cuda_stream)))
         self.recom_out = None
         self.recom_ucl = None
         self.recom_timing = None      # a list: (phase-1 ms, phase-2 ms) per step
+
+    def _recommend_begin(self):
+        """The users' clusters and phase 1 (recommend_terms) on the recommend
+        stream; returns the state _recommend_end continues."""
+        r, torch = self.recom, self.ctx.torch
+        ev = None
+        if self.recom_timing is not None:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
+        ucl = user_clusters(self.ctx, r["rows"], self.assign, r["row0"], self.X.shape[0], index=r["index"])
+        self.recom_ucl = ucl
+        state = recommend_terms(self.lk, self.rctx, self.X, r["x_mean"], self.assign, self.K, r["U"], r["u_mean"], ucl,
+                                r["unk_ptr"], r["unk_idx"], csr=self.csr)
+        if ev:
+            ev[1].record()
+        return state, ev
+
+    def _recommend_end(self, begun):
+        state, ev = begun
+        self.recom_out = recommend_chain(self.rctx, state, self.recom["n_top"])
+        if ev:
+            ev[2].record()
+            ev[2].synchronize()
+            self.recom_timing.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
 
     def recommend(self):
         r = self.recom
