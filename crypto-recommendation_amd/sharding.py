@@ -417,6 +417,9 @@ class ShardedLloyd:
         self.csr = None           # (crow, crows) of this iteration's assignment (recommend runs)
         self._rstream = None      # device rows: the recommend phase's stream (enable_recommend)
         self.rctx = None
+        self._rs_pending = False  # recommend work on that stream not yet joined into torch's
+        self._recom_out = None
+        self._recom_ucl = None
 
     def step(self):
         import ctypes as C
@@ -432,6 +435,9 @@ class ShardedLloyd:
                                                          None, p(self.bucket), p(self.assign), p(self.dist)))
         else:
             lk.lloyd_assign(ctx, X, self.C, self.metric, self.src, self.assign, self.dist)
+        # the previous step's recommend chain ran beside this assignment (it
+        # reads none of its outputs); everything after waits for it
+        self._join_recommend()
         # the recommend phase on its own stream (device rows): its similarities
         # and terms depend only on this assignment, so they run beside the
         # k-means sums, and each phase's host synchronisations wait for its own
@@ -471,7 +477,9 @@ class ShardedLloyd:
             torch = ctx.torch
             with torch.cuda.stream(rs):
                 self._recommend_end(rstate)
-            torch.cuda.current_stream(ctx.dev).wait_stream(rs)
+            # joined by the next step after its assignment is enqueued, or by
+            # the first read of recom_out / recom_ucl
+            self._rs_pending = True
         elif self.recom is not None:
             self.recommend()
         return cont
@@ -498,6 +506,31 @@ class ShardedLloyd:
         self.recom_out = None
         self.recom_ucl = None
         self.recom_timing = None      # a list: (phase-1 ms, phase-2 ms) per step
+
+    def _join_recommend(self):
+        if self._rs_pending:
+            self.ctx.torch.cuda.current_stream(self.ctx.dev).wait_stream(self._rstream)
+            self._rs_pending = False
+
+    @property
+    def recom_out(self):
+        """The last step's recommendations ([Q][n_top] int32, device)."""
+        self._join_recommend()
+        return self._recom_out
+
+    @recom_out.setter
+    def recom_out(self, v):
+        self._recom_out = v
+
+    @property
+    def recom_ucl(self):
+        """The last step's users' clusters (int32, device)."""
+        self._join_recommend()
+        return self._recom_ucl
+
+    @recom_ucl.setter
+    def recom_ucl(self, v):
+        self._recom_ucl = v
 
     def _recommend_begin(self):
         """The users' clusters and phase 1 (recommend_terms) on the recommend
